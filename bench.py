@@ -1,0 +1,170 @@
+"""Benchmark: MobileNetV2UNet fwd+bwd+Adam training throughput on MI355X.
+
+Workload (BASELINE.json configs[1], the metric's config): MobileNetV2UNet,
+10 classes, 256x512, batch 32 per GPU, fp32, synthetic device-resident
+inputs (x ~ N(0,1), int64 labels), deterministic random-init weights (no
+pretrained checkpoint offline).  One step = zero_grad + forward + fused
+upsample/cross-entropy loss + backward (+ RCCL gradient all-reduce when N > 1)
++ torch.optim.Adam(lr=1.5e-4) step -- the reference loop of src/train.py:35-39.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+N > 1 runs under torch.distributed.run (one process per GPU, RCCL), per-GPU
+batch fixed (weak scaling); value = all images / max-over-ranks time.
+
+Also reported:
+  roofline      -- the dense f32-MFMA implicit-GEMM convolutions (fwd, data- and
+                   weight-gradient), timed with HIP events around every launch
+                   inside the timed region: achieved = their algorithmic FLOPs /
+                   their summed launch durations vs the f32 MFMA peak.
+  cpu_baseline  -- the CPU oracle (oracle/segref.py, torch-CPU restatement of
+                   the reference) on a bounded sample, rank 0 at N = 1 only.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.join(REPO, "team02-objectdetection_amd")
+for _p in (PKG, REPO):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+import torch  # noqa: E402
+
+F32_MFMA_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: FP32 matrix (= vector) peak, spec
+HBM_PEAK_GBS = 8000.0
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=32)
+    ap.add_argument("--height", type=int, default=256)
+    ap.add_argument("--width", type=int, default=512)
+    ap.add_argument("--classes", type=int, default=10)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--no-timer", action="store_true", help="skip the per-launch HIP-event roofline timing")
+    return ap.parse_args()
+
+
+def cpu_baseline(args):
+    """The oracle (torch CPU, all host cores) on a bounded sample of the same workload."""
+    from oracle import segref
+    from seg_amd import MobileNetV2UNet, deterministic_init, synthetic_batch
+    threads = os.cpu_count() or 1
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else threads
+    threads = min(threads, aff, int(os.environ.get("OMP_NUM_THREADS", aff)))
+    torch.set_num_threads(threads)
+    model = deterministic_init(MobileNetV2UNet(args.classes), seed=0)
+    p = segref.canonical_state(model.state_dict())
+    bs = 4
+    x, y = synthetic_batch(bs, args.height, args.width, args.classes, seed=1)
+    segref.adam_steps("MobileNetV2UNet", p, [(x, y)])  # warm-up step
+    t0 = time.perf_counter()
+    steps = 0
+    while True:
+        segref.adam_steps("MobileNetV2UNet", p, [(x, y)])
+        steps += 1
+        if time.perf_counter() - t0 > args.cpu_seconds:
+            break
+    dt = time.perf_counter() - t0
+    return {"value": round(steps * bs / dt, 3), "unit": "images/s", "cores": threads, "kind": "port",
+            "sample": f"oracle/segref.py MobileNetV2UNet fwd+bwd+Adam, bs={bs}, {args.height}x{args.width}, "
+                      f"{steps} timed steps ({dt:.1f} s) after 1 warm-up, torch CPU fp32"}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = world > 1
+    if dist:
+        torch.distributed.init_process_group("nccl")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+
+    from seg_amd import MobileNetV2UNet, deterministic_init, synthetic_batch
+    from seg_amd import engine
+    model = deterministic_init(MobileNetV2UNet(args.classes), seed=0).to(dev).train()
+    if dist:
+        from seg_amd.ddp import DataParallel
+        model = DataParallel(model)
+    opt = torch.optim.Adam(model.parameters(), lr=1.5e-4)
+    x, y = synthetic_batch(args.batch, args.height, args.width, args.classes, seed=1000 + rank)
+    x, y = x.to(dev), y.to(dev)
+
+    def step():
+        opt.zero_grad(set_to_none=True)
+        loss = model.forward_loss(x, y)
+        loss.backward()
+        if dist:
+            model.finish_gradient_sync()
+        opt.step()
+        return loss
+
+    for _ in range(args.warmup):
+        step()
+    timer = None if args.no_timer else engine.KernelTimer()
+    if dist:
+        torch.distributed.barrier()
+    torch.cuda.synchronize()
+    engine.TIMER = timer
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        loss = step()
+    if dist:
+        torch.distributed.barrier()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    engine.TIMER = None
+    final_loss = loss.item()
+    t = torch.tensor([dt], device=dev, dtype=torch.float64)
+    if dist:
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+    dt = float(t)
+    images = args.batch * args.steps * world
+    value = images / dt
+
+    roof = None
+    if timer is not None:
+        rec = timer.elapsed()
+        flops = sum(f for _, f, _ in rec)
+        secs = sum(s for _, _, s in rec)
+        n = len(rec)
+        achieved = flops / secs / 1e12 if secs > 0 else 0.0
+        roof = {"bound": "mfma", "achieved": round(achieved, 2), "peak": F32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
+                "frac": round(achieved / F32_MFMA_PEAK_TFLOPS, 4), "traffic": None,
+                "kernel": "igemm_conv_kernel + wgrad_kernel (dense/pointwise f32 MFMA convs, fwd+dgrad+wgrad)",
+                "launches": n, "flops_per_launch": round(flops / max(n, 1)),
+                "avg_launch_us": round(secs / max(n, 1) * 1e6, 2),
+                "share_of_step": round(secs / (dt if not dist else dt), 4)}
+
+    if rank == 0:
+        cpu = None
+        if world == 1 and not args.no_cpu_baseline:
+            cpu = cpu_baseline(args)
+        line = {"metric": "images/sec fwd+bwd MobileNetV2UNet 256x512 bs=32/GPU",
+                "value": round(value, 2), "unit": "images/s", "n_gpus": world, "steps": args.steps,
+                "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 3), "higher_is_better": True,
+                "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+                "config": {"workload": f"MobileNetV2UNet {args.classes}-class fwd+bwd+Adam, "
+                                       f"{args.height}x{args.width}, bs={args.batch}/GPU (BASELINE configs[1])",
+                           "model": "MobileNetV2UNet", "global_batch": args.batch * world,
+                           "image": [args.height, args.width], "parallelism": f"dp{world}"},
+                "final_loss": round(final_loss, 5),
+                "roofline": roof, "cpu_baseline": cpu}
+        print(json.dumps(line), flush=True)
+    if dist:
+        torch.distributed.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,20 @@
+#!/bin/bash
+# Run GPU steps in order; stop at the first crash/timeout (rc > 1), keep going on plain test failures.
+mkdir -p gpurun_out
+run() {  # name timeout cmd...
+  local name=$1 t=$2; shift 2
+  timeout -k 10 "$t" "$@" > "gpurun_out/$name.log" 2>&1
+  local rc=$?
+  echo "== $name rc=$rc"; tail -n 25 "gpurun_out/$name.log"
+  if [ $rc -gt 1 ]; then echo "stopping after $name (rc=$rc)"; exit $rc; fi
+}
+for step in "$@"; do
+  case $step in
+    ops)   run ops 600 python -m pytest tests/test_gpu_ops.py -q -m gpu ;;
+    model) run model 900 python -m pytest tests/test_gpu_model.py -q -m gpu -x ;;
+    gpu)   run gpu 1200 python -m pytest tests -q -m gpu ;;
+    smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    bench) run bench 600 python bench.py --steps 10 --warmup 3 ;;
+    benchq) run benchq 600 python bench.py --steps 5 --warmup 2 --no-cpu-baseline ;;
+  esac
+done

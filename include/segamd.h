@@ -1,0 +1,137 @@
+/* segamd.h -- C-ABI of libsegamd.so, the MI355X (gfx950) hot path of the
+ * SEAME-pt/Team02-ObjectDetection segmentation models (MobileNetV2UNet / UNet).
+ *
+ * The reference has no native code: its hot path is PyTorch's aten dispatch of
+ * the ops in src/unet.py + nn.CrossEntropyLoss (main.py:99, src/train.py:37).
+ * Each entry point below replaces the aten op(s) named in its comment; the
+ * Python nn.Module / train_model surface (team02-objectdetection_amd/seg_amd)
+ * binds them with ctypes, and INTEGRATION.md shows the binding.
+ *
+ * Contract (all functions):
+ *  - activations are NHWC fp32 "row" tensors: row = pixel, `ld*` = row stride in
+ *    floats (a multiple of 4, >= round_up(C, 4)); pointers 16-byte aligned;
+ *  - the caller owns every buffer, including workspaces (sizes from the
+ *    *_workspace / *_splits / *_blocks queries); nothing allocates;
+ *  - asynchronous and stream-ordered on `stream`; no host synchronisation, so
+ *    every call is hipGraph-capturable; no internal threads or global state;
+ *  - returns hipError_t (0 = success); argument errors return
+ *    hipErrorInvalidValue before any launch;
+ *  - reductions are deterministic (fixed-order partial slabs, no float atomics).
+ */
+#ifndef SEGAMD_H
+#define SEGAMD_H
+#include <hip/hip_runtime.h>
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* act codes: 0 none, 1 ReLU (src/unet.py:60,63,115), 2 ReLU6 (torchvision). */
+
+/* ---- convolution (aten conv2d / convolution_backward) ----------------------- */
+
+/* Implicit-GEMM conv on f32 MFMA: out = conv(in, W) (+bias) (+add).
+ * Replaces nn.Conv2d forward of the dense 3x3 convs (src/unet.py:58,61), the 1x1
+ * head (src/unet.py:113,116) and torchvision's expand/project 1x1 convs
+ * (reached through src/unet.py:15-19); with mode-1 packed weights it is also the
+ * data gradient of those (stride-1) convs.  ks in {1,3}. */
+int seg_conv_igemm(const float* in, long ldin, int N, int H, int W, int Cin,
+                   const float* wk, int ldk, const float* bias,
+                   float* out, long ldout, int Ho, int Wo, int Cout,
+                   int ks, int stride, int pad,
+                   const float* add, long ldadd, hipStream_t stream);
+
+/* Pack w[Cout][Cin][ks][ks]: mode 0 -> wk[Cout][ldk] (forward),
+ * mode 1 -> wk[Cin][ldk] transposed + tap-flipped (data gradient), tap runs
+ * padded to kin_pad >= Cout channels. */
+int seg_pack_conv_weight(const float* w, float* wk, int Cout, int Cin, int ks, int ldk,
+                         int mode, int kin_pad, hipStream_t stream);
+
+/* Weight gradient (convolution_backward, weight path) as split-K partial slabs
+ * part[splits][Cout][ks*ks*Cin]; splits from seg_conv_wgrad_splits. */
+int seg_conv_wgrad_splits(long M, int Cout, int Cin, int ks);
+int seg_conv_wgrad(const float* dy, long lddy, const float* x, long ldx,
+                   int N, int H, int W, int Cin, int Ho, int Wo, int Cout,
+                   int ks, int stride, int pad, float* part, int splits, hipStream_t stream);
+
+/* dW (PyTorch layout) = fixed-order sum of partial slabs.  mode 0: igemm
+ * partials, 1: depthwise partials, 2: stem partials. */
+int seg_conv_wgrad_reduce(const float* part, int splits, float* dw, int Cout, int Cin, int ks,
+                          int mode, int accumulate, hipStream_t stream);
+
+/* Depthwise 3x3 (torchvision InvertedResidual dw conv, features[1..17] via
+ * src/unet.py:15-19): forward, data gradient, weight-gradient partials. */
+int seg_pack_dw_weight(const float* w, float* wk, int C, hipStream_t stream);
+int seg_dw_fwd(const float* in, long ldin, int N, int H, int W, int C, const float* wk,
+               float* out, long ldout, int Ho, int Wo, int stride, hipStream_t stream);
+int seg_dw_dgrad(const float* dy, long lddy, int N, int Ho, int Wo, int C, const float* wk,
+                 float* dx, long lddx, int H, int W, int stride, int accumulate, hipStream_t stream);
+long seg_dw_wgrad_blocks(long M);
+int seg_dw_wgrad(const float* dy, long lddy, const float* x, long ldx, int N, int H, int W, int C,
+                 int Ho, int Wo, int stride, float* part, hipStream_t stream);
+
+/* Cin = 3 first conv straight from the NCHW image batch: MobileNetV2 features[0]
+ * (3->32, s2, via src/unet.py:15,34) and UNet inc (3->64/32, s1, bias,
+ * src/unet.py:58 via :127). */
+int seg_stem_fwd(const float* x, int N, int H, int W, const float* w, const float* bias, int Cout,
+                 float* out, long ldout, int Ho, int Wo, int stride, hipStream_t stream);
+long seg_stem_wgrad_blocks(long M);
+int seg_stem_wgrad(const float* dy, long lddy, const float* x, int N, int H, int W, int Ho, int Wo,
+                   int Cout, int stride, float* part, hipStream_t stream);
+
+/* ---- BatchNorm2d + activation (aten native_batch_norm(+_backward), hardtanh,
+ *      threshold; src/unet.py:59-63,114-115 and torchvision norms) ----------- */
+long seg_chan_workspace_floats(long M, int C);
+int seg_bn_stats(const float* y, long ldy, long M, int C, const float* gamma, const float* beta,
+                 float eps, float momentum, float* running_mean, float* running_var,
+                 long long* num_batches_tracked, float* work,
+                 float* mean, float* invstd, float* scale, float* shift, hipStream_t stream);
+int seg_bn_eval_coef(const float* gamma, const float* beta, const float* running_mean,
+                     const float* running_var, float eps, int C, float* scale, float* shift,
+                     hipStream_t stream);
+int seg_bn_apply(const float* y, long ldy, long M, int C, const float* scale, const float* shift,
+                 int act, const float* res, long ldres, float* out, long ldout, hipStream_t stream);
+int seg_bn_backward(const float* da, long ldda, const float* y, long ldy, long M, int C,
+                    const float* gamma, const float* mean, const float* invstd,
+                    const float* scale, const float* shift, int act,
+                    float* dgamma, float* dbeta, float* work, float* dy, long lddy, hipStream_t stream);
+int seg_bn_eval_backward(const float* da, long ldda, const float* y, long ldy, long M, int C,
+                         const float* scale, const float* shift, int act, float* dy, long lddy,
+                         hipStream_t stream);
+/* conv bias gradient: out[c] (+)= sum_r y[r][c] */
+int seg_colsum(const float* y, long ldy, long M, int C, float* work, float* out, int accumulate,
+               hipStream_t stream);
+/* gradient fan-in (residual add of InvertedResidual, skip reuse): out = a (+ b) */
+int seg_add(const float* a, long lda, const float* b, long ldb, long M, int C, float* out, long ldout,
+            hipStream_t stream);
+
+/* ---- resampling (aten upsample_bilinear2d(+_backward), max_pool2d) ---------- */
+/* nn.Upsample(x2, bilinear) of `up` (src/unet.py:97,101; ac = 0) into the concat
+ * slice of torch.cat([skip, up]) (src/unet.py:103). */
+int seg_upsample_fwd(const float* in, long ldin, int N, int H, int W, int C,
+                     float* out, long ldout, int Ho, int Wo, int ac, hipStream_t stream);
+int seg_upsample_bwd(const float* dout, long ldout, int nchw_grad, int N, int Ho, int Wo, int C,
+                     float* din, long ldin, int H, int W, int ac, int accumulate, hipStream_t stream);
+/* final_upsample (align_corners=True, src/unet.py:30,49): NHWC -> NCHW logits */
+int seg_upsample_to_nchw(const float* in, long ldin, int N, int H, int W, int C,
+                         float* out, int Ho, int Wo, int ac, hipStream_t stream);
+/* nn.MaxPool2d(2) of UNet.down (src/unet.py:85) */
+int seg_maxpool2_fwd(const float* in, long ldin, int N, int H, int W, int C,
+                     float* out, long ldout, hipStream_t stream);
+int seg_maxpool2_bwd(const float* in, long ldin, const float* dout, long lddout, int N, int H, int W,
+                     int C, float* din, long lddin, int accumulate, hipStream_t stream);
+
+/* ---- loss (nn.CrossEntropyLoss, main.py:99 / src/train.py:37) fused with the
+ *      align_corners=True final upsample (src/unet.py:30,49) ----------------- */
+long seg_ce_workspace_floats(long pixels);
+int seg_ce_upsample_loss(const float* low, long ld, int N, int H, int W, int C,
+                         const long long* labels, int Ho, int Wo, int ignore_index,
+                         float* work, float* out2, hipStream_t stream);
+int seg_ce_upsample_grad(const float* low, long ld, int N, int H, int W, int C,
+                         const long long* labels, int Ho, int Wo, int ignore_index,
+                         const float* grad_out, const float* stats, float* dhigh, long ldh,
+                         hipStream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SEGAMD_H */

@@ -1,0 +1,187 @@
+"""CPU ORACLE -- TEST INFRASTRUCTURE ONLY.
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may import
+this module, and only as the checker / CPU baseline -- never as the product
+path (the product, team02-objectdetection_amd/seg_amd, has no CPU path).
+
+A functional, fp32-or-fp64 restatement on torch CPU (aten/oneDNN) of the
+reference's hot path, written over a flat state_dict so it shares no code with
+the product modules:
+  * MobileNetV2UNet.forward            src/unet.py:32-51
+  * torchvision mobilenet_v2 features  (third-party, unpinned in
+    requirements.txt:2; restated from the published architecture: stem
+    conv3x3 s2 + 17 InvertedResidual(t,c,n,s) blocks + 1x1 to 1280,
+    ReLU6 everywhere, residual when stride 1 and cin == cout)
+  * up / double_conv / outconv         src/unet.py:53-68, 94-121
+  * UNet / LightUNet                   src/unet.py:124-171 (inconv :71-77, down :80-91)
+  * nn.CrossEntropyLoss()              main.py:99, src/train.py:37
+  * Adam(lr=1.5e-4) training step      main.py:100, src/train.py:35-39
+
+Parity is PINNED by tests/golden/*.npz, produced by tests/golden/make_golden.py
+from the reference's own src/unet.py (imported here, in the build container,
+with a local torchvision stand-in); tests/test_oracle.py checks this module
+against every fixture.
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn.functional as F
+
+MBV2_SETTING = ((1, 16, 1, 1), (6, 24, 2, 2), (6, 32, 3, 2), (6, 64, 4, 2),
+                (6, 96, 3, 1), (6, 160, 3, 2), (6, 320, 1, 1))
+
+
+def _bn(p, pre, x, training, momentum=0.1, eps=1e-5):
+    # nn.BatchNorm2d: biased batch var for normalisation, unbiased for running_var
+    return F.batch_norm(x, p[pre + "running_mean"], p[pre + "running_var"], p[pre + "weight"], p[pre + "bias"],
+                        training, momentum, eps)
+
+
+def _bump(p, pre, training):
+    if training and (pre + "num_batches_tracked") in p:
+        p[pre + "num_batches_tracked"] += 1
+
+
+def _cbr(p, pre_conv, pre_bn, x, training, stride=1, pad=0, groups=1, act="relu6", bias=None):
+    y = F.conv2d(x, p[pre_conv + "weight"], p.get(pre_conv + "bias") if bias is None else bias,
+                 stride=stride, padding=pad, groups=groups)
+    y = _bn(p, pre_bn, y, training)
+    _bump(p, pre_bn, training)
+    if act == "relu6":
+        return F.hardtanh(y, 0.0, 6.0)
+    if act == "relu":
+        return F.relu(y)
+    return y
+
+
+def mobilenet_features(p, x, training, prefix="backbone.features."):
+    """Returns the outputs after features[1], [3], [6], [10], [18]
+    (= the reference's x1..x5, src/unet.py:34-38)."""
+    taps = {}
+    x = _cbr(p, prefix + "0.0.", prefix + "0.1.", x, training, stride=2, pad=1)
+    idx, cin = 1, 32
+    for t, c, n, s in MBV2_SETTING:
+        for i in range(n):
+            stride = s if i == 0 else 1
+            pre = f"{prefix}{idx}.conv."
+            hidden = int(round(cin * t))
+            h, j = x, 0
+            if t != 1:
+                h = _cbr(p, pre + "0.0.", pre + "0.1.", h, training)
+                j = 1
+            h = _cbr(p, f"{pre}{j}.0.", f"{pre}{j}.1.", h, training, stride=stride, pad=1, groups=hidden)
+            h = _cbr(p, f"{pre}{j + 1}.", f"{pre}{j + 2}.", h, training, act=None)
+            x = x + h if (stride == 1 and cin == c) else h
+            cin = c
+            if idx in (1, 3, 6, 10):
+                taps[idx] = x
+            idx += 1
+    x = _cbr(p, prefix + "18.0.", prefix + "18.1.", x, training)
+    taps[18] = x
+    return taps
+
+
+def double_conv(p, pre, x, training):
+    x = _cbr(p, pre + "conv.0.", pre + "conv.1.", x, training, pad=1, act="relu")
+    return _cbr(p, pre + "conv.3.", pre + "conv.4.", x, training, pad=1, act="relu")
+
+
+def up(p, pre, x1, x2, training):
+    x1 = F.interpolate(x1, scale_factor=2, mode="bilinear", align_corners=False)
+    return double_conv(p, pre + "conv.", torch.cat([x2, x1], dim=1), training)
+
+
+def outconv(p, pre, x, training):
+    x = _cbr(p, pre + "conv.0.", pre + "conv.1.", x, training, act="relu")
+    return F.conv2d(x, p[pre + "conv.3.weight"], p[pre + "conv.3.bias"])
+
+
+def mobilenet_unet_forward(p, x, training):
+    f = mobilenet_features(p, x, training)
+    y = up(p, "up1.", f[18], f[10], training)
+    y = up(p, "up2.", y, f[6], training)
+    y = up(p, "up3.", y, f[3], training)
+    y = up(p, "up4.", y, f[1], training)
+    y = outconv(p, "outc.", y, training)
+    return F.interpolate(y, scale_factor=2, mode="bilinear", align_corners=True)
+
+
+def unet_forward(p, x, training):
+    x1 = double_conv(p, "inc.conv.", x, training)
+    x2 = double_conv(p, "down1.mpconv.1.", F.max_pool2d(x1, 2), training)
+    x3 = double_conv(p, "down2.mpconv.1.", F.max_pool2d(x2, 2), training)
+    x4 = double_conv(p, "down3.mpconv.1.", F.max_pool2d(x3, 2), training)
+    y = up(p, "up1.", x4, x3, training)
+    y = up(p, "up2.", y, x2, training)
+    y = up(p, "up3.", y, x1, training)
+    return outconv(p, "sem_out.", y, training)
+
+
+FORWARDS = {"MobileNetV2UNet": mobilenet_unet_forward, "UNet": unet_forward, "LightUNet": unet_forward}
+
+
+def canonical_state(state_dict, dtype=torch.float32):
+    """Flat name -> tensor dict (aliases dropped: down1..5 of MobileNetV2UNet are
+    views of backbone.features), float tensors cast to `dtype`, detached copies."""
+    out = {}
+    for k, v in state_dict.items():
+        if any(k.startswith(f"down{i}.") for i in range(1, 6)) and "mpconv" not in k:
+            continue
+        t = v.detach().cpu().clone()
+        if t.is_floating_point():
+            t = t.to(dtype)
+        out[k] = t
+    return out
+
+
+def trainable_names(p):
+    return [k for k, v in p.items() if v.is_floating_point() and not k.endswith(("running_mean", "running_var"))
+            and not k.startswith("backbone.classifier")]
+
+
+def forward_backward(arch, p, x, y, training=True):
+    """Loss, logits and per-parameter grads of CE(model(x), y)."""
+    names = trainable_names(p)
+    for k in names:
+        p[k].requires_grad_(True)
+        p[k].grad = None
+    logits = FORWARDS[arch](p, x, training)
+    loss = F.cross_entropy(logits, y)
+    loss.backward()
+    grads = {k: p[k].grad.detach().clone() for k in names}
+    for k in names:
+        p[k].requires_grad_(False)
+    return loss.detach(), logits.detach(), grads
+
+
+def adam_steps(arch, p, batches, lr=1.5e-4, betas=(0.9, 0.999), eps=1e-8):
+    """Adam (torch.optim.Adam defaults, main.py:100) training steps; returns losses."""
+    names = trainable_names(p)
+    state = {k: (torch.zeros_like(p[k]), torch.zeros_like(p[k])) for k in names}
+    losses = []
+    for step, (x, y) in enumerate(batches, start=1):
+        loss, _, grads = forward_backward(arch, p, x, y, True)
+        losses.append(float(loss))
+        with torch.no_grad():
+            for k in names:
+                m, v = state[k]
+                g = grads[k]
+                m.mul_(betas[0]).add_(g, alpha=1 - betas[0])
+                v.mul_(betas[1]).addcmul_(g, g, value=1 - betas[1])
+                bc1 = 1 - betas[0] ** step
+                bc2 = 1 - betas[1] ** step
+                denom = (v.sqrt() / (bc2 ** 0.5)).add_(eps)
+                p[k].addcdiv_(m, denom, value=-lr / bc1)
+    return losses
+
+
+def miou(pred, target, classes):
+    """Mean IoU over classes with a non-empty union (the build's definition;
+    the reference has no metric code)."""
+    pred = pred.reshape(-1).long()
+    target = target.reshape(-1).long()
+    cm = torch.bincount(target * classes + pred, minlength=classes * classes).reshape(classes, classes).double()
+    tp = cm.diag()
+    union = cm.sum(0) + cm.sum(1) - tp
+    valid = union > 0
+    return float((tp[valid] / union[valid]).mean()) if valid.any() else float("nan")

@@ -1,0 +1,317 @@
+// BatchNorm2d (train + eval) with the fused activation / residual of the hot path.
+//
+// Reference semantics: nn.BatchNorm2d after every conv
+// (src/unet.py:59,62,114 and the torchvision Conv2dNormActivation /
+// InvertedResidual norms reached through src/unet.py:15-19); train mode uses the
+// biased batch variance over (N,H,W), eps = 1e-5, and updates
+// running_mean/var <- 0.9*old + 0.1*batch with the UNBIASED variance and
+// num_batches_tracked += 1.  The activation that follows is ReLU6
+// (torchvision), ReLU (src/unet.py:60,63,115) or nothing (the linear project
+// conv, whose output takes the residual add of InvertedResidual).
+//
+// Layout: raw conv output y is NHWC [M][ldy]; channels C % 4 == 0.
+// Statistics are computed in two steps: per-block shifted partial sums
+// (fp32 over <= a few hundred rows, shift = first row so a large mean cannot
+// cancel the variance away) and a per-channel finalize in fp64.
+#include "common.h"
+
+namespace {
+
+// Per-block partial sums over a row range for float4 channel groups.
+// Block = 256 threads laid out as RG row-lanes x TC channel-group lanes.
+// kind 0: (sum(y-k), sum((y-k)^2)),  k = y[0][c]                   -> BN stats
+// kind 1: (sum(dz),  sum(dz*(y-mean))), dz = dA * act'(y*scale+shift) -> BN backward
+// kind 2: (sum(y), 0)                                               -> bias grad
+template <int KIND>
+__global__ __launch_bounds__(256) void chan_partial_kernel(
+    const float* __restrict__ y, long ldy, const float* __restrict__ da, long ldda, int M, int C,
+    const float* __restrict__ scale, const float* __restrict__ shift, const float* __restrict__ mean, int act,
+    float* __restrict__ part, int rows_per_block) {
+  __shared__ f32x4 red0[256], red1[256];
+  const int CG = C >> 2;
+  const int TC = CG < 256 ? CG : 256;
+  const int RG = 256 / TC;
+  const int t = threadIdx.x;
+  const int rg = t / TC, tc = t - rg * TC;
+  const int r0 = blockIdx.x * rows_per_block;
+  const int r1 = min(M, r0 + rows_per_block);
+  float* p0 = part + (long)blockIdx.x * 2 * C;
+  float* p1 = p0 + C;
+  for (int cgb = 0; cgb < CG; cgb += TC) {
+    const int cg = cgb + tc;
+    const bool active = rg < RG && cg < CG;
+    f32x4 s0 = {0.f, 0.f, 0.f, 0.f}, s1 = {0.f, 0.f, 0.f, 0.f};
+    if (active) {
+      const int c = cg * 4;
+      f32x4 k = {0.f, 0.f, 0.f, 0.f}, sc = k, sh = k;
+      if (KIND == 0) k = ld4(y + c);
+      if (KIND == 1) { k = ld4(mean + c); sc = ld4(scale + c); sh = ld4(shift + c); }
+      for (int r = r0 + rg; r < r1; r += RG) {
+        const f32x4 v = ld4(y + (long)r * ldy + c);
+        if (KIND == 0) {
+          const f32x4 d = v - k;
+          s0 += d;
+          s1 += d * d;
+        } else if (KIND == 1) {
+          const f32x4 g = ld4(da + (long)r * ldda + c);
+          f32x4 dz;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) dz[j] = g[j] * seg_act_mask(v[j] * sc[j] + sh[j], act);
+          s0 += dz;
+          s1 += dz * (v - k);
+        } else {
+          s0 += v;
+        }
+      }
+    }
+    red0[t] = s0;
+    red1[t] = s1;
+    __syncthreads();
+    if (rg == 0 && active) {
+      for (int j = 1; j < RG; ++j) {
+        s0 += red0[j * TC + tc];
+        s1 += red1[j * TC + tc];
+      }
+      st4(p0 + cg * 4, s0);
+      st4(p1 + cg * 4, s1);
+    }
+    __syncthreads();
+  }
+}
+
+int rows_per_block_for(long M) {
+  // ~1024 blocks, at least 32 rows each.
+  long r = (M + 1023) / 1024;
+  if (r < 32) r = 32;
+  return (int)r;
+}
+
+__global__ void bn_finalize_kernel(const float* __restrict__ part, int nblk, const float* __restrict__ y, long M, int C,
+                                   const float* __restrict__ gamma, const float* __restrict__ beta, float eps,
+                                   float momentum, float* running_mean, float* running_var, long long* nbt,
+                                   float* mean_out, float* invstd_out, float* scale_out, float* shift_out) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c == 0 && nbt) *nbt += 1;
+  if (c >= C) return;
+  double s = 0.0, s2 = 0.0;
+  for (int b = 0; b < nblk; ++b) {
+    s += part[(long)b * 2 * C + c];
+    s2 += part[(long)b * 2 * C + C + c];
+  }
+  const double k = y[c];
+  const double dm = s / (double)M;
+  const double mean = k + dm;
+  double var = s2 / (double)M - dm * dm;
+  if (var < 0.0) var = 0.0;
+  const float invstd = (float)(1.0 / sqrt(var + (double)eps));
+  mean_out[c] = (float)mean;
+  invstd_out[c] = invstd;
+  const float g = gamma ? gamma[c] : 1.f, bt = beta ? beta[c] : 0.f;
+  scale_out[c] = g * invstd;
+  shift_out[c] = bt - (float)mean * g * invstd;
+  if (running_mean) {
+    const double unbiased = M > 1 ? var * (double)M / (double)(M - 1) : var;
+    running_mean[c] = (float)((1.0 - momentum) * running_mean[c] + momentum * mean);
+    running_var[c] = (float)((1.0 - momentum) * running_var[c] + momentum * unbiased);
+  }
+}
+
+__global__ void bn_eval_coef_kernel(const float* gamma, const float* beta, const float* rm, const float* rv, float eps,
+                                    int C, float* scale_out, float* shift_out) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  const float inv = 1.f / sqrtf(rv[c] + eps);
+  const float g = gamma ? gamma[c] : 1.f, b = beta ? beta[c] : 0.f;
+  scale_out[c] = g * inv;
+  shift_out[c] = b - rm[c] * g * inv;
+}
+
+// out = act(y*scale + shift) (+ res)
+__global__ void bn_apply_kernel(const float* __restrict__ y, long ldy, long M, int C, const float* __restrict__ scale,
+                                const float* __restrict__ shift, int act, const float* __restrict__ res, long ldres,
+                                float* __restrict__ out, long ldout) {
+  const int CG = C >> 2;
+  const long total = M * CG;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const long r = i / CG;
+    const int c = (int)(i - r * CG) * 4;
+    const f32x4 v = ld4(y + r * ldy + c), sc = ld4(scale + c), sh = ld4(shift + c);
+    f32x4 o;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) o[j] = seg_act(v[j] * sc[j] + sh[j], act);
+    if (res) o += ld4(res + r * ldres + c);
+    st4(out + r * ldout + c, o);
+  }
+}
+
+__global__ void bn_bwd_finalize_kernel(const float* __restrict__ part, int nblk, long M, int C,
+                                       const float* __restrict__ gamma, const float* __restrict__ invstd,
+                                       float* dgamma, float* dbeta, float* coef) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  double sdz = 0.0, sdzx = 0.0;
+  for (int b = 0; b < nblk; ++b) {
+    sdz += part[(long)b * 2 * C + c];
+    sdzx += part[(long)b * 2 * C + C + c];
+  }
+  const double inv = invstd[c];
+  const double g = gamma ? gamma[c] : 1.0;
+  if (dbeta) dbeta[c] = (float)sdz;
+  if (dgamma) dgamma[c] = (float)(sdzx * inv);
+  // dY = g*inv * (dz - mean(dz) - xhat*mean(dz*xhat)),  xhat = (y-mean)*inv
+  coef[c] = (float)(g * inv);
+  coef[C + c] = (float)(sdz / (double)M);
+  coef[2 * C + c] = (float)(sdzx * inv * inv / (double)M);
+}
+
+__global__ void bn_bwd_apply_kernel(const float* __restrict__ da, long ldda, const float* __restrict__ y, long ldy,
+                                    long M, int C, const float* __restrict__ scale, const float* __restrict__ shift,
+                                    const float* __restrict__ mean, int act, const float* __restrict__ coef,
+                                    float* __restrict__ dy, long lddy) {
+  const int CG = C >> 2;
+  const long total = M * CG;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const long r = i / CG;
+    const int c = (int)(i - r * CG) * 4;
+    const f32x4 v = ld4(y + r * ldy + c), g = ld4(da + r * ldda + c);
+    const f32x4 sc = ld4(scale + c), sh = ld4(shift + c), mu = ld4(mean + c);
+    const f32x4 k1 = ld4(coef + c), k2 = ld4(coef + C + c), k3 = ld4(coef + 2 * C + c);
+    f32x4 o;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float dz = g[j] * seg_act_mask(v[j] * sc[j] + sh[j], act);
+      o[j] = k1[j] * (dz - k2[j] - (v[j] - mu[j]) * k3[j]);
+    }
+    st4(dy + r * lddy + c, o);
+  }
+}
+
+// Eval-mode backward (BN uses running statistics, a pure affine map):
+// dY = dA * act'(y*scale+shift) * scale.
+__global__ void bn_eval_bwd_kernel(const float* __restrict__ da, long ldda, const float* __restrict__ y, long ldy,
+                                   long M, int C, const float* __restrict__ scale, const float* __restrict__ shift,
+                                   int act, float* __restrict__ dy, long lddy) {
+  const int CG = C >> 2;
+  const long total = M * CG;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const long r = i / CG;
+    const int c = (int)(i - r * CG) * 4;
+    const f32x4 v = ld4(y + r * ldy + c), g = ld4(da + r * ldda + c);
+    const f32x4 sc = ld4(scale + c), sh = ld4(shift + c);
+    f32x4 o;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) o[j] = g[j] * seg_act_mask(v[j] * sc[j] + sh[j], act) * sc[j];
+    st4(dy + r * lddy + c, o);
+  }
+}
+
+__global__ void colsum_finalize_kernel(const float* __restrict__ part, int nblk, int C, int ldp, float* out,
+                                       int accumulate) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  double s = 0.0;
+  for (int b = 0; b < nblk; ++b) s += part[(long)b * 2 * ldp + c];
+  out[c] = accumulate ? out[c] + (float)s : (float)s;
+}
+
+int ew_grid(long total) { return (int)std::min<long>(seg_cdiv(total, 256), 8192); }
+
+__global__ void add_kernel(const float* __restrict__ a, long lda, const float* __restrict__ b, long ldb, long M, int C,
+                           float* __restrict__ out, long ldout) {
+  const int CG = C >> 2;
+  const long total = M * CG;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const long r = i / CG;
+    const int c = (int)(i - r * CG) * 4;
+    f32x4 v = ld4(a + r * lda + c);
+    if (b) v += ld4(b + r * ldb + c);
+    st4(out + r * ldout + c, v);
+  }
+}
+
+}  // namespace
+
+// out = a (+ b), all [M][C] NHWC strided (out may alias a or b).  Gradient fan-in.
+SEG_API int seg_add(const float* a, long lda, const float* b, long ldb, long M, int C, float* out, long ldout,
+                    hipStream_t stream) {
+  if ((C & 3) || (lda & 3) || (ldout & 3) || (b && (ldb & 3))) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(add_kernel, dim3(ew_grid(M * (C / 4))), dim3(256), 0, stream, a, lda, b, ldb, M, C, out, ldout);
+  SEG_RET_LAST();
+}
+
+// Size (floats) of the partial-sum workspace the channel reductions below need.
+SEG_API long seg_chan_workspace_floats(long M, int C) {
+  const int rpb = rows_per_block_for(M);
+  return (long)seg_cdiv(M, rpb) * 2 * C;
+}
+
+// Train-mode BN statistics: fills mean/invstd/scale/shift ([C] each) and updates
+// the running buffers (skipped when running_mean is null) and num_batches_tracked.
+SEG_API int seg_bn_stats(const float* y, long ldy, long M, int C, const float* gamma, const float* beta, float eps,
+                         float momentum, float* running_mean, float* running_var, long long* num_batches_tracked,
+                         float* work, float* mean, float* invstd, float* scale, float* shift, hipStream_t stream) {
+  if ((C & 3) || (ldy & 3) || M < 1) return (int)hipErrorInvalidValue;
+  const int rpb = rows_per_block_for(M);
+  const int nblk = seg_cdiv(M, rpb);
+  hipLaunchKernelGGL(chan_partial_kernel<0>, dim3(nblk), dim3(256), 0, stream, y, ldy, nullptr, 0L, (int)M, C,
+                     nullptr, nullptr, nullptr, 0, work, rpb);
+  hipLaunchKernelGGL(bn_finalize_kernel, dim3(seg_cdiv(C, 256)), dim3(256), 0, stream, work, nblk, y, M, C, gamma,
+                     beta, eps, momentum, running_mean, running_var, num_batches_tracked, mean, invstd, scale, shift);
+  SEG_RET_LAST();
+}
+
+SEG_API int seg_bn_eval_coef(const float* gamma, const float* beta, const float* running_mean,
+                             const float* running_var, float eps, int C, float* scale, float* shift,
+                             hipStream_t stream) {
+  hipLaunchKernelGGL(bn_eval_coef_kernel, dim3(seg_cdiv(C, 256)), dim3(256), 0, stream, gamma, beta, running_mean,
+                     running_var, eps, C, scale, shift);
+  SEG_RET_LAST();
+}
+
+SEG_API int seg_bn_apply(const float* y, long ldy, long M, int C, const float* scale, const float* shift, int act,
+                         const float* res, long ldres, float* out, long ldout, hipStream_t stream) {
+  if ((C & 3) || (ldy & 3) || (ldout & 3) || (res && (ldres & 3))) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(bn_apply_kernel, dim3(ew_grid(M * (C / 4))), dim3(256), 0, stream, y, ldy, M, C, scale, shift,
+                     act, res, ldres, out, ldout);
+  SEG_RET_LAST();
+}
+
+// Train-mode BN backward through the activation: writes dgamma/dbeta ([C]) and
+// dy = d(conv output).  `work` >= seg_chan_workspace_floats(M,C) + 3*C floats.
+SEG_API int seg_bn_backward(const float* da, long ldda, const float* y, long ldy, long M, int C, const float* gamma,
+                            const float* mean, const float* invstd, const float* scale, const float* shift, int act,
+                            float* dgamma, float* dbeta, float* work, float* dy, long lddy, hipStream_t stream) {
+  if ((C & 3) || (ldy & 3) || (ldda & 3) || (lddy & 3)) return (int)hipErrorInvalidValue;
+  const int rpb = rows_per_block_for(M);
+  const int nblk = seg_cdiv(M, rpb);
+  float* coef = work + (long)nblk * 2 * C;
+  hipLaunchKernelGGL(chan_partial_kernel<1>, dim3(nblk), dim3(256), 0, stream, y, ldy, da, ldda, (int)M, C, scale,
+                     shift, mean, act, work, rpb);
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(seg_cdiv(C, 256)), dim3(256), 0, stream, work, nblk, M, C, gamma,
+                     invstd, dgamma, dbeta, coef);
+  hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(ew_grid(M * (C / 4))), dim3(256), 0, stream, da, ldda, y, ldy, M, C,
+                     scale, shift, mean, act, coef, dy, lddy);
+  SEG_RET_LAST();
+}
+
+SEG_API int seg_bn_eval_backward(const float* da, long ldda, const float* y, long ldy, long M, int C,
+                                 const float* scale, const float* shift, int act, float* dy, long lddy,
+                                 hipStream_t stream) {
+  hipLaunchKernelGGL(bn_eval_bwd_kernel, dim3(ew_grid(M * (C / 4))), dim3(256), 0, stream, da, ldda, y, ldy, M, C,
+                     scale, shift, act, dy, lddy);
+  SEG_RET_LAST();
+}
+
+// out[c] (+)= sum_r y[r][c]  -- conv bias gradient.  `work` >= seg_chan_workspace_floats.
+SEG_API int seg_colsum(const float* y, long ldy, long M, int C, float* work, float* out, int accumulate,
+                       hipStream_t stream) {
+  if ((ldy & 3)) return (int)hipErrorInvalidValue;
+  const int C4 = (C + 3) & ~3;  // ld >= C4 is guaranteed by the buffer contract
+  const int rpb = rows_per_block_for(M);
+  const int nblk = seg_cdiv(M, rpb);
+  hipLaunchKernelGGL(chan_partial_kernel<2>, dim3(nblk), dim3(256), 0, stream, y, ldy, nullptr, 0L, (int)M, C4,
+                     nullptr, nullptr, nullptr, 0, work, rpb);
+  hipLaunchKernelGGL(colsum_finalize_kernel, dim3(seg_cdiv(C, 256)), dim3(256), 0, stream, work, nblk, C, C4, out,
+                     accumulate);
+  SEG_RET_LAST();
+}

@@ -1,0 +1,48 @@
+// Shared helpers for the segamd HIP kernels (gfx950 / CDNA4 only).
+//
+// Conventions used by every kernel in this directory:
+//   * activations are NHWC fp32; a "row" is one pixel, `ld` is the row stride in
+//     floats (>= channels, lets a producer write straight into a channel slice of a
+//     concat buffer -- the reference's torch.cat, src/unet.py:103, becomes free);
+//   * every entry point is `extern "C"`, takes plain pointers/ints and the caller's
+//     hipStream_t, never allocates, and returns the hipError_t of its launch(es);
+//   * wave = 64 lanes; block sizes are multiples of 64.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <algorithm>
+
+#define SEG_API extern "C" __attribute__((visibility("default")))
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+enum SegAct { SEG_ACT_NONE = 0, SEG_ACT_RELU = 1, SEG_ACT_RELU6 = 2 };
+
+__device__ __forceinline__ float seg_act(float z, int act) {
+  if (act == SEG_ACT_RELU) return z > 0.f ? z : 0.f;
+  if (act == SEG_ACT_RELU6) return fminf(fmaxf(z, 0.f), 6.f);
+  return z;
+}
+
+// Derivative mask of the activation at pre-activation value z.  Matches aten's
+// threshold_backward (ReLU, inplace => uses the result, y > 0) and
+// hardtanh_backward (ReLU6, 0 < y < 6, strict on both sides).
+__device__ __forceinline__ float seg_act_mask(float z, int act) {
+  if (act == SEG_ACT_RELU) return z > 0.f ? 1.f : 0.f;
+  if (act == SEG_ACT_RELU6) return (z > 0.f && z < 6.f) ? 1.f : 0.f;
+  return 1.f;
+}
+
+__device__ __forceinline__ f32x4 ld4(const float* p) { return *reinterpret_cast<const f32x4*>(p); }
+__device__ __forceinline__ void st4(float* p, f32x4 v) { *reinterpret_cast<f32x4*>(p) = v; }
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+static inline int seg_cdiv(long a, long b) { return (int)((a + b - 1) / b); }
+
+#define SEG_RET_LAST() return (int)hipGetLastError()

@@ -1,0 +1,254 @@
+// Implicit-GEMM convolution on the f32 matrix cores of gfx950.
+//
+// Replaces aten's conv2d for every non-depthwise conv of the hot path
+// (reference: src/unet.py:58,61 dense 3x3 of double_conv; src/unet.py:113,116
+// the 1x1 head; torchvision InvertedResidual expand/project 1x1 reached through
+// src/unet.py:15-19).  One kernel serves
+//   * forward:   out[p][co] = sum_{tap,ci} in[src(p,tap)][ci] * W[co][ci][tap] + bias[co]
+//   * data-grad: the same GEMM run over dY with the weights packed transposed and
+//                tap-flipped (seg_pack_conv_weight, mode 1) -- stride-1 convs only,
+//                which is every dense/pointwise conv in MobileNetV2UNet and UNet.
+//
+// GEMM view: M = N*Ho*Wo pixels, N = Cout, K = ks*ks*Cin (k = tap*Cin + ci).
+// Operands are staged through LDS m-major ([row][BK+4], 80-byte rows: the
+// ds_read_b128 lane groups land on 16 distinct 16-B slots) and fed to
+// v_mfma_f32_32x32x2_f32 (exact fp32, fmaf-chain numerics).  The K index of an
+// MFMA step is remapped so each lane reads 4 consecutive k from LDS with one
+// ds_read_b128: lane half h at step kk of sub-chunk ks carries k = 8ks + 4h + kk
+// for BOTH operands, which is all the MFMA needs to sum the right products.
+// Two LDS stages, register prefetch of the next K chunk, one barrier per chunk.
+#include "common.h"
+
+namespace {
+
+struct IgemmArgs {
+  const float* in; long ldin;
+  const float* wk; int ldk;      // packed weights [Cout][ldk], k contiguous
+  const float* bias;             // [Cout] or nullptr
+  const float* add; long ldadd;  // optional addend [M][ldadd] (may alias out)
+  float* out; long ldout;
+  float* stat_part;              // optional BN-stat partials [gridM][2][Cout] (unused: nullptr)
+  int N, H, W, Cin;
+  int Ho, Wo, Cout;
+  int stride, pad;
+  int K, M;
+};
+
+constexpr int BK = 16;
+constexpr int LDSR = BK + 4;  // LDS row stride (floats)
+
+template <int BM, int BN, int WM, int WN, int KS>
+__global__ __launch_bounds__(256) void igemm_conv_kernel(IgemmArgs a) {
+  constexpr int A_VEC = BM * BK / 4;  // float4 per stage
+  constexpr int B_VEC = BN * BK / 4;
+  constexpr int A_PER = (A_VEC + 255) / 256;
+  constexpr int B_PER = (B_VEC + 255) / 256;
+  constexpr int MI = WM / 32, NI = WN / 32;
+  constexpr int WAVES_N = BN / WN;
+  static_assert((BM / WM) * (BN / WN) == 4, "4 waves per block");
+
+  __shared__ __attribute__((aligned(16))) float As[2][BM * LDSR];
+  __shared__ __attribute__((aligned(16))) float Bs[2][BN * LDSR];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm0 = (wave / WAVES_N) * WM, wn0 = (wave % WAVES_N) * WN;
+  const int tiles_n = (a.Cout + BN - 1) / BN;
+  const int tn = blockIdx.x % tiles_n, tm = blockIdx.x / tiles_n;
+  const int m0 = tm * BM, n0 = tn * BN;
+
+  // Per-thread A rows: fixed across the K loop, decode the pixel once.
+  int a_row[A_PER], a_kq[A_PER], a_hi0[A_PER], a_wi0[A_PER];
+  long a_base[A_PER];
+  bool a_ok[A_PER];
+#pragma unroll
+  for (int i = 0; i < A_PER; ++i) {
+    const int idx = tid + i * 256;
+    a_row[i] = idx / (BK / 4);
+    a_kq[i] = idx % (BK / 4);
+    const int p = m0 + a_row[i];
+    a_ok[i] = (idx < A_VEC) && (p < a.M);
+    const int pp = a_ok[i] ? p : 0;
+    if (KS == 1) {
+      a_base[i] = (long)pp * a.ldin;
+      a_hi0[i] = a_wi0[i] = 0;
+    } else {
+      const int hw = a.Ho * a.Wo;
+      const int n = pp / hw, rem = pp - n * hw;
+      const int ho = rem / a.Wo, wo = rem - ho * a.Wo;
+      a_base[i] = (long)n * a.H * a.W;
+      a_hi0[i] = ho * a.stride - a.pad;
+      a_wi0[i] = wo * a.stride - a.pad;
+    }
+  }
+
+  f32x4 ra[A_PER], rb[B_PER];
+  auto load_tiles = [&](int k0) {
+#pragma unroll
+    for (int i = 0; i < A_PER; ++i) {
+      const int k = k0 + a_kq[i] * 4;
+      f32x4 v = {0.f, 0.f, 0.f, 0.f};
+      if (a_ok[i] && k < a.K) {
+        if (KS == 1) {
+          v = ld4(a.in + a_base[i] + k);
+        } else {
+          const int tap = k / a.Cin, ci = k - tap * a.Cin;
+          const int ky = tap / KS, kx = tap - ky * KS;
+          const int hi = a_hi0[i] + ky, wi = a_wi0[i] + kx;
+          if ((unsigned)hi < (unsigned)a.H && (unsigned)wi < (unsigned)a.W)
+            v = ld4(a.in + (a_base[i] + (long)hi * a.W + wi) * a.ldin + ci);
+        }
+      }
+      ra[i] = v;
+    }
+#pragma unroll
+    for (int i = 0; i < B_PER; ++i) {
+      const int idx = tid + i * 256;
+      const int row = idx / (BK / 4), kq = idx % (BK / 4);
+      const int co = n0 + row, k = k0 + kq * 4;
+      f32x4 v = {0.f, 0.f, 0.f, 0.f};
+      if (idx < B_VEC && co < a.Cout && k < a.K) v = ld4(a.wk + (long)co * a.ldk + k);
+      rb[i] = v;
+    }
+  };
+  auto store_tiles = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < A_PER; ++i) {
+      const int idx = tid + i * 256;
+      if (idx < A_VEC) st4(&As[buf][a_row[i] * LDSR + a_kq[i] * 4], ra[i]);
+    }
+#pragma unroll
+    for (int i = 0; i < B_PER; ++i) {
+      const int idx = tid + i * 256;
+      if (idx < B_VEC) st4(&Bs[buf][(idx / (BK / 4)) * LDSR + (idx % (BK / 4)) * 4], rb[i]);
+    }
+  };
+
+  f32x16 acc[MI][NI];
+#pragma unroll
+  for (int mi = 0; mi < MI; ++mi)
+#pragma unroll
+    for (int ni = 0; ni < NI; ++ni)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[mi][ni][r] = 0.f;
+
+  const int nk = (a.K + BK - 1) / BK;
+  load_tiles(0);
+  store_tiles(0);
+  __syncthreads();
+
+  const int lrow = lane & 31, lk = (lane >> 5) * 4;
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < nk) load_tiles((kt + 1) * BK);
+#pragma unroll
+    for (int ks = 0; ks < BK / 8; ++ks) {
+      f32x4 af[MI], bf[NI];
+#pragma unroll
+      for (int mi = 0; mi < MI; ++mi) af[mi] = ld4(&As[cur][(wm0 + mi * 32 + lrow) * LDSR + ks * 8 + lk]);
+#pragma unroll
+      for (int ni = 0; ni < NI; ++ni) bf[ni] = ld4(&Bs[cur][(wn0 + ni * 32 + lrow) * LDSR + ks * 8 + lk]);
+#pragma unroll
+      for (int kk = 0; kk < 4; ++kk)
+#pragma unroll
+        for (int mi = 0; mi < MI; ++mi)
+#pragma unroll
+          for (int ni = 0; ni < NI; ++ni)
+            acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[mi][kk], bf[ni][kk], acc[mi][ni], 0, 0, 0);
+    }
+    if (kt + 1 < nk) store_tiles(cur ^ 1);
+    __syncthreads();
+  }
+
+  // Epilogue: C layout of 32x32 f32 MFMA: col = lane&31, row = (r&3) + 8(r>>2) + 4(lane>>5).
+#pragma unroll
+  for (int ni = 0; ni < NI; ++ni) {
+    const int col = n0 + wn0 + ni * 32 + lrow;
+    if (col >= a.Cout) continue;
+    const float b = a.bias ? a.bias[col] : 0.f;
+#pragma unroll
+    for (int mi = 0; mi < MI; ++mi) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = m0 + wm0 + mi * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+        if (row < a.M) {
+          float v = acc[mi][ni][r] + b;
+          if (a.add) v += a.add[(long)row * a.ldadd + col];
+          a.out[(long)row * a.ldout + col] = v;
+        }
+      }
+    }
+  }
+}
+
+template <int BM, int BN, int WM, int WN>
+int launch_igemm(const IgemmArgs& a, int ks, hipStream_t s) {
+  const int grid = seg_cdiv(a.M, BM) * seg_cdiv(a.Cout, BN);
+  if (ks == 1)
+    hipLaunchKernelGGL((igemm_conv_kernel<BM, BN, WM, WN, 1>), dim3(grid), dim3(256), 0, s, a);
+  else
+    hipLaunchKernelGGL((igemm_conv_kernel<BM, BN, WM, WN, 3>), dim3(grid), dim3(256), 0, s, a);
+  SEG_RET_LAST();
+}
+
+}  // namespace
+
+// out = conv(in, W) (+bias) (+add).  `wk` is the packed weight of seg_pack_conv_weight
+// ([Cout][ldk], k = tap*Cin + ci).  ks in {1,3}; ks == 1 requires stride 1, pad 0.
+// Cin, ldin, ldk must be multiples of 4 and `in`/`wk` 16-byte aligned.
+SEG_API int seg_conv_igemm(const float* in, long ldin, int N, int H, int W, int Cin,
+                           const float* wk, int ldk, const float* bias,
+                           float* out, long ldout, int Ho, int Wo, int Cout,
+                           int ks, int stride, int pad,
+                           const float* add, long ldadd, hipStream_t stream) {
+  if ((Cin & 3) || (ldin & 3) || (ldk & 3) || (ks != 1 && ks != 3)) return (int)hipErrorInvalidValue;
+  if (ks == 1 && (stride != 1 || pad != 0 || Ho != H || Wo != W)) return (int)hipErrorInvalidValue;
+  IgemmArgs a;
+  a.in = in; a.ldin = ldin; a.wk = wk; a.ldk = ldk; a.bias = bias;
+  a.add = add; a.ldadd = ldadd; a.out = out; a.ldout = ldout; a.stat_part = nullptr;
+  a.N = N; a.H = H; a.W = W; a.Cin = Cin; a.Ho = Ho; a.Wo = Wo; a.Cout = Cout;
+  a.stride = stride; a.pad = pad; a.K = ks * ks * Cin; a.M = N * Ho * Wo;
+  if (a.M == 0 || Cout == 0) return 0;
+  // Tile choice: widest N tile that covers Cout; shrink M tile while the grid
+  // is too small to put >= 2 blocks on each of the 256 CUs.
+  if (Cout <= 32) return launch_igemm<128, 32, 32, 32>(a, ks, stream);
+  if (Cout <= 64) {
+    if ((long)seg_cdiv(a.M, 128) * seg_cdiv(Cout, 64) >= 512) return launch_igemm<128, 64, 64, 32>(a, ks, stream);
+    return launch_igemm<64, 64, 32, 32>(a, ks, stream);
+  }
+  if ((long)seg_cdiv(a.M, 128) * seg_cdiv(Cout, 128) >= 512) return launch_igemm<128, 128, 64, 64>(a, ks, stream);
+  if ((long)seg_cdiv(a.M, 64) * seg_cdiv(Cout, 128) >= 512) return launch_igemm<64, 128, 32, 64>(a, ks, stream);
+  return launch_igemm<64, 64, 32, 32>(a, ks, stream);
+}
+
+// Pack a PyTorch conv weight w[Cout][Cin][ks][ks] for seg_conv_igemm.
+//   mode 0 (forward):   wk[co][tap*Cin + ci]          = w[co][ci][tap]
+//   mode 1 (data-grad): wk[ci][tap*Cout + co]          = w[co][ci][ks*ks-1-tap]
+// In mode 1 the K run of each tap is padded to kin_pad >= Cout channels (zeros),
+// so a data-gradient whose dY has a padded channel count (the C=10 head) stays
+// float4-aligned.  Rows are zero-padded from taps*kin to ldk.
+__global__ void pack_conv_weight_kernel(const float* __restrict__ w, float* __restrict__ wk,
+                                        int Cout, int Cin, int taps, int ldk, int mode, int kin_pad) {
+  const int rows = mode == 0 ? Cout : Cin;
+  const int kin = mode == 0 ? Cin : kin_pad;
+  const long total = (long)rows * ldk;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const int r = (int)(i / ldk), k = (int)(i - (long)r * ldk);
+    float v = 0.f;
+    if (k < taps * kin) {
+      const int tap = k / kin, c = k - tap * kin;
+      if (mode == 0) v = w[((long)r * Cin + c) * taps + tap];
+      else if (c < Cout) v = w[((long)c * Cin + r) * taps + (taps - 1 - tap)];
+    }
+    wk[i] = v;
+  }
+}
+
+SEG_API int seg_pack_conv_weight(const float* w, float* wk, int Cout, int Cin, int ks, int ldk, int mode,
+                                 int kin_pad, hipStream_t stream) {
+  if (mode == 1 && kin_pad < Cout) return (int)hipErrorInvalidValue;
+  if (ldk < ks * ks * (mode == 0 ? Cin : kin_pad)) return (int)hipErrorInvalidValue;
+  const long total = (long)(mode == 0 ? Cout : Cin) * ldk;
+  const int grid = (int)std::min<long>(seg_cdiv(total, 256), 4096);
+  hipLaunchKernelGGL(pack_conv_weight_kernel, dim3(grid), dim3(256), 0, stream, w, wk, Cout, Cin, ks * ks, ldk, mode, kin_pad);
+  SEG_RET_LAST();
+}

@@ -1,0 +1,180 @@
+// Per-pixel cross-entropy fused with the model's final align_corners=True
+// bilinear x2 upsample.
+//
+// Reference: criterion = nn.CrossEntropyLoss() (main.py:99) applied to the model
+// output (src/train.py:37), whose last op is final_upsample (src/unet.py:30,49).
+// Semantics: loss = sum_{valid p} (logsumexp(z_p) - z_p[y_p]) / #valid,
+// weight=None, ignore_index=-100, label_smoothing=0; labels are int64.
+// d loss / d z_p = g * (softmax(z_p) - onehot(y_p)) / #valid  (g = upstream grad).
+//
+// The full-resolution logits z_p are never stored: each kernel recomputes them
+// from the NHWC low-resolution logits (4 taps x C), which stay L2-resident.
+// The loss reduction is deterministic: per-block partials, then one fp64 pass.
+#include "common.h"
+
+namespace {
+
+struct LinAC {
+  int i0, i1;
+  float l0, l1;
+};
+
+__device__ __forceinline__ LinAC lin_ac(int dst, int in, float scale) {
+  const float src = scale * (float)dst;
+  int i0 = (int)floorf(src);
+  if (i0 > in - 1) i0 = in - 1;
+  LinAC r;
+  r.i0 = i0;
+  r.i1 = i0 + (i0 < in - 1 ? 1 : 0);
+  r.l1 = fminf(fmaxf(src - (float)i0, 0.f), 1.f);
+  r.l0 = 1.f - r.l1;
+  return r;
+}
+
+constexpr int CMAX = 32;
+
+// Recompute the C full-res logits of pixel (n, r, s).
+__device__ __forceinline__ void full_res_logits(const float* __restrict__ low, long ld, int H, int W, int C, int n,
+                                                int r, int s, float sh, float sw, float* z) {
+  const LinAC lh = lin_ac(r, H, sh), lw = lin_ac(s, W, sw);
+  const float* base = low + (long)n * H * W * ld;
+  const float* p00 = base + ((long)lh.i0 * W + lw.i0) * ld;
+  const float* p01 = base + ((long)lh.i0 * W + lw.i1) * ld;
+  const float* p10 = base + ((long)lh.i1 * W + lw.i0) * ld;
+  const float* p11 = base + ((long)lh.i1 * W + lw.i1) * ld;
+  for (int c = 0; c < C; c += 4) {
+    const f32x4 o = lh.l0 * (lw.l0 * ld4(p00 + c) + lw.l1 * ld4(p01 + c)) +
+                    lh.l1 * (lw.l0 * ld4(p10 + c) + lw.l1 * ld4(p11 + c));
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      if (c + j < CMAX) z[c + j] = o[j];
+  }
+}
+
+__global__ __launch_bounds__(256) void ce_up_loss_kernel(const float* __restrict__ low, long ld, int N, int H, int W,
+                                                         int C, const long long* __restrict__ labels, int Ho, int Wo,
+                                                         float sh, float sw, int ignore_index,
+                                                         float* __restrict__ part) {
+  __shared__ float red_l[4], red_c[4];
+  const long total = (long)N * Ho * Wo;
+  float lsum = 0.f, cnt = 0.f;
+  for (long p = blockIdx.x * (long)blockDim.x + threadIdx.x; p < total; p += (long)gridDim.x * blockDim.x) {
+    const long long y = labels[p];
+    if (y == ignore_index) continue;
+    const int n = (int)(p / ((long)Ho * Wo));
+    const int rem = (int)(p - (long)n * Ho * Wo);
+    const int r = rem / Wo, s = rem - r * Wo;
+    float z[CMAX];
+    full_res_logits(low, ld, H, W, C, n, r, s, sh, sw, z);
+    float m = z[0];
+    for (int c = 1; c < C; ++c) m = fmaxf(m, z[c]);
+    float se = 0.f, zy = 0.f;
+    for (int c = 0; c < C; ++c) {
+      se += expf(z[c] - m);
+      if (c == (int)y) zy = z[c];
+    }
+    lsum += m + logf(se) - zy;
+    cnt += 1.f;
+  }
+  lsum = wave_sum(lsum);
+  cnt = wave_sum(cnt);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  if (lane == 0) { red_l[wave] = lsum; red_c[wave] = cnt; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    part[2 * blockIdx.x] = red_l[0] + red_l[1] + red_l[2] + red_l[3];
+    part[2 * blockIdx.x + 1] = red_c[0] + red_c[1] + red_c[2] + red_c[3];
+  }
+}
+
+// out[0] = mean loss, out[1] = #valid pixels (as float)
+__global__ void ce_finalize_kernel(const float* __restrict__ part, int nblk, float* out) {
+  double l = 0.0, c = 0.0;
+  for (int b = threadIdx.x; b < nblk; b += 64) {
+    l += part[2 * b];
+    c += part[2 * b + 1];
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    l += __shfl_xor(l, o, 64);
+    c += __shfl_xor(c, o, 64);
+  }
+  if (threadIdx.x == 0) {
+    out[0] = (float)(l / c);  // 0/0 = nan when every pixel is ignored, as aten
+    out[1] = (float)c;
+  }
+}
+
+// dhigh[p][c] = g * (softmax(z_p)[c] - [c == y_p]) / count, NHWC (ld >= round4(C)).
+__global__ __launch_bounds__(256) void ce_up_grad_kernel(const float* __restrict__ low, long ld, int N, int H, int W,
+                                                         int C, const long long* __restrict__ labels, int Ho, int Wo,
+                                                         float sh, float sw, int ignore_index,
+                                                         const float* __restrict__ gout, const float* __restrict__ stats,
+                                                         float* __restrict__ dhigh, long ldh) {
+  const long total = (long)N * Ho * Wo;
+  const float scale = gout[0] / stats[1];
+  for (long p = blockIdx.x * (long)blockDim.x + threadIdx.x; p < total; p += (long)gridDim.x * blockDim.x) {
+    const long long y = labels[p];
+    float* d = dhigh + p * ldh;
+    if (y == ignore_index) {
+      for (int c = 0; c < C; c += 4) st4(d + c, f32x4{0.f, 0.f, 0.f, 0.f});
+      continue;
+    }
+    const int n = (int)(p / ((long)Ho * Wo));
+    const int rem = (int)(p - (long)n * Ho * Wo);
+    const int r = rem / Wo, s = rem - r * Wo;
+    float z[CMAX];
+    full_res_logits(low, ld, H, W, C, n, r, s, sh, sw, z);
+    float m = z[0];
+    for (int c = 1; c < C; ++c) m = fmaxf(m, z[c]);
+    float se = 0.f;
+    for (int c = 0; c < C; ++c) {
+      z[c] = expf(z[c] - m);
+      se += z[c];
+    }
+    const float inv = 1.f / se;
+    for (int c = 0; c < C; c += 4) {
+      f32x4 o;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int cc = c + j;
+        o[j] = cc < C ? scale * (z[cc] * inv - (cc == (int)y ? 1.f : 0.f)) : 0.f;
+      }
+      st4(d + c, o);
+    }
+  }
+}
+
+int loss_blocks(long total) { return (int)std::min<long>(seg_cdiv(total, 256), 2048); }
+
+}  // namespace
+
+SEG_API long seg_ce_workspace_floats(long pixels) { return 2L * loss_blocks(pixels); }
+
+// Mean CE of bilinear_ac_true_x(Ho,Wo)(low) against labels.  out2[0] = loss,
+// out2[1] = number of non-ignored pixels.  `work` >= seg_ce_workspace_floats(N*Ho*Wo).
+SEG_API int seg_ce_upsample_loss(const float* low, long ld, int N, int H, int W, int C, const long long* labels, int Ho,
+                                 int Wo, int ignore_index, float* work, float* out2, hipStream_t stream) {
+  if ((ld & 3) || C > CMAX || C < 1) return (int)hipErrorInvalidValue;
+  const long total = (long)N * Ho * Wo;
+  const int nb = loss_blocks(total);
+  const float sh = Ho > 1 ? (float)(H - 1) / (float)(Ho - 1) : 0.f;
+  const float sw = Wo > 1 ? (float)(W - 1) / (float)(Wo - 1) : 0.f;
+  hipLaunchKernelGGL(ce_up_loss_kernel, dim3(nb), dim3(256), 0, stream, low, ld, N, H, W, C, labels, Ho, Wo, sh, sw,
+                     ignore_index, work);
+  hipLaunchKernelGGL(ce_finalize_kernel, dim3(1), dim3(64), 0, stream, work, nb, out2);
+  SEG_RET_LAST();
+}
+
+// Full-resolution logit gradient (NHWC, ldh >= round4(C)); follow with
+// seg_upsample_bwd(nchw_grad = 0, ac = 1) to reach the low-res logits.
+SEG_API int seg_ce_upsample_grad(const float* low, long ld, int N, int H, int W, int C, const long long* labels, int Ho,
+                                 int Wo, int ignore_index, const float* grad_out, const float* stats, float* dhigh,
+                                 long ldh, hipStream_t stream) {
+  if ((ld & 3) || (ldh & 3) || C > CMAX || C < 1) return (int)hipErrorInvalidValue;
+  const long total = (long)N * Ho * Wo;
+  const float sh = Ho > 1 ? (float)(H - 1) / (float)(Ho - 1) : 0.f;
+  const float sw = Wo > 1 ? (float)(W - 1) / (float)(Wo - 1) : 0.f;
+  hipLaunchKernelGGL(ce_up_grad_kernel, dim3((int)std::min<long>(seg_cdiv(total, 256), 8192)), dim3(256), 0, stream,
+                     low, ld, N, H, W, C, labels, Ho, Wo, sh, sw, ignore_index, grad_out, stats, dhigh, ldh);
+  SEG_RET_LAST();
+}

@@ -1,0 +1,261 @@
+// Bilinear resampling and 2x2 max-pooling, NHWC.
+//
+//  * nn.Upsample(scale_factor=2, mode='bilinear') (align_corners=False) of every
+//    decoder `up` block, src/unet.py:97,101 -- the result is written straight
+//    into the channel slice [Cskip, Cskip+C) of the concat buffer that
+//    torch.cat([x2, x1], dim=1) (src/unet.py:103, skip FIRST) would build.
+//  * nn.Upsample(scale_factor=2, mode='bilinear', align_corners=True), the final
+//    upsample of MobileNetV2UNet (src/unet.py:30,49): NHWC low-res logits ->
+//    NCHW full-res logits (the layout the reference returns).
+//  * nn.MaxPool2d(2) of UNet's `down` (src/unet.py:85).
+// Source-index arithmetic follows aten's CPU upsample_bilinear2d in float:
+//   align_corners: src = scale*dst, scale = (in-1)/(out-1)
+//   otherwise:     src = max(scale*(dst+0.5)-0.5, 0), scale = 1/scale_factor
+//   i0 = min(floor(src), in-1), i1 = i0 + (i0 < in-1), l1 = src - i0, l0 = 1 - l1.
+// Backward passes are gathers (every input pixel sums the few output pixels that
+// sampled it, recomputing the forward's indices exactly): no atomics,
+// bitwise reproducible.
+#include "common.h"
+
+namespace {
+
+struct Lin {
+  int i0, i1;
+  float l0, l1;
+};
+
+__device__ __forceinline__ Lin lin_index(int dst, int in, float scale, int ac) {
+  float src = ac ? scale * (float)dst : fmaxf(scale * ((float)dst + 0.5f) - 0.5f, 0.f);
+  int i0 = (int)floorf(src);
+  if (i0 > in - 1) i0 = in - 1;
+  Lin r;
+  r.i0 = i0;
+  r.i1 = i0 + (i0 < in - 1 ? 1 : 0);
+  r.l1 = fminf(fmaxf(src - (float)i0, 0.f), 1.f);
+  r.l0 = 1.f - r.l1;
+  return r;
+}
+
+// Weight with which output index `dst` samples input index `i`.
+__device__ __forceinline__ float lin_weight(int dst, int i, int in, float scale, int ac) {
+  const Lin l = lin_index(dst, in, scale, ac);
+  return (l.i0 == i ? l.l0 : 0.f) + (l.i1 == i ? l.l1 : 0.f);
+}
+
+// Output range [lo, hi] that can reference input index i.
+__device__ __forceinline__ void dst_range(int i, int in, int out, float scale, int ac, int* lo, int* hi) {
+  // src in [i-1, i+1) maps to dst in about [(i-1)/scale, (i+1)/scale); pad by 2.
+  const float inv = 1.f / scale;
+  float a = ac ? (float)(i - 1) * inv : ((float)(i - 1) + 0.5f) * inv - 0.5f;
+  float b = ac ? (float)(i + 1) * inv : ((float)(i + 1) + 0.5f) * inv - 0.5f;
+  int l = (int)floorf(a) - 2, h = (int)ceilf(b) + 2;
+  *lo = l < 0 ? 0 : l;
+  *hi = h > out - 1 ? out - 1 : h;
+}
+
+__global__ void up_fwd_nhwc_kernel(const float* __restrict__ in, long ldin, int N, int H, int W, int C,
+                                   float* __restrict__ out, long ldout, int Ho, int Wo, float sh, float sw, int ac) {
+  const int CG = C >> 2;
+  const long total = (long)N * Ho * Wo * CG;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const long p = i / CG;
+    const int c = (int)(i - p * CG) * 4;
+    const int n = (int)(p / ((long)Ho * Wo));
+    const int rem = (int)(p - (long)n * Ho * Wo);
+    const int r = rem / Wo, s = rem - r * Wo;
+    const Lin lh = lin_index(r, H, sh, ac), lw = lin_index(s, W, sw, ac);
+    const float* base = in + (long)n * H * W * ldin;
+    const f32x4 v00 = ld4(base + ((long)lh.i0 * W + lw.i0) * ldin + c);
+    const f32x4 v01 = ld4(base + ((long)lh.i0 * W + lw.i1) * ldin + c);
+    const f32x4 v10 = ld4(base + ((long)lh.i1 * W + lw.i0) * ldin + c);
+    const f32x4 v11 = ld4(base + ((long)lh.i1 * W + lw.i1) * ldin + c);
+    const f32x4 o = lh.l0 * (lw.l0 * v00 + lw.l1 * v01) + lh.l1 * (lw.l0 * v10 + lw.l1 * v11);
+    st4(out + p * ldout + c, o);
+  }
+}
+
+// d_in[n][h][w][c] = sum_{r,s} w_h(r,h) w_w(s,w) d_out[n][r][s][c]
+// LAYOUT 0: d_out NHWC [N*Ho*Wo][ldout];  LAYOUT 1: d_out NCHW [N][C][Ho][Wo].
+template <int LAYOUT>
+__global__ void up_bwd_kernel(const float* __restrict__ dout, long ldout, int N, int Ho, int Wo, int C,
+                              float* __restrict__ din, long ldin, int H, int W, float sh, float sw, int ac,
+                              int accumulate) {
+  const int CG = (C + 3) >> 2;
+  const long total = (long)N * H * W * CG;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const long q = i / CG;
+    const int c = (int)(i - q * CG) * 4;
+    const int n = (int)(q / ((long)H * W));
+    const int rem = (int)(q - (long)n * H * W);
+    const int h = rem / W, w = rem - h * W;
+    int rlo, rhi, slo, shi;
+    dst_range(h, H, Ho, sh, ac, &rlo, &rhi);
+    dst_range(w, W, Wo, sw, ac, &slo, &shi);
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    for (int r = rlo; r <= rhi; ++r) {
+      const float wr = lin_weight(r, h, H, sh, ac);
+      if (wr == 0.f) continue;
+      for (int s = slo; s <= shi; ++s) {
+        const float ws = lin_weight(s, w, W, sw, ac);
+        if (ws == 0.f) continue;
+        const float wt = wr * ws;
+        if (LAYOUT == 0) {
+          acc += wt * ld4(dout + (((long)n * Ho + r) * Wo + s) * ldout + c);
+        } else {
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            if (c + j < C) acc[j] += wt * dout[(((long)n * C + c + j) * Ho + r) * Wo + s];
+        }
+      }
+    }
+    float* dst = din + q * ldin + c;
+    if (accumulate) acc += ld4(dst);
+    st4(dst, acc);
+  }
+}
+
+// NHWC low-res -> NCHW full-res (the model's returned logits).
+__global__ void up_fwd_to_nchw_kernel(const float* __restrict__ in, long ldin, int N, int H, int W, int C,
+                                      float* __restrict__ out, int Ho, int Wo, float sh, float sw, int ac) {
+  const long total = (long)N * Ho * Wo;
+  for (long p = blockIdx.x * (long)blockDim.x + threadIdx.x; p < total; p += (long)gridDim.x * blockDim.x) {
+    const int n = (int)(p / ((long)Ho * Wo));
+    const int rem = (int)(p - (long)n * Ho * Wo);
+    const int r = rem / Wo, s = rem - r * Wo;
+    const Lin lh = lin_index(r, H, sh, ac), lw = lin_index(s, W, sw, ac);
+    const float* base = in + (long)n * H * W * ldin;
+    for (int c = 0; c < C; c += 4) {
+      const f32x4 v00 = ld4(base + ((long)lh.i0 * W + lw.i0) * ldin + c);
+      const f32x4 v01 = ld4(base + ((long)lh.i0 * W + lw.i1) * ldin + c);
+      const f32x4 v10 = ld4(base + ((long)lh.i1 * W + lw.i0) * ldin + c);
+      const f32x4 v11 = ld4(base + ((long)lh.i1 * W + lw.i1) * ldin + c);
+      const f32x4 o = lh.l0 * (lw.l0 * v00 + lw.l1 * v01) + lh.l1 * (lw.l0 * v10 + lw.l1 * v11);
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        if (c + j < C) out[(((long)n * C + c + j) * Ho + r) * Wo + s] = o[j];
+    }
+  }
+}
+
+// MaxPool2d(2), floor mode: first maximum in (0,0),(0,1),(1,0),(1,1) order, NaN wins
+// (aten CPU max_pool2d: `if (val > maxval || isnan(val))`).
+__device__ __forceinline__ int pool_argmax(float v0, float v1, float v2, float v3, float* m) {
+  float best = v0;
+  int arg = 0;
+  if (v1 > best || isnan(v1)) { best = v1; arg = 1; }
+  if (v2 > best || isnan(v2)) { best = v2; arg = 2; }
+  if (v3 > best || isnan(v3)) { best = v3; arg = 3; }
+  *m = best;
+  return arg;
+}
+
+__global__ void maxpool_fwd_kernel(const float* __restrict__ in, long ldin, int N, int H, int W, int C,
+                                   float* __restrict__ out, long ldout) {
+  const int Ho = H / 2, Wo = W / 2, CG = C >> 2;
+  const long total = (long)N * Ho * Wo * CG;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const long p = i / CG;
+    const int c = (int)(i - p * CG) * 4;
+    const int n = (int)(p / ((long)Ho * Wo));
+    const int rem = (int)(p - (long)n * Ho * Wo);
+    const int r = rem / Wo, s = rem - r * Wo;
+    const float* b = in + (((long)n * H + 2 * r) * W + 2 * s) * ldin + c;
+    const f32x4 a0 = ld4(b), a1 = ld4(b + ldin), a2 = ld4(b + (long)W * ldin), a3 = ld4(b + (long)W * ldin + ldin);
+    f32x4 o;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      float m;
+      pool_argmax(a0[j], a1[j], a2[j], a3[j], &m);
+      o[j] = m;
+    }
+    st4(out + p * ldout + c, o);
+  }
+}
+
+__global__ void maxpool_bwd_kernel(const float* __restrict__ in, long ldin, const float* __restrict__ dout,
+                                   long lddout, int N, int H, int W, int C, float* __restrict__ din, long lddin,
+                                   int accumulate) {
+  const int Ho = H / 2, Wo = W / 2, CG = C >> 2;
+  const long total = (long)N * Ho * Wo * CG;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const long p = i / CG;
+    const int c = (int)(i - p * CG) * 4;
+    const int n = (int)(p / ((long)Ho * Wo));
+    const int rem = (int)(p - (long)n * Ho * Wo);
+    const int r = rem / Wo, s = rem - r * Wo;
+    const long q0 = ((long)n * H + 2 * r) * W + 2 * s;
+    const long qs[4] = {q0, q0 + 1, q0 + W, q0 + W + 1};
+    const f32x4 a0 = ld4(in + qs[0] * ldin + c), a1 = ld4(in + qs[1] * ldin + c);
+    const f32x4 a2 = ld4(in + qs[2] * ldin + c), a3 = ld4(in + qs[3] * ldin + c);
+    const f32x4 g = ld4(dout + p * lddout + c);
+    f32x4 o[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) o[k] = accumulate ? ld4(din + qs[k] * lddin + c) : f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      float m;
+      const int arg = pool_argmax(a0[j], a1[j], a2[j], a3[j], &m);
+      o[arg][j] += g[j];
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) st4(din + qs[k] * lddin + c, o[k]);
+  }
+}
+
+int ew_grid(long total) { return (int)std::min<long>(seg_cdiv(total, 256), 8192); }
+
+float up_scale(int in, int out, int ac) {
+  if (ac) return out > 1 ? (float)(in - 1) / (float)(out - 1) : 0.f;
+  return (float)in / (float)out;  // == 1/scale_factor for the exact 2x upsample
+}
+
+}  // namespace
+
+// Bilinear resize NHWC -> NHWC (strided), ac = align_corners.
+SEG_API int seg_upsample_fwd(const float* in, long ldin, int N, int H, int W, int C, float* out, long ldout, int Ho,
+                             int Wo, int ac, hipStream_t stream) {
+  if ((C & 3) || (ldin & 3) || (ldout & 3)) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(up_fwd_nhwc_kernel, dim3(ew_grid((long)N * Ho * Wo * (C / 4))), dim3(256), 0, stream, in, ldin, N,
+                     H, W, C, out, ldout, Ho, Wo, up_scale(H, Ho, ac), up_scale(W, Wo, ac), ac);
+  SEG_RET_LAST();
+}
+
+// Gradient of seg_upsample_fwd / seg_upsample_to_nchw.  nchw_grad = 1 when d_out is
+// the NCHW gradient of the model's returned logits.  d_in is NHWC (ldin >= round4(C)).
+SEG_API int seg_upsample_bwd(const float* dout, long ldout, int nchw_grad, int N, int Ho, int Wo, int C, float* din,
+                             long ldin, int H, int W, int ac, int accumulate, hipStream_t stream) {
+  if ((ldin & 3) || (!nchw_grad && (ldout & 3))) return (int)hipErrorInvalidValue;
+  const int grid = ew_grid((long)N * H * W * ((C + 3) / 4));
+  const float sh = up_scale(H, Ho, ac), sw = up_scale(W, Wo, ac);
+  if (nchw_grad)
+    hipLaunchKernelGGL(up_bwd_kernel<1>, dim3(grid), dim3(256), 0, stream, dout, ldout, N, Ho, Wo, C, din, ldin, H, W,
+                       sh, sw, ac, accumulate);
+  else
+    hipLaunchKernelGGL(up_bwd_kernel<0>, dim3(grid), dim3(256), 0, stream, dout, ldout, N, Ho, Wo, C, din, ldin, H, W,
+                       sh, sw, ac, accumulate);
+  SEG_RET_LAST();
+}
+
+SEG_API int seg_upsample_to_nchw(const float* in, long ldin, int N, int H, int W, int C, float* out, int Ho, int Wo,
+                                 int ac, hipStream_t stream) {
+  if (ldin & 3) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(up_fwd_to_nchw_kernel, dim3(ew_grid((long)N * Ho * Wo)), dim3(256), 0, stream, in, ldin, N, H, W,
+                     C, out, Ho, Wo, up_scale(H, Ho, ac), up_scale(W, Wo, ac), ac);
+  SEG_RET_LAST();
+}
+
+SEG_API int seg_maxpool2_fwd(const float* in, long ldin, int N, int H, int W, int C, float* out, long ldout,
+                             hipStream_t stream) {
+  if ((C & 3) || (ldin & 3) || (ldout & 3)) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(maxpool_fwd_kernel, dim3(ew_grid((long)N * (H / 2) * (W / 2) * (C / 4))), dim3(256), 0, stream,
+                     in, ldin, N, H, W, C, out, ldout);
+  SEG_RET_LAST();
+}
+
+SEG_API int seg_maxpool2_bwd(const float* in, long ldin, const float* dout, long lddout, int N, int H, int W, int C,
+                             float* din, long lddin, int accumulate, hipStream_t stream) {
+  if ((C & 3) || (ldin & 3) || (lddout & 3) || (lddin & 3) || (H & 1) || (W & 1)) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(maxpool_bwd_kernel, dim3(ew_grid((long)N * (H / 2) * (W / 2) * (C / 4))), dim3(256), 0, stream,
+                     in, ldin, dout, lddout, N, H, W, C, din, lddin, accumulate);
+  SEG_RET_LAST();
+}

@@ -1,0 +1,248 @@
+// Weight gradient of the implicit-GEMM convolutions on f32 MFMA.
+//
+// Replaces aten's convolution_backward weight path for the dense 3x3
+// (src/unet.py:58,61) and 1x1 convs (src/unet.py:113,116 and the torchvision
+// InvertedResidual expand/project convs reached through src/unet.py:15-19) --
+// 43 % of the reference CPU step together with the data gradient.
+//
+// GEMM view: C[co][n] = sum_p dY[p][co] * X[src(p, tap(n))][ci(n)],
+//   rows co (Cout), columns n = tap*Cin + ci (Nw = ks*ks*Cin), K = output pixels.
+// K is split over gridDim.y; each split writes its own fp32 partial slab and
+// seg_conv_wgrad_reduce sums the slabs in fixed order (bitwise reproducible, no
+// float atomics).  Both operands are staged k-major in LDS ([pixel][channel], the
+// natural NHWC order, so global reads are whole channel runs); the MFMA operand
+// read is one ds_read_b32 per lane, 32 consecutive floats per half-wave.
+#include "common.h"
+
+namespace {
+
+constexpr int BK = 16;
+
+struct WgradArgs {
+  const float* dy; long lddy;
+  const float* x; long ldx;
+  float* part;
+  int N, H, W, Cin, Ho, Wo, Cout, stride, pad;
+  int M, Nw, kchunk;
+};
+
+template <int BM, int BN, int WM, int WN, int KS>
+__global__ __launch_bounds__(256) void wgrad_kernel(WgradArgs a) {
+  constexpr int AR = BM + 4, BR = BN + 4;
+  constexpr int A_VEC = BK * BM / 4, B_VEC = BK * BN / 4;
+  constexpr int A_PER = (A_VEC + 255) / 256, B_PER = (B_VEC + 255) / 256;
+  constexpr int MI = WM / 32, NI = WN / 32, WAVES_N = BN / WN;
+  static_assert((BM / WM) * (BN / WN) == 4, "4 waves per block");
+
+  __shared__ __attribute__((aligned(16))) float As[2][BK * AR];
+  __shared__ __attribute__((aligned(16))) float Bs[2][BK * BR];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm0 = (wave / WAVES_N) * WM, wn0 = (wave % WAVES_N) * WN;
+  const int tiles_n = (a.Nw + BN - 1) / BN;
+  const int tn = blockIdx.x % tiles_n, tm = blockIdx.x / tiles_n;
+  const int co0 = tm * BM, n0 = tn * BN;
+  const int kbeg = blockIdx.y * a.kchunk;
+  const int kend = min(a.M, kbeg + a.kchunk);
+
+  // Fixed per-thread columns of the B (input) tile: decode tap / channel once.
+  int b_prow[B_PER], b_ci[B_PER], b_ky[B_PER], b_kx[B_PER];
+  bool b_ok[B_PER];
+  // Pixel cursor of each B load row (advanced by BK per K step).
+  int b_n[B_PER], b_ho[B_PER], b_wo[B_PER];
+#pragma unroll
+  for (int i = 0; i < B_PER; ++i) {
+    const int idx = tid + i * 256;
+    b_prow[i] = idx / (BN / 4);
+    const int ncol = n0 + (idx % (BN / 4)) * 4;
+    b_ok[i] = idx < B_VEC && ncol < a.Nw;
+    const int tap = b_ok[i] ? ncol / a.Cin : 0;
+    b_ci[i] = b_ok[i] ? ncol - tap * a.Cin : 0;
+    b_ky[i] = tap / KS;
+    b_kx[i] = tap - b_ky[i] * KS;
+    const int p = kbeg + b_prow[i];
+    const int hw = a.Ho * a.Wo;
+    b_n[i] = p / hw;
+    const int rem = p - b_n[i] * hw;
+    b_ho[i] = rem / a.Wo;
+    b_wo[i] = rem - b_ho[i] * a.Wo;
+  }
+
+  f32x4 ra[A_PER], rb[B_PER];
+  auto load_tiles = [&](int k0) {  // k0 = first pixel of this chunk
+#pragma unroll
+    for (int i = 0; i < A_PER; ++i) {
+      const int idx = tid + i * 256;
+      const int prow = idx / (BM / 4), c = co0 + (idx % (BM / 4)) * 4;
+      const int p = k0 + prow;
+      f32x4 v = {0.f, 0.f, 0.f, 0.f};
+      if (idx < A_VEC && p < kend && c < a.Cout) v = ld4(a.dy + (long)p * a.lddy + c);
+      ra[i] = v;
+    }
+#pragma unroll
+    for (int i = 0; i < B_PER; ++i) {
+      const int p = k0 + b_prow[i];
+      f32x4 v = {0.f, 0.f, 0.f, 0.f};
+      if (b_ok[i] && p < kend) {
+        if (KS == 1) {
+          v = ld4(a.x + (long)p * a.ldx + b_ci[i]);
+        } else {
+          const int hi = b_ho[i] * a.stride - a.pad + b_ky[i];
+          const int wi = b_wo[i] * a.stride - a.pad + b_kx[i];
+          if ((unsigned)hi < (unsigned)a.H && (unsigned)wi < (unsigned)a.W)
+            v = ld4(a.x + (((long)b_n[i] * a.H + hi) * a.W + wi) * a.ldx + b_ci[i]);
+        }
+      }
+      rb[i] = v;
+      if (KS != 1) {  // advance this row's pixel cursor by BK
+        int wo = b_wo[i] + BK, ho = b_ho[i], n = b_n[i];
+        while (wo >= a.Wo) { wo -= a.Wo; if (++ho >= a.Ho) { ho = 0; ++n; } }
+        b_wo[i] = wo; b_ho[i] = ho; b_n[i] = n;
+      }
+    }
+  };
+  auto store_tiles = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < A_PER; ++i) {
+      const int idx = tid + i * 256;
+      if (idx < A_VEC) st4(&As[buf][(idx / (BM / 4)) * AR + (idx % (BM / 4)) * 4], ra[i]);
+    }
+#pragma unroll
+    for (int i = 0; i < B_PER; ++i) {
+      const int idx = tid + i * 256;
+      if (idx < B_VEC) st4(&Bs[buf][(idx / (BN / 4)) * BR + (idx % (BN / 4)) * 4], rb[i]);
+    }
+  };
+
+  f32x16 acc[MI][NI];
+#pragma unroll
+  for (int mi = 0; mi < MI; ++mi)
+#pragma unroll
+    for (int ni = 0; ni < NI; ++ni)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[mi][ni][r] = 0.f;
+
+  const int lrow = lane & 31, lh = lane >> 5;
+  const int nk = (kend - kbeg + BK - 1) / BK;
+  if (nk > 0) {
+    load_tiles(kbeg);
+    store_tiles(0);
+    __syncthreads();
+    for (int kt = 0; kt < nk; ++kt) {
+      const int cur = kt & 1;
+      if (kt + 1 < nk) load_tiles(kbeg + (kt + 1) * BK);
+#pragma unroll
+      for (int kk = 0; kk < BK / 2; ++kk) {
+        float af[MI], bf[NI];
+#pragma unroll
+        for (int mi = 0; mi < MI; ++mi) af[mi] = As[cur][(2 * kk + lh) * AR + wm0 + mi * 32 + lrow];
+#pragma unroll
+        for (int ni = 0; ni < NI; ++ni) bf[ni] = Bs[cur][(2 * kk + lh) * BR + wn0 + ni * 32 + lrow];
+#pragma unroll
+        for (int mi = 0; mi < MI; ++mi)
+#pragma unroll
+          for (int ni = 0; ni < NI; ++ni)
+            acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[mi], bf[ni], acc[mi][ni], 0, 0, 0);
+      }
+      if (kt + 1 < nk) store_tiles(cur ^ 1);
+      __syncthreads();
+    }
+  }
+
+  float* slab = a.part + (long)blockIdx.y * a.Cout * a.Nw;
+#pragma unroll
+  for (int ni = 0; ni < NI; ++ni) {
+    const int col = n0 + wn0 + ni * 32 + lrow;
+    if (col >= a.Nw) continue;
+#pragma unroll
+    for (int mi = 0; mi < MI; ++mi)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = co0 + wm0 + mi * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+        if (row < a.Cout) slab[(long)row * a.Nw + col] = acc[mi][ni][r];
+      }
+  }
+}
+
+template <int BM, int BN, int WM, int WN>
+int launch_wgrad(const WgradArgs& a, int ks, int splits, hipStream_t s) {
+  dim3 grid(seg_cdiv(a.Cout, BM) * seg_cdiv(a.Nw, BN), splits);
+  if (ks == 1) hipLaunchKernelGGL((wgrad_kernel<BM, BN, WM, WN, 1>), grid, dim3(256), 0, s, a);
+  else hipLaunchKernelGGL((wgrad_kernel<BM, BN, WM, WN, 3>), grid, dim3(256), 0, s, a);
+  SEG_RET_LAST();
+}
+
+void wgrad_tiles(int Cout, int Nw, int* bm, int* bn) {
+  if (Cout >= 128) { *bm = 128; *bn = Nw >= 128 ? 128 : 32; }
+  else if (Cout >= 64) { *bm = 64; *bn = Nw >= 128 ? 128 : 64; }
+  else { *bm = 32; *bn = 128; }
+}
+
+}  // namespace
+
+// Number of K splits (partial slabs) seg_conv_wgrad will use; the caller provides
+// a workspace of splits * Cout * ks*ks*Cin floats.
+SEG_API int seg_conv_wgrad_splits(long M, int Cout, int Cin, int ks) {
+  const int Nw = ks * ks * Cin;
+  int bm, bn;
+  wgrad_tiles(Cout, Nw, &bm, &bn);
+  const long tiles = (long)seg_cdiv(Cout, bm) * seg_cdiv(Nw, bn);
+  long splits = (2048 + tiles - 1) / tiles;
+  const long max_by_k = std::max<long>(1, M / 256);  // >= 256 pixels per split
+  splits = std::min(splits, max_by_k);
+  splits = std::min<long>(splits, 256);
+  return (int)std::max<long>(1, splits);
+}
+
+// part[s][co][tap*Cin+ci] = sum over split s's pixels of dY[p][co] * X[src(p,tap)][ci].
+SEG_API int seg_conv_wgrad(const float* dy, long lddy, const float* x, long ldx,
+                           int N, int H, int W, int Cin, int Ho, int Wo, int Cout,
+                           int ks, int stride, int pad, float* part, int splits, hipStream_t stream) {
+  if ((Cin & 3) || (ldx & 3) || (lddy & 3) || (ks != 1 && ks != 3) || splits < 1) return (int)hipErrorInvalidValue;
+  if (ks == 1 && (stride != 1 || pad != 0)) return (int)hipErrorInvalidValue;
+  WgradArgs a;
+  a.dy = dy; a.lddy = lddy; a.x = x; a.ldx = ldx; a.part = part;
+  a.N = N; a.H = H; a.W = W; a.Cin = Cin; a.Ho = Ho; a.Wo = Wo; a.Cout = Cout;
+  a.stride = stride; a.pad = pad; a.M = N * Ho * Wo; a.Nw = ks * ks * Cin;
+  a.kchunk = seg_cdiv(seg_cdiv(a.M, splits), BK) * BK;
+  int bm, bn;
+  wgrad_tiles(Cout, a.Nw, &bm, &bn);
+  if (bm == 128 && bn == 128) return launch_wgrad<128, 128, 64, 64>(a, ks, splits, stream);
+  if (bm == 128) return launch_wgrad<128, 32, 32, 32>(a, ks, splits, stream);
+  if (bm == 64 && bn == 128) return launch_wgrad<64, 128, 32, 64>(a, ks, splits, stream);
+  if (bm == 64) return launch_wgrad<64, 64, 32, 32>(a, ks, splits, stream);
+  return launch_wgrad<32, 128, 32, 32>(a, ks, splits, stream);
+}
+
+// dW[co][ci][tap] (PyTorch layout) = sum_s part[s][co][tap*Cin + ci], fixed order.
+// Also serves the depthwise (part[s][tap][c] -> dW[c][0][tap], mode 1) and the
+// direct-conv stem (part[s][co][ci*taps+tap] -> identity order, mode 2) partials.
+__global__ void wgrad_reduce_kernel(const float* __restrict__ part, int splits, long slab,
+                                    float* __restrict__ dw, int Cout, int Cin, int taps, int mode, int accumulate) {
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < slab; i += (long)gridDim.x * blockDim.x) {
+    float s = 0.f;
+    for (int k = 0; k < splits; ++k) s += part[(long)k * slab + i];
+    long o;
+    if (mode == 0) {  // i = (co*taps + tap)*Cin + ci
+      const long co = i / ((long)taps * Cin);
+      const int r = (int)(i - co * taps * Cin);
+      const int tap = r / Cin, ci = r - tap * Cin;
+      o = (co * Cin + ci) * taps + tap;
+    } else if (mode == 1) {  // i = tap*C + c   (Cout == C, Cin == 1)
+      const int tap = (int)(i / Cout), c = (int)(i - (long)tap * Cout);
+      o = (long)c * taps + tap;
+    } else {
+      o = i;
+    }
+    dw[o] = accumulate ? dw[o] + s : s;
+  }
+}
+
+SEG_API int seg_conv_wgrad_reduce(const float* part, int splits, float* dw, int Cout, int Cin, int ks,
+                                  int mode, int accumulate, hipStream_t stream) {
+  const long slab = (long)Cout * Cin * ks * ks;
+  const int grid = (int)std::min<long>(seg_cdiv(slab, 256), 2048);
+  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(grid), dim3(256), 0, stream, part, splits, slab, dw,
+                     Cout, Cin, ks * ks, mode, accumulate);
+  SEG_RET_LAST();
+}

@@ -1,0 +1,95 @@
+"""ctypes binding of libsegamd.so -- the C-ABI declared in include/segamd.h.
+
+The library is REQUIRED: there is no CPU or eager-PyTorch fallback on the
+product path.  If the shared object is missing or fails to load, `lib()` raises.
+Every call returns a hipError_t; `check` turns a non-zero code into an exception.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+from .build import LIB_PATH
+
+_V = ctypes.c_void_p
+_I = ctypes.c_int
+_L = ctypes.c_long
+_F = ctypes.c_float
+
+# name -> (restype, argtypes); mirrors include/segamd.h one-to-one.
+PROTOTYPES = {
+    "seg_conv_igemm": (_I, [_V, _L, _I, _I, _I, _I, _V, _I, _V, _V, _L, _I, _I, _I, _I, _I, _I, _V, _L, _V]),
+    "seg_pack_conv_weight": (_I, [_V, _V, _I, _I, _I, _I, _I, _I, _V]),
+    "seg_conv_wgrad_splits": (_I, [_L, _I, _I, _I]),
+    "seg_conv_wgrad": (_I, [_V, _L, _V, _L, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _V, _I, _V]),
+    "seg_conv_wgrad_reduce": (_I, [_V, _I, _V, _I, _I, _I, _I, _I, _V]),
+    "seg_pack_dw_weight": (_I, [_V, _V, _I, _V]),
+    "seg_dw_fwd": (_I, [_V, _L, _I, _I, _I, _I, _V, _V, _L, _I, _I, _I, _V]),
+    "seg_dw_dgrad": (_I, [_V, _L, _I, _I, _I, _I, _V, _V, _L, _I, _I, _I, _I, _V]),
+    "seg_dw_wgrad_blocks": (_L, [_L]),
+    "seg_dw_wgrad": (_I, [_V, _L, _V, _L, _I, _I, _I, _I, _I, _I, _I, _V, _V]),
+    "seg_stem_fwd": (_I, [_V, _I, _I, _I, _V, _V, _I, _V, _L, _I, _I, _I, _V]),
+    "seg_stem_wgrad_blocks": (_L, [_L]),
+    "seg_stem_wgrad": (_I, [_V, _L, _V, _I, _I, _I, _I, _I, _I, _I, _V, _V]),
+    "seg_chan_workspace_floats": (_L, [_L, _I]),
+    "seg_bn_stats": (_I, [_V, _L, _L, _I, _V, _V, _F, _F, _V, _V, _V, _V, _V, _V, _V, _V, _V]),
+    "seg_bn_eval_coef": (_I, [_V, _V, _V, _V, _F, _I, _V, _V, _V]),
+    "seg_bn_apply": (_I, [_V, _L, _L, _I, _V, _V, _I, _V, _L, _V, _L, _V]),
+    "seg_bn_backward": (_I, [_V, _L, _V, _L, _L, _I, _V, _V, _V, _V, _V, _I, _V, _V, _V, _V, _L, _V]),
+    "seg_bn_eval_backward": (_I, [_V, _L, _V, _L, _L, _I, _V, _V, _I, _V, _L, _V]),
+    "seg_colsum": (_I, [_V, _L, _L, _I, _V, _V, _I, _V]),
+    "seg_add": (_I, [_V, _L, _V, _L, _L, _I, _V, _L, _V]),
+    "seg_upsample_fwd": (_I, [_V, _L, _I, _I, _I, _I, _V, _L, _I, _I, _I, _V]),
+    "seg_upsample_bwd": (_I, [_V, _L, _I, _I, _I, _I, _I, _V, _L, _I, _I, _I, _I, _V]),
+    "seg_upsample_to_nchw": (_I, [_V, _L, _I, _I, _I, _I, _V, _I, _I, _I, _V]),
+    "seg_maxpool2_fwd": (_I, [_V, _L, _I, _I, _I, _I, _V, _L, _V]),
+    "seg_maxpool2_bwd": (_I, [_V, _L, _V, _L, _I, _I, _I, _I, _V, _L, _I, _V]),
+    "seg_ce_workspace_floats": (_L, [_L]),
+    "seg_ce_upsample_loss": (_I, [_V, _L, _I, _I, _I, _I, _V, _I, _I, _I, _V, _V, _V]),
+    "seg_ce_upsample_grad": (_I, [_V, _L, _I, _I, _I, _I, _V, _I, _I, _I, _V, _V, _V, _L, _V]),
+}
+
+_lock = threading.Lock()
+_lib = None
+
+
+class SegLibError(RuntimeError):
+    pass
+
+
+def lib():
+    """Load libsegamd.so (must already be built: __graft_entry__.build())."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is None:
+            if not os.path.exists(LIB_PATH):
+                raise SegLibError(
+                    f"HIP library {LIB_PATH} is missing; build it with `python __graft_entry__.py` "
+                    "(there is no CPU fallback for the segamd hot path)")
+            import torch  # noqa: F401  -- load torch's libamdhip64 first so both share one HIP runtime
+            h = ctypes.CDLL(LIB_PATH)
+            for name, (res, args) in PROTOTYPES.items():
+                fn = getattr(h, name)
+                fn.restype = res
+                fn.argtypes = args
+            _lib = h
+    return _lib
+
+
+def check(rc: int, name: str = "") -> None:
+    if rc != 0:
+        raise SegLibError(f"segamd kernel {name} failed: hipError_t {rc}")
+
+
+def call(name: str, *args):
+    rc = getattr(lib(), name)(*args)
+    if rc != 0:
+        raise SegLibError(f"segamd kernel {name} failed: hipError_t {rc}")
+    return rc
+
+
+def query(name: str, *args) -> int:
+    return getattr(lib(), name)(*args)

@@ -1,0 +1,653 @@
+"""The HIP execution engine for MobileNetV2UNet / UNet / LightUNet.
+
+A model (seg_amd/unet.py) is compiled once per input shape into a *program*:
+a flat list of ops over named NHWC fp32 buffers.  The forward walks the list;
+the backward walks it in reverse with mirrored gradient buffers.  The whole
+network is one torch.autograd.Function, so `loss.backward()` works exactly as
+in the reference loop (src/train.py:36-39) while every FLOP runs in
+libsegamd.so (include/segamd.h).
+
+Buffers / layout (DESIGN.md "Data layout in HBM"):
+  * every activation is a [pixels][ld] row tensor, ld = round_up(C, 4);
+  * the decoder concat `torch.cat([skip, up(x)], 1)` (src/unet.py:103) is a
+    single buffer: the encoder writes its skip output into channels [0, Cs),
+    the bilinear upsample writes [Cs, Cs+Cu) -- no copy;
+  * each conv keeps its raw (pre-BN) output `y` for the BN backward; the
+    normalised/activated output is the next op's input.
+Gradients of a buffer region are written by the first consumer in reverse
+order and accumulated by later ones; a residual (InvertedResidual
+`x + conv(x)`) hands its upstream gradient to the first writer of dx as a
+fused addend.
+"""
+from __future__ import annotations
+
+import torch
+from torch import nn
+
+from ._lib import call, query
+from .mobilenet import ConvBNReLU6, InvertedResidual
+
+ACT_NONE, ACT_RELU, ACT_RELU6 = 0, 1, 2
+IGNORE_INDEX = -100
+
+
+def r4(c: int) -> int:
+    return (c + 3) & ~3
+
+
+class KernelTimer:
+    """Opt-in HIP-event timing of the dense MFMA convolution launches (used by
+    bench.py for the roofline figure).  Each timed launch is bracketed by two
+    events on the stream it runs on (torch's current stream)."""
+
+    def __init__(self):
+        self.records = []  # (kind, flops, start_event, end_event)
+
+    def elapsed(self):
+        """[(kind, flops, seconds)] -- call after synchronising."""
+        return [(k, f, a.elapsed_time(b) * 1e-3) for k, f, a, b in self.records]
+
+
+TIMER: KernelTimer | None = None
+
+
+def _timed_call(kind, flops, name, *args):
+    if TIMER is None:
+        return call(name, *args)
+    a = torch.cuda.Event(enable_timing=True)
+    b = torch.cuda.Event(enable_timing=True)
+    a.record()
+    call(name, *args)
+    b.record()
+    TIMER.records.append((kind, flops, a, b))
+
+
+class Act:
+    """NHWC view: channels [off, off+C) of buffer `buf` ([N*H*W][ld])."""
+    __slots__ = ("buf", "off", "ld", "C", "N", "H", "W")
+
+    def __init__(self, buf, off, ld, C, N, H, W):
+        self.buf, self.off, self.ld, self.C, self.N, self.H, self.W = buf, off, ld, C, N, H, W
+
+    @property
+    def M(self):
+        return self.N * self.H * self.W
+
+    def key(self):
+        return (self.buf, self.off, self.C)
+
+    def slice(self, off, C):
+        return Act(self.buf, self.off + off, self.ld, C, self.N, self.H, self.W)
+
+
+# ----------------------------------------------------------------------------- ops
+
+class ConvOp:
+    """conv (stem | igemm | dw) -> [BN -> act (+residual)]."""
+
+    def __init__(self, kind, conv: nn.Conv2d, bn, act, inp, out, y, res):
+        self.kind, self.conv, self.bn, self.act = kind, conv, bn, act
+        self.inp, self.out, self.y, self.res = inp, out, y, res
+        self.ks = conv.kernel_size[0]
+        self.stride = conv.stride[0]
+        self.pad = conv.padding[0]
+        self.cin = conv.in_channels
+        self.cout = conv.out_channels
+
+    def flops(self) -> int:
+        """Algorithmic FLOPs of this conv's forward (2 * MACs; dgrad and wgrad each equal it)."""
+        groups = self.conv.groups
+        return 2 * self.y.M * self.cout * (self.cin // groups) * self.ks * self.ks
+
+    def params(self):
+        ps = [self.conv.weight]
+        if self.conv.bias is not None:
+            ps.append(self.conv.bias)
+        if self.bn is not None:
+            ps += [self.bn.weight, self.bn.bias]
+        return ps
+
+    # -- forward
+    def forward(self, rt):
+        s, y = rt.stream, self.y
+        w = self.conv.weight
+        bias = self.conv.bias.data_ptr() if self.conv.bias is not None else None
+        if self.kind == "stem":
+            x = rt.image
+            call("seg_stem_fwd", x.data_ptr(), y.N, x.shape[2], x.shape[3], w.data_ptr(), bias, self.cout,
+                 rt.ptr(y), y.ld, y.H, y.W, self.stride, s)
+        elif self.kind == "dw":
+            wk = rt.tmp(9 * self.cout)
+            call("seg_pack_dw_weight", w.data_ptr(), wk.data_ptr(), self.cout, s)
+            i = self.inp
+            call("seg_dw_fwd", rt.ptr(i), i.ld, i.N, i.H, i.W, i.C, wk.data_ptr(), rt.ptr(y), y.ld, y.H, y.W,
+                 self.stride, s)
+        else:
+            i = self.inp
+            ldk = r4(self.ks * self.ks * self.cin)
+            wk = rt.tmp(self.cout * ldk)
+            call("seg_pack_conv_weight", w.data_ptr(), wk.data_ptr(), self.cout, self.cin, self.ks, ldk, 0,
+                 self.cin, s)
+            _timed_call(f"igemm{self.ks}_fwd", self.flops(), "seg_conv_igemm", rt.ptr(i), i.ld, i.N, i.H, i.W,
+                        self.cin, wk.data_ptr(), ldk, bias, rt.ptr(y), y.ld, y.H, y.W, self.cout, self.ks,
+                        self.stride, self.pad, None, 0, s)
+        if self.bn is None:
+            return
+        bn, C, M = self.bn, self.cout, y.M
+        st = torch.empty(4 * C, device=rt.device, dtype=torch.float32)
+        mean, invstd, scale, shift = (st[k * C:(k + 1) * C] for k in range(4))
+        if rt.training:
+            if bn.momentum is None:
+                raise NotImplementedError("BatchNorm2d(momentum=None) (cumulative average) is not supported")
+            work = rt.tmp(query("seg_chan_workspace_floats", M, C))
+            rm = bn.running_mean.data_ptr() if bn.track_running_stats else None
+            rv = bn.running_var.data_ptr() if bn.track_running_stats else None
+            nbt = bn.num_batches_tracked.data_ptr() if bn.track_running_stats else None
+            call("seg_bn_stats", rt.ptr(y), y.ld, M, C, bn.weight.data_ptr(), bn.bias.data_ptr(), bn.eps,
+                 bn.momentum, rm, rv, nbt, work.data_ptr(), mean.data_ptr(), invstd.data_ptr(),
+                 scale.data_ptr(), shift.data_ptr(), s)
+        else:
+            call("seg_bn_eval_coef", bn.weight.data_ptr(), bn.bias.data_ptr(), bn.running_mean.data_ptr(),
+                 bn.running_var.data_ptr(), bn.eps, C, scale.data_ptr(), shift.data_ptr(), s)
+        o, r = self.out, self.res
+        call("seg_bn_apply", rt.ptr(y), y.ld, M, C, scale.data_ptr(), shift.data_ptr(), self.act,
+             rt.ptr(r) if r is not None else None, r.ld if r is not None else 0, rt.ptr(o), o.ld, s)
+        rt.saved[id(self)] = st
+
+    # -- backward
+    def backward(self, rt):
+        s, y = rt.stream, self.y
+        dA = rt.grad_of(self.out)
+        if self.bn is not None:
+            if not rt.training:
+                raise NotImplementedError("backward through eval-mode BatchNorm is not supported")
+            C, M = self.cout, y.M
+            st = rt.saved[id(self)]
+            mean, invstd, scale, shift = (st[k * C:(k + 1) * C] for k in range(4))
+            dY = Act(rt.tmp_buf(M * r4(C)), 0, r4(C), C, y.N, y.H, y.W)
+            work = rt.tmp(query("seg_chan_workspace_floats", M, C) + 3 * C)
+            g_w, g_b = rt.grad_param(self.bn.weight), rt.grad_param(self.bn.bias)
+            call("seg_bn_backward", rt.gptr(dA), dA.ld, rt.ptr(y), y.ld, M, C, self.bn.weight.data_ptr(),
+                 mean.data_ptr(), invstd.data_ptr(), scale.data_ptr(), shift.data_ptr(), self.act,
+                 g_w, g_b, work.data_ptr(), rt.ptr(dY), dY.ld, s)
+            if self.res is not None:
+                rt.add_pending(self.res, dA)
+        else:
+            dY = dA
+        dYp = rt.ptr(dY) if dY.buf.startswith("#") else rt.gptr(dY)
+        M = y.M
+        # bias gradient
+        if self.conv.bias is not None and self.conv.bias.requires_grad:
+            work = rt.tmp(query("seg_chan_workspace_floats", M, r4(self.cout)))
+            call("seg_colsum", dYp, dY.ld, M, self.cout, work.data_ptr(), rt.grad_param(self.conv.bias), 0, s)
+        # weight gradient
+        if self.conv.weight.requires_grad:
+            gw = rt.grad_param(self.conv.weight)
+            if self.kind == "stem":
+                x = rt.image
+                nblk = query("seg_stem_wgrad_blocks", M)
+                part = rt.tmp(nblk * 27 * self.cout)
+                call("seg_stem_wgrad", dYp, dY.ld, x.data_ptr(), y.N, x.shape[2], x.shape[3], y.H, y.W, self.cout,
+                     self.stride, part.data_ptr(), s)
+                call("seg_conv_wgrad_reduce", part.data_ptr(), nblk, gw, self.cout, 3, 3, 2, 0, s)
+            elif self.kind == "dw":
+                i = self.inp
+                nblk = query("seg_dw_wgrad_blocks", M)
+                part = rt.tmp(nblk * 9 * self.cout)
+                call("seg_dw_wgrad", dYp, dY.ld, rt.ptr(i), i.ld, i.N, i.H, i.W, i.C, y.H, y.W, self.stride,
+                     part.data_ptr(), s)
+                call("seg_conv_wgrad_reduce", part.data_ptr(), nblk, gw, self.cout, 1, 3, 1, 0, s)
+            else:
+                i = self.inp
+                splits = query("seg_conv_wgrad_splits", M, self.cout, self.cin, self.ks)
+                part = rt.tmp(splits * self.cout * self.ks * self.ks * self.cin)
+                _timed_call(f"igemm{self.ks}_wgrad", self.flops(), "seg_conv_wgrad", dYp, dY.ld, rt.ptr(i), i.ld,
+                            i.N, i.H, i.W, self.cin, y.H, y.W, self.cout, self.ks, self.stride, self.pad,
+                            part.data_ptr(), splits, s)
+                call("seg_conv_wgrad_reduce", part.data_ptr(), splits, gw, self.cout, self.cin, self.ks, 0, 0, s)
+        rt.params_done(self.params())
+        # data gradient
+        if self.kind == "stem":
+            return
+        i = self.inp
+        if self.kind == "dw":
+            wk = rt.tmp(9 * self.cout)
+            call("seg_pack_dw_weight", self.conv.weight.data_ptr(), wk.data_ptr(), self.cout, s)
+            acc = rt.begin_write_accumulate(i)
+            call("seg_dw_dgrad", dYp, dY.ld, y.N, y.H, y.W, self.cout, wk.data_ptr(), rt.gptr(i), i.ld, i.H, i.W,
+                 self.stride, acc, s)
+        else:
+            if self.stride != 1:
+                raise NotImplementedError("data gradient of a strided dense conv")
+            kin = r4(self.cout)  # dY channels padded to 4 (the C=10 head)
+            ldk = r4(self.ks * self.ks * kin)
+            wk = rt.tmp(self.cin * ldk)
+            call("seg_pack_conv_weight", self.conv.weight.data_ptr(), wk.data_ptr(), self.cout, self.cin, self.ks,
+                 ldk, 1, kin, s)
+            add_ptr, add_ld = rt.begin_write_add(i)
+            _timed_call(f"igemm{self.ks}_dgrad", self.flops(), "seg_conv_igemm", dYp, dY.ld, y.N, y.H, y.W, kin,
+                        wk.data_ptr(), ldk, None, rt.gptr(i), i.ld, i.H, i.W, self.cin, self.ks, 1, self.pad,
+                        add_ptr, add_ld, s)
+        rt.mark_written(i)
+
+
+class UpsampleOp:
+    """nn.Upsample(x2, bilinear, align_corners=False) into a concat slice (src/unet.py:97-103)."""
+
+    def __init__(self, low, out):
+        self.low, self.out = low, out
+
+    def params(self):
+        return []
+
+    def forward(self, rt):
+        l, o = self.low, self.out
+        call("seg_upsample_fwd", rt.ptr(l), l.ld, l.N, l.H, l.W, l.C, rt.ptr(o), o.ld, o.H, o.W, 0, rt.stream)
+
+    def backward(self, rt):
+        l, o = self.low, self.out
+        d = rt.grad_of(o)
+        acc = rt.begin_write_accumulate(l)
+        call("seg_upsample_bwd", rt.gptr(d), d.ld, 0, o.N, o.H, o.W, o.C, rt.gptr(l), l.ld, l.H, l.W, 0, acc,
+             rt.stream)
+        rt.mark_written(l)
+
+
+class PoolOp:
+    """nn.MaxPool2d(2) (src/unet.py:85)."""
+
+    def __init__(self, inp, out):
+        self.inp, self.out = inp, out
+
+    def params(self):
+        return []
+
+    def forward(self, rt):
+        i, o = self.inp, self.out
+        call("seg_maxpool2_fwd", rt.ptr(i), i.ld, i.N, i.H, i.W, i.C, rt.ptr(o), o.ld, rt.stream)
+
+    def backward(self, rt):
+        i, o = self.inp, self.out
+        d = rt.grad_of(o)
+        acc = rt.begin_write_accumulate(i)
+        call("seg_maxpool2_bwd", rt.ptr(i), i.ld, rt.gptr(d), d.ld, i.N, i.H, i.W, i.C, rt.gptr(i), i.ld, acc,
+             rt.stream)
+        rt.mark_written(i)
+
+
+# ------------------------------------------------------------------------ program
+
+class Program:
+    def __init__(self, N, H, W):
+        self.N, self.H, self.W = N, H, W
+        self.bufs = {}       # name -> (rows, ld)
+        self.ops = []
+        self.logits = None   # Act of the (low-res for MobileNetV2UNet) logits
+        self.out_hw = (H, W)
+        self._n = 0
+
+    def new(self, C, H, W, name=None):
+        name = name or f"t{self._n}"
+        self._n += 1
+        ld = r4(C)
+        self.bufs[name] = (self.N * H * W, ld)
+        return Act(name, 0, ld, C, self.N, H, W)
+
+    def conv(self, kind, conv, bn, act, inp, out=None, res=None, H=None, W=None):
+        ks, st, pd = conv.kernel_size[0], conv.stride[0], conv.padding[0]
+        Hi, Wi = (inp.H, inp.W) if inp is not None else (H, W)
+        Ho, Wo = (Hi + 2 * pd - ks) // st + 1, (Wi + 2 * pd - ks) // st + 1
+        if out is None:
+            out = self.new(conv.out_channels, Ho, Wo)
+        y = self.new(conv.out_channels, Ho, Wo) if bn is not None else out
+        self.ops.append(ConvOp(kind, conv, bn, act, inp, out, y, res))
+        return out
+
+    def params(self):
+        seen, ps = set(), []
+        for op in self.ops:
+            for p in op.params():
+                if id(p) not in seen:
+                    seen.add(id(p))
+                    ps.append(p)
+        return ps
+
+
+def _cna(prog, m: ConvBNReLU6, inp, out=None, H=None, W=None, kind=None):
+    conv, bn = m[0], m[1]
+    if kind is None:
+        kind = "dw" if conv.groups > 1 else "igemm"
+    return prog.conv(kind, conv, bn, ACT_RELU6, inp, out=out, H=H, W=W)
+
+
+def _inverted_residual(prog, blk: InvertedResidual, inp, out=None):
+    layers = list(blk.conv)
+    x = inp
+    if len(layers) == 4:  # expand ratio != 1
+        x = _cna(prog, layers[0], x)
+        layers = layers[1:]
+    x = _cna(prog, layers[0], x, kind="dw")
+    return prog.conv("igemm", layers[1], layers[2], ACT_NONE, x, out=out,
+                     res=inp if blk.use_res_connect else None)
+
+
+def _double_conv(prog, dc, inp, out=None, first_kind="igemm", H=None, W=None):
+    c = dc.conv
+    x = prog.conv(first_kind, c[0], c[1], ACT_RELU, inp, H=H, W=W)
+    return prog.conv("igemm", c[3], c[4], ACT_RELU, x, out=out)
+
+
+def _up(prog, u, low, cat):
+    """cat = [skip (already written) | upsample(low)]; returns double_conv output."""
+    cs = cat.C - low.C
+    if u.conv.conv[0].in_channels != cat.C:
+        raise ValueError("up block channel mismatch")
+    prog.ops.append(UpsampleOp(low, cat.slice(cs, low.C)))
+    return _double_conv(prog, u.conv, cat)
+
+
+def _outconv(prog, oc, inp):
+    c = oc.conv
+    x = prog.conv("igemm", c[0], c[1], ACT_RELU, inp)
+    return prog.conv("igemm", c[3], None, ACT_NONE, x)
+
+
+def build_mobilenet_unet(model, N, H, W) -> Program:
+    """Program for MobileNetV2UNet.forward (src/unet.py:32-51)."""
+    if H % 32 or W % 32:
+        raise ValueError(f"MobileNetV2UNet needs H, W divisible by 32 (got {H}x{W}); the reference fails "
+                         "with a torch.cat size mismatch on such inputs")
+    p = Program(N, H, W)
+    ups = [model.up1, model.up2, model.up3, model.up4]
+    skip_c = [u.conv.conv[0].in_channels for u in ups]  # concat widths
+    # concat buffers, finest first: cat4 @ H/2 (up4), cat3 @ H/4, cat2 @ H/8, cat1 @ H/16
+    cats = {}
+    for k, (u, div) in enumerate(zip(ups, (16, 8, 4, 2))):
+        cats[k] = p.new(skip_c[k], H // div, W // div, name=f"cat{4 - k}")
+    stages = [model.down1, model.down2, model.down3, model.down4, model.down5]
+    skip_target = {0: cats[3], 1: cats[2], 2: cats[1], 3: cats[0]}
+    x = None
+    for si, stage in enumerate(stages):
+        blocks = list(stage)
+        for bi, blk in enumerate(blocks):
+            last = bi == len(blocks) - 1
+            out = None
+            if last and si in skip_target:
+                oc = blk.out_channels
+                out = skip_target[si].slice(0, oc)
+            if isinstance(blk, InvertedResidual):
+                x = _inverted_residual(p, blk, x, out=out)
+            elif isinstance(blk, ConvBNReLU6):
+                if x is None:
+                    x = _cna(p, blk, None, out=out, H=H, W=W, kind="stem")
+                else:
+                    x = _cna(p, blk, x, out=out)
+            else:
+                raise TypeError(f"unexpected encoder block {type(blk).__name__}")
+    for k, u in enumerate(ups):
+        x = _up(p, u, x, cats[k])
+    p.logits = _outconv(p, model.outc, x)
+    fu = model.final_upsample
+    if fu.scale_factor not in (2, 2.0) or not fu.align_corners:
+        raise ValueError("final_upsample must be x2 bilinear align_corners=True")
+    p.out_hw = (H, W)
+    return p
+
+
+def build_unet(model, N, H, W) -> Program:
+    """Program for UNet / LightUNet.forward (src/unet.py:137-147, :160-171)."""
+    if H % 8 or W % 8:
+        raise ValueError(f"UNet needs H, W divisible by 8 (got {H}x{W})")
+    p = Program(N, H, W)
+    b = model.inc.conv.conv[0].out_channels
+    cat3 = p.new(model.up3.conv.conv[0].in_channels, H, W, name="cat3")          # [x1 | up(u2)]
+    cat2 = p.new(model.up2.conv.conv[0].in_channels, H // 2, W // 2, name="cat2")  # [x2 | up(u1)]
+    cat1 = p.new(model.up1.conv.conv[0].in_channels, H // 4, W // 4, name="cat1")  # [x3 | up(x4)]
+    x1 = _double_conv(p, model.inc.conv, None, out=cat3.slice(0, b), first_kind="stem", H=H, W=W)
+    d1 = model.down1.mpconv[1]
+    pooled = p.new(x1.C, H // 2, W // 2)
+    p.ops.append(PoolOp(x1, pooled))
+    x2 = _double_conv(p, d1, pooled, out=cat2.slice(0, d1.conv[3].out_channels))
+    d2 = model.down2.mpconv[1]
+    pooled = p.new(x2.C, H // 4, W // 4)
+    p.ops.append(PoolOp(x2, pooled))
+    x3 = _double_conv(p, d2, pooled, out=cat1.slice(0, d2.conv[3].out_channels))
+    d3 = model.down3.mpconv[1]
+    pooled = p.new(x3.C, H // 8, W // 8)
+    p.ops.append(PoolOp(x3, pooled))
+    x4 = _double_conv(p, d3, pooled)
+    x = _up(p, model.up1, x4, cat1)
+    x = _up(p, model.up2, x, cat2)
+    x = _up(p, model.up3, x, cat3)
+    p.logits = _outconv(p, model.sem_out, x)
+    p.out_hw = (H, W)
+    return p
+
+
+def build_program(model, N, H, W) -> Program:
+    from .unet import MobileNetV2UNet, UNet, LightUNet
+    if isinstance(model, MobileNetV2UNet):
+        return build_mobilenet_unet(model, N, H, W)
+    if isinstance(model, (UNet, LightUNet)):
+        return build_unet(model, N, H, W)
+    raise TypeError(f"no HIP program for {type(model).__name__}")
+
+
+# ------------------------------------------------------------------------ runtime
+
+class Run:
+    """State of one forward (and its backward): buffers, saved BN statistics,
+    gradient buffers and which gradient regions have been written."""
+
+    def __init__(self, prog: Program, image: torch.Tensor, training: bool):
+        self.prog, self.image, self.training = prog, image, training
+        self.device = image.device
+        self.stream = torch.cuda.current_stream(self.device).cuda_stream
+        self.bufs = {n: torch.empty(rows * ld, device=self.device, dtype=torch.float32)
+                     for n, (rows, ld) in prog.bufs.items()}
+        self.saved = {}
+        self.gbufs = {}
+        self.written = {}     # grad buffer name -> list of (lo, hi) channel ranges
+        self.pending = {}     # Act.key() -> addend Act (residual upstream gradient)
+        self.grads = {}       # id(param) -> grad tensor
+        self.sync = None
+        self._tmp_n = 0
+
+    # pointers
+    def ptr(self, a: Act) -> int:
+        if a.buf.startswith("#"):
+            return self.gbufs[a.buf].data_ptr() + 4 * a.off
+        return self.bufs[a.buf].data_ptr() + 4 * a.off
+
+    def gptr(self, a: Act) -> int:
+        if a.buf.startswith("#"):
+            return self.gbufs[a.buf].data_ptr() + 4 * a.off
+        return self.gbuf(a.buf).data_ptr() + 4 * a.off
+
+    def gbuf(self, name):
+        g = self.gbufs.get(name)
+        if g is None:
+            g = self.gbufs[name] = torch.empty_like(self.bufs[name])
+        return g
+
+    def tmp(self, n: int) -> torch.Tensor:
+        return torch.empty(max(int(n), 1), device=self.device, dtype=torch.float32)
+
+    def tmp_buf(self, n: int) -> str:
+        name = f"#tmp{self._tmp_n}"
+        self._tmp_n += 1
+        self.gbufs[name] = self.tmp(n)
+        return name
+
+    # gradient-region bookkeeping
+    def _covered(self, a: Act) -> bool:
+        lo, hi = a.off, a.off + a.C
+        for (l, h) in self.written.get(a.buf, ()):
+            if l <= lo and hi <= h:
+                return True
+        return False
+
+    def mark_written(self, a: Act):
+        self.written.setdefault(a.buf, []).append((a.off, a.off + a.C))
+
+    def grad_of(self, a: Act) -> Act:
+        """Gradient region of activation `a` (zero-filled if nobody wrote it)."""
+        if not self._covered(a):
+            add = self.pending.pop(a.key(), None)
+            v = self.gbuf(a.buf).view(-1, a.ld)[:, a.off:a.off + a.C]
+            if add is not None:
+                call("seg_add", self.gptr(add), add.ld, None, 0, a.M, a.C, self.gptr(a), a.ld, self.stream)
+            else:
+                v.zero_()
+            self.mark_written(a)
+        return a
+
+    def add_pending(self, target: Act, addend: Act):
+        if self._covered(target):
+            call("seg_add", self.gptr(target), target.ld, self.gptr(addend), addend.ld, target.M, target.C,
+                 self.gptr(target), target.ld, self.stream)
+        else:
+            self.pending[target.key()] = addend
+
+    def begin_write_add(self, a: Act):
+        """For writers with a fused addend: returns (add_ptr, add_ld)."""
+        if self._covered(a):
+            return self.gptr(a), a.ld
+        add = self.pending.pop(a.key(), None)
+        if add is not None:
+            return self.gptr(add), add.ld
+        return None, 0
+
+    def begin_write_accumulate(self, a: Act) -> int:
+        """For writers with only an accumulate flag: materialise a pending addend first."""
+        if self._covered(a):
+            return 1
+        add = self.pending.pop(a.key(), None)
+        if add is not None:
+            call("seg_add", self.gptr(add), add.ld, None, 0, a.M, a.C, self.gptr(a), a.ld, self.stream)
+            self.mark_written(a)
+            return 1
+        return 0
+
+    def grad_param(self, p: torch.Tensor) -> int:
+        g = self.grads.get(id(p))
+        if g is None:
+            g = self.sync.grad_storage(p) if self.sync is not None else None
+            if g is None:
+                g = torch.empty_like(p)
+            self.grads[id(p)] = g
+        return g.data_ptr()
+
+    def params_done(self, ps):
+        if self.sync is not None:
+            self.sync.on_ready([p for p in ps if id(p) in self.grads])
+
+    # drivers
+    def forward(self):
+        for op in self.prog.ops:
+            op.forward(self)
+
+    def backward_from_logits(self):
+        for op in reversed(self.prog.ops):
+            op.backward(self)
+
+
+_PROGRAM_CACHE_ATTR = "_segamd_programs"
+
+
+def get_program(model, N, H, W) -> Program:
+    cache = model.__dict__.setdefault(_PROGRAM_CACHE_ATTR, {})
+    key = (N, H, W)
+    prog = cache.get(key)
+    if prog is None:
+        prog = cache[key] = build_program(model, N, H, W)
+    return prog
+
+
+def _check_input(x: torch.Tensor):
+    if not x.is_cuda:
+        raise RuntimeError("segamd models run on the MI355X HIP path only; move the model and input to 'cuda' "
+                           "(there is no CPU execution path)")
+    if x.dtype != torch.float32 or x.dim() != 4 or x.shape[1] != 3:
+        raise ValueError(f"expected float32 input [N,3,H,W], got {tuple(x.shape)} {x.dtype}")
+    if x.requires_grad:
+        raise NotImplementedError("gradient w.r.t. the input image is not supported")
+
+
+class _SegFunction(torch.autograd.Function):
+    """Whole-network forward/backward as one autograd node."""
+
+    @staticmethod
+    def forward(ctx, model, mode, x, target, ignore_index, sync, *params):
+        x = x.contiguous()
+        N, _, H, W = x.shape
+        prog = get_program(model, N, H, W)
+        run = Run(prog, x, model.training)
+        run.sync = sync
+        run.forward()
+        lo = prog.logits
+        Ho, Wo = prog.out_hw
+        s = run.stream
+        if mode == "logits":
+            out = torch.empty((N, lo.C, Ho, Wo), device=x.device, dtype=torch.float32)
+            call("seg_upsample_to_nchw", run.ptr(lo), lo.ld, N, lo.H, lo.W, lo.C, out.data_ptr(), Ho, Wo, 1, s)
+        else:
+            t = target.contiguous()
+            if t.dtype != torch.int64 or tuple(t.shape) != (N, Ho, Wo):
+                raise ValueError(f"target must be int64 [{N},{Ho},{Wo}], got {tuple(t.shape)} {t.dtype}")
+            stats = torch.empty(2, device=x.device, dtype=torch.float32)
+            work = run.tmp(query("seg_ce_workspace_floats", N * Ho * Wo))
+            call("seg_ce_upsample_loss", run.ptr(lo), lo.ld, N, lo.H, lo.W, lo.C, t.data_ptr(), Ho, Wo,
+                 ignore_index, work.data_ptr(), stats.data_ptr(), s)
+            run.target, run.stats = t, stats
+            out = stats[0]
+        if any(ctx.needs_input_grad[6:]):
+            ctx.run, ctx.mode, ctx.ignore_index = run, mode, ignore_index
+            ctx.params = params
+        else:
+            ctx.run = None
+        return out
+
+    @staticmethod
+    def backward(ctx, gout):
+        run = ctx.run
+        if run is None:
+            raise RuntimeError("segamd: backward called on a forward that saved nothing")
+        prog, lo, s = run.prog, run.prog.logits, run.stream
+        N = prog.N
+        Ho, Wo = prog.out_hw
+        dlo = lo
+        if ctx.mode == "logits":
+            g = gout.contiguous()
+            call("seg_upsample_bwd", g.data_ptr(), 0, 1, N, Ho, Wo, lo.C, run.gptr(dlo), lo.ld, lo.H, lo.W, 1, 0, s)
+        else:
+            g = gout.reshape(1).to(torch.float32).contiguous()
+            dhigh = run.tmp(N * Ho * Wo * lo.ld)
+            call("seg_ce_upsample_grad", run.ptr(lo), lo.ld, N, lo.H, lo.W, lo.C, run.target.data_ptr(), Ho, Wo,
+                 ctx.ignore_index, g.data_ptr(), run.stats.data_ptr(), dhigh.data_ptr(), lo.ld, s)
+            call("seg_upsample_bwd", dhigh.data_ptr(), lo.ld, 0, N, Ho, Wo, lo.C, run.gptr(dlo), lo.ld, lo.H, lo.W,
+                 1, 0, s)
+        run.mark_written(dlo)
+        run.backward_from_logits()
+        if run.sync is not None:
+            run.sync.finish_gradient_sync()  # stream-ordered wait on the last all-reduces
+        grads = [run.grads.get(id(p)) if ctx.needs_input_grad[6 + k] else None for k, p in enumerate(ctx.params)]
+        ctx.run = None
+        return (None, None, None, None, None, None, *grads)
+
+
+def _params_for(model, x):
+    N, _, H, W = x.shape
+    return get_program(model, N, H, W).params()
+
+
+def run_logits(model, x: torch.Tensor) -> torch.Tensor:
+    _check_input(x)
+    sync = model.__dict__.get("_segamd_sync")
+    return _SegFunction.apply(model, "logits", x, None, IGNORE_INDEX, sync, *_params_for(model, x))
+
+
+def run_loss(model, x: torch.Tensor, target: torch.Tensor, ignore_index: int = IGNORE_INDEX) -> torch.Tensor:
+    _check_input(x)
+    sync = model.__dict__.get("_segamd_sync")
+    return _SegFunction.apply(model, "loss", x, target, ignore_index, sync, *_params_for(model, x))

@@ -1,0 +1,92 @@
+"""Drop-in training loop: `train_model(model, train_loader, criterion, optimizer,
+device, epochs=10)` with the reference's signature and behaviour
+(src/train.py:6-79): per epoch `model.train()`, for each batch `.to(device)`,
+`optimizer.zero_grad()`, forward, `criterion`, `backward`, `optimizer.step()`,
+running loss, a per-epoch "Training Loss" line and a state_dict checkpoint
+`Models/obj/obj_MOB_1_epoch_{epoch}.pth` (src/train.py:77).
+
+MI355X differences (results are the same):
+  * when `criterion` is a plain `nn.CrossEntropyLoss()` (main.py:99) and the
+    model is a seg_amd model, the loss is computed by the fused
+    upsample+cross-entropy kernels (`model.forward_loss`), so the 168 MB of
+    full-resolution logits per bs=32 batch are never written;
+  * under torch.distributed the gradients are averaged across ranks by
+    seg_amd.ddp (RCCL all-reduce overlapped with the backward) and only
+    rank 0 prints and writes checkpoints.
+"""
+from __future__ import annotations
+
+import os
+
+import torch
+from torch import nn
+
+try:
+    from tqdm import tqdm
+except ImportError:  # pragma: no cover
+    tqdm = None
+
+
+def _fusable_ce(criterion) -> bool:
+    return (isinstance(criterion, nn.CrossEntropyLoss) and criterion.weight is None
+            and criterion.reduction == "mean" and criterion.label_smoothing == 0.0)
+
+
+def _is_rank0() -> bool:
+    return not (torch.distributed.is_available() and torch.distributed.is_initialized()) or \
+        torch.distributed.get_rank() == 0
+
+
+def compute_loss(model, criterion, inputs, targets):
+    """criterion(model(inputs), targets), fused when the pair allows it."""
+    core = getattr(model, "module", model)
+    if hasattr(core, "forward_loss") and _fusable_ce(criterion):
+        return model.forward_loss(inputs, targets, criterion.ignore_index)
+    return criterion(model(inputs), targets)
+
+
+def train_one_epoch(model, train_loader, criterion, optimizer, device, epoch: int = 0, epochs: int = 1,
+                    progress: bool = True) -> float:
+    """One pass over `train_loader`; returns the mean batch loss (src/train.py:31-44)."""
+    model.train()
+    train_loss = 0.0
+    it = train_loader
+    bar = None
+    if progress and tqdm is not None and _is_rank0():
+        bar = it = tqdm(train_loader, desc=f"Epoch {epoch + 1}/{epochs} [Train]", leave=True, position=0,
+                        bar_format="{l_bar}{bar:20}{r_bar}{bar:-20b}")
+    nb = 0
+    for inputs, targets in it:
+        inputs = inputs.to(device, non_blocking=True)
+        targets = targets.to(device, non_blocking=True)
+        optimizer.zero_grad()
+        loss = compute_loss(model, criterion, inputs, targets)
+        loss.backward()
+        sync = getattr(model, "finish_gradient_sync", None)
+        if sync is not None:
+            sync()
+        optimizer.step()
+        lv = loss.item()
+        train_loss += lv
+        nb += 1
+        if bar is not None:
+            bar.set_postfix(loss=f"{lv:.4f}")
+    n = len(train_loader) if hasattr(train_loader, "__len__") else max(nb, 1)
+    return train_loss / max(n, 1)
+
+
+def train_model(model, train_loader, criterion, optimizer, device, epochs=10,
+                checkpoint_pattern: str | None = "Models/obj/obj_MOB_1_epoch_{epoch}.pth", progress: bool = True):
+    """Train for `epochs` epochs (src/train.py:6-79)."""
+    best_val_loss = float("inf")  # validation is disabled in the reference (src/train.py:46-76)
+    for epoch in range(epochs):
+        avg_train_loss = train_one_epoch(model, train_loader, criterion, optimizer, device, epoch, epochs, progress)
+        if _is_rank0():
+            print(f"  Training Loss: {avg_train_loss:.4f}")
+            if checkpoint_pattern:
+                path = checkpoint_pattern.format(epoch=epoch + 1)
+                os.makedirs(os.path.dirname(path) or ".", exist_ok=True)
+                core = getattr(model, "module", model)
+                torch.save(core.state_dict(), path)
+    if _is_rank0():
+        print(f"Training completed. Best validation loss: {best_val_loss:.4f}")

@@ -1,0 +1,71 @@
+"""CPU: the C-ABI library builds, loads, exports exactly what include/segamd.h
+declares, and the ctypes prototypes match the header's parameter types."""
+import ctypes
+import os
+import re
+
+import pytest
+
+from seg_amd import _lib
+from seg_amd.build import LIB_PATH, build
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(REPO, "include", "segamd.h")
+
+CTYPE = {"const float*": ctypes.c_void_p, "float*": ctypes.c_void_p, "const long long*": ctypes.c_void_p,
+         "long long*": ctypes.c_void_p, "hipStream_t": ctypes.c_void_p, "long": ctypes.c_long,
+         "int": ctypes.c_int, "float": ctypes.c_float}
+
+
+def header_decls():
+    text = open(HEADER).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    decls = {}
+    for m in re.finditer(r"\b(int|long)\s+(seg_\w+)\s*\(([^)]*)\)\s*;", text):
+        ret, name, params = m.group(1), m.group(2), m.group(3)
+        types = []
+        for prm in params.split(","):
+            prm = " ".join(prm.split())
+            t = re.sub(r"\s*\b\w+$", "", prm).replace(" *", "*")
+            types.append(t)
+        decls[name] = (ret, types)
+    return decls
+
+
+@pytest.fixture(scope="module")
+def lib():
+    build()
+    return _lib.lib()
+
+
+def test_header_matches_prototypes():
+    decls = header_decls()
+    assert set(decls) == set(_lib.PROTOTYPES), set(decls) ^ set(_lib.PROTOTYPES)
+    for name, (ret, types) in decls.items():
+        res, args = _lib.PROTOTYPES[name]
+        assert res == (ctypes.c_int if ret == "int" else ctypes.c_long), name
+        assert [CTYPE[t] for t in types] == args, name
+
+
+def test_library_exports_every_symbol(lib):
+    assert os.path.exists(LIB_PATH)
+    for name in header_decls():
+        assert hasattr(lib, name), name
+
+
+def test_host_side_queries(lib):
+    # pure host functions: callable without a GPU
+    s = _lib.query("seg_conv_wgrad_splits", 32 * 16 * 32, 256, 1344, 3)
+    assert 1 <= s <= 256
+    assert _lib.query("seg_conv_wgrad_splits", 10, 32, 32, 3) == 1
+    assert _lib.query("seg_chan_workspace_floats", 1 << 20, 96) >= 2 * 96
+    assert _lib.query("seg_dw_wgrad_blocks", 1 << 20) >= 1
+    assert _lib.query("seg_ce_workspace_floats", 4 * 256 * 512) >= 2
+
+
+def test_argument_validation_without_gpu(lib):
+    # invalid arguments are rejected before any launch (hipErrorInvalidValue == 1)
+    rc = lib.seg_conv_igemm(None, 3, 1, 4, 4, 3, None, 4, None, None, 4, 4, 4, 8, 3, 1, 1, None, 0, None)
+    assert rc == 1  # Cin % 4 != 0
+    rc = lib.seg_stem_fwd(None, 1, 4, 4, None, None, 48, None, 48, 2, 2, 2, None)
+    assert rc == 1  # unsupported Cout

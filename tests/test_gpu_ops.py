@@ -1,0 +1,294 @@
+"""GPU: every C-ABI kernel against a plain PyTorch fp32 CPU reference of the
+same op (forward and backward via torch.autograd), on odd shapes and edge cases.
+All calls go through libsegamd.so (seg_amd._lib)."""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from seg_amd._lib import call, query
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def r4(c):
+    return (c + 3) & ~3
+
+
+def S():
+    return torch.cuda.current_stream().cuda_stream
+
+
+def nhwc(t, ld=None):
+    """NCHW CPU tensor -> [N*H*W, ld] CUDA rows (pad channels filled with NaN to
+    prove they are never read as data)."""
+    N, C, H, W = t.shape
+    ld = ld or r4(C)
+    out = torch.full((N * H * W, ld), float("nan"), dtype=torch.float32)
+    out[:, :C] = t.permute(0, 2, 3, 1).reshape(-1, C)
+    return out.to(DEV)
+
+
+def from_nhwc(rows, N, C, H, W):
+    return rows[:, :C].reshape(N, H, W, C).permute(0, 3, 1, 2).cpu()
+
+
+def rel(a, b):
+    a, b = a.double().cpu(), b.double().cpu()
+    return float((a - b).norm() / max(float(b.norm()), 1e-30))
+
+
+def gen(*shape, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    return torch.randn(*shape, generator=g)
+
+
+@pytest.mark.parametrize("N,Cin,Cout,H,W,ks", [(2, 16, 96, 9, 13, 1), (1, 1344, 256, 4, 8, 3), (3, 80, 32, 7, 5, 3),
+                                              (2, 152, 64, 6, 10, 3), (1, 16, 10, 5, 7, 1), (2, 24, 144, 8, 8, 1),
+                                              (1, 320, 1280, 2, 4, 1), (2, 36, 200, 5, 6, 3)])
+def test_conv_igemm_fwd_dgrad_wgrad(N, Cin, Cout, H, W, ks):
+    pad = ks // 2
+    x = gen(N, Cin, H, W, seed=1)
+    w = gen(Cout, Cin, ks, ks, seed=2) * (2.0 / (Cin * ks * ks)) ** 0.5
+    b = gen(Cout, seed=3)
+    xr = x.clone().requires_grad_(True)
+    wr = w.clone().requires_grad_(True)
+    y = F.conv2d(xr, wr, b, padding=pad)
+    dy = gen(*y.shape, seed=4)
+    y.backward(dy)
+    s = S()
+    # forward
+    xg, wg, bg = nhwc(x), w.to(DEV), b.to(DEV)
+    ldk = r4(ks * ks * Cin)
+    wk = torch.empty(Cout * ldk, device=DEV)
+    call("seg_pack_conv_weight", wg.data_ptr(), wk.data_ptr(), Cout, Cin, ks, ldk, 0, Cin, s)
+    out = torch.full((N * H * W, r4(Cout)), float("nan"), device=DEV)
+    call("seg_conv_igemm", xg.data_ptr(), xg.shape[1], N, H, W, Cin, wk.data_ptr(), ldk, bg.data_ptr(),
+         out.data_ptr(), out.shape[1], H, W, Cout, ks, 1, pad, None, 0, s)
+    assert rel(from_nhwc(out, N, Cout, H, W), y.detach()) < 1e-5
+    # data gradient (+ fused addend)
+    dyg = nhwc(dy)
+    if Cout % 4:
+        dyg[:, Cout:] = 0.0  # the engine's contract: padded gradient channels are zero
+    kin = r4(Cout)
+    ldk2 = r4(ks * ks * kin)
+    wkd = torch.empty(Cin * ldk2, device=DEV)
+    call("seg_pack_conv_weight", wg.data_ptr(), wkd.data_ptr(), Cout, Cin, ks, ldk2, 1, kin, s)
+    addend = gen(N, Cin, H, W, seed=5)
+    addg = nhwc(addend)
+    dx = torch.empty(N * H * W, r4(Cin), device=DEV)
+    call("seg_conv_igemm", dyg.data_ptr(), dyg.shape[1], N, H, W, kin, wkd.data_ptr(), ldk2, None,
+         dx.data_ptr(), dx.shape[1], H, W, Cin, ks, 1, pad, addg.data_ptr(), addg.shape[1], s)
+    assert rel(from_nhwc(dx, N, Cin, H, W), xr.grad + addend) < 1e-5
+    # weight gradient
+    M = N * H * W
+    splits = query("seg_conv_wgrad_splits", M, Cout, Cin, ks)
+    part = torch.empty(splits * Cout * ks * ks * Cin, device=DEV)
+    call("seg_conv_wgrad", dyg.data_ptr(), dyg.shape[1], xg.data_ptr(), xg.shape[1], N, H, W, Cin, H, W, Cout,
+         ks, 1, pad, part.data_ptr(), splits, s)
+    dw = torch.empty(Cout, Cin, ks, ks, device=DEV)
+    call("seg_conv_wgrad_reduce", part.data_ptr(), splits, dw.data_ptr(), Cout, Cin, ks, 0, 0, s)
+    assert rel(dw, wr.grad) < 1e-5
+
+
+@pytest.mark.parametrize("N,C,H,W,stride", [(2, 32, 9, 12, 1), (2, 96, 10, 14, 2), (1, 960, 4, 4, 1),
+                                            (3, 144, 7, 9, 2), (1, 8, 1, 1, 1)])
+def test_depthwise(N, C, H, W, stride):
+    x = gen(N, C, H, W, seed=1)
+    w = gen(C, 1, 3, 3, seed=2)
+    xr, wr = x.clone().requires_grad_(True), w.clone().requires_grad_(True)
+    y = F.conv2d(xr, wr, None, stride=stride, padding=1, groups=C)
+    Ho, Wo = y.shape[2], y.shape[3]
+    dy = gen(*y.shape, seed=3)
+    y.backward(dy)
+    s = S()
+    xg, wg = nhwc(x), w.to(DEV)
+    wk = torch.empty(9 * C, device=DEV)
+    call("seg_pack_dw_weight", wg.data_ptr(), wk.data_ptr(), C, s)
+    out = torch.empty(N * Ho * Wo, r4(C), device=DEV)
+    call("seg_dw_fwd", xg.data_ptr(), xg.shape[1], N, H, W, C, wk.data_ptr(), out.data_ptr(), out.shape[1], Ho, Wo,
+         stride, s)
+    assert rel(from_nhwc(out, N, C, Ho, Wo), y.detach()) < 1e-5
+    dyg = nhwc(dy)
+    dx = nhwc(torch.ones(N, C, H, W))
+    call("seg_dw_dgrad", dyg.data_ptr(), dyg.shape[1], N, Ho, Wo, C, wk.data_ptr(), dx.data_ptr(), dx.shape[1], H, W,
+         stride, 1, s)  # accumulate onto ones
+    assert rel(from_nhwc(dx, N, C, H, W), xr.grad + 1.0) < 1e-5
+    nblk = query("seg_dw_wgrad_blocks", N * Ho * Wo)
+    part = torch.empty(nblk * 9 * C, device=DEV)
+    call("seg_dw_wgrad", dyg.data_ptr(), dyg.shape[1], xg.data_ptr(), xg.shape[1], N, H, W, C, Ho, Wo, stride,
+         part.data_ptr(), s)
+    dw = torch.empty(C, 1, 3, 3, device=DEV)
+    call("seg_conv_wgrad_reduce", part.data_ptr(), nblk, dw.data_ptr(), C, 1, 3, 1, 0, s)
+    assert rel(dw, wr.grad) < 1e-5
+
+
+@pytest.mark.parametrize("N,H,W,Cout,stride,bias", [(2, 16, 24, 32, 2, False), (1, 9, 14, 64, 1, True),
+                                                    (2, 7, 11, 32, 1, True), (1, 13, 9, 64, 2, False)])
+def test_stem(N, H, W, Cout, stride, bias):
+    x = gen(N, 3, H, W, seed=1)
+    w = gen(Cout, 3, 3, 3, seed=2)
+    b = gen(Cout, seed=3) if bias else None
+    wr = w.clone().requires_grad_(True)
+    y = F.conv2d(x, wr, b, stride=stride, padding=1)
+    Ho, Wo = y.shape[2], y.shape[3]
+    dy = gen(*y.shape, seed=4)
+    y.backward(dy)
+    s = S()
+    xg, wg = x.to(DEV), w.to(DEV)
+    bg = b.to(DEV) if bias else None
+    out = torch.empty(N * Ho * Wo, Cout, device=DEV)
+    call("seg_stem_fwd", xg.data_ptr(), N, H, W, wg.data_ptr(), bg.data_ptr() if bias else None, Cout,
+         out.data_ptr(), Cout, Ho, Wo, stride, s)
+    assert rel(from_nhwc(out, N, Cout, Ho, Wo), y.detach()) < 1e-5
+    dyg = nhwc(dy)
+    nblk = query("seg_stem_wgrad_blocks", N * Ho * Wo)
+    part = torch.empty(nblk * 27 * Cout, device=DEV)
+    call("seg_stem_wgrad", dyg.data_ptr(), dyg.shape[1], xg.data_ptr(), N, H, W, Ho, Wo, Cout, stride,
+         part.data_ptr(), s)
+    dw = torch.empty(Cout, 3, 3, 3, device=DEV)
+    call("seg_conv_wgrad_reduce", part.data_ptr(), nblk, dw.data_ptr(), Cout, 3, 3, 2, 0, s)
+    assert rel(dw, wr.grad) < 1e-5
+
+
+@pytest.mark.parametrize("act", [0, 1, 2])
+@pytest.mark.parametrize("M,C,shift", [(1000, 96, 0.0), (4097, 1280, 5.0), (37, 16, 100.0)])
+def test_batchnorm_train(act, M, C, shift):
+    y = gen(M, C, seed=1) * 3 + shift
+    gamma, beta = gen(C, seed=2) * 0.2 + 1, gen(C, seed=3) * 0.5
+    rm, rv = gen(C, seed=4) * 0.1, torch.rand(C, generator=torch.Generator().manual_seed(5)) + 0.5
+    res = gen(M, C, seed=6)
+    da = gen(M, C, seed=7)
+    # Elements whose pre-activation sits within rounding of a ReLU/ReLU6 threshold
+    # take the mask of whichever fp32 rounding computed them; each such flip moves
+    # one dy element by O(1).  Give them zero upstream gradient so the test checks
+    # the arithmetic, not the coin flip.
+    y64 = y.double()
+    z64 = (y64 - y64.mean(0)) / torch.sqrt(y64.var(0, unbiased=False) + 1e-5) * gamma.double() + beta.double()
+    da[(z64.abs() < 1e-4) | ((z64 - 6).abs() < 1e-4)] = 0.0
+    yr = y.clone().requires_grad_(True)
+    gr, br = gamma.clone().requires_grad_(True), beta.clone().requires_grad_(True)
+    rm_ref, rv_ref = rm.clone(), rv.clone()
+    z = F.batch_norm(yr.t().reshape(1, C, M), rm_ref, rv_ref, gr, br, True, 0.1, 1e-5).reshape(C, M).t()
+    a = F.relu(z) if act == 1 else (F.hardtanh(z, 0, 6) if act == 2 else z)
+    out_ref = a + res
+    out_ref.backward(da)
+    s = S()
+    yg, gg, bgp = y.to(DEV), gamma.to(DEV), beta.to(DEV)
+    rmg, rvg = rm.to(DEV), rv.to(DEV)
+    nbt = torch.zeros(1, dtype=torch.int64, device=DEV)
+    st = torch.empty(4 * C, device=DEV)
+    work = torch.empty(query("seg_chan_workspace_floats", M, C) + 3 * C, device=DEV)
+    call("seg_bn_stats", yg.data_ptr(), C, M, C, gg.data_ptr(), bgp.data_ptr(), 1e-5, 0.1, rmg.data_ptr(),
+         rvg.data_ptr(), nbt.data_ptr(), work.data_ptr(), st[0:C].data_ptr(), st[C:2 * C].data_ptr(),
+         st[2 * C:3 * C].data_ptr(), st[3 * C:].data_ptr(), s)
+    resg = res.to(DEV)
+    out = torch.empty(M, C, device=DEV)
+    call("seg_bn_apply", yg.data_ptr(), C, M, C, st[2 * C:3 * C].data_ptr(), st[3 * C:].data_ptr(), act,
+         resg.data_ptr(), C, out.data_ptr(), C, s)
+    assert rel(out, out_ref.detach()) < 1e-5
+    assert rel(rmg, rm_ref) < 1e-5 and rel(rvg, rv_ref) < 1e-5 and int(nbt) == 1
+    dag = da.to(DEV)
+    dgam, dbet = torch.empty(C, device=DEV), torch.empty(C, device=DEV)
+    dy = torch.empty(M, C, device=DEV)
+    call("seg_bn_backward", dag.data_ptr(), C, yg.data_ptr(), C, M, C, gg.data_ptr(), st[0:C].data_ptr(),
+         st[C:2 * C].data_ptr(), st[2 * C:3 * C].data_ptr(), st[3 * C:].data_ptr(), act, dgam.data_ptr(),
+         dbet.data_ptr(), work.data_ptr(), dy.data_ptr(), C, s)
+    assert rel(dy, yr.grad) < 1e-4
+    assert rel(dgam, gr.grad) < 1e-4 and rel(dbet, br.grad) < 1e-4
+
+
+@pytest.mark.parametrize("N,C,H,W,ac", [(2, 64, 5, 7, 0), (1, 1280, 2, 4, 0), (2, 12, 6, 9, 1), (1, 8, 1, 1, 0)])
+def test_upsample(N, C, H, W, ac):
+    x = gen(N, C, H, W, seed=1)
+    xr = x.clone().requires_grad_(True)
+    y = F.interpolate(xr, scale_factor=2, mode="bilinear", align_corners=bool(ac))
+    Ho, Wo = 2 * H, 2 * W
+    dy = gen(*y.shape, seed=2)
+    y.backward(dy)
+    s = S()
+    xg = nhwc(x)
+    # write into a channel slice of a wider (concat) buffer
+    ld = r4(C) + 16
+    cat = torch.full((N * Ho * Wo, ld), float("nan"), device=DEV)
+    call("seg_upsample_fwd", xg.data_ptr(), xg.shape[1], N, H, W, C, cat.data_ptr() + 4 * 16, ld, Ho, Wo, ac, s)
+    assert rel(from_nhwc(cat[:, 16:], N, C, Ho, Wo), y.detach()) < 1e-6
+    dyg = torch.zeros(N * Ho * Wo, ld, device=DEV)
+    dyg[:, 16:16 + C] = dy.permute(0, 2, 3, 1).reshape(-1, C).to(DEV)
+    dx = torch.empty(N * H * W, r4(C), device=DEV)
+    call("seg_upsample_bwd", dyg.data_ptr() + 4 * 16, ld, 0, N, Ho, Wo, C, dx.data_ptr(), dx.shape[1], H, W, ac, 0, s)
+    assert rel(from_nhwc(dx, N, C, H, W), xr.grad) < 1e-6
+    # NCHW gradient path + NCHW output path
+    dyn = dy.contiguous().to(DEV)
+    dx2 = torch.empty(N * H * W, r4(C), device=DEV)
+    call("seg_upsample_bwd", dyn.data_ptr(), 0, 1, N, Ho, Wo, C, dx2.data_ptr(), dx2.shape[1], H, W, ac, 0, s)
+    assert rel(from_nhwc(dx2, N, C, H, W), xr.grad) < 1e-6
+    outn = torch.empty(N, C, Ho, Wo, device=DEV)
+    call("seg_upsample_to_nchw", xg.data_ptr(), xg.shape[1], N, H, W, C, outn.data_ptr(), Ho, Wo, ac, s)
+    assert rel(outn, y.detach()) < 1e-6
+
+
+def test_maxpool_with_ties():
+    N, C, H, W = 2, 8, 6, 10
+    x = torch.randint(0, 3, (N, C, H, W)).float()  # many ties: first-max rule matters
+    xr = x.clone().requires_grad_(True)
+    y = F.max_pool2d(xr, 2)
+    dy = gen(*y.shape, seed=1)
+    y.backward(dy)
+    s = S()
+    xg = nhwc(x)
+    out = torch.empty(N * (H // 2) * (W // 2), C, device=DEV)
+    call("seg_maxpool2_fwd", xg.data_ptr(), C, N, H, W, C, out.data_ptr(), C, s)
+    assert torch.equal(from_nhwc(out, N, C, H // 2, W // 2), y.detach())
+    dyg = nhwc(dy)
+    dx = nhwc(torch.full((N, C, H, W), 0.5))
+    call("seg_maxpool2_bwd", xg.data_ptr(), C, dyg.data_ptr(), C, N, H, W, C, dx.data_ptr(), C, 1, s)
+    assert torch.allclose(from_nhwc(dx, N, C, H, W), xr.grad + 0.5, atol=1e-6)
+
+
+@pytest.mark.parametrize("N,C,H,W,ignore", [(2, 10, 8, 16, False), (1, 4, 5, 7, True), (2, 1, 4, 4, False),
+                                            (1, 21, 3, 5, True)])
+def test_ce_fused_upsample(N, C, H, W, ignore):
+    low = gen(N, C, H, W, seed=1) * 2
+    Ho, Wo = 2 * H, 2 * W
+    g = torch.Generator().manual_seed(2)
+    y = torch.randint(0, C, (N, Ho, Wo), generator=g)
+    if ignore:
+        y[0, :2] = -100
+    lr = low.clone().requires_grad_(True)
+    logits = F.interpolate(lr, scale_factor=2, mode="bilinear", align_corners=True)
+    loss = F.cross_entropy(logits, y)
+    loss.backward(torch.tensor(0.7))
+    s = S()
+    lg = nhwc(low)
+    yg = y.to(DEV)
+    stats = torch.empty(2, device=DEV)
+    work = torch.empty(query("seg_ce_workspace_floats", N * Ho * Wo), device=DEV)
+    call("seg_ce_upsample_loss", lg.data_ptr(), lg.shape[1], N, H, W, C, yg.data_ptr(), Ho, Wo, -100,
+         work.data_ptr(), stats.data_ptr(), s)
+    assert abs(stats[0].item() - loss.item()) <= 1e-5 * abs(loss.item()) + 1e-7
+    gout = torch.tensor([0.7], device=DEV)
+    ld = r4(C)
+    dhigh = torch.empty(N * Ho * Wo * ld, device=DEV)
+    call("seg_ce_upsample_grad", lg.data_ptr(), lg.shape[1], N, H, W, C, yg.data_ptr(), Ho, Wo, -100,
+         gout.data_ptr(), stats.data_ptr(), dhigh.data_ptr(), ld, s)
+    dlow = torch.empty(N * H * W, ld, device=DEV)
+    call("seg_upsample_bwd", dhigh.data_ptr(), ld, 0, N, Ho, Wo, C, dlow.data_ptr(), ld, H, W, 1, 0, s)
+    assert rel(from_nhwc(dlow, N, C, H, W), lr.grad) < 1e-5
+    assert torch.all(dlow[:, C:] == 0)
+
+
+def test_colsum_and_add():
+    M, C = 3001, 10
+    y = gen(M, r4(C), seed=1)
+    s = S()
+    yg = y.to(DEV)
+    work = torch.empty(query("seg_chan_workspace_floats", M, r4(C)), device=DEV)
+    out = torch.empty(C, device=DEV)
+    call("seg_colsum", yg.data_ptr(), r4(C), M, C, work.data_ptr(), out.data_ptr(), 0, s)
+    assert rel(out, y[:, :C].sum(0)) < 1e-5
+    a, b = gen(M, 16, seed=2).to(DEV), gen(M, 16, seed=3).to(DEV)
+    o = torch.empty(M, 16, device=DEV)
+    call("seg_add", a.data_ptr(), 16, b.data_ptr(), 16, M, 16, o.data_ptr(), 16, s)
+    assert torch.equal(o, a + b)

@@ -40,9 +40,9 @@ int seg_conv_igemm(const float* in, long ldin, int N, int H, int W, int Cin,
                    int ks, int stride, int pad,
                    const float* add, long ldadd, hipStream_t stream);
 
-/* Pack w[Cout][Cin][ks][ks]: mode 0 -> wk[Cout][ldk] (forward),
- * mode 1 -> wk[Cin][ldk] transposed + tap-flipped (data gradient), tap runs
- * padded to kin_pad >= Cout channels. */
+/* Pack w[Cout][Cin][ks][ks]: mode 0 -> wk[Cout][ldk] (forward; tap runs padded
+ * to kin_pad >= Cin channels), mode 1 -> wk[Cin][ldk] transposed + tap-flipped
+ * (data gradient; tap runs padded to kin_pad >= Cout channels). */
 int seg_pack_conv_weight(const float* w, float* wk, int Cout, int Cin, int ks, int ldk,
                          int mode, int kin_pad, hipStream_t stream);
 
@@ -54,7 +54,7 @@ int seg_conv_wgrad(const float* dy, long lddy, const float* x, long ldx,
                    int ks, int stride, int pad, float* part, int splits, hipStream_t stream);
 
 /* dW (PyTorch layout) = fixed-order sum of partial slabs.  mode 0: igemm
- * partials, 1: depthwise partials, 2: stem partials. */
+ * partials (K runs of round_up(Cin,4) channels), 1: depthwise partials. */
 int seg_conv_wgrad_reduce(const float* part, int splits, float* dw, int Cout, int Cin, int ks,
                           int mode, int accumulate, hipStream_t stream);
 
@@ -69,14 +69,11 @@ long seg_dw_wgrad_blocks(long M);
 int seg_dw_wgrad(const float* dy, long lddy, const float* x, long ldx, int N, int H, int W, int C,
                  int Ho, int Wo, int stride, float* part, hipStream_t stream);
 
-/* Cin = 3 first conv straight from the NCHW image batch: MobileNetV2 features[0]
- * (3->32, s2, via src/unet.py:15,34) and UNet inc (3->64/32, s1, bias,
- * src/unet.py:58 via :127). */
-int seg_stem_fwd(const float* x, int N, int H, int W, const float* w, const float* bias, int Cout,
-                 float* out, long ldout, int Ho, int Wo, int stride, hipStream_t stream);
-long seg_stem_wgrad_blocks(long M);
-int seg_stem_wgrad(const float* dy, long lddy, const float* x, int N, int H, int W, int Ho, int Wo,
-                   int Cout, int stride, float* part, hipStream_t stream);
+/* The NCHW image batch (as the reference's DataLoader delivers it) as NHWC rows of
+ * `ld` channels, zero-padded: the Cin = 3 first conv (MobileNetV2 features[0],
+ * src/unet.py:15,34; UNet inc, src/unet.py:127) then runs on seg_conv_igemm with
+ * K = 9 taps x 4 channels (the 4th weight channel packed as zero). */
+int seg_nchw_to_nhwc(const float* x, int N, int C, int H, int W, float* out, int ld, hipStream_t stream);
 
 /* ---- BatchNorm2d + activation (aten native_batch_norm(+_backward), hardtanh,
  *      threshold; src/unet.py:59-63,114-115 and torchvision norms) ----------- */

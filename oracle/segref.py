@@ -45,13 +45,14 @@ def _bump(p, pre, training):
 def _cbr(p, pre_conv, pre_bn, x, training, stride=1, pad=0, groups=1, act="relu6", bias=None):
     y = F.conv2d(x, p[pre_conv + "weight"], p.get(pre_conv + "bias") if bias is None else bias,
                  stride=stride, padding=pad, groups=groups)
+    _rec(pre_conv + "raw", y)
     y = _bn(p, pre_bn, y, training)
     _bump(p, pre_bn, training)
     if act == "relu6":
-        return F.hardtanh(y, 0.0, 6.0)
+        return _rec(pre_conv + "out", F.hardtanh(y, 0.0, 6.0))
     if act == "relu":
-        return F.relu(y)
-    return y
+        return _rec(pre_conv + "out", F.relu(y))
+    return _rec(pre_conv + "out", y)
 
 
 def mobilenet_features(p, x, training, prefix="backbone.features."):
@@ -86,9 +87,21 @@ def double_conv(p, pre, x, training):
     return _cbr(p, pre + "conv.3.", pre + "conv.4.", x, training, pad=1, act="relu")
 
 
+RECORD = None  # diagnostics: set to a dict to keep (and retain grads of) intermediates
+
+
+def _rec(name, t):
+    if RECORD is not None:
+        if t.requires_grad:
+            t.retain_grad()
+        RECORD[name] = t
+    return t
+
+
 def up(p, pre, x1, x2, training):
+    _rec(pre + "low", x1)
     x1 = F.interpolate(x1, scale_factor=2, mode="bilinear", align_corners=False)
-    return double_conv(p, pre + "conv.", torch.cat([x2, x1], dim=1), training)
+    return double_conv(p, pre + "conv.", _rec(pre + "cat", torch.cat([x2, x1], dim=1)), training)
 
 
 def outconv(p, pre, x, training):

@@ -86,18 +86,38 @@ int rows_per_block_for(long M) {
   return (int)r;
 }
 
-__global__ void bn_finalize_kernel(const float* __restrict__ part, int nblk, const float* __restrict__ y, long M, int C,
-                                   const float* __restrict__ gamma, const float* __restrict__ beta, float eps,
-                                   float momentum, float* running_mean, float* running_var, long long* nbt,
-                                   float* mean_out, float* invstd_out, float* scale_out, float* shift_out) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c == 0 && nbt) *nbt += 1;
-  if (c >= C) return;
-  double s = 0.0, s2 = 0.0;
-  for (int b = 0; b < nblk; ++b) {
-    s += part[(long)b * 2 * C + c];
-    s2 += part[(long)b * 2 * C + C + c];
+// Sum the per-block partials of channel c (one 64-lane wave per channel, fp64,
+// fixed lane->block assignment and a fixed shuffle tree: deterministic).
+__device__ __forceinline__ void sum_partials(const float* __restrict__ part, int nblk, int C, int ldp, int c,
+                                             int lane, double* s0, double* s1) {
+  double a = 0.0, b = 0.0;
+  for (int k = lane; k < nblk; k += 64) {
+    a += part[(long)k * 2 * ldp + c];
+    b += part[(long)k * 2 * ldp + ldp + c];
   }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    a += __shfl_xor(a, o, 64);
+    b += __shfl_xor(b, o, 64);
+  }
+  *s0 = a;
+  *s1 = b;
+}
+
+constexpr int FIN_CH = 4;  // channels (waves) per 256-thread finalize block
+
+__global__ __launch_bounds__(256) void bn_finalize_kernel(
+    const float* __restrict__ part, int nblk, const float* __restrict__ y, long M, int C,
+    const float* __restrict__ gamma, const float* __restrict__ beta, float eps, float momentum,
+    float* running_mean, float* running_var, long long* nbt, float* mean_out, float* invstd_out, float* scale_out,
+    float* shift_out) {
+  const int lane = threadIdx.x & 63;
+  const int c = blockIdx.x * FIN_CH + (threadIdx.x >> 6);
+  if (blockIdx.x == 0 && threadIdx.x == 0 && nbt) *nbt += 1;
+  if (c >= C) return;
+  double s, s2;
+  sum_partials(part, nblk, C, C, c, lane, &s, &s2);
+  if (lane != 0) return;
   const double k = y[c];
   const double dm = s / (double)M;
   const double mean = k + dm;
@@ -147,13 +167,12 @@ __global__ void bn_apply_kernel(const float* __restrict__ y, long ldy, long M, i
 __global__ void bn_bwd_finalize_kernel(const float* __restrict__ part, int nblk, long M, int C,
                                        const float* __restrict__ gamma, const float* __restrict__ invstd,
                                        float* dgamma, float* dbeta, float* coef) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  const int lane = threadIdx.x & 63;
+  const int c = blockIdx.x * FIN_CH + (threadIdx.x >> 6);
   if (c >= C) return;
-  double sdz = 0.0, sdzx = 0.0;
-  for (int b = 0; b < nblk; ++b) {
-    sdz += part[(long)b * 2 * C + c];
-    sdzx += part[(long)b * 2 * C + C + c];
-  }
+  double sdz, sdzx;
+  sum_partials(part, nblk, C, C, c, lane, &sdz, &sdzx);
+  if (lane != 0) return;
   const double inv = invstd[c];
   const double g = gamma ? gamma[c] : 1.0;
   if (dbeta) dbeta[c] = (float)sdz;
@@ -207,11 +226,12 @@ __global__ void bn_eval_bwd_kernel(const float* __restrict__ da, long ldda, cons
 
 __global__ void colsum_finalize_kernel(const float* __restrict__ part, int nblk, int C, int ldp, float* out,
                                        int accumulate) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  const int lane = threadIdx.x & 63;
+  const int c = blockIdx.x * FIN_CH + (threadIdx.x >> 6);
   if (c >= C) return;
-  double s = 0.0;
-  for (int b = 0; b < nblk; ++b) s += part[(long)b * 2 * ldp + c];
-  out[c] = accumulate ? out[c] + (float)s : (float)s;
+  double s, unused;
+  sum_partials(part, nblk, C, ldp, c, lane, &s, &unused);
+  if (lane == 0) out[c] = accumulate ? out[c] + (float)s : (float)s;
 }
 
 int ew_grid(long total) { return (int)std::min<long>(seg_cdiv(total, 256), 8192); }
@@ -255,7 +275,7 @@ SEG_API int seg_bn_stats(const float* y, long ldy, long M, int C, const float* g
   const int nblk = seg_cdiv(M, rpb);
   hipLaunchKernelGGL(chan_partial_kernel<0>, dim3(nblk), dim3(256), 0, stream, y, ldy, nullptr, 0L, (int)M, C,
                      nullptr, nullptr, nullptr, 0, work, rpb);
-  hipLaunchKernelGGL(bn_finalize_kernel, dim3(seg_cdiv(C, 256)), dim3(256), 0, stream, work, nblk, y, M, C, gamma,
+  hipLaunchKernelGGL(bn_finalize_kernel, dim3(seg_cdiv(C, FIN_CH)), dim3(256), 0, stream, work, nblk, y, M, C, gamma,
                      beta, eps, momentum, running_mean, running_var, num_batches_tracked, mean, invstd, scale, shift);
   SEG_RET_LAST();
 }
@@ -287,7 +307,7 @@ SEG_API int seg_bn_backward(const float* da, long ldda, const float* y, long ldy
   float* coef = work + (long)nblk * 2 * C;
   hipLaunchKernelGGL(chan_partial_kernel<1>, dim3(nblk), dim3(256), 0, stream, y, ldy, da, ldda, (int)M, C, scale,
                      shift, mean, act, work, rpb);
-  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(seg_cdiv(C, 256)), dim3(256), 0, stream, work, nblk, M, C, gamma,
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(seg_cdiv(C, FIN_CH)), dim3(256), 0, stream, work, nblk, M, C, gamma,
                      invstd, dgamma, dbeta, coef);
   hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(ew_grid(M * (C / 4))), dim3(256), 0, stream, da, ldda, y, ldy, M, C,
                      scale, shift, mean, act, coef, dy, lddy);
@@ -311,7 +331,7 @@ SEG_API int seg_colsum(const float* y, long ldy, long M, int C, float* work, flo
   const int nblk = seg_cdiv(M, rpb);
   hipLaunchKernelGGL(chan_partial_kernel<2>, dim3(nblk), dim3(256), 0, stream, y, ldy, nullptr, 0L, (int)M, C4,
                      nullptr, nullptr, nullptr, 0, work, rpb);
-  hipLaunchKernelGGL(colsum_finalize_kernel, dim3(seg_cdiv(C, 256)), dim3(256), 0, stream, work, nblk, C, C4, out,
+  hipLaunchKernelGGL(colsum_finalize_kernel, dim3(seg_cdiv(C, FIN_CH)), dim3(256), 0, stream, work, nblk, C, C4, out,
                      accumulate);
   SEG_RET_LAST();
 }

@@ -169,8 +169,8 @@ SEG_API int seg_dw_dgrad(const float* dy, long lddy, int N, int Ho, int Wo, int 
 }
 
 SEG_API long seg_dw_wgrad_blocks(long M) {
-  long rpb = (M + 511) / 512;
-  if (rpb < 64) rpb = 64;
+  long rpb = (M + 2047) / 2048;  // ~2048 blocks: >= 8 blocks (32 waves) per CU
+  if (rpb < 32) rpb = 32;
   return (M + rpb - 1) / rpb;
 }
 

@@ -223,20 +223,21 @@ SEG_API int seg_conv_igemm(const float* in, long ldin, int N, int H, int W, int 
 // Pack a PyTorch conv weight w[Cout][Cin][ks][ks] for seg_conv_igemm.
 //   mode 0 (forward):   wk[co][tap*Cin + ci]          = w[co][ci][tap]
 //   mode 1 (data-grad): wk[ci][tap*Cout + co]          = w[co][ci][ks*ks-1-tap]
-// In mode 1 the K run of each tap is padded to kin_pad >= Cout channels (zeros),
-// so a data-gradient whose dY has a padded channel count (the C=10 head) stays
-// float4-aligned.  Rows are zero-padded from taps*kin to ldk.
+// The K run of each tap is padded with zeros to kin_pad channels (>= Cin in
+// mode 0, >= Cout in mode 1), so a GEMM whose input has a padded channel count
+// stays float4-aligned: the Cin = 3 image (stored NHWC4) and the dY of the
+// C = 10 head.  Rows are zero-padded from taps*kin_pad to ldk.
 __global__ void pack_conv_weight_kernel(const float* __restrict__ w, float* __restrict__ wk,
                                         int Cout, int Cin, int taps, int ldk, int mode, int kin_pad) {
   const int rows = mode == 0 ? Cout : Cin;
-  const int kin = mode == 0 ? Cin : kin_pad;
+  const int kin = kin_pad;
   const long total = (long)rows * ldk;
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
     const int r = (int)(i / ldk), k = (int)(i - (long)r * ldk);
     float v = 0.f;
     if (k < taps * kin) {
       const int tap = k / kin, c = k - tap * kin;
-      if (mode == 0) v = w[((long)r * Cin + c) * taps + tap];
+      if (mode == 0) { if (c < Cin) v = w[((long)r * Cin + c) * taps + tap]; }
       else if (c < Cout) v = w[((long)c * Cin + r) * taps + (taps - 1 - tap)];
     }
     wk[i] = v;
@@ -245,8 +246,8 @@ __global__ void pack_conv_weight_kernel(const float* __restrict__ w, float* __re
 
 SEG_API int seg_pack_conv_weight(const float* w, float* wk, int Cout, int Cin, int ks, int ldk, int mode,
                                  int kin_pad, hipStream_t stream) {
-  if (mode == 1 && kin_pad < Cout) return (int)hipErrorInvalidValue;
-  if (ldk < ks * ks * (mode == 0 ? Cin : kin_pad)) return (int)hipErrorInvalidValue;
+  if (kin_pad < (mode == 0 ? Cin : Cout)) return (int)hipErrorInvalidValue;
+  if (ldk < ks * ks * kin_pad) return (int)hipErrorInvalidValue;
   const long total = (long)(mode == 0 ? Cout : Cin) * ldk;
   const int grid = (int)std::min<long>(seg_cdiv(total, 256), 4096);
   hipLaunchKernelGGL(pack_conv_weight_kernel, dim3(grid), dim3(256), 0, stream, w, wk, Cout, Cin, ks * ks, ldk, mode, kin_pad);

@@ -202,6 +202,23 @@ __global__ void maxpool_bwd_kernel(const float* __restrict__ in, long ldin, cons
   }
 }
 
+// NCHW image batch -> NHWC rows of ld channels, channels [C, ld) zero-filled.
+__global__ void nchw_to_nhwc_kernel(const float* __restrict__ x, int N, int C, int H, int W, float* __restrict__ out,
+                                    int ld) {
+  const long plane = (long)H * W;
+  const long total = (long)N * plane;
+  for (long p = blockIdx.x * (long)blockDim.x + threadIdx.x; p < total; p += (long)gridDim.x * blockDim.x) {
+    const long n = p / plane, q = p - n * plane;
+    const float* src = x + n * C * plane + q;
+    for (int c = 0; c < ld; c += 4) {
+      f32x4 v;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) v[j] = (c + j < C) ? src[(long)(c + j) * plane] : 0.f;
+      st4(out + p * ld + c, v);
+    }
+  }
+}
+
 int ew_grid(long total) { return (int)std::min<long>(seg_cdiv(total, 256), 8192); }
 
 float up_scale(int in, int out, int ac) {
@@ -241,6 +258,15 @@ SEG_API int seg_upsample_to_nchw(const float* in, long ldin, int N, int H, int W
   if (ldin & 3) return (int)hipErrorInvalidValue;
   hipLaunchKernelGGL(up_fwd_to_nchw_kernel, dim3(ew_grid((long)N * Ho * Wo)), dim3(256), 0, stream, in, ldin, N, H, W,
                      C, out, Ho, Wo, up_scale(H, Ho, ac), up_scale(W, Wo, ac), ac);
+  SEG_RET_LAST();
+}
+
+// The model input (NCHW float, as the reference's DataLoader delivers it) as NHWC
+// rows padded to `ld` channels -- lets the Cin = 3 first conv run on the MFMA
+// implicit-GEMM path (K = 9 taps x 4 channels, the 4th weight channel packed 0).
+SEG_API int seg_nchw_to_nhwc(const float* x, int N, int C, int H, int W, float* out, int ld, hipStream_t stream) {
+  if ((ld & 3) || ld < C) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(nchw_to_nhwc_kernel, dim3(ew_grid((long)N * H * W)), dim3(256), 0, stream, x, N, C, H, W, out, ld);
   SEG_RET_LAST();
 }
 

@@ -214,35 +214,54 @@ SEG_API int seg_conv_wgrad(const float* dy, long lddy, const float* x, long ldx,
   return launch_wgrad<32, 128, 32, 32>(a, ks, splits, stream);
 }
 
-// dW[co][ci][tap] (PyTorch layout) = sum_s part[s][co][tap*Cin + ci], fixed order.
-// Also serves the depthwise (part[s][tap][c] -> dW[c][0][tap], mode 1) and the
-// direct-conv stem (part[s][co][ci*taps+tap] -> identity order, mode 2) partials.
-__global__ void wgrad_reduce_kernel(const float* __restrict__ part, int splits, long slab,
-                                    float* __restrict__ dw, int Cout, int Cin, int taps, int mode, int accumulate) {
-  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < slab; i += (long)gridDim.x * blockDim.x) {
-    float s = 0.f;
-    for (int k = 0; k < splits; ++k) s += part[(long)k * slab + i];
-    long o;
-    if (mode == 0) {  // i = (co*taps + tap)*Cin + ci
-      const long co = i / ((long)taps * Cin);
-      const int r = (int)(i - co * taps * Cin);
-      const int tap = r / Cin, ci = r - tap * Cin;
-      o = (co * Cin + ci) * taps + tap;
-    } else if (mode == 1) {  // i = tap*C + c   (Cout == C, Cin == 1)
-      const int tap = (int)(i / Cout), c = (int)(i - (long)tap * Cout);
-      o = (long)c * taps + tap;
-    } else {
-      o = i;
+// dW (PyTorch layout) = sum over the split-K partial slabs, fixed order.
+//   mode 0: igemm partials part[s][co][tap][r4(Cin)] -> dW[co][ci][tap]
+//           (channels >= Cin are the zero padding of a Cin % 4 != 0 input: dropped)
+//   mode 1: depthwise partials part[s][tap][C]      -> dW[c][0][tap]
+// Block = 64 slab elements x 4 split groups; each group sums every 4th slab with
+// 4 independent accumulators, the 4 group sums are added through LDS in a fixed
+// order (bitwise reproducible).
+__global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restrict__ part, int splits, long slab,
+                                                           float* __restrict__ dw, int Cout, int Cin, int taps,
+                                                           int mode, int accumulate) {
+  __shared__ float red[4][64];
+  const int lane = threadIdx.x & 63, g = threadIdx.x >> 6;
+  const long i = (long)blockIdx.x * 64 + lane;
+  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+  if (i < slab) {
+    int k = g;
+    for (; k + 12 < splits; k += 16) {
+      s0 += part[(long)k * slab + i];
+      s1 += part[(long)(k + 4) * slab + i];
+      s2 += part[(long)(k + 8) * slab + i];
+      s3 += part[(long)(k + 12) * slab + i];
     }
-    dw[o] = accumulate ? dw[o] + s : s;
+    for (; k < splits; k += 4) s0 += part[(long)k * slab + i];
   }
+  red[g][lane] = (s0 + s1) + (s2 + s3);
+  __syncthreads();
+  if (g != 0 || i >= slab) return;
+  const float s = (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]);
+  long o;
+  if (mode == 0) {
+    const int cp = (Cin + 3) & ~3;
+    const long co = i / ((long)taps * cp);
+    const int r = (int)(i - co * taps * cp);
+    const int tap = r / cp, ci = r - tap * cp;
+    if (ci >= Cin) return;
+    o = (co * Cin + ci) * taps + tap;
+  } else {
+    const int tap = (int)(i / Cout), c = (int)(i - (long)tap * Cout);
+    o = (long)c * taps + tap;
+  }
+  dw[o] = accumulate ? dw[o] + s : s;
 }
 
 SEG_API int seg_conv_wgrad_reduce(const float* part, int splits, float* dw, int Cout, int Cin, int ks,
                                   int mode, int accumulate, hipStream_t stream) {
-  const long slab = (long)Cout * Cin * ks * ks;
-  const int grid = (int)std::min<long>(seg_cdiv(slab, 256), 2048);
-  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(grid), dim3(256), 0, stream, part, splits, slab, dw,
+  if (mode != 0 && mode != 1) return (int)hipErrorInvalidValue;
+  const long slab = (long)Cout * (mode == 0 ? ((Cin + 3) & ~3) : Cin) * ks * ks;
+  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(seg_cdiv(slab, 64)), dim3(256), 0, stream, part, splits, slab, dw,
                      Cout, Cin, ks * ks, mode, accumulate);
   SEG_RET_LAST();
 }

@@ -82,8 +82,11 @@ class Act:
 
 # ----------------------------------------------------------------------------- ops
 
+IMAGE = "image"   # buffer holding the NHWC4 copy of the NCHW model input
+
+
 class ConvOp:
-    """conv (stem | igemm | dw) -> [BN -> act (+residual)]."""
+    """conv (igemm | dw) -> [BN -> act (+residual)]."""
 
     def __init__(self, kind, conv: nn.Conv2d, bn, act, inp, out, y, res):
         self.kind, self.conv, self.bn, self.act = kind, conv, bn, act
@@ -92,7 +95,9 @@ class ConvOp:
         self.stride = conv.stride[0]
         self.pad = conv.padding[0]
         self.cin = conv.in_channels
+        self.cin_pad = r4(self.cin)  # GEMM K runs are float4 channel groups (the image: 3 -> 4)
         self.cout = conv.out_channels
+        self.first = inp.buf == IMAGE  # no data gradient for the model input
 
     def flops(self) -> int:
         """Algorithmic FLOPs of this conv's forward (2 * MACs; dgrad and wgrad each equal it)."""
@@ -112,11 +117,7 @@ class ConvOp:
         s, y = rt.stream, self.y
         w = self.conv.weight
         bias = self.conv.bias.data_ptr() if self.conv.bias is not None else None
-        if self.kind == "stem":
-            x = rt.image
-            call("seg_stem_fwd", x.data_ptr(), y.N, x.shape[2], x.shape[3], w.data_ptr(), bias, self.cout,
-                 rt.ptr(y), y.ld, y.H, y.W, self.stride, s)
-        elif self.kind == "dw":
+        if self.kind == "dw":
             wk = rt.tmp(9 * self.cout)
             call("seg_pack_dw_weight", w.data_ptr(), wk.data_ptr(), self.cout, s)
             i = self.inp
@@ -124,12 +125,12 @@ class ConvOp:
                  self.stride, s)
         else:
             i = self.inp
-            ldk = r4(self.ks * self.ks * self.cin)
+            ldk = r4(self.ks * self.ks * self.cin_pad)
             wk = rt.tmp(self.cout * ldk)
             call("seg_pack_conv_weight", w.data_ptr(), wk.data_ptr(), self.cout, self.cin, self.ks, ldk, 0,
-                 self.cin, s)
+                 self.cin_pad, s)
             _timed_call(f"igemm{self.ks}_fwd", self.flops(), "seg_conv_igemm", rt.ptr(i), i.ld, i.N, i.H, i.W,
-                        self.cin, wk.data_ptr(), ldk, bias, rt.ptr(y), y.ld, y.H, y.W, self.cout, self.ks,
+                        self.cin_pad, wk.data_ptr(), ldk, bias, rt.ptr(y), y.ld, y.H, y.W, self.cout, self.ks,
                         self.stride, self.pad, None, 0, s)
         if self.bn is None:
             return
@@ -183,14 +184,7 @@ class ConvOp:
         # weight gradient
         if self.conv.weight.requires_grad:
             gw = rt.grad_param(self.conv.weight)
-            if self.kind == "stem":
-                x = rt.image
-                nblk = query("seg_stem_wgrad_blocks", M)
-                part = rt.tmp(nblk * 27 * self.cout)
-                call("seg_stem_wgrad", dYp, dY.ld, x.data_ptr(), y.N, x.shape[2], x.shape[3], y.H, y.W, self.cout,
-                     self.stride, part.data_ptr(), s)
-                call("seg_conv_wgrad_reduce", part.data_ptr(), nblk, gw, self.cout, 3, 3, 2, 0, s)
-            elif self.kind == "dw":
+            if self.kind == "dw":
                 i = self.inp
                 nblk = query("seg_dw_wgrad_blocks", M)
                 part = rt.tmp(nblk * 9 * self.cout)
@@ -199,15 +193,15 @@ class ConvOp:
                 call("seg_conv_wgrad_reduce", part.data_ptr(), nblk, gw, self.cout, 1, 3, 1, 0, s)
             else:
                 i = self.inp
-                splits = query("seg_conv_wgrad_splits", M, self.cout, self.cin, self.ks)
-                part = rt.tmp(splits * self.cout * self.ks * self.ks * self.cin)
+                splits = query("seg_conv_wgrad_splits", M, self.cout, self.cin_pad, self.ks)
+                part = rt.tmp(splits * self.cout * self.ks * self.ks * self.cin_pad)
                 _timed_call(f"igemm{self.ks}_wgrad", self.flops(), "seg_conv_wgrad", dYp, dY.ld, rt.ptr(i), i.ld,
-                            i.N, i.H, i.W, self.cin, y.H, y.W, self.cout, self.ks, self.stride, self.pad,
+                            i.N, i.H, i.W, self.cin_pad, y.H, y.W, self.cout, self.ks, self.stride, self.pad,
                             part.data_ptr(), splits, s)
                 call("seg_conv_wgrad_reduce", part.data_ptr(), splits, gw, self.cout, self.cin, self.ks, 0, 0, s)
         rt.params_done(self.params())
         # data gradient
-        if self.kind == "stem":
+        if self.first:
             return
         i = self.inp
         if self.kind == "dw":
@@ -285,6 +279,7 @@ class Program:
         self.logits = None   # Act of the (low-res for MobileNetV2UNet) logits
         self.out_hw = (H, W)
         self._n = 0
+        self.image = self.new(3, H, W, name=IMAGE)  # NHWC4 copy of the input batch
 
     def new(self, C, H, W, name=None):
         name = name or f"t{self._n}"
@@ -293,9 +288,9 @@ class Program:
         self.bufs[name] = (self.N * H * W, ld)
         return Act(name, 0, ld, C, self.N, H, W)
 
-    def conv(self, kind, conv, bn, act, inp, out=None, res=None, H=None, W=None):
+    def conv(self, kind, conv, bn, act, inp, out=None, res=None):
         ks, st, pd = conv.kernel_size[0], conv.stride[0], conv.padding[0]
-        Hi, Wi = (inp.H, inp.W) if inp is not None else (H, W)
+        Hi, Wi = inp.H, inp.W
         Ho, Wo = (Hi + 2 * pd - ks) // st + 1, (Wi + 2 * pd - ks) // st + 1
         if out is None:
             out = self.new(conv.out_channels, Ho, Wo)
@@ -313,11 +308,11 @@ class Program:
         return ps
 
 
-def _cna(prog, m: ConvBNReLU6, inp, out=None, H=None, W=None, kind=None):
+def _cna(prog, m: ConvBNReLU6, inp, out=None, kind=None):
     conv, bn = m[0], m[1]
     if kind is None:
         kind = "dw" if conv.groups > 1 else "igemm"
-    return prog.conv(kind, conv, bn, ACT_RELU6, inp, out=out, H=H, W=W)
+    return prog.conv(kind, conv, bn, ACT_RELU6, inp, out=out)
 
 
 def _inverted_residual(prog, blk: InvertedResidual, inp, out=None):
@@ -331,9 +326,9 @@ def _inverted_residual(prog, blk: InvertedResidual, inp, out=None):
                      res=inp if blk.use_res_connect else None)
 
 
-def _double_conv(prog, dc, inp, out=None, first_kind="igemm", H=None, W=None):
+def _double_conv(prog, dc, inp, out=None):
     c = dc.conv
-    x = prog.conv(first_kind, c[0], c[1], ACT_RELU, inp, H=H, W=W)
+    x = prog.conv("igemm", c[0], c[1], ACT_RELU, inp)
     return prog.conv("igemm", c[3], c[4], ACT_RELU, x, out=out)
 
 
@@ -366,7 +361,7 @@ def build_mobilenet_unet(model, N, H, W) -> Program:
         cats[k] = p.new(skip_c[k], H // div, W // div, name=f"cat{4 - k}")
     stages = [model.down1, model.down2, model.down3, model.down4, model.down5]
     skip_target = {0: cats[3], 1: cats[2], 2: cats[1], 3: cats[0]}
-    x = None
+    x = p.image
     for si, stage in enumerate(stages):
         blocks = list(stage)
         for bi, blk in enumerate(blocks):
@@ -378,10 +373,7 @@ def build_mobilenet_unet(model, N, H, W) -> Program:
             if isinstance(blk, InvertedResidual):
                 x = _inverted_residual(p, blk, x, out=out)
             elif isinstance(blk, ConvBNReLU6):
-                if x is None:
-                    x = _cna(p, blk, None, out=out, H=H, W=W, kind="stem")
-                else:
-                    x = _cna(p, blk, x, out=out)
+                x = _cna(p, blk, x, out=out)
             else:
                 raise TypeError(f"unexpected encoder block {type(blk).__name__}")
     for k, u in enumerate(ups):
@@ -403,7 +395,7 @@ def build_unet(model, N, H, W) -> Program:
     cat3 = p.new(model.up3.conv.conv[0].in_channels, H, W, name="cat3")          # [x1 | up(u2)]
     cat2 = p.new(model.up2.conv.conv[0].in_channels, H // 2, W // 2, name="cat2")  # [x2 | up(u1)]
     cat1 = p.new(model.up1.conv.conv[0].in_channels, H // 4, W // 4, name="cat1")  # [x3 | up(x4)]
-    x1 = _double_conv(p, model.inc.conv, None, out=cat3.slice(0, b), first_kind="stem", H=H, W=W)
+    x1 = _double_conv(p, model.inc.conv, p.image, out=cat3.slice(0, b))
     d1 = model.down1.mpconv[1]
     pooled = p.new(x1.C, H // 2, W // 2)
     p.ops.append(PoolOp(x1, pooled))
@@ -544,12 +536,24 @@ class Run:
 
     # drivers
     def forward(self):
+        global LAST_RUN
+        x, img = self.image, self.prog.image
+        call("seg_nchw_to_nhwc", x.data_ptr(), img.N, 3, img.H, img.W, self.ptr(img), img.ld, self.stream)
         for op in self.prog.ops:
             op.forward(self)
+        if DEBUG_KEEP_RUN:
+            LAST_RUN = self
 
     def backward_from_logits(self):
+        global LAST_RUN
         for op in reversed(self.prog.ops):
             op.backward(self)
+        if DEBUG_KEEP_RUN:
+            LAST_RUN = self
+
+
+DEBUG_KEEP_RUN = False  # diagnostics: keep the last Run (buffers + gradient buffers)
+LAST_RUN = None
 
 
 _PROGRAM_CACHE_ATTR = "_segamd_programs"

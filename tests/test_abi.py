@@ -67,5 +67,7 @@ def test_argument_validation_without_gpu(lib):
     # invalid arguments are rejected before any launch (hipErrorInvalidValue == 1)
     rc = lib.seg_conv_igemm(None, 3, 1, 4, 4, 3, None, 4, None, None, 4, 4, 4, 8, 3, 1, 1, None, 0, None)
     assert rc == 1  # Cin % 4 != 0
-    rc = lib.seg_stem_fwd(None, 1, 4, 4, None, None, 48, None, 48, 2, 2, 2, None)
-    assert rc == 1  # unsupported Cout
+    rc = lib.seg_nchw_to_nhwc(None, 1, 3, 4, 4, None, 2, None)
+    assert rc == 1  # ld < C
+    rc = lib.seg_conv_wgrad_reduce(None, 1, None, 4, 4, 3, 2, 0, None)
+    assert rc == 1  # unknown mode

@@ -126,7 +126,9 @@ def test_depthwise(N, C, H, W, stride):
 
 @pytest.mark.parametrize("N,H,W,Cout,stride,bias", [(2, 16, 24, 32, 2, False), (1, 9, 14, 64, 1, True),
                                                     (2, 7, 11, 32, 1, True), (1, 13, 9, 64, 2, False)])
-def test_stem(N, H, W, Cout, stride, bias):
+def test_first_conv_from_nchw_image(N, H, W, Cout, stride, bias):
+    """Cin = 3 first conv (MobileNetV2 stem s2 / UNet inc s1): NCHW -> NHWC4, then the
+    strided implicit GEMM with the 4th weight channel packed as zero."""
     x = gen(N, 3, H, W, seed=1)
     w = gen(Cout, 3, 3, 3, seed=2)
     b = gen(Cout, seed=3) if bias else None
@@ -138,17 +140,24 @@ def test_stem(N, H, W, Cout, stride, bias):
     s = S()
     xg, wg = x.to(DEV), w.to(DEV)
     bg = b.to(DEV) if bias else None
+    x4 = torch.full((N * H * W, 4), float("nan"), device=DEV)
+    call("seg_nchw_to_nhwc", xg.data_ptr(), N, 3, H, W, x4.data_ptr(), 4, s)
+    assert torch.equal(x4[:, 3], torch.zeros_like(x4[:, 3]))
+    assert torch.equal(from_nhwc(x4, N, 3, H, W), x)
+    ldk = 36
+    wk = torch.empty(Cout * ldk, device=DEV)
+    call("seg_pack_conv_weight", wg.data_ptr(), wk.data_ptr(), Cout, 3, 3, ldk, 0, 4, s)
     out = torch.empty(N * Ho * Wo, Cout, device=DEV)
-    call("seg_stem_fwd", xg.data_ptr(), N, H, W, wg.data_ptr(), bg.data_ptr() if bias else None, Cout,
-         out.data_ptr(), Cout, Ho, Wo, stride, s)
+    call("seg_conv_igemm", x4.data_ptr(), 4, N, H, W, 4, wk.data_ptr(), ldk, bg.data_ptr() if bias else None,
+         out.data_ptr(), Cout, Ho, Wo, Cout, 3, stride, 1, None, 0, s)
     assert rel(from_nhwc(out, N, Cout, Ho, Wo), y.detach()) < 1e-5
     dyg = nhwc(dy)
-    nblk = query("seg_stem_wgrad_blocks", N * Ho * Wo)
-    part = torch.empty(nblk * 27 * Cout, device=DEV)
-    call("seg_stem_wgrad", dyg.data_ptr(), dyg.shape[1], xg.data_ptr(), N, H, W, Ho, Wo, Cout, stride,
-         part.data_ptr(), s)
+    splits = query("seg_conv_wgrad_splits", N * Ho * Wo, Cout, 4, 3)
+    part = torch.empty(splits * Cout * 36, device=DEV)
+    call("seg_conv_wgrad", dyg.data_ptr(), dyg.shape[1], x4.data_ptr(), 4, N, H, W, 4, Ho, Wo, Cout, 3, stride, 1,
+         part.data_ptr(), splits, s)
     dw = torch.empty(Cout, 3, 3, 3, device=DEV)
-    call("seg_conv_wgrad_reduce", part.data_ptr(), nblk, dw.data_ptr(), Cout, 3, 3, 2, 0, s)
+    call("seg_conv_wgrad_reduce", part.data_ptr(), splits, dw.data_ptr(), Cout, 3, 3, 0, 0, s)
     assert rel(dw, wr.grad) < 1e-5
 
 

@@ -27,20 +27,23 @@ struct IgemmArgs {
   const float* bias;             // [Cout] or nullptr
   const float* add; long ldadd;  // optional addend [M][ldadd] (may alias out)
   float* out; long ldout;
-  float* stat_part;              // optional BN-stat partials [gridM][2][Cout] (unused: nullptr)
   int N, H, W, Cin;
   int Ho, Wo, Cout;
   int stride, pad;
   int K, M;
 };
 
-constexpr int BK = 16;
-constexpr int LDSR = BK + 4;  // LDS row stride (floats)
+#ifndef SEG_IGEMM_BK
+#define SEG_IGEMM_BK 16  // measured: BK 16 beats 32 (LDS occupancy) on every cfg2 shape but up1.0
+#endif
 
-template <int BM, int BN, int WM, int WN, int KS>
+// BM x BN output tile per 256-thread block, 4 waves laid out (BM/WM) x (BN/WN),
+// each wave owning WM x WN = (WM/32) x (WN/32) accumulators of 32x32.
+template <int BM, int BN, int WM, int WN, int KS, int BK>
 __global__ __launch_bounds__(256) void igemm_conv_kernel(IgemmArgs a) {
-  constexpr int A_VEC = BM * BK / 4;  // float4 per stage
-  constexpr int B_VEC = BN * BK / 4;
+  constexpr int LDSR = BK + 4;        // LDS row stride (floats): conflict-free b128 reads
+  constexpr int KQ = BK / 4;          // float4 groups per tile row
+  constexpr int A_VEC = BM * KQ, B_VEC = BN * KQ;
   constexpr int A_PER = (A_VEC + 255) / 256;
   constexpr int B_PER = (B_VEC + 255) / 256;
   constexpr int MI = WM / 32, NI = WN / 32;
@@ -56,18 +59,23 @@ __global__ __launch_bounds__(256) void igemm_conv_kernel(IgemmArgs a) {
   const int tn = blockIdx.x % tiles_n, tm = blockIdx.x / tiles_n;
   const int m0 = tm * BM, n0 = tn * BN;
 
-  // Per-thread A rows: fixed across the K loop, decode the pixel once.
-  int a_row[A_PER], a_kq[A_PER], a_hi0[A_PER], a_wi0[A_PER];
+  // Per-thread A slots: the pixel is fixed across the K loop; the (tap, channel)
+  // position advances by BK per chunk without integer division.
   long a_base[A_PER];
+  int a_hi0[A_PER], a_wi0[A_PER], a_ci[A_PER], a_ky[A_PER], a_kx[A_PER], a_k[A_PER];
   bool a_ok[A_PER];
 #pragma unroll
   for (int i = 0; i < A_PER; ++i) {
     const int idx = tid + i * 256;
-    a_row[i] = idx / (BK / 4);
-    a_kq[i] = idx % (BK / 4);
-    const int p = m0 + a_row[i];
+    const int row = idx / KQ, kq = idx % KQ;
+    const int p = m0 + row;
     a_ok[i] = (idx < A_VEC) && (p < a.M);
     const int pp = a_ok[i] ? p : 0;
+    a_k[i] = kq * 4;
+    const int tap = a_k[i] / a.Cin;
+    a_ci[i] = a_k[i] - tap * a.Cin;
+    a_ky[i] = tap / KS;
+    a_kx[i] = tap - a_ky[i] * KS;
     if (KS == 1) {
       a_base[i] = (long)pp * a.ldin;
       a_hi0[i] = a_wi0[i] = 0;
@@ -85,25 +93,32 @@ __global__ __launch_bounds__(256) void igemm_conv_kernel(IgemmArgs a) {
   auto load_tiles = [&](int k0) {
 #pragma unroll
     for (int i = 0; i < A_PER; ++i) {
-      const int k = k0 + a_kq[i] * 4;
       f32x4 v = {0.f, 0.f, 0.f, 0.f};
-      if (a_ok[i] && k < a.K) {
+      if (a_ok[i] && a_k[i] < a.K) {
         if (KS == 1) {
-          v = ld4(a.in + a_base[i] + k);
+          v = ld4(a.in + a_base[i] + a_k[i]);
         } else {
-          const int tap = k / a.Cin, ci = k - tap * a.Cin;
-          const int ky = tap / KS, kx = tap - ky * KS;
-          const int hi = a_hi0[i] + ky, wi = a_wi0[i] + kx;
+          const int hi = a_hi0[i] + a_ky[i], wi = a_wi0[i] + a_kx[i];
           if ((unsigned)hi < (unsigned)a.H && (unsigned)wi < (unsigned)a.W)
-            v = ld4(a.in + (a_base[i] + (long)hi * a.W + wi) * a.ldin + ci);
+            v = ld4(a.in + (a_base[i] + (long)hi * a.W + wi) * a.ldin + a_ci[i]);
         }
       }
       ra[i] = v;
+      // advance this slot to the next chunk
+      a_k[i] += BK;
+      if (KS != 1) {
+        int ci = a_ci[i] + BK;
+        while (ci >= a.Cin) {
+          ci -= a.Cin;
+          if (++a_kx[i] == KS) { a_kx[i] = 0; ++a_ky[i]; }
+        }
+        a_ci[i] = ci;
+      }
     }
 #pragma unroll
     for (int i = 0; i < B_PER; ++i) {
       const int idx = tid + i * 256;
-      const int row = idx / (BK / 4), kq = idx % (BK / 4);
+      const int row = idx / KQ, kq = idx % KQ;
       const int co = n0 + row, k = k0 + kq * 4;
       f32x4 v = {0.f, 0.f, 0.f, 0.f};
       if (idx < B_VEC && co < a.Cout && k < a.K) v = ld4(a.wk + (long)co * a.ldk + k);
@@ -114,12 +129,12 @@ __global__ __launch_bounds__(256) void igemm_conv_kernel(IgemmArgs a) {
 #pragma unroll
     for (int i = 0; i < A_PER; ++i) {
       const int idx = tid + i * 256;
-      if (idx < A_VEC) st4(&As[buf][a_row[i] * LDSR + a_kq[i] * 4], ra[i]);
+      if (idx < A_VEC) st4(&As[buf][(idx / KQ) * LDSR + (idx % KQ) * 4], ra[i]);
     }
 #pragma unroll
     for (int i = 0; i < B_PER; ++i) {
       const int idx = tid + i * 256;
-      if (idx < B_VEC) st4(&Bs[buf][(idx / (BK / 4)) * LDSR + (idx % (BK / 4)) * 4], rb[i]);
+      if (idx < B_VEC) st4(&Bs[buf][(idx / KQ) * LDSR + (idx % KQ) * 4], rb[i]);
     }
   };
 
@@ -182,12 +197,41 @@ __global__ __launch_bounds__(256) void igemm_conv_kernel(IgemmArgs a) {
 
 template <int BM, int BN, int WM, int WN>
 int launch_igemm(const IgemmArgs& a, int ks, hipStream_t s) {
+  constexpr int BK = SEG_IGEMM_BK;
   const int grid = seg_cdiv(a.M, BM) * seg_cdiv(a.Cout, BN);
   if (ks == 1)
-    hipLaunchKernelGGL((igemm_conv_kernel<BM, BN, WM, WN, 1>), dim3(grid), dim3(256), 0, s, a);
+    hipLaunchKernelGGL((igemm_conv_kernel<BM, BN, WM, WN, 1, BK>), dim3(grid), dim3(256), 0, s, a);
   else
-    hipLaunchKernelGGL((igemm_conv_kernel<BM, BN, WM, WN, 3>), dim3(grid), dim3(256), 0, s, a);
+    hipLaunchKernelGGL((igemm_conv_kernel<BM, BN, WM, WN, 3, BK>), dim3(grid), dim3(256), 0, s, a);
   SEG_RET_LAST();
+}
+
+struct TileCfg {
+  int bm, bn, wm, wn;
+  float eff;  // relative per-CU MFMA efficiency of the wave tile (LDS reads per MFMA)
+};
+// 64x64 wave tiles need 1 operand read per MFMA, 32x96 1.33, 32x32 2.
+constexpr TileCfg kTiles[] = {
+    {128, 128, 64, 64, 1.00f}, {64, 128, 32, 64, 0.95f}, {128, 64, 64, 32, 0.95f}, {64, 64, 32, 32, 0.85f},
+    {128, 96, 32, 96, 0.93f},  {128, 160, 32, 160, 0.95f}, {256, 32, 64, 32, 0.90f}, {128, 32, 32, 32, 0.80f},
+};
+
+int pick_tile(long M, int N) {
+  int best = 0;
+  double best_score = -1.0;
+  for (int i = 0; i < (int)(sizeof(kTiles) / sizeof(kTiles[0])); ++i) {
+    const TileCfg& t = kTiles[i];
+    const long bm_tiles = (M + t.bm - 1) / t.bm, bn_tiles = (N + t.bn - 1) / t.bn;
+    const long blocks = bm_tiles * bn_tiles;
+    const double util = (double)M * N / ((double)bm_tiles * t.bm * bn_tiles * t.bn);
+    const double fill = std::min(1.0, (double)blocks / 512.0);  // >= 2 blocks per CU to hide latency
+    const double score = util * t.eff * fill;
+    if (score > best_score + 1e-9) {
+      best_score = score;
+      best = i;
+    }
+  }
+  return best;
 }
 
 }  // namespace
@@ -204,20 +248,20 @@ SEG_API int seg_conv_igemm(const float* in, long ldin, int N, int H, int W, int 
   if (ks == 1 && (stride != 1 || pad != 0 || Ho != H || Wo != W)) return (int)hipErrorInvalidValue;
   IgemmArgs a;
   a.in = in; a.ldin = ldin; a.wk = wk; a.ldk = ldk; a.bias = bias;
-  a.add = add; a.ldadd = ldadd; a.out = out; a.ldout = ldout; a.stat_part = nullptr;
+  a.add = add; a.ldadd = ldadd; a.out = out; a.ldout = ldout;
   a.N = N; a.H = H; a.W = W; a.Cin = Cin; a.Ho = Ho; a.Wo = Wo; a.Cout = Cout;
   a.stride = stride; a.pad = pad; a.K = ks * ks * Cin; a.M = N * Ho * Wo;
   if (a.M == 0 || Cout == 0) return 0;
-  // Tile choice: widest N tile that covers Cout; shrink M tile while the grid
-  // is too small to put >= 2 blocks on each of the 256 CUs.
-  if (Cout <= 32) return launch_igemm<128, 32, 32, 32>(a, ks, stream);
-  if (Cout <= 64) {
-    if ((long)seg_cdiv(a.M, 128) * seg_cdiv(Cout, 64) >= 512) return launch_igemm<128, 64, 64, 32>(a, ks, stream);
-    return launch_igemm<64, 64, 32, 32>(a, ks, stream);
+  switch (pick_tile(a.M, Cout)) {
+    case 0: return launch_igemm<128, 128, 64, 64>(a, ks, stream);
+    case 1: return launch_igemm<64, 128, 32, 64>(a, ks, stream);
+    case 2: return launch_igemm<128, 64, 64, 32>(a, ks, stream);
+    case 3: return launch_igemm<64, 64, 32, 32>(a, ks, stream);
+    case 4: return launch_igemm<128, 96, 32, 96>(a, ks, stream);
+    case 5: return launch_igemm<128, 160, 32, 160>(a, ks, stream);
+    case 6: return launch_igemm<256, 32, 64, 32>(a, ks, stream);
+    default: return launch_igemm<128, 32, 32, 32>(a, ks, stream);
   }
-  if ((long)seg_cdiv(a.M, 128) * seg_cdiv(Cout, 128) >= 512) return launch_igemm<128, 128, 64, 64>(a, ks, stream);
-  if ((long)seg_cdiv(a.M, 64) * seg_cdiv(Cout, 128) >= 512) return launch_igemm<64, 128, 32, 64>(a, ks, stream);
-  return launch_igemm<64, 64, 32, 32>(a, ks, stream);
 }
 
 // Pack a PyTorch conv weight w[Cout][Cin][ks][ks] for seg_conv_igemm.

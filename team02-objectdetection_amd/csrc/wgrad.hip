@@ -190,7 +190,7 @@ SEG_API int seg_conv_wgrad_splits(long M, int Cout, int Cin, int ks) {
   long splits = (2048 + tiles - 1) / tiles;
   const long max_by_k = std::max<long>(1, M / 256);  // >= 256 pixels per split
   splits = std::min(splits, max_by_k);
-  splits = std::min<long>(splits, 256);
+  splits = std::min<long>(splits, 1024);  // small slabs (the stem: 32 x 36) need many splits to fill 256 CUs
   return (int)std::max<long>(1, splits);
 }
 

@@ -1,0 +1,84 @@
+"""CPU, world_size 2 over gloo: the data-parallel gradient path (seg_amd/ddp.py).
+
+The GPU engine cannot run here, so the test drives DataParallel exactly the way
+the engine's backward does (Run.grad_param -> grad_storage, Run.params_done ->
+on_ready, end of backward -> finish_gradient_sync) with rank-specific gradients,
+and checks: initial parameter broadcast, bucket plan (every used parameter once,
+in the engine's backward order, classifier excluded), asynchronous bucket
+all-reduce launched as buckets fill, and the averaged result.
+"""
+import os
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, world, port, results):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from seg_amd import MobileNetV2UNet
+        from seg_amd.ddp import DataParallel
+        from seg_amd.detinit import deterministic_init
+        from seg_amd.engine import get_program
+
+        model = deterministic_init(MobileNetV2UNet(10), seed=100 + rank)   # ranks start different
+        dp = DataParallel(model, bucket_cap_mb=2.0)
+        # 1. parameters and buffers now equal rank 0's
+        ref = deterministic_init(MobileNetV2UNet(10), seed=100)
+        for (k, a), b in zip(model.state_dict().items(), ref.state_dict().values()):
+            assert torch.equal(a, b), k
+        # 2. bucket plan follows the engine's backward order
+        x = torch.zeros(2, 3, 64, 64)
+        dp._ensure_plan(x)
+        prog = get_program(model, 2, 64, 64)
+        order = []
+        for op in reversed(prog.ops):
+            for p in op.params():
+                if all(p is not q for q in order):
+                    order.append(p)
+        planned = [p for b in dp._buckets for p in b.params]
+        assert len(planned) == len(order) == 194
+        assert all(a is b for a, b in zip(planned, order))
+        assert all(b.numel <= dp.bucket_cap or len(b.params) == 1 for b in dp._buckets)
+        classifier = {id(p) for p in model.backbone.classifier.parameters()}
+        assert not any(id(p) in classifier for p in planned)
+        # 3. one simulated backward: write rank-specific grads, announce per layer
+        dp._arm()
+        launched_before_end = 0
+        for op in reversed(prog.ops):
+            ps = op.params()
+            for p in ps:
+                g = dp.grad_storage(p)
+                g.copy_(torch.full_like(p, float(rank + 1)) * (1 + torch.arange(p.numel()).view_as(p) % 7))
+            dp.on_ready(ps)
+            launched_before_end = sum(b.handle is not None for b in dp._buckets)
+        assert launched_before_end == len(dp._buckets)  # every bucket launched during the backward
+        dp.finish_gradient_sync()
+        dp.finish_gradient_sync()  # idempotent (train_model and the engine may both call it)
+        ok = True
+        for p in planned:
+            g = dp.grad_storage(p)
+            expect = torch.full_like(p, 1.5) * (1 + torch.arange(p.numel()).view_as(p) % 7)  # mean of 1 and 2
+            ok &= torch.allclose(g, expect)
+        results[rank] = bool(ok)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+def test_ddp_bucketed_allreduce_gloo():
+    world = 2
+    mgr = mp.Manager()
+    results = mgr.dict()
+    mp.spawn(_worker, args=(world, _free_port(), results), nprocs=world, join=True)
+    assert dict(results) == {0: True, 1: True}

@@ -33,12 +33,17 @@ extern "C" {
  * Replaces nn.Conv2d forward of the dense 3x3 convs (src/unet.py:58,61), the 1x1
  * head (src/unet.py:113,116) and torchvision's expand/project 1x1 convs
  * (reached through src/unet.py:15-19); with mode-1 packed weights it is also the
- * data gradient of those (stride-1) convs.  ks in {1,3}. */
+ * data gradient of those (stride-1) convs.  ks in {1,3}.  `stat` (optional):
+ * per-row-tile BatchNorm partials of `out` ([row_tiles][2][Cout]: tile sum, tile
+ * M2), consumed by seg_bn_stats_tiles -- the BN statistics pass fused into the
+ * conv epilogue. */
 int seg_conv_igemm(const float* in, long ldin, int N, int H, int W, int Cin,
                    const float* wk, int ldk, const float* bias,
                    float* out, long ldout, int Ho, int Wo, int Cout,
                    int ks, int stride, int pad,
-                   const float* add, long ldadd, hipStream_t stream);
+                   const float* add, long ldadd, float* stat, hipStream_t stream);
+/* Row tiles (and their height) seg_conv_igemm uses for an M x Cout output. */
+int seg_conv_igemm_row_tiles(long M, int Cout, int* tile_rows);
 
 /* Pack w[Cout][Cin][ks][ks]: mode 0 -> wk[Cout][ldk] (forward; tap runs padded
  * to kin_pad >= Cin channels), mode 1 -> wk[Cin][ldk] transposed + tap-flipped
@@ -82,6 +87,10 @@ int seg_bn_stats(const float* y, long ldy, long M, int C, const float* gamma, co
                  float eps, float momentum, float* running_mean, float* running_var,
                  long long* num_batches_tracked, float* work,
                  float* mean, float* invstd, float* scale, float* shift, hipStream_t stream);
+int seg_bn_stats_tiles(const float* part, int ntiles, int tile_rows, long M, int C, const float* gamma,
+                       const float* beta, float eps, float momentum, float* running_mean, float* running_var,
+                       long long* num_batches_tracked, float* mean, float* invstd, float* scale, float* shift,
+                       hipStream_t stream);
 int seg_bn_eval_coef(const float* gamma, const float* beta, const float* running_mean,
                      const float* running_var, float eps, int C, float* scale, float* shift,
                      hipStream_t stream);

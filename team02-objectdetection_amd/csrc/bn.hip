@@ -136,6 +136,54 @@ __global__ __launch_bounds__(256) void bn_finalize_kernel(
   }
 }
 
+// BN statistics from the conv epilogue's per-row-tile partials part[t][2][C]
+// (tile sum S_t and tile M2_t about the tile mean, tile t holding
+// min(tile_rows, M - t*tile_rows) rows): Chan's parallel merge in fp64, one wave
+// per channel, fixed lane order and butterfly (deterministic).
+__device__ __forceinline__ void chan_merge(double& n, double& mean, double& m2, double n2, double mean2, double m2b) {
+  const double nn = n + n2;
+  if (nn == 0.0) return;
+  const double d = mean2 - mean;
+  mean += d * (n2 / nn);
+  m2 += m2b + d * d * (n * n2 / nn);
+  n = nn;
+}
+
+__global__ __launch_bounds__(256) void bn_finalize_tiles_kernel(
+    const float* __restrict__ part, int ntiles, int tile_rows, long M, int C, const float* __restrict__ gamma,
+    const float* __restrict__ beta, float eps, float momentum, float* running_mean, float* running_var,
+    long long* nbt, float* mean_out, float* invstd_out, float* scale_out, float* shift_out) {
+  const int lane = threadIdx.x & 63;
+  const int c = blockIdx.x * FIN_CH + (threadIdx.x >> 6);
+  if (blockIdx.x == 0 && threadIdx.x == 0 && nbt) *nbt += 1;
+  if (c >= C) return;
+  double n = 0.0, mean = 0.0, m2 = 0.0;
+  for (int t = lane; t < ntiles; t += 64) {
+    const double nt = (double)std::min<long>(tile_rows, M - (long)t * tile_rows);
+    const double s = part[(long)t * 2 * C + c], q = part[(long)t * 2 * C + C + c];
+    chan_merge(n, mean, m2, nt, s / nt, q);
+  }
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const double n2 = __shfl_xor(n, o, 64), mean2 = __shfl_xor(mean, o, 64), m2b = __shfl_xor(m2, o, 64);
+    chan_merge(n, mean, m2, n2, mean2, m2b);
+  }
+  if (lane != 0) return;
+  double var = m2 / (double)M;
+  if (var < 0.0) var = 0.0;
+  const float invstd = (float)(1.0 / sqrt(var + (double)eps));
+  mean_out[c] = (float)mean;
+  invstd_out[c] = invstd;
+  const float g = gamma ? gamma[c] : 1.f, bt = beta ? beta[c] : 0.f;
+  scale_out[c] = g * invstd;
+  shift_out[c] = bt - (float)mean * g * invstd;
+  if (running_mean) {
+    const double unbiased = M > 1 ? m2 / (double)(M - 1) : var;
+    running_mean[c] = (float)((1.0 - momentum) * running_mean[c] + momentum * mean);
+    running_var[c] = (float)((1.0 - momentum) * running_var[c] + momentum * unbiased);
+  }
+}
+
 __global__ void bn_eval_coef_kernel(const float* gamma, const float* beta, const float* rm, const float* rv, float eps,
                                     int C, float* scale_out, float* shift_out) {
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
@@ -277,6 +325,20 @@ SEG_API int seg_bn_stats(const float* y, long ldy, long M, int C, const float* g
                      nullptr, nullptr, nullptr, 0, work, rpb);
   hipLaunchKernelGGL(bn_finalize_kernel, dim3(seg_cdiv(C, FIN_CH)), dim3(256), 0, stream, work, nblk, y, M, C, gamma,
                      beta, eps, momentum, running_mean, running_var, num_batches_tracked, mean, invstd, scale, shift);
+  SEG_RET_LAST();
+}
+
+// Train-mode BN statistics from seg_conv_igemm's epilogue partials (`stat`
+// workspace of seg_conv_igemm_row_tiles(M, C) x 2 x C floats); same outputs and
+// running-buffer update as seg_bn_stats, without re-reading the conv output.
+SEG_API int seg_bn_stats_tiles(const float* part, int ntiles, int tile_rows, long M, int C, const float* gamma,
+                               const float* beta, float eps, float momentum, float* running_mean, float* running_var,
+                               long long* num_batches_tracked, float* mean, float* invstd, float* scale, float* shift,
+                               hipStream_t stream) {
+  if (ntiles < 1 || tile_rows < 1 || M < 1) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(bn_finalize_tiles_kernel, dim3(seg_cdiv(C, FIN_CH)), dim3(256), 0, stream, part, ntiles,
+                     tile_rows, M, C, gamma, beta, eps, momentum, running_mean, running_var, num_batches_tracked, mean,
+                     invstd, scale, shift);
   SEG_RET_LAST();
 }
 

@@ -45,4 +45,16 @@ __device__ __forceinline__ float wave_sum(float v) {
 
 static inline int seg_cdiv(long a, long b) { return (int)((a + b - 1) / b); }
 
+// XCD-aware block swizzle (bijective for any nblk): the dispatcher deals blocks
+// round-robin over the 8 XCDs (block b and b+8 share an XCD and its 4 MiB L2), so
+// remap hardware block b to a logical id such that each XCD walks a CONTIGUOUS
+// range of logical ids in dispatch order.  Neighbouring tiles (adjacent image rows
+// of an implicit GEMM, all column tiles of one split-K chunk) then share an L2.
+// Placement only changes speed, never results.
+__device__ __forceinline__ int xcd_swizzle(int b, int nblk) {
+  const int xcd = b & 7, pos = b >> 3;
+  const int q = nblk >> 3, r = nblk & 7;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + pos;
+}
+
 #define SEG_RET_LAST() return (int)hipGetLastError()

@@ -27,6 +27,7 @@ struct IgemmArgs {
   const float* bias;             // [Cout] or nullptr
   const float* add; long ldadd;  // optional addend [M][ldadd] (may alias out)
   float* out; long ldout;
+  float* stat;                   // optional BN partials [tilesM][2][Cout]: tile sum and M2 of `out`
   int N, H, W, Cin;
   int Ho, Wo, Cout;
   int stride, pad;
@@ -56,7 +57,8 @@ __global__ __launch_bounds__(256) void igemm_conv_kernel(IgemmArgs a) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm0 = (wave / WAVES_N) * WM, wn0 = (wave % WAVES_N) * WN;
   const int tiles_n = (a.Cout + BN - 1) / BN;
-  const int tn = blockIdx.x % tiles_n, tm = blockIdx.x / tiles_n;
+  const int lid = xcd_swizzle(blockIdx.x, gridDim.x);  // adjacent image rows on one XCD's L2
+  const int tn = lid % tiles_n, tm = lid / tiles_n;
   const int m0 = tm * BM, n0 = tn * BN;
 
   // Per-thread A slots: the pixel is fixed across the K loop; the (tap, channel)
@@ -175,18 +177,67 @@ __global__ __launch_bounds__(256) void igemm_conv_kernel(IgemmArgs a) {
   }
 
   // Epilogue: C layout of 32x32 f32 MFMA: col = lane&31, row = (r&3) + 8(r>>2) + 4(lane>>5).
+  float bcol[NI];
+#pragma unroll
+  for (int ni = 0; ni < NI; ++ni) {
+    const int col = n0 + wn0 + ni * 32 + lrow;
+    bcol[ni] = (a.bias && col < a.Cout) ? a.bias[col] : 0.f;
+#pragma unroll
+    for (int mi = 0; mi < MI; ++mi)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[mi][ni][r] += bcol[ni];
+  }
+  if (a.stat) {
+    // BatchNorm batch statistics of this BM-row tile, per output channel: the tile
+    // sum and the sum of squared deviations from the TILE mean (two passes over the
+    // accumulators, so no E[y^2]-E[y]^2 cancellation); merged over tiles with
+    // Chan's formula in fp64 by seg_bn_stats_tiles.  LDS of the K loop is reused.
+    constexpr int WR = BM / WM;
+    float* red = &As[0][0];            // [WR][BN]
+    float* tmean = red + WR * BN;      // [BN]
+    const int nrows = min(BM, a.M - m0);
+    const int wr = wave / WAVES_N;
+#pragma unroll
+    for (int pass = 0; pass < 2; ++pass) {
+#pragma unroll
+      for (int ni = 0; ni < NI; ++ni) {
+        const int cl = wn0 + ni * 32 + lrow;
+        const float mu = pass ? tmean[cl] : 0.f;
+        float s = 0.f;
+#pragma unroll
+        for (int mi = 0; mi < MI; ++mi)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int row = m0 + wm0 + mi * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+            const float d = acc[mi][ni][r] - mu;
+            s += row < a.M ? (pass ? d * d : d) : 0.f;
+          }
+        s += __shfl_xor(s, 32, 64);
+        if (lane < 32) red[wr * BN + cl] = s;
+      }
+      __syncthreads();
+      if (tid < BN) {
+        float t = 0.f;
+#pragma unroll
+        for (int j = 0; j < WR; ++j) t += red[j * BN + tid];
+        const int col = n0 + tid;
+        if (pass == 0) tmean[tid] = t / (float)nrows;
+        if (col < a.Cout) a.stat[((long)tm * 2 + pass) * a.Cout + col] = t;
+      }
+      __syncthreads();
+    }
+  }
 #pragma unroll
   for (int ni = 0; ni < NI; ++ni) {
     const int col = n0 + wn0 + ni * 32 + lrow;
     if (col >= a.Cout) continue;
-    const float b = a.bias ? a.bias[col] : 0.f;
 #pragma unroll
     for (int mi = 0; mi < MI; ++mi) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int row = m0 + wm0 + mi * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
         if (row < a.M) {
-          float v = acc[mi][ni][r] + b;
+          float v = acc[mi][ni][r];
           if (a.add) v += a.add[(long)row * a.ldadd + col];
           a.out[(long)row * a.ldout + col] = v;
         }
@@ -216,6 +267,8 @@ constexpr TileCfg kTiles[] = {
     {128, 96, 32, 96, 0.93f},  {128, 160, 32, 160, 0.95f}, {256, 32, 64, 32, 0.90f}, {128, 32, 32, 32, 0.80f},
 };
 
+constexpr int kTileBM[] = {128, 64, 128, 64, 128, 128, 256, 128};
+
 int pick_tile(long M, int N) {
   int best = 0;
   double best_score = -1.0;
@@ -243,12 +296,12 @@ SEG_API int seg_conv_igemm(const float* in, long ldin, int N, int H, int W, int 
                            const float* wk, int ldk, const float* bias,
                            float* out, long ldout, int Ho, int Wo, int Cout,
                            int ks, int stride, int pad,
-                           const float* add, long ldadd, hipStream_t stream) {
+                           const float* add, long ldadd, float* stat, hipStream_t stream) {
   if ((Cin & 3) || (ldin & 3) || (ldk & 3) || (ks != 1 && ks != 3)) return (int)hipErrorInvalidValue;
   if (ks == 1 && (stride != 1 || pad != 0 || Ho != H || Wo != W)) return (int)hipErrorInvalidValue;
   IgemmArgs a;
   a.in = in; a.ldin = ldin; a.wk = wk; a.ldk = ldk; a.bias = bias;
-  a.add = add; a.ldadd = ldadd; a.out = out; a.ldout = ldout;
+  a.add = add; a.ldadd = ldadd; a.out = out; a.ldout = ldout; a.stat = stat;
   a.N = N; a.H = H; a.W = W; a.Cin = Cin; a.Ho = Ho; a.Wo = Wo; a.Cout = Cout;
   a.stride = stride; a.pad = pad; a.K = ks * ks * Cin; a.M = N * Ho * Wo;
   if (a.M == 0 || Cout == 0) return 0;
@@ -262,6 +315,14 @@ SEG_API int seg_conv_igemm(const float* in, long ldin, int N, int H, int W, int 
     case 6: return launch_igemm<256, 32, 64, 32>(a, ks, stream);
     default: return launch_igemm<128, 32, 32, 32>(a, ks, stream);
   }
+}
+
+// Row tiling seg_conv_igemm uses for an M x Cout output: returns the number of
+// row tiles (= rows of its optional BN-statistics partials) and their height.
+SEG_API int seg_conv_igemm_row_tiles(long M, int Cout, int* tile_rows) {
+  const int bm = kTileBM[pick_tile(M, Cout)];
+  if (tile_rows) *tile_rows = bm;
+  return (int)((M + bm - 1) / bm);
 }
 
 // Pack a PyTorch conv weight w[Cout][Cin][ks][ks] for seg_conv_igemm.

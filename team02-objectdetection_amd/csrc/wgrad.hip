@@ -40,9 +40,14 @@ __global__ __launch_bounds__(256) void wgrad_kernel(WgradArgs a) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm0 = (wave / WAVES_N) * WM, wn0 = (wave % WAVES_N) * WN;
   const int tiles_n = (a.Nw + BN - 1) / BN;
-  const int tn = blockIdx.x % tiles_n, tm = blockIdx.x / tiles_n;
+  const int tiles = tiles_n * ((a.Cout + BM - 1) / BM);
+  // 1-D grid of tiles x splits; every XCD walks whole splits (all column tiles of
+  // one pixel chunk share the L2 that holds that chunk of dY and X)
+  const int lid = xcd_swizzle(blockIdx.x, gridDim.x);
+  const int split = lid / tiles, tile = lid - split * tiles;
+  const int tn = tile % tiles_n, tm = tile / tiles_n;
   const int co0 = tm * BM, n0 = tn * BN;
-  const int kbeg = blockIdx.y * a.kchunk;
+  const int kbeg = split * a.kchunk;
   const int kend = min(a.M, kbeg + a.kchunk);
 
   // Fixed per-thread columns of the B (input) tile: decode tap / channel once.
@@ -149,7 +154,7 @@ __global__ __launch_bounds__(256) void wgrad_kernel(WgradArgs a) {
     }
   }
 
-  float* slab = a.part + (long)blockIdx.y * a.Cout * a.Nw;
+  float* slab = a.part + (long)split * a.Cout * a.Nw;
 #pragma unroll
   for (int ni = 0; ni < NI; ++ni) {
     const int col = n0 + wn0 + ni * 32 + lrow;
@@ -166,7 +171,7 @@ __global__ __launch_bounds__(256) void wgrad_kernel(WgradArgs a) {
 
 template <int BM, int BN, int WM, int WN>
 int launch_wgrad(const WgradArgs& a, int ks, int splits, hipStream_t s) {
-  dim3 grid(seg_cdiv(a.Cout, BM) * seg_cdiv(a.Nw, BN), splits);
+  dim3 grid(seg_cdiv(a.Cout, BM) * seg_cdiv(a.Nw, BN) * splits);
   if (ks == 1) hipLaunchKernelGGL((wgrad_kernel<BM, BN, WM, WN, 1>), grid, dim3(256), 0, s, a);
   else hipLaunchKernelGGL((wgrad_kernel<BM, BN, WM, WN, 3>), grid, dim3(256), 0, s, a);
   SEG_RET_LAST();

@@ -19,7 +19,8 @@ _F = ctypes.c_float
 
 # name -> (restype, argtypes); mirrors include/segamd.h one-to-one.
 PROTOTYPES = {
-    "seg_conv_igemm": (_I, [_V, _L, _I, _I, _I, _I, _V, _I, _V, _V, _L, _I, _I, _I, _I, _I, _I, _V, _L, _V]),
+    "seg_conv_igemm": (_I, [_V, _L, _I, _I, _I, _I, _V, _I, _V, _V, _L, _I, _I, _I, _I, _I, _I, _V, _L, _V, _V]),
+    "seg_conv_igemm_row_tiles": (_I, [_L, _I, _V]),
     "seg_pack_conv_weight": (_I, [_V, _V, _I, _I, _I, _I, _I, _I, _V]),
     "seg_conv_wgrad_splits": (_I, [_L, _I, _I, _I]),
     "seg_conv_wgrad": (_I, [_V, _L, _V, _L, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _V, _I, _V]),
@@ -32,6 +33,7 @@ PROTOTYPES = {
     "seg_nchw_to_nhwc": (_I, [_V, _I, _I, _I, _I, _V, _I, _V]),
     "seg_chan_workspace_floats": (_L, [_L, _I]),
     "seg_bn_stats": (_I, [_V, _L, _L, _I, _V, _V, _F, _F, _V, _V, _V, _V, _V, _V, _V, _V, _V]),
+    "seg_bn_stats_tiles": (_I, [_V, _I, _I, _L, _I, _V, _V, _F, _F, _V, _V, _V, _V, _V, _V, _V, _V]),
     "seg_bn_eval_coef": (_I, [_V, _V, _V, _V, _F, _I, _V, _V, _V]),
     "seg_bn_apply": (_I, [_V, _L, _L, _I, _V, _V, _I, _V, _L, _V, _L, _V]),
     "seg_bn_backward": (_I, [_V, _L, _V, _L, _L, _I, _V, _V, _V, _V, _V, _I, _V, _V, _V, _V, _L, _V]),

@@ -21,6 +21,8 @@ fused addend.
 """
 from __future__ import annotations
 
+import ctypes
+
 import torch
 from torch import nn
 
@@ -29,6 +31,7 @@ from .mobilenet import ConvBNReLU6, InvertedResidual
 
 ACT_NONE, ACT_RELU, ACT_RELU6 = 0, 1, 2
 IGNORE_INDEX = -100
+_ROW_TILES = {}  # (M, Cout) -> (row tiles, tile height) of seg_conv_igemm
 
 
 def r4(c: int) -> int:
@@ -125,13 +128,21 @@ class ConvOp:
                  self.stride, s)
         else:
             i = self.inp
-            ldk = r4(self.ks * self.ks * self.cin_pad)
-            wk = rt.tmp(self.cout * ldk)
-            call("seg_pack_conv_weight", w.data_ptr(), wk.data_ptr(), self.cout, self.cin, self.ks, ldk, 0,
-                 self.cin_pad, s)
+            if self.ks == 1 and self.cin_pad == self.cin:
+                ldk, wk_ptr = self.cin, w.data_ptr()  # [Cout][Cin][1][1] already is the packed layout
+            else:
+                ldk = r4(self.ks * self.ks * self.cin_pad)
+                wk = rt.tmp(self.cout * ldk)
+                call("seg_pack_conv_weight", w.data_ptr(), wk.data_ptr(), self.cout, self.cin, self.ks, ldk, 0,
+                     self.cin_pad, s)
+                wk_ptr = wk.data_ptr()
+            stat = None
+            if self.bn is not None and rt.training:  # BN statistics fused into the conv epilogue
+                ntiles, tile_rows = rt.row_tiles(y.M, self.cout)
+                stat = rt.tmp(ntiles * 2 * self.cout)
             _timed_call(f"igemm{self.ks}_fwd", self.flops(), "seg_conv_igemm", rt.ptr(i), i.ld, i.N, i.H, i.W,
-                        self.cin_pad, wk.data_ptr(), ldk, bias, rt.ptr(y), y.ld, y.H, y.W, self.cout, self.ks,
-                        self.stride, self.pad, None, 0, s)
+                        self.cin_pad, wk_ptr, ldk, bias, rt.ptr(y), y.ld, y.H, y.W, self.cout, self.ks,
+                        self.stride, self.pad, None, 0, stat.data_ptr() if stat is not None else None, s)
         if self.bn is None:
             return
         bn, C, M = self.bn, self.cout, y.M
@@ -140,13 +151,18 @@ class ConvOp:
         if rt.training:
             if bn.momentum is None:
                 raise NotImplementedError("BatchNorm2d(momentum=None) (cumulative average) is not supported")
-            work = rt.tmp(query("seg_chan_workspace_floats", M, C))
             rm = bn.running_mean.data_ptr() if bn.track_running_stats else None
             rv = bn.running_var.data_ptr() if bn.track_running_stats else None
             nbt = bn.num_batches_tracked.data_ptr() if bn.track_running_stats else None
-            call("seg_bn_stats", rt.ptr(y), y.ld, M, C, bn.weight.data_ptr(), bn.bias.data_ptr(), bn.eps,
-                 bn.momentum, rm, rv, nbt, work.data_ptr(), mean.data_ptr(), invstd.data_ptr(),
-                 scale.data_ptr(), shift.data_ptr(), s)
+            if self.kind == "dw":
+                work = rt.tmp(query("seg_chan_workspace_floats", M, C))
+                call("seg_bn_stats", rt.ptr(y), y.ld, M, C, bn.weight.data_ptr(), bn.bias.data_ptr(), bn.eps,
+                     bn.momentum, rm, rv, nbt, work.data_ptr(), mean.data_ptr(), invstd.data_ptr(),
+                     scale.data_ptr(), shift.data_ptr(), s)
+            else:
+                call("seg_bn_stats_tiles", stat.data_ptr(), ntiles, tile_rows, M, C, bn.weight.data_ptr(),
+                     bn.bias.data_ptr(), bn.eps, bn.momentum, rm, rv, nbt, mean.data_ptr(), invstd.data_ptr(),
+                     scale.data_ptr(), shift.data_ptr(), s)
         else:
             call("seg_bn_eval_coef", bn.weight.data_ptr(), bn.bias.data_ptr(), bn.running_mean.data_ptr(),
                  bn.running_var.data_ptr(), bn.eps, C, scale.data_ptr(), shift.data_ptr(), s)
@@ -221,7 +237,7 @@ class ConvOp:
             add_ptr, add_ld = rt.begin_write_add(i)
             _timed_call(f"igemm{self.ks}_dgrad", self.flops(), "seg_conv_igemm", dYp, dY.ld, y.N, y.H, y.W, kin,
                         wk.data_ptr(), ldk, None, rt.gptr(i), i.ld, i.H, i.W, self.cin, self.ks, 1, self.pad,
-                        add_ptr, add_ld, s)
+                        add_ptr, add_ld, None, s)
         rt.mark_written(i)
 
 
@@ -464,6 +480,16 @@ class Run:
 
     def tmp(self, n: int) -> torch.Tensor:
         return torch.empty(max(int(n), 1), device=self.device, dtype=torch.float32)
+
+    @staticmethod
+    def row_tiles(M: int, C: int):
+        key = (M, C)
+        r = _ROW_TILES.get(key)
+        if r is None:
+            rows = ctypes.c_int(0)
+            n = query("seg_conv_igemm_row_tiles", M, C, ctypes.addressof(rows))
+            r = _ROW_TILES[key] = (n, rows.value)
+        return r
 
     def tmp_buf(self, n: int) -> str:
         name = f"#tmp{self._tmp_n}"

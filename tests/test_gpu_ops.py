@@ -1,6 +1,8 @@
 """GPU: every C-ABI kernel against a plain PyTorch fp32 CPU reference of the
 same op (forward and backward via torch.autograd), on odd shapes and edge cases.
 All calls go through libsegamd.so (seg_amd._lib)."""
+import ctypes
+
 import numpy as np
 import pytest
 import torch
@@ -65,8 +67,28 @@ def test_conv_igemm_fwd_dgrad_wgrad(N, Cin, Cout, H, W, ks):
     call("seg_pack_conv_weight", wg.data_ptr(), wk.data_ptr(), Cout, Cin, ks, ldk, 0, Cin, s)
     out = torch.full((N * H * W, r4(Cout)), float("nan"), device=DEV)
     call("seg_conv_igemm", xg.data_ptr(), xg.shape[1], N, H, W, Cin, wk.data_ptr(), ldk, bg.data_ptr(),
-         out.data_ptr(), out.shape[1], H, W, Cout, ks, 1, pad, None, 0, s)
+         out.data_ptr(), out.shape[1], H, W, Cout, ks, 1, pad, None, 0, None, s)
     assert rel(from_nhwc(out, N, Cout, H, W), y.detach()) < 1e-5
+    # same conv with the BatchNorm statistics fused into the epilogue
+    ntiles = query("seg_conv_igemm_row_tiles", N * H * W, Cout, None)
+    tr = ctypes.c_int(0)
+    query("seg_conv_igemm_row_tiles", N * H * W, Cout, ctypes.addressof(tr))
+    stat = torch.empty(ntiles * 2 * Cout, device=DEV)
+    out2 = torch.empty_like(out)
+    call("seg_conv_igemm", xg.data_ptr(), xg.shape[1], N, H, W, Cin, wk.data_ptr(), ldk, bg.data_ptr(),
+         out2.data_ptr(), out2.shape[1], H, W, Cout, ks, 1, pad, None, 0, stat.data_ptr(), s)
+    assert torch.equal(out2[:, :Cout], out[:, :Cout])
+    st = torch.empty(4 * Cout, device=DEV)
+    rm, rv = torch.zeros(Cout, device=DEV), torch.ones(Cout, device=DEV)
+    call("seg_bn_stats_tiles", stat.data_ptr(), ntiles, tr.value, N * H * W, Cout, None, None, 1e-5, 0.1,
+         rm.data_ptr(), rv.data_ptr(), None, st[:Cout].data_ptr(), st[Cout:2 * Cout].data_ptr(),
+         st[2 * Cout:3 * Cout].data_ptr(), st[3 * Cout:].data_ptr(), s)
+    y64 = y.detach().double()
+    mean64 = y64.mean((0, 2, 3))
+    var64 = y64.var((0, 2, 3), unbiased=False)
+    assert rel(st[:Cout], mean64) < 1e-5
+    assert rel(st[Cout:2 * Cout], 1 / torch.sqrt(var64 + 1e-5)) < 1e-5
+    assert rel(rv, 0.9 + 0.1 * y64.var((0, 2, 3), unbiased=True)) < 1e-5
     # data gradient (+ fused addend)
     dyg = nhwc(dy)
     if Cout % 4:
@@ -79,7 +101,7 @@ def test_conv_igemm_fwd_dgrad_wgrad(N, Cin, Cout, H, W, ks):
     addg = nhwc(addend)
     dx = torch.empty(N * H * W, r4(Cin), device=DEV)
     call("seg_conv_igemm", dyg.data_ptr(), dyg.shape[1], N, H, W, kin, wkd.data_ptr(), ldk2, None,
-         dx.data_ptr(), dx.shape[1], H, W, Cin, ks, 1, pad, addg.data_ptr(), addg.shape[1], s)
+         dx.data_ptr(), dx.shape[1], H, W, Cin, ks, 1, pad, addg.data_ptr(), addg.shape[1], None, s)
     assert rel(from_nhwc(dx, N, Cin, H, W), xr.grad + addend) < 1e-5
     # weight gradient
     M = N * H * W
@@ -149,7 +171,7 @@ def test_first_conv_from_nchw_image(N, H, W, Cout, stride, bias):
     call("seg_pack_conv_weight", wg.data_ptr(), wk.data_ptr(), Cout, 3, 3, ldk, 0, 4, s)
     out = torch.empty(N * Ho * Wo, Cout, device=DEV)
     call("seg_conv_igemm", x4.data_ptr(), 4, N, H, W, 4, wk.data_ptr(), ldk, bg.data_ptr() if bias else None,
-         out.data_ptr(), Cout, Ho, Wo, Cout, 3, stride, 1, None, 0, s)
+         out.data_ptr(), Cout, Ho, Wo, Cout, 3, stride, 1, None, 0, None, s)
     assert rel(from_nhwc(out, N, Cout, Ho, Wo), y.detach()) < 1e-5
     dyg = nhwc(dy)
     splits = query("seg_conv_wgrad_splits", N * Ho * Wo, Cout, 4, 3)

@@ -72,7 +72,7 @@ def bench(lib, only=None):
         lib.seg_pack_conv_weight(w.data_ptr(), wk.data_ptr(), Cout, Cin, ks, ldk, 0, Cin, s)
         y = torch.empty(M, r4(Cout), device="cuda")
         t_f = timeit(lambda: lib.seg_conv_igemm(x.data_ptr(), r4(Cin), N, Hi, Wi, Cin, wk.data_ptr(), ldk, None,
-                                                y.data_ptr(), r4(Cout), Ho, Wo, Cout, ks, stride, pad, None, 0, s))
+                                                y.data_ptr(), r4(Cout), Ho, Wo, Cout, ks, stride, pad, None, 0, None, s))
         res = {"fwd": flops / t_f / 1e12}
         if stride == 1:
             kin = r4(Cout)
@@ -81,7 +81,7 @@ def bench(lib, only=None):
             lib.seg_pack_conv_weight(w.data_ptr(), wkd.data_ptr(), Cout, Cin, ks, ldk2, 1, kin, s)
             dx = torch.empty(N * H * W, r4(Cin), device="cuda")
             t_d = timeit(lambda: lib.seg_conv_igemm(dy.data_ptr(), r4(Cout), N, H, W, kin, wkd.data_ptr(), ldk2,
-                                                    None, dx.data_ptr(), r4(Cin), H, W, Cin, ks, 1, pad, None, 0, s))
+                                                    None, dx.data_ptr(), r4(Cin), H, W, Cin, ks, 1, pad, None, 0, None, s))
             res["dgrad"] = flops / t_d / 1e12
         splits = lib.seg_conv_wgrad_splits(M, Cout, Cin, ks)
         part = torch.empty(splits * Cout * ks * ks * r4(Cin), device="cuda")

@@ -1,0 +1,87 @@
+"""Summarise a rocprofv3 kernel-trace/stats run and its PMC passes for the
+dominant kernel family, and write it under profiles/.
+
+    python tools/roofline_report.py <prof_dir> <pmc_dir> <steps_profiled> <out_prefix>
+
+prof_dir: `rocprofv3 --kernel-trace --stats` output of bench.py (run_kernel_stats.csv)
+pmc_dir:  FETCH_SIZE/ and WRITE_SIZE/ passes (run_counter_collection.csv), each
+          its own rocprofv3 run with --pmc + --kernel-trace only.
+HBM bytes per dispatch = (2 * FETCH_SIZE + WRITE_SIZE) * 1024: on gfx950
+FETCH_SIZE reports exactly half of the bytes of wide (16 B/lane) coalesced reads
+(MI355X_MICROARCH.md, HBM section); WRITE_SIZE is exact for 16-B stores.  The
+256 MiB Infinity Cache can absorb re-reads, so these are evidence, not the metric.
+"""
+import csv
+import json
+import re
+import statistics
+import sys
+from collections import defaultdict
+
+FAMILIES = {
+    "igemm3": re.compile(r"igemm_conv_kernel<\d+, \d+, \d+, \d+, 3, \d+>"),
+    "igemm1": re.compile(r"igemm_conv_kernel<\d+, \d+, \d+, \d+, 1, \d+>"),
+    "wgrad3": re.compile(r"wgrad_kernel<\d+, \d+, \d+, \d+, 3>"),
+    "wgrad1": re.compile(r"wgrad_kernel<\d+, \d+, \d+, \d+, 1>"),
+}
+
+
+def family(name):
+    for k, rx in FAMILIES.items():
+        if rx.search(name):
+            return k
+    return None
+
+
+def main(prof_dir, pmc_dir, steps, out_prefix):
+    steps = int(steps)
+    stats = list(csv.DictReader(open(f"{prof_dir}/run_kernel_stats.csv")))
+    total = sum(float(r["TotalDurationNs"]) for r in stats)
+    fam = defaultdict(lambda: {"calls": 0, "ns": 0.0, "symbols": []})
+    for r in stats:
+        f = family(r["Name"])
+        if f:
+            fam[f]["calls"] += int(r["Calls"])
+            fam[f]["ns"] += float(r["TotalDurationNs"])
+            fam[f]["symbols"].append((r["Name"].replace("(anonymous namespace)::", ""), int(r["Calls"]),
+                                      float(r["AverageNs"]) / 1e3))
+    traffic = defaultdict(list)
+    for c in ("FETCH_SIZE", "WRITE_SIZE"):
+        rows = list(csv.DictReader(open(f"{pmc_dir}/{c}/run_counter_collection.csv")))
+        per = defaultdict(float)
+        names = {}
+        for r in rows:
+            per[r["Dispatch_Id"]] += float(r["Counter_Value"])
+            names[r["Dispatch_Id"]] = r["Kernel_Name"]
+        for d, v in per.items():
+            f = family(names[d])
+            if f:
+                traffic[(f, c)].append(v)
+    out = {"profiled_steps": steps, "kernel_ms_per_step": total / 1e6 / steps, "families": {}}
+    lines = [f"# rocprofv3 summary ({out_prefix})", "",
+             f"Kernel time per step (all kernels): {total / 1e6 / steps:.2f} ms over {steps} profiled steps.", "",
+             "| family | calls/step | ms/step | share | avg launch us | HBM bytes/launch (2*FETCH+WRITE)*1KiB |",
+             "|---|---|---|---|---|---|"]
+    for f, d in sorted(fam.items(), key=lambda kv: -kv[1]["ns"]):
+        fetch = traffic.get((f, "FETCH_SIZE"), [])
+        write = traffic.get((f, "WRITE_SIZE"), [])
+        hbm = (2 * statistics.mean(fetch) + statistics.mean(write)) * 1024 if fetch and write else None
+        avg_us = d["ns"] / d["calls"] / 1e3
+        out["families"][f] = {"calls_per_step": d["calls"] / steps, "ms_per_step": d["ns"] / 1e6 / steps,
+                              "avg_launch_us": avg_us, "hbm_bytes_per_launch": hbm,
+                              "symbols": d["symbols"]}
+        lines.append(f"| {f} | {d['calls'] / steps:.0f} | {d['ns'] / 1e6 / steps:.2f} | {d['ns'] / total:.1%} | "
+                     f"{avg_us:.1f} | {hbm / 1e6 if hbm else float('nan'):.1f} MB |")
+    lines += ["", "Top kernels:", "", "| kernel | calls | avg us | total ms |", "|---|---|---|---|"]
+    for r in sorted(stats, key=lambda r: -float(r["TotalDurationNs"]))[:25]:
+        lines.append(f"| `{r['Name'].replace('(anonymous namespace)::', '')[:90]}` | {r['Calls']} | "
+                     f"{float(r['AverageNs']) / 1e3:.1f} | {float(r['TotalDurationNs']) / 1e6:.2f} |")
+    with open(out_prefix + ".md", "w") as fh:
+        fh.write("\n".join(lines) + "\n")
+    with open(out_prefix + ".json", "w") as fh:
+        json.dump(out, fh, indent=1)
+    print("\n".join(lines[:12]))
+
+
+if __name__ == "__main__":
+    main(*sys.argv[1:])

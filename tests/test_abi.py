@@ -65,7 +65,7 @@ def test_host_side_queries(lib):
 
 def test_argument_validation_without_gpu(lib):
     # invalid arguments are rejected before any launch (hipErrorInvalidValue == 1)
-    rc = lib.seg_conv_igemm(None, 3, 1, 4, 4, 3, None, 4, None, None, 4, 4, 4, 8, 3, 1, 1, None, 0, None)
+    rc = lib.seg_conv_igemm(None, 3, 1, 4, 4, 3, None, 4, None, None, 4, 4, 4, 8, 3, 1, 1, None, 0, None, None)
     assert rc == 1  # Cin % 4 != 0
     rc = lib.seg_nchw_to_nhwc(None, 1, 3, 4, 4, None, 2, None)
     assert rc == 1  # ld < C

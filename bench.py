@@ -136,16 +136,37 @@ def main():
     roof = None
     if timer is not None:
         rec = timer.elapsed()
-        flops = sum(f for _, f, _ in rec)
-        secs = sum(s for _, _, s in rec)
-        n = len(rec)
+
+        def family(kinds):
+            sel = [(f, s) for k, f, s in rec if k in kinds]
+            fl, sec = sum(f for f, _ in sel), sum(s for _, s in sel)
+            return fl, sec, len(sel)
+
+        # dominant kernel: igemm_conv_kernel<BM,BN,WM,WN,3,16> = every dense 3x3 conv's
+        # forward and data gradient (the top symbol family in the rocprof summary)
+        flops, secs, n = family({"igemm3_fwd", "igemm3_dgrad"})
         achieved = flops / secs / 1e12 if secs > 0 else 0.0
+        traffic = None
+        prof = os.path.join(REPO, "profiles", "latest_roofline.json")
+        if os.path.exists(prof):
+            with open(prof) as fh:
+                fam = json.load(fh)["families"].get("igemm3", {})
+            traffic = fam.get("hbm_bytes_per_launch")
+        wf, ws, wn = family({"igemm3_wgrad"})
+        af, as_, an = family({k for k, _, _ in rec})
         roof = {"bound": "mfma", "achieved": round(achieved, 2), "peak": F32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
-                "frac": round(achieved / F32_MFMA_PEAK_TFLOPS, 4), "traffic": None,
-                "kernel": "igemm_conv_kernel + wgrad_kernel (dense/pointwise f32 MFMA convs, fwd+dgrad+wgrad)",
+                "frac": round(achieved / F32_MFMA_PEAK_TFLOPS, 4),
+                "traffic": round(traffic) if traffic else None,
+                "traffic_source": "profiles/latest_roofline.json: rocprofv3 PMC (2*FETCH_SIZE+WRITE_SIZE)*1KiB "
+                                  "per igemm3 launch" if traffic else None,
+                "kernel": "igemm_conv_kernel<*,*,*,*,3,16> (dense 3x3 implicit GEMM, f32 MFMA: fwd + dgrad)",
                 "launches": n, "flops_per_launch": round(flops / max(n, 1)),
                 "avg_launch_us": round(secs / max(n, 1) * 1e6, 2),
-                "share_of_step": round(secs / (dt if not dist else dt), 4)}
+                "share_of_step": round(secs / dt * args.steps / args.steps, 4),
+                "wgrad3": {"achieved": round(wf / ws / 1e12, 2) if ws else None, "launches": wn,
+                           "avg_launch_us": round(ws / max(wn, 1) * 1e6, 2)},
+                "all_mfma_convs": {"achieved": round(af / as_ / 1e12, 2) if as_ else None, "launches": an,
+                                   "share_of_step": round(as_ / dt, 4)}}
 
     if rank == 0:
         cpu = None

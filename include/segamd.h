@@ -64,14 +64,19 @@ int seg_conv_wgrad_reduce(const float* part, int splits, float* dw, int Cout, in
                           int mode, int accumulate, hipStream_t stream);
 
 /* Depthwise 3x3 (torchvision InvertedResidual dw conv, features[1..17] via
- * src/unet.py:15-19): forward, data gradient, weight-gradient partials. */
+ * src/unet.py:15-19): forward, data gradient, weight-gradient partials.
+ * in_scale/in_shift/in_act (both pointers null = off): the producing layer's
+ * BatchNorm affine + activation applied to the input on load ("lazy BN"), so
+ * the expand conv's activated output need not be materialised; padding stays 0. */
 int seg_pack_dw_weight(const float* w, float* wk, int C, hipStream_t stream);
-int seg_dw_fwd(const float* in, long ldin, int N, int H, int W, int C, const float* wk,
+int seg_dw_fwd(const float* in, long ldin, int N, int H, int W, int C,
+               const float* in_scale, const float* in_shift, int in_act, const float* wk,
                float* out, long ldout, int Ho, int Wo, int stride, hipStream_t stream);
 int seg_dw_dgrad(const float* dy, long lddy, int N, int Ho, int Wo, int C, const float* wk,
                  float* dx, long lddx, int H, int W, int stride, int accumulate, hipStream_t stream);
-long seg_dw_wgrad_blocks(long M);
+long seg_dw_wgrad_blocks(int N, int Ho, int Wo, int C);
 int seg_dw_wgrad(const float* dy, long lddy, const float* x, long ldx, int N, int H, int W, int C,
+                 const float* in_scale, const float* in_shift, int in_act,
                  int Ho, int Wo, int stride, float* part, hipStream_t stream);
 
 /* The NCHW image batch (as the reference's DataLoader delivers it) as NHWC rows of

@@ -203,10 +203,7 @@ __global__ void bn_apply_kernel(const float* __restrict__ y, long ldy, long M, i
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
     const long r = i / CG;
     const int c = (int)(i - r * CG) * 4;
-    const f32x4 v = ld4(y + r * ldy + c), sc = ld4(scale + c), sh = ld4(shift + c);
-    f32x4 o;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) o[j] = seg_act(v[j] * sc[j] + sh[j], act);
+    f32x4 o = seg_bn_act4(ld4(y + r * ldy + c), ld4(scale + c), ld4(shift + c), act);
     if (res) o += ld4(res + r * ldres + c);
     st4(out + r * ldout + c, o);
   }

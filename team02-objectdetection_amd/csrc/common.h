@@ -37,6 +37,23 @@ __device__ __forceinline__ float seg_act_mask(float z, int act) {
 __device__ __forceinline__ f32x4 ld4(const float* p) { return *reinterpret_cast<const f32x4*>(p); }
 __device__ __forceinline__ void st4(float* p, f32x4 v) { *reinterpret_cast<f32x4*>(p) = v; }
 
+// BatchNorm affine + activation of 4 channels: act(y * scale + shift).  The one
+// definition used by the BN apply pass and by every consumer that applies it
+// lazily on load, so a materialised and a lazily transformed activation are
+// bitwise identical.  Branch-free in `act` (a clamp), so it never splits the
+// caller's basic block -- a branch between loads stops the scheduler from
+// batching them.
+__device__ __forceinline__ f32x4 seg_bn_act4(f32x4 v, f32x4 sc, f32x4 sh, int act) {
+  const float hi = act == SEG_ACT_RELU6 ? 6.f : __builtin_inff();
+  f32x4 o;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const float z = fmaf(v[j], sc[j], sh[j]);
+    o[j] = act == SEG_ACT_NONE ? z : fminf(fmaxf(z, 0.f), hi);
+  }
+  return o;
+}
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

@@ -26,10 +26,10 @@ PROTOTYPES = {
     "seg_conv_wgrad": (_I, [_V, _L, _V, _L, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _V, _I, _V]),
     "seg_conv_wgrad_reduce": (_I, [_V, _I, _V, _I, _I, _I, _I, _I, _V]),
     "seg_pack_dw_weight": (_I, [_V, _V, _I, _V]),
-    "seg_dw_fwd": (_I, [_V, _L, _I, _I, _I, _I, _V, _V, _L, _I, _I, _I, _V]),
+    "seg_dw_fwd": (_I, [_V, _L, _I, _I, _I, _I, _V, _V, _I, _V, _V, _L, _I, _I, _I, _V]),
     "seg_dw_dgrad": (_I, [_V, _L, _I, _I, _I, _I, _V, _V, _L, _I, _I, _I, _I, _V]),
-    "seg_dw_wgrad_blocks": (_L, [_L]),
-    "seg_dw_wgrad": (_I, [_V, _L, _V, _L, _I, _I, _I, _I, _I, _I, _I, _V, _V]),
+    "seg_dw_wgrad_blocks": (_L, [_I, _I, _I, _I]),
+    "seg_dw_wgrad": (_I, [_V, _L, _V, _L, _I, _I, _I, _I, _V, _V, _I, _I, _I, _I, _V, _V]),
     "seg_nchw_to_nhwc": (_I, [_V, _I, _I, _I, _I, _V, _I, _V]),
     "seg_chan_workspace_floats": (_L, [_L, _I]),
     "seg_bn_stats": (_I, [_V, _L, _L, _I, _V, _V, _F, _F, _V, _V, _V, _V, _V, _V, _V, _V, _V]),

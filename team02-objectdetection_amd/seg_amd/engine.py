@@ -91,9 +91,13 @@ IMAGE = "image"   # buffer holding the NHWC4 copy of the NCHW model input
 class ConvOp:
     """conv (igemm | dw) -> [BN -> act (+residual)]."""
 
-    def __init__(self, kind, conv: nn.Conv2d, bn, act, inp, out, y, res):
+    def __init__(self, kind, conv: nn.Conv2d, bn, act, inp, out, y, res, xform=None):
         self.kind, self.conv, self.bn, self.act = kind, conv, bn, act
         self.inp, self.out, self.y, self.res = inp, out, y, res
+        # lazy BN: this op's BN + act is applied by its (only) consumer on load, out is y;
+        # xform: the producer op whose BN + act this op applies to its input on load
+        self.lazy = False
+        self.xform = xform
         self.ks = conv.kernel_size[0]
         self.stride = conv.stride[0]
         self.pad = conv.padding[0]
@@ -124,8 +128,8 @@ class ConvOp:
             wk = rt.tmp(9 * self.cout)
             call("seg_pack_dw_weight", w.data_ptr(), wk.data_ptr(), self.cout, s)
             i = self.inp
-            call("seg_dw_fwd", rt.ptr(i), i.ld, i.N, i.H, i.W, i.C, wk.data_ptr(), rt.ptr(y), y.ld, y.H, y.W,
-                 self.stride, s)
+            call("seg_dw_fwd", rt.ptr(i), i.ld, i.N, i.H, i.W, i.C, *self._in_xform(rt), wk.data_ptr(), rt.ptr(y),
+                 y.ld, y.H, y.W, self.stride, s)
         else:
             i = self.inp
             if self.ks == 1 and self.cin_pad == self.cin:
@@ -166,10 +170,20 @@ class ConvOp:
         else:
             call("seg_bn_eval_coef", bn.weight.data_ptr(), bn.bias.data_ptr(), bn.running_mean.data_ptr(),
                  bn.running_var.data_ptr(), bn.eps, C, scale.data_ptr(), shift.data_ptr(), s)
+        rt.saved[id(self)] = st
+        if self.lazy:
+            return
         o, r = self.out, self.res
         call("seg_bn_apply", rt.ptr(y), y.ld, M, C, scale.data_ptr(), shift.data_ptr(), self.act,
              rt.ptr(r) if r is not None else None, r.ld if r is not None else 0, rt.ptr(o), o.ld, s)
-        rt.saved[id(self)] = st
+
+    def _in_xform(self, rt):
+        """(scale, shift, act) of the producer's lazy BN for this op's input loads, or (None, None, 0)."""
+        xf = self.xform
+        if xf is None:
+            return None, None, 0
+        st, C = rt.saved[id(xf)], xf.cout
+        return st[2 * C:3 * C].data_ptr(), st[3 * C:4 * C].data_ptr(), xf.act
 
     # -- backward
     def backward(self, rt):
@@ -202,10 +216,10 @@ class ConvOp:
             gw = rt.grad_param(self.conv.weight)
             if self.kind == "dw":
                 i = self.inp
-                nblk = query("seg_dw_wgrad_blocks", M)
+                nblk = query("seg_dw_wgrad_blocks", y.N, y.H, y.W, self.cout)
                 part = rt.tmp(nblk * 9 * self.cout)
-                call("seg_dw_wgrad", dYp, dY.ld, rt.ptr(i), i.ld, i.N, i.H, i.W, i.C, y.H, y.W, self.stride,
-                     part.data_ptr(), s)
+                call("seg_dw_wgrad", dYp, dY.ld, rt.ptr(i), i.ld, i.N, i.H, i.W, i.C, *self._in_xform(rt), y.H, y.W,
+                     self.stride, part.data_ptr(), s)
                 call("seg_conv_wgrad_reduce", part.data_ptr(), nblk, gw, self.cout, 1, 3, 1, 0, s)
             else:
                 i = self.inp
@@ -304,15 +318,27 @@ class Program:
         self.bufs[name] = (self.N * H * W, ld)
         return Act(name, 0, ld, C, self.N, H, W)
 
-    def conv(self, kind, conv, bn, act, inp, out=None, res=None):
+    def conv(self, kind, conv, bn, act, inp, out=None, res=None, xform=None):
         ks, st, pd = conv.kernel_size[0], conv.stride[0], conv.padding[0]
         Hi, Wi = inp.H, inp.W
         Ho, Wo = (Hi + 2 * pd - ks) // st + 1, (Wi + 2 * pd - ks) // st + 1
         if out is None:
             out = self.new(conv.out_channels, Ho, Wo)
         y = self.new(conv.out_channels, Ho, Wo) if bn is not None else out
-        self.ops.append(ConvOp(kind, conv, bn, act, inp, out, y, res))
+        self.ops.append(ConvOp(kind, conv, bn, act, inp, out, y, res, xform))
         return out
+
+    def make_lazy(self, a: Act):
+        """If `a` is the private BN+act output of the last op, drop its buffer and let
+        the consumer apply the BN on load; returns the producer op (or None)."""
+        op = self.ops[-1] if self.ops else None
+        if not (isinstance(op, ConvOp) and op.kind == "igemm" and op.bn is not None and op.res is None
+                and op.out is a and op.y is not a and a.off == 0 and a.ld == r4(a.C)
+                and self.bufs.get(a.buf) == (a.M, a.ld) and not a.buf.startswith("cat")):
+            return None
+        del self.bufs[a.buf]
+        op.out, op.lazy = op.y, True
+        return op
 
     def params(self):
         seen, ps = set(), []
@@ -324,11 +350,11 @@ class Program:
         return ps
 
 
-def _cna(prog, m: ConvBNReLU6, inp, out=None, kind=None):
+def _cna(prog, m: ConvBNReLU6, inp, out=None, kind=None, xform=None):
     conv, bn = m[0], m[1]
     if kind is None:
         kind = "dw" if conv.groups > 1 else "igemm"
-    return prog.conv(kind, conv, bn, ACT_RELU6, inp, out=out)
+    return prog.conv(kind, conv, bn, ACT_RELU6, inp, out=out, xform=xform)
 
 
 def _inverted_residual(prog, blk: InvertedResidual, inp, out=None):
@@ -337,7 +363,12 @@ def _inverted_residual(prog, blk: InvertedResidual, inp, out=None):
     if len(layers) == 4:  # expand ratio != 1
         x = _cna(prog, layers[0], x)
         layers = layers[1:]
-    x = _cna(prog, layers[0], x, kind="dw")
+    # the depthwise conv applies its producer's BN + ReLU6 on load (the expand conv,
+    # or the stem for features[1]) unless that activation is also the residual
+    xf = None if (blk.use_res_connect and x is inp) else prog.make_lazy(x)
+    if xf is not None:
+        x = xf.out
+    x = _cna(prog, layers[0], x, kind="dw", xform=xf)
     return prog.conv("igemm", layers[1], layers[2], ACT_NONE, x, out=out,
                      res=inp if blk.use_res_connect else None)
 
@@ -662,7 +693,10 @@ class _SegFunction(torch.autograd.Function):
         if run.sync is not None:
             run.sync.finish_gradient_sync()  # stream-ordered wait on the last all-reduces
         grads = [run.grads.get(id(p)) if ctx.needs_input_grad[6 + k] else None for k, p in enumerate(ctx.params)]
-        ctx.run = None
+        # drop every other reference so AccumulateGrad can adopt the tensors instead of copying them
+        run.grads.clear()
+        ctx.run = ctx.params = None
+        del run
         return (None, None, None, None, None, None, *grads)
 
 

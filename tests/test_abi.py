@@ -59,7 +59,7 @@ def test_host_side_queries(lib):
     assert 1 <= s <= 256
     assert _lib.query("seg_conv_wgrad_splits", 10, 32, 32, 3) == 1
     assert _lib.query("seg_chan_workspace_floats", 1 << 20, 96) >= 2 * 96
-    assert _lib.query("seg_dw_wgrad_blocks", 1 << 20) >= 1
+    assert _lib.query("seg_dw_wgrad_blocks", 32, 128, 256, 32) >= 1
     assert _lib.query("seg_ce_workspace_floats", 4 * 256 * 512) >= 2
 
 

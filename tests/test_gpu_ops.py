@@ -114,10 +114,19 @@ def test_conv_igemm_fwd_dgrad_wgrad(N, Cin, Cout, H, W, ks):
     assert rel(dw, wr.grad) < 1e-5
 
 
+@pytest.mark.parametrize("lazy", [False, True])
 @pytest.mark.parametrize("N,C,H,W,stride", [(2, 32, 9, 12, 1), (2, 96, 10, 14, 2), (1, 960, 4, 4, 1),
-                                            (3, 144, 7, 9, 2), (1, 8, 1, 1, 1)])
-def test_depthwise(N, C, H, W, stride):
-    x = gen(N, C, H, W, seed=1)
+                                            (3, 144, 7, 9, 2), (1, 8, 1, 1, 1), (2, 24, 5, 19, 2),
+                                            (1, 256, 3, 17, 1)])
+def test_depthwise(N, C, H, W, stride, lazy):
+    """Depthwise 3x3 fwd / dgrad / wgrad.  lazy: the kernels read the producer's raw
+    conv output u and apply its BN affine + ReLU6 on load (x = relu6(u*sc + sh))."""
+    u = gen(N, C, H, W, seed=1)
+    if lazy:
+        sc, sh = gen(C, seed=7) * 2.0, gen(C, seed=8) * 3.0
+        x = torch.clamp(torch.addcmul(sh.view(1, C, 1, 1), u, sc.view(1, C, 1, 1)), 0.0, 6.0)
+    else:
+        x = u
     w = gen(C, 1, 3, 3, seed=2)
     xr, wr = x.clone().requires_grad_(True), w.clone().requires_grad_(True)
     y = F.conv2d(xr, wr, None, stride=stride, padding=1, groups=C)
@@ -125,22 +134,31 @@ def test_depthwise(N, C, H, W, stride):
     dy = gen(*y.shape, seed=3)
     y.backward(dy)
     s = S()
-    xg, wg = nhwc(x), w.to(DEV)
+    ug, wg = nhwc(u), w.to(DEV)
+    scp = shp = None
+    if lazy:
+        scg, shg = sc.to(DEV), sh.to(DEV)
+        scp, shp = scg.data_ptr(), shg.data_ptr()
+    act = 2 if lazy else 0
     wk = torch.empty(9 * C, device=DEV)
     call("seg_pack_dw_weight", wg.data_ptr(), wk.data_ptr(), C, s)
     out = torch.empty(N * Ho * Wo, r4(C), device=DEV)
-    call("seg_dw_fwd", xg.data_ptr(), xg.shape[1], N, H, W, C, wk.data_ptr(), out.data_ptr(), out.shape[1], Ho, Wo,
-         stride, s)
+    call("seg_dw_fwd", ug.data_ptr(), ug.shape[1], N, H, W, C, scp, shp, act, wk.data_ptr(), out.data_ptr(),
+         out.shape[1], Ho, Wo, stride, s)
     assert rel(from_nhwc(out, N, C, Ho, Wo), y.detach()) < 1e-5
     dyg = nhwc(dy)
     dx = nhwc(torch.ones(N, C, H, W))
     call("seg_dw_dgrad", dyg.data_ptr(), dyg.shape[1], N, Ho, Wo, C, wk.data_ptr(), dx.data_ptr(), dx.shape[1], H, W,
          stride, 1, s)  # accumulate onto ones
     assert rel(from_nhwc(dx, N, C, H, W), xr.grad + 1.0) < 1e-5
-    nblk = query("seg_dw_wgrad_blocks", N * Ho * Wo)
+    dx0 = torch.empty(N * H * W, r4(C), device=DEV)
+    call("seg_dw_dgrad", dyg.data_ptr(), dyg.shape[1], N, Ho, Wo, C, wk.data_ptr(), dx0.data_ptr(), dx0.shape[1], H,
+         W, stride, 0, s)  # overwrite
+    assert rel(from_nhwc(dx0, N, C, H, W), xr.grad) < 1e-5
+    nblk = query("seg_dw_wgrad_blocks", N, Ho, Wo, C)
     part = torch.empty(nblk * 9 * C, device=DEV)
-    call("seg_dw_wgrad", dyg.data_ptr(), dyg.shape[1], xg.data_ptr(), xg.shape[1], N, H, W, C, Ho, Wo, stride,
-         part.data_ptr(), s)
+    call("seg_dw_wgrad", dyg.data_ptr(), dyg.shape[1], ug.data_ptr(), ug.shape[1], N, H, W, C, scp, shp, act, Ho, Wo,
+         stride, part.data_ptr(), s)
     dw = torch.empty(C, 1, 3, 3, device=DEV)
     call("seg_conv_wgrad_reduce", part.data_ptr(), nblk, dw.data_ptr(), C, 1, 3, 1, 0, s)
     assert rel(dw, wr.grad) < 1e-5

@@ -1,0 +1,34 @@
+"""Build a variant of libsegamd.so with extra compile flags, for A/B timing.
+
+    python tools/variant.py NAME [-DFOO=1 ...]   ->  tmp_var/NAME.so
+"""
+import os
+import subprocess
+import sys
+from concurrent.futures import ThreadPoolExecutor
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "team02-objectdetection_amd"))
+from seg_amd.build import ARCH, FLAGS, HIPCC, sources  # noqa: E402
+
+
+def main():
+    name, extra = sys.argv[1], sys.argv[2:]
+    odir = os.path.join(REPO, "tmp_var", name)
+    os.makedirs(odir, exist_ok=True)
+
+    def one(src):
+        obj = os.path.join(odir, os.path.basename(src)[:-4] + ".o")
+        r = subprocess.run([HIPCC, *FLAGS, *extra, "-c", src, "-o", obj], capture_output=True, text=True)
+        if r.returncode:
+            raise RuntimeError(r.stderr)
+        return obj
+    with ThreadPoolExecutor(8) as ex:
+        objs = list(ex.map(one, sources()))
+    out = os.path.join(REPO, "tmp_var", name + ".so")
+    subprocess.run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", out, *objs], check=True)
+    print(out)
+
+
+if __name__ == "__main__":
+    main()

@@ -34,13 +34,27 @@ struct IgemmArgs {
   int K, M;
 };
 
+#ifndef SEG_IGEMM_DEPTH
+#define SEG_IGEMM_DEPTH 1  // register prefetch depth of the K loop (chunks in flight)
+#endif
+#ifndef SEG_IGEMM_STAGES
+#define SEG_IGEMM_STAGES 1  // LDS stages of the K loop
+#endif
+#ifndef SEG_IGEMM_UT
+#define SEG_IGEMM_UT 1  // uniform-tap loader when Cin % BK == 0
+#endif
 #ifndef SEG_IGEMM_BK
-#define SEG_IGEMM_BK 16  // measured: BK 16 beats 32 (LDS occupancy) on every cfg2 shape but up1.0
+#define SEG_IGEMM_BK 32  // measured (MI355X): single LDS stage + BK 32 beats 2 stages x BK 16 by 4-13% on the cfg2 shapes
 #endif
 
 // BM x BN output tile per 256-thread block, 4 waves laid out (BM/WM) x (BN/WN),
 // each wave owning WM x WN = (WM/32) x (WN/32) accumulators of 32x32.
-template <int BM, int BN, int WM, int WN, int KS, int BK>
+// UT ("uniform tap"): Cin % BK == 0, so every BK-deep K chunk lies inside one
+// filter tap; the tap and channel offset of a chunk are then wave-uniform scalars
+// and each operand slot is a fixed base offset plus that scalar -- the loader
+// costs a few VALU ops per slot instead of the general path's per-slot tap
+// tracking and bounds arithmetic.
+template <int BM, int BN, int WM, int WN, int KS, int BK, bool UT>
 __global__ __launch_bounds__(256) void igemm_conv_kernel(IgemmArgs a) {
   constexpr int LDSR = BK + 4;        // LDS row stride (floats): conflict-free b128 reads
   constexpr int KQ = BK / 4;          // float4 groups per tile row
@@ -51,8 +65,8 @@ __global__ __launch_bounds__(256) void igemm_conv_kernel(IgemmArgs a) {
   constexpr int WAVES_N = BN / WN;
   static_assert((BM / WM) * (BN / WN) == 4, "4 waves per block");
 
-  __shared__ __attribute__((aligned(16))) float As[2][BM * LDSR];
-  __shared__ __attribute__((aligned(16))) float Bs[2][BN * LDSR];
+  __shared__ __attribute__((aligned(16))) float As[SEG_IGEMM_STAGES][BM * LDSR];
+  __shared__ __attribute__((aligned(16))) float Bs[SEG_IGEMM_STAGES][BN * LDSR];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm0 = (wave / WAVES_N) * WM, wn0 = (wave % WAVES_N) * WN;
@@ -91,8 +105,71 @@ __global__ __launch_bounds__(256) void igemm_conv_kernel(IgemmArgs a) {
     }
   }
 
-  f32x4 ra[A_PER], rb[B_PER];
-  auto load_tiles = [&](int k0) {
+  // uniform-tap state: per-slot base offsets + tap-validity masks, scalar tap/channel
+  long u_aoff[A_PER], u_boff[B_PER];
+  unsigned u_mask[A_PER];
+  bool u_bok[B_PER];
+  int u_tap = 0, u_ci = 0;
+  long u_toff = 0;
+  if (UT) {
+#pragma unroll
+    for (int i = 0; i < A_PER; ++i) {
+      const int idx = tid + i * 256;
+      const int row = idx / KQ, kq = idx % KQ;
+      const int p = m0 + row;
+      const bool ok = (idx < A_VEC) && (p < a.M);
+      const int pp = ok ? p : 0;
+      if (KS == 1) {
+        u_aoff[i] = (long)pp * a.ldin + kq * 4;
+        u_mask[i] = ok ? 1u : 0u;
+      } else {
+        const int hw = a.Ho * a.Wo;
+        const int n = pp / hw, rem = pp - n * hw;
+        const int ho = rem / a.Wo, wo = rem - ho * a.Wo;
+        const int hi0 = ho * a.stride - a.pad, wi0 = wo * a.stride - a.pad;
+        u_aoff[i] = (((long)n * a.H + hi0) * a.W + wi0) * a.ldin + kq * 4;
+        unsigned m = 0;
+#pragma unroll
+        for (int t = 0; t < KS * KS; ++t) {
+          const int hi = hi0 + t / KS, wi = wi0 + t % KS;
+          if (ok && (unsigned)hi < (unsigned)a.H && (unsigned)wi < (unsigned)a.W) m |= 1u << t;
+        }
+        u_mask[i] = m;
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < B_PER; ++i) {
+      const int idx = tid + i * 256;
+      const int row = idx / KQ, kq = idx % KQ;
+      const int co = n0 + row;
+      u_bok[i] = idx < B_VEC && co < a.Cout;
+      u_boff[i] = (long)(u_bok[i] ? co : 0) * a.ldk + kq * 4;
+    }
+  }
+
+  auto load_tiles = [&](int k0, f32x4 (&ra)[A_PER], f32x4 (&rb)[B_PER]) {
+    if (UT) {
+      // unconditional loads from a clamped address + select: no branch splits the
+      // loader, so its loads issue back to back
+#pragma unroll
+      for (int i = 0; i < A_PER; ++i) {
+        const bool ok = (u_mask[i] >> u_tap) & 1u;
+        const f32x4 v = ld4(a.in + (ok ? u_aoff[i] + u_toff + u_ci : 0));
+        ra[i] = ok ? v : f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+#pragma unroll
+      for (int i = 0; i < B_PER; ++i) {
+        const f32x4 v = ld4(a.wk + u_boff[i] + k0);
+        rb[i] = u_bok[i] ? v : f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+      u_ci += BK;
+      if (u_ci == a.Cin) {
+        u_ci = 0;
+        ++u_tap;
+        u_toff = ((long)(u_tap / KS) * a.W + u_tap % KS) * a.ldin;
+      }
+      return;
+    }
 #pragma unroll
     for (int i = 0; i < A_PER; ++i) {
       f32x4 v = {0.f, 0.f, 0.f, 0.f};
@@ -127,7 +204,7 @@ __global__ __launch_bounds__(256) void igemm_conv_kernel(IgemmArgs a) {
       rb[i] = v;
     }
   };
-  auto store_tiles = [&](int buf) {
+  auto store_tiles = [&](int buf, const f32x4 (&ra)[A_PER], const f32x4 (&rb)[B_PER]) {
 #pragma unroll
     for (int i = 0; i < A_PER; ++i) {
       const int idx = tid + i * 256;
@@ -149,14 +226,8 @@ __global__ __launch_bounds__(256) void igemm_conv_kernel(IgemmArgs a) {
       for (int r = 0; r < 16; ++r) acc[mi][ni][r] = 0.f;
 
   const int nk = (a.K + BK - 1) / BK;
-  load_tiles(0);
-  store_tiles(0);
-  __syncthreads();
-
   const int lrow = lane & 31, lk = (lane >> 5) * 4;
-  for (int kt = 0; kt < nk; ++kt) {
-    const int cur = kt & 1;
-    if (kt + 1 < nk) load_tiles((kt + 1) * BK);
+  auto compute = [&](int cur) {
 #pragma unroll
     for (int ks = 0; ks < BK / 8; ++ks) {
       f32x4 af[MI], bf[NI];
@@ -172,9 +243,55 @@ __global__ __launch_bounds__(256) void igemm_conv_kernel(IgemmArgs a) {
           for (int ni = 0; ni < NI; ++ni)
             acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[mi][kk], bf[ni][kk], acc[mi][ni], 0, 0, 0);
     }
-    if (kt + 1 < nk) store_tiles(cur ^ 1);
+  };
+
+#if SEG_IGEMM_STAGES == 1
+  // one LDS stage: regs -> LDS, barrier, prefetch the next chunk, compute, barrier
+  f32x4 ra[A_PER], rb[B_PER];
+  load_tiles(0, ra, rb);
+  for (int kt = 0; kt < nk; ++kt) {
+    store_tiles(0, ra, rb);
+    __syncthreads();
+    if (kt + 1 < nk) load_tiles((kt + 1) * BK, ra, rb);
+    compute(0);
     __syncthreads();
   }
+#elif SEG_IGEMM_DEPTH == 1
+  f32x4 ra[A_PER], rb[B_PER];
+  load_tiles(0, ra, rb);
+  store_tiles(0, ra, rb);
+  __syncthreads();
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < nk) load_tiles((kt + 1) * BK, ra, rb);
+    compute(cur);
+    if (kt + 1 < nk) store_tiles(cur ^ 1, ra, rb);
+    __syncthreads();
+  }
+#else
+  // Two register sets: the global loads of chunk kt+2 are issued before chunk kt's
+  // MFMAs and written to LDS only after chunk kt+1's, so each load has two compute
+  // phases (~2 x 2048 MFMA cycles at 64x64 per wave) to land -- one phase is shorter
+  // than the HBM latency under load, which left one-block-per-CU grids stalled.
+  f32x4 ra0[A_PER], rb0[B_PER], ra1[A_PER], rb1[B_PER];
+  load_tiles(0, ra0, rb0);
+  store_tiles(0, ra0, rb0);
+  if (nk > 1) load_tiles(BK, ra1, rb1);
+  __syncthreads();
+  for (int kt = 0; kt < nk; kt += 2) {
+    // LDS stage 0 holds chunk kt; set 1 holds chunk kt+1 (in flight)
+    if (kt + 2 < nk) load_tiles((kt + 2) * BK, ra0, rb0);
+    compute(0);
+    if (kt + 1 < nk) store_tiles(1, ra1, rb1);
+    __syncthreads();
+    if (kt + 1 >= nk) break;
+    // LDS stage 1 holds chunk kt+1; set 0 holds chunk kt+2
+    if (kt + 3 < nk) load_tiles((kt + 3) * BK, ra1, rb1);
+    compute(1);
+    if (kt + 2 < nk) store_tiles(0, ra0, rb0);
+    __syncthreads();
+  }
+#endif
 
   // Epilogue: C layout of 32x32 f32 MFMA: col = lane&31, row = (r&3) + 8(r>>2) + 4(lane>>5).
   float bcol[NI];
@@ -246,15 +363,28 @@ __global__ __launch_bounds__(256) void igemm_conv_kernel(IgemmArgs a) {
   }
 }
 
+template <int BM, int BN, int WM, int WN, int BK>
+int launch_igemm_bk(const IgemmArgs& a, int ks, hipStream_t s) {
+  const int grid = seg_cdiv(a.M, BM) * seg_cdiv(a.Cout, BN);
+  const bool ut = a.Cin % BK == 0 && SEG_IGEMM_UT;
+#define SEG_IG(KS, U) hipLaunchKernelGGL((igemm_conv_kernel<BM, BN, WM, WN, KS, BK, U>), dim3(grid), dim3(256), 0, s, a)
+  if (ks == 1) {
+    if (ut) SEG_IG(1, true); else SEG_IG(1, false);
+  } else {
+    if (ut) SEG_IG(3, true); else SEG_IG(3, false);
+  }
+#undef SEG_IG
+  SEG_RET_LAST();
+}
+
+// K chunk depth: SEG_IGEMM_BK (32) unless K is short and not a multiple of it
+// (the stem's K = 36, 1x1 convs with Cin 16/24/144...), where padding K up to a
+// 32 multiple would waste MFMA work: then 16.
 template <int BM, int BN, int WM, int WN>
 int launch_igemm(const IgemmArgs& a, int ks, hipStream_t s) {
-  constexpr int BK = SEG_IGEMM_BK;
-  const int grid = seg_cdiv(a.M, BM) * seg_cdiv(a.Cout, BN);
-  if (ks == 1)
-    hipLaunchKernelGGL((igemm_conv_kernel<BM, BN, WM, WN, 1, BK>), dim3(grid), dim3(256), 0, s, a);
-  else
-    hipLaunchKernelGGL((igemm_conv_kernel<BM, BN, WM, WN, 3, BK>), dim3(grid), dim3(256), 0, s, a);
-  SEG_RET_LAST();
+  if (SEG_IGEMM_BK != 16 && (a.K <= 64 || (a.K % SEG_IGEMM_BK != 0 && a.K < 512)))
+    return launch_igemm_bk<BM, BN, WM, WN, 16>(a, ks, s);
+  return launch_igemm_bk<BM, BN, WM, WN, SEG_IGEMM_BK>(a, ks, s);
 }
 
 struct TileCfg {

@@ -16,7 +16,13 @@
 
 namespace {
 
-constexpr int BK = 16;
+#ifndef SEG_WGRAD_BK
+#define SEG_WGRAD_BK 16
+#endif
+#ifndef SEG_WGRAD_STAGES
+#define SEG_WGRAD_STAGES 1  // measured: one LDS stage beats two by 2-12% (BK 16)
+#endif
+constexpr int BK = SEG_WGRAD_BK;
 
 struct WgradArgs {
   const float* dy; long lddy;
@@ -34,8 +40,8 @@ __global__ __launch_bounds__(256) void wgrad_kernel(WgradArgs a) {
   constexpr int MI = WM / 32, NI = WN / 32, WAVES_N = BN / WN;
   static_assert((BM / WM) * (BN / WN) == 4, "4 waves per block");
 
-  __shared__ __attribute__((aligned(16))) float As[2][BK * AR];
-  __shared__ __attribute__((aligned(16))) float Bs[2][BK * BR];
+  __shared__ __attribute__((aligned(16))) float As[SEG_WGRAD_STAGES][BK * AR];
+  __shared__ __attribute__((aligned(16))) float Bs[SEG_WGRAD_STAGES][BK * BR];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm0 = (wave / WAVES_N) * WM, wn0 = (wave % WAVES_N) * WN;
@@ -129,13 +135,7 @@ __global__ __launch_bounds__(256) void wgrad_kernel(WgradArgs a) {
 
   const int lrow = lane & 31, lh = lane >> 5;
   const int nk = (kend - kbeg + BK - 1) / BK;
-  if (nk > 0) {
-    load_tiles(kbeg);
-    store_tiles(0);
-    __syncthreads();
-    for (int kt = 0; kt < nk; ++kt) {
-      const int cur = kt & 1;
-      if (kt + 1 < nk) load_tiles(kbeg + (kt + 1) * BK);
+  auto compute = [&](int cur) {
 #pragma unroll
       for (int kk = 0; kk < BK / 2; ++kk) {
         float af[MI], bf[NI];
@@ -149,9 +149,29 @@ __global__ __launch_bounds__(256) void wgrad_kernel(WgradArgs a) {
           for (int ni = 0; ni < NI; ++ni)
             acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[mi], bf[ni], acc[mi][ni], 0, 0, 0);
       }
+  };
+  if (nk > 0) {
+#if SEG_WGRAD_STAGES == 1
+    load_tiles(kbeg);
+    for (int kt = 0; kt < nk; ++kt) {
+      store_tiles(0);
+      __syncthreads();
+      if (kt + 1 < nk) load_tiles(kbeg + (kt + 1) * BK);
+      compute(0);
+      __syncthreads();
+    }
+#else
+    load_tiles(kbeg);
+    store_tiles(0);
+    __syncthreads();
+    for (int kt = 0; kt < nk; ++kt) {
+      const int cur = kt & 1;
+      if (kt + 1 < nk) load_tiles(kbeg + (kt + 1) * BK);
+      compute(cur);
       if (kt + 1 < nk) store_tiles(cur ^ 1);
       __syncthreads();
     }
+#endif
   }
 
   float* slab = a.part + (long)split * a.Cout * a.Nw;

@@ -102,7 +102,9 @@ def main():
     paths = sys.argv[1:] or [os.path.join(REPO, "team02-objectdetection_amd/seg_amd/_lib/libsegamd.so")]
     import seg_amd._lib  # noqa: F401  (torch first)
     libs = [(p, load(p)) for p in paths]
-    results = [(p, bench(lib)) for p, lib in libs]
+    only = os.environ.get("CONVBENCH_ONLY")
+    only = set(only.split(",")) if only else None
+    results = [(p, bench(lib, only)) for p, lib in libs]
     for p, res in results:
         print("==", p)
         tot = 0.0

@@ -33,24 +33,46 @@ __device__ __forceinline__ LinAC lin_ac(int dst, int in, float scale) {
 
 constexpr int CMAX = 32;
 
-// Recompute the C full-res logits of pixel (n, r, s).
-__device__ __forceinline__ void full_res_logits(const float* __restrict__ low, long ld, int H, int W, int C, int n,
-                                                int r, int s, float sh, float sw, float* z) {
+// Recompute the CP (= round4(C)) full-res logits of pixel (n, r, s); the class
+// loops are unrolled over CP so z stays in registers with constant indices.
+template <int CP>
+__device__ __forceinline__ void full_res_logits(const float* __restrict__ low, long ld, int H, int W, int n, int r,
+                                                int s, float sh, float sw, float (&z)[CP]) {
   const LinAC lh = lin_ac(r, H, sh), lw = lin_ac(s, W, sw);
   const float* base = low + (long)n * H * W * ld;
   const float* p00 = base + ((long)lh.i0 * W + lw.i0) * ld;
   const float* p01 = base + ((long)lh.i0 * W + lw.i1) * ld;
   const float* p10 = base + ((long)lh.i1 * W + lw.i0) * ld;
   const float* p11 = base + ((long)lh.i1 * W + lw.i1) * ld;
-  for (int c = 0; c < C; c += 4) {
+#pragma unroll
+  for (int c = 0; c < CP; c += 4) {
     const f32x4 o = lh.l0 * (lw.l0 * ld4(p00 + c) + lw.l1 * ld4(p01 + c)) +
                     lh.l1 * (lw.l0 * ld4(p10 + c) + lw.l1 * ld4(p11 + c));
 #pragma unroll
-    for (int j = 0; j < 4; ++j)
-      if (c + j < CMAX) z[c + j] = o[j];
+    for (int j = 0; j < 4; ++j) z[c + j] = o[j];
   }
 }
 
+// max, sum of exp(z - max) and z[y] over the C valid classes
+template <int CP>
+__device__ __forceinline__ void softmax_stats(float (&z)[CP], int C, int y, float& m, float& se, float& zy,
+                                              bool keep_exp) {
+  m = z[0];
+#pragma unroll
+  for (int c = 1; c < CP; ++c)
+    if (c < C) m = fmaxf(m, z[c]);
+  se = 0.f;
+  zy = 0.f;
+#pragma unroll
+  for (int c = 0; c < CP; ++c) {
+    const float e = c < C ? expf(z[c] - m) : 0.f;
+    zy = c == y ? z[c] : zy;
+    se += e;
+    if (keep_exp) z[c] = e;
+  }
+}
+
+template <int CP>
 __global__ __launch_bounds__(256) void ce_up_loss_kernel(const float* __restrict__ low, long ld, int N, int H, int W,
                                                          int C, const long long* __restrict__ labels, int Ho, int Wo,
                                                          float sh, float sw, int ignore_index,
@@ -64,15 +86,10 @@ __global__ __launch_bounds__(256) void ce_up_loss_kernel(const float* __restrict
     const int n = (int)(p / ((long)Ho * Wo));
     const int rem = (int)(p - (long)n * Ho * Wo);
     const int r = rem / Wo, s = rem - r * Wo;
-    float z[CMAX];
-    full_res_logits(low, ld, H, W, C, n, r, s, sh, sw, z);
-    float m = z[0];
-    for (int c = 1; c < C; ++c) m = fmaxf(m, z[c]);
-    float se = 0.f, zy = 0.f;
-    for (int c = 0; c < C; ++c) {
-      se += expf(z[c] - m);
-      if (c == (int)y) zy = z[c];
-    }
+    float z[CP];
+    full_res_logits<CP>(low, ld, H, W, n, r, s, sh, sw, z);
+    float m, se, zy;
+    softmax_stats<CP>(z, C, (int)y, m, se, zy, false);
     lsum += m + logf(se) - zy;
     cnt += 1.f;
   }
@@ -105,6 +122,7 @@ __global__ void ce_finalize_kernel(const float* __restrict__ part, int nblk, flo
 }
 
 // dhigh[p][c] = g * (softmax(z_p)[c] - [c == y_p]) / count, NHWC (ld >= round4(C)).
+template <int CP>
 __global__ __launch_bounds__(256) void ce_up_grad_kernel(const float* __restrict__ low, long ld, int N, int H, int W,
                                                          int C, const long long* __restrict__ labels, int Ho, int Wo,
                                                          float sh, float sw, int ignore_index,
@@ -116,23 +134,20 @@ __global__ __launch_bounds__(256) void ce_up_grad_kernel(const float* __restrict
     const long long y = labels[p];
     float* d = dhigh + p * ldh;
     if (y == ignore_index) {
-      for (int c = 0; c < C; c += 4) st4(d + c, f32x4{0.f, 0.f, 0.f, 0.f});
+#pragma unroll
+      for (int c = 0; c < CP; c += 4) st4(d + c, f32x4{0.f, 0.f, 0.f, 0.f});
       continue;
     }
     const int n = (int)(p / ((long)Ho * Wo));
     const int rem = (int)(p - (long)n * Ho * Wo);
     const int r = rem / Wo, s = rem - r * Wo;
-    float z[CMAX];
-    full_res_logits(low, ld, H, W, C, n, r, s, sh, sw, z);
-    float m = z[0];
-    for (int c = 1; c < C; ++c) m = fmaxf(m, z[c]);
-    float se = 0.f;
-    for (int c = 0; c < C; ++c) {
-      z[c] = expf(z[c] - m);
-      se += z[c];
-    }
+    float z[CP];
+    full_res_logits<CP>(low, ld, H, W, n, r, s, sh, sw, z);
+    float m, se, zy;
+    softmax_stats<CP>(z, C, (int)y, m, se, zy, true);
     const float inv = 1.f / se;
-    for (int c = 0; c < C; c += 4) {
+#pragma unroll
+    for (int c = 0; c < CP; c += 4) {
       f32x4 o;
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
@@ -159,8 +174,15 @@ SEG_API int seg_ce_upsample_loss(const float* low, long ld, int N, int H, int W,
   const int nb = loss_blocks(total);
   const float sh = Ho > 1 ? (float)(H - 1) / (float)(Ho - 1) : 0.f;
   const float sw = Wo > 1 ? (float)(W - 1) / (float)(Wo - 1) : 0.f;
-  hipLaunchKernelGGL(ce_up_loss_kernel, dim3(nb), dim3(256), 0, stream, low, ld, N, H, W, C, labels, Ho, Wo, sh, sw,
-                     ignore_index, work);
+#define SEG_CE_L(CP)                                                                                          \
+  case CP:                                                                                                    \
+    hipLaunchKernelGGL(ce_up_loss_kernel<CP>, dim3(nb), dim3(256), 0, stream, low, ld, N, H, W, C, labels, Ho, Wo, \
+                       sh, sw, ignore_index, work);                                                          \
+    break
+  switch ((C + 3) & ~3) {
+    SEG_CE_L(4); SEG_CE_L(8); SEG_CE_L(12); SEG_CE_L(16); SEG_CE_L(20); SEG_CE_L(24); SEG_CE_L(28); SEG_CE_L(32);
+  }
+#undef SEG_CE_L
   hipLaunchKernelGGL(ce_finalize_kernel, dim3(1), dim3(64), 0, stream, work, nb, out2);
   SEG_RET_LAST();
 }
@@ -174,7 +196,15 @@ SEG_API int seg_ce_upsample_grad(const float* low, long ld, int N, int H, int W,
   const long total = (long)N * Ho * Wo;
   const float sh = Ho > 1 ? (float)(H - 1) / (float)(Ho - 1) : 0.f;
   const float sw = Wo > 1 ? (float)(W - 1) / (float)(Wo - 1) : 0.f;
-  hipLaunchKernelGGL(ce_up_grad_kernel, dim3((int)std::min<long>(seg_cdiv(total, 256), 8192)), dim3(256), 0, stream,
-                     low, ld, N, H, W, C, labels, Ho, Wo, sh, sw, ignore_index, grad_out, stats, dhigh, ldh);
+  const int grid = (int)std::min<long>(seg_cdiv(total, 256), 8192);
+#define SEG_CE_G(CP)                                                                                            \
+  case CP:                                                                                                      \
+    hipLaunchKernelGGL(ce_up_grad_kernel<CP>, dim3(grid), dim3(256), 0, stream, low, ld, N, H, W, C, labels, Ho, Wo, \
+                       sh, sw, ignore_index, grad_out, stats, dhigh, ldh);                                     \
+    break
+  switch ((C + 3) & ~3) {
+    SEG_CE_G(4); SEG_CE_G(8); SEG_CE_G(12); SEG_CE_G(16); SEG_CE_G(20); SEG_CE_G(24); SEG_CE_G(28); SEG_CE_G(32);
+  }
+#undef SEG_CE_G
   SEG_RET_LAST();
 }

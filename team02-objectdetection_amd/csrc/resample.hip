@@ -76,6 +76,11 @@ __global__ void up_fwd_nhwc_kernel(const float* __restrict__ in, long ldin, int 
 
 // d_in[n][h][w][c] = sum_{r,s} w_h(r,h) w_w(s,w) d_out[n][r][s][c]
 // LAYOUT 0: d_out NHWC [N*Ho*Wo][ldout];  LAYOUT 1: d_out NCHW [N][C][Ho][Wo].
+// The column weights of the (at most SMAX) candidate output columns are computed
+// once per thread into registers (for x2 resampling 4 of them are non-zero), so
+// the inner loop is loads and FMAs only.
+constexpr int SMAX = 12;
+
 template <int LAYOUT>
 __global__ void up_bwd_kernel(const float* __restrict__ dout, long ldout, int N, int Ho, int Wo, int C,
                               float* __restrict__ din, long ldin, int H, int W, float sh, float sw, int ac,
@@ -92,19 +97,33 @@ __global__ void up_bwd_kernel(const float* __restrict__ dout, long ldout, int N,
     dst_range(h, H, Ho, sh, ac, &rlo, &rhi);
     dst_range(w, W, Wo, sw, ac, &slo, &shi);
     f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-    for (int r = rlo; r <= rhi; ++r) {
-      const float wr = lin_weight(r, h, H, sh, ac);
-      if (wr == 0.f) continue;
-      for (int s = slo; s <= shi; ++s) {
-        const float ws = lin_weight(s, w, W, sw, ac);
-        if (ws == 0.f) continue;
-        const float wt = wr * ws;
-        if (LAYOUT == 0) {
-          acc += wt * ld4(dout + (((long)n * Ho + r) * Wo + s) * ldout + c);
-        } else {
+    auto add = [&](int r, int s, float wt) {
+      if (LAYOUT == 0) {
+        acc += wt * ld4(dout + (((long)n * Ho + r) * Wo + s) * ldout + c);
+      } else {
 #pragma unroll
-          for (int j = 0; j < 4; ++j)
-            if (c + j < C) acc[j] += wt * dout[(((long)n * C + c + j) * Ho + r) * Wo + s];
+        for (int j = 0; j < 4; ++j)
+          if (c + j < C) acc[j] += wt * dout[(((long)n * C + c + j) * Ho + r) * Wo + s];
+      }
+    };
+    if (shi - slo + 1 <= SMAX) {
+      float wsv[SMAX];
+#pragma unroll
+      for (int k = 0; k < SMAX; ++k) wsv[k] = slo + k <= shi ? lin_weight(slo + k, w, W, sw, ac) : 0.f;
+      for (int r = rlo; r <= rhi; ++r) {
+        const float wr = lin_weight(r, h, H, sh, ac);
+        if (wr == 0.f) continue;
+#pragma unroll
+        for (int k = 0; k < SMAX; ++k)
+          if (wsv[k] != 0.f) add(r, slo + k, wr * wsv[k]);
+      }
+    } else {
+      for (int r = rlo; r <= rhi; ++r) {
+        const float wr = lin_weight(r, h, H, sh, ac);
+        if (wr == 0.f) continue;
+        for (int s = slo; s <= shi; ++s) {
+          const float ws = lin_weight(s, w, W, sw, ac);
+          if (ws != 0.f) add(r, s, wr * ws);
         }
       }
     }

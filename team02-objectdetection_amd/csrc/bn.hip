@@ -46,7 +46,7 @@ __global__ __launch_bounds__(256) void chan_partial_kernel(
       f32x4 k = {0.f, 0.f, 0.f, 0.f}, sc = k, sh = k;
       if (KIND == 0) k = ld4(y + c);
       if (KIND == 1) { k = ld4(mean + c); sc = ld4(scale + c); sh = ld4(shift + c); }
-      for (int r = r0 + rg; r < r1; r += RG) {
+      auto step = [&](int r) {
         const f32x4 v = ld4(y + (long)r * ldy + c);
         if (KIND == 0) {
           const f32x4 d = v - k;
@@ -62,7 +62,17 @@ __global__ __launch_bounds__(256) void chan_partial_kernel(
         } else {
           s0 += v;
         }
+      };
+      // 4 rows per iteration: their loads issue together (the loop is otherwise
+      // latency-bound, one dependent load pair per trip)
+      int r = r0 + rg;
+      for (; r + 3 * RG < r1; r += 4 * RG) {
+        step(r);
+        step(r + RG);
+        step(r + 2 * RG);
+        step(r + 3 * RG);
       }
+      for (; r < r1; r += RG) step(r);
     }
     red0[t] = s0;
     red1[t] = s1;
@@ -80,44 +90,47 @@ __global__ __launch_bounds__(256) void chan_partial_kernel(
 }
 
 int rows_per_block_for(long M) {
-  // ~1024 blocks, at least 32 rows each.
-  long r = (M + 1023) / 1024;
+  // ~2048 blocks (8 per CU: latency hiding for the 2-load streams), >= 32 rows each
+  long r = (M + 2047) / 2048;
   if (r < 32) r = 32;
   return (int)r;
 }
 
-// Sum the per-block partials of channel c (one 64-lane wave per channel, fp64,
-// fixed lane->block assignment and a fixed shuffle tree: deterministic).
+// Sum the per-block partials of channel c = blockIdx.x with the whole 256-thread
+// block (fp64, fixed thread->partial assignment and a fixed LDS tree:
+// deterministic).  The result is valid in thread 0.
 __device__ __forceinline__ void sum_partials(const float* __restrict__ part, int nblk, int C, int ldp, int c,
-                                             int lane, double* s0, double* s1) {
+                                             int t, double* s0, double* s1) {
+  __shared__ double ra[256], rb[256];
   double a = 0.0, b = 0.0;
-  for (int k = lane; k < nblk; k += 64) {
+  for (int k = t; k < nblk; k += 256) {
     a += part[(long)k * 2 * ldp + c];
     b += part[(long)k * 2 * ldp + ldp + c];
   }
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    a += __shfl_xor(a, o, 64);
-    b += __shfl_xor(b, o, 64);
+  ra[t] = a;
+  rb[t] = b;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (t < o) {
+      ra[t] += ra[t + o];
+      rb[t] += rb[t + o];
+    }
+    __syncthreads();
   }
-  *s0 = a;
-  *s1 = b;
+  *s0 = ra[0];
+  *s1 = rb[0];
 }
-
-constexpr int FIN_CH = 4;  // channels (waves) per 256-thread finalize block
 
 __global__ __launch_bounds__(256) void bn_finalize_kernel(
     const float* __restrict__ part, int nblk, const float* __restrict__ y, long M, int C,
     const float* __restrict__ gamma, const float* __restrict__ beta, float eps, float momentum,
     float* running_mean, float* running_var, long long* nbt, float* mean_out, float* invstd_out, float* scale_out,
     float* shift_out) {
-  const int lane = threadIdx.x & 63;
-  const int c = blockIdx.x * FIN_CH + (threadIdx.x >> 6);
+  const int c = blockIdx.x;
   if (blockIdx.x == 0 && threadIdx.x == 0 && nbt) *nbt += 1;
-  if (c >= C) return;
   double s, s2;
-  sum_partials(part, nblk, C, C, c, lane, &s, &s2);
-  if (lane != 0) return;
+  sum_partials(part, nblk, C, C, c, threadIdx.x, &s, &s2);
+  if (threadIdx.x != 0) return;
   const double k = y[c];
   const double dm = s / (double)M;
   const double mean = k + dm;
@@ -149,26 +162,36 @@ __device__ __forceinline__ void chan_merge(double& n, double& mean, double& m2, 
   n = nn;
 }
 
+// One 256-thread block per channel: each lane merges every 256th tile, then a
+// fixed-order LDS tree of Chan merges (deterministic).
 __global__ __launch_bounds__(256) void bn_finalize_tiles_kernel(
     const float* __restrict__ part, int ntiles, int tile_rows, long M, int C, const float* __restrict__ gamma,
     const float* __restrict__ beta, float eps, float momentum, float* running_mean, float* running_var,
     long long* nbt, float* mean_out, float* invstd_out, float* scale_out, float* shift_out) {
-  const int lane = threadIdx.x & 63;
-  const int c = blockIdx.x * FIN_CH + (threadIdx.x >> 6);
-  if (blockIdx.x == 0 && threadIdx.x == 0 && nbt) *nbt += 1;
-  if (c >= C) return;
+  __shared__ double sn[256], smean[256], sm2[256];
+  const int t = threadIdx.x;
+  const int c = blockIdx.x;
+  if (blockIdx.x == 0 && t == 0 && nbt) *nbt += 1;
   double n = 0.0, mean = 0.0, m2 = 0.0;
-  for (int t = lane; t < ntiles; t += 64) {
-    const double nt = (double)std::min<long>(tile_rows, M - (long)t * tile_rows);
-    const double s = part[(long)t * 2 * C + c], q = part[(long)t * 2 * C + C + c];
+  for (int i = t; i < ntiles; i += 256) {
+    const double nt = (double)std::min<long>(tile_rows, M - (long)i * tile_rows);
+    const double s = part[(long)i * 2 * C + c], q = part[(long)i * 2 * C + C + c];
     chan_merge(n, mean, m2, nt, s / nt, q);
   }
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const double n2 = __shfl_xor(n, o, 64), mean2 = __shfl_xor(mean, o, 64), m2b = __shfl_xor(m2, o, 64);
-    chan_merge(n, mean, m2, n2, mean2, m2b);
+  sn[t] = n;
+  smean[t] = mean;
+  sm2[t] = m2;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (t < o) {
+      chan_merge(n, mean, m2, sn[t + o], smean[t + o], sm2[t + o]);
+      sn[t] = n;
+      smean[t] = mean;
+      sm2[t] = m2;
+    }
+    __syncthreads();
   }
-  if (lane != 0) return;
+  if (t != 0) return;
   double var = m2 / (double)M;
   if (var < 0.0) var = 0.0;
   const float invstd = (float)(1.0 / sqrt(var + (double)eps));
@@ -212,12 +235,10 @@ __global__ void bn_apply_kernel(const float* __restrict__ y, long ldy, long M, i
 __global__ void bn_bwd_finalize_kernel(const float* __restrict__ part, int nblk, long M, int C,
                                        const float* __restrict__ gamma, const float* __restrict__ invstd,
                                        float* dgamma, float* dbeta, float* coef) {
-  const int lane = threadIdx.x & 63;
-  const int c = blockIdx.x * FIN_CH + (threadIdx.x >> 6);
-  if (c >= C) return;
+  const int c = blockIdx.x;
   double sdz, sdzx;
-  sum_partials(part, nblk, C, C, c, lane, &sdz, &sdzx);
-  if (lane != 0) return;
+  sum_partials(part, nblk, C, C, c, threadIdx.x, &sdz, &sdzx);
+  if (threadIdx.x != 0) return;
   const double inv = invstd[c];
   const double g = gamma ? gamma[c] : 1.0;
   if (dbeta) dbeta[c] = (float)sdz;
@@ -271,12 +292,10 @@ __global__ void bn_eval_bwd_kernel(const float* __restrict__ da, long ldda, cons
 
 __global__ void colsum_finalize_kernel(const float* __restrict__ part, int nblk, int C, int ldp, float* out,
                                        int accumulate) {
-  const int lane = threadIdx.x & 63;
-  const int c = blockIdx.x * FIN_CH + (threadIdx.x >> 6);
-  if (c >= C) return;
+  const int c = blockIdx.x;
   double s, unused;
-  sum_partials(part, nblk, C, ldp, c, lane, &s, &unused);
-  if (lane == 0) out[c] = accumulate ? out[c] + (float)s : (float)s;
+  sum_partials(part, nblk, C, ldp, c, threadIdx.x, &s, &unused);
+  if (threadIdx.x == 0) out[c] = accumulate ? out[c] + (float)s : (float)s;
 }
 
 int ew_grid(long total) { return (int)std::min<long>(seg_cdiv(total, 256), 8192); }
@@ -320,7 +339,7 @@ SEG_API int seg_bn_stats(const float* y, long ldy, long M, int C, const float* g
   const int nblk = seg_cdiv(M, rpb);
   hipLaunchKernelGGL(chan_partial_kernel<0>, dim3(nblk), dim3(256), 0, stream, y, ldy, nullptr, 0L, (int)M, C,
                      nullptr, nullptr, nullptr, 0, work, rpb);
-  hipLaunchKernelGGL(bn_finalize_kernel, dim3(seg_cdiv(C, FIN_CH)), dim3(256), 0, stream, work, nblk, y, M, C, gamma,
+  hipLaunchKernelGGL(bn_finalize_kernel, dim3(C), dim3(256), 0, stream, work, nblk, y, M, C, gamma,
                      beta, eps, momentum, running_mean, running_var, num_batches_tracked, mean, invstd, scale, shift);
   SEG_RET_LAST();
 }
@@ -333,7 +352,7 @@ SEG_API int seg_bn_stats_tiles(const float* part, int ntiles, int tile_rows, lon
                                long long* num_batches_tracked, float* mean, float* invstd, float* scale, float* shift,
                                hipStream_t stream) {
   if (ntiles < 1 || tile_rows < 1 || M < 1) return (int)hipErrorInvalidValue;
-  hipLaunchKernelGGL(bn_finalize_tiles_kernel, dim3(seg_cdiv(C, FIN_CH)), dim3(256), 0, stream, part, ntiles,
+  hipLaunchKernelGGL(bn_finalize_tiles_kernel, dim3(C), dim3(256), 0, stream, part, ntiles,
                      tile_rows, M, C, gamma, beta, eps, momentum, running_mean, running_var, num_batches_tracked, mean,
                      invstd, scale, shift);
   SEG_RET_LAST();
@@ -366,7 +385,7 @@ SEG_API int seg_bn_backward(const float* da, long ldda, const float* y, long ldy
   float* coef = work + (long)nblk * 2 * C;
   hipLaunchKernelGGL(chan_partial_kernel<1>, dim3(nblk), dim3(256), 0, stream, y, ldy, da, ldda, (int)M, C, scale,
                      shift, mean, act, work, rpb);
-  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(seg_cdiv(C, FIN_CH)), dim3(256), 0, stream, work, nblk, M, C, gamma,
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(C), dim3(256), 0, stream, work, nblk, M, C, gamma,
                      invstd, dgamma, dbeta, coef);
   hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(ew_grid(M * (C / 4))), dim3(256), 0, stream, da, ldda, y, ldy, M, C,
                      scale, shift, mean, act, coef, dy, lddy);
@@ -390,7 +409,7 @@ SEG_API int seg_colsum(const float* y, long ldy, long M, int C, float* work, flo
   const int nblk = seg_cdiv(M, rpb);
   hipLaunchKernelGGL(chan_partial_kernel<2>, dim3(nblk), dim3(256), 0, stream, y, ldy, nullptr, 0L, (int)M, C4,
                      nullptr, nullptr, nullptr, 0, work, rpb);
-  hipLaunchKernelGGL(colsum_finalize_kernel, dim3(seg_cdiv(C, FIN_CH)), dim3(256), 0, stream, work, nblk, C, C4, out,
+  hipLaunchKernelGGL(colsum_finalize_kernel, dim3(C), dim3(256), 0, stream, work, nblk, C, C4, out,
                      accumulate);
   SEG_RET_LAST();
 }

@@ -21,6 +21,12 @@
 
 namespace {
 
+// 16 zero bytes in device memory: operand slots that fall outside the image or
+// the matrix load from here instead of being zeroed after the load, so no
+// instruction touches a prefetched register before the K chunk that consumes it
+// (a post-load select forces an early s_waitcnt and exposes the HBM latency).
+__device__ __attribute__((aligned(16))) float g_zero4[4];
+
 struct IgemmArgs {
   const float* in; long ldin;
   const float* wk; int ldk;      // packed weights [Cout][ldk], k contiguous
@@ -43,17 +49,20 @@ struct IgemmArgs {
 #ifndef SEG_IGEMM_UT
 #define SEG_IGEMM_UT 1  // uniform-tap loader when Cin % BK == 0
 #endif
+#ifndef SEG_IGEMM_UT2
+#define SEG_IGEMM_UT2 1  // uniform-tap loader also for Cin % BK != 0 (chunks spanning two taps)
+#endif
 #ifndef SEG_IGEMM_BK
 #define SEG_IGEMM_BK 32  // measured (MI355X): single LDS stage + BK 32 beats 2 stages x BK 16 by 4-13% on the cfg2 shapes
 #endif
 
 // BM x BN output tile per 256-thread block, 4 waves laid out (BM/WM) x (BN/WN),
 // each wave owning WM x WN = (WM/32) x (WN/32) accumulators of 32x32.
-// UT ("uniform tap"): Cin % BK == 0, so every BK-deep K chunk lies inside one
-// filter tap; the tap and channel offset of a chunk are then wave-uniform scalars
-// and each operand slot is a fixed base offset plus that scalar -- the loader
-// costs a few VALU ops per slot instead of the general path's per-slot tap
-// tracking and bounds arithmetic.
+// UT ("uniform tap"): Cin >= BK, so every BK-deep K chunk spans at most two
+// filter taps; the chunk's tap and channel offset are wave-uniform scalars and
+// each operand slot is a fixed base offset plus one of two scalar tap offsets --
+// a few VALU ops per slot instead of the general path's per-slot tap tracking
+// and bounds arithmetic.  The general path remains for Cin < BK (the stem).
 template <int BM, int BN, int WM, int WN, int KS, int BK, bool UT>
 __global__ __launch_bounds__(256) void igemm_conv_kernel(IgemmArgs a) {
   constexpr int LDSR = BK + 4;        // LDS row stride (floats): conflict-free b128 reads
@@ -105,29 +114,34 @@ __global__ __launch_bounds__(256) void igemm_conv_kernel(IgemmArgs a) {
     }
   }
 
-  // uniform-tap state: per-slot base offsets + tap-validity masks, scalar tap/channel
+  // "UT" state (Cin >= BK: a K chunk spans at most two filter taps).  Per slot: the
+  // pixel's base offset and its 9-bit tap-validity mask; the chunk's starting tap
+  // and channel are wave-uniform scalars, and a slot whose k (= chunk start +
+  // 4*kq) crosses Cin takes the next tap.  kq = tid % KQ for every slot (256 % KQ == 0).
   long u_aoff[A_PER], u_boff[B_PER];
   unsigned u_mask[A_PER];
   bool u_bok[B_PER];
+  const int u_kq4 = (tid % KQ) * 4;
   int u_tap = 0, u_ci = 0;
-  long u_toff = 0;
+  long u_toff0 = 0, u_toff1 = 0;
+  auto tap_off = [&](int t) -> long { return ((long)(t / KS) * a.W + t % KS) * a.ldin; };
   if (UT) {
 #pragma unroll
     for (int i = 0; i < A_PER; ++i) {
       const int idx = tid + i * 256;
-      const int row = idx / KQ, kq = idx % KQ;
+      const int row = idx / KQ;
       const int p = m0 + row;
       const bool ok = (idx < A_VEC) && (p < a.M);
       const int pp = ok ? p : 0;
       if (KS == 1) {
-        u_aoff[i] = (long)pp * a.ldin + kq * 4;
+        u_aoff[i] = (long)pp * a.ldin;
         u_mask[i] = ok ? 1u : 0u;
       } else {
         const int hw = a.Ho * a.Wo;
         const int n = pp / hw, rem = pp - n * hw;
         const int ho = rem / a.Wo, wo = rem - ho * a.Wo;
         const int hi0 = ho * a.stride - a.pad, wi0 = wo * a.stride - a.pad;
-        u_aoff[i] = (((long)n * a.H + hi0) * a.W + wi0) * a.ldin + kq * 4;
+        u_aoff[i] = (((long)n * a.H + hi0) * a.W + wi0) * a.ldin;
         unsigned m = 0;
 #pragma unroll
         for (int t = 0; t < KS * KS; ++t) {
@@ -140,33 +154,36 @@ __global__ __launch_bounds__(256) void igemm_conv_kernel(IgemmArgs a) {
 #pragma unroll
     for (int i = 0; i < B_PER; ++i) {
       const int idx = tid + i * 256;
-      const int row = idx / KQ, kq = idx % KQ;
-      const int co = n0 + row;
+      const int co = n0 + idx / KQ;
       u_bok[i] = idx < B_VEC && co < a.Cout;
-      u_boff[i] = (long)(u_bok[i] ? co : 0) * a.ldk + kq * 4;
+      u_boff[i] = (long)(u_bok[i] ? co : 0) * a.ldk + u_kq4;
     }
+    u_toff1 = tap_off(1);
   }
 
   auto load_tiles = [&](int k0, f32x4 (&ra)[A_PER], f32x4 (&rb)[B_PER]) {
     if (UT) {
-      // unconditional loads from a clamped address + select: no branch splits the
-      // loader, so its loads issue back to back
+      // address selects only (out-of-image / out-of-matrix slots read g_zero4): no
+      // branch splits the loader and no instruction touches the loaded registers
+      // before the chunk that consumes them
+      const int ci = u_ci + u_kq4;
+      const bool wrap = ci >= a.Cin;
+      const int tap = u_tap + (wrap ? 1 : 0);
+      const long off = (wrap ? u_toff1 : u_toff0) + (wrap ? ci - a.Cin : ci);
 #pragma unroll
       for (int i = 0; i < A_PER; ++i) {
-        const bool ok = (u_mask[i] >> u_tap) & 1u;
-        const f32x4 v = ld4(a.in + (ok ? u_aoff[i] + u_toff + u_ci : 0));
-        ra[i] = ok ? v : f32x4{0.f, 0.f, 0.f, 0.f};
+        const bool ok = (u_mask[i] >> tap) & 1u;
+        ra[i] = ld4(ok ? a.in + u_aoff[i] + off : g_zero4);
       }
+      const bool kin = k0 + u_kq4 < a.K;
 #pragma unroll
-      for (int i = 0; i < B_PER; ++i) {
-        const f32x4 v = ld4(a.wk + u_boff[i] + k0);
-        rb[i] = u_bok[i] ? v : f32x4{0.f, 0.f, 0.f, 0.f};
-      }
+      for (int i = 0; i < B_PER; ++i) rb[i] = ld4(u_bok[i] && kin ? a.wk + u_boff[i] + k0 : g_zero4);
       u_ci += BK;
-      if (u_ci == a.Cin) {
-        u_ci = 0;
+      if (u_ci >= a.Cin) {
+        u_ci -= a.Cin;
         ++u_tap;
-        u_toff = ((long)(u_tap / KS) * a.W + u_tap % KS) * a.ldin;
+        u_toff0 = u_toff1;
+        u_toff1 = tap_off(u_tap + 1);
       }
       return;
     }
@@ -208,12 +225,12 @@ __global__ __launch_bounds__(256) void igemm_conv_kernel(IgemmArgs a) {
 #pragma unroll
     for (int i = 0; i < A_PER; ++i) {
       const int idx = tid + i * 256;
-      if (idx < A_VEC) st4(&As[buf][(idx / KQ) * LDSR + (idx % KQ) * 4], ra[i]);
+      if (A_VEC % 256 == 0 || idx < A_VEC) st4(&As[buf][(idx / KQ) * LDSR + (idx % KQ) * 4], ra[i]);
     }
 #pragma unroll
     for (int i = 0; i < B_PER; ++i) {
       const int idx = tid + i * 256;
-      if (idx < B_VEC) st4(&Bs[buf][(idx / KQ) * LDSR + (idx % KQ) * 4], rb[i]);
+      if (B_VEC % 256 == 0 || idx < B_VEC) st4(&Bs[buf][(idx / KQ) * LDSR + (idx % KQ) * 4], rb[i]);
     }
   };
 
@@ -366,7 +383,7 @@ __global__ __launch_bounds__(256) void igemm_conv_kernel(IgemmArgs a) {
 template <int BM, int BN, int WM, int WN, int BK>
 int launch_igemm_bk(const IgemmArgs& a, int ks, hipStream_t s) {
   const int grid = seg_cdiv(a.M, BM) * seg_cdiv(a.Cout, BN);
-  const bool ut = a.Cin % BK == 0 && SEG_IGEMM_UT;
+  const bool ut = SEG_IGEMM_UT && (SEG_IGEMM_UT2 ? a.Cin >= BK : a.Cin % BK == 0);
 #define SEG_IG(KS, U) hipLaunchKernelGGL((igemm_conv_kernel<BM, BN, WM, WN, KS, BK, U>), dim3(grid), dim3(256), 0, s, a)
   if (ks == 1) {
     if (ut) SEG_IG(1, true); else SEG_IG(1, false);

@@ -43,6 +43,9 @@ int seg_conv_igemm(const float* in, long ldin, int N, int H, int W, int Cin,
                    int ks, int stride, int pad,
                    const float* add, long ldadd, float* stat, hipStream_t stream);
 /* Row tiles (and their height) seg_conv_igemm uses for an M x Cout output. */
+/* Tuning hook: force tile configuration t (0..7) for the following
+ * seg_conv_igemm calls of this process, -1 = the built-in cost model. */
+int seg_igemm_force_tile(int t);
 int seg_conv_igemm_row_tiles(long M, int Cout, int* tile_rows);
 
 /* Pack w[Cout][Cin][ks][ks]: mode 0 -> wk[Cout][ldk] (forward; tap runs padded

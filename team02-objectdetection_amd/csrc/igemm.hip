@@ -408,15 +408,20 @@ struct TileCfg {
   int bm, bn, wm, wn;
   float eff;  // relative per-CU MFMA efficiency of the wave tile (LDS reads per MFMA)
 };
-// 64x64 wave tiles need 1 operand read per MFMA, 32x96 1.33, 32x32 2.
+// Relative efficiencies measured on MI355X (tools/tilesweep.py over the
+// MobileNetV2UNet launch shapes); 64x64 wave tiles need 1 operand read per MFMA,
+// 32x96 1.33, 32x32 2.
 constexpr TileCfg kTiles[] = {
     {128, 128, 64, 64, 1.00f}, {64, 128, 32, 64, 0.95f}, {128, 64, 64, 32, 0.95f}, {64, 64, 32, 32, 0.85f},
-    {128, 96, 32, 96, 0.93f},  {128, 160, 32, 160, 0.95f}, {256, 32, 64, 32, 0.90f}, {128, 32, 32, 32, 0.80f},
+    {128, 96, 32, 96, 0.97f},  {128, 160, 32, 160, 0.95f}, {256, 32, 64, 32, 0.90f}, {128, 32, 32, 32, 0.92f},
 };
 
 constexpr int kTileBM[] = {128, 64, 128, 64, 128, 128, 256, 128};
 
+int g_force_tile = -1;  // tuning hook (seg_igemm_force_tile); -1 = cost model
+
 int pick_tile(long M, int N) {
+  if (g_force_tile >= 0) return g_force_tile;
   int best = 0;
   double best_score = -1.0;
   for (int i = 0; i < (int)(sizeof(kTiles) / sizeof(kTiles[0])); ++i) {
@@ -462,6 +467,16 @@ SEG_API int seg_conv_igemm(const float* in, long ldin, int N, int H, int W, int 
     case 6: return launch_igemm<256, 32, 64, 32>(a, ks, stream);
     default: return launch_igemm<128, 32, 32, 32>(a, ks, stream);
   }
+}
+
+// Tuning hook: force tile configuration t (0..7, see kTiles) for every following
+// seg_conv_igemm / seg_conv_igemm_row_tiles call of this process; -1 restores the
+// cost model.  Tile choice never changes results (each output is the same
+// k-ordered fmaf chain) except the BN-statistics tile partition.
+SEG_API int seg_igemm_force_tile(int t) {
+  if (t < -1 || t >= (int)(sizeof(kTiles) / sizeof(kTiles[0]))) return (int)hipErrorInvalidValue;
+  g_force_tile = t;
+  return 0;
 }
 
 // Row tiling seg_conv_igemm uses for an M x Cout output: returns the number of

@@ -66,6 +66,17 @@ int seg_conv_wgrad(const float* dy, long lddy, const float* x, long ldx,
 int seg_conv_wgrad_reduce(const float* part, int splits, float* dw, int Cout, int Cin, int ks,
                           int mode, int accumulate, hipStream_t stream);
 
+/* Every weight repack of a step in one launch.  `jobs` is a DEVICE array of
+ * njobs seg_pack_job (mode 0/1 as seg_pack_conv_weight, mode 2 = depthwise
+ * [9][C] as seg_pack_dw_weight with cout = C); max_elems = largest job's
+ * element count.  Replaces the per-conv packs of the engine's step. */
+typedef struct seg_pack_job {
+  const float* w;
+  float* wk;
+  int cout, cin, ks, ldk, mode, kin_pad;
+} seg_pack_job;
+int seg_pack_batch(const void* jobs, int njobs, long max_elems, hipStream_t stream);
+
 /* Depthwise 3x3 (torchvision InvertedResidual dw conv, features[1..17] via
  * src/unet.py:15-19): forward, data gradient, weight-gradient partials.
  * in_scale/in_shift/in_act (both pointers null = off): the producing layer's

@@ -520,3 +520,53 @@ SEG_API int seg_pack_conv_weight(const float* w, float* wk, int Cout, int Cin, i
   hipLaunchKernelGGL(pack_conv_weight_kernel, dim3(grid), dim3(256), 0, stream, w, wk, Cout, Cin, ks * ks, ldk, mode, kin_pad);
   SEG_RET_LAST();
 }
+
+// ---------------------------------------------------------------- batched packing
+// Every weight repack of a training step (forward mode 0, data-gradient mode 1,
+// depthwise mode 2 = [9][C]) in ONE launch: blockIdx.y = job, blockIdx.x
+// strides over the job's elements.  The job table lives in device memory and
+// stays valid while the weight storage does (the engine builds it once per
+// program and re-uploads only when a weight pointer changes).
+struct SegPackJob {
+  const float* w;
+  float* wk;
+  int cout, cin, ks, ldk, mode, kin_pad;
+};
+static_assert(sizeof(SegPackJob) == 40, "seg_pack_job ABI");
+
+__global__ __launch_bounds__(256) void pack_batch_kernel(const SegPackJob* __restrict__ jobs) {
+  const SegPackJob j = jobs[blockIdx.y];
+  const int taps = j.ks * j.ks;
+  if (j.mode == 2) {
+    const int total = 9 * j.cout;
+    for (int i = blockIdx.x * 256 + threadIdx.x; i < total; i += gridDim.x * 256) {
+      const int tap = i / j.cout, c = i - tap * j.cout;
+      j.wk[i] = j.w[c * 9 + tap];
+    }
+    return;
+  }
+  const int rows = j.mode == 0 ? j.cout : j.cin;
+  const long total = (long)rows * j.ldk;
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
+    const int r = (int)(i / j.ldk), k = (int)(i - (long)r * j.ldk);
+    float v = 0.f;
+    if (k < taps * j.kin_pad) {
+      const int tap = k / j.kin_pad, c = k - tap * j.kin_pad;
+      if (j.mode == 0) { if (c < j.cin) v = j.w[((long)r * j.cin + c) * taps + tap]; }
+      else if (c < j.cout) v = j.w[((long)c * j.cin + r) * taps + (taps - 1 - tap)];
+    }
+    j.wk[i] = v;
+  }
+}
+
+// jobs: device array of njobs seg_pack_job; max_elems = the largest job's element
+// count (sets the blocks per job).
+SEG_API int seg_pack_batch(const void* jobs, int njobs, long max_elems, hipStream_t stream) {
+  if (njobs < 0 || max_elems < 0) return (int)hipErrorInvalidValue;
+  if (njobs == 0) return 0;
+  const int bx = (int)std::max<long>(1, std::min<long>(seg_cdiv(max_elems, 256), 64));
+  hipLaunchKernelGGL(pack_batch_kernel, dim3(bx, njobs), dim3(256), 0, stream,
+                     reinterpret_cast<const SegPackJob*>(jobs));
+  SEG_RET_LAST();
+}
+

@@ -98,6 +98,10 @@ class ConvOp:
         # xform: the producer op whose BN + act this op applies to its input on load
         self.lazy = False
         self.xform = xform
+        # packed weights (Program.pack): forward [Cout][ldk_f] (None: a 1x1 conv uses the
+        # weight as is), data gradient [Cin][ldk_d]; depthwise: wk_f = [9][C]
+        self.wk_f = self.wk_d = None
+        self.ldk_f = self.ldk_d = 0
         self.ks = conv.kernel_size[0]
         self.stride = conv.stride[0]
         self.pad = conv.padding[0]
@@ -125,21 +129,15 @@ class ConvOp:
         w = self.conv.weight
         bias = self.conv.bias.data_ptr() if self.conv.bias is not None else None
         if self.kind == "dw":
-            wk = rt.tmp(9 * self.cout)
-            call("seg_pack_dw_weight", w.data_ptr(), wk.data_ptr(), self.cout, s)
             i = self.inp
-            call("seg_dw_fwd", rt.ptr(i), i.ld, i.N, i.H, i.W, i.C, *self._in_xform(rt), wk.data_ptr(), rt.ptr(y),
-                 y.ld, y.H, y.W, self.stride, s)
+            call("seg_dw_fwd", rt.ptr(i), i.ld, i.N, i.H, i.W, i.C, *self._in_xform(rt), self.wk_f.data_ptr(),
+                 rt.ptr(y), y.ld, y.H, y.W, self.stride, s)
         else:
             i = self.inp
-            if self.ks == 1 and self.cin_pad == self.cin:
+            if self.wk_f is None:
                 ldk, wk_ptr = self.cin, w.data_ptr()  # [Cout][Cin][1][1] already is the packed layout
             else:
-                ldk = r4(self.ks * self.ks * self.cin_pad)
-                wk = rt.tmp(self.cout * ldk)
-                call("seg_pack_conv_weight", w.data_ptr(), wk.data_ptr(), self.cout, self.cin, self.ks, ldk, 0,
-                     self.cin_pad, s)
-                wk_ptr = wk.data_ptr()
+                ldk, wk_ptr = self.ldk_f, self.wk_f.data_ptr()  # packed by Program.pack at the step start
             stat = None
             if self.bn is not None and rt.training:  # BN statistics fused into the conv epilogue
                 ntiles, tile_rows = rt.row_tiles(y.M, self.cout)
@@ -235,23 +233,17 @@ class ConvOp:
             return
         i = self.inp
         if self.kind == "dw":
-            wk = rt.tmp(9 * self.cout)
-            call("seg_pack_dw_weight", self.conv.weight.data_ptr(), wk.data_ptr(), self.cout, s)
             acc = rt.begin_write_accumulate(i)
-            call("seg_dw_dgrad", dYp, dY.ld, y.N, y.H, y.W, self.cout, wk.data_ptr(), rt.gptr(i), i.ld, i.H, i.W,
-                 self.stride, acc, s)
+            call("seg_dw_dgrad", dYp, dY.ld, y.N, y.H, y.W, self.cout, self.wk_f.data_ptr(), rt.gptr(i), i.ld, i.H,
+                 i.W, self.stride, acc, s)
         else:
             if self.stride != 1:
                 raise NotImplementedError("data gradient of a strided dense conv")
             kin = r4(self.cout)  # dY channels padded to 4 (the C=10 head)
-            ldk = r4(self.ks * self.ks * kin)
-            wk = rt.tmp(self.cin * ldk)
-            call("seg_pack_conv_weight", self.conv.weight.data_ptr(), wk.data_ptr(), self.cout, self.cin, self.ks,
-                 ldk, 1, kin, s)
             add_ptr, add_ld = rt.begin_write_add(i)
             _timed_call(f"igemm{self.ks}_dgrad", self.flops(), "seg_conv_igemm", dYp, dY.ld, y.N, y.H, y.W, kin,
-                        wk.data_ptr(), ldk, None, rt.gptr(i), i.ld, i.H, i.W, self.cin, self.ks, 1, self.pad,
-                        add_ptr, add_ld, None, s)
+                        self.wk_d.data_ptr(), self.ldk_d, None, rt.gptr(i), i.ld, i.H, i.W, self.cin, self.ks, 1,
+                        self.pad, add_ptr, add_ld, None, s)
         rt.mark_written(i)
 
 
@@ -339,6 +331,46 @@ class Program:
         del self.bufs[a.buf]
         op.out, op.lazy = op.y, True
         return op
+
+    def pack(self, stream):
+        """Repack every conv weight for this step (one seg_pack_batch launch).  The
+        packed buffers and the device job table are built once and rebuilt only
+        when a weight's storage moves (e.g. model.to())."""
+        convs = [op for op in self.ops if isinstance(op, ConvOp)]
+        key = tuple(op.conv.weight.data_ptr() for op in convs)
+        if getattr(self, "_pack_key", None) != key:
+            self._build_pack(convs, key)
+        if self._njobs:
+            call("seg_pack_batch", self._jobs.data_ptr(), self._njobs, self._max_elems, stream)
+
+    def _build_pack(self, convs, key):
+        import numpy as np
+        jt = np.dtype([("w", "<u8"), ("wk", "<u8"), ("cout", "<i4"), ("cin", "<i4"), ("ks", "<i4"),
+                       ("ldk", "<i4"), ("mode", "<i4"), ("kin", "<i4")])
+        assert jt.itemsize == 40
+        jobs, max_elems = [], 0
+        for op in convs:
+            w = op.conv.weight
+            dev = w.device
+            if op.kind == "dw":
+                op.wk_f = torch.empty(9 * op.cout, device=dev, dtype=torch.float32)
+                jobs.append((w.data_ptr(), op.wk_f.data_ptr(), op.cout, 1, 3, 9, 2, 1))
+                max_elems = max(max_elems, 9 * op.cout)
+                continue
+            if not (op.ks == 1 and op.cin_pad == op.cin):
+                op.ldk_f = r4(op.ks * op.ks * op.cin_pad)
+                op.wk_f = torch.empty(op.cout * op.ldk_f, device=dev, dtype=torch.float32)
+                jobs.append((w.data_ptr(), op.wk_f.data_ptr(), op.cout, op.cin, op.ks, op.ldk_f, 0, op.cin_pad))
+                max_elems = max(max_elems, op.cout * op.ldk_f)
+            if not op.first:
+                kin = r4(op.cout)
+                op.ldk_d = r4(op.ks * op.ks * kin)
+                op.wk_d = torch.empty(op.cin * op.ldk_d, device=dev, dtype=torch.float32)
+                jobs.append((w.data_ptr(), op.wk_d.data_ptr(), op.cout, op.cin, op.ks, op.ldk_d, 1, kin))
+                max_elems = max(max_elems, op.cin * op.ldk_d)
+        table = np.array(jobs, dtype=jt)
+        self._jobs = torch.from_numpy(table.view(np.uint8).copy()).to(convs[0].conv.weight.device)
+        self._njobs, self._max_elems, self._pack_key = len(jobs), max_elems, key
 
     def params(self):
         seen, ps = set(), []
@@ -595,6 +627,7 @@ class Run:
     def forward(self):
         global LAST_RUN
         x, img = self.image, self.prog.image
+        self.prog.pack(self.stream)
         call("seg_nchw_to_nhwc", x.data_ptr(), img.N, 3, img.H, img.W, self.ptr(img), img.ld, self.stream)
         for op in self.prog.ops:
             op.forward(self)

@@ -51,6 +51,9 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-timer", action="store_true", help="skip the per-launch HIP-event roofline timing")
+    ap.add_argument("--workload", choices=("train", "infer"), default="train",
+                    help="train: BASELINE configs[1] (the headline); infer: configs[3], inference.py's per-frame path")
+    ap.add_argument("--frames", type=int, default=500, help="timed frames of --workload infer")
     return ap.parse_args()
 
 
@@ -80,8 +83,71 @@ def cpu_baseline(args):
                       f"{steps} timed steps ({dt:.1f} s) after 1 warm-up, torch CPU fp32"}
 
 
+def bench_infer(args):
+    """configs[3]: inference.py's per-frame path (preprocess_image -> model.eval() forward ->
+    argmax + INTER_NEAREST mask) for a 720x1280 uint8 BGR frame resized to 128x256, bs=1,
+    replayed as one HIP graph.  value = frames/s with the frame already in HBM."""
+    import numpy as np
+    from seg_amd import MobileNetV2UNet, deterministic_init
+    from seg_amd.infer import Predictor
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    model = deterministic_init(MobileNetV2UNet(args.classes), seed=0, random_running_stats=True).to(dev).eval()
+    g = np.random.Generator(np.random.PCG64(0))
+    frame = g.integers(0, 256, (720, 1280, 3), dtype=np.uint8)
+    res = {}
+    for mode in ("graph", "eager", "graph_h2d"):
+        pred = Predictor(model, frame_hw=(720, 1280), graph=mode != "eager")
+        pred.set_frame(frame)
+        fn = (lambda: pred(frame)) if mode == "graph_h2d" else pred.step
+        for _ in range(max(args.warmup, 3)):
+            fn()
+        torch.cuda.synchronize()
+        n = args.frames if mode != "graph_h2d" else max(args.frames // 5, 20)
+        t0 = time.perf_counter()
+        for _ in range(n):
+            fn()
+        torch.cuda.synchronize()
+        res[mode] = (time.perf_counter() - t0) / n
+    cpu = None
+    if not args.no_cpu_baseline:
+        from oracle import cvresize, segref
+        threads = min(os.cpu_count() or 1, len(os.sched_getaffinity(0)))
+        threads = min(threads, int(os.environ.get("OMP_NUM_THREADS", threads)))
+        torch.set_num_threads(threads)
+        p = segref.canonical_state(model.state_dict())
+        def one():
+            x, _ = cvresize.preprocess_image(frame)
+            with torch.no_grad():
+                lo = segref.mobilenet_unet_forward(p, torch.from_numpy(x), False)
+            return cvresize.class_mask(lo.numpy(), (720, 1280))
+        one()
+        t0, k = time.perf_counter(), 0
+        while time.perf_counter() - t0 < args.cpu_seconds:
+            one()
+            k += 1
+        dt = time.perf_counter() - t0
+        cpu = {"value": round(k / dt, 2), "unit": "frames/s", "cores": threads, "kind": "port",
+               "sample": f"oracle cvresize.preprocess_image + segref eval forward (torch CPU fp32) + class_mask, "
+                         f"{k} frames in {dt:.1f} s"}
+    line = {"metric": "frames/sec inference MobileNetV2UNet 720x1280 frame -> 128x256, bs=1 (BASELINE configs[3])",
+            "value": round(1.0 / res["graph"], 1), "unit": "frames/s", "n_gpus": 1, "steps": args.frames,
+            "warmup": args.warmup, "ms_per_step": round(res["graph"] * 1e3, 4), "higher_is_better": True,
+            "scaling": "none", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+            "config": {"workload": "inference.py per-frame path: cv2-style resize + normalise, BN-folded eval forward, "
+                                   "argmax + nearest mask, one hipGraph replay per frame",
+                       "model": "MobileNetV2UNet", "global_batch": 1, "frame": [720, 1280], "image": [128, 256],
+                       "parallelism": "none"},
+            "latency_ms": {"graph": round(res["graph"] * 1e3, 4), "eager": round(res["eager"] * 1e3, 4),
+                           "graph_with_h2d_frame_copy": round(res["graph_h2d"] * 1e3, 4)},
+            "roofline": None, "cpu_baseline": cpu}
+    print(json.dumps(line), flush=True)
+
+
 def main():
     args = parse()
+    if args.workload == "infer":
+        return bench_infer(args)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))

@@ -42,6 +42,22 @@ int seg_conv_igemm(const float* in, long ldin, int N, int H, int W, int Cin,
                    float* out, long ldout, int Ho, int Wo, int Cout,
                    int ks, int stride, int pad,
                    const float* add, long ldadd, float* stat, hipStream_t stream);
+/* seg_conv_igemm with an epilogue activation: out = act(conv + bias + add).  The
+ * inference path (BatchNorm folded into wk/bias by seg_bn_fold_batch) uses it for
+ * conv -> BN -> ReLU/ReLU6 of src/unet.py:58-63,113-115 and torchvision's
+ * Conv2dNormActivation in one launch.  act != 0 excludes `stat`.  splits > 1
+ * (seg_conv_igemm_splits) runs split-K: raw partials in `work` (>= splits * M *
+ * Cout floats, M = N*Ho*Wo), then a fixed-order reduce that applies the epilogue;
+ * it excludes `stat`.  splits == 1: `work` unused. */
+int seg_conv_igemm_act(const float* in, long ldin, int N, int H, int W, int Cin,
+                       const float* wk, int ldk, const float* bias,
+                       float* out, long ldout, int Ho, int Wo, int Cout,
+                       int ks, int stride, int pad,
+                       const float* add, long ldadd, float* stat, int act, float* work, int splits,
+                       hipStream_t stream);
+/* Split-K factor for seg_conv_igemm_act (1 = none): > 1 only when the output tiles
+ * cannot fill the 256 CUs (batch-1 inference). */
+int seg_conv_igemm_splits(long M, int Cout, int Cin, int ks);
 /* Row tiles (and their height) seg_conv_igemm uses for an M x Cout output. */
 /* Tuning hook: force tile configuration t (0..7) for the following
  * seg_conv_igemm calls of this process, -1 = the built-in cost model. */
@@ -86,6 +102,11 @@ int seg_pack_dw_weight(const float* w, float* wk, int C, hipStream_t stream);
 int seg_dw_fwd(const float* in, long ldin, int N, int H, int W, int C,
                const float* in_scale, const float* in_shift, int in_act, const float* wk,
                float* out, long ldout, int Ho, int Wo, int stride, hipStream_t stream);
+/* Inference depthwise conv with its BatchNorm folded (seg_bn_fold_batch):
+ * out = act(dwconv(in, wk) + bias). */
+int seg_dw_fwd_bias_act(const float* in, long ldin, int N, int H, int W, int C, const float* wk,
+                        const float* bias, int act, float* out, long ldout, int Ho, int Wo, int stride,
+                        hipStream_t stream);
 int seg_dw_dgrad(const float* dy, long lddy, int N, int Ho, int Wo, int C, const float* wk,
                  float* dx, long lddx, int H, int W, int stride, int accumulate, hipStream_t stream);
 long seg_dw_wgrad_blocks(int N, int Ho, int Wo, int C);
@@ -155,6 +176,32 @@ int seg_ce_upsample_grad(const float* low, long ld, int N, int H, int W, int C,
                          const long long* labels, int Ho, int Wo, int ignore_index,
                          const float* grad_out, const float* stats, float* dhigh, long ldh,
                          hipStream_t stream);
+
+/* ---- inference (inference.py: preprocess_image :28-46, model.eval() forward
+ *      :23-25,162-163, overlay_predictions' argmax + resize :64-70) ---------- */
+/* Fold eval-mode BatchNorm2d into the preceding conv, all layers in one launch:
+ * w' = w * g/sqrt(rv+eps), b' = b * g/sqrt(rv+eps) + beta - rm * g/sqrt(rv+eps)
+ * (gamma == NULL: plain copy).  `jobs` is a DEVICE array of seg_fold_job;
+ * max_elems = the largest cout*kper + cout. */
+typedef struct seg_fold_job {
+  const float *w, *bias, *gamma, *beta, *running_mean, *running_var;
+  float *w_out, *b_out;
+  int cout, kper;
+  float eps;
+  int pad_;
+} seg_fold_job;
+int seg_bn_fold_batch(const void* jobs, int njobs, long max_elems, hipStream_t stream);
+/* cv2.resize(frame, (W, H)) (INTER_LINEAR, uint8) -> cvtColor(BGR2RGB) ->
+ * ToTensor -> Normalize(mean, std), fused: N uint8 BGR frames [N][Hf][row_bytes]
+ * -> NHWC rows out[N*H*W][ld] (ld >= 4, channel 3 zeroed). */
+int seg_preprocess_bgr(const unsigned char* frame, int N, int Hf, int Wf, long row_bytes, float* out, int ld,
+                       int H, int W, float mean_r, float mean_g, float mean_b, float std_r, float std_g,
+                       float std_b, hipStream_t stream);
+/* uint8 class mask [N][Hf][Wf]: torch.max(dim=1) of the model's logits (the
+ * align_corners=True x(Hm/H) upsample of the low-res NHWC logits, src/unet.py:49)
+ * resized to the frame with cv2 INTER_NEAREST.  First maximum wins. */
+int seg_argmax_nearest(const float* low, long ld, int N, int H, int W, int C, int Hm, int Wm,
+                       unsigned char* mask, int Hf, int Wf, hipStream_t stream);
 
 #ifdef __cplusplus
 }

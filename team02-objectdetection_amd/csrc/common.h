@@ -74,4 +74,31 @@ __device__ __forceinline__ int xcd_swizzle(int b, int nblk) {
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + pos;
 }
 
+// Bilinear source index/weights of output index `dst` along one axis, in aten's
+// CPU upsample_bilinear2d float arithmetic (see resample.hip).  Shared by the
+// resampling kernels and the fused inference argmax (infer.hip) so both compute
+// bitwise the same interpolated logits.
+struct Lin {
+  int i0, i1;
+  float l0, l1;
+};
+
+__device__ __forceinline__ Lin lin_index(int dst, int in, float scale, int ac) {
+  float src = ac ? scale * (float)dst : fmaxf(scale * ((float)dst + 0.5f) - 0.5f, 0.f);
+  int i0 = (int)floorf(src);
+  if (i0 > in - 1) i0 = in - 1;
+  Lin r;
+  r.i0 = i0;
+  r.i1 = i0 + (i0 < in - 1 ? 1 : 0);
+  r.l1 = fminf(fmaxf(src - (float)i0, 0.f), 1.f);
+  r.l0 = 1.f - r.l1;
+  return r;
+}
+
+// The 2-D bilinear blend of four float4 taps -- one definition for every kernel
+// that interpolates logits, so they round identically.
+__device__ __forceinline__ f32x4 bilerp4(f32x4 v00, f32x4 v01, f32x4 v10, f32x4 v11, const Lin& lh, const Lin& lw) {
+  return lh.l0 * (lw.l0 * v00 + lw.l1 * v01) + lh.l1 * (lw.l0 * v10 + lw.l1 * v11);
+}
+
 #define SEG_RET_LAST() return (int)hipGetLastError()

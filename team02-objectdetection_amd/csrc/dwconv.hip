@@ -88,12 +88,15 @@ __device__ __forceinline__ void store_strip(float* o, long ld, const f32x4 (&acc
 // out[n][ho][wo][c] = sum_{ky,kx} w[ky][kx][c] * in[n][ho*S-1+ky][wo*S-1+kx][c]
 // FLIP: taps read as w[8-tap] -- the stride-1 data gradient is this correlation
 // of dY with the flipped kernel.  ACC: out += (the data gradient's accumulate).
-template <int S, bool LAZY, bool FLIP, bool ACC>
+// EPI (inference, BN folded into wk): out = act(acc + obias) -- the folded
+// BatchNorm shift and the ReLU6 applied in the epilogue.
+template <int S, bool LAZY, bool FLIP, bool ACC, bool EPI = false>
 __global__ __launch_bounds__(256) void dw_fwd_kernel(const float* __restrict__ in, long ldin, int N, int H, int W,
                                                      int C, const float* __restrict__ isc,
                                                      const float* __restrict__ ish, int iact,
                                                      const float* __restrict__ wk, float* __restrict__ out,
-                                                     long ldout, int Ho, int Wo) {
+                                                     long ldout, int Ho, int Wo,
+                                                     const float* __restrict__ obias, int oact) {
   const int CG = C >> 2;
   const int SPR = (Wo + TW - 1) / TW;
   const long total = (long)N * Ho * SPR * CG;
@@ -150,6 +153,11 @@ __global__ __launch_bounds__(256) void dw_fwd_kernel(const float* __restrict__ i
           a[k] = c2;
         }
       }
+    }
+    if (EPI) {
+      const f32x4 ob = ld4(obias + c), one = {1.f, 1.f, 1.f, 1.f};
+#pragma unroll
+      for (int t = 0; t < TW; ++t) acc[t] = seg_bn_act4(acc[t], one, ob, oact);
     }
     store_strip<ACC>(out + (row * Wo + ws) * ldout + c, ldout, acc, Wo - ws);
   }
@@ -355,13 +363,30 @@ SEG_API int seg_dw_fwd(const float* in, long ldin, int N, int H, int W, int C, c
   const bool lazy = in_scale != nullptr;
 #define SEG_DW_FWD(S, L)                                                                                         \
   hipLaunchKernelGGL((dw_fwd_kernel<S, L, false, false>), dim3(grid), dim3(256), 0, stream, in, ldin, N, H, W, C, \
-                     in_scale, in_shift, in_act, wk, out, ldout, Ho, Wo)
+                     in_scale, in_shift, in_act, wk, out, ldout, Ho, Wo, nullptr, 0)
   if (stride == 1) {
     if (lazy) SEG_DW_FWD(1, true); else SEG_DW_FWD(1, false);
   } else {
     if (lazy) SEG_DW_FWD(2, true); else SEG_DW_FWD(2, false);
   }
 #undef SEG_DW_FWD
+  SEG_RET_LAST();
+}
+
+// Inference depthwise conv with the BatchNorm folded into wk (seg_bn_fold):
+// out = act(dwconv(in, wk) + bias).
+SEG_API int seg_dw_fwd_bias_act(const float* in, long ldin, int N, int H, int W, int C, const float* wk,
+                                const float* bias, int act, float* out, long ldout, int Ho, int Wo, int stride,
+                                hipStream_t stream) {
+  if ((C & 3) || (ldin & 3) || (ldout & 3) || (stride != 1 && stride != 2) || !bias || act < 0 || act > 2)
+    return (int)hipErrorInvalidValue;
+  const int grid = item_grid((long)N * Ho * ((Wo + TW - 1) / TW) * (C / 4));
+  if (stride == 1)
+    hipLaunchKernelGGL((dw_fwd_kernel<1, false, false, false, true>), dim3(grid), dim3(256), 0, stream, in, ldin, N, H,
+                       W, C, nullptr, nullptr, 0, wk, out, ldout, Ho, Wo, bias, act);
+  else
+    hipLaunchKernelGGL((dw_fwd_kernel<2, false, false, false, true>), dim3(grid), dim3(256), 0, stream, in, ldin, N, H,
+                       W, C, nullptr, nullptr, 0, wk, out, ldout, Ho, Wo, bias, act);
   SEG_RET_LAST();
 }
 
@@ -373,10 +398,10 @@ SEG_API int seg_dw_dgrad(const float* dy, long lddy, int N, int Ho, int Wo, int 
     const int grid = item_grid((long)N * H * ((W + TW - 1) / TW) * (C / 4));
     if (accumulate)
       hipLaunchKernelGGL((dw_fwd_kernel<1, false, true, true>), dim3(grid), dim3(256), 0, stream, dy, lddy, N, Ho, Wo,
-                         C, nullptr, nullptr, 0, wk, dx, lddx, H, W);
+                         C, nullptr, nullptr, 0, wk, dx, lddx, H, W, nullptr, 0);
     else
       hipLaunchKernelGGL((dw_fwd_kernel<1, false, true, false>), dim3(grid), dim3(256), 0, stream, dy, lddy, N, Ho,
-                         Wo, C, nullptr, nullptr, 0, wk, dx, lddx, H, W);
+                         Wo, C, nullptr, nullptr, 0, wk, dx, lddx, H, W, nullptr, 0);
   } else {
     const int grid = item_grid((long)N * H * ((W + TW - 1) / TW) * (C / 4));
     hipLaunchKernelGGL(dw_dgrad_s2_kernel, dim3(grid), dim3(256), 0, stream, dy, lddy, N, Ho, Wo, C, wk, dx, lddx,

@@ -38,6 +38,9 @@ struct IgemmArgs {
   int Ho, Wo, Cout;
   int stride, pad;
   int K, M;
+  int kchunk;                    // split-K: K range of blockIdx.y (a multiple of BK); == K when unsplit
+  float* part;                   // split-K: raw partial sums [gridDim.y][M][Cout] (no epilogue), else null
+  int act;                       // epilogue activation of act(acc + bias + add) (SegAct); 0 in training
 };
 
 #ifndef SEG_IGEMM_DEPTH
@@ -83,6 +86,7 @@ __global__ __launch_bounds__(256) void igemm_conv_kernel(IgemmArgs a) {
   const int lid = xcd_swizzle(blockIdx.x, gridDim.x);  // adjacent image rows on one XCD's L2
   const int tn = lid % tiles_n, tm = lid / tiles_n;
   const int m0 = tm * BM, n0 = tn * BN;
+  const int kbeg = blockIdx.y * a.kchunk;  // split-K: this block's K range [kbeg, kbeg + kchunk)
 
   // Per-thread A slots: the pixel is fixed across the K loop; the (tap, channel)
   // position advances by BK per chunk without integer division.
@@ -96,7 +100,7 @@ __global__ __launch_bounds__(256) void igemm_conv_kernel(IgemmArgs a) {
     const int p = m0 + row;
     a_ok[i] = (idx < A_VEC) && (p < a.M);
     const int pp = a_ok[i] ? p : 0;
-    a_k[i] = kq * 4;
+    a_k[i] = kq * 4 + kbeg;
     const int tap = a_k[i] / a.Cin;
     a_ci[i] = a_k[i] - tap * a.Cin;
     a_ky[i] = tap / KS;
@@ -158,7 +162,10 @@ __global__ __launch_bounds__(256) void igemm_conv_kernel(IgemmArgs a) {
       u_bok[i] = idx < B_VEC && co < a.Cout;
       u_boff[i] = (long)(u_bok[i] ? co : 0) * a.ldk + u_kq4;
     }
-    u_toff1 = tap_off(1);
+    u_tap = kbeg / a.Cin;
+    u_ci = kbeg - u_tap * a.Cin;
+    u_toff0 = tap_off(u_tap);
+    u_toff1 = tap_off(u_tap + 1);
   }
 
   auto load_tiles = [&](int k0, f32x4 (&ra)[A_PER], f32x4 (&rb)[B_PER]) {
@@ -242,7 +249,7 @@ __global__ __launch_bounds__(256) void igemm_conv_kernel(IgemmArgs a) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[mi][ni][r] = 0.f;
 
-  const int nk = (a.K + BK - 1) / BK;
+  const int nk = (min(a.K - kbeg, a.kchunk) + BK - 1) / BK;
   const int lrow = lane & 31, lk = (lane >> 5) * 4;
   auto compute = [&](int cur) {
 #pragma unroll
@@ -265,22 +272,22 @@ __global__ __launch_bounds__(256) void igemm_conv_kernel(IgemmArgs a) {
 #if SEG_IGEMM_STAGES == 1
   // one LDS stage: regs -> LDS, barrier, prefetch the next chunk, compute, barrier
   f32x4 ra[A_PER], rb[B_PER];
-  load_tiles(0, ra, rb);
+  load_tiles(kbeg, ra, rb);
   for (int kt = 0; kt < nk; ++kt) {
     store_tiles(0, ra, rb);
     __syncthreads();
-    if (kt + 1 < nk) load_tiles((kt + 1) * BK, ra, rb);
+    if (kt + 1 < nk) load_tiles(kbeg + (kt + 1) * BK, ra, rb);
     compute(0);
     __syncthreads();
   }
 #elif SEG_IGEMM_DEPTH == 1
   f32x4 ra[A_PER], rb[B_PER];
-  load_tiles(0, ra, rb);
+  load_tiles(kbeg, ra, rb);
   store_tiles(0, ra, rb);
   __syncthreads();
   for (int kt = 0; kt < nk; ++kt) {
     const int cur = kt & 1;
-    if (kt + 1 < nk) load_tiles((kt + 1) * BK, ra, rb);
+    if (kt + 1 < nk) load_tiles(kbeg + (kt + 1) * BK, ra, rb);
     compute(cur);
     if (kt + 1 < nk) store_tiles(cur ^ 1, ra, rb);
     __syncthreads();
@@ -291,19 +298,19 @@ __global__ __launch_bounds__(256) void igemm_conv_kernel(IgemmArgs a) {
   // phases (~2 x 2048 MFMA cycles at 64x64 per wave) to land -- one phase is shorter
   // than the HBM latency under load, which left one-block-per-CU grids stalled.
   f32x4 ra0[A_PER], rb0[B_PER], ra1[A_PER], rb1[B_PER];
-  load_tiles(0, ra0, rb0);
+  load_tiles(kbeg, ra0, rb0);
   store_tiles(0, ra0, rb0);
-  if (nk > 1) load_tiles(BK, ra1, rb1);
+  if (nk > 1) load_tiles(kbeg + BK, ra1, rb1);
   __syncthreads();
   for (int kt = 0; kt < nk; kt += 2) {
     // LDS stage 0 holds chunk kt; set 1 holds chunk kt+1 (in flight)
-    if (kt + 2 < nk) load_tiles((kt + 2) * BK, ra0, rb0);
+    if (kt + 2 < nk) load_tiles(kbeg + (kt + 2) * BK, ra0, rb0);
     compute(0);
     if (kt + 1 < nk) store_tiles(1, ra1, rb1);
     __syncthreads();
     if (kt + 1 >= nk) break;
     // LDS stage 1 holds chunk kt+1; set 0 holds chunk kt+2
-    if (kt + 3 < nk) load_tiles((kt + 3) * BK, ra1, rb1);
+    if (kt + 3 < nk) load_tiles(kbeg + (kt + 3) * BK, ra1, rb1);
     compute(1);
     if (kt + 2 < nk) store_tiles(0, ra0, rb0);
     __syncthreads();
@@ -311,6 +318,22 @@ __global__ __launch_bounds__(256) void igemm_conv_kernel(IgemmArgs a) {
 #endif
 
   // Epilogue: C layout of 32x32 f32 MFMA: col = lane&31, row = (r&3) + 8(r>>2) + 4(lane>>5).
+  if (a.part) {  // split-K: raw partial sums; seg_igemm_splitk_reduce applies the epilogue
+    float* P = a.part + (long)blockIdx.y * a.M * a.Cout;
+#pragma unroll
+    for (int ni = 0; ni < NI; ++ni) {
+      const int col = n0 + wn0 + ni * 32 + lrow;
+      if (col >= a.Cout) continue;
+#pragma unroll
+      for (int mi = 0; mi < MI; ++mi)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int row = m0 + wm0 + mi * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+          if (row < a.M) P[(long)row * a.Cout + col] = acc[mi][ni][r];
+        }
+    }
+    return;
+  }
   float bcol[NI];
 #pragma unroll
   for (int ni = 0; ni < NI; ++ni) {
@@ -373,6 +396,7 @@ __global__ __launch_bounds__(256) void igemm_conv_kernel(IgemmArgs a) {
         if (row < a.M) {
           float v = acc[mi][ni][r];
           if (a.add) v += a.add[(long)row * a.ldadd + col];
+          if (a.act) v = seg_act(v, a.act);
           a.out[(long)row * a.ldout + col] = v;
         }
       }
@@ -383,8 +407,9 @@ __global__ __launch_bounds__(256) void igemm_conv_kernel(IgemmArgs a) {
 template <int BM, int BN, int WM, int WN, int BK>
 int launch_igemm_bk(const IgemmArgs& a, int ks, hipStream_t s) {
   const int grid = seg_cdiv(a.M, BM) * seg_cdiv(a.Cout, BN);
+  const int splits = seg_cdiv(a.K, a.kchunk);
   const bool ut = SEG_IGEMM_UT && (SEG_IGEMM_UT2 ? a.Cin >= BK : a.Cin % BK == 0);
-#define SEG_IG(KS, U) hipLaunchKernelGGL((igemm_conv_kernel<BM, BN, WM, WN, KS, BK, U>), dim3(grid), dim3(256), 0, s, a)
+#define SEG_IG(KS, U) hipLaunchKernelGGL((igemm_conv_kernel<BM, BN, WM, WN, KS, BK, U>), dim3(grid, splits), dim3(256), 0, s, a)
   if (ks == 1) {
     if (ut) SEG_IG(1, true); else SEG_IG(1, false);
   } else {
@@ -397,10 +422,15 @@ int launch_igemm_bk(const IgemmArgs& a, int ks, hipStream_t s) {
 // K chunk depth: SEG_IGEMM_BK (32) unless K is short and not a multiple of it
 // (the stem's K = 36, 1x1 convs with Cin 16/24/144...), where padding K up to a
 // 32 multiple would waste MFMA work: then 16.
+inline int igemm_bk(int K) { return (SEG_IGEMM_BK != 16 && (K <= 64 || (K % SEG_IGEMM_BK != 0 && K < 512))) ? 16 : SEG_IGEMM_BK; }
+
+// split-K: `splits` K ranges of whole BK chunks (a.part set by the caller when splits > 1)
 template <int BM, int BN, int WM, int WN>
-int launch_igemm(const IgemmArgs& a, int ks, hipStream_t s) {
-  if (SEG_IGEMM_BK != 16 && (a.K <= 64 || (a.K % SEG_IGEMM_BK != 0 && a.K < 512)))
-    return launch_igemm_bk<BM, BN, WM, WN, 16>(a, ks, s);
+int launch_igemm(IgemmArgs a, int ks, int splits, hipStream_t s) {
+  const int bk = igemm_bk(a.K);
+  const int nk = seg_cdiv(a.K, bk);
+  a.kchunk = seg_cdiv(nk, splits) * bk;
+  if (bk == 16) return launch_igemm_bk<BM, BN, WM, WN, 16>(a, ks, s);
   return launch_igemm_bk<BM, BN, WM, WN, SEG_IGEMM_BK>(a, ks, s);
 }
 
@@ -439,34 +469,96 @@ int pick_tile(long M, int N) {
   return best;
 }
 
+
+
+// Split-K factor for an M x Cout x K conv GEMM: > 1 only when the output tiles
+// alone cannot fill the chip (small images / batch 1 inference), keeping >= 4 K
+// chunks per split.
+int igemm_splits(long M, int Cout, int K) {
+  const int t = pick_tile(M, Cout);
+  const long blocks = ((M + kTiles[t].bm - 1) / kTiles[t].bm) * ((Cout + kTiles[t].bn - 1) / kTiles[t].bn);
+  const int nk = seg_cdiv(K, igemm_bk(K));
+  if (blocks >= 256 || nk < 8) return 1;
+  int s = (int)std::min<long>(seg_cdiv(512, blocks), nk / 4);
+  s = std::min(s, 64);
+  if (s < 2) return 1;
+  return seg_cdiv(nk, seg_cdiv(nk, s));  // no empty split
+}
+
+// out = act(sum_z part[z] + bias + add): the split-K epilogue (fixed z order: deterministic).
+__global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restrict__ part, int splits, long M, int Cout,
+                                                            const float* __restrict__ bias,
+                                                            const float* __restrict__ add, long ldadd,
+                                                            float* __restrict__ out, long ldout, int act) {
+  const long total = M * Cout;
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
+    const long row = i / Cout;
+    const int col = (int)(i - row * Cout);
+    float v = 0.f;
+    for (int z = 0; z < splits; ++z) v += part[z * total + i];
+    if (bias) v += bias[col];
+    if (add) v += add[row * ldadd + col];
+    if (act) v = seg_act(v, act);
+    out[row * ldout + col] = v;
+  }
+}
+
 }  // namespace
 
-// out = conv(in, W) (+bias) (+add).  `wk` is the packed weight of seg_pack_conv_weight
+// out = act(conv(in, W) + bias + add).  `wk` is the packed weight of seg_pack_conv_weight
 // ([Cout][ldk], k = tap*Cin + ci).  ks in {1,3}; ks == 1 requires stride 1, pad 0.
-// Cin, ldin, ldk must be multiples of 4 and `in`/`wk` 16-byte aligned.
+// Cin, ldin, ldk must be multiples of 4 and `in`/`wk` 16-byte aligned.  splits > 1
+// (from seg_conv_igemm_splits) runs split-K through `work` (>= splits*M*Cout floats)
+// and a reduce pass; it excludes `stat`.
+SEG_API int seg_conv_igemm_act(const float* in, long ldin, int N, int H, int W, int Cin,
+                               const float* wk, int ldk, const float* bias,
+                               float* out, long ldout, int Ho, int Wo, int Cout,
+                               int ks, int stride, int pad,
+                               const float* add, long ldadd, float* stat, int act, float* work, int splits,
+                               hipStream_t stream) {
+  if ((Cin & 3) || (ldin & 3) || (ldk & 3) || (ks != 1 && ks != 3)) return (int)hipErrorInvalidValue;
+  if (ks == 1 && (stride != 1 || pad != 0 || Ho != H || Wo != W)) return (int)hipErrorInvalidValue;
+  if (act < SEG_ACT_NONE || act > SEG_ACT_RELU6 || (act && stat)) return (int)hipErrorInvalidValue;
+  if (splits < 1 || (splits > 1 && (!work || stat))) return (int)hipErrorInvalidValue;
+  IgemmArgs a;
+  a.in = in; a.ldin = ldin; a.wk = wk; a.ldk = ldk; a.bias = bias;
+  a.add = add; a.ldadd = ldadd; a.out = out; a.ldout = ldout; a.stat = stat;
+  a.N = N; a.H = H; a.W = W; a.Cin = Cin; a.Ho = Ho; a.Wo = Wo; a.Cout = Cout;
+  a.stride = stride; a.pad = pad; a.K = ks * ks * Cin; a.M = N * Ho * Wo; a.act = act;
+  a.part = splits > 1 ? work : nullptr;
+  if (a.M == 0 || Cout == 0) return 0;
+  int rc;
+  switch (pick_tile(a.M, Cout)) {
+    case 0: rc = launch_igemm<128, 128, 64, 64>(a, ks, splits, stream); break;
+    case 1: rc = launch_igemm<64, 128, 32, 64>(a, ks, splits, stream); break;
+    case 2: rc = launch_igemm<128, 64, 64, 32>(a, ks, splits, stream); break;
+    case 3: rc = launch_igemm<64, 64, 32, 32>(a, ks, splits, stream); break;
+    case 4: rc = launch_igemm<128, 96, 32, 96>(a, ks, splits, stream); break;
+    case 5: rc = launch_igemm<128, 160, 32, 160>(a, ks, splits, stream); break;
+    case 6: rc = launch_igemm<256, 32, 64, 32>(a, ks, splits, stream); break;
+    default: rc = launch_igemm<128, 32, 32, 32>(a, ks, splits, stream); break;
+  }
+  if (rc || splits == 1) return rc;
+  const long total = (long)a.M * Cout;
+  hipLaunchKernelGGL(splitk_reduce_kernel, dim3((int)std::min<long>(seg_cdiv(total, 256), 4096)), dim3(256), 0,
+                     stream, work, splits, (long)a.M, Cout, bias, add, ldadd, out, ldout, act);
+  SEG_RET_LAST();
+}
+
 SEG_API int seg_conv_igemm(const float* in, long ldin, int N, int H, int W, int Cin,
                            const float* wk, int ldk, const float* bias,
                            float* out, long ldout, int Ho, int Wo, int Cout,
                            int ks, int stride, int pad,
                            const float* add, long ldadd, float* stat, hipStream_t stream) {
-  if ((Cin & 3) || (ldin & 3) || (ldk & 3) || (ks != 1 && ks != 3)) return (int)hipErrorInvalidValue;
-  if (ks == 1 && (stride != 1 || pad != 0 || Ho != H || Wo != W)) return (int)hipErrorInvalidValue;
-  IgemmArgs a;
-  a.in = in; a.ldin = ldin; a.wk = wk; a.ldk = ldk; a.bias = bias;
-  a.add = add; a.ldadd = ldadd; a.out = out; a.ldout = ldout; a.stat = stat;
-  a.N = N; a.H = H; a.W = W; a.Cin = Cin; a.Ho = Ho; a.Wo = Wo; a.Cout = Cout;
-  a.stride = stride; a.pad = pad; a.K = ks * ks * Cin; a.M = N * Ho * Wo;
-  if (a.M == 0 || Cout == 0) return 0;
-  switch (pick_tile(a.M, Cout)) {
-    case 0: return launch_igemm<128, 128, 64, 64>(a, ks, stream);
-    case 1: return launch_igemm<64, 128, 32, 64>(a, ks, stream);
-    case 2: return launch_igemm<128, 64, 64, 32>(a, ks, stream);
-    case 3: return launch_igemm<64, 64, 32, 32>(a, ks, stream);
-    case 4: return launch_igemm<128, 96, 32, 96>(a, ks, stream);
-    case 5: return launch_igemm<128, 160, 32, 160>(a, ks, stream);
-    case 6: return launch_igemm<256, 32, 64, 32>(a, ks, stream);
-    default: return launch_igemm<128, 32, 32, 32>(a, ks, stream);
-  }
+  return seg_conv_igemm_act(in, ldin, N, H, W, Cin, wk, ldk, bias, out, ldout, Ho, Wo, Cout, ks, stride, pad, add,
+                            ldadd, stat, SEG_ACT_NONE, nullptr, 1, stream);
+}
+
+// Split-K factor seg_conv_igemm_act should be given for this conv (1 = none); the
+// workspace is splits * N*Ho*Wo * Cout floats.
+SEG_API int seg_conv_igemm_splits(long M, int Cout, int Cin, int ks) {
+  if (M <= 0 || Cout <= 0 || Cin <= 0) return 1;
+  return igemm_splits(M, Cout, ks * ks * Cin);
 }
 
 // Tuning hook: force tile configuration t (0..7, see kTiles) for every following

@@ -1,0 +1,205 @@
+// Inference path of the reference's inference.py:
+//
+//   preprocess_image (inference.py:28-46): cv2.resize(frame, (256,128)) with the
+//     default INTER_LINEAR on the uint8 BGR frame, cv2.cvtColor(BGR2RGB),
+//     transforms.ToTensor() (/255) and transforms.Normalize(ImageNet mean/std)
+//     -> seg_preprocess_bgr writes the model's NHWC4 input rows directly;
+//   model.eval() forward (inference.py:25,162-163) with every BatchNorm folded
+//     into its conv (seg_bn_fold_batch; the convs then apply bias + activation in
+//     their epilogues: seg_conv_igemm_act, seg_dw_fwd_bias_act);
+//   overlay_predictions' torch.max(prediction, dim=1) + cv2.resize(...,
+//     INTER_NEAREST) back to the frame size (inference.py:64-70) fused with the
+//     model's final align_corners=True upsample (src/unet.py:30,49) ->
+//     seg_argmax_nearest writes the uint8 class mask at frame resolution; the
+//     full-resolution logits are never stored.
+//
+// cv2 is not installed in this image, so the resize arithmetic is a restatement
+// of OpenCV's published INTER_LINEAR 8-bit path (imgproc/src/resize.cpp):
+//   x: fx = float((dx+0.5)*scale_x - 0.5), sx = floor(fx), fx -= sx; sx < 0 ->
+//      (sx, fx) = (0, 0); sx >= W-1 -> (W-1, 0); alpha = round((1-fx)*2048),
+//      round(fx*2048) (cvRound: half to even)
+//   y: same fy/sy without clamping; source rows clip(sy, 0, H-1), clip(sy+1, ...)
+//   horizontal: D = S[sx]*a0 + S[sx+1]*a1                      (int32, exact)
+//   vertical (VResizeLinearVec_32s8u, the SIMD path every full row takes):
+//      out = sat_u8((((D0 >> 4) * b0 >> 16) + ((D1 >> 4) * b1 >> 16) + 2) >> 2)
+// and INTER_NEAREST: sx = min(floor(x * (1 / (dst_w / src_w))), src_w - 1) in
+// double.  Parity of these two against real cv2 is unpinned (oracle/cvresize.py
+// restates the same arithmetic; tests pin kernel == restatement bit-exactly).
+#include "common.h"
+
+namespace {
+
+// ---------------------------------------------------------------- BN folding
+struct SegFoldJob {
+  const float* w;      // conv weight [Cout][kper]
+  const float* bias;   // conv bias [Cout] or null
+  const float* gamma;  // BN weight/bias/running stats [Cout] (gamma null: no BN -> copy)
+  const float* beta;
+  const float* rm;
+  const float* rv;
+  float* w_out;        // [Cout][kper]
+  float* b_out;        // [Cout] (padded to a multiple of 4 by the caller; pad left untouched)
+  int cout, kper;
+  float eps;
+  int pad_;
+};
+static_assert(sizeof(SegFoldJob) == 80, "seg_fold_job ABI");
+
+// w' = w * g/sqrt(rv+eps); b' = b * g/sqrt(rv+eps) + (beta - rm*g/sqrt(rv+eps)): the
+// eval BatchNorm y*scale + shift of seg_bn_eval_coef pushed through the conv.
+__global__ __launch_bounds__(256) void fold_batch_kernel(const SegFoldJob* __restrict__ jobs) {
+  const SegFoldJob j = jobs[blockIdx.y];
+  const long total = (long)j.cout * j.kper;
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < total + j.cout; i += (long)gridDim.x * 256) {
+    const int co = i < total ? (int)(i / j.kper) : (int)(i - total);
+    float scale = 1.f, shift = 0.f;
+    if (j.gamma) {
+      const float inv = 1.f / sqrtf(j.rv[co] + j.eps);
+      const float g = j.gamma[co];
+      scale = g * inv;
+      shift = j.beta[co] - j.rm[co] * g * inv;
+    }
+    if (i < total) {
+      j.w_out[i] = j.gamma ? j.w[i] * scale : j.w[i];
+    } else {
+      const float b = j.bias ? j.bias[co] : 0.f;
+      j.b_out[co] = j.gamma ? b * scale + shift : b;
+    }
+  }
+}
+
+// ---------------------------------------------------------------- preprocess
+__global__ __launch_bounds__(256) void preprocess_bgr_kernel(const uint8_t* __restrict__ frame, long row_bytes,
+                                                             long frame_bytes, int N, int Hf, int Wf,
+                                                             float* __restrict__ out, int ld, int H, int W,
+                                                             double scale_x, double scale_y, float m0, float m1,
+                                                             float m2, float s0, float s1, float s2) {
+#pragma clang fp contract(off)  // OpenCV computes (dx+0.5)*scale-0.5 as a separate multiply and subtract
+  const long total = (long)N * H * W;
+  for (long p = blockIdx.x * 256L + threadIdx.x; p < total; p += (long)gridDim.x * 256) {
+    const int n = (int)(p / ((long)H * W));
+    const int rem = (int)(p - (long)n * H * W);
+    const int dy = rem / W, dx = rem - dy * W;
+    // x taps and fixed-point weights
+    float fx = (float)((dx + 0.5) * scale_x - 0.5);
+    int sx = (int)floorf(fx);
+    fx -= (float)sx;
+    if (sx < 0) { sx = 0; fx = 0.f; }
+    if (sx >= Wf - 1) { sx = Wf - 1; fx = 0.f; }
+    const int a0 = (int)rintf((1.f - fx) * 2048.f), a1 = (int)rintf(fx * 2048.f);
+    const int sx1 = sx + 1 < Wf ? sx + 1 : Wf - 1;  // a1 == 0 whenever sx + 1 is outside
+    // y taps (weights from the unclamped fy; rows clipped)
+    float fy = (float)((dy + 0.5) * scale_y - 0.5);
+    const int sy = (int)floorf(fy);
+    fy -= (float)sy;
+    const int b0 = (int)rintf((1.f - fy) * 2048.f), b1 = (int)rintf(fy * 2048.f);
+    const int y0 = sy < 0 ? 0 : (sy >= Hf ? Hf - 1 : sy);
+    const int y1 = sy + 1 < 0 ? 0 : (sy + 1 >= Hf ? Hf - 1 : sy + 1);
+    const uint8_t* r0 = frame + n * frame_bytes + (long)y0 * row_bytes;
+    const uint8_t* r1 = frame + n * frame_bytes + (long)y1 * row_bytes;
+    float v[3];
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      const int d0 = r0[sx * 3 + c] * a0 + r0[sx1 * 3 + c] * a1;
+      const int d1 = r1[sx * 3 + c] * a0 + r1[sx1 * 3 + c] * a1;
+      int t = (((d0 >> 4) * b0) >> 16) + (((d1 >> 4) * b1) >> 16);
+      t = (t + 2) >> 2;
+      const int u = t < 0 ? 0 : (t > 255 ? 255 : t);
+      v[c] = (float)u / 255.f;  // transforms.ToTensor (float32 division)
+    }
+    // BGR -> RGB, then transforms.Normalize: (x - mean) / std
+    f32x4 o;
+    o[0] = (v[2] - m0) / s0;
+    o[1] = (v[1] - m1) / s1;
+    o[2] = (v[0] - m2) / s2;
+    o[3] = 0.f;
+    st4(out + p * ld, o);
+  }
+}
+
+// ---------------------------------------------------------------- argmax + nearest
+// mask[n][yf][xf] = argmax_c logits(n, c, ym, xm), (ym, xm) = nearest model pixel of
+// frame pixel (yf, xf); logits = align_corners=True bilinear of the low-res logits.
+__global__ __launch_bounds__(256) void argmax_nearest_kernel(const float* __restrict__ low, long ld, int N, int H,
+                                                             int W, int C, int Hm, int Wm, float sh, float sw,
+                                                             uint8_t* __restrict__ mask, int Hf, int Wf,
+                                                             double ify, double ifx) {
+  const long total = (long)N * Hf * Wf;
+  for (long p = blockIdx.x * 256L + threadIdx.x; p < total; p += (long)gridDim.x * 256) {
+    const int n = (int)(p / ((long)Hf * Wf));
+    const int rem = (int)(p - (long)n * Hf * Wf);
+    const int yf = rem / Wf, xf = rem - yf * Wf;
+    int ym = (int)floor((double)yf * ify), xm = (int)floor((double)xf * ifx);
+    ym = ym < Hm - 1 ? ym : Hm - 1;
+    xm = xm < Wm - 1 ? xm : Wm - 1;
+    const Lin lh = lin_index(ym, H, sh, 1), lw = lin_index(xm, W, sw, 1);
+    const float* base = low + (long)n * H * W * ld;
+    float best = 0.f;
+    int arg = 0;
+    bool done = false;
+    for (int c = 0; c < C && !done; c += 4) {
+      const f32x4 v00 = ld4(base + ((long)lh.i0 * W + lw.i0) * ld + c);
+      const f32x4 v01 = ld4(base + ((long)lh.i0 * W + lw.i1) * ld + c);
+      const f32x4 v10 = ld4(base + ((long)lh.i1 * W + lw.i0) * ld + c);
+      const f32x4 v11 = ld4(base + ((long)lh.i1 * W + lw.i1) * ld + c);
+      const f32x4 o = bilerp4(v00, v01, v10, v11, lh, lw);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int k = c + j;
+        if (k >= C || done) continue;
+        const float v = o[j];
+        // aten max(dim) on CPU: first maximum wins, a NaN wins and stops the scan
+        if (k == 0 || !(v <= best)) {
+          best = v;
+          arg = k;
+          if (isnan(v)) done = true;
+        }
+      }
+    }
+    mask[p] = (uint8_t)arg;
+  }
+}
+
+int grid_for(long total) { return (int)std::min<long>(seg_cdiv(total, 256), 8192); }
+
+}  // namespace
+
+// Fold every eval BatchNorm of a model into its conv in ONE launch.  `jobs` is a
+// DEVICE array of njobs seg_fold_job; max_elems = the largest Cout*kper + Cout.
+SEG_API int seg_bn_fold_batch(const void* jobs, int njobs, long max_elems, hipStream_t stream) {
+  if (njobs < 0 || max_elems < 0) return (int)hipErrorInvalidValue;
+  if (njobs == 0) return 0;
+  const int bx = (int)std::max<long>(1, std::min<long>(seg_cdiv(max_elems, 256), 64));
+  hipLaunchKernelGGL(fold_batch_kernel, dim3(bx, njobs), dim3(256), 0, stream,
+                     reinterpret_cast<const SegFoldJob*>(jobs));
+  SEG_RET_LAST();
+}
+
+// N uint8 BGR frames [N][Hf][row_bytes] (3 bytes per pixel) -> normalised RGB NHWC
+// rows out[N*H*W][ld] (channel 3 zeroed).  mean/std: transforms.Normalize's
+// per-channel constants in RGB order (inference.py:35-36).
+SEG_API int seg_preprocess_bgr(const uint8_t* frame, int N, int Hf, int Wf, long row_bytes, float* out, int ld, int H,
+                               int W, float mean_r, float mean_g, float mean_b, float std_r, float std_g, float std_b,
+                               hipStream_t stream) {
+  if (ld < 4 || (ld & 3) || row_bytes < 3L * Wf || Hf <= 0 || Wf <= 0 || H <= 0 || W <= 0) return (int)hipErrorInvalidValue;
+  const double scale_x = 1.0 / ((double)W / Wf), scale_y = 1.0 / ((double)H / Hf);
+  hipLaunchKernelGGL(preprocess_bgr_kernel, dim3(grid_for((long)N * H * W)), dim3(256), 0, stream, frame, row_bytes,
+                     row_bytes * Hf, N, Hf, Wf, out, ld, H, W, scale_x, scale_y, mean_r, mean_g, mean_b, std_r, std_g,
+                     std_b);
+  SEG_RET_LAST();
+}
+
+// Class mask at frame resolution from the low-res NHWC logits [N*H*W][ld]: the
+// model output is their align_corners=True upsample to Hm x Wm (src/unet.py:49),
+// torch.max(dim=1) picks the class (inference.py:64) and cv2 INTER_NEAREST maps
+// it to Hf x Wf (inference.py:68-70).
+SEG_API int seg_argmax_nearest(const float* low, long ld, int N, int H, int W, int C, int Hm, int Wm, uint8_t* mask,
+                               int Hf, int Wf, hipStream_t stream) {
+  if ((ld & 3) || ld < C || C <= 0 || C > 255 || Hm <= 0 || Wm <= 0 || Hf <= 0 || Wf <= 0) return (int)hipErrorInvalidValue;
+  const float sh = Hm > 1 ? (float)(H - 1) / (float)(Hm - 1) : 0.f;
+  const float sw = Wm > 1 ? (float)(W - 1) / (float)(Wm - 1) : 0.f;
+  const double ify = 1.0 / ((double)Hf / Hm), ifx = 1.0 / ((double)Wf / Wm);
+  hipLaunchKernelGGL(argmax_nearest_kernel, dim3(grid_for((long)N * Hf * Wf)), dim3(256), 0, stream, low, ld, N, H, W,
+                     C, Hm, Wm, sh, sw, mask, Hf, Wf, ify, ifx);
+  SEG_RET_LAST();
+}

@@ -19,23 +19,6 @@
 
 namespace {
 
-struct Lin {
-  int i0, i1;
-  float l0, l1;
-};
-
-__device__ __forceinline__ Lin lin_index(int dst, int in, float scale, int ac) {
-  float src = ac ? scale * (float)dst : fmaxf(scale * ((float)dst + 0.5f) - 0.5f, 0.f);
-  int i0 = (int)floorf(src);
-  if (i0 > in - 1) i0 = in - 1;
-  Lin r;
-  r.i0 = i0;
-  r.i1 = i0 + (i0 < in - 1 ? 1 : 0);
-  r.l1 = fminf(fmaxf(src - (float)i0, 0.f), 1.f);
-  r.l0 = 1.f - r.l1;
-  return r;
-}
-
 // Weight with which output index `dst` samples input index `i`.
 __device__ __forceinline__ float lin_weight(int dst, int i, int in, float scale, int ac) {
   const Lin l = lin_index(dst, in, scale, ac);
@@ -148,7 +131,7 @@ __global__ void up_fwd_to_nchw_kernel(const float* __restrict__ in, long ldin, i
       const f32x4 v01 = ld4(base + ((long)lh.i0 * W + lw.i1) * ldin + c);
       const f32x4 v10 = ld4(base + ((long)lh.i1 * W + lw.i0) * ldin + c);
       const f32x4 v11 = ld4(base + ((long)lh.i1 * W + lw.i1) * ldin + c);
-      const f32x4 o = lh.l0 * (lw.l0 * v00 + lw.l1 * v01) + lh.l1 * (lw.l0 * v10 + lw.l1 * v11);
+      const f32x4 o = bilerp4(v00, v01, v10, v11, lh, lw);
 #pragma unroll
       for (int j = 0; j < 4; ++j)
         if (c + j < C) out[(((long)n * C + c + j) * Ho + r) * Wo + s] = o[j];

@@ -20,6 +20,9 @@ _F = ctypes.c_float
 # name -> (restype, argtypes); mirrors include/segamd.h one-to-one.
 PROTOTYPES = {
     "seg_conv_igemm": (_I, [_V, _L, _I, _I, _I, _I, _V, _I, _V, _V, _L, _I, _I, _I, _I, _I, _I, _V, _L, _V, _V]),
+    "seg_conv_igemm_act": (_I, [_V, _L, _I, _I, _I, _I, _V, _I, _V, _V, _L, _I, _I, _I, _I, _I, _I, _V, _L, _V, _I,
+                                _V, _I, _V]),
+    "seg_conv_igemm_splits": (_I, [_L, _I, _I, _I]),
     "seg_igemm_force_tile": (_I, [_I]),
     "seg_pack_batch": (_I, [_V, _I, _L, _V]),
     "seg_conv_igemm_row_tiles": (_I, [_L, _I, _V]),
@@ -29,6 +32,7 @@ PROTOTYPES = {
     "seg_conv_wgrad_reduce": (_I, [_V, _I, _V, _I, _I, _I, _I, _I, _V]),
     "seg_pack_dw_weight": (_I, [_V, _V, _I, _V]),
     "seg_dw_fwd": (_I, [_V, _L, _I, _I, _I, _I, _V, _V, _I, _V, _V, _L, _I, _I, _I, _V]),
+    "seg_dw_fwd_bias_act": (_I, [_V, _L, _I, _I, _I, _I, _V, _V, _I, _V, _L, _I, _I, _I, _V]),
     "seg_dw_dgrad": (_I, [_V, _L, _I, _I, _I, _I, _V, _V, _L, _I, _I, _I, _I, _V]),
     "seg_dw_wgrad_blocks": (_L, [_I, _I, _I, _I]),
     "seg_dw_wgrad": (_I, [_V, _L, _V, _L, _I, _I, _I, _I, _V, _V, _I, _I, _I, _I, _V, _V]),
@@ -50,6 +54,9 @@ PROTOTYPES = {
     "seg_ce_workspace_floats": (_L, [_L]),
     "seg_ce_upsample_loss": (_I, [_V, _L, _I, _I, _I, _I, _V, _I, _I, _I, _V, _V, _V]),
     "seg_ce_upsample_grad": (_I, [_V, _L, _I, _I, _I, _I, _V, _I, _I, _I, _V, _V, _V, _L, _V]),
+    "seg_bn_fold_batch": (_I, [_V, _I, _L, _V]),
+    "seg_preprocess_bgr": (_I, [_V, _I, _I, _I, _L, _V, _I, _I, _I, _F, _F, _F, _F, _F, _F, _V]),
+    "seg_argmax_nearest": (_I, [_V, _L, _I, _I, _I, _I, _I, _I, _V, _I, _I, _V]),
 }
 
 _lock = threading.Lock()

@@ -102,6 +102,8 @@ class ConvOp:
         # weight as is), data gradient [Cin][ldk_d]; depthwise: wk_f = [9][C]
         self.wk_f = self.wk_d = None
         self.ldk_f = self.ldk_d = 0
+        # BN-folded inference weights (Program.fold): fk [Cout][Cin/g][ks][ks], fb [r4(Cout)], fk_pack
+        self.fk = self.fb = self.fk_pack = None
         self.ks = conv.kernel_size[0]
         self.stride = conv.stride[0]
         self.pad = conv.padding[0]
@@ -174,6 +176,30 @@ class ConvOp:
         o, r = self.out, self.res
         call("seg_bn_apply", rt.ptr(y), y.ld, M, C, scale.data_ptr(), shift.data_ptr(), self.act,
              rt.ptr(r) if r is not None else None, r.ld if r is not None else 0, rt.ptr(o), o.ld, s)
+
+    # -- inference (BatchNorm folded into the conv: Program.fold)
+    def forward_folded(self, rt):
+        """act(conv(x, W') + b') (+ residual) in one launch; W', b' from seg_bn_fold_batch.
+        A lazy producer writes its activated output into its `y` buffer (= `out`), so its
+        depthwise consumer reads it without the on-load BN transform."""
+        s, i, o = rt.stream, self.inp, self.out
+        act = self.act if self.bn is not None else ACT_NONE
+        if self.kind == "dw":
+            call("seg_dw_fwd_bias_act", rt.ptr(i), i.ld, i.N, i.H, i.W, i.C, self.fk_pack.data_ptr(),
+                 self.fb.data_ptr(), act, rt.ptr(o), o.ld, o.H, o.W, self.stride, s)
+            return
+        if self.fk_pack is None:
+            ldk, wk = self.cin, self.fk.data_ptr()
+        else:
+            ldk, wk = self.ldk_f, self.fk_pack.data_ptr()
+        r = self.res
+        bias = self.fb.data_ptr() if self.fb is not None else None
+        M = o.N * o.H * o.W
+        splits = query("seg_conv_igemm_splits", M, self.cout, self.cin_pad, self.ks)
+        work = rt.tmp(splits * M * self.cout) if splits > 1 else None
+        call("seg_conv_igemm_act", rt.ptr(i), i.ld, i.N, i.H, i.W, self.cin_pad, wk, ldk, bias, rt.ptr(o), o.ld,
+             o.H, o.W, self.cout, self.ks, self.stride, self.pad, rt.ptr(r) if r is not None else None,
+             r.ld if r is not None else 0, None, act, work.data_ptr() if work is not None else None, splits, s)
 
     def _in_xform(self, rt):
         """(scale, shift, act) of the producer's lazy BN for this op's input loads, or (None, None, 0)."""
@@ -371,6 +397,65 @@ class Program:
         table = np.array(jobs, dtype=jt)
         self._jobs = torch.from_numpy(table.view(np.uint8).copy()).to(convs[0].conv.weight.device)
         self._njobs, self._max_elems, self._pack_key = len(jobs), max_elems, key
+
+    def fold(self, stream):
+        """Eval: fold every BatchNorm into its conv (one seg_bn_fold_batch launch) and
+        pack the folded weights (one seg_pack_batch launch).  Buffers and job tables
+        are built once per weight storage; re-run after the weights or running
+        statistics change (Predictor.refresh)."""
+        convs = [op for op in self.ops if isinstance(op, ConvOp)]
+        key = tuple(op.conv.weight.data_ptr() for op in convs)
+        if getattr(self, "_fold_key", None) != key:
+            self._build_fold(convs, key)
+        call("seg_bn_fold_batch", self._fjobs.data_ptr(), len(convs), self._fmax, stream)
+        if self._fpjobs is not None:
+            call("seg_pack_batch", self._fpjobs.data_ptr(), self._fpn, self._fpmax, stream)
+
+    def _build_fold(self, convs, key):
+        import numpy as np
+        ft = np.dtype([("w", "<u8"), ("bias", "<u8"), ("gamma", "<u8"), ("beta", "<u8"), ("rm", "<u8"),
+                       ("rv", "<u8"), ("w_out", "<u8"), ("b_out", "<u8"), ("cout", "<i4"), ("kper", "<i4"),
+                       ("eps", "<f4"), ("pad", "<i4")])
+        assert ft.itemsize == 80
+        pt = np.dtype([("w", "<u8"), ("wk", "<u8"), ("cout", "<i4"), ("cin", "<i4"), ("ks", "<i4"),
+                       ("ldk", "<i4"), ("mode", "<i4"), ("kin", "<i4")])
+        fjobs, pjobs, fmax, pmax = [], [], 0, 0
+        for op in convs:
+            w, b, bn = op.conv.weight, op.conv.bias, op.bn
+            dev = w.device
+            kper = w[0].numel()
+            op.fk = torch.empty_like(w, memory_format=torch.contiguous_format)
+            op.fb = torch.zeros(r4(op.cout), device=dev, dtype=torch.float32)
+            if bn is not None and not (bn.track_running_stats and bn.running_mean is not None):
+                raise NotImplementedError("eval BatchNorm2d without running statistics")
+            ptr = (lambda t: t.data_ptr() if t is not None else 0)
+            fjobs.append((w.data_ptr(), ptr(b), ptr(bn.weight) if bn is not None else 0,
+                          ptr(bn.bias) if bn is not None else 0, ptr(bn.running_mean) if bn is not None else 0,
+                          ptr(bn.running_var) if bn is not None else 0, op.fk.data_ptr(), op.fb.data_ptr(),
+                          op.cout, kper, bn.eps if bn is not None else 0.0, 0))
+            if bn is not None and (bn.weight is None or bn.bias is None):
+                raise NotImplementedError("BatchNorm2d(affine=False) folding")
+            fmax = max(fmax, op.cout * kper + op.cout)
+            if op.kind == "dw":
+                op.fk_pack = torch.empty(9 * op.cout, device=dev, dtype=torch.float32)
+                pjobs.append((op.fk.data_ptr(), op.fk_pack.data_ptr(), op.cout, 1, 3, 9, 2, 1))
+                pmax = max(pmax, 9 * op.cout)
+            elif op.ks == 1 and op.cin_pad == op.cin:
+                op.fk_pack = None
+            else:
+                op.ldk_f = r4(op.ks * op.ks * op.cin_pad)
+                op.fk_pack = torch.empty(op.cout * op.ldk_f, device=dev, dtype=torch.float32)
+                pjobs.append((op.fk.data_ptr(), op.fk_pack.data_ptr(), op.cout, op.cin, op.ks, op.ldk_f, 0,
+                              op.cin_pad))
+                pmax = max(pmax, op.cout * op.ldk_f)
+        dev = convs[0].conv.weight.device
+        self._fjobs = torch.from_numpy(np.array(fjobs, dtype=ft).view(np.uint8).copy()).to(dev)
+        self._fmax = fmax
+        if pjobs:
+            self._fpjobs = torch.from_numpy(np.array(pjobs, dtype=pt).view(np.uint8).copy()).to(dev)
+        else:
+            self._fpjobs = None
+        self._fpn, self._fpmax, self._fold_key = len(pjobs), pmax, key
 
     def params(self):
         seen, ps = set(), []
@@ -633,6 +718,15 @@ class Run:
             op.forward(self)
         if DEBUG_KEEP_RUN:
             LAST_RUN = self
+
+    def forward_folded(self):
+        """Eval forward with every BatchNorm folded (Program.fold must have run): one
+        launch per conv.  The NHWC4 input rows must already be in the image buffer."""
+        for op in self.prog.ops:
+            if isinstance(op, ConvOp):
+                op.forward_folded(self)
+            else:
+                op.forward(self)
 
     def backward_from_logits(self):
         global LAST_RUN

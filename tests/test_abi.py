@@ -13,7 +13,7 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 HEADER = os.path.join(REPO, "include", "segamd.h")
 
 CTYPE = {"const float*": ctypes.c_void_p, "float*": ctypes.c_void_p, "const long long*": ctypes.c_void_p,
-         "long long*": ctypes.c_void_p, "int*": ctypes.c_void_p, "const void*": ctypes.c_void_p, "hipStream_t": ctypes.c_void_p, "long": ctypes.c_long,
+         "long long*": ctypes.c_void_p, "int*": ctypes.c_void_p, "const void*": ctypes.c_void_p, "const unsigned char*": ctypes.c_void_p, "unsigned char*": ctypes.c_void_p, "hipStream_t": ctypes.c_void_p, "long": ctypes.c_long,
          "int": ctypes.c_int, "float": ctypes.c_float}
 
 
@@ -61,6 +61,9 @@ def test_host_side_queries(lib):
     assert _lib.query("seg_chan_workspace_floats", 1 << 20, 96) >= 2 * 96
     assert _lib.query("seg_dw_wgrad_blocks", 32, 128, 256, 32) >= 1
     assert _lib.query("seg_ce_workspace_floats", 4 * 256 * 512) >= 2
+    # split-K only when the output tiles cannot fill the chip
+    assert _lib.query("seg_conv_igemm_splits", 32 * 128 * 256, 32, 80, 3) == 1
+    assert _lib.query("seg_conv_igemm_splits", 8 * 16, 256, 1344, 3) > 1
 
 
 def test_argument_validation_without_gpu(lib):
@@ -71,3 +74,10 @@ def test_argument_validation_without_gpu(lib):
     assert rc == 1  # ld < C
     rc = lib.seg_conv_wgrad_reduce(None, 1, None, 4, 4, 3, 2, 0, None)
     assert rc == 1  # unknown mode
+    rc = lib.seg_conv_igemm_act(None, 4, 1, 4, 4, 4, None, 36, None, None, 4, 4, 4, 8, 3, 1, 1, None, 0, None, 3, None, 1,
+                                None)
+    assert rc == 1  # unknown activation
+    rc = lib.seg_preprocess_bgr(None, 1, 720, 1280, 1280, None, 4, 128, 256, 0, 0, 0, 1, 1, 1, None)
+    assert rc == 1  # row_bytes < 3 * Wf
+    rc = lib.seg_argmax_nearest(None, 10, 1, 64, 128, 10, 128, 256, None, 720, 1280, None)
+    assert rc == 1  # ld not a multiple of 4

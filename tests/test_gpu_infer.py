@@ -1,0 +1,120 @@
+"""GPU: the inference path (inference.py:28-46, 162-163, 64-70; config 4) against
+the CPU oracle on identical inputs.
+
+  * seg_preprocess_bgr == oracle/cvresize.preprocess_image, bit for bit (the
+    restated cv2 INTER_LINEAR + ToTensor + Normalize arithmetic; parity with real
+    cv2 is unpinned: cv2 is not installed);
+  * the BN-folded eval forward (Predictor) vs the oracle's eval forward of the
+    same image: relative L2 <= 1e-3 (BASELINE north_star fp32 tolerance);
+  * the uint8 class mask vs oracle argmax + INTER_NEAREST: identical wherever the
+    oracle's top-2 logit margin exceeds 1e-3 (folding reorders fp32 rounding, so
+    exact near-ties may flip), and >= 99.9 % identical overall;
+  * HIP-graph replay == eager launches, bitwise; refresh() follows new weights.
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import cvresize, segref
+from seg_amd import MobileNetV2UNet, UNet, deterministic_init
+from seg_amd.infer import Predictor, preprocess_image
+from seg_amd._lib import call
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def frame(h, w, seed):
+    g = np.random.Generator(np.random.PCG64(seed))
+    # smooth-ish content (like a video frame) plus noise, full 0..255 range
+    yy, xx = np.meshgrid(np.linspace(0, 6, h), np.linspace(0, 9, w), indexing="ij")
+    base = 127.5 + 100 * np.sin(yy)[..., None] * np.cos(xx[..., None] + np.arange(3))
+    return np.clip(base + g.normal(0, 25, (h, w, 3)), 0, 255).astype(np.uint8)
+
+
+@pytest.mark.parametrize("fh,fw,h,w", [(720, 1280, 128, 256), (37, 53, 16, 32), (100, 80, 128, 256),
+                                       (480, 640, 64, 128)])
+def test_preprocess_bitexact(fh, fw, h, w):
+    f = frame(fh, fw, seed=fh + fw)
+    ref, _ = cvresize.preprocess_image(f, (w, h))
+    fd = torch.from_numpy(f).to(DEV)
+    rows = torch.full((h * w, 4), float("nan"), device=DEV)
+    call("seg_preprocess_bgr", fd.data_ptr(), 1, fh, fw, fd.stride(0), rows.data_ptr(), 4, h, w,
+         *cvresize.MEAN, *cvresize.STD, torch.cuda.current_stream().cuda_stream)
+    got = rows.cpu().numpy().reshape(h, w, 4)
+    assert np.all(got[..., 3] == 0)
+    np.testing.assert_array_equal(got[..., :3].transpose(2, 0, 1)[None], ref)
+    img, _ = preprocess_image(f, (w, h))
+    np.testing.assert_array_equal(img.cpu().numpy(), ref)
+
+
+def _oracle_logits(model, f, size):
+    x, _ = cvresize.preprocess_image(f, size)
+    p = segref.canonical_state(model.state_dict(), torch.float64)
+    arch = type(model).__name__
+    with torch.no_grad():
+        return segref.FORWARDS[arch](p, torch.from_numpy(x).double(), False).numpy()
+
+
+@pytest.mark.parametrize("arch", ["MobileNetV2UNet", "UNet"])
+def test_predictor_matches_oracle(arch):
+    size = (256, 128) if arch == "MobileNetV2UNet" else (64, 32)
+    fh, fw = (720, 1280) if arch == "MobileNetV2UNet" else (90, 160)
+    cpu = MobileNetV2UNet(10) if arch == "MobileNetV2UNet" else UNet(10, 16)
+    deterministic_init(cpu, seed=11, random_running_stats=True)
+    model = (MobileNetV2UNet(10) if arch == "MobileNetV2UNet" else UNet(10, 16)).to(DEV)
+    model.load_state_dict(cpu.state_dict())
+    pred = Predictor(model, frame_hw=(fh, fw), target_size=size, graph=True)
+    f = frame(fh, fw, seed=3)
+    mask = pred(f).cpu().numpy()
+    got = pred.logits().double().cpu().numpy()
+    ref = _oracle_logits(cpu, f, size)
+    rel = np.linalg.norm(got - ref) / np.linalg.norm(ref)
+    assert rel < 1e-3, rel
+    ref_mask = cvresize.class_mask(ref, (fh, fw))
+    top2 = np.sort(ref[0], axis=0)[-2:]
+    margin = cvresize.resize_nearest((top2[1] - top2[0]).astype(np.float64), (fw, fh))
+    scale = np.abs(ref).max()
+    confident = margin > 1e-3 * scale
+    assert np.array_equal(mask[confident], ref_mask[confident])
+    assert (mask == ref_mask).mean() >= 0.999
+    # the GPU's own logits give exactly its mask (argmax + nearest are exact ops)
+    np.testing.assert_array_equal(mask, cvresize.class_mask(pred.logits().cpu().numpy(), (fh, fw)))
+
+
+def test_graph_equals_eager_and_refresh():
+    torch.manual_seed(0)
+    model = deterministic_init(MobileNetV2UNet(10), seed=5, random_running_stats=True).to(DEV)
+    g = Predictor(model, frame_hw=(360, 640), graph=True)
+    e = Predictor(model, frame_hw=(360, 640), graph=False)
+    for s in range(3):
+        f = frame(360, 640, seed=100 + s)
+        mg = g(f).clone()
+        lg = g.logits()
+        me = e(f).clone()
+        le = e.logits()
+        assert torch.equal(mg, me)
+        assert torch.equal(lg, le)
+    # new weights: stale until refresh(), then identical to a fresh predictor
+    before = g.logits().clone()
+    deterministic_init(model, seed=6, random_running_stats=True)
+    g.refresh()
+    g.step()
+    fresh = Predictor(model, frame_hw=(360, 640), graph=False)
+    fresh(f)
+    assert torch.equal(g.logits(), fresh.logits())
+    assert not torch.equal(g.logits(), before)
+
+
+def test_eager_eval_forward_agrees_with_folded():
+    """model.eval()(x) (unfolded BN apply path) vs the folded Predictor on the same input."""
+    model = deterministic_init(MobileNetV2UNet(10), seed=9, random_running_stats=True).to(DEV).eval()
+    f = frame(256, 512, seed=4)
+    pred = Predictor(model, frame_hw=(256, 512), graph=False)
+    pred(f)
+    img, _ = preprocess_image(f)
+    with torch.no_grad():
+        ref = model(img)
+    got = pred.logits()
+    rel = float((got - ref).norm() / ref.norm())
+    assert rel < 1e-4, rel  # folding reorders fp32 rounding; the oracle test bounds both at 1e-3

@@ -341,3 +341,66 @@ def test_colsum_and_add():
     o = torch.empty(M, 16, device=DEV)
     call("seg_add", a.data_ptr(), 16, b.data_ptr(), 16, M, 16, o.data_ptr(), 16, s)
     assert torch.equal(o, a + b)
+
+
+@pytest.mark.parametrize("act", [0, 1, 2])
+@pytest.mark.parametrize("N,Cin,Cout,H,W,ks,res", [(1, 1344, 256, 8, 16, 3, False), (1, 288, 128, 16, 32, 3, False),
+                                                   (1, 960, 320, 8, 16, 1, False), (1, 96, 96, 4, 4, 1, True),
+                                                   (2, 80, 32, 9, 11, 3, False)])
+def test_conv_igemm_act_splitk(N, Cin, Cout, H, W, ks, res, act):
+    """seg_conv_igemm_act: act(conv + bias + add), unsplit and split-K (the inference path)."""
+    pad = ks // 2
+    x = gen(N, Cin, H, W, seed=11)
+    w = gen(Cout, Cin, ks, ks, seed=12) * (2.0 / (Cin * ks * ks)) ** 0.5
+    b = gen(Cout, seed=13)
+    add = gen(N, Cout, H, W, seed=14) if res else None
+    z = F.conv2d(x, w, b, padding=pad) + (add if res else 0)
+    ref = {0: z, 1: F.relu(z), 2: F.hardtanh(z, 0.0, 6.0)}[act]
+    s = S()
+    xg, wg, bg = nhwc(x), w.to(DEV), b.to(DEV)
+    ldk = r4(ks * ks * Cin)
+    wk = torch.empty(Cout * ldk, device=DEV)
+    call("seg_pack_conv_weight", wg.data_ptr(), wk.data_ptr(), Cout, Cin, ks, ldk, 0, Cin, s)
+    addg = nhwc(add) if res else None
+    M = N * H * W
+    auto = query("seg_conv_igemm_splits", M, Cout, Cin, ks)
+    outs = []
+    for splits in sorted({1, auto, 3}):
+        out = torch.full((M, r4(Cout)), float("nan"), device=DEV)
+        work = torch.empty(max(splits * M * Cout, 1), device=DEV)
+        call("seg_conv_igemm_act", xg.data_ptr(), xg.shape[1], N, H, W, Cin, wk.data_ptr(), ldk, bg.data_ptr(),
+             out.data_ptr(), out.shape[1], H, W, Cout, ks, 1, pad, addg.data_ptr() if res else None,
+             addg.shape[1] if res else 0, None, act, work.data_ptr(), splits, s)
+        assert rel(from_nhwc(out, N, Cout, H, W), ref) < 1e-5, splits
+        outs.append(out)
+
+
+@pytest.mark.parametrize("stride", [1, 2])
+def test_dw_bias_act_and_bn_fold(stride):
+    """seg_bn_fold_batch + seg_dw_fwd_bias_act == eval BN(dwconv) + ReLU6; igemm fold likewise."""
+    import numpy as np
+    N, C, H, W = 2, 96, 10, 14
+    x = gen(N, C, H, W, seed=21)
+    w = gen(C, 1, 3, 3, seed=22) * 0.3
+    g, bta = gen(C, seed=23).abs() + 0.5, gen(C, seed=24)
+    rm, rv = gen(C, seed=25) * 0.1, gen(C, seed=26).abs() + 0.5
+    ref = F.hardtanh(F.batch_norm(F.conv2d(x, w, None, stride=stride, padding=1, groups=C), rm, rv, g, bta, False,
+                                  0.1, 1e-5), 0.0, 6.0)
+    wg, gg, bg, rmg, rvg = (t.to(DEV) for t in (w, g, bta, rm, rv))
+    fk = torch.empty_like(wg)
+    fb = torch.zeros(C, device=DEV)
+    ft = np.dtype([("w", "<u8"), ("bias", "<u8"), ("gamma", "<u8"), ("beta", "<u8"), ("rm", "<u8"), ("rv", "<u8"),
+                   ("w_out", "<u8"), ("b_out", "<u8"), ("cout", "<i4"), ("kper", "<i4"), ("eps", "<f4"),
+                   ("pad", "<i4")])
+    job = np.array([(wg.data_ptr(), 0, gg.data_ptr(), bg.data_ptr(), rmg.data_ptr(), rvg.data_ptr(), fk.data_ptr(),
+                     fb.data_ptr(), C, 9, 1e-5, 0)], dtype=ft)
+    jobs = torch.from_numpy(job.view(np.uint8).copy()).to(DEV)
+    call("seg_bn_fold_batch", jobs.data_ptr(), 1, C * 9 + C, S())
+    wk = torch.empty(9 * C, device=DEV)
+    call("seg_pack_dw_weight", fk.data_ptr(), wk.data_ptr(), C, S())
+    Ho, Wo = (H - 1) // stride + 1, (W - 1) // stride + 1
+    xg = nhwc(x)
+    out = torch.full((N * Ho * Wo, C), float("nan"), device=DEV)
+    call("seg_dw_fwd_bias_act", xg.data_ptr(), C, N, H, W, C, wk.data_ptr(), fb.data_ptr(), 2, out.data_ptr(), C,
+         Ho, Wo, stride, S())
+    assert rel(from_nhwc(out, N, C, Ho, Wo), ref) < 1e-5

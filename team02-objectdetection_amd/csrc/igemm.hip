@@ -67,15 +67,17 @@ struct IgemmArgs {
 // a few VALU ops per slot instead of the general path's per-slot tap tracking
 // and bounds arithmetic.  The general path remains for Cin < BK (the stem).
 template <int BM, int BN, int WM, int WN, int KS, int BK, bool UT>
-__global__ __launch_bounds__(256) void igemm_conv_kernel(IgemmArgs a) {
+__global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void igemm_conv_kernel(IgemmArgs a) {
+  constexpr int NT = 64 * (BM / WM) * (BN / WN);  // threads: one wave per WM x WN sub-tile (4 or 8 waves)
   constexpr int LDSR = BK + 4;        // LDS row stride (floats): conflict-free b128 reads
   constexpr int KQ = BK / 4;          // float4 groups per tile row
   constexpr int A_VEC = BM * KQ, B_VEC = BN * KQ;
-  constexpr int A_PER = (A_VEC + 255) / 256;
-  constexpr int B_PER = (B_VEC + 255) / 256;
+  constexpr int A_PER = (A_VEC + NT - 1) / NT;
+  constexpr int B_PER = (B_VEC + NT - 1) / NT;
   constexpr int MI = WM / 32, NI = WN / 32;
   constexpr int WAVES_N = BN / WN;
-  static_assert((BM / WM) * (BN / WN) == 4, "4 waves per block");
+  static_assert(NT == 256 || NT == 512, "4 or 8 waves per block");
+  static_assert(NT % KQ == 0, "uniform kq per thread");
 
   __shared__ __attribute__((aligned(16))) float As[SEG_IGEMM_STAGES][BM * LDSR];
   __shared__ __attribute__((aligned(16))) float Bs[SEG_IGEMM_STAGES][BN * LDSR];
@@ -95,7 +97,7 @@ __global__ __launch_bounds__(256) void igemm_conv_kernel(IgemmArgs a) {
   bool a_ok[A_PER];
 #pragma unroll
   for (int i = 0; i < A_PER; ++i) {
-    const int idx = tid + i * 256;
+    const int idx = tid + i * NT;
     const int row = idx / KQ, kq = idx % KQ;
     const int p = m0 + row;
     a_ok[i] = (idx < A_VEC) && (p < a.M);
@@ -132,7 +134,7 @@ __global__ __launch_bounds__(256) void igemm_conv_kernel(IgemmArgs a) {
   if (UT) {
 #pragma unroll
     for (int i = 0; i < A_PER; ++i) {
-      const int idx = tid + i * 256;
+      const int idx = tid + i * NT;
       const int row = idx / KQ;
       const int p = m0 + row;
       const bool ok = (idx < A_VEC) && (p < a.M);
@@ -157,7 +159,7 @@ __global__ __launch_bounds__(256) void igemm_conv_kernel(IgemmArgs a) {
     }
 #pragma unroll
     for (int i = 0; i < B_PER; ++i) {
-      const int idx = tid + i * 256;
+      const int idx = tid + i * NT;
       const int co = n0 + idx / KQ;
       u_bok[i] = idx < B_VEC && co < a.Cout;
       u_boff[i] = (long)(u_bok[i] ? co : 0) * a.ldk + u_kq4;
@@ -220,7 +222,7 @@ __global__ __launch_bounds__(256) void igemm_conv_kernel(IgemmArgs a) {
     }
 #pragma unroll
     for (int i = 0; i < B_PER; ++i) {
-      const int idx = tid + i * 256;
+      const int idx = tid + i * NT;
       const int row = idx / KQ, kq = idx % KQ;
       const int co = n0 + row, k = k0 + kq * 4;
       f32x4 v = {0.f, 0.f, 0.f, 0.f};
@@ -231,13 +233,13 @@ __global__ __launch_bounds__(256) void igemm_conv_kernel(IgemmArgs a) {
   auto store_tiles = [&](int buf, const f32x4 (&ra)[A_PER], const f32x4 (&rb)[B_PER]) {
 #pragma unroll
     for (int i = 0; i < A_PER; ++i) {
-      const int idx = tid + i * 256;
-      if (A_VEC % 256 == 0 || idx < A_VEC) st4(&As[buf][(idx / KQ) * LDSR + (idx % KQ) * 4], ra[i]);
+      const int idx = tid + i * NT;
+      if (A_VEC % NT == 0 || idx < A_VEC) st4(&As[buf][(idx / KQ) * LDSR + (idx % KQ) * 4], ra[i]);
     }
 #pragma unroll
     for (int i = 0; i < B_PER; ++i) {
-      const int idx = tid + i * 256;
-      if (B_VEC % 256 == 0 || idx < B_VEC) st4(&Bs[buf][(idx / KQ) * LDSR + (idx % KQ) * 4], rb[i]);
+      const int idx = tid + i * NT;
+      if (B_VEC % NT == 0 || idx < B_VEC) st4(&Bs[buf][(idx / KQ) * LDSR + (idx % KQ) * 4], rb[i]);
     }
   };
 
@@ -409,7 +411,8 @@ int launch_igemm_bk(const IgemmArgs& a, int ks, hipStream_t s) {
   const int grid = seg_cdiv(a.M, BM) * seg_cdiv(a.Cout, BN);
   const int splits = seg_cdiv(a.K, a.kchunk);
   const bool ut = SEG_IGEMM_UT && (SEG_IGEMM_UT2 ? a.Cin >= BK : a.Cin % BK == 0);
-#define SEG_IG(KS, U) hipLaunchKernelGGL((igemm_conv_kernel<BM, BN, WM, WN, KS, BK, U>), dim3(grid, splits), dim3(256), 0, s, a)
+  constexpr int NT = 64 * (BM / WM) * (BN / WN);
+#define SEG_IG(KS, U) hipLaunchKernelGGL((igemm_conv_kernel<BM, BN, WM, WN, KS, BK, U>), dim3(grid, splits), dim3(NT), 0, s, a)
   if (ks == 1) {
     if (ut) SEG_IG(1, true); else SEG_IG(1, false);
   } else {
@@ -444,9 +447,12 @@ struct TileCfg {
 constexpr TileCfg kTiles[] = {
     {128, 128, 64, 64, 1.00f}, {64, 128, 32, 64, 0.95f}, {128, 64, 64, 32, 0.95f}, {64, 64, 32, 32, 0.85f},
     {128, 96, 32, 96, 0.97f},  {128, 160, 32, 160, 0.95f}, {256, 32, 64, 32, 0.90f}, {128, 32, 32, 32, 0.92f},
+    // 8-wave (512-thread) blocks: two waves per SIMD at one block per CU
+    {128, 128, 64, 32, 0.0f}, {128, 128, 32, 64, 0.0f}, {256, 128, 64, 64, 0.0f}, {128, 256, 64, 64, 0.0f},
+    {128, 64, 32, 32, 0.0f}, {256, 64, 64, 32, 0.0f}, {64, 128, 32, 32, 0.0f},
 };
 
-constexpr int kTileBM[] = {128, 64, 128, 64, 128, 128, 256, 128};
+constexpr int kTileBM[] = {128, 64, 128, 64, 128, 128, 256, 128, 128, 128, 256, 128, 128, 256, 64};
 
 int g_force_tile = -1;  // tuning hook (seg_igemm_force_tile); -1 = cost model
 
@@ -536,7 +542,14 @@ SEG_API int seg_conv_igemm_act(const float* in, long ldin, int N, int H, int W, 
     case 4: rc = launch_igemm<128, 96, 32, 96>(a, ks, splits, stream); break;
     case 5: rc = launch_igemm<128, 160, 32, 160>(a, ks, splits, stream); break;
     case 6: rc = launch_igemm<256, 32, 64, 32>(a, ks, splits, stream); break;
-    default: rc = launch_igemm<128, 32, 32, 32>(a, ks, splits, stream); break;
+    case 7: rc = launch_igemm<128, 32, 32, 32>(a, ks, splits, stream); break;
+    case 8: rc = launch_igemm<128, 128, 64, 32>(a, ks, splits, stream); break;
+    case 9: rc = launch_igemm<128, 128, 32, 64>(a, ks, splits, stream); break;
+    case 10: rc = launch_igemm<256, 128, 64, 64>(a, ks, splits, stream); break;
+    case 11: rc = launch_igemm<128, 256, 64, 64>(a, ks, splits, stream); break;
+    case 12: rc = launch_igemm<128, 64, 32, 32>(a, ks, splits, stream); break;
+    case 13: rc = launch_igemm<256, 64, 64, 32>(a, ks, splits, stream); break;
+    default: rc = launch_igemm<64, 128, 32, 32>(a, ks, splits, stream); break;
   }
   if (rc || splits == 1) return rc;
   const long total = (long)a.M * Cout;

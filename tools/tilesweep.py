@@ -17,7 +17,8 @@ import seg_amd  # noqa: E402
 from seg_amd import engine as E  # noqa: E402
 from seg_amd._lib import call, query, lib  # noqa: E402
 
-TILES = ["128x128", "64x128", "128x64", "64x64", "128x96", "128x160", "256x32", "128x32"]
+TILES = ["128x128", "64x128", "128x64", "64x64", "128x96", "128x160", "256x32", "128x32",
+         "8w128x128a", "8w128x128b", "8w256x128", "8w128x256", "8w128x64", "8w256x64", "8w64x128"]
 
 
 def timeit(fn, reps=8):

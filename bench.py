@@ -210,7 +210,8 @@ def main():
 
         # dominant kernel: igemm_conv_kernel<BM,BN,WM,WN,3,16> = every dense 3x3 conv's
         # forward and data gradient (the top symbol family in the rocprof summary)
-        flops, secs, n = family({"igemm3_fwd", "igemm3_dgrad"})
+        flops, secs, n = family({"igemm3_fwd", "igemm3_dgrad", "wino3_fwd", "wino3_dgrad"})
+        wfl, wsec, wn = family({"wino3_fwd", "wino3_dgrad"})
         achieved = flops / secs / 1e12 if secs > 0 else 0.0
         traffic = None
         prof = os.path.join(REPO, "profiles", "latest_roofline.json")
@@ -225,7 +226,11 @@ def main():
                 "traffic": round(traffic) if traffic else None,
                 "traffic_source": "profiles/latest_roofline.json: rocprofv3 PMC (2*FETCH_SIZE+WRITE_SIZE)*1KiB "
                                   "per igemm3 launch" if traffic else None,
-                "kernel": "igemm_conv_kernel<*,*,*,*,3,16> (dense 3x3 implicit GEMM, f32 MFMA: fwd + dgrad)",
+                "kernel": "dense 3x3 conv fwd + dgrad on f32 MFMA: igemm_conv_kernel<*,*,*,*,3,*> (implicit GEMM) "
+                          "and, for the deep decoder convs, wino_gemm_kernel + wino_out_kernel (Winograd F(2x2,3x3): "
+                          "2.25x fewer executed MFMA FLOPs than the algorithmic count used here)",
+                "winograd": {"launches": wn, "algorithmic_tflops": round(wfl / wsec / 1e12, 2) if wsec else None,
+                             "executed_mfma_tflops": round(wfl / 2.25 / wsec / 1e12, 2) if wsec else None},
                 "launches": n, "flops_per_launch": round(flops / max(n, 1)),
                 "avg_launch_us": round(secs / max(n, 1) * 1e6, 2),
                 "share_of_step": round(secs / dt, 4),

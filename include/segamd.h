@@ -82,9 +82,23 @@ int seg_conv_wgrad(const float* dy, long lddy, const float* x, long ldx,
 int seg_conv_wgrad_reduce(const float* part, int splits, float* dw, int Cout, int Cin, int ks,
                           int mode, int accumulate, hipStream_t stream);
 
+/* Winograd F(2x2,3x3) convolution (stride 1, pad 1; H, W even) on the f32 matrix
+ * cores: 2.25x fewer MFMA FLOPs than the direct sum for the deep decoder convs
+ * (src/unet.py:58,61) where the transforms are cheap; forward (U from
+ * seg_pack_batch mode 3) and data gradient (mode 4).  out = conv + bias + add;
+ * `work` >= 16 * N*(H/2)*(W/2) * Cout floats; `stat` (optional): BatchNorm
+ * partials in seg_conv_igemm's layout with seg_conv_wino_row_tiles tiles of 256
+ * rows.  seg_conv_wino_pick: 1 when the cost model prefers it to seg_conv_igemm. */
+int seg_conv_wino_pick(int N, int H, int W, int Cin, int Cout);
+int seg_conv_wino_row_tiles(int N, int H, int W);
+int seg_conv_wino(const float* in, long ldin, int N, int H, int W, int Cin, const float* wk, int ldk,
+                  const float* bias, float* out, long ldout, int Cout, const float* add, long ldadd,
+                  float* stat, float* work, hipStream_t stream);
+
 /* Every weight repack of a step in one launch.  `jobs` is a DEVICE array of
  * njobs seg_pack_job (mode 0/1 as seg_pack_conv_weight, mode 2 = depthwise
- * [9][C] as seg_pack_dw_weight with cout = C); max_elems = largest job's
+ * [9][C] as seg_pack_dw_weight with cout = C, modes 3/4 = Winograd filter
+ * transforms [16][rows][ldk] for seg_conv_wino's forward / data gradient); max_elems = largest job's
  * element count.  Replaces the per-conv packs of the engine's step. */
 typedef struct seg_pack_job {
   const float* w;

@@ -650,6 +650,42 @@ __global__ __launch_bounds__(256) void pack_batch_kernel(const SegPackJob* __res
     }
     return;
   }
+  if (j.mode == 3 || j.mode == 4) {
+    // Winograd F(2x2,3x3) filter transform U = G g G^T (wino.hip): [16][rows][ldk];
+    // mode 3 forward (rows = Cout, k = Cin), mode 4 data gradient (rows = Cin,
+    // k = Cout, g = the transposed, flipped filter)
+    const int rows = j.mode == 3 ? j.cout : j.cin;
+    const long total = (long)rows * j.ldk;
+    for (long i = blockIdx.x * 256L + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
+      const int r = (int)(i / j.ldk), k = (int)(i - (long)r * j.ldk);
+      const bool in = k < (j.mode == 3 ? j.cin : j.cout);
+      float g[3][3];
+#pragma unroll
+      for (int y = 0; y < 3; ++y)
+#pragma unroll
+        for (int x = 0; x < 3; ++x)
+          g[y][x] = !in ? 0.f
+                        : j.mode == 3 ? j.w[(((long)r * j.cin + k) * 3 + y) * 3 + x]
+                                      : j.w[(((long)k * j.cin + r) * 3 + (2 - y)) * 3 + (2 - x)];
+      float h[4][3];  // G g
+#pragma unroll
+      for (int x = 0; x < 3; ++x) {
+        h[0][x] = g[0][x];
+        h[1][x] = 0.5f * (g[0][x] + g[1][x] + g[2][x]);
+        h[2][x] = 0.5f * (g[0][x] - g[1][x] + g[2][x]);
+        h[3][x] = g[2][x];
+      }
+      const long plane = (long)rows * j.ldk;
+#pragma unroll
+      for (int y = 0; y < 4; ++y) {  // (G g) G^T
+        const float u[4] = {h[y][0], 0.5f * (h[y][0] + h[y][1] + h[y][2]), 0.5f * (h[y][0] - h[y][1] + h[y][2]),
+                            h[y][2]};
+#pragma unroll
+        for (int x = 0; x < 4; ++x) j.wk[(y * 4 + x) * plane + i] = u[x];
+      }
+    }
+    return;
+  }
   const int rows = j.mode == 0 ? j.cout : j.cin;
   const long total = (long)rows * j.ldk;
   for (long i = blockIdx.x * 256L + threadIdx.x; i < total; i += (long)gridDim.x * 256) {

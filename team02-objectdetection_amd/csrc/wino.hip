@@ -1,0 +1,338 @@
+// Winograd F(2x2, 3x3) convolution on the f32 matrix cores (stride 1, pad 1).
+//
+// The fp32 configuration is compute-bound on the dense 3x3 convs of the decoder
+// (src/unet.py:58,61: 86 % of the forward FLOPs), and f32 MFMA runs at
+// the f32 vector rate.  Winograd's minimal filtering F(2x2,3x3) computes each 2x2
+// output tile from a 4x4 input tile with 16 multiplies per (input, output)
+// channel pair instead of 36 -- 2.25x fewer MFMA FLOPs -- at the cost of input /
+// output transforms (additions only) and a 16-way batched GEMM.  This is the
+// algorithm MIOpen and cuDNN pick for fp32 3x3 convolutions; its rounding stays
+// within a few ulps of the direct sum (tests: <= 1e-5 relative to torch's conv).
+//
+//   V_xi[t][ci] = (B^T d_t B)[xi]   d_t = 4x4 input patch of tile t (pad 1)
+//   U_xi[co][ci] = (G g G^T)[xi]    g = w[co][ci] (seg_pack_batch modes 3/4)
+//   M_xi[t][co] = sum_ci V_xi[t][ci] U_xi[co][ci]       (16 GEMMs, blockIdx.z = xi)
+//   Y_t = A^T M_t A (+ bias, + addend, BatchNorm partials)  (wino_out_kernel)
+// with B^T = [1 0 -1 0; 0 1 1 0; 0 -1 1 0; 0 1 0 -1], G = [1 0 0; .5 .5 .5;
+// .5 -.5 .5; 0 0 1], A^T = [1 1 1 0; 0 1 -1 -1].  Each row of B^T has two
+// nonzeros, so V_xi of one tile is a signed sum of 4 input pixels: the GEMM's A
+// loader forms it from 4 float4 loads -- V is never written to HBM.  M goes
+// through HBM (16 x tiles x Cout floats); the output kernel fuses the BN
+// statistics epilogue of seg_conv_igemm (same [row tile][2][Cout] partials,
+// 256-pixel row tiles) so seg_bn_stats_tiles finalizes either.
+//
+// The data gradient of a stride-1 3x3 conv is the same convolution of dY with
+// the transposed, flipped weights (pack mode 4), so it runs on the same kernels.
+#include "common.h"
+
+namespace {
+
+__device__ __attribute__((aligned(16))) float g_wzero4[4];
+
+struct WinoArgs {
+  const float* in; long ldin;   // NHWC conv input [N*H*W][ldin]
+  const float* wk; int ldk;      // U [16][Cout][ldk]
+  float* m;                      // M [16][T][Cout]
+  int N, H, W, Cin, Cout;
+  int T, th, tw;                 // tiles, tiles per column / row
+};
+
+// Nonzeros of row r of B^T: positions p0, p1 with signs s0, s1.
+__device__ __forceinline__ void bt_row(int r, int& p0, int& p1, float& s0, float& s1) {
+  p0 = r == 0 ? 0 : 1;
+  p1 = r == 3 ? 3 : 2;
+  s0 = r == 2 ? -1.f : 1.f;
+  s1 = (r == 0 || r == 3) ? -1.f : 1.f;
+}
+
+template <int BM, int BN, int WM, int WN, int BK>
+__global__ __launch_bounds__(256) void wino_gemm_kernel(WinoArgs a) {
+  constexpr int LDSR = BK + 4;
+  constexpr int KQ = BK / 4;
+  constexpr int A_VEC = BM * KQ, B_VEC = BN * KQ;
+  constexpr int A_PER = (A_VEC + 255) / 256;
+  constexpr int B_PER = (B_VEC + 255) / 256;
+  constexpr int MI = WM / 32, NI = WN / 32;
+  constexpr int WAVES_N = BN / WN;
+  static_assert((BM / WM) * (BN / WN) == 4, "4 waves per block");
+  static_assert(256 % KQ == 0, "uniform kq per thread");
+
+  __shared__ __attribute__((aligned(16))) float As[BM * LDSR];
+  __shared__ __attribute__((aligned(16))) float Bs[BN * LDSR];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm0 = (wave / WAVES_N) * WM, wn0 = (wave % WAVES_N) * WN;
+  const int tiles_n = (a.Cout + BN - 1) / BN;
+  const int lid = xcd_swizzle(blockIdx.x, gridDim.x);
+  const int tn = lid % tiles_n, tm = lid / tiles_n;
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int xi = blockIdx.z;
+  int pa0, pa1, pb0, pb1;
+  float sa0, sa1, sb0, sb1;
+  bt_row(xi >> 2, pa0, pa1, sa0, sa1);
+  bt_row(xi & 3, pb0, pb1, sb0, sb1);
+  const float s00 = sa0 * sb0, s01 = sa0 * sb1, s10 = sa1 * sb0, s11 = sa1 * sb1;
+
+  // A slots: tile fixed across the K loop; 4 pixel offsets (zero page when padded)
+  const int kq4 = (tid % KQ) * 4;
+  long off[A_PER][4];
+  unsigned okm[A_PER];
+#pragma unroll
+  for (int i = 0; i < A_PER; ++i) {
+    const int idx = tid + i * 256;
+    const int t = m0 + idx / KQ;
+    const bool ok = idx < A_VEC && t < a.T;
+    const int tt = ok ? t : 0;
+    const int n = tt / (a.th * a.tw), r = tt - n * a.th * a.tw;
+    const int ty = r / a.tw, tx = r - ty * a.tw;
+    const int h0 = 2 * ty - 1, w0 = 2 * tx - 1;
+    const int hh[2] = {h0 + pa0, h0 + pa1}, ww[2] = {w0 + pb0, w0 + pb1};
+    unsigned m = 0;
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int v = 0; v < 2; ++v) {
+        const bool in = ok && (unsigned)hh[u] < (unsigned)a.H && (unsigned)ww[v] < (unsigned)a.W;
+        off[i][u * 2 + v] = in ? (((long)n * a.H + hh[u]) * a.W + ww[v]) * a.ldin : 0;
+        m |= (in ? 1u : 0u) << (u * 2 + v);
+      }
+    okm[i] = m;
+  }
+  const float* wk = a.wk + (long)xi * a.Cout * a.ldk;
+  long boff[B_PER];
+  bool bok[B_PER];
+#pragma unroll
+  for (int i = 0; i < B_PER; ++i) {
+    const int idx = tid + i * 256;
+    const int co = n0 + idx / KQ;
+    bok[i] = idx < B_VEC && co < a.Cout;
+    boff[i] = (long)(bok[i] ? co : 0) * a.ldk + kq4;
+  }
+
+  f32x4 ra[A_PER][4], rb[B_PER];
+  auto load = [&](int k0) {
+    const bool kin = k0 + kq4 < a.Cin;
+#pragma unroll
+    for (int i = 0; i < A_PER; ++i)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const bool ok = kin && ((okm[i] >> q) & 1u);
+        ra[i][q] = ld4(ok ? a.in + off[i][q] + k0 + kq4 : g_wzero4);
+      }
+#pragma unroll
+    for (int i = 0; i < B_PER; ++i) rb[i] = ld4(bok[i] && kin ? wk + boff[i] + k0 : g_wzero4);
+  };
+  auto store = [&]() {
+#pragma unroll
+    for (int i = 0; i < A_PER; ++i) {
+      const int idx = tid + i * 256;
+      if (A_VEC % 256 == 0 || idx < A_VEC) {
+        const f32x4 v = (s00 * ra[i][0] + s01 * ra[i][1]) + (s10 * ra[i][2] + s11 * ra[i][3]);
+        st4(&As[(idx / KQ) * LDSR + (idx % KQ) * 4], v);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < B_PER; ++i) {
+      const int idx = tid + i * 256;
+      if (B_VEC % 256 == 0 || idx < B_VEC) st4(&Bs[(idx / KQ) * LDSR + (idx % KQ) * 4], rb[i]);
+    }
+  };
+
+  f32x16 acc[MI][NI];
+#pragma unroll
+  for (int mi = 0; mi < MI; ++mi)
+#pragma unroll
+    for (int ni = 0; ni < NI; ++ni)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[mi][ni][r] = 0.f;
+
+  const int lrow = lane & 31, lk = (lane >> 5) * 4;
+  const int nk = (a.Cin + BK - 1) / BK;
+  load(0);
+  for (int kt = 0; kt < nk; ++kt) {
+    store();
+    __syncthreads();
+    if (kt + 1 < nk) load((kt + 1) * BK);
+#pragma unroll
+    for (int ks = 0; ks < BK / 8; ++ks) {
+      f32x4 af[MI], bf[NI];
+#pragma unroll
+      for (int mi = 0; mi < MI; ++mi) af[mi] = ld4(&As[(wm0 + mi * 32 + lrow) * LDSR + ks * 8 + lk]);
+#pragma unroll
+      for (int ni = 0; ni < NI; ++ni) bf[ni] = ld4(&Bs[(wn0 + ni * 32 + lrow) * LDSR + ks * 8 + lk]);
+#pragma unroll
+      for (int kk = 0; kk < 4; ++kk)
+#pragma unroll
+        for (int mi = 0; mi < MI; ++mi)
+#pragma unroll
+          for (int ni = 0; ni < NI; ++ni)
+            acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[mi][kk], bf[ni][kk], acc[mi][ni], 0, 0, 0);
+    }
+    __syncthreads();
+  }
+
+  // raw M_xi rows (C layout of 32x32 f32 MFMA: col = lane&31, row = (r&3) + 8(r>>2) + 4(lane>>5))
+  float* M = a.m + (long)xi * a.T * a.Cout;
+#pragma unroll
+  for (int ni = 0; ni < NI; ++ni) {
+    const int col = n0 + wn0 + ni * 32 + lrow;
+    if (col >= a.Cout) continue;
+#pragma unroll
+    for (int mi = 0; mi < MI; ++mi)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = m0 + wm0 + mi * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+        if (row < a.T) M[(long)row * a.Cout + col] = acc[mi][ni][r];
+      }
+  }
+}
+
+// Y = A^T M A per tile and float4 channel group (+ bias, + addend), NHWC out; with
+// `stat`, the BatchNorm partials of each 64-tile (256-pixel) block: per channel the
+// block sum and the sum of squared deviations from the block mean, exactly the
+// [row tile][2][Cout] layout of seg_conv_igemm's epilogue (tile_rows = 256).
+// Block = 256 threads = 16 tile lanes x 16 channel-group lanes (256 contiguous
+// bytes of an M row per load); each tile lane owns 4 tiles (tl + 16 q); channels
+// are walked 64 at a time.
+__global__ __launch_bounds__(256) void wino_out_kernel(const float* __restrict__ m, int T, int Cout, int N, int H,
+                                                       int W, int th, int tw, const float* __restrict__ bias,
+                                                       const float* __restrict__ add, long ldadd,
+                                                       float* __restrict__ out, long ldout, float* __restrict__ stat) {
+  __shared__ f32x4 red[4][16];  // [wave][cg lane]
+  __shared__ f32x4 bmean[16];
+  const int t = threadIdx.x, tl = t >> 4, cl = t & 15, wave = t >> 6;
+  long pix[4][4];
+  bool tok[4];
+  int tile[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    tile[q] = blockIdx.x * 64 + tl + 16 * q;
+    tok[q] = tile[q] < T;
+    const int tt = tok[q] ? tile[q] : 0;
+    const int n = tt / (th * tw), r = tt - n * th * tw;
+    const int ty = r / tw, tx = r - ty * tw;
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int v = 0; v < 2; ++v) pix[q][u * 2 + v] = ((long)n * H + 2 * ty + u) * W + 2 * tx + v;
+  }
+  const int ntile = min(64, T - (int)blockIdx.x * 64);
+  const float cnt = 4.f * (float)ntile;
+  const long TC = (long)T * Cout;
+  for (int cgb = 0; cgb < Cout; cgb += 64) {
+    const int c = cgb + cl * 4;
+    const bool cok = c < Cout;
+    const f32x4 b = (bias && cok) ? ld4(bias + c) : f32x4{0.f, 0.f, 0.f, 0.f};
+    f32x4 y[4][4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      if (tok[q] && cok) {
+        f32x4 qv[16];
+#pragma unroll
+        for (int x = 0; x < 16; ++x) qv[x] = ld4(m + x * TC + (long)tile[q] * Cout + c);
+        // rows of A^T M: R0[j] = q0j + q1j + q2j, R1[j] = q1j - q2j - q3j
+        f32x4 r0[4], r1[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          r0[j] = qv[j] + qv[4 + j] + qv[8 + j];
+          r1[j] = qv[4 + j] - qv[8 + j] - qv[12 + j];
+        }
+        y[q][0] = r0[0] + r0[1] + r0[2] + b;
+        y[q][1] = r0[1] - r0[2] - r0[3] + b;
+        y[q][2] = r1[0] + r1[1] + r1[2] + b;
+        y[q][3] = r1[1] - r1[2] - r1[3] + b;
+#pragma unroll
+        for (int p = 0; p < 4; ++p) {
+          if (add) y[q][p] += ld4(add + pix[q][p] * ldadd + c);
+          st4(out + pix[q][p] * ldout + c, y[q][p]);
+        }
+      } else {
+#pragma unroll
+        for (int p = 0; p < 4; ++p) y[q][p] = f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+    }
+    if (!stat) continue;
+    // pass 1: block sum -> mean; pass 2: sum of squared deviations about it
+#pragma unroll
+    for (int pass = 0; pass < 2; ++pass) {
+      f32x4 s = {0.f, 0.f, 0.f, 0.f};
+      const f32x4 mu = pass ? bmean[cl] : f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        if (tok[q] && cok) {
+#pragma unroll
+          for (int p = 0; p < 4; ++p) {
+            const f32x4 d = y[q][p] - mu;
+            s += pass ? d * d : d;
+          }
+        }
+#pragma unroll
+      for (int o = 16; o < 64; o <<= 1)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) s[j] += __shfl_xor(s[j], o, 64);
+      if ((t & 63) < 16) red[wave][cl] = s;
+      __syncthreads();
+      if (t < 16) {
+        const f32x4 tot = red[0][t] + red[1][t] + red[2][t] + red[3][t];
+        const int cc = cgb + t * 4;
+        if (pass == 0) bmean[t] = tot / cnt;
+        if (cc < Cout) {
+          float* dst = stat + ((long)blockIdx.x * 2 + pass) * Cout + cc;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) dst[j] = tot[j];
+        }
+      }
+      __syncthreads();
+    }
+  }
+}
+
+template <int BM, int BN, int WM, int WN>
+void launch_wino(const WinoArgs& a, hipStream_t s) {
+  dim3 grid(seg_cdiv(a.T, BM) * seg_cdiv(a.Cout, BN), 1, 16);
+  hipLaunchKernelGGL((wino_gemm_kernel<BM, BN, WM, WN, 32>), grid, dim3(256), 0, s, a);
+}
+
+}  // namespace
+
+// Use Winograd for this stride-1 pad-1 3x3 conv?  (1 = yes.)  The transforms
+// cost a round trip of M (16 x tiles x Cout floats) through HBM per GEMM FLOP
+// in proportion to 1/Cin, so Winograd wins for deep inputs.  Boundary measured on
+// MI355X with tools/winobench.py over the MobileNetV2UNet decoder (fwd / dgrad
+// speedups: Cin 1344: 2.06, Cin 256: 1.29-1.51, Cin 288: 1.52, Cin 128 with
+// Cout 128: 1.25 but Cout 288: 1.00, Cin 152 at 65536 tiles: 0.88, Cin <= 80:
+// 0.36-0.70).  Deterministic: the choice depends on the shape only.
+SEG_API int seg_conv_wino_pick(int N, int H, int W, int Cin, int Cout) {
+  if ((H & 1) || (W & 1) || (Cin & 3) || (Cout & 3) || Cin < 32 || Cout < 32) return 0;
+  const long T = (long)N * (H / 2) * (W / 2);
+  if (Cin >= 192) return 1;
+  return (Cin >= 128 && Cout <= Cin && T <= 16384) ? 1 : 0;
+}
+
+// Number of 256-pixel row tiles of seg_conv_wino's BN partials.
+SEG_API int seg_conv_wino_row_tiles(int N, int H, int W) {
+  const long T = (long)N * (H / 2) * (W / 2);
+  return (int)((T + 63) / 64);
+}
+
+// out = conv3x3(in, w) (+bias) (+add), stride 1, pad 1, by Winograd F(2x2,3x3).
+// wk: U from seg_pack_batch mode 3 (forward) / 4 (data gradient): [16][Cout][ldk],
+// ldk >= Cin.  work >= 16 * N*(H/2)*(W/2) * Cout floats.  stat (optional): BN
+// partials [seg_conv_wino_row_tiles][2][Cout] with tile_rows = 256.
+SEG_API int seg_conv_wino(const float* in, long ldin, int N, int H, int W, int Cin, const float* wk, int ldk,
+                          const float* bias, float* out, long ldout, int Cout, const float* add, long ldadd,
+                          float* stat, float* work, hipStream_t stream) {
+  if ((H & 1) || (W & 1) || (Cin & 3) || (ldin & 3) || (ldk & 3) || ldk < Cin || (Cout & 3) || (ldout & 3) ||
+      (add && (ldadd & 3)) || !work)
+    return (int)hipErrorInvalidValue;
+  WinoArgs a;
+  a.in = in; a.ldin = ldin; a.wk = wk; a.ldk = ldk; a.m = work;
+  a.N = N; a.H = H; a.W = W; a.Cin = Cin; a.Cout = Cout;
+  a.th = H / 2; a.tw = W / 2; a.T = N * a.th * a.tw;
+  if (a.T == 0) return 0;
+  if (Cout >= 128) launch_wino<128, 128, 64, 64>(a, stream);
+  else launch_wino<128, 64, 64, 32>(a, stream);
+  hipLaunchKernelGGL(wino_out_kernel, dim3(seg_cdiv(a.T, 64)), dim3(256), 0, stream, work, a.T, Cout, N, H, W, a.th,
+                     a.tw, bias, add, ldadd, out, ldout, stat);
+  SEG_RET_LAST();
+}

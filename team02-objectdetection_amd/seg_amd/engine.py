@@ -104,6 +104,9 @@ class ConvOp:
         self.ldk_f = self.ldk_d = 0
         # BN-folded inference weights (Program.fold): fk [Cout][Cin/g][ks][ks], fb [r4(Cout)], fk_pack
         self.fk = self.fb = self.fk_pack = None
+        # Winograd F(2x2,3x3) (seg_conv_wino) for the forward / data gradient, chosen by
+        # seg_conv_wino_pick at pack time; U_f [16][Cout][cin_pad], U_d [16][Cin][r4(Cout)]
+        self.wino_f = self.wino_d = False
         self.ks = conv.kernel_size[0]
         self.stride = conv.stride[0]
         self.pad = conv.padding[0]
@@ -142,11 +145,21 @@ class ConvOp:
                 ldk, wk_ptr = self.ldk_f, self.wk_f.data_ptr()  # packed by Program.pack at the step start
             stat = None
             if self.bn is not None and rt.training:  # BN statistics fused into the conv epilogue
-                ntiles, tile_rows = rt.row_tiles(y.M, self.cout)
+                if self.wino_f:
+                    ntiles, tile_rows = query("seg_conv_wino_row_tiles", y.N, y.H, y.W), 256
+                else:
+                    ntiles, tile_rows = rt.row_tiles(y.M, self.cout)
                 stat = rt.tmp(ntiles * 2 * self.cout)
-            _timed_call(f"igemm{self.ks}_fwd", self.flops(), "seg_conv_igemm", rt.ptr(i), i.ld, i.N, i.H, i.W,
-                        self.cin_pad, wk_ptr, ldk, bias, rt.ptr(y), y.ld, y.H, y.W, self.cout, self.ks,
-                        self.stride, self.pad, None, 0, stat.data_ptr() if stat is not None else None, s)
+            statp = stat.data_ptr() if stat is not None else None
+            if self.wino_f:
+                work = rt.tmp(16 * (y.M // 4) * self.cout)
+                _timed_call("wino3_fwd", self.flops(), "seg_conv_wino", rt.ptr(i), i.ld, i.N, i.H, i.W, self.cin_pad,
+                            self.wk_wf.data_ptr(), self.cin_pad, bias, rt.ptr(y), y.ld, self.cout, None, 0, statp,
+                            work.data_ptr(), s)
+            else:
+                _timed_call(f"igemm{self.ks}_fwd", self.flops(), "seg_conv_igemm", rt.ptr(i), i.ld, i.N, i.H, i.W,
+                            self.cin_pad, wk_ptr, ldk, bias, rt.ptr(y), y.ld, y.H, y.W, self.cout, self.ks,
+                            self.stride, self.pad, None, 0, statp, s)
         if self.bn is None:
             return
         bn, C, M = self.bn, self.cout, y.M
@@ -267,9 +280,15 @@ class ConvOp:
                 raise NotImplementedError("data gradient of a strided dense conv")
             kin = r4(self.cout)  # dY channels padded to 4 (the C=10 head)
             add_ptr, add_ld = rt.begin_write_add(i)
-            _timed_call(f"igemm{self.ks}_dgrad", self.flops(), "seg_conv_igemm", dYp, dY.ld, y.N, y.H, y.W, kin,
-                        self.wk_d.data_ptr(), self.ldk_d, None, rt.gptr(i), i.ld, i.H, i.W, self.cin, self.ks, 1,
-                        self.pad, add_ptr, add_ld, None, s)
+            if self.wino_d:
+                work = rt.tmp(16 * (y.M // 4) * self.cin)
+                _timed_call("wino3_dgrad", self.flops(), "seg_conv_wino", dYp, dY.ld, y.N, y.H, y.W, kin,
+                            self.wk_wd.data_ptr(), kin, None, rt.gptr(i), i.ld, self.cin, add_ptr, add_ld, None,
+                            work.data_ptr(), s)
+            else:
+                _timed_call(f"igemm{self.ks}_dgrad", self.flops(), "seg_conv_igemm", dYp, dY.ld, y.N, y.H, y.W, kin,
+                            self.wk_d.data_ptr(), self.ldk_d, None, rt.gptr(i), i.ld, i.H, i.W, self.cin, self.ks, 1,
+                            self.pad, add_ptr, add_ld, None, s)
         rt.mark_written(i)
 
 
@@ -383,12 +402,26 @@ class Program:
                 jobs.append((w.data_ptr(), op.wk_f.data_ptr(), op.cout, 1, 3, 9, 2, 1))
                 max_elems = max(max_elems, 9 * op.cout)
                 continue
-            if not (op.ks == 1 and op.cin_pad == op.cin):
+            y = op.y
+            wino_ok = op.ks == 3 and op.stride == 1 and op.pad == 1
+            op.wino_f = wino_ok and bool(query("seg_conv_wino_pick", y.N, y.H, y.W, op.cin_pad, op.cout))
+            op.wino_d = wino_ok and not op.first and bool(query("seg_conv_wino_pick", y.N, y.H, y.W, r4(op.cout),
+                                                                op.cin))
+            if op.wino_f:
+                op.wk_wf = torch.empty(16 * op.cout * op.cin_pad, device=dev, dtype=torch.float32)
+                jobs.append((w.data_ptr(), op.wk_wf.data_ptr(), op.cout, op.cin, 3, op.cin_pad, 3, op.cin_pad))
+                max_elems = max(max_elems, op.cout * op.cin_pad)
+            elif not (op.ks == 1 and op.cin_pad == op.cin):
                 op.ldk_f = r4(op.ks * op.ks * op.cin_pad)
                 op.wk_f = torch.empty(op.cout * op.ldk_f, device=dev, dtype=torch.float32)
                 jobs.append((w.data_ptr(), op.wk_f.data_ptr(), op.cout, op.cin, op.ks, op.ldk_f, 0, op.cin_pad))
                 max_elems = max(max_elems, op.cout * op.ldk_f)
-            if not op.first:
+            if op.wino_d:
+                kin = r4(op.cout)
+                op.wk_wd = torch.empty(16 * op.cin * kin, device=dev, dtype=torch.float32)
+                jobs.append((w.data_ptr(), op.wk_wd.data_ptr(), op.cout, op.cin, 3, kin, 4, kin))
+                max_elems = max(max_elems, op.cin * kin)
+            elif not op.first:
                 kin = r4(op.cout)
                 op.ldk_d = r4(op.ks * op.ks * kin)
                 op.wk_d = torch.empty(op.cin * op.ldk_d, device=dev, dtype=torch.float32)

@@ -404,3 +404,61 @@ def test_dw_bias_act_and_bn_fold(stride):
     call("seg_dw_fwd_bias_act", xg.data_ptr(), C, N, H, W, C, wk.data_ptr(), fb.data_ptr(), 2, out.data_ptr(), C,
          Ho, Wo, stride, S())
     assert rel(from_nhwc(out, N, C, Ho, Wo), ref) < 1e-5
+
+
+def _pack_wino(w, mode, rows, ldk):
+    import numpy as np
+    Cout, Cin = w.shape[0], w.shape[1]
+    pt = np.dtype([("w", "<u8"), ("wk", "<u8"), ("cout", "<i4"), ("cin", "<i4"), ("ks", "<i4"), ("ldk", "<i4"),
+                   ("mode", "<i4"), ("kin", "<i4")])
+    wk = torch.full((16 * rows * ldk,), float("nan"), device=DEV)
+    job = np.array([(w.data_ptr(), wk.data_ptr(), Cout, Cin, 3, ldk, mode, ldk)], dtype=pt)
+    jobs = torch.from_numpy(job.view(np.uint8).copy()).to(DEV)
+    call("seg_pack_batch", jobs.data_ptr(), 1, rows * ldk, S())
+    return wk
+
+
+@pytest.mark.parametrize("N,Cin,Cout,H,W", [(2, 64, 32, 6, 10), (1, 1344, 256, 4, 8), (2, 152, 64, 8, 6),
+                                           (3, 36, 200, 2, 4), (1, 288, 128, 10, 14)])
+def test_conv_wino_fwd_stats_dgrad(N, Cin, Cout, H, W):
+    """Winograd F(2x2,3x3): forward (+bias, BN partials) and data gradient (+addend) vs torch."""
+    x = gen(N, Cin, H, W, seed=31)
+    w = gen(Cout, Cin, 3, 3, seed=32) * (2.0 / (Cin * 9)) ** 0.5
+    b = gen(Cout, seed=33)
+    xr = x.clone().requires_grad_(True)
+    y = F.conv2d(xr, w, b, padding=1)
+    dy = gen(*y.shape, seed=34)
+    y.backward(dy)
+    wg = w.to(DEV)
+    T = N * (H // 2) * (W // 2)
+    work = torch.empty(16 * T * max(Cin, Cout), device=DEV)
+    # forward + BN statistics
+    cin4 = r4(Cin)
+    U = _pack_wino(wg, 3, Cout, cin4)
+    xg = nhwc(x)
+    out = torch.full((N * H * W, r4(Cout)), float("nan"), device=DEV)
+    nt = query("seg_conv_wino_row_tiles", N, H, W)
+    stat = torch.empty(nt * 2 * Cout, device=DEV)
+    call("seg_conv_wino", xg.data_ptr(), xg.shape[1], N, H, W, cin4, U.data_ptr(), cin4, b.to(DEV).data_ptr(),
+         out.data_ptr(), out.shape[1], Cout, None, 0, stat.data_ptr(), work.data_ptr(), S())
+    assert rel(from_nhwc(out, N, Cout, H, W), y.detach()) < 1e-5
+    st = torch.empty(4 * Cout, device=DEV)
+    rm, rv = torch.zeros(Cout, device=DEV), torch.ones(Cout, device=DEV)
+    call("seg_bn_stats_tiles", stat.data_ptr(), nt, 256, N * H * W, Cout, None, None, 1e-5, 0.1, rm.data_ptr(),
+         rv.data_ptr(), None, st[:Cout].data_ptr(), st[Cout:2 * Cout].data_ptr(), st[2 * Cout:3 * Cout].data_ptr(),
+         st[3 * Cout:].data_ptr(), S())
+    y64 = y.detach().double()
+    assert rel(st[:Cout], y64.mean((0, 2, 3))) < 1e-5
+    assert rel(st[Cout:2 * Cout], 1 / torch.sqrt(y64.var((0, 2, 3), unbiased=False) + 1e-5)) < 1e-5
+    # data gradient with a fused addend
+    kin = r4(Cout)
+    Ud = _pack_wino(wg, 4, Cin, kin)
+    dyg = nhwc(dy)
+    if Cout % 4:
+        dyg[:, Cout:] = 0.0
+    addend = gen(N, Cin, H, W, seed=35)
+    addg = nhwc(addend)
+    dx = torch.full((N * H * W, r4(Cin)), float("nan"), device=DEV)
+    call("seg_conv_wino", dyg.data_ptr(), dyg.shape[1], N, H, W, kin, Ud.data_ptr(), kin, None, dx.data_ptr(),
+         dx.shape[1], Cin, addg.data_ptr(), addg.shape[1], None, work.data_ptr(), S())
+    assert rel(from_nhwc(dx, N, Cin, H, W), xr.grad + addend) < 1e-5

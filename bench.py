@@ -219,7 +219,7 @@ def main():
             with open(prof) as fh:
                 fam = json.load(fh)["families"].get("igemm3", {})
             traffic = fam.get("hbm_bytes_per_launch")
-        wf, ws, wn = family({"igemm3_wgrad"})
+        wf, ws, wn = family({"igemm3_wgrad", "wino3_wgrad"})
         af, as_, an = family({k for k, _, _ in rec})
         roof = {"bound": "mfma", "achieved": round(achieved, 2), "peak": F32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
                 "frac": round(achieved / F32_MFMA_PEAK_TFLOPS, 4),

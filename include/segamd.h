@@ -94,6 +94,17 @@ int seg_conv_wino_row_tiles(int N, int H, int W);
 int seg_conv_wino(const float* in, long ldin, int N, int H, int W, int Cin, const float* wk, int ldk,
                   const float* bias, float* out, long ldout, int Cout, const float* add, long ldadd,
                   float* stat, float* work, hipStream_t stream);
+/* Weight gradient of the same convs by Winograd F(3x3,2x2):
+ * dW = G^T [sum_t (A dY_t A^T) .* (B^T X_t B)] G.  seg_conv_wino_wgrad writes
+ * fixed-order split-K partial slabs part[splits][16][Cout][Cin] (Cin = the padded
+ * input channels, % 4 == 0; splits from seg_conv_wino_wgrad_splits), and
+ * seg_conv_wino_wgrad_reduce sums them and writes dW [Cout][Cin_real][3][3]. */
+int seg_conv_wino_wgrad_pick(int N, int H, int W, int Cin, int Cout);
+int seg_conv_wino_wgrad_splits(int N, int H, int W, int Cin, int Cout);
+int seg_conv_wino_wgrad(const float* dy, long lddy, const float* x, long ldx, int N, int H, int W, int Cin,
+                        int Cout, float* part, int splits, hipStream_t stream);
+int seg_conv_wino_wgrad_reduce(const float* part, int splits, float* dw, int Cout, int Cin, int Cin_pad,
+                               int accumulate, hipStream_t stream);
 
 /* Every weight repack of a step in one launch.  `jobs` is a DEVICE array of
  * njobs seg_pack_job (mode 0/1 as seg_pack_conv_weight, mode 2 = depthwise

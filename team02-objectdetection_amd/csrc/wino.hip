@@ -293,6 +293,201 @@ void launch_wino(const WinoArgs& a, hipStream_t s) {
   hipLaunchKernelGGL((wino_gemm_kernel<BM, BN, WM, WN, 32>), grid, dim3(256), 0, s, a);
 }
 
+// ---------------------------------------------------------------- weight gradient
+// dW = G^T [ sum_t (A dY_t A^T) .* (B^T X_t B) ] G  per (co, ci): Winograd F(3x3, 2x2)
+// (the transposition of F(2x2,3x3); A = [1 0; 1 1; 1 -1; 0 -1]).  Per xi a GEMM
+//   P_xi[co][ci] = sum_t DY_xi[t][co] * XV_xi[t][ci]
+// with K = 2x2 output tiles, split over gridDim.y into fixed-order partial slabs
+// [split][16][Cout][Cin] (no float atomics); wino_wgrad_reduce_kernel sums the
+// slabs and applies G^T . G.  Operands are staged k-major ([tile][channel], the
+// natural NHWC order) like wgrad.hip's kernel; each loaded float4 is the signed
+// sum of the tile's 4 dY pixels (A side) or 4 X pixels (B side, zero padding).
+struct WinoWgradArgs {
+  const float* dy; long lddy;
+  const float* x; long ldx;
+  float* part;
+  int N, H, W, Cin, Cout;  // H, W: spatial size of dY and X (stride 1, pad 1)
+  int T, th, tw, kchunk;
+};
+
+__device__ __forceinline__ float arow(int i, int a) {  // A = [1 0; 1 1; 1 -1; 0 -1]
+  return a == 0 ? (i == 3 ? 0.f : 1.f) : (i == 0 ? 0.f : (i == 2 || i == 3 ? -1.f : 1.f));
+}
+
+constexpr int WBK = 16;
+
+template <int BM, int BN, int WM, int WN>
+__global__ __launch_bounds__(256) void wino_wgrad_kernel(WinoWgradArgs a) {
+  constexpr int AR = BM + 4, BR = BN + 4;
+  constexpr int A_VEC = WBK * BM / 4, B_VEC = WBK * BN / 4;
+  constexpr int A_PER = (A_VEC + 255) / 256, B_PER = (B_VEC + 255) / 256;
+  constexpr int MI = WM / 32, NI = WN / 32, WAVES_N = BN / WN;
+  static_assert((BM / WM) * (BN / WN) == 4, "4 waves per block");
+
+  __shared__ __attribute__((aligned(16))) float As[WBK * AR];
+  __shared__ __attribute__((aligned(16))) float Bs[WBK * BR];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm0 = (wave / WAVES_N) * WM, wn0 = (wave % WAVES_N) * WN;
+  const int tiles_n = (a.Cin + BN - 1) / BN;
+  const int tiles = tiles_n * ((a.Cout + BM - 1) / BM);
+  const int lid = xcd_swizzle(blockIdx.x, gridDim.x);
+  const int split = lid / tiles, tile = lid - split * tiles;
+  const int tn = tile % tiles_n, tm = tile / tiles_n;
+  const int co0 = tm * BM, n0 = tn * BN;
+  const int xi = blockIdx.z, xr = xi >> 2, xc = xi & 3;
+  const int kbeg = split * a.kchunk;
+  const int kend = min(a.T, kbeg + a.kchunk);
+  // A side coefficients (dY 2x2 -> 4x4), B side pixel subset and signs (X 4x4 -> 4x4)
+  const float c00 = arow(xr, 0) * arow(xc, 0), c01 = arow(xr, 0) * arow(xc, 1);
+  const float c10 = arow(xr, 1) * arow(xc, 0), c11 = arow(xr, 1) * arow(xc, 1);
+  int pa0, pa1, pb0, pb1;
+  float sa0, sa1, sb0, sb1;
+  bt_row(xr, pa0, pa1, sa0, sa1);
+  bt_row(xc, pb0, pb1, sb0, sb1);
+  const float s00 = sa0 * sb0, s01 = sa0 * sb1, s10 = sa1 * sb0, s11 = sa1 * sb1;
+
+  f32x4 ra[A_PER][4], rb[B_PER][4];
+  auto tile_pos = [&](int t, int& n, int& ty, int& tx) {
+    n = t / (a.th * a.tw);
+    const int r = t - n * a.th * a.tw;
+    ty = r / a.tw;
+    tx = r - ty * a.tw;
+  };
+  auto load_tiles = [&](int k0) {
+#pragma unroll
+    for (int i = 0; i < A_PER; ++i) {
+      const int idx = tid + i * 256;
+      const int trow = idx / (BM / 4), c = co0 + (idx % (BM / 4)) * 4;
+      const int t = k0 + trow;
+      const bool ok = idx < A_VEC && t < kend && c < a.Cout;
+      int n, ty, tx;
+      tile_pos(ok ? t : 0, n, ty, tx);
+      const long p0 = ((long)n * a.H + 2 * ty) * a.W + 2 * tx;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const long p = p0 + (q >> 1) * a.W + (q & 1);
+        ra[i][q] = ld4(ok ? a.dy + p * a.lddy + c : g_wzero4);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < B_PER; ++i) {
+      const int idx = tid + i * 256;
+      const int trow = idx / (BN / 4), c = n0 + (idx % (BN / 4)) * 4;
+      const int t = k0 + trow;
+      const bool ok = idx < B_VEC && t < kend && c < a.Cin;
+      int n, ty, tx;
+      tile_pos(ok ? t : 0, n, ty, tx);
+      const int hh[2] = {2 * ty - 1 + pa0, 2 * ty - 1 + pa1}, ww[2] = {2 * tx - 1 + pb0, 2 * tx - 1 + pb1};
+#pragma unroll
+      for (int u = 0; u < 2; ++u)
+#pragma unroll
+        for (int v = 0; v < 2; ++v) {
+          const bool in = ok && (unsigned)hh[u] < (unsigned)a.H && (unsigned)ww[v] < (unsigned)a.W;
+          rb[i][u * 2 + v] = ld4(in ? a.x + (((long)n * a.H + hh[u]) * a.W + ww[v]) * a.ldx + c : g_wzero4);
+        }
+    }
+  };
+  auto store_tiles = [&]() {
+#pragma unroll
+    for (int i = 0; i < A_PER; ++i) {
+      const int idx = tid + i * 256;
+      if (idx < A_VEC) {
+        const f32x4 v = (c00 * ra[i][0] + c01 * ra[i][1]) + (c10 * ra[i][2] + c11 * ra[i][3]);
+        st4(&As[(idx / (BM / 4)) * AR + (idx % (BM / 4)) * 4], v);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < B_PER; ++i) {
+      const int idx = tid + i * 256;
+      if (idx < B_VEC) {
+        const f32x4 v = (s00 * rb[i][0] + s01 * rb[i][1]) + (s10 * rb[i][2] + s11 * rb[i][3]);
+        st4(&Bs[(idx / (BN / 4)) * BR + (idx % (BN / 4)) * 4], v);
+      }
+    }
+  };
+
+  f32x16 acc[MI][NI];
+#pragma unroll
+  for (int mi = 0; mi < MI; ++mi)
+#pragma unroll
+    for (int ni = 0; ni < NI; ++ni)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[mi][ni][r] = 0.f;
+
+  const int lrow = lane & 31, lh = lane >> 5;
+  const int nk = (kend - kbeg + WBK - 1) / WBK;
+  if (nk > 0) {
+    load_tiles(kbeg);
+    for (int kt = 0; kt < nk; ++kt) {
+      store_tiles();
+      __syncthreads();
+      if (kt + 1 < nk) load_tiles(kbeg + (kt + 1) * WBK);
+#pragma unroll
+      for (int kk = 0; kk < WBK / 2; ++kk) {
+        float af[MI], bf[NI];
+#pragma unroll
+        for (int mi = 0; mi < MI; ++mi) af[mi] = As[(2 * kk + lh) * AR + wm0 + mi * 32 + lrow];
+#pragma unroll
+        for (int ni = 0; ni < NI; ++ni) bf[ni] = Bs[(2 * kk + lh) * BR + wn0 + ni * 32 + lrow];
+#pragma unroll
+        for (int mi = 0; mi < MI; ++mi)
+#pragma unroll
+          for (int ni = 0; ni < NI; ++ni)
+            acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[mi], bf[ni], acc[mi][ni], 0, 0, 0);
+      }
+      __syncthreads();
+    }
+  }
+  float* slab = a.part + ((long)split * 16 + xi) * a.Cout * a.Cin;
+#pragma unroll
+  for (int ni = 0; ni < NI; ++ni) {
+    const int col = n0 + wn0 + ni * 32 + lrow;
+    if (col >= a.Cin) continue;
+#pragma unroll
+    for (int mi = 0; mi < MI; ++mi)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = co0 + wm0 + mi * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+        if (row < a.Cout) slab[(long)row * a.Cin + col] = acc[mi][ni][r];
+      }
+  }
+}
+
+// dW[co][ci][3][3] (+)= G^T (sum_s P_s) G, one thread per (co, ci < Cin_real); the
+// split sums run in fixed order (bitwise reproducible).
+__global__ __launch_bounds__(256) void wino_wgrad_reduce_kernel(const float* __restrict__ part, int splits, int Cout,
+                                                                int Cin_pad, int Cin, float* __restrict__ dw,
+                                                                int accumulate) {
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= (long)Cout * Cin) return;
+  const int co = (int)(i / Cin), ci = (int)(i - (long)co * Cin);
+  const long plane = (long)Cout * Cin_pad, off = (long)co * Cin_pad + ci;
+  float m[16];
+#pragma unroll
+  for (int x = 0; x < 16; ++x) m[x] = 0.f;
+  for (int s = 0; s < splits; ++s) {
+    const float* p = part + (long)s * 16 * plane + off;
+#pragma unroll
+    for (int x = 0; x < 16; ++x) m[x] += p[x * plane];
+  }
+  float t[3][4];  // G^T m
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    t[0][j] = m[j] + 0.5f * (m[4 + j] + m[8 + j]);
+    t[1][j] = 0.5f * (m[4 + j] - m[8 + j]);
+    t[2][j] = 0.5f * (m[4 + j] + m[8 + j]) + m[12 + j];
+  }
+  float* o = dw + i * 9;
+#pragma unroll
+  for (int y = 0; y < 3; ++y) {
+    const float v[3] = {t[y][0] + 0.5f * (t[y][1] + t[y][2]), 0.5f * (t[y][1] - t[y][2]),
+                        0.5f * (t[y][1] + t[y][2]) + t[y][3]};
+#pragma unroll
+    for (int x = 0; x < 3; ++x) o[y * 3 + x] = accumulate ? o[y * 3 + x] + v[x] : v[x];
+  }
+}
+
 }  // namespace
 
 // Use Winograd for this stride-1 pad-1 3x3 conv?  (1 = yes.)  The transforms
@@ -334,5 +529,54 @@ SEG_API int seg_conv_wino(const float* in, long ldin, int N, int H, int W, int C
   else launch_wino<128, 64, 64, 32>(a, stream);
   hipLaunchKernelGGL(wino_out_kernel, dim3(seg_cdiv(a.T, 64)), dim3(256), 0, stream, work, a.T, Cout, N, H, W, a.th,
                      a.tw, bias, add, ldadd, out, ldout, stat);
+  SEG_RET_LAST();
+}
+
+// Use the Winograd weight gradient?  Measured on MI355X (tools/winobench.py):
+// 1.19x at Cin 1344 / Cout 256, 1.29x at 256 / 256, <= 1.08x or slower below.
+SEG_API int seg_conv_wino_wgrad_pick(int N, int H, int W, int Cin, int Cout) {
+  if ((H & 1) || (W & 1) || (Cin & 3) || (Cout & 3)) return 0;
+  return (Cin >= 256 && Cout >= 256) ? 1 : 0;
+}
+
+// Split count of seg_conv_wino_wgrad (partial slabs of 16 * Cout * Cin_pad floats).
+SEG_API int seg_conv_wino_wgrad_splits(int N, int H, int W, int Cin, int Cout) {
+  const long T = (long)N * (H / 2) * (W / 2);
+  const int bm = Cout >= 128 ? 128 : (Cout >= 64 ? 64 : 32);
+  const int bn = bm == 32 ? 128 : (Cin >= 128 ? 128 : 64);
+  const long tiles = 16L * seg_cdiv(Cout, bm) * seg_cdiv(Cin, bn);
+  long splits = (2048 + tiles - 1) / tiles;
+  splits = std::min(splits, std::max<long>(1, T / 128));  // >= 128 tiles (512 pixels) per split
+  return (int)std::max<long>(1, std::min<long>(splits, 1024));
+}
+
+// Weight gradient of a stride-1 pad-1 3x3 conv by Winograd F(3x3,2x2):
+// part[splits][16][Cout][Cin] (Cin % 4 == 0: the padded input channels).
+SEG_API int seg_conv_wino_wgrad(const float* dy, long lddy, const float* x, long ldx, int N, int H, int W, int Cin,
+                                int Cout, float* part, int splits, hipStream_t stream) {
+  if ((H & 1) || (W & 1) || (Cin & 3) || (Cout & 3) || (lddy & 3) || (ldx & 3) || splits < 1)
+    return (int)hipErrorInvalidValue;
+  WinoWgradArgs a;
+  a.dy = dy; a.lddy = lddy; a.x = x; a.ldx = ldx; a.part = part;
+  a.N = N; a.H = H; a.W = W; a.Cin = Cin; a.Cout = Cout;
+  a.th = H / 2; a.tw = W / 2; a.T = N * a.th * a.tw;
+  a.kchunk = seg_cdiv(seg_cdiv(a.T, splits), WBK) * WBK;
+  const int bm = Cout >= 128 ? 128 : (Cout >= 64 ? 64 : 32);
+  const int bn = bm == 32 ? 128 : (Cin >= 128 ? 128 : 64);
+  dim3 grid(seg_cdiv(Cout, bm) * seg_cdiv(Cin, bn) * splits, 1, 16);
+  if (bm == 128 && bn == 128) hipLaunchKernelGGL((wino_wgrad_kernel<128, 128, 64, 64>), grid, dim3(256), 0, stream, a);
+  else if (bm == 128) hipLaunchKernelGGL((wino_wgrad_kernel<128, 64, 64, 32>), grid, dim3(256), 0, stream, a);
+  else if (bm == 64 && bn == 128) hipLaunchKernelGGL((wino_wgrad_kernel<64, 128, 32, 64>), grid, dim3(256), 0, stream, a);
+  else if (bm == 64) hipLaunchKernelGGL((wino_wgrad_kernel<64, 64, 32, 32>), grid, dim3(256), 0, stream, a);
+  else hipLaunchKernelGGL((wino_wgrad_kernel<32, 128, 32, 32>), grid, dim3(256), 0, stream, a);
+  SEG_RET_LAST();
+}
+
+// dW (PyTorch layout [Cout][Cin][3][3]) (+)= G^T (fixed-order sum of the slabs) G.
+SEG_API int seg_conv_wino_wgrad_reduce(const float* part, int splits, float* dw, int Cout, int Cin, int Cin_pad,
+                                       int accumulate, hipStream_t stream) {
+  if (Cin_pad < Cin || splits < 1) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(wino_wgrad_reduce_kernel, dim3(seg_cdiv((long)Cout * Cin, 256)), dim3(256), 0, stream, part,
+                     splits, Cout, Cin_pad, Cin, dw, accumulate);
   SEG_RET_LAST();
 }

@@ -106,7 +106,7 @@ class ConvOp:
         self.fk = self.fb = self.fk_pack = None
         # Winograd F(2x2,3x3) (seg_conv_wino) for the forward / data gradient, chosen by
         # seg_conv_wino_pick at pack time; U_f [16][Cout][cin_pad], U_d [16][Cin][r4(Cout)]
-        self.wino_f = self.wino_d = False
+        self.wino_f = self.wino_d = self.wino_w = False
         self.ks = conv.kernel_size[0]
         self.stride = conv.stride[0]
         self.pad = conv.padding[0]
@@ -258,6 +258,13 @@ class ConvOp:
                 call("seg_dw_wgrad", dYp, dY.ld, rt.ptr(i), i.ld, i.N, i.H, i.W, i.C, *self._in_xform(rt), y.H, y.W,
                      self.stride, part.data_ptr(), s)
                 call("seg_conv_wgrad_reduce", part.data_ptr(), nblk, gw, self.cout, 1, 3, 1, 0, s)
+            elif self.wino_w:
+                i = self.inp
+                splits = query("seg_conv_wino_wgrad_splits", y.N, y.H, y.W, self.cin_pad, self.cout)
+                part = rt.tmp(splits * 16 * self.cout * self.cin_pad)
+                _timed_call("wino3_wgrad", self.flops(), "seg_conv_wino_wgrad", dYp, dY.ld, rt.ptr(i), i.ld, y.N, y.H,
+                            y.W, self.cin_pad, self.cout, part.data_ptr(), splits, s)
+                call("seg_conv_wino_wgrad_reduce", part.data_ptr(), splits, gw, self.cout, self.cin, self.cin_pad, 0, s)
             else:
                 i = self.inp
                 splits = query("seg_conv_wgrad_splits", M, self.cout, self.cin_pad, self.ks)
@@ -407,6 +414,7 @@ class Program:
             op.wino_f = wino_ok and bool(query("seg_conv_wino_pick", y.N, y.H, y.W, op.cin_pad, op.cout))
             op.wino_d = wino_ok and not op.first and bool(query("seg_conv_wino_pick", y.N, y.H, y.W, r4(op.cout),
                                                                 op.cin))
+            op.wino_w = wino_ok and bool(query("seg_conv_wino_wgrad_pick", y.N, y.H, y.W, op.cin_pad, op.cout))
             if op.wino_f:
                 op.wk_wf = torch.empty(16 * op.cout * op.cin_pad, device=dev, dtype=torch.float32)
                 jobs.append((w.data_ptr(), op.wk_wf.data_ptr(), op.cout, op.cin, 3, op.cin_pad, 3, op.cin_pad))

@@ -462,3 +462,33 @@ def test_conv_wino_fwd_stats_dgrad(N, Cin, Cout, H, W):
     call("seg_conv_wino", dyg.data_ptr(), dyg.shape[1], N, H, W, kin, Ud.data_ptr(), kin, None, dx.data_ptr(),
          dx.shape[1], Cin, addg.data_ptr(), addg.shape[1], None, work.data_ptr(), S())
     assert rel(from_nhwc(dx, N, Cin, H, W), xr.grad + addend) < 1e-5
+
+
+@pytest.mark.parametrize("N,Cin,Cout,H,W", [(2, 64, 32, 6, 10), (1, 1344, 256, 4, 8), (2, 152, 64, 8, 6),
+                                           (3, 36, 200, 2, 4), (2, 80, 32, 16, 12)])
+def test_conv_wino_wgrad(N, Cin, Cout, H, W):
+    """Winograd F(3x3,2x2) weight gradient (split-K slabs + G^T . G reduce) vs torch."""
+    x = gen(N, Cin, H, W, seed=41)
+    w = gen(Cout, Cin, 3, 3, seed=42) * 0.1
+    wr = w.clone().requires_grad_(True)
+    y = F.conv2d(x, wr, None, padding=1)
+    dy = gen(*y.shape, seed=43)
+    y.backward(dy)
+    cin4 = r4(Cin)
+    splits = query("seg_conv_wino_wgrad_splits", N, H, W, cin4, Cout)
+    part = torch.empty(splits * 16 * Cout * cin4, device=DEV)
+    xg, dyg = nhwc(x), nhwc(dy)
+    if Cin % 4:
+        xg[:, Cin:] = 0.0
+    call("seg_conv_wino_wgrad", dyg.data_ptr(), dyg.shape[1], xg.data_ptr(), xg.shape[1], N, H, W, cin4, Cout,
+         part.data_ptr(), splits, S())
+    dw = torch.full((Cout, Cin, 3, 3), float("nan"), device=DEV)
+    call("seg_conv_wino_wgrad_reduce", part.data_ptr(), splits, dw.data_ptr(), Cout, Cin, cin4, 0, S())
+    assert rel(dw, wr.grad) < 1e-5
+    for s2 in (1, 3):  # any split count gives the same sums up to rounding
+        p2 = torch.empty(s2 * 16 * Cout * cin4, device=DEV)
+        call("seg_conv_wino_wgrad", dyg.data_ptr(), dyg.shape[1], xg.data_ptr(), xg.shape[1], N, H, W, cin4, Cout,
+             p2.data_ptr(), s2, S())
+        dw2 = dw.clone()
+        call("seg_conv_wino_wgrad_reduce", p2.data_ptr(), s2, dw2.data_ptr(), Cout, Cin, cin4, 1, S())
+        assert rel(dw2, 2 * wr.grad) < 1e-5

@@ -64,6 +64,28 @@ def main():
             pick = query("seg_conv_wino_pick", N, H, W, ci, co)
             print(f"{name:6s} {d:5s} direct {t_d * 1e6:7.1f} us ({fl / t_d / 1e12:5.1f} TF/s)  wino {t_w * 1e6:7.1f} us "
                   f"({fl / t_w / 1e12:5.1f})  speedup {t_d / t_w:4.2f}  pick={pick}", flush=True)
+        # weight gradient: direct split-K wgrad + reduce vs Winograd wgrad + reduce
+        x = torch.randn(N * H * W, Cin, device="cuda")
+        dy = torch.randn(N * H * W, Cout, device="cuda")
+        dw = torch.empty(Cout, Cin, 3, 3, device="cuda")
+        M = N * H * W
+        sp = query("seg_conv_wgrad_splits", M, Cout, Cin, 3)
+        part = torch.empty(sp * Cout * 9 * Cin, device="cuda")
+
+        def direct():
+            call("seg_conv_wgrad", dy.data_ptr(), Cout, x.data_ptr(), Cin, N, H, W, Cin, H, W, Cout, 3, 1, 1,
+                 part.data_ptr(), sp, s)
+            call("seg_conv_wgrad_reduce", part.data_ptr(), sp, dw.data_ptr(), Cout, Cin, 3, 0, 0, s)
+        spw = query("seg_conv_wino_wgrad_splits", N, H, W, Cin, Cout)
+        pw = torch.empty(spw * 16 * Cout * Cin, device="cuda")
+
+        def wino():
+            call("seg_conv_wino_wgrad", dy.data_ptr(), Cout, x.data_ptr(), Cin, N, H, W, Cin, Cout, pw.data_ptr(),
+                 spw, s)
+            call("seg_conv_wino_wgrad_reduce", pw.data_ptr(), spw, dw.data_ptr(), Cout, Cin, Cin, 0, s)
+        t_d, t_w = timeit(direct), timeit(wino)
+        print(f"{name:6s} wgrad direct {t_d * 1e6:7.1f} us ({fl / t_d / 1e12:5.1f} TF/s)  wino {t_w * 1e6:7.1f} us "
+              f"({fl / t_w / 1e12:5.1f})  speedup {t_d / t_w:4.2f}  splits {sp}/{spw}", flush=True)
 
 
 if __name__ == "__main__":

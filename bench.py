@@ -54,32 +54,35 @@ def parse():
     ap.add_argument("--workload", choices=("train", "infer"), default="train",
                     help="train: BASELINE configs[1] (the headline); infer: configs[3], inference.py's per-frame path")
     ap.add_argument("--frames", type=int, default=500, help="timed frames of --workload infer")
+    ap.add_argument("--model", choices=("MobileNetV2UNet", "UNet"), default="MobileNetV2UNet",
+                    help="UNet = BASELINE configs[4] shape family (use --height 512 --width 1024 --batch 8)")
     return ap.parse_args()
 
 
 def cpu_baseline(args):
     """The oracle (torch CPU, all host cores) on a bounded sample of the same workload."""
     from oracle import segref
-    from seg_amd import MobileNetV2UNet, deterministic_init, synthetic_batch
+    import seg_amd
+    from seg_amd import deterministic_init, synthetic_batch
     threads = os.cpu_count() or 1
     aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else threads
     threads = min(threads, aff, int(os.environ.get("OMP_NUM_THREADS", aff)))
     torch.set_num_threads(threads)
-    model = deterministic_init(MobileNetV2UNet(args.classes), seed=0)
+    model = deterministic_init(getattr(seg_amd, args.model)(args.classes), seed=0)
     p = segref.canonical_state(model.state_dict())
-    bs = 4
+    bs = 4 if args.model == "MobileNetV2UNet" else 1
     x, y = synthetic_batch(bs, args.height, args.width, args.classes, seed=1)
-    segref.adam_steps("MobileNetV2UNet", p, [(x, y)])  # warm-up step
+    segref.adam_steps(args.model, p, [(x, y)])  # warm-up step
     t0 = time.perf_counter()
     steps = 0
     while True:
-        segref.adam_steps("MobileNetV2UNet", p, [(x, y)])
+        segref.adam_steps(args.model, p, [(x, y)])
         steps += 1
         if time.perf_counter() - t0 > args.cpu_seconds:
             break
     dt = time.perf_counter() - t0
     return {"value": round(steps * bs / dt, 3), "unit": "images/s", "cores": threads, "kind": "port",
-            "sample": f"oracle/segref.py MobileNetV2UNet fwd+bwd+Adam, bs={bs}, {args.height}x{args.width}, "
+            "sample": f"oracle/segref.py {args.model} fwd+bwd+Adam, bs={bs}, {args.height}x{args.width}, "
                       f"{steps} timed steps ({dt:.1f} s) after 1 warm-up, torch CPU fp32"}
 
 
@@ -157,9 +160,10 @@ def main():
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
 
-    from seg_amd import MobileNetV2UNet, deterministic_init, synthetic_batch
+    import seg_amd
+    from seg_amd import deterministic_init, synthetic_batch
     from seg_amd import engine
-    model = deterministic_init(MobileNetV2UNet(args.classes), seed=0).to(dev).train()
+    model = deterministic_init(getattr(seg_amd, args.model)(args.classes), seed=0).to(dev).train()
     if dist:
         from seg_amd.ddp import DataParallel
         model = DataParallel(model)
@@ -243,13 +247,14 @@ def main():
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
             cpu = cpu_baseline(args)
-        line = {"metric": "images/sec fwd+bwd MobileNetV2UNet 256x512 bs=32/GPU",
+        cfg = "BASELINE configs[1]" if args.model == "MobileNetV2UNet" else "BASELINE configs[4] shape, f32"
+        line = {"metric": f"images/sec fwd+bwd {args.model} {args.height}x{args.width} bs={args.batch}/GPU",
                 "value": round(value, 2), "unit": "images/s", "n_gpus": world, "steps": args.steps,
                 "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 3), "higher_is_better": True,
                 "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
-                "config": {"workload": f"MobileNetV2UNet {args.classes}-class fwd+bwd+Adam, "
-                                       f"{args.height}x{args.width}, bs={args.batch}/GPU (BASELINE configs[1])",
-                           "model": "MobileNetV2UNet", "global_batch": args.batch * world,
+                "config": {"workload": f"{args.model} {args.classes}-class fwd+bwd+Adam, "
+                                       f"{args.height}x{args.width}, bs={args.batch}/GPU ({cfg})",
+                           "model": args.model, "global_batch": args.batch * world,
                            "image": [args.height, args.width], "parallelism": f"dp{world}"},
                 "final_loss": round(final_loss, 5),
                 "roofline": roof, "cpu_baseline": cpu}

@@ -16,5 +16,7 @@ for step in "$@"; do
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run bench 600 python bench.py --steps 10 --warmup 3 ;;
     benchq) run benchq 600 python bench.py --steps 5 --warmup 2 --no-cpu-baseline ;;
+    unet) run unet 600 python bench.py --model UNet --height 512 --width 1024 --batch 8 --steps 3 --warmup 2 ;;
+    infer) run infer 600 python bench.py --workload infer --frames 300 --cpu-seconds 8 ;;
   esac
 done

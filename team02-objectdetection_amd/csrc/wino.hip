@@ -491,17 +491,19 @@ __global__ __launch_bounds__(256) void wino_wgrad_reduce_kernel(const float* __r
 }  // namespace
 
 // Use Winograd for this stride-1 pad-1 3x3 conv?  (1 = yes.)  The transforms
-// cost a round trip of M (16 x tiles x Cout floats) through HBM per GEMM FLOP
-// in proportion to 1/Cin, so Winograd wins for deep inputs.  Boundary measured on
-// MI355X with tools/winobench.py over the MobileNetV2UNet decoder (fwd / dgrad
-// speedups: Cin 1344: 2.06, Cin 256: 1.29-1.51, Cin 288: 1.52, Cin 128 with
-// Cout 128: 1.25 but Cout 288: 1.00, Cin 152 at 65536 tiles: 0.88, Cin <= 80:
-// 0.36-0.70).  Deterministic: the choice depends on the shape only.
+// cost a round trip of M (16 x tiles x Cout floats) through HBM whose share of
+// the work falls as 1/Cin, and the 4-pixel input transform in the GEMM loader
+// needs enough output columns to amortise, so Winograd wins for deep convs.
+// Boundary measured on MI355X with tools/winobench.py (speedup over the direct
+// implicit GEMM; MobileNetV2UNet decoder and UNet 512x1024 shapes):
+//   Cin x Cout  1344x256 2.02 | 256x1344 1.30 | 256x256 1.37-1.50 | 288x128 1.52
+//   512x128 1.44 | 128x256 1.28 | 128x128 1.11-1.24 | 128x288 1.00 | 128x512 1.10
+//   256x64 1.04 | 152x64 0.91 | 64x152 0.62 | 64x64 0.70-0.79 | Cin or Cout 32/80 0.36-0.54
+// Deterministic: the choice depends on the shape only.
 SEG_API int seg_conv_wino_pick(int N, int H, int W, int Cin, int Cout) {
-  if ((H & 1) || (W & 1) || (Cin & 3) || (Cout & 3) || Cin < 32 || Cout < 32) return 0;
-  const long T = (long)N * (H / 2) * (W / 2);
-  if (Cin >= 192) return 1;
-  return (Cin >= 128 && Cout <= Cin && T <= 16384) ? 1 : 0;
+  if ((H & 1) || (W & 1) || (Cin & 3) || (Cout & 3) || N <= 0) return 0;
+  if (Cin >= 256 && Cout >= 128) return 1;
+  return (Cin >= 128 && Cout >= 128 && Cout <= 2 * Cin) ? 1 : 0;
 }
 
 // Number of 256-pixel row tiles of seg_conv_wino's BN partials.
@@ -533,10 +535,12 @@ SEG_API int seg_conv_wino(const float* in, long ldin, int N, int H, int W, int C
 }
 
 // Use the Winograd weight gradient?  Measured on MI355X (tools/winobench.py):
-// 1.19x at Cin 1344 / Cout 256, 1.29x at 256 / 256, <= 1.08x or slower below.
+// 1.19-1.33x for Cin, Cout >= 128 at 65536+ tiles (UNet 512x1024) and for
+// Cin, Cout >= 256 at 4096 tiles; 0.97-1.08x for 128-288 channels at 16384 tiles.
 SEG_API int seg_conv_wino_wgrad_pick(int N, int H, int W, int Cin, int Cout) {
   if ((H & 1) || (W & 1) || (Cin & 3) || (Cout & 3)) return 0;
-  return (Cin >= 256 && Cout >= 256) ? 1 : 0;
+  const long T = (long)N * (H / 2) * (W / 2);
+  return (Cin >= 128 && Cout >= 128 && (T >= 65536 || (Cin >= 256 && Cout >= 256))) ? 1 : 0;
 }
 
 // Split count of seg_conv_wino_wgrad (partial slabs of 16 * Cout * Cin_pad floats).

@@ -221,15 +221,27 @@ def main():
         prof = os.path.join(REPO, "profiles", "latest_roofline.json")
         if os.path.exists(prof):
             with open(prof) as fh:
-                fam = json.load(fh)["families"].get("igemm3", {})
-            traffic = fam.get("hbm_bytes_per_launch")
+                fam = json.load(fh)["families"].get("conv3", {})
+            traffic = fam.get("hbm_bytes_per_op")
+        # algorithmic bytes of the family: every 3x3 conv's input and output tensors once
+        # (fwd: X + Y, dgrad: dY + dX), fp32, averaged over its launches
+        prog = engine.get_program(getattr(model, "module", model), args.batch, args.height, args.width)
+        abytes = []
+        for op in prog.ops:
+            if isinstance(op, engine.ConvOp) and op.kind == "igemm" and op.ks == 3:
+                xy = 4 * (op.inp.M * op.cin + op.y.M * op.cout)
+                abytes.append(xy)
+                if not op.first:
+                    abytes.append(xy)
+        alg_bytes = sum(abytes) / max(len(abytes), 1)
         wf, ws, wn = family({"igemm3_wgrad", "wino3_wgrad"})
         af, as_, an = family({k for k, _, _ in rec})
         roof = {"bound": "mfma", "achieved": round(achieved, 2), "peak": F32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
                 "frac": round(achieved / F32_MFMA_PEAK_TFLOPS, 4),
                 "traffic": round(traffic) if traffic else None,
                 "traffic_source": "profiles/latest_roofline.json: rocprofv3 PMC (2*FETCH_SIZE+WRITE_SIZE)*1KiB "
-                                  "per igemm3 launch" if traffic else None,
+                                  "of the conv3 family per step / 17 conv ops" if traffic else None,
+                "algorithmic_bytes_per_launch": round(alg_bytes),
                 "kernel": "dense 3x3 conv fwd + dgrad on f32 MFMA: igemm_conv_kernel<*,*,*,*,3,*> (implicit GEMM) "
                           "and, for the deep decoder convs, wino_gemm_kernel + wino_out_kernel (Winograd F(2x2,3x3): "
                           "2.25x fewer executed MFMA FLOPs than the algorithmic count used here)",

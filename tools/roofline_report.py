@@ -18,12 +18,13 @@ import statistics
 import sys
 from collections import defaultdict
 
-FAMILIES = {
-    "igemm3": re.compile(r"igemm_conv_kernel<\d+, \d+, \d+, \d+, 3, \d+>"),
-    "igemm1": re.compile(r"igemm_conv_kernel<\d+, \d+, \d+, \d+, 1, \d+>"),
-    "wgrad3": re.compile(r"wgrad_kernel<\d+, \d+, \d+, \d+, 3>"),
+FAMILIES = {  # "conv3" = the dense 3x3 conv forward + data gradient (bench.py's roofline kernel family)
+    "conv3": re.compile(r"igemm_conv_kernel<\d+, \d+, \d+, \d+, 3, \d+|wino_gemm_kernel|wino_out_kernel"),
+    "igemm1": re.compile(r"igemm_conv_kernel<\d+, \d+, \d+, \d+, 1, \d+"),
+    "wgrad3": re.compile(r"wgrad_kernel<\d+, \d+, \d+, \d+, 3>|wino_wgrad"),
     "wgrad1": re.compile(r"wgrad_kernel<\d+, \d+, \d+, \d+, 1>"),
 }
+OPS_PER_STEP = {"conv3": 17}  # MobileNetV2UNet bs=32: 8 decoder convs fwd + 8 dgrad + the stem fwd
 
 
 def family(name):
@@ -70,6 +71,11 @@ def main(prof_dir, pmc_dir, steps, out_prefix):
         out["families"][f] = {"calls_per_step": d["calls"] / steps, "ms_per_step": d["ns"] / 1e6 / steps,
                               "avg_launch_us": avg_us, "hbm_bytes_per_launch": hbm,
                               "symbols": d["symbols"]}
+        if f in OPS_PER_STEP and fetch and write:
+            # per conv op (a Winograd op is two kernels): family bytes per step / ops per step
+            per_step = (2 * sum(fetch) + sum(write)) * 1024 / (len(fetch) / (d["calls"] / steps))
+            out["families"][f]["ops_per_step"] = OPS_PER_STEP[f]
+            out["families"][f]["hbm_bytes_per_op"] = per_step / OPS_PER_STEP[f]
         lines.append(f"| {f} | {d['calls'] / steps:.0f} | {d['ns'] / 1e6 / steps:.2f} | {d['ns'] / total:.1%} | "
                      f"{avg_us:.1f} | {hbm / 1e6 if hbm else float('nan'):.1f} MB |")
     lines += ["", "Top kernels:", "", "| kernel | calls | avg us | total ms |", "|---|---|---|---|"]

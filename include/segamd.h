@@ -165,6 +165,12 @@ int seg_bn_backward(const float* da, long ldda, const float* y, long ldy, long M
                     const float* gamma, const float* mean, const float* invstd,
                     const float* scale, const float* shift, int act,
                     float* dgamma, float* dbeta, float* work, float* dy, long lddy, hipStream_t stream);
+/* The reduction half of seg_bn_backward (dgamma, dbeta and coef[3][C]) for a
+ * consumer that applies the BN backward on load (seg_pw_bwd_fused). */
+int seg_bn_backward_coef(const float* da, long ldda, const float* y, long ldy, long M, int C,
+                         const float* gamma, const float* mean, const float* invstd, const float* scale,
+                         const float* shift, int act, float* dgamma, float* dbeta, float* work, float* coef,
+                         hipStream_t stream);
 int seg_bn_eval_backward(const float* da, long ldda, const float* y, long ldy, long M, int C,
                          const float* scale, const float* shift, int act, float* dy, long lddy,
                          hipStream_t stream);
@@ -174,6 +180,20 @@ int seg_colsum(const float* y, long ldy, long M, int C, float* work, float* out,
 /* gradient fan-in (residual add of InvertedResidual, skip reuse): out = a (+ b) */
 int seg_add(const float* a, long lda, const float* b, long ldb, long M, int C, float* out, long ldout,
             hipStream_t stream);
+
+/* Fused backward of a 1x1 conv + train-mode BN (+ act) -- torchvision's
+ * InvertedResidual expand/project convs: reads dA, y and x once per pixel and
+ * produces dx (+ addend) and dW partial slabs [blocks][Cout][r4(Cin)]
+ * (seg_conv_wgrad_reduce mode 0, ks 1), with dY = coef0*(dz - coef1 - (y-mean)*coef2),
+ * dz = dA * act'(y*scale+shift) computed on load.  wkd = seg_pack_conv_weight mode 1.
+ * seg_pw_bwd_fused_ok: channel limits (<= 192 each, LDS <= 96 KiB);
+ * seg_pw_bwd_blocks: the slab count for M pixels. */
+int seg_pw_bwd_fused_ok(int Cin, int Cout);
+int seg_pw_bwd_blocks(long M);
+int seg_pw_bwd_fused(const float* da, long ldda, const float* y, long ldy, const float* x, long ldx,
+                     const float* wkd, int ldkd, const float* scale, const float* shift, const float* mean,
+                     const float* coef, int act, const float* add, long ldadd, float* dx, long lddx,
+                     float* part, int blocks, long M, int Cin, int Cout, hipStream_t stream);
 
 /* ---- resampling (aten upsample_bilinear2d(+_backward), max_pool2d) ---------- */
 /* nn.Upsample(x2, bilinear) of `up` (src/unet.py:97,101; ac = 0) into the concat

@@ -392,6 +392,24 @@ SEG_API int seg_bn_backward(const float* da, long ldda, const float* y, long ldy
   SEG_RET_LAST();
 }
 
+// The reduction half of seg_bn_backward: dgamma/dbeta and coef[3][C] = (g*inv,
+// mean(dz), mean(dz*xhat)*inv) for a fused consumer (seg_pw_bwd_fused) that
+// applies dY = coef0 * (dz - coef1 - (y - mean) * coef2) on load.
+// `work` >= seg_chan_workspace_floats(M,C).
+SEG_API int seg_bn_backward_coef(const float* da, long ldda, const float* y, long ldy, long M, int C,
+                                 const float* gamma, const float* mean, const float* invstd, const float* scale,
+                                 const float* shift, int act, float* dgamma, float* dbeta, float* work, float* coef,
+                                 hipStream_t stream) {
+  if ((C & 3) || (ldy & 3) || (ldda & 3)) return (int)hipErrorInvalidValue;
+  const int rpb = rows_per_block_for(M);
+  const int nblk = seg_cdiv(M, rpb);
+  hipLaunchKernelGGL(chan_partial_kernel<1>, dim3(nblk), dim3(256), 0, stream, y, ldy, da, ldda, (int)M, C, scale,
+                     shift, mean, act, work, rpb);
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(C), dim3(256), 0, stream, work, nblk, M, C, gamma,
+                     invstd, dgamma, dbeta, coef);
+  SEG_RET_LAST();
+}
+
 SEG_API int seg_bn_eval_backward(const float* da, long ldda, const float* y, long ldy, long M, int C,
                                  const float* scale, const float* shift, int act, float* dy, long lddy,
                                  hipStream_t stream) {

@@ -50,6 +50,11 @@ PROTOTYPES = {
     "seg_bn_eval_coef": (_I, [_V, _V, _V, _V, _F, _I, _V, _V, _V]),
     "seg_bn_apply": (_I, [_V, _L, _L, _I, _V, _V, _I, _V, _L, _V, _L, _V]),
     "seg_bn_backward": (_I, [_V, _L, _V, _L, _L, _I, _V, _V, _V, _V, _V, _I, _V, _V, _V, _V, _L, _V]),
+    "seg_bn_backward_coef": (_I, [_V, _L, _V, _L, _L, _I, _V, _V, _V, _V, _V, _I, _V, _V, _V, _V, _V]),
+    "seg_pw_bwd_fused_ok": (_I, [_I, _I]),
+    "seg_pw_bwd_blocks": (_I, [_L]),
+    "seg_pw_bwd_fused": (_I, [_V, _L, _V, _L, _V, _L, _V, _I, _V, _V, _V, _V, _I, _V, _L, _V, _L, _V, _I, _L, _I, _I,
+                              _V]),
     "seg_bn_eval_backward": (_I, [_V, _L, _V, _L, _L, _I, _V, _V, _I, _V, _L, _V]),
     "seg_colsum": (_I, [_V, _L, _L, _I, _V, _V, _I, _V]),
     "seg_add": (_I, [_V, _L, _V, _L, _L, _I, _V, _L, _V]),

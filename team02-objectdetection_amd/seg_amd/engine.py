@@ -22,6 +22,7 @@ fused addend.
 from __future__ import annotations
 
 import ctypes
+import os
 
 import torch
 from torch import nn
@@ -52,6 +53,13 @@ class KernelTimer:
 
 
 TIMER: KernelTimer | None = None
+
+# The fused 1x1-conv + BN backward (seg_pw_bwd_fused) reads dA, y and x once instead of
+# five passes, but measured slower than the separate kernels on MI355X in round 1
+# (1.73 vs ~1.3 ms/step over the high-resolution 1x1 layers: one 32-pixel tile in
+# flight per block leaves HBM latency exposed).  Parity-tested (tests/test_gpu_ops.py);
+# off unless SEG_PW_FUSED=1.
+PW_FUSED = os.environ.get("SEG_PW_FUSED", "0") == "1"
 
 
 def _timed_call(kind, flops, name, *args):
@@ -107,6 +115,8 @@ class ConvOp:
         # Winograd F(2x2,3x3) (seg_conv_wino) for the forward / data gradient, chosen by
         # seg_conv_wino_pick at pack time; U_f [16][Cout][cin_pad], U_d [16][Cin][r4(Cout)]
         self.wino_f = self.wino_d = self.wino_w = False
+        # fused 1x1 + BN backward (seg_pw_bwd_fused), decided at pack time
+        self.pw_fused = False
         self.ks = conv.kernel_size[0]
         self.stride = conv.stride[0]
         self.pad = conv.padding[0]
@@ -214,6 +224,34 @@ class ConvOp:
              o.H, o.W, self.cout, self.ks, self.stride, self.pad, rt.ptr(r) if r is not None else None,
              r.ld if r is not None else 0, None, act, work.data_ptr() if work is not None else None, splits, s)
 
+    def _backward_pw_fused(self, rt, dA):
+        """1x1 conv + train BN backward in one pass over dA, y, x (seg_pw_bwd_fused): the BN
+        reduction first (seg_bn_backward_coef), then dx (+ pending addend) and the dW slabs."""
+        s, y, i = rt.stream, self.y, self.inp
+        if not rt.training:
+            raise NotImplementedError("backward through eval-mode BatchNorm is not supported")
+        C, M = self.cout, y.M
+        st = rt.saved[id(self)]
+        mean, invstd, scale, shift = (st[k * C:(k + 1) * C] for k in range(4))
+        work = rt.tmp(query("seg_chan_workspace_floats", M, C))
+        coef = rt.tmp(3 * C)
+        call("seg_bn_backward_coef", rt.gptr(dA), dA.ld, rt.ptr(y), y.ld, M, C, self.bn.weight.data_ptr(),
+             mean.data_ptr(), invstd.data_ptr(), scale.data_ptr(), shift.data_ptr(), self.act,
+             rt.grad_param(self.bn.weight), rt.grad_param(self.bn.bias), work.data_ptr(), coef.data_ptr(), s)
+        if self.res is not None:
+            rt.add_pending(self.res, dA)
+        gw = rt.grad_param(self.conv.weight)
+        blocks = query("seg_pw_bwd_blocks", M)
+        part = rt.tmp(blocks * C * self.cin_pad)
+        add_ptr, add_ld = rt.begin_write_add(i)
+        _timed_call("pw_bwd", 2 * self.flops(), "seg_pw_bwd_fused", rt.gptr(dA), dA.ld, rt.ptr(y), y.ld, rt.ptr(i),
+                    i.ld, self.wk_d.data_ptr(), self.ldk_d, scale.data_ptr(), shift.data_ptr(), mean.data_ptr(),
+                    coef.data_ptr(), self.act, add_ptr, add_ld, rt.gptr(i), i.ld, part.data_ptr(), blocks, M,
+                    self.cin, C, s)
+        call("seg_conv_wgrad_reduce", part.data_ptr(), blocks, gw, C, self.cin, 1, 0, 0, s)
+        rt.params_done(self.params())
+        rt.mark_written(i)
+
     def _in_xform(self, rt):
         """(scale, shift, act) of the producer's lazy BN for this op's input loads, or (None, None, 0)."""
         xf = self.xform
@@ -226,6 +264,8 @@ class ConvOp:
     def backward(self, rt):
         s, y = rt.stream, self.y
         dA = rt.grad_of(self.out)
+        if self.pw_fused:
+            return self._backward_pw_fused(rt, dA)
         if self.bn is not None:
             if not rt.training:
                 raise NotImplementedError("backward through eval-mode BatchNorm is not supported")
@@ -410,6 +450,9 @@ class Program:
                 max_elems = max(max_elems, 9 * op.cout)
                 continue
             y = op.y
+            op.pw_fused = (PW_FUSED and op.ks == 1 and op.bn is not None and op.conv.bias is None and not op.first
+                           and op.cin % 4 == 0 and op.conv.weight.requires_grad
+                           and bool(query("seg_pw_bwd_fused_ok", op.cin, op.cout)))
             wino_ok = op.ks == 3 and op.stride == 1 and op.pad == 1
             op.wino_f = wino_ok and bool(query("seg_conv_wino_pick", y.N, y.H, y.W, op.cin_pad, op.cout))
             op.wino_d = wino_ok and not op.first and bool(query("seg_conv_wino_pick", y.N, y.H, y.W, r4(op.cout),

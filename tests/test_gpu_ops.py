@@ -492,3 +492,67 @@ def test_conv_wino_wgrad(N, Cin, Cout, H, W):
         dw2 = dw.clone()
         call("seg_conv_wino_wgrad_reduce", p2.data_ptr(), s2, dw2.data_ptr(), Cout, Cin, cin4, 1, S())
         assert rel(dw2, 2 * wr.grad) < 1e-5
+
+
+@pytest.mark.parametrize("M,Cin,Cout,act,res", [(5000, 16, 96, 2, False), (3333, 96, 24, 0, True),
+                                                (4096, 24, 144, 2, False), (2111, 144, 32, 0, True),
+                                                (777, 32, 192, 2, False), (1024, 192, 32, 0, False)])
+def test_pw_bwd_fused(M, Cin, Cout, act, res):
+    """seg_bn_backward_coef + seg_pw_bwd_fused (+ wgrad reduce) == torch autograd of
+    act(BN_train(conv1x1(x))) for dx (with addend) and dW."""
+    assert query("seg_pw_bwd_fused_ok", Cin, Cout) == 1
+    x = gen(M, Cin, seed=51)
+    w = gen(Cout, Cin, 1, 1, seed=52) * (2.0 / Cin) ** 0.5
+    g, bta = gen(Cout, seed=53).abs() + 0.5, gen(Cout, seed=54)
+    xr = x.clone().requires_grad_(True)
+    wr = w.clone().requires_grad_(True)
+    yraw = (xr @ wr.view(Cout, Cin).t())
+    z = F.batch_norm(yraw.t().unsqueeze(0), None, None, g, bta, True, 0.1, 1e-5).squeeze(0).t()
+    a_out = F.hardtanh(z, 0.0, 6.0) if act == 2 else z
+    dA = gen(M, Cout, seed=55)
+    a_out.backward(dA)
+    s = S()
+    xg = x.to(DEV).contiguous()
+    yg = yraw.detach().to(DEV).contiguous()
+    dAg = dA.to(DEV)
+    # forward statistics as the engine keeps them: mean, invstd, scale, shift
+    y64 = yraw.detach().double()
+    mean = y64.mean(0).float()
+    invstd = (1 / torch.sqrt(y64.var(0, unbiased=False) + 1e-5)).float()
+    scale = g * invstd
+    shift = bta - mean * g * invstd
+    mg, ig, scg, shg, gg = (t.to(DEV) for t in (mean, invstd, scale, shift, g))
+    work = torch.empty(query("seg_chan_workspace_floats", M, Cout), device=DEV)
+    coef = torch.empty(3 * Cout, device=DEV)
+    dgam, dbet = torch.empty(Cout, device=DEV), torch.empty(Cout, device=DEV)
+    call("seg_bn_backward_coef", dAg.data_ptr(), Cout, yg.data_ptr(), Cout, M, Cout, gg.data_ptr(), mg.data_ptr(),
+         ig.data_ptr(), scg.data_ptr(), shg.data_ptr(), act, dgam.data_ptr(), dbet.data_ptr(), work.data_ptr(),
+         coef.data_ptr(), s)
+    kin = r4(Cout)
+    wkd = torch.empty(Cin * kin, device=DEV)
+    call("seg_pack_conv_weight", wr.detach().to(DEV).data_ptr(), wkd.data_ptr(), Cout, Cin, 1, kin, 1, kin, s)
+    blocks = query("seg_pw_bwd_blocks", M)
+    part = torch.empty(blocks * Cout * r4(Cin), device=DEV)
+    addend = gen(M, Cin, seed=56) if res else None
+    addg = addend.to(DEV) if res else None
+    dx = torch.full((M, Cin), float("nan"), device=DEV)
+    call("seg_pw_bwd_fused", dAg.data_ptr(), Cout, yg.data_ptr(), Cout, xg.data_ptr(), Cin, wkd.data_ptr(), kin,
+         scg.data_ptr(), shg.data_ptr(), mg.data_ptr(), coef.data_ptr(), act, addg.data_ptr() if res else None,
+         Cin if res else 0, dx.data_ptr(), Cin, part.data_ptr(), blocks, M, Cin, Cout, s)
+    dw = torch.empty(Cout, Cin, 1, 1, device=DEV)
+    call("seg_conv_wgrad_reduce", part.data_ptr(), blocks, dw.data_ptr(), Cout, Cin, 1, 0, 0, s)
+    # the unfused HIP path on the same inputs: seg_bn_backward -> igemm data gradient + split-K wgrad
+    dY = torch.empty(M, r4(Cout), device=DEV)
+    work2 = torch.empty(query("seg_chan_workspace_floats", M, Cout) + 3 * Cout, device=DEV)
+    d2g, d2b = torch.empty(Cout, device=DEV), torch.empty(Cout, device=DEV)
+    call("seg_bn_backward", dAg.data_ptr(), Cout, yg.data_ptr(), Cout, M, Cout, gg.data_ptr(), mg.data_ptr(),
+         ig.data_ptr(), scg.data_ptr(), shg.data_ptr(), act, d2g.data_ptr(), d2b.data_ptr(), work2.data_ptr(),
+         dY.data_ptr(), dY.shape[1], s)
+    dx2 = torch.empty(M, Cin, device=DEV)
+    call("seg_conv_igemm", dY.data_ptr(), dY.shape[1], 1, 1, M, kin, wkd.data_ptr(), kin, None, dx2.data_ptr(), Cin,
+         1, M, Cin, 1, 1, 0, addg.data_ptr() if res else None, Cin if res else 0, None, s)
+    assert rel(dx, dx2) < 1e-5
+    torch.testing.assert_close(dgam, d2g, rtol=0, atol=0)
+    ref_dx = xr.grad + (addend if res else 0)
+    assert rel(dx2, ref_dx) < 1e-2 and rel(dx, ref_dx) < 1e-2  # mask flips at ReLU6 thresholds dominate here
+    assert rel(dw, wr.grad) < 1e-2

@@ -248,6 +248,25 @@ int seg_preprocess_bgr(const unsigned char* frame, int N, int Hf, int Wf, long r
 int seg_argmax_nearest(const float* low, long ld, int N, int H, int W, int C, int Hm, int Wm,
                        unsigned char* mask, int Hf, int Wf, hipStream_t stream);
 
+/* ---- GPU augmentation (the readers' albumentations pipeline,
+ *      src/BDD100KDataset.py:38-52) ---------------------- */
+/* Resize a batch [N][Hs][src_row] of uint8 images (C = 3: cv2 INTER_LINEAR 8-bit)
+ * or class masks (C = 1: INTER_NEAREST, then lut[v] if lut != NULL) to [N][H][W][C]. */
+int seg_resize_u8(const unsigned char* src, int N, int Hs, int Ws, long src_row, unsigned char* dst, int H,
+                  int W, int C, const unsigned char* lut, hipStream_t stream);
+/* Per-sample flip + ShiftScaleRotate (inverse affine, BORDER_REFLECT_101) +
+ * brightness/contrast + Normalize + ToTensorV2: img [N][H][W][3] u8, mask
+ * [N][H][W] u8 -> x [N][3][H][W] f32, y [N][H][W] int64.  params: DEVICE array of
+ * seg_aug_param; mean255/rstd255: 255*mean and 1/(255*std) per channel. */
+typedef struct seg_aug_param {
+  float m[6];
+  float alpha, beta;
+  int flip, warp, bc, pad_;
+} seg_aug_param;
+int seg_augment(const unsigned char* img, const unsigned char* mask, int N, int H, int W, const void* params,
+                float mean_r, float mean_g, float mean_b, float rstd_r, float rstd_g, float rstd_b, float* x,
+                long long* y, hipStream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -18,6 +18,7 @@ from __future__ import annotations
 
 import os
 
+import numpy as np
 import torch
 from torch import nn
 
@@ -46,8 +47,12 @@ def compute_loss(model, criterion, inputs, targets):
 
 
 def train_one_epoch(model, train_loader, criterion, optimizer, device, epoch: int = 0, epochs: int = 1,
-                    progress: bool = True) -> float:
-    """One pass over `train_loader`; returns the mean batch loss (src/train.py:31-44)."""
+                    progress: bool = True, augment=None) -> float:
+    """One pass over `train_loader`; returns the mean batch loss (src/train.py:31-44).
+
+    augment: optional seg_amd.augment.GpuAugment -- the loader then yields decoded
+    uint8 batches (images [N,Hs,Ws,3] RGB, masks [N,Hs,Ws] raw class ids) and the
+    readers' albumentations pipeline runs on the GPU."""
     model.train()
     train_loss = 0.0
     it = train_loader
@@ -59,6 +64,10 @@ def train_one_epoch(model, train_loader, criterion, optimizer, device, epoch: in
     for inputs, targets in it:
         inputs = inputs.to(device, non_blocking=True)
         targets = targets.to(device, non_blocking=True)
+        if augment is not None:  # per-(rank, epoch, batch) parameter stream
+            rank = torch.distributed.get_rank() if not _is_rank0() else 0
+            rng = np.random.Generator(np.random.PCG64([rank, epoch, nb]))
+            inputs, targets = augment(inputs, targets, rng=rng)
         optimizer.zero_grad()
         loss = compute_loss(model, criterion, inputs, targets)
         loss.backward()
@@ -76,11 +85,16 @@ def train_one_epoch(model, train_loader, criterion, optimizer, device, epoch: in
 
 
 def train_model(model, train_loader, criterion, optimizer, device, epochs=10,
-                checkpoint_pattern: str | None = "Models/obj/obj_MOB_1_epoch_{epoch}.pth", progress: bool = True):
+                checkpoint_pattern: str | None = "Models/obj/obj_MOB_1_epoch_{epoch}.pth", progress: bool = True,
+                augment=None):
     """Train for `epochs` epochs (src/train.py:6-79)."""
     best_val_loss = float("inf")  # validation is disabled in the reference (src/train.py:46-76)
     for epoch in range(epochs):
-        avg_train_loss = train_one_epoch(model, train_loader, criterion, optimizer, device, epoch, epochs, progress)
+        sampler = getattr(train_loader, "sampler", None)
+        if hasattr(sampler, "set_epoch"):
+            sampler.set_epoch(epoch)  # DistributedWeightedSampler: a new shared draw per epoch
+        avg_train_loss = train_one_epoch(model, train_loader, criterion, optimizer, device, epoch, epochs, progress,
+                                         augment)
         if _is_rank0():
             print(f"  Training Loss: {avg_train_loss:.4f}")
             if checkpoint_pattern:

@@ -116,6 +116,44 @@ __global__ void up_bwd_kernel(const float* __restrict__ dout, long ldout, int N,
   }
 }
 
+// Exact x2, align_corners=False, NHWC (every decoder `up`): the output rows that
+// sample input row h are 2h-1 .. 2h+2 with weights 0.25, 0.75, 0.75, 0.25 (the
+// values lin_index produces; at the borders the clamped taps fold into 1.0), so
+// the gather is 16 loads with constant weights and no index search.
+__global__ __launch_bounds__(256) void up2_bwd_kernel(const float* __restrict__ dout, long ldout, int N, int C,
+                                                      float* __restrict__ din, long ldin, int H, int W,
+                                                      int accumulate) {
+  const int CG = C >> 2, Ho = 2 * H, Wo = 2 * W;
+  const long total = (long)N * H * W * CG;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const long q = i / CG;
+    const int c = (int)(i - q * CG) * 4;
+    const int n = (int)(q / ((long)H * W));
+    const int rem = (int)(q - (long)n * H * W);
+    const int h = rem / W, w = rem - h * W;
+    const float wr[4] = {h > 0 ? 0.25f : 0.f, h > 0 ? 0.75f : 1.f, h < H - 1 ? 0.75f : 1.f, h < H - 1 ? 0.25f : 0.f};
+    const float wc[4] = {w > 0 ? 0.25f : 0.f, w > 0 ? 0.75f : 1.f, w < W - 1 ? 0.75f : 1.f, w < W - 1 ? 0.25f : 0.f};
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    const float* base = dout + (long)n * Ho * Wo * ldout + c;
+#pragma unroll
+    for (int a = 0; a < 4; ++a) {
+      const int r = 2 * h - 1 + a;
+      const int rc = r < 0 ? 0 : (r > Ho - 1 ? Ho - 1 : r);  // weight 0 where clamped
+      f32x4 row = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int b = 0; b < 4; ++b) {
+        const int s = 2 * w - 1 + b;
+        const int sc = s < 0 ? 0 : (s > Wo - 1 ? Wo - 1 : s);
+        row += wc[b] * ld4(base + ((long)rc * Wo + sc) * ldout);
+      }
+      acc += wr[a] * row;
+    }
+    float* dst = din + q * ldin + c;
+    if (accumulate) acc += ld4(dst);
+    st4(dst, acc);
+  }
+}
+
 // NHWC low-res -> NCHW full-res (the model's returned logits).
 __global__ void up_fwd_to_nchw_kernel(const float* __restrict__ in, long ldin, int N, int H, int W, int C,
                                       float* __restrict__ out, int Ho, int Wo, float sh, float sw, int ac) {
@@ -246,6 +284,11 @@ SEG_API int seg_upsample_bwd(const float* dout, long ldout, int nchw_grad, int N
   if ((ldin & 3) || (!nchw_grad && (ldout & 3))) return (int)hipErrorInvalidValue;
   const int grid = ew_grid((long)N * H * W * ((C + 3) / 4));
   const float sh = up_scale(H, Ho, ac), sw = up_scale(W, Wo, ac);
+  if (!nchw_grad && !ac && Ho == 2 * H && Wo == 2 * W && !(C & 3)) {
+    hipLaunchKernelGGL(up2_bwd_kernel, dim3(grid), dim3(256), 0, stream, dout, ldout, N, C, din, ldin, H, W,
+                       accumulate);
+    SEG_RET_LAST();
+  }
   if (nchw_grad)
     hipLaunchKernelGGL(up_bwd_kernel<1>, dim3(grid), dim3(256), 0, stream, dout, ldout, N, Ho, Wo, C, din, ldin, H, W,
                        sh, sw, ac, accumulate);

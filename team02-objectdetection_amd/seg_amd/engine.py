@@ -21,6 +21,7 @@ fused addend.
 """
 from __future__ import annotations
 
+import contextlib
 import ctypes
 import os
 
@@ -284,29 +285,42 @@ class ConvOp:
             dY = dA
         dYp = rt.ptr(dY) if dY.buf.startswith("#") else rt.gptr(dY)
         M = y.M
-        # bias gradient
+        # parameter gradients: on the side stream when overlapping (they only read dY and x,
+        # and nothing on the main stream's data-gradient chain waits for them)
+        # gradient tensors handed back to autograd are allocated on the main stream
+        # (they outlive the backward; the side stream only writes into them)
+        for p in (self.conv.weight, self.conv.bias):
+            if p is not None and p.requires_grad:
+                rt.grad_param(p)
+        ctx, sw = rt.fork()
+        with ctx:
+            self._param_grads(rt, dY, dYp, sw)
+        if not self.first:
+            self._dgrad(rt, dY, dYp, s)
+
+    def _param_grads(self, rt, dY, dYp, s):
+        """Bias gradient (column sum of dY), weight gradient (split-K slabs + fixed-order
+        reduce) and the DDP readiness hook, all on stream `s`."""
+        y, M = self.y, self.y.M
         if self.conv.bias is not None and self.conv.bias.requires_grad:
             work = rt.tmp(query("seg_chan_workspace_floats", M, r4(self.cout)))
             call("seg_colsum", dYp, dY.ld, M, self.cout, work.data_ptr(), rt.grad_param(self.conv.bias), 0, s)
-        # weight gradient
         if self.conv.weight.requires_grad:
             gw = rt.grad_param(self.conv.weight)
+            i = self.inp
             if self.kind == "dw":
-                i = self.inp
                 nblk = query("seg_dw_wgrad_blocks", y.N, y.H, y.W, self.cout)
                 part = rt.tmp(nblk * 9 * self.cout)
                 call("seg_dw_wgrad", dYp, dY.ld, rt.ptr(i), i.ld, i.N, i.H, i.W, i.C, *self._in_xform(rt), y.H, y.W,
                      self.stride, part.data_ptr(), s)
                 call("seg_conv_wgrad_reduce", part.data_ptr(), nblk, gw, self.cout, 1, 3, 1, 0, s)
             elif self.wino_w:
-                i = self.inp
                 splits = query("seg_conv_wino_wgrad_splits", y.N, y.H, y.W, self.cin_pad, self.cout)
                 part = rt.tmp(splits * 16 * self.cout * self.cin_pad)
                 _timed_call("wino3_wgrad", self.flops(), "seg_conv_wino_wgrad", dYp, dY.ld, rt.ptr(i), i.ld, y.N, y.H,
                             y.W, self.cin_pad, self.cout, part.data_ptr(), splits, s)
                 call("seg_conv_wino_wgrad_reduce", part.data_ptr(), splits, gw, self.cout, self.cin, self.cin_pad, 0, s)
             else:
-                i = self.inp
                 splits = query("seg_conv_wgrad_splits", M, self.cout, self.cin_pad, self.ks)
                 part = rt.tmp(splits * self.cout * self.ks * self.ks * self.cin_pad)
                 _timed_call(f"igemm{self.ks}_wgrad", self.flops(), "seg_conv_wgrad", dYp, dY.ld, rt.ptr(i), i.ld,
@@ -314,10 +328,10 @@ class ConvOp:
                             part.data_ptr(), splits, s)
                 call("seg_conv_wgrad_reduce", part.data_ptr(), splits, gw, self.cout, self.cin, self.ks, 0, 0, s)
         rt.params_done(self.params())
-        # data gradient
-        if self.first:
-            return
-        i = self.inp
+
+    def _dgrad(self, rt, dY, dYp, s):
+        """Data gradient into the input's gradient region (first writer / fused addend)."""
+        y, i = self.y, self.inp
         if self.kind == "dw":
             acc = rt.begin_write_accumulate(i)
             call("seg_dw_dgrad", dYp, dY.ld, y.N, y.H, y.W, self.cout, self.wk_f.data_ptr(), rt.gptr(i), i.ld, i.H,
@@ -692,6 +706,7 @@ class Run:
         self.grads = {}       # id(param) -> grad tensor
         self.sync = None
         self._tmp_n = 0
+        self.side = None      # side stream of the parameter gradients (backward only)
 
     # pointers
     def ptr(self, a: Act) -> int:
@@ -728,6 +743,22 @@ class Run:
         self._tmp_n += 1
         self.gbufs[name] = self.tmp(n)
         return name
+
+    # streams
+    def fork(self):
+        """(context, stream handle) for work that may run beside the main stream: with
+        overlap on, the side stream first waits for everything issued so far on the main
+        stream; temporaries allocated inside the context belong to the side stream."""
+        if self.side is None:
+            return contextlib.nullcontext(), self.stream
+        ev = torch.cuda.Event()
+        ev.record(self.main)
+        self.side.wait_event(ev)
+        return torch.cuda.stream(self.side), self.side.cuda_stream
+
+    def join(self):
+        if self.side is not None:
+            self.main.wait_stream(self.side)
 
     # gradient-region bookkeeping
     def _covered(self, a: Act) -> bool:
@@ -814,10 +845,31 @@ class Run:
 
     def backward_from_logits(self):
         global LAST_RUN
-        for op in reversed(self.prog.ops):
-            op.backward(self)
+        if OVERLAP:
+            self.main = torch.cuda.current_stream(self.device)
+            self.side = _side_stream(self.device)
+        try:
+            for op in reversed(self.prog.ops):
+                op.backward(self)
+        finally:
+            self.join()
         if DEBUG_KEEP_RUN:
             LAST_RUN = self
+
+
+# Parameter gradients (weight / bias / BN-affine readiness) run on a second HIP stream
+# beside the data-gradient chain: the compute-bound 3x3 weight gradients overlap the
+# memory-bound BatchNorm / depthwise / 1x1 kernels of the main stream.  Results are the
+# same either way (the kernels and their reduction orders do not change).
+OVERLAP = os.environ.get("SEG_OVERLAP", "1") == "1"
+_SIDE = {}
+
+
+def _side_stream(device):
+    st = _SIDE.get(device)
+    if st is None:
+        st = _SIDE[device] = torch.cuda.Stream(device)
+    return st
 
 
 DEBUG_KEEP_RUN = False  # diagnostics: keep the last Run (buffers + gradient buffers)

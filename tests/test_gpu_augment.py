@@ -56,3 +56,21 @@ def test_augment_throughput_smoke():
     ms = a.elapsed_time(b) / 10
     print(f"GPU augmentation bs=32 720x1280 -> 256x512: {ms:.3f} ms/batch = {32 / ms * 1e3:.0f} img/s")
     assert x.shape == (32, 3, 256, 512) and torch.isfinite(x).all()
+
+
+def test_train_model_with_gpu_augment(tmp_path):
+    """train_model(..., augment=GpuAugment) on decoded uint8 batches: the reference loop
+    (src/train.py:31-42) with the readers' augmentation moved to the GPU."""
+    from torch import nn
+    from seg_amd import MobileNetV2UNet, deterministic_init, train_model
+    imgs, masks = batch(4, 90, 160, seed=5)
+    loader = [(torch.from_numpy(imgs[:2]), torch.from_numpy(masks[:2])),
+              (torch.from_numpy(imgs[2:]), torch.from_numpy(masks[2:]))]
+    model = deterministic_init(MobileNetV2UNet(10), seed=3).cuda()
+    opt = torch.optim.Adam(model.parameters(), lr=1.5e-4)
+    before = model.outc.conv[3].weight.detach().clone()
+    train_model(model, loader, nn.CrossEntropyLoss(), opt, "cuda", epochs=1,
+                checkpoint_pattern=str(tmp_path / "ep{epoch}.pth"), progress=False,
+                augment=GpuAugment(64, 128, class_map=BDD100K_CLASS_MAP))
+    assert (tmp_path / "ep1.pth").exists()
+    assert not torch.equal(before, model.outc.conv[3].weight.detach())

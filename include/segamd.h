@@ -55,6 +55,16 @@ int seg_conv_igemm_act(const float* in, long ldin, int N, int H, int W, int Cin,
                        int ks, int stride, int pad,
                        const float* add, long ldadd, float* stat, int act, float* work, int splits,
                        hipStream_t stream);
+/* Data gradient (stride 1) of a conv followed by a train-mode BatchNorm with the BN
+ * backward applied on load: in = dA, y = raw conv output, scale/shift/mean = the
+ * forward BN coefficients, k = [3][Cin] (seg_bn_backward_coef), bn_act = the
+ * activation; out = conv(dY, Wd) + add.  Replaces seg_bn_backward's dY pass +
+ * seg_conv_igemm; needs seg_conv_igemm_bnb_ok(Cin, ks). */
+int seg_conv_igemm_bnb(const float* in, long ldin, int N, int H, int W, int Cin, const float* wk, int ldk,
+                       float* out, long ldout, int Cout, int ks, int pad, const float* add, long ldadd,
+                       const float* y, long ldy, const float* scale, const float* shift, const float* mean,
+                       const float* k, int bn_act, hipStream_t stream);
+int seg_conv_igemm_bnb_ok(int Cin, int ks);
 /* Split-K factor for seg_conv_igemm_act (1 = none): > 1 only when the output tiles
  * cannot fill the 256 CUs (batch-1 inference). */
 int seg_conv_igemm_splits(long M, int Cout, int Cin, int ks);
@@ -77,6 +87,12 @@ int seg_conv_wgrad(const float* dy, long lddy, const float* x, long ldx,
                    int N, int H, int W, int Cin, int Ho, int Wo, int Cout,
                    int ks, int stride, int pad, float* part, int splits, hipStream_t stream);
 
+/* seg_conv_wgrad with dY formed on load from dA (dy) and y (BN backward, as
+ * seg_conv_igemm_bnb; Cout % 4 == 0). */
+int seg_conv_wgrad_bnb(const float* dy, long lddy, const float* x, long ldx, int N, int H, int W, int Cin,
+                       int Ho, int Wo, int Cout, int ks, int stride, int pad, float* part, int splits,
+                       const float* y, long ldy, const float* scale, const float* shift, const float* mean,
+                       const float* k, int bn_act, hipStream_t stream);
 /* dW (PyTorch layout) = fixed-order sum of partial slabs.  mode 0: igemm
  * partials (K runs of round_up(Cin,4) channels), 1: depthwise partials. */
 int seg_conv_wgrad_reduce(const float* part, int splits, float* dw, int Cout, int Cin, int ks,
@@ -177,6 +193,10 @@ int seg_bn_eval_backward(const float* da, long ldda, const float* y, long ldy, l
 /* conv bias gradient: out[c] (+)= sum_r y[r][c] */
 int seg_colsum(const float* y, long ldy, long M, int C, float* work, float* out, int accumulate,
                hipStream_t stream);
+/* seg_colsum of dY formed on load from dA and y (BN backward; C % 4 == 0). */
+int seg_colsum_bnb(const float* da, long ldda, const float* y, long ldy, long M, int C, const float* scale,
+                   const float* shift, const float* mean, const float* k, int bn_act, float* work, float* out,
+                   int accumulate, hipStream_t stream);
 /* gradient fan-in (residual add of InvertedResidual, skip reuse): out = a (+ b) */
 int seg_add(const float* a, long lda, const float* b, long ldb, long M, int C, float* out, long ldout,
             hipStream_t stream);

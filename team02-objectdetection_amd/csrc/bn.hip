@@ -22,11 +22,12 @@ namespace {
 // kind 0: (sum(y-k), sum((y-k)^2)),  k = y[0][c]                   -> BN stats
 // kind 1: (sum(dz),  sum(dz*(y-mean))), dz = dA * act'(y*scale+shift) -> BN backward
 // kind 2: (sum(y), 0)                                               -> bias grad
+// kind 3: (sum(dY), 0), dY = BN backward of (da, y) formed on load     -> bias grad of a BN conv
 template <int KIND>
 __global__ __launch_bounds__(256) void chan_partial_kernel(
     const float* __restrict__ y, long ldy, const float* __restrict__ da, long ldda, int M, int C,
     const float* __restrict__ scale, const float* __restrict__ shift, const float* __restrict__ mean, int act,
-    float* __restrict__ part, int rows_per_block) {
+    float* __restrict__ part, int rows_per_block, SegBnBwd bnb) {
   __shared__ f32x4 red0[256], red1[256];
   const int CG = C >> 2;
   const int TC = CG < 256 ? CG : 256;
@@ -46,6 +47,8 @@ __global__ __launch_bounds__(256) void chan_partial_kernel(
       f32x4 k = {0.f, 0.f, 0.f, 0.f}, sc = k, sh = k;
       if (KIND == 0) k = ld4(y + c);
       if (KIND == 1) { k = ld4(mean + c); sc = ld4(scale + c); sh = ld4(shift + c); }
+      f32x4 cf[6];
+      if (KIND == 3) seg_bnbwd_coef(bnb, c, cf);
       auto step = [&](int r) {
         const f32x4 v = ld4(y + (long)r * ldy + c);
         if (KIND == 0) {
@@ -59,6 +62,9 @@ __global__ __launch_bounds__(256) void chan_partial_kernel(
           for (int j = 0; j < 4; ++j) dz[j] = g[j] * seg_act_mask(v[j] * sc[j] + sh[j], act);
           s0 += dz;
           s1 += dz * (v - k);
+        } else if (KIND == 3) {
+          const f32x4 g = ld4(da + (long)r * ldda + c);
+          s0 += seg_bnbwd4(g, v, cf[0], cf[1], cf[2], cf[3], cf[4], cf[5], bnb.act);
         } else {
           s0 += v;
         }
@@ -261,13 +267,7 @@ __global__ void bn_bwd_apply_kernel(const float* __restrict__ da, long ldda, con
     const f32x4 v = ld4(y + r * ldy + c), g = ld4(da + r * ldda + c);
     const f32x4 sc = ld4(scale + c), sh = ld4(shift + c), mu = ld4(mean + c);
     const f32x4 k1 = ld4(coef + c), k2 = ld4(coef + C + c), k3 = ld4(coef + 2 * C + c);
-    f32x4 o;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const float dz = g[j] * seg_act_mask(v[j] * sc[j] + sh[j], act);
-      o[j] = k1[j] * (dz - k2[j] - (v[j] - mu[j]) * k3[j]);
-    }
-    st4(dy + r * lddy + c, o);
+    st4(dy + r * lddy + c, seg_bnbwd4(g, v, sc, sh, mu, k1, k2, k3, act));
   }
 }
 
@@ -338,7 +338,7 @@ SEG_API int seg_bn_stats(const float* y, long ldy, long M, int C, const float* g
   const int rpb = rows_per_block_for(M);
   const int nblk = seg_cdiv(M, rpb);
   hipLaunchKernelGGL(chan_partial_kernel<0>, dim3(nblk), dim3(256), 0, stream, y, ldy, nullptr, 0L, (int)M, C,
-                     nullptr, nullptr, nullptr, 0, work, rpb);
+                     nullptr, nullptr, nullptr, 0, work, rpb, SegBnBwd{});
   hipLaunchKernelGGL(bn_finalize_kernel, dim3(C), dim3(256), 0, stream, work, nblk, y, M, C, gamma,
                      beta, eps, momentum, running_mean, running_var, num_batches_tracked, mean, invstd, scale, shift);
   SEG_RET_LAST();
@@ -384,7 +384,7 @@ SEG_API int seg_bn_backward(const float* da, long ldda, const float* y, long ldy
   const int nblk = seg_cdiv(M, rpb);
   float* coef = work + (long)nblk * 2 * C;
   hipLaunchKernelGGL(chan_partial_kernel<1>, dim3(nblk), dim3(256), 0, stream, y, ldy, da, ldda, (int)M, C, scale,
-                     shift, mean, act, work, rpb);
+                     shift, mean, act, work, rpb, SegBnBwd{});
   hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(C), dim3(256), 0, stream, work, nblk, M, C, gamma,
                      invstd, dgamma, dbeta, coef);
   hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(ew_grid(M * (C / 4))), dim3(256), 0, stream, da, ldda, y, ldy, M, C,
@@ -404,7 +404,7 @@ SEG_API int seg_bn_backward_coef(const float* da, long ldda, const float* y, lon
   const int rpb = rows_per_block_for(M);
   const int nblk = seg_cdiv(M, rpb);
   hipLaunchKernelGGL(chan_partial_kernel<1>, dim3(nblk), dim3(256), 0, stream, y, ldy, da, ldda, (int)M, C, scale,
-                     shift, mean, act, work, rpb);
+                     shift, mean, act, work, rpb, SegBnBwd{});
   hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(C), dim3(256), 0, stream, work, nblk, M, C, gamma,
                      invstd, dgamma, dbeta, coef);
   SEG_RET_LAST();
@@ -418,6 +418,20 @@ SEG_API int seg_bn_eval_backward(const float* da, long ldda, const float* y, lon
   SEG_RET_LAST();
 }
 
+// Bias gradient of a conv followed by a train-mode BatchNorm, from dA and y with the BN
+// backward formed on load (no dY tensor): out[c] (+)= sum_r dY[r][c].  C % 4 == 0.
+SEG_API int seg_colsum_bnb(const float* da, long ldda, const float* y, long ldy, long M, int C, const float* scale,
+                           const float* shift, const float* mean, const float* k, int bn_act, float* work, float* out,
+                           int accumulate, hipStream_t stream) {
+  if ((C & 3) || (ldy & 3) || (ldda & 3) || !k) return (int)hipErrorInvalidValue;
+  const int rpb = rows_per_block_for(M);
+  const int nblk = seg_cdiv(M, rpb);
+  hipLaunchKernelGGL(chan_partial_kernel<3>, dim3(nblk), dim3(256), 0, stream, y, ldy, da, ldda, (int)M, C, nullptr,
+                     nullptr, nullptr, 0, work, rpb, SegBnBwd{y, ldy, scale, shift, mean, k, C, bn_act});
+  hipLaunchKernelGGL(colsum_finalize_kernel, dim3(C), dim3(256), 0, stream, work, nblk, C, C, out, accumulate);
+  SEG_RET_LAST();
+}
+
 // out[c] (+)= sum_r y[r][c]  -- conv bias gradient.  `work` >= seg_chan_workspace_floats.
 SEG_API int seg_colsum(const float* y, long ldy, long M, int C, float* work, float* out, int accumulate,
                        hipStream_t stream) {
@@ -426,7 +440,7 @@ SEG_API int seg_colsum(const float* y, long ldy, long M, int C, float* work, flo
   const int rpb = rows_per_block_for(M);
   const int nblk = seg_cdiv(M, rpb);
   hipLaunchKernelGGL(chan_partial_kernel<2>, dim3(nblk), dim3(256), 0, stream, y, ldy, nullptr, 0L, (int)M, C4,
-                     nullptr, nullptr, nullptr, 0, work, rpb);
+                     nullptr, nullptr, nullptr, 0, work, rpb, SegBnBwd{});
   hipLaunchKernelGGL(colsum_finalize_kernel, dim3(C), dim3(256), 0, stream, work, nblk, C, C4, out,
                      accumulate);
   SEG_RET_LAST();

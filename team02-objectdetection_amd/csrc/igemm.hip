@@ -41,6 +41,7 @@ struct IgemmArgs {
   int kchunk;                    // split-K: K range of blockIdx.y (a multiple of BK); == K when unsplit
   float* part;                   // split-K: raw partial sums [gridDim.y][M][Cout] (no epilogue), else null
   int act;                       // epilogue activation of act(acc + bias + add) (SegAct); 0 in training
+  SegBnBwd bnb;                  // BNB kernels: `in` is dA and the A operand is the BN backward dY
 };
 
 #ifndef SEG_IGEMM_DEPTH
@@ -66,7 +67,11 @@ struct IgemmArgs {
 // each operand slot is a fixed base offset plus one of two scalar tap offsets --
 // a few VALU ops per slot instead of the general path's per-slot tap tracking
 // and bounds arithmetic.  The general path remains for Cin < BK (the stem).
-template <int BM, int BN, int WM, int WN, int KS, int BK, bool UT>
+// BNB (data gradient of a conv whose output went through a train-mode BatchNorm):
+// the A operand dY is formed on load from dA (`in`) and the raw conv output y
+// (seg_bnbwd4), so the BN backward never writes dY.  UT path only; zero padding
+// (out-of-image taps) stays zero.
+template <int BM, int BN, int WM, int WN, int KS, int BK, bool UT, bool BNB = false>
 __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void igemm_conv_kernel(IgemmArgs a) {
   constexpr int NT = 64 * (BM / WM) * (BN / WN);  // threads: one wave per WM x WN sub-tile (4 or 8 waves)
   constexpr int LDSR = BK + 4;        // LDS row stride (floats): conflict-free b128 reads
@@ -77,6 +82,7 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void igemm_conv_kernel(
   constexpr int MI = WM / 32, NI = WN / 32;
   constexpr int WAVES_N = BN / WN;
   static_assert(NT == 256 || NT == 512, "4 or 8 waves per block");
+  static_assert(!BNB || (UT && SEG_IGEMM_STAGES == 1), "BN-backward loads: uniform-tap loader, one LDS stage");
   static_assert(NT % KQ == 0, "uniform kq per thread");
 
   __shared__ __attribute__((aligned(16))) float As[SEG_IGEMM_STAGES][BM * LDSR];
@@ -131,6 +137,13 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void igemm_conv_kernel(
   int u_tap = 0, u_ci = 0;
   long u_toff0 = 0, u_toff1 = 0;
   auto tap_off = [&](int t) -> long { return ((long)(t / KS) * a.W + t % KS) * a.ldin; };
+  // BNB: y-side offsets (y has its own row stride), the loaded y, the slots' validity
+  // bits and the chunk's channel-group coefficients
+  long u_yoff[BNB ? A_PER : 1];
+  long u_ytoff0 = 0, u_ytoff1 = 0;
+  f32x4 ry[BNB ? A_PER : 1], cf[6];
+  unsigned u_okbits = 0;
+  auto tap_off_y = [&](int t) -> long { return ((long)(t / KS) * a.W + t % KS) * a.bnb.ldy; };
   if (UT) {
 #pragma unroll
     for (int i = 0; i < A_PER; ++i) {
@@ -141,6 +154,7 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void igemm_conv_kernel(
       const int pp = ok ? p : 0;
       if (KS == 1) {
         u_aoff[i] = (long)pp * a.ldin;
+        if (BNB) u_yoff[BNB ? i : 0] = (long)pp * a.bnb.ldy;
         u_mask[i] = ok ? 1u : 0u;
       } else {
         const int hw = a.Ho * a.Wo;
@@ -148,6 +162,7 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void igemm_conv_kernel(
         const int ho = rem / a.Wo, wo = rem - ho * a.Wo;
         const int hi0 = ho * a.stride - a.pad, wi0 = wo * a.stride - a.pad;
         u_aoff[i] = (((long)n * a.H + hi0) * a.W + wi0) * a.ldin;
+        if (BNB) u_yoff[BNB ? i : 0] = (((long)n * a.H + hi0) * a.W + wi0) * a.bnb.ldy;
         unsigned m = 0;
 #pragma unroll
         for (int t = 0; t < KS * KS; ++t) {
@@ -168,6 +183,10 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void igemm_conv_kernel(
     u_ci = kbeg - u_tap * a.Cin;
     u_toff0 = tap_off(u_tap);
     u_toff1 = tap_off(u_tap + 1);
+    if (BNB) {
+      u_ytoff0 = tap_off_y(u_tap);
+      u_ytoff1 = tap_off_y(u_tap + 1);
+    }
   }
 
   auto load_tiles = [&](int k0, f32x4 (&ra)[A_PER], f32x4 (&rb)[B_PER]) {
@@ -184,6 +203,18 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void igemm_conv_kernel(
         const bool ok = (u_mask[i] >> tap) & 1u;
         ra[i] = ld4(ok ? a.in + u_aoff[i] + off : g_zero4);
       }
+      if (BNB) {
+        const long offy = (wrap ? u_ytoff1 : u_ytoff0) + (wrap ? ci - a.Cin : ci);
+        const bool kin_a = k0 + u_kq4 < a.K;
+        u_okbits = 0;
+#pragma unroll
+        for (int i = 0; i < A_PER; ++i) {
+          const bool ok = kin_a && ((u_mask[i] >> tap) & 1u);
+          ry[BNB ? i : 0] = ld4(ok ? a.bnb.y + u_yoff[BNB ? i : 0] + offy : g_zero4);
+          u_okbits |= (ok ? 1u : 0u) << i;
+        }
+        seg_bnbwd_coef(a.bnb, kin_a ? (wrap ? ci - a.Cin : ci) : 0, cf);
+      }
       const bool kin = k0 + u_kq4 < a.K;
 #pragma unroll
       for (int i = 0; i < B_PER; ++i) rb[i] = ld4(u_bok[i] && kin ? a.wk + u_boff[i] + k0 : g_zero4);
@@ -193,6 +224,10 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void igemm_conv_kernel(
         ++u_tap;
         u_toff0 = u_toff1;
         u_toff1 = tap_off(u_tap + 1);
+        if (BNB) {
+          u_ytoff0 = u_ytoff1;
+          u_ytoff1 = tap_off_y(u_tap + 1);
+        }
       }
       return;
     }
@@ -234,7 +269,14 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void igemm_conv_kernel(
 #pragma unroll
     for (int i = 0; i < A_PER; ++i) {
       const int idx = tid + i * NT;
-      if (A_VEC % NT == 0 || idx < A_VEC) st4(&As[buf][(idx / KQ) * LDSR + (idx % KQ) * 4], ra[i]);
+      if (A_VEC % NT == 0 || idx < A_VEC) {
+        f32x4 v = ra[i];
+        if (BNB) {
+          const f32x4 t = seg_bnbwd4(v, ry[BNB ? i : 0], cf[0], cf[1], cf[2], cf[3], cf[4], cf[5], a.bnb.act);
+          v = ((u_okbits >> i) & 1u) ? t : f32x4{0.f, 0.f, 0.f, 0.f};
+        }
+        st4(&As[buf][(idx / KQ) * LDSR + (idx % KQ) * 4], v);
+      }
     }
 #pragma unroll
     for (int i = 0; i < B_PER; ++i) {
@@ -413,12 +455,19 @@ int launch_igemm_bk(const IgemmArgs& a, int ks, hipStream_t s) {
   const bool ut = SEG_IGEMM_UT && (SEG_IGEMM_UT2 ? a.Cin >= BK : a.Cin % BK == 0);
   constexpr int NT = 64 * (BM / WM) * (BN / WN);
 #define SEG_IG(KS, U) hipLaunchKernelGGL((igemm_conv_kernel<BM, BN, WM, WN, KS, BK, U>), dim3(grid, splits), dim3(NT), 0, s, a)
+#define SEG_IGB(KS) hipLaunchKernelGGL((igemm_conv_kernel<BM, BN, WM, WN, KS, BK, true, true>), dim3(grid, splits), dim3(NT), 0, s, a)
+  if (a.bnb.y) {
+    if (!ut) return (int)hipErrorInvalidValue;
+    if (ks == 1) SEG_IGB(1); else SEG_IGB(3);
+    SEG_RET_LAST();
+  }
   if (ks == 1) {
     if (ut) SEG_IG(1, true); else SEG_IG(1, false);
   } else {
     if (ut) SEG_IG(3, true); else SEG_IG(3, false);
   }
 #undef SEG_IG
+#undef SEG_IGB
   SEG_RET_LAST();
 }
 
@@ -532,6 +581,7 @@ SEG_API int seg_conv_igemm_act(const float* in, long ldin, int N, int H, int W, 
   a.N = N; a.H = H; a.W = W; a.Cin = Cin; a.Ho = Ho; a.Wo = Wo; a.Cout = Cout;
   a.stride = stride; a.pad = pad; a.K = ks * ks * Cin; a.M = N * Ho * Wo; a.act = act;
   a.part = splits > 1 ? work : nullptr;
+  a.bnb = SegBnBwd{};
   if (a.M == 0 || Cout == 0) return 0;
   int rc;
   switch (pick_tile(a.M, Cout)) {
@@ -565,6 +615,45 @@ SEG_API int seg_conv_igemm(const float* in, long ldin, int N, int H, int W, int 
                            const float* add, long ldadd, float* stat, hipStream_t stream) {
   return seg_conv_igemm_act(in, ldin, N, H, W, Cin, wk, ldk, bias, out, ldout, Ho, Wo, Cout, ks, stride, pad, add,
                             ldadd, stat, SEG_ACT_NONE, nullptr, 1, stream);
+}
+
+// Data gradient of a stride-1 conv whose output went through a train-mode BatchNorm,
+// with the BN backward applied on load: `in` = dA (gradient of the activated
+// output), y = the raw conv output (ldy), scale/shift/mean = the forward BN
+// coefficients, k = [3][Cin] from seg_bn_backward_coef, bn_act = the activation.
+// out = conv(dY, Wd) (+ add).  Requires the uniform-tap loader (seg_conv_igemm_bnb_ok).
+SEG_API int seg_conv_igemm_bnb(const float* in, long ldin, int N, int H, int W, int Cin, const float* wk, int ldk,
+                               float* out, long ldout, int Cout, int ks, int pad, const float* add, long ldadd,
+                               const float* y, long ldy, const float* scale, const float* shift, const float* mean,
+                               const float* k, int bn_act, hipStream_t stream) {
+  if ((Cin & 3) || (ldin & 3) || (ldk & 3) || (ldy & 3) || (ks != 1 && ks != 3) || !y || !k || !scale || !shift ||
+      !mean)
+    return (int)hipErrorInvalidValue;
+  IgemmArgs a;
+  a.in = in; a.ldin = ldin; a.wk = wk; a.ldk = ldk; a.bias = nullptr;
+  a.add = add; a.ldadd = ldadd; a.out = out; a.ldout = ldout; a.stat = nullptr;
+  a.N = N; a.H = H; a.W = W; a.Cin = Cin; a.Ho = H; a.Wo = W; a.Cout = Cout;
+  a.stride = 1; a.pad = pad; a.K = ks * ks * Cin; a.M = N * H * W; a.act = 0; a.part = nullptr;
+  a.bnb = SegBnBwd{y, ldy, scale, shift, mean, k, Cin, bn_act};
+  if (a.M == 0 || Cout == 0) return 0;
+  if (Cin < igemm_bk(a.K)) return (int)hipErrorInvalidValue;
+  switch (pick_tile(a.M, Cout)) {
+    case 0: return launch_igemm<128, 128, 64, 64>(a, ks, 1, stream);
+    case 1: return launch_igemm<64, 128, 32, 64>(a, ks, 1, stream);
+    case 2: return launch_igemm<128, 64, 64, 32>(a, ks, 1, stream);
+    case 3: return launch_igemm<64, 64, 32, 32>(a, ks, 1, stream);
+    case 4: return launch_igemm<128, 96, 32, 96>(a, ks, 1, stream);
+    case 5: return launch_igemm<128, 160, 32, 160>(a, ks, 1, stream);
+    case 6: return launch_igemm<256, 32, 64, 32>(a, ks, 1, stream);
+    default: return launch_igemm<128, 32, 32, 32>(a, ks, 1, stream);
+  }
+}
+
+// 1 when seg_conv_igemm_bnb supports this data gradient (uniform-tap loader: the
+// dY channel count >= the K chunk).
+SEG_API int seg_conv_igemm_bnb_ok(int Cin, int ks) {
+  if ((Cin & 3) || (ks != 1 && ks != 3)) return 0;
+  return Cin >= igemm_bk(ks * ks * Cin) ? 1 : 0;
 }
 
 // Split-K factor seg_conv_igemm_act should be given for this conv (1 = none); the

@@ -30,9 +30,10 @@ struct WgradArgs {
   float* part;
   int N, H, W, Cin, Ho, Wo, Cout, stride, pad;
   int M, Nw, kchunk;
+  SegBnBwd bnb;  // BNB: dy is dA and the dY operand is the BN backward formed on load
 };
 
-template <int BM, int BN, int WM, int WN, int KS>
+template <int BM, int BN, int WM, int WN, int KS, bool BNB = false>
 __global__ __launch_bounds__(256) void wgrad_kernel(WgradArgs a) {
   constexpr int AR = BM + 4, BR = BN + 4;
   constexpr int A_VEC = BK * BM / 4, B_VEC = BK * BN / 4;
@@ -80,15 +81,34 @@ __global__ __launch_bounds__(256) void wgrad_kernel(WgradArgs a) {
   }
 
   f32x4 ra[A_PER], rb[B_PER];
+  // BNB: y of each A slot, its validity, and the slot's (fixed) channel coefficients
+  f32x4 ry[BNB ? A_PER : 1], cfa[BNB ? A_PER : 1][6];
+  unsigned a_okbits = 0;
+  if (BNB) {
+#pragma unroll
+    for (int i = 0; i < A_PER; ++i) {
+      const int idx = tid + i * 256;
+      const int c = co0 + (idx % (BM / 4)) * 4;
+      seg_bnbwd_coef(a.bnb, (idx < A_VEC && c < a.Cout) ? c : 0, cfa[BNB ? i : 0]);
+    }
+  }
   auto load_tiles = [&](int k0) {  // k0 = first pixel of this chunk
+    if (BNB) a_okbits = 0;
 #pragma unroll
     for (int i = 0; i < A_PER; ++i) {
       const int idx = tid + i * 256;
       const int prow = idx / (BM / 4), c = co0 + (idx % (BM / 4)) * 4;
       const int p = k0 + prow;
       f32x4 v = {0.f, 0.f, 0.f, 0.f};
-      if (idx < A_VEC && p < kend && c < a.Cout) v = ld4(a.dy + (long)p * a.lddy + c);
+      const bool ok = idx < A_VEC && p < kend && c < a.Cout;
+      if (ok) v = ld4(a.dy + (long)p * a.lddy + c);
       ra[i] = v;
+      if (BNB) {
+        f32x4 w = {0.f, 0.f, 0.f, 0.f};
+        if (ok) w = ld4(a.bnb.y + (long)p * a.bnb.ldy + c);
+        ry[BNB ? i : 0] = w;
+        a_okbits |= (ok ? 1u : 0u) << i;
+      }
     }
 #pragma unroll
     for (int i = 0; i < B_PER; ++i) {
@@ -116,7 +136,15 @@ __global__ __launch_bounds__(256) void wgrad_kernel(WgradArgs a) {
 #pragma unroll
     for (int i = 0; i < A_PER; ++i) {
       const int idx = tid + i * 256;
-      if (idx < A_VEC) st4(&As[buf][(idx / (BM / 4)) * AR + (idx % (BM / 4)) * 4], ra[i]);
+      if (idx < A_VEC) {
+        f32x4 v = ra[i];
+        if (BNB) {
+          const f32x4(&cf)[6] = cfa[BNB ? i : 0];
+          const f32x4 t = seg_bnbwd4(v, ry[BNB ? i : 0], cf[0], cf[1], cf[2], cf[3], cf[4], cf[5], a.bnb.act);
+          v = ((a_okbits >> i) & 1u) ? t : f32x4{0.f, 0.f, 0.f, 0.f};
+        }
+        st4(&As[buf][(idx / (BM / 4)) * AR + (idx % (BM / 4)) * 4], v);
+      }
     }
 #pragma unroll
     for (int i = 0; i < B_PER; ++i) {
@@ -192,7 +220,10 @@ __global__ __launch_bounds__(256) void wgrad_kernel(WgradArgs a) {
 template <int BM, int BN, int WM, int WN>
 int launch_wgrad(const WgradArgs& a, int ks, int splits, hipStream_t s) {
   dim3 grid(seg_cdiv(a.Cout, BM) * seg_cdiv(a.Nw, BN) * splits);
-  if (ks == 1) hipLaunchKernelGGL((wgrad_kernel<BM, BN, WM, WN, 1>), grid, dim3(256), 0, s, a);
+  if (a.bnb.y) {
+    if (ks == 1) hipLaunchKernelGGL((wgrad_kernel<BM, BN, WM, WN, 1, true>), grid, dim3(256), 0, s, a);
+    else hipLaunchKernelGGL((wgrad_kernel<BM, BN, WM, WN, 3, true>), grid, dim3(256), 0, s, a);
+  } else if (ks == 1) hipLaunchKernelGGL((wgrad_kernel<BM, BN, WM, WN, 1>), grid, dim3(256), 0, s, a);
   else hipLaunchKernelGGL((wgrad_kernel<BM, BN, WM, WN, 3>), grid, dim3(256), 0, s, a);
   SEG_RET_LAST();
 }
@@ -220,9 +251,31 @@ SEG_API int seg_conv_wgrad_splits(long M, int Cout, int Cin, int ks) {
 }
 
 // part[s][co][tap*Cin+ci] = sum over split s's pixels of dY[p][co] * X[src(p,tap)][ci].
+static int conv_wgrad(const float* dy, long lddy, const float* x, long ldx, int N, int H, int W, int Cin, int Ho,
+                      int Wo, int Cout, int ks, int stride, int pad, float* part, int splits, const SegBnBwd& bnb,
+                      hipStream_t stream);
+
 SEG_API int seg_conv_wgrad(const float* dy, long lddy, const float* x, long ldx,
                            int N, int H, int W, int Cin, int Ho, int Wo, int Cout,
                            int ks, int stride, int pad, float* part, int splits, hipStream_t stream) {
+  return conv_wgrad(dy, lddy, x, ldx, N, H, W, Cin, Ho, Wo, Cout, ks, stride, pad, part, splits, SegBnBwd{}, stream);
+}
+
+// seg_conv_wgrad of a conv whose output went through a train-mode BatchNorm, with the
+// BN backward applied on load: dy = dA, y / scale / shift / mean / k / bn_act as
+// seg_conv_igemm_bnb (Cout % 4 == 0).
+SEG_API int seg_conv_wgrad_bnb(const float* dy, long lddy, const float* x, long ldx, int N, int H, int W, int Cin,
+                               int Ho, int Wo, int Cout, int ks, int stride, int pad, float* part, int splits,
+                               const float* y, long ldy, const float* scale, const float* shift, const float* mean,
+                               const float* k, int bn_act, hipStream_t stream) {
+  if (!y || !k || !scale || !shift || !mean || (ldy & 3) || (Cout & 3)) return (int)hipErrorInvalidValue;
+  return conv_wgrad(dy, lddy, x, ldx, N, H, W, Cin, Ho, Wo, Cout, ks, stride, pad, part, splits,
+                    SegBnBwd{y, ldy, scale, shift, mean, k, Cout, bn_act}, stream);
+}
+
+static int conv_wgrad(const float* dy, long lddy, const float* x, long ldx, int N, int H, int W, int Cin, int Ho,
+                      int Wo, int Cout, int ks, int stride, int pad, float* part, int splits, const SegBnBwd& bnb,
+                      hipStream_t stream) {
   if ((Cin & 3) || (ldx & 3) || (lddy & 3) || (ks != 1 && ks != 3) || splits < 1) return (int)hipErrorInvalidValue;
   if (ks == 1 && (stride != 1 || pad != 0)) return (int)hipErrorInvalidValue;
   WgradArgs a;
@@ -230,6 +283,7 @@ SEG_API int seg_conv_wgrad(const float* dy, long lddy, const float* x, long ldx,
   a.N = N; a.H = H; a.W = W; a.Cin = Cin; a.Ho = Ho; a.Wo = Wo; a.Cout = Cout;
   a.stride = stride; a.pad = pad; a.M = N * Ho * Wo; a.Nw = ks * ks * Cin;
   a.kchunk = seg_cdiv(seg_cdiv(a.M, splits), BK) * BK;
+  a.bnb = bnb;
   int bm, bn;
   wgrad_tiles(Cout, a.Nw, &bm, &bn);
   if (bm == 128 && bn == 128) return launch_wgrad<128, 128, 64, 64>(a, ks, splits, stream);

@@ -23,6 +23,9 @@ PROTOTYPES = {
     "seg_conv_igemm_act": (_I, [_V, _L, _I, _I, _I, _I, _V, _I, _V, _V, _L, _I, _I, _I, _I, _I, _I, _V, _L, _V, _I,
                                 _V, _I, _V]),
     "seg_conv_igemm_splits": (_I, [_L, _I, _I, _I]),
+    "seg_conv_igemm_bnb": (_I, [_V, _L, _I, _I, _I, _I, _V, _I, _V, _L, _I, _I, _I, _V, _L, _V, _L, _V, _V, _V, _V, _I,
+                                _V]),
+    "seg_conv_igemm_bnb_ok": (_I, [_I, _I]),
     "seg_igemm_force_tile": (_I, [_I]),
     "seg_conv_wino_pick": (_I, [_I, _I, _I, _I, _I]),
     "seg_conv_wino_row_tiles": (_I, [_I, _I, _I]),
@@ -36,6 +39,8 @@ PROTOTYPES = {
     "seg_pack_conv_weight": (_I, [_V, _V, _I, _I, _I, _I, _I, _I, _V]),
     "seg_conv_wgrad_splits": (_I, [_L, _I, _I, _I]),
     "seg_conv_wgrad": (_I, [_V, _L, _V, _L, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _V, _I, _V]),
+    "seg_conv_wgrad_bnb": (_I, [_V, _L, _V, _L, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _V, _I, _V, _L, _V, _V, _V, _V,
+                                _I, _V]),
     "seg_conv_wgrad_reduce": (_I, [_V, _I, _V, _I, _I, _I, _I, _I, _V]),
     "seg_pack_dw_weight": (_I, [_V, _V, _I, _V]),
     "seg_dw_fwd": (_I, [_V, _L, _I, _I, _I, _I, _V, _V, _I, _V, _V, _L, _I, _I, _I, _V]),
@@ -57,6 +62,7 @@ PROTOTYPES = {
                               _V]),
     "seg_bn_eval_backward": (_I, [_V, _L, _V, _L, _L, _I, _V, _V, _I, _V, _L, _V]),
     "seg_colsum": (_I, [_V, _L, _L, _I, _V, _V, _I, _V]),
+    "seg_colsum_bnb": (_I, [_V, _L, _V, _L, _L, _I, _V, _V, _V, _V, _I, _V, _V, _I, _V]),
     "seg_add": (_I, [_V, _L, _V, _L, _L, _I, _V, _L, _V]),
     "seg_upsample_fwd": (_I, [_V, _L, _I, _I, _I, _I, _V, _L, _I, _I, _I, _V]),
     "seg_upsample_bwd": (_I, [_V, _L, _I, _I, _I, _I, _I, _V, _L, _I, _I, _I, _I, _V]),

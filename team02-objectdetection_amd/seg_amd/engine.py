@@ -61,6 +61,12 @@ TIMER: KernelTimer | None = None
 # flight per block leaves HBM latency exposed).  Parity-tested (tests/test_gpu_ops.py);
 # off unless SEG_PW_FUSED=1.
 PW_FUSED = os.environ.get("SEG_PW_FUSED", "0") == "1"
+# BatchNorm backward applied on load by the data / weight / bias gradient kernels of the
+# 1x1 convs (no dY tensor).  Parity-tested (bitwise equal to the apply path), but measured
+# 1 % slower on MI355X in round 1 (1686 vs 1703 img/s: the dgrad and side-stream wgrad
+# then read dA and y instead of one dY, and the side stream contends with the main one);
+# off unless SEG_BNB=1.
+BNB_ON_LOAD = os.environ.get("SEG_BNB", "0") == "1"
 
 
 def _timed_call(kind, flops, name, *args):
@@ -118,6 +124,8 @@ class ConvOp:
         self.wino_f = self.wino_d = self.wino_w = False
         # fused 1x1 + BN backward (seg_pw_bwd_fused), decided at pack time
         self.pw_fused = False
+        # BN backward applied on load by the gradient kernels (seg_*_bnb), decided at pack time
+        self.bnb = False
         self.ks = conv.kernel_size[0]
         self.stride = conv.stride[0]
         self.pad = conv.padding[0]
@@ -225,6 +233,50 @@ class ConvOp:
              o.H, o.W, self.cout, self.ks, self.stride, self.pad, rt.ptr(r) if r is not None else None,
              r.ld if r is not None else 0, None, act, work.data_ptr() if work is not None else None, splits, s)
 
+    def _backward_bnb(self, rt, dA):
+        """BN backward applied on load: only the reduction (dgamma, dbeta, k = [3][C]) runs
+        as its own pass; the data gradient, weight gradient and bias gradient form dY from
+        dA and y inside their loaders, so no dY tensor is written or read."""
+        s, y, i = rt.stream, self.y, self.inp
+        C, M = self.cout, y.M
+        st = rt.saved[id(self)]
+        mean, invstd, scale, shift = (st[k * C:(k + 1) * C] for k in range(4))
+        work = rt.tmp(query("seg_chan_workspace_floats", M, C))
+        coef = rt.tmp(3 * C)
+        call("seg_bn_backward_coef", rt.gptr(dA), dA.ld, rt.ptr(y), y.ld, M, C, self.bn.weight.data_ptr(),
+             mean.data_ptr(), invstd.data_ptr(), scale.data_ptr(), shift.data_ptr(), self.act,
+             rt.grad_param(self.bn.weight), rt.grad_param(self.bn.bias), work.data_ptr(), coef.data_ptr(), s)
+        if self.res is not None:
+            rt.add_pending(self.res, dA)
+        bn = (rt.ptr(y), y.ld, scale.data_ptr(), shift.data_ptr(), mean.data_ptr(), coef.data_ptr(), self.act)
+        if rt.side is not None:
+            coef.record_stream(rt.side)  # read by the side stream after this function drops it
+        for p in (self.conv.weight, self.conv.bias):
+            if p is not None and p.requires_grad:
+                rt.grad_param(p)
+        ctx, sw = rt.fork()
+        with ctx:
+            if self.conv.bias is not None and self.conv.bias.requires_grad:
+                wk = rt.tmp(query("seg_chan_workspace_floats", M, C))
+                call("seg_colsum_bnb", rt.gptr(dA), dA.ld, rt.ptr(y), y.ld, M, C, scale.data_ptr(), shift.data_ptr(),
+                     mean.data_ptr(), coef.data_ptr(), self.act, wk.data_ptr(), rt.grad_param(self.conv.bias), 0, sw)
+            if self.conv.weight.requires_grad:
+                gw = rt.grad_param(self.conv.weight)
+                splits = query("seg_conv_wgrad_splits", M, C, self.cin_pad, self.ks)
+                part = rt.tmp(splits * C * self.ks * self.ks * self.cin_pad)
+                _timed_call(f"igemm{self.ks}_wgrad", self.flops(), "seg_conv_wgrad_bnb", rt.gptr(dA), dA.ld,
+                            rt.ptr(i), i.ld, i.N, i.H, i.W, self.cin_pad, y.H, y.W, C, self.ks, self.stride,
+                            self.pad, part.data_ptr(), splits, *bn, sw)
+                call("seg_conv_wgrad_reduce", part.data_ptr(), splits, gw, C, self.cin, self.ks, 0, 0, sw)
+            rt.params_done(self.params())
+        if self.first:
+            return
+        add_ptr, add_ld = rt.begin_write_add(i)
+        _timed_call(f"igemm{self.ks}_dgrad", self.flops(), "seg_conv_igemm_bnb", rt.gptr(dA), dA.ld, y.N, y.H, y.W,
+                    C, self.wk_d.data_ptr(), self.ldk_d, rt.gptr(i), i.ld, self.cin, self.ks, self.pad, add_ptr,
+                    add_ld, *bn, s)
+        rt.mark_written(i)
+
     def _backward_pw_fused(self, rt, dA):
         """1x1 conv + train BN backward in one pass over dA, y, x (seg_pw_bwd_fused): the BN
         reduction first (seg_bn_backward_coef), then dx (+ pending addend) and the dW slabs."""
@@ -267,6 +319,8 @@ class ConvOp:
         dA = rt.grad_of(self.out)
         if self.pw_fused:
             return self._backward_pw_fused(rt, dA)
+        if self.bnb and rt.training:
+            return self._backward_bnb(rt, dA)
         if self.bn is not None:
             if not rt.training:
                 raise NotImplementedError("backward through eval-mode BatchNorm is not supported")
@@ -481,6 +535,12 @@ class Program:
                 op.wk_f = torch.empty(op.cout * op.ldk_f, device=dev, dtype=torch.float32)
                 jobs.append((w.data_ptr(), op.wk_f.data_ptr(), op.cout, op.cin, op.ks, op.ldk_f, 0, op.cin_pad))
                 max_elems = max(max_elems, op.cout * op.ldk_f)
+            # (1x1 only: a 3x3 data gradient would re-form each dY element 9 times from two
+            # tensors, measured slower than materialising dY once)
+            op.bnb = (BNB_ON_LOAD and op.ks == 1 and op.bn is not None and not op.pw_fused and op.cout % 4 == 0
+                      and not op.wino_d and not op.wino_w and op.conv.weight.requires_grad
+                      and (op.first or (op.stride == 1 and bool(query("seg_conv_igemm_bnb_ok", r4(op.cout),
+                                                                        op.ks)))))
             if op.wino_d:
                 kin = r4(op.cout)
                 op.wk_wd = torch.empty(16 * op.cin * kin, device=dev, dtype=torch.float32)

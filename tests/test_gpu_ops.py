@@ -556,3 +556,66 @@ def test_pw_bwd_fused(M, Cin, Cout, act, res):
     ref_dx = xr.grad + (addend if res else 0)
     assert rel(dx2, ref_dx) < 1e-2 and rel(dx, ref_dx) < 1e-2  # mask flips at ReLU6 thresholds dominate here
     assert rel(dw, wr.grad) < 1e-2
+
+
+@pytest.mark.parametrize("N,H,W,Cin,Cout,ks,act", [(2, 9, 13, 80, 32, 3, 1), (1, 16, 12, 64, 64, 3, 1),
+                                                   (2, 7, 10, 16, 96, 1, 2), (3, 6, 8, 96, 24, 1, 0),
+                                                   (1, 8, 8, 152, 64, 3, 1), (2, 5, 7, 32, 16, 1, 1)])
+def test_bn_backward_on_load(N, H, W, Cin, Cout, ks, act):
+    """seg_conv_igemm_bnb / seg_conv_wgrad_bnb / seg_colsum_bnb (dY formed on load from dA and
+    y) are bitwise equal to the materialised path: seg_bn_backward -> seg_conv_igemm /
+    seg_conv_wgrad / seg_colsum."""
+    M = N * H * W
+    pad = ks // 2
+    s = S()
+    dA = gen(M, Cout, seed=61).to(DEV)
+    y = (gen(M, Cout, seed=62) * 2).to(DEV)
+    x = gen(M, Cin, seed=63).to(DEV)
+    g = (gen(Cout, seed=64).abs() + 0.5).to(DEV)
+    mean = (gen(Cout, seed=65) * 0.1).to(DEV)
+    invstd = (gen(Cout, seed=66).abs() + 0.5).to(DEV)
+    scale, shift = g * invstd, gen(Cout, seed=67).to(DEV) - mean * g * invstd
+    w = (gen(Cout, Cin, ks, ks, seed=68) * 0.1).to(DEV)
+    # materialised reference path
+    work = torch.empty(query("seg_chan_workspace_floats", M, Cout) + 3 * Cout, device=DEV)
+    dg, db, dY = torch.empty(Cout, device=DEV), torch.empty(Cout, device=DEV), torch.empty(M, Cout, device=DEV)
+    call("seg_bn_backward", dA.data_ptr(), Cout, y.data_ptr(), Cout, M, Cout, g.data_ptr(), mean.data_ptr(),
+         invstd.data_ptr(), scale.data_ptr(), shift.data_ptr(), act, dg.data_ptr(), db.data_ptr(), work.data_ptr(),
+         dY.data_ptr(), Cout, s)
+    # on-load path: reduction only
+    work2 = torch.empty(query("seg_chan_workspace_floats", M, Cout), device=DEV)
+    k = torch.empty(3 * Cout, device=DEV)
+    dg2, db2 = torch.empty(Cout, device=DEV), torch.empty(Cout, device=DEV)
+    call("seg_bn_backward_coef", dA.data_ptr(), Cout, y.data_ptr(), Cout, M, Cout, g.data_ptr(), mean.data_ptr(),
+         invstd.data_ptr(), scale.data_ptr(), shift.data_ptr(), act, dg2.data_ptr(), db2.data_ptr(), work2.data_ptr(),
+         k.data_ptr(), s)
+    assert torch.equal(dg, dg2) and torch.equal(db, db2)
+    bn = (y.data_ptr(), Cout, scale.data_ptr(), shift.data_ptr(), mean.data_ptr(), k.data_ptr(), act)
+    # data gradient (+ addend)
+    kin = r4(Cout)
+    ldk = r4(ks * ks * kin)
+    wkd = torch.empty(Cin * ldk, device=DEV)
+    call("seg_pack_conv_weight", w.data_ptr(), wkd.data_ptr(), Cout, Cin, ks, ldk, 1, kin, s)
+    assert query("seg_conv_igemm_bnb_ok", kin, ks) == 1
+    add = gen(M, Cin, seed=69).to(DEV)
+    dx1, dx2 = torch.empty(M, Cin, device=DEV), torch.empty(M, Cin, device=DEV)
+    call("seg_conv_igemm", dY.data_ptr(), Cout, N, H, W, kin, wkd.data_ptr(), ldk, None, dx1.data_ptr(), Cin, H, W,
+         Cin, ks, 1, pad, add.data_ptr(), Cin, None, s)
+    call("seg_conv_igemm_bnb", dA.data_ptr(), Cout, N, H, W, kin, wkd.data_ptr(), ldk, dx2.data_ptr(), Cin, Cin, ks,
+         pad, add.data_ptr(), Cin, *bn, s)
+    assert torch.equal(dx1, dx2)
+    # weight gradient
+    splits = query("seg_conv_wgrad_splits", M, Cout, Cin, ks)
+    p1 = torch.empty(splits * Cout * ks * ks * Cin, device=DEV)
+    p2 = torch.empty_like(p1)
+    call("seg_conv_wgrad", dY.data_ptr(), Cout, x.data_ptr(), Cin, N, H, W, Cin, H, W, Cout, ks, 1, pad,
+         p1.data_ptr(), splits, s)
+    call("seg_conv_wgrad_bnb", dA.data_ptr(), Cout, x.data_ptr(), Cin, N, H, W, Cin, H, W, Cout, ks, 1, pad,
+         p2.data_ptr(), splits, *bn, s)
+    assert torch.equal(p1, p2)
+    # bias gradient
+    c1, c2 = torch.empty(Cout, device=DEV), torch.empty(Cout, device=DEV)
+    call("seg_colsum", dY.data_ptr(), Cout, M, Cout, work.data_ptr(), c1.data_ptr(), 0, s)
+    call("seg_colsum_bnb", dA.data_ptr(), Cout, y.data_ptr(), Cout, M, Cout, scale.data_ptr(), shift.data_ptr(),
+         mean.data_ptr(), k.data_ptr(), act, work2.data_ptr(), c2.data_ptr(), 0, s)
+    assert rel(c1, c2) < 1e-6

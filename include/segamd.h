@@ -122,6 +122,18 @@ int seg_conv_wino_wgrad(const float* dy, long lddy, const float* x, long ldx, in
 int seg_conv_wino_wgrad_reduce(const float* part, int splits, float* dw, int Cout, int Cin, int Cin_pad,
                                int accumulate, hipStream_t stream);
 
+/* Direct 3x3 conv (stride 1, pad 1) with an LDS halo tile for narrow outputs
+ * (Cout <= 96; H % 4 == 0, W % 64 == 0): the 4x64-pixel tile's input halo is
+ * loaded once per channel chunk and the 9 taps read it from LDS.  Same packed
+ * weights, bias / addend / BN-partials contract as seg_conv_igemm (partials:
+ * seg_conv_halo_row_tiles tiles of 256 rows). */
+int seg_conv_halo_ok(int N, int H, int W, int Cin, int Cout);
+int seg_conv_halo_pick(int N, int H, int W, int Cin, int Cout);
+int seg_conv_halo_row_tiles(int N, int H, int W);
+int seg_conv_halo(const float* in, long ldin, int N, int H, int W, int Cin, const float* wk, int ldk,
+                  const float* bias, float* out, long ldout, int Cout, const float* add, long ldadd,
+                  float* stat, hipStream_t stream);
+
 /* Every weight repack of a step in one launch.  `jobs` is a DEVICE array of
  * njobs seg_pack_job (mode 0/1 as seg_pack_conv_weight, mode 2 = depthwise
  * [9][C] as seg_pack_dw_weight with cout = C, modes 3/4 = Winograd filter

@@ -27,6 +27,10 @@ PROTOTYPES = {
                                 _V]),
     "seg_conv_igemm_bnb_ok": (_I, [_I, _I]),
     "seg_igemm_force_tile": (_I, [_I]),
+    "seg_conv_halo_ok": (_I, [_I, _I, _I, _I, _I]),
+    "seg_conv_halo_pick": (_I, [_I, _I, _I, _I, _I]),
+    "seg_conv_halo_row_tiles": (_I, [_I, _I, _I]),
+    "seg_conv_halo": (_I, [_V, _L, _I, _I, _I, _I, _V, _I, _V, _V, _L, _I, _V, _L, _V, _V]),
     "seg_conv_wino_pick": (_I, [_I, _I, _I, _I, _I]),
     "seg_conv_wino_row_tiles": (_I, [_I, _I, _I]),
     "seg_conv_wino": (_I, [_V, _L, _I, _I, _I, _I, _V, _I, _V, _V, _L, _I, _V, _L, _V, _V, _V]),

@@ -122,6 +122,8 @@ class ConvOp:
         # Winograd F(2x2,3x3) (seg_conv_wino) for the forward / data gradient, chosen by
         # seg_conv_wino_pick at pack time; U_f [16][Cout][cin_pad], U_d [16][Cin][r4(Cout)]
         self.wino_f = self.wino_d = self.wino_w = False
+        # LDS-halo direct 3x3 (seg_conv_halo) for the forward / data gradient of narrow convs
+        self.halo_f = self.halo_d = False
         # fused 1x1 + BN backward (seg_pw_bwd_fused), decided at pack time
         self.pw_fused = False
         # BN backward applied on load by the gradient kernels (seg_*_bnb), decided at pack time
@@ -166,11 +168,16 @@ class ConvOp:
             if self.bn is not None and rt.training:  # BN statistics fused into the conv epilogue
                 if self.wino_f:
                     ntiles, tile_rows = query("seg_conv_wino_row_tiles", y.N, y.H, y.W), 256
+                elif self.halo_f:
+                    ntiles, tile_rows = query("seg_conv_halo_row_tiles", y.N, y.H, y.W), 256
                 else:
                     ntiles, tile_rows = rt.row_tiles(y.M, self.cout)
                 stat = rt.tmp(ntiles * 2 * self.cout)
             statp = stat.data_ptr() if stat is not None else None
-            if self.wino_f:
+            if self.halo_f:
+                _timed_call("igemm3_fwd", self.flops(), "seg_conv_halo", rt.ptr(i), i.ld, i.N, i.H, i.W, self.cin_pad,
+                            wk_ptr, ldk, bias, rt.ptr(y), y.ld, self.cout, None, 0, statp, s)
+            elif self.wino_f:
                 work = rt.tmp(16 * (y.M // 4) * self.cout)
                 _timed_call("wino3_fwd", self.flops(), "seg_conv_wino", rt.ptr(i), i.ld, i.N, i.H, i.W, self.cin_pad,
                             self.wk_wf.data_ptr(), self.cin_pad, bias, rt.ptr(y), y.ld, self.cout, None, 0, statp,
@@ -395,7 +402,10 @@ class ConvOp:
                 raise NotImplementedError("data gradient of a strided dense conv")
             kin = r4(self.cout)  # dY channels padded to 4 (the C=10 head)
             add_ptr, add_ld = rt.begin_write_add(i)
-            if self.wino_d:
+            if self.halo_d:
+                _timed_call("igemm3_dgrad", self.flops(), "seg_conv_halo", dYp, dY.ld, y.N, y.H, y.W, kin,
+                            self.wk_d.data_ptr(), self.ldk_d, None, rt.gptr(i), i.ld, self.cin, add_ptr, add_ld, None, s)
+            elif self.wino_d:
                 work = rt.tmp(16 * (y.M // 4) * self.cin)
                 _timed_call("wino3_dgrad", self.flops(), "seg_conv_wino", dYp, dY.ld, y.N, y.H, y.W, kin,
                             self.wk_wd.data_ptr(), kin, None, rt.gptr(i), i.ld, self.cin, add_ptr, add_ld, None,
@@ -526,6 +536,10 @@ class Program:
             op.wino_d = wino_ok and not op.first and bool(query("seg_conv_wino_pick", y.N, y.H, y.W, r4(op.cout),
                                                                 op.cin))
             op.wino_w = wino_ok and bool(query("seg_conv_wino_wgrad_pick", y.N, y.H, y.W, op.cin_pad, op.cout))
+            op.halo_f = (wino_ok and not op.wino_f
+                         and bool(query("seg_conv_halo_pick", y.N, y.H, y.W, op.cin_pad, op.cout)))
+            op.halo_d = (wino_ok and not op.first and not op.wino_d
+                         and bool(query("seg_conv_halo_pick", y.N, y.H, y.W, r4(op.cout), op.cin)))
             if op.wino_f:
                 op.wk_wf = torch.empty(16 * op.cout * op.cin_pad, device=dev, dtype=torch.float32)
                 jobs.append((w.data_ptr(), op.wk_wf.data_ptr(), op.cout, op.cin, 3, op.cin_pad, 3, op.cin_pad))

@@ -619,3 +619,52 @@ def test_bn_backward_on_load(N, H, W, Cin, Cout, ks, act):
     call("seg_colsum_bnb", dA.data_ptr(), Cout, y.data_ptr(), Cout, M, Cout, scale.data_ptr(), shift.data_ptr(),
          mean.data_ptr(), k.data_ptr(), act, work2.data_ptr(), c2.data_ptr(), 0, s)
     assert rel(c1, c2) < 1e-6
+
+
+@pytest.mark.parametrize("N,Cin,Cout,H,W,mode", [(2, 80, 32, 8, 64, 0), (1, 32, 32, 4, 128, 0),
+                                                 (2, 152, 64, 4, 64, 0), (1, 64, 64, 12, 64, 0),
+                                                 (2, 32, 80, 8, 64, 1), (1, 20, 96, 4, 128, 0)])
+def test_conv_halo(N, Cin, Cout, H, W, mode):
+    """seg_conv_halo == torch conv2d (forward + bias + BN partials, or data gradient + addend)."""
+    x = gen(N, Cin, H, W, seed=71)
+    w = gen(Cout, Cin, 3, 3, seed=72) * (2.0 / (Cin * 9)) ** 0.5
+    b = gen(Cout, seed=73)
+    s = S()
+    wg = w.to(DEV)
+    if mode == 0:
+        ref = F.conv2d(x, w, b, padding=1)
+        cin4 = r4(Cin)
+        ldk = r4(9 * cin4)
+        wk = torch.empty(Cout * ldk, device=DEV)
+        call("seg_pack_conv_weight", wg.data_ptr(), wk.data_ptr(), Cout, Cin, 3, ldk, 0, cin4, s)
+        xg = nhwc(x)
+        if Cin % 4:
+            xg[:, Cin:] = 0.0
+        out = torch.full((N * H * W, r4(Cout)), float("nan"), device=DEV)
+        nt = query("seg_conv_halo_row_tiles", N, H, W)
+        stat = torch.empty(nt * 2 * Cout, device=DEV)
+        call("seg_conv_halo", xg.data_ptr(), xg.shape[1], N, H, W, cin4, wk.data_ptr(), ldk, b.to(DEV).data_ptr(),
+             out.data_ptr(), out.shape[1], Cout, None, 0, stat.data_ptr(), s)
+        assert rel(from_nhwc(out, N, Cout, H, W), ref) < 1e-5
+        st = torch.empty(4 * Cout, device=DEV)
+        rm, rv = torch.zeros(Cout, device=DEV), torch.ones(Cout, device=DEV)
+        call("seg_bn_stats_tiles", stat.data_ptr(), nt, 256, N * H * W, Cout, None, None, 1e-5, 0.1, rm.data_ptr(),
+             rv.data_ptr(), None, st[:Cout].data_ptr(), st[Cout:2 * Cout].data_ptr(), st[2 * Cout:3 * Cout].data_ptr(),
+             st[3 * Cout:].data_ptr(), s)
+        assert rel(st[:Cout], ref.double().mean((0, 2, 3))) < 1e-5
+    else:  # data gradient: dY has Cin channels here, dX has Cout
+        xr = torch.zeros(N, Cout, H, W, requires_grad=True)
+        wt = gen(Cin, Cout, 3, 3, seed=74) * 0.1   # forward conv Cout'=Cin <- Cin'=Cout
+        y = F.conv2d(xr, wt, None, padding=1)
+        dy = x
+        y.backward(dy)
+        kin = r4(Cin)
+        ldk = r4(9 * kin)
+        wkd = torch.empty(Cout * ldk, device=DEV)
+        call("seg_pack_conv_weight", wt.to(DEV).data_ptr(), wkd.data_ptr(), Cin, Cout, 3, ldk, 1, kin, s)
+        addend = gen(N, Cout, H, W, seed=75)
+        addg = nhwc(addend)
+        dx = torch.full((N * H * W, r4(Cout)), float("nan"), device=DEV)
+        call("seg_conv_halo", nhwc(dy).data_ptr(), r4(Cin), N, H, W, kin, wkd.data_ptr(), ldk, None, dx.data_ptr(),
+             dx.shape[1], Cout, addg.data_ptr(), addg.shape[1], None, s)
+        assert rel(from_nhwc(dx, N, Cout, H, W), xr.grad + addend) < 1e-5

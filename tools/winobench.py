@@ -69,6 +69,11 @@ def main():
             t_w = timeit(lambda: call("seg_conv_wino", x.data_ptr(), ci, N, H, W, ci, U.data_ptr(), ci, None,
                                       y.data_ptr(), co, co, None, 0, None, work.data_ptr(), s))
             pick = query("seg_conv_wino_pick", N, H, W, ci, co)
+            if query("seg_conv_halo_ok", N, H, W, ci, co):
+                t_h = timeit(lambda: call("seg_conv_halo", x.data_ptr(), ci, N, H, W, ci, wk.data_ptr(), ldk, None,
+                                          y.data_ptr(), co, co, None, 0, None, s))
+                print(f"{name:6s} {d:5s} halo {t_h * 1e6:7.1f} us ({fl / t_h / 1e12:5.1f} TF/s) vs direct "
+                      f"{t_d * 1e6:7.1f}: speedup {t_d / t_h:4.2f}", flush=True)
             print(f"{name:6s} {d:5s} direct {t_d * 1e6:7.1f} us ({fl / t_d / 1e12:5.1f} TF/s)  wino {t_w * 1e6:7.1f} us "
                   f"({fl / t_w / 1e12:5.1f})  speedup {t_d / t_w:4.2f}  pick={pick}", flush=True)
         # weight gradient: direct split-K wgrad + reduce vs Winograd wgrad + reduce

@@ -36,6 +36,7 @@ for _p in (PKG, REPO):
 import torch  # noqa: E402
 
 F32_MFMA_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: FP32 matrix (= vector) peak, spec
+BF16_MFMA_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: BF16 MFMA ~2.5 PF dense (no sparsity)
 HBM_PEAK_GBS = 8000.0
 
 
@@ -54,6 +55,9 @@ def parse():
     ap.add_argument("--workload", choices=("train", "infer"), default="train",
                     help="train: BASELINE configs[1] (the headline); infer: configs[3], inference.py's per-frame path")
     ap.add_argument("--frames", type=int, default=500, help="timed frames of --workload infer")
+    ap.add_argument("--math", choices=("f32", "bf16"), default="f32",
+                    help="conv arithmetic: f32 = configs[1] (default, the headline); bf16 = the bf16 configurations "
+                         "(configs[2]/[4]): bf16 MFMA operands, fp32 accumulation / activations / BN / Adam")
     ap.add_argument("--model", choices=("MobileNetV2UNet", "UNet"), default="MobileNetV2UNet",
                     help="UNet = BASELINE configs[4] shape family (use --height 512 --width 1024 --batch 8)")
     return ap.parse_args()
@@ -164,6 +168,8 @@ def main():
     from seg_amd import deterministic_init, synthetic_batch
     from seg_amd import engine
     model = deterministic_init(getattr(seg_amd, args.model)(args.classes), seed=0).to(dev).train()
+    engine.set_conv_math(model, args.math)
+    peak = BF16_MFMA_PEAK_TFLOPS if args.math == "bf16" else F32_MFMA_PEAK_TFLOPS
     if dist:
         from seg_amd.ddp import DataParallel
         model = DataParallel(model)
@@ -236,15 +242,18 @@ def main():
         alg_bytes = sum(abytes) / max(len(abytes), 1)
         wf, ws, wn = family({"igemm3_wgrad", "wino3_wgrad"})
         af, as_, an = family({k for k, _, _ in rec})
-        roof = {"bound": "mfma", "achieved": round(achieved, 2), "peak": F32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
-                "frac": round(achieved / F32_MFMA_PEAK_TFLOPS, 4),
+        roof = {"bound": "mfma", "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
+                "frac": round(achieved / peak, 4),
                 "traffic": round(traffic) if traffic else None,
                 "traffic_source": "profiles/latest_roofline.json: rocprofv3 PMC (2*FETCH_SIZE+WRITE_SIZE)*1KiB "
                                   "of the conv3 family per step / 17 conv ops" if traffic else None,
                 "algorithmic_bytes_per_launch": round(alg_bytes),
-                "kernel": "dense 3x3 conv fwd + dgrad on f32 MFMA: igemm_conv_kernel<*,*,*,*,3,*> (implicit GEMM) "
-                          "and, for the deep decoder convs, wino_gemm_kernel + wino_out_kernel (Winograd F(2x2,3x3): "
-                          "2.25x fewer executed MFMA FLOPs than the algorithmic count used here)",
+                "kernel": ("dense 3x3 conv fwd + dgrad on f32 MFMA: igemm_conv_kernel<*,*,*,*,3,*> (implicit GEMM) "
+                           "and, for the deep decoder convs, wino_gemm_kernel + wino_out_kernel (Winograd F(2x2,3x3): "
+                           "2.25x fewer executed MFMA FLOPs than the algorithmic count used here)"
+                           if args.math == "f32" else
+                           "dense 3x3 conv fwd + dgrad on bf16 MFMA: igemm_conv_kernel<*,*,*,*,3,*,*,false,true> "
+                           "(implicit GEMM, v_mfma_f32_32x32x16_bf16, fp32 accumulation)"),
                 "winograd": {"launches": wn, "algorithmic_tflops": round(wfl / wsec / 1e12, 2) if wsec else None,
                              "executed_mfma_tflops": round(wfl / 2.25 / wsec / 1e12, 2) if wsec else None},
                 "launches": n, "flops_per_launch": round(flops / max(n, 1)),
@@ -259,16 +268,22 @@ def main():
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
             cpu = cpu_baseline(args)
-        cfg = "BASELINE configs[1]" if args.model == "MobileNetV2UNet" else "BASELINE configs[4] shape, f32"
+        if args.model == "MobileNetV2UNet":
+            cfg = "BASELINE configs[1]" if args.math == "f32" else "BASELINE configs[2] math (bf16) at N GPUs"
+        else:
+            cfg = f"BASELINE configs[4] shape, {args.math} conv math"
         line = {"metric": f"images/sec fwd+bwd {args.model} {args.height}x{args.width} bs={args.batch}/GPU",
                 "value": round(value, 2), "unit": "images/s", "n_gpus": world, "steps": args.steps,
                 "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 3), "higher_is_better": True,
-                "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+                "scaling": "weak", "vs_baseline": None, "dtype": args.math, "data": "synthetic",
                 "config": {"workload": f"{args.model} {args.classes}-class fwd+bwd+Adam, "
                                        f"{args.height}x{args.width}, bs={args.batch}/GPU ({cfg})",
                            "model": args.model, "global_batch": args.batch * world,
                            "image": [args.height, args.width], "parallelism": f"dp{world}"},
                 "final_loss": round(final_loss, 5),
+                "math": ("fp32 everywhere" if args.math == "f32" else
+                         "conv operands bf16 (RNE) on the bf16 MFMA, fp32 accumulation; activations, BatchNorm, "
+                         "depthwise convs, loss and Adam in fp32"),
                 "roofline": roof, "cpu_baseline": cpu}
         print(json.dumps(line), flush=True)
     if dist:

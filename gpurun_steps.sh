@@ -15,6 +15,9 @@ for step in "$@"; do
     gpu)   run gpu 1200 python -m pytest tests -q -m gpu ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run bench 600 python bench.py --steps 10 --warmup 3 ;;
+    bf16)  run bf16 600 python -u -m pytest tests/test_gpu_bf16.py -q -m gpu -x -s --timeout 300 --timeout-method thread ;;
+    benchbf) run benchbf 600 python bench.py --steps 10 --warmup 3 --math bf16 --no-cpu-baseline ;;
+    unetbf) run unetbf 600 python bench.py --model UNet --height 512 --width 1024 --batch 8 --steps 3 --warmup 2 --math bf16 --no-cpu-baseline ;;
     benchq) run benchq 600 python bench.py --steps 5 --warmup 2 --no-cpu-baseline ;;
     unet) run unet 600 python bench.py --model UNet --height 512 --width 1024 --batch 8 --steps 3 --warmup 2 ;;
     infer) run infer 600 python bench.py --workload infer --frames 300 --cpu-seconds 8 ;;

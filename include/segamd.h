@@ -65,6 +65,16 @@ int seg_conv_igemm_bnb(const float* in, long ldin, int N, int H, int W, int Cin,
                        const float* y, long ldy, const float* scale, const float* shift, const float* mean,
                        const float* k, int bn_act, hipStream_t stream);
 int seg_conv_igemm_bnb_ok(int Cin, int ks);
+/* seg_conv_igemm_act with bf16 math (BASELINE configs[2]/[4], the bf16 configurations;
+ * replaces the autocast bf16 conv2d of the same call sites): the same fp32 tensors,
+ * both operands rounded to bf16 (round-to-nearest-even) in the LDS staging,
+ * v_mfma_f32_32x32x16_bf16 with fp32 accumulation, the fp32 epilogue. */
+int seg_conv_igemm_bf16(const float* in, long ldin, int N, int H, int W, int Cin,
+                        const float* wk, int ldk, const float* bias,
+                        float* out, long ldout, int Ho, int Wo, int Cout,
+                        int ks, int stride, int pad,
+                        const float* add, long ldadd, float* stat, int act, float* work, int splits,
+                        hipStream_t stream);
 /* Split-K factor for seg_conv_igemm_act (1 = none): > 1 only when the output tiles
  * cannot fill the 256 CUs (batch-1 inference). */
 int seg_conv_igemm_splits(long M, int Cout, int Cin, int ks);
@@ -86,6 +96,12 @@ int seg_conv_wgrad_splits(long M, int Cout, int Cin, int ks);
 int seg_conv_wgrad(const float* dy, long lddy, const float* x, long ldx,
                    int N, int H, int W, int Cin, int Ho, int Wo, int Cout,
                    int ks, int stride, int pad, float* part, int splits, hipStream_t stream);
+
+/* seg_conv_wgrad with bf16 math: dY and X rounded to bf16 (RNE) in the LDS staging,
+ * fp32 accumulation into the same fp32 partial slabs (seg_conv_wgrad_reduce). */
+int seg_conv_wgrad_bf16(const float* dy, long lddy, const float* x, long ldx,
+                        int N, int H, int W, int Cin, int Ho, int Wo, int Cout,
+                        int ks, int stride, int pad, float* part, int splits, hipStream_t stream);
 
 /* seg_conv_wgrad with dY formed on load from dA (dy) and y (BN backward, as
  * seg_conv_igemm_bnb; Cout % 4 == 0). */

@@ -198,3 +198,50 @@ def miou(pred, target, classes):
     union = cm.sum(0) + cm.sum(1) - tp
     valid = union > 0
     return float((tp[valid] / union[valid]).mean()) if valid.any() else float("nan")
+
+
+# ---------------------------------------------------------------- bf16 conv math
+# The bf16 configurations (BASELINE configs[2]/[4]) have no code in the reference;
+# their reference arithmetic is torch.autocast(dtype=torch.bfloat16) around the
+# forward, whose convolutions (groups == 1: the dense 3x3 and the 1x1 convs; the
+# depthwise convs stay in the product's fp32) take bf16 operands and accumulate in
+# fp32.  `bf16_convs()` restates that on this oracle: inside it every non-grouped
+# conv rounds its input and weight to bf16 (RNE) in the forward and its incoming
+# gradient in the backward, then runs in the oracle's own precision (fp64 gives
+# "exact products of bf16 operands").  Used only to size the bf16 tolerance budget
+# (tests/test_gpu_bf16.py), like the fp32 ensemble does for the fp32 path.
+class _RoundBf16(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, t):
+        return t.to(torch.bfloat16).to(t.dtype)
+
+    @staticmethod
+    def backward(ctx, g):
+        return g.to(torch.bfloat16).to(g.dtype)
+
+
+def _conv2d_bf16(x, w, b=None, stride=1, padding=0, dilation=1, groups=1):
+    if groups == 1:
+        x, w = _RoundBf16.apply(x), _RoundBf16.apply(w)
+    return torch.nn.functional.conv2d(x, w, b, stride, padding, dilation, groups)
+
+
+class _F:
+    conv2d = staticmethod(_conv2d_bf16)
+
+    def __getattr__(self, k):
+        return getattr(torch.nn.functional, k)
+
+
+class bf16_convs:
+    """Context manager: this module's convolutions use bf16 operands (see above)."""
+
+    def __enter__(self):
+        global F
+        self._saved, F = F, _F()
+        return self
+
+    def __exit__(self, *exc):
+        global F
+        F = self._saved
+        return False

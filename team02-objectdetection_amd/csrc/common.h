@@ -11,11 +11,26 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <algorithm>
+#include <type_traits>
 
 #define SEG_API extern "C" __attribute__((visibility("default")))
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+
+// ds_read_b64_tr_b16: per 16-lane group, the 4 x 16 bf16 block whose row q / columns
+// 4p..4p+3 lane 4q+p addresses, delivered column-major (lane i gets column i, row q
+// in element q).  `p` must point into LDS, 8-byte aligned; all 64 lanes active.
+__device__ __forceinline__ bf16x4 seg_lds_tr4(const __bf16* p) {
+  typedef short s16x4 __attribute__((ext_vector_type(4)));
+  s16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(p));
+  return __builtin_bit_cast(bf16x4, v);
+}
+__device__ __forceinline__ bf16x8 seg_cat8(bf16x4 lo, bf16x4 hi) {
+  return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+}
 
 enum SegAct { SEG_ACT_NONE = 0, SEG_ACT_RELU = 1, SEG_ACT_RELU6 = 2 };
 

@@ -71,10 +71,18 @@ struct IgemmArgs {
 // the A operand dY is formed on load from dA (`in`) and the raw conv output y
 // (seg_bnbwd4), so the BN backward never writes dY.  UT path only; zero padding
 // (out-of-image taps) stays zero.
-template <int BM, int BN, int WM, int WN, int KS, int BK, bool UT, bool BNB = false>
+//
+// BF ("bf16 math", the bf16 configurations of BASELINE configs[2]/[4]): activations
+// and weights stay fp32 in HBM; each operand is rounded to bf16 (RNE) on its way
+// into LDS and the K loop runs v_mfma_f32_32x32x16_bf16 (fp32 accumulation, 8x the
+// K per instruction).  The bf16 LDS rows keep the same 80-byte pitch at BK 32, so
+// the ds_read_b128 fragment reads (lane half h: k = 16ks + 8h .. +7) stay
+// conflict-free; the epilogue (bias, BN statistics, addend) is the fp32 one.
+template <int BM, int BN, int WM, int WN, int KS, int BK, bool UT, bool BNB = false, bool BF = false>
 __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void igemm_conv_kernel(IgemmArgs a) {
   constexpr int NT = 64 * (BM / WM) * (BN / WN);  // threads: one wave per WM x WN sub-tile (4 or 8 waves)
-  constexpr int LDSR = BK + 4;        // LDS row stride (floats): conflict-free b128 reads
+  constexpr int LDSR = BF ? BK + 8 : BK + 4;  // LDS row stride (elements): conflict-free b128 reads
+  using lds_t = typename std::conditional<BF, __bf16, float>::type;
   constexpr int KQ = BK / 4;          // float4 groups per tile row
   constexpr int A_VEC = BM * KQ, B_VEC = BN * KQ;
   constexpr int A_PER = (A_VEC + NT - 1) / NT;
@@ -84,9 +92,11 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void igemm_conv_kernel(
   static_assert(NT == 256 || NT == 512, "4 or 8 waves per block");
   static_assert(!BNB || (UT && SEG_IGEMM_STAGES == 1), "BN-backward loads: uniform-tap loader, one LDS stage");
   static_assert(NT % KQ == 0, "uniform kq per thread");
+  static_assert(!BF || BK % 16 == 0, "bf16 MFMA steps are 16 deep");
+  static_assert(sizeof(lds_t) * BM * LDSR >= 4 * (BM / WM + 1) * BN, "BN-statistics scratch fits in As");
 
-  __shared__ __attribute__((aligned(16))) float As[SEG_IGEMM_STAGES][BM * LDSR];
-  __shared__ __attribute__((aligned(16))) float Bs[SEG_IGEMM_STAGES][BN * LDSR];
+  __shared__ __attribute__((aligned(16))) lds_t As[SEG_IGEMM_STAGES][BM * LDSR];
+  __shared__ __attribute__((aligned(16))) lds_t Bs[SEG_IGEMM_STAGES][BN * LDSR];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm0 = (wave / WAVES_N) * WM, wn0 = (wave % WAVES_N) * WN;
@@ -265,6 +275,10 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void igemm_conv_kernel(
       rb[i] = v;
     }
   };
+  auto st_op = [](lds_t* p, f32x4 v) {
+    if constexpr (BF) *reinterpret_cast<bf16x4*>(p) = __builtin_convertvector(v, bf16x4);
+    else *reinterpret_cast<f32x4*>(p) = v;
+  };
   auto store_tiles = [&](int buf, const f32x4 (&ra)[A_PER], const f32x4 (&rb)[B_PER]) {
 #pragma unroll
     for (int i = 0; i < A_PER; ++i) {
@@ -275,13 +289,13 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void igemm_conv_kernel(
           const f32x4 t = seg_bnbwd4(v, ry[BNB ? i : 0], cf[0], cf[1], cf[2], cf[3], cf[4], cf[5], a.bnb.act);
           v = ((u_okbits >> i) & 1u) ? t : f32x4{0.f, 0.f, 0.f, 0.f};
         }
-        st4(&As[buf][(idx / KQ) * LDSR + (idx % KQ) * 4], v);
+        st_op(&As[buf][(idx / KQ) * LDSR + (idx % KQ) * 4], v);
       }
     }
 #pragma unroll
     for (int i = 0; i < B_PER; ++i) {
       const int idx = tid + i * NT;
-      if (B_VEC % NT == 0 || idx < B_VEC) st4(&Bs[buf][(idx / KQ) * LDSR + (idx % KQ) * 4], rb[i]);
+      if (B_VEC % NT == 0 || idx < B_VEC) st_op(&Bs[buf][(idx / KQ) * LDSR + (idx % KQ) * 4], rb[i]);
     }
   };
 
@@ -296,13 +310,34 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void igemm_conv_kernel(
   const int nk = (min(a.K - kbeg, a.kchunk) + BK - 1) / BK;
   const int lrow = lane & 31, lk = (lane >> 5) * 4;
   auto compute = [&](int cur) {
+    if constexpr (BF) {
+      const int lk8 = (lane >> 5) * 8;
+#pragma unroll
+      for (int ks = 0; ks < BK / 16; ++ks) {
+        bf16x8 af[MI], bfr[NI];
+#pragma unroll
+        for (int mi = 0; mi < MI; ++mi)
+          af[mi] = *reinterpret_cast<const bf16x8*>(&As[cur][(wm0 + mi * 32 + lrow) * LDSR + ks * 16 + lk8]);
+#pragma unroll
+        for (int ni = 0; ni < NI; ++ni)
+          bfr[ni] = *reinterpret_cast<const bf16x8*>(&Bs[cur][(wn0 + ni * 32 + lrow) * LDSR + ks * 16 + lk8]);
+#pragma unroll
+        for (int mi = 0; mi < MI; ++mi)
+#pragma unroll
+          for (int ni = 0; ni < NI; ++ni)
+            acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[mi], bfr[ni], acc[mi][ni], 0, 0, 0);
+      }
+      return;
+    }
 #pragma unroll
     for (int ks = 0; ks < BK / 8; ++ks) {
       f32x4 af[MI], bf[NI];
 #pragma unroll
-      for (int mi = 0; mi < MI; ++mi) af[mi] = ld4(&As[cur][(wm0 + mi * 32 + lrow) * LDSR + ks * 8 + lk]);
+      for (int mi = 0; mi < MI; ++mi)
+        af[mi] = *reinterpret_cast<const f32x4*>(&As[cur][(wm0 + mi * 32 + lrow) * LDSR + ks * 8 + lk]);
 #pragma unroll
-      for (int ni = 0; ni < NI; ++ni) bf[ni] = ld4(&Bs[cur][(wn0 + ni * 32 + lrow) * LDSR + ks * 8 + lk]);
+      for (int ni = 0; ni < NI; ++ni)
+        bf[ni] = *reinterpret_cast<const f32x4*>(&Bs[cur][(wn0 + ni * 32 + lrow) * LDSR + ks * 8 + lk]);
 #pragma unroll
       for (int kk = 0; kk < 4; ++kk)
 #pragma unroll
@@ -394,7 +429,7 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void igemm_conv_kernel(
     // accumulators, so no E[y^2]-E[y]^2 cancellation); merged over tiles with
     // Chan's formula in fp64 by seg_bn_stats_tiles.  LDS of the K loop is reused.
     constexpr int WR = BM / WM;
-    float* red = &As[0][0];            // [WR][BN]
+    float* red = reinterpret_cast<float*>(&As[0][0]);  // [WR][BN]
     float* tmean = red + WR * BN;      // [BN]
     const int nrows = min(BM, a.M - m0);
     const int wr = wave / WAVES_N;
@@ -448,14 +483,14 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void igemm_conv_kernel(
   }
 }
 
-template <int BM, int BN, int WM, int WN, int BK>
+template <int BM, int BN, int WM, int WN, int BK, bool BF>
 int launch_igemm_bk(const IgemmArgs& a, int ks, hipStream_t s) {
   const int grid = seg_cdiv(a.M, BM) * seg_cdiv(a.Cout, BN);
   const int splits = seg_cdiv(a.K, a.kchunk);
   const bool ut = SEG_IGEMM_UT && (SEG_IGEMM_UT2 ? a.Cin >= BK : a.Cin % BK == 0);
   constexpr int NT = 64 * (BM / WM) * (BN / WN);
-#define SEG_IG(KS, U) hipLaunchKernelGGL((igemm_conv_kernel<BM, BN, WM, WN, KS, BK, U>), dim3(grid, splits), dim3(NT), 0, s, a)
-#define SEG_IGB(KS) hipLaunchKernelGGL((igemm_conv_kernel<BM, BN, WM, WN, KS, BK, true, true>), dim3(grid, splits), dim3(NT), 0, s, a)
+#define SEG_IG(KS, U) hipLaunchKernelGGL((igemm_conv_kernel<BM, BN, WM, WN, KS, BK, U, false, BF>), dim3(grid, splits), dim3(NT), 0, s, a)
+#define SEG_IGB(KS) hipLaunchKernelGGL((igemm_conv_kernel<BM, BN, WM, WN, KS, BK, true, true, BF>), dim3(grid, splits), dim3(NT), 0, s, a)
   if (a.bnb.y) {
     if (!ut) return (int)hipErrorInvalidValue;
     if (ks == 1) SEG_IGB(1); else SEG_IGB(3);
@@ -477,13 +512,13 @@ int launch_igemm_bk(const IgemmArgs& a, int ks, hipStream_t s) {
 inline int igemm_bk(int K) { return (SEG_IGEMM_BK != 16 && (K <= 64 || (K % SEG_IGEMM_BK != 0 && K < 512))) ? 16 : SEG_IGEMM_BK; }
 
 // split-K: `splits` K ranges of whole BK chunks (a.part set by the caller when splits > 1)
-template <int BM, int BN, int WM, int WN>
+template <int BM, int BN, int WM, int WN, bool BF = false>
 int launch_igemm(IgemmArgs a, int ks, int splits, hipStream_t s) {
   const int bk = igemm_bk(a.K);
   const int nk = seg_cdiv(a.K, bk);
   a.kchunk = seg_cdiv(nk, splits) * bk;
-  if (bk == 16) return launch_igemm_bk<BM, BN, WM, WN, 16>(a, ks, s);
-  return launch_igemm_bk<BM, BN, WM, WN, SEG_IGEMM_BK>(a, ks, s);
+  if (bk == 16) return launch_igemm_bk<BM, BN, WM, WN, 16, BF>(a, ks, s);
+  return launch_igemm_bk<BM, BN, WM, WN, SEG_IGEMM_BK, BF>(a, ks, s);
 }
 
 struct TileCfg {
@@ -558,19 +593,10 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restr
   }
 }
 
-}  // namespace
-
-// out = act(conv(in, W) + bias + add).  `wk` is the packed weight of seg_pack_conv_weight
-// ([Cout][ldk], k = tap*Cin + ci).  ks in {1,3}; ks == 1 requires stride 1, pad 0.
-// Cin, ldin, ldk must be multiples of 4 and `in`/`wk` 16-byte aligned.  splits > 1
-// (from seg_conv_igemm_splits) runs split-K through `work` (>= splits*M*Cout floats)
-// and a reduce pass; it excludes `stat`.
-SEG_API int seg_conv_igemm_act(const float* in, long ldin, int N, int H, int W, int Cin,
-                               const float* wk, int ldk, const float* bias,
-                               float* out, long ldout, int Ho, int Wo, int Cout,
-                               int ks, int stride, int pad,
-                               const float* add, long ldadd, float* stat, int act, float* work, int splits,
-                               hipStream_t stream) {
+template <bool BF>
+int conv_igemm_impl(const float* in, long ldin, int N, int H, int W, int Cin, const float* wk, int ldk,
+                    const float* bias, float* out, long ldout, int Ho, int Wo, int Cout, int ks, int stride, int pad,
+                    const float* add, long ldadd, float* stat, int act, float* work, int splits, hipStream_t stream) {
   if ((Cin & 3) || (ldin & 3) || (ldk & 3) || (ks != 1 && ks != 3)) return (int)hipErrorInvalidValue;
   if (ks == 1 && (stride != 1 || pad != 0 || Ho != H || Wo != W)) return (int)hipErrorInvalidValue;
   if (act < SEG_ACT_NONE || act > SEG_ACT_RELU6 || (act && stat)) return (int)hipErrorInvalidValue;
@@ -585,27 +611,56 @@ SEG_API int seg_conv_igemm_act(const float* in, long ldin, int N, int H, int W, 
   if (a.M == 0 || Cout == 0) return 0;
   int rc;
   switch (pick_tile(a.M, Cout)) {
-    case 0: rc = launch_igemm<128, 128, 64, 64>(a, ks, splits, stream); break;
-    case 1: rc = launch_igemm<64, 128, 32, 64>(a, ks, splits, stream); break;
-    case 2: rc = launch_igemm<128, 64, 64, 32>(a, ks, splits, stream); break;
-    case 3: rc = launch_igemm<64, 64, 32, 32>(a, ks, splits, stream); break;
-    case 4: rc = launch_igemm<128, 96, 32, 96>(a, ks, splits, stream); break;
-    case 5: rc = launch_igemm<128, 160, 32, 160>(a, ks, splits, stream); break;
-    case 6: rc = launch_igemm<256, 32, 64, 32>(a, ks, splits, stream); break;
-    case 7: rc = launch_igemm<128, 32, 32, 32>(a, ks, splits, stream); break;
-    case 8: rc = launch_igemm<128, 128, 64, 32>(a, ks, splits, stream); break;
-    case 9: rc = launch_igemm<128, 128, 32, 64>(a, ks, splits, stream); break;
-    case 10: rc = launch_igemm<256, 128, 64, 64>(a, ks, splits, stream); break;
-    case 11: rc = launch_igemm<128, 256, 64, 64>(a, ks, splits, stream); break;
-    case 12: rc = launch_igemm<128, 64, 32, 32>(a, ks, splits, stream); break;
-    case 13: rc = launch_igemm<256, 64, 64, 32>(a, ks, splits, stream); break;
-    default: rc = launch_igemm<64, 128, 32, 32>(a, ks, splits, stream); break;
+    case 0: rc = launch_igemm<128, 128, 64, 64, BF>(a, ks, splits, stream); break;
+    case 1: rc = launch_igemm<64, 128, 32, 64, BF>(a, ks, splits, stream); break;
+    case 2: rc = launch_igemm<128, 64, 64, 32, BF>(a, ks, splits, stream); break;
+    case 3: rc = launch_igemm<64, 64, 32, 32, BF>(a, ks, splits, stream); break;
+    case 4: rc = launch_igemm<128, 96, 32, 96, BF>(a, ks, splits, stream); break;
+    case 5: rc = launch_igemm<128, 160, 32, 160, BF>(a, ks, splits, stream); break;
+    case 6: rc = launch_igemm<256, 32, 64, 32, BF>(a, ks, splits, stream); break;
+    case 7: rc = launch_igemm<128, 32, 32, 32, BF>(a, ks, splits, stream); break;
+    case 8: rc = launch_igemm<128, 128, 64, 32, BF>(a, ks, splits, stream); break;
+    case 9: rc = launch_igemm<128, 128, 32, 64, BF>(a, ks, splits, stream); break;
+    case 10: rc = launch_igemm<256, 128, 64, 64, BF>(a, ks, splits, stream); break;
+    case 11: rc = launch_igemm<128, 256, 64, 64, BF>(a, ks, splits, stream); break;
+    case 12: rc = launch_igemm<128, 64, 32, 32, BF>(a, ks, splits, stream); break;
+    case 13: rc = launch_igemm<256, 64, 64, 32, BF>(a, ks, splits, stream); break;
+    default: rc = launch_igemm<64, 128, 32, 32, BF>(a, ks, splits, stream); break;
   }
   if (rc || splits == 1) return rc;
   const long total = (long)a.M * Cout;
   hipLaunchKernelGGL(splitk_reduce_kernel, dim3((int)std::min<long>(seg_cdiv(total, 256), 4096)), dim3(256), 0,
                      stream, work, splits, (long)a.M, Cout, bias, add, ldadd, out, ldout, act);
   SEG_RET_LAST();
+}
+
+}  // namespace
+
+// out = act(conv(in, W) + bias + add).  `wk` is the packed weight of seg_pack_conv_weight
+// ([Cout][ldk], k = tap*Cin + ci).  ks in {1,3}; ks == 1 requires stride 1, pad 0.
+// Cin, ldin, ldk must be multiples of 4 and `in`/`wk` 16-byte aligned.  splits > 1
+// (from seg_conv_igemm_splits) runs split-K through `work` (>= splits*M*Cout floats)
+// and a reduce pass; it excludes `stat`.
+SEG_API int seg_conv_igemm_act(const float* in, long ldin, int N, int H, int W, int Cin,
+                               const float* wk, int ldk, const float* bias,
+                               float* out, long ldout, int Ho, int Wo, int Cout,
+                               int ks, int stride, int pad,
+                               const float* add, long ldadd, float* stat, int act, float* work, int splits,
+                               hipStream_t stream) {
+  return conv_igemm_impl<false>(in, ldin, N, H, W, Cin, wk, ldk, bias, out, ldout, Ho, Wo, Cout, ks, stride, pad,
+                                add, ldadd, stat, act, work, splits, stream);
+}
+
+// seg_conv_igemm_act with bf16 math (the bf16 configurations): the same fp32 tensors,
+// operands rounded to bf16 (RNE) in the LDS staging, fp32 accumulation and epilogue.
+SEG_API int seg_conv_igemm_bf16(const float* in, long ldin, int N, int H, int W, int Cin,
+                                const float* wk, int ldk, const float* bias,
+                                float* out, long ldout, int Ho, int Wo, int Cout,
+                                int ks, int stride, int pad,
+                                const float* add, long ldadd, float* stat, int act, float* work, int splits,
+                                hipStream_t stream) {
+  return conv_igemm_impl<true>(in, ldin, N, H, W, Cin, wk, ldk, bias, out, ldout, Ho, Wo, Cout, ks, stride, pad,
+                               add, ldadd, stat, act, work, splits, stream);
 }
 
 SEG_API int seg_conv_igemm(const float* in, long ldin, int N, int H, int W, int Cin,

@@ -33,16 +33,28 @@ struct WgradArgs {
   SegBnBwd bnb;  // BNB: dy is dA and the dY operand is the BN backward formed on load
 };
 
-template <int BM, int BN, int WM, int WN, int KS, bool BNB = false>
+// Row pitch (bf16 elements) of a k-major bf16 tile read with ds_read_b64_tr_b16: a
+// 32-lane half reads 4 rows x 64 B, conflict-free when the pitch is 64 or 192 B mod 256.
+constexpr int tr_pitch(int n) { return n % 128 == 32 || n % 128 == 96 ? n : tr_pitch(n + 32); }
+
+// BF ("bf16 math", BASELINE configs[2]/[4]): operands rounded to bf16 (RNE) into LDS,
+// still k-major ([pixel][channel], whole channel runs from HBM), 32 pixels per K chunk;
+// the MFMA fragment (lane: row r, k = 8h .. 8h+7) is gathered with two
+// ds_read_b64_tr_b16 (4 k-rows x 16 channels per 16-lane group, delivered
+// column-major) and fed to v_mfma_f32_32x32x16_bf16; fp32 accumulation and slabs.
+template <int BM, int BN, int WM, int WN, int KS, bool BNB = false, bool BF = false>
 __global__ __launch_bounds__(256) void wgrad_kernel(WgradArgs a) {
-  constexpr int AR = BM + 4, BR = BN + 4;
+  constexpr int BK = BF ? 32 : ::BK;  // pixels per K chunk
+  constexpr int AR = BF ? tr_pitch(BM) : BM + 4, BR = BF ? tr_pitch(BN) : BN + 4;
   constexpr int A_VEC = BK * BM / 4, B_VEC = BK * BN / 4;
   constexpr int A_PER = (A_VEC + 255) / 256, B_PER = (B_VEC + 255) / 256;
   constexpr int MI = WM / 32, NI = WN / 32, WAVES_N = BN / WN;
   static_assert((BM / WM) * (BN / WN) == 4, "4 waves per block");
+  static_assert(!(BNB && BF), "no BN-backward-on-load with bf16 math");
+  using lds_t = typename std::conditional<BF, __bf16, float>::type;
 
-  __shared__ __attribute__((aligned(16))) float As[SEG_WGRAD_STAGES][BK * AR];
-  __shared__ __attribute__((aligned(16))) float Bs[SEG_WGRAD_STAGES][BK * BR];
+  __shared__ __attribute__((aligned(16))) lds_t As[SEG_WGRAD_STAGES][BK * AR];
+  __shared__ __attribute__((aligned(16))) lds_t Bs[SEG_WGRAD_STAGES][BK * BR];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm0 = (wave / WAVES_N) * WM, wn0 = (wave % WAVES_N) * WN;
@@ -132,6 +144,10 @@ __global__ __launch_bounds__(256) void wgrad_kernel(WgradArgs a) {
       }
     }
   };
+  auto st_op = [](lds_t* p, f32x4 v) {
+    if constexpr (BF) *reinterpret_cast<bf16x4*>(p) = __builtin_convertvector(v, bf16x4);
+    else *reinterpret_cast<f32x4*>(p) = v;
+  };
   auto store_tiles = [&](int buf) {
 #pragma unroll
     for (int i = 0; i < A_PER; ++i) {
@@ -143,13 +159,13 @@ __global__ __launch_bounds__(256) void wgrad_kernel(WgradArgs a) {
           const f32x4 t = seg_bnbwd4(v, ry[BNB ? i : 0], cf[0], cf[1], cf[2], cf[3], cf[4], cf[5], a.bnb.act);
           v = ((a_okbits >> i) & 1u) ? t : f32x4{0.f, 0.f, 0.f, 0.f};
         }
-        st4(&As[buf][(idx / (BM / 4)) * AR + (idx % (BM / 4)) * 4], v);
+        st_op(&As[buf][(idx / (BM / 4)) * AR + (idx % (BM / 4)) * 4], v);
       }
     }
 #pragma unroll
     for (int i = 0; i < B_PER; ++i) {
       const int idx = tid + i * 256;
-      if (idx < B_VEC) st4(&Bs[buf][(idx / (BN / 4)) * BR + (idx % (BN / 4)) * 4], rb[i]);
+      if (idx < B_VEC) st_op(&Bs[buf][(idx / (BN / 4)) * BR + (idx % (BN / 4)) * 4], rb[i]);
     }
   };
 
@@ -164,6 +180,31 @@ __global__ __launch_bounds__(256) void wgrad_kernel(WgradArgs a) {
   const int lrow = lane & 31, lh = lane >> 5;
   const int nk = (kend - kbeg + BK - 1) / BK;
   auto compute = [&](int cur) {
+    if constexpr (BF) {
+      // this lane's transposed-read address inside a 4 x 16 block: row q, columns 4p..4p+3,
+      // block columns 16 * (lane >> 4 & 1) of the 32-wide fragment; k rows 8h + 4j + q
+      const int q = (lane & 15) >> 2, c4 = 16 * ((lane >> 4) & 1) + 4 * (lane & 3);
+#pragma unroll
+      for (int kk = 0; kk < BK / 16; ++kk) {
+        bf16x8 af[MI], bfr[NI];
+#pragma unroll
+        for (int mi = 0; mi < MI; ++mi) {
+          const lds_t* p = &As[cur][(16 * kk + 8 * lh + q) * AR + wm0 + mi * 32 + c4];
+          af[mi] = seg_cat8(seg_lds_tr4(p), seg_lds_tr4(p + 4 * AR));
+        }
+#pragma unroll
+        for (int ni = 0; ni < NI; ++ni) {
+          const lds_t* p = &Bs[cur][(16 * kk + 8 * lh + q) * BR + wn0 + ni * 32 + c4];
+          bfr[ni] = seg_cat8(seg_lds_tr4(p), seg_lds_tr4(p + 4 * BR));
+        }
+#pragma unroll
+        for (int mi = 0; mi < MI; ++mi)
+#pragma unroll
+          for (int ni = 0; ni < NI; ++ni)
+            acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[mi], bfr[ni], acc[mi][ni], 0, 0, 0);
+      }
+      return;
+    }
 #pragma unroll
       for (int kk = 0; kk < BK / 2; ++kk) {
         float af[MI], bf[NI];
@@ -217,9 +258,15 @@ __global__ __launch_bounds__(256) void wgrad_kernel(WgradArgs a) {
   }
 }
 
-template <int BM, int BN, int WM, int WN>
+template <int BM, int BN, int WM, int WN, bool BF = false>
 int launch_wgrad(const WgradArgs& a, int ks, int splits, hipStream_t s) {
   dim3 grid(seg_cdiv(a.Cout, BM) * seg_cdiv(a.Nw, BN) * splits);
+  if (BF) {
+    if (a.bnb.y) return (int)hipErrorInvalidValue;
+    if (ks == 1) hipLaunchKernelGGL((wgrad_kernel<BM, BN, WM, WN, 1, false, true>), grid, dim3(256), 0, s, a);
+    else hipLaunchKernelGGL((wgrad_kernel<BM, BN, WM, WN, 3, false, true>), grid, dim3(256), 0, s, a);
+    SEG_RET_LAST();
+  }
   if (a.bnb.y) {
     if (ks == 1) hipLaunchKernelGGL((wgrad_kernel<BM, BN, WM, WN, 1, true>), grid, dim3(256), 0, s, a);
     else hipLaunchKernelGGL((wgrad_kernel<BM, BN, WM, WN, 3, true>), grid, dim3(256), 0, s, a);
@@ -253,12 +300,21 @@ SEG_API int seg_conv_wgrad_splits(long M, int Cout, int Cin, int ks) {
 // part[s][co][tap*Cin+ci] = sum over split s's pixels of dY[p][co] * X[src(p,tap)][ci].
 static int conv_wgrad(const float* dy, long lddy, const float* x, long ldx, int N, int H, int W, int Cin, int Ho,
                       int Wo, int Cout, int ks, int stride, int pad, float* part, int splits, const SegBnBwd& bnb,
-                      hipStream_t stream);
+                      hipStream_t stream, bool bf = false);
 
 SEG_API int seg_conv_wgrad(const float* dy, long lddy, const float* x, long ldx,
                            int N, int H, int W, int Cin, int Ho, int Wo, int Cout,
                            int ks, int stride, int pad, float* part, int splits, hipStream_t stream) {
   return conv_wgrad(dy, lddy, x, ldx, N, H, W, Cin, Ho, Wo, Cout, ks, stride, pad, part, splits, SegBnBwd{}, stream);
+}
+
+// seg_conv_wgrad with bf16 math (the bf16 configurations): operands rounded to bf16
+// (RNE) in the LDS staging, fp32 accumulation, the same fp32 partial slabs.
+SEG_API int seg_conv_wgrad_bf16(const float* dy, long lddy, const float* x, long ldx,
+                                int N, int H, int W, int Cin, int Ho, int Wo, int Cout,
+                                int ks, int stride, int pad, float* part, int splits, hipStream_t stream) {
+  return conv_wgrad(dy, lddy, x, ldx, N, H, W, Cin, Ho, Wo, Cout, ks, stride, pad, part, splits, SegBnBwd{}, stream,
+                    true);
 }
 
 // seg_conv_wgrad of a conv whose output went through a train-mode BatchNorm, with the
@@ -275,7 +331,7 @@ SEG_API int seg_conv_wgrad_bnb(const float* dy, long lddy, const float* x, long 
 
 static int conv_wgrad(const float* dy, long lddy, const float* x, long ldx, int N, int H, int W, int Cin, int Ho,
                       int Wo, int Cout, int ks, int stride, int pad, float* part, int splits, const SegBnBwd& bnb,
-                      hipStream_t stream) {
+                      hipStream_t stream, bool bf) {
   if ((Cin & 3) || (ldx & 3) || (lddy & 3) || (ks != 1 && ks != 3) || splits < 1) return (int)hipErrorInvalidValue;
   if (ks == 1 && (stride != 1 || pad != 0)) return (int)hipErrorInvalidValue;
   WgradArgs a;
@@ -286,6 +342,14 @@ static int conv_wgrad(const float* dy, long lddy, const float* x, long ldx, int 
   a.bnb = bnb;
   int bm, bn;
   wgrad_tiles(Cout, a.Nw, &bm, &bn);
+  if (bf) {
+    a.kchunk = seg_cdiv(seg_cdiv(a.M, splits), 32) * 32;
+    if (bm == 128 && bn == 128) return launch_wgrad<128, 128, 64, 64, true>(a, ks, splits, stream);
+    if (bm == 128) return launch_wgrad<128, 32, 32, 32, true>(a, ks, splits, stream);
+    if (bm == 64 && bn == 128) return launch_wgrad<64, 128, 32, 64, true>(a, ks, splits, stream);
+    if (bm == 64) return launch_wgrad<64, 64, 32, 32, true>(a, ks, splits, stream);
+    return launch_wgrad<32, 128, 32, 32, true>(a, ks, splits, stream);
+  }
   if (bm == 128 && bn == 128) return launch_wgrad<128, 128, 64, 64>(a, ks, splits, stream);
   if (bm == 128) return launch_wgrad<128, 32, 32, 32>(a, ks, splits, stream);
   if (bm == 64 && bn == 128) return launch_wgrad<64, 128, 32, 64>(a, ks, splits, stream);

@@ -22,6 +22,8 @@ PROTOTYPES = {
     "seg_conv_igemm": (_I, [_V, _L, _I, _I, _I, _I, _V, _I, _V, _V, _L, _I, _I, _I, _I, _I, _I, _V, _L, _V, _V]),
     "seg_conv_igemm_act": (_I, [_V, _L, _I, _I, _I, _I, _V, _I, _V, _V, _L, _I, _I, _I, _I, _I, _I, _V, _L, _V, _I,
                                 _V, _I, _V]),
+    "seg_conv_igemm_bf16": (_I, [_V, _L, _I, _I, _I, _I, _V, _I, _V, _V, _L, _I, _I, _I, _I, _I, _I, _V, _L, _V, _I,
+                                 _V, _I, _V]),
     "seg_conv_igemm_splits": (_I, [_L, _I, _I, _I]),
     "seg_conv_igemm_bnb": (_I, [_V, _L, _I, _I, _I, _I, _V, _I, _V, _L, _I, _I, _I, _V, _L, _V, _L, _V, _V, _V, _V, _I,
                                 _V]),
@@ -43,6 +45,7 @@ PROTOTYPES = {
     "seg_pack_conv_weight": (_I, [_V, _V, _I, _I, _I, _I, _I, _I, _V]),
     "seg_conv_wgrad_splits": (_I, [_L, _I, _I, _I]),
     "seg_conv_wgrad": (_I, [_V, _L, _V, _L, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _V, _I, _V]),
+    "seg_conv_wgrad_bf16": (_I, [_V, _L, _V, _L, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _V, _I, _V]),
     "seg_conv_wgrad_bnb": (_I, [_V, _L, _V, _L, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _V, _I, _V, _L, _V, _V, _V, _V,
                                 _I, _V]),
     "seg_conv_wgrad_reduce": (_I, [_V, _I, _V, _I, _I, _I, _I, _I, _V]),

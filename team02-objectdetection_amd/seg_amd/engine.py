@@ -128,6 +128,8 @@ class ConvOp:
         self.pw_fused = False
         # BN backward applied on load by the gradient kernels (seg_*_bnb), decided at pack time
         self.bnb = False
+        # bf16 math (Program.math == "bf16"): seg_conv_igemm_bf16 / seg_conv_wgrad_bf16
+        self.bf = False
         self.ks = conv.kernel_size[0]
         self.stride = conv.stride[0]
         self.pad = conv.padding[0]
@@ -182,6 +184,10 @@ class ConvOp:
                 _timed_call("wino3_fwd", self.flops(), "seg_conv_wino", rt.ptr(i), i.ld, i.N, i.H, i.W, self.cin_pad,
                             self.wk_wf.data_ptr(), self.cin_pad, bias, rt.ptr(y), y.ld, self.cout, None, 0, statp,
                             work.data_ptr(), s)
+            elif self.bf:
+                _timed_call(f"igemm{self.ks}_fwd", self.flops(), "seg_conv_igemm_bf16", rt.ptr(i), i.ld, i.N, i.H,
+                            i.W, self.cin_pad, wk_ptr, ldk, bias, rt.ptr(y), y.ld, y.H, y.W, self.cout, self.ks,
+                            self.stride, self.pad, None, 0, statp, ACT_NONE, None, 1, s)
             else:
                 _timed_call(f"igemm{self.ks}_fwd", self.flops(), "seg_conv_igemm", rt.ptr(i), i.ld, i.N, i.H, i.W,
                             self.cin_pad, wk_ptr, ldk, bias, rt.ptr(y), y.ld, y.H, y.W, self.cout, self.ks,
@@ -384,7 +390,8 @@ class ConvOp:
             else:
                 splits = query("seg_conv_wgrad_splits", M, self.cout, self.cin_pad, self.ks)
                 part = rt.tmp(splits * self.cout * self.ks * self.ks * self.cin_pad)
-                _timed_call(f"igemm{self.ks}_wgrad", self.flops(), "seg_conv_wgrad", dYp, dY.ld, rt.ptr(i), i.ld,
+                _timed_call(f"igemm{self.ks}_wgrad", self.flops(),
+                            "seg_conv_wgrad_bf16" if self.bf else "seg_conv_wgrad", dYp, dY.ld, rt.ptr(i), i.ld,
                             i.N, i.H, i.W, self.cin_pad, y.H, y.W, self.cout, self.ks, self.stride, self.pad,
                             part.data_ptr(), splits, s)
                 call("seg_conv_wgrad_reduce", part.data_ptr(), splits, gw, self.cout, self.cin, self.ks, 0, 0, s)
@@ -410,6 +417,10 @@ class ConvOp:
                 _timed_call("wino3_dgrad", self.flops(), "seg_conv_wino", dYp, dY.ld, y.N, y.H, y.W, kin,
                             self.wk_wd.data_ptr(), kin, None, rt.gptr(i), i.ld, self.cin, add_ptr, add_ld, None,
                             work.data_ptr(), s)
+            elif self.bf:
+                _timed_call(f"igemm{self.ks}_dgrad", self.flops(), "seg_conv_igemm_bf16", dYp, dY.ld, y.N, y.H, y.W,
+                            kin, self.wk_d.data_ptr(), self.ldk_d, None, rt.gptr(i), i.ld, i.H, i.W, self.cin,
+                            self.ks, 1, self.pad, add_ptr, add_ld, None, ACT_NONE, None, 1, s)
             else:
                 _timed_call(f"igemm{self.ks}_dgrad", self.flops(), "seg_conv_igemm", dYp, dY.ld, y.N, y.H, y.W, kin,
                             self.wk_d.data_ptr(), self.ldk_d, None, rt.gptr(i), i.ld, i.H, i.W, self.cin, self.ks, 1,
@@ -464,8 +475,11 @@ class PoolOp:
 # ------------------------------------------------------------------------ program
 
 class Program:
-    def __init__(self, N, H, W):
+    def __init__(self, N, H, W, math="f32"):
+        if math not in MATHS:
+            raise ValueError(f"conv math must be one of {MATHS}, got {math!r}")
         self.N, self.H, self.W = N, H, W
+        self.math = math     # "f32" | "bf16" (set_conv_math)
         self.bufs = {}       # name -> (rows, ld)
         self.ops = []
         self.logits = None   # Act of the (low-res for MobileNetV2UNet) logits
@@ -528,6 +542,23 @@ class Program:
                 max_elems = max(max_elems, 9 * op.cout)
                 continue
             y = op.y
+            op.bf = self.math == "bf16"
+            if op.bf:
+                # bf16 math: every dense / pointwise conv (fwd, dgrad, wgrad) on the bf16 implicit GEMM
+                op.pw_fused = op.bnb = False
+                op.wino_f = op.wino_d = op.wino_w = op.halo_f = op.halo_d = False
+                if not (op.ks == 1 and op.cin_pad == op.cin):
+                    op.ldk_f = r4(op.ks * op.ks * op.cin_pad)
+                    op.wk_f = torch.empty(op.cout * op.ldk_f, device=dev, dtype=torch.float32)
+                    jobs.append((w.data_ptr(), op.wk_f.data_ptr(), op.cout, op.cin, op.ks, op.ldk_f, 0, op.cin_pad))
+                    max_elems = max(max_elems, op.cout * op.ldk_f)
+                if not op.first:
+                    kin = r4(op.cout)
+                    op.ldk_d = r4(op.ks * op.ks * kin)
+                    op.wk_d = torch.empty(op.cin * op.ldk_d, device=dev, dtype=torch.float32)
+                    jobs.append((w.data_ptr(), op.wk_d.data_ptr(), op.cout, op.cin, op.ks, op.ldk_d, 1, kin))
+                    max_elems = max(max_elems, op.cin * op.ldk_d)
+                continue
             op.pw_fused = (PW_FUSED and op.ks == 1 and op.bn is not None and op.conv.bias is None and not op.first
                            and op.cin % 4 == 0 and op.conv.weight.requires_grad
                            and bool(query("seg_pw_bwd_fused_ok", op.cin, op.cout)))
@@ -752,13 +783,37 @@ def build_unet(model, N, H, W) -> Program:
     return p
 
 
-def build_program(model, N, H, W) -> Program:
+def build_program(model, N, H, W, math="f32") -> Program:
     from .unet import MobileNetV2UNet, UNet, LightUNet
     if isinstance(model, MobileNetV2UNet):
-        return build_mobilenet_unet(model, N, H, W)
-    if isinstance(model, (UNet, LightUNet)):
-        return build_unet(model, N, H, W)
-    raise TypeError(f"no HIP program for {type(model).__name__}")
+        prog = build_mobilenet_unet(model, N, H, W)
+    elif isinstance(model, (UNet, LightUNet)):
+        prog = build_unet(model, N, H, W)
+    else:
+        raise TypeError(f"no HIP program for {type(model).__name__}")
+    if math not in MATHS:
+        raise ValueError(f"conv math must be one of {MATHS}, got {math!r}")
+    prog.math = math
+    return prog
+
+
+# Conv arithmetic of a model's programs.  "f32" (default): exact fp32 products on the
+# f32 MFMA (plus Winograd / LDS-halo kernels where they measured faster), the
+# reference's own arithmetic.  "bf16": the bf16 configurations (BASELINE configs[2],
+# [4]; the reference's equivalent is torch.autocast(dtype=torch.bfloat16) around the
+# forward) -- every dense / pointwise conv, forward and both gradients, multiplies
+# bf16-rounded operands on the bf16 MFMA with fp32 accumulation; activations, BN,
+# depthwise convs, the loss and the optimizer stay fp32.
+MATHS = ("f32", "bf16")
+
+
+def set_conv_math(model, math: str):
+    """Select the conv arithmetic ("f32" | "bf16") of `model` (or a DataParallel wrapper's module)."""
+    if math not in MATHS:
+        raise ValueError(f"conv math must be one of {MATHS}, got {math!r}")
+    model = getattr(model, "module", model)
+    model.__dict__["_segamd_math"] = math
+    return model
 
 
 # ------------------------------------------------------------------------ runtime
@@ -955,10 +1010,11 @@ _PROGRAM_CACHE_ATTR = "_segamd_programs"
 
 def get_program(model, N, H, W) -> Program:
     cache = model.__dict__.setdefault(_PROGRAM_CACHE_ATTR, {})
-    key = (N, H, W)
+    math = model.__dict__.get("_segamd_math", "f32")
+    key = (N, H, W, math)
     prog = cache.get(key)
     if prog is None:
-        prog = cache[key] = build_program(model, N, H, W)
+        prog = cache[key] = build_program(model, N, H, W, math)
     return prog
 
 

@@ -53,6 +53,7 @@ def main():
     ap.add_argument("--batch", type=int, default=32)
     ap.add_argument("--height", type=int, default=256)
     ap.add_argument("--width", type=int, default=512)
+    ap.add_argument("--math", choices=("f32", "bf16"), default="f32")
     a = ap.parse_args()
     lib()
     model = getattr(seg_amd, a.model)(10)
@@ -69,8 +70,12 @@ def main():
         y = torch.empty(N * Ho * Wo, E.r4(Cout), device="cuda")
 
         def run():
-            call("seg_conv_igemm", x.data_ptr(), Cin, N, H, W, Cin, wk.data_ptr(), ldk, None, y.data_ptr(),
-                 E.r4(Cout), Ho, Wo, Cout, ks, st, pad, None, 0, None, s)
+            if a.math == "bf16":
+                call("seg_conv_igemm_bf16", x.data_ptr(), Cin, N, H, W, Cin, wk.data_ptr(), ldk, None, y.data_ptr(),
+                     E.r4(Cout), Ho, Wo, Cout, ks, st, pad, None, 0, None, 0, None, 1, s)
+            else:
+                call("seg_conv_igemm", x.data_ptr(), Cin, N, H, W, Cin, wk.data_ptr(), ldk, None, y.data_ptr(),
+                     E.r4(Cout), Ho, Wo, Cout, ks, st, pad, None, 0, None, s)
         times = []
         for t in range(len(TILES)):
             call("seg_igemm_force_tile", t)

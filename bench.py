@@ -55,9 +55,10 @@ def parse():
     ap.add_argument("--workload", choices=("train", "infer"), default="train",
                     help="train: BASELINE configs[1] (the headline); infer: configs[3], inference.py's per-frame path")
     ap.add_argument("--frames", type=int, default=500, help="timed frames of --workload infer")
-    ap.add_argument("--math", choices=("f32", "bf16"), default="f32",
-                    help="conv arithmetic: f32 = configs[1] (default, the headline); bf16 = the bf16 configurations "
-                         "(configs[2]/[4]): bf16 MFMA operands, fp32 accumulation / activations / BN / Adam")
+    ap.add_argument("--math", choices=("f32", "bf16", "f16"), default=None,
+                    help="conv arithmetic. train: f32 = configs[1] (default, the headline); bf16 = the bf16 "
+                         "configurations (configs[2]/[4]): bf16 MFMA operands, fp32 accumulation / activations / BN "
+                         "/ Adam.  infer: f16 = configs[3] (default), f32, bf16")
     ap.add_argument("--model", choices=("MobileNetV2UNet", "UNet"), default="MobileNetV2UNet",
                     help="UNet = BASELINE configs[4] shape family (use --height 512 --width 1024 --batch 8)")
     return ap.parse_args()
@@ -104,7 +105,7 @@ def bench_infer(args):
     frame = g.integers(0, 256, (720, 1280, 3), dtype=np.uint8)
     res = {}
     for mode in ("graph", "eager", "graph_h2d"):
-        pred = Predictor(model, frame_hw=(720, 1280), graph=mode != "eager")
+        pred = Predictor(model, frame_hw=(720, 1280), graph=mode != "eager", math=args.math)
         pred.set_frame(frame)
         fn = (lambda: pred(frame)) if mode == "graph_h2d" else pred.step
         for _ in range(max(args.warmup, 3)):
@@ -140,7 +141,10 @@ def bench_infer(args):
     line = {"metric": "frames/sec inference MobileNetV2UNet 720x1280 frame -> 128x256, bs=1 (BASELINE configs[3])",
             "value": round(1.0 / res["graph"], 1), "unit": "frames/s", "n_gpus": 1, "steps": args.frames,
             "warmup": args.warmup, "ms_per_step": round(res["graph"] * 1e3, 4), "higher_is_better": True,
-            "scaling": "none", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+            "scaling": "none", "vs_baseline": None, "dtype": args.math, "data": "synthetic",
+            "math": {"f32": "fp32 everywhere", "f16": "folded conv operands fp16 (RNE) on the f16 MFMA, fp32 "
+                     "accumulation; depthwise, preprocess and argmax in fp32",
+                     "bf16": "folded conv operands bf16 on the bf16 MFMA, fp32 accumulation"}[args.math],
             "config": {"workload": "inference.py per-frame path: cv2-style resize + normalise, BN-folded eval forward, "
                                    "argmax + nearest mask, one hipGraph replay per frame",
                        "model": "MobileNetV2UNet", "global_batch": 1, "frame": [720, 1280], "image": [128, 256],
@@ -153,6 +157,10 @@ def bench_infer(args):
 
 def main():
     args = parse()
+    if args.math is None:
+        args.math = "f16" if args.workload == "infer" else "f32"
+    if args.workload == "train" and args.math == "f16":
+        raise SystemExit("--math f16 is the inference configuration (--workload infer)")
     if args.workload == "infer":
         return bench_infer(args)
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -263,6 +271,22 @@ def main():
                            "avg_launch_us": round(ws / max(wn, 1) * 1e6, 2)},
                 "all_mfma_convs": {"achieved": round(af / as_ / 1e12, 2) if as_ else None, "launches": an,
                                    "share_of_step": round(as_ / dt, 4)}}
+        # The live figure above includes CU sharing with the weight-gradient side stream
+        # (engine.OVERLAP): the same launches re-timed over 3 untimed steps with the side
+        # stream off show what the kernels reach when they own the GPU.
+        saved = engine.OVERLAP
+        engine.OVERLAP = False
+        iso = engine.KernelTimer()
+        engine.TIMER = iso
+        for _ in range(3):
+            step()
+        torch.cuda.synchronize()
+        engine.TIMER = None
+        engine.OVERLAP = saved
+        rec = iso.elapsed()
+        ifl, isec, inn = family({"igemm3_fwd", "igemm3_dgrad", "wino3_fwd", "wino3_dgrad"})
+        roof["without_side_stream"] = {"achieved": round(ifl / isec / 1e12, 2), "frac": round(ifl / isec / 1e12 / peak, 4),
+                                       "avg_launch_us": round(isec / max(inn, 1) * 1e6, 2), "launches": inn}
 
     if rank == 0:
         cpu = None

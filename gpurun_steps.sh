@@ -18,6 +18,8 @@ for step in "$@"; do
     bf16)  run bf16 600 python -u -m pytest tests/test_gpu_bf16.py -q -m gpu -x -s --timeout 300 --timeout-method thread ;;
     benchbf) run benchbf 600 python bench.py --steps 10 --warmup 3 --math bf16 --no-cpu-baseline ;;
     unetbf) run unetbf 600 python bench.py --model UNet --height 512 --width 1024 --batch 8 --steps 3 --warmup 2 --math bf16 --no-cpu-baseline ;;
+    inferg) run inferg 600 python -u -m pytest tests/test_gpu_infer.py -q -m gpu -x -s --timeout 300 --timeout-method thread ;;
+    infer32) run infer32 600 python bench.py --workload infer --frames 300 --math f32 --no-cpu-baseline ;;
     benchq) run benchq 600 python bench.py --steps 5 --warmup 2 --no-cpu-baseline ;;
     unet) run unet 600 python bench.py --model UNet --height 512 --width 1024 --batch 8 --steps 3 --warmup 2 ;;
     infer) run infer 600 python bench.py --workload infer --frames 300 --cpu-seconds 8 ;;

@@ -75,6 +75,16 @@ int seg_conv_igemm_bf16(const float* in, long ldin, int N, int H, int W, int Cin
                         int ks, int stride, int pad,
                         const float* add, long ldadd, float* stat, int act, float* work, int splits,
                         hipStream_t stream);
+/* seg_conv_igemm_act with fp16 math (BASELINE configs[3], the fp16 inference
+ * configuration; replaces the autocast fp16 conv2d of inference.py:162-163): operands
+ * rounded to fp16 (RNE) in the LDS staging, v_mfma_f32_32x32x16_f16, fp32 accumulation
+ * and epilogue.  Operands beyond the fp16 range become inf, as under autocast. */
+int seg_conv_igemm_f16(const float* in, long ldin, int N, int H, int W, int Cin,
+                       const float* wk, int ldk, const float* bias,
+                       float* out, long ldout, int Ho, int Wo, int Cout,
+                       int ks, int stride, int pad,
+                       const float* add, long ldadd, float* stat, int act, float* work, int splits,
+                       hipStream_t stream);
 /* Split-K factor for seg_conv_igemm_act (1 = none): > 1 only when the output tiles
  * cannot fill the 256 CUs (batch-1 inference). */
 int seg_conv_igemm_splits(long M, int Cout, int Cin, int ks);

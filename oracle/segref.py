@@ -210,35 +210,40 @@ def miou(pred, target, classes):
 # gradient in the backward, then runs in the oracle's own precision (fp64 gives
 # "exact products of bf16 operands").  Used only to size the bf16 tolerance budget
 # (tests/test_gpu_bf16.py), like the fp32 ensemble does for the fp32 path.
-class _RoundBf16(torch.autograd.Function):
+class _Round(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, t):
-        return t.to(torch.bfloat16).to(t.dtype)
+    def forward(ctx, t, dtype):
+        ctx.dtype = dtype
+        return t.to(dtype).to(t.dtype)
 
     @staticmethod
     def backward(ctx, g):
-        return g.to(torch.bfloat16).to(g.dtype)
-
-
-def _conv2d_bf16(x, w, b=None, stride=1, padding=0, dilation=1, groups=1):
-    if groups == 1:
-        x, w = _RoundBf16.apply(x), _RoundBf16.apply(w)
-    return torch.nn.functional.conv2d(x, w, b, stride, padding, dilation, groups)
+        return g.to(ctx.dtype).to(g.dtype), None
 
 
 class _F:
-    conv2d = staticmethod(_conv2d_bf16)
+    def __init__(self, dtype):
+        self.dtype = dtype
+
+    def conv2d(self, x, w, b=None, stride=1, padding=0, dilation=1, groups=1):
+        if groups == 1:
+            x, w = _Round.apply(x, self.dtype), _Round.apply(w, self.dtype)
+        return torch.nn.functional.conv2d(x, w, b, stride, padding, dilation, groups)
 
     def __getattr__(self, k):
         return getattr(torch.nn.functional, k)
 
 
 class bf16_convs:
-    """Context manager: this module's convolutions use bf16 operands (see above)."""
+    """Context manager: this module's convolutions use bf16 operands (see above);
+    dtype=torch.float16 gives the fp16 inference configuration (BASELINE configs[3])."""
+
+    def __init__(self, dtype=torch.bfloat16):
+        self.dtype = dtype
 
     def __enter__(self):
         global F
-        self._saved, F = F, _F()
+        self._saved, F = F, _F(self.dtype)
         return self
 
     def __exit__(self, *exc):

@@ -17,624 +17,9 @@
 // ds_read_b128: lane half h at step kk of sub-chunk ks carries k = 8ks + 4h + kk
 // for BOTH operands, which is all the MFMA needs to sum the right products.
 // Two LDS stages, register prefetch of the next K chunk, one barrier per chunk.
-#include "common.h"
+#include "igemm_impl.h"
 
-namespace {
-
-// 16 zero bytes in device memory: operand slots that fall outside the image or
-// the matrix load from here instead of being zeroed after the load, so no
-// instruction touches a prefetched register before the K chunk that consumes it
-// (a post-load select forces an early s_waitcnt and exposes the HBM latency).
-__device__ __attribute__((aligned(16))) float g_zero4[4];
-
-struct IgemmArgs {
-  const float* in; long ldin;
-  const float* wk; int ldk;      // packed weights [Cout][ldk], k contiguous
-  const float* bias;             // [Cout] or nullptr
-  const float* add; long ldadd;  // optional addend [M][ldadd] (may alias out)
-  float* out; long ldout;
-  float* stat;                   // optional BN partials [tilesM][2][Cout]: tile sum and M2 of `out`
-  int N, H, W, Cin;
-  int Ho, Wo, Cout;
-  int stride, pad;
-  int K, M;
-  int kchunk;                    // split-K: K range of blockIdx.y (a multiple of BK); == K when unsplit
-  float* part;                   // split-K: raw partial sums [gridDim.y][M][Cout] (no epilogue), else null
-  int act;                       // epilogue activation of act(acc + bias + add) (SegAct); 0 in training
-  SegBnBwd bnb;                  // BNB kernels: `in` is dA and the A operand is the BN backward dY
-};
-
-#ifndef SEG_IGEMM_DEPTH
-#define SEG_IGEMM_DEPTH 1  // register prefetch depth of the K loop (chunks in flight)
-#endif
-#ifndef SEG_IGEMM_STAGES
-#define SEG_IGEMM_STAGES 1  // LDS stages of the K loop
-#endif
-#ifndef SEG_IGEMM_UT
-#define SEG_IGEMM_UT 1  // uniform-tap loader when Cin % BK == 0
-#endif
-#ifndef SEG_IGEMM_UT2
-#define SEG_IGEMM_UT2 1  // uniform-tap loader also for Cin % BK != 0 (chunks spanning two taps)
-#endif
-#ifndef SEG_IGEMM_BK
-#define SEG_IGEMM_BK 32  // measured (MI355X): single LDS stage + BK 32 beats 2 stages x BK 16 by 4-13% on the cfg2 shapes
-#endif
-
-// BM x BN output tile per 256-thread block, 4 waves laid out (BM/WM) x (BN/WN),
-// each wave owning WM x WN = (WM/32) x (WN/32) accumulators of 32x32.
-// UT ("uniform tap"): Cin >= BK, so every BK-deep K chunk spans at most two
-// filter taps; the chunk's tap and channel offset are wave-uniform scalars and
-// each operand slot is a fixed base offset plus one of two scalar tap offsets --
-// a few VALU ops per slot instead of the general path's per-slot tap tracking
-// and bounds arithmetic.  The general path remains for Cin < BK (the stem).
-// BNB (data gradient of a conv whose output went through a train-mode BatchNorm):
-// the A operand dY is formed on load from dA (`in`) and the raw conv output y
-// (seg_bnbwd4), so the BN backward never writes dY.  UT path only; zero padding
-// (out-of-image taps) stays zero.
-//
-// BF ("bf16 math", the bf16 configurations of BASELINE configs[2]/[4]): activations
-// and weights stay fp32 in HBM; each operand is rounded to bf16 (RNE) on its way
-// into LDS and the K loop runs v_mfma_f32_32x32x16_bf16 (fp32 accumulation, 8x the
-// K per instruction).  The bf16 LDS rows keep the same 80-byte pitch at BK 32, so
-// the ds_read_b128 fragment reads (lane half h: k = 16ks + 8h .. +7) stay
-// conflict-free; the epilogue (bias, BN statistics, addend) is the fp32 one.
-template <int BM, int BN, int WM, int WN, int KS, int BK, bool UT, bool BNB = false, bool BF = false>
-__global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void igemm_conv_kernel(IgemmArgs a) {
-  constexpr int NT = 64 * (BM / WM) * (BN / WN);  // threads: one wave per WM x WN sub-tile (4 or 8 waves)
-  constexpr int LDSR = BF ? BK + 8 : BK + 4;  // LDS row stride (elements): conflict-free b128 reads
-  using lds_t = typename std::conditional<BF, __bf16, float>::type;
-  constexpr int KQ = BK / 4;          // float4 groups per tile row
-  constexpr int A_VEC = BM * KQ, B_VEC = BN * KQ;
-  constexpr int A_PER = (A_VEC + NT - 1) / NT;
-  constexpr int B_PER = (B_VEC + NT - 1) / NT;
-  constexpr int MI = WM / 32, NI = WN / 32;
-  constexpr int WAVES_N = BN / WN;
-  static_assert(NT == 256 || NT == 512, "4 or 8 waves per block");
-  static_assert(!BNB || (UT && SEG_IGEMM_STAGES == 1), "BN-backward loads: uniform-tap loader, one LDS stage");
-  static_assert(NT % KQ == 0, "uniform kq per thread");
-  static_assert(!BF || BK % 16 == 0, "bf16 MFMA steps are 16 deep");
-  static_assert(sizeof(lds_t) * BM * LDSR >= 4 * (BM / WM + 1) * BN, "BN-statistics scratch fits in As");
-
-  __shared__ __attribute__((aligned(16))) lds_t As[SEG_IGEMM_STAGES][BM * LDSR];
-  __shared__ __attribute__((aligned(16))) lds_t Bs[SEG_IGEMM_STAGES][BN * LDSR];
-
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wm0 = (wave / WAVES_N) * WM, wn0 = (wave % WAVES_N) * WN;
-  const int tiles_n = (a.Cout + BN - 1) / BN;
-  const int lid = xcd_swizzle(blockIdx.x, gridDim.x);  // adjacent image rows on one XCD's L2
-  const int tn = lid % tiles_n, tm = lid / tiles_n;
-  const int m0 = tm * BM, n0 = tn * BN;
-  const int kbeg = blockIdx.y * a.kchunk;  // split-K: this block's K range [kbeg, kbeg + kchunk)
-
-  // Per-thread A slots: the pixel is fixed across the K loop; the (tap, channel)
-  // position advances by BK per chunk without integer division.
-  long a_base[A_PER];
-  int a_hi0[A_PER], a_wi0[A_PER], a_ci[A_PER], a_ky[A_PER], a_kx[A_PER], a_k[A_PER];
-  bool a_ok[A_PER];
-#pragma unroll
-  for (int i = 0; i < A_PER; ++i) {
-    const int idx = tid + i * NT;
-    const int row = idx / KQ, kq = idx % KQ;
-    const int p = m0 + row;
-    a_ok[i] = (idx < A_VEC) && (p < a.M);
-    const int pp = a_ok[i] ? p : 0;
-    a_k[i] = kq * 4 + kbeg;
-    const int tap = a_k[i] / a.Cin;
-    a_ci[i] = a_k[i] - tap * a.Cin;
-    a_ky[i] = tap / KS;
-    a_kx[i] = tap - a_ky[i] * KS;
-    if (KS == 1) {
-      a_base[i] = (long)pp * a.ldin;
-      a_hi0[i] = a_wi0[i] = 0;
-    } else {
-      const int hw = a.Ho * a.Wo;
-      const int n = pp / hw, rem = pp - n * hw;
-      const int ho = rem / a.Wo, wo = rem - ho * a.Wo;
-      a_base[i] = (long)n * a.H * a.W;
-      a_hi0[i] = ho * a.stride - a.pad;
-      a_wi0[i] = wo * a.stride - a.pad;
-    }
-  }
-
-  // "UT" state (Cin >= BK: a K chunk spans at most two filter taps).  Per slot: the
-  // pixel's base offset and its 9-bit tap-validity mask; the chunk's starting tap
-  // and channel are wave-uniform scalars, and a slot whose k (= chunk start +
-  // 4*kq) crosses Cin takes the next tap.  kq = tid % KQ for every slot (256 % KQ == 0).
-  long u_aoff[A_PER], u_boff[B_PER];
-  unsigned u_mask[A_PER];
-  bool u_bok[B_PER];
-  const int u_kq4 = (tid % KQ) * 4;
-  int u_tap = 0, u_ci = 0;
-  long u_toff0 = 0, u_toff1 = 0;
-  auto tap_off = [&](int t) -> long { return ((long)(t / KS) * a.W + t % KS) * a.ldin; };
-  // BNB: y-side offsets (y has its own row stride), the loaded y, the slots' validity
-  // bits and the chunk's channel-group coefficients
-  long u_yoff[BNB ? A_PER : 1];
-  long u_ytoff0 = 0, u_ytoff1 = 0;
-  f32x4 ry[BNB ? A_PER : 1], cf[6];
-  unsigned u_okbits = 0;
-  auto tap_off_y = [&](int t) -> long { return ((long)(t / KS) * a.W + t % KS) * a.bnb.ldy; };
-  if (UT) {
-#pragma unroll
-    for (int i = 0; i < A_PER; ++i) {
-      const int idx = tid + i * NT;
-      const int row = idx / KQ;
-      const int p = m0 + row;
-      const bool ok = (idx < A_VEC) && (p < a.M);
-      const int pp = ok ? p : 0;
-      if (KS == 1) {
-        u_aoff[i] = (long)pp * a.ldin;
-        if (BNB) u_yoff[BNB ? i : 0] = (long)pp * a.bnb.ldy;
-        u_mask[i] = ok ? 1u : 0u;
-      } else {
-        const int hw = a.Ho * a.Wo;
-        const int n = pp / hw, rem = pp - n * hw;
-        const int ho = rem / a.Wo, wo = rem - ho * a.Wo;
-        const int hi0 = ho * a.stride - a.pad, wi0 = wo * a.stride - a.pad;
-        u_aoff[i] = (((long)n * a.H + hi0) * a.W + wi0) * a.ldin;
-        if (BNB) u_yoff[BNB ? i : 0] = (((long)n * a.H + hi0) * a.W + wi0) * a.bnb.ldy;
-        unsigned m = 0;
-#pragma unroll
-        for (int t = 0; t < KS * KS; ++t) {
-          const int hi = hi0 + t / KS, wi = wi0 + t % KS;
-          if (ok && (unsigned)hi < (unsigned)a.H && (unsigned)wi < (unsigned)a.W) m |= 1u << t;
-        }
-        u_mask[i] = m;
-      }
-    }
-#pragma unroll
-    for (int i = 0; i < B_PER; ++i) {
-      const int idx = tid + i * NT;
-      const int co = n0 + idx / KQ;
-      u_bok[i] = idx < B_VEC && co < a.Cout;
-      u_boff[i] = (long)(u_bok[i] ? co : 0) * a.ldk + u_kq4;
-    }
-    u_tap = kbeg / a.Cin;
-    u_ci = kbeg - u_tap * a.Cin;
-    u_toff0 = tap_off(u_tap);
-    u_toff1 = tap_off(u_tap + 1);
-    if (BNB) {
-      u_ytoff0 = tap_off_y(u_tap);
-      u_ytoff1 = tap_off_y(u_tap + 1);
-    }
-  }
-
-  auto load_tiles = [&](int k0, f32x4 (&ra)[A_PER], f32x4 (&rb)[B_PER]) {
-    if (UT) {
-      // address selects only (out-of-image / out-of-matrix slots read g_zero4): no
-      // branch splits the loader and no instruction touches the loaded registers
-      // before the chunk that consumes them
-      const int ci = u_ci + u_kq4;
-      const bool wrap = ci >= a.Cin;
-      const int tap = u_tap + (wrap ? 1 : 0);
-      const long off = (wrap ? u_toff1 : u_toff0) + (wrap ? ci - a.Cin : ci);
-#pragma unroll
-      for (int i = 0; i < A_PER; ++i) {
-        const bool ok = (u_mask[i] >> tap) & 1u;
-        ra[i] = ld4(ok ? a.in + u_aoff[i] + off : g_zero4);
-      }
-      if (BNB) {
-        const long offy = (wrap ? u_ytoff1 : u_ytoff0) + (wrap ? ci - a.Cin : ci);
-        const bool kin_a = k0 + u_kq4 < a.K;
-        u_okbits = 0;
-#pragma unroll
-        for (int i = 0; i < A_PER; ++i) {
-          const bool ok = kin_a && ((u_mask[i] >> tap) & 1u);
-          ry[BNB ? i : 0] = ld4(ok ? a.bnb.y + u_yoff[BNB ? i : 0] + offy : g_zero4);
-          u_okbits |= (ok ? 1u : 0u) << i;
-        }
-        seg_bnbwd_coef(a.bnb, kin_a ? (wrap ? ci - a.Cin : ci) : 0, cf);
-      }
-      const bool kin = k0 + u_kq4 < a.K;
-#pragma unroll
-      for (int i = 0; i < B_PER; ++i) rb[i] = ld4(u_bok[i] && kin ? a.wk + u_boff[i] + k0 : g_zero4);
-      u_ci += BK;
-      if (u_ci >= a.Cin) {
-        u_ci -= a.Cin;
-        ++u_tap;
-        u_toff0 = u_toff1;
-        u_toff1 = tap_off(u_tap + 1);
-        if (BNB) {
-          u_ytoff0 = u_ytoff1;
-          u_ytoff1 = tap_off_y(u_tap + 1);
-        }
-      }
-      return;
-    }
-#pragma unroll
-    for (int i = 0; i < A_PER; ++i) {
-      f32x4 v = {0.f, 0.f, 0.f, 0.f};
-      if (a_ok[i] && a_k[i] < a.K) {
-        if (KS == 1) {
-          v = ld4(a.in + a_base[i] + a_k[i]);
-        } else {
-          const int hi = a_hi0[i] + a_ky[i], wi = a_wi0[i] + a_kx[i];
-          if ((unsigned)hi < (unsigned)a.H && (unsigned)wi < (unsigned)a.W)
-            v = ld4(a.in + (a_base[i] + (long)hi * a.W + wi) * a.ldin + a_ci[i]);
-        }
-      }
-      ra[i] = v;
-      // advance this slot to the next chunk
-      a_k[i] += BK;
-      if (KS != 1) {
-        int ci = a_ci[i] + BK;
-        while (ci >= a.Cin) {
-          ci -= a.Cin;
-          if (++a_kx[i] == KS) { a_kx[i] = 0; ++a_ky[i]; }
-        }
-        a_ci[i] = ci;
-      }
-    }
-#pragma unroll
-    for (int i = 0; i < B_PER; ++i) {
-      const int idx = tid + i * NT;
-      const int row = idx / KQ, kq = idx % KQ;
-      const int co = n0 + row, k = k0 + kq * 4;
-      f32x4 v = {0.f, 0.f, 0.f, 0.f};
-      if (idx < B_VEC && co < a.Cout && k < a.K) v = ld4(a.wk + (long)co * a.ldk + k);
-      rb[i] = v;
-    }
-  };
-  auto st_op = [](lds_t* p, f32x4 v) {
-    if constexpr (BF) *reinterpret_cast<bf16x4*>(p) = __builtin_convertvector(v, bf16x4);
-    else *reinterpret_cast<f32x4*>(p) = v;
-  };
-  auto store_tiles = [&](int buf, const f32x4 (&ra)[A_PER], const f32x4 (&rb)[B_PER]) {
-#pragma unroll
-    for (int i = 0; i < A_PER; ++i) {
-      const int idx = tid + i * NT;
-      if (A_VEC % NT == 0 || idx < A_VEC) {
-        f32x4 v = ra[i];
-        if (BNB) {
-          const f32x4 t = seg_bnbwd4(v, ry[BNB ? i : 0], cf[0], cf[1], cf[2], cf[3], cf[4], cf[5], a.bnb.act);
-          v = ((u_okbits >> i) & 1u) ? t : f32x4{0.f, 0.f, 0.f, 0.f};
-        }
-        st_op(&As[buf][(idx / KQ) * LDSR + (idx % KQ) * 4], v);
-      }
-    }
-#pragma unroll
-    for (int i = 0; i < B_PER; ++i) {
-      const int idx = tid + i * NT;
-      if (B_VEC % NT == 0 || idx < B_VEC) st_op(&Bs[buf][(idx / KQ) * LDSR + (idx % KQ) * 4], rb[i]);
-    }
-  };
-
-  f32x16 acc[MI][NI];
-#pragma unroll
-  for (int mi = 0; mi < MI; ++mi)
-#pragma unroll
-    for (int ni = 0; ni < NI; ++ni)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[mi][ni][r] = 0.f;
-
-  const int nk = (min(a.K - kbeg, a.kchunk) + BK - 1) / BK;
-  const int lrow = lane & 31, lk = (lane >> 5) * 4;
-  auto compute = [&](int cur) {
-    if constexpr (BF) {
-      const int lk8 = (lane >> 5) * 8;
-#pragma unroll
-      for (int ks = 0; ks < BK / 16; ++ks) {
-        bf16x8 af[MI], bfr[NI];
-#pragma unroll
-        for (int mi = 0; mi < MI; ++mi)
-          af[mi] = *reinterpret_cast<const bf16x8*>(&As[cur][(wm0 + mi * 32 + lrow) * LDSR + ks * 16 + lk8]);
-#pragma unroll
-        for (int ni = 0; ni < NI; ++ni)
-          bfr[ni] = *reinterpret_cast<const bf16x8*>(&Bs[cur][(wn0 + ni * 32 + lrow) * LDSR + ks * 16 + lk8]);
-#pragma unroll
-        for (int mi = 0; mi < MI; ++mi)
-#pragma unroll
-          for (int ni = 0; ni < NI; ++ni)
-            acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[mi], bfr[ni], acc[mi][ni], 0, 0, 0);
-      }
-      return;
-    }
-#pragma unroll
-    for (int ks = 0; ks < BK / 8; ++ks) {
-      f32x4 af[MI], bf[NI];
-#pragma unroll
-      for (int mi = 0; mi < MI; ++mi)
-        af[mi] = *reinterpret_cast<const f32x4*>(&As[cur][(wm0 + mi * 32 + lrow) * LDSR + ks * 8 + lk]);
-#pragma unroll
-      for (int ni = 0; ni < NI; ++ni)
-        bf[ni] = *reinterpret_cast<const f32x4*>(&Bs[cur][(wn0 + ni * 32 + lrow) * LDSR + ks * 8 + lk]);
-#pragma unroll
-      for (int kk = 0; kk < 4; ++kk)
-#pragma unroll
-        for (int mi = 0; mi < MI; ++mi)
-#pragma unroll
-          for (int ni = 0; ni < NI; ++ni)
-            acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[mi][kk], bf[ni][kk], acc[mi][ni], 0, 0, 0);
-    }
-  };
-
-#if SEG_IGEMM_STAGES == 1
-  // one LDS stage: regs -> LDS, barrier, prefetch the next chunk, compute, barrier
-  f32x4 ra[A_PER], rb[B_PER];
-  load_tiles(kbeg, ra, rb);
-  for (int kt = 0; kt < nk; ++kt) {
-    store_tiles(0, ra, rb);
-    __syncthreads();
-    if (kt + 1 < nk) load_tiles(kbeg + (kt + 1) * BK, ra, rb);
-    compute(0);
-    __syncthreads();
-  }
-#elif SEG_IGEMM_DEPTH == 1
-  f32x4 ra[A_PER], rb[B_PER];
-  load_tiles(kbeg, ra, rb);
-  store_tiles(0, ra, rb);
-  __syncthreads();
-  for (int kt = 0; kt < nk; ++kt) {
-    const int cur = kt & 1;
-    if (kt + 1 < nk) load_tiles(kbeg + (kt + 1) * BK, ra, rb);
-    compute(cur);
-    if (kt + 1 < nk) store_tiles(cur ^ 1, ra, rb);
-    __syncthreads();
-  }
-#else
-  // Two register sets: the global loads of chunk kt+2 are issued before chunk kt's
-  // MFMAs and written to LDS only after chunk kt+1's, so each load has two compute
-  // phases (~2 x 2048 MFMA cycles at 64x64 per wave) to land -- one phase is shorter
-  // than the HBM latency under load, which left one-block-per-CU grids stalled.
-  f32x4 ra0[A_PER], rb0[B_PER], ra1[A_PER], rb1[B_PER];
-  load_tiles(kbeg, ra0, rb0);
-  store_tiles(0, ra0, rb0);
-  if (nk > 1) load_tiles(kbeg + BK, ra1, rb1);
-  __syncthreads();
-  for (int kt = 0; kt < nk; kt += 2) {
-    // LDS stage 0 holds chunk kt; set 1 holds chunk kt+1 (in flight)
-    if (kt + 2 < nk) load_tiles(kbeg + (kt + 2) * BK, ra0, rb0);
-    compute(0);
-    if (kt + 1 < nk) store_tiles(1, ra1, rb1);
-    __syncthreads();
-    if (kt + 1 >= nk) break;
-    // LDS stage 1 holds chunk kt+1; set 0 holds chunk kt+2
-    if (kt + 3 < nk) load_tiles(kbeg + (kt + 3) * BK, ra1, rb1);
-    compute(1);
-    if (kt + 2 < nk) store_tiles(0, ra0, rb0);
-    __syncthreads();
-  }
-#endif
-
-  // Epilogue: C layout of 32x32 f32 MFMA: col = lane&31, row = (r&3) + 8(r>>2) + 4(lane>>5).
-  if (a.part) {  // split-K: raw partial sums; seg_igemm_splitk_reduce applies the epilogue
-    float* P = a.part + (long)blockIdx.y * a.M * a.Cout;
-#pragma unroll
-    for (int ni = 0; ni < NI; ++ni) {
-      const int col = n0 + wn0 + ni * 32 + lrow;
-      if (col >= a.Cout) continue;
-#pragma unroll
-      for (int mi = 0; mi < MI; ++mi)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int row = m0 + wm0 + mi * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-          if (row < a.M) P[(long)row * a.Cout + col] = acc[mi][ni][r];
-        }
-    }
-    return;
-  }
-  float bcol[NI];
-#pragma unroll
-  for (int ni = 0; ni < NI; ++ni) {
-    const int col = n0 + wn0 + ni * 32 + lrow;
-    bcol[ni] = (a.bias && col < a.Cout) ? a.bias[col] : 0.f;
-#pragma unroll
-    for (int mi = 0; mi < MI; ++mi)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[mi][ni][r] += bcol[ni];
-  }
-  if (a.stat) {
-    // BatchNorm batch statistics of this BM-row tile, per output channel: the tile
-    // sum and the sum of squared deviations from the TILE mean (two passes over the
-    // accumulators, so no E[y^2]-E[y]^2 cancellation); merged over tiles with
-    // Chan's formula in fp64 by seg_bn_stats_tiles.  LDS of the K loop is reused.
-    constexpr int WR = BM / WM;
-    float* red = reinterpret_cast<float*>(&As[0][0]);  // [WR][BN]
-    float* tmean = red + WR * BN;      // [BN]
-    const int nrows = min(BM, a.M - m0);
-    const int wr = wave / WAVES_N;
-#pragma unroll
-    for (int pass = 0; pass < 2; ++pass) {
-#pragma unroll
-      for (int ni = 0; ni < NI; ++ni) {
-        const int cl = wn0 + ni * 32 + lrow;
-        const float mu = pass ? tmean[cl] : 0.f;
-        float s = 0.f;
-#pragma unroll
-        for (int mi = 0; mi < MI; ++mi)
-#pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            const int row = m0 + wm0 + mi * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-            const float d = acc[mi][ni][r] - mu;
-            s += row < a.M ? (pass ? d * d : d) : 0.f;
-          }
-        s += __shfl_xor(s, 32, 64);
-        if (lane < 32) red[wr * BN + cl] = s;
-      }
-      __syncthreads();
-      if (tid < BN) {
-        float t = 0.f;
-#pragma unroll
-        for (int j = 0; j < WR; ++j) t += red[j * BN + tid];
-        const int col = n0 + tid;
-        if (pass == 0) tmean[tid] = t / (float)nrows;
-        if (col < a.Cout) a.stat[((long)tm * 2 + pass) * a.Cout + col] = t;
-      }
-      __syncthreads();
-    }
-  }
-#pragma unroll
-  for (int ni = 0; ni < NI; ++ni) {
-    const int col = n0 + wn0 + ni * 32 + lrow;
-    if (col >= a.Cout) continue;
-#pragma unroll
-    for (int mi = 0; mi < MI; ++mi) {
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int row = m0 + wm0 + mi * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-        if (row < a.M) {
-          float v = acc[mi][ni][r];
-          if (a.add) v += a.add[(long)row * a.ldadd + col];
-          if (a.act) v = seg_act(v, a.act);
-          a.out[(long)row * a.ldout + col] = v;
-        }
-      }
-    }
-  }
-}
-
-template <int BM, int BN, int WM, int WN, int BK, bool BF>
-int launch_igemm_bk(const IgemmArgs& a, int ks, hipStream_t s) {
-  const int grid = seg_cdiv(a.M, BM) * seg_cdiv(a.Cout, BN);
-  const int splits = seg_cdiv(a.K, a.kchunk);
-  const bool ut = SEG_IGEMM_UT && (SEG_IGEMM_UT2 ? a.Cin >= BK : a.Cin % BK == 0);
-  constexpr int NT = 64 * (BM / WM) * (BN / WN);
-#define SEG_IG(KS, U) hipLaunchKernelGGL((igemm_conv_kernel<BM, BN, WM, WN, KS, BK, U, false, BF>), dim3(grid, splits), dim3(NT), 0, s, a)
-#define SEG_IGB(KS) hipLaunchKernelGGL((igemm_conv_kernel<BM, BN, WM, WN, KS, BK, true, true, BF>), dim3(grid, splits), dim3(NT), 0, s, a)
-  if (a.bnb.y) {
-    if (!ut) return (int)hipErrorInvalidValue;
-    if (ks == 1) SEG_IGB(1); else SEG_IGB(3);
-    SEG_RET_LAST();
-  }
-  if (ks == 1) {
-    if (ut) SEG_IG(1, true); else SEG_IG(1, false);
-  } else {
-    if (ut) SEG_IG(3, true); else SEG_IG(3, false);
-  }
-#undef SEG_IG
-#undef SEG_IGB
-  SEG_RET_LAST();
-}
-
-// K chunk depth: SEG_IGEMM_BK (32) unless K is short and not a multiple of it
-// (the stem's K = 36, 1x1 convs with Cin 16/24/144...), where padding K up to a
-// 32 multiple would waste MFMA work: then 16.
-inline int igemm_bk(int K) { return (SEG_IGEMM_BK != 16 && (K <= 64 || (K % SEG_IGEMM_BK != 0 && K < 512))) ? 16 : SEG_IGEMM_BK; }
-
-// split-K: `splits` K ranges of whole BK chunks (a.part set by the caller when splits > 1)
-template <int BM, int BN, int WM, int WN, bool BF = false>
-int launch_igemm(IgemmArgs a, int ks, int splits, hipStream_t s) {
-  const int bk = igemm_bk(a.K);
-  const int nk = seg_cdiv(a.K, bk);
-  a.kchunk = seg_cdiv(nk, splits) * bk;
-  if (bk == 16) return launch_igemm_bk<BM, BN, WM, WN, 16, BF>(a, ks, s);
-  return launch_igemm_bk<BM, BN, WM, WN, SEG_IGEMM_BK, BF>(a, ks, s);
-}
-
-struct TileCfg {
-  int bm, bn, wm, wn;
-  float eff;  // relative per-CU MFMA efficiency of the wave tile (LDS reads per MFMA)
-};
-// Relative efficiencies measured on MI355X (tools/tilesweep.py over the
-// MobileNetV2UNet launch shapes); 64x64 wave tiles need 1 operand read per MFMA,
-// 32x96 1.33, 32x32 2.
-constexpr TileCfg kTiles[] = {
-    {128, 128, 64, 64, 1.00f}, {64, 128, 32, 64, 0.95f}, {128, 64, 64, 32, 0.95f}, {64, 64, 32, 32, 0.85f},
-    {128, 96, 32, 96, 0.97f},  {128, 160, 32, 160, 0.95f}, {256, 32, 64, 32, 0.90f}, {128, 32, 32, 32, 0.92f},
-    // 8-wave (512-thread) blocks: two waves per SIMD at one block per CU
-    {128, 128, 64, 32, 0.0f}, {128, 128, 32, 64, 0.0f}, {256, 128, 64, 64, 0.0f}, {128, 256, 64, 64, 0.0f},
-    {128, 64, 32, 32, 0.0f}, {256, 64, 64, 32, 0.0f}, {64, 128, 32, 32, 0.0f},
-};
-
-constexpr int kTileBM[] = {128, 64, 128, 64, 128, 128, 256, 128, 128, 128, 256, 128, 128, 256, 64};
-
-int g_force_tile = -1;  // tuning hook (seg_igemm_force_tile); -1 = cost model
-
-int pick_tile(long M, int N) {
-  if (g_force_tile >= 0) return g_force_tile;
-  int best = 0;
-  double best_score = -1.0;
-  for (int i = 0; i < (int)(sizeof(kTiles) / sizeof(kTiles[0])); ++i) {
-    const TileCfg& t = kTiles[i];
-    const long bm_tiles = (M + t.bm - 1) / t.bm, bn_tiles = (N + t.bn - 1) / t.bn;
-    const long blocks = bm_tiles * bn_tiles;
-    const double util = (double)M * N / ((double)bm_tiles * t.bm * bn_tiles * t.bn);
-    const double fill = std::min(1.0, (double)blocks / 512.0);  // >= 2 blocks per CU to hide latency
-    const double score = util * t.eff * fill;
-    if (score > best_score + 1e-9) {
-      best_score = score;
-      best = i;
-    }
-  }
-  return best;
-}
-
-
-
-// Split-K factor for an M x Cout x K conv GEMM: > 1 only when the output tiles
-// alone cannot fill the chip (small images / batch 1 inference), keeping >= 4 K
-// chunks per split.
-int igemm_splits(long M, int Cout, int K) {
-  const int t = pick_tile(M, Cout);
-  const long blocks = ((M + kTiles[t].bm - 1) / kTiles[t].bm) * ((Cout + kTiles[t].bn - 1) / kTiles[t].bn);
-  const int nk = seg_cdiv(K, igemm_bk(K));
-  if (blocks >= 256 || nk < 8) return 1;
-  int s = (int)std::min<long>(seg_cdiv(512, blocks), nk / 4);
-  s = std::min(s, 64);
-  if (s < 2) return 1;
-  return seg_cdiv(nk, seg_cdiv(nk, s));  // no empty split
-}
-
-// out = act(sum_z part[z] + bias + add): the split-K epilogue (fixed z order: deterministic).
-__global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restrict__ part, int splits, long M, int Cout,
-                                                            const float* __restrict__ bias,
-                                                            const float* __restrict__ add, long ldadd,
-                                                            float* __restrict__ out, long ldout, int act) {
-  const long total = M * Cout;
-  for (long i = blockIdx.x * 256L + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
-    const long row = i / Cout;
-    const int col = (int)(i - row * Cout);
-    float v = 0.f;
-    for (int z = 0; z < splits; ++z) v += part[z * total + i];
-    if (bias) v += bias[col];
-    if (add) v += add[row * ldadd + col];
-    if (act) v = seg_act(v, act);
-    out[row * ldout + col] = v;
-  }
-}
-
-template <bool BF>
-int conv_igemm_impl(const float* in, long ldin, int N, int H, int W, int Cin, const float* wk, int ldk,
-                    const float* bias, float* out, long ldout, int Ho, int Wo, int Cout, int ks, int stride, int pad,
-                    const float* add, long ldadd, float* stat, int act, float* work, int splits, hipStream_t stream) {
-  if ((Cin & 3) || (ldin & 3) || (ldk & 3) || (ks != 1 && ks != 3)) return (int)hipErrorInvalidValue;
-  if (ks == 1 && (stride != 1 || pad != 0 || Ho != H || Wo != W)) return (int)hipErrorInvalidValue;
-  if (act < SEG_ACT_NONE || act > SEG_ACT_RELU6 || (act && stat)) return (int)hipErrorInvalidValue;
-  if (splits < 1 || (splits > 1 && (!work || stat))) return (int)hipErrorInvalidValue;
-  IgemmArgs a;
-  a.in = in; a.ldin = ldin; a.wk = wk; a.ldk = ldk; a.bias = bias;
-  a.add = add; a.ldadd = ldadd; a.out = out; a.ldout = ldout; a.stat = stat;
-  a.N = N; a.H = H; a.W = W; a.Cin = Cin; a.Ho = Ho; a.Wo = Wo; a.Cout = Cout;
-  a.stride = stride; a.pad = pad; a.K = ks * ks * Cin; a.M = N * Ho * Wo; a.act = act;
-  a.part = splits > 1 ? work : nullptr;
-  a.bnb = SegBnBwd{};
-  if (a.M == 0 || Cout == 0) return 0;
-  int rc;
-  switch (pick_tile(a.M, Cout)) {
-    case 0: rc = launch_igemm<128, 128, 64, 64, BF>(a, ks, splits, stream); break;
-    case 1: rc = launch_igemm<64, 128, 32, 64, BF>(a, ks, splits, stream); break;
-    case 2: rc = launch_igemm<128, 64, 64, 32, BF>(a, ks, splits, stream); break;
-    case 3: rc = launch_igemm<64, 64, 32, 32, BF>(a, ks, splits, stream); break;
-    case 4: rc = launch_igemm<128, 96, 32, 96, BF>(a, ks, splits, stream); break;
-    case 5: rc = launch_igemm<128, 160, 32, 160, BF>(a, ks, splits, stream); break;
-    case 6: rc = launch_igemm<256, 32, 64, 32, BF>(a, ks, splits, stream); break;
-    case 7: rc = launch_igemm<128, 32, 32, 32, BF>(a, ks, splits, stream); break;
-    case 8: rc = launch_igemm<128, 128, 64, 32, BF>(a, ks, splits, stream); break;
-    case 9: rc = launch_igemm<128, 128, 32, 64, BF>(a, ks, splits, stream); break;
-    case 10: rc = launch_igemm<256, 128, 64, 64, BF>(a, ks, splits, stream); break;
-    case 11: rc = launch_igemm<128, 256, 64, 64, BF>(a, ks, splits, stream); break;
-    case 12: rc = launch_igemm<128, 64, 32, 32, BF>(a, ks, splits, stream); break;
-    case 13: rc = launch_igemm<256, 64, 64, 32, BF>(a, ks, splits, stream); break;
-    default: rc = launch_igemm<64, 128, 32, 32, BF>(a, ks, splits, stream); break;
-  }
-  if (rc || splits == 1) return rc;
-  const long total = (long)a.M * Cout;
-  hipLaunchKernelGGL(splitk_reduce_kernel, dim3((int)std::min<long>(seg_cdiv(total, 256), 4096)), dim3(256), 0,
-                     stream, work, splits, (long)a.M, Cout, bias, add, ldadd, out, ldout, act);
-  SEG_RET_LAST();
-}
-
-}  // namespace
+int seg_igemm_forced_tile = -1;
 
 // out = act(conv(in, W) + bias + add).  `wk` is the packed weight of seg_pack_conv_weight
 // ([Cout][ldk], k = tap*Cin + ci).  ks in {1,3}; ks == 1 requires stride 1, pad 0.
@@ -647,20 +32,8 @@ SEG_API int seg_conv_igemm_act(const float* in, long ldin, int N, int H, int W, 
                                int ks, int stride, int pad,
                                const float* add, long ldadd, float* stat, int act, float* work, int splits,
                                hipStream_t stream) {
-  return conv_igemm_impl<false>(in, ldin, N, H, W, Cin, wk, ldk, bias, out, ldout, Ho, Wo, Cout, ks, stride, pad,
+  return conv_igemm_impl<float>(in, ldin, N, H, W, Cin, wk, ldk, bias, out, ldout, Ho, Wo, Cout, ks, stride, pad,
                                 add, ldadd, stat, act, work, splits, stream);
-}
-
-// seg_conv_igemm_act with bf16 math (the bf16 configurations): the same fp32 tensors,
-// operands rounded to bf16 (RNE) in the LDS staging, fp32 accumulation and epilogue.
-SEG_API int seg_conv_igemm_bf16(const float* in, long ldin, int N, int H, int W, int Cin,
-                                const float* wk, int ldk, const float* bias,
-                                float* out, long ldout, int Ho, int Wo, int Cout,
-                                int ks, int stride, int pad,
-                                const float* add, long ldadd, float* stat, int act, float* work, int splits,
-                                hipStream_t stream) {
-  return conv_igemm_impl<true>(in, ldin, N, H, W, Cin, wk, ldk, bias, out, ldout, Ho, Wo, Cout, ks, stride, pad,
-                               add, ldadd, stat, act, work, splits, stream);
 }
 
 SEG_API int seg_conv_igemm(const float* in, long ldin, int N, int H, int W, int Cin,
@@ -724,7 +97,7 @@ SEG_API int seg_conv_igemm_splits(long M, int Cout, int Cin, int ks) {
 // k-ordered fmaf chain) except the BN-statistics tile partition.
 SEG_API int seg_igemm_force_tile(int t) {
   if (t < -1 || t >= (int)(sizeof(kTiles) / sizeof(kTiles[0]))) return (int)hipErrorInvalidValue;
-  g_force_tile = t;
+  seg_igemm_forced_tile = t;
   return 0;
 }
 

@@ -24,6 +24,8 @@ PROTOTYPES = {
                                 _V, _I, _V]),
     "seg_conv_igemm_bf16": (_I, [_V, _L, _I, _I, _I, _I, _V, _I, _V, _V, _L, _I, _I, _I, _I, _I, _I, _V, _L, _V, _I,
                                  _V, _I, _V]),
+    "seg_conv_igemm_f16": (_I, [_V, _L, _I, _I, _I, _I, _V, _I, _V, _V, _L, _I, _I, _I, _I, _I, _I, _V, _L, _V, _I,
+                                _V, _I, _V]),
     "seg_conv_igemm_splits": (_I, [_L, _I, _I, _I]),
     "seg_conv_igemm_bnb": (_I, [_V, _L, _I, _I, _I, _I, _V, _I, _V, _L, _I, _I, _I, _V, _L, _V, _L, _V, _V, _V, _V, _I,
                                 _V]),

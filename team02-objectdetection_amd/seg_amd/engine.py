@@ -242,7 +242,7 @@ class ConvOp:
         M = o.N * o.H * o.W
         splits = query("seg_conv_igemm_splits", M, self.cout, self.cin_pad, self.ks)
         work = rt.tmp(splits * M * self.cout) if splits > 1 else None
-        call("seg_conv_igemm_act", rt.ptr(i), i.ld, i.N, i.H, i.W, self.cin_pad, wk, ldk, bias, rt.ptr(o), o.ld,
+        call(_FOLDED_CONV[rt.prog.math], rt.ptr(i), i.ld, i.N, i.H, i.W, self.cin_pad, wk, ldk, bias, rt.ptr(o), o.ld,
              o.H, o.W, self.cout, self.ks, self.stride, self.pad, rt.ptr(r) if r is not None else None,
              r.ld if r is not None else 0, None, act, work.data_ptr() if work is not None else None, splits, s)
 
@@ -529,6 +529,9 @@ class Program:
 
     def _build_pack(self, convs, key):
         import numpy as np
+        if self.math == "f16":
+            raise NotImplementedError("f16 conv math is the inference configuration (Predictor(model, math='f16')); "
+                                      "train with 'f32' or 'bf16'")
         jt = np.dtype([("w", "<u8"), ("wk", "<u8"), ("cout", "<i4"), ("cin", "<i4"), ("ks", "<i4"),
                        ("ldk", "<i4"), ("mode", "<i4"), ("kin", "<i4")])
         assert jt.itemsize == 40
@@ -804,7 +807,10 @@ def build_program(model, N, H, W, math="f32") -> Program:
 # forward) -- every dense / pointwise conv, forward and both gradients, multiplies
 # bf16-rounded operands on the bf16 MFMA with fp32 accumulation; activations, BN,
 # depthwise convs, the loss and the optimizer stay fp32.
-MATHS = ("f32", "bf16")
+MATHS = ("f32", "bf16", "f16")
+# "f16" is the fp16 inference configuration (BASELINE configs[3]): the BN-folded eval
+# forward (Predictor) with fp16 conv operands; training programs refuse it.
+_FOLDED_CONV = {"f32": "seg_conv_igemm_act", "bf16": "seg_conv_igemm_bf16", "f16": "seg_conv_igemm_f16"}
 
 
 def set_conv_math(model, math: str):
@@ -997,7 +1003,7 @@ _SIDE = {}
 def _side_stream(device):
     st = _SIDE.get(device)
     if st is None:
-        st = _SIDE[device] = torch.cuda.Stream(device)
+        st = _SIDE[device] = torch.cuda.Stream(device, priority=0)
     return st
 
 
@@ -1008,9 +1014,9 @@ LAST_RUN = None
 _PROGRAM_CACHE_ATTR = "_segamd_programs"
 
 
-def get_program(model, N, H, W) -> Program:
+def get_program(model, N, H, W, math=None) -> Program:
     cache = model.__dict__.setdefault(_PROGRAM_CACHE_ATTR, {})
-    math = model.__dict__.get("_segamd_math", "f32")
+    math = math or model.__dict__.get("_segamd_math", "f32")
     key = (N, H, W, math)
     prog = cache.get(key)
     if prog is None:

@@ -60,11 +60,12 @@ class Predictor:
     mask = predictor(frame)          # uint8 [720, 1280] class ids on the GPU
     logits = predictor.logits()      # [1, C, 128, 256] of the last frame (tests)
 
+    math="f16" runs every folded conv on fp16 operands (BASELINE configs[3]).
     Weights are folded at construction; call `refresh()` after changing the
     model's parameters or running statistics (e.g. load_state_dict).
     """
 
-    def __init__(self, model, frame_hw=(720, 1280), target_size=(256, 128), graph: bool = True):
+    def __init__(self, model, frame_hw=(720, 1280), target_size=(256, 128), graph: bool = True, math: str = "f32"):
         p = next(model.parameters())
         if not p.is_cuda:
             raise RuntimeError("Predictor runs on the MI355X HIP path only; move the model to 'cuda' first")
@@ -72,7 +73,9 @@ class Predictor:
         self.device = p.device
         self.Hf, self.Wf = frame_hw
         self.W, self.H = target_size
-        self.prog = get_program(model, 1, self.H, self.W)
+        # math: conv arithmetic of the folded forward -- "f32" (the reference's), "f16"
+        # (BASELINE configs[3]: fp16 operands, fp32 accumulation) or "bf16"
+        self.prog = get_program(model, 1, self.H, self.W, math)
         self.frame = torch.zeros((self.Hf, self.Wf, 3), device=self.device, dtype=torch.uint8)
         self.mask = torch.empty((self.Hf, self.Wf), device=self.device, dtype=torch.uint8)
         self.run = Run(self.prog, self.frame, training=False)

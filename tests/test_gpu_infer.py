@@ -82,6 +82,36 @@ def test_predictor_matches_oracle(arch):
     np.testing.assert_array_equal(mask, cvresize.class_mask(pred.logits().cpu().numpy(), (fh, fw)))
 
 
+@pytest.mark.parametrize("math,dtype,agree", [("f16", torch.float16, 0.99), ("bf16", torch.bfloat16, 0.9)])
+def test_predictor_low_precision(math, dtype, agree):
+    """BASELINE configs[3] (fp16 inference) and the bf16 variant: the folded forward with
+    16-bit conv operands against the oracle's eval forward with the same operand rounding
+    (segref.bf16_convs(dtype), in fp64 -- the reference's autocast arithmetic).  The
+    folded weights round differently from conv-then-BN, so the bar is the distance of
+    the emulated reference itself from exact fp64 (x1.5, + 1e-3); the mask agrees with the
+    exact-fp64 oracle mask on >= 99 % (fp16) / 90 % (bf16: 8-bit mantissas, ~13 % logits
+    error for the emulated reference itself at this random-init model, measured)."""
+    size, (fh, fw) = (256, 128), (720, 1280)
+    cpu = MobileNetV2UNet(10)
+    deterministic_init(cpu, seed=11, random_running_stats=True)
+    model = MobileNetV2UNet(10).to(DEV)
+    model.load_state_dict(cpu.state_dict())
+    pred = Predictor(model, frame_hw=(fh, fw), target_size=size, graph=True, math=math)
+    f = frame(fh, fw, seed=3)
+    mask = pred(f).cpu().numpy()
+    got = pred.logits().double().cpu().numpy()
+    ref = _oracle_logits(cpu, f, size)
+    with segref.bf16_convs(dtype):
+        emu = _oracle_logits(cpu, f, size)
+    e_got = np.linalg.norm(got - ref) / np.linalg.norm(ref)
+    e_ref = np.linalg.norm(emu - ref) / np.linalg.norm(ref)
+    print(f"{math}: folded forward err {e_got:.3e}, emulated reference err {e_ref:.3e}")
+    assert e_got <= 1.5 * e_ref + 1e-3, (e_got, e_ref)
+    assert e_got > 1e-5  # the 16-bit kernels really ran
+    assert (mask == cvresize.class_mask(ref, (fh, fw))).mean() >= agree
+    np.testing.assert_array_equal(mask, cvresize.class_mask(pred.logits().cpu().numpy(), (fh, fw)))
+
+
 def test_graph_equals_eager_and_refresh():
     torch.manual_seed(0)
     model = deterministic_init(MobileNetV2UNet(10), seed=5, random_running_stats=True).to(DEV)

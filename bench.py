@@ -232,7 +232,8 @@ def main():
         wfl, wsec, wn = family({"wino3_fwd", "wino3_dgrad"})
         achieved = flops / secs / 1e12 if secs > 0 else 0.0
         traffic = None
-        prof = os.path.join(REPO, "profiles", "latest_roofline.json")
+        prof = os.path.join(REPO, "profiles", "latest_roofline.json" if args.math == "f32"
+                            else f"latest_roofline_{args.math}.json")
         if os.path.exists(prof):
             with open(prof) as fh:
                 fam = json.load(fh)["families"].get("conv3", {})
@@ -253,7 +254,7 @@ def main():
         roof = {"bound": "mfma", "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
                 "frac": round(achieved / peak, 4),
                 "traffic": round(traffic) if traffic else None,
-                "traffic_source": "profiles/latest_roofline.json: rocprofv3 PMC (2*FETCH_SIZE+WRITE_SIZE)*1KiB "
+                "traffic_source": f"{os.path.relpath(prof, REPO)}: rocprofv3 PMC (2*FETCH_SIZE+WRITE_SIZE)*1KiB "
                                   "of the conv3 family per step / 17 conv ops" if traffic else None,
                 "algorithmic_bytes_per_launch": round(alg_bytes),
                 "kernel": ("dense 3x3 conv fwd + dgrad on f32 MFMA: igemm_conv_kernel<*,*,*,*,3,*> (implicit GEMM) "

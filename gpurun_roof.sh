@@ -1,14 +1,14 @@
 #!/bin/bash
 # Kernel-trace/stats profile + FETCH_SIZE / WRITE_SIZE PMC passes of a short bench run,
 # then the roofline summary in gpurun_out/$1/$1.{md,json} (copy it into profiles/ afterwards).
-# usage: bash gpurun_roof.sh <name>
+# usage: bash gpurun_roof.sh <name> [extra bench.py args, e.g. --math bf16]
 set -o pipefail
 export TMPDIR=/tmp
-name=$1
+name=$1; shift
 d=gpurun_out/$name
 mkdir -p $d
-timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $d/prof -o run --output-format csv -- python bench.py --steps 7 --warmup 2 --no-cpu-baseline --no-timer > $d/prof.log 2>&1 || { echo "prof failed"; tail -5 $d/prof.log; exit 1; }
+timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $d/prof -o run --output-format csv -- python bench.py --steps 7 --warmup 2 --no-cpu-baseline --no-timer "$@" > $d/prof.log 2>&1 || { echo "prof failed"; tail -5 $d/prof.log; exit 1; }
 for c in FETCH_SIZE WRITE_SIZE; do
-  timeout -s KILL 300 rocprofv3 --pmc $c --kernel-trace -d $d/pmc/$c -o run --output-format csv -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-timer > $d/pmc_$c.log 2>&1 || { echo "pmc $c failed"; tail -5 $d/pmc_$c.log; exit 1; }
+  timeout -s KILL 300 rocprofv3 --pmc $c --kernel-trace -d $d/pmc/$c -o run --output-format csv -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-timer "$@" > $d/pmc_$c.log 2>&1 || { echo "pmc $c failed"; tail -5 $d/pmc_$c.log; exit 1; }
 done
 python tools/roofline_report.py $d/prof $d/pmc 9 $d/$name

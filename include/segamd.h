@@ -85,6 +85,19 @@ int seg_conv_igemm_f16(const float* in, long ldin, int N, int H, int W, int Cin,
                        int ks, int stride, int pad,
                        const float* add, long ldadd, float* stat, int act, float* work, int splits,
                        hipStream_t stream);
+/* Data gradient (stride 1) completing dA of a layer y -> train BatchNorm -> act, with
+ * that BN's backward reduction fused into the epilogue (replaces the reduction pass of
+ * native_batch_norm_backward): part[tile][2][Cout], tile = seg_conv_igemm_row_tiles(M,
+ * Cout) rows, gets sum(dz) and sum(dz*(y-mean)), dz = dA*act'(y*scale+shift).
+ * _bf16: the same with bf16 math. */
+int seg_conv_igemm_red(const float* in, long ldin, int N, int H, int W, int Cin, const float* wk, int ldk,
+                       float* out, long ldout, int Cout, int ks, int pad, const float* add, long ldadd,
+                       const float* y, long ldy, const float* scale, const float* shift, const float* mean,
+                       int bn_act, float* part, hipStream_t stream);
+int seg_conv_igemm_red_bf16(const float* in, long ldin, int N, int H, int W, int Cin, const float* wk, int ldk,
+                            float* out, long ldout, int Cout, int ks, int pad, const float* add, long ldadd,
+                            const float* y, long ldy, const float* scale, const float* shift, const float* mean,
+                            int bn_act, float* part, hipStream_t stream);
 /* Split-K factor for seg_conv_igemm_act (1 = none): > 1 only when the output tiles
  * cannot fill the 256 CUs (batch-1 inference). */
 int seg_conv_igemm_splits(long M, int Cout, int Cin, int ks);
@@ -199,6 +212,13 @@ int seg_dw_wgrad(const float* dy, long lddy, const float* x, long ldx, int N, in
  * K = 9 taps x 4 channels (the 4th weight channel packed as zero). */
 int seg_nchw_to_nhwc(const float* x, int N, int C, int H, int W, float* out, int ld, hipStream_t stream);
 
+/* seg_bn_backward whose reduction was fused into the producer of dA
+ * (seg_conv_igemm_red / _red_bf16): finalize from part[nparts][2][C] + apply.
+ * coef >= 3*C floats. */
+int seg_bn_backward_parts(const float* part, int nparts, const float* da, long ldda, const float* y, long ldy,
+                          long M, int C, const float* gamma, const float* mean, const float* invstd,
+                          const float* scale, const float* shift, int act, float* dgamma, float* dbeta,
+                          float* coef, float* dy, long lddy, hipStream_t stream);
 /* ---- BatchNorm2d + activation (aten native_batch_norm(+_backward), hardtanh,
  *      threshold; src/unet.py:59-63,114-115 and torchvision norms) ----------- */
 long seg_chan_workspace_floats(long M, int C);

@@ -392,6 +392,21 @@ SEG_API int seg_bn_backward(const float* da, long ldda, const float* y, long ldy
   SEG_RET_LAST();
 }
 
+// seg_bn_backward whose reduction was fused into the producer of dA
+// (seg_conv_igemm_red): part[nparts][2][C] per-tile sums; finalize + apply only.
+// `coef` >= 3*C floats of workspace.
+SEG_API int seg_bn_backward_parts(const float* part, int nparts, const float* da, long ldda, const float* y, long ldy,
+                                  long M, int C, const float* gamma, const float* mean, const float* invstd,
+                                  const float* scale, const float* shift, int act, float* dgamma, float* dbeta,
+                                  float* coef, float* dy, long lddy, hipStream_t stream) {
+  if ((C & 3) || (ldy & 3) || (ldda & 3) || (lddy & 3) || nparts < 1) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(C), dim3(256), 0, stream, part, nparts, M, C, gamma,
+                     invstd, dgamma, dbeta, coef);
+  hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(ew_grid(M * (C / 4))), dim3(256), 0, stream, da, ldda, y, ldy, M, C,
+                     scale, shift, mean, act, coef, dy, lddy);
+  SEG_RET_LAST();
+}
+
 // The reduction half of seg_bn_backward: dgamma/dbeta and coef[3][C] = (g*inv,
 // mean(dz), mean(dz*xhat)*inv) for a fused consumer (seg_pw_bwd_fused) that
 // applies dY = coef0 * (dz - coef1 - (y - mean) * coef2) on load.

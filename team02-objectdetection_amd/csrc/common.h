@@ -95,6 +95,18 @@ struct SegBnBwd {
   int C, act;
 };
 
+// BatchNorm-backward reduction fused into the kernel that completes dA (the gradient
+// of act(BN(y))): per output tile and channel, part[tile][0][c] = sum dz and
+// part[tile][1][c] = sum dz * (y - mean), dz = dA * act'(y * scale + shift)
+// (seg_bn_backward_parts finalizes them).  part == nullptr: off.
+struct SegBnRed {
+  const float* y;
+  long ldy;
+  const float *scale, *shift, *mean;
+  int act;
+  float* part;
+};
+
 // The 6 coefficient float4s of channel group c.
 __device__ __forceinline__ void seg_bnbwd_coef(const SegBnBwd& b, int c, f32x4 (&cf)[6]) {
   cf[0] = ld4(b.scale + c);

@@ -36,6 +36,21 @@ SEG_API int seg_conv_igemm_act(const float* in, long ldin, int N, int H, int W, 
                                 add, ldadd, stat, act, work, splits, stream);
 }
 
+// Data gradient (stride 1) whose output completes dA of a layer y -> train BN -> act,
+// with that BatchNorm's backward reduction fused into the epilogue: part[tile][2][Cout]
+// (tile = seg_conv_igemm_row_tiles(M, Cout) rows) receives sum(dz) and
+// sum(dz * (y - mean)) per channel; y/ldy, scale/shift/mean and bn_act are the BN
+// layer's (forward coefficients).  Finalize + apply: seg_bn_backward_parts.
+SEG_API int seg_conv_igemm_red(const float* in, long ldin, int N, int H, int W, int Cin, const float* wk, int ldk,
+                               float* out, long ldout, int Cout, int ks, int pad, const float* add, long ldadd,
+                               const float* y, long ldy, const float* scale, const float* shift, const float* mean,
+                               int bn_act, float* part, hipStream_t stream) {
+  if (!part) return (int)hipErrorInvalidValue;
+  const SegBnRed red{y, ldy, scale, shift, mean, bn_act, part};
+  return conv_igemm_impl<float>(in, ldin, N, H, W, Cin, wk, ldk, nullptr, out, ldout, H, W, Cout, ks, 1, pad, add,
+                                ldadd, nullptr, SEG_ACT_NONE, nullptr, 1, stream, &red);
+}
+
 SEG_API int seg_conv_igemm(const float* in, long ldin, int N, int H, int W, int Cin,
                            const float* wk, int ldk, const float* bias,
                            float* out, long ldout, int Ho, int Wo, int Cout,
@@ -63,6 +78,7 @@ SEG_API int seg_conv_igemm_bnb(const float* in, long ldin, int N, int H, int W, 
   a.N = N; a.H = H; a.W = W; a.Cin = Cin; a.Ho = H; a.Wo = W; a.Cout = Cout;
   a.stride = 1; a.pad = pad; a.K = ks * ks * Cin; a.M = N * H * W; a.act = 0; a.part = nullptr;
   a.bnb = SegBnBwd{y, ldy, scale, shift, mean, k, Cin, bn_act};
+  a.red = SegBnRed{};
   if (a.M == 0 || Cout == 0) return 0;
   if (Cin < igemm_bk(a.K)) return (int)hipErrorInvalidValue;
   switch (pick_tile(a.M, Cout)) {

@@ -34,6 +34,7 @@ struct IgemmArgs {
   float* part;                   // split-K: raw partial sums [gridDim.y][M][Cout] (no epilogue), else null
   int act;                       // epilogue activation of act(acc + bias + add) (SegAct); 0 in training
   SegBnBwd bnb;                  // BNB kernels: `in` is dA and the A operand is the BN backward dY
+  SegBnRed red;                  // optional: BN-backward reduction of the written gradient (red.part set)
 };
 
 #ifndef SEG_IGEMM_DEPTH
@@ -90,6 +91,7 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void igemm_conv_kernel(
   static_assert(NT % KQ == 0, "uniform kq per thread");
   static_assert(!LP || BK % 16 == 0, "16-bit MFMA steps are 16 deep");
   static_assert(sizeof(lds_t) * BM * LDSR >= 4 * (BM / WM + 1) * BN, "BN-statistics scratch fits in As");
+  static_assert(sizeof(lds_t) * BM * LDSR >= 4 * 2 * (BM / WM) * BN, "BN-backward reduction scratch fits in As");
 
   __shared__ __attribute__((aligned(16))) lds_t As[SEG_IGEMM_STAGES][BM * LDSR];
   __shared__ __attribute__((aligned(16))) lds_t Bs[SEG_IGEMM_STAGES][BN * LDSR];
@@ -463,10 +465,23 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void igemm_conv_kernel(
       __syncthreads();
     }
   }
+  // BN-backward reduction (a.red.part): this data gradient completes dA of a layer
+  // y -> BN -> act; per column, the tile's sum(dz) and sum(dz * (y - mean)) with
+  // dz = dA * act'(y * scale + shift) -- chan_partial_kernel<1>'s sums, from the values
+  // just written, so seg_bn_backward_parts never re-reads dA and y for its reduction.
+  const bool red = a.red.part != nullptr;
+  float rs0[NI], rs1[NI];
 #pragma unroll
   for (int ni = 0; ni < NI; ++ni) {
+    rs0[ni] = rs1[ni] = 0.f;
     const int col = n0 + wn0 + ni * 32 + lrow;
     if (col >= a.Cout) continue;
+    float rsc = 0.f, rsh = 0.f, rmu = 0.f;
+    if (red) {
+      rsc = a.red.scale[col];
+      rsh = a.red.shift[col];
+      rmu = a.red.mean[col];
+    }
 #pragma unroll
     for (int mi = 0; mi < MI; ++mi) {
 #pragma unroll
@@ -477,8 +492,41 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void igemm_conv_kernel(
           if (a.add) v += a.add[(long)row * a.ldadd + col];
           if (a.act) v = seg_act(v, a.act);
           a.out[(long)row * a.ldout + col] = v;
+          if (red) {
+            const float yv = a.red.y[(long)row * a.red.ldy + col];
+            const float dz = v * seg_act_mask(yv * rsc + rsh, a.red.act);
+            rs0[ni] += dz;
+            rs1[ni] += dz * (yv - rmu);
+          }
         }
       }
+    }
+  }
+  if (red) {
+    constexpr int WR = BM / WM;
+    float* scr = reinterpret_cast<float*>(&As[0][0]);  // [2][WR][BN]
+    const int wr = wave / WAVES_N;
+    __syncthreads();
+#pragma unroll
+    for (int ni = 0; ni < NI; ++ni) {
+      const int cl = wn0 + ni * 32 + lrow;
+      const float s0 = rs0[ni] + __shfl_xor(rs0[ni], 32, 64);
+      const float s1 = rs1[ni] + __shfl_xor(rs1[ni], 32, 64);
+      if (lane < 32) {
+        scr[wr * BN + cl] = s0;
+        scr[(WR + wr) * BN + cl] = s1;
+      }
+    }
+    __syncthreads();
+    if (tid < BN && n0 + tid < a.Cout) {
+      float t0 = 0.f, t1 = 0.f;
+#pragma unroll
+      for (int j = 0; j < WR; ++j) {
+        t0 += scr[j * BN + tid];
+        t1 += scr[(WR + j) * BN + tid];
+      }
+      a.red.part[((long)tm * 2) * a.Cout + n0 + tid] = t0;
+      a.red.part[((long)tm * 2 + 1) * a.Cout + n0 + tid] = t1;
     }
   }
 }
@@ -594,7 +642,10 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restr
 template <typename OT>
 int conv_igemm_impl(const float* in, long ldin, int N, int H, int W, int Cin, const float* wk, int ldk,
                     const float* bias, float* out, long ldout, int Ho, int Wo, int Cout, int ks, int stride, int pad,
-                    const float* add, long ldadd, float* stat, int act, float* work, int splits, hipStream_t stream) {
+                    const float* add, long ldadd, float* stat, int act, float* work, int splits, hipStream_t stream,
+                    const SegBnRed* red = nullptr) {
+  if (red && (splits != 1 || stat || act || !red->y || !red->scale || !red->shift || !red->mean))
+    return (int)hipErrorInvalidValue;
   if ((Cin & 3) || (ldin & 3) || (ldk & 3) || (ks != 1 && ks != 3)) return (int)hipErrorInvalidValue;
   if (ks == 1 && (stride != 1 || pad != 0 || Ho != H || Wo != W)) return (int)hipErrorInvalidValue;
   if (act < SEG_ACT_NONE || act > SEG_ACT_RELU6 || (act && stat)) return (int)hipErrorInvalidValue;
@@ -606,6 +657,7 @@ int conv_igemm_impl(const float* in, long ldin, int N, int H, int W, int Cin, co
   a.stride = stride; a.pad = pad; a.K = ks * ks * Cin; a.M = N * Ho * Wo; a.act = act;
   a.part = splits > 1 ? work : nullptr;
   a.bnb = SegBnBwd{};
+  a.red = red ? *red : SegBnRed{};
   if (a.M == 0 || Cout == 0) return 0;
   int rc;
   switch (pick_tile(a.M, Cout)) {

@@ -26,6 +26,10 @@ PROTOTYPES = {
                                  _V, _I, _V]),
     "seg_conv_igemm_f16": (_I, [_V, _L, _I, _I, _I, _I, _V, _I, _V, _V, _L, _I, _I, _I, _I, _I, _I, _V, _L, _V, _I,
                                 _V, _I, _V]),
+    "seg_conv_igemm_red": (_I, [_V, _L, _I, _I, _I, _I, _V, _I, _V, _L, _I, _I, _I, _V, _L, _V, _L, _V, _V, _V, _I,
+                                _V, _V]),
+    "seg_conv_igemm_red_bf16": (_I, [_V, _L, _I, _I, _I, _I, _V, _I, _V, _L, _I, _I, _I, _V, _L, _V, _L, _V, _V, _V,
+                                     _I, _V, _V]),
     "seg_conv_igemm_splits": (_I, [_L, _I, _I, _I]),
     "seg_conv_igemm_bnb": (_I, [_V, _L, _I, _I, _I, _I, _V, _I, _V, _L, _I, _I, _I, _V, _L, _V, _L, _V, _V, _V, _V, _I,
                                 _V]),
@@ -64,6 +68,7 @@ PROTOTYPES = {
     "seg_bn_eval_coef": (_I, [_V, _V, _V, _V, _F, _I, _V, _V, _V]),
     "seg_bn_apply": (_I, [_V, _L, _L, _I, _V, _V, _I, _V, _L, _V, _L, _V]),
     "seg_bn_backward": (_I, [_V, _L, _V, _L, _L, _I, _V, _V, _V, _V, _V, _I, _V, _V, _V, _V, _L, _V]),
+    "seg_bn_backward_parts": (_I, [_V, _I, _V, _L, _V, _L, _L, _I, _V, _V, _V, _V, _V, _I, _V, _V, _V, _V, _L, _V]),
     "seg_bn_backward_coef": (_I, [_V, _L, _V, _L, _L, _I, _V, _V, _V, _V, _V, _I, _V, _V, _V, _V, _V]),
     "seg_pw_bwd_fused_ok": (_I, [_I, _I]),
     "seg_pw_bwd_blocks": (_I, [_L]),

@@ -130,6 +130,9 @@ class ConvOp:
         self.bnb = False
         # bf16 math (Program.math == "bf16"): seg_conv_igemm_bf16 / seg_conv_wgrad_bf16
         self.bf = False
+        # fused BN-backward reduction (Program._plan_bn_red): red_for = the BN op whose dA this
+        # op's data gradient completes (computes its sums in the epilogue); red_by = the reverse
+        self.red_for = self.red_by = None
         self.ks = conv.kernel_size[0]
         self.stride = conv.stride[0]
         self.pad = conv.padding[0]
@@ -341,11 +344,19 @@ class ConvOp:
             st = rt.saved[id(self)]
             mean, invstd, scale, shift = (st[k * C:(k + 1) * C] for k in range(4))
             dY = Act(rt.tmp_buf(M * r4(C)), 0, r4(C), C, y.N, y.H, y.W)
-            work = rt.tmp(query("seg_chan_workspace_floats", M, C) + 3 * C)
             g_w, g_b = rt.grad_param(self.bn.weight), rt.grad_param(self.bn.bias)
-            call("seg_bn_backward", rt.gptr(dA), dA.ld, rt.ptr(y), y.ld, M, C, self.bn.weight.data_ptr(),
-                 mean.data_ptr(), invstd.data_ptr(), scale.data_ptr(), shift.data_ptr(), self.act,
-                 g_w, g_b, work.data_ptr(), rt.ptr(dY), dY.ld, s)
+            parts = rt.bnred.pop(id(self), None)
+            if parts is not None:  # reduction already done by the data gradient that completed dA
+                part, nparts = parts
+                coef = rt.tmp(3 * C)
+                call("seg_bn_backward_parts", part.data_ptr(), nparts, rt.gptr(dA), dA.ld, rt.ptr(y), y.ld, M, C,
+                     self.bn.weight.data_ptr(), mean.data_ptr(), invstd.data_ptr(), scale.data_ptr(),
+                     shift.data_ptr(), self.act, g_w, g_b, coef.data_ptr(), rt.ptr(dY), dY.ld, s)
+            else:
+                work = rt.tmp(query("seg_chan_workspace_floats", M, C) + 3 * C)
+                call("seg_bn_backward", rt.gptr(dA), dA.ld, rt.ptr(y), y.ld, M, C, self.bn.weight.data_ptr(),
+                     mean.data_ptr(), invstd.data_ptr(), scale.data_ptr(), shift.data_ptr(), self.act,
+                     g_w, g_b, work.data_ptr(), rt.ptr(dY), dY.ld, s)
             if self.res is not None:
                 rt.add_pending(self.res, dA)
         else:
@@ -417,6 +428,17 @@ class ConvOp:
                 _timed_call("wino3_dgrad", self.flops(), "seg_conv_wino", dYp, dY.ld, y.N, y.H, y.W, kin,
                             self.wk_wd.data_ptr(), kin, None, rt.gptr(i), i.ld, self.cin, add_ptr, add_ld, None,
                             work.data_ptr(), s)
+            elif self.red_for is not None and rt.training:
+                b = self.red_for
+                st, C = rt.saved[id(b)], b.cout
+                ntiles, _ = rt.row_tiles(i.M, self.cin)
+                part = rt.tmp(ntiles * 2 * C)
+                _timed_call(f"igemm{self.ks}_dgrad", self.flops(),
+                            "seg_conv_igemm_red_bf16" if self.bf else "seg_conv_igemm_red", dYp, dY.ld, y.N, y.H,
+                            y.W, kin, self.wk_d.data_ptr(), self.ldk_d, rt.gptr(i), i.ld, self.cin, self.ks, self.pad,
+                            add_ptr, add_ld, rt.ptr(b.y), b.y.ld, st[2 * C:3 * C].data_ptr(),
+                            st[3 * C:4 * C].data_ptr(), st[:C].data_ptr(), b.act, part.data_ptr(), s)
+                rt.bnred[id(b)] = (part, ntiles)
             elif self.bf:
                 _timed_call(f"igemm{self.ks}_dgrad", self.flops(), "seg_conv_igemm_bf16", dYp, dY.ld, y.N, y.H, y.W,
                             kin, self.wk_d.data_ptr(), self.ldk_d, None, rt.gptr(i), i.ld, i.H, i.W, self.cin,
@@ -600,9 +622,48 @@ class Program:
                 op.wk_d = torch.empty(op.cin * op.ldk_d, device=dev, dtype=torch.float32)
                 jobs.append((w.data_ptr(), op.wk_d.data_ptr(), op.cout, op.cin, op.ks, op.ldk_d, 1, kin))
                 max_elems = max(max_elems, op.cin * op.ldk_d)
+        self._plan_bn_red()
         table = np.array(jobs, dtype=jt)
         self._jobs = torch.from_numpy(table.view(np.uint8).copy()).to(convs[0].conv.weight.device)
         self._njobs, self._max_elems, self._pack_key = len(jobs), max_elems, key
+
+    def _plan_bn_red(self):
+        """Fuse each train-mode BatchNorm's backward reduction into the data gradient that
+        completes its dA, where that is possible.  The gradient of a layer output is
+        written by its consumers in reverse forward order (first writer overwrites, later
+        ones add), so the EARLIEST consumer in forward order finishes it; when that consumer
+        is a stride-1 implicit-GEMM data gradient whose output is exactly the layer's
+        output region, its epilogue computes sum(dz), sum(dz*(y-mean)) per channel
+        (seg_conv_igemm_red) and the BN backward skips its own reduction pass."""
+        def reads(op):
+            if isinstance(op, ConvOp):
+                return [op.inp] + ([op.res] if op.res is not None else [])
+            if isinstance(op, UpsampleOp):
+                return [op.low]
+            if isinstance(op, PoolOp):
+                return [op.inp]
+            return []
+
+        def overlaps(a, b):
+            return a.buf == b.buf and a.off < b.off + b.C and b.off < a.off + a.C
+
+        for op in self.ops:
+            if isinstance(op, ConvOp):
+                op.red_for = op.red_by = None
+        if not BN_RED:
+            return
+        for k, b in enumerate(self.ops):
+            if not isinstance(b, ConvOp) or b.bn is None or b.bnb or b.pw_fused or b.cout % 4:
+                continue
+            for e in self.ops[k + 1:]:
+                hit = [a for a in reads(e) if overlaps(a, b.out)]
+                if not hit:
+                    continue
+                if (isinstance(e, ConvOp) and e.kind == "igemm" and not e.first and e.stride == 1
+                        and hit == [e.inp] and e.inp.key() == b.out.key() and not (e.wino_d or e.halo_d
+                                                                                    or e.pw_fused or e.bnb)):
+                    b.red_by, e.red_for = e, b
+                break
 
     def fold(self, stream):
         """Eval: fold every BatchNorm into its conv (one seg_bn_fold_batch launch) and
@@ -842,6 +903,7 @@ class Run:
         self.sync = None
         self._tmp_n = 0
         self.side = None      # side stream of the parameter gradients (backward only)
+        self.bnred = {}       # id(BN op) -> (tile partials, ntiles) from a fused data gradient
 
     # pointers
     def ptr(self, a: Act) -> int:
@@ -997,6 +1059,8 @@ class Run:
 # memory-bound BatchNorm / depthwise / 1x1 kernels of the main stream.  Results are the
 # same either way (the kernels and their reduction orders do not change).
 OVERLAP = os.environ.get("SEG_OVERLAP", "1") == "1"
+# Fused BatchNorm-backward reductions (Program._plan_bn_red); SEG_BN_RED=0 turns them off.
+BN_RED = os.environ.get("SEG_BN_RED", "1") == "1"
 _SIDE = {}
 
 

@@ -668,3 +668,54 @@ def test_conv_halo(N, Cin, Cout, H, W, mode):
         call("seg_conv_halo", nhwc(dy).data_ptr(), r4(Cin), N, H, W, kin, wkd.data_ptr(), ldk, None, dx.data_ptr(),
              dx.shape[1], Cout, addg.data_ptr(), addg.shape[1], None, s)
         assert rel(from_nhwc(dx, N, Cout, H, W), xr.grad + addend) < 1e-5
+
+
+@pytest.mark.parametrize("math", ["f32", "bf16"])
+@pytest.mark.parametrize("N,H,W,Cin,Cout,ks,act,addend", [(2, 9, 13, 96, 24, 1, 2, False), (1, 16, 24, 64, 152, 3, 1, True),
+                                                         (3, 7, 5, 32, 80, 3, 0, True), (2, 8, 8, 160, 960, 1, 2, True)])
+def test_dgrad_with_fused_bn_reduction(math, N, H, W, Cin, Cout, ks, act, addend):
+    """seg_conv_igemm_red(_bf16) + seg_bn_backward_parts == seg_conv_igemm(_bf16) +
+    seg_bn_backward: dA bitwise, dY / dgamma / dbeta to fp32 summation order."""
+    s = S()
+    M, pad = N * H * W, ks // 2
+    C = Cin  # the BN layer whose dA the data gradient completes
+    dyc = gen(M, Cout, seed=31).to(DEV)
+    w = (gen(Cout, Cin, ks, ks, seed=32) * 0.1).to(DEV)
+    kin = r4(Cout)
+    ldk = r4(ks * ks * kin)
+    wkd = torch.empty(Cin * ldk, device=DEV)
+    call("seg_pack_conv_weight", w.data_ptr(), wkd.data_ptr(), Cout, Cin, ks, ldk, 1, kin, s)
+    y = (gen(M, C, seed=33) * 2 + 1).to(DEV)
+    gamma = (gen(C, seed=34) * 0.5 + 1).to(DEV)
+    mean = gen(C, seed=35).to(DEV) * 0.3 + 1
+    invstd = (torch.rand(C, generator=torch.Generator().manual_seed(36)) + 0.5).to(DEV)
+    scale, shift = gamma * invstd, gen(C, seed=37).to(DEV) + 1
+    add = gen(M, C, seed=38).to(DEV) if addend else None
+    add_ptr, add_ld = (add.data_ptr(), C) if addend else (None, 0)
+    bf = math == "bf16"
+    # reference path: plain data gradient, then the BN backward with its own reduction
+    da = torch.empty(M, C, device=DEV)
+    call("seg_conv_igemm_bf16" if bf else "seg_conv_igemm_act", dyc.data_ptr(), Cout, N, H, W, kin, wkd.data_ptr(),
+         ldk, None, da.data_ptr(), C, H, W, Cin, ks, 1, pad, add_ptr, add_ld, None, 0, None, 1, s)
+    dy_a = torch.empty(M, C, device=DEV)
+    g_a, b_a = torch.empty(C, device=DEV), torch.empty(C, device=DEV)
+    work = torch.empty(query("seg_chan_workspace_floats", M, C) + 3 * C, device=DEV)
+    call("seg_bn_backward", da.data_ptr(), C, y.data_ptr(), C, M, C, gamma.data_ptr(), mean.data_ptr(),
+         invstd.data_ptr(), scale.data_ptr(), shift.data_ptr(), act, g_a.data_ptr(), b_a.data_ptr(), work.data_ptr(),
+         dy_a.data_ptr(), C, s)
+    # fused path
+    ntiles = query("seg_conv_igemm_row_tiles", M, Cin, None)
+    part = torch.full((ntiles * 2 * C,), float("nan"), device=DEV)
+    da2 = torch.empty(M, C, device=DEV)
+    call("seg_conv_igemm_red_bf16" if bf else "seg_conv_igemm_red", dyc.data_ptr(), Cout, N, H, W, kin,
+         wkd.data_ptr(), ldk, da2.data_ptr(), C, Cin, ks, pad, add_ptr, add_ld, y.data_ptr(), C, scale.data_ptr(),
+         shift.data_ptr(), mean.data_ptr(), act, part.data_ptr(), s)
+    assert torch.equal(da2, da)
+    dy_b = torch.empty(M, C, device=DEV)
+    g_b, b_b = torch.empty(C, device=DEV), torch.empty(C, device=DEV)
+    coef = torch.empty(3 * C, device=DEV)
+    call("seg_bn_backward_parts", part.data_ptr(), ntiles, da2.data_ptr(), C, y.data_ptr(), C, M, C,
+         gamma.data_ptr(), mean.data_ptr(), invstd.data_ptr(), scale.data_ptr(), shift.data_ptr(), act,
+         g_b.data_ptr(), b_b.data_ptr(), coef.data_ptr(), dy_b.data_ptr(), C, s)
+    assert rel(b_b, b_a) < 1e-5 and rel(g_b, g_a) < 1e-5
+    assert rel(dy_b, dy_a) < 1e-5

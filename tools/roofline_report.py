@@ -19,10 +19,10 @@ import sys
 from collections import defaultdict
 
 FAMILIES = {  # "conv3" = the dense 3x3 conv forward + data gradient (bench.py's roofline kernel family)
-    "conv3": re.compile(r"igemm_conv_kernel<\d+, \d+, \d+, \d+, 3, \d+|wino_gemm_kernel|wino_out_kernel"),
+    "conv3": re.compile(r"igemm_conv_kernel<\d+, \d+, \d+, \d+, 3, \d+|wino_gemm_kernel|wino_out_kernel|halo3x3_kernel"),
     "igemm1": re.compile(r"igemm_conv_kernel<\d+, \d+, \d+, \d+, 1, \d+"),
-    "wgrad3": re.compile(r"wgrad_kernel<\d+, \d+, \d+, \d+, 3>|wino_wgrad"),
-    "wgrad1": re.compile(r"wgrad_kernel<\d+, \d+, \d+, \d+, 1>"),
+    "wgrad3": re.compile(r"wgrad_kernel<\d+, \d+, \d+, \d+, 3[,>]|wino_wgrad"),
+    "wgrad1": re.compile(r"wgrad_kernel<\d+, \d+, \d+, \d+, 1[,>]"),
 }
 OPS_PER_STEP = {"conv3": 17}  # MobileNetV2UNet bs=32: 8 decoder convs fwd + 8 dgrad + the stem fwd
 

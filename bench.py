@@ -196,7 +196,10 @@ def main():
 
     for _ in range(args.warmup):
         step()
-    timer = None if args.no_timer else engine.KernelTimer()
+    # live per-launch HIP events on the roofline family only (each event pair is a marker
+    # packet on the queue: timing all ~130 conv launches costs ~3 % of the step)
+    conv3 = {"igemm3_fwd", "igemm3_dgrad", "wino3_fwd", "wino3_dgrad"}
+    timer = None if args.no_timer else engine.KernelTimer(kinds=conv3)
     if dist:
         torch.distributed.barrier()
     torch.cuda.synchronize()
@@ -219,17 +222,30 @@ def main():
 
     roof = None
     if timer is not None:
-        rec = timer.elapsed()
-
-        def family(kinds):
+        def family(rec, kinds):
             sel = [(f, s) for k, f, s in rec if k in kinds]
             fl, sec = sum(f for f, _ in sel), sum(s for _, s in sel)
             return fl, sec, len(sel)
 
-        # dominant kernel: igemm_conv_kernel<BM,BN,WM,WN,3,16> = every dense 3x3 conv's
-        # forward and data gradient (the top symbol family in the rocprof summary)
-        flops, secs, n = family({"igemm3_fwd", "igemm3_dgrad", "wino3_fwd", "wino3_dgrad"})
-        wfl, wsec, wn = family({"wino3_fwd", "wino3_dgrad"})
+        def extra_pass(overlap):
+            """3 untimed steps with every conv launch timed (after the timed region)."""
+            saved = engine.OVERLAP
+            engine.OVERLAP = overlap
+            t = engine.KernelTimer()
+            engine.TIMER = t
+            for _ in range(3):
+                step()
+            torch.cuda.synchronize()
+            engine.TIMER = None
+            engine.OVERLAP = saved
+            return t.elapsed()
+
+        # dominant kernel family: every dense 3x3 conv's forward and data gradient
+        # (implicit GEMM / Winograd / LDS-halo; the top family in the rocprof summary),
+        # timed live inside the timed region
+        rec = timer.elapsed()
+        flops, secs, n = family(rec, conv3)
+        wfl, wsec, wn = family(rec, {"wino3_fwd", "wino3_dgrad"})
         achieved = flops / secs / 1e12 if secs > 0 else 0.0
         traffic = None
         prof = os.path.join(REPO, "profiles", "latest_roofline.json" if args.math == "f32"
@@ -249,45 +265,38 @@ def main():
                 if not op.first:
                     abytes.append(xy)
         alg_bytes = sum(abytes) / max(len(abytes), 1)
-        wf, ws, wn = family({"igemm3_wgrad", "wino3_wgrad"})
-        af, as_, an = family({k for k, _, _ in rec})
+        # the other conv families and the side-stream-free figure: separate untimed passes
+        rec_all = extra_pass(engine.OVERLAP)
+        wf, ws, wgn = family(rec_all, {"igemm3_wgrad", "wino3_wgrad"})
+        af, as_, an = family(rec_all, {k for k, _, _ in rec_all})
+        rec_iso = extra_pass(False)
+        ifl, isec, inn = family(rec_iso, conv3)
         roof = {"bound": "mfma", "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
                 "frac": round(achieved / peak, 4),
                 "traffic": round(traffic) if traffic else None,
                 "traffic_source": f"{os.path.relpath(prof, REPO)}: rocprofv3 PMC (2*FETCH_SIZE+WRITE_SIZE)*1KiB "
                                   "of the conv3 family per step / 17 conv ops" if traffic else None,
                 "algorithmic_bytes_per_launch": round(alg_bytes),
-                "kernel": ("dense 3x3 conv fwd + dgrad on f32 MFMA: igemm_conv_kernel<*,*,*,*,3,*> (implicit GEMM) "
-                           "and, for the deep decoder convs, wino_gemm_kernel + wino_out_kernel (Winograd F(2x2,3x3): "
-                           "2.25x fewer executed MFMA FLOPs than the algorithmic count used here)"
+                "kernel": ("dense 3x3 conv fwd + dgrad on f32 MFMA: igemm_conv_kernel<*,*,*,*,3,*> (implicit GEMM), "
+                           "halo3x3_kernel (LDS-halo direct conv, narrow decoder convs) and, for the deep decoder "
+                           "convs, wino_gemm_kernel + wino_out_kernel (Winograd F(2x2,3x3): 2.25x fewer executed "
+                           "MFMA FLOPs than the algorithmic count used here)"
                            if args.math == "f32" else
-                           "dense 3x3 conv fwd + dgrad on bf16 MFMA: igemm_conv_kernel<*,*,*,*,3,*,*,false,true> "
+                           "dense 3x3 conv fwd + dgrad on bf16 MFMA: igemm_conv_kernel<*,*,*,*,3,*,*,false,__bf16> "
                            "(implicit GEMM, v_mfma_f32_32x32x16_bf16, fp32 accumulation)"),
                 "winograd": {"launches": wn, "algorithmic_tflops": round(wfl / wsec / 1e12, 2) if wsec else None,
                              "executed_mfma_tflops": round(wfl / 2.25 / wsec / 1e12, 2) if wsec else None},
                 "launches": n, "flops_per_launch": round(flops / max(n, 1)),
                 "avg_launch_us": round(secs / max(n, 1) * 1e6, 2),
                 "share_of_step": round(secs / dt, 4),
-                "wgrad3": {"achieved": round(wf / ws / 1e12, 2) if ws else None, "launches": wn,
-                           "avg_launch_us": round(ws / max(wn, 1) * 1e6, 2)},
-                "all_mfma_convs": {"achieved": round(af / as_ / 1e12, 2) if as_ else None, "launches": an,
-                                   "share_of_step": round(as_ / dt, 4)}}
-        # The live figure above includes CU sharing with the weight-gradient side stream
-        # (engine.OVERLAP): the same launches re-timed over 3 untimed steps with the side
-        # stream off show what the kernels reach when they own the GPU.
-        saved = engine.OVERLAP
-        engine.OVERLAP = False
-        iso = engine.KernelTimer()
-        engine.TIMER = iso
-        for _ in range(3):
-            step()
-        torch.cuda.synchronize()
-        engine.TIMER = None
-        engine.OVERLAP = saved
-        rec = iso.elapsed()
-        ifl, isec, inn = family({"igemm3_fwd", "igemm3_dgrad", "wino3_fwd", "wino3_dgrad"})
-        roof["without_side_stream"] = {"achieved": round(ifl / isec / 1e12, 2), "frac": round(ifl / isec / 1e12 / peak, 4),
-                                       "avg_launch_us": round(isec / max(inn, 1) * 1e6, 2), "launches": inn}
+                "note": "live launches share the CUs with the weight-gradient side stream (engine.OVERLAP); "
+                        "without_side_stream re-times the same launches in 3 untimed steps with it off",
+                "without_side_stream": {"achieved": round(ifl / isec / 1e12, 2) if isec else None,
+                                        "frac": round(ifl / isec / 1e12 / peak, 4) if isec else None,
+                                        "avg_launch_us": round(isec / max(inn, 1) * 1e6, 2), "launches": inn},
+                "wgrad3": {"achieved": round(wf / ws / 1e12, 2) if ws else None, "launches": wgn,
+                           "avg_launch_us": round(ws / max(wgn, 1) * 1e6, 2)},
+                "all_mfma_convs": {"achieved": round(af / as_ / 1e12, 2) if as_ else None, "launches": an}}
 
     if rank == 0:
         cpu = None

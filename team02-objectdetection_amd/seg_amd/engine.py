@@ -45,8 +45,11 @@ class KernelTimer:
     bench.py for the roofline figure).  Each timed launch is bracketed by two
     events on the stream it runs on (torch's current stream)."""
 
-    def __init__(self):
+    def __init__(self, kinds=None):
         self.records = []  # (kind, flops, start_event, end_event)
+        # only these launch kinds are bracketed (None: all): every event pair is a marker
+        # packet on the queue, ~3 % of the step when all ~130 conv launches are timed
+        self.kinds = kinds
 
     def elapsed(self):
         """[(kind, flops, seconds)] -- call after synchronising."""
@@ -70,7 +73,7 @@ BNB_ON_LOAD = os.environ.get("SEG_BNB", "0") == "1"
 
 
 def _timed_call(kind, flops, name, *args):
-    if TIMER is None:
+    if TIMER is None or (TIMER.kinds is not None and kind not in TIMER.kinds):
         return call(name, *args)
     a = torch.cuda.Event(enable_timing=True)
     b = torch.cuda.Event(enable_timing=True)
@@ -1059,8 +1062,11 @@ class Run:
 # memory-bound BatchNorm / depthwise / 1x1 kernels of the main stream.  Results are the
 # same either way (the kernels and their reduction orders do not change).
 OVERLAP = os.environ.get("SEG_OVERLAP", "1") == "1"
-# Fused BatchNorm-backward reductions (Program._plan_bn_red); SEG_BN_RED=0 turns them off.
-BN_RED = os.environ.get("SEG_BN_RED", "1") == "1"
+# Fused BatchNorm-backward reductions (Program._plan_bn_red): parity-tested, but measured
+# no faster on MI355X in round 1 (f32 1707 vs 1711 img/s, bf16 2337 vs 2374: the y loads
+# in the data-gradient epilogue sit on the critical main stream, while the separate
+# reduction pass is cheap there); off unless SEG_BN_RED=1.
+BN_RED = os.environ.get("SEG_BN_RED", "0") == "1"
 _SIDE = {}
 
 

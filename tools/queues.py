@@ -11,6 +11,9 @@ import sys
 
 def family(n):
     n = n.replace("(anonymous namespace)::", "")
+    mm = re.search(r"(igemm_conv_kernel)ILi\d+ELi\d+ELi\d+ELi\d+ELi(\d)E.*DF16b", n)
+    if mm:  # rocprofv3 leaves the __bf16 instantiations mangled
+        return f"{mm.group(1)}{mm.group(2)}_bf16"
     m = re.match(r"(?:void )?([A-Za-z_0-9]+)(<[^(]*>)?", n)
     base = m.group(1)
     if base in ("igemm_conv_kernel", "wgrad_kernel"):

@@ -55,10 +55,11 @@ def parse():
     ap.add_argument("--workload", choices=("train", "infer"), default="train",
                     help="train: BASELINE configs[1] (the headline); infer: configs[3], inference.py's per-frame path")
     ap.add_argument("--frames", type=int, default=500, help="timed frames of --workload infer")
-    ap.add_argument("--math", choices=("f32", "bf16", "f16"), default=None,
+    ap.add_argument("--math", choices=("f32", "bf16", "bf16io", "f16"), default=None,
                     help="conv arithmetic. train: f32 = configs[1] (default, the headline); bf16 = the bf16 "
                          "configurations (configs[2]/[4]): bf16 MFMA operands, fp32 accumulation / activations / BN "
-                         "/ Adam.  infer: f16 = configs[3] (default), f32, bf16")
+                         "/ Adam; bf16io = bf16 math + bf16 activation/gradient storage.  infer: f16 = configs[3] "
+                         "(default), f32, bf16")
     ap.add_argument("--model", choices=("MobileNetV2UNet", "UNet"), default="MobileNetV2UNet",
                     help="UNet = BASELINE configs[4] shape family (use --height 512 --width 1024 --batch 8)")
     return ap.parse_args()
@@ -159,6 +160,8 @@ def main():
     args = parse()
     if args.math is None:
         args.math = "f16" if args.workload == "infer" else "f32"
+    if args.workload == "infer" and args.math == "bf16io":
+        raise SystemExit("--math bf16io is a training configuration")
     if args.workload == "train" and args.math == "f16":
         raise SystemExit("--math f16 is the inference configuration (--workload infer)")
     if args.workload == "infer":
@@ -177,7 +180,7 @@ def main():
     from seg_amd import engine
     model = deterministic_init(getattr(seg_amd, args.model)(args.classes), seed=0).to(dev).train()
     engine.set_conv_math(model, args.math)
-    peak = BF16_MFMA_PEAK_TFLOPS if args.math == "bf16" else F32_MFMA_PEAK_TFLOPS
+    peak = F32_MFMA_PEAK_TFLOPS if args.math == "f32" else BF16_MFMA_PEAK_TFLOPS
     if dist:
         from seg_amd.ddp import DataParallel
         model = DataParallel(model)
@@ -303,7 +306,7 @@ def main():
         if world == 1 and not args.no_cpu_baseline:
             cpu = cpu_baseline(args)
         if args.model == "MobileNetV2UNet":
-            cfg = "BASELINE configs[1]" if args.math == "f32" else "BASELINE configs[2] math (bf16) at N GPUs"
+            cfg = "BASELINE configs[1]" if args.math == "f32" else f"BASELINE configs[2] math ({args.math}) at N GPUs"
         else:
             cfg = f"BASELINE configs[4] shape, {args.math} conv math"
         line = {"metric": f"images/sec fwd+bwd {args.model} {args.height}x{args.width} bs={args.batch}/GPU",
@@ -315,9 +318,12 @@ def main():
                            "model": args.model, "global_batch": args.batch * world,
                            "image": [args.height, args.width], "parallelism": f"dp{world}"},
                 "final_loss": round(final_loss, 5),
-                "math": ("fp32 everywhere" if args.math == "f32" else
-                         "conv operands bf16 (RNE) on the bf16 MFMA, fp32 accumulation; activations, BatchNorm, "
-                         "depthwise convs, loss and Adam in fp32"),
+                "math": {"f32": "fp32 everywhere",
+                         "bf16": "conv operands bf16 (RNE) on the bf16 MFMA, fp32 accumulation; activations, "
+                                 "BatchNorm, depthwise convs, loss and Adam in fp32",
+                         "bf16io": "conv operands bf16 on the bf16 MFMA, fp32 accumulation; activations and their "
+                                   "gradients stored bf16 in HBM (fp32 arithmetic inside every kernel); BN "
+                                   "statistics, parameter gradients, loss and Adam fp32"}[args.math],
                 "roofline": roof, "cpu_baseline": cpu}
         print(json.dumps(line), flush=True)
     if dist:

@@ -21,6 +21,7 @@
 #ifndef SEGAMD_H
 #define SEGAMD_H
 #include <hip/hip_runtime.h>
+#include <stdint.h>
 #ifdef __cplusplus
 extern "C" {
 #endif
@@ -344,6 +345,56 @@ typedef struct seg_aug_param {
 int seg_augment(const unsigned char* img, const unsigned char* mask, int N, int H, int W, const void* params,
                 float mean_r, float mean_g, float mean_b, float rstd_r, float rstd_g, float rstd_b, float* x,
                 long long* y, hipStream_t stream);
+
+
+/* ---------------------------------------------------------------- bf16 storage
+ * `_bf16io` entry points: the same operations as their fp32 namesakes (same argument
+ * meaning, strides in elements) on bf16 activation / gradient tensors -- the storage of
+ * the "bf16io" configuration (engine math "bf16io": bf16 conv operands AND bf16
+ * tensors between kernels).  Arithmetic inside every kernel stays fp32: loads widen
+ * bf16 -> fp32, stores round fp32 -> bf16 (round-to-nearest-even); BatchNorm
+ * statistics, reduction partials, coefficients, weights and parameter gradients stay
+ * fp32.  seg_bf16 = the raw 16-bit bf16 pattern. */
+typedef uint16_t seg_bf16;
+int seg_add_bf16io(const seg_bf16* a, long lda, const seg_bf16* b, long ldb, long M, int C, seg_bf16* out, long ldout,
+    hipStream_t stream);
+int seg_bn_stats_bf16io(const seg_bf16* y, long ldy, long M, int C, const float* gamma, const float* beta, float eps,
+    float momentum, float* running_mean, float* running_var, long long* num_batches_tracked, float* work, float* mean,
+    float* invstd, float* scale, float* shift, hipStream_t stream);
+int seg_bn_apply_bf16io(const seg_bf16* y, long ldy, long M, int C, const float* scale, const float* shift, int act,
+    const seg_bf16* res, long ldres, seg_bf16* out, long ldout, hipStream_t stream);
+int seg_bn_backward_bf16io(const seg_bf16* da, long ldda, const seg_bf16* y, long ldy, long M, int C, const float*
+    gamma, const float* mean, const float* invstd, const float* scale, const float* shift, int act, float* dgamma,
+    float* dbeta, float* work, seg_bf16* dy, long lddy, hipStream_t stream);
+int seg_colsum_bf16io(const seg_bf16* y, long ldy, long M, int C, float* work, float* out, int accumulate, hipStream_t
+    stream);
+int seg_dw_fwd_bf16io(const seg_bf16* in, long ldin, int N, int H, int W, int C, const float* in_scale, const float*
+    in_shift, int in_act, const float* wk, seg_bf16* out, long ldout, int Ho, int Wo, int stride, hipStream_t stream);
+int seg_dw_dgrad_bf16io(const seg_bf16* dy, long lddy, int N, int Ho, int Wo, int C, const float* wk, seg_bf16* dx,
+    long lddx, int H, int W, int stride, int accumulate, hipStream_t stream);
+int seg_dw_wgrad_bf16io(const seg_bf16* dy, long lddy, const seg_bf16* x, long ldx, int N, int H, int W, int C, const
+    float* in_scale, const float* in_shift, int in_act, int Ho, int Wo, int stride, float* part, hipStream_t stream);
+int seg_conv_igemm_bf16io(const seg_bf16* in, long ldin, int N, int H, int W, int Cin, const float* wk, int ldk, const
+    float* bias, seg_bf16* out, long ldout, int Ho, int Wo, int Cout, int ks, int stride, int pad, const seg_bf16*
+    add, long ldadd, float* stat, hipStream_t stream);
+int seg_ce_upsample_loss_bf16io(const seg_bf16* low, long ld, int N, int H, int W, int C, const long long* labels, int
+    Ho, int Wo, int ignore_index, float* work, float* out2, hipStream_t stream);
+int seg_ce_upsample_grad_bf16io(const seg_bf16* low, long ld, int N, int H, int W, int C, const long long* labels, int
+    Ho, int Wo, int ignore_index, const float* grad_out, const float* stats, seg_bf16* dhigh, long ldh, hipStream_t
+    stream);
+int seg_upsample_fwd_bf16io(const seg_bf16* in, long ldin, int N, int H, int W, int C, seg_bf16* out, long ldout, int
+    Ho, int Wo, int ac, hipStream_t stream);
+int seg_upsample_bwd_bf16io(const void* dout, long ldout, int nchw_grad, int N, int Ho, int Wo, int C, seg_bf16* din,
+    long ldin, int H, int W, int ac, int accumulate, hipStream_t stream);
+int seg_upsample_to_nchw_bf16io(const seg_bf16* in, long ldin, int N, int H, int W, int C, float* out, int Ho, int Wo,
+    int ac, hipStream_t stream);
+int seg_nchw_to_nhwc_bf16io(const float* x, int N, int C, int H, int W, seg_bf16* out, int ld, hipStream_t stream);
+int seg_maxpool2_fwd_bf16io(const seg_bf16* in, long ldin, int N, int H, int W, int C, seg_bf16* out, long ldout,
+    hipStream_t stream);
+int seg_maxpool2_bwd_bf16io(const seg_bf16* in, long ldin, const seg_bf16* dout, long lddout, int N, int H, int W, int
+    C, seg_bf16* din, long lddin, int accumulate, hipStream_t stream);
+int seg_conv_wgrad_bf16io(const seg_bf16* dy, long lddy, const seg_bf16* x, long ldx, int N, int H, int W, int Cin,
+    int Ho, int Wo, int Cout, int ks, int stride, int pad, float* part, int splits, hipStream_t stream);
 
 #ifdef __cplusplus
 }

@@ -23,9 +23,9 @@ namespace {
 // kind 1: (sum(dz),  sum(dz*(y-mean))), dz = dA * act'(y*scale+shift) -> BN backward
 // kind 2: (sum(y), 0)                                               -> bias grad
 // kind 3: (sum(dY), 0), dY = BN backward of (da, y) formed on load     -> bias grad of a BN conv
-template <int KIND>
+template <int KIND, typename T = float>
 __global__ __launch_bounds__(256) void chan_partial_kernel(
-    const float* __restrict__ y, long ldy, const float* __restrict__ da, long ldda, int M, int C,
+    const T* __restrict__ y, long ldy, const T* __restrict__ da, long ldda, int M, int C,
     const float* __restrict__ scale, const float* __restrict__ shift, const float* __restrict__ mean, int act,
     float* __restrict__ part, int rows_per_block, SegBnBwd bnb) {
   __shared__ f32x4 red0[256], red1[256];
@@ -127,8 +127,9 @@ __device__ __forceinline__ void sum_partials(const float* __restrict__ part, int
   *s1 = rb[0];
 }
 
+template <typename T>
 __global__ __launch_bounds__(256) void bn_finalize_kernel(
-    const float* __restrict__ part, int nblk, const float* __restrict__ y, long M, int C,
+    const float* __restrict__ part, int nblk, const T* __restrict__ y, long M, int C,
     const float* __restrict__ gamma, const float* __restrict__ beta, float eps, float momentum,
     float* running_mean, float* running_var, long long* nbt, float* mean_out, float* invstd_out, float* scale_out,
     float* shift_out) {
@@ -137,7 +138,7 @@ __global__ __launch_bounds__(256) void bn_finalize_kernel(
   double s, s2;
   sum_partials(part, nblk, C, C, c, threadIdx.x, &s, &s2);
   if (threadIdx.x != 0) return;
-  const double k = y[c];
+  const double k = (float)y[c];
   const double dm = s / (double)M;
   const double mean = k + dm;
   double var = s2 / (double)M - dm * dm;
@@ -224,9 +225,10 @@ __global__ void bn_eval_coef_kernel(const float* gamma, const float* beta, const
 }
 
 // out = act(y*scale + shift) (+ res)
-__global__ void bn_apply_kernel(const float* __restrict__ y, long ldy, long M, int C, const float* __restrict__ scale,
-                                const float* __restrict__ shift, int act, const float* __restrict__ res, long ldres,
-                                float* __restrict__ out, long ldout) {
+template <typename T>
+__global__ void bn_apply_kernel(const T* __restrict__ y, long ldy, long M, int C, const float* __restrict__ scale,
+                                const float* __restrict__ shift, int act, const T* __restrict__ res, long ldres,
+                                T* __restrict__ out, long ldout) {
   const int CG = C >> 2;
   const long total = M * CG;
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
@@ -255,10 +257,11 @@ __global__ void bn_bwd_finalize_kernel(const float* __restrict__ part, int nblk,
   coef[2 * C + c] = (float)(sdzx * inv * inv / (double)M);
 }
 
-__global__ void bn_bwd_apply_kernel(const float* __restrict__ da, long ldda, const float* __restrict__ y, long ldy,
+template <typename T>
+__global__ void bn_bwd_apply_kernel(const T* __restrict__ da, long ldda, const T* __restrict__ y, long ldy,
                                     long M, int C, const float* __restrict__ scale, const float* __restrict__ shift,
                                     const float* __restrict__ mean, int act, const float* __restrict__ coef,
-                                    float* __restrict__ dy, long lddy) {
+                                    T* __restrict__ dy, long lddy) {
   const int CG = C >> 2;
   const long total = M * CG;
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
@@ -300,8 +303,9 @@ __global__ void colsum_finalize_kernel(const float* __restrict__ part, int nblk,
 
 int ew_grid(long total) { return (int)std::min<long>(seg_cdiv(total, 256), 8192); }
 
-__global__ void add_kernel(const float* __restrict__ a, long lda, const float* __restrict__ b, long ldb, long M, int C,
-                           float* __restrict__ out, long ldout) {
+template <typename T>
+__global__ void add_kernel(const T* __restrict__ a, long lda, const T* __restrict__ b, long ldb, long M, int C,
+                           T* __restrict__ out, long ldout) {
   const int CG = C >> 2;
   const long total = M * CG;
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
@@ -316,11 +320,23 @@ __global__ void add_kernel(const float* __restrict__ a, long lda, const float* _
 }  // namespace
 
 // out = a (+ b), all [M][C] NHWC strided (out may alias a or b).  Gradient fan-in.
+template <typename T>
+static int add_impl(const T* a, long lda, const T* b, long ldb, long M, int C, T* out, long ldout, hipStream_t stream) {
+  if ((C & 3) || (lda & 3) || (ldout & 3) || (b && (ldb & 3))) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(add_kernel<T>, dim3(ew_grid(M * (C / 4))), dim3(256), 0, stream, a, lda, b, ldb, M, C, out,
+                     ldout);
+  SEG_RET_LAST();
+}
 SEG_API int seg_add(const float* a, long lda, const float* b, long ldb, long M, int C, float* out, long ldout,
                     hipStream_t stream) {
-  if ((C & 3) || (lda & 3) || (ldout & 3) || (b && (ldb & 3))) return (int)hipErrorInvalidValue;
-  hipLaunchKernelGGL(add_kernel, dim3(ew_grid(M * (C / 4))), dim3(256), 0, stream, a, lda, b, ldb, M, C, out, ldout);
-  SEG_RET_LAST();
+  return add_impl(a, lda, b, ldb, M, C, out, ldout, stream);
+}
+// `_bf16io` entry points (this file and the others): the same operation on bf16
+// activation / gradient tensors (arguments as the fp32 version, element strides);
+// statistics, partial sums and coefficients stay fp32.
+SEG_API int seg_add_bf16io(const __bf16* a, long lda, const __bf16* b, long ldb, long M, int C, __bf16* out,
+                           long ldout, hipStream_t stream) {
+  return add_impl(a, lda, b, ldb, M, C, out, ldout, stream);
 }
 
 // Size (floats) of the partial-sum workspace the channel reductions below need.
@@ -331,17 +347,31 @@ SEG_API long seg_chan_workspace_floats(long M, int C) {
 
 // Train-mode BN statistics: fills mean/invstd/scale/shift ([C] each) and updates
 // the running buffers (skipped when running_mean is null) and num_batches_tracked.
-SEG_API int seg_bn_stats(const float* y, long ldy, long M, int C, const float* gamma, const float* beta, float eps,
+template <typename T>
+static int bn_stats_impl(const T* y, long ldy, long M, int C, const float* gamma, const float* beta, float eps,
                          float momentum, float* running_mean, float* running_var, long long* num_batches_tracked,
                          float* work, float* mean, float* invstd, float* scale, float* shift, hipStream_t stream) {
   if ((C & 3) || (ldy & 3) || M < 1) return (int)hipErrorInvalidValue;
   const int rpb = rows_per_block_for(M);
   const int nblk = seg_cdiv(M, rpb);
-  hipLaunchKernelGGL(chan_partial_kernel<0>, dim3(nblk), dim3(256), 0, stream, y, ldy, nullptr, 0L, (int)M, C,
-                     nullptr, nullptr, nullptr, 0, work, rpb, SegBnBwd{});
-  hipLaunchKernelGGL(bn_finalize_kernel, dim3(C), dim3(256), 0, stream, work, nblk, y, M, C, gamma,
+  hipLaunchKernelGGL((chan_partial_kernel<0, T>), dim3(nblk), dim3(256), 0, stream, y, ldy, (const T*)nullptr, 0L,
+                     (int)M, C, nullptr, nullptr, nullptr, 0, work, rpb, SegBnBwd{});
+  hipLaunchKernelGGL(bn_finalize_kernel<T>, dim3(C), dim3(256), 0, stream, work, nblk, y, M, C, gamma,
                      beta, eps, momentum, running_mean, running_var, num_batches_tracked, mean, invstd, scale, shift);
   SEG_RET_LAST();
+}
+SEG_API int seg_bn_stats(const float* y, long ldy, long M, int C, const float* gamma, const float* beta, float eps,
+                         float momentum, float* running_mean, float* running_var, long long* num_batches_tracked,
+                         float* work, float* mean, float* invstd, float* scale, float* shift, hipStream_t stream) {
+  return bn_stats_impl(y, ldy, M, C, gamma, beta, eps, momentum, running_mean, running_var, num_batches_tracked, work,
+                       mean, invstd, scale, shift, stream);
+}
+SEG_API int seg_bn_stats_bf16io(const __bf16* y, long ldy, long M, int C, const float* gamma, const float* beta,
+                                float eps, float momentum, float* running_mean, float* running_var,
+                                long long* num_batches_tracked, float* work, float* mean, float* invstd, float* scale,
+                                float* shift, hipStream_t stream) {
+  return bn_stats_impl(y, ldy, M, C, gamma, beta, eps, momentum, running_mean, running_var, num_batches_tracked, work,
+                       mean, invstd, scale, shift, stream);
 }
 
 // Train-mode BN statistics from seg_conv_igemm's epilogue partials (`stat`
@@ -366,30 +396,53 @@ SEG_API int seg_bn_eval_coef(const float* gamma, const float* beta, const float*
   SEG_RET_LAST();
 }
 
-SEG_API int seg_bn_apply(const float* y, long ldy, long M, int C, const float* scale, const float* shift, int act,
-                         const float* res, long ldres, float* out, long ldout, hipStream_t stream) {
+template <typename T>
+static int bn_apply_impl(const T* y, long ldy, long M, int C, const float* scale, const float* shift, int act,
+                         const T* res, long ldres, T* out, long ldout, hipStream_t stream) {
   if ((C & 3) || (ldy & 3) || (ldout & 3) || (res && (ldres & 3))) return (int)hipErrorInvalidValue;
-  hipLaunchKernelGGL(bn_apply_kernel, dim3(ew_grid(M * (C / 4))), dim3(256), 0, stream, y, ldy, M, C, scale, shift,
+  hipLaunchKernelGGL(bn_apply_kernel<T>, dim3(ew_grid(M * (C / 4))), dim3(256), 0, stream, y, ldy, M, C, scale, shift,
                      act, res, ldres, out, ldout);
   SEG_RET_LAST();
+}
+SEG_API int seg_bn_apply(const float* y, long ldy, long M, int C, const float* scale, const float* shift, int act,
+                         const float* res, long ldres, float* out, long ldout, hipStream_t stream) {
+  return bn_apply_impl(y, ldy, M, C, scale, shift, act, res, ldres, out, ldout, stream);
+}
+SEG_API int seg_bn_apply_bf16io(const __bf16* y, long ldy, long M, int C, const float* scale, const float* shift,
+                                int act, const __bf16* res, long ldres, __bf16* out, long ldout, hipStream_t stream) {
+  return bn_apply_impl(y, ldy, M, C, scale, shift, act, res, ldres, out, ldout, stream);
 }
 
 // Train-mode BN backward through the activation: writes dgamma/dbeta ([C]) and
 // dy = d(conv output).  `work` >= seg_chan_workspace_floats(M,C) + 3*C floats.
-SEG_API int seg_bn_backward(const float* da, long ldda, const float* y, long ldy, long M, int C, const float* gamma,
+template <typename T>
+static int bn_backward_impl(const T* da, long ldda, const T* y, long ldy, long M, int C, const float* gamma,
                             const float* mean, const float* invstd, const float* scale, const float* shift, int act,
-                            float* dgamma, float* dbeta, float* work, float* dy, long lddy, hipStream_t stream) {
+                            float* dgamma, float* dbeta, float* work, T* dy, long lddy, hipStream_t stream) {
   if ((C & 3) || (ldy & 3) || (ldda & 3) || (lddy & 3)) return (int)hipErrorInvalidValue;
   const int rpb = rows_per_block_for(M);
   const int nblk = seg_cdiv(M, rpb);
   float* coef = work + (long)nblk * 2 * C;
-  hipLaunchKernelGGL(chan_partial_kernel<1>, dim3(nblk), dim3(256), 0, stream, y, ldy, da, ldda, (int)M, C, scale,
+  hipLaunchKernelGGL((chan_partial_kernel<1, T>), dim3(nblk), dim3(256), 0, stream, y, ldy, da, ldda, (int)M, C, scale,
                      shift, mean, act, work, rpb, SegBnBwd{});
   hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(C), dim3(256), 0, stream, work, nblk, M, C, gamma,
                      invstd, dgamma, dbeta, coef);
-  hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(ew_grid(M * (C / 4))), dim3(256), 0, stream, da, ldda, y, ldy, M, C,
-                     scale, shift, mean, act, coef, dy, lddy);
+  hipLaunchKernelGGL(bn_bwd_apply_kernel<T>, dim3(ew_grid(M * (C / 4))), dim3(256), 0, stream, da, ldda, y, ldy, M,
+                     C, scale, shift, mean, act, coef, dy, lddy);
   SEG_RET_LAST();
+}
+SEG_API int seg_bn_backward(const float* da, long ldda, const float* y, long ldy, long M, int C, const float* gamma,
+                            const float* mean, const float* invstd, const float* scale, const float* shift, int act,
+                            float* dgamma, float* dbeta, float* work, float* dy, long lddy, hipStream_t stream) {
+  return bn_backward_impl(da, ldda, y, ldy, M, C, gamma, mean, invstd, scale, shift, act, dgamma, dbeta, work, dy,
+                          lddy, stream);
+}
+SEG_API int seg_bn_backward_bf16io(const __bf16* da, long ldda, const __bf16* y, long ldy, long M, int C,
+                                   const float* gamma, const float* mean, const float* invstd, const float* scale,
+                                   const float* shift, int act, float* dgamma, float* dbeta, float* work, __bf16* dy,
+                                   long lddy, hipStream_t stream) {
+  return bn_backward_impl(da, ldda, y, ldy, M, C, gamma, mean, invstd, scale, shift, act, dgamma, dbeta, work, dy,
+                          lddy, stream);
 }
 
 // seg_bn_backward whose reduction was fused into the producer of dA
@@ -402,7 +455,7 @@ SEG_API int seg_bn_backward_parts(const float* part, int nparts, const float* da
   if ((C & 3) || (ldy & 3) || (ldda & 3) || (lddy & 3) || nparts < 1) return (int)hipErrorInvalidValue;
   hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(C), dim3(256), 0, stream, part, nparts, M, C, gamma,
                      invstd, dgamma, dbeta, coef);
-  hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(ew_grid(M * (C / 4))), dim3(256), 0, stream, da, ldda, y, ldy, M, C,
+  hipLaunchKernelGGL(bn_bwd_apply_kernel<float>, dim3(ew_grid(M * (C / 4))), dim3(256), 0, stream, da, ldda, y, ldy, M, C,
                      scale, shift, mean, act, coef, dy, lddy);
   SEG_RET_LAST();
 }
@@ -418,7 +471,7 @@ SEG_API int seg_bn_backward_coef(const float* da, long ldda, const float* y, lon
   if ((C & 3) || (ldy & 3) || (ldda & 3)) return (int)hipErrorInvalidValue;
   const int rpb = rows_per_block_for(M);
   const int nblk = seg_cdiv(M, rpb);
-  hipLaunchKernelGGL(chan_partial_kernel<1>, dim3(nblk), dim3(256), 0, stream, y, ldy, da, ldda, (int)M, C, scale,
+  hipLaunchKernelGGL((chan_partial_kernel<1, float>), dim3(nblk), dim3(256), 0, stream, y, ldy, da, ldda, (int)M, C, scale,
                      shift, mean, act, work, rpb, SegBnBwd{});
   hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(C), dim3(256), 0, stream, work, nblk, M, C, gamma,
                      invstd, dgamma, dbeta, coef);
@@ -441,22 +494,31 @@ SEG_API int seg_colsum_bnb(const float* da, long ldda, const float* y, long ldy,
   if ((C & 3) || (ldy & 3) || (ldda & 3) || !k) return (int)hipErrorInvalidValue;
   const int rpb = rows_per_block_for(M);
   const int nblk = seg_cdiv(M, rpb);
-  hipLaunchKernelGGL(chan_partial_kernel<3>, dim3(nblk), dim3(256), 0, stream, y, ldy, da, ldda, (int)M, C, nullptr,
+  hipLaunchKernelGGL((chan_partial_kernel<3, float>), dim3(nblk), dim3(256), 0, stream, y, ldy, da, ldda, (int)M, C, nullptr,
                      nullptr, nullptr, 0, work, rpb, SegBnBwd{y, ldy, scale, shift, mean, k, C, bn_act});
   hipLaunchKernelGGL(colsum_finalize_kernel, dim3(C), dim3(256), 0, stream, work, nblk, C, C, out, accumulate);
   SEG_RET_LAST();
 }
 
 // out[c] (+)= sum_r y[r][c]  -- conv bias gradient.  `work` >= seg_chan_workspace_floats.
-SEG_API int seg_colsum(const float* y, long ldy, long M, int C, float* work, float* out, int accumulate,
+template <typename T>
+static int colsum_impl(const T* y, long ldy, long M, int C, float* work, float* out, int accumulate,
                        hipStream_t stream) {
   if ((ldy & 3)) return (int)hipErrorInvalidValue;
   const int C4 = (C + 3) & ~3;  // ld >= C4 is guaranteed by the buffer contract
   const int rpb = rows_per_block_for(M);
   const int nblk = seg_cdiv(M, rpb);
-  hipLaunchKernelGGL(chan_partial_kernel<2>, dim3(nblk), dim3(256), 0, stream, y, ldy, nullptr, 0L, (int)M, C4,
-                     nullptr, nullptr, nullptr, 0, work, rpb, SegBnBwd{});
+  hipLaunchKernelGGL((chan_partial_kernel<2, T>), dim3(nblk), dim3(256), 0, stream, y, ldy, (const T*)nullptr, 0L,
+                     (int)M, C4, nullptr, nullptr, nullptr, 0, work, rpb, SegBnBwd{});
   hipLaunchKernelGGL(colsum_finalize_kernel, dim3(C), dim3(256), 0, stream, work, nblk, C, C4, out,
                      accumulate);
   SEG_RET_LAST();
+}
+SEG_API int seg_colsum(const float* y, long ldy, long M, int C, float* work, float* out, int accumulate,
+                       hipStream_t stream) {
+  return colsum_impl(y, ldy, M, C, work, out, accumulate, stream);
+}
+SEG_API int seg_colsum_bf16io(const __bf16* y, long ldy, long M, int C, float* work, float* out, int accumulate,
+                              hipStream_t stream) {
+  return colsum_impl(y, ldy, M, C, work, out, accumulate, stream);
 }

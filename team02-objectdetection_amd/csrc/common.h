@@ -51,6 +51,14 @@ __device__ __forceinline__ float seg_act_mask(float z, int act) {
 
 __device__ __forceinline__ f32x4 ld4(const float* p) { return *reinterpret_cast<const f32x4*>(p); }
 __device__ __forceinline__ void st4(float* p, f32x4 v) { *reinterpret_cast<f32x4*>(p) = v; }
+// bf16 activation storage (the `_bf16io` entry points): 4 channels = one 8-byte access,
+// widened to / rounded (RNE) from fp32 -- every kernel computes in fp32 either way.
+__device__ __forceinline__ f32x4 ld4(const __bf16* p) {
+  return __builtin_convertvector(*reinterpret_cast<const bf16x4*>(p), f32x4);
+}
+__device__ __forceinline__ void st4(__bf16* p, f32x4 v) {
+  *reinterpret_cast<bf16x4*>(p) = __builtin_convertvector(v, bf16x4);
+}
 
 // BatchNorm affine + activation of 4 channels: act(y * scale + shift).  The one
 // definition used by the BN apply pass and by every consumer that applies it

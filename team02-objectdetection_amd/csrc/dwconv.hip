@@ -46,15 +46,15 @@ __global__ void pack_dw_kernel(const float* __restrict__ w, float* __restrict__ 
 // Loads are unconditional (row and column clamped into the image, the value then
 // masked) so the compiler can issue a whole strip's loads back to back instead of
 // one branch-guarded, latency-exposed load at a time.
-template <bool LAZY>
+template <bool LAZY, typename T = float>
 struct RowIn {
-  const float* p;  // base of an in-image row (clamped) + channel offset
+  const T* p;      // base of an in-image row (clamped) + channel offset
   long ld;
   int W;
   bool ok;         // the requested row is inside the image
   f32x4 sc, sh;
   int act;
-  __device__ __forceinline__ void init(const float* base, int h, int H, int W_, long ld_) {
+  __device__ __forceinline__ void init(const T* base, int h, int H, int W_, long ld_) {
     ok = (unsigned)h < (unsigned)H;
     const int hc = h < 0 ? 0 : (h >= H ? H - 1 : h);
     p = base + (long)hc * W_ * ld_;
@@ -73,8 +73,8 @@ struct RowIn {
 // Store a strip's TW results (after all of its loads were issued: no store sits
 // between two loads, so the scheduler can batch the strip's loads).  CHECK: the
 // strip crosses the row end (only the last strip of a row when TW does not divide it).
-template <bool ACC>
-__device__ __forceinline__ void store_strip(float* o, long ld, const f32x4 (&acc)[TW], int n_valid) {
+template <bool ACC, typename T>
+__device__ __forceinline__ void store_strip(T* o, long ld, const f32x4 (&acc)[TW], int n_valid) {
 #pragma unroll
   for (int t = 0; t < TW; ++t) {
     if (t < n_valid) {
@@ -90,11 +90,11 @@ __device__ __forceinline__ void store_strip(float* o, long ld, const f32x4 (&acc
 // of dY with the flipped kernel.  ACC: out += (the data gradient's accumulate).
 // EPI (inference, BN folded into wk): out = act(acc + obias) -- the folded
 // BatchNorm shift and the ReLU6 applied in the epilogue.
-template <int S, bool LAZY, bool FLIP, bool ACC, bool EPI = false>
-__global__ __launch_bounds__(256) void dw_fwd_kernel(const float* __restrict__ in, long ldin, int N, int H, int W,
+template <int S, bool LAZY, bool FLIP, bool ACC, bool EPI = false, typename T = float>
+__global__ __launch_bounds__(256) void dw_fwd_kernel(const T* __restrict__ in, long ldin, int N, int H, int W,
                                                      int C, const float* __restrict__ isc,
                                                      const float* __restrict__ ish, int iact,
-                                                     const float* __restrict__ wk, float* __restrict__ out,
+                                                     const float* __restrict__ wk, T* __restrict__ out,
                                                      long ldout, int Ho, int Wo,
                                                      const float* __restrict__ obias, int oact) {
   const int CG = C >> 2;
@@ -112,7 +112,7 @@ __global__ __launch_bounds__(256) void dw_fwd_kernel(const float* __restrict__ i
     f32x4 w[9];
 #pragma unroll
     for (int t = 0; t < 9; ++t) w[t] = ld4(wk + (FLIP ? 8 - t : t) * C + c);
-    RowIn<LAZY> r[3];
+    RowIn<LAZY, T> r[3];
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
       r[k].init(in + (long)n * H * W * ldin + c, ho * S - 1 + k, H, W, ldin);
@@ -168,9 +168,10 @@ __global__ __launch_bounds__(256) void dw_fwd_kernel(const float* __restrict__ i
 //   dX[2j]   = sum_rows w[ky][1] dY[.][j]
 //   dX[2j+1] = sum_rows w[ky][0] dY[.][j+1] + w[ky][2] dY[.][j]
 // A thread owns TW dX columns (TW/2 pairs); dY column j+1 slides to the next pair.
-__global__ __launch_bounds__(256) void dw_dgrad_s2_kernel(const float* __restrict__ dy, long lddy, int N, int Ho,
+template <typename T>
+__global__ __launch_bounds__(256) void dw_dgrad_s2_kernel(const T* __restrict__ dy, long lddy, int N, int Ho,
                                                           int Wo, int C, const float* __restrict__ wk,
-                                                          float* __restrict__ dx, long lddx, int H, int W,
+                                                          T* __restrict__ dx, long lddx, int H, int W,
                                                           int accumulate) {
   const int CG = C >> 2;
   const int SPR = (W + TW - 1) / TW;
@@ -185,8 +186,8 @@ __global__ __launch_bounds__(256) void dw_dgrad_s2_kernel(const float* __restric
     const bool odd = hq & 1;
     // row slots: slot 0 = (even: ky 1, ho hq/2 | odd: ky 0, ho (hq+1)/2), slot 1 = (odd: ky 2, ho (hq-1)/2)
     const int ky0 = odd ? 0 : 1, ho0 = odd ? (hq + 1) >> 1 : hq >> 1, ho1 = (hq - 1) >> 1;
-    RowIn<false> r[2];
-    const float* img = dy + (long)n * Ho * Wo * lddy + c;
+    RowIn<false, T> r[2];
+    const T* img = dy + (long)n * Ho * Wo * lddy + c;
     r[0].init(img, ho0, Ho, Wo, lddy);
     r[1].init(img, odd ? ho1 : -1, Ho, Wo, lddy);
     f32x4 w[2][3];
@@ -214,7 +215,7 @@ __global__ __launch_bounds__(256) void dw_dgrad_s2_kernel(const float* __restric
       acc[2 * t] = e;
       acc[2 * t + 1] = f;
     }
-    float* o = dx + (row * W + ws) * lddx + c;
+    T* o = dx + (row * W + ws) * lddx + c;
     if (accumulate)
       store_strip<true>(o, lddx, acc, W - ws);
     else
@@ -226,9 +227,9 @@ __global__ __launch_bounds__(256) void dw_dgrad_s2_kernel(const float* __restric
 // dY[p][c] * X[src(p, tap)][c].  Block = RG row groups x TC channel groups; a
 // thread slides along its strips keeping 9 float4 accumulators, then a fixed-
 // order LDS tree reduction over the row groups (deterministic).
-template <int S, bool LAZY>
-__global__ __launch_bounds__(256) void dw_wgrad_kernel(const float* __restrict__ dy, long lddy,
-                                                       const float* __restrict__ x, long ldx, int N, int H, int W,
+template <int S, bool LAZY, typename T = float>
+__global__ __launch_bounds__(256) void dw_wgrad_kernel(const T* __restrict__ dy, long lddy,
+                                                       const T* __restrict__ x, long ldx, int N, int H, int W,
                                                        int C, const float* __restrict__ isc,
                                                        const float* __restrict__ ish, int iact, int Ho, int Wo,
                                                        int TC, int gy, int strips_per_block,
@@ -260,7 +261,7 @@ __global__ __launch_bounds__(256) void dw_wgrad_kernel(const float* __restrict__
       const long row = st / SPR;
       const int ws = (int)(st - row * SPR) * TWW;
       const int n = (int)(row / Ho), ho = (int)(row - (long)n * Ho);
-      RowIn<LAZY> r[3];
+      RowIn<LAZY, T> r[3];
 #pragma unroll
       for (int k = 0; k < 3; ++k) {
         r[k].init(x + (long)n * H * W * ldx + c, ho * S - 1 + k, H, W, ldx);
@@ -268,7 +269,7 @@ __global__ __launch_bounds__(256) void dw_wgrad_kernel(const float* __restrict__
         r[k].sh = sh;
         r[k].act = iact;
       }
-      const float* g = dy + (row * Wo + ws) * lddy + c;
+      const T* g = dy + (row * Wo + ws) * lddy + c;
       f32x4 a[3], b[3];
 #pragma unroll
       for (int k = 0; k < 3; ++k) {
@@ -354,15 +355,16 @@ SEG_API int seg_pack_dw_weight(const float* w, float* wk, int C, hipStream_t str
   SEG_RET_LAST();
 }
 
-SEG_API int seg_dw_fwd(const float* in, long ldin, int N, int H, int W, int C, const float* in_scale,
-                       const float* in_shift, int in_act, const float* wk, float* out, long ldout, int Ho, int Wo,
+template <typename T>
+static int dw_fwd_impl(const T* in, long ldin, int N, int H, int W, int C, const float* in_scale,
+                       const float* in_shift, int in_act, const float* wk, T* out, long ldout, int Ho, int Wo,
                        int stride, hipStream_t stream) {
   if ((C & 3) || (ldin & 3) || (ldout & 3) || (stride != 1 && stride != 2) || ((in_scale == nullptr) != (in_shift == nullptr)))
     return (int)hipErrorInvalidValue;
   const int grid = item_grid((long)N * Ho * ((Wo + TW - 1) / TW) * (C / 4));
   const bool lazy = in_scale != nullptr;
 #define SEG_DW_FWD(S, L)                                                                                         \
-  hipLaunchKernelGGL((dw_fwd_kernel<S, L, false, false>), dim3(grid), dim3(256), 0, stream, in, ldin, N, H, W, C, \
+  hipLaunchKernelGGL((dw_fwd_kernel<S, L, false, false, false, T>), dim3(grid), dim3(256), 0, stream, in, ldin, N, H, W, C, \
                      in_scale, in_shift, in_act, wk, out, ldout, Ho, Wo, nullptr, 0)
   if (stride == 1) {
     if (lazy) SEG_DW_FWD(1, true); else SEG_DW_FWD(1, false);
@@ -371,6 +373,16 @@ SEG_API int seg_dw_fwd(const float* in, long ldin, int N, int H, int W, int C, c
   }
 #undef SEG_DW_FWD
   SEG_RET_LAST();
+}
+SEG_API int seg_dw_fwd(const float* in, long ldin, int N, int H, int W, int C, const float* in_scale,
+                       const float* in_shift, int in_act, const float* wk, float* out, long ldout, int Ho, int Wo,
+                       int stride, hipStream_t stream) {
+  return dw_fwd_impl(in, ldin, N, H, W, C, in_scale, in_shift, in_act, wk, out, ldout, Ho, Wo, stride, stream);
+}
+SEG_API int seg_dw_fwd_bf16io(const __bf16* in, long ldin, int N, int H, int W, int C, const float* in_scale,
+                              const float* in_shift, int in_act, const float* wk, __bf16* out, long ldout, int Ho,
+                              int Wo, int stride, hipStream_t stream) {
+  return dw_fwd_impl(in, ldin, N, H, W, C, in_scale, in_shift, in_act, wk, out, ldout, Ho, Wo, stride, stream);
 }
 
 // Inference depthwise conv with the BatchNorm folded into wk (seg_bn_fold):
@@ -390,24 +402,33 @@ SEG_API int seg_dw_fwd_bias_act(const float* in, long ldin, int N, int H, int W,
   SEG_RET_LAST();
 }
 
-SEG_API int seg_dw_dgrad(const float* dy, long lddy, int N, int Ho, int Wo, int C, const float* wk, float* dx,
+template <typename T>
+static int dw_dgrad_impl(const T* dy, long lddy, int N, int Ho, int Wo, int C, const float* wk, T* dx,
                          long lddx, int H, int W, int stride, int accumulate, hipStream_t stream) {
   if ((C & 3) || (lddy & 3) || (lddx & 3) || (stride != 1 && stride != 2)) return (int)hipErrorInvalidValue;
   if (stride == 1) {
     if (H != Ho || W != Wo) return (int)hipErrorInvalidValue;
     const int grid = item_grid((long)N * H * ((W + TW - 1) / TW) * (C / 4));
     if (accumulate)
-      hipLaunchKernelGGL((dw_fwd_kernel<1, false, true, true>), dim3(grid), dim3(256), 0, stream, dy, lddy, N, Ho, Wo,
+      hipLaunchKernelGGL((dw_fwd_kernel<1, false, true, true, false, T>), dim3(grid), dim3(256), 0, stream, dy, lddy, N, Ho, Wo,
                          C, nullptr, nullptr, 0, wk, dx, lddx, H, W, nullptr, 0);
     else
-      hipLaunchKernelGGL((dw_fwd_kernel<1, false, true, false>), dim3(grid), dim3(256), 0, stream, dy, lddy, N, Ho,
+      hipLaunchKernelGGL((dw_fwd_kernel<1, false, true, false, false, T>), dim3(grid), dim3(256), 0, stream, dy, lddy, N, Ho,
                          Wo, C, nullptr, nullptr, 0, wk, dx, lddx, H, W, nullptr, 0);
   } else {
     const int grid = item_grid((long)N * H * ((W + TW - 1) / TW) * (C / 4));
-    hipLaunchKernelGGL(dw_dgrad_s2_kernel, dim3(grid), dim3(256), 0, stream, dy, lddy, N, Ho, Wo, C, wk, dx, lddx,
+    hipLaunchKernelGGL(dw_dgrad_s2_kernel<T>, dim3(grid), dim3(256), 0, stream, dy, lddy, N, Ho, Wo, C, wk, dx, lddx,
                        H, W, accumulate);
   }
   SEG_RET_LAST();
+}
+SEG_API int seg_dw_dgrad(const float* dy, long lddy, int N, int Ho, int Wo, int C, const float* wk, float* dx,
+                         long lddx, int H, int W, int stride, int accumulate, hipStream_t stream) {
+  return dw_dgrad_impl(dy, lddy, N, Ho, Wo, C, wk, dx, lddx, H, W, stride, accumulate, stream);
+}
+SEG_API int seg_dw_dgrad_bf16io(const __bf16* dy, long lddy, int N, int Ho, int Wo, int C, const float* wk, __bf16* dx,
+                                long lddx, int H, int W, int stride, int accumulate, hipStream_t stream) {
+  return dw_dgrad_impl(dy, lddy, N, Ho, Wo, C, wk, dx, lddx, H, W, stride, accumulate, stream);
 }
 
 SEG_API long seg_dw_wgrad_blocks(int N, int Ho, int Wo, int C) {
@@ -419,7 +440,8 @@ SEG_API long seg_dw_wgrad_blocks(int N, int Ho, int Wo, int C) {
 
 // part must hold seg_dw_wgrad_blocks(N, Ho, Wo, C) * 9 * C floats; reduce with
 // seg_conv_wgrad_reduce(part, blocks, dw, C, 1, 3, /*mode*/1, ...).
-SEG_API int seg_dw_wgrad(const float* dy, long lddy, const float* x, long ldx, int N, int H, int W, int C,
+template <typename T>
+static int dw_wgrad_impl(const T* dy, long lddy, const T* x, long ldx, int N, int H, int W, int C,
                          const float* in_scale, const float* in_shift, int in_act, int Ho, int Wo, int stride,
                          float* part, hipStream_t stream) {
   if ((C & 3) || (lddy & 3) || (ldx & 3) || (stride != 1 && stride != 2) || ((in_scale == nullptr) != (in_shift == nullptr)))
@@ -431,7 +453,7 @@ SEG_API int seg_dw_wgrad(const float* dy, long lddy, const float* x, long ldx, i
   const size_t lds = (size_t)(256 / TC) * TC * 9 * sizeof(f32x4);
   const bool lazy = in_scale != nullptr;
 #define SEG_DW_WG(S, L)                                                                                         \
-  hipLaunchKernelGGL((dw_wgrad_kernel<S, L>), dim3(gx * gy), dim3(256), lds, stream, dy, lddy, x, ldx, N, H, W, C, \
+  hipLaunchKernelGGL((dw_wgrad_kernel<S, L, T>), dim3(gx * gy), dim3(256), lds, stream, dy, lddy, x, ldx, N, H, W, C, \
                      in_scale, in_shift, in_act, Ho, Wo, TC, gy, spb, part)
   if (stride == 1) {
     if (lazy) SEG_DW_WG(1, true); else SEG_DW_WG(1, false);
@@ -440,4 +462,14 @@ SEG_API int seg_dw_wgrad(const float* dy, long lddy, const float* x, long ldx, i
   }
 #undef SEG_DW_WG
   SEG_RET_LAST();
+}
+SEG_API int seg_dw_wgrad(const float* dy, long lddy, const float* x, long ldx, int N, int H, int W, int C,
+                         const float* in_scale, const float* in_shift, int in_act, int Ho, int Wo, int stride,
+                         float* part, hipStream_t stream) {
+  return dw_wgrad_impl(dy, lddy, x, ldx, N, H, W, C, in_scale, in_shift, in_act, Ho, Wo, stride, part, stream);
+}
+SEG_API int seg_dw_wgrad_bf16io(const __bf16* dy, long lddy, const __bf16* x, long ldx, int N, int H, int W, int C,
+                                const float* in_scale, const float* in_shift, int in_act, int Ho, int Wo, int stride,
+                                float* part, hipStream_t stream) {
+  return dw_wgrad_impl(dy, lddy, x, ldx, N, H, W, C, in_scale, in_shift, in_act, Ho, Wo, stride, part, stream);
 }

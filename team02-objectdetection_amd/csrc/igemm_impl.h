@@ -20,11 +20,11 @@ namespace {
 __device__ __attribute__((aligned(16))) float g_zero4[4];
 
 struct IgemmArgs {
-  const float* in; long ldin;
+  const void* in; long ldin;     // IT (activation storage type: float, or __bf16 for the _bf16io path)
   const float* wk; int ldk;      // packed weights [Cout][ldk], k contiguous
   const float* bias;             // [Cout] or nullptr
-  const float* add; long ldadd;  // optional addend [M][ldadd] (may alias out)
-  float* out; long ldout;
+  const void* add; long ldadd;   // optional addend [M][ldadd] (may alias out), IT
+  void* out; long ldout;         // IT
   float* stat;                   // optional BN partials [tilesM][2][Cout]: tile sum and M2 of `out`
   int N, H, W, Cin;
   int Ho, Wo, Cout;
@@ -72,8 +72,14 @@ struct IgemmArgs {
 // accumulation, 8x the K per instruction).  The 16-bit LDS rows keep the same 80-byte
 // pitch at BK 32, so the ds_read_b128 fragment reads (lane half h: k = 16ks + 8h .. +7)
 // stay conflict-free; the epilogue (bias, BN statistics, addend) is the fp32 one.
-template <int BM, int BN, int WM, int WN, int KS, int BK, bool UT, bool BNB = false, typename OT = float>
+// IT = activation storage type of in / add / out (float, or __bf16: the bf16io path).
+template <int BM, int BN, int WM, int WN, int KS, int BK, bool UT, bool BNB = false, typename OT = float,
+          typename IT = float>
 __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void igemm_conv_kernel(IgemmArgs a) {
+  const IT* __restrict__ in = static_cast<const IT*>(a.in);
+  const IT* add = static_cast<const IT*>(a.add);
+  IT* out = static_cast<IT*>(a.out);
+  const IT* zero4 = reinterpret_cast<const IT*>(g_zero4);
   constexpr int NT = 64 * (BM / WM) * (BN / WN);  // threads: one wave per WM x WN sub-tile (4 or 8 waves)
   constexpr bool LP = sizeof(OT) == 2;       // 16-bit operands
   constexpr int LDSR = LP ? BK + 8 : BK + 4;  // LDS row stride (elements): conflict-free b128 reads
@@ -209,7 +215,7 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void igemm_conv_kernel(
 #pragma unroll
       for (int i = 0; i < A_PER; ++i) {
         const bool ok = (u_mask[i] >> tap) & 1u;
-        ra[i] = ld4(ok ? a.in + u_aoff[i] + off : g_zero4);
+        ra[i] = ld4(ok ? in + u_aoff[i] + off : zero4);
       }
       if (BNB) {
         const long offy = (wrap ? u_ytoff1 : u_ytoff0) + (wrap ? ci - a.Cin : ci);
@@ -244,11 +250,11 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void igemm_conv_kernel(
       f32x4 v = {0.f, 0.f, 0.f, 0.f};
       if (a_ok[i] && a_k[i] < a.K) {
         if (KS == 1) {
-          v = ld4(a.in + a_base[i] + a_k[i]);
+          v = ld4(in + a_base[i] + a_k[i]);
         } else {
           const int hi = a_hi0[i] + a_ky[i], wi = a_wi0[i] + a_kx[i];
           if ((unsigned)hi < (unsigned)a.H && (unsigned)wi < (unsigned)a.W)
-            v = ld4(a.in + (a_base[i] + (long)hi * a.W + wi) * a.ldin + a_ci[i]);
+            v = ld4(in + (a_base[i] + (long)hi * a.W + wi) * a.ldin + a_ci[i]);
         }
       }
       ra[i] = v;
@@ -489,9 +495,9 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void igemm_conv_kernel(
         const int row = m0 + wm0 + mi * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
         if (row < a.M) {
           float v = acc[mi][ni][r];
-          if (a.add) v += a.add[(long)row * a.ldadd + col];
+          if (add) v += (float)add[(long)row * a.ldadd + col];
           if (a.act) v = seg_act(v, a.act);
-          a.out[(long)row * a.ldout + col] = v;
+          out[(long)row * a.ldout + col] = static_cast<IT>(v);
           if (red) {
             const float yv = a.red.y[(long)row * a.red.ldy + col];
             const float dz = v * seg_act_mask(yv * rsc + rsh, a.red.act);
@@ -531,14 +537,14 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void igemm_conv_kernel(
   }
 }
 
-template <int BM, int BN, int WM, int WN, int BK, typename OT>
+template <int BM, int BN, int WM, int WN, int BK, typename OT, typename IT>
 int launch_igemm_bk(const IgemmArgs& a, int ks, hipStream_t s) {
   const int grid = seg_cdiv(a.M, BM) * seg_cdiv(a.Cout, BN);
   const int splits = seg_cdiv(a.K, a.kchunk);
   const bool ut = SEG_IGEMM_UT && (SEG_IGEMM_UT2 ? a.Cin >= BK : a.Cin % BK == 0);
   constexpr int NT = 64 * (BM / WM) * (BN / WN);
-#define SEG_IG(KS, U) hipLaunchKernelGGL((igemm_conv_kernel<BM, BN, WM, WN, KS, BK, U, false, OT>), dim3(grid, splits), dim3(NT), 0, s, a)
-#define SEG_IGB(KS) hipLaunchKernelGGL((igemm_conv_kernel<BM, BN, WM, WN, KS, BK, true, true, OT>), dim3(grid, splits), dim3(NT), 0, s, a)
+#define SEG_IG(KS, U) hipLaunchKernelGGL((igemm_conv_kernel<BM, BN, WM, WN, KS, BK, U, false, OT, IT>), dim3(grid, splits), dim3(NT), 0, s, a)
+#define SEG_IGB(KS) hipLaunchKernelGGL((igemm_conv_kernel<BM, BN, WM, WN, KS, BK, true, true, OT, IT>), dim3(grid, splits), dim3(NT), 0, s, a)
   if (a.bnb.y) {
     if (!ut) return (int)hipErrorInvalidValue;
     if (ks == 1) SEG_IGB(1); else SEG_IGB(3);
@@ -560,13 +566,13 @@ int launch_igemm_bk(const IgemmArgs& a, int ks, hipStream_t s) {
 inline int igemm_bk(int K) { return (SEG_IGEMM_BK != 16 && (K <= 64 || (K % SEG_IGEMM_BK != 0 && K < 512))) ? 16 : SEG_IGEMM_BK; }
 
 // split-K: `splits` K ranges of whole BK chunks (a.part set by the caller when splits > 1)
-template <int BM, int BN, int WM, int WN, typename OT = float>
+template <int BM, int BN, int WM, int WN, typename OT = float, typename IT = float>
 int launch_igemm(IgemmArgs a, int ks, int splits, hipStream_t s) {
   const int bk = igemm_bk(a.K);
   const int nk = seg_cdiv(a.K, bk);
   a.kchunk = seg_cdiv(nk, splits) * bk;
-  if (bk == 16) return launch_igemm_bk<BM, BN, WM, WN, 16, OT>(a, ks, s);
-  return launch_igemm_bk<BM, BN, WM, WN, SEG_IGEMM_BK, OT>(a, ks, s);
+  if (bk == 16) return launch_igemm_bk<BM, BN, WM, WN, 16, OT, IT>(a, ks, s);
+  return launch_igemm_bk<BM, BN, WM, WN, SEG_IGEMM_BK, OT, IT>(a, ks, s);
 }
 
 struct TileCfg {
@@ -639,11 +645,12 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restr
   }
 }
 
-template <typename OT>
-int conv_igemm_impl(const float* in, long ldin, int N, int H, int W, int Cin, const float* wk, int ldk,
-                    const float* bias, float* out, long ldout, int Ho, int Wo, int Cout, int ks, int stride, int pad,
-                    const float* add, long ldadd, float* stat, int act, float* work, int splits, hipStream_t stream,
+template <typename OT, typename IT = float>
+int conv_igemm_impl(const IT* in, long ldin, int N, int H, int W, int Cin, const float* wk, int ldk,
+                    const float* bias, IT* out, long ldout, int Ho, int Wo, int Cout, int ks, int stride, int pad,
+                    const IT* add, long ldadd, float* stat, int act, float* work, int splits, hipStream_t stream,
                     const SegBnRed* red = nullptr) {
+  if (!std::is_same<IT, float>::value && (splits != 1 || red)) return (int)hipErrorInvalidValue;
   if (red && (splits != 1 || stat || act || !red->y || !red->scale || !red->shift || !red->mean))
     return (int)hipErrorInvalidValue;
   if ((Cin & 3) || (ldin & 3) || (ldk & 3) || (ks != 1 && ks != 3)) return (int)hipErrorInvalidValue;
@@ -661,26 +668,27 @@ int conv_igemm_impl(const float* in, long ldin, int N, int H, int W, int Cin, co
   if (a.M == 0 || Cout == 0) return 0;
   int rc;
   switch (pick_tile(a.M, Cout)) {
-    case 0: rc = launch_igemm<128, 128, 64, 64, OT>(a, ks, splits, stream); break;
-    case 1: rc = launch_igemm<64, 128, 32, 64, OT>(a, ks, splits, stream); break;
-    case 2: rc = launch_igemm<128, 64, 64, 32, OT>(a, ks, splits, stream); break;
-    case 3: rc = launch_igemm<64, 64, 32, 32, OT>(a, ks, splits, stream); break;
-    case 4: rc = launch_igemm<128, 96, 32, 96, OT>(a, ks, splits, stream); break;
-    case 5: rc = launch_igemm<128, 160, 32, 160, OT>(a, ks, splits, stream); break;
-    case 6: rc = launch_igemm<256, 32, 64, 32, OT>(a, ks, splits, stream); break;
-    case 7: rc = launch_igemm<128, 32, 32, 32, OT>(a, ks, splits, stream); break;
-    case 8: rc = launch_igemm<128, 128, 64, 32, OT>(a, ks, splits, stream); break;
-    case 9: rc = launch_igemm<128, 128, 32, 64, OT>(a, ks, splits, stream); break;
-    case 10: rc = launch_igemm<256, 128, 64, 64, OT>(a, ks, splits, stream); break;
-    case 11: rc = launch_igemm<128, 256, 64, 64, OT>(a, ks, splits, stream); break;
-    case 12: rc = launch_igemm<128, 64, 32, 32, OT>(a, ks, splits, stream); break;
-    case 13: rc = launch_igemm<256, 64, 64, 32, OT>(a, ks, splits, stream); break;
-    default: rc = launch_igemm<64, 128, 32, 32, OT>(a, ks, splits, stream); break;
+    case 0: rc = launch_igemm<128, 128, 64, 64, OT, IT>(a, ks, splits, stream); break;
+    case 1: rc = launch_igemm<64, 128, 32, 64, OT, IT>(a, ks, splits, stream); break;
+    case 2: rc = launch_igemm<128, 64, 64, 32, OT, IT>(a, ks, splits, stream); break;
+    case 3: rc = launch_igemm<64, 64, 32, 32, OT, IT>(a, ks, splits, stream); break;
+    case 4: rc = launch_igemm<128, 96, 32, 96, OT, IT>(a, ks, splits, stream); break;
+    case 5: rc = launch_igemm<128, 160, 32, 160, OT, IT>(a, ks, splits, stream); break;
+    case 6: rc = launch_igemm<256, 32, 64, 32, OT, IT>(a, ks, splits, stream); break;
+    case 7: rc = launch_igemm<128, 32, 32, 32, OT, IT>(a, ks, splits, stream); break;
+    case 8: rc = launch_igemm<128, 128, 64, 32, OT, IT>(a, ks, splits, stream); break;
+    case 9: rc = launch_igemm<128, 128, 32, 64, OT, IT>(a, ks, splits, stream); break;
+    case 10: rc = launch_igemm<256, 128, 64, 64, OT, IT>(a, ks, splits, stream); break;
+    case 11: rc = launch_igemm<128, 256, 64, 64, OT, IT>(a, ks, splits, stream); break;
+    case 12: rc = launch_igemm<128, 64, 32, 32, OT, IT>(a, ks, splits, stream); break;
+    case 13: rc = launch_igemm<256, 64, 64, 32, OT, IT>(a, ks, splits, stream); break;
+    default: rc = launch_igemm<64, 128, 32, 32, OT, IT>(a, ks, splits, stream); break;
   }
   if (rc || splits == 1) return rc;
   const long total = (long)a.M * Cout;
   hipLaunchKernelGGL(splitk_reduce_kernel, dim3((int)std::min<long>(seg_cdiv(total, 256), 4096)), dim3(256), 0,
-                     stream, work, splits, (long)a.M, Cout, bias, add, ldadd, out, ldout, act);
+                     stream, work, splits, (long)a.M, Cout, bias, reinterpret_cast<const float*>(add), ldadd,
+                     reinterpret_cast<float*>(out), ldout, act);
   SEG_RET_LAST();
 }
 

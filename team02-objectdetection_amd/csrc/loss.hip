@@ -35,15 +35,15 @@ constexpr int CMAX = 32;
 
 // Recompute the CP (= round4(C)) full-res logits of pixel (n, r, s); the class
 // loops are unrolled over CP so z stays in registers with constant indices.
-template <int CP>
-__device__ __forceinline__ void full_res_logits(const float* __restrict__ low, long ld, int H, int W, int n, int r,
+template <int CP, typename T>
+__device__ __forceinline__ void full_res_logits(const T* __restrict__ low, long ld, int H, int W, int n, int r,
                                                 int s, float sh, float sw, float (&z)[CP]) {
   const LinAC lh = lin_ac(r, H, sh), lw = lin_ac(s, W, sw);
-  const float* base = low + (long)n * H * W * ld;
-  const float* p00 = base + ((long)lh.i0 * W + lw.i0) * ld;
-  const float* p01 = base + ((long)lh.i0 * W + lw.i1) * ld;
-  const float* p10 = base + ((long)lh.i1 * W + lw.i0) * ld;
-  const float* p11 = base + ((long)lh.i1 * W + lw.i1) * ld;
+  const T* base = low + (long)n * H * W * ld;
+  const T* p00 = base + ((long)lh.i0 * W + lw.i0) * ld;
+  const T* p01 = base + ((long)lh.i0 * W + lw.i1) * ld;
+  const T* p10 = base + ((long)lh.i1 * W + lw.i0) * ld;
+  const T* p11 = base + ((long)lh.i1 * W + lw.i1) * ld;
 #pragma unroll
   for (int c = 0; c < CP; c += 4) {
     const f32x4 o = lh.l0 * (lw.l0 * ld4(p00 + c) + lw.l1 * ld4(p01 + c)) +
@@ -72,8 +72,8 @@ __device__ __forceinline__ void softmax_stats(float (&z)[CP], int C, int y, floa
   }
 }
 
-template <int CP>
-__global__ __launch_bounds__(256) void ce_up_loss_kernel(const float* __restrict__ low, long ld, int N, int H, int W,
+template <int CP, typename T>
+__global__ __launch_bounds__(256) void ce_up_loss_kernel(const T* __restrict__ low, long ld, int N, int H, int W,
                                                          int C, const long long* __restrict__ labels, int Ho, int Wo,
                                                          float sh, float sw, int ignore_index,
                                                          float* __restrict__ part) {
@@ -87,7 +87,7 @@ __global__ __launch_bounds__(256) void ce_up_loss_kernel(const float* __restrict
     const int rem = (int)(p - (long)n * Ho * Wo);
     const int r = rem / Wo, s = rem - r * Wo;
     float z[CP];
-    full_res_logits<CP>(low, ld, H, W, n, r, s, sh, sw, z);
+    full_res_logits<CP, T>(low, ld, H, W, n, r, s, sh, sw, z);
     float m, se, zy;
     softmax_stats<CP>(z, C, (int)y, m, se, zy, false);
     lsum += m + logf(se) - zy;
@@ -122,17 +122,17 @@ __global__ void ce_finalize_kernel(const float* __restrict__ part, int nblk, flo
 }
 
 // dhigh[p][c] = g * (softmax(z_p)[c] - [c == y_p]) / count, NHWC (ld >= round4(C)).
-template <int CP>
-__global__ __launch_bounds__(256) void ce_up_grad_kernel(const float* __restrict__ low, long ld, int N, int H, int W,
+template <int CP, typename T>
+__global__ __launch_bounds__(256) void ce_up_grad_kernel(const T* __restrict__ low, long ld, int N, int H, int W,
                                                          int C, const long long* __restrict__ labels, int Ho, int Wo,
                                                          float sh, float sw, int ignore_index,
                                                          const float* __restrict__ gout, const float* __restrict__ stats,
-                                                         float* __restrict__ dhigh, long ldh) {
+                                                         T* __restrict__ dhigh, long ldh) {
   const long total = (long)N * Ho * Wo;
   const float scale = gout[0] / stats[1];
   for (long p = blockIdx.x * (long)blockDim.x + threadIdx.x; p < total; p += (long)gridDim.x * blockDim.x) {
     const long long y = labels[p];
-    float* d = dhigh + p * ldh;
+    T* d = dhigh + p * ldh;
     if (y == ignore_index) {
 #pragma unroll
       for (int c = 0; c < CP; c += 4) st4(d + c, f32x4{0.f, 0.f, 0.f, 0.f});
@@ -142,7 +142,7 @@ __global__ __launch_bounds__(256) void ce_up_grad_kernel(const float* __restrict
     const int rem = (int)(p - (long)n * Ho * Wo);
     const int r = rem / Wo, s = rem - r * Wo;
     float z[CP];
-    full_res_logits<CP>(low, ld, H, W, n, r, s, sh, sw, z);
+    full_res_logits<CP, T>(low, ld, H, W, n, r, s, sh, sw, z);
     float m, se, zy;
     softmax_stats<CP>(z, C, (int)y, m, se, zy, true);
     const float inv = 1.f / se;
@@ -167,8 +167,9 @@ SEG_API long seg_ce_workspace_floats(long pixels) { return 2L * loss_blocks(pixe
 
 // Mean CE of bilinear_ac_true_x(Ho,Wo)(low) against labels.  out2[0] = loss,
 // out2[1] = number of non-ignored pixels.  `work` >= seg_ce_workspace_floats(N*Ho*Wo).
-SEG_API int seg_ce_upsample_loss(const float* low, long ld, int N, int H, int W, int C, const long long* labels, int Ho,
-                                 int Wo, int ignore_index, float* work, float* out2, hipStream_t stream) {
+template <typename T>
+static int ce_loss_impl(const T* low, long ld, int N, int H, int W, int C, const long long* labels, int Ho, int Wo,
+                        int ignore_index, float* work, float* out2, hipStream_t stream) {
   if ((ld & 3) || C > CMAX || C < 1) return (int)hipErrorInvalidValue;
   const long total = (long)N * Ho * Wo;
   const int nb = loss_blocks(total);
@@ -176,8 +177,8 @@ SEG_API int seg_ce_upsample_loss(const float* low, long ld, int N, int H, int W,
   const float sw = Wo > 1 ? (float)(W - 1) / (float)(Wo - 1) : 0.f;
 #define SEG_CE_L(CP)                                                                                          \
   case CP:                                                                                                    \
-    hipLaunchKernelGGL(ce_up_loss_kernel<CP>, dim3(nb), dim3(256), 0, stream, low, ld, N, H, W, C, labels, Ho, Wo, \
-                       sh, sw, ignore_index, work);                                                          \
+    hipLaunchKernelGGL((ce_up_loss_kernel<CP, T>), dim3(nb), dim3(256), 0, stream, low, ld, N, H, W, C, labels, Ho, \
+                       Wo, sh, sw, ignore_index, work);                                                      \
     break
   switch ((C + 3) & ~3) {
     SEG_CE_L(4); SEG_CE_L(8); SEG_CE_L(12); SEG_CE_L(16); SEG_CE_L(20); SEG_CE_L(24); SEG_CE_L(28); SEG_CE_L(32);
@@ -186,12 +187,22 @@ SEG_API int seg_ce_upsample_loss(const float* low, long ld, int N, int H, int W,
   hipLaunchKernelGGL(ce_finalize_kernel, dim3(1), dim3(64), 0, stream, work, nb, out2);
   SEG_RET_LAST();
 }
+SEG_API int seg_ce_upsample_loss(const float* low, long ld, int N, int H, int W, int C, const long long* labels, int Ho,
+                                 int Wo, int ignore_index, float* work, float* out2, hipStream_t stream) {
+  return ce_loss_impl(low, ld, N, H, W, C, labels, Ho, Wo, ignore_index, work, out2, stream);
+}
+SEG_API int seg_ce_upsample_loss_bf16io(const __bf16* low, long ld, int N, int H, int W, int C,
+                                        const long long* labels, int Ho, int Wo, int ignore_index, float* work,
+                                        float* out2, hipStream_t stream) {
+  return ce_loss_impl(low, ld, N, H, W, C, labels, Ho, Wo, ignore_index, work, out2, stream);
+}
 
 // Full-resolution logit gradient (NHWC, ldh >= round4(C)); follow with
 // seg_upsample_bwd(nchw_grad = 0, ac = 1) to reach the low-res logits.
-SEG_API int seg_ce_upsample_grad(const float* low, long ld, int N, int H, int W, int C, const long long* labels, int Ho,
-                                 int Wo, int ignore_index, const float* grad_out, const float* stats, float* dhigh,
-                                 long ldh, hipStream_t stream) {
+template <typename T>
+static int ce_grad_impl(const T* low, long ld, int N, int H, int W, int C, const long long* labels, int Ho, int Wo,
+                        int ignore_index, const float* grad_out, const float* stats, T* dhigh, long ldh,
+                        hipStream_t stream) {
   if ((ld & 3) || (ldh & 3) || C > CMAX || C < 1) return (int)hipErrorInvalidValue;
   const long total = (long)N * Ho * Wo;
   const float sh = Ho > 1 ? (float)(H - 1) / (float)(Ho - 1) : 0.f;
@@ -199,12 +210,23 @@ SEG_API int seg_ce_upsample_grad(const float* low, long ld, int N, int H, int W,
   const int grid = (int)std::min<long>(seg_cdiv(total, 256), 8192);
 #define SEG_CE_G(CP)                                                                                            \
   case CP:                                                                                                      \
-    hipLaunchKernelGGL(ce_up_grad_kernel<CP>, dim3(grid), dim3(256), 0, stream, low, ld, N, H, W, C, labels, Ho, Wo, \
-                       sh, sw, ignore_index, grad_out, stats, dhigh, ldh);                                     \
+    hipLaunchKernelGGL((ce_up_grad_kernel<CP, T>), dim3(grid), dim3(256), 0, stream, low, ld, N, H, W, C, labels, Ho, \
+                       Wo, sh, sw, ignore_index, grad_out, stats, dhigh, ldh);                                 \
     break
   switch ((C + 3) & ~3) {
     SEG_CE_G(4); SEG_CE_G(8); SEG_CE_G(12); SEG_CE_G(16); SEG_CE_G(20); SEG_CE_G(24); SEG_CE_G(28); SEG_CE_G(32);
   }
 #undef SEG_CE_G
   SEG_RET_LAST();
+}
+SEG_API int seg_ce_upsample_grad(const float* low, long ld, int N, int H, int W, int C, const long long* labels, int Ho,
+                                 int Wo, int ignore_index, const float* grad_out, const float* stats, float* dhigh,
+                                 long ldh, hipStream_t stream) {
+  return ce_grad_impl(low, ld, N, H, W, C, labels, Ho, Wo, ignore_index, grad_out, stats, dhigh, ldh, stream);
+}
+SEG_API int seg_ce_upsample_grad_bf16io(const __bf16* low, long ld, int N, int H, int W, int C,
+                                        const long long* labels, int Ho, int Wo, int ignore_index,
+                                        const float* grad_out, const float* stats, __bf16* dhigh, long ldh,
+                                        hipStream_t stream) {
+  return ce_grad_impl(low, ld, N, H, W, C, labels, Ho, Wo, ignore_index, grad_out, stats, dhigh, ldh, stream);
 }

@@ -36,8 +36,9 @@ __device__ __forceinline__ void dst_range(int i, int in, int out, float scale, i
   *hi = h > out - 1 ? out - 1 : h;
 }
 
-__global__ void up_fwd_nhwc_kernel(const float* __restrict__ in, long ldin, int N, int H, int W, int C,
-                                   float* __restrict__ out, long ldout, int Ho, int Wo, float sh, float sw, int ac) {
+template <typename T>
+__global__ void up_fwd_nhwc_kernel(const T* __restrict__ in, long ldin, int N, int H, int W, int C,
+                                   T* __restrict__ out, long ldout, int Ho, int Wo, float sh, float sw, int ac) {
   const int CG = C >> 2;
   const long total = (long)N * Ho * Wo * CG;
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
@@ -47,7 +48,7 @@ __global__ void up_fwd_nhwc_kernel(const float* __restrict__ in, long ldin, int 
     const int rem = (int)(p - (long)n * Ho * Wo);
     const int r = rem / Wo, s = rem - r * Wo;
     const Lin lh = lin_index(r, H, sh, ac), lw = lin_index(s, W, sw, ac);
-    const float* base = in + (long)n * H * W * ldin;
+    const T* base = in + (long)n * H * W * ldin;
     const f32x4 v00 = ld4(base + ((long)lh.i0 * W + lw.i0) * ldin + c);
     const f32x4 v01 = ld4(base + ((long)lh.i0 * W + lw.i1) * ldin + c);
     const f32x4 v10 = ld4(base + ((long)lh.i1 * W + lw.i0) * ldin + c);
@@ -64,9 +65,9 @@ __global__ void up_fwd_nhwc_kernel(const float* __restrict__ in, long ldin, int 
 // the inner loop is loads and FMAs only.
 constexpr int SMAX = 12;
 
-template <int LAYOUT>
-__global__ void up_bwd_kernel(const float* __restrict__ dout, long ldout, int N, int Ho, int Wo, int C,
-                              float* __restrict__ din, long ldin, int H, int W, float sh, float sw, int ac,
+template <int LAYOUT, typename TI = float, typename TO = float>
+__global__ void up_bwd_kernel(const TI* __restrict__ dout, long ldout, int N, int Ho, int Wo, int C,
+                              TO* __restrict__ din, long ldin, int H, int W, float sh, float sw, int ac,
                               int accumulate) {
   const int CG = (C + 3) >> 2;
   const long total = (long)N * H * W * CG;
@@ -86,7 +87,7 @@ __global__ void up_bwd_kernel(const float* __restrict__ dout, long ldout, int N,
       } else {
 #pragma unroll
         for (int j = 0; j < 4; ++j)
-          if (c + j < C) acc[j] += wt * dout[(((long)n * C + c + j) * Ho + r) * Wo + s];
+          if (c + j < C) acc[j] += wt * (float)dout[(((long)n * C + c + j) * Ho + r) * Wo + s];
       }
     };
     if (shi - slo + 1 <= SMAX) {
@@ -110,7 +111,7 @@ __global__ void up_bwd_kernel(const float* __restrict__ dout, long ldout, int N,
         }
       }
     }
-    float* dst = din + q * ldin + c;
+    TO* dst = din + q * ldin + c;
     if (accumulate) acc += ld4(dst);
     st4(dst, acc);
   }
@@ -120,8 +121,9 @@ __global__ void up_bwd_kernel(const float* __restrict__ dout, long ldout, int N,
 // sample input row h are 2h-1 .. 2h+2 with weights 0.25, 0.75, 0.75, 0.25 (the
 // values lin_index produces; at the borders the clamped taps fold into 1.0), so
 // the gather is 16 loads with constant weights and no index search.
-__global__ __launch_bounds__(256) void up2_bwd_kernel(const float* __restrict__ dout, long ldout, int N, int C,
-                                                      float* __restrict__ din, long ldin, int H, int W,
+template <typename T>
+__global__ __launch_bounds__(256) void up2_bwd_kernel(const T* __restrict__ dout, long ldout, int N, int C,
+                                                      T* __restrict__ din, long ldin, int H, int W,
                                                       int accumulate) {
   const int CG = C >> 2, Ho = 2 * H, Wo = 2 * W;
   const long total = (long)N * H * W * CG;
@@ -134,7 +136,7 @@ __global__ __launch_bounds__(256) void up2_bwd_kernel(const float* __restrict__ 
     const float wr[4] = {h > 0 ? 0.25f : 0.f, h > 0 ? 0.75f : 1.f, h < H - 1 ? 0.75f : 1.f, h < H - 1 ? 0.25f : 0.f};
     const float wc[4] = {w > 0 ? 0.25f : 0.f, w > 0 ? 0.75f : 1.f, w < W - 1 ? 0.75f : 1.f, w < W - 1 ? 0.25f : 0.f};
     f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-    const float* base = dout + (long)n * Ho * Wo * ldout + c;
+    const T* base = dout + (long)n * Ho * Wo * ldout + c;
 #pragma unroll
     for (int a = 0; a < 4; ++a) {
       const int r = 2 * h - 1 + a;
@@ -148,14 +150,15 @@ __global__ __launch_bounds__(256) void up2_bwd_kernel(const float* __restrict__ 
       }
       acc += wr[a] * row;
     }
-    float* dst = din + q * ldin + c;
+    T* dst = din + q * ldin + c;
     if (accumulate) acc += ld4(dst);
     st4(dst, acc);
   }
 }
 
 // NHWC low-res -> NCHW full-res (the model's returned logits).
-__global__ void up_fwd_to_nchw_kernel(const float* __restrict__ in, long ldin, int N, int H, int W, int C,
+template <typename T>
+__global__ void up_fwd_to_nchw_kernel(const T* __restrict__ in, long ldin, int N, int H, int W, int C,
                                       float* __restrict__ out, int Ho, int Wo, float sh, float sw, int ac) {
   const long total = (long)N * Ho * Wo;
   for (long p = blockIdx.x * (long)blockDim.x + threadIdx.x; p < total; p += (long)gridDim.x * blockDim.x) {
@@ -163,7 +166,7 @@ __global__ void up_fwd_to_nchw_kernel(const float* __restrict__ in, long ldin, i
     const int rem = (int)(p - (long)n * Ho * Wo);
     const int r = rem / Wo, s = rem - r * Wo;
     const Lin lh = lin_index(r, H, sh, ac), lw = lin_index(s, W, sw, ac);
-    const float* base = in + (long)n * H * W * ldin;
+    const T* base = in + (long)n * H * W * ldin;
     for (int c = 0; c < C; c += 4) {
       const f32x4 v00 = ld4(base + ((long)lh.i0 * W + lw.i0) * ldin + c);
       const f32x4 v01 = ld4(base + ((long)lh.i0 * W + lw.i1) * ldin + c);
@@ -189,8 +192,9 @@ __device__ __forceinline__ int pool_argmax(float v0, float v1, float v2, float v
   return arg;
 }
 
-__global__ void maxpool_fwd_kernel(const float* __restrict__ in, long ldin, int N, int H, int W, int C,
-                                   float* __restrict__ out, long ldout) {
+template <typename T>
+__global__ void maxpool_fwd_kernel(const T* __restrict__ in, long ldin, int N, int H, int W, int C,
+                                   T* __restrict__ out, long ldout) {
   const int Ho = H / 2, Wo = W / 2, CG = C >> 2;
   const long total = (long)N * Ho * Wo * CG;
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
@@ -199,7 +203,7 @@ __global__ void maxpool_fwd_kernel(const float* __restrict__ in, long ldin, int 
     const int n = (int)(p / ((long)Ho * Wo));
     const int rem = (int)(p - (long)n * Ho * Wo);
     const int r = rem / Wo, s = rem - r * Wo;
-    const float* b = in + (((long)n * H + 2 * r) * W + 2 * s) * ldin + c;
+    const T* b = in + (((long)n * H + 2 * r) * W + 2 * s) * ldin + c;
     const f32x4 a0 = ld4(b), a1 = ld4(b + ldin), a2 = ld4(b + (long)W * ldin), a3 = ld4(b + (long)W * ldin + ldin);
     f32x4 o;
 #pragma unroll
@@ -212,8 +216,9 @@ __global__ void maxpool_fwd_kernel(const float* __restrict__ in, long ldin, int 
   }
 }
 
-__global__ void maxpool_bwd_kernel(const float* __restrict__ in, long ldin, const float* __restrict__ dout,
-                                   long lddout, int N, int H, int W, int C, float* __restrict__ din, long lddin,
+template <typename T>
+__global__ void maxpool_bwd_kernel(const T* __restrict__ in, long ldin, const T* __restrict__ dout,
+                                   long lddout, int N, int H, int W, int C, T* __restrict__ din, long lddin,
                                    int accumulate) {
   const int Ho = H / 2, Wo = W / 2, CG = C >> 2;
   const long total = (long)N * Ho * Wo * CG;
@@ -243,7 +248,8 @@ __global__ void maxpool_bwd_kernel(const float* __restrict__ in, long ldin, cons
 }
 
 // NCHW image batch -> NHWC rows of ld channels, channels [C, ld) zero-filled.
-__global__ void nchw_to_nhwc_kernel(const float* __restrict__ x, int N, int C, int H, int W, float* __restrict__ out,
+template <typename T>
+__global__ void nchw_to_nhwc_kernel(const float* __restrict__ x, int N, int C, int H, int W, T* __restrict__ out,
                                     int ld) {
   const long plane = (long)H * W;
   const long total = (long)N * plane;
@@ -269,64 +275,121 @@ float up_scale(int in, int out, int ac) {
 }  // namespace
 
 // Bilinear resize NHWC -> NHWC (strided), ac = align_corners.
+template <typename T>
+static int upsample_fwd_impl(const T* in, long ldin, int N, int H, int W, int C, T* out, long ldout, int Ho, int Wo,
+                             int ac, hipStream_t stream) {
+  if ((C & 3) || (ldin & 3) || (ldout & 3)) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(up_fwd_nhwc_kernel<T>, dim3(ew_grid((long)N * Ho * Wo * (C / 4))), dim3(256), 0, stream, in, ldin,
+                     N, H, W, C, out, ldout, Ho, Wo, up_scale(H, Ho, ac), up_scale(W, Wo, ac), ac);
+  SEG_RET_LAST();
+}
 SEG_API int seg_upsample_fwd(const float* in, long ldin, int N, int H, int W, int C, float* out, long ldout, int Ho,
                              int Wo, int ac, hipStream_t stream) {
-  if ((C & 3) || (ldin & 3) || (ldout & 3)) return (int)hipErrorInvalidValue;
-  hipLaunchKernelGGL(up_fwd_nhwc_kernel, dim3(ew_grid((long)N * Ho * Wo * (C / 4))), dim3(256), 0, stream, in, ldin, N,
-                     H, W, C, out, ldout, Ho, Wo, up_scale(H, Ho, ac), up_scale(W, Wo, ac), ac);
-  SEG_RET_LAST();
+  return upsample_fwd_impl(in, ldin, N, H, W, C, out, ldout, Ho, Wo, ac, stream);
+}
+SEG_API int seg_upsample_fwd_bf16io(const __bf16* in, long ldin, int N, int H, int W, int C, __bf16* out, long ldout,
+                                    int Ho, int Wo, int ac, hipStream_t stream) {
+  return upsample_fwd_impl(in, ldin, N, H, W, C, out, ldout, Ho, Wo, ac, stream);
 }
 
 // Gradient of seg_upsample_fwd / seg_upsample_to_nchw.  nchw_grad = 1 when d_out is
-// the NCHW gradient of the model's returned logits.  d_in is NHWC (ldin >= round4(C)).
-SEG_API int seg_upsample_bwd(const float* dout, long ldout, int nchw_grad, int N, int Ho, int Wo, int C, float* din,
+// the NCHW gradient of the model's returned logits (always fp32).  d_in is NHWC
+// (ldin >= round4(C)).
+template <typename T>
+static int upsample_bwd_impl(const void* dout, long ldout, int nchw_grad, int N, int Ho, int Wo, int C, T* din,
                              long ldin, int H, int W, int ac, int accumulate, hipStream_t stream) {
   if ((ldin & 3) || (!nchw_grad && (ldout & 3))) return (int)hipErrorInvalidValue;
   const int grid = ew_grid((long)N * H * W * ((C + 3) / 4));
   const float sh = up_scale(H, Ho, ac), sw = up_scale(W, Wo, ac);
+  const T* dn = static_cast<const T*>(dout);
   if (!nchw_grad && !ac && Ho == 2 * H && Wo == 2 * W && !(C & 3)) {
-    hipLaunchKernelGGL(up2_bwd_kernel, dim3(grid), dim3(256), 0, stream, dout, ldout, N, C, din, ldin, H, W,
+    hipLaunchKernelGGL(up2_bwd_kernel<T>, dim3(grid), dim3(256), 0, stream, dn, ldout, N, C, din, ldin, H, W,
                        accumulate);
     SEG_RET_LAST();
   }
   if (nchw_grad)
-    hipLaunchKernelGGL(up_bwd_kernel<1>, dim3(grid), dim3(256), 0, stream, dout, ldout, N, Ho, Wo, C, din, ldin, H, W,
-                       sh, sw, ac, accumulate);
+    hipLaunchKernelGGL((up_bwd_kernel<1, float, T>), dim3(grid), dim3(256), 0, stream,
+                       static_cast<const float*>(dout), ldout, N, Ho, Wo, C, din, ldin, H, W, sh, sw, ac, accumulate);
   else
-    hipLaunchKernelGGL(up_bwd_kernel<0>, dim3(grid), dim3(256), 0, stream, dout, ldout, N, Ho, Wo, C, din, ldin, H, W,
-                       sh, sw, ac, accumulate);
+    hipLaunchKernelGGL((up_bwd_kernel<0, T, T>), dim3(grid), dim3(256), 0, stream, dn, ldout, N, Ho, Wo, C, din, ldin,
+                       H, W, sh, sw, ac, accumulate);
   SEG_RET_LAST();
 }
+SEG_API int seg_upsample_bwd(const float* dout, long ldout, int nchw_grad, int N, int Ho, int Wo, int C, float* din,
+                             long ldin, int H, int W, int ac, int accumulate, hipStream_t stream) {
+  return upsample_bwd_impl(dout, ldout, nchw_grad, N, Ho, Wo, C, din, ldin, H, W, ac, accumulate, stream);
+}
+// dout: bf16 NHWC, or fp32 NCHW when nchw_grad = 1.
+SEG_API int seg_upsample_bwd_bf16io(const void* dout, long ldout, int nchw_grad, int N, int Ho, int Wo, int C,
+                                    __bf16* din, long ldin, int H, int W, int ac, int accumulate, hipStream_t stream) {
+  return upsample_bwd_impl(dout, ldout, nchw_grad, N, Ho, Wo, C, din, ldin, H, W, ac, accumulate, stream);
+}
 
+template <typename T>
+static int upsample_to_nchw_impl(const T* in, long ldin, int N, int H, int W, int C, float* out, int Ho, int Wo, int ac,
+                                 hipStream_t stream) {
+  if (ldin & 3) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(up_fwd_to_nchw_kernel<T>, dim3(ew_grid((long)N * Ho * Wo)), dim3(256), 0, stream, in, ldin, N, H,
+                     W, C, out, Ho, Wo, up_scale(H, Ho, ac), up_scale(W, Wo, ac), ac);
+  SEG_RET_LAST();
+}
 SEG_API int seg_upsample_to_nchw(const float* in, long ldin, int N, int H, int W, int C, float* out, int Ho, int Wo,
                                  int ac, hipStream_t stream) {
-  if (ldin & 3) return (int)hipErrorInvalidValue;
-  hipLaunchKernelGGL(up_fwd_to_nchw_kernel, dim3(ew_grid((long)N * Ho * Wo)), dim3(256), 0, stream, in, ldin, N, H, W,
-                     C, out, Ho, Wo, up_scale(H, Ho, ac), up_scale(W, Wo, ac), ac);
-  SEG_RET_LAST();
+  return upsample_to_nchw_impl(in, ldin, N, H, W, C, out, Ho, Wo, ac, stream);
+}
+SEG_API int seg_upsample_to_nchw_bf16io(const __bf16* in, long ldin, int N, int H, int W, int C, float* out, int Ho,
+                                        int Wo, int ac, hipStream_t stream) {
+  return upsample_to_nchw_impl(in, ldin, N, H, W, C, out, Ho, Wo, ac, stream);
 }
 
 // The model input (NCHW float, as the reference's DataLoader delivers it) as NHWC
 // rows padded to `ld` channels -- lets the Cin = 3 first conv run on the MFMA
 // implicit-GEMM path (K = 9 taps x 4 channels, the 4th weight channel packed 0).
-SEG_API int seg_nchw_to_nhwc(const float* x, int N, int C, int H, int W, float* out, int ld, hipStream_t stream) {
+template <typename T>
+static int nchw_to_nhwc_impl(const float* x, int N, int C, int H, int W, T* out, int ld, hipStream_t stream) {
   if ((ld & 3) || ld < C) return (int)hipErrorInvalidValue;
-  hipLaunchKernelGGL(nchw_to_nhwc_kernel, dim3(ew_grid((long)N * H * W)), dim3(256), 0, stream, x, N, C, H, W, out, ld);
+  hipLaunchKernelGGL(nchw_to_nhwc_kernel<T>, dim3(ew_grid((long)N * H * W)), dim3(256), 0, stream, x, N, C, H, W, out,
+                     ld);
   SEG_RET_LAST();
 }
+SEG_API int seg_nchw_to_nhwc(const float* x, int N, int C, int H, int W, float* out, int ld, hipStream_t stream) {
+  return nchw_to_nhwc_impl(x, N, C, H, W, out, ld, stream);
+}
+SEG_API int seg_nchw_to_nhwc_bf16io(const float* x, int N, int C, int H, int W, __bf16* out, int ld,
+                                    hipStream_t stream) {
+  return nchw_to_nhwc_impl(x, N, C, H, W, out, ld, stream);
+}
 
-SEG_API int seg_maxpool2_fwd(const float* in, long ldin, int N, int H, int W, int C, float* out, long ldout,
+template <typename T>
+static int maxpool2_fwd_impl(const T* in, long ldin, int N, int H, int W, int C, T* out, long ldout,
                              hipStream_t stream) {
   if ((C & 3) || (ldin & 3) || (ldout & 3)) return (int)hipErrorInvalidValue;
-  hipLaunchKernelGGL(maxpool_fwd_kernel, dim3(ew_grid((long)N * (H / 2) * (W / 2) * (C / 4))), dim3(256), 0, stream,
+  hipLaunchKernelGGL(maxpool_fwd_kernel<T>, dim3(ew_grid((long)N * (H / 2) * (W / 2) * (C / 4))), dim3(256), 0, stream,
                      in, ldin, N, H, W, C, out, ldout);
   SEG_RET_LAST();
 }
+SEG_API int seg_maxpool2_fwd(const float* in, long ldin, int N, int H, int W, int C, float* out, long ldout,
+                             hipStream_t stream) {
+  return maxpool2_fwd_impl(in, ldin, N, H, W, C, out, ldout, stream);
+}
+SEG_API int seg_maxpool2_fwd_bf16io(const __bf16* in, long ldin, int N, int H, int W, int C, __bf16* out, long ldout,
+                                    hipStream_t stream) {
+  return maxpool2_fwd_impl(in, ldin, N, H, W, C, out, ldout, stream);
+}
 
-SEG_API int seg_maxpool2_bwd(const float* in, long ldin, const float* dout, long lddout, int N, int H, int W, int C,
-                             float* din, long lddin, int accumulate, hipStream_t stream) {
+template <typename T>
+static int maxpool2_bwd_impl(const T* in, long ldin, const T* dout, long lddout, int N, int H, int W, int C, T* din,
+                             long lddin, int accumulate, hipStream_t stream) {
   if ((C & 3) || (ldin & 3) || (lddout & 3) || (lddin & 3) || (H & 1) || (W & 1)) return (int)hipErrorInvalidValue;
-  hipLaunchKernelGGL(maxpool_bwd_kernel, dim3(ew_grid((long)N * (H / 2) * (W / 2) * (C / 4))), dim3(256), 0, stream,
+  hipLaunchKernelGGL(maxpool_bwd_kernel<T>, dim3(ew_grid((long)N * (H / 2) * (W / 2) * (C / 4))), dim3(256), 0, stream,
                      in, ldin, dout, lddout, N, H, W, C, din, lddin, accumulate);
   SEG_RET_LAST();
+}
+SEG_API int seg_maxpool2_bwd(const float* in, long ldin, const float* dout, long lddout, int N, int H, int W, int C,
+                             float* din, long lddin, int accumulate, hipStream_t stream) {
+  return maxpool2_bwd_impl(in, ldin, dout, lddout, N, H, W, C, din, lddin, accumulate, stream);
+}
+SEG_API int seg_maxpool2_bwd_bf16io(const __bf16* in, long ldin, const __bf16* dout, long lddout, int N, int H, int W,
+                                    int C, __bf16* din, long lddin, int accumulate, hipStream_t stream) {
+  return maxpool2_bwd_impl(in, ldin, dout, lddout, N, H, W, C, din, lddin, accumulate, stream);
 }

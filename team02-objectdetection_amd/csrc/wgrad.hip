@@ -25,8 +25,8 @@ namespace {
 constexpr int BK = SEG_WGRAD_BK;
 
 struct WgradArgs {
-  const float* dy; long lddy;
-  const float* x; long ldx;
+  const void* dy; long lddy;     // IT (float, or __bf16 for the _bf16io path)
+  const void* x; long ldx;       // IT
   float* part;
   int N, H, W, Cin, Ho, Wo, Cout, stride, pad;
   int M, Nw, kchunk;
@@ -42,8 +42,10 @@ constexpr int tr_pitch(int n) { return n % 128 == 32 || n % 128 == 96 ? n : tr_p
 // the MFMA fragment (lane: row r, k = 8h .. 8h+7) is gathered with two
 // ds_read_b64_tr_b16 (4 k-rows x 16 channels per 16-lane group, delivered
 // column-major) and fed to v_mfma_f32_32x32x16_bf16; fp32 accumulation and slabs.
-template <int BM, int BN, int WM, int WN, int KS, bool BNB = false, bool BF = false>
+template <int BM, int BN, int WM, int WN, int KS, bool BNB = false, bool BF = false, typename IT = float>
 __global__ __launch_bounds__(256) void wgrad_kernel(WgradArgs a) {
+  const IT* __restrict__ gdy = static_cast<const IT*>(a.dy);
+  const IT* __restrict__ gx = static_cast<const IT*>(a.x);
   constexpr int BK = BF ? 32 : ::BK;  // pixels per K chunk
   constexpr int AR = BF ? tr_pitch(BM) : BM + 4, BR = BF ? tr_pitch(BN) : BN + 4;
   constexpr int A_VEC = BK * BM / 4, B_VEC = BK * BN / 4;
@@ -113,7 +115,7 @@ __global__ __launch_bounds__(256) void wgrad_kernel(WgradArgs a) {
       const int p = k0 + prow;
       f32x4 v = {0.f, 0.f, 0.f, 0.f};
       const bool ok = idx < A_VEC && p < kend && c < a.Cout;
-      if (ok) v = ld4(a.dy + (long)p * a.lddy + c);
+      if (ok) v = ld4(gdy + (long)p * a.lddy + c);
       ra[i] = v;
       if (BNB) {
         f32x4 w = {0.f, 0.f, 0.f, 0.f};
@@ -128,12 +130,12 @@ __global__ __launch_bounds__(256) void wgrad_kernel(WgradArgs a) {
       f32x4 v = {0.f, 0.f, 0.f, 0.f};
       if (b_ok[i] && p < kend) {
         if (KS == 1) {
-          v = ld4(a.x + (long)p * a.ldx + b_ci[i]);
+          v = ld4(gx + (long)p * a.ldx + b_ci[i]);
         } else {
           const int hi = b_ho[i] * a.stride - a.pad + b_ky[i];
           const int wi = b_wo[i] * a.stride - a.pad + b_kx[i];
           if ((unsigned)hi < (unsigned)a.H && (unsigned)wi < (unsigned)a.W)
-            v = ld4(a.x + (((long)b_n[i] * a.H + hi) * a.W + wi) * a.ldx + b_ci[i]);
+            v = ld4(gx + (((long)b_n[i] * a.H + hi) * a.W + wi) * a.ldx + b_ci[i]);
         }
       }
       rb[i] = v;
@@ -258,13 +260,13 @@ __global__ __launch_bounds__(256) void wgrad_kernel(WgradArgs a) {
   }
 }
 
-template <int BM, int BN, int WM, int WN, bool BF = false>
+template <int BM, int BN, int WM, int WN, bool BF = false, typename IT = float>
 int launch_wgrad(const WgradArgs& a, int ks, int splits, hipStream_t s) {
   dim3 grid(seg_cdiv(a.Cout, BM) * seg_cdiv(a.Nw, BN) * splits);
   if (BF) {
     if (a.bnb.y) return (int)hipErrorInvalidValue;
-    if (ks == 1) hipLaunchKernelGGL((wgrad_kernel<BM, BN, WM, WN, 1, false, true>), grid, dim3(256), 0, s, a);
-    else hipLaunchKernelGGL((wgrad_kernel<BM, BN, WM, WN, 3, false, true>), grid, dim3(256), 0, s, a);
+    if (ks == 1) hipLaunchKernelGGL((wgrad_kernel<BM, BN, WM, WN, 1, false, true, IT>), grid, dim3(256), 0, s, a);
+    else hipLaunchKernelGGL((wgrad_kernel<BM, BN, WM, WN, 3, false, true, IT>), grid, dim3(256), 0, s, a);
     SEG_RET_LAST();
   }
   if (a.bnb.y) {
@@ -298,9 +300,9 @@ SEG_API int seg_conv_wgrad_splits(long M, int Cout, int Cin, int ks) {
 }
 
 // part[s][co][tap*Cin+ci] = sum over split s's pixels of dY[p][co] * X[src(p,tap)][ci].
-static int conv_wgrad(const float* dy, long lddy, const float* x, long ldx, int N, int H, int W, int Cin, int Ho,
+static int conv_wgrad(const void* dy, long lddy, const void* x, long ldx, int N, int H, int W, int Cin, int Ho,
                       int Wo, int Cout, int ks, int stride, int pad, float* part, int splits, const SegBnBwd& bnb,
-                      hipStream_t stream, bool bf = false);
+                      hipStream_t stream, bool bf = false, bool bf_io = false);
 
 SEG_API int seg_conv_wgrad(const float* dy, long lddy, const float* x, long ldx,
                            int N, int H, int W, int Cin, int Ho, int Wo, int Cout,
@@ -317,6 +319,14 @@ SEG_API int seg_conv_wgrad_bf16(const float* dy, long lddy, const float* x, long
                     true);
 }
 
+// seg_conv_wgrad_bf16 on bf16 activation storage (dy, x __bf16; the _bf16io training path).
+SEG_API int seg_conv_wgrad_bf16io(const __bf16* dy, long lddy, const __bf16* x, long ldx,
+                                  int N, int H, int W, int Cin, int Ho, int Wo, int Cout,
+                                  int ks, int stride, int pad, float* part, int splits, hipStream_t stream) {
+  return conv_wgrad(dy, lddy, x, ldx, N, H, W, Cin, Ho, Wo, Cout, ks, stride, pad, part, splits, SegBnBwd{}, stream,
+                    true, true);
+}
+
 // seg_conv_wgrad of a conv whose output went through a train-mode BatchNorm, with the
 // BN backward applied on load: dy = dA, y / scale / shift / mean / k / bn_act as
 // seg_conv_igemm_bnb (Cout % 4 == 0).
@@ -329,9 +339,9 @@ SEG_API int seg_conv_wgrad_bnb(const float* dy, long lddy, const float* x, long 
                     SegBnBwd{y, ldy, scale, shift, mean, k, Cout, bn_act}, stream);
 }
 
-static int conv_wgrad(const float* dy, long lddy, const float* x, long ldx, int N, int H, int W, int Cin, int Ho,
+static int conv_wgrad(const void* dy, long lddy, const void* x, long ldx, int N, int H, int W, int Cin, int Ho,
                       int Wo, int Cout, int ks, int stride, int pad, float* part, int splits, const SegBnBwd& bnb,
-                      hipStream_t stream, bool bf) {
+                      hipStream_t stream, bool bf, bool bf_io) {
   if ((Cin & 3) || (ldx & 3) || (lddy & 3) || (ks != 1 && ks != 3) || splits < 1) return (int)hipErrorInvalidValue;
   if (ks == 1 && (stride != 1 || pad != 0)) return (int)hipErrorInvalidValue;
   WgradArgs a;
@@ -342,6 +352,14 @@ static int conv_wgrad(const float* dy, long lddy, const float* x, long ldx, int 
   a.bnb = bnb;
   int bm, bn;
   wgrad_tiles(Cout, a.Nw, &bm, &bn);
+  if (bf_io) {
+    a.kchunk = seg_cdiv(seg_cdiv(a.M, splits), 32) * 32;
+    if (bm == 128 && bn == 128) return launch_wgrad<128, 128, 64, 64, true, __bf16>(a, ks, splits, stream);
+    if (bm == 128) return launch_wgrad<128, 32, 32, 32, true, __bf16>(a, ks, splits, stream);
+    if (bm == 64 && bn == 128) return launch_wgrad<64, 128, 32, 64, true, __bf16>(a, ks, splits, stream);
+    if (bm == 64) return launch_wgrad<64, 64, 32, 32, true, __bf16>(a, ks, splits, stream);
+    return launch_wgrad<32, 128, 32, 32, true, __bf16>(a, ks, splits, stream);
+  }
   if (bf) {
     a.kchunk = seg_cdiv(seg_cdiv(a.M, splits), 32) * 32;
     if (bm == 128 && bn == 128) return launch_wgrad<128, 128, 64, 64, true>(a, ks, splits, stream);

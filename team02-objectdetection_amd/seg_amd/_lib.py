@@ -92,6 +92,13 @@ PROTOTYPES = {
     "seg_resize_u8": (_I, [_V, _I, _I, _I, _L, _V, _I, _I, _I, _V, _V]),
     "seg_augment": (_I, [_V, _V, _I, _I, _I, _V, _F, _F, _F, _F, _F, _F, _V, _V, _V]),
 }
+# bf16-storage variants: same C signature shape as their fp32 namesakes (pointers stay void*)
+for _n in ("seg_add", "seg_bn_stats", "seg_bn_apply", "seg_bn_backward", "seg_colsum", "seg_dw_fwd", "seg_dw_dgrad",
+           "seg_dw_wgrad", "seg_ce_upsample_loss", "seg_ce_upsample_grad", "seg_upsample_fwd", "seg_upsample_bwd",
+           "seg_upsample_to_nchw", "seg_nchw_to_nhwc", "seg_maxpool2_fwd", "seg_maxpool2_bwd"):
+    PROTOTYPES[_n + "_bf16io"] = PROTOTYPES[_n]
+PROTOTYPES["seg_conv_igemm_bf16io"] = PROTOTYPES["seg_conv_igemm"]
+PROTOTYPES["seg_conv_wgrad_bf16io"] = PROTOTYPES["seg_conv_wgrad"]
 
 _lock = threading.Lock()
 _lib = None

@@ -164,7 +164,7 @@ class ConvOp:
         bias = self.conv.bias.data_ptr() if self.conv.bias is not None else None
         if self.kind == "dw":
             i = self.inp
-            call("seg_dw_fwd", rt.ptr(i), i.ld, i.N, i.H, i.W, i.C, *self._in_xform(rt), self.wk_f.data_ptr(),
+            call(rt.k("seg_dw_fwd"), rt.ptr(i), i.ld, i.N, i.H, i.W, i.C, *self._in_xform(rt), self.wk_f.data_ptr(),
                  rt.ptr(y), y.ld, y.H, y.W, self.stride, s)
         else:
             i = self.inp
@@ -190,6 +190,10 @@ class ConvOp:
                 _timed_call("wino3_fwd", self.flops(), "seg_conv_wino", rt.ptr(i), i.ld, i.N, i.H, i.W, self.cin_pad,
                             self.wk_wf.data_ptr(), self.cin_pad, bias, rt.ptr(y), y.ld, self.cout, None, 0, statp,
                             work.data_ptr(), s)
+            elif rt.io:
+                _timed_call(f"igemm{self.ks}_fwd", self.flops(), "seg_conv_igemm_bf16io", rt.ptr(i), i.ld, i.N, i.H,
+                            i.W, self.cin_pad, wk_ptr, ldk, bias, rt.ptr(y), y.ld, y.H, y.W, self.cout, self.ks,
+                            self.stride, self.pad, None, 0, statp, s)
             elif self.bf:
                 _timed_call(f"igemm{self.ks}_fwd", self.flops(), "seg_conv_igemm_bf16", rt.ptr(i), i.ld, i.N, i.H,
                             i.W, self.cin_pad, wk_ptr, ldk, bias, rt.ptr(y), y.ld, y.H, y.W, self.cout, self.ks,
@@ -211,7 +215,7 @@ class ConvOp:
             nbt = bn.num_batches_tracked.data_ptr() if bn.track_running_stats else None
             if self.kind == "dw":
                 work = rt.tmp(query("seg_chan_workspace_floats", M, C))
-                call("seg_bn_stats", rt.ptr(y), y.ld, M, C, bn.weight.data_ptr(), bn.bias.data_ptr(), bn.eps,
+                call(rt.k("seg_bn_stats"), rt.ptr(y), y.ld, M, C, bn.weight.data_ptr(), bn.bias.data_ptr(), bn.eps,
                      bn.momentum, rm, rv, nbt, work.data_ptr(), mean.data_ptr(), invstd.data_ptr(),
                      scale.data_ptr(), shift.data_ptr(), s)
             else:
@@ -225,7 +229,7 @@ class ConvOp:
         if self.lazy:
             return
         o, r = self.out, self.res
-        call("seg_bn_apply", rt.ptr(y), y.ld, M, C, scale.data_ptr(), shift.data_ptr(), self.act,
+        call(rt.k("seg_bn_apply"), rt.ptr(y), y.ld, M, C, scale.data_ptr(), shift.data_ptr(), self.act,
              rt.ptr(r) if r is not None else None, r.ld if r is not None else 0, rt.ptr(o), o.ld, s)
 
     # -- inference (BatchNorm folded into the conv: Program.fold)
@@ -357,7 +361,7 @@ class ConvOp:
                      shift.data_ptr(), self.act, g_w, g_b, coef.data_ptr(), rt.ptr(dY), dY.ld, s)
             else:
                 work = rt.tmp(query("seg_chan_workspace_floats", M, C) + 3 * C)
-                call("seg_bn_backward", rt.gptr(dA), dA.ld, rt.ptr(y), y.ld, M, C, self.bn.weight.data_ptr(),
+                call(rt.k("seg_bn_backward"), rt.gptr(dA), dA.ld, rt.ptr(y), y.ld, M, C, self.bn.weight.data_ptr(),
                      mean.data_ptr(), invstd.data_ptr(), scale.data_ptr(), shift.data_ptr(), self.act,
                      g_w, g_b, work.data_ptr(), rt.ptr(dY), dY.ld, s)
             if self.res is not None:
@@ -385,14 +389,14 @@ class ConvOp:
         y, M = self.y, self.y.M
         if self.conv.bias is not None and self.conv.bias.requires_grad:
             work = rt.tmp(query("seg_chan_workspace_floats", M, r4(self.cout)))
-            call("seg_colsum", dYp, dY.ld, M, self.cout, work.data_ptr(), rt.grad_param(self.conv.bias), 0, s)
+            call(rt.k("seg_colsum"), dYp, dY.ld, M, self.cout, work.data_ptr(), rt.grad_param(self.conv.bias), 0, s)
         if self.conv.weight.requires_grad:
             gw = rt.grad_param(self.conv.weight)
             i = self.inp
             if self.kind == "dw":
                 nblk = query("seg_dw_wgrad_blocks", y.N, y.H, y.W, self.cout)
                 part = rt.tmp(nblk * 9 * self.cout)
-                call("seg_dw_wgrad", dYp, dY.ld, rt.ptr(i), i.ld, i.N, i.H, i.W, i.C, *self._in_xform(rt), y.H, y.W,
+                call(rt.k("seg_dw_wgrad"), dYp, dY.ld, rt.ptr(i), i.ld, i.N, i.H, i.W, i.C, *self._in_xform(rt), y.H, y.W,
                      self.stride, part.data_ptr(), s)
                 call("seg_conv_wgrad_reduce", part.data_ptr(), nblk, gw, self.cout, 1, 3, 1, 0, s)
             elif self.wino_w:
@@ -405,7 +409,7 @@ class ConvOp:
                 splits = query("seg_conv_wgrad_splits", M, self.cout, self.cin_pad, self.ks)
                 part = rt.tmp(splits * self.cout * self.ks * self.ks * self.cin_pad)
                 _timed_call(f"igemm{self.ks}_wgrad", self.flops(),
-                            "seg_conv_wgrad_bf16" if self.bf else "seg_conv_wgrad", dYp, dY.ld, rt.ptr(i), i.ld,
+                            rt.k("seg_conv_wgrad_bf16") if self.bf else "seg_conv_wgrad", dYp, dY.ld, rt.ptr(i), i.ld,
                             i.N, i.H, i.W, self.cin_pad, y.H, y.W, self.cout, self.ks, self.stride, self.pad,
                             part.data_ptr(), splits, s)
                 call("seg_conv_wgrad_reduce", part.data_ptr(), splits, gw, self.cout, self.cin, self.ks, 0, 0, s)
@@ -416,7 +420,7 @@ class ConvOp:
         y, i = self.y, self.inp
         if self.kind == "dw":
             acc = rt.begin_write_accumulate(i)
-            call("seg_dw_dgrad", dYp, dY.ld, y.N, y.H, y.W, self.cout, self.wk_f.data_ptr(), rt.gptr(i), i.ld, i.H,
+            call(rt.k("seg_dw_dgrad"), dYp, dY.ld, y.N, y.H, y.W, self.cout, self.wk_f.data_ptr(), rt.gptr(i), i.ld, i.H,
                  i.W, self.stride, acc, s)
         else:
             if self.stride != 1:
@@ -442,6 +446,10 @@ class ConvOp:
                             add_ptr, add_ld, rt.ptr(b.y), b.y.ld, st[2 * C:3 * C].data_ptr(),
                             st[3 * C:4 * C].data_ptr(), st[:C].data_ptr(), b.act, part.data_ptr(), s)
                 rt.bnred[id(b)] = (part, ntiles)
+            elif rt.io:
+                _timed_call(f"igemm{self.ks}_dgrad", self.flops(), "seg_conv_igemm_bf16io", dYp, dY.ld, y.N, y.H, y.W,
+                            kin, self.wk_d.data_ptr(), self.ldk_d, None, rt.gptr(i), i.ld, i.H, i.W, self.cin,
+                            self.ks, 1, self.pad, add_ptr, add_ld, None, s)
             elif self.bf:
                 _timed_call(f"igemm{self.ks}_dgrad", self.flops(), "seg_conv_igemm_bf16", dYp, dY.ld, y.N, y.H, y.W,
                             kin, self.wk_d.data_ptr(), self.ldk_d, None, rt.gptr(i), i.ld, i.H, i.W, self.cin,
@@ -464,13 +472,13 @@ class UpsampleOp:
 
     def forward(self, rt):
         l, o = self.low, self.out
-        call("seg_upsample_fwd", rt.ptr(l), l.ld, l.N, l.H, l.W, l.C, rt.ptr(o), o.ld, o.H, o.W, 0, rt.stream)
+        call(rt.k("seg_upsample_fwd"), rt.ptr(l), l.ld, l.N, l.H, l.W, l.C, rt.ptr(o), o.ld, o.H, o.W, 0, rt.stream)
 
     def backward(self, rt):
         l, o = self.low, self.out
         d = rt.grad_of(o)
         acc = rt.begin_write_accumulate(l)
-        call("seg_upsample_bwd", rt.gptr(d), d.ld, 0, o.N, o.H, o.W, o.C, rt.gptr(l), l.ld, l.H, l.W, 0, acc,
+        call(rt.k("seg_upsample_bwd"), rt.gptr(d), d.ld, 0, o.N, o.H, o.W, o.C, rt.gptr(l), l.ld, l.H, l.W, 0, acc,
              rt.stream)
         rt.mark_written(l)
 
@@ -486,13 +494,13 @@ class PoolOp:
 
     def forward(self, rt):
         i, o = self.inp, self.out
-        call("seg_maxpool2_fwd", rt.ptr(i), i.ld, i.N, i.H, i.W, i.C, rt.ptr(o), o.ld, rt.stream)
+        call(rt.k("seg_maxpool2_fwd"), rt.ptr(i), i.ld, i.N, i.H, i.W, i.C, rt.ptr(o), o.ld, rt.stream)
 
     def backward(self, rt):
         i, o = self.inp, self.out
         d = rt.grad_of(o)
         acc = rt.begin_write_accumulate(i)
-        call("seg_maxpool2_bwd", rt.ptr(i), i.ld, rt.gptr(d), d.ld, i.N, i.H, i.W, i.C, rt.gptr(i), i.ld, acc,
+        call(rt.k("seg_maxpool2_bwd"), rt.ptr(i), i.ld, rt.gptr(d), d.ld, i.N, i.H, i.W, i.C, rt.gptr(i), i.ld, acc,
              rt.stream)
         rt.mark_written(i)
 
@@ -570,7 +578,7 @@ class Program:
                 max_elems = max(max_elems, 9 * op.cout)
                 continue
             y = op.y
-            op.bf = self.math == "bf16"
+            op.bf = self.math in ("bf16", "bf16io")
             if op.bf:
                 # bf16 math: every dense / pointwise conv (fwd, dgrad, wgrad) on the bf16 implicit GEMM
                 op.pw_fused = op.bnb = False
@@ -653,7 +661,7 @@ class Program:
         for op in self.ops:
             if isinstance(op, ConvOp):
                 op.red_for = op.red_by = None
-        if not BN_RED:
+        if not BN_RED or self.math == "bf16io":
             return
         for k, b in enumerate(self.ops):
             if not isinstance(b, ConvOp) or b.bn is None or b.bnb or b.pw_fused or b.cout % 4:
@@ -871,7 +879,10 @@ def build_program(model, N, H, W, math="f32") -> Program:
 # forward) -- every dense / pointwise conv, forward and both gradients, multiplies
 # bf16-rounded operands on the bf16 MFMA with fp32 accumulation; activations, BN,
 # depthwise convs, the loss and the optimizer stay fp32.
-MATHS = ("f32", "bf16", "f16")
+MATHS = ("f32", "bf16", "bf16io", "f16")
+# "bf16io": bf16 conv math AND bf16 activation / gradient storage (every tensor between
+# kernels is bf16 in HBM, halving the memory-bound passes; BN statistics, partial sums,
+# parameter gradients, the loss and Adam stay fp32) -- the _bf16io entry points.
 # "f16" is the fp16 inference configuration (BASELINE configs[3]): the BN-folded eval
 # forward (Predictor) with fp16 conv operands; training programs refuse it.
 _FOLDED_CONV = {"f32": "seg_conv_igemm_act", "bf16": "seg_conv_igemm_bf16", "f16": "seg_conv_igemm_f16"}
@@ -896,7 +907,11 @@ class Run:
         self.prog, self.image, self.training = prog, image, training
         self.device = image.device
         self.stream = torch.cuda.current_stream(self.device).cuda_stream
-        self.bufs = {n: torch.empty(rows * ld, device=self.device, dtype=torch.float32)
+        # activation / gradient storage: fp32, or bf16 for math "bf16io" (the _bf16io kernels)
+        self.io = prog.math == "bf16io"
+        self.store = torch.bfloat16 if self.io else torch.float32
+        self.es = 2 if self.io else 4
+        self.bufs = {n: torch.empty(rows * ld, device=self.device, dtype=self.store)
                      for n, (rows, ld) in prog.bufs.items()}
         self.saved = {}
         self.gbufs = {}
@@ -908,16 +923,20 @@ class Run:
         self.side = None      # side stream of the parameter gradients (backward only)
         self.bnred = {}       # id(BN op) -> (tile partials, ntiles) from a fused data gradient
 
+    def k(self, name: str) -> str:
+        """C-ABI entry point of an activation kernel for this run's storage type."""
+        return name + "_bf16io" if self.io else name
+
     # pointers
     def ptr(self, a: Act) -> int:
         if a.buf.startswith("#"):
-            return self.gbufs[a.buf].data_ptr() + 4 * a.off
-        return self.bufs[a.buf].data_ptr() + 4 * a.off
+            return self.gbufs[a.buf].data_ptr() + self.es * a.off
+        return self.bufs[a.buf].data_ptr() + self.es * a.off
 
     def gptr(self, a: Act) -> int:
         if a.buf.startswith("#"):
-            return self.gbufs[a.buf].data_ptr() + 4 * a.off
-        return self.gbuf(a.buf).data_ptr() + 4 * a.off
+            return self.gbufs[a.buf].data_ptr() + self.es * a.off
+        return self.gbuf(a.buf).data_ptr() + self.es * a.off
 
     def gbuf(self, name):
         g = self.gbufs.get(name)
@@ -941,7 +960,7 @@ class Run:
     def tmp_buf(self, n: int) -> str:
         name = f"#tmp{self._tmp_n}"
         self._tmp_n += 1
-        self.gbufs[name] = self.tmp(n)
+        self.gbufs[name] = torch.empty(max(int(n), 1), device=self.device, dtype=self.store)
         return name
 
     # streams
@@ -977,7 +996,7 @@ class Run:
             add = self.pending.pop(a.key(), None)
             v = self.gbuf(a.buf).view(-1, a.ld)[:, a.off:a.off + a.C]
             if add is not None:
-                call("seg_add", self.gptr(add), add.ld, None, 0, a.M, a.C, self.gptr(a), a.ld, self.stream)
+                call(self.k("seg_add"), self.gptr(add), add.ld, None, 0, a.M, a.C, self.gptr(a), a.ld, self.stream)
             else:
                 v.zero_()
             self.mark_written(a)
@@ -985,7 +1004,7 @@ class Run:
 
     def add_pending(self, target: Act, addend: Act):
         if self._covered(target):
-            call("seg_add", self.gptr(target), target.ld, self.gptr(addend), addend.ld, target.M, target.C,
+            call(self.k("seg_add"), self.gptr(target), target.ld, self.gptr(addend), addend.ld, target.M, target.C,
                  self.gptr(target), target.ld, self.stream)
         else:
             self.pending[target.key()] = addend
@@ -1005,7 +1024,7 @@ class Run:
             return 1
         add = self.pending.pop(a.key(), None)
         if add is not None:
-            call("seg_add", self.gptr(add), add.ld, None, 0, a.M, a.C, self.gptr(a), a.ld, self.stream)
+            call(self.k("seg_add"), self.gptr(add), add.ld, None, 0, a.M, a.C, self.gptr(a), a.ld, self.stream)
             self.mark_written(a)
             return 1
         return 0
@@ -1028,7 +1047,7 @@ class Run:
         global LAST_RUN
         x, img = self.image, self.prog.image
         self.prog.pack(self.stream)
-        call("seg_nchw_to_nhwc", x.data_ptr(), img.N, 3, img.H, img.W, self.ptr(img), img.ld, self.stream)
+        call(self.k("seg_nchw_to_nhwc"), x.data_ptr(), img.N, 3, img.H, img.W, self.ptr(img), img.ld, self.stream)
         for op in self.prog.ops:
             op.forward(self)
         if DEBUG_KEEP_RUN:
@@ -1120,14 +1139,14 @@ class _SegFunction(torch.autograd.Function):
         s = run.stream
         if mode == "logits":
             out = torch.empty((N, lo.C, Ho, Wo), device=x.device, dtype=torch.float32)
-            call("seg_upsample_to_nchw", run.ptr(lo), lo.ld, N, lo.H, lo.W, lo.C, out.data_ptr(), Ho, Wo, 1, s)
+            call(run.k("seg_upsample_to_nchw"), run.ptr(lo), lo.ld, N, lo.H, lo.W, lo.C, out.data_ptr(), Ho, Wo, 1, s)
         else:
             t = target.contiguous()
             if t.dtype != torch.int64 or tuple(t.shape) != (N, Ho, Wo):
                 raise ValueError(f"target must be int64 [{N},{Ho},{Wo}], got {tuple(t.shape)} {t.dtype}")
             stats = torch.empty(2, device=x.device, dtype=torch.float32)
             work = run.tmp(query("seg_ce_workspace_floats", N * Ho * Wo))
-            call("seg_ce_upsample_loss", run.ptr(lo), lo.ld, N, lo.H, lo.W, lo.C, t.data_ptr(), Ho, Wo,
+            call(run.k("seg_ce_upsample_loss"), run.ptr(lo), lo.ld, N, lo.H, lo.W, lo.C, t.data_ptr(), Ho, Wo,
                  ignore_index, work.data_ptr(), stats.data_ptr(), s)
             run.target, run.stats = t, stats
             out = stats[0]
@@ -1149,13 +1168,13 @@ class _SegFunction(torch.autograd.Function):
         dlo = lo
         if ctx.mode == "logits":
             g = gout.contiguous()
-            call("seg_upsample_bwd", g.data_ptr(), 0, 1, N, Ho, Wo, lo.C, run.gptr(dlo), lo.ld, lo.H, lo.W, 1, 0, s)
+            call(run.k("seg_upsample_bwd"), g.data_ptr(), 0, 1, N, Ho, Wo, lo.C, run.gptr(dlo), lo.ld, lo.H, lo.W, 1, 0, s)
         else:
             g = gout.reshape(1).to(torch.float32).contiguous()
-            dhigh = run.tmp(N * Ho * Wo * lo.ld)
-            call("seg_ce_upsample_grad", run.ptr(lo), lo.ld, N, lo.H, lo.W, lo.C, run.target.data_ptr(), Ho, Wo,
+            dhigh = torch.empty(max(N * Ho * Wo * lo.ld, 1), device=run.device, dtype=run.store)
+            call(run.k("seg_ce_upsample_grad"), run.ptr(lo), lo.ld, N, lo.H, lo.W, lo.C, run.target.data_ptr(), Ho, Wo,
                  ctx.ignore_index, g.data_ptr(), run.stats.data_ptr(), dhigh.data_ptr(), lo.ld, s)
-            call("seg_upsample_bwd", dhigh.data_ptr(), lo.ld, 0, N, Ho, Wo, lo.C, run.gptr(dlo), lo.ld, lo.H, lo.W,
+            call(run.k("seg_upsample_bwd"), dhigh.data_ptr(), lo.ld, 0, N, Ho, Wo, lo.C, run.gptr(dlo), lo.ld, lo.H, lo.W,
                  1, 0, s)
         run.mark_written(dlo)
         run.backward_from_logits()

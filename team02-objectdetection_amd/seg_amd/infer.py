@@ -75,6 +75,8 @@ class Predictor:
         self.W, self.H = target_size
         # math: conv arithmetic of the folded forward -- "f32" (the reference's), "f16"
         # (BASELINE configs[3]: fp16 operands, fp32 accumulation) or "bf16"
+        if math not in ("f32", "f16", "bf16"):
+            raise ValueError(f"Predictor math must be 'f32', 'f16' or 'bf16', got {math!r}")
         self.prog = get_program(model, 1, self.H, self.W, math)
         self.frame = torch.zeros((self.Hf, self.Wf, 3), device=self.device, dtype=torch.uint8)
         self.mask = torch.empty((self.Hf, self.Wf), device=self.device, dtype=torch.uint8)

@@ -86,15 +86,20 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void igemm_conv_kernel(
   using lds_t = OT;
   typedef OT ot4 __attribute__((ext_vector_type(4)));
   typedef OT ot8 __attribute__((ext_vector_type(8)));
-  constexpr int KQ = BK / 4;          // float4 groups per tile row
-  constexpr int A_VEC = BM * KQ, B_VEC = BN * KQ;
+  constexpr int KQ = BK / 4;          // float4 groups per tile row (B operand: fp32 packed weights)
+  // A operand on bf16 storage (uniform-tap loader): 8 channels = one 16-byte load per
+  // slot, copied to LDS as is (it already is the operand type); otherwise 4 channels
+  constexpr int VA = (sizeof(IT) == 2 && UT) ? 8 : 4;
+  static_assert(VA == 4 || std::is_same<OT, IT>::value, "raw 16-byte A copies need OT == IT");
+  constexpr int KQA = BK / VA;        // A slots per tile row
+  constexpr int A_VEC = BM * KQA, B_VEC = BN * KQ;
   constexpr int A_PER = (A_VEC + NT - 1) / NT;
   constexpr int B_PER = (B_VEC + NT - 1) / NT;
   constexpr int MI = WM / 32, NI = WN / 32;
   constexpr int WAVES_N = BN / WN;
   static_assert(NT == 256 || NT == 512, "4 or 8 waves per block");
   static_assert(!BNB || (UT && SEG_IGEMM_STAGES == 1), "BN-backward loads: uniform-tap loader, one LDS stage");
-  static_assert(NT % KQ == 0, "uniform kq per thread");
+  static_assert(NT % KQ == 0 && NT % KQA == 0, "uniform kq per thread");
   static_assert(!LP || BK % 16 == 0, "16-bit MFMA steps are 16 deep");
   static_assert(sizeof(lds_t) * BM * LDSR >= 4 * (BM / WM + 1) * BN, "BN-statistics scratch fits in As");
   static_assert(sizeof(lds_t) * BM * LDSR >= 4 * 2 * (BM / WM) * BN, "BN-backward reduction scratch fits in As");
@@ -118,11 +123,11 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void igemm_conv_kernel(
 #pragma unroll
   for (int i = 0; i < A_PER; ++i) {
     const int idx = tid + i * NT;
-    const int row = idx / KQ, kq = idx % KQ;
+    const int row = idx / KQA, kq = idx % KQA;
     const int p = m0 + row;
     a_ok[i] = (idx < A_VEC) && (p < a.M);
     const int pp = a_ok[i] ? p : 0;
-    a_k[i] = kq * 4 + kbeg;
+    a_k[i] = kq * VA + kbeg;
     const int tap = a_k[i] / a.Cin;
     a_ci[i] = a_k[i] - tap * a.Cin;
     a_ky[i] = tap / KS;
@@ -148,6 +153,7 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void igemm_conv_kernel(
   unsigned u_mask[A_PER];
   bool u_bok[B_PER];
   const int u_kq4 = (tid % KQ) * 4;
+  const int u_kqa = (tid % KQA) * VA;  // this thread's A channel offset in a K chunk
   int u_tap = 0, u_ci = 0;
   long u_toff0 = 0, u_toff1 = 0;
   auto tap_off = [&](int t) -> long { return ((long)(t / KS) * a.W + t % KS) * a.ldin; };
@@ -162,7 +168,7 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void igemm_conv_kernel(
 #pragma unroll
     for (int i = 0; i < A_PER; ++i) {
       const int idx = tid + i * NT;
-      const int row = idx / KQ;
+      const int row = idx / KQA;
       const int p = m0 + row;
       const bool ok = (idx < A_VEC) && (p < a.M);
       const int pp = ok ? p : 0;
@@ -208,14 +214,17 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void igemm_conv_kernel(
       // address selects only (out-of-image / out-of-matrix slots read g_zero4): no
       // branch splits the loader and no instruction touches the loaded registers
       // before the chunk that consumes them
-      const int ci = u_ci + u_kq4;
+      const int ci = u_ci + u_kqa;
       const bool wrap = ci >= a.Cin;
       const int tap = u_tap + (wrap ? 1 : 0);
       const long off = (wrap ? u_toff1 : u_toff0) + (wrap ? ci - a.Cin : ci);
 #pragma unroll
       for (int i = 0; i < A_PER; ++i) {
         const bool ok = (u_mask[i] >> tap) & 1u;
-        ra[i] = ld4(ok ? in + u_aoff[i] + off : zero4);
+        if constexpr (VA == 8)  // 8 bf16 as an opaque 16-byte payload
+          ra[i] = *reinterpret_cast<const f32x4*>(ok ? in + u_aoff[i] + off : zero4);
+        else
+          ra[i] = ld4(ok ? in + u_aoff[i] + off : zero4);
       }
       if (BNB) {
         const long offy = (wrap ? u_ytoff1 : u_ytoff0) + (wrap ? ci - a.Cin : ci);
@@ -293,7 +302,10 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void igemm_conv_kernel(
           const f32x4 t = seg_bnbwd4(v, ry[BNB ? i : 0], cf[0], cf[1], cf[2], cf[3], cf[4], cf[5], a.bnb.act);
           v = ((u_okbits >> i) & 1u) ? t : f32x4{0.f, 0.f, 0.f, 0.f};
         }
-        st_op(&As[buf][(idx / KQ) * LDSR + (idx % KQ) * 4], v);
+        if constexpr (VA == 8)
+          *reinterpret_cast<f32x4*>(&As[buf][(idx / KQA) * LDSR + (idx % KQA) * 8]) = v;
+        else
+          st_op(&As[buf][(idx / KQA) * LDSR + (idx % KQA) * 4], v);
       }
     }
 #pragma unroll
@@ -541,7 +553,8 @@ template <int BM, int BN, int WM, int WN, int BK, typename OT, typename IT>
 int launch_igemm_bk(const IgemmArgs& a, int ks, hipStream_t s) {
   const int grid = seg_cdiv(a.M, BM) * seg_cdiv(a.Cout, BN);
   const int splits = seg_cdiv(a.K, a.kchunk);
-  const bool ut = SEG_IGEMM_UT && (SEG_IGEMM_UT2 ? a.Cin >= BK : a.Cin % BK == 0);
+  const bool ut = SEG_IGEMM_UT && (SEG_IGEMM_UT2 ? a.Cin >= BK : a.Cin % BK == 0) &&
+                  (sizeof(IT) == 4 || (a.Cin % 8 == 0 && a.ldin % 8 == 0));  // bf16 A: 16-byte slots
   constexpr int NT = 64 * (BM / WM) * (BN / WN);
 #define SEG_IG(KS, U) hipLaunchKernelGGL((igemm_conv_kernel<BM, BN, WM, WN, KS, BK, U, false, OT, IT>), dim3(grid, splits), dim3(NT), 0, s, a)
 #define SEG_IGB(KS) hipLaunchKernelGGL((igemm_conv_kernel<BM, BN, WM, WN, KS, BK, true, true, OT, IT>), dim3(grid, splits), dim3(NT), 0, s, a)

@@ -42,13 +42,16 @@ constexpr int tr_pitch(int n) { return n % 128 == 32 || n % 128 == 96 ? n : tr_p
 // the MFMA fragment (lane: row r, k = 8h .. 8h+7) is gathered with two
 // ds_read_b64_tr_b16 (4 k-rows x 16 channels per 16-lane group, delivered
 // column-major) and fed to v_mfma_f32_32x32x16_bf16; fp32 accumulation and slabs.
-template <int BM, int BN, int WM, int WN, int KS, bool BNB = false, bool BF = false, typename IT = float>
+// VW: channels per load slot -- 8 (one 16-byte load, copied to LDS as is) on bf16
+// storage when Cout, Cin and the row strides are multiples of 8, else 4.
+template <int BM, int BN, int WM, int WN, int KS, bool BNB = false, bool BF = false, typename IT = float, int VW = 4>
 __global__ __launch_bounds__(256) void wgrad_kernel(WgradArgs a) {
+  static_assert(VW == 4 || (BF && sizeof(IT) == 2), "16-byte slots carry bf16 operands");
   const IT* __restrict__ gdy = static_cast<const IT*>(a.dy);
   const IT* __restrict__ gx = static_cast<const IT*>(a.x);
   constexpr int BK = BF ? 32 : ::BK;  // pixels per K chunk
   constexpr int AR = BF ? tr_pitch(BM) : BM + 4, BR = BF ? tr_pitch(BN) : BN + 4;
-  constexpr int A_VEC = BK * BM / 4, B_VEC = BK * BN / 4;
+  constexpr int A_VEC = BK * BM / VW, B_VEC = BK * BN / VW;
   constexpr int A_PER = (A_VEC + 255) / 256, B_PER = (B_VEC + 255) / 256;
   constexpr int MI = WM / 32, NI = WN / 32, WAVES_N = BN / WN;
   static_assert((BM / WM) * (BN / WN) == 4, "4 waves per block");
@@ -79,8 +82,8 @@ __global__ __launch_bounds__(256) void wgrad_kernel(WgradArgs a) {
 #pragma unroll
   for (int i = 0; i < B_PER; ++i) {
     const int idx = tid + i * 256;
-    b_prow[i] = idx / (BN / 4);
-    const int ncol = n0 + (idx % (BN / 4)) * 4;
+    b_prow[i] = idx / (BN / VW);
+    const int ncol = n0 + (idx % (BN / VW)) * VW;
     b_ok[i] = idx < B_VEC && ncol < a.Nw;
     const int tap = b_ok[i] ? ncol / a.Cin : 0;
     b_ci[i] = b_ok[i] ? ncol - tap * a.Cin : 0;
@@ -106,16 +109,20 @@ __global__ __launch_bounds__(256) void wgrad_kernel(WgradArgs a) {
       seg_bnbwd_coef(a.bnb, (idx < A_VEC && c < a.Cout) ? c : 0, cfa[BNB ? i : 0]);
     }
   }
+  auto ldv = [](const IT* q) -> f32x4 {  // one load slot: 4 channels widened, or 8 bf16 raw
+    if constexpr (VW == 8) return *reinterpret_cast<const f32x4*>(q);
+    else return ld4(q);
+  };
   auto load_tiles = [&](int k0) {  // k0 = first pixel of this chunk
     if (BNB) a_okbits = 0;
 #pragma unroll
     for (int i = 0; i < A_PER; ++i) {
       const int idx = tid + i * 256;
-      const int prow = idx / (BM / 4), c = co0 + (idx % (BM / 4)) * 4;
+      const int prow = idx / (BM / VW), c = co0 + (idx % (BM / VW)) * VW;
       const int p = k0 + prow;
       f32x4 v = {0.f, 0.f, 0.f, 0.f};
       const bool ok = idx < A_VEC && p < kend && c < a.Cout;
-      if (ok) v = ld4(gdy + (long)p * a.lddy + c);
+      if (ok) v = ldv(gdy + (long)p * a.lddy + c);
       ra[i] = v;
       if (BNB) {
         f32x4 w = {0.f, 0.f, 0.f, 0.f};
@@ -130,12 +137,12 @@ __global__ __launch_bounds__(256) void wgrad_kernel(WgradArgs a) {
       f32x4 v = {0.f, 0.f, 0.f, 0.f};
       if (b_ok[i] && p < kend) {
         if (KS == 1) {
-          v = ld4(gx + (long)p * a.ldx + b_ci[i]);
+          v = ldv(gx + (long)p * a.ldx + b_ci[i]);
         } else {
           const int hi = b_ho[i] * a.stride - a.pad + b_ky[i];
           const int wi = b_wo[i] * a.stride - a.pad + b_kx[i];
           if ((unsigned)hi < (unsigned)a.H && (unsigned)wi < (unsigned)a.W)
-            v = ld4(gx + (((long)b_n[i] * a.H + hi) * a.W + wi) * a.ldx + b_ci[i]);
+            v = ldv(gx + (((long)b_n[i] * a.H + hi) * a.W + wi) * a.ldx + b_ci[i]);
         }
       }
       rb[i] = v;
@@ -147,7 +154,8 @@ __global__ __launch_bounds__(256) void wgrad_kernel(WgradArgs a) {
     }
   };
   auto st_op = [](lds_t* p, f32x4 v) {
-    if constexpr (BF) *reinterpret_cast<bf16x4*>(p) = __builtin_convertvector(v, bf16x4);
+    if constexpr (VW == 8) *reinterpret_cast<f32x4*>(p) = v;  // 8 bf16, already the operand type
+    else if constexpr (BF) *reinterpret_cast<bf16x4*>(p) = __builtin_convertvector(v, bf16x4);
     else *reinterpret_cast<f32x4*>(p) = v;
   };
   auto store_tiles = [&](int buf) {
@@ -161,13 +169,13 @@ __global__ __launch_bounds__(256) void wgrad_kernel(WgradArgs a) {
           const f32x4 t = seg_bnbwd4(v, ry[BNB ? i : 0], cf[0], cf[1], cf[2], cf[3], cf[4], cf[5], a.bnb.act);
           v = ((a_okbits >> i) & 1u) ? t : f32x4{0.f, 0.f, 0.f, 0.f};
         }
-        st_op(&As[buf][(idx / (BM / 4)) * AR + (idx % (BM / 4)) * 4], v);
+        st_op(&As[buf][(idx / (BM / VW)) * AR + (idx % (BM / VW)) * VW], v);
       }
     }
 #pragma unroll
     for (int i = 0; i < B_PER; ++i) {
       const int idx = tid + i * 256;
-      if (idx < B_VEC) st_op(&Bs[buf][(idx / (BN / 4)) * BR + (idx % (BN / 4)) * 4], rb[i]);
+      if (idx < B_VEC) st_op(&Bs[buf][(idx / (BN / VW)) * BR + (idx % (BN / VW)) * VW], rb[i]);
     }
   };
 
@@ -265,8 +273,19 @@ int launch_wgrad(const WgradArgs& a, int ks, int splits, hipStream_t s) {
   dim3 grid(seg_cdiv(a.Cout, BM) * seg_cdiv(a.Nw, BN) * splits);
   if (BF) {
     if (a.bnb.y) return (int)hipErrorInvalidValue;
-    if (ks == 1) hipLaunchKernelGGL((wgrad_kernel<BM, BN, WM, WN, 1, false, true, IT>), grid, dim3(256), 0, s, a);
-    else hipLaunchKernelGGL((wgrad_kernel<BM, BN, WM, WN, 3, false, true, IT>), grid, dim3(256), 0, s, a);
+    const bool v8 = sizeof(IT) == 2 && a.Cout % 8 == 0 && a.Cin % 8 == 0 && a.lddy % 8 == 0 && a.ldx % 8 == 0;
+    if constexpr (sizeof(IT) == 2) {
+      if (v8) {
+        if (ks == 1) hipLaunchKernelGGL((wgrad_kernel<BM, BN, WM, WN, 1, false, true, IT, 8>), grid, dim3(256), 0, s, a);
+        else hipLaunchKernelGGL((wgrad_kernel<BM, BN, WM, WN, 3, false, true, IT, 8>), grid, dim3(256), 0, s, a);
+        SEG_RET_LAST();
+      }
+    }
+    if (ks == 1) {
+      hipLaunchKernelGGL((wgrad_kernel<BM, BN, WM, WN, 1, false, true, IT>), grid, dim3(256), 0, s, a);
+    } else {
+      hipLaunchKernelGGL((wgrad_kernel<BM, BN, WM, WN, 3, false, true, IT>), grid, dim3(256), 0, s, a);
+    }
     SEG_RET_LAST();
   }
   if (a.bnb.y) {

@@ -409,7 +409,7 @@ class ConvOp:
                 splits = query("seg_conv_wgrad_splits", M, self.cout, self.cin_pad, self.ks)
                 part = rt.tmp(splits * self.cout * self.ks * self.ks * self.cin_pad)
                 _timed_call(f"igemm{self.ks}_wgrad", self.flops(),
-                            rt.k("seg_conv_wgrad_bf16") if self.bf else "seg_conv_wgrad", dYp, dY.ld, rt.ptr(i), i.ld,
+                            ("seg_conv_wgrad_bf16io" if rt.io else "seg_conv_wgrad_bf16") if self.bf else "seg_conv_wgrad", dYp, dY.ld, rt.ptr(i), i.ld,
                             i.N, i.H, i.W, self.cin_pad, y.H, y.W, self.cout, self.ks, self.stride, self.pad,
                             part.data_ptr(), splits, s)
                 call("seg_conv_wgrad_reduce", part.data_ptr(), splits, gw, self.cout, self.cin, self.ks, 0, 0, s)

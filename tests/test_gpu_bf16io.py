@@ -156,7 +156,8 @@ def test_resample_pool_layout():
     n32, n16 = torch.empty(N, C, 2 * H, 2 * W, device=DEV), torch.empty(N, C, 2 * H, 2 * W, device=DEV)
     call("seg_upsample_to_nchw", x32.data_ptr(), C, N, H, W, C, n32.data_ptr(), 2 * H, 2 * W, 1, s)
     call("seg_upsample_to_nchw_bf16io", x16.data_ptr(), C, N, H, W, C, n16.data_ptr(), 2 * H, 2 * W, 1, s)
-    assert torch.equal(n32, n16)
+    # fp32 output: the two instantiations may contract the blend into FMAs differently
+    torch.testing.assert_close(n16, n32, rtol=1e-6, atol=1e-6)
     # image NCHW fp32 -> NHWC4 rows
     img = torch.randn(N, 3, H, W, device=DEV)
     h32, h16 = torch.empty(N * H * W, 4, device=DEV), torch.empty(N * H * W, 4, device=DEV, dtype=BF)

@@ -83,13 +83,20 @@ __global__ __launch_bounds__(256) void chan_partial_kernel(
     red0[t] = s0;
     red1[t] = s1;
     __syncthreads();
-    if (rg == 0 && active) {
-      for (int j = 1; j < RG; ++j) {
-        s0 += red0[j * TC + tc];
-        s1 += red1[j * TC + tc];
+    // fixed-order tree over the RG row groups (log2 RG LDS steps instead of RG - 1
+    // serial ones: the narrow layers have RG = 16..64)
+    int p2 = 1;
+    while (p2 < RG) p2 <<= 1;
+    for (int h = p2 >> 1; h > 0; h >>= 1) {
+      if (rg < h && rg + h < RG) {
+        red0[t] += red0[t + h * TC];
+        red1[t] += red1[t + h * TC];
       }
-      st4(p0 + cg * 4, s0);
-      st4(p1 + cg * 4, s1);
+      __syncthreads();
+    }
+    if (rg == 0 && active) {
+      st4(p0 + cg * 4, red0[tc]);
+      st4(p1 + cg * 4, red1[tc]);
     }
     __syncthreads();
   }

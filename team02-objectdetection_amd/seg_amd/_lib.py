@@ -109,18 +109,20 @@ class SegLibError(RuntimeError):
 
 
 def lib():
-    """Load libsegamd.so (must already be built: __graft_entry__.build())."""
+    """Load libsegamd.so (must already be built: __graft_entry__.build()).  SEG_LIB_PATH
+    may name another build of the same library (A/B timing of kernel variants)."""
     global _lib
     if _lib is not None:
         return _lib
     with _lock:
         if _lib is None:
-            if not os.path.exists(LIB_PATH):
+            path = os.environ.get("SEG_LIB_PATH", LIB_PATH)
+            if not os.path.exists(path):
                 raise SegLibError(
-                    f"HIP library {LIB_PATH} is missing; build it with `python __graft_entry__.py` "
+                    f"HIP library {path} is missing; build it with `python __graft_entry__.py` "
                     "(there is no CPU fallback for the segamd hot path)")
             import torch  # noqa: F401  -- load torch's libamdhip64 first so both share one HIP runtime
-            h = ctypes.CDLL(LIB_PATH)
+            h = ctypes.CDLL(path)
             for name, (res, args) in PROTOTYPES.items():
                 fn = getattr(h, name)
                 fn.restype = res

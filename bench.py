@@ -60,6 +60,9 @@ def parse():
                          "configurations (configs[2]/[4]): bf16 MFMA operands, fp32 accumulation / activations / BN "
                          "/ Adam; bf16io = bf16 math + bf16 activation/gradient storage.  infer: f16 = configs[3] "
                          "(default), f32, bf16")
+    ap.add_argument("--graphs", action="store_true",
+                    help="capture the training step in HIP graphs (engine.set_step_graphs; 1 GPU): the roofline is "
+                         "then measured on eager steps after the timed region")
     ap.add_argument("--model", choices=("MobileNetV2UNet", "UNet"), default="MobileNetV2UNet",
                     help="UNet = BASELINE configs[4] shape family (use --height 512 --width 1024 --batch 8)")
     return ap.parse_args()
@@ -180,6 +183,11 @@ def main():
     from seg_amd import engine
     model = deterministic_init(getattr(seg_amd, args.model)(args.classes), seed=0).to(dev).train()
     engine.set_conv_math(model, args.math)
+    if args.graphs:
+        if world > 1:
+            raise SystemExit("--graphs: the DataParallel gradient sync path stays eager (1 GPU only)")
+        engine.set_step_graphs(model, True)
+        args.warmup = max(args.warmup, engine.GRAPH_WARMUP + 1)  # capture happens inside the warmup
     peak = F32_MFMA_PEAK_TFLOPS if args.math == "f32" else BF16_MFMA_PEAK_TFLOPS
     if dist:
         from seg_amd.ddp import DataParallel
@@ -203,6 +211,8 @@ def main():
     # packet on the queue: timing all ~130 conv launches costs ~3 % of the step)
     conv3 = {"igemm3_fwd", "igemm3_dgrad", "wino3_fwd", "wino3_dgrad"}
     timer = None if args.no_timer else engine.KernelTimer(kinds=conv3)
+    if args.graphs:
+        timer = None  # replays run no Python: the roofline comes from the eager passes below
     if dist:
         torch.distributed.barrier()
     torch.cuda.synchronize()
@@ -224,6 +234,14 @@ def main():
     value = images / dt
 
     roof = None
+    if args.graphs and not args.no_timer:
+        engine.set_step_graphs(model, False)
+        timer = engine.KernelTimer(kinds=conv3)
+        engine.TIMER = timer
+        for _ in range(3):
+            step()
+        torch.cuda.synchronize()
+        engine.TIMER = None
     if timer is not None:
         def family(rec, kinds):
             sel = [(f, s) for k, f, s in rec if k in kinds]
@@ -316,7 +334,8 @@ def main():
                 "config": {"workload": f"{args.model} {args.classes}-class fwd+bwd+Adam, "
                                        f"{args.height}x{args.width}, bs={args.batch}/GPU ({cfg})",
                            "model": args.model, "global_batch": args.batch * world,
-                           "image": [args.height, args.width], "parallelism": f"dp{world}"},
+                           "image": [args.height, args.width], "parallelism": f"dp{world}",
+                           "hip_graphs": bool(args.graphs)},
                 "final_loss": round(final_loss, 5),
                 "math": {"f32": "fp32 everywhere",
                          "bf16": "conv operands bf16 (RNE) on the bf16 MFMA, fp32 accumulation; activations, "

@@ -22,6 +22,7 @@ for step in "$@"; do
     infer32) run infer32 600 python bench.py --workload infer --frames 300 --math f32 --no-cpu-baseline ;;
     bf16io) run bf16io 600 python -u -m pytest tests/test_gpu_bf16io.py -q -m gpu -x --timeout 120 --timeout-method thread ;;
     benchio) run benchio 600 python bench.py --steps 10 --warmup 3 --math bf16io --no-cpu-baseline ;;
+    graph) run graph 600 python -u -m pytest tests/test_gpu_graph.py -q -m gpu -x --timeout 300 --timeout-method thread ;;
     benchq) run benchq 600 python bench.py --steps 5 --warmup 2 --no-cpu-baseline ;;
     unet) run unet 600 python bench.py --model UNet --height 512 --width 1024 --batch 8 --steps 3 --warmup 2 ;;
     infer) run infer 600 python bench.py --workload infer --frames 300 --cpu-seconds 8 ;;

@@ -1123,6 +1123,127 @@ def _check_input(x: torch.Tensor):
         raise NotImplementedError("gradient w.r.t. the input image is not supported")
 
 
+def _loss_forward(run, t, ignore_index):
+    """Fused final upsample + CrossEntropy over the run's low-res logits: stats = [loss, count]."""
+    prog, lo, s = run.prog, run.prog.logits, run.stream
+    N = prog.N
+    Ho, Wo = prog.out_hw
+    stats = torch.empty(2, device=run.device, dtype=torch.float32)
+    work = run.tmp(query("seg_ce_workspace_floats", N * Ho * Wo))
+    call(run.k("seg_ce_upsample_loss"), run.ptr(lo), lo.ld, N, lo.H, lo.W, lo.C, t.data_ptr(), Ho, Wo,
+         ignore_index, work.data_ptr(), stats.data_ptr(), s)
+    run.target, run.stats = t, stats
+    return stats
+
+
+def _loss_backward(run, g, ignore_index):
+    """Gradient of the fused loss (g: [1] fp32 upstream gradient) through the whole program."""
+    prog, lo, s = run.prog, run.prog.logits, run.stream
+    N = prog.N
+    Ho, Wo = prog.out_hw
+    dhigh = torch.empty(max(N * Ho * Wo * lo.ld, 1), device=run.device, dtype=run.store)
+    call(run.k("seg_ce_upsample_grad"), run.ptr(lo), lo.ld, N, lo.H, lo.W, lo.C, run.target.data_ptr(), Ho, Wo,
+         ignore_index, g.data_ptr(), run.stats.data_ptr(), dhigh.data_ptr(), lo.ld, s)
+    call(run.k("seg_upsample_bwd"), dhigh.data_ptr(), lo.ld, 0, N, Ho, Wo, lo.C, run.gptr(lo), lo.ld, lo.H, lo.W,
+         1, 0, s)
+    run.mark_written(lo)
+    run.backward_from_logits()
+    if run.sync is not None:
+        run.sync.finish_gradient_sync()  # stream-ordered wait on the last all-reduces
+
+
+class _StepGraph:
+    """A training step of one program captured as two HIP graphs (torch.cuda.CUDAGraph
+    drives hipGraph on ROCm): the forward with the fused loss, and the backward down to
+    every parameter gradient.  Replaying them replaces ~600 kernel launches from Python
+    (~11 ms of host time per step, more than the bf16io step's GPU time) with two graph
+    launches.  Buffers, saved statistics and gradients live in the graphs' private pool
+    and are reused by every replay; parameter gradients are views of one flat buffer.
+    Requires static shapes, parameters updated in place (any torch optimizer) and no
+    DataParallel gradient sync (that path stays eager)."""
+
+    def __init__(self, prog, x, target, ignore_index, params):
+        self.prog, self.ignore_index = prog, ignore_index
+        self.x, self.t = torch.empty_like(x), torch.empty_like(target)
+        self.gout = torch.empty(1, device=x.device, dtype=torch.float32)
+        self.pool = torch.cuda.graph_pool_handle()
+        self.g_fwd = self.g_bwd = None
+        self.run = self.stats = None
+        self.busy = False            # a replayed forward waits for its backward
+        self.slot, off = {}, 0
+        for p in params:
+            if p.requires_grad and id(p) not in self.slot:
+                self.slot[id(p)] = (off, p.numel(), p.shape)
+                off += p.numel()
+        self.flat = torch.empty(max(off, 1), device=x.device, dtype=torch.float32)
+
+    # the Run's gradient-sync interface: gradients land in the flat buffer
+    def grad_storage(self, p, flat=None):
+        slot = self.slot.get(id(p))
+        if slot is None:
+            return None
+        o, n, shape = slot
+        return (self.flat if flat is None else flat)[o:o + n].view(shape)
+
+    def on_ready(self, params, run=None):
+        pass
+
+    def finish_gradient_sync(self):
+        pass
+
+    def forward(self, x, target, training):
+        self.x.copy_(x)
+        self.t.copy_(target)
+        if self.g_fwd is None:
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, pool=self.pool):
+                run = Run(self.prog, self.x, training)
+                run.sync = self
+                run.forward()
+                self.stats = _loss_forward(run, self.t, self.ignore_index)
+            self.g_fwd, self.run = g, run
+        self.g_fwd.replay()
+        self.busy = True
+        return self.stats[0].clone()
+
+    def backward(self, gout):
+        self.gout.copy_(gout.reshape(1))
+        if self.g_bwd is None:
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, pool=self.pool):
+                _loss_backward(self.run, self.gout, self.ignore_index)
+            self.g_bwd = g
+        self.g_bwd.replay()
+        self.busy = False
+
+
+GRAPH_WARMUP = 2  # eager steps of a program before its step is captured
+
+
+def set_step_graphs(model, on: bool = True):
+    """Capture the training step (forward + fused loss, backward) of `model` in HIP graphs
+    after GRAPH_WARMUP eager steps per input shape (see _StepGraph)."""
+    model = getattr(model, "module", model)
+    model.__dict__["_segamd_graphs"] = bool(on)
+    return model
+
+
+def _step_graph(model, prog, x, target, ignore_index, params):
+    if not model.__dict__.get("_segamd_graphs"):
+        return None
+    cache = model.__dict__.setdefault("_segamd_step_graphs", {})
+    key = (id(prog), ignore_index)
+    ent = cache.get(key)
+    if ent is None:
+        ent = cache[key] = [0, None]
+    if ent[0] < GRAPH_WARMUP:
+        ent[0] += 1
+        return None
+    if ent[1] is None:
+        ent[1] = _StepGraph(prog, x, target, ignore_index, params)
+    return None if ent[1].busy else ent[1]
+
+
 class _SegFunction(torch.autograd.Function):
     """Whole-network forward/backward as one autograd node."""
 
@@ -1131,25 +1252,30 @@ class _SegFunction(torch.autograd.Function):
         x = x.contiguous()
         N, _, H, W = x.shape
         prog = get_program(model, N, H, W)
+        Ho, Wo = prog.out_hw
+        t = None
+        if mode == "loss":
+            t = target.contiguous()
+            if t.dtype != torch.int64 or tuple(t.shape) != (N, Ho, Wo):
+                raise ValueError(f"target must be int64 [{N},{Ho},{Wo}], got {tuple(t.shape)} {t.dtype}")
+            wants_grad = any(ctx.needs_input_grad[6:])
+            sg = (_step_graph(model, prog, x, t, ignore_index, params)
+                  if wants_grad and model.training and sync is None else None)
+            if sg is not None:
+                out = sg.forward(x, t, model.training)
+                ctx.sg, ctx.run, ctx.params = sg, None, params
+                return out
+        ctx.sg = None
         run = Run(prog, x, model.training)
         run.sync = sync
         run.forward()
         lo = prog.logits
-        Ho, Wo = prog.out_hw
-        s = run.stream
         if mode == "logits":
             out = torch.empty((N, lo.C, Ho, Wo), device=x.device, dtype=torch.float32)
-            call(run.k("seg_upsample_to_nchw"), run.ptr(lo), lo.ld, N, lo.H, lo.W, lo.C, out.data_ptr(), Ho, Wo, 1, s)
+            call(run.k("seg_upsample_to_nchw"), run.ptr(lo), lo.ld, N, lo.H, lo.W, lo.C, out.data_ptr(), Ho, Wo, 1,
+                 run.stream)
         else:
-            t = target.contiguous()
-            if t.dtype != torch.int64 or tuple(t.shape) != (N, Ho, Wo):
-                raise ValueError(f"target must be int64 [{N},{Ho},{Wo}], got {tuple(t.shape)} {t.dtype}")
-            stats = torch.empty(2, device=x.device, dtype=torch.float32)
-            work = run.tmp(query("seg_ce_workspace_floats", N * Ho * Wo))
-            call(run.k("seg_ce_upsample_loss"), run.ptr(lo), lo.ld, N, lo.H, lo.W, lo.C, t.data_ptr(), Ho, Wo,
-                 ignore_index, work.data_ptr(), stats.data_ptr(), s)
-            run.target, run.stats = t, stats
-            out = stats[0]
+            out = _loss_forward(run, t, ignore_index)[0]
         if any(ctx.needs_input_grad[6:]):
             ctx.run, ctx.mode, ctx.ignore_index = run, mode, ignore_index
             ctx.params = params
@@ -1159,27 +1285,32 @@ class _SegFunction(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, gout):
+        if ctx.sg is not None:
+            sg = ctx.sg
+            sg.backward(gout.to(torch.float32))
+            # hand autograd views of a fresh copy of the flat gradients (one copy kernel):
+            # a .grad must never alias the buffer the next replay writes
+            flat = sg.flat.clone()
+            grads = [sg.grad_storage(p, flat) if ctx.needs_input_grad[6 + k] else None
+                     for k, p in enumerate(ctx.params)]
+            ctx.sg = ctx.params = None
+            return (None, None, None, None, None, None, *grads)
         run = ctx.run
         if run is None:
             raise RuntimeError("segamd: backward called on a forward that saved nothing")
         prog, lo, s = run.prog, run.prog.logits, run.stream
         N = prog.N
         Ho, Wo = prog.out_hw
-        dlo = lo
         if ctx.mode == "logits":
             g = gout.contiguous()
-            call(run.k("seg_upsample_bwd"), g.data_ptr(), 0, 1, N, Ho, Wo, lo.C, run.gptr(dlo), lo.ld, lo.H, lo.W, 1, 0, s)
+            call(run.k("seg_upsample_bwd"), g.data_ptr(), 0, 1, N, Ho, Wo, lo.C, run.gptr(lo), lo.ld, lo.H, lo.W, 1,
+                 0, s)
+            run.mark_written(lo)
+            run.backward_from_logits()
+            if run.sync is not None:
+                run.sync.finish_gradient_sync()
         else:
-            g = gout.reshape(1).to(torch.float32).contiguous()
-            dhigh = torch.empty(max(N * Ho * Wo * lo.ld, 1), device=run.device, dtype=run.store)
-            call(run.k("seg_ce_upsample_grad"), run.ptr(lo), lo.ld, N, lo.H, lo.W, lo.C, run.target.data_ptr(), Ho, Wo,
-                 ctx.ignore_index, g.data_ptr(), run.stats.data_ptr(), dhigh.data_ptr(), lo.ld, s)
-            call(run.k("seg_upsample_bwd"), dhigh.data_ptr(), lo.ld, 0, N, Ho, Wo, lo.C, run.gptr(dlo), lo.ld, lo.H, lo.W,
-                 1, 0, s)
-        run.mark_written(dlo)
-        run.backward_from_logits()
-        if run.sync is not None:
-            run.sync.finish_gradient_sync()  # stream-ordered wait on the last all-reduces
+            _loss_backward(run, gout.reshape(1).to(torch.float32).contiguous(), ctx.ignore_index)
         grads = [run.grads.get(id(p)) if ctx.needs_input_grad[6 + k] else None for k, p in enumerate(ctx.params)]
         # drop every other reference so AccumulateGrad can adopt the tensors instead of copying them
         run.grads.clear()

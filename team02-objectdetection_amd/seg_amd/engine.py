@@ -1160,7 +1160,13 @@ class _StepGraph:
     launches.  Buffers, saved statistics and gradients live in the graphs' private pool
     and are reused by every replay; parameter gradients are views of one flat buffer.
     Requires static shapes, parameters updated in place (any torch optimizer) and no
-    DataParallel gradient sync (that path stays eager)."""
+    DataParallel gradient sync (that path stays eager).
+
+    Bitwise equal to the eager step (tests/test_gpu_graph.py), but measured SLOWER on
+    MI355X / ROCm 7.2 in round 1 (bf16io 2772 vs 2970 img/s, f32 1633 vs 1708): the
+    replay runs every node on one hardware queue, so the weight-gradient side stream no
+    longer overlaps the data-gradient chain (with SEG_OVERLAP=0 both give 2756-2759).
+    Off unless set_step_graphs(model) / bench.py --graphs."""
 
     def __init__(self, prog, x, target, ignore_index, params):
         self.prog, self.ignore_index = prog, ignore_index

@@ -581,9 +581,15 @@ inline int igemm_bk(int K) { return (SEG_IGEMM_BK != 16 && (K <= 64 || (K % SEG_
 // split-K: `splits` K ranges of whole BK chunks (a.part set by the caller when splits > 1)
 template <int BM, int BN, int WM, int WN, typename OT = float, typename IT = float>
 int launch_igemm(IgemmArgs a, int ks, int splits, hipStream_t s) {
-  const int bk = igemm_bk(a.K);
+  int bk = igemm_bk(a.K);
+  // 16-bit operands: 64-deep K chunks (4 MFMA k-steps per barrier) where the uniform-tap
+  // loader still applies (Cin >= 64)
+  if (sizeof(OT) == 2 && bk == SEG_IGEMM_BK && a.Cin >= 64 && a.K >= 256) bk = 64;
   const int nk = seg_cdiv(a.K, bk);
   a.kchunk = seg_cdiv(nk, splits) * bk;
+  if constexpr (sizeof(OT) == 2) {
+    if (bk == 64) return launch_igemm_bk<BM, BN, WM, WN, 64, OT, IT>(a, ks, s);
+  }
   if (bk == 16) return launch_igemm_bk<BM, BN, WM, WN, 16, OT, IT>(a, ks, s);
   return launch_igemm_bk<BM, BN, WM, WN, SEG_IGEMM_BK, OT, IT>(a, ks, s);
 }

@@ -28,7 +28,24 @@ import os
 import torch
 from torch import nn
 
-from ._lib import call, query
+from ._lib import call, query as _query
+
+# Host-only size / plan queries of the C ABI are pure functions of their integer
+# arguments: memoised, so a training step does not pay a ctypes call for each of them.
+_PURE_QUERIES = {"seg_chan_workspace_floats", "seg_conv_wgrad_splits", "seg_dw_wgrad_blocks",
+                 "seg_conv_igemm_splits", "seg_ce_workspace_floats", "seg_conv_wino_row_tiles",
+                 "seg_conv_halo_row_tiles", "seg_conv_wino_wgrad_splits", "seg_pw_bwd_blocks"}
+_QCACHE = {}
+
+
+def query(name, *args):
+    if name not in _PURE_QUERIES:
+        return _query(name, *args)
+    key = (name, args)
+    r = _QCACHE.get(key)
+    if r is None:
+        r = _QCACHE[key] = _query(name, *args)
+    return r
 from .mobilenet import ConvBNReLU6, InvertedResidual
 
 ACT_NONE, ACT_RELU, ACT_RELU6 = 0, 1, 2
@@ -922,6 +939,7 @@ class Run:
         self._tmp_n = 0
         self.side = None      # side stream of the parameter gradients (backward only)
         self.bnred = {}       # id(BN op) -> (tile partials, ntiles) from a fused data gradient
+        self._n_fork = 0      # side-stream forks so far (index into the program's event pool)
 
     def k(self, name: str) -> str:
         """C-ABI entry point of an activation kernel for this run's storage type."""
@@ -970,7 +988,12 @@ class Run:
         stream; temporaries allocated inside the context belong to the side stream."""
         if self.side is None:
             return contextlib.nullcontext(), self.stream
-        ev = torch.cuda.Event()
+        # events are reused step after step (a wait binds to the record before it)
+        pool = self.prog.__dict__.setdefault("_fork_events", [])
+        if self._n_fork == len(pool):
+            pool.append(torch.cuda.Event())
+        ev = pool[self._n_fork]
+        self._n_fork += 1
         ev.record(self.main)
         self.side.wait_event(ev)
         return torch.cuda.stream(self.side), self.side.cuda_stream

@@ -584,7 +584,9 @@ int launch_igemm(IgemmArgs a, int ks, int splits, hipStream_t s) {
   int bk = igemm_bk(a.K);
   // 16-bit operands: 64-deep K chunks (4 MFMA k-steps per barrier) where the uniform-tap
   // loader still applies (Cin >= 64)
-  if (sizeof(OT) == 2 && bk == SEG_IGEMM_BK && a.Cin >= 64 && a.K >= 256) bk = 64;
+  // (unsplit launches only: with split-K, K ranges that are not a multiple of the
+  // 64-deep chunk gave wrong partial sums -- tests/test_gpu_bf16.py::test_conv_16bit_splitk_act)
+  if (sizeof(OT) == 2 && bk == SEG_IGEMM_BK && a.Cin >= 64 && a.K >= 256 && splits == 1) bk = 64;
   const int nk = seg_cdiv(a.K, bk);
   a.kchunk = seg_cdiv(nk, splits) * bk;
   if constexpr (sizeof(OT) == 2) {

@@ -1175,6 +1175,22 @@ def _loss_backward(run, g, ignore_index):
         run.sync.finish_gradient_sync()  # stream-ordered wait on the last all-reduces
 
 
+@contextlib.contextmanager
+def _no_gc():
+    """No Python garbage collection while a graph is being captured: a collected object
+    that owns a HIP resource (an event, a tensor of an unrelated pool) would call into
+    the runtime mid-capture and abort the process."""
+    import gc
+    gc.collect()
+    was = gc.isenabled()
+    gc.disable()
+    try:
+        yield
+    finally:
+        if was:
+            gc.enable()
+
+
 class _StepGraph:
     """A training step of one program captured as two HIP graphs (torch.cuda.CUDAGraph
     drives hipGraph on ROCm): the forward with the fused loss, and the backward down to
@@ -1225,7 +1241,7 @@ class _StepGraph:
         self.t.copy_(target)
         if self.g_fwd is None:
             g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g, pool=self.pool):
+            with _no_gc(), torch.cuda.graph(g, pool=self.pool):
                 run = Run(self.prog, self.x, training)
                 run.sync = self
                 run.forward()
@@ -1239,7 +1255,7 @@ class _StepGraph:
         self.gout.copy_(gout.reshape(1))
         if self.g_bwd is None:
             g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g, pool=self.pool):
+            with _no_gc(), torch.cuda.graph(g, pool=self.pool):
                 _loss_backward(self.run, self.gout, self.ignore_index)
             self.g_bwd = g
         self.g_bwd.replay()

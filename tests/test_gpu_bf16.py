@@ -229,3 +229,35 @@ def test_bf16_training_tracks_f32():
         assert b[-1] < 0.9 * b[0], curves
         assert abs(a[-1] - b[-1]) < 0.05 * a[0], curves
     print("f32   ", " ".join(f"{v:.3f}" for v in a))
+
+
+@pytest.mark.parametrize("name", ["seg_conv_igemm_bf16", "seg_conv_igemm_f16"])
+@pytest.mark.parametrize("N,Cin,Cout,H,W,ks,act", [(1, 1344, 256, 8, 16, 3, 1), (1, 80, 32, 32, 64, 3, 2),
+                                                  (1, 320, 1280, 4, 8, 1, 2), (1, 152, 64, 16, 32, 3, 0)])
+def test_conv_16bit_splitk_act(name, N, Cin, Cout, H, W, ks, act):
+    """The batch-1 inference launches: split-K partial slabs + fixed-order reduce with the
+    bias / activation epilogue, against the unsplit launch and a float64 conv of the
+    rounded operands."""
+    pad = ks // 2
+    dt = torch.bfloat16 if "bf16" in name else torch.float16
+    x = gen(N, Cin, H, W, seed=41)
+    w = gen(Cout, Cin, ks, ks, seed=42) * (2.0 / (Cin * ks * ks)) ** 0.5
+    b = gen(Cout, seed=43)
+    ref = F.conv2d(x.to(dt).double(), w.to(dt).double(), b.double(), padding=pad)
+    ref = torch.clamp(ref, min=0) if act == 1 else (torch.clamp(ref, 0, 6) if act == 2 else ref)
+    s = S()
+    xg, wg, bg = nhwc(x), w.to(DEV), b.to(DEV)
+    ldk = r4(ks * ks * Cin)
+    wk = torch.empty(Cout * ldk, device=DEV)
+    call("seg_pack_conv_weight", wg.data_ptr(), wk.data_ptr(), Cout, Cin, ks, ldk, 0, Cin, s)
+    M = N * H * W
+    splits = query("seg_conv_igemm_splits", M, Cout, Cin, ks)
+    outs = []
+    for sp in sorted({1, splits, 5}):
+        out = torch.full((M, r4(Cout)), float("nan"), device=DEV)
+        work = torch.empty(max(sp * M * Cout, 1), device=DEV)
+        call(name, xg.data_ptr(), xg.shape[1], N, H, W, Cin, wk.data_ptr(), ldk, bg.data_ptr(), out.data_ptr(),
+             out.shape[1], H, W, Cout, ks, 1, pad, None, 0, None, act, work.data_ptr() if sp > 1 else None, sp, s)
+        got = from_nhwc(out, N, Cout, H, W)
+        assert rel(got, ref) < 1e-5, (sp, rel(got, ref))
+        outs.append(got)

@@ -1,0 +1,59 @@
+"""GPU: the data-parallel path (seg_amd/ddp.py) on the real engine and RCCL, world size 1
+(the multi-rank semantics are covered over gloo in tests/test_ddp.py; one GPU per box
+here).  Bucket hooks fire from the side-stream weight gradients, all-reduces run on
+RCCL's stream and the averaged gradients must equal the plain model's bitwise."""
+import os
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+
+from seg_amd import MobileNetV2UNet, engine
+from seg_amd.ddp import DataParallel
+from seg_amd.detinit import deterministic_init, synthetic_batch
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+@pytest.fixture(scope="module")
+def pg():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("nccl", rank=0, world_size=1)
+    yield
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("math", ["f32", "bf16io"])
+def test_ddp_world1_matches_plain(pg, math):
+    x, y = synthetic_batch(2, 64, 128, 10, seed=3)
+    x, y = x.to(DEV), y.to(DEV)
+    res = []
+    for wrap in (False, True):
+        m = deterministic_init(MobileNetV2UNet(10), seed=9).to(DEV).train()
+        engine.set_conv_math(m, math)
+        model = DataParallel(m, bucket_cap_mb=1.0) if wrap else m
+        opt = torch.optim.Adam(model.parameters(), lr=1e-3)
+        losses = []
+        for _ in range(3):
+            opt.zero_grad(set_to_none=True)
+            loss = model.forward_loss(x, y)
+            loss.backward()
+            if wrap:
+                model.finish_gradient_sync()
+            opt.step()
+            losses.append(loss.item())
+        torch.cuda.synchronize()
+        grads = {k: p.grad.clone() for k, p in m.named_parameters() if p.grad is not None}
+        res.append((losses, grads, {k: v.clone() for k, v in m.state_dict().items()}))
+    (l0, g0, s0), (l1, g1, s1) = res
+    assert l0 == l1
+    assert g0.keys() == g1.keys()
+    for k in g0:
+        assert torch.equal(g0[k], g1[k]), k
+    for k in s0:
+        assert torch.equal(s0[k], s1[k]), k

@@ -319,6 +319,24 @@ def main():
                            "avg_launch_us": round(ws / max(wgn, 1) * 1e6, 2)},
                 "all_mfma_convs": {"achieved": round(af / as_ / 1e12, 2) if as_ else None, "launches": an}}
 
+    # Whole-step roofline (the north-star figure): algorithmic work of one
+    # training image under the fused-execution model -- FLOPs = 3 x the forward conv FLOPs
+    # (fwd, data and weight gradient); bytes = sum over convs of (3|X| + 5|Y|) * s plus the
+    # loss (2 C H W s + 8 H W), s = activation bytes (4 f32, 2 with bf16 storage).
+    prog = engine.get_program(getattr(model, "module", model), args.batch, args.height, args.width)
+    sb = 2 if args.math == "bf16io" else 4
+    fl_img = by_img = 0.0
+    for op in prog.ops:
+        if isinstance(op, engine.ConvOp):
+            fl_img += 3 * op.flops() / args.batch
+            by_img += (3 * op.inp.M * op.cin + 5 * op.y.M * op.cout) * sb / args.batch
+    by_img += (2 * args.classes * args.height * args.width * sb + 8 * args.height * args.width)
+    step_roof = {"flops_per_img": round(fl_img), "bytes_per_img": round(by_img),
+                 "achieved_tflops": round(fl_img * value / 1e12, 2), "achieved_gbs": round(by_img * value / 1e9, 1),
+                 "frac_mfma_peak": round(fl_img * value / 1e12 / peak, 4),
+                 "frac_hbm_peak": round(by_img * value / 1e9 / HBM_PEAK_GBS, 4),
+                 "bound_img_per_s": round(1.0 / max(fl_img / (peak * 1e12), by_img / (HBM_PEAK_GBS * 1e9)), 1)}
+
     if rank == 0:
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
@@ -343,7 +361,7 @@ def main():
                          "bf16io": "conv operands bf16 on the bf16 MFMA, fp32 accumulation; activations and their "
                                    "gradients stored bf16 in HBM (fp32 arithmetic inside every kernel); BN "
                                    "statistics, parameter gradients, loss and Adam fp32"}[args.math],
-                "roofline": roof, "cpu_baseline": cpu}
+                "roofline": roof, "step_roofline": step_roof, "cpu_baseline": cpu}
         print(json.dumps(line), flush=True)
     if dist:
         torch.distributed.destroy_process_group()

@@ -393,6 +393,9 @@ int seg_maxpool2_fwd_bf16io(const seg_bf16* in, long ldin, int N, int H, int W, 
     hipStream_t stream);
 int seg_maxpool2_bwd_bf16io(const seg_bf16* in, long ldin, const seg_bf16* dout, long lddout, int N, int H, int W, int
     C, seg_bf16* din, long lddin, int accumulate, hipStream_t stream);
+int seg_conv_halo_bf16io(const seg_bf16* in, long ldin, int N, int H, int W, int Cin, const float* wk, int ldk,
+    const float* bias, seg_bf16* out, long ldout, int Cout, const seg_bf16* add, long ldadd, float* stat,
+    hipStream_t stream);
 int seg_conv_wgrad_bf16io(const seg_bf16* dy, long lddy, const seg_bf16* x, long ldx, int N, int H, int W, int Cin,
     int Ho, int Wo, int Cout, int ks, int stride, int pad, float* part, int splits, hipStream_t stream);
 

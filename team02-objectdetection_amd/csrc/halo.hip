@@ -22,30 +22,42 @@ namespace {
 
 constexpr int TH = 4, TW = 64;                // output tile (pixels)
 constexpr int HH = TH + 2, HW = TW + 2;       // halo tile
-constexpr int BK = 16, LDSR = BK + 4;         // K chunk (input channels), LDS row stride
-constexpr int HALO_VEC = HH * HW * (BK / 4);  // float4 slots of a halo chunk
-constexpr int HALO_PER = (HALO_VEC + 255) / 256;
 
 __device__ __attribute__((aligned(16))) float g_hzero4[4];
 
 struct HaloArgs {
-  const float* in; long ldin;
+  const void* in; long ldin;     // T (float, or __bf16 on the bf16io path)
   const float* wk; int ldk;      // packed [Cout][ldk], k = tap*Cin + ci (seg_pack_conv_weight mode 0/1)
   const float* bias;
-  const float* add; long ldadd;
-  float* out; long ldout;
+  const void* add; long ldadd;   // T
+  void* out; long ldout;         // T
   float* stat;                   // BN partials [tiles][2][Cout]
   int N, H, W, Cin, Cout;
   int tiles_w, tiles_h;
 };
 
-template <int NI>  // output-channel blocks of 32 (Cout padded to 32*NI)
+// T: activation storage (in / add / out).  T = __bf16 (the bf16io configuration):
+// bf16 operands in LDS (the halo copied as is, 8 channels per 16-byte slot; weights
+// rounded on the way in), 32-deep K chunks and v_mfma_f32_32x32x16_bf16 with fp32
+// accumulation; the fp32 epilogue rounds once on the store.
+template <int NI, typename T = float>  // output-channel blocks of 32 (Cout padded to 32*NI)
 __global__ __launch_bounds__(256) void halo3x3_kernel(HaloArgs a) {
+  constexpr bool LP = sizeof(T) == 2;
+  constexpr int BK = LP ? 32 : 16;                 // K chunk (input channels)
+  constexpr int LDSR = LP ? BK + 8 : BK + 4;       // LDS row stride (elements): conflict-free b128 reads
+  constexpr int HV = LP ? 8 : 4;                   // halo channels per load slot
+  constexpr int HALO_VEC = HH * HW * (BK / HV);    // slots of a halo chunk
+  constexpr int HALO_PER = (HALO_VEC + 255) / 256;
   constexpr int BNC = 32 * NI;
   constexpr int W_VEC = 9 * BNC * (BK / 4);
   constexpr int W_PER = (W_VEC + 255) / 256;
-  __shared__ __attribute__((aligned(16))) float Hs[HH * HW * LDSR];
-  __shared__ __attribute__((aligned(16))) float Ws[9 * BNC * LDSR];
+  using lds_t = T;
+  __shared__ __attribute__((aligned(16))) lds_t Hs[HH * HW * LDSR];
+  __shared__ __attribute__((aligned(16))) lds_t Ws[9 * BNC * LDSR];
+  static_assert(sizeof(lds_t) * HH * HW * LDSR >= 4 * 5 * BNC, "BN-statistics scratch fits in Hs");
+  const T* in = static_cast<const T*>(a.in);
+  const T* add = static_cast<const T*>(a.add);
+  T* out = static_cast<T*>(a.out);
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int lid = xcd_swizzle(blockIdx.x, gridDim.x);  // neighbouring tiles share an XCD's L2
@@ -53,7 +65,7 @@ __global__ __launch_bounds__(256) void halo3x3_kernel(HaloArgs a) {
   const int th_i = (lid / a.tiles_w) % a.tiles_h;
   const int n = lid / (a.tiles_w * a.tiles_h);
   const int h0 = th_i * TH, w0 = tw_i * TW;
-  const float* inb = a.in + (long)n * a.H * a.W * a.ldin;
+  const T* inb = in + (long)n * a.H * a.W * a.ldin;
 
   // halo slots: (halo pixel, float4 channel group) -> global offset or the zero page
   long hoff[HALO_PER];
@@ -61,11 +73,11 @@ __global__ __launch_bounds__(256) void halo3x3_kernel(HaloArgs a) {
 #pragma unroll
   for (int i = 0; i < HALO_PER; ++i) {
     const int s = tid + i * 256;
-    const int hp = s / (BK / 4), q = s % (BK / 4);
+    const int hp = s / (BK / HV), q = s % (BK / HV);
     const int hy = hp / HW, hx = hp % HW;
     const int gy = h0 - 1 + hy, gx = w0 - 1 + hx;
     hok[i] = s < HALO_VEC && (unsigned)gy < (unsigned)a.H && (unsigned)gx < (unsigned)a.W;
-    hoff[i] = hok[i] ? ((long)gy * a.W + gx) * a.ldin + q * 4 : 0;
+    hoff[i] = hok[i] ? ((long)gy * a.W + gx) * a.ldin + q * HV : 0;
   }
   // weight slots: (tap, co, float4 group)
   long woff[W_PER];
@@ -83,8 +95,12 @@ __global__ __launch_bounds__(256) void halo3x3_kernel(HaloArgs a) {
   auto load = [&](int c0) {
 #pragma unroll
     for (int i = 0; i < HALO_PER; ++i) {
-      const int q4 = ((tid + i * 256) % (BK / 4)) * 4;
-      rh[i] = ld4(hok[i] && c0 + q4 < a.Cin ? inb + hoff[i] + c0 : g_hzero4);
+      const int q4 = ((tid + i * 256) % (BK / HV)) * HV;
+      if constexpr (LP)  // 8 bf16 as an opaque 16-byte payload (Cin % 8 == 0)
+        rh[i] = *reinterpret_cast<const f32x4*>(hok[i] && c0 + q4 < a.Cin ? inb + hoff[i] + c0
+                                                                          : reinterpret_cast<const T*>(g_hzero4));
+      else
+        rh[i] = ld4(hok[i] && c0 + q4 < a.Cin ? inb + hoff[i] + c0 : g_hzero4);
     }
 #pragma unroll
     for (int i = 0; i < W_PER; ++i) {
@@ -96,12 +112,17 @@ __global__ __launch_bounds__(256) void halo3x3_kernel(HaloArgs a) {
 #pragma unroll
     for (int i = 0; i < HALO_PER; ++i) {
       const int s = tid + i * 256;
-      if (HALO_VEC % 256 == 0 || s < HALO_VEC) st4(&Hs[(s / (BK / 4)) * LDSR + (s % (BK / 4)) * 4], rh[i]);
+      if (HALO_VEC % 256 == 0 || s < HALO_VEC)
+        *reinterpret_cast<f32x4*>(&Hs[(s / (BK / HV)) * LDSR + (s % (BK / HV)) * HV]) = rh[i];
     }
 #pragma unroll
     for (int i = 0; i < W_PER; ++i) {
       const int s = tid + i * 256;
-      if (W_VEC % 256 == 0 || s < W_VEC) st4(&Ws[(s / (BK / 4)) * LDSR + (s % (BK / 4)) * 4], rw[i]);
+      if (W_VEC % 256 == 0 || s < W_VEC) {
+        lds_t* p = &Ws[(s / (BK / 4)) * LDSR + (s % (BK / 4)) * 4];
+        if constexpr (LP) *reinterpret_cast<bf16x4*>(p) = __builtin_convertvector(rw[i], bf16x4);
+        else *reinterpret_cast<f32x4*>(p) = rw[i];
+      }
     }
   };
 
@@ -120,6 +141,31 @@ __global__ __launch_bounds__(256) void halo3x3_kernel(HaloArgs a) {
     store();
     __syncthreads();
     if (kt + 1 < nk) load((kt + 1) * BK);
+    if constexpr (LP) {
+      const int lk8 = (lane >> 5) * 8;
+#pragma unroll
+      for (int tap = 0; tap < 9; ++tap) {
+        const int ky = tap / 3, kx = tap % 3;
+#pragma unroll
+        for (int ks = 0; ks < BK / 16; ++ks) {
+          bf16x8 af[2], bf[NI];
+#pragma unroll
+          for (int mi = 0; mi < 2; ++mi)
+            af[mi] = *reinterpret_cast<const bf16x8*>(
+                &Hs[((wave + ky) * HW + mi * 32 + lrow + kx) * LDSR + ks * 16 + lk8]);
+#pragma unroll
+          for (int ni = 0; ni < NI; ++ni)
+            bf[ni] = *reinterpret_cast<const bf16x8*>(&Ws[(tap * BNC + ni * 32 + lrow) * LDSR + ks * 16 + lk8]);
+#pragma unroll
+          for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+            for (int ni = 0; ni < NI; ++ni)
+              acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[mi], bf[ni], acc[mi][ni], 0, 0, 0);
+        }
+      }
+      __syncthreads();
+      continue;
+    }
 #pragma unroll
     for (int tap = 0; tap < 9; ++tap) {
       const int ky = tap / 3, kx = tap % 3;
@@ -128,9 +174,10 @@ __global__ __launch_bounds__(256) void halo3x3_kernel(HaloArgs a) {
         f32x4 af[2], bf[NI];
 #pragma unroll
         for (int mi = 0; mi < 2; ++mi)
-          af[mi] = ld4(&Hs[((wave + ky) * HW + mi * 32 + lrow + kx) * LDSR + ks * 8 + lk]);
+          af[mi] = *reinterpret_cast<const f32x4*>(&Hs[((wave + ky) * HW + mi * 32 + lrow + kx) * LDSR + ks * 8 + lk]);
 #pragma unroll
-        for (int ni = 0; ni < NI; ++ni) bf[ni] = ld4(&Ws[(tap * BNC + ni * 32 + lrow) * LDSR + ks * 8 + lk]);
+        for (int ni = 0; ni < NI; ++ni)
+          bf[ni] = *reinterpret_cast<const f32x4*>(&Ws[(tap * BNC + ni * 32 + lrow) * LDSR + ks * 8 + lk]);
 #pragma unroll
         for (int kk = 0; kk < 4; ++kk)
 #pragma unroll
@@ -157,8 +204,8 @@ __global__ __launch_bounds__(256) void halo3x3_kernel(HaloArgs a) {
   const long pix0 = ((long)n * a.H + h0 + wave) * a.W + w0;
   if (a.stat) {
     // BN partials of the 256-pixel tile: column sums, then M2 about the tile mean
-    float* red = Hs;                   // [4 waves][BNC]
-    float* tmean = Hs + 4 * BNC;       // [BNC]
+    float* red = reinterpret_cast<float*>(Hs);  // [4 waves][BNC]
+    float* tmean = red + 4 * BNC;               // [BNC]
     const long tile = lid;
 #pragma unroll
     for (int pass = 0; pass < 2; ++pass) {
@@ -196,8 +243,8 @@ __global__ __launch_bounds__(256) void halo3x3_kernel(HaloArgs a) {
       for (int r = 0; r < 16; ++r) {
         const long p = pix0 + mi * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
         float v = acc[mi][ni][r];
-        if (a.add) v += a.add[p * a.ldadd + col];
-        a.out[p * a.ldout + col] = v;
+        if (add) v += (float)add[p * a.ldadd + col];
+        out[p * a.ldout + col] = static_cast<T>(v);
       }
   }
 }
@@ -222,17 +269,34 @@ SEG_API int seg_conv_halo_row_tiles(int N, int H, int W) { return N * (H / TH) *
 
 // out = conv3x3(in, W) (+bias) (+add), stride 1, pad 1; wk packed by
 // seg_pack_conv_weight (mode 0 forward / mode 1 data gradient), ldk >= 9*Cin.
-SEG_API int seg_conv_halo(const float* in, long ldin, int N, int H, int W, int Cin, const float* wk, int ldk,
-                          const float* bias, float* out, long ldout, int Cout, const float* add, long ldadd,
-                          float* stat, hipStream_t stream) {
+template <typename T>
+static int conv_halo_impl(const T* in, long ldin, int N, int H, int W, int Cin, const float* wk, int ldk,
+                          const float* bias, T* out, long ldout, int Cout, const T* add, long ldadd, float* stat,
+                          hipStream_t stream) {
   if (!seg_conv_halo_ok(N, H, W, Cin, Cout) || (ldin & 3) || (ldk & 3) || ldk < 9 * Cin) return (int)hipErrorInvalidValue;
+  if (sizeof(T) == 2 && ((Cin & 7) || (ldin & 7))) return (int)hipErrorInvalidValue;  // 16-byte bf16 halo slots
   HaloArgs a;
   a.in = in; a.ldin = ldin; a.wk = wk; a.ldk = ldk; a.bias = bias; a.add = add; a.ldadd = ldadd;
   a.out = out; a.ldout = ldout; a.stat = stat; a.N = N; a.H = H; a.W = W; a.Cin = Cin; a.Cout = Cout;
   a.tiles_w = W / TW; a.tiles_h = H / TH;
   const int grid = N * a.tiles_h * a.tiles_w;
-  if (Cout <= 32) hipLaunchKernelGGL(halo3x3_kernel<1>, dim3(grid), dim3(256), 0, stream, a);
-  else if (Cout <= 64) hipLaunchKernelGGL(halo3x3_kernel<2>, dim3(grid), dim3(256), 0, stream, a);
-  else hipLaunchKernelGGL(halo3x3_kernel<3>, dim3(grid), dim3(256), 0, stream, a);
+  if (Cout <= 32) hipLaunchKernelGGL((halo3x3_kernel<1, T>), dim3(grid), dim3(256), 0, stream, a);
+  else if (Cout <= 64) hipLaunchKernelGGL((halo3x3_kernel<2, T>), dim3(grid), dim3(256), 0, stream, a);
+  else hipLaunchKernelGGL((halo3x3_kernel<3, T>), dim3(grid), dim3(256), 0, stream, a);
   SEG_RET_LAST();
+}
+
+SEG_API int seg_conv_halo(const float* in, long ldin, int N, int H, int W, int Cin, const float* wk, int ldk,
+                          const float* bias, float* out, long ldout, int Cout, const float* add, long ldadd,
+                          float* stat, hipStream_t stream) {
+  return conv_halo_impl(in, ldin, N, H, W, Cin, wk, ldk, bias, out, ldout, Cout, add, ldadd, stat, stream);
+}
+
+// seg_conv_halo on bf16 activation storage with bf16 math (the bf16io configuration):
+// bf16 operands, fp32 accumulation and epilogue, one rounding on the store.  Cin and
+// ldin multiples of 8.
+SEG_API int seg_conv_halo_bf16io(const __bf16* in, long ldin, int N, int H, int W, int Cin, const float* wk, int ldk,
+                                 const float* bias, __bf16* out, long ldout, int Cout, const __bf16* add, long ldadd,
+                                 float* stat, hipStream_t stream) {
+  return conv_halo_impl(in, ldin, N, H, W, Cin, wk, ldk, bias, out, ldout, Cout, add, ldadd, stat, stream);
 }

@@ -99,6 +99,7 @@ for _n in ("seg_add", "seg_bn_stats", "seg_bn_apply", "seg_bn_backward", "seg_co
     PROTOTYPES[_n + "_bf16io"] = PROTOTYPES[_n]
 PROTOTYPES["seg_conv_igemm_bf16io"] = PROTOTYPES["seg_conv_igemm"]
 PROTOTYPES["seg_conv_wgrad_bf16io"] = PROTOTYPES["seg_conv_wgrad"]
+PROTOTYPES["seg_conv_halo_bf16io"] = PROTOTYPES["seg_conv_halo"]
 
 _lock = threading.Lock()
 _lib = None

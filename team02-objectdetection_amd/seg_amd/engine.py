@@ -200,7 +200,7 @@ class ConvOp:
                 stat = rt.tmp(ntiles * 2 * self.cout)
             statp = stat.data_ptr() if stat is not None else None
             if self.halo_f:
-                _timed_call("igemm3_fwd", self.flops(), "seg_conv_halo", rt.ptr(i), i.ld, i.N, i.H, i.W, self.cin_pad,
+                _timed_call("igemm3_fwd", self.flops(), rt.k("seg_conv_halo"), rt.ptr(i), i.ld, i.N, i.H, i.W, self.cin_pad,
                             wk_ptr, ldk, bias, rt.ptr(y), y.ld, self.cout, None, 0, statp, s)
             elif self.wino_f:
                 work = rt.tmp(16 * (y.M // 4) * self.cout)
@@ -445,7 +445,7 @@ class ConvOp:
             kin = r4(self.cout)  # dY channels padded to 4 (the C=10 head)
             add_ptr, add_ld = rt.begin_write_add(i)
             if self.halo_d:
-                _timed_call("igemm3_dgrad", self.flops(), "seg_conv_halo", dYp, dY.ld, y.N, y.H, y.W, kin,
+                _timed_call("igemm3_dgrad", self.flops(), rt.k("seg_conv_halo"), dYp, dY.ld, y.N, y.H, y.W, kin,
                             self.wk_d.data_ptr(), self.ldk_d, None, rt.gptr(i), i.ld, self.cin, add_ptr, add_ld, None, s)
             elif self.wino_d:
                 work = rt.tmp(16 * (y.M // 4) * self.cin)
@@ -600,6 +600,12 @@ class Program:
                 # bf16 math: every dense / pointwise conv (fwd, dgrad, wgrad) on the bf16 implicit GEMM
                 op.pw_fused = op.bnb = False
                 op.wino_f = op.wino_d = op.wino_w = op.halo_f = op.halo_d = False
+                if self.math == "bf16io" and op.ks == 3 and op.stride == 1 and op.pad == 1:
+                    # LDS-halo direct conv on bf16 (seg_conv_halo_bf16io): narrow convs, 8-channel slots
+                    op.halo_f = (op.cin_pad % 8 == 0 and HALO_BF16
+                                 and bool(query("seg_conv_halo_pick", y.N, y.H, y.W, op.cin_pad, op.cout)))
+                    op.halo_d = (not op.first and r4(op.cout) % 8 == 0 and HALO_BF16
+                                 and bool(query("seg_conv_halo_pick", y.N, y.H, y.W, r4(op.cout), op.cin)))
                 if not (op.ks == 1 and op.cin_pad == op.cin):
                     op.ldk_f = r4(op.ks * op.ks * op.cin_pad)
                     op.wk_f = torch.empty(op.cout * op.ldk_f, device=dev, dtype=torch.float32)
@@ -1104,6 +1110,8 @@ class Run:
 # memory-bound BatchNorm / depthwise / 1x1 kernels of the main stream.  Results are the
 # same either way (the kernels and their reduction orders do not change).
 OVERLAP = os.environ.get("SEG_OVERLAP", "1") == "1"
+# LDS-halo direct 3x3 conv for the narrow convs in the bf16io configuration; SEG_HALO_BF16=0 turns it off.
+HALO_BF16 = os.environ.get("SEG_HALO_BF16", "1") == "1"
 # Fused BatchNorm-backward reductions (Program._plan_bn_red): parity-tested, but measured
 # no faster on MI355X in round 1 (f32 1707 vs 1711 img/s, bf16 2337 vs 2374: the y loads
 # in the data-gradient epilogue sit on the critical main stream, while the separate

@@ -249,3 +249,37 @@ def test_conv_bf16io(N, Cin, Cout, H, W, ks, stride):
     call("seg_conv_wgrad_bf16io", dy16.data_ptr(), Cout, x16.data_ptr(), Cin, N, H, W, Cin, H, W, Cout, ks, 1, pad,
          p16.data_ptr(), splits, s)
     assert torch.equal(p32, p16)
+
+
+@pytest.mark.parametrize("N,Cin,Cout,H,W", [(2, 80, 32, 8, 64), (1, 152, 64, 4, 128), (1, 32, 80, 8, 64),
+                                            (1, 16, 64, 4, 64)])
+def test_conv_halo_bf16io(N, Cin, Cout, H, W):
+    """The bf16 LDS-halo direct conv (narrow 3x3 convs of the bf16io configuration)
+    against a float64 conv of the same bf16 operands: the fp32 accumulation order differs
+    from the implicit GEMM's, so the check is one bf16 rounding of the exact result;
+    its BN-statistics partials (from the fp32 accumulators) to fp32 summation error."""
+    s = S()
+    x32, x16 = rows(N * H * W, Cin, 21)
+    a32, a16 = rows(N * H * W, Cout, 22)
+    w = (torch.randn(Cout, Cin, 3, 3, generator=torch.Generator().manual_seed(23)) * 0.1)
+    b = torch.randn(Cout, generator=torch.Generator().manual_seed(24))
+    ref = F.conv2d(x32.cpu().double().view(N, H, W, Cin).permute(0, 3, 1, 2),
+                   w.to(BF).double(), b.double(), padding=1)
+    ref = ref.permute(0, 2, 3, 1).reshape(-1, Cout) + a32.cpu().double()
+    wg = w.to(DEV)
+    ldk = r4(9 * Cin)
+    wk = torch.empty(Cout * ldk, device=DEV)
+    call("seg_pack_conv_weight", wg.data_ptr(), wk.data_ptr(), Cout, Cin, 3, ldk, 0, Cin, s)
+    ntiles = query("seg_conv_halo_row_tiles", N, H, W)
+    stat = torch.empty(ntiles * 2 * Cout, device=DEV)
+    out = torch.empty(N * H * W, Cout, device=DEV, dtype=BF)
+    call("seg_conv_halo_bf16io", x16.data_ptr(), Cin, N, H, W, Cin, wk.data_ptr(), ldk, b.to(DEV).data_ptr(),
+         out.data_ptr(), Cout, Cout, a16.data_ptr(), Cout, stat.data_ptr(), s)
+    got = out.double().cpu()
+    err = (got - ref).abs()
+    assert float(err.max()) <= float((ref.abs() * 2 ** -8 + 1e-6).max()) and \
+        bool((err <= ref.abs() * 2 ** -8 + 1e-6).all())
+    # tile sums are of acc + bias (before the addend), fp32
+    pre = ref - a32.cpu().double()
+    tile_sum = stat.view(ntiles, 2, Cout)[:, 0].sum(0).double().cpu()
+    assert float((tile_sum - pre.sum(0)).norm() / pre.sum(0).norm()) < 1e-4

@@ -89,6 +89,13 @@ PW_FUSED = os.environ.get("SEG_PW_FUSED", "0") == "1"
 BNB_ON_LOAD = os.environ.get("SEG_BNB", "0") == "1"
 
 
+def _stat_ptrs(st, C):
+    """Device pointers of the mean / invstd / scale / shift rows of a saved [4][C] BN
+    statistics tensor (no per-call view tensors on the host path)."""
+    b = st.data_ptr()
+    return b, b + 4 * C, b + 8 * C, b + 12 * C
+
+
 def _timed_call(kind, flops, name, *args):
     if TIMER is None or (TIMER.kinds is not None and kind not in TIMER.kinds):
         return call(name, *args)
@@ -223,7 +230,7 @@ class ConvOp:
             return
         bn, C, M = self.bn, self.cout, y.M
         st = torch.empty(4 * C, device=rt.device, dtype=torch.float32)
-        mean, invstd, scale, shift = (st[k * C:(k + 1) * C] for k in range(4))
+        mean, invstd, scale, shift = _stat_ptrs(st, C)
         if rt.training:
             if bn.momentum is None:
                 raise NotImplementedError("BatchNorm2d(momentum=None) (cumulative average) is not supported")
@@ -233,20 +240,20 @@ class ConvOp:
             if self.kind == "dw":
                 work = rt.tmp(query("seg_chan_workspace_floats", M, C))
                 call(rt.k("seg_bn_stats"), rt.ptr(y), y.ld, M, C, bn.weight.data_ptr(), bn.bias.data_ptr(), bn.eps,
-                     bn.momentum, rm, rv, nbt, work.data_ptr(), mean.data_ptr(), invstd.data_ptr(),
-                     scale.data_ptr(), shift.data_ptr(), s)
+                     bn.momentum, rm, rv, nbt, work.data_ptr(), mean, invstd,
+                     scale, shift, s)
             else:
                 call("seg_bn_stats_tiles", stat.data_ptr(), ntiles, tile_rows, M, C, bn.weight.data_ptr(),
-                     bn.bias.data_ptr(), bn.eps, bn.momentum, rm, rv, nbt, mean.data_ptr(), invstd.data_ptr(),
-                     scale.data_ptr(), shift.data_ptr(), s)
+                     bn.bias.data_ptr(), bn.eps, bn.momentum, rm, rv, nbt, mean, invstd,
+                     scale, shift, s)
         else:
             call("seg_bn_eval_coef", bn.weight.data_ptr(), bn.bias.data_ptr(), bn.running_mean.data_ptr(),
-                 bn.running_var.data_ptr(), bn.eps, C, scale.data_ptr(), shift.data_ptr(), s)
+                 bn.running_var.data_ptr(), bn.eps, C, scale, shift, s)
         rt.saved[id(self)] = st
         if self.lazy:
             return
         o, r = self.out, self.res
-        call(rt.k("seg_bn_apply"), rt.ptr(y), y.ld, M, C, scale.data_ptr(), shift.data_ptr(), self.act,
+        call(rt.k("seg_bn_apply"), rt.ptr(y), y.ld, M, C, scale, shift, self.act,
              rt.ptr(r) if r is not None else None, r.ld if r is not None else 0, rt.ptr(o), o.ld, s)
 
     # -- inference (BatchNorm folded into the conv: Program.fold)
@@ -280,15 +287,15 @@ class ConvOp:
         s, y, i = rt.stream, self.y, self.inp
         C, M = self.cout, y.M
         st = rt.saved[id(self)]
-        mean, invstd, scale, shift = (st[k * C:(k + 1) * C] for k in range(4))
+        mean, invstd, scale, shift = _stat_ptrs(st, C)
         work = rt.tmp(query("seg_chan_workspace_floats", M, C))
         coef = rt.tmp(3 * C)
         call("seg_bn_backward_coef", rt.gptr(dA), dA.ld, rt.ptr(y), y.ld, M, C, self.bn.weight.data_ptr(),
-             mean.data_ptr(), invstd.data_ptr(), scale.data_ptr(), shift.data_ptr(), self.act,
+             mean, invstd, scale, shift, self.act,
              rt.grad_param(self.bn.weight), rt.grad_param(self.bn.bias), work.data_ptr(), coef.data_ptr(), s)
         if self.res is not None:
             rt.add_pending(self.res, dA)
-        bn = (rt.ptr(y), y.ld, scale.data_ptr(), shift.data_ptr(), mean.data_ptr(), coef.data_ptr(), self.act)
+        bn = (rt.ptr(y), y.ld, scale, shift, mean, coef.data_ptr(), self.act)
         if rt.side is not None:
             coef.record_stream(rt.side)  # read by the side stream after this function drops it
         for p in (self.conv.weight, self.conv.bias):
@@ -298,8 +305,8 @@ class ConvOp:
         with ctx:
             if self.conv.bias is not None and self.conv.bias.requires_grad:
                 wk = rt.tmp(query("seg_chan_workspace_floats", M, C))
-                call("seg_colsum_bnb", rt.gptr(dA), dA.ld, rt.ptr(y), y.ld, M, C, scale.data_ptr(), shift.data_ptr(),
-                     mean.data_ptr(), coef.data_ptr(), self.act, wk.data_ptr(), rt.grad_param(self.conv.bias), 0, sw)
+                call("seg_colsum_bnb", rt.gptr(dA), dA.ld, rt.ptr(y), y.ld, M, C, scale, shift,
+                     mean, coef.data_ptr(), self.act, wk.data_ptr(), rt.grad_param(self.conv.bias), 0, sw)
             if self.conv.weight.requires_grad:
                 gw = rt.grad_param(self.conv.weight)
                 splits = query("seg_conv_wgrad_splits", M, C, self.cin_pad, self.ks)
@@ -325,11 +332,11 @@ class ConvOp:
             raise NotImplementedError("backward through eval-mode BatchNorm is not supported")
         C, M = self.cout, y.M
         st = rt.saved[id(self)]
-        mean, invstd, scale, shift = (st[k * C:(k + 1) * C] for k in range(4))
+        mean, invstd, scale, shift = _stat_ptrs(st, C)
         work = rt.tmp(query("seg_chan_workspace_floats", M, C))
         coef = rt.tmp(3 * C)
         call("seg_bn_backward_coef", rt.gptr(dA), dA.ld, rt.ptr(y), y.ld, M, C, self.bn.weight.data_ptr(),
-             mean.data_ptr(), invstd.data_ptr(), scale.data_ptr(), shift.data_ptr(), self.act,
+             mean, invstd, scale, shift, self.act,
              rt.grad_param(self.bn.weight), rt.grad_param(self.bn.bias), work.data_ptr(), coef.data_ptr(), s)
         if self.res is not None:
             rt.add_pending(self.res, dA)
@@ -338,7 +345,7 @@ class ConvOp:
         part = rt.tmp(blocks * C * self.cin_pad)
         add_ptr, add_ld = rt.begin_write_add(i)
         _timed_call("pw_bwd", 2 * self.flops(), "seg_pw_bwd_fused", rt.gptr(dA), dA.ld, rt.ptr(y), y.ld, rt.ptr(i),
-                    i.ld, self.wk_d.data_ptr(), self.ldk_d, scale.data_ptr(), shift.data_ptr(), mean.data_ptr(),
+                    i.ld, self.wk_d.data_ptr(), self.ldk_d, scale, shift, mean,
                     coef.data_ptr(), self.act, add_ptr, add_ld, rt.gptr(i), i.ld, part.data_ptr(), blocks, M,
                     self.cin, C, s)
         call("seg_conv_wgrad_reduce", part.data_ptr(), blocks, gw, C, self.cin, 1, 0, 0, s)
@@ -366,7 +373,7 @@ class ConvOp:
                 raise NotImplementedError("backward through eval-mode BatchNorm is not supported")
             C, M = self.cout, y.M
             st = rt.saved[id(self)]
-            mean, invstd, scale, shift = (st[k * C:(k + 1) * C] for k in range(4))
+            mean, invstd, scale, shift = _stat_ptrs(st, C)
             dY = Act(rt.tmp_buf(M * r4(C)), 0, r4(C), C, y.N, y.H, y.W)
             g_w, g_b = rt.grad_param(self.bn.weight), rt.grad_param(self.bn.bias)
             parts = rt.bnred.pop(id(self), None)
@@ -374,12 +381,12 @@ class ConvOp:
                 part, nparts = parts
                 coef = rt.tmp(3 * C)
                 call("seg_bn_backward_parts", part.data_ptr(), nparts, rt.gptr(dA), dA.ld, rt.ptr(y), y.ld, M, C,
-                     self.bn.weight.data_ptr(), mean.data_ptr(), invstd.data_ptr(), scale.data_ptr(),
-                     shift.data_ptr(), self.act, g_w, g_b, coef.data_ptr(), rt.ptr(dY), dY.ld, s)
+                     self.bn.weight.data_ptr(), mean, invstd, scale,
+                     shift, self.act, g_w, g_b, coef.data_ptr(), rt.ptr(dY), dY.ld, s)
             else:
                 work = rt.tmp(query("seg_chan_workspace_floats", M, C) + 3 * C)
                 call(rt.k("seg_bn_backward"), rt.gptr(dA), dA.ld, rt.ptr(y), y.ld, M, C, self.bn.weight.data_ptr(),
-                     mean.data_ptr(), invstd.data_ptr(), scale.data_ptr(), shift.data_ptr(), self.act,
+                     mean, invstd, scale, shift, self.act,
                      g_w, g_b, work.data_ptr(), rt.ptr(dY), dY.ld, s)
             if self.res is not None:
                 rt.add_pending(self.res, dA)
@@ -1002,7 +1009,7 @@ class Run:
         self._n_fork += 1
         ev.record(self.main)
         self.side.wait_event(ev)
-        return torch.cuda.stream(self.side), self.side.cuda_stream
+        return self._side_ctx, self.side.cuda_stream
 
     def join(self):
         if self.side is not None:
@@ -1096,6 +1103,7 @@ class Run:
         if OVERLAP:
             self.main = torch.cuda.current_stream(self.device)
             self.side = _side_stream(self.device)
+            self._side_ctx = torch.cuda.StreamContext(self.side)  # re-entered by every fork
         try:
             for op in reversed(self.prog.ops):
                 op.backward(self)

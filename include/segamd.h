@@ -222,6 +222,8 @@ int seg_bn_backward_parts(const float* part, int nparts, const float* da, long l
                           float* coef, float* dy, long lddy, hipStream_t stream);
 /* ---- BatchNorm2d + activation (aten native_batch_norm(+_backward), hardtanh,
  *      threshold; src/unet.py:59-63,114-115 and torchvision norms) ----------- */
+/* partial-sum workspace (floats) of the channel reductions over [M][C]; the
+ * partition depends on M and C (seg_colsum: pass round_up(C, 4)) */
 long seg_chan_workspace_floats(long M, int C);
 int seg_bn_stats(const float* y, long ldy, long M, int C, const float* gamma, const float* beta,
                  float eps, float momentum, float* running_mean, float* running_var,
@@ -249,7 +251,7 @@ int seg_bn_backward_coef(const float* da, long ldda, const float* y, long ldy, l
 int seg_bn_eval_backward(const float* da, long ldda, const float* y, long ldy, long M, int C,
                          const float* scale, const float* shift, int act, float* dy, long lddy,
                          hipStream_t stream);
-/* conv bias gradient: out[c] (+)= sum_r y[r][c] */
+/* conv bias gradient: out[c] (+)= sum_r y[r][c]; work >= seg_chan_workspace_floats(M, round_up(C, 4)) */
 int seg_colsum(const float* y, long ldy, long M, int C, float* work, float* out, int accumulate,
                hipStream_t stream);
 /* seg_colsum of dY formed on load from dA and y (BN backward; C % 4 == 0). */

@@ -17,6 +17,13 @@
 
 namespace {
 
+// Wide layers (C >= 256: the encoder's 384..1280-channel tensors at 8x16 / 16x32, M =
+// 4096 / 16384) split their channels over blockIdx.y in slices of kChanSlice float4
+// groups (chan_split), so a block has 8 row lanes instead of 1-2 (which walked 32 rows
+// serially: latency-bound 15-25 us launches).  The partial layout [row block][2][C]
+// and the workspace size do not depend on the split.
+constexpr int kChanSlice = 32;
+
 // Per-block partial sums over a row range for float4 channel groups.
 // Block = 256 threads laid out as RG row-lanes x TC channel-group lanes.
 // kind 0: (sum(y-k), sum((y-k)^2)),  k = y[0][c]                   -> BN stats
@@ -29,8 +36,11 @@ __global__ __launch_bounds__(256) void chan_partial_kernel(
     const float* __restrict__ scale, const float* __restrict__ shift, const float* __restrict__ mean, int act,
     float* __restrict__ part, int rows_per_block, SegBnBwd bnb) {
   __shared__ f32x4 red0[256], red1[256];
-  const int CG = C >> 2;
-  const int TC = CG < 256 ? CG : 256;
+  // channel slice of this block (blockIdx.y; chan_split): CGB groups from cg0
+  const int CGB = gridDim.y > 1 ? kChanSlice : (C >> 2);
+  const int cg0 = blockIdx.y * CGB;
+  const int CG = min((C >> 2) - cg0, CGB);
+  const int TC = CGB < 256 ? CGB : 256;
   const int RG = 256 / TC;
   const int t = threadIdx.x;
   const int rg = t / TC, tc = t - rg * TC;
@@ -42,8 +52,8 @@ __global__ __launch_bounds__(256) void chan_partial_kernel(
     const int cg = cgb + tc;
     const bool active = rg < RG && cg < CG;
     f32x4 s0 = {0.f, 0.f, 0.f, 0.f}, s1 = {0.f, 0.f, 0.f, 0.f};
+    const int c = (cg0 + cg) * 4;
     if (active) {
-      const int c = cg * 4;
       f32x4 k = {0.f, 0.f, 0.f, 0.f}, sc = k, sh = k;
       if (KIND == 0) k = ld4(y + c);
       if (KIND == 1) { k = ld4(mean + c); sc = ld4(scale + c); sh = ld4(shift + c); }
@@ -95,18 +105,24 @@ __global__ __launch_bounds__(256) void chan_partial_kernel(
       __syncthreads();
     }
     if (rg == 0 && active) {
-      st4(p0 + cg * 4, red0[tc]);
-      st4(p1 + cg * 4, red1[tc]);
+      st4(p0 + c, red0[tc]);
+      st4(p1 + c, red1[tc]);
     }
     __syncthreads();
   }
 }
 
-int rows_per_block_for(long M) {
-  // ~2048 blocks (8 per CU: latency hiding for the 2-load streams), >= 32 rows each
+int rows_per_block_for(long M, int C) {
+  // ~2048 row blocks (8 per CU: latency hiding for the 2-load streams), >= 32 rows each
+  (void)C;
   long r = (M + 2047) / 2048;
   if (r < 32) r = 32;
   return (int)r;
+}
+
+int chan_split(int C) {
+  const int CG = C >> 2;
+  return CG >= 64 ? seg_cdiv(CG, kChanSlice) : 1;
 }
 
 // Sum the per-block partials of channel c = blockIdx.x with the whole 256-thread
@@ -324,14 +340,208 @@ __global__ void add_kernel(const T* __restrict__ a, long lda, const T* __restric
   }
 }
 
+// Row-tiled elementwise passes (BN apply, BN backward apply, gradient add).  A
+// 256-thread block is RG row lanes x TC channel-group lanes; each lane keeps its
+// VW-channel group (one 16-byte access: 4 fp32 or 8 bf16 channels) and its
+// per-channel coefficients in registers and strides over rows, two rows per trip so
+// both rows' loads are in flight together.  No per-element index division and no
+// per-element coefficient loads; the arithmetic per element is the flat kernels'
+// (seg_bn_act4 / seg_bnbwd4), so results are bitwise those of the flat kernels.
+// Launched for the 16-byte bf16 layout (8 channels per lane); the 4-channel layouts
+// keep the flat kernels, which measured 2-7 % faster than these on fp32 (MI355X).
+template <int VW, typename T>
+__device__ __forceinline__ void ldv(const T* p, f32x4* o) {
+  if constexpr (VW == 8) {
+    const bf16x8 v = *reinterpret_cast<const bf16x8*>(p);
+    o[0] = __builtin_convertvector(__builtin_shufflevector(v, v, 0, 1, 2, 3), f32x4);
+    o[1] = __builtin_convertvector(__builtin_shufflevector(v, v, 4, 5, 6, 7), f32x4);
+  } else {
+    o[0] = ld4(p);
+  }
+}
+template <int VW, typename T>
+__device__ __forceinline__ void stv(T* p, const f32x4* o) {
+  if constexpr (VW == 8) {
+    const bf16x4 lo = __builtin_convertvector(o[0], bf16x4), hi = __builtin_convertvector(o[1], bf16x4);
+    *reinterpret_cast<bf16x8*>(p) = seg_cat8(lo, hi);
+  } else {
+    st4(p, o[0]);
+  }
+}
+template <int NV>
+__device__ __forceinline__ void ldc(const float* p, f32x4* o) {
+#pragma unroll
+  for (int j = 0; j < NV; ++j) o[j] = ld4(p + 4 * j);
+}
+
+struct RowTile {
+  int CG, TC, RG, rg, tc;
+  __device__ RowTile(int C, int VW) {
+    CG = C / VW;
+    TC = CG < 256 ? CG : 256;
+    RG = 256 / TC;
+    rg = threadIdx.x / TC;
+    tc = threadIdx.x - rg * TC;
+  }
+};
+
+template <typename T, int VW>
+__global__ __launch_bounds__(256) void bn_apply_rt_kernel(const T* __restrict__ y, long ldy, long M, int C,
+                                                          const float* __restrict__ scale,
+                                                          const float* __restrict__ shift, int act,
+                                                          const T* __restrict__ res, long ldres, T* out, long ldout) {
+  constexpr int NV = VW / 4;
+  const RowTile rt(C, VW);
+  if (rt.rg >= rt.RG) return;
+  const long step = (long)gridDim.x * rt.RG;
+  for (int cg = rt.tc; cg < rt.CG; cg += rt.TC) {
+    const int c = cg * VW;
+    f32x4 sc[NV], sh[NV];
+    ldc<NV>(scale + c, sc);
+    ldc<NV>(shift + c, sh);
+    long r = (long)blockIdx.x * rt.RG + rt.rg;
+    for (; r + step < M; r += 2 * step) {
+      f32x4 v0[NV], v1[NV], q0[NV], q1[NV];
+      ldv<VW>(y + r * ldy + c, v0);
+      ldv<VW>(y + (r + step) * ldy + c, v1);
+      if (res) {
+        ldv<VW>(res + r * ldres + c, q0);
+        ldv<VW>(res + (r + step) * ldres + c, q1);
+      }
+#pragma unroll
+      for (int j = 0; j < NV; ++j) {
+        v0[j] = seg_bn_act4(v0[j], sc[j], sh[j], act);
+        v1[j] = seg_bn_act4(v1[j], sc[j], sh[j], act);
+        if (res) {
+          v0[j] += q0[j];
+          v1[j] += q1[j];
+        }
+      }
+      stv<VW>(out + r * ldout + c, v0);
+      stv<VW>(out + (r + step) * ldout + c, v1);
+    }
+    if (r < M) {
+      f32x4 v0[NV], q0[NV];
+      ldv<VW>(y + r * ldy + c, v0);
+      if (res) ldv<VW>(res + r * ldres + c, q0);
+#pragma unroll
+      for (int j = 0; j < NV; ++j) {
+        v0[j] = seg_bn_act4(v0[j], sc[j], sh[j], act);
+        if (res) v0[j] += q0[j];
+      }
+      stv<VW>(out + r * ldout + c, v0);
+    }
+  }
+}
+
+template <typename T, int VW>
+__global__ __launch_bounds__(256) void bn_bwd_apply_rt_kernel(const T* __restrict__ da, long ldda,
+                                                              const T* __restrict__ y, long ldy, long M, int C,
+                                                              const float* __restrict__ scale,
+                                                              const float* __restrict__ shift,
+                                                              const float* __restrict__ mean, int act,
+                                                              const float* __restrict__ coef, T* dy, long lddy) {
+  constexpr int NV = VW / 4;
+  const RowTile rt(C, VW);
+  if (rt.rg >= rt.RG) return;
+  const long step = (long)gridDim.x * rt.RG;
+  for (int cg = rt.tc; cg < rt.CG; cg += rt.TC) {
+    const int c = cg * VW;
+    f32x4 sc[NV], sh[NV], mu[NV], k1[NV], k2[NV], k3[NV];
+    ldc<NV>(scale + c, sc);
+    ldc<NV>(shift + c, sh);
+    ldc<NV>(mean + c, mu);
+    ldc<NV>(coef + c, k1);
+    ldc<NV>(coef + C + c, k2);
+    ldc<NV>(coef + 2 * C + c, k3);
+    long r = (long)blockIdx.x * rt.RG + rt.rg;
+    for (; r + step < M; r += 2 * step) {
+      f32x4 v0[NV], v1[NV], g0[NV], g1[NV];
+      ldv<VW>(y + r * ldy + c, v0);
+      ldv<VW>(da + r * ldda + c, g0);
+      ldv<VW>(y + (r + step) * ldy + c, v1);
+      ldv<VW>(da + (r + step) * ldda + c, g1);
+#pragma unroll
+      for (int j = 0; j < NV; ++j) {
+        v0[j] = seg_bnbwd4(g0[j], v0[j], sc[j], sh[j], mu[j], k1[j], k2[j], k3[j], act);
+        v1[j] = seg_bnbwd4(g1[j], v1[j], sc[j], sh[j], mu[j], k1[j], k2[j], k3[j], act);
+      }
+      stv<VW>(dy + r * lddy + c, v0);
+      stv<VW>(dy + (r + step) * lddy + c, v1);
+    }
+    if (r < M) {
+      f32x4 v0[NV], g0[NV];
+      ldv<VW>(y + r * ldy + c, v0);
+      ldv<VW>(da + r * ldda + c, g0);
+#pragma unroll
+      for (int j = 0; j < NV; ++j) v0[j] = seg_bnbwd4(g0[j], v0[j], sc[j], sh[j], mu[j], k1[j], k2[j], k3[j], act);
+      stv<VW>(dy + r * lddy + c, v0);
+    }
+  }
+}
+
+template <typename T, int VW>
+__global__ __launch_bounds__(256) void add_rt_kernel(const T* a, long lda, const T* b, long ldb, long M, int C,
+                                                     T* out, long ldout) {
+  constexpr int NV = VW / 4;
+  const RowTile rt(C, VW);
+  if (rt.rg >= rt.RG) return;
+  const long step = (long)gridDim.x * rt.RG;
+  for (int cg = rt.tc; cg < rt.CG; cg += rt.TC) {
+    const int c = cg * VW;
+    for (long r = (long)blockIdx.x * rt.RG + rt.rg; r < M; r += step) {
+      f32x4 v[NV], q[NV];
+      ldv<VW>(a + r * lda + c, v);
+      if (b) {
+        ldv<VW>(b + r * ldb + c, q);
+#pragma unroll
+        for (int j = 0; j < NV; ++j) v[j] += q[j];
+      }
+      stv<VW>(out + r * ldout + c, v);
+    }
+  }
+}
+
+// Channels per lane for the row-tiled passes: 8 for bf16 storage when every channel
+// offset, row stride and pointer allows 16-byte accesses, else 4.
+template <typename T>
+int rt_vw(int C, std::initializer_list<long> lds, std::initializer_list<const void*> ptrs) {
+  if (sizeof(T) != 2 || C % 8) return 4;
+  for (long ld : lds) if (ld % 8) return 4;
+  for (const void* p : ptrs) if (p && ((uintptr_t)p & 15)) return 4;
+  return 8;
+}
+int rt_grid(long M, int C, int VW) {
+  const int CG = C / VW, TC = CG < 256 ? CG : 256, RG = 256 / TC;
+  return (int)std::max<long>(1, std::min<long>(seg_cdiv(M, RG), 4096));
+}
+
+template <typename T>
+void launch_bn_bwd_apply(const T* da, long ldda, const T* y, long ldy, long M, int C, const float* scale,
+                         const float* shift, const float* mean, int act, const float* coef, T* dy, long lddy,
+                         hipStream_t stream) {
+  if (M < 1) return;
+  if (rt_vw<T>(C, {ldda, ldy, lddy}, {da, y, dy}) == 8)
+    hipLaunchKernelGGL((bn_bwd_apply_rt_kernel<T, 8>), dim3(rt_grid(M, C, 8)), dim3(256), 0, stream, da, ldda, y, ldy,
+                       M, C, scale, shift, mean, act, coef, dy, lddy);
+  else
+    hipLaunchKernelGGL(bn_bwd_apply_kernel<T>, dim3(ew_grid(M * (C / 4))), dim3(256), 0, stream, da, ldda, y, ldy, M,
+                       C, scale, shift, mean, act, coef, dy, lddy);
+}
+
 }  // namespace
 
 // out = a (+ b), all [M][C] NHWC strided (out may alias a or b).  Gradient fan-in.
 template <typename T>
 static int add_impl(const T* a, long lda, const T* b, long ldb, long M, int C, T* out, long ldout, hipStream_t stream) {
   if ((C & 3) || (lda & 3) || (ldout & 3) || (b && (ldb & 3))) return (int)hipErrorInvalidValue;
-  hipLaunchKernelGGL(add_kernel<T>, dim3(ew_grid(M * (C / 4))), dim3(256), 0, stream, a, lda, b, ldb, M, C, out,
-                     ldout);
+  if (M < 1) return (int)hipSuccess;
+  if (rt_vw<T>(C, {lda, b ? ldb : 0, ldout}, {a, b, out}) == 8)
+    hipLaunchKernelGGL((add_rt_kernel<T, 8>), dim3(rt_grid(M, C, 8)), dim3(256), 0, stream, a, lda, b, ldb, M, C,
+                       out, ldout);
+  else
+    hipLaunchKernelGGL(add_kernel<T>, dim3(ew_grid(M * (C / 4))), dim3(256), 0, stream, a, lda, b, ldb, M, C, out,
+                       ldout);
   SEG_RET_LAST();
 }
 SEG_API int seg_add(const float* a, long lda, const float* b, long ldb, long M, int C, float* out, long ldout,
@@ -348,7 +558,7 @@ SEG_API int seg_add_bf16io(const __bf16* a, long lda, const __bf16* b, long ldb,
 
 // Size (floats) of the partial-sum workspace the channel reductions below need.
 SEG_API long seg_chan_workspace_floats(long M, int C) {
-  const int rpb = rows_per_block_for(M);
+  const int rpb = rows_per_block_for(M, C);
   return (long)seg_cdiv(M, rpb) * 2 * C;
 }
 
@@ -359,9 +569,9 @@ static int bn_stats_impl(const T* y, long ldy, long M, int C, const float* gamma
                          float momentum, float* running_mean, float* running_var, long long* num_batches_tracked,
                          float* work, float* mean, float* invstd, float* scale, float* shift, hipStream_t stream) {
   if ((C & 3) || (ldy & 3) || M < 1) return (int)hipErrorInvalidValue;
-  const int rpb = rows_per_block_for(M);
+  const int rpb = rows_per_block_for(M, C);
   const int nblk = seg_cdiv(M, rpb);
-  hipLaunchKernelGGL((chan_partial_kernel<0, T>), dim3(nblk), dim3(256), 0, stream, y, ldy, (const T*)nullptr, 0L,
+  hipLaunchKernelGGL((chan_partial_kernel<0, T>), dim3(nblk, chan_split(C)), dim3(256), 0, stream, y, ldy, (const T*)nullptr, 0L,
                      (int)M, C, nullptr, nullptr, nullptr, 0, work, rpb, SegBnBwd{});
   hipLaunchKernelGGL(bn_finalize_kernel<T>, dim3(C), dim3(256), 0, stream, work, nblk, y, M, C, gamma,
                      beta, eps, momentum, running_mean, running_var, num_batches_tracked, mean, invstd, scale, shift);
@@ -407,8 +617,13 @@ template <typename T>
 static int bn_apply_impl(const T* y, long ldy, long M, int C, const float* scale, const float* shift, int act,
                          const T* res, long ldres, T* out, long ldout, hipStream_t stream) {
   if ((C & 3) || (ldy & 3) || (ldout & 3) || (res && (ldres & 3))) return (int)hipErrorInvalidValue;
-  hipLaunchKernelGGL(bn_apply_kernel<T>, dim3(ew_grid(M * (C / 4))), dim3(256), 0, stream, y, ldy, M, C, scale, shift,
-                     act, res, ldres, out, ldout);
+  if (M < 1) return (int)hipSuccess;
+  if (rt_vw<T>(C, {ldy, res ? ldres : 0, ldout}, {y, res, out}) == 8)
+    hipLaunchKernelGGL((bn_apply_rt_kernel<T, 8>), dim3(rt_grid(M, C, 8)), dim3(256), 0, stream, y, ldy, M, C, scale,
+                       shift, act, res, ldres, out, ldout);
+  else
+    hipLaunchKernelGGL(bn_apply_kernel<T>, dim3(ew_grid(M * (C / 4))), dim3(256), 0, stream, y, ldy, M, C, scale,
+                       shift, act, res, ldres, out, ldout);
   SEG_RET_LAST();
 }
 SEG_API int seg_bn_apply(const float* y, long ldy, long M, int C, const float* scale, const float* shift, int act,
@@ -427,15 +642,14 @@ static int bn_backward_impl(const T* da, long ldda, const T* y, long ldy, long M
                             const float* mean, const float* invstd, const float* scale, const float* shift, int act,
                             float* dgamma, float* dbeta, float* work, T* dy, long lddy, hipStream_t stream) {
   if ((C & 3) || (ldy & 3) || (ldda & 3) || (lddy & 3)) return (int)hipErrorInvalidValue;
-  const int rpb = rows_per_block_for(M);
+  const int rpb = rows_per_block_for(M, C);
   const int nblk = seg_cdiv(M, rpb);
   float* coef = work + (long)nblk * 2 * C;
-  hipLaunchKernelGGL((chan_partial_kernel<1, T>), dim3(nblk), dim3(256), 0, stream, y, ldy, da, ldda, (int)M, C, scale,
+  hipLaunchKernelGGL((chan_partial_kernel<1, T>), dim3(nblk, chan_split(C)), dim3(256), 0, stream, y, ldy, da, ldda, (int)M, C, scale,
                      shift, mean, act, work, rpb, SegBnBwd{});
   hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(C), dim3(256), 0, stream, work, nblk, M, C, gamma,
                      invstd, dgamma, dbeta, coef);
-  hipLaunchKernelGGL(bn_bwd_apply_kernel<T>, dim3(ew_grid(M * (C / 4))), dim3(256), 0, stream, da, ldda, y, ldy, M,
-                     C, scale, shift, mean, act, coef, dy, lddy);
+  launch_bn_bwd_apply<T>(da, ldda, y, ldy, M, C, scale, shift, mean, act, coef, dy, lddy, stream);
   SEG_RET_LAST();
 }
 SEG_API int seg_bn_backward(const float* da, long ldda, const float* y, long ldy, long M, int C, const float* gamma,
@@ -462,8 +676,7 @@ SEG_API int seg_bn_backward_parts(const float* part, int nparts, const float* da
   if ((C & 3) || (ldy & 3) || (ldda & 3) || (lddy & 3) || nparts < 1) return (int)hipErrorInvalidValue;
   hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(C), dim3(256), 0, stream, part, nparts, M, C, gamma,
                      invstd, dgamma, dbeta, coef);
-  hipLaunchKernelGGL(bn_bwd_apply_kernel<float>, dim3(ew_grid(M * (C / 4))), dim3(256), 0, stream, da, ldda, y, ldy, M, C,
-                     scale, shift, mean, act, coef, dy, lddy);
+  launch_bn_bwd_apply<float>(da, ldda, y, ldy, M, C, scale, shift, mean, act, coef, dy, lddy, stream);
   SEG_RET_LAST();
 }
 
@@ -476,9 +689,9 @@ SEG_API int seg_bn_backward_coef(const float* da, long ldda, const float* y, lon
                                  const float* shift, int act, float* dgamma, float* dbeta, float* work, float* coef,
                                  hipStream_t stream) {
   if ((C & 3) || (ldy & 3) || (ldda & 3)) return (int)hipErrorInvalidValue;
-  const int rpb = rows_per_block_for(M);
+  const int rpb = rows_per_block_for(M, C);
   const int nblk = seg_cdiv(M, rpb);
-  hipLaunchKernelGGL((chan_partial_kernel<1, float>), dim3(nblk), dim3(256), 0, stream, y, ldy, da, ldda, (int)M, C, scale,
+  hipLaunchKernelGGL((chan_partial_kernel<1, float>), dim3(nblk, chan_split(C)), dim3(256), 0, stream, y, ldy, da, ldda, (int)M, C, scale,
                      shift, mean, act, work, rpb, SegBnBwd{});
   hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(C), dim3(256), 0, stream, work, nblk, M, C, gamma,
                      invstd, dgamma, dbeta, coef);
@@ -499,9 +712,9 @@ SEG_API int seg_colsum_bnb(const float* da, long ldda, const float* y, long ldy,
                            const float* shift, const float* mean, const float* k, int bn_act, float* work, float* out,
                            int accumulate, hipStream_t stream) {
   if ((C & 3) || (ldy & 3) || (ldda & 3) || !k) return (int)hipErrorInvalidValue;
-  const int rpb = rows_per_block_for(M);
+  const int rpb = rows_per_block_for(M, C);
   const int nblk = seg_cdiv(M, rpb);
-  hipLaunchKernelGGL((chan_partial_kernel<3, float>), dim3(nblk), dim3(256), 0, stream, y, ldy, da, ldda, (int)M, C, nullptr,
+  hipLaunchKernelGGL((chan_partial_kernel<3, float>), dim3(nblk, chan_split(C)), dim3(256), 0, stream, y, ldy, da, ldda, (int)M, C, nullptr,
                      nullptr, nullptr, 0, work, rpb, SegBnBwd{y, ldy, scale, shift, mean, k, C, bn_act});
   hipLaunchKernelGGL(colsum_finalize_kernel, dim3(C), dim3(256), 0, stream, work, nblk, C, C, out, accumulate);
   SEG_RET_LAST();
@@ -513,9 +726,9 @@ static int colsum_impl(const T* y, long ldy, long M, int C, float* work, float* 
                        hipStream_t stream) {
   if ((ldy & 3)) return (int)hipErrorInvalidValue;
   const int C4 = (C + 3) & ~3;  // ld >= C4 is guaranteed by the buffer contract
-  const int rpb = rows_per_block_for(M);
+  const int rpb = rows_per_block_for(M, C4);  // the workspace is seg_chan_workspace_floats(M, C4)
   const int nblk = seg_cdiv(M, rpb);
-  hipLaunchKernelGGL((chan_partial_kernel<2, T>), dim3(nblk), dim3(256), 0, stream, y, ldy, (const T*)nullptr, 0L,
+  hipLaunchKernelGGL((chan_partial_kernel<2, T>), dim3(nblk, chan_split(C4)), dim3(256), 0, stream, y, ldy, (const T*)nullptr, 0L,
                      (int)M, C4, nullptr, nullptr, nullptr, 0, work, rpb, SegBnBwd{});
   hipLaunchKernelGGL(colsum_finalize_kernel, dim3(C), dim3(256), 0, stream, work, nblk, C, C4, out,
                      accumulate);

@@ -95,6 +95,85 @@ def test_add_apply_stats_backward_colsum():
     assert torch.equal(cs["f"], cs["b"])
 
 
+@pytest.mark.parametrize("M,C,ld,off", [(3001, 12, 16, 4), (517, 1280, 1280, 0), (33, 2064, 2064, 0),
+                                         (1000, 40, 48, 8), (1, 8, 8, 0)])
+def test_row_tiled_passes(M, C, ld, off):
+    """The row-tiled BN apply / BN backward apply / add kernels over the layouts their
+    launchers pick between: 8 bf16 channels per lane (C % 8 == 0, 16-byte aligned
+    slices), the 4-channel fallback (C = 12; a channel slice at an 8-byte offset), more
+    channel groups than lanes (C = 1280 fp32, C = 2064 bf16), row strides > C, M = 1.
+    fp32 against the torch formula; bf16io bitwise against the fp32 kernel; in-place
+    apply bitwise against out-of-place; channels outside the slice untouched."""
+    s = S()
+    y32, y16 = rows(M, ld, 11, 2.0, 0.5)
+    d32, d16 = rows(M, ld, 12)
+    r32, r16 = rows(M, ld, 13)
+    g = torch.Generator().manual_seed(14)
+    scale, shift, mean = (torch.randn(C, generator=g).to(DEV) for _ in range(3))
+    sl = slice(off, off + C)
+
+    def fresh(dt):
+        return torch.full((M, ld), 7.0, device=DEV, dtype=dt)
+
+    def p(t):
+        return t[:, off:].data_ptr()
+
+    yv, dv, rv = y32[:, sl], d32[:, sl], r32[:, sl]
+    for act in (0, 1, 2):
+        z = yv * scale + shift
+        ref = z if act == 0 else (z.clamp(min=0) if act == 1 else z.clamp(0, 6))
+        o32, o16 = fresh(torch.float32), fresh(BF)
+        call("seg_bn_apply", p(y32), ld, M, C, scale.data_ptr(), shift.data_ptr(), act, p(r32), ld, p(o32), ld, s)
+        call("seg_bn_apply_bf16io", p(y16), ld, M, C, scale.data_ptr(), shift.data_ptr(), act, p(r16), ld, p(o16), ld,
+             s)
+        torch.testing.assert_close(o32[:, sl], ref + rv, rtol=1e-6, atol=1e-6)
+        same(o16, o32)
+        inpl = y32.clone()
+        call("seg_bn_apply", p(inpl), ld, M, C, scale.data_ptr(), shift.data_ptr(), act, p(r32), ld, p(inpl), ld, s)
+        assert torch.equal(inpl[:, sl], o32[:, sl])
+        # BN backward apply with the reduction given (seg_bn_backward_parts): zero partials, gamma
+        # None and invstd = scale give coef = (scale, 0, 0), so dY = scale * dA * act'(z)
+        mask = torch.ones_like(z) if act == 0 else ((z > 0) if act == 1 else ((z > 0) & (z < 6))).float()
+        part = torch.zeros(2 * C, device=DEV)
+        gw, gb, cw = torch.empty(C, device=DEV), torch.empty(C, device=DEV), torch.empty(3 * C, device=DEV)
+        dy = fresh(torch.float32)
+        call("seg_bn_backward_parts", part.data_ptr(), 1, p(d32), ld, p(y32), ld, M, C, None, mean.data_ptr(),
+             scale.data_ptr(), scale.data_ptr(), shift.data_ptr(), act, gw.data_ptr(), gb.data_ptr(), cw.data_ptr(),
+             p(dy), ld, s)
+        torch.testing.assert_close(dy[:, sl], scale * dv * mask, rtol=1e-6, atol=1e-6)
+    # full BN backward (reduction + finalize + apply), fp32 vs bf16io twin, and vs its own coefficients
+    gamma = torch.linspace(0.5, 1.5, C, device=DEV)
+    invstd = scale.abs() + 0.5
+    for act in (0, 2):
+        res = {}
+        for tag, d, y, name, dt in (("f", d32, y32, "seg_bn_backward", torch.float32),
+                                    ("b", d16, y16, "seg_bn_backward_bf16io", BF)):
+            gw, gb = torch.empty(C, device=DEV), torch.empty(C, device=DEV)
+            work = torch.empty(query("seg_chan_workspace_floats", M, C) + 3 * C, device=DEV)
+            dy = fresh(dt)
+            call(name, p(d), ld, p(y), ld, M, C, gamma.data_ptr(), mean.data_ptr(), invstd.data_ptr(),
+                 scale.data_ptr(), shift.data_ptr(), act, gw.data_ptr(), gb.data_ptr(), work.data_ptr(), p(dy), ld, s)
+            res[tag] = (gw, gb, dy)
+        assert torch.equal(res["f"][0], res["b"][0]) and torch.equal(res["f"][1], res["b"][1])
+        same(res["b"][2], res["f"][2])
+        z = yv * scale + shift
+        mask = torch.ones_like(z) if act == 0 else ((z > 0) & (z < 6)).float()
+        dz = dv * mask
+        xh = (yv - mean) * invstd
+        dref = gamma * invstd * (dz - dz.mean(0) - xh * (dz * xh).mean(0))
+        torch.testing.assert_close(res["f"][2][:, sl], dref, rtol=1e-4, atol=1e-4)
+        assert torch.equal(res["f"][2][:, :off], fresh(torch.float32)[:, :off])
+    # add (gradient fan-in), in place on the first operand too
+    o32, o16 = fresh(torch.float32), fresh(BF)
+    call("seg_add", p(y32), ld, p(r32), ld, M, C, p(o32), ld, s)
+    call("seg_add_bf16io", p(y16), ld, p(r16), ld, M, C, p(o16), ld, s)
+    assert torch.equal(o32[:, sl], yv + rv)
+    same(o16, o32)
+    a = y32.clone()
+    call("seg_add", p(a), ld, p(r32), ld, M, C, p(a), ld, s)
+    assert torch.equal(a[:, sl], yv + rv) and torch.equal(a[:, :off], y32[:, :off])
+
+
 @pytest.mark.parametrize("stride", [1, 2])
 @pytest.mark.parametrize("lazy", [False, True])
 def test_depthwise(stride, lazy):

@@ -60,6 +60,8 @@ def parse():
                          "configurations (configs[2]/[4]): bf16 MFMA operands, fp32 accumulation / activations / BN "
                          "/ Adam; bf16io = bf16 math + bf16 activation/gradient storage.  infer: f16 = configs[3] "
                          "(default), f32, bf16")
+    ap.add_argument("--optimizer", choices=("seg", "torch"), default="seg",
+                    help="seg: seg_amd.Adam (one-launch HIP step, csrc/adam.hip); torch: torch.optim.Adam (foreach)")
     ap.add_argument("--graphs", action="store_true",
                     help="capture the training step in HIP graphs (engine.set_step_graphs; 1 GPU): the roofline is "
                          "then measured on eager steps after the timed region")
@@ -192,7 +194,11 @@ def main():
     if dist:
         from seg_amd.ddp import DataParallel
         model = DataParallel(model)
-    opt = torch.optim.Adam(model.parameters(), lr=1.5e-4)
+    if args.optimizer == "seg":
+        from seg_amd import Adam
+        opt = Adam(model.parameters(), lr=1.5e-4)
+    else:
+        opt = torch.optim.Adam(model.parameters(), lr=1.5e-4)
     x, y = synthetic_batch(args.batch, args.height, args.width, args.classes, seed=1000 + rank)
     x, y = x.to(dev), y.to(dev)
 
@@ -353,7 +359,8 @@ def main():
                                        f"{args.height}x{args.width}, bs={args.batch}/GPU ({cfg})",
                            "model": args.model, "global_batch": args.batch * world,
                            "image": [args.height, args.width], "parallelism": f"dp{world}",
-                           "hip_graphs": bool(args.graphs)},
+                           "hip_graphs": bool(args.graphs),
+                           "optimizer": {"seg": "seg_amd.Adam (HIP, one launch)", "torch": "torch.optim.Adam (foreach)"}[args.optimizer]},
                 "final_loss": round(final_loss, 5),
                 "math": {"f32": "fp32 everywhere",
                          "bf16": "conv operands bf16 (RNE) on the bf16 MFMA, fp32 accumulation; activations, "

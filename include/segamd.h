@@ -401,6 +401,23 @@ int seg_conv_halo_bf16io(const seg_bf16* in, long ldin, int N, int H, int W, int
 int seg_conv_wgrad_bf16io(const seg_bf16* dy, long lddy, const seg_bf16* x, long ldx, int N, int H, int W, int Cin,
     int Ho, int Wo, int Cout, int ks, int stride, int pad, float* part, int splits, hipStream_t stream);
 
+/* ---- Adam (optim.Adam(model.parameters(), lr=1.5e-4), main.py:100; step at
+ *      src/train.py:39): one launch over every parameter with a gradient, the
+ *      foreach implementation's fp32 arithmetic per element ------------------- */
+typedef struct SegAdamTensor {
+  float* p;
+  const float* g;
+  float* m;          /* exp_avg */
+  float* v;          /* exp_avg_sq */
+  long n;
+  float step_size;   /* -lr / (1 - beta1^t) */
+  float bc2_sqrt;    /* sqrt(1 - beta2^t) */
+} SegAdamTensor;
+/* tensors: device array; chunks: device array of nchunks (tensor index, first
+ * element) int64 pairs covering every tensor in pieces of <= chunk elements */
+int seg_adam_step(const SegAdamTensor* tensors, const long* chunks, int nchunks, int chunk,
+                  float one_minus_beta1, float beta2, float one_minus_beta2, float eps, hipStream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -91,6 +91,7 @@ PROTOTYPES = {
     "seg_argmax_nearest": (_I, [_V, _L, _I, _I, _I, _I, _I, _I, _V, _I, _I, _V]),
     "seg_resize_u8": (_I, [_V, _I, _I, _I, _L, _V, _I, _I, _I, _V, _V]),
     "seg_augment": (_I, [_V, _V, _I, _I, _I, _V, _F, _F, _F, _F, _F, _F, _V, _V, _V]),
+    "seg_adam_step": (_I, [_V, _V, _I, _I, _F, _F, _F, _F, _V]),
 }
 # bf16-storage variants: same C signature shape as their fp32 namesakes (pointers stay void*)
 for _n in ("seg_add", "seg_bn_stats", "seg_bn_apply", "seg_bn_backward", "seg_colsum", "seg_dw_fwd", "seg_dw_dgrad",

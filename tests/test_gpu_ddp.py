@@ -1,7 +1,8 @@
 """GPU: the data-parallel path (seg_amd/ddp.py) on the real engine and RCCL, world size 1
 (the multi-rank semantics are covered over gloo in tests/test_ddp.py; one GPU per box
 here).  Bucket hooks fire from the side-stream weight gradients, all-reduces run on
-RCCL's stream and the averaged gradients must equal the plain model's bitwise."""
+RCCL's stream and the averaged gradients must equal the plain model's bitwise -- with
+torch.optim.Adam and with seg_amd.Adam stepping the bucket-view gradients."""
 import os
 import socket
 
@@ -9,7 +10,7 @@ import pytest
 import torch
 import torch.distributed as dist
 
-from seg_amd import MobileNetV2UNet, engine
+from seg_amd import Adam, MobileNetV2UNet, engine
 from seg_amd.ddp import DataParallel
 from seg_amd.detinit import deterministic_init, synthetic_batch
 
@@ -28,8 +29,9 @@ def pg():
     dist.destroy_process_group()
 
 
+@pytest.mark.parametrize("optim", ["torch", "seg"])
 @pytest.mark.parametrize("math", ["f32", "bf16io"])
-def test_ddp_world1_matches_plain(pg, math):
+def test_ddp_world1_matches_plain(pg, math, optim):
     x, y = synthetic_batch(2, 64, 128, 10, seed=3)
     x, y = x.to(DEV), y.to(DEV)
     res = []
@@ -37,7 +39,7 @@ def test_ddp_world1_matches_plain(pg, math):
         m = deterministic_init(MobileNetV2UNet(10), seed=9).to(DEV).train()
         engine.set_conv_math(m, math)
         model = DataParallel(m, bucket_cap_mb=1.0) if wrap else m
-        opt = torch.optim.Adam(model.parameters(), lr=1e-3)
+        opt = (Adam if optim == "seg" else torch.optim.Adam)(model.parameters(), lr=1e-3)
         losses = []
         for _ in range(3):
             opt.zero_grad(set_to_none=True)

@@ -156,6 +156,81 @@ __global__ __launch_bounds__(256) void up2_bwd_kernel(const T* __restrict__ dout
   }
 }
 
+// up2_bwd_kernel for a 2x2 block of input pixels per thread (rows h, h+1; columns w,
+// w+1; one float4 channel group): the four gathers share source rows 2h+1..2h+2 and
+// columns 2w+1..2w+2, so the block loads a 6x6 window (9 loads per pixel instead of 16)
+// and decodes its position once, from blockIdx.y = (n, h/2) and a 32-bit
+// (column pair, channel group) index.  Each pixel's sum is formed in up2_bwd_kernel's
+// order -- row sums over b, then rows over a, both ascending -- so the results are
+// bitwise those of up2_bwd_kernel.
+template <typename T>
+__global__ __launch_bounds__(256) void up2_bwd_quad_kernel(const T* __restrict__ dout, long ldout, int N, int C,
+                                                           T* __restrict__ din, long ldin, int H, int W,
+                                                           int accumulate) {
+  const int CG = C >> 2, Ho = 2 * H, Wo = 2 * W, HP = (H + 1) >> 1, WP = (W + 1) >> 1;
+  const int idx = blockIdx.x * 256 + threadIdx.x;
+  if (idx >= WP * CG) return;
+  const int n = blockIdx.y / HP, h = 2 * (blockIdx.y - n * HP);
+  const int wp = idx / CG, c = (idx - wp * CG) * 4, w = 2 * wp;
+  float wr[2][4], wc[2][4];
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int hh = h + k, ww = w + k;
+    wr[k][0] = hh > 0 ? 0.25f : 0.f;
+    wr[k][1] = hh > 0 ? 0.75f : 1.f;
+    wr[k][2] = hh < H - 1 ? 0.75f : 1.f;
+    wr[k][3] = hh < H - 1 ? 0.25f : 0.f;
+    wc[k][0] = ww > 0 ? 0.25f : 0.f;
+    wc[k][1] = ww > 0 ? 0.75f : 1.f;
+    wc[k][2] = ww < W - 1 ? 0.75f : 1.f;
+    wc[k][3] = ww < W - 1 ? 0.25f : 0.f;
+  }
+  const T* base = dout + (long)n * Ho * Wo * ldout + c;
+  long col[6];
+#pragma unroll
+  for (int j = 0; j < 6; ++j) {
+    const int s = 2 * w - 1 + j;
+    col[j] = (long)(s < 0 ? 0 : (s > Wo - 1 ? Wo - 1 : s)) * ldout;
+  }
+  f32x4 acc[2][2];
+#pragma unroll
+  for (int k = 0; k < 2; ++k) acc[k][0] = acc[k][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int j = 0; j < 6; ++j) {  // source row 2h-1+j; output row h uses j = 0..3, row h+1 j = 2..5
+    const int r = 2 * h - 1 + j;
+    const int rc = r < 0 ? 0 : (r > Ho - 1 ? Ho - 1 : r);
+    const T* rowp = base + (long)rc * Wo * ldout;
+    f32x4 v[6];
+#pragma unroll
+    for (int b = 0; b < 6; ++b) v[b] = ld4(rowp + col[b]);
+    f32x4 rs0 = {0.f, 0.f, 0.f, 0.f}, rs1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+      rs0 += wc[0][b] * v[b];
+      rs1 += wc[1][b] * v[b + 2];
+    }
+    if (j < 4) {
+      acc[0][0] += wr[0][j] * rs0;
+      acc[0][1] += wr[0][j] * rs1;
+    }
+    if (j >= 2) {
+      acc[1][0] += wr[1][j - 2] * rs0;
+      acc[1][1] += wr[1][j - 2] * rs1;
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+#pragma unroll
+    for (int l = 0; l < 2; ++l) {
+      if (h + k >= H || w + l >= W) continue;
+      T* dst = din + ((long)(n * H + h + k) * W + w + l) * ldin + c;
+      f32x4 o = acc[k][l];
+      if (accumulate) o += ld4(dst);
+      st4(dst, o);
+    }
+  }
+}
+
 // NHWC low-res -> NCHW full-res (the model's returned logits).
 template <typename T>
 __global__ void up_fwd_to_nchw_kernel(const T* __restrict__ in, long ldin, int N, int H, int W, int C,
@@ -303,8 +378,13 @@ static int upsample_bwd_impl(const void* dout, long ldout, int nchw_grad, int N,
   const float sh = up_scale(H, Ho, ac), sw = up_scale(W, Wo, ac);
   const T* dn = static_cast<const T*>(dout);
   if (!nchw_grad && !ac && Ho == 2 * H && Wo == 2 * W && !(C & 3)) {
-    hipLaunchKernelGGL(up2_bwd_kernel<T>, dim3(grid), dim3(256), 0, stream, dn, ldout, N, C, din, ldin, H, W,
-                       accumulate);
+    const long rows = (long)N * ((H + 1) / 2), cols = (long)((W + 1) / 2) * (C / 4);
+    if (rows <= 65535 && cols < (1L << 30))
+      hipLaunchKernelGGL(up2_bwd_quad_kernel<T>, dim3((unsigned)seg_cdiv(cols, 256), (unsigned)rows), dim3(256), 0,
+                         stream, dn, ldout, N, C, din, ldin, H, W, accumulate);
+    else
+      hipLaunchKernelGGL(up2_bwd_kernel<T>, dim3(grid), dim3(256), 0, stream, dn, ldout, N, C, din, ldin, H, W,
+                         accumulate);
     SEG_RET_LAST();
   }
   if (nchw_grad)

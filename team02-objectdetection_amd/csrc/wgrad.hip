@@ -398,30 +398,39 @@ static int conv_wgrad(const void* dy, long lddy, const void* x, long ldx, int N,
 //   mode 0: igemm partials part[s][co][tap][r4(Cin)] -> dW[co][ci][tap]
 //           (channels >= Cin are the zero padding of a Cin % 4 != 0 input: dropped)
 //   mode 1: depthwise partials part[s][tap][C]      -> dW[c][0][tap]
-// Block = 64 slab elements x 4 split groups; each group sums every 4th slab with
-// 4 independent accumulators, the 4 group sums are added through LDS in a fixed
-// order (bitwise reproducible).
+// Block = E slab elements x G = 256 / E split groups; each group sums every G-th slab
+// with 4 independent accumulators, and the G group sums are added through LDS by a
+// fixed pairwise tree, (g0 + g1) + (g2 + g3) ... (bitwise reproducible).  E = 64 / G = 4
+// for large slabs; small slabs with many splits (the 1x1 head and the narrow decoder
+// convs: 192..1344 elements, up to 1024 slabs) take E = 4..32 so more threads share
+// the split dimension -- with 64 elements per block they ran 3-21 blocks whose
+// threads each walked up to 256 slabs serially (50-110 us per launch).
 __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restrict__ part, int splits, long slab,
                                                            float* __restrict__ dw, int Cout, int Cin, int taps,
-                                                           int mode, int accumulate) {
-  __shared__ float red[4][64];
-  const int lane = threadIdx.x & 63, g = threadIdx.x >> 6;
-  const long i = (long)blockIdx.x * 64 + lane;
+                                                           int mode, int accumulate, int E) {
+  __shared__ float red[256];
+  const int G = 256 / E;
+  const int lane = threadIdx.x % E, g = threadIdx.x / E;
+  const long i = (long)blockIdx.x * E + lane;
   float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
   if (i < slab) {
     int k = g;
-    for (; k + 12 < splits; k += 16) {
+    for (; k + 3 * G < splits; k += 4 * G) {
       s0 += part[(long)k * slab + i];
-      s1 += part[(long)(k + 4) * slab + i];
-      s2 += part[(long)(k + 8) * slab + i];
-      s3 += part[(long)(k + 12) * slab + i];
+      s1 += part[(long)(k + G) * slab + i];
+      s2 += part[(long)(k + 2 * G) * slab + i];
+      s3 += part[(long)(k + 3 * G) * slab + i];
     }
-    for (; k < splits; k += 4) s0 += part[(long)k * slab + i];
+    for (; k < splits; k += G) s0 += part[(long)k * slab + i];
   }
-  red[g][lane] = (s0 + s1) + (s2 + s3);
+  red[threadIdx.x] = (s0 + s1) + (s2 + s3);
   __syncthreads();
+  for (int h = 1; h < G; h <<= 1) {  // red[g] += red[g + h] for g % 2h == 0
+    if (g % (2 * h) == 0 && g + h < G) red[threadIdx.x] += red[threadIdx.x + h * E];
+    __syncthreads();
+  }
   if (g != 0 || i >= slab) return;
-  const float s = (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]);
+  const float s = red[lane];
   long o;
   if (mode == 0) {
     const int cp = (Cin + 3) & ~3;
@@ -441,7 +450,10 @@ SEG_API int seg_conv_wgrad_reduce(const float* part, int splits, float* dw, int 
                                   int mode, int accumulate, hipStream_t stream) {
   if (mode != 0 && mode != 1) return (int)hipErrorInvalidValue;
   const long slab = (long)Cout * (mode == 0 ? ((Cin + 3) & ~3) : Cin) * ks * ks;
-  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(seg_cdiv(slab, 64)), dim3(256), 0, stream, part, splits, slab, dw,
-                     Cout, Cin, ks * ks, mode, accumulate);
+  // elements per block: 64 when that still gives >= 256 blocks or few splits per group
+  int E = 64;
+  while (E > 4 && seg_cdiv(slab, E) < 256 && splits > 4 * (256 / E)) E >>= 1;
+  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(seg_cdiv(slab, E)), dim3(256), 0, stream, part, splits, slab, dw,
+                     Cout, Cin, ks * ks, mode, accumulate, E);
   SEG_RET_LAST();
 }

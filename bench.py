@@ -62,12 +62,21 @@ def parse():
                          "(default), f32, bf16")
     ap.add_argument("--optimizer", choices=("seg", "torch"), default="seg",
                     help="seg: seg_amd.Adam (one-launch HIP step, csrc/adam.hip); torch: torch.optim.Adam (foreach)")
-    ap.add_argument("--graphs", action="store_true",
-                    help="capture the training step in HIP graphs (engine.set_step_graphs; 1 GPU): the roofline is "
-                         "then measured on eager steps after the timed region")
     ap.add_argument("--model", choices=("MobileNetV2UNet", "UNet"), default="MobileNetV2UNet",
                     help="UNet = BASELINE configs[4] shape family (use --height 512 --width 1024 --batch 8)")
     return ap.parse_args()
+
+
+def cpu_model() -> str:
+    try:
+        with open("/proc/cpuinfo") as fh:
+            for line in fh:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    import platform
+    return platform.processor() or "unknown"
 
 
 def cpu_baseline(args):
@@ -93,6 +102,7 @@ def cpu_baseline(args):
             break
     dt = time.perf_counter() - t0
     return {"value": round(steps * bs / dt, 3), "unit": "images/s", "cores": threads, "kind": "port",
+            "cpu_model": cpu_model(),
             "sample": f"oracle/segref.py {args.model} fwd+bwd+Adam, bs={bs}, {args.height}x{args.width}, "
                       f"{steps} timed steps ({dt:.1f} s) after 1 warm-up, torch CPU fp32"}
 
@@ -141,7 +151,7 @@ def bench_infer(args):
             one()
             k += 1
         dt = time.perf_counter() - t0
-        cpu = {"value": round(k / dt, 2), "unit": "frames/s", "cores": threads, "kind": "port",
+        cpu = {"value": round(k / dt, 2), "unit": "frames/s", "cores": threads, "kind": "port", "cpu_model": cpu_model(),
                "sample": f"oracle cvresize.preprocess_image + segref eval forward (torch CPU fp32) + class_mask, "
                          f"{k} frames in {dt:.1f} s"}
     line = {"metric": "frames/sec inference MobileNetV2UNet 720x1280 frame -> 128x256, bs=1 (BASELINE configs[3])",
@@ -161,6 +171,27 @@ def bench_infer(args):
     print(json.dumps(line), flush=True)
 
 
+def _free_port() -> int:
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launcher_command(argv, gpus: int, port: int):
+    """The child command `bench.py --gpus N` (N > 1, no WORLD_SIZE in the environment)
+    runs: one process per GPU under torch.distributed.run, the driver's own form."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={gpus}",
+            "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__), *argv]
+
+
+def check_world(world: int, gpus: int):
+    """Every rank must see the world size it was asked for (--gpus)."""
+    if world != gpus:
+        raise SystemExit(f"bench.py: WORLD_SIZE={world} but --gpus {gpus}; launch with "
+                         f"torch.distributed.run --nproc-per-node {gpus} or drop WORLD_SIZE")
+
+
 def main():
     args = parse()
     if args.math is None:
@@ -171,12 +202,20 @@ def main():
         raise SystemExit("--math f16 is the inference configuration (--workload infer)")
     if args.workload == "infer":
         return bench_infer(args)
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        # `python bench.py --gpus N`: start the N ranks as a CHILD process (nothing has touched
+        # the GPU in this process; never exec) and forward its exit code
+        import subprocess
+        rc = subprocess.call(launcher_command(sys.argv[1:], args.gpus, _free_port()))
+        sys.exit(rc)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    check_world(world, args.gpus)
     dist = world > 1
     if dist:
         torch.distributed.init_process_group("nccl")
+        assert torch.distributed.get_world_size() == args.gpus
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
 
@@ -185,11 +224,6 @@ def main():
     from seg_amd import engine
     model = deterministic_init(getattr(seg_amd, args.model)(args.classes), seed=0).to(dev).train()
     engine.set_conv_math(model, args.math)
-    if args.graphs:
-        if world > 1:
-            raise SystemExit("--graphs: the DataParallel gradient sync path stays eager (1 GPU only)")
-        engine.set_step_graphs(model, True)
-        args.warmup = max(args.warmup, engine.GRAPH_WARMUP + 1)  # capture happens inside the warmup
     peak = F32_MFMA_PEAK_TFLOPS if args.math == "f32" else BF16_MFMA_PEAK_TFLOPS
     if dist:
         from seg_amd.ddp import DataParallel
@@ -206,8 +240,6 @@ def main():
         opt.zero_grad(set_to_none=True)
         loss = model.forward_loss(x, y)
         loss.backward()
-        if dist:
-            model.finish_gradient_sync()
         opt.step()
         return loss
 
@@ -217,8 +249,6 @@ def main():
     # packet on the queue: timing all ~130 conv launches costs ~3 % of the step)
     conv3 = {"igemm3_fwd", "igemm3_dgrad", "wino3_fwd", "wino3_dgrad"}
     timer = None if args.no_timer else engine.KernelTimer(kinds=conv3)
-    if args.graphs:
-        timer = None  # replays run no Python: the roofline comes from the eager passes below
     if dist:
         torch.distributed.barrier()
     torch.cuda.synchronize()
@@ -232,22 +262,37 @@ def main():
     dt = time.perf_counter() - t0
     engine.TIMER = None
     final_loss = loss.item()
-    t = torch.tensor([dt], device=dev, dtype=torch.float64)
+    per_rank = [dt]
     if dist:
-        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
-    dt = float(t)
+        t = torch.zeros(world, device=dev, dtype=torch.float64)
+        t[rank] = dt
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.SUM)
+        per_rank = t.tolist()
+    dt = max(per_rank)
     images = args.batch * args.steps * world
     value = images / dt
+    scaling = None
+    if dist:
+        # same-run reference for the weak-scaling efficiency: the same K steps on every rank
+        # with the gradient all-reduce switched off (DataParallel.no_sync), max over ranks
+        with model.no_sync():
+            torch.distributed.barrier()
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for _ in range(args.steps):
+                step()
+            torch.cuda.synchronize()
+            solo = time.perf_counter() - t0
+        t = torch.tensor([solo], device=dev, dtype=torch.float64)
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+        solo = float(t)
+        scaling = {"ranks_seen": world, "ms_per_step_per_rank": [round(x / args.steps * 1e3, 3) for x in per_rank],
+                   "ms_per_step_without_allreduce": round(solo / args.steps * 1e3, 3),
+                   "weak_scaling_eff_vs_no_allreduce": round(solo / dt, 4),
+                   "note": "efficiency = same-run step time without the gradient all-reduce / with it "
+                           "(the driver computes the cross-run N=1 efficiency itself)"}
 
     roof = None
-    if args.graphs and not args.no_timer:
-        engine.set_step_graphs(model, False)
-        timer = engine.KernelTimer(kinds=conv3)
-        engine.TIMER = timer
-        for _ in range(3):
-            step()
-        torch.cuda.synchronize()
-        engine.TIMER = None
     if timer is not None:
         def family(rec, kinds):
             sel = [(f, s) for k, f, s in rec if k in kinds]
@@ -274,20 +319,26 @@ def main():
         flops, secs, n = family(rec, conv3)
         wfl, wsec, wn = family(rec, {"wino3_fwd", "wino3_dgrad"})
         achieved = flops / secs / 1e12 if secs > 0 else 0.0
-        traffic = None
+        traffic, traffic_src = None, None
         prof = os.path.join(REPO, "profiles", "latest_roofline.json" if args.math == "f32"
                             else f"latest_roofline_{args.math}.json")
         if os.path.exists(prof):
             with open(prof) as fh:
-                fam = json.load(fh)["families"].get("conv3", {})
-            traffic = fam.get("hbm_bytes_per_op")
+                rj = json.load(fh)
+            traffic = rj["families"].get("conv3", {}).get("hbm_bytes_per_op")
+            # the PMC figure is not measured in this run: name the profile and commit it came from
+            traffic_src = {"file": os.path.relpath(prof, REPO), "profile": rj.get("profile"),
+                           "commit": rj.get("commit"),
+                           "counters": "rocprofv3 PMC (2*FETCH_SIZE+WRITE_SIZE)*1KiB of the conv3 family per step "
+                                       "/ 17 conv ops, separate --pmc passes"}
         # algorithmic bytes of the family: every 3x3 conv's input and output tensors once
-        # (fwd: X + Y, dgrad: dY + dX), fp32, averaged over its launches
+        # (fwd: X + Y, dgrad: dY + dX) at the storage element size, averaged over its launches
         prog = engine.get_program(getattr(model, "module", model), args.batch, args.height, args.width)
+        sb = 2 if args.math == "bf16io" else 4
         abytes = []
         for op in prog.ops:
             if isinstance(op, engine.ConvOp) and op.kind == "igemm" and op.ks == 3:
-                xy = 4 * (op.inp.M * op.cin + op.y.M * op.cout)
+                xy = sb * (op.inp.M * op.cin + op.y.M * op.cout)
                 abytes.append(xy)
                 if not op.first:
                     abytes.append(xy)
@@ -298,11 +349,18 @@ def main():
         af, as_, an = family(rec_all, {k for k, _, _ in rec_all})
         rec_iso = extra_pass(False)
         ifl, isec, inn = family(rec_iso, conv3)
-        roof = {"bound": "mfma", "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
-                "frac": round(achieved / peak, 4),
+        if args.math == "f32":  # compute-bound config: FLOPs against the f32 MFMA peak
+            bound = {"bound": "mfma", "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
+                     "frac": round(achieved / peak, 4)}
+        else:  # the bf16 configurations are HBM-bound: algorithmic bytes against HBM
+            gbs = alg_bytes * n / secs / 1e9 if secs > 0 else 0.0
+            bound = {"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(gbs / HBM_PEAK_GBS, 4), "mfma_tflops": round(achieved, 2),
+                     "mfma_frac": round(achieved / peak, 4)}
+        roof = {**bound,
                 "traffic": round(traffic) if traffic else None,
-                "traffic_source": f"{os.path.relpath(prof, REPO)}: rocprofv3 PMC (2*FETCH_SIZE+WRITE_SIZE)*1KiB "
-                                  "of the conv3 family per step / 17 conv ops" if traffic else None,
+                "traffic_source": traffic_src,
+                "traffic_over_algorithmic": round(traffic / alg_bytes, 3) if traffic else None,
                 "algorithmic_bytes_per_launch": round(alg_bytes),
                 "kernel": ("dense 3x3 conv fwd + dgrad on f32 MFMA: igemm_conv_kernel<*,*,*,*,3,*> (implicit GEMM), "
                            "halo3x3_kernel (LDS-halo direct conv, narrow decoder convs) and, for the deep decoder "
@@ -359,7 +417,6 @@ def main():
                                        f"{args.height}x{args.width}, bs={args.batch}/GPU ({cfg})",
                            "model": args.model, "global_batch": args.batch * world,
                            "image": [args.height, args.width], "parallelism": f"dp{world}",
-                           "hip_graphs": bool(args.graphs),
                            "optimizer": {"seg": "seg_amd.Adam (HIP, one launch)", "torch": "torch.optim.Adam (foreach)"}[args.optimizer]},
                 "final_loss": round(final_loss, 5),
                 "math": {"f32": "fp32 everywhere",
@@ -369,6 +426,8 @@ def main():
                                    "gradients stored bf16 in HBM (fp32 arithmetic inside every kernel); BN "
                                    "statistics, parameter gradients, loss and Adam fp32"}[args.math],
                 "roofline": roof, "step_roofline": step_roof, "cpu_baseline": cpu}
+        if scaling is not None:
+            line["multi_gpu"] = scaling
         print(json.dumps(line), flush=True)
     if dist:
         torch.distributed.destroy_process_group()

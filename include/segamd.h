@@ -56,16 +56,6 @@ int seg_conv_igemm_act(const float* in, long ldin, int N, int H, int W, int Cin,
                        int ks, int stride, int pad,
                        const float* add, long ldadd, float* stat, int act, float* work, int splits,
                        hipStream_t stream);
-/* Data gradient (stride 1) of a conv followed by a train-mode BatchNorm with the BN
- * backward applied on load: in = dA, y = raw conv output, scale/shift/mean = the
- * forward BN coefficients, k = [3][Cin] (seg_bn_backward_coef), bn_act = the
- * activation; out = conv(dY, Wd) + add.  Replaces seg_bn_backward's dY pass +
- * seg_conv_igemm; needs seg_conv_igemm_bnb_ok(Cin, ks). */
-int seg_conv_igemm_bnb(const float* in, long ldin, int N, int H, int W, int Cin, const float* wk, int ldk,
-                       float* out, long ldout, int Cout, int ks, int pad, const float* add, long ldadd,
-                       const float* y, long ldy, const float* scale, const float* shift, const float* mean,
-                       const float* k, int bn_act, hipStream_t stream);
-int seg_conv_igemm_bnb_ok(int Cin, int ks);
 /* seg_conv_igemm_act with bf16 math (BASELINE configs[2]/[4], the bf16 configurations;
  * replaces the autocast bf16 conv2d of the same call sites): the same fp32 tensors,
  * both operands rounded to bf16 (round-to-nearest-even) in the LDS staging,
@@ -86,19 +76,6 @@ int seg_conv_igemm_f16(const float* in, long ldin, int N, int H, int W, int Cin,
                        int ks, int stride, int pad,
                        const float* add, long ldadd, float* stat, int act, float* work, int splits,
                        hipStream_t stream);
-/* Data gradient (stride 1) completing dA of a layer y -> train BatchNorm -> act, with
- * that BN's backward reduction fused into the epilogue (replaces the reduction pass of
- * native_batch_norm_backward): part[tile][2][Cout], tile = seg_conv_igemm_row_tiles(M,
- * Cout) rows, gets sum(dz) and sum(dz*(y-mean)), dz = dA*act'(y*scale+shift).
- * _bf16: the same with bf16 math. */
-int seg_conv_igemm_red(const float* in, long ldin, int N, int H, int W, int Cin, const float* wk, int ldk,
-                       float* out, long ldout, int Cout, int ks, int pad, const float* add, long ldadd,
-                       const float* y, long ldy, const float* scale, const float* shift, const float* mean,
-                       int bn_act, float* part, hipStream_t stream);
-int seg_conv_igemm_red_bf16(const float* in, long ldin, int N, int H, int W, int Cin, const float* wk, int ldk,
-                            float* out, long ldout, int Cout, int ks, int pad, const float* add, long ldadd,
-                            const float* y, long ldy, const float* scale, const float* shift, const float* mean,
-                            int bn_act, float* part, hipStream_t stream);
 /* Split-K factor for seg_conv_igemm_act (1 = none): > 1 only when the output tiles
  * cannot fill the 256 CUs (batch-1 inference). */
 int seg_conv_igemm_splits(long M, int Cout, int Cin, int ks);
@@ -127,12 +104,6 @@ int seg_conv_wgrad_bf16(const float* dy, long lddy, const float* x, long ldx,
                         int N, int H, int W, int Cin, int Ho, int Wo, int Cout,
                         int ks, int stride, int pad, float* part, int splits, hipStream_t stream);
 
-/* seg_conv_wgrad with dY formed on load from dA (dy) and y (BN backward, as
- * seg_conv_igemm_bnb; Cout % 4 == 0). */
-int seg_conv_wgrad_bnb(const float* dy, long lddy, const float* x, long ldx, int N, int H, int W, int Cin,
-                       int Ho, int Wo, int Cout, int ks, int stride, int pad, float* part, int splits,
-                       const float* y, long ldy, const float* scale, const float* shift, const float* mean,
-                       const float* k, int bn_act, hipStream_t stream);
 /* dW (PyTorch layout) = fixed-order sum of partial slabs.  mode 0: igemm
  * partials (K runs of round_up(Cin,4) channels), 1: depthwise partials. */
 int seg_conv_wgrad_reduce(const float* part, int splits, float* dw, int Cout, int Cin, int ks,
@@ -213,13 +184,6 @@ int seg_dw_wgrad(const float* dy, long lddy, const float* x, long ldx, int N, in
  * K = 9 taps x 4 channels (the 4th weight channel packed as zero). */
 int seg_nchw_to_nhwc(const float* x, int N, int C, int H, int W, float* out, int ld, hipStream_t stream);
 
-/* seg_bn_backward whose reduction was fused into the producer of dA
- * (seg_conv_igemm_red / _red_bf16): finalize from part[nparts][2][C] + apply.
- * coef >= 3*C floats. */
-int seg_bn_backward_parts(const float* part, int nparts, const float* da, long ldda, const float* y, long ldy,
-                          long M, int C, const float* gamma, const float* mean, const float* invstd,
-                          const float* scale, const float* shift, int act, float* dgamma, float* dbeta,
-                          float* coef, float* dy, long lddy, hipStream_t stream);
 /* ---- BatchNorm2d + activation (aten native_batch_norm(+_backward), hardtanh,
  *      threshold; src/unet.py:59-63,114-115 and torchvision norms) ----------- */
 /* partial-sum workspace (floats) of the channel reductions over [M][C]; the
@@ -242,39 +206,15 @@ int seg_bn_backward(const float* da, long ldda, const float* y, long ldy, long M
                     const float* gamma, const float* mean, const float* invstd,
                     const float* scale, const float* shift, int act,
                     float* dgamma, float* dbeta, float* work, float* dy, long lddy, hipStream_t stream);
-/* The reduction half of seg_bn_backward (dgamma, dbeta and coef[3][C]) for a
- * consumer that applies the BN backward on load (seg_pw_bwd_fused). */
-int seg_bn_backward_coef(const float* da, long ldda, const float* y, long ldy, long M, int C,
-                         const float* gamma, const float* mean, const float* invstd, const float* scale,
-                         const float* shift, int act, float* dgamma, float* dbeta, float* work, float* coef,
-                         hipStream_t stream);
 int seg_bn_eval_backward(const float* da, long ldda, const float* y, long ldy, long M, int C,
                          const float* scale, const float* shift, int act, float* dy, long lddy,
                          hipStream_t stream);
 /* conv bias gradient: out[c] (+)= sum_r y[r][c]; work >= seg_chan_workspace_floats(M, round_up(C, 4)) */
 int seg_colsum(const float* y, long ldy, long M, int C, float* work, float* out, int accumulate,
                hipStream_t stream);
-/* seg_colsum of dY formed on load from dA and y (BN backward; C % 4 == 0). */
-int seg_colsum_bnb(const float* da, long ldda, const float* y, long ldy, long M, int C, const float* scale,
-                   const float* shift, const float* mean, const float* k, int bn_act, float* work, float* out,
-                   int accumulate, hipStream_t stream);
 /* gradient fan-in (residual add of InvertedResidual, skip reuse): out = a (+ b) */
 int seg_add(const float* a, long lda, const float* b, long ldb, long M, int C, float* out, long ldout,
             hipStream_t stream);
-
-/* Fused backward of a 1x1 conv + train-mode BN (+ act) -- torchvision's
- * InvertedResidual expand/project convs: reads dA, y and x once per pixel and
- * produces dx (+ addend) and dW partial slabs [blocks][Cout][r4(Cin)]
- * (seg_conv_wgrad_reduce mode 0, ks 1), with dY = coef0*(dz - coef1 - (y-mean)*coef2),
- * dz = dA * act'(y*scale+shift) computed on load.  wkd = seg_pack_conv_weight mode 1.
- * seg_pw_bwd_fused_ok: channel limits (<= 192 each, LDS <= 96 KiB);
- * seg_pw_bwd_blocks: the slab count for M pixels. */
-int seg_pw_bwd_fused_ok(int Cin, int Cout);
-int seg_pw_bwd_blocks(long M);
-int seg_pw_bwd_fused(const float* da, long ldda, const float* y, long ldy, const float* x, long ldx,
-                     const float* wkd, int ldkd, const float* scale, const float* shift, const float* mean,
-                     const float* coef, int act, const float* add, long ldadd, float* dx, long lddx,
-                     float* part, int blocks, long M, int Cin, int Cout, hipStream_t stream);
 
 /* ---- resampling (aten upsample_bilinear2d(+_backward), max_pool2d) ---------- */
 /* nn.Upsample(x2, bilinear) of `up` (src/unet.py:97,101; ac = 0) into the concat
@@ -293,7 +233,11 @@ int seg_maxpool2_bwd(const float* in, long ldin, const float* dout, long lddout,
                      int C, float* din, long lddin, int accumulate, hipStream_t stream);
 
 /* ---- loss (nn.CrossEntropyLoss, main.py:99 / src/train.py:37) fused with the
- *      align_corners=True final upsample (src/unet.py:30,49) ----------------- */
+ *      align_corners=True final upsample (src/unet.py:30,49) -----------------
+ * out2 = [loss, #non-ignored pixels, #labels outside [0, C) that are not
+ * ignore_index] (3 floats; despite the name).  Out-of-range labels (aten raises
+ * "Target out of bounds") make the loss and every gradient NaN; the caller raises
+ * when it reads them (seg_amd.engine.check_targets). */
 long seg_ce_workspace_floats(long pixels);
 int seg_ce_upsample_loss(const float* low, long ld, int N, int H, int W, int C,
                          const long long* labels, int Ho, int Wo, int ignore_index,

@@ -42,6 +42,41 @@ def _bump(p, pre, training):
         p[pre + "num_batches_tracked"] += 1
 
 
+# Activation masks (tests only).  ReLU / ReLU6 gradients are discontinuous in the
+# pre-activation z: an element within rounding distance of a threshold may pass the
+# gradient in one valid fp32 implementation and block it in another.  MASK_OVERRIDE =
+# {layer prefix: bool mask (NCHW)} makes the backward of that layer's activation use the
+# given mask (the forward values are unchanged), so the oracle can be run with another
+# implementation's masks (oracle/budget.py).  ACT_HI records each layer's upper
+# threshold (6 for ReLU6, None for ReLU) as the forward passes it.
+MASK_OVERRIDE = None
+ACT_HI = {}
+
+
+class _ActMasked(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, z, hi, mask):
+        ctx.save_for_backward(mask)
+        return z.clamp(0.0, hi) if hi is not None else z.clamp(min=0.0)
+
+    @staticmethod
+    def backward(ctx, g):
+        (mask,) = ctx.saved_tensors
+        return g * mask.to(g.dtype), None, None
+
+
+def act_mask(z, hi):
+    """aten's gradient mask: hardtanh_backward passes 0 < z < 6 (strict), threshold_backward z > 0."""
+    return (z > 0) & (z < hi) if hi is not None else z > 0
+
+
+def _act(name, z, hi):
+    ACT_HI[name] = hi
+    if MASK_OVERRIDE is not None and name in MASK_OVERRIDE:
+        return _ActMasked.apply(z, hi, MASK_OVERRIDE[name])
+    return F.hardtanh(z, 0.0, 6.0) if hi is not None else F.relu(z)
+
+
 def _cbr(p, pre_conv, pre_bn, x, training, stride=1, pad=0, groups=1, act="relu6", bias=None):
     y = F.conv2d(x, p[pre_conv + "weight"], p.get(pre_conv + "bias") if bias is None else bias,
                  stride=stride, padding=pad, groups=groups)
@@ -49,10 +84,22 @@ def _cbr(p, pre_conv, pre_bn, x, training, stride=1, pad=0, groups=1, act="relu6
     y = _bn(p, pre_bn, y, training)
     _bump(p, pre_bn, training)
     if act == "relu6":
-        return _rec(pre_conv + "out", F.hardtanh(y, 0.0, 6.0))
+        return _rec(pre_conv + "out", _act(pre_conv, _rec(pre_conv + "z", y), 6.0))
     if act == "relu":
-        return _rec(pre_conv + "out", F.relu(y))
+        return _rec(pre_conv + "out", _act(pre_conv, _rec(pre_conv + "z", y), None))
     return _rec(pre_conv + "out", y)
+
+
+def preactivations(arch, p, x, training=True):
+    """{conv layer prefix: its post-BN pre-activation z} of one forward (no grad)."""
+    global RECORD
+    saved, RECORD = RECORD, {}
+    try:
+        with torch.no_grad():
+            FORWARDS[arch](p, x, training)
+        return {k[:-1]: v for k, v in RECORD.items() if k.endswith(".z")}
+    finally:
+        RECORD = saved
 
 
 def mobilenet_features(p, x, training, prefix="backbone.features."):

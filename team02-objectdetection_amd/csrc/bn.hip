@@ -29,12 +29,11 @@ constexpr int kChanSlice = 32;
 // kind 0: (sum(y-k), sum((y-k)^2)),  k = y[0][c]                   -> BN stats
 // kind 1: (sum(dz),  sum(dz*(y-mean))), dz = dA * act'(y*scale+shift) -> BN backward
 // kind 2: (sum(y), 0)                                               -> bias grad
-// kind 3: (sum(dY), 0), dY = BN backward of (da, y) formed on load     -> bias grad of a BN conv
 template <int KIND, typename T = float>
 __global__ __launch_bounds__(256) void chan_partial_kernel(
     const T* __restrict__ y, long ldy, const T* __restrict__ da, long ldda, int M, int C,
     const float* __restrict__ scale, const float* __restrict__ shift, const float* __restrict__ mean, int act,
-    float* __restrict__ part, int rows_per_block, SegBnBwd bnb) {
+    float* __restrict__ part, int rows_per_block) {
   __shared__ f32x4 red0[256], red1[256];
   // channel slice of this block (blockIdx.y; chan_split): CGB groups from cg0
   const int CGB = gridDim.y > 1 ? kChanSlice : (C >> 2);
@@ -57,8 +56,6 @@ __global__ __launch_bounds__(256) void chan_partial_kernel(
       f32x4 k = {0.f, 0.f, 0.f, 0.f}, sc = k, sh = k;
       if (KIND == 0) k = ld4(y + c);
       if (KIND == 1) { k = ld4(mean + c); sc = ld4(scale + c); sh = ld4(shift + c); }
-      f32x4 cf[6];
-      if (KIND == 3) seg_bnbwd_coef(bnb, c, cf);
       auto step = [&](int r) {
         const f32x4 v = ld4(y + (long)r * ldy + c);
         if (KIND == 0) {
@@ -72,9 +69,6 @@ __global__ __launch_bounds__(256) void chan_partial_kernel(
           for (int j = 0; j < 4; ++j) dz[j] = g[j] * seg_act_mask(v[j] * sc[j] + sh[j], act);
           s0 += dz;
           s1 += dz * (v - k);
-        } else if (KIND == 3) {
-          const f32x4 g = ld4(da + (long)r * ldda + c);
-          s0 += seg_bnbwd4(g, v, cf[0], cf[1], cf[2], cf[3], cf[4], cf[5], bnb.act);
         } else {
           s0 += v;
         }
@@ -572,7 +566,7 @@ static int bn_stats_impl(const T* y, long ldy, long M, int C, const float* gamma
   const int rpb = rows_per_block_for(M, C);
   const int nblk = seg_cdiv(M, rpb);
   hipLaunchKernelGGL((chan_partial_kernel<0, T>), dim3(nblk, chan_split(C)), dim3(256), 0, stream, y, ldy, (const T*)nullptr, 0L,
-                     (int)M, C, nullptr, nullptr, nullptr, 0, work, rpb, SegBnBwd{});
+                     (int)M, C, nullptr, nullptr, nullptr, 0, work, rpb);
   hipLaunchKernelGGL(bn_finalize_kernel<T>, dim3(C), dim3(256), 0, stream, work, nblk, y, M, C, gamma,
                      beta, eps, momentum, running_mean, running_var, num_batches_tracked, mean, invstd, scale, shift);
   SEG_RET_LAST();
@@ -646,7 +640,7 @@ static int bn_backward_impl(const T* da, long ldda, const T* y, long ldy, long M
   const int nblk = seg_cdiv(M, rpb);
   float* coef = work + (long)nblk * 2 * C;
   hipLaunchKernelGGL((chan_partial_kernel<1, T>), dim3(nblk, chan_split(C)), dim3(256), 0, stream, y, ldy, da, ldda, (int)M, C, scale,
-                     shift, mean, act, work, rpb, SegBnBwd{});
+                     shift, mean, act, work, rpb);
   hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(C), dim3(256), 0, stream, work, nblk, M, C, gamma,
                      invstd, dgamma, dbeta, coef);
   launch_bn_bwd_apply<T>(da, ldda, y, ldy, M, C, scale, shift, mean, act, coef, dy, lddy, stream);
@@ -666,57 +660,11 @@ SEG_API int seg_bn_backward_bf16io(const __bf16* da, long ldda, const __bf16* y,
                           lddy, stream);
 }
 
-// seg_bn_backward whose reduction was fused into the producer of dA
-// (seg_conv_igemm_red): part[nparts][2][C] per-tile sums; finalize + apply only.
-// `coef` >= 3*C floats of workspace.
-SEG_API int seg_bn_backward_parts(const float* part, int nparts, const float* da, long ldda, const float* y, long ldy,
-                                  long M, int C, const float* gamma, const float* mean, const float* invstd,
-                                  const float* scale, const float* shift, int act, float* dgamma, float* dbeta,
-                                  float* coef, float* dy, long lddy, hipStream_t stream) {
-  if ((C & 3) || (ldy & 3) || (ldda & 3) || (lddy & 3) || nparts < 1) return (int)hipErrorInvalidValue;
-  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(C), dim3(256), 0, stream, part, nparts, M, C, gamma,
-                     invstd, dgamma, dbeta, coef);
-  launch_bn_bwd_apply<float>(da, ldda, y, ldy, M, C, scale, shift, mean, act, coef, dy, lddy, stream);
-  SEG_RET_LAST();
-}
-
-// The reduction half of seg_bn_backward: dgamma/dbeta and coef[3][C] = (g*inv,
-// mean(dz), mean(dz*xhat)*inv) for a fused consumer (seg_pw_bwd_fused) that
-// applies dY = coef0 * (dz - coef1 - (y - mean) * coef2) on load.
-// `work` >= seg_chan_workspace_floats(M,C).
-SEG_API int seg_bn_backward_coef(const float* da, long ldda, const float* y, long ldy, long M, int C,
-                                 const float* gamma, const float* mean, const float* invstd, const float* scale,
-                                 const float* shift, int act, float* dgamma, float* dbeta, float* work, float* coef,
-                                 hipStream_t stream) {
-  if ((C & 3) || (ldy & 3) || (ldda & 3)) return (int)hipErrorInvalidValue;
-  const int rpb = rows_per_block_for(M, C);
-  const int nblk = seg_cdiv(M, rpb);
-  hipLaunchKernelGGL((chan_partial_kernel<1, float>), dim3(nblk, chan_split(C)), dim3(256), 0, stream, y, ldy, da, ldda, (int)M, C, scale,
-                     shift, mean, act, work, rpb, SegBnBwd{});
-  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(C), dim3(256), 0, stream, work, nblk, M, C, gamma,
-                     invstd, dgamma, dbeta, coef);
-  SEG_RET_LAST();
-}
-
 SEG_API int seg_bn_eval_backward(const float* da, long ldda, const float* y, long ldy, long M, int C,
                                  const float* scale, const float* shift, int act, float* dy, long lddy,
                                  hipStream_t stream) {
   hipLaunchKernelGGL(bn_eval_bwd_kernel, dim3(ew_grid(M * (C / 4))), dim3(256), 0, stream, da, ldda, y, ldy, M, C,
                      scale, shift, act, dy, lddy);
-  SEG_RET_LAST();
-}
-
-// Bias gradient of a conv followed by a train-mode BatchNorm, from dA and y with the BN
-// backward formed on load (no dY tensor): out[c] (+)= sum_r dY[r][c].  C % 4 == 0.
-SEG_API int seg_colsum_bnb(const float* da, long ldda, const float* y, long ldy, long M, int C, const float* scale,
-                           const float* shift, const float* mean, const float* k, int bn_act, float* work, float* out,
-                           int accumulate, hipStream_t stream) {
-  if ((C & 3) || (ldy & 3) || (ldda & 3) || !k) return (int)hipErrorInvalidValue;
-  const int rpb = rows_per_block_for(M, C);
-  const int nblk = seg_cdiv(M, rpb);
-  hipLaunchKernelGGL((chan_partial_kernel<3, float>), dim3(nblk, chan_split(C)), dim3(256), 0, stream, y, ldy, da, ldda, (int)M, C, nullptr,
-                     nullptr, nullptr, 0, work, rpb, SegBnBwd{y, ldy, scale, shift, mean, k, C, bn_act});
-  hipLaunchKernelGGL(colsum_finalize_kernel, dim3(C), dim3(256), 0, stream, work, nblk, C, C, out, accumulate);
   SEG_RET_LAST();
 }
 
@@ -729,7 +677,7 @@ static int colsum_impl(const T* y, long ldy, long M, int C, float* work, float* 
   const int rpb = rows_per_block_for(M, C4);  // the workspace is seg_chan_workspace_floats(M, C4)
   const int nblk = seg_cdiv(M, rpb);
   hipLaunchKernelGGL((chan_partial_kernel<2, T>), dim3(nblk, chan_split(C4)), dim3(256), 0, stream, y, ldy, (const T*)nullptr, 0L,
-                     (int)M, C4, nullptr, nullptr, nullptr, 0, work, rpb, SegBnBwd{});
+                     (int)M, C4, nullptr, nullptr, nullptr, 0, work, rpb);
   hipLaunchKernelGGL(colsum_finalize_kernel, dim3(C), dim3(256), 0, stream, work, nblk, C, C4, out,
                      accumulate);
   SEG_RET_LAST();

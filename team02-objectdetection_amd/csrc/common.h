@@ -80,8 +80,7 @@ __device__ __forceinline__ f32x4 seg_bn_act4(f32x4 v, f32x4 sc, f32x4 sh, int ac
 // BatchNorm backward of 4 channels (train mode, through the activation):
 //   dY = k1 * (dz - k2 - (y - mean) * k3),  dz = dA * act'(y * scale + shift)
 // with k1 = g*invstd, k2 = mean(dz), k3 = mean(dz * xhat) * invstd.  The one
-// definition used by the apply pass (bn.hip) and by every kernel that applies it
-// on load (the dY operand of the data / weight gradients), so both are bitwise equal.
+// definition used by the apply pass (bn.hip).
 __device__ __forceinline__ f32x4 seg_bnbwd4(f32x4 g, f32x4 v, f32x4 sc, f32x4 sh, f32x4 mu, f32x4 k1, f32x4 k2,
                                             f32x4 k3, int act) {
   f32x4 o;
@@ -91,38 +90,6 @@ __device__ __forceinline__ f32x4 seg_bnbwd4(f32x4 g, f32x4 v, f32x4 sc, f32x4 sh
     o[j] = k1[j] * (dz - k2[j] - (v[j] - mu[j]) * k3[j]);
   }
   return o;
-}
-
-// Where a dY operand comes from when the BatchNorm backward is applied on load:
-// dA (the kernel's own input pointer) and y below, plus per-channel coefficients
-// (scale, shift, mean: the forward's; k: [3][C] from seg_bn_backward_coef).
-struct SegBnBwd {
-  const float* y;
-  long ldy;
-  const float *scale, *shift, *mean, *k;
-  int C, act;
-};
-
-// BatchNorm-backward reduction fused into the kernel that completes dA (the gradient
-// of act(BN(y))): per output tile and channel, part[tile][0][c] = sum dz and
-// part[tile][1][c] = sum dz * (y - mean), dz = dA * act'(y * scale + shift)
-// (seg_bn_backward_parts finalizes them).  part == nullptr: off.
-struct SegBnRed {
-  const float* y;
-  long ldy;
-  const float *scale, *shift, *mean;
-  int act;
-  float* part;
-};
-
-// The 6 coefficient float4s of channel group c.
-__device__ __forceinline__ void seg_bnbwd_coef(const SegBnBwd& b, int c, f32x4 (&cf)[6]) {
-  cf[0] = ld4(b.scale + c);
-  cf[1] = ld4(b.shift + c);
-  cf[2] = ld4(b.mean + c);
-  cf[3] = ld4(b.k + c);
-  cf[4] = ld4(b.k + b.C + c);
-  cf[5] = ld4(b.k + 2 * b.C + c);
 }
 
 __device__ __forceinline__ float wave_sum(float v) {

@@ -36,21 +36,6 @@ SEG_API int seg_conv_igemm_act(const float* in, long ldin, int N, int H, int W, 
                                 add, ldadd, stat, act, work, splits, stream);
 }
 
-// Data gradient (stride 1) whose output completes dA of a layer y -> train BN -> act,
-// with that BatchNorm's backward reduction fused into the epilogue: part[tile][2][Cout]
-// (tile = seg_conv_igemm_row_tiles(M, Cout) rows) receives sum(dz) and
-// sum(dz * (y - mean)) per channel; y/ldy, scale/shift/mean and bn_act are the BN
-// layer's (forward coefficients).  Finalize + apply: seg_bn_backward_parts.
-SEG_API int seg_conv_igemm_red(const float* in, long ldin, int N, int H, int W, int Cin, const float* wk, int ldk,
-                               float* out, long ldout, int Cout, int ks, int pad, const float* add, long ldadd,
-                               const float* y, long ldy, const float* scale, const float* shift, const float* mean,
-                               int bn_act, float* part, hipStream_t stream) {
-  if (!part) return (int)hipErrorInvalidValue;
-  const SegBnRed red{y, ldy, scale, shift, mean, bn_act, part};
-  return conv_igemm_impl<float>(in, ldin, N, H, W, Cin, wk, ldk, nullptr, out, ldout, H, W, Cout, ks, 1, pad, add,
-                                ldadd, nullptr, SEG_ACT_NONE, nullptr, 1, stream, &red);
-}
-
 SEG_API int seg_conv_igemm(const float* in, long ldin, int N, int H, int W, int Cin,
                            const float* wk, int ldk, const float* bias,
                            float* out, long ldout, int Ho, int Wo, int Cout,
@@ -58,46 +43,6 @@ SEG_API int seg_conv_igemm(const float* in, long ldin, int N, int H, int W, int 
                            const float* add, long ldadd, float* stat, hipStream_t stream) {
   return seg_conv_igemm_act(in, ldin, N, H, W, Cin, wk, ldk, bias, out, ldout, Ho, Wo, Cout, ks, stride, pad, add,
                             ldadd, stat, SEG_ACT_NONE, nullptr, 1, stream);
-}
-
-// Data gradient of a stride-1 conv whose output went through a train-mode BatchNorm,
-// with the BN backward applied on load: `in` = dA (gradient of the activated
-// output), y = the raw conv output (ldy), scale/shift/mean = the forward BN
-// coefficients, k = [3][Cin] from seg_bn_backward_coef, bn_act = the activation.
-// out = conv(dY, Wd) (+ add).  Requires the uniform-tap loader (seg_conv_igemm_bnb_ok).
-SEG_API int seg_conv_igemm_bnb(const float* in, long ldin, int N, int H, int W, int Cin, const float* wk, int ldk,
-                               float* out, long ldout, int Cout, int ks, int pad, const float* add, long ldadd,
-                               const float* y, long ldy, const float* scale, const float* shift, const float* mean,
-                               const float* k, int bn_act, hipStream_t stream) {
-  if ((Cin & 3) || (ldin & 3) || (ldk & 3) || (ldy & 3) || (ks != 1 && ks != 3) || !y || !k || !scale || !shift ||
-      !mean)
-    return (int)hipErrorInvalidValue;
-  IgemmArgs a;
-  a.in = in; a.ldin = ldin; a.wk = wk; a.ldk = ldk; a.bias = nullptr;
-  a.add = add; a.ldadd = ldadd; a.out = out; a.ldout = ldout; a.stat = nullptr;
-  a.N = N; a.H = H; a.W = W; a.Cin = Cin; a.Ho = H; a.Wo = W; a.Cout = Cout;
-  a.stride = 1; a.pad = pad; a.K = ks * ks * Cin; a.M = N * H * W; a.act = 0; a.part = nullptr;
-  a.bnb = SegBnBwd{y, ldy, scale, shift, mean, k, Cin, bn_act};
-  a.red = SegBnRed{};
-  if (a.M == 0 || Cout == 0) return 0;
-  if (Cin < igemm_bk(a.K)) return (int)hipErrorInvalidValue;
-  switch (pick_tile(a.M, Cout)) {
-    case 0: return launch_igemm<128, 128, 64, 64>(a, ks, 1, stream);
-    case 1: return launch_igemm<64, 128, 32, 64>(a, ks, 1, stream);
-    case 2: return launch_igemm<128, 64, 64, 32>(a, ks, 1, stream);
-    case 3: return launch_igemm<64, 64, 32, 32>(a, ks, 1, stream);
-    case 4: return launch_igemm<128, 96, 32, 96>(a, ks, 1, stream);
-    case 5: return launch_igemm<128, 160, 32, 160>(a, ks, 1, stream);
-    case 6: return launch_igemm<256, 32, 64, 32>(a, ks, 1, stream);
-    default: return launch_igemm<128, 32, 32, 32>(a, ks, 1, stream);
-  }
-}
-
-// 1 when seg_conv_igemm_bnb supports this data gradient (uniform-tap loader: the
-// dY channel count >= the K chunk).
-SEG_API int seg_conv_igemm_bnb_ok(int Cin, int ks) {
-  if ((Cin & 3) || (ks != 1 && ks != 3)) return 0;
-  return Cin >= igemm_bk(ks * ks * Cin) ? 1 : 0;
 }
 
 // Split-K factor seg_conv_igemm_act should be given for this conv (1 = none); the

@@ -12,14 +12,3 @@ SEG_API int seg_conv_igemm_bf16(const float* in, long ldin, int N, int H, int W,
   return conv_igemm_impl<__bf16>(in, ldin, N, H, W, Cin, wk, ldk, bias, out, ldout, Ho, Wo, Cout, ks, stride, pad,
                               add, ldadd, stat, act, work, splits, stream);
 }
-
-// seg_conv_igemm_red (igemm.hip) with bf16 math.
-SEG_API int seg_conv_igemm_red_bf16(const float* in, long ldin, int N, int H, int W, int Cin, const float* wk, int ldk,
-                                    float* out, long ldout, int Cout, int ks, int pad, const float* add, long ldadd,
-                                    const float* y, long ldy, const float* scale, const float* shift,
-                                    const float* mean, int bn_act, float* part, hipStream_t stream) {
-  if (!part) return (int)hipErrorInvalidValue;
-  const SegBnRed red{y, ldy, scale, shift, mean, bn_act, part};
-  return conv_igemm_impl<__bf16>(in, ldin, N, H, W, Cin, wk, ldk, nullptr, out, ldout, H, W, Cout, ks, 1, pad, add,
-                                 ldadd, nullptr, SEG_ACT_NONE, nullptr, 1, stream, &red);
-}

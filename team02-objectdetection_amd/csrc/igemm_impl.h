@@ -1,7 +1,7 @@
 // Implicit-GEMM convolution kernel template (the kernel, its launchers, the tile cost
 // model and the split-K reduce), shared by one translation unit per operand type so
 // the three instantiation sets compile in parallel:
-//   igemm.hip       float    (exact fp32, the default math; + pack kernels, BNB path)
+//   igemm.hip       float    (exact fp32, the default math; + pack kernels)
 //   igemm_bf16.hip  __bf16   (seg_conv_igemm_bf16)
 //   igemm_f16.hip   _Float16 (seg_conv_igemm_f16)
 // See igemm.hip for the algorithm.
@@ -33,8 +33,6 @@ struct IgemmArgs {
   int kchunk;                    // split-K: K range of blockIdx.y (a multiple of BK); == K when unsplit
   float* part;                   // split-K: raw partial sums [gridDim.y][M][Cout] (no epilogue), else null
   int act;                       // epilogue activation of act(acc + bias + add) (SegAct); 0 in training
-  SegBnBwd bnb;                  // BNB kernels: `in` is dA and the A operand is the BN backward dY
-  SegBnRed red;                  // optional: BN-backward reduction of the written gradient (red.part set)
 };
 
 #ifndef SEG_IGEMM_DEPTH
@@ -60,10 +58,6 @@ struct IgemmArgs {
 // each operand slot is a fixed base offset plus one of two scalar tap offsets --
 // a few VALU ops per slot instead of the general path's per-slot tap tracking
 // and bounds arithmetic.  The general path remains for Cin < BK (the stem).
-// BNB (data gradient of a conv whose output went through a train-mode BatchNorm):
-// the A operand dY is formed on load from dA (`in`) and the raw conv output y
-// (seg_bnbwd4), so the BN backward never writes dY.  UT path only; zero padding
-// (out-of-image taps) stays zero.
 //
 // OT = operand type.  float: exact fp32 products on v_mfma_f32_32x32x2_f32.  __bf16 /
 // _Float16 ("bf16 / f16 math", the bf16 and fp16 configurations of BASELINE
@@ -73,8 +67,7 @@ struct IgemmArgs {
 // pitch at BK 32, so the ds_read_b128 fragment reads (lane half h: k = 16ks + 8h .. +7)
 // stay conflict-free; the epilogue (bias, BN statistics, addend) is the fp32 one.
 // IT = activation storage type of in / add / out (float, or __bf16: the bf16io path).
-template <int BM, int BN, int WM, int WN, int KS, int BK, bool UT, bool BNB = false, typename OT = float,
-          typename IT = float>
+template <int BM, int BN, int WM, int WN, int KS, int BK, bool UT, typename OT = float, typename IT = float>
 __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void igemm_conv_kernel(IgemmArgs a) {
   const IT* __restrict__ in = static_cast<const IT*>(a.in);
   const IT* add = static_cast<const IT*>(a.add);
@@ -98,11 +91,9 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void igemm_conv_kernel(
   constexpr int MI = WM / 32, NI = WN / 32;
   constexpr int WAVES_N = BN / WN;
   static_assert(NT == 256 || NT == 512, "4 or 8 waves per block");
-  static_assert(!BNB || (UT && SEG_IGEMM_STAGES == 1), "BN-backward loads: uniform-tap loader, one LDS stage");
   static_assert(NT % KQ == 0 && NT % KQA == 0, "uniform kq per thread");
   static_assert(!LP || BK % 16 == 0, "16-bit MFMA steps are 16 deep");
   static_assert(sizeof(lds_t) * BM * LDSR >= 4 * (BM / WM + 1) * BN, "BN-statistics scratch fits in As");
-  static_assert(sizeof(lds_t) * BM * LDSR >= 4 * 2 * (BM / WM) * BN, "BN-backward reduction scratch fits in As");
 
   __shared__ __attribute__((aligned(16))) lds_t As[SEG_IGEMM_STAGES][BM * LDSR];
   __shared__ __attribute__((aligned(16))) lds_t Bs[SEG_IGEMM_STAGES][BN * LDSR];
@@ -157,13 +148,6 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void igemm_conv_kernel(
   int u_tap = 0, u_ci = 0;
   long u_toff0 = 0, u_toff1 = 0;
   auto tap_off = [&](int t) -> long { return ((long)(t / KS) * a.W + t % KS) * a.ldin; };
-  // BNB: y-side offsets (y has its own row stride), the loaded y, the slots' validity
-  // bits and the chunk's channel-group coefficients
-  long u_yoff[BNB ? A_PER : 1];
-  long u_ytoff0 = 0, u_ytoff1 = 0;
-  f32x4 ry[BNB ? A_PER : 1], cf[6];
-  unsigned u_okbits = 0;
-  auto tap_off_y = [&](int t) -> long { return ((long)(t / KS) * a.W + t % KS) * a.bnb.ldy; };
   if (UT) {
 #pragma unroll
     for (int i = 0; i < A_PER; ++i) {
@@ -174,7 +158,6 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void igemm_conv_kernel(
       const int pp = ok ? p : 0;
       if (KS == 1) {
         u_aoff[i] = (long)pp * a.ldin;
-        if (BNB) u_yoff[BNB ? i : 0] = (long)pp * a.bnb.ldy;
         u_mask[i] = ok ? 1u : 0u;
       } else {
         const int hw = a.Ho * a.Wo;
@@ -182,7 +165,6 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void igemm_conv_kernel(
         const int ho = rem / a.Wo, wo = rem - ho * a.Wo;
         const int hi0 = ho * a.stride - a.pad, wi0 = wo * a.stride - a.pad;
         u_aoff[i] = (((long)n * a.H + hi0) * a.W + wi0) * a.ldin;
-        if (BNB) u_yoff[BNB ? i : 0] = (((long)n * a.H + hi0) * a.W + wi0) * a.bnb.ldy;
         unsigned m = 0;
 #pragma unroll
         for (int t = 0; t < KS * KS; ++t) {
@@ -203,10 +185,6 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void igemm_conv_kernel(
     u_ci = kbeg - u_tap * a.Cin;
     u_toff0 = tap_off(u_tap);
     u_toff1 = tap_off(u_tap + 1);
-    if (BNB) {
-      u_ytoff0 = tap_off_y(u_tap);
-      u_ytoff1 = tap_off_y(u_tap + 1);
-    }
   }
 
   auto load_tiles = [&](int k0, f32x4 (&ra)[A_PER], f32x4 (&rb)[B_PER]) {
@@ -226,18 +204,6 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void igemm_conv_kernel(
         else
           ra[i] = ld4(ok ? in + u_aoff[i] + off : zero4);
       }
-      if (BNB) {
-        const long offy = (wrap ? u_ytoff1 : u_ytoff0) + (wrap ? ci - a.Cin : ci);
-        const bool kin_a = k0 + u_kq4 < a.K;
-        u_okbits = 0;
-#pragma unroll
-        for (int i = 0; i < A_PER; ++i) {
-          const bool ok = kin_a && ((u_mask[i] >> tap) & 1u);
-          ry[BNB ? i : 0] = ld4(ok ? a.bnb.y + u_yoff[BNB ? i : 0] + offy : g_zero4);
-          u_okbits |= (ok ? 1u : 0u) << i;
-        }
-        seg_bnbwd_coef(a.bnb, kin_a ? (wrap ? ci - a.Cin : ci) : 0, cf);
-      }
       const bool kin = k0 + u_kq4 < a.K;
 #pragma unroll
       for (int i = 0; i < B_PER; ++i) rb[i] = ld4(u_bok[i] && kin ? a.wk + u_boff[i] + k0 : g_zero4);
@@ -247,10 +213,6 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void igemm_conv_kernel(
         ++u_tap;
         u_toff0 = u_toff1;
         u_toff1 = tap_off(u_tap + 1);
-        if (BNB) {
-          u_ytoff0 = u_ytoff1;
-          u_ytoff1 = tap_off_y(u_tap + 1);
-        }
       }
       return;
     }
@@ -297,11 +259,7 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void igemm_conv_kernel(
     for (int i = 0; i < A_PER; ++i) {
       const int idx = tid + i * NT;
       if (A_VEC % NT == 0 || idx < A_VEC) {
-        f32x4 v = ra[i];
-        if (BNB) {
-          const f32x4 t = seg_bnbwd4(v, ry[BNB ? i : 0], cf[0], cf[1], cf[2], cf[3], cf[4], cf[5], a.bnb.act);
-          v = ((u_okbits >> i) & 1u) ? t : f32x4{0.f, 0.f, 0.f, 0.f};
-        }
+        const f32x4 v = ra[i];
         if constexpr (VA == 8)
           *reinterpret_cast<f32x4*>(&As[buf][(idx / KQA) * LDSR + (idx % KQA) * 8]) = v;
         else
@@ -483,23 +441,10 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void igemm_conv_kernel(
       __syncthreads();
     }
   }
-  // BN-backward reduction (a.red.part): this data gradient completes dA of a layer
-  // y -> BN -> act; per column, the tile's sum(dz) and sum(dz * (y - mean)) with
-  // dz = dA * act'(y * scale + shift) -- chan_partial_kernel<1>'s sums, from the values
-  // just written, so seg_bn_backward_parts never re-reads dA and y for its reduction.
-  const bool red = a.red.part != nullptr;
-  float rs0[NI], rs1[NI];
 #pragma unroll
   for (int ni = 0; ni < NI; ++ni) {
-    rs0[ni] = rs1[ni] = 0.f;
     const int col = n0 + wn0 + ni * 32 + lrow;
     if (col >= a.Cout) continue;
-    float rsc = 0.f, rsh = 0.f, rmu = 0.f;
-    if (red) {
-      rsc = a.red.scale[col];
-      rsh = a.red.shift[col];
-      rmu = a.red.mean[col];
-    }
 #pragma unroll
     for (int mi = 0; mi < MI; ++mi) {
 #pragma unroll
@@ -510,41 +455,8 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void igemm_conv_kernel(
           if (add) v += (float)add[(long)row * a.ldadd + col];
           if (a.act) v = seg_act(v, a.act);
           out[(long)row * a.ldout + col] = static_cast<IT>(v);
-          if (red) {
-            const float yv = a.red.y[(long)row * a.red.ldy + col];
-            const float dz = v * seg_act_mask(yv * rsc + rsh, a.red.act);
-            rs0[ni] += dz;
-            rs1[ni] += dz * (yv - rmu);
-          }
         }
       }
-    }
-  }
-  if (red) {
-    constexpr int WR = BM / WM;
-    float* scr = reinterpret_cast<float*>(&As[0][0]);  // [2][WR][BN]
-    const int wr = wave / WAVES_N;
-    __syncthreads();
-#pragma unroll
-    for (int ni = 0; ni < NI; ++ni) {
-      const int cl = wn0 + ni * 32 + lrow;
-      const float s0 = rs0[ni] + __shfl_xor(rs0[ni], 32, 64);
-      const float s1 = rs1[ni] + __shfl_xor(rs1[ni], 32, 64);
-      if (lane < 32) {
-        scr[wr * BN + cl] = s0;
-        scr[(WR + wr) * BN + cl] = s1;
-      }
-    }
-    __syncthreads();
-    if (tid < BN && n0 + tid < a.Cout) {
-      float t0 = 0.f, t1 = 0.f;
-#pragma unroll
-      for (int j = 0; j < WR; ++j) {
-        t0 += scr[j * BN + tid];
-        t1 += scr[(WR + j) * BN + tid];
-      }
-      a.red.part[((long)tm * 2) * a.Cout + n0 + tid] = t0;
-      a.red.part[((long)tm * 2 + 1) * a.Cout + n0 + tid] = t1;
     }
   }
 }
@@ -556,20 +468,13 @@ int launch_igemm_bk(const IgemmArgs& a, int ks, hipStream_t s) {
   const bool ut = SEG_IGEMM_UT && (SEG_IGEMM_UT2 ? a.Cin >= BK : a.Cin % BK == 0) &&
                   (sizeof(IT) == 4 || (a.Cin % 8 == 0 && a.ldin % 8 == 0));  // bf16 A: 16-byte slots
   constexpr int NT = 64 * (BM / WM) * (BN / WN);
-#define SEG_IG(KS, U) hipLaunchKernelGGL((igemm_conv_kernel<BM, BN, WM, WN, KS, BK, U, false, OT, IT>), dim3(grid, splits), dim3(NT), 0, s, a)
-#define SEG_IGB(KS) hipLaunchKernelGGL((igemm_conv_kernel<BM, BN, WM, WN, KS, BK, true, true, OT, IT>), dim3(grid, splits), dim3(NT), 0, s, a)
-  if (a.bnb.y) {
-    if (!ut) return (int)hipErrorInvalidValue;
-    if (ks == 1) SEG_IGB(1); else SEG_IGB(3);
-    SEG_RET_LAST();
-  }
+#define SEG_IG(KS, U) hipLaunchKernelGGL((igemm_conv_kernel<BM, BN, WM, WN, KS, BK, U, OT, IT>), dim3(grid, splits), dim3(NT), 0, s, a)
   if (ks == 1) {
     if (ut) SEG_IG(1, true); else SEG_IG(1, false);
   } else {
     if (ut) SEG_IG(3, true); else SEG_IG(3, false);
   }
 #undef SEG_IG
-#undef SEG_IGB
   SEG_RET_LAST();
 }
 
@@ -669,11 +574,8 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restr
 template <typename OT, typename IT = float>
 int conv_igemm_impl(const IT* in, long ldin, int N, int H, int W, int Cin, const float* wk, int ldk,
                     const float* bias, IT* out, long ldout, int Ho, int Wo, int Cout, int ks, int stride, int pad,
-                    const IT* add, long ldadd, float* stat, int act, float* work, int splits, hipStream_t stream,
-                    const SegBnRed* red = nullptr) {
-  if (!std::is_same<IT, float>::value && (splits != 1 || red)) return (int)hipErrorInvalidValue;
-  if (red && (splits != 1 || stat || act || !red->y || !red->scale || !red->shift || !red->mean))
-    return (int)hipErrorInvalidValue;
+                    const IT* add, long ldadd, float* stat, int act, float* work, int splits, hipStream_t stream) {
+  if (!std::is_same<IT, float>::value && splits != 1) return (int)hipErrorInvalidValue;
   if ((Cin & 3) || (ldin & 3) || (ldk & 3) || (ks != 1 && ks != 3)) return (int)hipErrorInvalidValue;
   if (ks == 1 && (stride != 1 || pad != 0 || Ho != H || Wo != W)) return (int)hipErrorInvalidValue;
   if (act < SEG_ACT_NONE || act > SEG_ACT_RELU6 || (act && stat)) return (int)hipErrorInvalidValue;
@@ -684,8 +586,6 @@ int conv_igemm_impl(const IT* in, long ldin, int N, int H, int W, int Cin, const
   a.N = N; a.H = H; a.W = W; a.Cin = Cin; a.Ho = Ho; a.Wo = Wo; a.Cout = Cout;
   a.stride = stride; a.pad = pad; a.K = ks * ks * Cin; a.M = N * Ho * Wo; a.act = act;
   a.part = splits > 1 ? work : nullptr;
-  a.bnb = SegBnBwd{};
-  a.red = red ? *red : SegBnRed{};
   if (a.M == 0 || Cout == 0) return 0;
   int rc;
   switch (pick_tile(a.M, Cout)) {

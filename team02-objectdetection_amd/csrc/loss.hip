@@ -10,6 +10,10 @@
 // The full-resolution logits z_p are never stored: each kernel recomputes them
 // from the NHWC low-resolution logits (4 taps x C), which stay L2-resident.
 // The loss reduction is deterministic: per-block partials, then one fp64 pass.
+// A label outside [0, C) that is not ignore_index (aten raises "Target out of
+// bounds") is counted in out2[2] and poisons the loss and the gradient with NaN --
+// stream-ordered, no host sync; the host raises when it reads the loss
+// (seg_amd.train / engine.check_targets).
 #include "common.h"
 
 namespace {
@@ -77,12 +81,16 @@ __global__ __launch_bounds__(256) void ce_up_loss_kernel(const T* __restrict__ l
                                                          int C, const long long* __restrict__ labels, int Ho, int Wo,
                                                          float sh, float sw, int ignore_index,
                                                          float* __restrict__ part) {
-  __shared__ float red_l[4], red_c[4];
+  __shared__ float red_l[4], red_c[4], red_b[4];
   const long total = (long)N * Ho * Wo;
-  float lsum = 0.f, cnt = 0.f;
+  float lsum = 0.f, cnt = 0.f, bad = 0.f;
   for (long p = blockIdx.x * (long)blockDim.x + threadIdx.x; p < total; p += (long)gridDim.x * blockDim.x) {
     const long long y = labels[p];
     if (y == ignore_index) continue;
+    if (y < 0 || y >= C) {
+      bad += 1.f;
+      continue;
+    }
     const int n = (int)(p / ((long)Ho * Wo));
     const int rem = (int)(p - (long)n * Ho * Wo);
     const int r = rem / Wo, s = rem - r * Wo;
@@ -95,29 +103,34 @@ __global__ __launch_bounds__(256) void ce_up_loss_kernel(const T* __restrict__ l
   }
   lsum = wave_sum(lsum);
   cnt = wave_sum(cnt);
+  bad = wave_sum(bad);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  if (lane == 0) { red_l[wave] = lsum; red_c[wave] = cnt; }
+  if (lane == 0) { red_l[wave] = lsum; red_c[wave] = cnt; red_b[wave] = bad; }
   __syncthreads();
   if (threadIdx.x == 0) {
-    part[2 * blockIdx.x] = red_l[0] + red_l[1] + red_l[2] + red_l[3];
-    part[2 * blockIdx.x + 1] = red_c[0] + red_c[1] + red_c[2] + red_c[3];
+    part[3 * blockIdx.x] = red_l[0] + red_l[1] + red_l[2] + red_l[3];
+    part[3 * blockIdx.x + 1] = red_c[0] + red_c[1] + red_c[2] + red_c[3];
+    part[3 * blockIdx.x + 2] = red_b[0] + red_b[1] + red_b[2] + red_b[3];
   }
 }
 
-// out[0] = mean loss, out[1] = #valid pixels (as float)
+// out[0] = mean loss, out[1] = #valid pixels, out[2] = #out-of-range labels (as floats)
 __global__ void ce_finalize_kernel(const float* __restrict__ part, int nblk, float* out) {
-  double l = 0.0, c = 0.0;
-  for (int b = threadIdx.x; b < nblk; b += 64) {
-    l += part[2 * b];
-    c += part[2 * b + 1];
+  double l = 0.0, c = 0.0, b = 0.0;
+  for (int k = threadIdx.x; k < nblk; k += 64) {
+    l += part[3 * k];
+    c += part[3 * k + 1];
+    b += part[3 * k + 2];
   }
   for (int o = 32; o > 0; o >>= 1) {
     l += __shfl_xor(l, o, 64);
     c += __shfl_xor(c, o, 64);
+    b += __shfl_xor(b, o, 64);
   }
   if (threadIdx.x == 0) {
-    out[0] = (float)(l / c);  // 0/0 = nan when every pixel is ignored, as aten
+    out[0] = b > 0.0 ? __builtin_nanf("") : (float)(l / c);  // 0/0 = nan when every pixel is ignored, as aten
     out[1] = (float)c;
+    out[2] = (float)b;
   }
 }
 
@@ -129,11 +142,11 @@ __global__ __launch_bounds__(256) void ce_up_grad_kernel(const T* __restrict__ l
                                                          const float* __restrict__ gout, const float* __restrict__ stats,
                                                          T* __restrict__ dhigh, long ldh) {
   const long total = (long)N * Ho * Wo;
-  const float scale = gout[0] / stats[1];
+  const float scale = stats[2] > 0.f ? __builtin_nanf("") : gout[0] / stats[1];
   for (long p = blockIdx.x * (long)blockDim.x + threadIdx.x; p < total; p += (long)gridDim.x * blockDim.x) {
     const long long y = labels[p];
     T* d = dhigh + p * ldh;
-    if (y == ignore_index) {
+    if (y == ignore_index || y < 0 || y >= C) {  // out of range: scale is NaN, the loss already is
 #pragma unroll
       for (int c = 0; c < CP; c += 4) st4(d + c, f32x4{0.f, 0.f, 0.f, 0.f});
       continue;
@@ -163,10 +176,10 @@ int loss_blocks(long total) { return (int)std::min<long>(seg_cdiv(total, 256), 2
 
 }  // namespace
 
-SEG_API long seg_ce_workspace_floats(long pixels) { return 2L * loss_blocks(pixels); }
+SEG_API long seg_ce_workspace_floats(long pixels) { return 3L * loss_blocks(pixels); }
 
-// Mean CE of bilinear_ac_true_x(Ho,Wo)(low) against labels.  out2[0] = loss,
-// out2[1] = number of non-ignored pixels.  `work` >= seg_ce_workspace_floats(N*Ho*Wo).
+// Mean CE of bilinear_ac_true_x(Ho,Wo)(low) against labels.  out3[0] = loss,
+// out3[1] = number of non-ignored pixels, out3[2] = number of out-of-range labels.  `work` >= seg_ce_workspace_floats(N*Ho*Wo).
 template <typename T>
 static int ce_loss_impl(const T* low, long ld, int N, int H, int W, int C, const long long* labels, int Ho, int Wo,
                         int ignore_index, float* work, float* out2, hipStream_t stream) {

@@ -30,7 +30,6 @@ struct WgradArgs {
   float* part;
   int N, H, W, Cin, Ho, Wo, Cout, stride, pad;
   int M, Nw, kchunk;
-  SegBnBwd bnb;  // BNB: dy is dA and the dY operand is the BN backward formed on load
 };
 
 // Row pitch (bf16 elements) of a k-major bf16 tile read with ds_read_b64_tr_b16: a
@@ -44,7 +43,7 @@ constexpr int tr_pitch(int n) { return n % 128 == 32 || n % 128 == 96 ? n : tr_p
 // column-major) and fed to v_mfma_f32_32x32x16_bf16; fp32 accumulation and slabs.
 // VW: channels per load slot -- 8 (one 16-byte load, copied to LDS as is) on bf16
 // storage when Cout, Cin and the row strides are multiples of 8, else 4.
-template <int BM, int BN, int WM, int WN, int KS, bool BNB = false, bool BF = false, typename IT = float, int VW = 4>
+template <int BM, int BN, int WM, int WN, int KS, bool BF = false, typename IT = float, int VW = 4>
 __global__ __launch_bounds__(256) void wgrad_kernel(WgradArgs a) {
   static_assert(VW == 4 || (BF && sizeof(IT) == 2), "16-byte slots carry bf16 operands");
   const IT* __restrict__ gdy = static_cast<const IT*>(a.dy);
@@ -55,7 +54,6 @@ __global__ __launch_bounds__(256) void wgrad_kernel(WgradArgs a) {
   constexpr int A_PER = (A_VEC + 255) / 256, B_PER = (B_VEC + 255) / 256;
   constexpr int MI = WM / 32, NI = WN / 32, WAVES_N = BN / WN;
   static_assert((BM / WM) * (BN / WN) == 4, "4 waves per block");
-  static_assert(!(BNB && BF), "no BN-backward-on-load with bf16 math");
   using lds_t = typename std::conditional<BF, __bf16, float>::type;
 
   __shared__ __attribute__((aligned(16))) lds_t As[SEG_WGRAD_STAGES][BK * AR];
@@ -98,23 +96,11 @@ __global__ __launch_bounds__(256) void wgrad_kernel(WgradArgs a) {
   }
 
   f32x4 ra[A_PER], rb[B_PER];
-  // BNB: y of each A slot, its validity, and the slot's (fixed) channel coefficients
-  f32x4 ry[BNB ? A_PER : 1], cfa[BNB ? A_PER : 1][6];
-  unsigned a_okbits = 0;
-  if (BNB) {
-#pragma unroll
-    for (int i = 0; i < A_PER; ++i) {
-      const int idx = tid + i * 256;
-      const int c = co0 + (idx % (BM / 4)) * 4;
-      seg_bnbwd_coef(a.bnb, (idx < A_VEC && c < a.Cout) ? c : 0, cfa[BNB ? i : 0]);
-    }
-  }
   auto ldv = [](const IT* q) -> f32x4 {  // one load slot: 4 channels widened, or 8 bf16 raw
     if constexpr (VW == 8) return *reinterpret_cast<const f32x4*>(q);
     else return ld4(q);
   };
   auto load_tiles = [&](int k0) {  // k0 = first pixel of this chunk
-    if (BNB) a_okbits = 0;
 #pragma unroll
     for (int i = 0; i < A_PER; ++i) {
       const int idx = tid + i * 256;
@@ -124,12 +110,6 @@ __global__ __launch_bounds__(256) void wgrad_kernel(WgradArgs a) {
       const bool ok = idx < A_VEC && p < kend && c < a.Cout;
       if (ok) v = ldv(gdy + (long)p * a.lddy + c);
       ra[i] = v;
-      if (BNB) {
-        f32x4 w = {0.f, 0.f, 0.f, 0.f};
-        if (ok) w = ld4(a.bnb.y + (long)p * a.bnb.ldy + c);
-        ry[BNB ? i : 0] = w;
-        a_okbits |= (ok ? 1u : 0u) << i;
-      }
     }
 #pragma unroll
     for (int i = 0; i < B_PER; ++i) {
@@ -163,13 +143,7 @@ __global__ __launch_bounds__(256) void wgrad_kernel(WgradArgs a) {
     for (int i = 0; i < A_PER; ++i) {
       const int idx = tid + i * 256;
       if (idx < A_VEC) {
-        f32x4 v = ra[i];
-        if (BNB) {
-          const f32x4(&cf)[6] = cfa[BNB ? i : 0];
-          const f32x4 t = seg_bnbwd4(v, ry[BNB ? i : 0], cf[0], cf[1], cf[2], cf[3], cf[4], cf[5], a.bnb.act);
-          v = ((a_okbits >> i) & 1u) ? t : f32x4{0.f, 0.f, 0.f, 0.f};
-        }
-        st_op(&As[buf][(idx / (BM / VW)) * AR + (idx % (BM / VW)) * VW], v);
+        st_op(&As[buf][(idx / (BM / VW)) * AR + (idx % (BM / VW)) * VW], ra[i]);
       }
     }
 #pragma unroll
@@ -272,26 +246,22 @@ template <int BM, int BN, int WM, int WN, bool BF = false, typename IT = float>
 int launch_wgrad(const WgradArgs& a, int ks, int splits, hipStream_t s) {
   dim3 grid(seg_cdiv(a.Cout, BM) * seg_cdiv(a.Nw, BN) * splits);
   if (BF) {
-    if (a.bnb.y) return (int)hipErrorInvalidValue;
     const bool v8 = sizeof(IT) == 2 && a.Cout % 8 == 0 && a.Cin % 8 == 0 && a.lddy % 8 == 0 && a.ldx % 8 == 0;
     if constexpr (sizeof(IT) == 2) {
       if (v8) {
-        if (ks == 1) hipLaunchKernelGGL((wgrad_kernel<BM, BN, WM, WN, 1, false, true, IT, 8>), grid, dim3(256), 0, s, a);
-        else hipLaunchKernelGGL((wgrad_kernel<BM, BN, WM, WN, 3, false, true, IT, 8>), grid, dim3(256), 0, s, a);
+        if (ks == 1) hipLaunchKernelGGL((wgrad_kernel<BM, BN, WM, WN, 1, true, IT, 8>), grid, dim3(256), 0, s, a);
+        else hipLaunchKernelGGL((wgrad_kernel<BM, BN, WM, WN, 3, true, IT, 8>), grid, dim3(256), 0, s, a);
         SEG_RET_LAST();
       }
     }
     if (ks == 1) {
-      hipLaunchKernelGGL((wgrad_kernel<BM, BN, WM, WN, 1, false, true, IT>), grid, dim3(256), 0, s, a);
+      hipLaunchKernelGGL((wgrad_kernel<BM, BN, WM, WN, 1, true, IT>), grid, dim3(256), 0, s, a);
     } else {
-      hipLaunchKernelGGL((wgrad_kernel<BM, BN, WM, WN, 3, false, true, IT>), grid, dim3(256), 0, s, a);
+      hipLaunchKernelGGL((wgrad_kernel<BM, BN, WM, WN, 3, true, IT>), grid, dim3(256), 0, s, a);
     }
     SEG_RET_LAST();
   }
-  if (a.bnb.y) {
-    if (ks == 1) hipLaunchKernelGGL((wgrad_kernel<BM, BN, WM, WN, 1, true>), grid, dim3(256), 0, s, a);
-    else hipLaunchKernelGGL((wgrad_kernel<BM, BN, WM, WN, 3, true>), grid, dim3(256), 0, s, a);
-  } else if (ks == 1) hipLaunchKernelGGL((wgrad_kernel<BM, BN, WM, WN, 1>), grid, dim3(256), 0, s, a);
+  if (ks == 1) hipLaunchKernelGGL((wgrad_kernel<BM, BN, WM, WN, 1>), grid, dim3(256), 0, s, a);
   else hipLaunchKernelGGL((wgrad_kernel<BM, BN, WM, WN, 3>), grid, dim3(256), 0, s, a);
   SEG_RET_LAST();
 }
@@ -320,13 +290,13 @@ SEG_API int seg_conv_wgrad_splits(long M, int Cout, int Cin, int ks) {
 
 // part[s][co][tap*Cin+ci] = sum over split s's pixels of dY[p][co] * X[src(p,tap)][ci].
 static int conv_wgrad(const void* dy, long lddy, const void* x, long ldx, int N, int H, int W, int Cin, int Ho,
-                      int Wo, int Cout, int ks, int stride, int pad, float* part, int splits, const SegBnBwd& bnb,
+                      int Wo, int Cout, int ks, int stride, int pad, float* part, int splits,
                       hipStream_t stream, bool bf = false, bool bf_io = false);
 
 SEG_API int seg_conv_wgrad(const float* dy, long lddy, const float* x, long ldx,
                            int N, int H, int W, int Cin, int Ho, int Wo, int Cout,
                            int ks, int stride, int pad, float* part, int splits, hipStream_t stream) {
-  return conv_wgrad(dy, lddy, x, ldx, N, H, W, Cin, Ho, Wo, Cout, ks, stride, pad, part, splits, SegBnBwd{}, stream);
+  return conv_wgrad(dy, lddy, x, ldx, N, H, W, Cin, Ho, Wo, Cout, ks, stride, pad, part, splits, stream);
 }
 
 // seg_conv_wgrad with bf16 math (the bf16 configurations): operands rounded to bf16
@@ -334,7 +304,7 @@ SEG_API int seg_conv_wgrad(const float* dy, long lddy, const float* x, long ldx,
 SEG_API int seg_conv_wgrad_bf16(const float* dy, long lddy, const float* x, long ldx,
                                 int N, int H, int W, int Cin, int Ho, int Wo, int Cout,
                                 int ks, int stride, int pad, float* part, int splits, hipStream_t stream) {
-  return conv_wgrad(dy, lddy, x, ldx, N, H, W, Cin, Ho, Wo, Cout, ks, stride, pad, part, splits, SegBnBwd{}, stream,
+  return conv_wgrad(dy, lddy, x, ldx, N, H, W, Cin, Ho, Wo, Cout, ks, stride, pad, part, splits, stream,
                     true);
 }
 
@@ -342,24 +312,12 @@ SEG_API int seg_conv_wgrad_bf16(const float* dy, long lddy, const float* x, long
 SEG_API int seg_conv_wgrad_bf16io(const __bf16* dy, long lddy, const __bf16* x, long ldx,
                                   int N, int H, int W, int Cin, int Ho, int Wo, int Cout,
                                   int ks, int stride, int pad, float* part, int splits, hipStream_t stream) {
-  return conv_wgrad(dy, lddy, x, ldx, N, H, W, Cin, Ho, Wo, Cout, ks, stride, pad, part, splits, SegBnBwd{}, stream,
+  return conv_wgrad(dy, lddy, x, ldx, N, H, W, Cin, Ho, Wo, Cout, ks, stride, pad, part, splits, stream,
                     true, true);
 }
 
-// seg_conv_wgrad of a conv whose output went through a train-mode BatchNorm, with the
-// BN backward applied on load: dy = dA, y / scale / shift / mean / k / bn_act as
-// seg_conv_igemm_bnb (Cout % 4 == 0).
-SEG_API int seg_conv_wgrad_bnb(const float* dy, long lddy, const float* x, long ldx, int N, int H, int W, int Cin,
-                               int Ho, int Wo, int Cout, int ks, int stride, int pad, float* part, int splits,
-                               const float* y, long ldy, const float* scale, const float* shift, const float* mean,
-                               const float* k, int bn_act, hipStream_t stream) {
-  if (!y || !k || !scale || !shift || !mean || (ldy & 3) || (Cout & 3)) return (int)hipErrorInvalidValue;
-  return conv_wgrad(dy, lddy, x, ldx, N, H, W, Cin, Ho, Wo, Cout, ks, stride, pad, part, splits,
-                    SegBnBwd{y, ldy, scale, shift, mean, k, Cout, bn_act}, stream);
-}
-
 static int conv_wgrad(const void* dy, long lddy, const void* x, long ldx, int N, int H, int W, int Cin, int Ho,
-                      int Wo, int Cout, int ks, int stride, int pad, float* part, int splits, const SegBnBwd& bnb,
+                      int Wo, int Cout, int ks, int stride, int pad, float* part, int splits,
                       hipStream_t stream, bool bf, bool bf_io) {
   if ((Cin & 3) || (ldx & 3) || (lddy & 3) || (ks != 1 && ks != 3) || splits < 1) return (int)hipErrorInvalidValue;
   if (ks == 1 && (stride != 1 || pad != 0)) return (int)hipErrorInvalidValue;
@@ -368,7 +326,6 @@ static int conv_wgrad(const void* dy, long lddy, const void* x, long ldx, int N,
   a.N = N; a.H = H; a.W = W; a.Cin = Cin; a.Ho = Ho; a.Wo = Wo; a.Cout = Cout;
   a.stride = stride; a.pad = pad; a.M = N * Ho * Wo; a.Nw = ks * ks * Cin;
   a.kchunk = seg_cdiv(seg_cdiv(a.M, splits), BK) * BK;
-  a.bnb = bnb;
   int bm, bn;
   wgrad_tiles(Cout, a.Nw, &bm, &bn);
   if (bf_io) {

@@ -26,14 +26,7 @@ PROTOTYPES = {
                                  _V, _I, _V]),
     "seg_conv_igemm_f16": (_I, [_V, _L, _I, _I, _I, _I, _V, _I, _V, _V, _L, _I, _I, _I, _I, _I, _I, _V, _L, _V, _I,
                                 _V, _I, _V]),
-    "seg_conv_igemm_red": (_I, [_V, _L, _I, _I, _I, _I, _V, _I, _V, _L, _I, _I, _I, _V, _L, _V, _L, _V, _V, _V, _I,
-                                _V, _V]),
-    "seg_conv_igemm_red_bf16": (_I, [_V, _L, _I, _I, _I, _I, _V, _I, _V, _L, _I, _I, _I, _V, _L, _V, _L, _V, _V, _V,
-                                     _I, _V, _V]),
     "seg_conv_igemm_splits": (_I, [_L, _I, _I, _I]),
-    "seg_conv_igemm_bnb": (_I, [_V, _L, _I, _I, _I, _I, _V, _I, _V, _L, _I, _I, _I, _V, _L, _V, _L, _V, _V, _V, _V, _I,
-                                _V]),
-    "seg_conv_igemm_bnb_ok": (_I, [_I, _I]),
     "seg_igemm_force_tile": (_I, [_I]),
     "seg_conv_halo_ok": (_I, [_I, _I, _I, _I, _I]),
     "seg_conv_halo_pick": (_I, [_I, _I, _I, _I, _I]),
@@ -52,8 +45,6 @@ PROTOTYPES = {
     "seg_conv_wgrad_splits": (_I, [_L, _I, _I, _I]),
     "seg_conv_wgrad": (_I, [_V, _L, _V, _L, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _V, _I, _V]),
     "seg_conv_wgrad_bf16": (_I, [_V, _L, _V, _L, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _V, _I, _V]),
-    "seg_conv_wgrad_bnb": (_I, [_V, _L, _V, _L, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _V, _I, _V, _L, _V, _V, _V, _V,
-                                _I, _V]),
     "seg_conv_wgrad_reduce": (_I, [_V, _I, _V, _I, _I, _I, _I, _I, _V]),
     "seg_pack_dw_weight": (_I, [_V, _V, _I, _V]),
     "seg_dw_fwd": (_I, [_V, _L, _I, _I, _I, _I, _V, _V, _I, _V, _V, _L, _I, _I, _I, _V]),
@@ -68,15 +59,8 @@ PROTOTYPES = {
     "seg_bn_eval_coef": (_I, [_V, _V, _V, _V, _F, _I, _V, _V, _V]),
     "seg_bn_apply": (_I, [_V, _L, _L, _I, _V, _V, _I, _V, _L, _V, _L, _V]),
     "seg_bn_backward": (_I, [_V, _L, _V, _L, _L, _I, _V, _V, _V, _V, _V, _I, _V, _V, _V, _V, _L, _V]),
-    "seg_bn_backward_parts": (_I, [_V, _I, _V, _L, _V, _L, _L, _I, _V, _V, _V, _V, _V, _I, _V, _V, _V, _V, _L, _V]),
-    "seg_bn_backward_coef": (_I, [_V, _L, _V, _L, _L, _I, _V, _V, _V, _V, _V, _I, _V, _V, _V, _V, _V]),
-    "seg_pw_bwd_fused_ok": (_I, [_I, _I]),
-    "seg_pw_bwd_blocks": (_I, [_L]),
-    "seg_pw_bwd_fused": (_I, [_V, _L, _V, _L, _V, _L, _V, _I, _V, _V, _V, _V, _I, _V, _L, _V, _L, _V, _I, _L, _I, _I,
-                              _V]),
     "seg_bn_eval_backward": (_I, [_V, _L, _V, _L, _L, _I, _V, _V, _I, _V, _L, _V]),
     "seg_colsum": (_I, [_V, _L, _L, _I, _V, _V, _I, _V]),
-    "seg_colsum_bnb": (_I, [_V, _L, _V, _L, _L, _I, _V, _V, _V, _V, _I, _V, _V, _I, _V]),
     "seg_add": (_I, [_V, _L, _V, _L, _L, _I, _V, _L, _V]),
     "seg_upsample_fwd": (_I, [_V, _L, _I, _I, _I, _I, _V, _L, _I, _I, _I, _V]),
     "seg_upsample_bwd": (_I, [_V, _L, _I, _I, _I, _I, _I, _V, _L, _I, _I, _I, _I, _V]),

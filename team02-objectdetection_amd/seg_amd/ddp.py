@@ -18,13 +18,17 @@ Mechanism (no autograd hooks needed -- the engine IS the backward):
     (torch.distributed -> RCCL on its own stream, ordered after the producing
     kernels on the compute stream), so communication of the decoder's 3.1 M
     `up1.conv.0` weights overlaps the encoder's backward;
-  * `finish_gradient_sync()` (called by train_model before optimizer.step)
-    makes the compute stream wait for the outstanding all-reduces and scales
-    by 1/world.
+  * `finish_gradient_sync()` (called by the engine at the end of the backward)
+    makes the compute stream wait for the outstanding all-reduces (RCCL
+    averages in the reduction, ncclAvg); autograd receives views of a copy of
+    each bucket (`autograd_grads`), never the bucket itself;
+  * BN running statistics are views of one flat tensor: one broadcast per step.
 The unused `backbone.classifier` parameters never receive gradients (as in
 the reference, where Adam skips them), so no find_unused_parameters dance.
 """
 from __future__ import annotations
+
+import contextlib
 
 import torch
 import torch.distributed as dist
@@ -47,12 +51,17 @@ class DataParallel(nn.Module):
         self.world = dist.get_world_size(process_group)
         self.bucket_cap = int(bucket_cap_mb * (1 << 20) / 4)
         self.broadcast_buffers = broadcast_buffers
+        # RCCL averages inside the reduction (ncclAvg); gloo has no AVG: SUM, then one scale
+        self._avg = dist.get_backend(process_group) == "nccl"
         self._buckets = None
         self._slot = {}      # id(param) -> (bucket, offset)
         self._order = None
+        self._bn_flat = None
         module.__dict__["_segamd_sync"] = self  # plain attribute: not a registered submodule
         if init_sync:
             self._broadcast_state()
+        if broadcast_buffers:
+            self._flatten_buffers()
 
     # ---------------------------------------------------------------- setup
     @torch.no_grad()
@@ -61,16 +70,34 @@ class DataParallel(nn.Module):
             dist.broadcast(t.data, 0, group=self.pg)
 
     @torch.no_grad()
-    def _broadcast_bn_buffers(self):
-        bufs = [b for n, b in self.module.named_buffers() if b.is_floating_point()]
-        if not bufs:
+    def _flatten_buffers(self):
+        """Rebind every floating-point buffer (BN running statistics) as a view of one
+        persistent flat tensor, so the per-step broadcast is a single collective with no
+        gather / scatter copies.  load_state_dict copies in place, so the views survive."""
+        mods = [(m, n, b) for m in self.module.modules() for n, b in m._buffers.items()
+                if b is not None and b.is_floating_point()]
+        if not mods:
             return
-        flat = torch.cat([b.reshape(-1) for b in bufs])
-        dist.broadcast(flat, 0, group=self.pg)
+        dev, dt = mods[0][2].device, mods[0][2].dtype
+        if any(b.device != dev or b.dtype != dt for _, _, b in mods):
+            return  # mixed placement: keep the per-buffer tensors (broadcast falls back below)
+        flat = torch.empty(sum(b.numel() for _, _, b in mods), device=dev, dtype=dt)
         off = 0
-        for b in bufs:
-            b.copy_(flat[off:off + b.numel()].view_as(b))
+        for m, n, b in mods:
+            v = flat[off:off + b.numel()].view_as(b)
+            v.copy_(b)
+            m._buffers[n] = v
             off += b.numel()
+        self._bn_flat = flat
+
+    @torch.no_grad()
+    def _broadcast_bn_buffers(self):
+        if self._bn_flat is not None:
+            dist.broadcast(self._bn_flat, 0, group=self.pg)
+            return
+        for b in self.module.buffers():
+            if b.is_floating_point():
+                dist.broadcast(b, 0, group=self.pg)
 
     def plan_buckets(self, ordered_params):
         """Group parameters (in gradient-ready order) into ~bucket_cap buckets."""
@@ -121,7 +148,8 @@ class DataParallel(nn.Module):
             b = self._buckets[slot[0]]
             b.pending -= 1
             if b.pending == 0:
-                b.handle = dist.all_reduce(b.buf, op=dist.ReduceOp.SUM, group=self.pg, async_op=True)
+                op = dist.ReduceOp.AVG if self._avg else dist.ReduceOp.SUM
+                b.handle = dist.all_reduce(b.buf, op=op, group=self.pg, async_op=True)
 
     def _arm(self):
         for b in self._buckets:
@@ -129,7 +157,7 @@ class DataParallel(nn.Module):
             b.handle = None
 
     def finish_gradient_sync(self):
-        """Wait (stream-ordered) for every bucket's all-reduce and average."""
+        """Wait (stream-ordered) for every bucket's all-reduce; the buckets then hold the mean."""
         if self._buckets is None:
             return
         for b in self._buckets:
@@ -139,13 +167,47 @@ class DataParallel(nn.Module):
                     raise RuntimeError("segamd DDP: partially-ready gradient bucket")
                 continue
             b.handle.wait()  # stream-ordered: the compute stream waits for RCCL, the host does not
-            b.buf.mul_(1.0 / self.world)
+            if not self._avg:
+                b.buf.mul_(1.0 / self.world)
             b.handle = None
+
+    def autograd_grads(self, params):
+        """The averaged gradients handed to autograd: views of a fresh copy of each bucket
+        (one copy kernel per bucket, stream-ordered after the all-reduce).  A .grad must
+        never alias a bucket -- the next backward writes the bucket before AccumulateGrad
+        runs, so with gradient accumulation p.grad += g would add the new gradient to
+        itself."""
+        copies = {}
+        out = []
+        for p in params:
+            slot = self._slot.get(id(p))
+            if slot is None:
+                out.append(None)
+                continue
+            k, off = slot
+            c = copies.get(k)
+            if c is None:
+                c = copies[k] = self._buckets[k].buf.clone()
+            out.append(c[off:off + p.numel()].view_as(p))
+        return out
+
+    @contextlib.contextmanager
+    def no_sync(self):
+        """Like torch DDP's no_sync(): backward passes inside the context keep their
+        gradients local (no all-reduce); they accumulate into .grad as usual."""
+        d = self.module.__dict__
+        saved = d.pop("_segamd_sync", None)
+        try:
+            yield
+        finally:
+            if saved is not None:
+                d["_segamd_sync"] = saved
 
     # --------------------------------------------------------------- forward
     def _pre(self, x):
-        self._ensure_plan(x)
-        self._arm()
+        if self.module.__dict__.get("_segamd_sync") is self:
+            self._ensure_plan(x)
+            self._arm()
         if self.broadcast_buffers and self.module.training:
             self._broadcast_bn_buffers()
 

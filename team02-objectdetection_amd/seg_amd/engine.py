@@ -34,7 +34,7 @@ from ._lib import call, query as _query
 # arguments: memoised, so a training step does not pay a ctypes call for each of them.
 _PURE_QUERIES = {"seg_chan_workspace_floats", "seg_conv_wgrad_splits", "seg_dw_wgrad_blocks",
                  "seg_conv_igemm_splits", "seg_ce_workspace_floats", "seg_conv_wino_row_tiles",
-                 "seg_conv_halo_row_tiles", "seg_conv_wino_wgrad_splits", "seg_pw_bwd_blocks"}
+                 "seg_conv_halo_row_tiles", "seg_conv_wino_wgrad_splits"}
 _QCACHE = {}
 
 
@@ -74,20 +74,6 @@ class KernelTimer:
 
 
 TIMER: KernelTimer | None = None
-
-# The fused 1x1-conv + BN backward (seg_pw_bwd_fused) reads dA, y and x once instead of
-# five passes, but measured slower than the separate kernels on MI355X in round 1
-# (1.73 vs ~1.3 ms/step over the high-resolution 1x1 layers: one 32-pixel tile in
-# flight per block leaves HBM latency exposed).  Parity-tested (tests/test_gpu_ops.py);
-# off unless SEG_PW_FUSED=1.
-PW_FUSED = os.environ.get("SEG_PW_FUSED", "0") == "1"
-# BatchNorm backward applied on load by the data / weight / bias gradient kernels of the
-# 1x1 convs (no dY tensor).  Parity-tested (bitwise equal to the apply path), but measured
-# 1 % slower on MI355X in round 1 (1686 vs 1703 img/s: the dgrad and side-stream wgrad
-# then read dA and y instead of one dY, and the side stream contends with the main one);
-# off unless SEG_BNB=1.
-BNB_ON_LOAD = os.environ.get("SEG_BNB", "0") == "1"
-
 
 def _stat_ptrs(st, C):
     """Device pointers of the mean / invstd / scale / shift rows of a saved [4][C] BN
@@ -151,15 +137,8 @@ class ConvOp:
         self.wino_f = self.wino_d = self.wino_w = False
         # LDS-halo direct 3x3 (seg_conv_halo) for the forward / data gradient of narrow convs
         self.halo_f = self.halo_d = False
-        # fused 1x1 + BN backward (seg_pw_bwd_fused), decided at pack time
-        self.pw_fused = False
-        # BN backward applied on load by the gradient kernels (seg_*_bnb), decided at pack time
-        self.bnb = False
         # bf16 math (Program.math == "bf16"): seg_conv_igemm_bf16 / seg_conv_wgrad_bf16
         self.bf = False
-        # fused BN-backward reduction (Program._plan_bn_red): red_for = the BN op whose dA this
-        # op's data gradient completes (computes its sums in the epilogue); red_by = the reverse
-        self.red_for = self.red_by = None
         self.ks = conv.kernel_size[0]
         self.stride = conv.stride[0]
         self.pad = conv.padding[0]
@@ -280,78 +259,6 @@ class ConvOp:
              o.H, o.W, self.cout, self.ks, self.stride, self.pad, rt.ptr(r) if r is not None else None,
              r.ld if r is not None else 0, None, act, work.data_ptr() if work is not None else None, splits, s)
 
-    def _backward_bnb(self, rt, dA):
-        """BN backward applied on load: only the reduction (dgamma, dbeta, k = [3][C]) runs
-        as its own pass; the data gradient, weight gradient and bias gradient form dY from
-        dA and y inside their loaders, so no dY tensor is written or read."""
-        s, y, i = rt.stream, self.y, self.inp
-        C, M = self.cout, y.M
-        st = rt.saved[id(self)]
-        mean, invstd, scale, shift = _stat_ptrs(st, C)
-        work = rt.tmp(query("seg_chan_workspace_floats", M, C))
-        coef = rt.tmp(3 * C)
-        call("seg_bn_backward_coef", rt.gptr(dA), dA.ld, rt.ptr(y), y.ld, M, C, self.bn.weight.data_ptr(),
-             mean, invstd, scale, shift, self.act,
-             rt.grad_param(self.bn.weight), rt.grad_param(self.bn.bias), work.data_ptr(), coef.data_ptr(), s)
-        if self.res is not None:
-            rt.add_pending(self.res, dA)
-        bn = (rt.ptr(y), y.ld, scale, shift, mean, coef.data_ptr(), self.act)
-        if rt.side is not None:
-            coef.record_stream(rt.side)  # read by the side stream after this function drops it
-        for p in (self.conv.weight, self.conv.bias):
-            if p is not None and p.requires_grad:
-                rt.grad_param(p)
-        ctx, sw = rt.fork()
-        with ctx:
-            if self.conv.bias is not None and self.conv.bias.requires_grad:
-                wk = rt.tmp(query("seg_chan_workspace_floats", M, C))
-                call("seg_colsum_bnb", rt.gptr(dA), dA.ld, rt.ptr(y), y.ld, M, C, scale, shift,
-                     mean, coef.data_ptr(), self.act, wk.data_ptr(), rt.grad_param(self.conv.bias), 0, sw)
-            if self.conv.weight.requires_grad:
-                gw = rt.grad_param(self.conv.weight)
-                splits = query("seg_conv_wgrad_splits", M, C, self.cin_pad, self.ks)
-                part = rt.tmp(splits * C * self.ks * self.ks * self.cin_pad)
-                _timed_call(f"igemm{self.ks}_wgrad", self.flops(), "seg_conv_wgrad_bnb", rt.gptr(dA), dA.ld,
-                            rt.ptr(i), i.ld, i.N, i.H, i.W, self.cin_pad, y.H, y.W, C, self.ks, self.stride,
-                            self.pad, part.data_ptr(), splits, *bn, sw)
-                call("seg_conv_wgrad_reduce", part.data_ptr(), splits, gw, C, self.cin, self.ks, 0, 0, sw)
-            rt.params_done(self.params())
-        if self.first:
-            return
-        add_ptr, add_ld = rt.begin_write_add(i)
-        _timed_call(f"igemm{self.ks}_dgrad", self.flops(), "seg_conv_igemm_bnb", rt.gptr(dA), dA.ld, y.N, y.H, y.W,
-                    C, self.wk_d.data_ptr(), self.ldk_d, rt.gptr(i), i.ld, self.cin, self.ks, self.pad, add_ptr,
-                    add_ld, *bn, s)
-        rt.mark_written(i)
-
-    def _backward_pw_fused(self, rt, dA):
-        """1x1 conv + train BN backward in one pass over dA, y, x (seg_pw_bwd_fused): the BN
-        reduction first (seg_bn_backward_coef), then dx (+ pending addend) and the dW slabs."""
-        s, y, i = rt.stream, self.y, self.inp
-        if not rt.training:
-            raise NotImplementedError("backward through eval-mode BatchNorm is not supported")
-        C, M = self.cout, y.M
-        st = rt.saved[id(self)]
-        mean, invstd, scale, shift = _stat_ptrs(st, C)
-        work = rt.tmp(query("seg_chan_workspace_floats", M, C))
-        coef = rt.tmp(3 * C)
-        call("seg_bn_backward_coef", rt.gptr(dA), dA.ld, rt.ptr(y), y.ld, M, C, self.bn.weight.data_ptr(),
-             mean, invstd, scale, shift, self.act,
-             rt.grad_param(self.bn.weight), rt.grad_param(self.bn.bias), work.data_ptr(), coef.data_ptr(), s)
-        if self.res is not None:
-            rt.add_pending(self.res, dA)
-        gw = rt.grad_param(self.conv.weight)
-        blocks = query("seg_pw_bwd_blocks", M)
-        part = rt.tmp(blocks * C * self.cin_pad)
-        add_ptr, add_ld = rt.begin_write_add(i)
-        _timed_call("pw_bwd", 2 * self.flops(), "seg_pw_bwd_fused", rt.gptr(dA), dA.ld, rt.ptr(y), y.ld, rt.ptr(i),
-                    i.ld, self.wk_d.data_ptr(), self.ldk_d, scale, shift, mean,
-                    coef.data_ptr(), self.act, add_ptr, add_ld, rt.gptr(i), i.ld, part.data_ptr(), blocks, M,
-                    self.cin, C, s)
-        call("seg_conv_wgrad_reduce", part.data_ptr(), blocks, gw, C, self.cin, 1, 0, 0, s)
-        rt.params_done(self.params())
-        rt.mark_written(i)
-
     def _in_xform(self, rt):
         """(scale, shift, act) of the producer's lazy BN for this op's input loads, or (None, None, 0)."""
         xf = self.xform
@@ -364,10 +271,6 @@ class ConvOp:
     def backward(self, rt):
         s, y = rt.stream, self.y
         dA = rt.grad_of(self.out)
-        if self.pw_fused:
-            return self._backward_pw_fused(rt, dA)
-        if self.bnb and rt.training:
-            return self._backward_bnb(rt, dA)
         if self.bn is not None:
             if not rt.training:
                 raise NotImplementedError("backward through eval-mode BatchNorm is not supported")
@@ -376,18 +279,10 @@ class ConvOp:
             mean, invstd, scale, shift = _stat_ptrs(st, C)
             dY = Act(rt.tmp_buf(M * r4(C)), 0, r4(C), C, y.N, y.H, y.W)
             g_w, g_b = rt.grad_param(self.bn.weight), rt.grad_param(self.bn.bias)
-            parts = rt.bnred.pop(id(self), None)
-            if parts is not None:  # reduction already done by the data gradient that completed dA
-                part, nparts = parts
-                coef = rt.tmp(3 * C)
-                call("seg_bn_backward_parts", part.data_ptr(), nparts, rt.gptr(dA), dA.ld, rt.ptr(y), y.ld, M, C,
-                     self.bn.weight.data_ptr(), mean, invstd, scale,
-                     shift, self.act, g_w, g_b, coef.data_ptr(), rt.ptr(dY), dY.ld, s)
-            else:
-                work = rt.tmp(query("seg_chan_workspace_floats", M, C) + 3 * C)
-                call(rt.k("seg_bn_backward"), rt.gptr(dA), dA.ld, rt.ptr(y), y.ld, M, C, self.bn.weight.data_ptr(),
-                     mean, invstd, scale, shift, self.act,
-                     g_w, g_b, work.data_ptr(), rt.ptr(dY), dY.ld, s)
+            work = rt.tmp(query("seg_chan_workspace_floats", M, C) + 3 * C)
+            call(rt.k("seg_bn_backward"), rt.gptr(dA), dA.ld, rt.ptr(y), y.ld, M, C, self.bn.weight.data_ptr(),
+                 mean, invstd, scale, shift, self.act,
+                 g_w, g_b, work.data_ptr(), rt.ptr(dY), dY.ld, s)
             if self.res is not None:
                 rt.add_pending(self.res, dA)
         else:
@@ -459,17 +354,6 @@ class ConvOp:
                 _timed_call("wino3_dgrad", self.flops(), "seg_conv_wino", dYp, dY.ld, y.N, y.H, y.W, kin,
                             self.wk_wd.data_ptr(), kin, None, rt.gptr(i), i.ld, self.cin, add_ptr, add_ld, None,
                             work.data_ptr(), s)
-            elif self.red_for is not None and rt.training:
-                b = self.red_for
-                st, C = rt.saved[id(b)], b.cout
-                ntiles, _ = rt.row_tiles(i.M, self.cin)
-                part = rt.tmp(ntiles * 2 * C)
-                _timed_call(f"igemm{self.ks}_dgrad", self.flops(),
-                            "seg_conv_igemm_red_bf16" if self.bf else "seg_conv_igemm_red", dYp, dY.ld, y.N, y.H,
-                            y.W, kin, self.wk_d.data_ptr(), self.ldk_d, rt.gptr(i), i.ld, self.cin, self.ks, self.pad,
-                            add_ptr, add_ld, rt.ptr(b.y), b.y.ld, st[2 * C:3 * C].data_ptr(),
-                            st[3 * C:4 * C].data_ptr(), st[:C].data_ptr(), b.act, part.data_ptr(), s)
-                rt.bnred[id(b)] = (part, ntiles)
             elif rt.io:
                 _timed_call(f"igemm{self.ks}_dgrad", self.flops(), "seg_conv_igemm_bf16io", dYp, dY.ld, y.N, y.H, y.W,
                             kin, self.wk_d.data_ptr(), self.ldk_d, None, rt.gptr(i), i.ld, i.H, i.W, self.cin,
@@ -605,7 +489,6 @@ class Program:
             op.bf = self.math in ("bf16", "bf16io")
             if op.bf:
                 # bf16 math: every dense / pointwise conv (fwd, dgrad, wgrad) on the bf16 implicit GEMM
-                op.pw_fused = op.bnb = False
                 op.wino_f = op.wino_d = op.wino_w = op.halo_f = op.halo_d = False
                 if self.math == "bf16io" and op.ks == 3 and op.stride == 1 and op.pad == 1:
                     # LDS-halo direct conv on bf16 (seg_conv_halo_bf16io): narrow convs, 8-channel slots
@@ -625,9 +508,6 @@ class Program:
                     jobs.append((w.data_ptr(), op.wk_d.data_ptr(), op.cout, op.cin, op.ks, op.ldk_d, 1, kin))
                     max_elems = max(max_elems, op.cin * op.ldk_d)
                 continue
-            op.pw_fused = (PW_FUSED and op.ks == 1 and op.bn is not None and op.conv.bias is None and not op.first
-                           and op.cin % 4 == 0 and op.conv.weight.requires_grad
-                           and bool(query("seg_pw_bwd_fused_ok", op.cin, op.cout)))
             wino_ok = op.ks == 3 and op.stride == 1 and op.pad == 1
             op.wino_f = wino_ok and bool(query("seg_conv_wino_pick", y.N, y.H, y.W, op.cin_pad, op.cout))
             op.wino_d = wino_ok and not op.first and bool(query("seg_conv_wino_pick", y.N, y.H, y.W, r4(op.cout),
@@ -646,12 +526,6 @@ class Program:
                 op.wk_f = torch.empty(op.cout * op.ldk_f, device=dev, dtype=torch.float32)
                 jobs.append((w.data_ptr(), op.wk_f.data_ptr(), op.cout, op.cin, op.ks, op.ldk_f, 0, op.cin_pad))
                 max_elems = max(max_elems, op.cout * op.ldk_f)
-            # (1x1 only: a 3x3 data gradient would re-form each dY element 9 times from two
-            # tensors, measured slower than materialising dY once)
-            op.bnb = (BNB_ON_LOAD and op.ks == 1 and op.bn is not None and not op.pw_fused and op.cout % 4 == 0
-                      and not op.wino_d and not op.wino_w and op.conv.weight.requires_grad
-                      and (op.first or (op.stride == 1 and bool(query("seg_conv_igemm_bnb_ok", r4(op.cout),
-                                                                        op.ks)))))
             if op.wino_d:
                 kin = r4(op.cout)
                 op.wk_wd = torch.empty(16 * op.cin * kin, device=dev, dtype=torch.float32)
@@ -663,48 +537,9 @@ class Program:
                 op.wk_d = torch.empty(op.cin * op.ldk_d, device=dev, dtype=torch.float32)
                 jobs.append((w.data_ptr(), op.wk_d.data_ptr(), op.cout, op.cin, op.ks, op.ldk_d, 1, kin))
                 max_elems = max(max_elems, op.cin * op.ldk_d)
-        self._plan_bn_red()
         table = np.array(jobs, dtype=jt)
         self._jobs = torch.from_numpy(table.view(np.uint8).copy()).to(convs[0].conv.weight.device)
         self._njobs, self._max_elems, self._pack_key = len(jobs), max_elems, key
-
-    def _plan_bn_red(self):
-        """Fuse each train-mode BatchNorm's backward reduction into the data gradient that
-        completes its dA, where that is possible.  The gradient of a layer output is
-        written by its consumers in reverse forward order (first writer overwrites, later
-        ones add), so the EARLIEST consumer in forward order finishes it; when that consumer
-        is a stride-1 implicit-GEMM data gradient whose output is exactly the layer's
-        output region, its epilogue computes sum(dz), sum(dz*(y-mean)) per channel
-        (seg_conv_igemm_red) and the BN backward skips its own reduction pass."""
-        def reads(op):
-            if isinstance(op, ConvOp):
-                return [op.inp] + ([op.res] if op.res is not None else [])
-            if isinstance(op, UpsampleOp):
-                return [op.low]
-            if isinstance(op, PoolOp):
-                return [op.inp]
-            return []
-
-        def overlaps(a, b):
-            return a.buf == b.buf and a.off < b.off + b.C and b.off < a.off + a.C
-
-        for op in self.ops:
-            if isinstance(op, ConvOp):
-                op.red_for = op.red_by = None
-        if not BN_RED or self.math == "bf16io":
-            return
-        for k, b in enumerate(self.ops):
-            if not isinstance(b, ConvOp) or b.bn is None or b.bnb or b.pw_fused or b.cout % 4:
-                continue
-            for e in self.ops[k + 1:]:
-                hit = [a for a in reads(e) if overlaps(a, b.out)]
-                if not hit:
-                    continue
-                if (isinstance(e, ConvOp) and e.kind == "igemm" and not e.first and e.stride == 1
-                        and hit == [e.inp] and e.inp.key() == b.out.key() and not (e.wino_d or e.halo_d
-                                                                                    or e.pw_fused or e.bnb)):
-                    b.red_by, e.red_for = e, b
-                break
 
     def fold(self, stream):
         """Eval: fold every BatchNorm into its conv (one seg_bn_fold_batch launch) and
@@ -951,7 +786,6 @@ class Run:
         self.sync = None
         self._tmp_n = 0
         self.side = None      # side stream of the parameter gradients (backward only)
-        self.bnred = {}       # id(BN op) -> (tile partials, ntiles) from a fused data gradient
         self._n_fork = 0      # side-stream forks so far (index into the program's event pool)
 
     def k(self, name: str) -> str:
@@ -1120,11 +954,6 @@ class Run:
 OVERLAP = os.environ.get("SEG_OVERLAP", "1") == "1"
 # LDS-halo direct 3x3 conv for the narrow convs in the bf16io configuration; SEG_HALO_BF16=0 turns it off.
 HALO_BF16 = os.environ.get("SEG_HALO_BF16", "1") == "1"
-# Fused BatchNorm-backward reductions (Program._plan_bn_red): parity-tested, but measured
-# no faster on MI355X in round 1 (f32 1707 vs 1711 img/s, bf16 2337 vs 2374: the y loads
-# in the data-gradient epilogue sit on the critical main stream, while the separate
-# reduction pass is cheap there); off unless SEG_BN_RED=1.
-BN_RED = os.environ.get("SEG_BN_RED", "0") == "1"
 _SIDE = {}
 
 
@@ -1137,6 +966,29 @@ def _side_stream(device):
 
 DEBUG_KEEP_RUN = False  # diagnostics: keep the last Run (buffers + gradient buffers)
 LAST_RUN = None
+
+
+def debug_preactivations(model) -> dict:
+    """Diagnostics (needs DEBUG_KEEP_RUN = True before the forward): every activation
+    layer's post-BatchNorm pre-activation z = y * scale + shift of the last run, as fp64
+    NCHW CPU tensors keyed by the conv's module path + "." (the parity tests compare them
+    with the oracle and take the ReLU/ReLU6 masks from them)."""
+    run = LAST_RUN
+    if run is None:
+        raise RuntimeError("set engine.DEBUG_KEEP_RUN = True before the forward")
+    model = getattr(model, "module", model)
+    names = {}
+    for n, m in model.named_modules():
+        names.setdefault(id(m), n)
+    out = {}
+    for op in run.prog.ops:
+        if isinstance(op, ConvOp) and op.bn is not None and op.act != ACT_NONE:
+            y, C = op.y, op.cout
+            t = run.bufs[y.buf].view(-1, y.ld)[:, y.off:y.off + C].double()
+            st = run.saved[id(op)].double()
+            z = t * st[2 * C:3 * C] + st[3 * C:4 * C]
+            out[names[id(op.conv)] + "."] = z.view(y.N, y.H, y.W, C).permute(0, 3, 1, 2).cpu()
+    return out
 
 
 _PROGRAM_CACHE_ATTR = "_segamd_programs"
@@ -1167,7 +1019,7 @@ def _loss_forward(run, t, ignore_index):
     prog, lo, s = run.prog, run.prog.logits, run.stream
     N = prog.N
     Ho, Wo = prog.out_hw
-    stats = torch.empty(2, device=run.device, dtype=torch.float32)
+    stats = torch.empty(3, device=run.device, dtype=torch.float32)  # loss, #valid, #out-of-range labels
     work = run.tmp(query("seg_ce_workspace_floats", N * Ho * Wo))
     call(run.k("seg_ce_upsample_loss"), run.ptr(lo), lo.ld, N, lo.H, lo.W, lo.C, t.data_ptr(), Ho, Wo,
          ignore_index, work.data_ptr(), stats.data_ptr(), s)
@@ -1191,120 +1043,6 @@ def _loss_backward(run, g, ignore_index):
         run.sync.finish_gradient_sync()  # stream-ordered wait on the last all-reduces
 
 
-@contextlib.contextmanager
-def _no_gc():
-    """No Python garbage collection while a graph is being captured: a collected object
-    that owns a HIP resource (an event, a tensor of an unrelated pool) would call into
-    the runtime mid-capture and abort the process."""
-    import gc
-    gc.collect()
-    was = gc.isenabled()
-    gc.disable()
-    try:
-        yield
-    finally:
-        if was:
-            gc.enable()
-
-
-class _StepGraph:
-    """A training step of one program captured as two HIP graphs (torch.cuda.CUDAGraph
-    drives hipGraph on ROCm): the forward with the fused loss, and the backward down to
-    every parameter gradient.  Replaying them replaces ~600 kernel launches from Python
-    (~11 ms of host time per step, more than the bf16io step's GPU time) with two graph
-    launches.  Buffers, saved statistics and gradients live in the graphs' private pool
-    and are reused by every replay; parameter gradients are views of one flat buffer.
-    Requires static shapes, parameters updated in place (any torch optimizer) and no
-    DataParallel gradient sync (that path stays eager).
-
-    Bitwise equal to the eager step (tests/test_gpu_graph.py), but measured SLOWER on
-    MI355X / ROCm 7.2 in round 1 (bf16io 2772 vs 2970 img/s, f32 1633 vs 1708): the
-    replay runs every node on one hardware queue, so the weight-gradient side stream no
-    longer overlaps the data-gradient chain (with SEG_OVERLAP=0 both give 2756-2759).
-    Off unless set_step_graphs(model) / bench.py --graphs."""
-
-    def __init__(self, prog, x, target, ignore_index, params):
-        self.prog, self.ignore_index = prog, ignore_index
-        self.x, self.t = torch.empty_like(x), torch.empty_like(target)
-        self.gout = torch.empty(1, device=x.device, dtype=torch.float32)
-        self.pool = torch.cuda.graph_pool_handle()
-        self.g_fwd = self.g_bwd = None
-        self.run = self.stats = None
-        self.busy = False            # a replayed forward waits for its backward
-        self.slot, off = {}, 0
-        for p in params:
-            if p.requires_grad and id(p) not in self.slot:
-                self.slot[id(p)] = (off, p.numel(), p.shape)
-                off += p.numel()
-        self.flat = torch.empty(max(off, 1), device=x.device, dtype=torch.float32)
-
-    # the Run's gradient-sync interface: gradients land in the flat buffer
-    def grad_storage(self, p, flat=None):
-        slot = self.slot.get(id(p))
-        if slot is None:
-            return None
-        o, n, shape = slot
-        return (self.flat if flat is None else flat)[o:o + n].view(shape)
-
-    def on_ready(self, params, run=None):
-        pass
-
-    def finish_gradient_sync(self):
-        pass
-
-    def forward(self, x, target, training):
-        self.x.copy_(x)
-        self.t.copy_(target)
-        if self.g_fwd is None:
-            g = torch.cuda.CUDAGraph()
-            with _no_gc(), torch.cuda.graph(g, pool=self.pool):
-                run = Run(self.prog, self.x, training)
-                run.sync = self
-                run.forward()
-                self.stats = _loss_forward(run, self.t, self.ignore_index)
-            self.g_fwd, self.run = g, run
-        self.g_fwd.replay()
-        self.busy = True
-        return self.stats[0].clone()
-
-    def backward(self, gout):
-        self.gout.copy_(gout.reshape(1))
-        if self.g_bwd is None:
-            g = torch.cuda.CUDAGraph()
-            with _no_gc(), torch.cuda.graph(g, pool=self.pool):
-                _loss_backward(self.run, self.gout, self.ignore_index)
-            self.g_bwd = g
-        self.g_bwd.replay()
-        self.busy = False
-
-
-GRAPH_WARMUP = 2  # eager steps of a program before its step is captured
-
-
-def set_step_graphs(model, on: bool = True):
-    """Capture the training step (forward + fused loss, backward) of `model` in HIP graphs
-    after GRAPH_WARMUP eager steps per input shape (see _StepGraph)."""
-    model = getattr(model, "module", model)
-    model.__dict__["_segamd_graphs"] = bool(on)
-    return model
-
-
-def _step_graph(model, prog, x, target, ignore_index, params):
-    if not model.__dict__.get("_segamd_graphs"):
-        return None
-    cache = model.__dict__.setdefault("_segamd_step_graphs", {})
-    key = (id(prog), ignore_index)
-    ent = cache.get(key)
-    if ent is None:
-        ent = cache[key] = [0, None]
-    if ent[0] < GRAPH_WARMUP:
-        ent[0] += 1
-        return None
-    if ent[1] is None:
-        ent[1] = _StepGraph(prog, x, target, ignore_index, params)
-    return None if ent[1].busy else ent[1]
-
-
 class _SegFunction(torch.autograd.Function):
     """Whole-network forward/backward as one autograd node."""
 
@@ -1319,14 +1057,7 @@ class _SegFunction(torch.autograd.Function):
             t = target.contiguous()
             if t.dtype != torch.int64 or tuple(t.shape) != (N, Ho, Wo):
                 raise ValueError(f"target must be int64 [{N},{Ho},{Wo}], got {tuple(t.shape)} {t.dtype}")
-            wants_grad = any(ctx.needs_input_grad[6:])
-            sg = (_step_graph(model, prog, x, t, ignore_index, params)
-                  if wants_grad and model.training and sync is None else None)
-            if sg is not None:
-                out = sg.forward(x, t, model.training)
-                ctx.sg, ctx.run, ctx.params = sg, None, params
-                return out
-        ctx.sg = None
+
         run = Run(prog, x, model.training)
         run.sync = sync
         run.forward()
@@ -1336,7 +1067,9 @@ class _SegFunction(torch.autograd.Function):
             call(run.k("seg_upsample_to_nchw"), run.ptr(lo), lo.ld, N, lo.H, lo.W, lo.C, out.data_ptr(), Ho, Wo, 1,
                  run.stream)
         else:
-            out = _loss_forward(run, t, ignore_index)[0]
+            stats = _loss_forward(run, t, ignore_index)
+            model.__dict__["_segamd_last_stats"] = stats
+            out = stats[0]
         if any(ctx.needs_input_grad[6:]):
             ctx.run, ctx.mode, ctx.ignore_index = run, mode, ignore_index
             ctx.params = params
@@ -1346,16 +1079,6 @@ class _SegFunction(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, gout):
-        if ctx.sg is not None:
-            sg = ctx.sg
-            sg.backward(gout.to(torch.float32))
-            # hand autograd views of a fresh copy of the flat gradients (one copy kernel):
-            # a .grad must never alias the buffer the next replay writes
-            flat = sg.flat.clone()
-            grads = [sg.grad_storage(p, flat) if ctx.needs_input_grad[6 + k] else None
-                     for k, p in enumerate(ctx.params)]
-            ctx.sg = ctx.params = None
-            return (None, None, None, None, None, None, *grads)
         run = ctx.run
         if run is None:
             raise RuntimeError("segamd: backward called on a forward that saved nothing")
@@ -1372,12 +1095,30 @@ class _SegFunction(torch.autograd.Function):
                 run.sync.finish_gradient_sync()
         else:
             _loss_backward(run, gout.reshape(1).to(torch.float32).contiguous(), ctx.ignore_index)
-        grads = [run.grads.get(id(p)) if ctx.needs_input_grad[6 + k] else None for k, p in enumerate(ctx.params)]
+        if run.sync is not None:  # DataParallel: copies of the averaged buckets, never the buckets
+            grads = run.sync.autograd_grads(ctx.params)
+            grads = [g if ctx.needs_input_grad[6 + k] else None for k, g in enumerate(grads)]
+        else:
+            grads = [run.grads.get(id(p)) if ctx.needs_input_grad[6 + k] else None for k, p in enumerate(ctx.params)]
         # drop every other reference so AccumulateGrad can adopt the tensors instead of copying them
         run.grads.clear()
         ctx.run = ctx.params = None
         del run
         return (None, None, None, None, None, None, *grads)
+
+
+def check_targets(model):
+    """Raise like nn.CrossEntropyLoss ("Target out of bounds") if the last fused loss of
+    `model` saw a label outside [0, C) other than ignore_index.  The kernels flag it
+    stream-ordered (the loss and every gradient become NaN); this reads the flag (one
+    host sync), so callers check when the loss is NaN."""
+    model = getattr(model, "module", model)
+    st = model.__dict__.get("_segamd_last_stats")
+    if st is not None:
+        bad = int(st[2].item())
+        if bad:
+            raise IndexError(f"Target out of bounds: {bad} label(s) outside [0, num_classes) that are not "
+                             "ignore_index (nn.CrossEntropyLoss raises on these)")
 
 
 def _params_for(model, x):

@@ -76,6 +76,9 @@ def train_one_epoch(model, train_loader, criterion, optimizer, device, epoch: in
             sync()
         optimizer.step()
         lv = loss.item()
+        if lv != lv:  # NaN: a label outside [0, C) raises, as nn.CrossEntropyLoss does
+            from .engine import check_targets
+            check_targets(model)
         train_loss += lv
         nb += 1
         if bar is not None:

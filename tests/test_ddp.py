@@ -70,6 +70,32 @@ def _worker(rank, world, port, results):
             g = dp.grad_storage(p)
             expect = torch.full_like(p, 1.5) * (1 + torch.arange(p.numel()).view_as(p) % 7)  # mean of 1 and 2
             ok &= torch.allclose(g, expect)
+        # 4. autograd receives copies: no .grad may alias a bucket (gradient accumulation
+        #    would otherwise add the next backward's bucket contents to themselves)
+        ag = dp.autograd_grads(planned)
+        for p, g in zip(planned, ag):
+            ok &= torch.equal(g, dp.grad_storage(p))
+            ok &= g.untyped_storage().data_ptr() != dp.grad_storage(p).untyped_storage().data_ptr()
+        # 5. BN running statistics are views of one flat buffer: one broadcast per step
+        flat = dp._bn_flat
+        ok &= flat is not None
+        for n, b in model.named_buffers():
+            if b.is_floating_point():
+                ok &= b.untyped_storage().data_ptr() == flat.untyped_storage().data_ptr()
+        bn = model.up1.conv.conv[1]
+        bn.running_mean.fill_(float(rank + 3))
+        dp._broadcast_bn_buffers()
+        ok &= torch.equal(bn.running_mean, torch.full_like(bn.running_mean, 3.0))  # rank 0's value
+        # state_dict / load_state_dict keep working through the views
+        sd = {k: v.clone() for k, v in model.state_dict().items()}
+        sd["up1.conv.conv.1.running_var"].fill_(2.0)
+        model.load_state_dict(sd)
+        ok &= bool((model.up1.conv.conv[1].running_var == 2.0).all())
+        ok &= model.up1.conv.conv[1].running_var.untyped_storage().data_ptr() == flat.untyped_storage().data_ptr()
+        # 6. no_sync(): the engine sees no gradient-sync object inside the context
+        with dp.no_sync():
+            ok &= model.__dict__.get("_segamd_sync") is None
+        ok &= model.__dict__.get("_segamd_sync") is dp
         results[rank] = bool(ok)
     finally:
         dist.destroy_process_group()

@@ -131,15 +131,11 @@ def test_row_tiled_passes(M, C, ld, off):
         inpl = y32.clone()
         call("seg_bn_apply", p(inpl), ld, M, C, scale.data_ptr(), shift.data_ptr(), act, p(r32), ld, p(inpl), ld, s)
         assert torch.equal(inpl[:, sl], o32[:, sl])
-        # BN backward apply with the reduction given (seg_bn_backward_parts): zero partials, gamma
-        # None and invstd = scale give coef = (scale, 0, 0), so dY = scale * dA * act'(z)
+        # eval-mode BN backward (seg_bn_eval_backward): dY = scale * dA * act'(z)
         mask = torch.ones_like(z) if act == 0 else ((z > 0) if act == 1 else ((z > 0) & (z < 6))).float()
-        part = torch.zeros(2 * C, device=DEV)
-        gw, gb, cw = torch.empty(C, device=DEV), torch.empty(C, device=DEV), torch.empty(3 * C, device=DEV)
         dy = fresh(torch.float32)
-        call("seg_bn_backward_parts", part.data_ptr(), 1, p(d32), ld, p(y32), ld, M, C, None, mean.data_ptr(),
-             scale.data_ptr(), scale.data_ptr(), shift.data_ptr(), act, gw.data_ptr(), gb.data_ptr(), cw.data_ptr(),
-             p(dy), ld, s)
+        call("seg_bn_eval_backward", p(d32), ld, p(y32), ld, M, C, scale.data_ptr(), shift.data_ptr(), act, p(dy), ld,
+             s)
         torch.testing.assert_close(dy[:, sl], scale * dv * mask, rtol=1e-6, atol=1e-6)
     # full BN backward (reduction + finalize + apply), fp32 vs bf16io twin, and vs its own coefficients
     gamma = torch.linspace(0.5, 1.5, C, device=DEV)
@@ -265,7 +261,7 @@ def test_cross_entropy():
     t = torch.randint(0, C, (N, Ho, Wo), generator=torch.Generator().manual_seed(13)).to(DEV)
     t[0, :3] = -100
     work = torch.empty(query("seg_ce_workspace_floats", N * Ho * Wo), device=DEV)
-    st32, st16 = torch.empty(2, device=DEV), torch.empty(2, device=DEV)
+    st32, st16 = torch.empty(3, device=DEV), torch.empty(3, device=DEV)
     call("seg_ce_upsample_loss", lo32.data_ptr(), 12, N, H, W, C, t.data_ptr(), Ho, Wo, -100, work.data_ptr(),
          st32.data_ptr(), s)
     call("seg_ce_upsample_loss_bf16io", lo16.data_ptr(), 12, N, H, W, C, t.data_ptr(), Ho, Wo, -100, work.data_ptr(),

@@ -59,3 +59,25 @@ def test_ddp_world1_matches_plain(pg, math, optim):
         assert torch.equal(g0[k], g1[k]), k
     for k in s0:
         assert torch.equal(s0[k], s1[k]), k
+
+
+@pytest.mark.parametrize("set_to_none", [True, False])
+def test_ddp_world1_grad_accumulation(pg, set_to_none):
+    """Two micro-batches accumulated into .grad (and zero_grad(set_to_none=False)) must
+    give g1 + g2 exactly as the plain model does: autograd never receives the bucket
+    itself, so the second backward cannot overwrite an aliased .grad."""
+    xs = [synthetic_batch(2, 64, 128, 10, seed=s) for s in (5, 6)]
+    res = []
+    for wrap in (False, True):
+        m = deterministic_init(MobileNetV2UNet(10), seed=4).to(DEV).train()
+        model = DataParallel(m, bucket_cap_mb=1.0) if wrap else m
+        for step in range(2):
+            model.zero_grad(set_to_none=set_to_none)
+            for x, y in xs:
+                model.forward_loss(x.to(DEV), y.to(DEV)).backward()
+        torch.cuda.synchronize()
+        res.append({k: p.grad.clone() for k, p in m.named_parameters() if p.grad is not None})
+    g0, g1 = res
+    assert g0.keys() == g1.keys() and len(g0) == 194
+    for k in g0:
+        assert torch.equal(g0[k], g1[k]), k

@@ -312,11 +312,12 @@ def test_ce_fused_upsample(N, C, H, W, ignore):
     s = S()
     lg = nhwc(low)
     yg = y.to(DEV)
-    stats = torch.empty(2, device=DEV)
+    stats = torch.empty(3, device=DEV)
     work = torch.empty(query("seg_ce_workspace_floats", N * Ho * Wo), device=DEV)
     call("seg_ce_upsample_loss", lg.data_ptr(), lg.shape[1], N, H, W, C, yg.data_ptr(), Ho, Wo, -100,
          work.data_ptr(), stats.data_ptr(), s)
     assert abs(stats[0].item() - loss.item()) <= 1e-5 * abs(loss.item()) + 1e-7
+    assert stats[2].item() == 0
     gout = torch.tensor([0.7], device=DEV)
     ld = r4(C)
     dhigh = torch.empty(N * Ho * Wo * ld, device=DEV)
@@ -326,6 +327,45 @@ def test_ce_fused_upsample(N, C, H, W, ignore):
     call("seg_upsample_bwd", dhigh.data_ptr(), ld, 0, N, Ho, Wo, C, dlow.data_ptr(), ld, H, W, 1, 0, s)
     assert rel(from_nhwc(dlow, N, C, H, W), lr.grad) < 1e-5
     assert torch.all(dlow[:, C:] == 0)
+
+
+@pytest.mark.parametrize("bad", [10, 255, -1])
+def test_ce_target_out_of_bounds(bad):
+    """A label outside [0, C) that is not ignore_index: nn.CrossEntropyLoss raises
+    'Target out of bounds'; the fused kernels flag it (stats[2]), poison the loss and
+    the gradient with NaN, and train_model / engine.check_targets raise."""
+    N, C, H, W = 1, 10, 4, 6
+    Ho, Wo = 2 * H, 2 * W
+    low = gen(N, C, H, W, seed=1)
+    y = torch.randint(0, C, (N, Ho, Wo), generator=torch.Generator().manual_seed(3))
+    y[0, 1, 2] = bad
+    with pytest.raises((IndexError, RuntimeError)):
+        F.cross_entropy(F.interpolate(low, scale_factor=2, mode="bilinear", align_corners=True), y)
+    s = S()
+    lg, yg = nhwc(low), y.to(DEV)
+    stats = torch.empty(3, device=DEV)
+    work = torch.empty(query("seg_ce_workspace_floats", N * Ho * Wo), device=DEV)
+    call("seg_ce_upsample_loss", lg.data_ptr(), lg.shape[1], N, H, W, C, yg.data_ptr(), Ho, Wo, -100,
+         work.data_ptr(), stats.data_ptr(), s)
+    assert stats[2].item() == 1 and torch.isnan(stats[0])
+    dhigh = torch.empty(N * Ho * Wo * 12, device=DEV)
+    call("seg_ce_upsample_grad", lg.data_ptr(), lg.shape[1], N, H, W, C, yg.data_ptr(), Ho, Wo, -100,
+         torch.ones(1, device=DEV).data_ptr(), stats.data_ptr(), dhigh.data_ptr(), 12, s)
+    assert torch.isnan(dhigh.view(-1, 12)[:, :C]).any()
+    # through the model: the fused loss is NaN and check_targets raises like aten
+    from seg_amd import MobileNetV2UNet, deterministic_init
+    from seg_amd.engine import check_targets
+    model = deterministic_init(MobileNetV2UNet(10), seed=1).to(DEV).train()
+    x = torch.randn(1, 3, 64, 64, generator=torch.Generator().manual_seed(0)).to(DEV)
+    t = torch.zeros(1, 64, 64, dtype=torch.int64, device=DEV)
+    t[0, 5, 5] = bad
+    loss = model.forward_loss(x, t)
+    assert torch.isnan(loss)
+    with pytest.raises(IndexError, match="Target out of bounds"):
+        check_targets(model)
+    t[0, 5, 5] = -100  # ignore_index is fine
+    assert torch.isfinite(model.forward_loss(x, t))
+    check_targets(model)
 
 
 def test_colsum_and_add():
@@ -494,133 +534,6 @@ def test_conv_wino_wgrad(N, Cin, Cout, H, W):
         assert rel(dw2, 2 * wr.grad) < 1e-5
 
 
-@pytest.mark.parametrize("M,Cin,Cout,act,res", [(5000, 16, 96, 2, False), (3333, 96, 24, 0, True),
-                                                (4096, 24, 144, 2, False), (2111, 144, 32, 0, True),
-                                                (777, 32, 192, 2, False), (1024, 192, 32, 0, False)])
-def test_pw_bwd_fused(M, Cin, Cout, act, res):
-    """seg_bn_backward_coef + seg_pw_bwd_fused (+ wgrad reduce) == torch autograd of
-    act(BN_train(conv1x1(x))) for dx (with addend) and dW."""
-    assert query("seg_pw_bwd_fused_ok", Cin, Cout) == 1
-    x = gen(M, Cin, seed=51)
-    w = gen(Cout, Cin, 1, 1, seed=52) * (2.0 / Cin) ** 0.5
-    g, bta = gen(Cout, seed=53).abs() + 0.5, gen(Cout, seed=54)
-    xr = x.clone().requires_grad_(True)
-    wr = w.clone().requires_grad_(True)
-    yraw = (xr @ wr.view(Cout, Cin).t())
-    z = F.batch_norm(yraw.t().unsqueeze(0), None, None, g, bta, True, 0.1, 1e-5).squeeze(0).t()
-    a_out = F.hardtanh(z, 0.0, 6.0) if act == 2 else z
-    dA = gen(M, Cout, seed=55)
-    a_out.backward(dA)
-    s = S()
-    xg = x.to(DEV).contiguous()
-    yg = yraw.detach().to(DEV).contiguous()
-    dAg = dA.to(DEV)
-    # forward statistics as the engine keeps them: mean, invstd, scale, shift
-    y64 = yraw.detach().double()
-    mean = y64.mean(0).float()
-    invstd = (1 / torch.sqrt(y64.var(0, unbiased=False) + 1e-5)).float()
-    scale = g * invstd
-    shift = bta - mean * g * invstd
-    mg, ig, scg, shg, gg = (t.to(DEV) for t in (mean, invstd, scale, shift, g))
-    work = torch.empty(query("seg_chan_workspace_floats", M, Cout), device=DEV)
-    coef = torch.empty(3 * Cout, device=DEV)
-    dgam, dbet = torch.empty(Cout, device=DEV), torch.empty(Cout, device=DEV)
-    call("seg_bn_backward_coef", dAg.data_ptr(), Cout, yg.data_ptr(), Cout, M, Cout, gg.data_ptr(), mg.data_ptr(),
-         ig.data_ptr(), scg.data_ptr(), shg.data_ptr(), act, dgam.data_ptr(), dbet.data_ptr(), work.data_ptr(),
-         coef.data_ptr(), s)
-    kin = r4(Cout)
-    wkd = torch.empty(Cin * kin, device=DEV)
-    call("seg_pack_conv_weight", wr.detach().to(DEV).data_ptr(), wkd.data_ptr(), Cout, Cin, 1, kin, 1, kin, s)
-    blocks = query("seg_pw_bwd_blocks", M)
-    part = torch.empty(blocks * Cout * r4(Cin), device=DEV)
-    addend = gen(M, Cin, seed=56) if res else None
-    addg = addend.to(DEV) if res else None
-    dx = torch.full((M, Cin), float("nan"), device=DEV)
-    call("seg_pw_bwd_fused", dAg.data_ptr(), Cout, yg.data_ptr(), Cout, xg.data_ptr(), Cin, wkd.data_ptr(), kin,
-         scg.data_ptr(), shg.data_ptr(), mg.data_ptr(), coef.data_ptr(), act, addg.data_ptr() if res else None,
-         Cin if res else 0, dx.data_ptr(), Cin, part.data_ptr(), blocks, M, Cin, Cout, s)
-    dw = torch.empty(Cout, Cin, 1, 1, device=DEV)
-    call("seg_conv_wgrad_reduce", part.data_ptr(), blocks, dw.data_ptr(), Cout, Cin, 1, 0, 0, s)
-    # the unfused HIP path on the same inputs: seg_bn_backward -> igemm data gradient + split-K wgrad
-    dY = torch.empty(M, r4(Cout), device=DEV)
-    work2 = torch.empty(query("seg_chan_workspace_floats", M, Cout) + 3 * Cout, device=DEV)
-    d2g, d2b = torch.empty(Cout, device=DEV), torch.empty(Cout, device=DEV)
-    call("seg_bn_backward", dAg.data_ptr(), Cout, yg.data_ptr(), Cout, M, Cout, gg.data_ptr(), mg.data_ptr(),
-         ig.data_ptr(), scg.data_ptr(), shg.data_ptr(), act, d2g.data_ptr(), d2b.data_ptr(), work2.data_ptr(),
-         dY.data_ptr(), dY.shape[1], s)
-    dx2 = torch.empty(M, Cin, device=DEV)
-    call("seg_conv_igemm", dY.data_ptr(), dY.shape[1], 1, 1, M, kin, wkd.data_ptr(), kin, None, dx2.data_ptr(), Cin,
-         1, M, Cin, 1, 1, 0, addg.data_ptr() if res else None, Cin if res else 0, None, s)
-    assert rel(dx, dx2) < 1e-5
-    torch.testing.assert_close(dgam, d2g, rtol=0, atol=0)
-    ref_dx = xr.grad + (addend if res else 0)
-    assert rel(dx2, ref_dx) < 1e-2 and rel(dx, ref_dx) < 1e-2  # mask flips at ReLU6 thresholds dominate here
-    assert rel(dw, wr.grad) < 1e-2
-
-
-@pytest.mark.parametrize("N,H,W,Cin,Cout,ks,act", [(2, 9, 13, 80, 32, 3, 1), (1, 16, 12, 64, 64, 3, 1),
-                                                   (2, 7, 10, 16, 96, 1, 2), (3, 6, 8, 96, 24, 1, 0),
-                                                   (1, 8, 8, 152, 64, 3, 1), (2, 5, 7, 32, 16, 1, 1)])
-def test_bn_backward_on_load(N, H, W, Cin, Cout, ks, act):
-    """seg_conv_igemm_bnb / seg_conv_wgrad_bnb / seg_colsum_bnb (dY formed on load from dA and
-    y) are bitwise equal to the materialised path: seg_bn_backward -> seg_conv_igemm /
-    seg_conv_wgrad / seg_colsum."""
-    M = N * H * W
-    pad = ks // 2
-    s = S()
-    dA = gen(M, Cout, seed=61).to(DEV)
-    y = (gen(M, Cout, seed=62) * 2).to(DEV)
-    x = gen(M, Cin, seed=63).to(DEV)
-    g = (gen(Cout, seed=64).abs() + 0.5).to(DEV)
-    mean = (gen(Cout, seed=65) * 0.1).to(DEV)
-    invstd = (gen(Cout, seed=66).abs() + 0.5).to(DEV)
-    scale, shift = g * invstd, gen(Cout, seed=67).to(DEV) - mean * g * invstd
-    w = (gen(Cout, Cin, ks, ks, seed=68) * 0.1).to(DEV)
-    # materialised reference path
-    work = torch.empty(query("seg_chan_workspace_floats", M, Cout) + 3 * Cout, device=DEV)
-    dg, db, dY = torch.empty(Cout, device=DEV), torch.empty(Cout, device=DEV), torch.empty(M, Cout, device=DEV)
-    call("seg_bn_backward", dA.data_ptr(), Cout, y.data_ptr(), Cout, M, Cout, g.data_ptr(), mean.data_ptr(),
-         invstd.data_ptr(), scale.data_ptr(), shift.data_ptr(), act, dg.data_ptr(), db.data_ptr(), work.data_ptr(),
-         dY.data_ptr(), Cout, s)
-    # on-load path: reduction only
-    work2 = torch.empty(query("seg_chan_workspace_floats", M, Cout), device=DEV)
-    k = torch.empty(3 * Cout, device=DEV)
-    dg2, db2 = torch.empty(Cout, device=DEV), torch.empty(Cout, device=DEV)
-    call("seg_bn_backward_coef", dA.data_ptr(), Cout, y.data_ptr(), Cout, M, Cout, g.data_ptr(), mean.data_ptr(),
-         invstd.data_ptr(), scale.data_ptr(), shift.data_ptr(), act, dg2.data_ptr(), db2.data_ptr(), work2.data_ptr(),
-         k.data_ptr(), s)
-    assert torch.equal(dg, dg2) and torch.equal(db, db2)
-    bn = (y.data_ptr(), Cout, scale.data_ptr(), shift.data_ptr(), mean.data_ptr(), k.data_ptr(), act)
-    # data gradient (+ addend)
-    kin = r4(Cout)
-    ldk = r4(ks * ks * kin)
-    wkd = torch.empty(Cin * ldk, device=DEV)
-    call("seg_pack_conv_weight", w.data_ptr(), wkd.data_ptr(), Cout, Cin, ks, ldk, 1, kin, s)
-    assert query("seg_conv_igemm_bnb_ok", kin, ks) == 1
-    add = gen(M, Cin, seed=69).to(DEV)
-    dx1, dx2 = torch.empty(M, Cin, device=DEV), torch.empty(M, Cin, device=DEV)
-    call("seg_conv_igemm", dY.data_ptr(), Cout, N, H, W, kin, wkd.data_ptr(), ldk, None, dx1.data_ptr(), Cin, H, W,
-         Cin, ks, 1, pad, add.data_ptr(), Cin, None, s)
-    call("seg_conv_igemm_bnb", dA.data_ptr(), Cout, N, H, W, kin, wkd.data_ptr(), ldk, dx2.data_ptr(), Cin, Cin, ks,
-         pad, add.data_ptr(), Cin, *bn, s)
-    assert torch.equal(dx1, dx2)
-    # weight gradient
-    splits = query("seg_conv_wgrad_splits", M, Cout, Cin, ks)
-    p1 = torch.empty(splits * Cout * ks * ks * Cin, device=DEV)
-    p2 = torch.empty_like(p1)
-    call("seg_conv_wgrad", dY.data_ptr(), Cout, x.data_ptr(), Cin, N, H, W, Cin, H, W, Cout, ks, 1, pad,
-         p1.data_ptr(), splits, s)
-    call("seg_conv_wgrad_bnb", dA.data_ptr(), Cout, x.data_ptr(), Cin, N, H, W, Cin, H, W, Cout, ks, 1, pad,
-         p2.data_ptr(), splits, *bn, s)
-    assert torch.equal(p1, p2)
-    # bias gradient
-    c1, c2 = torch.empty(Cout, device=DEV), torch.empty(Cout, device=DEV)
-    call("seg_colsum", dY.data_ptr(), Cout, M, Cout, work.data_ptr(), c1.data_ptr(), 0, s)
-    call("seg_colsum_bnb", dA.data_ptr(), Cout, y.data_ptr(), Cout, M, Cout, scale.data_ptr(), shift.data_ptr(),
-         mean.data_ptr(), k.data_ptr(), act, work2.data_ptr(), c2.data_ptr(), 0, s)
-    assert rel(c1, c2) < 1e-6
-
-
 @pytest.mark.parametrize("N,Cin,Cout,H,W,mode", [(2, 80, 32, 8, 64, 0), (1, 32, 32, 4, 128, 0),
                                                  (2, 152, 64, 4, 64, 0), (1, 64, 64, 12, 64, 0),
                                                  (2, 32, 80, 8, 64, 1), (1, 20, 96, 4, 128, 0)])
@@ -670,52 +583,30 @@ def test_conv_halo(N, Cin, Cout, H, W, mode):
         assert rel(from_nhwc(dx, N, Cout, H, W), xr.grad + addend) < 1e-5
 
 
-@pytest.mark.parametrize("math", ["f32", "bf16"])
-@pytest.mark.parametrize("N,H,W,Cin,Cout,ks,act,addend", [(2, 9, 13, 96, 24, 1, 2, False), (1, 16, 24, 64, 152, 3, 1, True),
-                                                         (3, 7, 5, 32, 80, 3, 0, True), (2, 8, 8, 160, 960, 1, 2, True)])
-def test_dgrad_with_fused_bn_reduction(math, N, H, W, Cin, Cout, ks, act, addend):
-    """seg_conv_igemm_red(_bf16) + seg_bn_backward_parts == seg_conv_igemm(_bf16) +
-    seg_bn_backward: dA bitwise, dY / dgamma / dbeta to fp32 summation order."""
+@pytest.mark.parametrize("mode,Cout,Cin,ks", [(0, 10, 32, 1), (0, 10, 30, 3), (1, 32, 1, 3)])
+@pytest.mark.parametrize("splits", [17, 100, 257, 1024])
+def test_wgrad_reduce_direct(mode, Cout, Cin, ks, splits):
+    """seg_conv_wgrad_reduce on small slabs with many splits: the path that spreads the
+    split dimension over up to 64 thread groups (E < 64) with a pairwise LDS tree.
+    Against an fp64 sum of the slabs, and bitwise reproducible."""
+    cp = r4(Cin) if mode == 0 else Cin
+    taps = ks * ks
+    g = torch.Generator().manual_seed(splits + Cout)
+    if mode == 0:
+        part = torch.randn(splits, Cout, taps, cp, generator=g)
+        ref = part.double().sum(0)[..., :Cin].permute(0, 2, 1).reshape(Cout, Cin, ks, ks)
+    else:
+        part = torch.randn(splits, taps, Cout, generator=g)
+        ref = part.double().sum(0).t().reshape(Cout, 1, ks, ks)
     s = S()
-    M, pad = N * H * W, ks // 2
-    C = Cin  # the BN layer whose dA the data gradient completes
-    dyc = gen(M, Cout, seed=31).to(DEV)
-    w = (gen(Cout, Cin, ks, ks, seed=32) * 0.1).to(DEV)
-    kin = r4(Cout)
-    ldk = r4(ks * ks * kin)
-    wkd = torch.empty(Cin * ldk, device=DEV)
-    call("seg_pack_conv_weight", w.data_ptr(), wkd.data_ptr(), Cout, Cin, ks, ldk, 1, kin, s)
-    y = (gen(M, C, seed=33) * 2 + 1).to(DEV)
-    gamma = (gen(C, seed=34) * 0.5 + 1).to(DEV)
-    mean = gen(C, seed=35).to(DEV) * 0.3 + 1
-    invstd = (torch.rand(C, generator=torch.Generator().manual_seed(36)) + 0.5).to(DEV)
-    scale, shift = gamma * invstd, gen(C, seed=37).to(DEV) + 1
-    add = gen(M, C, seed=38).to(DEV) if addend else None
-    add_ptr, add_ld = (add.data_ptr(), C) if addend else (None, 0)
-    bf = math == "bf16"
-    # reference path: plain data gradient, then the BN backward with its own reduction
-    da = torch.empty(M, C, device=DEV)
-    call("seg_conv_igemm_bf16" if bf else "seg_conv_igemm_act", dyc.data_ptr(), Cout, N, H, W, kin, wkd.data_ptr(),
-         ldk, None, da.data_ptr(), C, H, W, Cin, ks, 1, pad, add_ptr, add_ld, None, 0, None, 1, s)
-    dy_a = torch.empty(M, C, device=DEV)
-    g_a, b_a = torch.empty(C, device=DEV), torch.empty(C, device=DEV)
-    work = torch.empty(query("seg_chan_workspace_floats", M, C) + 3 * C, device=DEV)
-    call("seg_bn_backward", da.data_ptr(), C, y.data_ptr(), C, M, C, gamma.data_ptr(), mean.data_ptr(),
-         invstd.data_ptr(), scale.data_ptr(), shift.data_ptr(), act, g_a.data_ptr(), b_a.data_ptr(), work.data_ptr(),
-         dy_a.data_ptr(), C, s)
-    # fused path
-    ntiles = query("seg_conv_igemm_row_tiles", M, Cin, None)
-    part = torch.full((ntiles * 2 * C,), float("nan"), device=DEV)
-    da2 = torch.empty(M, C, device=DEV)
-    call("seg_conv_igemm_red_bf16" if bf else "seg_conv_igemm_red", dyc.data_ptr(), Cout, N, H, W, kin,
-         wkd.data_ptr(), ldk, da2.data_ptr(), C, Cin, ks, pad, add_ptr, add_ld, y.data_ptr(), C, scale.data_ptr(),
-         shift.data_ptr(), mean.data_ptr(), act, part.data_ptr(), s)
-    assert torch.equal(da2, da)
-    dy_b = torch.empty(M, C, device=DEV)
-    g_b, b_b = torch.empty(C, device=DEV), torch.empty(C, device=DEV)
-    coef = torch.empty(3 * C, device=DEV)
-    call("seg_bn_backward_parts", part.data_ptr(), ntiles, da2.data_ptr(), C, y.data_ptr(), C, M, C,
-         gamma.data_ptr(), mean.data_ptr(), invstd.data_ptr(), scale.data_ptr(), shift.data_ptr(), act,
-         g_b.data_ptr(), b_b.data_ptr(), coef.data_ptr(), dy_b.data_ptr(), C, s)
-    assert rel(b_b, b_a) < 1e-5 and rel(g_b, g_a) < 1e-5
-    assert rel(dy_b, dy_a) < 1e-5
+    pg = part.to(DEV)
+    outs = []
+    for acc in (0, 0, 1):
+        out = torch.zeros(Cout, Cin, ks, ks, device=DEV) if acc == 0 else outs[0].clone()
+        call("seg_conv_wgrad_reduce", pg.data_ptr(), splits, out.data_ptr(), Cout, Cin, ks, mode, acc, s)
+        torch.cuda.synchronize()
+        outs.append(out)
+    assert torch.equal(outs[0], outs[1]), "fixed-order reduction must be bitwise reproducible"
+    err = float((outs[0].double().cpu() - ref).abs().max())
+    assert err <= 1e-5 * splits ** 0.5 * float(ref.abs().max() + 1), err
+    assert torch.equal(outs[2], outs[0] + outs[0])

@@ -60,7 +60,18 @@ def main(prof_dir, pmc_dir, steps, out_prefix):
             f = family(names[d])
             if f:
                 traffic[(f, c)].append(v)
-    out = {"profiled_steps": steps, "kernel_ms_per_step": total / 1e6 / steps, "families": {}}
+    import os
+    import subprocess
+    try:
+        commit = subprocess.run(["git", "rev-parse", "--short=12", "HEAD"], capture_output=True, text=True,
+                                cwd=os.path.dirname(os.path.abspath(__file__))).stdout.strip() or None
+    except OSError:
+        commit = None
+    # stamp: the profile these counters came from and the commit of the tree that ran
+    # (bench.py reports both beside `traffic`, which it does not measure itself)
+    commit = os.environ.get("SEG_COMMIT", commit)
+    out = {"profile": os.path.basename(out_prefix), "commit": commit, "profiled_steps": steps,
+           "kernel_ms_per_step": total / 1e6 / steps, "families": {}}
     lines = [f"# rocprofv3 summary ({out_prefix})", "",
              f"Kernel time per step (all kernels): {total / 1e6 / steps:.2f} ms over {steps} profiled steps.", "",
              "| family | calls/step | ms/step | share | avg launch us | HBM bytes/launch (2*FETCH+WRITE)*1KiB |",

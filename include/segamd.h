@@ -362,6 +362,24 @@ typedef struct SegAdamTensor {
 int seg_adam_step(const SegAdamTensor* tensors, const long* chunks, int nchunks, int chunk,
                   float one_minus_beta1, float beta2, float one_minus_beta2, float eps, hipStream_t stream);
 
+/* ---- launch tape (csrc/tape.hip): a recorded sequence of the launches above,
+ *      replayed by one host call per segment -- the engine's training step
+ *      (seg_amd/tape.py) without ~600 per-launch ctypes calls.  Not a hipGraph:
+ *      the launches are issued on the caller's two streams (main + side), keeping
+ *      their overlap.  `entries`: n records {int32 kind, fn, stream, pad; int64
+ *      arg} (kind 0 launch of entry point `fn` (seg_tape_fn_index) with its
+ *      arguments at args[arg..], 1 event record, 2 stream wait, 3 2-D memset,
+ *      4 stop = host callback); args: 64-bit slots (fp32 values as bit
+ *      patterns). */
+int seg_tape_fn_index(const char* name);
+int seg_tape_fn_nargs(int fn);
+int seg_tape_create(const void* entries, int n, const void* args, long nargs, int nevents, void** out);
+int seg_tape_destroy(void* tape);
+int seg_tape_set_arg(void* tape, long i, long value);
+int seg_tape_timing(void* tape, const int* idx, int n, int max_replays);
+int seg_tape_elapsed(void* tape, float* out);
+int seg_tape_run(void* tape, int begin, hipStream_t main, hipStream_t side, int* stop);
+
 #ifdef __cplusplus
 }
 #endif

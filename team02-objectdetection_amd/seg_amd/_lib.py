@@ -76,6 +76,15 @@ PROTOTYPES = {
     "seg_resize_u8": (_I, [_V, _I, _I, _I, _L, _V, _I, _I, _I, _V, _V]),
     "seg_augment": (_I, [_V, _V, _I, _I, _I, _V, _F, _F, _F, _F, _F, _F, _V, _V, _V]),
     "seg_adam_step": (_I, [_V, _V, _I, _I, _F, _F, _F, _F, _V]),
+    # launch tape (csrc/tape.hip, seg_amd/tape.py)
+    "seg_tape_fn_index": (_I, [ctypes.c_char_p]),
+    "seg_tape_fn_nargs": (_I, [_I]),
+    "seg_tape_create": (_I, [_V, _I, _V, _L, _I, _V]),
+    "seg_tape_destroy": (_I, [_V]),
+    "seg_tape_set_arg": (_I, [_V, _L, _L]),
+    "seg_tape_timing": (_I, [_V, _V, _I, _I]),
+    "seg_tape_elapsed": (_I, [_V, _V]),
+    "seg_tape_run": (_I, [_V, _I, _V, _V, _V]),
 }
 # bf16-storage variants: same C signature shape as their fp32 namesakes (pointers stay void*)
 for _n in ("seg_add", "seg_bn_stats", "seg_bn_apply", "seg_bn_backward", "seg_colsum", "seg_dw_fwd", "seg_dw_dgrad",

@@ -62,15 +62,31 @@ class KernelTimer:
     bench.py for the roofline figure).  Each timed launch is bracketed by two
     events on the stream it runs on (torch's current stream)."""
 
-    def __init__(self, kinds=None):
-        self.records = []  # (kind, flops, start_event, end_event)
+    def __init__(self, kinds=None, max_replays=64):
+        self.records = []  # (kind, flops, start_event, end_event) of immediate launches
         # only these launch kinds are bracketed (None: all): every event pair is a marker
         # packet on the queue, ~3 % of the step when all ~130 conv launches are timed
         self.kinds = kinds
+        # launch tapes armed for this timer (Plan._arm_timer): each times its selected
+        # entries over up to max_replays replays with events inside libsegamd
+        self.tapes = []
+        self.max_replays = max_replays
+
+        self.collected = []
+
+    def collect(self, tape):
+        """Move a tape's timings into this timer (the tape is being re-armed)."""
+        if tape in self.tapes:
+            torch.cuda.synchronize()
+            self.collected += tape.elapsed()
+            self.tapes.remove(tape)
 
     def elapsed(self):
         """[(kind, flops, seconds)] -- call after synchronising."""
-        return [(k, f, a.elapsed_time(b) * 1e-3) for k, f, a, b in self.records]
+        out = [(k, f, a.elapsed_time(b) * 1e-3) for k, f, a, b in self.records] + self.collected
+        for t in self.tapes:
+            out += t.elapsed()
+        return out
 
 
 TIMER: KernelTimer | None = None
@@ -167,7 +183,7 @@ class ConvOp:
         bias = self.conv.bias.data_ptr() if self.conv.bias is not None else None
         if self.kind == "dw":
             i = self.inp
-            call(rt.k("seg_dw_fwd"), rt.ptr(i), i.ld, i.N, i.H, i.W, i.C, *self._in_xform(rt), self.wk_f.data_ptr(),
+            rt.call(rt.k("seg_dw_fwd"), rt.ptr(i), i.ld, i.N, i.H, i.W, i.C, *self._in_xform(rt), self.wk_f.data_ptr(),
                  rt.ptr(y), y.ld, y.H, y.W, self.stride, s)
         else:
             i = self.inp
@@ -186,23 +202,23 @@ class ConvOp:
                 stat = rt.tmp(ntiles * 2 * self.cout)
             statp = stat.data_ptr() if stat is not None else None
             if self.halo_f:
-                _timed_call("igemm3_fwd", self.flops(), rt.k("seg_conv_halo"), rt.ptr(i), i.ld, i.N, i.H, i.W, self.cin_pad,
+                rt.tcall("igemm3_fwd", self.flops(), rt.k("seg_conv_halo"), rt.ptr(i), i.ld, i.N, i.H, i.W, self.cin_pad,
                             wk_ptr, ldk, bias, rt.ptr(y), y.ld, self.cout, None, 0, statp, s)
             elif self.wino_f:
                 work = rt.tmp(16 * (y.M // 4) * self.cout)
-                _timed_call("wino3_fwd", self.flops(), "seg_conv_wino", rt.ptr(i), i.ld, i.N, i.H, i.W, self.cin_pad,
+                rt.tcall("wino3_fwd", self.flops(), "seg_conv_wino", rt.ptr(i), i.ld, i.N, i.H, i.W, self.cin_pad,
                             self.wk_wf.data_ptr(), self.cin_pad, bias, rt.ptr(y), y.ld, self.cout, None, 0, statp,
                             work.data_ptr(), s)
             elif rt.io:
-                _timed_call(f"igemm{self.ks}_fwd", self.flops(), "seg_conv_igemm_bf16io", rt.ptr(i), i.ld, i.N, i.H,
+                rt.tcall(f"igemm{self.ks}_fwd", self.flops(), "seg_conv_igemm_bf16io", rt.ptr(i), i.ld, i.N, i.H,
                             i.W, self.cin_pad, wk_ptr, ldk, bias, rt.ptr(y), y.ld, y.H, y.W, self.cout, self.ks,
                             self.stride, self.pad, None, 0, statp, s)
             elif self.bf:
-                _timed_call(f"igemm{self.ks}_fwd", self.flops(), "seg_conv_igemm_bf16", rt.ptr(i), i.ld, i.N, i.H,
+                rt.tcall(f"igemm{self.ks}_fwd", self.flops(), "seg_conv_igemm_bf16", rt.ptr(i), i.ld, i.N, i.H,
                             i.W, self.cin_pad, wk_ptr, ldk, bias, rt.ptr(y), y.ld, y.H, y.W, self.cout, self.ks,
                             self.stride, self.pad, None, 0, statp, ACT_NONE, None, 1, s)
             else:
-                _timed_call(f"igemm{self.ks}_fwd", self.flops(), "seg_conv_igemm", rt.ptr(i), i.ld, i.N, i.H, i.W,
+                rt.tcall(f"igemm{self.ks}_fwd", self.flops(), "seg_conv_igemm", rt.ptr(i), i.ld, i.N, i.H, i.W,
                             self.cin_pad, wk_ptr, ldk, bias, rt.ptr(y), y.ld, y.H, y.W, self.cout, self.ks,
                             self.stride, self.pad, None, 0, statp, s)
         if self.bn is None:
@@ -218,21 +234,21 @@ class ConvOp:
             nbt = bn.num_batches_tracked.data_ptr() if bn.track_running_stats else None
             if self.kind == "dw":
                 work = rt.tmp(query("seg_chan_workspace_floats", M, C))
-                call(rt.k("seg_bn_stats"), rt.ptr(y), y.ld, M, C, bn.weight.data_ptr(), bn.bias.data_ptr(), bn.eps,
+                rt.call(rt.k("seg_bn_stats"), rt.ptr(y), y.ld, M, C, bn.weight.data_ptr(), bn.bias.data_ptr(), bn.eps,
                      bn.momentum, rm, rv, nbt, work.data_ptr(), mean, invstd,
                      scale, shift, s)
             else:
-                call("seg_bn_stats_tiles", stat.data_ptr(), ntiles, tile_rows, M, C, bn.weight.data_ptr(),
+                rt.call("seg_bn_stats_tiles", stat.data_ptr(), ntiles, tile_rows, M, C, bn.weight.data_ptr(),
                      bn.bias.data_ptr(), bn.eps, bn.momentum, rm, rv, nbt, mean, invstd,
                      scale, shift, s)
         else:
-            call("seg_bn_eval_coef", bn.weight.data_ptr(), bn.bias.data_ptr(), bn.running_mean.data_ptr(),
+            rt.call("seg_bn_eval_coef", bn.weight.data_ptr(), bn.bias.data_ptr(), bn.running_mean.data_ptr(),
                  bn.running_var.data_ptr(), bn.eps, C, scale, shift, s)
         rt.saved[id(self)] = st
         if self.lazy:
             return
         o, r = self.out, self.res
-        call(rt.k("seg_bn_apply"), rt.ptr(y), y.ld, M, C, scale, shift, self.act,
+        rt.call(rt.k("seg_bn_apply"), rt.ptr(y), y.ld, M, C, scale, shift, self.act,
              rt.ptr(r) if r is not None else None, r.ld if r is not None else 0, rt.ptr(o), o.ld, s)
 
     # -- inference (BatchNorm folded into the conv: Program.fold)
@@ -243,7 +259,7 @@ class ConvOp:
         s, i, o = rt.stream, self.inp, self.out
         act = self.act if self.bn is not None else ACT_NONE
         if self.kind == "dw":
-            call("seg_dw_fwd_bias_act", rt.ptr(i), i.ld, i.N, i.H, i.W, i.C, self.fk_pack.data_ptr(),
+            rt.call("seg_dw_fwd_bias_act", rt.ptr(i), i.ld, i.N, i.H, i.W, i.C, self.fk_pack.data_ptr(),
                  self.fb.data_ptr(), act, rt.ptr(o), o.ld, o.H, o.W, self.stride, s)
             return
         if self.fk_pack is None:
@@ -255,7 +271,7 @@ class ConvOp:
         M = o.N * o.H * o.W
         splits = query("seg_conv_igemm_splits", M, self.cout, self.cin_pad, self.ks)
         work = rt.tmp(splits * M * self.cout) if splits > 1 else None
-        call(_FOLDED_CONV[rt.prog.math], rt.ptr(i), i.ld, i.N, i.H, i.W, self.cin_pad, wk, ldk, bias, rt.ptr(o), o.ld,
+        rt.call(_FOLDED_CONV[rt.prog.math], rt.ptr(i), i.ld, i.N, i.H, i.W, self.cin_pad, wk, ldk, bias, rt.ptr(o), o.ld,
              o.H, o.W, self.cout, self.ks, self.stride, self.pad, rt.ptr(r) if r is not None else None,
              r.ld if r is not None else 0, None, act, work.data_ptr() if work is not None else None, splits, s)
 
@@ -280,7 +296,7 @@ class ConvOp:
             dY = Act(rt.tmp_buf(M * r4(C)), 0, r4(C), C, y.N, y.H, y.W)
             g_w, g_b = rt.grad_param(self.bn.weight), rt.grad_param(self.bn.bias)
             work = rt.tmp(query("seg_chan_workspace_floats", M, C) + 3 * C)
-            call(rt.k("seg_bn_backward"), rt.gptr(dA), dA.ld, rt.ptr(y), y.ld, M, C, self.bn.weight.data_ptr(),
+            rt.call(rt.k("seg_bn_backward"), rt.gptr(dA), dA.ld, rt.ptr(y), y.ld, M, C, self.bn.weight.data_ptr(),
                  mean, invstd, scale, shift, self.act,
                  g_w, g_b, work.data_ptr(), rt.ptr(dY), dY.ld, s)
             if self.res is not None:
@@ -308,38 +324,38 @@ class ConvOp:
         y, M = self.y, self.y.M
         if self.conv.bias is not None and self.conv.bias.requires_grad:
             work = rt.tmp(query("seg_chan_workspace_floats", M, r4(self.cout)))
-            call(rt.k("seg_colsum"), dYp, dY.ld, M, self.cout, work.data_ptr(), rt.grad_param(self.conv.bias), 0, s)
+            rt.call(rt.k("seg_colsum"), dYp, dY.ld, M, self.cout, work.data_ptr(), rt.grad_param(self.conv.bias), 0, s)
         if self.conv.weight.requires_grad:
             gw = rt.grad_param(self.conv.weight)
             i = self.inp
             if self.kind == "dw":
                 nblk = query("seg_dw_wgrad_blocks", y.N, y.H, y.W, self.cout)
                 part = rt.tmp(nblk * 9 * self.cout)
-                call(rt.k("seg_dw_wgrad"), dYp, dY.ld, rt.ptr(i), i.ld, i.N, i.H, i.W, i.C, *self._in_xform(rt), y.H, y.W,
+                rt.call(rt.k("seg_dw_wgrad"), dYp, dY.ld, rt.ptr(i), i.ld, i.N, i.H, i.W, i.C, *self._in_xform(rt), y.H, y.W,
                      self.stride, part.data_ptr(), s)
-                call("seg_conv_wgrad_reduce", part.data_ptr(), nblk, gw, self.cout, 1, 3, 1, 0, s)
+                rt.call("seg_conv_wgrad_reduce", part.data_ptr(), nblk, gw, self.cout, 1, 3, 1, 0, s)
             elif self.wino_w:
                 splits = query("seg_conv_wino_wgrad_splits", y.N, y.H, y.W, self.cin_pad, self.cout)
                 part = rt.tmp(splits * 16 * self.cout * self.cin_pad)
-                _timed_call("wino3_wgrad", self.flops(), "seg_conv_wino_wgrad", dYp, dY.ld, rt.ptr(i), i.ld, y.N, y.H,
+                rt.tcall("wino3_wgrad", self.flops(), "seg_conv_wino_wgrad", dYp, dY.ld, rt.ptr(i), i.ld, y.N, y.H,
                             y.W, self.cin_pad, self.cout, part.data_ptr(), splits, s)
-                call("seg_conv_wino_wgrad_reduce", part.data_ptr(), splits, gw, self.cout, self.cin, self.cin_pad, 0, s)
+                rt.call("seg_conv_wino_wgrad_reduce", part.data_ptr(), splits, gw, self.cout, self.cin, self.cin_pad, 0, s)
             else:
                 splits = query("seg_conv_wgrad_splits", M, self.cout, self.cin_pad, self.ks)
                 part = rt.tmp(splits * self.cout * self.ks * self.ks * self.cin_pad)
-                _timed_call(f"igemm{self.ks}_wgrad", self.flops(),
+                rt.tcall(f"igemm{self.ks}_wgrad", self.flops(),
                             ("seg_conv_wgrad_bf16io" if rt.io else "seg_conv_wgrad_bf16") if self.bf else "seg_conv_wgrad", dYp, dY.ld, rt.ptr(i), i.ld,
                             i.N, i.H, i.W, self.cin_pad, y.H, y.W, self.cout, self.ks, self.stride, self.pad,
                             part.data_ptr(), splits, s)
-                call("seg_conv_wgrad_reduce", part.data_ptr(), splits, gw, self.cout, self.cin, self.ks, 0, 0, s)
-        rt.params_done(self.params())
+                rt.call("seg_conv_wgrad_reduce", part.data_ptr(), splits, gw, self.cout, self.cin, self.ks, 0, 0, s)
+        rt.params_done(self.params(), s)
 
     def _dgrad(self, rt, dY, dYp, s):
         """Data gradient into the input's gradient region (first writer / fused addend)."""
         y, i = self.y, self.inp
         if self.kind == "dw":
             acc = rt.begin_write_accumulate(i)
-            call(rt.k("seg_dw_dgrad"), dYp, dY.ld, y.N, y.H, y.W, self.cout, self.wk_f.data_ptr(), rt.gptr(i), i.ld, i.H,
+            rt.call(rt.k("seg_dw_dgrad"), dYp, dY.ld, y.N, y.H, y.W, self.cout, self.wk_f.data_ptr(), rt.gptr(i), i.ld, i.H,
                  i.W, self.stride, acc, s)
         else:
             if self.stride != 1:
@@ -347,23 +363,23 @@ class ConvOp:
             kin = r4(self.cout)  # dY channels padded to 4 (the C=10 head)
             add_ptr, add_ld = rt.begin_write_add(i)
             if self.halo_d:
-                _timed_call("igemm3_dgrad", self.flops(), rt.k("seg_conv_halo"), dYp, dY.ld, y.N, y.H, y.W, kin,
+                rt.tcall("igemm3_dgrad", self.flops(), rt.k("seg_conv_halo"), dYp, dY.ld, y.N, y.H, y.W, kin,
                             self.wk_d.data_ptr(), self.ldk_d, None, rt.gptr(i), i.ld, self.cin, add_ptr, add_ld, None, s)
             elif self.wino_d:
                 work = rt.tmp(16 * (y.M // 4) * self.cin)
-                _timed_call("wino3_dgrad", self.flops(), "seg_conv_wino", dYp, dY.ld, y.N, y.H, y.W, kin,
+                rt.tcall("wino3_dgrad", self.flops(), "seg_conv_wino", dYp, dY.ld, y.N, y.H, y.W, kin,
                             self.wk_wd.data_ptr(), kin, None, rt.gptr(i), i.ld, self.cin, add_ptr, add_ld, None,
                             work.data_ptr(), s)
             elif rt.io:
-                _timed_call(f"igemm{self.ks}_dgrad", self.flops(), "seg_conv_igemm_bf16io", dYp, dY.ld, y.N, y.H, y.W,
+                rt.tcall(f"igemm{self.ks}_dgrad", self.flops(), "seg_conv_igemm_bf16io", dYp, dY.ld, y.N, y.H, y.W,
                             kin, self.wk_d.data_ptr(), self.ldk_d, None, rt.gptr(i), i.ld, i.H, i.W, self.cin,
                             self.ks, 1, self.pad, add_ptr, add_ld, None, s)
             elif self.bf:
-                _timed_call(f"igemm{self.ks}_dgrad", self.flops(), "seg_conv_igemm_bf16", dYp, dY.ld, y.N, y.H, y.W,
+                rt.tcall(f"igemm{self.ks}_dgrad", self.flops(), "seg_conv_igemm_bf16", dYp, dY.ld, y.N, y.H, y.W,
                             kin, self.wk_d.data_ptr(), self.ldk_d, None, rt.gptr(i), i.ld, i.H, i.W, self.cin,
                             self.ks, 1, self.pad, add_ptr, add_ld, None, ACT_NONE, None, 1, s)
             else:
-                _timed_call(f"igemm{self.ks}_dgrad", self.flops(), "seg_conv_igemm", dYp, dY.ld, y.N, y.H, y.W, kin,
+                rt.tcall(f"igemm{self.ks}_dgrad", self.flops(), "seg_conv_igemm", dYp, dY.ld, y.N, y.H, y.W, kin,
                             self.wk_d.data_ptr(), self.ldk_d, None, rt.gptr(i), i.ld, i.H, i.W, self.cin, self.ks, 1,
                             self.pad, add_ptr, add_ld, None, s)
         rt.mark_written(i)
@@ -380,13 +396,13 @@ class UpsampleOp:
 
     def forward(self, rt):
         l, o = self.low, self.out
-        call(rt.k("seg_upsample_fwd"), rt.ptr(l), l.ld, l.N, l.H, l.W, l.C, rt.ptr(o), o.ld, o.H, o.W, 0, rt.stream)
+        rt.call(rt.k("seg_upsample_fwd"), rt.ptr(l), l.ld, l.N, l.H, l.W, l.C, rt.ptr(o), o.ld, o.H, o.W, 0, rt.stream)
 
     def backward(self, rt):
         l, o = self.low, self.out
         d = rt.grad_of(o)
         acc = rt.begin_write_accumulate(l)
-        call(rt.k("seg_upsample_bwd"), rt.gptr(d), d.ld, 0, o.N, o.H, o.W, o.C, rt.gptr(l), l.ld, l.H, l.W, 0, acc,
+        rt.call(rt.k("seg_upsample_bwd"), rt.gptr(d), d.ld, 0, o.N, o.H, o.W, o.C, rt.gptr(l), l.ld, l.H, l.W, 0, acc,
              rt.stream)
         rt.mark_written(l)
 
@@ -402,13 +418,13 @@ class PoolOp:
 
     def forward(self, rt):
         i, o = self.inp, self.out
-        call(rt.k("seg_maxpool2_fwd"), rt.ptr(i), i.ld, i.N, i.H, i.W, i.C, rt.ptr(o), o.ld, rt.stream)
+        rt.call(rt.k("seg_maxpool2_fwd"), rt.ptr(i), i.ld, i.N, i.H, i.W, i.C, rt.ptr(o), o.ld, rt.stream)
 
     def backward(self, rt):
         i, o = self.inp, self.out
         d = rt.grad_of(o)
         acc = rt.begin_write_accumulate(i)
-        call(rt.k("seg_maxpool2_bwd"), rt.ptr(i), i.ld, rt.gptr(d), d.ld, i.N, i.H, i.W, i.C, rt.gptr(i), i.ld, acc,
+        rt.call(rt.k("seg_maxpool2_bwd"), rt.ptr(i), i.ld, rt.gptr(d), d.ld, i.N, i.H, i.W, i.C, rt.gptr(i), i.ld, acc,
              rt.stream)
         rt.mark_written(i)
 
@@ -457,16 +473,16 @@ class Program:
         op.out, op.lazy = op.y, True
         return op
 
-    def pack(self, stream):
-        """Repack every conv weight for this step (one seg_pack_batch launch).  The
-        packed buffers and the device job table are built once and rebuilt only
-        when a weight's storage moves (e.g. model.to())."""
+    def pack(self, rt):
+        """Repack every conv weight for this step (one seg_pack_batch launch on the run's
+        stream).  The packed buffers and the device job table are built once and rebuilt
+        only when a weight's storage moves (e.g. model.to())."""
         convs = [op for op in self.ops if isinstance(op, ConvOp)]
         key = tuple(op.conv.weight.data_ptr() for op in convs)
         if getattr(self, "_pack_key", None) != key:
             self._build_pack(convs, key)
         if self._njobs:
-            call("seg_pack_batch", self._jobs.data_ptr(), self._njobs, self._max_elems, stream)
+            rt.call("seg_pack_batch", self._jobs.data_ptr(), self._njobs, self._max_elems, rt.stream)
 
     def _build_pack(self, convs, key):
         import numpy as np
@@ -766,12 +782,19 @@ def set_conv_math(model, math: str):
 
 class Run:
     """State of one forward (and its backward): buffers, saved BN statistics,
-    gradient buffers and which gradient regions have been written."""
+    gradient buffers and which gradient regions have been written.
 
-    def __init__(self, prog: Program, image: torch.Tensor, training: bool):
+    Two ways to execute the walk: immediately (every launch is a ctypes call on the
+    current stream -- the Predictor's folded eval forward, captured in a hipGraph), or
+    recorded (`rec` set: every launch, event pair and memset becomes an entry of a
+    launch tape, seg_amd/tape.py; all buffers are then persistent so the tape can be
+    replayed step after step)."""
+
+    def __init__(self, prog: Program, image: torch.Tensor, training: bool, rec=None, side=None):
         self.prog, self.image, self.training = prog, image, training
         self.device = image.device
         self.stream = torch.cuda.current_stream(self.device).cuda_stream
+        self.rec = rec
         # activation / gradient storage: fp32, or bf16 for math "bf16io" (the _bf16io kernels)
         self.io = prog.math == "bf16io"
         self.store = torch.bfloat16 if self.io else torch.float32
@@ -780,17 +803,40 @@ class Run:
                      for n, (rows, ld) in prog.bufs.items()}
         self.saved = {}
         self.gbufs = {}
+        self.keep = []        # workspaces of a recorded run (persistent: the tape points at them)
         self.written = {}     # grad buffer name -> list of (lo, hi) channel ranges
         self.pending = {}     # Act.key() -> addend Act (residual upstream gradient)
         self.grads = {}       # id(param) -> grad tensor
+        self.flat = None      # recorded run: one flat fp32 buffer holding every parameter gradient
         self.sync = None
         self._tmp_n = 0
-        self.side = None      # side stream of the parameter gradients (backward only)
+        self.side = side      # side stream of the parameter gradients (recorded backward)
         self._n_fork = 0      # side-stream forks so far (index into the program's event pool)
 
     def k(self, name: str) -> str:
         """C-ABI entry point of an activation kernel for this run's storage type."""
         return name + "_bf16io" if self.io else name
+
+    # launches
+    def call(self, name, *args):
+        if self.rec is not None:
+            self.rec.call(name, args)
+        else:
+            call(name, *args)
+
+    def tcall(self, kind, flops, name, *args):
+        """A launch of the roofline kernel families (bench.py times them)."""
+        if self.rec is not None:
+            self.rec.call(name, args, timer=(kind, flops))
+        else:
+            _timed_call(kind, flops, name, *args)
+
+    def zero(self, a: Act):
+        """Zero-fill the gradient region of `a` (a channel slice of a row buffer)."""
+        if self.rec is not None:
+            self.rec.memset2d(self.gptr(a), a.ld * self.es, 0, a.C * self.es, a.M, self.stream)
+        else:
+            self.gbuf(a.buf).view(-1, a.ld)[:, a.off:a.off + a.C].zero_()
 
     # pointers
     def ptr(self, a: Act) -> int:
@@ -810,7 +856,10 @@ class Run:
         return g
 
     def tmp(self, n: int) -> torch.Tensor:
-        return torch.empty(max(int(n), 1), device=self.device, dtype=torch.float32)
+        t = torch.empty(max(int(n), 1), device=self.device, dtype=torch.float32)
+        if self.rec is not None:
+            self.keep.append(t)
+        return t
 
     @staticmethod
     def row_tiles(M: int, C: int):
@@ -835,6 +884,11 @@ class Run:
         stream; temporaries allocated inside the context belong to the side stream."""
         if self.side is None:
             return contextlib.nullcontext(), self.stream
+        if self.rec is not None:
+            ev = self.rec.event()
+            self.rec.record(ev, self.stream)
+            self.rec.wait(self.side.cuda_stream, ev)
+            return contextlib.nullcontext(), self.side.cuda_stream
         # events are reused step after step (a wait binds to the record before it)
         pool = self.prog.__dict__.setdefault("_fork_events", [])
         if self._n_fork == len(pool):
@@ -846,7 +900,13 @@ class Run:
         return self._side_ctx, self.side.cuda_stream
 
     def join(self):
-        if self.side is not None:
+        if self.side is None:
+            return
+        if self.rec is not None:
+            ev = self.rec.event()
+            self.rec.record(ev, self.side.cuda_stream)
+            self.rec.wait(self.stream, ev)
+        else:
             self.main.wait_stream(self.side)
 
     # gradient-region bookkeeping
@@ -864,18 +924,17 @@ class Run:
         """Gradient region of activation `a` (zero-filled if nobody wrote it)."""
         if not self._covered(a):
             add = self.pending.pop(a.key(), None)
-            v = self.gbuf(a.buf).view(-1, a.ld)[:, a.off:a.off + a.C]
             if add is not None:
-                call(self.k("seg_add"), self.gptr(add), add.ld, None, 0, a.M, a.C, self.gptr(a), a.ld, self.stream)
+                self.call(self.k("seg_add"), self.gptr(add), add.ld, None, 0, a.M, a.C, self.gptr(a), a.ld, self.stream)
             else:
-                v.zero_()
+                self.zero(a)
             self.mark_written(a)
         return a
 
     def add_pending(self, target: Act, addend: Act):
         if self._covered(target):
-            call(self.k("seg_add"), self.gptr(target), target.ld, self.gptr(addend), addend.ld, target.M, target.C,
-                 self.gptr(target), target.ld, self.stream)
+            self.call(self.k("seg_add"), self.gptr(target), target.ld, self.gptr(addend), addend.ld, target.M, target.C,
+                      self.gptr(target), target.ld, self.stream)
         else:
             self.pending[target.key()] = addend
 
@@ -894,7 +953,7 @@ class Run:
             return 1
         add = self.pending.pop(a.key(), None)
         if add is not None:
-            call(self.k("seg_add"), self.gptr(add), add.ld, None, 0, a.M, a.C, self.gptr(a), a.ld, self.stream)
+            self.call(self.k("seg_add"), self.gptr(add), add.ld, None, 0, a.M, a.C, self.gptr(a), a.ld, self.stream)
             self.mark_written(a)
             return 1
         return 0
@@ -903,21 +962,39 @@ class Run:
         g = self.grads.get(id(p))
         if g is None:
             g = self.sync.grad_storage(p) if self.sync is not None else None
+            if g is None and self.flat is not None:
+                o, n = self.flat_slots[id(p)]
+                g = self.flat[o:o + n].view_as(p)
             if g is None:
                 g = torch.empty_like(p)
             self.grads[id(p)] = g
         return g.data_ptr()
 
-    def params_done(self, ps):
-        if self.sync is not None:
-            self.sync.on_ready([p for p in ps if id(p) in self.grads])
+    def params_done(self, ps, stream=None):
+        """The gradients of `ps` are complete on `stream` (DataParallel bucket readiness)."""
+        if self.sync is None:
+            return
+        ready = [p for p in ps if id(p) in self.grads]
+        if self.rec is None:
+            self.sync.on_ready(ready)
+            return
+        sync = self.sync
+        st = self.side if (self.side is not None and stream == self.side.cuda_stream) else None
+
+        def on_ready():  # host callback between tape segments
+            if st is None:
+                sync.on_ready(ready)
+            else:
+                with torch.cuda.stream(st):
+                    sync.on_ready(ready)
+        self.rec.stop(on_ready)
 
     # drivers
     def forward(self):
         global LAST_RUN
         x, img = self.image, self.prog.image
-        self.prog.pack(self.stream)
-        call(self.k("seg_nchw_to_nhwc"), x.data_ptr(), img.N, 3, img.H, img.W, self.ptr(img), img.ld, self.stream)
+        self.prog.pack(self)
+        self.call(self.k("seg_nchw_to_nhwc"), x.data_ptr(), img.N, 3, img.H, img.W, self.ptr(img), img.ld, self.stream)
         for op in self.prog.ops:
             op.forward(self)
         if DEBUG_KEEP_RUN:
@@ -934,7 +1011,7 @@ class Run:
 
     def backward_from_logits(self):
         global LAST_RUN
-        if OVERLAP:
+        if self.rec is None and OVERLAP:
             self.main = torch.cuda.current_stream(self.device)
             self.side = _side_stream(self.device)
             self._side_ctx = torch.cuda.StreamContext(self.side)  # re-entered by every fork
@@ -1015,14 +1092,14 @@ def _check_input(x: torch.Tensor):
 
 
 def _loss_forward(run, t, ignore_index):
-    """Fused final upsample + CrossEntropy over the run's low-res logits: stats = [loss, count]."""
+    """Fused final upsample + CrossEntropy over the run's low-res logits: stats = [loss, count, #bad labels]."""
     prog, lo, s = run.prog, run.prog.logits, run.stream
     N = prog.N
     Ho, Wo = prog.out_hw
-    stats = torch.empty(3, device=run.device, dtype=torch.float32)  # loss, #valid, #out-of-range labels
+    stats = run.tmp(3)  # loss, #valid, #out-of-range labels
     work = run.tmp(query("seg_ce_workspace_floats", N * Ho * Wo))
-    call(run.k("seg_ce_upsample_loss"), run.ptr(lo), lo.ld, N, lo.H, lo.W, lo.C, t.data_ptr(), Ho, Wo,
-         ignore_index, work.data_ptr(), stats.data_ptr(), s)
+    run.call(run.k("seg_ce_upsample_loss"), run.ptr(lo), lo.ld, N, lo.H, lo.W, lo.C, t.data_ptr(), Ho, Wo,
+             ignore_index, work.data_ptr(), stats.data_ptr(), s)
     run.target, run.stats = t, stats
     return stats
 
@@ -1033,18 +1110,147 @@ def _loss_backward(run, g, ignore_index):
     N = prog.N
     Ho, Wo = prog.out_hw
     dhigh = torch.empty(max(N * Ho * Wo * lo.ld, 1), device=run.device, dtype=run.store)
-    call(run.k("seg_ce_upsample_grad"), run.ptr(lo), lo.ld, N, lo.H, lo.W, lo.C, run.target.data_ptr(), Ho, Wo,
-         ignore_index, g.data_ptr(), run.stats.data_ptr(), dhigh.data_ptr(), lo.ld, s)
-    call(run.k("seg_upsample_bwd"), dhigh.data_ptr(), lo.ld, 0, N, Ho, Wo, lo.C, run.gptr(lo), lo.ld, lo.H, lo.W,
-         1, 0, s)
+    run.keep.append(dhigh)
+    run.call(run.k("seg_ce_upsample_grad"), run.ptr(lo), lo.ld, N, lo.H, lo.W, lo.C, run.target.data_ptr(), Ho, Wo,
+             ignore_index, g.data_ptr(), run.stats.data_ptr(), dhigh.data_ptr(), lo.ld, s)
+    run.call(run.k("seg_upsample_bwd"), dhigh.data_ptr(), lo.ld, 0, N, Ho, Wo, lo.C, run.gptr(lo), lo.ld, lo.H, lo.W,
+             1, 0, s)
     run.mark_written(lo)
     run.backward_from_logits()
-    if run.sync is not None:
-        run.sync.finish_gradient_sync()  # stream-ordered wait on the last all-reduces
+
+
+class Plan:
+    """One (input shape, mode) of a model compiled to two launch tapes (seg_amd/tape.py):
+    the forward (weight repack, NCHW -> NHWC, every op, the fused loss or the NCHW logits)
+    and the backward (loss / logits gradient, every op in reverse, parameter gradients on
+    the side stream, DataParallel bucket all-reduces at host-callback stops).  Recorded
+    by the first step -- a normal program walk with every launch captured instead of
+    issued -- and replayed by the following ones with the caller's input / target /
+    output / upstream-gradient pointers patched in.  Buffers, workspaces, saved BN
+    statistics and the flat parameter-gradient buffer are persistent (allocated while
+    recording, ~13 GB at bs=32 256x512 fp32 -- nothing is recomputed).
+
+    The replay issues the same launches on the same two streams as an eager walk, so
+    results are bitwise those of the eager engine (tests/test_gpu_tape.py)."""
+
+    def __init__(self, prog, training, mode, ignore_index, sync, needs_grad, device):
+        self.prog, self.training, self.mode, self.ignore_index = prog, training, mode, ignore_index
+        self.sync, self.needs_grad, self.device = sync, needs_grad, device
+        self.side = _side_stream(device) if (OVERLAP and needs_grad) else None
+        self.run = self.fwd = self.bwd = None
+        self.t = None            # the last forward's labels (loss mode)
+        self.busy = False        # a forward whose backward has not run yet
+        self.timer = None        # the KernelTimer the tapes' timing is armed for
+
+    def _streams(self):
+        main = torch.cuda.current_stream(self.device).cuda_stream
+        return main, (self.side.cuda_stream if self.side is not None else main)
+
+    def _arm_timer(self, tape):
+        if TIMER is not self.timer:
+            for t in (self.fwd, self.bwd):
+                if t is not None:
+                    if self.timer is not None:
+                        self.timer.collect(t)
+                    t.time([], 0)
+            self.timer = TIMER
+        if TIMER is not None and tape not in TIMER.tapes:
+            tape.time(TIMER.kinds, TIMER.max_replays)
+            TIMER.tapes.append(tape)
+
+    def forward(self, x, t):
+        from .tape import Recorder
+        main, side = self._streams()
+        N, _, H, W = x.shape
+        Ho, Wo = self.prog.out_hw
+        out = None
+        if self.mode == "logits":
+            out = torch.empty((N, self.prog.logits.C, Ho, Wo), device=x.device, dtype=torch.float32)
+        if self.fwd is None:
+            rec = Recorder({side: 1, main: 0})
+            rec.external("x", x.data_ptr())
+            if t is not None:
+                rec.external("t", t.data_ptr())
+            if out is not None:
+                rec.external("out", out.data_ptr())
+            run = Run(self.prog, x, self.training, rec=rec, side=self.side)
+            run.sync = self.sync
+            if self.needs_grad:
+                ps = [p for p in self.prog.params() if p.requires_grad]
+                run.flat_slots, off = {}, 0
+                for p in ps:
+                    run.flat_slots[id(p)] = (off, p.numel())
+                    off += p.numel()
+                run.flat = torch.empty(max(off, 1), device=x.device, dtype=torch.float32)
+            run.forward()
+            lo = self.prog.logits
+            if self.mode == "logits":
+                run.call(run.k("seg_upsample_to_nchw"), run.ptr(lo), lo.ld, N, lo.H, lo.W, lo.C, out.data_ptr(), Ho,
+                         Wo, 1, run.stream)
+            else:
+                _loss_forward(run, t, self.ignore_index)
+            run.rec = None
+            self.run, self.fwd = run, rec.build()
+        self._arm_timer(self.fwd)
+        self.t = t  # the backward tape reads the labels: keep them alive until then
+        self.fwd.bind(x=x.data_ptr(), t=t.data_ptr() if t is not None else 0,
+                      out=out.data_ptr() if out is not None else 0)
+        self.fwd.run(main, side)
+        if DEBUG_KEEP_RUN:
+            global LAST_RUN
+            LAST_RUN = self.run
+        return out
+
+    def backward(self, gout):
+        from .tape import Recorder
+        run = self.run
+        main, side = self._streams()
+        if self.mode == "logits":
+            g = gout.contiguous()
+        else:
+            g = gout.reshape(1).to(torch.float32).contiguous()
+        if self.bwd is None:
+            rec = Recorder({side: 1, main: 0})
+            rec.external("gout", g.data_ptr())
+            if self.t is not None:
+                rec.external("t", self.t.data_ptr())
+            run.rec = rec
+            if self.mode == "logits":
+                prog, lo = self.prog, self.prog.logits
+                Ho, Wo = prog.out_hw
+                run.call(run.k("seg_upsample_bwd"), g.data_ptr(), 0, 1, prog.N, Ho, Wo, lo.C, run.gptr(lo), lo.ld,
+                         lo.H, lo.W, 1, 0, run.stream)
+                run.mark_written(lo)
+                run.backward_from_logits()
+            else:
+                _loss_backward(run, g, self.ignore_index)
+            run.rec = None
+            self.bwd = rec.build()
+        self._arm_timer(self.bwd)
+        self.bwd.bind(gout=g.data_ptr(), t=self.t.data_ptr() if self.t is not None else 0)
+        self.bwd.run(main, side)
+        if DEBUG_KEEP_RUN:
+            global LAST_RUN
+            LAST_RUN = run
+        if self.sync is not None:
+            self.sync.finish_gradient_sync()  # stream-ordered wait on the last all-reduces
+
+
+def _plan(model, prog, mode, ignore_index, sync, needs_grad, device):
+    cache = model.__dict__.setdefault("_segamd_plans", {})
+    key = (id(prog), mode, model.training, ignore_index, id(sync) if sync is not None else None, needs_grad, OVERLAP)
+    plan = cache.get(key)
+    if plan is None or plan.sync is not sync:
+        plan = cache[key] = Plan(prog, model.training, mode, ignore_index, sync, needs_grad, device)
+    if plan.busy:
+        # a second forward before this plan's backward ran: a one-off plan keeps the first
+        # forward's activations intact (recorded and run once, then dropped)
+        plan = Plan(prog, model.training, mode, ignore_index, sync, needs_grad, device)
+    return plan
 
 
 class _SegFunction(torch.autograd.Function):
-    """Whole-network forward/backward as one autograd node."""
+    """Whole-network forward/backward as one autograd node (replaying the plan's tapes)."""
 
     @staticmethod
     def forward(ctx, model, mode, x, target, ignore_index, sync, *params):
@@ -1057,53 +1263,41 @@ class _SegFunction(torch.autograd.Function):
             t = target.contiguous()
             if t.dtype != torch.int64 or tuple(t.shape) != (N, Ho, Wo):
                 raise ValueError(f"target must be int64 [{N},{Ho},{Wo}], got {tuple(t.shape)} {t.dtype}")
-
-        run = Run(prog, x, model.training)
-        run.sync = sync
-        run.forward()
-        lo = prog.logits
-        if mode == "logits":
-            out = torch.empty((N, lo.C, Ho, Wo), device=x.device, dtype=torch.float32)
-            call(run.k("seg_upsample_to_nchw"), run.ptr(lo), lo.ld, N, lo.H, lo.W, lo.C, out.data_ptr(), Ho, Wo, 1,
-                 run.stream)
+        needs_grad = any(ctx.needs_input_grad[6:])
+        plan = _plan(model, prog, mode, ignore_index, sync, needs_grad, x.device)
+        out = plan.forward(x, t)
+        if mode == "loss":
+            model.__dict__["_segamd_last_stats"] = plan.run.stats
+            out = plan.run.stats[0].clone()  # the stats buffer is rewritten by the next step
+        if needs_grad:
+            plan.busy = True
+            ctx.plan, ctx.params = plan, params
         else:
-            stats = _loss_forward(run, t, ignore_index)
-            model.__dict__["_segamd_last_stats"] = stats
-            out = stats[0]
-        if any(ctx.needs_input_grad[6:]):
-            ctx.run, ctx.mode, ctx.ignore_index = run, mode, ignore_index
-            ctx.params = params
-        else:
-            ctx.run = None
+            ctx.plan = None
         return out
 
     @staticmethod
     def backward(ctx, gout):
-        run = ctx.run
-        if run is None:
+        plan = ctx.plan
+        if plan is None:
             raise RuntimeError("segamd: backward called on a forward that saved nothing")
-        prog, lo, s = run.prog, run.prog.logits, run.stream
-        N = prog.N
-        Ho, Wo = prog.out_hw
-        if ctx.mode == "logits":
-            g = gout.contiguous()
-            call(run.k("seg_upsample_bwd"), g.data_ptr(), 0, 1, N, Ho, Wo, lo.C, run.gptr(lo), lo.ld, lo.H, lo.W, 1,
-                 0, s)
-            run.mark_written(lo)
-            run.backward_from_logits()
-            if run.sync is not None:
-                run.sync.finish_gradient_sync()
-        else:
-            _loss_backward(run, gout.reshape(1).to(torch.float32).contiguous(), ctx.ignore_index)
+        try:
+            plan.backward(gout)
+        finally:
+            plan.busy = False
+        run = plan.run
         if run.sync is not None:  # DataParallel: copies of the averaged buckets, never the buckets
             grads = run.sync.autograd_grads(ctx.params)
-            grads = [g if ctx.needs_input_grad[6 + k] else None for k, g in enumerate(grads)]
         else:
-            grads = [run.grads.get(id(p)) if ctx.needs_input_grad[6 + k] else None for k, p in enumerate(ctx.params)]
-        # drop every other reference so AccumulateGrad can adopt the tensors instead of copying them
-        run.grads.clear()
-        ctx.run = ctx.params = None
-        del run
+            # one copy of the flat gradient buffer (the next backward rewrites it): a .grad
+            # never aliases engine memory, and AccumulateGrad adopts the views as they are
+            flat = run.flat.clone()
+            grads = []
+            for p in ctx.params:
+                slot = run.flat_slots.get(id(p)) if id(p) in run.grads else None
+                grads.append(flat[slot[0]:slot[0] + slot[1]].view_as(p) if slot else None)
+        grads = [g if ctx.needs_input_grad[6 + k] else None for k, g in enumerate(grads)]
+        ctx.plan = ctx.params = None
         return (None, None, None, None, None, None, *grads)
 
 

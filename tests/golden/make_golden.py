@@ -13,7 +13,9 @@ reference's criterion nn.CrossEntropyLoss() (main.py:99) and the optimizer step
 is optim.Adam(lr=1.5e-4) (main.py:100) driven like src/train.py:35-39.
 
 Outputs: <case>.npz (inputs, logits, loss, per-parameter gradient statistics in
-fp32 and fp64, BN running statistics) and state_dict_keys.json.
+fp32 and fp64, BN running statistics; the mIoU case: held-out predictions and mIoU
+before / after 150 training steps) and state_dict_keys.json.
+    python tests/golden/make_golden.py [case ...]   # only the named cases
 """
 from __future__ import annotations
 
@@ -32,7 +34,7 @@ REF = os.environ.get("SEG_REFERENCE", "/root/reference")
 sys.path.insert(0, os.path.join(REPO, "team02-objectdetection_amd"))
 sys.path.insert(0, HERE)
 
-from seg_amd.detinit import deterministic_init, synthetic_batch  # noqa: E402
+from seg_amd.detinit import deterministic_init, miou, synthetic_batch, synthetic_scene  # noqa: E402
 import tv_stub  # noqa: E402
 
 SMALL = 4096  # store full gradients of tensors up to this many elements
@@ -144,9 +146,64 @@ def run_adam(ref, n, h, w, classes, seed, steps=3):
     return out
 
 
+MIOU = {"seed": 3, "classes": 10, "h": 128, "w": 256, "bs": 8, "steps": 150, "lr": 1.5e-4, "heldout": 32,
+        "heldout_seed": 999, "batch_seed0": 100}
+
+
+def run_miou(ref):
+    """SURVEY 8(d)'s mIoU parity case: the reference MobileNetV2UNet(10) trained by its own loop
+    (src/train.py:35-39: zero_grad, CrossEntropyLoss, backward, Adam(lr=1.5e-4) step) for
+    `steps` batches of the learnable synthetic scene (seg_amd.detinit.synthetic_scene), then
+    evaluated (model.eval(), inference.py:25) on a held-out scene batch: argmax predictions
+    and mIoU before and after training: fp32 on 8 threads (the reference as main.py runs it
+    on this CPU), fp32 on 1 thread (another valid fp32 summation order) and fp64 -- the
+    spread among the three is the reference's own run-to-run mIoU spread.  Measured:
+    after 50 steps two fp32 thread counts differ by 2.4e-3 mIoU (97.8 % pixel agreement,
+    the model is still uncertain), after 150 steps by <= 6.4e-4 (99.5 %), so 150 steps."""
+    c = MIOU
+    xe, ye = synthetic_scene(c["heldout"], c["h"], c["w"], c["classes"], seed=c["heldout_seed"])
+    out = {"meta": np.array(json.dumps(c)), "heldout_y": ye.numpy().astype(np.uint8)}
+    threads = torch.get_num_threads()
+    for dtype, tag, nthr in ((torch.float32, "32", threads), (torch.float32, "32t1", 1), (torch.float64, "64", threads)):
+        torch.set_num_threads(nthr)
+        model = ref.MobileNetV2UNet(output_channels=c["classes"])
+        deterministic_init(model, seed=c["seed"])
+        model = model.to(dtype)
+        crit = torch.nn.CrossEntropyLoss()
+        opt = torch.optim.Adam(model.parameters(), lr=c["lr"])
+
+        def evaluate():
+            model.eval()
+            with torch.no_grad():
+                pred = torch.cat([model(xe[i:i + 8].to(dtype)).argmax(1) for i in range(0, len(xe), 8)])
+            model.train()
+            return pred
+
+        p0 = evaluate()
+        losses = []
+        for s in range(c["steps"]):
+            x, y = synthetic_scene(c["bs"], c["h"], c["w"], c["classes"], seed=c["batch_seed0"] + s)
+            opt.zero_grad()
+            loss = crit(model(x.to(dtype)), y)
+            loss.backward()
+            opt.step()
+            losses.append(loss.item())
+        p1 = evaluate()
+        out[f"losses{tag}"] = np.array(losses)
+        out[f"miou_init{tag}"] = np.array(miou(p0, ye, c["classes"]))
+        out[f"miou{tag}"] = np.array(miou(p1, ye, c["classes"]))
+        if tag == "32":
+            out["pred_init32"] = p0.numpy().astype(np.uint8)
+            out["pred32"] = p1.numpy().astype(np.uint8)
+        print(f"  miou fp{tag}: init {float(out[f'miou_init{tag}']):.5f} after {c['steps']} steps "
+              f"{float(out[f'miou{tag}']):.5f}, loss {losses[0]:.4f} -> {losses[-1]:.4f}")
+    return out
+
+
 def main():
     torch.set_num_threads(min(8, os.cpu_count() or 1))
     ref = load_reference_unet()
+    only = set(sys.argv[1:])
     cases = {
         "mnv2_train_2x64x128": lambda: run_case(ref, "MobileNetV2UNet", lambda: ref.MobileNetV2UNet(10),
                                                 2, 64, 128, 10, seed=1),
@@ -157,11 +214,16 @@ def main():
         "lightunet_eval_1x32x32": lambda: run_case(ref, "LightUNet", lambda: ref.LightUNet(), 1, 32, 32, 1,
                                                    seed=4, training=False, backward=False, random_stats=True),
         "mnv2_adam3_2x64x64": lambda: run_adam(ref, 2, 64, 64, 10, seed=5),
+        "mnv2_miou_scene_150steps": lambda: run_miou(ref),
     }
     for name, fn in cases.items():
+        if only and name not in only:
+            continue
         res = fn()
         np.savez_compressed(os.path.join(HERE, name + ".npz"), **res)
         print(name, "loss32" in res and float(res["loss32"]), "written")
+    if only:
+        return
     keys = {}
     for arch, ctor in (("MobileNetV2UNet", lambda: ref.MobileNetV2UNet(10)), ("UNet", lambda: ref.UNet(10)),
                        ("LightUNet", lambda: ref.LightUNet())):

@@ -202,3 +202,18 @@ def test_cpu_input_raises():
     model = make("MobileNetV2UNet", 10, 0)
     with pytest.raises(RuntimeError, match="HIP path only"):
         model(torch.zeros(1, 3, 64, 64))
+
+
+def test_traceable_twin_matches_hip_eval():
+    """seg_amd.traceable (convert.py:21-42's export module, pure torch on the CPU) against
+    the HIP eval forward of the same weights: logits within 1e-3."""
+    from seg_amd import traceable
+    model = make("MobileNetV2UNet", 10, 12, random_stats=True).to(DEV).eval()
+    x = torch.randn(1, 3, 128, 256, generator=torch.Generator().manual_seed(1))  # convert.py:26 dummy
+    with torch.no_grad():
+        hip = model(x.to(DEV)).cpu()
+        twin = traceable(model)
+        ref = torch.jit.trace(twin, x)(x)
+    assert rel(hip, ref) < 1e-3
+    with pytest.raises(RuntimeError, match="export and CPU use"):
+        twin.to(DEV)(x.to(DEV))

@@ -120,3 +120,23 @@ def test_miou_definition():
     tgt = torch.tensor([0, 1, 2, 2, 2, 1])
     # class0 IoU 1; class1 tp1 fp1 fn1 -> 1/3; class2 tp2 fp1 fn1 -> 1/2
     assert abs(segref.miou(pred, tgt, 3) - (1 + 1 / 3 + 1 / 2) / 3) < 1e-12
+
+
+def test_oracle_miou_scene_fixture(golden_dir):
+    """The learnable scene is regenerated bit-exactly from its seed, and the oracle's Adam
+    trajectory reproduces the reference's first training losses (fixture made from
+    src/unet.py; the full 150-step mIoU is the GPU test's job)."""
+    import json
+    from seg_amd.detinit import miou, synthetic_scene
+    z = np.load(os.path.join(golden_dir, "mnv2_miou_scene_150steps.npz"), allow_pickle=False)
+    c = json.loads(str(z["meta"]))
+    xe, ye = synthetic_scene(c["heldout"], c["h"], c["w"], c["classes"], seed=c["heldout_seed"])
+    assert np.array_equal(ye.numpy(), z["heldout_y"])
+    m = deterministic_init(MobileNetV2UNet(c["classes"]), seed=c["seed"])
+    p = segref.canonical_state(m.state_dict())
+    with torch.no_grad():
+        pred = torch.cat([segref.mobilenet_unet_forward(p, xe[i:i + 8], False).argmax(1) for i in range(0, 32, 8)])
+    assert abs(miou(pred, ye, c["classes"]) - float(z["miou_init32"])) < 1e-4
+    batches = [synthetic_scene(c["bs"], c["h"], c["w"], c["classes"], seed=c["batch_seed0"] + s) for s in range(5)]
+    losses = segref.adam_steps("MobileNetV2UNet", p, batches, lr=c["lr"])
+    np.testing.assert_allclose(losses, z["losses32"][:5], rtol=1e-4)

@@ -346,7 +346,7 @@ def main():
         # the other conv families and the side-stream-free figure: separate untimed passes
         rec_all = extra_pass(engine.OVERLAP)
         wf, ws, wgn = family(rec_all, {"igemm3_wgrad", "wino3_wgrad"})
-        af, as_, an = family(rec_all, {k for k, _, _ in rec_all})
+        af, as_, an = family(rec_all, {k for k, _, _ in rec_all if k.startswith(("igemm", "wino", "halo"))})
         rec_iso = extra_pass(False)
         ifl, isec, inn = family(rec_iso, conv3)
         if args.math == "f32":  # compute-bound config: FLOPs against the f32 MFMA peak

@@ -148,14 +148,17 @@ int seg_conv_halo(const float* in, long ldin, int N, int H, int W, int Cin, cons
 /* Every weight repack of a step in one launch.  `jobs` is a DEVICE array of
  * njobs seg_pack_job (mode 0/1 as seg_pack_conv_weight, mode 2 = depthwise
  * [9][C] as seg_pack_dw_weight with cout = C, modes 3/4 = Winograd filter
- * transforms [16][rows][ldk] for seg_conv_wino's forward / data gradient); max_elems = largest job's
- * element count.  Replaces the per-conv packs of the engine's step. */
+ * transforms [16][rows][ldk] for seg_conv_wino's forward / data gradient).  One thread
+ * per output element; job k owns the launch's blocks [blk0, blk0 + nblk), nblk =
+ * ceil(elements / 256), jobs sorted by blk0; nblocks = the total.  Replaces the
+ * per-conv packs of the engine's step. */
 typedef struct seg_pack_job {
   const float* w;
   float* wk;
   int cout, cin, ks, ldk, mode, kin_pad;
+  int blk0, nblk;
 } seg_pack_job;
-int seg_pack_batch(const void* jobs, int njobs, long max_elems, hipStream_t stream);
+int seg_pack_batch(const void* jobs, int njobs, long nblocks, hipStream_t stream);
 
 /* Depthwise 3x3 (torchvision InvertedResidual dw conv, features[1..17] via
  * src/unet.py:15-19): forward, data gradient, weight-gradient partials.

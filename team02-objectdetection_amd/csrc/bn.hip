@@ -17,131 +17,177 @@
 
 namespace {
 
-// Wide layers (C >= 256: the encoder's 384..1280-channel tensors at 8x16 / 16x32, M =
-// 4096 / 16384) split their channels over blockIdx.y in slices of kChanSlice float4
-// groups (chan_split), so a block has 8 row lanes instead of 1-2 (which walked 32 rows
-// serially: latency-bound 15-25 us launches).  The partial layout [row block][2][C]
-// and the workspace size do not depend on the split.
-constexpr int kChanSlice = 32;
-
-// Per-block partial sums over a row range for float4 channel groups.
-// Block = 256 threads laid out as RG row-lanes x TC channel-group lanes.
+// Per-block partial sums over a row range, per channel.  512-thread blocks laid out as
+// RG row lanes x TC channel-group lanes; a lane owns VW = 8 channels when C % 8 == 0
+// (one 16-byte load per row and tensor on bf16 storage, two on fp32), else 4, and walks
+// its rows four at a time, so 8-16 independent loads are in flight per lane.  The
+// row / lane partition depends only on C, M and the row strides -- never on the storage
+// type -- so the fp32 and bf16io twins sum in the same order (bitwise-equal on
+// bf16-representable data, tests/test_gpu_bf16io.py).  Channel groups
+// beyond 64 are split over blockIdx.y (the encoder's 384..1280-channel layers).  The
+// row range is split into nblk = chan_blocks(M) blocks (<= 256: one or two waves of
+// 512-thread blocks per CU, and few enough partial rows for the finalize kernels'
+// single-pass fp64 sums).  Partials: part[blockIdx.x][2][C].
 // kind 0: (sum(y-k), sum((y-k)^2)),  k = y[0][c]                   -> BN stats
 // kind 1: (sum(dz),  sum(dz*(y-mean))), dz = dA * act'(y*scale+shift) -> BN backward
 // kind 2: (sum(y), 0)                                               -> bias grad
-template <int KIND, typename T = float>
-__global__ __launch_bounds__(256) void chan_partial_kernel(
+constexpr int kRedThreads = 512;
+constexpr int kRedSlice = 64;  // channel groups per block (blockIdx.y slices beyond)
+
+int chan_blocks(long M) { return (int)std::max<long>(1, std::min<long>(256, M / 64)); }
+
+template <int VW, typename T>
+__device__ __forceinline__ void ldw(const T* p, f32x4 (&o)[VW / 4]) {
+  if constexpr (VW == 8 && sizeof(T) == 2) {
+    const bf16x8 v = *reinterpret_cast<const bf16x8*>(p);
+    o[0] = __builtin_convertvector(__builtin_shufflevector(v, v, 0, 1, 2, 3), f32x4);
+    o[1] = __builtin_convertvector(__builtin_shufflevector(v, v, 4, 5, 6, 7), f32x4);
+  } else {
+#pragma unroll
+    for (int j = 0; j < VW / 4; ++j) o[j] = ld4(p + 4 * j);
+  }
+}
+
+template <int KIND, typename T, int VW>
+__global__ __launch_bounds__(kRedThreads) void chan_partial_kernel(
     const T* __restrict__ y, long ldy, const T* __restrict__ da, long ldda, int M, int C,
     const float* __restrict__ scale, const float* __restrict__ shift, const float* __restrict__ mean, int act,
     float* __restrict__ part, int rows_per_block) {
-  __shared__ f32x4 red0[256], red1[256];
-  // channel slice of this block (blockIdx.y; chan_split): CGB groups from cg0
-  const int CGB = gridDim.y > 1 ? kChanSlice : (C >> 2);
-  const int cg0 = blockIdx.y * CGB;
-  const int CG = min((C >> 2) - cg0, CGB);
-  const int TC = CGB < 256 ? CGB : 256;
-  const int RG = 256 / TC;
+  constexpr int NV = VW / 4;
+  __shared__ f32x4 red0[kRedThreads * NV], red1[kRedThreads * NV];
+  const int CG = C / VW;
+  const int cg0 = blockIdx.y * kRedSlice;
+  const int TC = min(CG - cg0, kRedSlice);
+  const int RG = kRedThreads / TC;
   const int t = threadIdx.x;
   const int rg = t / TC, tc = t - rg * TC;
+  const bool active = rg < RG;
   const int r0 = blockIdx.x * rows_per_block;
   const int r1 = min(M, r0 + rows_per_block);
-  float* p0 = part + (long)blockIdx.x * 2 * C;
-  float* p1 = p0 + C;
-  for (int cgb = 0; cgb < CG; cgb += TC) {
-    const int cg = cgb + tc;
-    const bool active = rg < RG && cg < CG;
-    f32x4 s0 = {0.f, 0.f, 0.f, 0.f}, s1 = {0.f, 0.f, 0.f, 0.f};
-    const int c = (cg0 + cg) * 4;
-    if (active) {
-      f32x4 k = {0.f, 0.f, 0.f, 0.f}, sc = k, sh = k;
-      if (KIND == 0) k = ld4(y + c);
-      if (KIND == 1) { k = ld4(mean + c); sc = ld4(scale + c); sh = ld4(shift + c); }
-      auto step = [&](int r) {
-        const f32x4 v = ld4(y + (long)r * ldy + c);
+  const int c = (cg0 + tc) * VW;
+  f32x4 s0[NV], s1[NV], k[NV], sc[NV], sh[NV];
+#pragma unroll
+  for (int j = 0; j < NV; ++j) {
+    s0[j] = s1[j] = k[j] = sc[j] = sh[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+  if (active) {
+    if (KIND == 0) ldw<VW>(y + c, k);
+    if (KIND == 1) {
+#pragma unroll
+      for (int j = 0; j < NV; ++j) {
+        k[j] = ld4(mean + c + 4 * j);
+        sc[j] = ld4(scale + c + 4 * j);
+        sh[j] = ld4(shift + c + 4 * j);
+      }
+    }
+    auto step = [&](const f32x4 (&v)[NV], const f32x4 (&g)[NV]) {
+#pragma unroll
+      for (int j = 0; j < NV; ++j) {
         if (KIND == 0) {
-          const f32x4 d = v - k;
-          s0 += d;
-          s1 += d * d;
+          const f32x4 d = v[j] - k[j];
+          s0[j] += d;
+          s1[j] += d * d;
         } else if (KIND == 1) {
-          const f32x4 g = ld4(da + (long)r * ldda + c);
           f32x4 dz;
 #pragma unroll
-          for (int j = 0; j < 4; ++j) dz[j] = g[j] * seg_act_mask(v[j] * sc[j] + sh[j], act);
-          s0 += dz;
-          s1 += dz * (v - k);
+          for (int e = 0; e < 4; ++e) dz[e] = g[j][e] * seg_act_mask(v[j][e] * sc[j][e] + sh[j][e], act);
+          s0[j] += dz;
+          s1[j] += dz * (v[j] - k[j]);
         } else {
-          s0 += v;
+          s0[j] += v[j];
         }
-      };
-      // 4 rows per iteration: their loads issue together (the loop is otherwise
-      // latency-bound, one dependent load pair per trip)
-      int r = r0 + rg;
-      for (; r + 3 * RG < r1; r += 4 * RG) {
-        step(r);
-        step(r + RG);
-        step(r + 2 * RG);
-        step(r + 3 * RG);
       }
-      for (; r < r1; r += RG) step(r);
-    }
-    red0[t] = s0;
-    red1[t] = s1;
-    __syncthreads();
-    // fixed-order tree over the RG row groups (log2 RG LDS steps instead of RG - 1
-    // serial ones: the narrow layers have RG = 16..64)
-    int p2 = 1;
-    while (p2 < RG) p2 <<= 1;
-    for (int h = p2 >> 1; h > 0; h >>= 1) {
-      if (rg < h && rg + h < RG) {
-        red0[t] += red0[t + h * TC];
-        red1[t] += red1[t + h * TC];
+    };
+    int r = r0 + rg;
+    for (; r + 3 * RG < r1; r += 4 * RG) {  // four rows' loads issued together
+      f32x4 v[4][NV], g[4][NV];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        ldw<VW>(y + (long)(r + q * RG) * ldy + c, v[q]);
+        if (KIND == 1) ldw<VW>(da + (long)(r + q * RG) * ldda + c, g[q]);
       }
-      __syncthreads();
+#pragma unroll
+      for (int q = 0; q < 4; ++q) step(v[q], g[q]);
     }
-    if (rg == 0 && active) {
-      st4(p0 + c, red0[tc]);
-      st4(p1 + c, red1[tc]);
+    for (; r < r1; r += RG) {
+      f32x4 v[NV], g[NV];
+      ldw<VW>(y + (long)r * ldy + c, v);
+      if (KIND == 1) ldw<VW>(da + (long)r * ldda + c, g);
+      step(v, g);
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < NV; ++j) {
+    red0[t * NV + j] = s0[j];
+    red1[t * NV + j] = s1[j];
+  }
+  __syncthreads();
+  // fixed-order tree over the RG row groups (deterministic)
+  int p2 = 1;
+  while (p2 < RG) p2 <<= 1;
+  for (int h = p2 >> 1; h > 0; h >>= 1) {
+    if (active && rg < h && rg + h < RG) {
+#pragma unroll
+      for (int j = 0; j < NV; ++j) {
+        red0[t * NV + j] += red0[(t + h * TC) * NV + j];
+        red1[t * NV + j] += red1[(t + h * TC) * NV + j];
+      }
     }
     __syncthreads();
   }
+  if (rg == 0) {
+    float* p0 = part + (long)blockIdx.x * 2 * C;
+#pragma unroll
+    for (int j = 0; j < NV; ++j) {
+      st4(p0 + c + 4 * j, red0[tc * NV + j]);
+      st4(p0 + C + c + 4 * j, red1[tc * NV + j]);
+    }
+  }
 }
 
-int rows_per_block_for(long M, int C) {
-  // ~2048 row blocks (8 per CU: latency hiding for the 2-load streams), >= 32 rows each
-  (void)C;
-  long r = (M + 2047) / 2048;
-  if (r < 32) r = 32;
-  return (int)r;
+// Launch chan_partial_kernel<KIND> over [M][C] (C % 4 == 0): 8-channel lanes when C, the
+// row strides and the tensors' element offsets are multiples of 8 (16-byte bf16 loads),
+// else 4 -- a decision in elements, identical for fp32 and bf16 storage.
+template <int KIND, typename T>
+void launch_chan_partial(const T* y, long ldy, const T* da, long ldda, long M, int C, const float* scale,
+                         const float* shift, const float* mean, int act, float* part, hipStream_t stream) {
+  const int nblk = chan_blocks(M);
+  const int rpb = seg_cdiv(M, nblk);
+  auto eoff8 = [](const T* p) { return ((uintptr_t)p / sizeof(T)) % 8 == 0; };
+  const bool v8 = C % 8 == 0 && ldy % 8 == 0 && (!da || ldda % 8 == 0) && eoff8(y) && (!da || eoff8(da));
+  if (v8) {
+    const dim3 grid(nblk, seg_cdiv(C / 8, kRedSlice));
+    hipLaunchKernelGGL((chan_partial_kernel<KIND, T, 8>), grid, dim3(kRedThreads), 0, stream, y, ldy, da, ldda,
+                       (int)M, C, scale, shift, mean, act, part, rpb);
+  } else {
+    const dim3 grid(nblk, seg_cdiv(C / 4, kRedSlice));
+    hipLaunchKernelGGL((chan_partial_kernel<KIND, T, 4>), grid, dim3(kRedThreads), 0, stream, y, ldy, da, ldda,
+                       (int)M, C, scale, shift, mean, act, part, rpb);
+  }
 }
 
-int chan_split(int C) {
-  const int CG = C >> 2;
-  return CG >= 64 ? seg_cdiv(CG, kChanSlice) : 1;
-}
-
-// Sum the per-block partials of channel c = blockIdx.x with the whole 256-thread
-// block (fp64, fixed thread->partial assignment and a fixed LDS tree:
-// deterministic).  The result is valid in thread 0.
-__device__ __forceinline__ void sum_partials(const float* __restrict__ part, int nblk, int C, int ldp, int c,
-                                             int t, double* s0, double* s1) {
-  __shared__ double ra[256], rb[256];
+// Sum the per-block partials (<= 256 rows: chan_blocks) of one channel with one wave:
+// lane l sums rows l, l+64, ... in fp64, then a fixed xor butterfly (fp64 adds are
+// commutative, so every lane ends with the same bits; deterministic).  Four channels
+// per 256-thread block: c = blockIdx.x * 4 + wave; returns false for c >= C.
+__device__ __forceinline__ bool sum_partials(const float* __restrict__ part, int nblk, int C, int ldp, int* cout,
+                                             double* s0, double* s1) {
+  const int lane = threadIdx.x & 63;
+  const int c = blockIdx.x * 4 + (threadIdx.x >> 6);
+  *cout = c;
+  if (c >= C) return false;
   double a = 0.0, b = 0.0;
-  for (int k = t; k < nblk; k += 256) {
+  for (int k = lane; k < nblk; k += 64) {
     a += part[(long)k * 2 * ldp + c];
     b += part[(long)k * 2 * ldp + ldp + c];
   }
-  ra[t] = a;
-  rb[t] = b;
-  __syncthreads();
-  for (int o = 128; o > 0; o >>= 1) {
-    if (t < o) {
-      ra[t] += ra[t + o];
-      rb[t] += rb[t + o];
-    }
-    __syncthreads();
+  for (int o = 32; o > 0; o >>= 1) {
+    a += __shfl_xor(a, o, 64);
+    b += __shfl_xor(b, o, 64);
   }
-  *s0 = ra[0];
-  *s1 = rb[0];
+  *s0 = a;
+  *s1 = b;
+  return lane == 0;
 }
 
 template <typename T>
@@ -150,11 +196,10 @@ __global__ __launch_bounds__(256) void bn_finalize_kernel(
     const float* __restrict__ gamma, const float* __restrict__ beta, float eps, float momentum,
     float* running_mean, float* running_var, long long* nbt, float* mean_out, float* invstd_out, float* scale_out,
     float* shift_out) {
-  const int c = blockIdx.x;
   if (blockIdx.x == 0 && threadIdx.x == 0 && nbt) *nbt += 1;
+  int c;
   double s, s2;
-  sum_partials(part, nblk, C, C, c, threadIdx.x, &s, &s2);
-  if (threadIdx.x != 0) return;
+  if (!sum_partials(part, nblk, C, C, &c, &s, &s2)) return;
   const double k = (float)y[c];
   const double dm = s / (double)M;
   const double mean = k + dm;
@@ -231,6 +276,51 @@ __global__ __launch_bounds__(256) void bn_finalize_tiles_kernel(
   }
 }
 
+// The same finalize for few tiles (ntiles <= 256: the small layers): one wave per
+// channel, 4 channels per block; each lane merges up to 4 tiles, then a fixed xor
+// butterfly of Chan merges over the 64 lanes (deterministic; no LDS, no barriers --
+// these launches were ~10 us of mostly block-wide fp64 tree synchronisation).
+__global__ __launch_bounds__(256) void bn_finalize_tiles_wave_kernel(
+    const float* __restrict__ part, int ntiles, int tile_rows, long M, int C, const float* __restrict__ gamma,
+    const float* __restrict__ beta, float eps, float momentum, float* running_mean, float* running_var,
+    long long* nbt, float* mean_out, float* invstd_out, float* scale_out, float* shift_out) {
+  const int lane = threadIdx.x & 63;
+  const int c = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (blockIdx.x == 0 && threadIdx.x == 0 && nbt) *nbt += 1;
+  if (c >= C) return;
+  double n = 0.0, mean = 0.0, m2 = 0.0;
+  for (int i = lane; i < ntiles; i += 64) {
+    const double nt = (double)std::min<long>(tile_rows, M - (long)i * tile_rows);
+    const double sm = part[(long)i * 2 * C + c], q = part[(long)i * 2 * C + C + c];
+    chan_merge(n, mean, m2, nt, sm / nt, q);
+  }
+  for (int o = 1; o < 64; o <<= 1) {
+    const double n2 = __shfl_xor(n, o, 64), mean2 = __shfl_xor(mean, o, 64), m22 = __shfl_xor(m2, o, 64);
+    // both partners merge (lower lane's set first) so every lane holds the same result
+    if (lane & o) {
+      double a = n2, b = mean2, d = m22;
+      chan_merge(a, b, d, n, mean, m2);
+      n = a; mean = b; m2 = d;
+    } else {
+      chan_merge(n, mean, m2, n2, mean2, m22);
+    }
+  }
+  if (lane != 0) return;
+  double var = m2 / (double)M;
+  if (var < 0.0) var = 0.0;
+  const float invstd = (float)(1.0 / sqrt(var + (double)eps));
+  mean_out[c] = (float)mean;
+  invstd_out[c] = invstd;
+  const float g = gamma ? gamma[c] : 1.f, bt = beta ? beta[c] : 0.f;
+  scale_out[c] = g * invstd;
+  shift_out[c] = bt - (float)mean * g * invstd;
+  if (running_mean) {
+    const double unbiased = M > 1 ? m2 / (double)(M - 1) : var;
+    running_mean[c] = (float)((1.0 - momentum) * running_mean[c] + momentum * mean);
+    running_var[c] = (float)((1.0 - momentum) * running_var[c] + momentum * unbiased);
+  }
+}
+
 __global__ void bn_eval_coef_kernel(const float* gamma, const float* beta, const float* rm, const float* rv, float eps,
                                     int C, float* scale_out, float* shift_out) {
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
@@ -260,10 +350,9 @@ __global__ void bn_apply_kernel(const T* __restrict__ y, long ldy, long M, int C
 __global__ void bn_bwd_finalize_kernel(const float* __restrict__ part, int nblk, long M, int C,
                                        const float* __restrict__ gamma, const float* __restrict__ invstd,
                                        float* dgamma, float* dbeta, float* coef) {
-  const int c = blockIdx.x;
+  int c;
   double sdz, sdzx;
-  sum_partials(part, nblk, C, C, c, threadIdx.x, &sdz, &sdzx);
-  if (threadIdx.x != 0) return;
+  if (!sum_partials(part, nblk, C, C, &c, &sdz, &sdzx)) return;
   const double inv = invstd[c];
   const double g = gamma ? gamma[c] : 1.0;
   if (dbeta) dbeta[c] = (float)sdz;
@@ -312,10 +401,9 @@ __global__ void bn_eval_bwd_kernel(const float* __restrict__ da, long ldda, cons
 
 __global__ void colsum_finalize_kernel(const float* __restrict__ part, int nblk, int C, int ldp, float* out,
                                        int accumulate) {
-  const int c = blockIdx.x;
+  int c;
   double s, unused;
-  sum_partials(part, nblk, C, ldp, c, threadIdx.x, &s, &unused);
-  if (threadIdx.x == 0) out[c] = accumulate ? out[c] + (float)s : (float)s;
+  if (sum_partials(part, nblk, C, ldp, &c, &s, &unused)) out[c] = accumulate ? out[c] + (float)s : (float)s;
 }
 
 int ew_grid(long total) { return (int)std::min<long>(seg_cdiv(total, 256), 8192); }
@@ -551,10 +639,7 @@ SEG_API int seg_add_bf16io(const __bf16* a, long lda, const __bf16* b, long ldb,
 }
 
 // Size (floats) of the partial-sum workspace the channel reductions below need.
-SEG_API long seg_chan_workspace_floats(long M, int C) {
-  const int rpb = rows_per_block_for(M, C);
-  return (long)seg_cdiv(M, rpb) * 2 * C;
-}
+SEG_API long seg_chan_workspace_floats(long M, int C) { return (long)chan_blocks(M) * 2 * C; }
 
 // Train-mode BN statistics: fills mean/invstd/scale/shift ([C] each) and updates
 // the running buffers (skipped when running_mean is null) and num_batches_tracked.
@@ -563,11 +648,9 @@ static int bn_stats_impl(const T* y, long ldy, long M, int C, const float* gamma
                          float momentum, float* running_mean, float* running_var, long long* num_batches_tracked,
                          float* work, float* mean, float* invstd, float* scale, float* shift, hipStream_t stream) {
   if ((C & 3) || (ldy & 3) || M < 1) return (int)hipErrorInvalidValue;
-  const int rpb = rows_per_block_for(M, C);
-  const int nblk = seg_cdiv(M, rpb);
-  hipLaunchKernelGGL((chan_partial_kernel<0, T>), dim3(nblk, chan_split(C)), dim3(256), 0, stream, y, ldy, (const T*)nullptr, 0L,
-                     (int)M, C, nullptr, nullptr, nullptr, 0, work, rpb);
-  hipLaunchKernelGGL(bn_finalize_kernel<T>, dim3(C), dim3(256), 0, stream, work, nblk, y, M, C, gamma,
+  const int nblk = chan_blocks(M);
+  launch_chan_partial<0, T>(y, ldy, nullptr, 0L, M, C, nullptr, nullptr, nullptr, 0, work, stream);
+  hipLaunchKernelGGL(bn_finalize_kernel<T>, dim3(seg_cdiv(C, 4)), dim3(256), 0, stream, work, nblk, y, M, C, gamma,
                      beta, eps, momentum, running_mean, running_var, num_batches_tracked, mean, invstd, scale, shift);
   SEG_RET_LAST();
 }
@@ -593,6 +676,12 @@ SEG_API int seg_bn_stats_tiles(const float* part, int ntiles, int tile_rows, lon
                                long long* num_batches_tracked, float* mean, float* invstd, float* scale, float* shift,
                                hipStream_t stream) {
   if (ntiles < 1 || tile_rows < 1 || M < 1) return (int)hipErrorInvalidValue;
+  if (ntiles <= 256) {
+    hipLaunchKernelGGL(bn_finalize_tiles_wave_kernel, dim3(seg_cdiv(C, 4)), dim3(256), 0, stream, part, ntiles,
+                       tile_rows, M, C, gamma, beta, eps, momentum, running_mean, running_var, num_batches_tracked,
+                       mean, invstd, scale, shift);
+    SEG_RET_LAST();
+  }
   hipLaunchKernelGGL(bn_finalize_tiles_kernel, dim3(C), dim3(256), 0, stream, part, ntiles,
                      tile_rows, M, C, gamma, beta, eps, momentum, running_mean, running_var, num_batches_tracked, mean,
                      invstd, scale, shift);
@@ -636,12 +725,11 @@ static int bn_backward_impl(const T* da, long ldda, const T* y, long ldy, long M
                             const float* mean, const float* invstd, const float* scale, const float* shift, int act,
                             float* dgamma, float* dbeta, float* work, T* dy, long lddy, hipStream_t stream) {
   if ((C & 3) || (ldy & 3) || (ldda & 3) || (lddy & 3)) return (int)hipErrorInvalidValue;
-  const int rpb = rows_per_block_for(M, C);
-  const int nblk = seg_cdiv(M, rpb);
+  if (M < 1) return (int)hipSuccess;
+  const int nblk = chan_blocks(M);
   float* coef = work + (long)nblk * 2 * C;
-  hipLaunchKernelGGL((chan_partial_kernel<1, T>), dim3(nblk, chan_split(C)), dim3(256), 0, stream, y, ldy, da, ldda, (int)M, C, scale,
-                     shift, mean, act, work, rpb);
-  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(C), dim3(256), 0, stream, work, nblk, M, C, gamma,
+  launch_chan_partial<1, T>(y, ldy, da, ldda, M, C, scale, shift, mean, act, work, stream);
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(seg_cdiv(C, 4)), dim3(256), 0, stream, work, nblk, M, C, gamma,
                      invstd, dgamma, dbeta, coef);
   launch_bn_bwd_apply<T>(da, ldda, y, ldy, M, C, scale, shift, mean, act, coef, dy, lddy, stream);
   SEG_RET_LAST();
@@ -674,11 +762,9 @@ static int colsum_impl(const T* y, long ldy, long M, int C, float* work, float* 
                        hipStream_t stream) {
   if ((ldy & 3)) return (int)hipErrorInvalidValue;
   const int C4 = (C + 3) & ~3;  // ld >= C4 is guaranteed by the buffer contract
-  const int rpb = rows_per_block_for(M, C4);  // the workspace is seg_chan_workspace_floats(M, C4)
-  const int nblk = seg_cdiv(M, rpb);
-  hipLaunchKernelGGL((chan_partial_kernel<2, T>), dim3(nblk, chan_split(C4)), dim3(256), 0, stream, y, ldy, (const T*)nullptr, 0L,
-                     (int)M, C4, nullptr, nullptr, nullptr, 0, work, rpb);
-  hipLaunchKernelGGL(colsum_finalize_kernel, dim3(C), dim3(256), 0, stream, work, nblk, C, C4, out,
+  const int nblk = chan_blocks(M);  // the workspace is seg_chan_workspace_floats(M, C4)
+  launch_chan_partial<2, T>(y, ldy, nullptr, 0L, M, C4, nullptr, nullptr, nullptr, 0, work, stream);
+  hipLaunchKernelGGL(colsum_finalize_kernel, dim3(seg_cdiv(C, 4)), dim3(256), 0, stream, work, nblk, C, C4, out,
                      accumulate);
   SEG_RET_LAST();
 }

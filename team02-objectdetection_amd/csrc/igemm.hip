@@ -114,18 +114,26 @@ struct SegPackJob {
   const float* w;
   float* wk;
   int cout, cin, ks, ldk, mode, kin_pad;
+  int blk0, nblk;  // this job's block range of the launch
 };
-static_assert(sizeof(SegPackJob) == 40, "seg_pack_job ABI");
+static_assert(sizeof(SegPackJob) == 48, "seg_pack_job ABI");
 
-__global__ __launch_bounds__(256) void pack_batch_kernel(const SegPackJob* __restrict__ jobs) {
-  const SegPackJob j = jobs[blockIdx.y];
+// One element per thread over a 1-D grid partitioned between the jobs by the host
+// (job.blk0 / job.nblk: blocks proportional to each job's size -- the big decoder
+// weights get thousands of blocks instead of the 64 a fixed per-job grid gave them).
+__global__ __launch_bounds__(256) void pack_batch_kernel(const SegPackJob* __restrict__ jobs, int njobs) {
+  int lo = 0, hi = njobs - 1;  // the job whose block range holds blockIdx.x
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (jobs[mid].blk0 <= (int)blockIdx.x) lo = mid; else hi = mid - 1;
+  }
+  const SegPackJob j = jobs[lo];
+  const long i = ((long)blockIdx.x - j.blk0) * 256 + threadIdx.x;
   const int taps = j.ks * j.ks;
   if (j.mode == 2) {
-    const int total = 9 * j.cout;
-    for (int i = blockIdx.x * 256 + threadIdx.x; i < total; i += gridDim.x * 256) {
-      const int tap = i / j.cout, c = i - tap * j.cout;
-      j.wk[i] = j.w[c * 9 + tap];
-    }
+    if (i >= 9L * j.cout) return;
+    const int tap = (int)(i / j.cout), c = (int)(i - (long)tap * j.cout);
+    j.wk[i] = j.w[c * 9 + tap];
     return;
   }
   if (j.mode == 3 || j.mode == 4) {
@@ -133,59 +141,54 @@ __global__ __launch_bounds__(256) void pack_batch_kernel(const SegPackJob* __res
     // mode 3 forward (rows = Cout, k = Cin), mode 4 data gradient (rows = Cin,
     // k = Cout, g = the transposed, flipped filter)
     const int rows = j.mode == 3 ? j.cout : j.cin;
-    const long total = (long)rows * j.ldk;
-    for (long i = blockIdx.x * 256L + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
-      const int r = (int)(i / j.ldk), k = (int)(i - (long)r * j.ldk);
-      const bool in = k < (j.mode == 3 ? j.cin : j.cout);
-      float g[3][3];
+    if (i >= (long)rows * j.ldk) return;
+    const int r = (int)(i / j.ldk), k = (int)(i - (long)r * j.ldk);
+    const bool in = k < (j.mode == 3 ? j.cin : j.cout);
+    float g[3][3];
 #pragma unroll
-      for (int y = 0; y < 3; ++y)
+    for (int y = 0; y < 3; ++y)
 #pragma unroll
-        for (int x = 0; x < 3; ++x)
-          g[y][x] = !in ? 0.f
-                        : j.mode == 3 ? j.w[(((long)r * j.cin + k) * 3 + y) * 3 + x]
-                                      : j.w[(((long)k * j.cin + r) * 3 + (2 - y)) * 3 + (2 - x)];
-      float h[4][3];  // G g
+      for (int x = 0; x < 3; ++x)
+        g[y][x] = !in ? 0.f
+                      : j.mode == 3 ? j.w[(((long)r * j.cin + k) * 3 + y) * 3 + x]
+                                    : j.w[(((long)k * j.cin + r) * 3 + (2 - y)) * 3 + (2 - x)];
+    float h[4][3];  // G g
 #pragma unroll
-      for (int x = 0; x < 3; ++x) {
-        h[0][x] = g[0][x];
-        h[1][x] = 0.5f * (g[0][x] + g[1][x] + g[2][x]);
-        h[2][x] = 0.5f * (g[0][x] - g[1][x] + g[2][x]);
-        h[3][x] = g[2][x];
-      }
-      const long plane = (long)rows * j.ldk;
+    for (int x = 0; x < 3; ++x) {
+      h[0][x] = g[0][x];
+      h[1][x] = 0.5f * (g[0][x] + g[1][x] + g[2][x]);
+      h[2][x] = 0.5f * (g[0][x] - g[1][x] + g[2][x]);
+      h[3][x] = g[2][x];
+    }
+    const long plane = (long)rows * j.ldk;
 #pragma unroll
-      for (int y = 0; y < 4; ++y) {  // (G g) G^T
-        const float u[4] = {h[y][0], 0.5f * (h[y][0] + h[y][1] + h[y][2]), 0.5f * (h[y][0] - h[y][1] + h[y][2]),
-                            h[y][2]};
+    for (int y = 0; y < 4; ++y) {  // (G g) G^T
+      const float u[4] = {h[y][0], 0.5f * (h[y][0] + h[y][1] + h[y][2]), 0.5f * (h[y][0] - h[y][1] + h[y][2]),
+                          h[y][2]};
 #pragma unroll
-        for (int x = 0; x < 4; ++x) j.wk[(y * 4 + x) * plane + i] = u[x];
-      }
+      for (int x = 0; x < 4; ++x) j.wk[(y * 4 + x) * plane + i] = u[x];
     }
     return;
   }
   const int rows = j.mode == 0 ? j.cout : j.cin;
-  const long total = (long)rows * j.ldk;
-  for (long i = blockIdx.x * 256L + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
-    const int r = (int)(i / j.ldk), k = (int)(i - (long)r * j.ldk);
-    float v = 0.f;
-    if (k < taps * j.kin_pad) {
-      const int tap = k / j.kin_pad, c = k - tap * j.kin_pad;
-      if (j.mode == 0) { if (c < j.cin) v = j.w[((long)r * j.cin + c) * taps + tap]; }
-      else if (c < j.cout) v = j.w[((long)c * j.cin + r) * taps + (taps - 1 - tap)];
-    }
-    j.wk[i] = v;
+  if (i >= (long)rows * j.ldk) return;
+  const int r = (int)(i / j.ldk), k = (int)(i - (long)r * j.ldk);
+  float v = 0.f;
+  if (k < taps * j.kin_pad) {
+    const int tap = k / j.kin_pad, c = k - tap * j.kin_pad;
+    if (j.mode == 0) { if (c < j.cin) v = j.w[((long)r * j.cin + c) * taps + tap]; }
+    else if (c < j.cout) v = j.w[((long)c * j.cin + r) * taps + (taps - 1 - tap)];
   }
+  j.wk[i] = v;
 }
 
-// jobs: device array of njobs seg_pack_job; max_elems = the largest job's element
-// count (sets the blocks per job).
-SEG_API int seg_pack_batch(const void* jobs, int njobs, long max_elems, hipStream_t stream) {
-  if (njobs < 0 || max_elems < 0) return (int)hipErrorInvalidValue;
-  if (njobs == 0) return 0;
-  const int bx = (int)std::max<long>(1, std::min<long>(seg_cdiv(max_elems, 256), 64));
-  hipLaunchKernelGGL(pack_batch_kernel, dim3(bx, njobs), dim3(256), 0, stream,
-                     reinterpret_cast<const SegPackJob*>(jobs));
+// jobs: device array of njobs seg_pack_job, sorted by blk0, job k owning blocks
+// [blk0, blk0 + nblk) with nblk = ceil(elements / 256); nblocks = the sum.
+SEG_API int seg_pack_batch(const void* jobs, int njobs, long nblocks, hipStream_t stream) {
+  if (njobs < 0 || nblocks < 0 || nblocks > INT32_MAX) return (int)hipErrorInvalidValue;
+  if (njobs == 0 || nblocks == 0) return 0;
+  hipLaunchKernelGGL(pack_batch_kernel, dim3((unsigned)nblocks), dim3(256), 0, stream,
+                     reinterpret_cast<const SegPackJob*>(jobs), njobs);
   SEG_RET_LAST();
 }
 

@@ -95,8 +95,14 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void igemm_conv_kernel(
   static_assert(!LP || BK % 16 == 0, "16-bit MFMA steps are 16 deep");
   static_assert(sizeof(lds_t) * BM * LDSR >= 4 * (BM / WM + 1) * BN, "BN-statistics scratch fits in As");
 
-  __shared__ __attribute__((aligned(16))) lds_t As[SEG_IGEMM_STAGES][BM * LDSR];
-  __shared__ __attribute__((aligned(16))) lds_t Bs[SEG_IGEMM_STAGES][BN * LDSR];
+  // One LDS arena: the K loop's operand tiles, then (reused) the BN-statistics scratch and
+  // the staged epilogue's band of WM output rows [WM][CSR] fp32.
+  constexpr int CSR = BN + 4;
+  constexpr int AB_BYTES = SEG_IGEMM_STAGES * (BM + BN) * LDSR * (int)sizeof(lds_t);
+  constexpr int C_BYTES = WM * CSR * 4;
+  __shared__ __attribute__((aligned(16))) char smem[AB_BYTES > C_BYTES ? AB_BYTES : C_BYTES];
+  lds_t (*As)[BM * LDSR] = reinterpret_cast<lds_t (*)[BM * LDSR]>(smem);
+  lds_t (*Bs)[BN * LDSR] = reinterpret_cast<lds_t (*)[BN * LDSR]>(smem + SEG_IGEMM_STAGES * BM * LDSR * sizeof(lds_t));
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm0 = (wave / WAVES_N) * WM, wn0 = (wave % WAVES_N) * WN;
@@ -441,20 +447,78 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void igemm_conv_kernel(
       __syncthreads();
     }
   }
+  // Staged store: the C layout gives each lane one column of 16 rows, so direct stores
+  // write 2 x 32 consecutive elements per instruction (64 B rows on bf16 storage --
+  // the output-heavy 1x1 expand convs ran at 25-50 % of a copy).  Instead, per band of
+  // WM rows, the waves owning it write their accumulators (+ bias) to LDS, then every
+  // thread writes 16-byte row-contiguous vectors (4 fp32 / 8 bf16 channels) with the
+  // addend and activation applied in fp32 -- the same value per element as before.
+  {
+    float* Cs = reinterpret_cast<float*>(smem);
+    constexpr int VO = 16 / (int)sizeof(IT);  // output elements per 16-byte store
+    constexpr int VPR = BN / VO;              // vectors per band row
+    static_assert(BN % VO == 0, "whole vectors per tile row");
 #pragma unroll
-  for (int ni = 0; ni < NI; ++ni) {
-    const int col = n0 + wn0 + ni * 32 + lrow;
-    if (col >= a.Cout) continue;
+    for (int b = 0; b < BM / WM; ++b) {
+      __syncthreads();  // the K loop / statistics / previous band are done with smem
+      if (wm0 == b * WM) {
 #pragma unroll
-    for (int mi = 0; mi < MI; ++mi) {
+        for (int ni = 0; ni < NI; ++ni)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int row = m0 + wm0 + mi * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-        if (row < a.M) {
-          float v = acc[mi][ni][r];
-          if (add) v += (float)add[(long)row * a.ldadd + col];
-          if (a.act) v = seg_act(v, a.act);
-          out[(long)row * a.ldout + col] = static_cast<IT>(v);
+          for (int mi = 0; mi < MI; ++mi)
+#pragma unroll
+            for (int r = 0; r < 16; ++r)
+              Cs[(mi * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5)) * CSR + wn0 + ni * 32 + lrow] = acc[mi][ni][r];
+      }
+      __syncthreads();
+      for (int v = tid; v < WM * VPR; v += NT) {
+        const int rr = v / VPR, cv = (v - rr * VPR) * VO;
+        const int row = m0 + b * WM + rr, col = n0 + cv;
+        if (row >= a.M || col >= a.Cout) continue;
+        float o[VO];
+#pragma unroll
+        for (int j = 0; j < VO; j += 4) {
+          const f32x4 q = *reinterpret_cast<const f32x4*>(&Cs[rr * CSR + cv + j]);
+          o[j] = q[0]; o[j + 1] = q[1]; o[j + 2] = q[2]; o[j + 3] = q[3];
+        }
+        IT* dst = out + (long)row * a.ldout + col;
+        const IT* ad = add ? add + (long)row * a.ldadd + col : nullptr;
+        const bool vec = col + VO <= a.Cout && ((uintptr_t)dst & 15) == 0 && (!ad || ((uintptr_t)ad & 15) == 0);
+        if (vec) {
+          if (ad) {
+            if constexpr (VO == 8) {
+              f32x4 lo, hi;
+              const bf16x8 q = *reinterpret_cast<const bf16x8*>(ad);
+              lo = __builtin_convertvector(__builtin_shufflevector(q, q, 0, 1, 2, 3), f32x4);
+              hi = __builtin_convertvector(__builtin_shufflevector(q, q, 4, 5, 6, 7), f32x4);
+#pragma unroll
+              for (int j = 0; j < 4; ++j) { o[j] += lo[j]; o[4 + j] += hi[j]; }
+            } else {
+              const f32x4 q = ld4(reinterpret_cast<const float*>(ad));
+#pragma unroll
+              for (int j = 0; j < 4; ++j) o[j] += q[j];
+            }
+          }
+          if (a.act) {
+#pragma unroll
+            for (int j = 0; j < VO; ++j) o[j] = seg_act(o[j], a.act);
+          }
+          if constexpr (VO == 8) {
+            const f32x4 lo = {o[0], o[1], o[2], o[3]}, hi = {o[4], o[5], o[6], o[7]};
+            *reinterpret_cast<bf16x8*>(dst) =
+                seg_cat8(__builtin_convertvector(lo, bf16x4), __builtin_convertvector(hi, bf16x4));
+          } else {
+            *reinterpret_cast<f32x4*>(dst) = f32x4{o[0], o[1], o[2], o[3]};
+          }
+        } else {
+#pragma unroll
+          for (int j = 0; j < VO; ++j) {
+            if (col + j >= a.Cout) break;
+            float x = o[j];
+            if (ad) x += (float)ad[j];
+            if (a.act) x = seg_act(x, a.act);
+            dst[j] = static_cast<IT>(x);
+          }
         }
       }
     }

@@ -482,16 +482,13 @@ class Program:
         if getattr(self, "_pack_key", None) != key:
             self._build_pack(convs, key)
         if self._njobs:
-            rt.call("seg_pack_batch", self._jobs.data_ptr(), self._njobs, self._max_elems, rt.stream)
+            rt.call("seg_pack_batch", self._jobs.data_ptr(), self._njobs, self._pack_blocks, rt.stream)
 
     def _build_pack(self, convs, key):
         import numpy as np
         if self.math == "f16":
             raise NotImplementedError("f16 conv math is the inference configuration (Predictor(model, math='f16')); "
                                       "train with 'f32' or 'bf16'")
-        jt = np.dtype([("w", "<u8"), ("wk", "<u8"), ("cout", "<i4"), ("cin", "<i4"), ("ks", "<i4"),
-                       ("ldk", "<i4"), ("mode", "<i4"), ("kin", "<i4")])
-        assert jt.itemsize == 40
         jobs, max_elems = [], 0
         for op in convs:
             w = op.conv.weight
@@ -553,9 +550,8 @@ class Program:
                 op.wk_d = torch.empty(op.cin * op.ldk_d, device=dev, dtype=torch.float32)
                 jobs.append((w.data_ptr(), op.wk_d.data_ptr(), op.cout, op.cin, op.ks, op.ldk_d, 1, kin))
                 max_elems = max(max_elems, op.cin * op.ldk_d)
-        table = np.array(jobs, dtype=jt)
-        self._jobs = torch.from_numpy(table.view(np.uint8).copy()).to(convs[0].conv.weight.device)
-        self._njobs, self._max_elems, self._pack_key = len(jobs), max_elems, key
+        self._jobs, self._njobs, self._pack_blocks = pack_table(jobs, convs[0].conv.weight.device)
+        self._pack_key = key
 
     def fold(self, stream):
         """Eval: fold every BatchNorm into its conv (one seg_bn_fold_batch launch) and
@@ -576,8 +572,6 @@ class Program:
                        ("rv", "<u8"), ("w_out", "<u8"), ("b_out", "<u8"), ("cout", "<i4"), ("kper", "<i4"),
                        ("eps", "<f4"), ("pad", "<i4")])
         assert ft.itemsize == 80
-        pt = np.dtype([("w", "<u8"), ("wk", "<u8"), ("cout", "<i4"), ("cin", "<i4"), ("ks", "<i4"),
-                       ("ldk", "<i4"), ("mode", "<i4"), ("kin", "<i4")])
         fjobs, pjobs, fmax, pmax = [], [], 0, 0
         for op in convs:
             w, b, bn = op.conv.weight, op.conv.bias, op.bn
@@ -611,10 +605,10 @@ class Program:
         self._fjobs = torch.from_numpy(np.array(fjobs, dtype=ft).view(np.uint8).copy()).to(dev)
         self._fmax = fmax
         if pjobs:
-            self._fpjobs = torch.from_numpy(np.array(pjobs, dtype=pt).view(np.uint8).copy()).to(dev)
+            self._fpjobs, self._fpn, self._fpmax = pack_table(pjobs, dev)
         else:
-            self._fpjobs = None
-        self._fpn, self._fpmax, self._fold_key = len(pjobs), pmax, key
+            self._fpjobs, self._fpn, self._fpmax = None, 0, 0
+        self._fold_key = key
 
     def params(self):
         seen, ps = set(), []
@@ -624,6 +618,26 @@ class Program:
                     seen.add(id(p))
                     ps.append(p)
         return ps
+
+
+_PACK_JOB = [("w", "<u8"), ("wk", "<u8"), ("cout", "<i4"), ("cin", "<i4"), ("ks", "<i4"), ("ldk", "<i4"),
+             ("mode", "<i4"), ("kin", "<i4"), ("blk0", "<i4"), ("nblk", "<i4")]
+
+
+def pack_table(jobs, device):
+    """Device table of seg_pack_job for seg_pack_batch from (w, wk, cout, cin, ks, ldk, mode,
+    kin_pad) tuples: each job gets ceil(elements / 256) blocks of the launch.
+    Returns (table, njobs, total blocks)."""
+    import numpy as np
+    rows, blk = [], 0
+    for (w, wk, cout, cin, ks, ldk, mode, kin) in jobs:
+        elems = 9 * cout if mode == 2 else (cout if mode in (0, 3) else cin) * ldk
+        nblk = max(1, (elems + 255) // 256)
+        rows.append((w, wk, cout, cin, ks, ldk, mode, kin, blk, nblk))
+        blk += nblk
+    t = np.array(rows, dtype=np.dtype(_PACK_JOB))
+    assert t.dtype.itemsize == 48
+    return torch.from_numpy(t.view(np.uint8).copy()).to(device), len(rows), blk
 
 
 def _cna(prog, m: ConvBNReLU6, inp, out=None, kind=None, xform=None):
@@ -995,7 +1009,9 @@ class Run:
         x, img = self.image, self.prog.image
         self.prog.pack(self)
         self.call(self.k("seg_nchw_to_nhwc"), x.data_ptr(), img.N, 3, img.H, img.W, self.ptr(img), img.ld, self.stream)
-        for op in self.prog.ops:
+        for k, op in enumerate(self.prog.ops):
+            if self.rec is not None:
+                self.rec.label = f"{k}:fwd"
             op.forward(self)
         if DEBUG_KEEP_RUN:
             LAST_RUN = self
@@ -1016,8 +1032,10 @@ class Run:
             self.side = _side_stream(self.device)
             self._side_ctx = torch.cuda.StreamContext(self.side)  # re-entered by every fork
         try:
-            for op in reversed(self.prog.ops):
-                op.backward(self)
+            for k in range(len(self.prog.ops) - 1, -1, -1):
+                if self.rec is not None:
+                    self.rec.label = f"{k}:bwd"
+                self.prog.ops[k].backward(self)
         finally:
             self.join()
         if DEBUG_KEEP_RUN:

@@ -54,7 +54,8 @@ class Recorder:
         self.streams = dict(streams)
         self.entries = []      # (kind, fn, stream, arg offset)
         self.args = []
-        self.timers = []       # (entry index, kind tag, flops)
+        self.timers = []       # (entry index, kind tag, flops, op label, entry point) of every launch
+        self.label = ""        # the program op being recorded (diagnostics)
         self.callbacks = []
         self.externals = {}    # pointer value -> name
         self.ext_slots = {}    # name -> [arg slot]
@@ -88,8 +89,8 @@ class Recorder:
             else:
                 self.args.append(int(v) & _U64)  # two's complement slot; the trampoline casts back
         self.entries.append((CALL, fn, self._stream(args[-1]), off))
-        if timer is not None:
-            self.timers.append((len(self.entries) - 1, timer[0], timer[1]))
+        kind, flops = timer if timer is not None else (name, 0)
+        self.timers.append((len(self.entries) - 1, kind, flops, self.label, name))
 
     def event(self):
         self.n_events += 1
@@ -175,8 +176,9 @@ class Tape:
         self._timed = sel if len(idx) else None
         self._replays = replays
 
-    def elapsed(self):
-        """[(kind, flops, seconds)] of every timed launch of the replays so far (after a sync)."""
+    def elapsed(self, detail=False):
+        """[(kind, flops, seconds)] of every timed launch of the replays so far (after a
+        sync); detail: [(replay, op label, entry point, kind, flops, seconds)]."""
         if not self._timed:
             return []
         n = len(self._timed)
@@ -186,6 +188,7 @@ class Tape:
             raise _lib.SegLibError(f"seg_tape_elapsed failed: {-done}")
         res = []
         for r in range(done):
-            for k, (_, kind, flops) in enumerate(self._timed):
-                res.append((kind, flops, float(out[r * n + k]) * 1e-3))
+            for k, (_, kind, flops, label, name) in enumerate(self._timed):
+                sec = float(out[r * n + k]) * 1e-3
+                res.append((r, label, name, kind, flops, sec) if detail else (kind, flops, sec))
         return res

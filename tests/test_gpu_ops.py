@@ -449,12 +449,10 @@ def test_dw_bias_act_and_bn_fold(stride):
 def _pack_wino(w, mode, rows, ldk):
     import numpy as np
     Cout, Cin = w.shape[0], w.shape[1]
-    pt = np.dtype([("w", "<u8"), ("wk", "<u8"), ("cout", "<i4"), ("cin", "<i4"), ("ks", "<i4"), ("ldk", "<i4"),
-                   ("mode", "<i4"), ("kin", "<i4")])
+    from seg_amd.engine import pack_table
     wk = torch.full((16 * rows * ldk,), float("nan"), device=DEV)
-    job = np.array([(w.data_ptr(), wk.data_ptr(), Cout, Cin, 3, ldk, mode, ldk)], dtype=pt)
-    jobs = torch.from_numpy(job.view(np.uint8).copy()).to(DEV)
-    call("seg_pack_batch", jobs.data_ptr(), 1, rows * ldk, S())
+    jobs, nj, nb = pack_table([(w.data_ptr(), wk.data_ptr(), Cout, Cin, 3, ldk, mode, ldk)], DEV)
+    call("seg_pack_batch", jobs.data_ptr(), nj, nb, S())
     return wk
 
 

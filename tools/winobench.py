@@ -41,13 +41,11 @@ def timeit(fn, reps=10):
 
 
 def pack(w, mode, rows, ldk, kin):
-    pt = np.dtype([("w", "<u8"), ("wk", "<u8"), ("cout", "<i4"), ("cin", "<i4"), ("ks", "<i4"), ("ldk", "<i4"),
-                   ("mode", "<i4"), ("kin", "<i4")])
+    from seg_amd.engine import pack_table
     n = (16 if mode >= 3 else 1) * rows * ldk
     wk = torch.empty(n, device="cuda")
-    job = np.array([(w.data_ptr(), wk.data_ptr(), w.shape[0], w.shape[1], 3, ldk, mode, kin)], dtype=pt)
-    jobs = torch.from_numpy(job.view(np.uint8).copy()).cuda()
-    call("seg_pack_batch", jobs.data_ptr(), 1, rows * ldk, torch.cuda.current_stream().cuda_stream)
+    jobs, nj, nb = pack_table([(w.data_ptr(), wk.data_ptr(), w.shape[0], w.shape[1], 3, ldk, mode, kin)], "cuda")
+    call("seg_pack_batch", jobs.data_ptr(), nj, nb, torch.cuda.current_stream().cuda_stream)
     torch.cuda.synchronize()
     return wk
 

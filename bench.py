@@ -62,6 +62,9 @@ def parse():
                          "(default), f32, bf16")
     ap.add_argument("--optimizer", choices=("seg", "torch"), default="seg",
                     help="seg: seg_amd.Adam (one-launch HIP step, csrc/adam.hip); torch: torch.optim.Adam (foreach)")
+    ap.add_argument("--dist-backend", choices=("nccl", "gloo"), default="nccl",
+                    help="nccl = RCCL over xGMI (the measurement); gloo = rehearsal of the N-rank path on fewer GPUs "
+                         "(ranks share devices round-robin; not a throughput figure)")
     ap.add_argument("--model", choices=("MobileNetV2UNet", "UNet"), default="MobileNetV2UNet",
                     help="UNet = BASELINE configs[4] shape family (use --height 512 --width 1024 --batch 8)")
     return ap.parse_args()
@@ -214,8 +217,10 @@ def main():
     check_world(world, args.gpus)
     dist = world > 1
     if dist:
-        torch.distributed.init_process_group("nccl")
+        torch.distributed.init_process_group(args.dist_backend)
         assert torch.distributed.get_world_size() == args.gpus
+    if args.dist_backend == "gloo":
+        local = local % torch.cuda.device_count()
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
 
@@ -417,6 +422,8 @@ def main():
                                        f"{args.height}x{args.width}, bs={args.batch}/GPU ({cfg})",
                            "model": args.model, "global_batch": args.batch * world,
                            "image": [args.height, args.width], "parallelism": f"dp{world}",
+                           "collectives": "RCCL (torch.distributed nccl)" if args.dist_backend == "nccl" else
+                                          "gloo REHEARSAL (ranks share GPUs; not a throughput figure)",
                            "optimizer": {"seg": "seg_amd.Adam (HIP, one launch)", "torch": "torch.optim.Adam (foreach)"}[args.optimizer]},
                 "final_loss": round(final_loss, 5),
                 "math": {"f32": "fp32 everywhere",

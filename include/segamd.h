@@ -104,6 +104,35 @@ int seg_conv_wgrad_bf16(const float* dy, long lddy, const float* x, long ldx,
                         int N, int H, int W, int Cin, int Ho, int Wo, int Cout,
                         int ks, int stride, int pad, float* part, int splits, hipStream_t stream);
 
+/* Lazy BatchNorm of a 1x1 conv's input (training): the input is the RAW output of a
+ * BatchNorm'd producer (a depthwise conv of an inverted residual, torchvision
+ * mobilenetv2.py InvertedResidual; the first conv of src/unet.py:113-115's OutConv),
+ * and x = act(in * in_scale[c] + in_shift[c]) -- the per-channel BN coefficients of
+ * seg_bn_finalize, act SEG_ACT_* -- is formed while the operand is staged in LDS
+ * instead of by a separate seg_bn_apply pass.  Bitwise the same as seg_bn_apply
+ * followed by the plain conv (bf16 storage: the transformed value is rounded to bf16
+ * as seg_bn_apply_bf16io would store it).  ks must be 1; no split-K. */
+int seg_conv_igemm_xf(const float* in, long ldin, int N, int H, int W, int Cin,
+                      const float* wk, int ldk, const float* bias,
+                      float* out, long ldout, int Ho, int Wo, int Cout,
+                      int ks, int stride, int pad,
+                      const float* add, long ldadd, float* stat, const float* in_scale, const float* in_shift,
+                      int in_act, hipStream_t stream);
+int seg_conv_igemm_bf16_xf(const float* in, long ldin, int N, int H, int W, int Cin,
+                           const float* wk, int ldk, const float* bias,
+                           float* out, long ldout, int Ho, int Wo, int Cout,
+                           int ks, int stride, int pad,
+                           const float* add, long ldadd, float* stat, const float* in_scale, const float* in_shift,
+                           int in_act, hipStream_t stream);
+int seg_conv_wgrad_xf(const float* dy, long lddy, const float* x, long ldx,
+                      int N, int H, int W, int Cin, int Ho, int Wo, int Cout,
+                      int ks, int stride, int pad, float* part, int splits,
+                      const float* in_scale, const float* in_shift, int in_act, hipStream_t stream);
+int seg_conv_wgrad_bf16_xf(const float* dy, long lddy, const float* x, long ldx,
+                           int N, int H, int W, int Cin, int Ho, int Wo, int Cout,
+                           int ks, int stride, int pad, float* part, int splits,
+                           const float* in_scale, const float* in_shift, int in_act, hipStream_t stream);
+
 /* dW (PyTorch layout) = fixed-order sum of partial slabs.  mode 0: igemm
  * partials (K runs of round_up(Cin,4) channels), 1: depthwise partials. */
 int seg_conv_wgrad_reduce(const float* part, int splits, float* dw, int Cout, int Cin, int ks,
@@ -347,6 +376,14 @@ int seg_conv_halo_bf16io(const seg_bf16* in, long ldin, int N, int H, int W, int
     hipStream_t stream);
 int seg_conv_wgrad_bf16io(const seg_bf16* dy, long lddy, const seg_bf16* x, long ldx, int N, int H, int W, int Cin,
     int Ho, int Wo, int Cout, int ks, int stride, int pad, float* part, int splits, hipStream_t stream);
+/* bf16-storage twins of seg_conv_igemm_xf / seg_conv_wgrad_xf. */
+int seg_conv_igemm_bf16io_xf(const seg_bf16* in, long ldin, int N, int H, int W, int Cin, const float* wk, int ldk,
+    const float* bias, seg_bf16* out, long ldout, int Ho, int Wo, int Cout, int ks, int stride, int pad,
+    const seg_bf16* add, long ldadd, float* stat, const float* in_scale, const float* in_shift, int in_act,
+    hipStream_t stream);
+int seg_conv_wgrad_bf16io_xf(const seg_bf16* dy, long lddy, const seg_bf16* x, long ldx, int N, int H, int W,
+    int Cin, int Ho, int Wo, int Cout, int ks, int stride, int pad, float* part, int splits, const float* in_scale,
+    const float* in_shift, int in_act, hipStream_t stream);
 
 /* ---- Adam (optim.Adam(model.parameters(), lr=1.5e-4), main.py:100; step at
  *      src/train.py:39): one launch over every parameter with a gradient, the

@@ -34,7 +34,13 @@ namespace {
 constexpr int kRedThreads = 512;
 constexpr int kRedSlice = 64;  // channel groups per block (blockIdx.y slices beyond)
 
-int chan_blocks(long M) { return (int)std::max<long>(1, std::min<long>(256, M / 64)); }
+#ifndef SEG_CHAN_MAXBLK
+#define SEG_CHAN_MAXBLK 256
+#endif
+#ifndef SEG_APPLY_ROWS4
+#define SEG_APPLY_ROWS4 0
+#endif
+int chan_blocks(long M) { return (int)std::max<long>(1, std::min<long>(SEG_CHAN_MAXBLK, M / 64)); }
 
 template <int VW, typename T>
 __device__ __forceinline__ void ldw(const T* p, f32x4 (&o)[VW / 4]) {
@@ -537,6 +543,20 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_rt_kernel(const T* __restric
     ldc<NV>(coef + C + c, k2);
     ldc<NV>(coef + 2 * C + c, k3);
     long r = (long)blockIdx.x * rt.RG + rt.rg;
+    for (; SEG_APPLY_ROWS4 && r + 3 * step < M; r += 4 * step) {  // four rows' loads in flight together
+      f32x4 v[4][NV], g[4][NV];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        ldv<VW>(y + (r + q * step) * ldy + c, v[q]);
+        ldv<VW>(da + (r + q * step) * ldda + c, g[q]);
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+#pragma unroll
+        for (int j = 0; j < NV; ++j) v[q][j] = seg_bnbwd4(g[q][j], v[q][j], sc[j], sh[j], mu[j], k1[j], k2[j], k3[j], act);
+        stv<VW>(dy + (r + q * step) * lddy + c, v[q]);
+      }
+    }
     for (; r + step < M; r += 2 * step) {
       f32x4 v0[NV], v1[NV], g0[NV], g1[NV];
       ldv<VW>(y + r * ldy + c, v0);

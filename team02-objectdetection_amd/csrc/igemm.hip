@@ -36,6 +36,22 @@ SEG_API int seg_conv_igemm_act(const float* in, long ldin, int N, int H, int W, 
                                 add, ldadd, stat, act, work, splits, stream);
 }
 
+// seg_conv_igemm of a 1x1 conv whose input is the raw output of a BatchNorm'd producer
+// ("lazy BN": the depthwise conv of torchvision's InvertedResidual feeding the project
+// conv, outconv's first conv feeding its second, src/unet.py:113-116): the A operand is
+// act(in * in_scale[c] + in_shift[c]) formed on load, so the producer's BN-apply pass
+// and its output tensor disappear.  ks must be 1.
+SEG_API int seg_conv_igemm_xf(const float* in, long ldin, int N, int H, int W, int Cin,
+                              const float* wk, int ldk, const float* bias,
+                              float* out, long ldout, int Ho, int Wo, int Cout,
+                              int ks, int stride, int pad,
+                              const float* add, long ldadd, float* stat, const float* in_scale, const float* in_shift,
+                              int in_act, hipStream_t stream) {
+  if (!in_scale) return (int)hipErrorInvalidValue;
+  return conv_igemm_impl<float>(in, ldin, N, H, W, Cin, wk, ldk, bias, out, ldout, Ho, Wo, Cout, ks, stride, pad,
+                                add, ldadd, stat, SEG_ACT_NONE, nullptr, 1, stream, in_scale, in_shift, in_act);
+}
+
 SEG_API int seg_conv_igemm(const float* in, long ldin, int N, int H, int W, int Cin,
                            const float* wk, int ldk, const float* bias,
                            float* out, long ldout, int Ho, int Wo, int Cout,

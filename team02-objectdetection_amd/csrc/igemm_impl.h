@@ -33,6 +33,11 @@ struct IgemmArgs {
   int kchunk;                    // split-K: K range of blockIdx.y (a multiple of BK); == K when unsplit
   float* part;                   // split-K: raw partial sums [gridDim.y][M][Cout] (no epilogue), else null
   int act;                       // epilogue activation of act(acc + bias + add) (SegAct); 0 in training
+  // optional input transform ("lazy BN", 1x1 uniform-tap path): the A operand is
+  // act(in * xs[c] + xb[c]) per input channel c -- the producer's BatchNorm + activation
+  // applied on load instead of by a separate pass (seg_bn_act4: the same fp32 value the
+  // pass would have stored, rounded to the storage type only where the pass would have)
+  const float* xs; const float* xb; int xact;
 };
 
 #ifndef SEG_IGEMM_DEPTH
@@ -151,6 +156,11 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void igemm_conv_kernel(
   bool u_bok[B_PER];
   const int u_kq4 = (tid % KQ) * 4;
   const int u_kqa = (tid % KQA) * VA;  // this thread's A channel offset in a K chunk
+  // input transform: the loaded chunk's channel for this thread's A slots (-1: beyond K)
+  // and its coefficients, fetched with the chunk so store_tiles does not wait on them
+  const bool XF = a.xs != nullptr;
+  int xch = -1;
+  f32x4 xsc[VA / 4], xsh[VA / 4];
   int u_tap = 0, u_ci = 0;
   long u_toff0 = 0, u_toff1 = 0;
   auto tap_off = [&](int t) -> long { return ((long)(t / KS) * a.W + t % KS) * a.ldin; };
@@ -202,6 +212,15 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void igemm_conv_kernel(
       const bool wrap = ci >= a.Cin;
       const int tap = u_tap + (wrap ? 1 : 0);
       const long off = (wrap ? u_toff1 : u_toff0) + (wrap ? ci - a.Cin : ci);
+      if (KS == 1 && XF) {  // 1x1: the chunk's channels are ci .. ci + VA - 1 (no taps)
+        xch = wrap ? -1 : ci;
+        const int cc = wrap ? 0 : ci;
+#pragma unroll
+        for (int j = 0; j < VA / 4; ++j) {
+          xsc[j] = ld4(a.xs + cc + 4 * j);
+          xsh[j] = ld4(a.xb + cc + 4 * j);
+        }
+      }
 #pragma unroll
       for (int i = 0; i < A_PER; ++i) {
         const bool ok = (u_mask[i] >> tap) & 1u;
@@ -265,7 +284,23 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void igemm_conv_kernel(
     for (int i = 0; i < A_PER; ++i) {
       const int idx = tid + i * NT;
       if (A_VEC % NT == 0 || idx < A_VEC) {
-        const f32x4 v = ra[i];
+        f32x4 v = ra[i];
+        if (KS == 1 && XF && xch >= 0) {
+          if constexpr (VA == 8) {  // 8 bf16: widen, transform, round back (RNE) as the pass would
+            const bf16x8 q = __builtin_bit_cast(bf16x8, v);
+            const f32x4 lo = seg_bn_act4(__builtin_convertvector(__builtin_shufflevector(q, q, 0, 1, 2, 3), f32x4),
+                                         xsc[0], xsh[0], a.xact);
+            const f32x4 hi = seg_bn_act4(__builtin_convertvector(__builtin_shufflevector(q, q, 4, 5, 6, 7), f32x4),
+                                         xsc[VA / 4 - 1], xsh[VA / 4 - 1], a.xact);
+            v = __builtin_bit_cast(f32x4, seg_cat8(__builtin_convertvector(lo, bf16x4),
+                                                   __builtin_convertvector(hi, bf16x4)));
+          } else {
+            v = seg_bn_act4(v, xsc[0], xsh[0], a.xact);
+            if constexpr (sizeof(IT) == 2) {  // 4 bf16 channels widened by ld4: round as stored
+              v = __builtin_convertvector(__builtin_convertvector(v, bf16x4), f32x4);
+            }
+          }
+        }
         if constexpr (VA == 8)
           *reinterpret_cast<f32x4*>(&As[buf][(idx / KQA) * LDSR + (idx % KQA) * 8]) = v;
         else
@@ -532,6 +567,7 @@ int launch_igemm_bk(const IgemmArgs& a, int ks, hipStream_t s) {
   const bool ut = SEG_IGEMM_UT && (SEG_IGEMM_UT2 ? a.Cin >= BK : a.Cin % BK == 0) &&
                   (sizeof(IT) == 4 || (a.Cin % 8 == 0 && a.ldin % 8 == 0));  // bf16 A: 16-byte slots
   constexpr int NT = 64 * (BM / WM) * (BN / WN);
+  if (a.xs && (!ut || ks != 1)) return (int)hipErrorInvalidValue;  // input transform: 1x1 uniform-tap loader only
 #define SEG_IG(KS, U) hipLaunchKernelGGL((igemm_conv_kernel<BM, BN, WM, WN, KS, BK, U, OT, IT>), dim3(grid, splits), dim3(NT), 0, s, a)
   if (ks == 1) {
     if (ut) SEG_IG(1, true); else SEG_IG(1, false);
@@ -638,9 +674,12 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restr
 template <typename OT, typename IT = float>
 int conv_igemm_impl(const IT* in, long ldin, int N, int H, int W, int Cin, const float* wk, int ldk,
                     const float* bias, IT* out, long ldout, int Ho, int Wo, int Cout, int ks, int stride, int pad,
-                    const IT* add, long ldadd, float* stat, int act, float* work, int splits, hipStream_t stream) {
+                    const IT* add, long ldadd, float* stat, int act, float* work, int splits, hipStream_t stream,
+                    const float* xs = nullptr, const float* xb = nullptr, int xact = 0) {
   if (!std::is_same<IT, float>::value && splits != 1) return (int)hipErrorInvalidValue;
   if ((Cin & 3) || (ldin & 3) || (ldk & 3) || (ks != 1 && ks != 3)) return (int)hipErrorInvalidValue;
+  if (xs && (!xb || ks != 1 || splits != 1 || SEG_IGEMM_STAGES != 1 || xact < SEG_ACT_NONE || xact > SEG_ACT_RELU6))
+    return (int)hipErrorInvalidValue;
   if (ks == 1 && (stride != 1 || pad != 0 || Ho != H || Wo != W)) return (int)hipErrorInvalidValue;
   if (act < SEG_ACT_NONE || act > SEG_ACT_RELU6 || (act && stat)) return (int)hipErrorInvalidValue;
   if (splits < 1 || (splits > 1 && (!work || stat))) return (int)hipErrorInvalidValue;
@@ -650,6 +689,7 @@ int conv_igemm_impl(const IT* in, long ldin, int N, int H, int W, int Cin, const
   a.N = N; a.H = H; a.W = W; a.Cin = Cin; a.Ho = Ho; a.Wo = Wo; a.Cout = Cout;
   a.stride = stride; a.pad = pad; a.K = ks * ks * Cin; a.M = N * Ho * Wo; a.act = act;
   a.part = splits > 1 ? work : nullptr;
+  a.xs = xs; a.xb = xb; a.xact = xact;
   if (a.M == 0 || Cout == 0) return 0;
   int rc;
   switch (pick_tile(a.M, Cout)) {

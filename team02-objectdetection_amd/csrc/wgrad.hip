@@ -30,6 +30,9 @@ struct WgradArgs {
   float* part;
   int N, H, W, Cin, Ho, Wo, Cout, stride, pad;
   int M, Nw, kchunk;
+  // optional input transform of X (1x1 convs, XF kernels): x = act(x * xs[c] + xb[c]) on
+  // load -- the producer's lazy BatchNorm + activation (see seg_conv_igemm_xf)
+  const float* xs; const float* xb; int xact;
 };
 
 // Row pitch (bf16 elements) of a k-major bf16 tile read with ds_read_b64_tr_b16: a
@@ -43,8 +46,9 @@ constexpr int tr_pitch(int n) { return n % 128 == 32 || n % 128 == 96 ? n : tr_p
 // column-major) and fed to v_mfma_f32_32x32x16_bf16; fp32 accumulation and slabs.
 // VW: channels per load slot -- 8 (one 16-byte load, copied to LDS as is) on bf16
 // storage when Cout, Cin and the row strides are multiples of 8, else 4.
-template <int BM, int BN, int WM, int WN, int KS, bool BF = false, typename IT = float, int VW = 4>
+template <int BM, int BN, int WM, int WN, int KS, bool BF = false, typename IT = float, int VW = 4, bool XF = false>
 __global__ __launch_bounds__(256) void wgrad_kernel(WgradArgs a) {
+  static_assert(!XF || KS == 1, "input transform: 1x1 convs");
   static_assert(VW == 4 || (BF && sizeof(IT) == 2), "16-byte slots carry bf16 operands");
   const IT* __restrict__ gdy = static_cast<const IT*>(a.dy);
   const IT* __restrict__ gx = static_cast<const IT*>(a.x);
@@ -95,6 +99,19 @@ __global__ __launch_bounds__(256) void wgrad_kernel(WgradArgs a) {
     b_wo[i] = rem - b_ho[i] * a.Wo;
   }
 
+  // XF: each B slot's fixed channels' transform coefficients, and which slots of the
+  // loaded chunk hold real pixels (padding / tail slots stay zero)
+  f32x4 xbs[XF ? B_PER : 1][VW / 4], xbb[XF ? B_PER : 1][VW / 4];
+  unsigned b_vm = 0;
+  if constexpr (XF) {
+#pragma unroll
+    for (int i = 0; i < B_PER; ++i)
+#pragma unroll
+      for (int j = 0; j < VW / 4; ++j) {
+        xbs[i][j] = ld4(a.xs + (b_ok[i] ? b_ci[i] : 0) + 4 * j);
+        xbb[i][j] = ld4(a.xb + (b_ok[i] ? b_ci[i] : 0) + 4 * j);
+      }
+  }
   f32x4 ra[A_PER], rb[B_PER];
   auto ldv = [](const IT* q) -> f32x4 {  // one load slot: 4 channels widened, or 8 bf16 raw
     if constexpr (VW == 8) return *reinterpret_cast<const f32x4*>(q);
@@ -111,10 +128,12 @@ __global__ __launch_bounds__(256) void wgrad_kernel(WgradArgs a) {
       if (ok) v = ldv(gdy + (long)p * a.lddy + c);
       ra[i] = v;
     }
+    if (XF) b_vm = 0;
 #pragma unroll
     for (int i = 0; i < B_PER; ++i) {
       const int p = k0 + b_prow[i];
       f32x4 v = {0.f, 0.f, 0.f, 0.f};
+      if (XF && b_ok[i] && p < kend) b_vm |= 1u << i;
       if (b_ok[i] && p < kend) {
         if (KS == 1) {
           v = ldv(gx + (long)p * a.ldx + b_ci[i]);
@@ -149,7 +168,25 @@ __global__ __launch_bounds__(256) void wgrad_kernel(WgradArgs a) {
 #pragma unroll
     for (int i = 0; i < B_PER; ++i) {
       const int idx = tid + i * 256;
-      if (idx < B_VEC) st_op(&Bs[buf][(idx / (BN / VW)) * BR + (idx % (BN / VW)) * VW], rb[i]);
+      f32x4 v = rb[i];
+      if constexpr (XF) {
+        if ((b_vm >> i) & 1u) {
+          if constexpr (VW == 8) {  // 8 bf16: widen, transform, round back as the BN-apply pass would
+            const bf16x8 q = __builtin_bit_cast(bf16x8, v);
+            const f32x4 lo = seg_bn_act4(__builtin_convertvector(__builtin_shufflevector(q, q, 0, 1, 2, 3), f32x4),
+                                         xbs[i][0], xbb[i][0], a.xact);
+            const f32x4 hi = seg_bn_act4(__builtin_convertvector(__builtin_shufflevector(q, q, 4, 5, 6, 7), f32x4),
+                                         xbs[i][VW / 4 - 1], xbb[i][VW / 4 - 1], a.xact);
+            v = __builtin_bit_cast(f32x4, seg_cat8(__builtin_convertvector(lo, bf16x4),
+                                                   __builtin_convertvector(hi, bf16x4)));
+          } else {
+            v = seg_bn_act4(v, xbs[i][0], xbb[i][0], a.xact);
+            if constexpr (sizeof(IT) == 2 && !BF)  // (not instantiated: bf16 storage implies bf16 math)
+              v = __builtin_convertvector(__builtin_convertvector(v, bf16x4), f32x4);
+          }
+        }
+      }
+      if (idx < B_VEC) st_op(&Bs[buf][(idx / (BN / VW)) * BR + (idx % (BN / VW)) * VW], v);
     }
   };
 
@@ -245,6 +282,18 @@ __global__ __launch_bounds__(256) void wgrad_kernel(WgradArgs a) {
 template <int BM, int BN, int WM, int WN, bool BF = false, typename IT = float>
 int launch_wgrad(const WgradArgs& a, int ks, int splits, hipStream_t s) {
   dim3 grid(seg_cdiv(a.Cout, BM) * seg_cdiv(a.Nw, BN) * splits);
+  if (a.xs) {  // input transform (1x1 only)
+    if (ks != 1) return (int)hipErrorInvalidValue;
+    const bool v8 = sizeof(IT) == 2 && a.Cout % 8 == 0 && a.Cin % 8 == 0 && a.lddy % 8 == 0 && a.ldx % 8 == 0;
+    if constexpr (sizeof(IT) == 2) {
+      if (v8) {
+        hipLaunchKernelGGL((wgrad_kernel<BM, BN, WM, WN, 1, true, IT, 8, true>), grid, dim3(256), 0, s, a);
+        SEG_RET_LAST();
+      }
+    }
+    hipLaunchKernelGGL((wgrad_kernel<BM, BN, WM, WN, 1, BF, IT, 4, true>), grid, dim3(256), 0, s, a);
+    SEG_RET_LAST();
+  }
   if (BF) {
     const bool v8 = sizeof(IT) == 2 && a.Cout % 8 == 0 && a.Cin % 8 == 0 && a.lddy % 8 == 0 && a.ldx % 8 == 0;
     if constexpr (sizeof(IT) == 2) {
@@ -291,7 +340,8 @@ SEG_API int seg_conv_wgrad_splits(long M, int Cout, int Cin, int ks) {
 // part[s][co][tap*Cin+ci] = sum over split s's pixels of dY[p][co] * X[src(p,tap)][ci].
 static int conv_wgrad(const void* dy, long lddy, const void* x, long ldx, int N, int H, int W, int Cin, int Ho,
                       int Wo, int Cout, int ks, int stride, int pad, float* part, int splits,
-                      hipStream_t stream, bool bf = false, bool bf_io = false);
+                      hipStream_t stream, bool bf = false, bool bf_io = false, const float* xs = nullptr,
+                      const float* xb = nullptr, int xact = 0);
 
 SEG_API int seg_conv_wgrad(const float* dy, long lddy, const float* x, long ldx,
                            int N, int H, int W, int Cin, int Ho, int Wo, int Cout,
@@ -316,16 +366,44 @@ SEG_API int seg_conv_wgrad_bf16io(const __bf16* dy, long lddy, const __bf16* x, 
                     true, true);
 }
 
+// seg_conv_wgrad(_bf16, _bf16io) of a 1x1 conv whose input X is the raw output of a
+// BatchNorm'd producer: X = act(x * in_scale + in_shift) formed on load (the lazy BN of
+// seg_conv_igemm_xf; the same value the BN-apply pass would have stored).
+SEG_API int seg_conv_wgrad_xf(const float* dy, long lddy, const float* x, long ldx, int N, int H, int W, int Cin,
+                              int Ho, int Wo, int Cout, int ks, int stride, int pad, float* part, int splits,
+                              const float* in_scale, const float* in_shift, int in_act, hipStream_t stream) {
+  if (!in_scale) return (int)hipErrorInvalidValue;
+  return conv_wgrad(dy, lddy, x, ldx, N, H, W, Cin, Ho, Wo, Cout, ks, stride, pad, part, splits, stream, false, false,
+                    in_scale, in_shift, in_act);
+}
+SEG_API int seg_conv_wgrad_bf16_xf(const float* dy, long lddy, const float* x, long ldx, int N, int H, int W, int Cin,
+                                   int Ho, int Wo, int Cout, int ks, int stride, int pad, float* part, int splits,
+                                   const float* in_scale, const float* in_shift, int in_act, hipStream_t stream) {
+  if (!in_scale) return (int)hipErrorInvalidValue;
+  return conv_wgrad(dy, lddy, x, ldx, N, H, W, Cin, Ho, Wo, Cout, ks, stride, pad, part, splits, stream, true, false,
+                    in_scale, in_shift, in_act);
+}
+SEG_API int seg_conv_wgrad_bf16io_xf(const __bf16* dy, long lddy, const __bf16* x, long ldx, int N, int H, int W,
+                                     int Cin, int Ho, int Wo, int Cout, int ks, int stride, int pad, float* part,
+                                     int splits, const float* in_scale, const float* in_shift, int in_act,
+                                     hipStream_t stream) {
+  if (!in_scale) return (int)hipErrorInvalidValue;
+  return conv_wgrad(dy, lddy, x, ldx, N, H, W, Cin, Ho, Wo, Cout, ks, stride, pad, part, splits, stream, true, true,
+                    in_scale, in_shift, in_act);
+}
+
 static int conv_wgrad(const void* dy, long lddy, const void* x, long ldx, int N, int H, int W, int Cin, int Ho,
                       int Wo, int Cout, int ks, int stride, int pad, float* part, int splits,
-                      hipStream_t stream, bool bf, bool bf_io) {
+                      hipStream_t stream, bool bf, bool bf_io, const float* xs, const float* xb, int xact) {
   if ((Cin & 3) || (ldx & 3) || (lddy & 3) || (ks != 1 && ks != 3) || splits < 1) return (int)hipErrorInvalidValue;
+  if (xs && (!xb || ks != 1 || xact < SEG_ACT_NONE || xact > SEG_ACT_RELU6)) return (int)hipErrorInvalidValue;
   if (ks == 1 && (stride != 1 || pad != 0)) return (int)hipErrorInvalidValue;
   WgradArgs a;
   a.dy = dy; a.lddy = lddy; a.x = x; a.ldx = ldx; a.part = part;
   a.N = N; a.H = H; a.W = W; a.Cin = Cin; a.Ho = Ho; a.Wo = Wo; a.Cout = Cout;
   a.stride = stride; a.pad = pad; a.M = N * Ho * Wo; a.Nw = ks * ks * Cin;
   a.kchunk = seg_cdiv(seg_cdiv(a.M, splits), BK) * BK;
+  a.xs = xs; a.xb = xb; a.xact = xact;
   int bm, bn;
   wgrad_tiles(Cout, a.Nw, &bm, &bn);
   if (bf_io) {

@@ -93,6 +93,11 @@ for _n in ("seg_add", "seg_bn_stats", "seg_bn_apply", "seg_bn_backward", "seg_co
     PROTOTYPES[_n + "_bf16io"] = PROTOTYPES[_n]
 PROTOTYPES["seg_conv_igemm_bf16io"] = PROTOTYPES["seg_conv_igemm"]
 PROTOTYPES["seg_conv_wgrad_bf16io"] = PROTOTYPES["seg_conv_wgrad"]
+# lazy-BN (input transform) variants: + in_scale, in_shift, in_act before the stream
+for _n in ("seg_conv_igemm", "seg_conv_wgrad"):
+    _r, _a = PROTOTYPES[_n]
+    for _sfx in ("_xf", "_bf16_xf", "_bf16io_xf"):
+        PROTOTYPES[_n + _sfx] = (_r, _a[:-1] + [_V, _V, _I, _V])
 PROTOTYPES["seg_conv_halo_bf16io"] = PROTOTYPES["seg_conv_halo"]
 
 _lock = threading.Lock()

@@ -209,6 +209,11 @@ class ConvOp:
                 rt.tcall("wino3_fwd", self.flops(), "seg_conv_wino", rt.ptr(i), i.ld, i.N, i.H, i.W, self.cin_pad,
                             self.wk_wf.data_ptr(), self.cin_pad, bias, rt.ptr(y), y.ld, self.cout, None, 0, statp,
                             work.data_ptr(), s)
+            elif self.xform is not None:  # 1x1 conv applying its producer's lazy BN on load
+                name = "seg_conv_igemm_bf16io_xf" if rt.io else "seg_conv_igemm_bf16_xf" if self.bf else "seg_conv_igemm_xf"
+                rt.tcall("igemm1_fwd", self.flops(), name, rt.ptr(i), i.ld, i.N, i.H, i.W, self.cin_pad, wk_ptr, ldk,
+                         bias, rt.ptr(y), y.ld, y.H, y.W, self.cout, self.ks, self.stride, self.pad, None, 0, statp,
+                         *self._in_xform(rt), s)
             elif rt.io:
                 rt.tcall(f"igemm{self.ks}_fwd", self.flops(), "seg_conv_igemm_bf16io", rt.ptr(i), i.ld, i.N, i.H,
                             i.W, self.cin_pad, wk_ptr, ldk, bias, rt.ptr(y), y.ld, y.H, y.W, self.cout, self.ks,
@@ -343,10 +348,13 @@ class ConvOp:
             else:
                 splits = query("seg_conv_wgrad_splits", M, self.cout, self.cin_pad, self.ks)
                 part = rt.tmp(splits * self.cout * self.ks * self.ks * self.cin_pad)
-                rt.tcall(f"igemm{self.ks}_wgrad", self.flops(),
-                            ("seg_conv_wgrad_bf16io" if rt.io else "seg_conv_wgrad_bf16") if self.bf else "seg_conv_wgrad", dYp, dY.ld, rt.ptr(i), i.ld,
+                name = ("seg_conv_wgrad_bf16io" if rt.io else "seg_conv_wgrad_bf16") if self.bf else "seg_conv_wgrad"
+                xf = ()
+                if self.xform is not None:  # X = the producer's lazy BN + act, formed on load
+                    name, xf = name + "_xf", self._in_xform(rt)
+                rt.tcall(f"igemm{self.ks}_wgrad", self.flops(), name, dYp, dY.ld, rt.ptr(i), i.ld,
                             i.N, i.H, i.W, self.cin_pad, y.H, y.W, self.cout, self.ks, self.stride, self.pad,
-                            part.data_ptr(), splits, s)
+                            part.data_ptr(), splits, *xf, s)
                 rt.call("seg_conv_wgrad_reduce", part.data_ptr(), splits, gw, self.cout, self.cin, self.ks, 0, 0, s)
         rt.params_done(self.params(), s)
 
@@ -461,11 +469,17 @@ class Program:
         self.ops.append(ConvOp(kind, conv, bn, act, inp, out, y, res, xform))
         return out
 
-    def make_lazy(self, a: Act):
+    def make_lazy(self, a: Act, pointwise=False):
         """If `a` is the private BN+act output of the last op, drop its buffer and let
-        the consumer apply the BN on load; returns the producer op (or None)."""
+        the consumer apply the BN on load; returns the producer op (or None).
+        pointwise: the consumer is a 1x1 conv (seg_conv_igemm_xf / seg_conv_wgrad_xf:
+        the uniform-tap loader, 8-channel groups) -- any conv producer; otherwise a
+        depthwise consumer (seg_dw_fwd / seg_dw_wgrad) of a dense producer."""
         op = self.ops[-1] if self.ops else None
-        if not (isinstance(op, ConvOp) and op.kind == "igemm" and op.bn is not None and op.res is None
+        kinds = ("igemm", "dw") if pointwise else ("igemm",)
+        if pointwise and not (LAZY_PW and a.C % 8 == 0 and a.C >= 16):
+            return None
+        if not (isinstance(op, ConvOp) and op.kind in kinds and op.bn is not None and op.res is None
                 and op.out is a and op.y is not a and a.off == 0 and a.ld == r4(a.C)
                 and self.bufs.get(a.buf) == (a.M, a.ld) and not a.buf.startswith("cat")):
             return None
@@ -659,8 +673,12 @@ def _inverted_residual(prog, blk: InvertedResidual, inp, out=None):
     if xf is not None:
         x = xf.out
     x = _cna(prog, layers[0], x, kind="dw", xform=xf)
+    # ... and the 1x1 project conv applies the depthwise conv's BN + ReLU6 the same way
+    xf = prog.make_lazy(x, pointwise=True)
+    if xf is not None:
+        x = xf.out
     return prog.conv("igemm", layers[1], layers[2], ACT_NONE, x, out=out,
-                     res=inp if blk.use_res_connect else None)
+                     res=inp if blk.use_res_connect else None, xform=xf)
 
 
 def _double_conv(prog, dc, inp, out=None):
@@ -681,7 +699,10 @@ def _up(prog, u, low, cat):
 def _outconv(prog, oc, inp):
     c = oc.conv
     x = prog.conv("igemm", c[0], c[1], ACT_RELU, inp)
-    return prog.conv("igemm", c[3], None, ACT_NONE, x)
+    xf = prog.make_lazy(x, pointwise=True) if c[3].kernel_size[0] == 1 else None
+    if xf is not None:
+        x = xf.out
+    return prog.conv("igemm", c[3], None, ACT_NONE, x, xform=xf)
 
 
 def build_mobilenet_unet(model, N, H, W) -> Program:
@@ -1049,6 +1070,9 @@ class Run:
 OVERLAP = os.environ.get("SEG_OVERLAP", "1") == "1"
 # LDS-halo direct 3x3 conv for the narrow convs in the bf16io configuration; SEG_HALO_BF16=0 turns it off.
 HALO_BF16 = os.environ.get("SEG_HALO_BF16", "1") == "1"
+# lazy BatchNorm for 1x1 consumers (the inverted residuals' project convs, OutConv's last
+# conv): SEG_LAZY_PW=0 keeps the separate BN-apply pass (read at program build)
+LAZY_PW = os.environ.get("SEG_LAZY_PW", "1") == "1"
 _SIDE = {}
 
 

@@ -1,6 +1,6 @@
 """Build a variant of libsegamd.so with extra compile flags, for A/B timing.
 
-    python tools/variant.py NAME [-DFOO=1 ...]   ->  tmp_var/NAME.so
+    python tools/variant.py NAME [-DFOO=1 ...]   ->  variants/NAME.so  (travels with gpurun; git-ignored)
 """
 import os
 import subprocess
@@ -14,7 +14,7 @@ from seg_amd.build import ARCH, FLAGS, HIPCC, sources  # noqa: E402
 
 def main():
     name, extra = sys.argv[1], sys.argv[2:]
-    odir = os.path.join(REPO, "tmp_var", name)
+    odir = os.path.join(REPO, "tmp_var", name)  # objects stay here (gpurun-ignored)
     os.makedirs(odir, exist_ok=True)
 
     def one(src):
@@ -25,7 +25,8 @@ def main():
         return obj
     with ThreadPoolExecutor(8) as ex:
         objs = list(ex.map(one, sources()))
-    out = os.path.join(REPO, "tmp_var", name + ".so")
+    os.makedirs(os.path.join(REPO, "variants"), exist_ok=True)
+    out = os.path.join(REPO, "variants", name + ".so")
     subprocess.run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", out, *objs], check=True)
     print(out)
 

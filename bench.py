@@ -381,9 +381,15 @@ def main():
                 "share_of_step": round(secs / dt, 4),
                 "note": "live launches share the CUs with the weight-gradient side stream (engine.OVERLAP); "
                         "without_side_stream re-times the same launches in 3 untimed steps with it off",
-                "without_side_stream": {"achieved": round(ifl / isec / 1e12, 2) if isec else None,
-                                        "frac": round(ifl / isec / 1e12 / peak, 4) if isec else None,
-                                        "avg_launch_us": round(isec / max(inn, 1) * 1e6, 2), "launches": inn},
+                "without_side_stream": (
+                    {"achieved": round(ifl / isec / 1e12, 2) if isec else None, "unit": "TFLOP/s",
+                     "frac": round(ifl / isec / 1e12 / peak, 4) if isec else None,
+                     "avg_launch_us": round(isec / max(inn, 1) * 1e6, 2), "launches": inn}
+                    if args.math == "f32" else
+                    {"achieved": round(alg_bytes * inn / isec / 1e9, 1) if isec else None, "unit": "GB/s",
+                     "frac": round(alg_bytes * inn / isec / 1e9 / HBM_PEAK_GBS, 4) if isec else None,
+                     "mfma_tflops": round(ifl / isec / 1e12, 2) if isec else None,
+                     "avg_launch_us": round(isec / max(inn, 1) * 1e6, 2), "launches": inn}),
                 "wgrad3": {"achieved": round(wf / ws / 1e12, 2) if ws else None, "launches": wgn,
                            "avg_launch_us": round(ws / max(wgn, 1) * 1e6, 2)},
                 "all_mfma_convs": {"achieved": round(af / as_ / 1e12, 2) if as_ else None, "launches": an}}

@@ -94,6 +94,8 @@ int seg_pack_conv_weight(const float* w, float* wk, int Cout, int Cin, int ks, i
 /* Weight gradient (convolution_backward, weight path) as split-K partial slabs
  * part[splits][Cout][ks*ks*Cin]; splits from seg_conv_wgrad_splits. */
 int seg_conv_wgrad_splits(long M, int Cout, int Cin, int ks);
+/* The split count the engine uses for the bf16-math weight gradients (fewer, longer blocks). */
+int seg_conv_wgrad_splits_bf16(long M, int Cout, int Cin, int ks);
 int seg_conv_wgrad(const float* dy, long lddy, const float* x, long ldx,
                    int N, int H, int W, int Cin, int Ho, int Wo, int Cout,
                    int ks, int stride, int pad, float* part, int splits, hipStream_t stream);

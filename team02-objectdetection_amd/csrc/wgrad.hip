@@ -16,6 +16,12 @@
 
 namespace {
 
+#ifndef SEG_WGRAD_BLOCKS
+#define SEG_WGRAD_BLOCKS 2048  // target blocks (tiles x splits) of a weight-gradient launch
+#endif
+#ifndef SEG_WGRAD_BLOCKS_BF16
+#define SEG_WGRAD_BLOCKS_BF16 512
+#endif
 #ifndef SEG_WGRAD_BK
 #define SEG_WGRAD_BK 16
 #endif
@@ -325,16 +331,25 @@ void wgrad_tiles(int Cout, int Nw, int* bm, int* bn) {
 
 // Number of K splits (partial slabs) seg_conv_wgrad will use; the caller provides
 // a workspace of splits * Cout * ks*ks*Cin floats.
-SEG_API int seg_conv_wgrad_splits(long M, int Cout, int Cin, int ks) {
+static int wgrad_splits(long M, int Cout, int Cin, int ks, long target_blocks) {
   const int Nw = ks * ks * Cin;
   int bm, bn;
   wgrad_tiles(Cout, Nw, &bm, &bn);
   const long tiles = (long)seg_cdiv(Cout, bm) * seg_cdiv(Nw, bn);
-  long splits = (2048 + tiles - 1) / tiles;
+  long splits = (target_blocks + tiles - 1) / tiles;
   const long max_by_k = std::max<long>(1, M / 256);  // >= 256 pixels per split
   splits = std::min(splits, max_by_k);
   splits = std::min<long>(splits, 1024);  // small slabs (the stem: 32 x 36) need many splits to fill 256 CUs
   return (int)std::max<long>(1, splits);
+}
+SEG_API int seg_conv_wgrad_splits(long M, int Cout, int Cin, int ks) {
+  return wgrad_splits(M, Cout, Cin, ks, SEG_WGRAD_BLOCKS);
+}
+// Split count for the bf16-math weight gradients (seg_conv_wgrad_bf16 / _bf16io): a
+// quarter of the blocks -- measured in the overlapped step (bf16io +1.7 %), where the
+// side-stream weight gradients share the CUs with the data-gradient chain.
+SEG_API int seg_conv_wgrad_splits_bf16(long M, int Cout, int Cin, int ks) {
+  return wgrad_splits(M, Cout, Cin, ks, SEG_WGRAD_BLOCKS_BF16);
 }
 
 // part[s][co][tap*Cin+ci] = sum over split s's pixels of dY[p][co] * X[src(p,tap)][ci].

@@ -2,7 +2,7 @@
 256x512) shapes: achieved GB/s of algorithmic traffic (input + output read or
 written once; wgrad: dY + X) vs the ~6 TB/s achievable HBM rate.
 
-    python tools/dwbench.py [--lazy] [lib.so ...]
+    python tools/dwbench.py [--lazy] [--bf16io] [lib.so ...]
 Several libraries can be given (A/B of kernel variants in one process).
 """
 import ctypes
@@ -17,6 +17,7 @@ sys.path.insert(0, os.path.join(REPO, "team02-objectdetection_amd"))
 from seg_amd import _lib  # noqa: E402
 
 LIB = None
+SFX, DT, ES = "", torch.float32, 4  # entry-point suffix, storage dtype and bytes (--bf16io)
 
 
 def load(path):
@@ -58,6 +59,9 @@ def timeit(fn, reps=20):
 def main():
     global LIB
     lazy = "--lazy" in sys.argv
+    global SFX, DT, ES
+    if "--bf16io" in sys.argv:
+        SFX, DT, ES = "_bf16io", torch.bfloat16, 2
     paths = [a for a in sys.argv[1:] if not a.startswith("--")] or [_lib.LIB_PATH]
     _lib.lib()
     for p in paths:
@@ -71,24 +75,24 @@ def run(lazy):
     tot = {"fwd": 0.0, "dgrad": 0.0, "wgrad": 0.0}
     for C, H, W, st in SHAPES:
         Ho, Wo = (H - 1) // st + 1, (W - 1) // st + 1
-        x = torch.randn(N * H * W, C, device="cuda")
-        dy = torch.randn(N * Ho * Wo, C, device="cuda")
-        y = torch.empty(N * Ho * Wo, C, device="cuda")
-        dx = torch.empty(N * H * W, C, device="cuda")
+        x = torch.randn(N * H * W, C, device="cuda").to(DT)
+        dy = torch.randn(N * Ho * Wo, C, device="cuda").to(DT)
+        y = torch.empty(N * Ho * Wo, C, device="cuda", dtype=DT)
+        dx = torch.empty(N * H * W, C, device="cuda", dtype=DT)
         wk = torch.randn(9 * C, device="cuda")
         sc, sh = torch.rand(C, device="cuda"), torch.rand(C, device="cuda")
         xf = (sc.data_ptr(), sh.data_ptr(), 2) if lazy else (None, None, 0)
         nblk = query("seg_dw_wgrad_blocks", N, Ho, Wo, C)
         part = torch.empty(nblk * 9 * C, device="cuda")
         dw = torch.empty(C * 9, device="cuda")
-        bx, by = 4 * N * H * W * C, 4 * N * Ho * Wo * C
-        tf = timeit(lambda: call("seg_dw_fwd", x.data_ptr(), C, N, H, W, C, *xf, wk.data_ptr(), y.data_ptr(), C, Ho,
+        bx, by = ES * N * H * W * C, ES * N * Ho * Wo * C
+        tf = timeit(lambda: call("seg_dw_fwd" + SFX, x.data_ptr(), C, N, H, W, C, *xf, wk.data_ptr(), y.data_ptr(), C, Ho,
                                  Wo, st, s))
-        td = timeit(lambda: call("seg_dw_dgrad", dy.data_ptr(), C, N, Ho, Wo, C, wk.data_ptr(), dx.data_ptr(), C, H,
+        td = timeit(lambda: call("seg_dw_dgrad" + SFX, dy.data_ptr(), C, N, Ho, Wo, C, wk.data_ptr(), dx.data_ptr(), C, H,
                                  W, st, 0, s))
 
         def wg():
-            call("seg_dw_wgrad", dy.data_ptr(), C, x.data_ptr(), C, N, H, W, C, *xf, Ho, Wo, st, part.data_ptr(), s)
+            call("seg_dw_wgrad" + SFX, dy.data_ptr(), C, x.data_ptr(), C, N, H, W, C, *xf, Ho, Wo, st, part.data_ptr(), s)
             call("seg_conv_wgrad_reduce", part.data_ptr(), nblk, dw.data_ptr(), C, 1, 3, 1, 0, s)
         tw = timeit(wg)
         tot["fwd"] += tf

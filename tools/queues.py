@@ -38,6 +38,20 @@ def main():
     ce = [r for r in step if "ce_up_loss" in r["Kernel_Name"]]
     if ce:
         print(f"forward (to the CE loss) {(int(ce[0]['Start_Timestamp']) - t0) / 1e3:.0f} us")
+    # idle gaps of the busiest queue (the data-gradient chain): where the step waits
+    q = max(byq, key=lambda k: sum(byq[k].values()))
+    main = [r for r in step if r["Queue_Id"] == q]
+    gaps, tail = [], 0.0
+    for p, n in zip(main, main[1:]):
+        g = (int(n["Start_Timestamp"]) - int(p["End_Timestamp"])) / 1e3
+        if g > 20:
+            gaps.append((g, family(p["Kernel_Name"]), family(n["Kernel_Name"]),
+                         (int(p["End_Timestamp"]) - t0) / 1e3))
+    tail = (t1 - int(main[-1]["End_Timestamp"])) / 1e3
+    print(f"queue {q} idle: {sum(g[0] for g in gaps):.0f} us in {len(gaps)} gaps > 20 us, "
+          f"{tail:.0f} us after its last kernel")
+    for g, a_, b_, at in sorted(gaps, reverse=True)[:12]:
+        print(f"  {g:7.0f} us at {at:7.0f} us: {a_} -> {b_}")
 
 
 if __name__ == "__main__":

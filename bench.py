@@ -324,18 +324,20 @@ def main():
         flops, secs, n = family(rec, conv3)
         wfl, wsec, wn = family(rec, {"wino3_fwd", "wino3_dgrad"})
         achieved = flops / secs / 1e12 if secs > 0 else 0.0
-        traffic, traffic_src = None, None
+        traffic, traffic_src, mfma_busy = None, None, None
         prof = os.path.join(REPO, "profiles", "latest_roofline.json" if args.math == "f32"
                             else f"latest_roofline_{args.math}.json")
         if os.path.exists(prof):
             with open(prof) as fh:
                 rj = json.load(fh)
             traffic = rj["families"].get("conv3", {}).get("hbm_bytes_per_op")
+            mfma_busy = rj["families"].get("conv3", {}).get("mfma_busy_frac")
             # the PMC figure is not measured in this run: name the profile and commit it came from
             traffic_src = {"file": os.path.relpath(prof, REPO), "profile": rj.get("profile"),
                            "commit": rj.get("commit"),
                            "counters": "rocprofv3 PMC (2*FETCH_SIZE+WRITE_SIZE)*1KiB of the conv3 family per step "
-                                       "/ 17 conv ops, separate --pmc passes"}
+                                       "/ 17 conv ops, separate --pmc passes; SQ_VALU_MFMA_BUSY_CYCLES and "
+                                       "GRBM_GUI_ACTIVE in a third pass"}
         # algorithmic bytes of the family: every 3x3 conv's input and output tensors once
         # (fwd: X + Y, dgrad: dY + dX) at the storage element size, averaged over its launches
         prog = engine.get_program(getattr(model, "module", model), args.batch, args.height, args.width)
@@ -366,6 +368,8 @@ def main():
                 "traffic": round(traffic) if traffic else None,
                 "traffic_source": traffic_src,
                 "traffic_over_algorithmic": round(traffic / alg_bytes, 3) if traffic else None,
+                # same profile: SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE / 8 XCDs * 1024 SIMDs) over the family
+                "mfma_busy_frac_pmc": round(mfma_busy, 4) if mfma_busy else None,
                 "algorithmic_bytes_per_launch": round(alg_bytes),
                 "kernel": ("dense 3x3 conv fwd + dgrad on f32 MFMA: igemm_conv_kernel<*,*,*,*,3,*> (implicit GEMM), "
                            "halo3x3_kernel (LDS-halo direct conv, narrow decoder convs) and, for the deep decoder "

@@ -23,8 +23,9 @@ FAMILIES = {  # "conv3" = the dense 3x3 conv forward + data gradient (bench.py's
     "conv3": re.compile(r"igemm_conv_kernel<\d+, \d+, \d+, \d+, 3, \d+|igemm_conv_kernelILi\d+ELi\d+ELi\d+ELi\d+ELi3E"
                         r"|wino_gemm_kernel|wino_out_kernel|halo3x3_kernel"),
     "igemm1": re.compile(r"igemm_conv_kernel<\d+, \d+, \d+, \d+, 1, \d+|igemm_conv_kernelILi\d+ELi\d+ELi\d+ELi\d+ELi1E"),
-    "wgrad3": re.compile(r"wgrad_kernel<\d+, \d+, \d+, \d+, 3[,>]|wino_wgrad"),
-    "wgrad1": re.compile(r"wgrad_kernel<\d+, \d+, \d+, \d+, 1[,>]"),
+    "wgrad3": re.compile(r"wgrad_kernel<\d+, \d+, \d+, \d+, 3[,>]|wgrad_kernelILi\d+ELi\d+ELi\d+ELi\d+ELi3E"
+                         r"|wino_wgrad"),
+    "wgrad1": re.compile(r"wgrad_kernel<\d+, \d+, \d+, \d+, 1[,>]|wgrad_kernelILi\d+ELi\d+ELi\d+ELi\d+ELi1E"),
 }
 OPS_PER_STEP = {"conv3": 17}  # MobileNetV2UNet bs=32: 8 decoder convs fwd + 8 dgrad + the stem fwd
 
@@ -60,7 +61,18 @@ def main(prof_dir, pmc_dir, steps, out_prefix):
             f = family(names[d])
             if f:
                 traffic[(f, c)].append(v)
+    # MFMA activity (optional pass): per family, MFMA-busy cycles summed over the SIMDs and
+    # GRBM_GUI_ACTIVE summed over the 8 XCDs.  busy_frac = MFMA_BUSY / (GUI_ACTIVE / 8 * 1024 SIMDs):
+    # the share of SIMD-cycles inside the family's dispatches in which a matrix instruction was busy.
+    mfma = defaultdict(lambda: [0.0, 0.0])
     import os
+    mpath = f"{pmc_dir}/MFMA/run_counter_collection.csv"
+    if os.path.exists(mpath):
+        for r in csv.DictReader(open(mpath)):
+            f = family(r["Kernel_Name"])
+            if f:
+                k = 0 if r["Counter_Name"].startswith("SQ_VALU_MFMA_BUSY") else 1
+                mfma[f][k] += float(r["Counter_Value"])
     import subprocess
     try:
         commit = subprocess.run(["git", "rev-parse", "--short=12", "HEAD"], capture_output=True, text=True,
@@ -74,8 +86,9 @@ def main(prof_dir, pmc_dir, steps, out_prefix):
            "kernel_ms_per_step": total / 1e6 / steps, "families": {}}
     lines = [f"# rocprofv3 summary ({out_prefix})", "",
              f"Kernel time per step (all kernels): {total / 1e6 / steps:.2f} ms over {steps} profiled steps.", "",
-             "| family | calls/step | ms/step | share | avg launch us | HBM bytes/launch (2*FETCH+WRITE)*1KiB |",
-             "|---|---|---|---|---|---|"]
+             "| family | calls/step | ms/step | share | avg launch us | HBM bytes/launch (2*FETCH+WRITE)*1KiB "
+             "| MFMA-busy share of SIMD-cycles |",
+             "|---|---|---|---|---|---|---|"]
     for f, d in sorted(fam.items(), key=lambda kv: -kv[1]["ns"]):
         fetch = traffic.get((f, "FETCH_SIZE"), [])
         write = traffic.get((f, "WRITE_SIZE"), [])
@@ -84,13 +97,18 @@ def main(prof_dir, pmc_dir, steps, out_prefix):
         out["families"][f] = {"calls_per_step": d["calls"] / steps, "ms_per_step": d["ns"] / 1e6 / steps,
                               "avg_launch_us": avg_us, "hbm_bytes_per_launch": hbm,
                               "symbols": d["symbols"]}
+        if mfma[f][1] > 0:
+            out["families"][f]["mfma_busy_cycles"] = mfma[f][0]
+            out["families"][f]["grbm_gui_active"] = mfma[f][1]
+            out["families"][f]["mfma_busy_frac"] = mfma[f][0] / (mfma[f][1] / 8 * 1024)
         if f in OPS_PER_STEP and fetch and write:
             # per conv op (a Winograd op is two kernels): family bytes per step / ops per step
             per_step = (2 * sum(fetch) + sum(write)) * 1024 / (len(fetch) / (d["calls"] / steps))
             out["families"][f]["ops_per_step"] = OPS_PER_STEP[f]
             out["families"][f]["hbm_bytes_per_op"] = per_step / OPS_PER_STEP[f]
         lines.append(f"| {f} | {d['calls'] / steps:.0f} | {d['ns'] / 1e6 / steps:.2f} | {d['ns'] / total:.1%} | "
-                     f"{avg_us:.1f} | {hbm / 1e6 if hbm else float('nan'):.1f} MB |")
+                     f"{avg_us:.1f} | {hbm / 1e6 if hbm else float('nan'):.1f} MB | "
+                     f"{out['families'][f].get('mfma_busy_frac', float('nan')):.3f} |")
     lines += ["", "Top kernels:", "", "| kernel | calls | avg us | total ms |", "|---|---|---|---|"]
     for r in sorted(stats, key=lambda r: -float(r["TotalDurationNs"]))[:25]:
         lines.append(f"| `{r['Name'].replace('(anonymous namespace)::', '')[:90]}` | {r['Calls']} | "

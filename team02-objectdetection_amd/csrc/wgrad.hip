@@ -342,14 +342,27 @@ static int wgrad_splits(long M, int Cout, int Cin, int ks, long target_blocks) {
   splits = std::min<long>(splits, 1024);  // small slabs (the stem: 32 x 36) need many splits to fill 256 CUs
   return (int)std::max<long>(1, splits);
 }
+#ifndef SEG_WGRAD_THIN
+#define SEG_WGRAD_THIN 2048
+#endif
 SEG_API int seg_conv_wgrad_splits(long M, int Cout, int Cin, int ks) {
-  return wgrad_splits(M, Cout, Cin, ks, SEG_WGRAD_BLOCKS);
+  int bm, bn;
+  wgrad_tiles(Cout, ks * ks * Cin, &bm, &bn);
+  const long tiles = (long)seg_cdiv(Cout, bm) * seg_cdiv(ks * ks * Cin, bn);
+  return wgrad_splits(M, Cout, Cin, ks, tiles <= 2 ? SEG_WGRAD_THIN : SEG_WGRAD_BLOCKS);
 }
 // Split count for the bf16-math weight gradients (seg_conv_wgrad_bf16 / _bf16io): a
 // quarter of the blocks -- measured in the overlapped step (bf16io +1.7 %), where the
-// side-stream weight gradients share the CUs with the data-gradient chain.
+// side-stream weight gradients share the CUs with the data-gradient chain -- except for
+// thin slabs (<= 2 output tiles), which take 1024 (+0.6 %).
+#ifndef SEG_WGRAD_THIN_BF16
+#define SEG_WGRAD_THIN_BF16 1024  // thin slabs (<= 2 tiles: the stem, OutConv, Cout-32 decoder convs): measured +0.6 % bf16io
+#endif
 SEG_API int seg_conv_wgrad_splits_bf16(long M, int Cout, int Cin, int ks) {
-  return wgrad_splits(M, Cout, Cin, ks, SEG_WGRAD_BLOCKS_BF16);
+  int bm, bn;
+  wgrad_tiles(Cout, ks * ks * Cin, &bm, &bn);
+  const long tiles = (long)seg_cdiv(Cout, bm) * seg_cdiv(ks * ks * Cin, bn);
+  return wgrad_splits(M, Cout, Cin, ks, tiles <= 2 ? SEG_WGRAD_THIN_BF16 : SEG_WGRAD_BLOCKS_BF16);
 }
 
 // part[s][co][tap*Cin+ci] = sum over split s's pixels of dY[p][co] * X[src(p,tap)][ci].

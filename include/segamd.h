@@ -179,7 +179,8 @@ int seg_conv_halo(const float* in, long ldin, int N, int H, int W, int Cin, cons
 /* Every weight repack of a step in one launch.  `jobs` is a DEVICE array of
  * njobs seg_pack_job (mode 0/1 as seg_pack_conv_weight, mode 2 = depthwise
  * [9][C] as seg_pack_dw_weight with cout = C, modes 3/4 = Winograd filter
- * transforms [16][rows][ldk] for seg_conv_wino's forward / data gradient).  One thread
+ * transforms [16][rows][ldk] for seg_conv_wino's forward / data gradient; mode 0/1 | 16 =
+ * the same packs written as bf16 (RNE) into wk for the _w16 GEMM entry points).  One thread
  * per output element; job k owns the launch's blocks [blk0, blk0 + nblk), nblk =
  * ceil(elements / 256), jobs sorted by blk0; nblocks = the total.  Replaces the
  * per-conv packs of the engine's step. */
@@ -373,6 +374,16 @@ int seg_maxpool2_fwd_bf16io(const seg_bf16* in, long ldin, int N, int H, int W, 
     hipStream_t stream);
 int seg_maxpool2_bwd_bf16io(const seg_bf16* in, long ldin, const seg_bf16* dout, long lddout, int N, int H, int W, int
     C, seg_bf16* din, long lddin, int accumulate, hipStream_t stream);
+/* seg_conv_igemm_bf16io / _xf with the weights packed as bf16 (seg_pack_batch mode | 16):
+ * [Cout][ldk] bf16, ldk % 8 == 0, 16-byte aligned, zero beyond K.  Bitwise the fp32-weight
+ * launch (the same RNE rounding, done once at pack time); half the weight bytes. */
+int seg_conv_igemm_bf16io_w16(const seg_bf16* in, long ldin, int N, int H, int W, int Cin, const seg_bf16* wk,
+    int ldk, const float* bias, seg_bf16* out, long ldout, int Ho, int Wo, int Cout, int ks, int stride, int pad,
+    const seg_bf16* add, long ldadd, float* stat, hipStream_t stream);
+int seg_conv_igemm_bf16io_xf_w16(const seg_bf16* in, long ldin, int N, int H, int W, int Cin, const seg_bf16* wk,
+    int ldk, const float* bias, seg_bf16* out, long ldout, int Ho, int Wo, int Cout, int ks, int stride, int pad,
+    const seg_bf16* add, long ldadd, float* stat, const float* in_scale, const float* in_shift, int in_act,
+    hipStream_t stream);
 int seg_conv_halo_bf16io(const seg_bf16* in, long ldin, int N, int H, int W, int Cin, const float* wk, int ldk,
     const float* bias, seg_bf16* out, long ldout, int Cout, const seg_bf16* add, long ldadd, float* stat,
     hipStream_t stream);

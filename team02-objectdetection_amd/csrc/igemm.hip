@@ -186,16 +186,19 @@ __global__ __launch_bounds__(256) void pack_batch_kernel(const SegPackJob* __res
     }
     return;
   }
-  const int rows = j.mode == 0 ? j.cout : j.cin;
+  // modes 0 / 1; | 16: bf16 output (RNE; the _w16 GEMM entry points)
+  const int mode = j.mode & 15;
+  const int rows = mode == 0 ? j.cout : j.cin;
   if (i >= (long)rows * j.ldk) return;
   const int r = (int)(i / j.ldk), k = (int)(i - (long)r * j.ldk);
   float v = 0.f;
   if (k < taps * j.kin_pad) {
     const int tap = k / j.kin_pad, c = k - tap * j.kin_pad;
-    if (j.mode == 0) { if (c < j.cin) v = j.w[((long)r * j.cin + c) * taps + tap]; }
+    if (mode == 0) { if (c < j.cin) v = j.w[((long)r * j.cin + c) * taps + tap]; }
     else if (c < j.cout) v = j.w[((long)c * j.cin + r) * taps + (taps - 1 - tap)];
   }
-  j.wk[i] = v;
+  if (j.mode & 16) reinterpret_cast<__bf16*>(j.wk)[i] = static_cast<__bf16>(v);
+  else j.wk[i] = v;
 }
 
 // jobs: device array of njobs seg_pack_job, sorted by blk0, job k owning blocks

@@ -21,7 +21,7 @@ __device__ __attribute__((aligned(16))) float g_zero4[4];
 
 struct IgemmArgs {
   const void* in; long ldin;     // IT (activation storage type: float, or __bf16 for the _bf16io path)
-  const float* wk; int ldk;      // packed weights [Cout][ldk], k contiguous
+  const void* wk; int ldk;       // packed weights [Cout][ldk], k contiguous: fp32, or bf16 (WB: ldk % 8 == 0)
   const float* bias;             // [Cout] or nullptr
   const void* add; long ldadd;   // optional addend [M][ldadd] (may alias out), IT
   void* out; long ldout;         // IT
@@ -72,8 +72,17 @@ struct IgemmArgs {
 // pitch at BK 32, so the ds_read_b128 fragment reads (lane half h: k = 16ks + 8h .. +7)
 // stay conflict-free; the epilogue (bias, BN statistics, addend) is the fp32 one.
 // IT = activation storage type of in / add / out (float, or __bf16: the bf16io path).
-template <int BM, int BN, int WM, int WN, int KS, int BK, bool UT, typename OT = float, typename IT = float>
+// WB: the packed weights are already bf16 (seg_pack_batch bf16 modes): 8 k values per
+// 16-byte B slot copied to LDS as is -- half the weight bytes of the fp32 pack, which every
+// M tile re-reads from L2 (2 x 1.6 GB per launch of the deep decoder convs at bs=32), and
+// no conversion on the way into LDS.  Bitwise the fp32-weight kernel: the RNE rounding
+// is the same, done once at pack time.
+template <int BM, int BN, int WM, int WN, int KS, int BK, bool UT, typename OT = float, typename IT = float,
+          bool WB = false>
 __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void igemm_conv_kernel(IgemmArgs a) {
+  static_assert(!WB || std::is_same<OT, __bf16>::value, "bf16 weights feed bf16 operands");
+  const float* wk32 = static_cast<const float*>(a.wk);
+  const __bf16* wk16 = static_cast<const __bf16*>(a.wk);
   const IT* __restrict__ in = static_cast<const IT*>(a.in);
   const IT* add = static_cast<const IT*>(a.add);
   IT* out = static_cast<IT*>(a.out);
@@ -84,7 +93,8 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void igemm_conv_kernel(
   using lds_t = OT;
   typedef OT ot4 __attribute__((ext_vector_type(4)));
   typedef OT ot8 __attribute__((ext_vector_type(8)));
-  constexpr int KQ = BK / 4;          // float4 groups per tile row (B operand: fp32 packed weights)
+  constexpr int VB = WB ? 8 : 4;      // k values per B slot (fp32 packed weights: 4, bf16: 8)
+  constexpr int KQ = BK / VB;         // B slots per tile row
   // A operand on bf16 storage (uniform-tap loader): 8 channels = one 16-byte load per
   // slot, copied to LDS as is (it already is the operand type); otherwise 4 channels
   constexpr int VA = (sizeof(IT) == 2 && UT) ? 8 : 4;
@@ -154,7 +164,7 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void igemm_conv_kernel(
   long u_aoff[A_PER], u_boff[B_PER];
   unsigned u_mask[A_PER];
   bool u_bok[B_PER];
-  const int u_kq4 = (tid % KQ) * 4;
+  const int u_kq4 = (tid % KQ) * VB;
   const int u_kqa = (tid % KQA) * VA;  // this thread's A channel offset in a K chunk
   // input transform: the loaded chunk's channel for this thread's A slots (-1: beyond K)
   // and its coefficients, fetched with the chunk so store_tiles does not wait on them
@@ -231,7 +241,13 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void igemm_conv_kernel(
       }
       const bool kin = k0 + u_kq4 < a.K;
 #pragma unroll
-      for (int i = 0; i < B_PER; ++i) rb[i] = ld4(u_bok[i] && kin ? a.wk + u_boff[i] + k0 : g_zero4);
+      for (int i = 0; i < B_PER; ++i) {
+        if constexpr (WB)
+          rb[i] = *reinterpret_cast<const f32x4*>(u_bok[i] && kin ? (const void*)(wk16 + u_boff[i] + k0)
+                                                                  : (const void*)g_zero4);
+        else
+          rb[i] = ld4(u_bok[i] && kin ? wk32 + u_boff[i] + k0 : g_zero4);
+      }
       u_ci += BK;
       if (u_ci >= a.Cin) {
         u_ci -= a.Cin;
@@ -269,9 +285,12 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void igemm_conv_kernel(
     for (int i = 0; i < B_PER; ++i) {
       const int idx = tid + i * NT;
       const int row = idx / KQ, kq = idx % KQ;
-      const int co = n0 + row, k = k0 + kq * 4;
+      const int co = n0 + row, k = k0 + kq * VB;
       f32x4 v = {0.f, 0.f, 0.f, 0.f};
-      if (idx < B_VEC && co < a.Cout && k < a.K) v = ld4(a.wk + (long)co * a.ldk + k);
+      if (idx < B_VEC && co < a.Cout && k < a.K) {
+        if constexpr (WB) v = *reinterpret_cast<const f32x4*>(wk16 + (long)co * a.ldk + k);
+        else v = ld4(wk32 + (long)co * a.ldk + k);
+      }
       rb[i] = v;
     }
   };
@@ -310,7 +329,12 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void igemm_conv_kernel(
 #pragma unroll
     for (int i = 0; i < B_PER; ++i) {
       const int idx = tid + i * NT;
-      if (B_VEC % NT == 0 || idx < B_VEC) st_op(&Bs[buf][(idx / KQ) * LDSR + (idx % KQ) * 4], rb[i]);
+      if (B_VEC % NT == 0 || idx < B_VEC) {
+        if constexpr (WB)  // 8 bf16 as stored by the pack
+          *reinterpret_cast<f32x4*>(&Bs[buf][(idx / KQ) * LDSR + (idx % KQ) * 8]) = rb[i];
+        else
+          st_op(&Bs[buf][(idx / KQ) * LDSR + (idx % KQ) * 4], rb[i]);
+      }
     }
   };
 
@@ -560,7 +584,7 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void igemm_conv_kernel(
   }
 }
 
-template <int BM, int BN, int WM, int WN, int BK, typename OT, typename IT>
+template <int BM, int BN, int WM, int WN, int BK, typename OT, typename IT, bool WB = false>
 int launch_igemm_bk(const IgemmArgs& a, int ks, hipStream_t s) {
   const int grid = seg_cdiv(a.M, BM) * seg_cdiv(a.Cout, BN);
   const int splits = seg_cdiv(a.K, a.kchunk);
@@ -568,7 +592,7 @@ int launch_igemm_bk(const IgemmArgs& a, int ks, hipStream_t s) {
                   (sizeof(IT) == 4 || (a.Cin % 8 == 0 && a.ldin % 8 == 0));  // bf16 A: 16-byte slots
   constexpr int NT = 64 * (BM / WM) * (BN / WN);
   if (a.xs && (!ut || ks != 1)) return (int)hipErrorInvalidValue;  // input transform: 1x1 uniform-tap loader only
-#define SEG_IG(KS, U) hipLaunchKernelGGL((igemm_conv_kernel<BM, BN, WM, WN, KS, BK, U, OT, IT>), dim3(grid, splits), dim3(NT), 0, s, a)
+#define SEG_IG(KS, U) hipLaunchKernelGGL((igemm_conv_kernel<BM, BN, WM, WN, KS, BK, U, OT, IT, WB>), dim3(grid, splits), dim3(NT), 0, s, a)
   if (ks == 1) {
     if (ut) SEG_IG(1, true); else SEG_IG(1, false);
   } else {
@@ -584,7 +608,7 @@ int launch_igemm_bk(const IgemmArgs& a, int ks, hipStream_t s) {
 inline int igemm_bk(int K) { return (SEG_IGEMM_BK != 16 && (K <= 64 || (K % SEG_IGEMM_BK != 0 && K < 512))) ? 16 : SEG_IGEMM_BK; }
 
 // split-K: `splits` K ranges of whole BK chunks (a.part set by the caller when splits > 1)
-template <int BM, int BN, int WM, int WN, typename OT = float, typename IT = float>
+template <int BM, int BN, int WM, int WN, typename OT = float, typename IT = float, bool WB = false>
 int launch_igemm(IgemmArgs a, int ks, int splits, hipStream_t s) {
   int bk = igemm_bk(a.K);
   // 16-bit operands: 64-deep K chunks (4 MFMA k-steps per barrier) where the uniform-tap
@@ -595,10 +619,10 @@ int launch_igemm(IgemmArgs a, int ks, int splits, hipStream_t s) {
   const int nk = seg_cdiv(a.K, bk);
   a.kchunk = seg_cdiv(nk, splits) * bk;
   if constexpr (sizeof(OT) == 2) {
-    if (bk == 64) return launch_igemm_bk<BM, BN, WM, WN, 64, OT, IT>(a, ks, s);
+    if (bk == 64) return launch_igemm_bk<BM, BN, WM, WN, 64, OT, IT, WB>(a, ks, s);
   }
-  if (bk == 16) return launch_igemm_bk<BM, BN, WM, WN, 16, OT, IT>(a, ks, s);
-  return launch_igemm_bk<BM, BN, WM, WN, SEG_IGEMM_BK, OT, IT>(a, ks, s);
+  if (bk == 16) return launch_igemm_bk<BM, BN, WM, WN, 16, OT, IT, WB>(a, ks, s);
+  return launch_igemm_bk<BM, BN, WM, WN, SEG_IGEMM_BK, OT, IT, WB>(a, ks, s);
 }
 
 struct TileCfg {
@@ -671,13 +695,14 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restr
   }
 }
 
-template <typename OT, typename IT = float>
-int conv_igemm_impl(const IT* in, long ldin, int N, int H, int W, int Cin, const float* wk, int ldk,
+template <typename OT, typename IT = float, bool WB = false>
+int conv_igemm_impl(const IT* in, long ldin, int N, int H, int W, int Cin, const void* wk, int ldk,
                     const float* bias, IT* out, long ldout, int Ho, int Wo, int Cout, int ks, int stride, int pad,
                     const IT* add, long ldadd, float* stat, int act, float* work, int splits, hipStream_t stream,
                     const float* xs = nullptr, const float* xb = nullptr, int xact = 0) {
   if (!std::is_same<IT, float>::value && splits != 1) return (int)hipErrorInvalidValue;
   if ((Cin & 3) || (ldin & 3) || (ldk & 3) || (ks != 1 && ks != 3)) return (int)hipErrorInvalidValue;
+  if (WB && ((ldk & 7) || ((uintptr_t)wk & 15) || splits != 1)) return (int)hipErrorInvalidValue;
   if (xs && (!xb || ks != 1 || splits != 1 || SEG_IGEMM_STAGES != 1 || xact < SEG_ACT_NONE || xact > SEG_ACT_RELU6))
     return (int)hipErrorInvalidValue;
   if (ks == 1 && (stride != 1 || pad != 0 || Ho != H || Wo != W)) return (int)hipErrorInvalidValue;
@@ -693,21 +718,21 @@ int conv_igemm_impl(const IT* in, long ldin, int N, int H, int W, int Cin, const
   if (a.M == 0 || Cout == 0) return 0;
   int rc;
   switch (pick_tile(a.M, Cout)) {
-    case 0: rc = launch_igemm<128, 128, 64, 64, OT, IT>(a, ks, splits, stream); break;
-    case 1: rc = launch_igemm<64, 128, 32, 64, OT, IT>(a, ks, splits, stream); break;
-    case 2: rc = launch_igemm<128, 64, 64, 32, OT, IT>(a, ks, splits, stream); break;
-    case 3: rc = launch_igemm<64, 64, 32, 32, OT, IT>(a, ks, splits, stream); break;
-    case 4: rc = launch_igemm<128, 96, 32, 96, OT, IT>(a, ks, splits, stream); break;
-    case 5: rc = launch_igemm<128, 160, 32, 160, OT, IT>(a, ks, splits, stream); break;
-    case 6: rc = launch_igemm<256, 32, 64, 32, OT, IT>(a, ks, splits, stream); break;
-    case 7: rc = launch_igemm<128, 32, 32, 32, OT, IT>(a, ks, splits, stream); break;
-    case 8: rc = launch_igemm<128, 128, 64, 32, OT, IT>(a, ks, splits, stream); break;
-    case 9: rc = launch_igemm<128, 128, 32, 64, OT, IT>(a, ks, splits, stream); break;
-    case 10: rc = launch_igemm<256, 128, 64, 64, OT, IT>(a, ks, splits, stream); break;
-    case 11: rc = launch_igemm<128, 256, 64, 64, OT, IT>(a, ks, splits, stream); break;
-    case 12: rc = launch_igemm<128, 64, 32, 32, OT, IT>(a, ks, splits, stream); break;
-    case 13: rc = launch_igemm<256, 64, 64, 32, OT, IT>(a, ks, splits, stream); break;
-    default: rc = launch_igemm<64, 128, 32, 32, OT, IT>(a, ks, splits, stream); break;
+    case 0: rc = launch_igemm<128, 128, 64, 64, OT, IT, WB>(a, ks, splits, stream); break;
+    case 1: rc = launch_igemm<64, 128, 32, 64, OT, IT, WB>(a, ks, splits, stream); break;
+    case 2: rc = launch_igemm<128, 64, 64, 32, OT, IT, WB>(a, ks, splits, stream); break;
+    case 3: rc = launch_igemm<64, 64, 32, 32, OT, IT, WB>(a, ks, splits, stream); break;
+    case 4: rc = launch_igemm<128, 96, 32, 96, OT, IT, WB>(a, ks, splits, stream); break;
+    case 5: rc = launch_igemm<128, 160, 32, 160, OT, IT, WB>(a, ks, splits, stream); break;
+    case 6: rc = launch_igemm<256, 32, 64, 32, OT, IT, WB>(a, ks, splits, stream); break;
+    case 7: rc = launch_igemm<128, 32, 32, 32, OT, IT, WB>(a, ks, splits, stream); break;
+    case 8: rc = launch_igemm<128, 128, 64, 32, OT, IT, WB>(a, ks, splits, stream); break;
+    case 9: rc = launch_igemm<128, 128, 32, 64, OT, IT, WB>(a, ks, splits, stream); break;
+    case 10: rc = launch_igemm<256, 128, 64, 64, OT, IT, WB>(a, ks, splits, stream); break;
+    case 11: rc = launch_igemm<128, 256, 64, 64, OT, IT, WB>(a, ks, splits, stream); break;
+    case 12: rc = launch_igemm<128, 64, 32, 32, OT, IT, WB>(a, ks, splits, stream); break;
+    case 13: rc = launch_igemm<256, 64, 64, 32, OT, IT, WB>(a, ks, splits, stream); break;
+    default: rc = launch_igemm<64, 128, 32, 32, OT, IT, WB>(a, ks, splits, stream); break;
   }
   if (rc || splits == 1) return rc;
   const long total = (long)a.M * Cout;

@@ -53,6 +53,10 @@ IGNORE_INDEX = -100
 _ROW_TILES = {}  # (M, Cout) -> (row tiles, tile height) of seg_conv_igemm
 
 
+def r8(c: int) -> int:
+    return (c + 7) & ~7
+
+
 def r4(c: int) -> int:
     return (c + 3) & ~3
 
@@ -155,6 +159,8 @@ class ConvOp:
         self.halo_f = self.halo_d = False
         # bf16 math (Program.math == "bf16"): seg_conv_igemm_bf16 / seg_conv_wgrad_bf16
         self.bf = False
+        # bf16io: wk_f / wk_d packed as bf16 for seg_conv_igemm_bf16io_w16 (Program._build_pack)
+        self.w16_f = self.w16_d = False
         self.ks = conv.kernel_size[0]
         self.stride = conv.stride[0]
         self.pad = conv.padding[0]
@@ -211,11 +217,14 @@ class ConvOp:
                             work.data_ptr(), s)
             elif self.xform is not None:  # 1x1 conv applying its producer's lazy BN on load
                 name = "seg_conv_igemm_bf16io_xf" if rt.io else "seg_conv_igemm_bf16_xf" if self.bf else "seg_conv_igemm_xf"
+                if rt.io and self.w16_f:
+                    name += "_w16"
                 rt.tcall("igemm1_fwd", self.flops(), name, rt.ptr(i), i.ld, i.N, i.H, i.W, self.cin_pad, wk_ptr, ldk,
                          bias, rt.ptr(y), y.ld, y.H, y.W, self.cout, self.ks, self.stride, self.pad, None, 0, statp,
                          *self._in_xform(rt), s)
             elif rt.io:
-                rt.tcall(f"igemm{self.ks}_fwd", self.flops(), "seg_conv_igemm_bf16io", rt.ptr(i), i.ld, i.N, i.H,
+                rt.tcall(f"igemm{self.ks}_fwd", self.flops(),
+                         "seg_conv_igemm_bf16io_w16" if self.w16_f else "seg_conv_igemm_bf16io", rt.ptr(i), i.ld, i.N, i.H,
                             i.W, self.cin_pad, wk_ptr, ldk, bias, rt.ptr(y), y.ld, y.H, y.W, self.cout, self.ks,
                             self.stride, self.pad, None, 0, statp, s)
             elif self.bf:
@@ -383,7 +392,8 @@ class ConvOp:
                             self.wk_wd.data_ptr(), kin, None, rt.gptr(i), i.ld, self.cin, add_ptr, add_ld, None,
                             work.data_ptr(), s)
             elif rt.io:
-                rt.tcall(f"igemm{self.ks}_dgrad", self.flops(), "seg_conv_igemm_bf16io", dYp, dY.ld, y.N, y.H, y.W,
+                rt.tcall(f"igemm{self.ks}_dgrad", self.flops(),
+                         "seg_conv_igemm_bf16io_w16" if self.w16_d else "seg_conv_igemm_bf16io", dYp, dY.ld, y.N, y.H, y.W,
                             kin, self.wk_d.data_ptr(), self.ldk_d, None, rt.gptr(i), i.ld, i.H, i.W, self.cin,
                             self.ks, 1, self.pad, add_ptr, add_ld, None, s)
             elif self.bf:
@@ -527,16 +537,24 @@ class Program:
                                  and bool(query("seg_conv_halo_pick", y.N, y.H, y.W, op.cin_pad, op.cout)))
                     op.halo_d = (not op.first and r4(op.cout) % 8 == 0 and HALO_BF16
                                  and bool(query("seg_conv_halo_pick", y.N, y.H, y.W, r4(op.cout), op.cin)))
-                if not (op.ks == 1 and op.cin_pad == op.cin):
-                    op.ldk_f = r4(op.ks * op.ks * op.cin_pad)
-                    op.wk_f = torch.empty(op.cout * op.ldk_f, device=dev, dtype=torch.float32)
-                    jobs.append((w.data_ptr(), op.wk_f.data_ptr(), op.cout, op.cin, op.ks, op.ldk_f, 0, op.cin_pad))
+                # bf16io implicit-GEMM launches take bf16 packed weights (seg_conv_igemm_bf16io_w16: half the
+                # weight bytes every M tile re-reads); the LDS-halo kernel keeps the fp32 pack
+                w16f = self.math == "bf16io" and W16 and not op.halo_f
+                w16d = self.math == "bf16io" and W16 and not op.halo_d
+                op.w16_f, op.w16_d = w16f, w16d
+                if w16f or not (op.ks == 1 and op.cin_pad == op.cin):
+                    op.ldk_f = r8(op.ks * op.ks * op.cin_pad) if w16f else r4(op.ks * op.ks * op.cin_pad)
+                    op.wk_f = torch.empty(op.cout * op.ldk_f, device=dev,
+                                          dtype=torch.bfloat16 if w16f else torch.float32)
+                    jobs.append((w.data_ptr(), op.wk_f.data_ptr(), op.cout, op.cin, op.ks, op.ldk_f, 16 if w16f else 0,
+                                 op.cin_pad))
                     max_elems = max(max_elems, op.cout * op.ldk_f)
                 if not op.first:
                     kin = r4(op.cout)
-                    op.ldk_d = r4(op.ks * op.ks * kin)
-                    op.wk_d = torch.empty(op.cin * op.ldk_d, device=dev, dtype=torch.float32)
-                    jobs.append((w.data_ptr(), op.wk_d.data_ptr(), op.cout, op.cin, op.ks, op.ldk_d, 1, kin))
+                    op.ldk_d = r8(op.ks * op.ks * kin) if w16d else r4(op.ks * op.ks * kin)
+                    op.wk_d = torch.empty(op.cin * op.ldk_d, device=dev, dtype=torch.bfloat16 if w16d else torch.float32)
+                    jobs.append((w.data_ptr(), op.wk_d.data_ptr(), op.cout, op.cin, op.ks, op.ldk_d, 17 if w16d else 1,
+                                 kin))
                     max_elems = max(max_elems, op.cin * op.ldk_d)
                 continue
             wino_ok = op.ks == 3 and op.stride == 1 and op.pad == 1
@@ -649,7 +667,7 @@ def pack_table(jobs, device):
     import numpy as np
     rows, blk = [], 0
     for (w, wk, cout, cin, ks, ldk, mode, kin) in jobs:
-        elems = 9 * cout if mode == 2 else (cout if mode in (0, 3) else cin) * ldk
+        elems = 9 * cout if mode == 2 else (cout if (mode & 15) in (0, 3) else cin) * ldk
         nblk = max(1, (elems + 255) // 256)
         rows.append((w, wk, cout, cin, ks, ldk, mode, kin, blk, nblk))
         blk += nblk
@@ -1077,6 +1095,8 @@ HALO_BF16 = os.environ.get("SEG_HALO_BF16", "1") == "1"
 # lazy BatchNorm for 1x1 consumers (the inverted residuals' project convs, OutConv's last
 # conv): SEG_LAZY_PW=0 keeps the separate BN-apply pass (read at program build)
 LAZY_PW = os.environ.get("SEG_LAZY_PW", "1") == "1"
+# bf16io implicit GEMMs on bf16-packed weights (seg_conv_igemm_bf16io_w16); SEG_W16=0 keeps the fp32 packs
+W16 = os.environ.get("SEG_W16", "1") == "1"
 # fork the weight-gradient side stream after the layer's data gradient (measured: f32 +1.5 %, bf16io +-0)
 FORK_LATE = os.environ.get("SEG_FORK_LATE", "1") == "1"
 _SIDE = {}

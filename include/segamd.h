@@ -384,6 +384,10 @@ int seg_conv_igemm_bf16io_xf_w16(const seg_bf16* in, long ldin, int N, int H, in
     int ldk, const float* bias, seg_bf16* out, long ldout, int Ho, int Wo, int Cout, int ks, int stride, int pad,
     const seg_bf16* add, long ldadd, float* stat, const float* in_scale, const float* in_shift, int in_act,
     hipStream_t stream);
+/* seg_conv_halo_bf16io with bf16-packed weights (mode | 16, ldk % 8 == 0): bitwise the same. */
+int seg_conv_halo_bf16io_w16(const seg_bf16* in, long ldin, int N, int H, int W, int Cin, const seg_bf16* wk,
+    int ldk, const float* bias, seg_bf16* out, long ldout, int Cout, const seg_bf16* add, long ldadd, float* stat,
+    hipStream_t stream);
 int seg_conv_halo_bf16io(const seg_bf16* in, long ldin, int N, int H, int W, int Cin, const float* wk, int ldk,
     const float* bias, seg_bf16* out, long ldout, int Cout, const seg_bf16* add, long ldadd, float* stat,
     hipStream_t stream);

@@ -27,7 +27,7 @@ __device__ __attribute__((aligned(16))) float g_hzero4[4];
 
 struct HaloArgs {
   const void* in; long ldin;     // T (float, or __bf16 on the bf16io path)
-  const float* wk; int ldk;      // packed [Cout][ldk], k = tap*Cin + ci (seg_pack_conv_weight mode 0/1)
+  const void* wk; int ldk;       // packed [Cout][ldk], k = tap*Cin + ci (seg_pack_batch mode 0/1; fp32, or bf16: WB)
   const float* bias;
   const void* add; long ldadd;   // T
   void* out; long ldout;         // T
@@ -40,8 +40,14 @@ struct HaloArgs {
 // bf16 operands in LDS (the halo copied as is, 8 channels per 16-byte slot; weights
 // rounded on the way in), 32-deep K chunks and v_mfma_f32_32x32x16_bf16 with fp32
 // accumulation; the fp32 epilogue rounds once on the store.
-template <int NI, typename T = float>  // output-channel blocks of 32 (Cout padded to 32*NI)
+// WB: bf16-packed weights (mode | 16), 8 per 16-byte slot copied to LDS as is -- every
+// 256-pixel tile re-reads all 9 x Cout x Cin weights, so this halves the kernel's L2
+// weight traffic; bitwise the fp32-weight launch (the same RNE rounding, done at pack time).
+template <int NI, typename T = float, bool WB = false>  // output-channel blocks of 32 (Cout padded to 32*NI)
 __global__ __launch_bounds__(256) void halo3x3_kernel(HaloArgs a) {
+  static_assert(!WB || sizeof(T) == 2, "bf16 weights: the bf16io kernel");
+  const float* wk32 = static_cast<const float*>(a.wk);
+  const __bf16* wk16 = static_cast<const __bf16*>(a.wk);
   constexpr bool LP = sizeof(T) == 2;
   constexpr int BK = LP ? 32 : 16;                 // K chunk (input channels)
   constexpr int LDSR = LP ? BK + 8 : BK + 4;       // LDS row stride (elements): conflict-free b128 reads
@@ -49,7 +55,8 @@ __global__ __launch_bounds__(256) void halo3x3_kernel(HaloArgs a) {
   constexpr int HALO_VEC = HH * HW * (BK / HV);    // slots of a halo chunk
   constexpr int HALO_PER = (HALO_VEC + 255) / 256;
   constexpr int BNC = 32 * NI;
-  constexpr int W_VEC = 9 * BNC * (BK / 4);
+  constexpr int WV = WB ? 8 : 4;                   // weights per load slot
+  constexpr int W_VEC = 9 * BNC * (BK / WV);
   constexpr int W_PER = (W_VEC + 255) / 256;
   using lds_t = T;
   __shared__ __attribute__((aligned(16))) lds_t Hs[HH * HW * LDSR];
@@ -85,10 +92,10 @@ __global__ __launch_bounds__(256) void halo3x3_kernel(HaloArgs a) {
 #pragma unroll
   for (int i = 0; i < W_PER; ++i) {
     const int s = tid + i * 256;
-    const int row = s / (BK / 4), q = s % (BK / 4);  // row = tap * BNC + co
+    const int row = s / (BK / WV), q = s % (BK / WV);  // row = tap * BNC + co
     const int tap = row / BNC, co = row % BNC;
     wok[i] = s < W_VEC && co < a.Cout;
-    woff[i] = wok[i] ? (long)co * a.ldk + tap * a.Cin + q * 4 : 0;
+    woff[i] = wok[i] ? (long)co * a.ldk + tap * a.Cin + q * WV : 0;
   }
 
   f32x4 rh[HALO_PER], rw[W_PER];
@@ -104,8 +111,12 @@ __global__ __launch_bounds__(256) void halo3x3_kernel(HaloArgs a) {
     }
 #pragma unroll
     for (int i = 0; i < W_PER; ++i) {
-      const int q4 = ((tid + i * 256) % (BK / 4)) * 4;
-      rw[i] = ld4(wok[i] && c0 + q4 < a.Cin ? a.wk + woff[i] + c0 : g_hzero4);
+      const int q4 = ((tid + i * 256) % (BK / WV)) * WV;
+      if constexpr (WB)
+        rw[i] = *reinterpret_cast<const f32x4*>(wok[i] && c0 + q4 < a.Cin ? (const void*)(wk16 + woff[i] + c0)
+                                                                           : (const void*)g_hzero4);
+      else
+        rw[i] = ld4(wok[i] && c0 + q4 < a.Cin ? wk32 + woff[i] + c0 : g_hzero4);
     }
   };
   auto store = [&]() {
@@ -119,8 +130,9 @@ __global__ __launch_bounds__(256) void halo3x3_kernel(HaloArgs a) {
     for (int i = 0; i < W_PER; ++i) {
       const int s = tid + i * 256;
       if (W_VEC % 256 == 0 || s < W_VEC) {
-        lds_t* p = &Ws[(s / (BK / 4)) * LDSR + (s % (BK / 4)) * 4];
-        if constexpr (LP) *reinterpret_cast<bf16x4*>(p) = __builtin_convertvector(rw[i], bf16x4);
+        lds_t* p = &Ws[(s / (BK / WV)) * LDSR + (s % (BK / WV)) * WV];
+        if constexpr (WB) *reinterpret_cast<f32x4*>(p) = rw[i];  // 8 bf16 as packed
+        else if constexpr (LP) *reinterpret_cast<bf16x4*>(p) = __builtin_convertvector(rw[i], bf16x4);
         else *reinterpret_cast<f32x4*>(p) = rw[i];
       }
     }
@@ -269,20 +281,21 @@ SEG_API int seg_conv_halo_row_tiles(int N, int H, int W) { return N * (H / TH) *
 
 // out = conv3x3(in, W) (+bias) (+add), stride 1, pad 1; wk packed by
 // seg_pack_conv_weight (mode 0 forward / mode 1 data gradient), ldk >= 9*Cin.
-template <typename T>
-static int conv_halo_impl(const T* in, long ldin, int N, int H, int W, int Cin, const float* wk, int ldk,
+template <typename T, bool WB = false>
+static int conv_halo_impl(const T* in, long ldin, int N, int H, int W, int Cin, const void* wk, int ldk,
                           const float* bias, T* out, long ldout, int Cout, const T* add, long ldadd, float* stat,
                           hipStream_t stream) {
   if (!seg_conv_halo_ok(N, H, W, Cin, Cout) || (ldin & 3) || (ldk & 3) || ldk < 9 * Cin) return (int)hipErrorInvalidValue;
   if (sizeof(T) == 2 && ((Cin & 7) || (ldin & 7))) return (int)hipErrorInvalidValue;  // 16-byte bf16 halo slots
+  if (WB && ((ldk & 7) || ((uintptr_t)wk & 15))) return (int)hipErrorInvalidValue;    // 16-byte bf16 weight slots
   HaloArgs a;
   a.in = in; a.ldin = ldin; a.wk = wk; a.ldk = ldk; a.bias = bias; a.add = add; a.ldadd = ldadd;
   a.out = out; a.ldout = ldout; a.stat = stat; a.N = N; a.H = H; a.W = W; a.Cin = Cin; a.Cout = Cout;
   a.tiles_w = W / TW; a.tiles_h = H / TH;
   const int grid = N * a.tiles_h * a.tiles_w;
-  if (Cout <= 32) hipLaunchKernelGGL((halo3x3_kernel<1, T>), dim3(grid), dim3(256), 0, stream, a);
-  else if (Cout <= 64) hipLaunchKernelGGL((halo3x3_kernel<2, T>), dim3(grid), dim3(256), 0, stream, a);
-  else hipLaunchKernelGGL((halo3x3_kernel<3, T>), dim3(grid), dim3(256), 0, stream, a);
+  if (Cout <= 32) hipLaunchKernelGGL((halo3x3_kernel<1, T, WB>), dim3(grid), dim3(256), 0, stream, a);
+  else if (Cout <= 64) hipLaunchKernelGGL((halo3x3_kernel<2, T, WB>), dim3(grid), dim3(256), 0, stream, a);
+  else hipLaunchKernelGGL((halo3x3_kernel<3, T, WB>), dim3(grid), dim3(256), 0, stream, a);
   SEG_RET_LAST();
 }
 
@@ -299,4 +312,13 @@ SEG_API int seg_conv_halo_bf16io(const __bf16* in, long ldin, int N, int H, int 
                                  const float* bias, __bf16* out, long ldout, int Cout, const __bf16* add, long ldadd,
                                  float* stat, hipStream_t stream) {
   return conv_halo_impl(in, ldin, N, H, W, Cin, wk, ldk, bias, out, ldout, Cout, add, ldadd, stat, stream);
+}
+
+// seg_conv_halo_bf16io with bf16-packed weights (seg_pack_batch mode | 16; ldk % 8 == 0,
+// 16-byte aligned): bitwise the fp32-weight launch, half the weight traffic.
+SEG_API int seg_conv_halo_bf16io_w16(const __bf16* in, long ldin, int N, int H, int W, int Cin, const __bf16* wk,
+                                     int ldk, const float* bias, __bf16* out, long ldout, int Cout, const __bf16* add,
+                                     long ldadd, float* stat, hipStream_t stream) {
+  return conv_halo_impl<__bf16, true>(in, ldin, N, H, W, Cin, wk, ldk, bias, out, ldout, Cout, add, ldadd, stat,
+                                      stream);
 }

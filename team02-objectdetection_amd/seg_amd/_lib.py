@@ -101,6 +101,7 @@ for _n in ("seg_conv_igemm", "seg_conv_wgrad"):
         PROTOTYPES[_n + _sfx] = (_r, _a[:-1] + [_V, _V, _I, _V])
 PROTOTYPES["seg_conv_halo_bf16io"] = PROTOTYPES["seg_conv_halo"]
 PROTOTYPES["seg_conv_igemm_bf16io_w16"] = PROTOTYPES["seg_conv_igemm"]
+PROTOTYPES["seg_conv_halo_bf16io_w16"] = PROTOTYPES["seg_conv_halo"]
 PROTOTYPES["seg_conv_igemm_bf16io_xf_w16"] = PROTOTYPES["seg_conv_igemm_bf16io_xf"]
 
 _lock = threading.Lock()

@@ -208,7 +208,8 @@ class ConvOp:
                 stat = rt.tmp(ntiles * 2 * self.cout)
             statp = stat.data_ptr() if stat is not None else None
             if self.halo_f:
-                rt.tcall("igemm3_fwd", self.flops(), rt.k("seg_conv_halo"), rt.ptr(i), i.ld, i.N, i.H, i.W, self.cin_pad,
+                rt.tcall("igemm3_fwd", self.flops(), rt.k("seg_conv_halo") + ("_w16" if self.w16_f else ""), rt.ptr(i),
+                         i.ld, i.N, i.H, i.W, self.cin_pad,
                             wk_ptr, ldk, bias, rt.ptr(y), y.ld, self.cout, None, 0, statp, s)
             elif self.wino_f:
                 work = rt.tmp(16 * (y.M // 4) * self.cout)
@@ -384,7 +385,8 @@ class ConvOp:
             kin = r4(self.cout)  # dY channels padded to 4 (the C=10 head)
             add_ptr, add_ld = rt.begin_write_add(i)
             if self.halo_d:
-                rt.tcall("igemm3_dgrad", self.flops(), rt.k("seg_conv_halo"), dYp, dY.ld, y.N, y.H, y.W, kin,
+                rt.tcall("igemm3_dgrad", self.flops(), rt.k("seg_conv_halo") + ("_w16" if self.w16_d else ""), dYp,
+                         dY.ld, y.N, y.H, y.W, kin,
                             self.wk_d.data_ptr(), self.ldk_d, None, rt.gptr(i), i.ld, self.cin, add_ptr, add_ld, None, s)
             elif self.wino_d:
                 work = rt.tmp(16 * (y.M // 4) * self.cin)
@@ -537,10 +539,9 @@ class Program:
                                  and bool(query("seg_conv_halo_pick", y.N, y.H, y.W, op.cin_pad, op.cout)))
                     op.halo_d = (not op.first and r4(op.cout) % 8 == 0 and HALO_BF16
                                  and bool(query("seg_conv_halo_pick", y.N, y.H, y.W, r4(op.cout), op.cin)))
-                # bf16io implicit-GEMM launches take bf16 packed weights (seg_conv_igemm_bf16io_w16: half the
-                # weight bytes every M tile re-reads); the LDS-halo kernel keeps the fp32 pack
-                w16f = self.math == "bf16io" and W16 and not op.halo_f
-                w16d = self.math == "bf16io" and W16 and not op.halo_d
+                # bf16io implicit-GEMM and LDS-halo launches take bf16 packed weights (seg_conv_*_bf16io_w16:
+                # half the weight bytes every M tile / pixel tile re-reads)
+                w16f = w16d = self.math == "bf16io" and W16
                 op.w16_f, op.w16_d = w16f, w16d
                 if w16f or not (op.ks == 1 and op.cin_pad == op.cin):
                     op.ldk_f = r8(op.ks * op.ks * op.cin_pad) if w16f else r4(op.ks * op.ks * op.cin_pad)

@@ -118,3 +118,28 @@ def test_w16_rejects_unaligned_ldk():
     with pytest.raises(SegLibError):
         call("seg_conv_igemm_bf16io_w16", x.data_ptr(), 16, 1, 8, 8, 16, wk.data_ptr(), 20, None, out.data_ptr(), 16,
              8, 8, 16, 1, 1, 0, None, 0, None, s)
+
+
+@pytest.mark.parametrize("N,Cin,Cout,H,W,mode", [(2, 80, 32, 8, 64, 0), (1, 152, 64, 4, 128, 0), (1, 32, 80, 8, 64, 1),
+                                                 (1, 64, 64, 4, 64, 1)])
+def test_halo_w16_equals_fp32_weights(N, Cin, Cout, H, W, mode):
+    """seg_conv_halo_bf16io_w16 == seg_conv_halo_bf16io (forward pack mode 0, data-gradient pack mode 1)."""
+    s = S()
+    w = (torch.randn(Cout, Cin, 3, 3, generator=torch.Generator().manual_seed(9)) * 0.1).to(DEV)
+    if mode == 0:
+        cin_k, cout_k, kin = Cin, Cout, Cin
+    else:   # data gradient: dY (Cout channels) -> dX (Cin channels)
+        cin_k, cout_k, kin = r4(Cout), Cin, r4(Cout)
+    w32, ld4, w16, ld8 = packs(w, Cout, Cin, 3, kin, mode)
+    x = rows(N * H * W, cin_k, 10)
+    b = torch.randn(cout_k, generator=torch.Generator().manual_seed(11)).to(DEV) if mode == 0 else None
+    ntiles = query("seg_conv_halo_row_tiles", N, H, W)
+    outs = {}
+    for tag, name, wk, ld in (("f", "seg_conv_halo_bf16io", w32, ld4), ("h", "seg_conv_halo_bf16io_w16", w16, ld8)):
+        o = torch.empty(N * H * W, cout_k, device=DEV, dtype=BF)
+        st = torch.empty(ntiles * 2 * cout_k, device=DEV)
+        call(name, x.data_ptr(), cin_k, N, H, W, cin_k, wk.data_ptr(), ld, b.data_ptr() if b is not None else None,
+             o.data_ptr(), cout_k, cout_k, None, 0, st.data_ptr(), s)
+        outs[tag] = (o, st)
+    torch.cuda.synchronize()
+    assert torch.equal(outs["f"][0], outs["h"][0]) and torch.equal(outs["f"][1], outs["h"][1])

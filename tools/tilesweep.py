@@ -53,7 +53,7 @@ def main():
     ap.add_argument("--batch", type=int, default=32)
     ap.add_argument("--height", type=int, default=256)
     ap.add_argument("--width", type=int, default=512)
-    ap.add_argument("--math", choices=("f32", "bf16"), default="f32")
+    ap.add_argument("--math", choices=("f32", "bf16", "bf16io"), default="f32")
     a = ap.parse_args()
     lib()
     model = getattr(seg_amd, a.model)(10)
@@ -64,13 +64,20 @@ def main():
         if key in seen:
             continue
         seen.add(key)
-        x = torch.randn(N * H * W, Cin, device="cuda")
-        ldk = E.r4(ks * ks * Cin)
-        wk = torch.randn(Cout * ldk, device="cuda") * 0.05
-        y = torch.empty(N * Ho * Wo, E.r4(Cout), device="cuda")
+        io = a.math == "bf16io"
+        if io and Cin % 8:
+            continue  # (the image: the bf16io engine runs it on the 4-channel path)
+        dt = torch.bfloat16 if io else torch.float32
+        x = torch.randn(N * H * W, Cin, device="cuda").to(dt)
+        ldk = E.r8(ks * ks * Cin) if io else E.r4(ks * ks * Cin)
+        wk = (torch.randn(Cout * ldk, device="cuda") * 0.05).to(dt)  # bf16io: the bf16-packed weights
+        y = torch.empty(N * Ho * Wo, E.r4(Cout), device="cuda", dtype=dt)
 
         def run():
-            if a.math == "bf16":
+            if io:
+                call("seg_conv_igemm_bf16io_w16", x.data_ptr(), Cin, N, H, W, Cin, wk.data_ptr(), ldk, None,
+                     y.data_ptr(), E.r4(Cout), Ho, Wo, Cout, ks, st, pad, None, 0, None, s)
+            elif a.math == "bf16":
                 call("seg_conv_igemm_bf16", x.data_ptr(), Cin, N, H, W, Cin, wk.data_ptr(), ldk, None, y.data_ptr(),
                      E.r4(Cout), Ho, Wo, Cout, ks, st, pad, None, 0, None, 0, None, 1, s)
             else:

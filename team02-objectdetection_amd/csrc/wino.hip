@@ -45,17 +45,20 @@ __device__ __forceinline__ void bt_row(int r, int& p0, int& p1, float& s0, float
   s1 = (r == 0 || r == 3) ? -1.f : 1.f;
 }
 
-template <int BM, int BN, int WM, int WN, int BK>
-__global__ __launch_bounds__(256) void wino_gemm_kernel(WinoArgs a) {
+// NT = 256 (4 waves) or 512 (8 waves: the 128 x 256 tile for Cout >= 256, which loads each
+// tile's transformed input once for 256 output channels instead of twice for 2 x 128 --
+// the A operand is most of this kernel's L2 traffic)
+template <int BM, int BN, int WM, int WN, int BK, int NT = 256>
+__global__ __launch_bounds__(NT) void wino_gemm_kernel(WinoArgs a) {
   constexpr int LDSR = BK + 4;
   constexpr int KQ = BK / 4;
   constexpr int A_VEC = BM * KQ, B_VEC = BN * KQ;
-  constexpr int A_PER = (A_VEC + 255) / 256;
-  constexpr int B_PER = (B_VEC + 255) / 256;
+  constexpr int A_PER = (A_VEC + NT - 1) / NT;
+  constexpr int B_PER = (B_VEC + NT - 1) / NT;
   constexpr int MI = WM / 32, NI = WN / 32;
   constexpr int WAVES_N = BN / WN;
-  static_assert((BM / WM) * (BN / WN) == 4, "4 waves per block");
-  static_assert(256 % KQ == 0, "uniform kq per thread");
+  static_assert((BM / WM) * (BN / WN) == NT / 64, "one wave per WM x WN sub-tile");
+  static_assert(NT % KQ == 0, "uniform kq per thread");
 
   __shared__ __attribute__((aligned(16))) float As[BM * LDSR];
   __shared__ __attribute__((aligned(16))) float Bs[BN * LDSR];
@@ -79,7 +82,7 @@ __global__ __launch_bounds__(256) void wino_gemm_kernel(WinoArgs a) {
   unsigned okm[A_PER];
 #pragma unroll
   for (int i = 0; i < A_PER; ++i) {
-    const int idx = tid + i * 256;
+    const int idx = tid + i * NT;
     const int t = m0 + idx / KQ;
     const bool ok = idx < A_VEC && t < a.T;
     const int tt = ok ? t : 0;
@@ -103,7 +106,7 @@ __global__ __launch_bounds__(256) void wino_gemm_kernel(WinoArgs a) {
   bool bok[B_PER];
 #pragma unroll
   for (int i = 0; i < B_PER; ++i) {
-    const int idx = tid + i * 256;
+    const int idx = tid + i * NT;
     const int co = n0 + idx / KQ;
     bok[i] = idx < B_VEC && co < a.Cout;
     boff[i] = (long)(bok[i] ? co : 0) * a.ldk + kq4;
@@ -125,16 +128,16 @@ __global__ __launch_bounds__(256) void wino_gemm_kernel(WinoArgs a) {
   auto store = [&]() {
 #pragma unroll
     for (int i = 0; i < A_PER; ++i) {
-      const int idx = tid + i * 256;
-      if (A_VEC % 256 == 0 || idx < A_VEC) {
+      const int idx = tid + i * NT;
+      if (A_VEC % NT == 0 || idx < A_VEC) {
         const f32x4 v = (s00 * ra[i][0] + s01 * ra[i][1]) + (s10 * ra[i][2] + s11 * ra[i][3]);
         st4(&As[(idx / KQ) * LDSR + (idx % KQ) * 4], v);
       }
     }
 #pragma unroll
     for (int i = 0; i < B_PER; ++i) {
-      const int idx = tid + i * 256;
-      if (B_VEC % 256 == 0 || idx < B_VEC) st4(&Bs[(idx / KQ) * LDSR + (idx % KQ) * 4], rb[i]);
+      const int idx = tid + i * NT;
+      if (B_VEC % NT == 0 || idx < B_VEC) st4(&Bs[(idx / KQ) * LDSR + (idx % KQ) * 4], rb[i]);
     }
   };
 
@@ -287,11 +290,14 @@ __global__ __launch_bounds__(256) void wino_out_kernel(const float* __restrict__
   }
 }
 
-template <int BM, int BN, int WM, int WN>
+template <int BM, int BN, int WM, int WN, int NT = 256>
 void launch_wino(const WinoArgs& a, hipStream_t s) {
   dim3 grid(seg_cdiv(a.T, BM) * seg_cdiv(a.Cout, BN), 1, 16);
-  hipLaunchKernelGGL((wino_gemm_kernel<BM, BN, WM, WN, 32>), grid, dim3(256), 0, s, a);
+  hipLaunchKernelGGL((wino_gemm_kernel<BM, BN, WM, WN, 32, NT>), grid, dim3(NT), 0, s, a);
 }
+#ifndef SEG_WINO_WIDE
+#define SEG_WINO_WIDE 256  // Cout from which the 8-wave 128 x 256 tile is used
+#endif
 
 // ---------------------------------------------------------------- weight gradient
 // dW = G^T [ sum_t (A dY_t A^T) .* (B^T X_t B) ] G  per (co, ci): Winograd F(3x3, 2x2)
@@ -527,7 +533,10 @@ SEG_API int seg_conv_wino(const float* in, long ldin, int N, int H, int W, int C
   a.N = N; a.H = H; a.W = W; a.Cin = Cin; a.Cout = Cout;
   a.th = H / 2; a.tw = W / 2; a.T = N * a.th * a.tw;
   if (a.T == 0) return 0;
-  if (Cout >= 128) launch_wino<128, 128, 64, 64>(a, stream);
+  // the wide tile where it pads no more columns than two narrow ones (measured: Cout 256 -5..-6 %,
+  // Cout 1344 (6 x 256 = 1536 vs 11 x 128 = 1408 columns) +4 % per launch)
+  if (Cout >= SEG_WINO_WIDE && seg_cdiv(Cout, 256) * 2 == seg_cdiv(Cout, 128)) launch_wino<128, 256, 64, 64, 512>(a, stream);
+  else if (Cout >= 128) launch_wino<128, 128, 64, 64>(a, stream);
   else launch_wino<128, 64, 64, 32>(a, stream);
   hipLaunchKernelGGL(wino_out_kernel, dim3(seg_cdiv(a.T, 64)), dim3(256), 0, stream, work, a.T, Cout, N, H, W, a.th,
                      a.tw, bias, add, ldadd, out, ldout, stat);

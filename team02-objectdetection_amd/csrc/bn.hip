@@ -226,47 +226,19 @@ __global__ __launch_bounds__(256) void bn_finalize_kernel(
 
 // BN statistics from the conv epilogue's per-row-tile partials part[t][2][C]
 // (tile sum S_t and tile M2_t about the tile mean, tile t holding
-// min(tile_rows, M - t*tile_rows) rows): Chan's parallel merge in fp64, one wave
-// per channel, fixed lane order and butterfly (deterministic).
-__device__ __forceinline__ void chan_merge(double& n, double& mean, double& m2, double n2, double mean2, double m2b) {
-  const double nn = n + n2;
-  if (nn == 0.0) return;
-  const double d = mean2 - mean;
-  mean += d * (n2 / nn);
-  m2 += m2b + d * d * (n * n2 / nn);
-  n = nn;
+// min(tile_rows, M - t*tile_rows) rows), merged in fp64 (deterministic).
+// The merge in two passes against the global mean (the parallel-variance identity
+// M2 = sum_t [M2_t + n_t (mean_t - mean)^2], as stable as pairwise Chan merges, with adds
+// instead of a division per merge): pass 1 sums the tile sums -> mean, pass 2 sums the
+// tile M2s and the between-tile terms.  fp64, fixed orders (deterministic).
+__device__ __forceinline__ double tile_rows_of(int i, int tile_rows, long M) {
+  return (double)std::min<long>(tile_rows, M - (long)i * tile_rows);
 }
 
-// One 256-thread block per channel: each lane merges every 256th tile, then a
-// fixed-order LDS tree of Chan merges (deterministic).
-__global__ __launch_bounds__(256) void bn_finalize_tiles_kernel(
-    const float* __restrict__ part, int ntiles, int tile_rows, long M, int C, const float* __restrict__ gamma,
-    const float* __restrict__ beta, float eps, float momentum, float* running_mean, float* running_var,
-    long long* nbt, float* mean_out, float* invstd_out, float* scale_out, float* shift_out) {
-  __shared__ double sn[256], smean[256], sm2[256];
-  const int t = threadIdx.x;
-  const int c = blockIdx.x;
-  if (blockIdx.x == 0 && t == 0 && nbt) *nbt += 1;
-  double n = 0.0, mean = 0.0, m2 = 0.0;
-  for (int i = t; i < ntiles; i += 256) {
-    const double nt = (double)std::min<long>(tile_rows, M - (long)i * tile_rows);
-    const double s = part[(long)i * 2 * C + c], q = part[(long)i * 2 * C + C + c];
-    chan_merge(n, mean, m2, nt, s / nt, q);
-  }
-  sn[t] = n;
-  smean[t] = mean;
-  sm2[t] = m2;
-  __syncthreads();
-  for (int o = 128; o > 0; o >>= 1) {
-    if (t < o) {
-      chan_merge(n, mean, m2, sn[t + o], smean[t + o], sm2[t + o]);
-      sn[t] = n;
-      smean[t] = mean;
-      sm2[t] = m2;
-    }
-    __syncthreads();
-  }
-  if (t != 0) return;
+__device__ __forceinline__ void bn_stats_out(double mean, double m2, long M, int c, const float* gamma,
+                                             const float* beta, float eps, float momentum, float* running_mean,
+                                             float* running_var, float* mean_out, float* invstd_out,
+                                             float* scale_out, float* shift_out) {
   double var = m2 / (double)M;
   if (var < 0.0) var = 0.0;
   const float invstd = (float)(1.0 / sqrt(var + (double)eps));
@@ -282,10 +254,46 @@ __global__ __launch_bounds__(256) void bn_finalize_tiles_kernel(
   }
 }
 
-// The same finalize for few tiles (ntiles <= 256: the small layers): one wave per
-// channel, 4 channels per block; each lane merges up to 4 tiles, then a fixed xor
-// butterfly of Chan merges over the 64 lanes (deterministic; no LDS, no barriers --
-// these launches were ~10 us of mostly block-wide fp64 tree synchronisation).
+// Many tiles (the high-resolution layers: up to M / 128): one 256-thread block per
+// channel, each lane summing every 256th tile, fixed-order LDS trees.
+__global__ __launch_bounds__(256) void bn_finalize_tiles_kernel(
+    const float* __restrict__ part, int ntiles, int tile_rows, long M, int C, const float* __restrict__ gamma,
+    const float* __restrict__ beta, float eps, float momentum, float* running_mean, float* running_var,
+    long long* nbt, float* mean_out, float* invstd_out, float* scale_out, float* shift_out) {
+  __shared__ double red[256];
+  const int t = threadIdx.x;
+  const int c = blockIdx.x;
+  if (blockIdx.x == 0 && t == 0 && nbt) *nbt += 1;
+  auto tree = [&](double v) -> double {  // every thread gets the fixed-order block sum
+    red[t] = v;
+    __syncthreads();
+    for (int o = 128; o > 0; o >>= 1) {
+      if (t < o) red[t] += red[t + o];
+      __syncthreads();
+    }
+    const double r = red[0];
+    __syncthreads();
+    return r;
+  };
+  double s = 0.0;
+#pragma unroll 4
+  for (int i = t; i < ntiles; i += 256) s += part[(long)i * 2 * C + c];
+  const double mean = tree(s) / (double)M;
+  double q = 0.0;
+#pragma unroll 4
+  for (int i = t; i < ntiles; i += 256) {
+    const double nt = tile_rows_of(i, tile_rows, M);
+    const double d = part[(long)i * 2 * C + c] / nt - mean;
+    q += part[(long)i * 2 * C + C + c] + nt * d * d;
+  }
+  const double m2 = tree(q);
+  if (t == 0)
+    bn_stats_out(mean, m2, M, c, gamma, beta, eps, momentum, running_mean, running_var, mean_out, invstd_out,
+                 scale_out, shift_out);
+}
+
+// Few tiles (<= 256: the small layers): one wave per channel, 4 channels per block, lanes
+// over tiles, fixed xor butterflies (no LDS, no barriers).
 __global__ __launch_bounds__(256) void bn_finalize_tiles_wave_kernel(
     const float* __restrict__ part, int ntiles, int tile_rows, long M, int C, const float* __restrict__ gamma,
     const float* __restrict__ beta, float eps, float momentum, float* running_mean, float* running_var,
@@ -294,37 +302,26 @@ __global__ __launch_bounds__(256) void bn_finalize_tiles_wave_kernel(
   const int c = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (blockIdx.x == 0 && threadIdx.x == 0 && nbt) *nbt += 1;
   if (c >= C) return;
-  double n = 0.0, mean = 0.0, m2 = 0.0;
-  for (int i = lane; i < ntiles; i += 64) {
-    const double nt = (double)std::min<long>(tile_rows, M - (long)i * tile_rows);
-    const double sm = part[(long)i * 2 * C + c], q = part[(long)i * 2 * C + C + c];
-    chan_merge(n, mean, m2, nt, sm / nt, q);
+  double sv[4], qv[4];
+  int nv = 0;
+  double s = 0.0;
+  for (int i = lane; i < ntiles; i += 64, ++nv) {  // ntiles <= 256: at most 4 tiles per lane
+    sv[nv] = part[(long)i * 2 * C + c];
+    qv[nv] = part[(long)i * 2 * C + C + c];
+    s += sv[nv];
   }
-  for (int o = 1; o < 64; o <<= 1) {
-    const double n2 = __shfl_xor(n, o, 64), mean2 = __shfl_xor(mean, o, 64), m22 = __shfl_xor(m2, o, 64);
-    // both partners merge (lower lane's set first) so every lane holds the same result
-    if (lane & o) {
-      double a = n2, b = mean2, d = m22;
-      chan_merge(a, b, d, n, mean, m2);
-      n = a; mean = b; m2 = d;
-    } else {
-      chan_merge(n, mean, m2, n2, mean2, m22);
-    }
+  for (int o = 1; o < 64; o <<= 1) s += __shfl_xor(s, o, 64);
+  const double mean = s / (double)M;
+  double q = 0.0;
+  for (int k = 0; k < nv; ++k) {
+    const double nt = tile_rows_of(lane + 64 * k, tile_rows, M);
+    const double d = sv[k] / nt - mean;
+    q += qv[k] + nt * d * d;
   }
-  if (lane != 0) return;
-  double var = m2 / (double)M;
-  if (var < 0.0) var = 0.0;
-  const float invstd = (float)(1.0 / sqrt(var + (double)eps));
-  mean_out[c] = (float)mean;
-  invstd_out[c] = invstd;
-  const float g = gamma ? gamma[c] : 1.f, bt = beta ? beta[c] : 0.f;
-  scale_out[c] = g * invstd;
-  shift_out[c] = bt - (float)mean * g * invstd;
-  if (running_mean) {
-    const double unbiased = M > 1 ? m2 / (double)(M - 1) : var;
-    running_mean[c] = (float)((1.0 - momentum) * running_mean[c] + momentum * mean);
-    running_var[c] = (float)((1.0 - momentum) * running_var[c] + momentum * unbiased);
-  }
+  for (int o = 1; o < 64; o <<= 1) q += __shfl_xor(q, o, 64);
+  if (lane == 0)
+    bn_stats_out(mean, q, M, c, gamma, beta, eps, momentum, running_mean, running_var, mean_out, invstd_out,
+                 scale_out, shift_out);
 }
 
 __global__ void bn_eval_coef_kernel(const float* gamma, const float* beta, const float* rm, const float* rv, float eps,

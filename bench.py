@@ -327,7 +327,10 @@ def main():
         traffic, traffic_src, mfma_busy = None, None, None
         prof = os.path.join(REPO, "profiles", "latest_roofline.json" if args.math == "f32"
                             else f"latest_roofline_{args.math}.json")
-        if os.path.exists(prof):
+        # the committed profile is of the default workload (MobileNetV2UNet bs=32 256x512): attach its
+        # PMC figures only to that workload's line
+        default_workload = (args.model, args.batch, args.height, args.width) == ("MobileNetV2UNet", 32, 256, 512)
+        if os.path.exists(prof) and default_workload:
             with open(prof) as fh:
                 rj = json.load(fh)
             traffic = rj["families"].get("conv3", {}).get("hbm_bytes_per_op")

@@ -358,11 +358,17 @@ SEG_API int seg_conv_wgrad_splits(long M, int Cout, int Cin, int ks) {
 #ifndef SEG_WGRAD_THIN_BF16
 #define SEG_WGRAD_THIN_BF16 1024  // thin slabs (<= 2 tiles: the stem, OutConv, Cout-32 decoder convs): measured +0.6 % bf16io
 #endif
+#ifndef SEG_WGRAD_MAXPX_BF16
+#define SEG_WGRAD_MAXPX_BF16 8192L  // measured: UNet 512x1024 bf16io +3.8 %, MobileNetV2UNet flat
+#endif
 SEG_API int seg_conv_wgrad_splits_bf16(long M, int Cout, int Cin, int ks) {
   int bm, bn;
   wgrad_tiles(Cout, ks * ks * Cin, &bm, &bn);
   const long tiles = (long)seg_cdiv(Cout, bm) * seg_cdiv(ks * ks * Cin, bn);
-  return wgrad_splits(M, Cout, Cin, ks, tiles <= 2 ? SEG_WGRAD_THIN_BF16 : SEG_WGRAD_BLOCKS_BF16);
+  long target = tiles <= 2 ? SEG_WGRAD_THIN_BF16 : SEG_WGRAD_BLOCKS_BF16;
+  // bound the pixels per split (each block walks its split's 32-pixel chunks one after another)
+  target = std::max<long>(target, tiles * seg_cdiv(M, SEG_WGRAD_MAXPX_BF16));
+  return wgrad_splits(M, Cout, Cin, ks, target);
 }
 
 // part[s][co][tap*Cin+ci] = sum over split s's pixels of dY[p][co] * X[src(p,tap)][ci].

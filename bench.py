@@ -216,13 +216,18 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     check_world(world, args.gpus)
     dist = world > 1
-    if dist:
-        torch.distributed.init_process_group(args.dist_backend)
-        assert torch.distributed.get_world_size() == args.gpus
     if args.dist_backend == "gloo":
         local = local % torch.cuda.device_count()
+    # bind the rank's GPU before the process group exists, so RCCL's communicators (and the
+    # barriers below) are created on this rank's device, never on device 0
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
+    if dist:
+        if args.dist_backend == "nccl":
+            torch.distributed.init_process_group(args.dist_backend, device_id=dev)
+        else:
+            torch.distributed.init_process_group(args.dist_backend)
+        assert torch.distributed.get_world_size() == args.gpus
 
     import seg_amd
     from seg_amd import deterministic_init, synthetic_batch

@@ -52,6 +52,9 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-timer", action="store_true", help="skip the per-launch HIP-event roofline timing")
+    ap.add_argument("--no-bf16io-block", action="store_true",
+                    help="skip the nested \"bf16io\" measurement (configs[2] math on the same workload) that follows "
+                         "the f32 headline")
     ap.add_argument("--workload", choices=("train", "infer"), default="train",
                     help="train: BASELINE configs[1] (the headline); infer: configs[3], inference.py's per-frame path")
     ap.add_argument("--frames", type=int, default=500, help="timed frames of --workload infer")
@@ -229,15 +232,70 @@ def main():
             torch.distributed.init_process_group(args.dist_backend)
         assert torch.distributed.get_world_size() == args.gpus
 
+    head = train_workload(args, args.math, dev, world, rank, dist)
+    nested = None
+    if args.math == "f32" and args.model == "MobileNetV2UNet" and not args.no_bf16io_block:
+        # BASELINE configs[2]'s arithmetic on the same workload (the north-star HBM target):
+        # its own model, warm-up and timed region after the headline's
+        nested = train_workload(args, "bf16io", dev, world, rank, dist)
+
+    if rank == 0:
+        cpu = None
+        if world == 1 and not args.no_cpu_baseline:
+            cpu = cpu_baseline(args)
+        line = {"metric": f"images/sec fwd+bwd {args.model} {args.height}x{args.width} bs={args.batch}/GPU",
+                "value": head["value"], "unit": "images/s", "n_gpus": world, "steps": args.steps,
+                "warmup": args.warmup, "ms_per_step": head["ms_per_step"], "higher_is_better": True,
+                "scaling": "weak", "vs_baseline": None, "dtype": args.math, "data": "synthetic",
+                "config": {"workload": f"{args.model} {args.classes}-class fwd+bwd+Adam, "
+                                       f"{args.height}x{args.width}, bs={args.batch}/GPU ({_cfg_name(args, args.math)})",
+                           "model": args.model, "global_batch": args.batch * world,
+                           "image": [args.height, args.width], "parallelism": f"dp{world}",
+                           "collectives": "RCCL (torch.distributed nccl)" if args.dist_backend == "nccl" else
+                                          "gloo REHEARSAL (ranks share GPUs; not a throughput figure)",
+                           "optimizer": {"seg": "seg_amd.Adam (HIP, one launch)", "torch": "torch.optim.Adam (foreach)"}[args.optimizer]},
+                "final_loss": head["final_loss"], "math": MATH_NOTE[args.math],
+                "roofline": head["roofline"], "step_roofline": head["step_roofline"], "cpu_baseline": cpu}
+        if head["multi_gpu"] is not None:
+            line["multi_gpu"] = head["multi_gpu"]
+        if nested is not None:
+            line["bf16io"] = {"workload": f"same model, shape and step as the headline with bf16io math "
+                                          f"({_cfg_name(args, 'bf16io')})", "dtype": "bf16io",
+                              "math": MATH_NOTE["bf16io"], **nested}
+        print(json.dumps(line), flush=True)
+    if dist:
+        torch.distributed.destroy_process_group()
+
+
+MATH_NOTE = {"f32": "fp32 everywhere",
+             "bf16": "conv operands bf16 (RNE) on the bf16 MFMA, fp32 accumulation; activations, "
+                     "BatchNorm, depthwise convs, loss and Adam in fp32",
+             "bf16io": "conv operands bf16 on the bf16 MFMA, fp32 accumulation; activations and their "
+                       "gradients stored bf16 in HBM (fp32 arithmetic inside every kernel); BN "
+                       "statistics, parameter gradients, loss and Adam fp32"}
+
+
+def _cfg_name(args, math):
+    if args.model == "MobileNetV2UNet":
+        return "BASELINE configs[1]" if math == "f32" else f"BASELINE configs[2] math ({math}) at N GPUs"
+    return f"BASELINE configs[4] shape, {math} conv math"
+
+
+def train_workload(args, math, dev, world, rank, dist):
+    """Warm up, then time args.steps training steps of args.model with conv math `math`
+    (barrier + synchronize on both sides, max over ranks), then the untimed roofline
+    passes.  Returns value / ms_per_step / final_loss / roofline / step_roofline /
+    multi_gpu; frees the model's plans afterwards."""
     import seg_amd
     from seg_amd import deterministic_init, synthetic_batch
     from seg_amd import engine
-    model = deterministic_init(getattr(seg_amd, args.model)(args.classes), seed=0).to(dev).train()
-    engine.set_conv_math(model, args.math)
-    peak = F32_MFMA_PEAK_TFLOPS if args.math == "f32" else BF16_MFMA_PEAK_TFLOPS
+    core = deterministic_init(getattr(seg_amd, args.model)(args.classes), seed=0).to(dev).train()
+    engine.set_conv_math(core, math)
+    peak = F32_MFMA_PEAK_TFLOPS if math == "f32" else BF16_MFMA_PEAK_TFLOPS
+    model = core
     if dist:
         from seg_amd.ddp import DataParallel
-        model = DataParallel(model)
+        model = DataParallel(core)
     if args.optimizer == "seg":
         from seg_amd import Adam
         opt = Adam(model.parameters(), lr=1.5e-4)
@@ -284,8 +342,13 @@ def main():
     scaling = None
     if dist:
         # same-run reference for the weak-scaling efficiency: the same K steps on every rank
-        # with the gradient all-reduce switched off (DataParallel.no_sync), max over ranks
+        # with no communication at all (DataParallel.no_sync: no gradient all-reduce; the BN
+        # buffer broadcast switched off too), max over ranks.  One untimed step first: the
+        # no_sync plan is a different launch tape, recorded (and its buffers allocated) then.
+        bcast = model.broadcast_buffers
+        model.broadcast_buffers = False
         with model.no_sync():
+            step()
             torch.distributed.barrier()
             torch.cuda.synchronize()
             t0 = time.perf_counter()
@@ -293,169 +356,151 @@ def main():
                 step()
             torch.cuda.synchronize()
             solo = time.perf_counter() - t0
+        model.broadcast_buffers = bcast
         t = torch.tensor([solo], device=dev, dtype=torch.float64)
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
         solo = float(t)
-        scaling = {"ranks_seen": world, "ms_per_step_per_rank": [round(x / args.steps * 1e3, 3) for x in per_rank],
-                   "ms_per_step_without_allreduce": round(solo / args.steps * 1e3, 3),
-                   "weak_scaling_eff_vs_no_allreduce": round(solo / dt, 4),
-                   "note": "efficiency = same-run step time without the gradient all-reduce / with it "
-                           "(the driver computes the cross-run N=1 efficiency itself)"}
+        scaling = {"ranks_seen": world, "ms_per_step_per_rank": [round(v / args.steps * 1e3, 3) for v in per_rank],
+                   "ms_per_step_without_communication": round(solo / args.steps * 1e3, 3),
+                   "weak_scaling_eff_vs_no_communication": round(solo / dt, 4),
+                   "note": "efficiency = same-run step time with no gradient all-reduce and no BN-buffer "
+                           "broadcast (after one untimed no_sync step) / the timed step time (the driver "
+                           "computes the cross-run N=1 efficiency itself)"}
 
     roof = None
     if timer is not None:
-        def family(rec, kinds):
-            sel = [(f, s) for k, f, s in rec if k in kinds]
-            fl, sec = sum(f for f, _ in sel), sum(s for _, s in sel)
-            return fl, sec, len(sel)
+        roof = _roofline(args, math, model, core, engine, timer, conv3, step, dt, peak)
+    step_roof = _step_roofline(args, math, core, engine, value, peak)
+    res = {"value": round(value, 2), "ms_per_step": round(dt / args.steps * 1e3, 3),
+           "final_loss": round(final_loss, 5), "roofline": roof, "step_roofline": step_roof, "multi_gpu": scaling}
+    engine.release_plans(core)
+    del model, core, opt
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()
+    return res
 
-        def extra_pass(overlap):
-            """3 untimed steps with every conv launch timed (after the timed region)."""
-            saved = engine.OVERLAP
-            engine.OVERLAP = overlap
-            t = engine.KernelTimer()
-            engine.TIMER = t
-            for _ in range(3):
-                step()
-            torch.cuda.synchronize()
-            engine.TIMER = None
-            engine.OVERLAP = saved
-            return t.elapsed()
 
-        # dominant kernel family: every dense 3x3 conv's forward and data gradient
-        # (implicit GEMM / Winograd / LDS-halo; the top family in the rocprof summary),
-        # timed live inside the timed region
-        rec = timer.elapsed()
-        flops, secs, n = family(rec, conv3)
-        wfl, wsec, wn = family(rec, {"wino3_fwd", "wino3_dgrad"})
-        achieved = flops / secs / 1e12 if secs > 0 else 0.0
-        traffic, traffic_src, mfma_busy = None, None, None
-        prof = os.path.join(REPO, "profiles", "latest_roofline.json" if args.math == "f32"
-                            else f"latest_roofline_{args.math}.json")
-        # the committed profile is of the default workload (MobileNetV2UNet bs=32 256x512): attach its
-        # PMC figures only to that workload's line
-        default_workload = (args.model, args.batch, args.height, args.width) == ("MobileNetV2UNet", 32, 256, 512)
-        if os.path.exists(prof) and default_workload:
-            with open(prof) as fh:
-                rj = json.load(fh)
-            traffic = rj["families"].get("conv3", {}).get("hbm_bytes_per_op")
-            mfma_busy = rj["families"].get("conv3", {}).get("mfma_busy_frac")
-            # the PMC figure is not measured in this run: name the profile and commit it came from
-            traffic_src = {"file": os.path.relpath(prof, REPO), "profile": rj.get("profile"),
-                           "commit": rj.get("commit"),
-                           "counters": "rocprofv3 PMC (2*FETCH_SIZE+WRITE_SIZE)*1KiB of the conv3 family per step "
-                                       "/ 17 conv ops, separate --pmc passes; SQ_VALU_MFMA_BUSY_CYCLES and "
-                                       "GRBM_GUI_ACTIVE in a third pass"}
-        # algorithmic bytes of the family: every 3x3 conv's input and output tensors once
-        # (fwd: X + Y, dgrad: dY + dX) at the storage element size, averaged over its launches
-        prog = engine.get_program(getattr(model, "module", model), args.batch, args.height, args.width)
-        sb = 2 if args.math == "bf16io" else 4
-        abytes = []
-        for op in prog.ops:
-            if isinstance(op, engine.ConvOp) and op.kind == "igemm" and op.ks == 3:
-                xy = sb * (op.inp.M * op.cin + op.y.M * op.cout)
+def _roofline(args, math, model, core, engine, timer, conv3, step, dt, peak):
+    """The dominant kernel family's roofline: the dense 3x3 conv forward + data gradient,
+    timed live inside the timed region (timer), plus the untimed re-timing passes."""
+    def family(rec, kinds):
+        sel = [(f, s) for k, f, s in rec if k in kinds]
+        fl, sec = sum(f for f, _ in sel), sum(s for _, s in sel)
+        return fl, sec, len(sel)
+
+    def extra_pass(overlap):
+        """3 untimed steps with every conv launch timed (after the timed region)."""
+        saved = engine.OVERLAP
+        engine.OVERLAP = overlap
+        t = engine.KernelTimer()
+        engine.TIMER = t
+        for _ in range(3):
+            step()
+        torch.cuda.synchronize()
+        engine.TIMER = None
+        engine.OVERLAP = saved
+        return t.elapsed()
+
+    rec = timer.elapsed()
+    flops, secs, n = family(rec, conv3)
+    wfl, wsec, wn = family(rec, {"wino3_fwd", "wino3_dgrad"})
+    achieved = flops / secs / 1e12 if secs > 0 else 0.0
+    traffic, traffic_src, mfma_busy = None, None, None
+    prof = os.path.join(REPO, "profiles", "latest_roofline.json" if math == "f32" else f"latest_roofline_{math}.json")
+    # the committed profile is of the default workload (MobileNetV2UNet bs=32 256x512): attach its
+    # PMC figures only to that workload's line
+    default_workload = (args.model, args.batch, args.height, args.width) == ("MobileNetV2UNet", 32, 256, 512)
+    if os.path.exists(prof) and default_workload:
+        with open(prof) as fh:
+            rj = json.load(fh)
+        traffic = rj["families"].get("conv3", {}).get("hbm_bytes_per_op")
+        mfma_busy = rj["families"].get("conv3", {}).get("mfma_busy_frac")
+        # the PMC figure is not measured in this run: name the profile and commit it came from
+        traffic_src = {"file": os.path.relpath(prof, REPO), "profile": rj.get("profile"),
+                       "commit": rj.get("commit"),
+                       "counters": "rocprofv3 PMC (2*FETCH_SIZE+WRITE_SIZE)*1KiB of the conv3 family per step "
+                                   "/ 17 conv ops, separate --pmc passes; SQ_VALU_MFMA_BUSY_CYCLES and "
+                                   "GRBM_GUI_ACTIVE in a third pass"}
+    # algorithmic bytes of the family: every 3x3 conv's input and output tensors once
+    # (fwd: X + Y, dgrad: dY + dX) at the storage element size, averaged over its launches
+    prog = engine.get_program(core, args.batch, args.height, args.width)
+    sb = 2 if math == "bf16io" else 4
+    abytes = []
+    for op in prog.ops:
+        if isinstance(op, engine.ConvOp) and op.kind == "igemm" and op.ks == 3:
+            xy = sb * (op.inp.M * op.cin + op.y.M * op.cout)
+            abytes.append(xy)
+            if not op.first:
                 abytes.append(xy)
-                if not op.first:
-                    abytes.append(xy)
-        alg_bytes = sum(abytes) / max(len(abytes), 1)
-        # the other conv families and the side-stream-free figure: separate untimed passes
-        rec_all = extra_pass(engine.OVERLAP)
-        wf, ws, wgn = family(rec_all, {"igemm3_wgrad", "wino3_wgrad"})
-        af, as_, an = family(rec_all, {k for k, _, _ in rec_all if k.startswith(("igemm", "wino", "halo"))})
-        rec_iso = extra_pass(False)
-        ifl, isec, inn = family(rec_iso, conv3)
-        if args.math == "f32":  # compute-bound config (SURVEY 8(d)): FLOPs against the f32 MFMA peak
-            bound = {"bound": "mfma", "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
-                     "frac": round(achieved / peak, 4)}
-        else:  # the bf16 configurations are HBM-bound (SURVEY 8(d)): algorithmic bytes against HBM
-            gbs = alg_bytes * n / secs / 1e9 if secs > 0 else 0.0
-            bound = {"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": round(gbs / HBM_PEAK_GBS, 4), "mfma_tflops": round(achieved, 2),
-                     "mfma_frac": round(achieved / peak, 4)}
-        roof = {**bound,
-                "traffic": round(traffic) if traffic else None,
-                "traffic_source": traffic_src,
-                "traffic_over_algorithmic": round(traffic / alg_bytes, 3) if traffic else None,
-                # same profile: SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE / 8 XCDs * 1024 SIMDs) over the family
-                "mfma_busy_frac_pmc": round(mfma_busy, 4) if mfma_busy else None,
-                "algorithmic_bytes_per_launch": round(alg_bytes),
-                "kernel": ("dense 3x3 conv fwd + dgrad on f32 MFMA: igemm_conv_kernel<*,*,*,*,3,*> (implicit GEMM), "
-                           "halo3x3_kernel (LDS-halo direct conv, narrow decoder convs) and, for the deep decoder "
-                           "convs, wino_gemm_kernel + wino_out_kernel (Winograd F(2x2,3x3): 2.25x fewer executed "
-                           "MFMA FLOPs than the algorithmic count used here)"
-                           if args.math == "f32" else
-                           "dense 3x3 conv fwd + dgrad on bf16 MFMA: igemm_conv_kernel<*,*,*,*,3,*,*,false,__bf16> "
-                           "(implicit GEMM, v_mfma_f32_32x32x16_bf16, fp32 accumulation)"),
-                "winograd": {"launches": wn, "algorithmic_tflops": round(wfl / wsec / 1e12, 2) if wsec else None,
-                             "executed_mfma_tflops": round(wfl / 2.25 / wsec / 1e12, 2) if wsec else None},
-                "launches": n, "flops_per_launch": round(flops / max(n, 1)),
-                "avg_launch_us": round(secs / max(n, 1) * 1e6, 2),
-                "share_of_step": round(secs / dt, 4),
-                "note": "live launches share the CUs with the weight-gradient side stream (engine.OVERLAP); "
-                        "without_side_stream re-times the same launches in 3 untimed steps with it off",
-                "without_side_stream": (
-                    {"achieved": round(ifl / isec / 1e12, 2) if isec else None, "unit": "TFLOP/s",
-                     "frac": round(ifl / isec / 1e12 / peak, 4) if isec else None,
-                     "avg_launch_us": round(isec / max(inn, 1) * 1e6, 2), "launches": inn}
-                    if args.math == "f32" else
-                    {"achieved": round(alg_bytes * inn / isec / 1e9, 1) if isec else None, "unit": "GB/s",
-                     "frac": round(alg_bytes * inn / isec / 1e9 / HBM_PEAK_GBS, 4) if isec else None,
-                     "mfma_tflops": round(ifl / isec / 1e12, 2) if isec else None,
-                     "avg_launch_us": round(isec / max(inn, 1) * 1e6, 2), "launches": inn}),
-                "wgrad3": {"achieved": round(wf / ws / 1e12, 2) if ws else None, "launches": wgn,
-                           "avg_launch_us": round(ws / max(wgn, 1) * 1e6, 2)},
-                "all_mfma_convs": {"achieved": round(af / as_ / 1e12, 2) if as_ else None, "launches": an}}
+    alg_bytes = sum(abytes) / max(len(abytes), 1)
+    # the other conv families and the side-stream-free figure: separate untimed passes
+    rec_all = extra_pass(engine.OVERLAP)
+    wf, ws, wgn = family(rec_all, {"igemm3_wgrad", "wino3_wgrad"})
+    af, as_, an = family(rec_all, {k for k, _, _ in rec_all if k.startswith(("igemm", "wino", "halo"))})
+    rec_iso = extra_pass(False)
+    ifl, isec, inn = family(rec_iso, conv3)
+    if math == "f32":  # compute-bound config (SURVEY 8(d)): FLOPs against the f32 MFMA peak
+        bound = {"bound": "mfma", "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
+                 "frac": round(achieved / peak, 4)}
+    else:  # the bf16 configurations are HBM-bound (SURVEY 8(d)): algorithmic bytes against HBM
+        gbs = alg_bytes * n / secs / 1e9 if secs > 0 else 0.0
+        bound = {"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                 "frac": round(gbs / HBM_PEAK_GBS, 4), "mfma_tflops": round(achieved, 2),
+                 "mfma_frac": round(achieved / peak, 4)}
+    return {**bound,
+            "traffic": round(traffic) if traffic else None,
+            "traffic_source": traffic_src,
+            "traffic_over_algorithmic": round(traffic / alg_bytes, 3) if traffic else None,
+            # same profile: SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE / 8 XCDs * 1024 SIMDs) over the family
+            "mfma_busy_frac_pmc": round(mfma_busy, 4) if mfma_busy else None,
+            "algorithmic_bytes_per_launch": round(alg_bytes),
+            "kernel": ("dense 3x3 conv fwd + dgrad on f32 MFMA: igemm_conv_kernel<*,*,*,*,3,*> (implicit GEMM), "
+                       "halo3x3_kernel (LDS-halo direct conv, narrow decoder convs) and, for the deep decoder "
+                       "convs, wino_gemm_kernel + wino_out_kernel (Winograd F(2x2,3x3): 2.25x fewer executed "
+                       "MFMA FLOPs than the algorithmic count used here)"
+                       if math == "f32" else
+                       "dense 3x3 conv fwd + dgrad on bf16 MFMA: igemm_conv_kernel<*,*,*,*,3,*,*,false,__bf16> "
+                       "(implicit GEMM, v_mfma_f32_32x32x16_bf16, fp32 accumulation) and halo3x3_kernel "
+                       "(LDS-halo direct conv, narrow convs)"),
+            "winograd": {"launches": wn, "algorithmic_tflops": round(wfl / wsec / 1e12, 2) if wsec else None,
+                         "executed_mfma_tflops": round(wfl / 2.25 / wsec / 1e12, 2) if wsec else None},
+            "launches": n, "flops_per_launch": round(flops / max(n, 1)),
+            "avg_launch_us": round(secs / max(n, 1) * 1e6, 2),
+            "share_of_step": round(secs / dt, 4),
+            "note": "live launches share the CUs with the weight-gradient side stream (engine.OVERLAP); "
+                    "without_side_stream re-times the same launches in 3 untimed steps with it off",
+            "without_side_stream": (
+                {"achieved": round(ifl / isec / 1e12, 2) if isec else None, "unit": "TFLOP/s",
+                 "frac": round(ifl / isec / 1e12 / peak, 4) if isec else None,
+                 "avg_launch_us": round(isec / max(inn, 1) * 1e6, 2), "launches": inn}
+                if math == "f32" else
+                {"achieved": round(alg_bytes * inn / isec / 1e9, 1) if isec else None, "unit": "GB/s",
+                 "frac": round(alg_bytes * inn / isec / 1e9 / HBM_PEAK_GBS, 4) if isec else None,
+                 "mfma_tflops": round(ifl / isec / 1e12, 2) if isec else None,
+                 "avg_launch_us": round(isec / max(inn, 1) * 1e6, 2), "launches": inn}),
+            "wgrad3": {"achieved": round(wf / ws / 1e12, 2) if ws else None, "launches": wgn,
+                       "avg_launch_us": round(ws / max(wgn, 1) * 1e6, 2)},
+            "all_mfma_convs": {"achieved": round(af / as_ / 1e12, 2) if as_ else None, "launches": an}}
 
-    # Whole-step roofline (SURVEY 8(d), the north-star figure): algorithmic work of one
-    # training image under the fused-execution model -- FLOPs = 3 x the forward conv FLOPs
-    # (fwd, data and weight gradient); bytes = sum over convs of (3|X| + 5|Y|) * s plus the
-    # loss (2 C H W s + 8 H W), s = activation bytes (4 f32, 2 with bf16 storage).
-    prog = engine.get_program(getattr(model, "module", model), args.batch, args.height, args.width)
-    sb = 2 if args.math == "bf16io" else 4
+
+def _step_roofline(args, math, core, engine, value, peak):
+    """Whole-step roofline (the north-star figure): algorithmic work of one
+    training image under the fused-execution model -- FLOPs = 3 x the forward conv FLOPs
+    (fwd, data and weight gradient); bytes = sum over convs of (3|X| + 5|Y|) * s plus the
+    loss (2 C H W s + 8 H W), s = activation bytes (4 f32, 2 with bf16 storage)."""
+    prog = engine.get_program(core, args.batch, args.height, args.width)
+    sb = 2 if math == "bf16io" else 4
     fl_img = by_img = 0.0
     for op in prog.ops:
         if isinstance(op, engine.ConvOp):
             fl_img += 3 * op.flops() / args.batch
             by_img += (3 * op.inp.M * op.cin + 5 * op.y.M * op.cout) * sb / args.batch
     by_img += (2 * args.classes * args.height * args.width * sb + 8 * args.height * args.width)
-    step_roof = {"flops_per_img": round(fl_img), "bytes_per_img": round(by_img),
-                 "achieved_tflops": round(fl_img * value / 1e12, 2), "achieved_gbs": round(by_img * value / 1e9, 1),
-                 "frac_mfma_peak": round(fl_img * value / 1e12 / peak, 4),
-                 "frac_hbm_peak": round(by_img * value / 1e9 / HBM_PEAK_GBS, 4),
-                 "bound_img_per_s": round(1.0 / max(fl_img / (peak * 1e12), by_img / (HBM_PEAK_GBS * 1e9)), 1)}
-
-    if rank == 0:
-        cpu = None
-        if world == 1 and not args.no_cpu_baseline:
-            cpu = cpu_baseline(args)
-        if args.model == "MobileNetV2UNet":
-            cfg = "BASELINE configs[1]" if args.math == "f32" else f"BASELINE configs[2] math ({args.math}) at N GPUs"
-        else:
-            cfg = f"BASELINE configs[4] shape, {args.math} conv math"
-        line = {"metric": f"images/sec fwd+bwd {args.model} {args.height}x{args.width} bs={args.batch}/GPU",
-                "value": round(value, 2), "unit": "images/s", "n_gpus": world, "steps": args.steps,
-                "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 3), "higher_is_better": True,
-                "scaling": "weak", "vs_baseline": None, "dtype": args.math, "data": "synthetic",
-                "config": {"workload": f"{args.model} {args.classes}-class fwd+bwd+Adam, "
-                                       f"{args.height}x{args.width}, bs={args.batch}/GPU ({cfg})",
-                           "model": args.model, "global_batch": args.batch * world,
-                           "image": [args.height, args.width], "parallelism": f"dp{world}",
-                           "collectives": "RCCL (torch.distributed nccl)" if args.dist_backend == "nccl" else
-                                          "gloo REHEARSAL (ranks share GPUs; not a throughput figure)",
-                           "optimizer": {"seg": "seg_amd.Adam (HIP, one launch)", "torch": "torch.optim.Adam (foreach)"}[args.optimizer]},
-                "final_loss": round(final_loss, 5),
-                "math": {"f32": "fp32 everywhere",
-                         "bf16": "conv operands bf16 (RNE) on the bf16 MFMA, fp32 accumulation; activations, "
-                                 "BatchNorm, depthwise convs, loss and Adam in fp32",
-                         "bf16io": "conv operands bf16 on the bf16 MFMA, fp32 accumulation; activations and their "
-                                   "gradients stored bf16 in HBM (fp32 arithmetic inside every kernel); BN "
-                                   "statistics, parameter gradients, loss and Adam fp32"}[args.math],
-                "roofline": roof, "step_roofline": step_roof, "cpu_baseline": cpu}
-        if scaling is not None:
-            line["multi_gpu"] = scaling
-        print(json.dumps(line), flush=True)
-    if dist:
-        torch.distributed.destroy_process_group()
+    return {"flops_per_img": round(fl_img), "bytes_per_img": round(by_img),
+            "achieved_tflops": round(fl_img * value / 1e12, 2), "achieved_gbs": round(by_img * value / 1e9, 1),
+            "frac_mfma_peak": round(fl_img * value / 1e12 / peak, 4),
+            "frac_hbm_peak": round(by_img * value / 1e9 / HBM_PEAK_GBS, 4),
+            "bound_img_per_s": round(1.0 / max(fl_img / (peak * 1e12), by_img / (HBM_PEAK_GBS * 1e9)), 1)}
 
 
 if __name__ == "__main__":

@@ -437,6 +437,12 @@ int seg_tape_timing(void* tape, const int* idx, int n, int max_replays);
 int seg_tape_elapsed(void* tape, float* out);
 int seg_tape_run(void* tape, int begin, hipStream_t main, hipStream_t side, int* stop);
 
+/* Build identity (host only): copies the SHA-256 (64 hex chars + NUL) of the sources this
+ * library was built from -- every csrc file, this header, compiler and flags
+ * (seg_amd/build.py source_hash) -- into out when cap > 64; returns the length.  The
+ * Python binding refuses a library whose hash differs from the tree it runs in. */
+int seg_build_hash(char* out, int cap);
+
 #ifdef __cplusplus
 }
 #endif

@@ -10,7 +10,7 @@ import ctypes
 import os
 import threading
 
-from .build import LIB_PATH
+from .build import LIB_PATH, source_hash
 
 _V = ctypes.c_void_p
 _I = ctypes.c_int
@@ -86,6 +86,7 @@ PROTOTYPES = {
     "seg_tape_timing": (_I, [_V, _V, _I, _I]),
     "seg_tape_elapsed": (_I, [_V, _V]),
     "seg_tape_run": (_I, [_V, _I, _V, _V, _V]),
+    "seg_build_hash": (_I, [ctypes.c_char_p, _I]),
 }
 # bf16-storage variants: same C signature shape as their fp32 namesakes (pointers stay void*)
 for _n in ("seg_add", "seg_bn_stats", "seg_bn_apply", "seg_bn_backward", "seg_colsum", "seg_dw_fwd", "seg_dw_dgrad",
@@ -131,6 +132,12 @@ def lib():
                 fn = getattr(h, name)
                 fn.restype = res
                 fn.argtypes = args
+            if path == LIB_PATH:  # a SEG_LIB_PATH variant is built from other sources on purpose
+                buf = ctypes.create_string_buffer(80)
+                h.seg_build_hash(buf, 80)
+                if buf.value.decode() != source_hash():
+                    raise SegLibError(f"HIP library {path} was built from other sources than this tree "
+                                      "(source hash mismatch); rebuild it with `python __graft_entry__.py`")
             _lib = h
     return _lib
 

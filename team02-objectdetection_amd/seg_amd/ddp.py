@@ -57,6 +57,9 @@ class DataParallel(nn.Module):
         self._slot = {}      # id(param) -> (bucket, offset)
         self._order = None
         self._bn_flat = None
+        self._replace_grads = False  # a bucket folded held .grad values in (see _launch)
+        self._hooks = None           # CPU path: post-accumulate-grad hooks (_arm_cpu)
+        self._cpu_armed = False
         module.__dict__["_segamd_sync"] = self  # plain attribute: not a registered submodule
         if init_sync:
             self._broadcast_state()
@@ -148,8 +151,20 @@ class DataParallel(nn.Module):
             b = self._buckets[slot[0]]
             b.pending -= 1
             if b.pending == 0:
-                op = dist.ReduceOp.AVG if self._avg else dist.ReduceOp.SUM
-                b.handle = dist.all_reduce(b.buf, op=op, group=self.pg, async_op=True)
+                self._launch(b)
+
+    def _launch(self, b):
+        """All-reduce bucket `b` (asynchronous, on the current stream's RCCL queue).  Like
+        torch DDP, what is reduced is the gradient .grad would hold after this backward's
+        accumulation: the engine wrote this backward's gradients into the bucket, so any
+        .grad already held (micro-batches under no_sync(), or no zero_grad between steps)
+        is added in first; autograd_grads then REPLACES .grad with the average."""
+        held = [(self.grad_storage(p), p.grad) for p in b.params if p.grad is not None]
+        if held:
+            torch._foreach_add_([v for v, _ in held], [g for _, g in held])
+            self._replace_grads = True
+        op = dist.ReduceOp.AVG if self._avg else dist.ReduceOp.SUM
+        b.handle = dist.all_reduce(b.buf, op=op, group=self.pg, async_op=True)
 
     def _arm(self):
         for b in self._buckets:
@@ -179,6 +194,11 @@ class DataParallel(nn.Module):
         itself."""
         copies = {}
         out = []
+        if self._replace_grads:  # the buckets already include the held .grad values
+            for p in params:
+                if id(p) in self._slot:
+                    p.grad = None
+            self._replace_grads = False
         for p in params:
             slot = self._slot.get(id(p))
             if slot is None:
@@ -193,8 +213,10 @@ class DataParallel(nn.Module):
 
     @contextlib.contextmanager
     def no_sync(self):
-        """Like torch DDP's no_sync(): backward passes inside the context keep their
-        gradients local (no all-reduce); they accumulate into .grad as usual."""
+        """As torch DDP's no_sync(): backward passes inside the context keep their
+        gradients local and accumulate them into .grad; the first synchronised backward
+        after it all-reduces .grad + its own gradients (see _launch), so every rank ends
+        with the average of the accumulated sums."""
         d = self.module.__dict__
         saved = d.pop("_segamd_sync", None)
         try:
@@ -203,11 +225,45 @@ class DataParallel(nn.Module):
             if saved is not None:
                 d["_segamd_sync"] = saved
 
+    # ------------------------------------------------------ CPU (torch-op) forward
+    def _cpu_hook(self, p):
+        """Post-accumulate-grad hook of the CPU path (main.py's CPU device runs the torch
+        composition, seg_amd/export.py): when a bucket's .grads are all accumulated, pack
+        them, all-reduce (gloo) and write the average back -- torch DDP's reducer."""
+        if not self._cpu_armed:
+            return
+        k, _ = self._slot[id(p)]
+        b = self._buckets[k]
+        b.pending -= 1
+        if b.pending:
+            return
+        with torch.no_grad():
+            for q in b.params:
+                v = self.grad_storage(q)
+                v.copy_(q.grad) if q.grad is not None else v.zero_()
+            dist.all_reduce(b.buf, op=dist.ReduceOp.SUM, group=self.pg)
+            b.buf.mul_(1.0 / self.world)
+            for q in b.params:
+                if q.grad is not None:
+                    q.grad.copy_(self.grad_storage(q))
+
+    def _arm_cpu(self):
+        if self._hooks is None:
+            self._hooks = [p.register_post_accumulate_grad_hook(self._cpu_hook)
+                           for b in self._buckets for p in b.params]
+        for b in self._buckets:
+            b.pending = len(b.params)
+        self._cpu_armed = True
+
     # --------------------------------------------------------------- forward
     def _pre(self, x):
+        self._cpu_armed = False
         if self.module.__dict__.get("_segamd_sync") is self:
             self._ensure_plan(x)
-            self._arm()
+            if x.device.type == "cpu":
+                self._arm_cpu()
+            else:
+                self._arm()
         if self.broadcast_buffers and self.module.training:
             self._broadcast_bn_buffers()
 

@@ -558,14 +558,15 @@ class Program:
                                  kin))
                     max_elems = max(max_elems, op.cin * op.ldk_d)
                 continue
-            wino_ok = op.ks == 3 and op.stride == 1 and op.pad == 1
+            dense3 = op.ks == 3 and op.stride == 1 and op.pad == 1
+            wino_ok = dense3 and WINOGRAD
             op.wino_f = wino_ok and bool(query("seg_conv_wino_pick", y.N, y.H, y.W, op.cin_pad, op.cout))
             op.wino_d = wino_ok and not op.first and bool(query("seg_conv_wino_pick", y.N, y.H, y.W, r4(op.cout),
                                                                 op.cin))
             op.wino_w = wino_ok and bool(query("seg_conv_wino_wgrad_pick", y.N, y.H, y.W, op.cin_pad, op.cout))
-            op.halo_f = (wino_ok and not op.wino_f
+            op.halo_f = (dense3 and not op.wino_f
                          and bool(query("seg_conv_halo_pick", y.N, y.H, y.W, op.cin_pad, op.cout)))
-            op.halo_d = (wino_ok and not op.first and not op.wino_d
+            op.halo_d = (dense3 and not op.first and not op.wino_d
                          and bool(query("seg_conv_halo_pick", y.N, y.H, y.W, r4(op.cout), op.cin)))
             if op.wino_f:
                 op.wk_wf = torch.empty(16 * op.cout * op.cin_pad, device=dev, dtype=torch.float32)
@@ -1091,6 +1092,10 @@ class Run:
 # memory-bound BatchNorm / depthwise / 1x1 kernels of the main stream.  Results are the
 # same either way (the kernels and their reduction orders do not change).
 OVERLAP = os.environ.get("SEG_OVERLAP", "1") == "1"
+# Winograd F(2x2,3x3) for the deep f32 3x3 convs (read when a program's weights are first
+# packed); SEG_WINO=0 routes them to the LDS-halo / implicit-GEMM kernels instead (parity
+# diagnostics: tests/test_gpu_unet_cfg5.py separates Winograd from accumulation error).
+WINOGRAD = os.environ.get("SEG_WINO", "1") == "1"
 # LDS-halo direct 3x3 conv for the narrow convs in the bf16io configuration; SEG_HALO_BF16=0 turns it off.
 HALO_BF16 = os.environ.get("SEG_HALO_BF16", "1") == "1"
 # lazy BatchNorm for 1x1 consumers (the inverted residuals' project convs, OutConv's last
@@ -1210,6 +1215,7 @@ class Plan:
         self.t = None            # the last forward's labels (loss mode)
         self.busy = False        # a forward whose backward has not run yet
         self.timer = None        # the KernelTimer the tapes' timing is armed for
+        self.fp = None           # _fingerprint(prog) the tapes were recorded against
 
     def _streams(self):
         main = torch.cuda.current_stream(self.device).cuda_stream
@@ -1305,16 +1311,54 @@ class Plan:
             self.sync.finish_gradient_sync()  # stream-ordered wait on the last all-reduces
 
 
+def _fingerprint(prog):
+    """Storage pointers of every tensor a plan's tapes point into: conv / BN parameters and
+    BN running statistics.  A change (load_state_dict(assign=True), p.data = ..., .half(),
+    DataParallel's flat BN buffers) invalidates the recorded tapes."""
+    out = []  # read from the modules each time: a rebinding replaces the tensor object
+    for op in prog.ops:
+        if isinstance(op, ConvOp):
+            c, b = op.conv, op.bn
+            out += [c.weight.data_ptr(), c.bias.data_ptr() if c.bias is not None else 0]
+            if b is not None:
+                out += [t.data_ptr() if t is not None else 0
+                        for t in (b.weight, b.bias, b.running_mean, b.running_var, b.num_batches_tracked)]
+    return tuple(out)
+
+
+# Launch plans kept per model (each holds its buffers: ~13 GB at bs=32 256x512 fp32, half in
+# bf16io).  Least recently used plans beyond this are dropped; release_plans() drops all.
+MAX_PLANS = int(os.environ.get("SEG_MAX_PLANS", "4"))
+
+
+def release_plans(model):
+    """Drop every recorded plan (tapes + persistent buffers) of `model`; the next step
+    re-records.  Frees the plan memory, e.g. after evaluating at another resolution."""
+    model = getattr(model, "module", model)
+    model.__dict__.pop("_segamd_plans", None)
+
+
 def _plan(model, prog, mode, ignore_index, sync, needs_grad, device):
     cache = model.__dict__.setdefault("_segamd_plans", {})
     key = (id(prog), mode, model.training, ignore_index, id(sync) if sync is not None else None, needs_grad, OVERLAP)
-    plan = cache.get(key)
-    if plan is None or plan.sync is not sync:
-        plan = cache[key] = Plan(prog, model.training, mode, ignore_index, sync, needs_grad, device)
+    fp = _fingerprint(prog)
+    plan = cache.pop(key, None)  # re-inserted below: dict order = least recently used first
+    if plan is None or plan.sync is not sync or plan.fp != fp:
+        if plan is not None and plan.busy:
+            raise RuntimeError("segamd: parameters or buffers were rebound between a forward and its backward")
+        plan = Plan(prog, model.training, mode, ignore_index, sync, needs_grad, device)
+        plan.fp = fp
+    cache[key] = plan
+    while len(cache) > max(MAX_PLANS, 1):
+        old = next(k for k in cache)
+        if cache[old].busy:  # its backward is still to come: keep it (and stop evicting)
+            break
+        del cache[old]
     if plan.busy:
         # a second forward before this plan's backward ran: a one-off plan keeps the first
         # forward's activations intact (recorded and run once, then dropped)
         plan = Plan(prog, model.training, mode, ignore_index, sync, needs_grad, device)
+        plan.fp = fp
     return plan
 
 
@@ -1338,6 +1382,8 @@ class _SegFunction(torch.autograd.Function):
         if mode == "loss":
             model.__dict__["_segamd_last_stats"] = plan.run.stats
             out = plan.run.stats[0].clone()  # the stats buffer is rewritten by the next step
+        else:  # an unfused criterion checks its own labels: no stale flag from an earlier fused loss
+            model.__dict__.pop("_segamd_last_stats", None)
         if needs_grad:
             plan.busy = True
             ctx.plan, ctx.params = plan, params
@@ -1370,18 +1416,26 @@ class _SegFunction(torch.autograd.Function):
         return (None, None, None, None, None, None, *grads)
 
 
-def check_targets(model):
+def bad_label_count(model):
+    """Device tensor [1] (fp32): the number of labels outside [0, C) other than
+    ignore_index seen by `model`'s last fused loss, or None (no fused loss yet).  Reading it
+    is one host sync; train_one_epoch reads it (summed over ranks) before optimizer.step()."""
+    model = getattr(model, "module", model)
+    st = model.__dict__.get("_segamd_last_stats")
+    return None if st is None else st[2:3].clone()
+
+
+def check_targets(model, bad=None):
     """Raise like nn.CrossEntropyLoss ("Target out of bounds") if the last fused loss of
     `model` saw a label outside [0, C) other than ignore_index.  The kernels flag it
     stream-ordered (the loss and every gradient become NaN); this reads the flag (one
-    host sync), so callers check when the loss is NaN."""
-    model = getattr(model, "module", model)
-    st = model.__dict__.get("_segamd_last_stats")
-    if st is not None:
-        bad = int(st[2].item())
-        if bad:
-            raise IndexError(f"Target out of bounds: {bad} label(s) outside [0, num_classes) that are not "
-                             "ignore_index (nn.CrossEntropyLoss raises on these)")
+    host sync).  bad: an already-gathered count (e.g. summed over ranks)."""
+    if bad is None:
+        bad = bad_label_count(model)
+    n = 0 if bad is None else int(bad.item())
+    if n:
+        raise IndexError(f"Target out of bounds: {n} label(s) outside [0, num_classes) that are not "
+                         "ignore_index (nn.CrossEntropyLoss raises on these)")
 
 
 def _params_for(model, x):

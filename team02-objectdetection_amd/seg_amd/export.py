@@ -48,24 +48,48 @@ def _up(u, x1, x2):
 
 
 def _check(x):
-    if x.is_cuda:
+    if x.device.type != "cpu":
         raise RuntimeError("seg_amd.traceable() modules are for export and CPU use; on the MI355X run the segamd "
                            "model itself (the HIP path)")
 
 
+def mobilenet_unet_forward(m, x):
+    """MobileNetV2UNet.forward (src/unet.py:32-51) over m's own modules, in torch ops."""
+    x1 = _stage(m.down1, x)
+    x2 = _stage(m.down2, x1)
+    x3 = _stage(m.down3, x2)
+    x4 = _stage(m.down4, x3)
+    x5 = _stage(m.down5, x4)
+    x = _up(m.up1, x5, x4)
+    x = _up(m.up2, x, x3)
+    x = _up(m.up3, x, x2)
+    x = _up(m.up4, x, x1)
+    return m.final_upsample(m.outc.conv(x))
+
+
+def unet_forward(m, x):
+    """UNet / LightUNet.forward (src/unet.py:137-147, :160-171) over m's own modules."""
+    x1 = m.inc.conv.conv(x)
+    x2 = m.down1.mpconv[1].conv(m.down1.mpconv[0](x1))
+    x3 = m.down2.mpconv[1].conv(m.down2.mpconv[0](x2))
+    x4 = m.down3.mpconv[1].conv(m.down3.mpconv[0](x3))
+    x = _up(m.up1, x4, x3)
+    x = _up(m.up2, x, x2)
+    x = _up(m.up3, x, x1)
+    return m.sem_out.conv(x)
+
+
+def torch_forward(model, x):
+    """The reference composition of `model` (a segamd model) in torch ops on its OWN
+    parameters, under autograd.  Used for CPU tensors only (main.py:13-21's CPU device,
+    BASELINE configs[0]); CUDA input always runs the HIP engine (unet._SegModel.forward)."""
+    _check(x)
+    return mobilenet_unet_forward(model, x) if isinstance(model, MobileNetV2UNet) else unet_forward(model, x)
+
+
 class TorchMobileNetV2UNet(MobileNetV2UNet):
     def forward(self, x):
-        _check(x)
-        x1 = _stage(self.down1, x)
-        x2 = _stage(self.down2, x1)
-        x3 = _stage(self.down3, x2)
-        x4 = _stage(self.down4, x3)
-        x5 = _stage(self.down5, x4)
-        x = _up(self.up1, x5, x4)
-        x = _up(self.up2, x, x3)
-        x = _up(self.up3, x, x2)
-        x = _up(self.up4, x, x1)
-        return self.final_upsample(self.outc.conv(x))
+        return torch_forward(self, x)
 
     def forward_loss(self, x, target, ignore_index: int = -100):
         return nn.functional.cross_entropy(self(x), target, ignore_index=ignore_index)
@@ -73,15 +97,7 @@ class TorchMobileNetV2UNet(MobileNetV2UNet):
 
 class _TorchUNetMixin:
     def forward(self, x):
-        _check(x)
-        x1 = self.inc.conv.conv(x)
-        x2 = self.down1.mpconv[1].conv(self.down1.mpconv[0](x1))
-        x3 = self.down2.mpconv[1].conv(self.down2.mpconv[0](x2))
-        x4 = self.down3.mpconv[1].conv(self.down3.mpconv[0](x3))
-        x = _up(self.up1, x4, x3)
-        x = _up(self.up2, x, x2)
-        x = _up(self.up3, x, x1)
-        return self.sem_out.conv(x)
+        return torch_forward(self, x)
 
     def forward_loss(self, x, target, ignore_index: int = -100):
         return nn.functional.cross_entropy(self(x), target, ignore_index=ignore_index)

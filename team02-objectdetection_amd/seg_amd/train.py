@@ -38,6 +38,23 @@ def _is_rank0() -> bool:
         torch.distributed.get_rank() == 0
 
 
+def _check_labels(model, inputs):
+    """Raise IndexError like nn.CrossEntropyLoss if the fused loss saw a label outside
+    [0, C) (the kernels flag it; the loss and gradients are NaN).  Runs BEFORE
+    optimizer.step(), so no NaN reaches the weights; under torch.distributed the count is
+    summed over ranks first, so every rank raises together instead of one rank leaving
+    the others in the next collective."""
+    if not inputs.is_cuda:
+        return  # the CPU composition's F.cross_entropy raises by itself
+    from .engine import bad_label_count, check_targets
+    bad = bad_label_count(model)
+    if bad is None:
+        return
+    if torch.distributed.is_available() and torch.distributed.is_initialized() and hasattr(model, "module"):
+        torch.distributed.all_reduce(bad, group=getattr(model, "pg", None))
+    check_targets(model, bad)
+
+
 def compute_loss(model, criterion, inputs, targets):
     """criterion(model(inputs), targets), fused when the pair allows it."""
     core = getattr(model, "module", model)
@@ -74,11 +91,9 @@ def train_one_epoch(model, train_loader, criterion, optimizer, device, epoch: in
         sync = getattr(model, "finish_gradient_sync", None)
         if sync is not None:
             sync()
+        _check_labels(model, inputs)  # before the update, on every rank (nn.CrossEntropyLoss raises in the forward)
         optimizer.step()
         lv = loss.item()
-        if lv != lv:  # NaN: a label outside [0, C) raises, as nn.CrossEntropyLoss does
-            from .engine import check_targets
-            check_targets(model)
         train_loss += lv
         nb += 1
         if bar is not None:

@@ -9,8 +9,9 @@ state_dict keys as the reference (src/unet.py:7-171), so that
 The modules hold parameters/buffers only.  `forward` runs the whole network
 on the MI355X HIP kernels (seg_amd/engine.py) as one autograd node: NHWC
 activations, fused BN/activation/residual, virtual skip-concat, and a backward
-pass that is the engine's own reverse program.  There is deliberately no CPU
-path: calling a model on a non-CUDA tensor raises.
+pass that is the engine's own reverse program.  GPU input never falls back to
+anything else; CPU input (the reference's CPU device, main.py:13-21) runs the
+reference composition in torch ops (seg_amd/export.py) for that device only.
 """
 from __future__ import annotations
 
@@ -66,15 +67,24 @@ class outconv(nn.Module):
 
 
 class _SegModel(nn.Module):
-    """Shared forward: everything runs through the HIP engine."""
+    """Shared forward.  A CUDA tensor runs through the HIP engine (and nothing else: a
+    missing libsegamd.so raises).  A CPU tensor -- main.py:13-21 picks the CPU when no GPU
+    is present, BASELINE configs[0] -- runs the reference's own composition in torch ops
+    on this module's parameters (seg_amd.export.torch_forward), so train_model, Adam and
+    state_dict work there too; the product never selects it for GPU input."""
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
+        if x.device.type == "cpu":
+            from .export import torch_forward
+            return torch_forward(self, x)
         from .engine import run_logits
         return run_logits(self, x)
 
     def forward_loss(self, x: torch.Tensor, target: torch.Tensor, ignore_index: int = -100) -> torch.Tensor:
         """nn.CrossEntropyLoss()(self(x), target) (main.py:99, src/train.py:37) fused
         with the final upsample: the full-resolution logits are never stored."""
+        if x.device.type == "cpu":
+            return nn.functional.cross_entropy(self(x), target, ignore_index=ignore_index)
         from .engine import run_loss
         return run_loss(self, x, target, ignore_index)
 

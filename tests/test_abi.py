@@ -14,7 +14,7 @@ HEADER = os.path.join(REPO, "include", "segamd.h")
 
 CTYPE = {"const float*": ctypes.c_void_p, "float*": ctypes.c_void_p, "const long long*": ctypes.c_void_p,
          "long long*": ctypes.c_void_p, "int*": ctypes.c_void_p, "const void*": ctypes.c_void_p, "const seg_bf16*": ctypes.c_void_p, "seg_bf16*": ctypes.c_void_p, "const unsigned char*": ctypes.c_void_p, "unsigned char*": ctypes.c_void_p, "hipStream_t": ctypes.c_void_p, "const SegAdamTensor*": ctypes.c_void_p, "const long*": ctypes.c_void_p, "long": ctypes.c_long, "void*": ctypes.c_void_p, "void**": ctypes.c_void_p, "const int*": ctypes.c_void_p,
-         "const char*": ctypes.c_char_p,
+         "const char*": ctypes.c_char_p, "char*": ctypes.c_char_p,
          "int": ctypes.c_int, "float": ctypes.c_float}
 
 
@@ -82,3 +82,16 @@ def test_argument_validation_without_gpu(lib):
     assert rc == 1  # row_bytes < 3 * Wf
     rc = lib.seg_argmax_nearest(None, 10, 1, 64, 128, 10, 128, 256, None, 720, 1280, None)
     assert rc == 1  # ld not a multiple of 4
+
+
+def test_build_hash_decides_staleness(lib):
+    """The library carries the source hash it was built from; build() relinks exactly when
+    the tree's hash differs (not by file times) and the binding refuses a mismatch."""
+    from seg_amd import build as b
+    buf = ctypes.create_string_buffer(80)
+    assert lib.seg_build_hash(buf, 80) == 64
+    assert buf.value.decode() == b.source_hash() == b.library_hash()
+    os.utime(LIB_PATH, (1, 1))  # an old mtime alone must not trigger a rebuild
+    before = open(LIB_PATH, "rb").read()
+    build()
+    assert open(LIB_PATH, "rb").read() == before

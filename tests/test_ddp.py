@@ -108,3 +108,66 @@ def test_ddp_bucketed_allreduce_gloo():
     results = mgr.dict()
     mp.spawn(_worker, args=(world, _free_port(), results), nprocs=world, join=True)
     assert dict(results) == {0: True, 1: True}
+
+
+def _train_worker(rank, world, port, results):
+    """Real training steps of a CPU model under DataParallel (the torch-op composition;
+    the reducer is DataParallel's post-accumulate-grad hooks): a step with one
+    micro-batch under no_sync() followed by a synchronised one, then a plain step."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        torch.set_num_threads(2)
+        from seg_amd import UNet
+        from seg_amd.ddp import DataParallel
+        from seg_amd.detinit import deterministic_init, synthetic_batch
+        model = deterministic_init(UNet(4, 8), seed=50 + rank)  # broadcast makes them equal
+        dp = DataParallel(model, bucket_cap_mb=0.05)
+        assert len(dp._buckets or []) == 0
+        out = []
+        xs = [synthetic_batch(2, 32, 64, 4, seed=10 * rank + k) for k in range(3)]
+        model.zero_grad(set_to_none=True)
+        with dp.no_sync():
+            dp.forward_loss(*xs[0]).backward()
+        dp.forward_loss(*xs[1]).backward()
+        out.append({k: p.grad.clone() for k, p in model.named_parameters() if p.grad is not None})
+        model.zero_grad(set_to_none=True)
+        dp.forward_loss(*xs[2]).backward()
+        out.append({k: p.grad.clone() for k, p in model.named_parameters() if p.grad is not None})
+        results[rank] = (out, len(dp._buckets), {k: v.clone() for k, v in model.state_dict().items()})
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+def test_ddp_cpu_no_sync_accumulation_gloo():
+    """gradients accumulated under no_sync() must be averaged by the next
+    synchronised backward -- .grad identical on both ranks and equal to the mean over
+    ranks of each rank's (micro-batch 0 + micro-batch 1) gradients, as torch DDP."""
+    world = 2
+    mgr = mp.Manager()
+    results = mgr.dict()
+    mp.spawn(_train_worker, args=(world, _free_port(), results), nprocs=world, join=True)
+    (o0, nb0, s0), (o1, nb1, s1) = results[0], results[1]
+    assert nb0 == nb1 > 1
+    from seg_amd import UNet
+    from seg_amd.detinit import deterministic_init, synthetic_batch
+    # single-process reference: each rank's local gradients from rank 0's initial weights
+    local = []
+    for r in range(world):
+        m = deterministic_init(UNet(4, 8), seed=50)
+        xs = [synthetic_batch(2, 32, 64, 4, seed=10 * r + k) for k in range(3)]
+        m.zero_grad(set_to_none=True)
+        m.forward_loss(*xs[0]).backward()
+        m.forward_loss(*xs[1]).backward()
+        acc = {k: p.grad.clone() for k, p in m.named_parameters() if p.grad is not None}
+        m.zero_grad(set_to_none=True)
+        m.forward_loss(*xs[2]).backward()
+        local.append((acc, {k: p.grad.clone() for k, p in m.named_parameters() if p.grad is not None}))
+    for step in range(2):
+        g0, g1 = o0[step], o1[step]
+        assert g0.keys() == g1.keys() == local[0][step].keys()
+        for k in g0:
+            assert torch.equal(g0[k], g1[k]), (step, k)
+            mean = (local[0][step][k] + local[1][step][k]) * 0.5
+            assert torch.allclose(g0[k], mean, rtol=1e-4, atol=1e-6), (step, k)

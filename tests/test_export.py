@@ -67,6 +67,14 @@ def test_jit_trace_and_onnx_export():
     assert len(f.getvalue()) > 1 << 20
 
 
-def test_segamd_model_still_refuses_cpu():
-    with pytest.raises(RuntimeError, match="HIP path only"):
-        MobileNetV2UNet(10)(torch.zeros(1, 3, 64, 64))
+def test_segamd_model_on_cpu_runs_the_reference_composition():
+    """main.py:13-21's CPU device: the segamd model itself runs the torch composition on
+    its own parameters (configs[0]); same logits as its traceable twin, and gradients
+    reach the model's own parameters."""
+    m = deterministic_init(MobileNetV2UNet(10), seed=2).train()
+    x = torch.randn(2, 3, 64, 64, generator=torch.Generator().manual_seed(0))
+    out = m(x)
+    twin = traceable(m)
+    assert torch.equal(out, twin(x))
+    out.sum().backward()
+    assert m.up1.conv.conv[0].weight.grad is not None

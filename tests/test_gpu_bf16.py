@@ -155,16 +155,21 @@ def _flat_grads(model):
     return out
 
 
-@pytest.mark.parametrize("math", ["bf16", "bf16io"])
-@pytest.mark.parametrize("arch,N,H,W", [("MobileNetV2UNet", 2, 64, 128), ("UNet", 2, 32, 64)])
-def test_model_bf16_vs_oracle(arch, N, H, W, math):
+@pytest.mark.parametrize("arch,N,H,W,math", [
+    ("MobileNetV2UNet", 2, 64, 128, "bf16"), ("MobileNetV2UNet", 2, 64, 128, "bf16io"),
+    ("UNet", 2, 32, 64, "bf16"), ("UNet", 2, 32, 64, "bf16io"),
+    # BASELINE configs[2]'s resolution (256x512) in its storage configuration: the kernel
+    # choices of the deep encoder layers and the 1344-channel up1 concat at full width
+    ("MobileNetV2UNet", 2, 256, 512, "bf16io")])
+def test_model_bf16_vs_oracle(arch, N, H, W, math, record):
     """One training forward + backward in bf16 math against the fp64 oracle.  Budget = the
     reference's OWN bf16 error: the same oracle with autocast-style bf16 conv operands
     (segref.bf16_convs) run in fp64.  At these tiny random-init shapes the train-mode
     BatchNorms amplify bf16 rounding chaotically (MobileNetV2UNet: ~20 % logits error
     for the emulated reference itself, measured), so the bar is relative to it:
     logits / loss error <= 1.5x the reference's (+1e-3), each gradient tensor
-    <= 3x the reference's (+1e-3 of its norm, +1e-4 of the global norm)."""
+    <= 3x the reference's (+1e-3 of its norm, +1e-4 of the global norm); bf16io
+    (which also rounds every stored tensor) 3x / 6x."""
     ctor = (lambda: MobileNetV2UNet(10)) if arch == "MobileNetV2UNet" else (lambda: UNet(10, 64))
     model_cpu = deterministic_init(ctor(), seed=5)
     x, y = synthetic_batch(N, H, W, 10, seed=6)
@@ -191,13 +196,18 @@ def test_model_bf16_vs_oracle(arch, N, H, W, math):
     assert got_l <= fz * ref_l + 1e-3
     g = _flat_grads(model)
     gnorm = float(torch.sqrt(sum((t ** 2).sum() for t in g64.values())))
-    bad = []
+    bad, worst, wname = [], 0.0, None
     for k, t64 in g64.items():
         assert k in g, f"missing grad {k}"
         d = float((g[k] - t64).norm())
         budget = fg * float((ge[k] - t64).norm()) + 1e-3 * float(t64.norm()) + 1e-4 * gnorm
+        if d / budget > worst:
+            worst, wname = d / budget, k
         if d > budget:
             bad.append((k, d, budget))
+    print(f"worst gradient {worst:.3f} of budget ({wname})")
+    record(arch=arch, shape=[N, H, W], math=math, logits_err=got_z, logits_err_ref_bf16=ref_z, loss_err=got_l,
+           loss_err_ref_bf16=ref_l, worst=worst, worst_name=wname)
     assert not bad, bad[:8]
 
 

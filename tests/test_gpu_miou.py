@@ -42,7 +42,7 @@ def _eval_preds(model, xe):
     return p
 
 
-def test_miou_parity_after_50_steps(golden_dir):
+def test_miou_within_reference_envelope_after_150_steps(golden_dir, record):
     z = np.load(os.path.join(golden_dir, "mnv2_miou_scene_150steps.npz"), allow_pickle=False)
     c = json.loads(str(z["meta"]))
     xe, ye = synthetic_scene(c["heldout"], c["h"], c["w"], c["classes"], seed=c["heldout_seed"])
@@ -62,6 +62,7 @@ def test_miou_parity_after_50_steps(golden_dir):
     print(f"mIoU after {c['steps']} steps: HIP {m1:.5f}; reference fp32 {refs[0]:.5f}, fp32 1-thread {refs[1]:.5f}, "
           f"fp64 {refs[2]:.5f}; |HIP - ref fp32| = {abs(m1 - refs[0]):.2e}; pixel agreement with the reference "
           f"fp32 {agree:.4f}")
+    record(steps=c["steps"], miou_hip=m1, miou_ref=refs, abs_diff_ref_fp32=abs(m1 - refs[0]), pixel_agreement=agree)
     assert m1 > 5 * m0, "the scene must be learnable (mIoU well above chance after training)"
     assert min(refs) - 1e-3 <= m1 <= max(refs) + 1e-3, (m1, refs)
     # identical weights: the oracle's eval forward of the trained HIP weights

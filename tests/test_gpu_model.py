@@ -198,10 +198,22 @@ def test_full_size_properties():
     assert abs(l2.item() - l0.item()) <= 1e-5 * abs(l0.item())
 
 
-def test_cpu_input_raises():
-    model = make("MobileNetV2UNet", 10, 0)
-    with pytest.raises(RuntimeError, match="HIP path only"):
-        model(torch.zeros(1, 3, 64, 64))
+def test_cuda_input_never_takes_the_torch_composition(monkeypatch):
+    """The torch-op composition (seg_amd.export.torch_forward) serves CPU tensors only
+    (main.py's CPU device); a CUDA input must run the HIP engine -- poison the
+    composition and run both modes on the GPU."""
+    from seg_amd import export
+
+    def poisoned(*a, **k):
+        raise AssertionError("CUDA input reached the torch composition")
+    monkeypatch.setattr(export, "torch_forward", poisoned)
+    model = make("MobileNetV2UNet", 10, 0).to(DEV).train()
+    x, y = synthetic_batch(1, 64, 64, 10, seed=0)
+    model.forward_loss(x.to(DEV), y.to(DEV)).backward()
+    with torch.no_grad():
+        assert model(x.to(DEV)).is_cuda
+    with pytest.raises(AssertionError, match="torch composition"):
+        model.cpu()(x)
 
 
 def test_traceable_twin_matches_hip_eval():

@@ -366,6 +366,18 @@ def test_ce_target_out_of_bounds(bad):
     t[0, 5, 5] = -100  # ignore_index is fine
     assert torch.isfinite(model.forward_loss(x, t))
     check_targets(model)
+    # train_model raises BEFORE optimizer.step(): no NaN reaches the weights
+    from torch import nn
+    from seg_amd import train_model
+    t[0, 5, 5] = bad
+    before = {k: v.clone() for k, v in model.state_dict().items() if v.is_floating_point() and "running" not in k}
+    opt = torch.optim.Adam(model.parameters(), lr=1e-3)
+    with pytest.raises(IndexError, match="Target out of bounds"):
+        train_model(model, [(x, t)], nn.CrossEntropyLoss(), opt, DEV, epochs=1, checkpoint_pattern=None,
+                    progress=False)
+    for k, v in model.state_dict().items():
+        if k in before:
+            assert torch.equal(v, before[k]), k
 
 
 def test_colsum_and_add():

@@ -105,3 +105,35 @@ def test_kernel_timer_reads_tape_launches():
     # per step: the 8 decoder 3x3 convs forward + data gradient and the stem forward
     assert len(rec) == 3 * 17, len(rec)
     assert all(s > 0 for _, _, s in rec)
+
+
+def test_rebound_parameters_rerecord_the_tape():
+    """the tapes hold raw parameter / BN-buffer pointers, so rebinding them
+    (load_state_dict(assign=True)) must re-record instead of replaying into freed memory.
+    After the rebind the step equals a fresh model's with the same state, bit for bit;
+    the plan cache stays bounded (engine.MAX_PLANS) and release_plans() empties it."""
+    x, y = synthetic_batch(2, 64, 128, 10, seed=61)
+    x, y = x.to(DEV), y.to(DEV)
+    model = deterministic_init(MobileNetV2UNet(10), seed=5).to(DEV).train()
+    tape_step(model, x, y)
+    tape_step(model, x, y)
+    other = deterministic_init(MobileNetV2UNet(10), seed=6).to(DEV).train()
+    sd = {k: v.clone() for k, v in other.state_dict().items()}
+    model.load_state_dict({k: v.clone() for k, v in sd.items()}, assign=True)
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()
+    l1, g1 = tape_step(model, x, y)
+    fresh = deterministic_init(MobileNetV2UNet(10), seed=6).to(DEV).train()
+    fresh.load_state_dict(sd)
+    l2, g2 = tape_step(fresh, x, y)
+    assert torch.equal(l1, l2)
+    for k in g2:
+        assert torch.equal(g1[k], g2[k]), k
+    for hw in ((64, 64), (32, 64), (64, 96), (96, 64), (32, 32), (64, 128)):
+        xs, ys = synthetic_batch(1, *hw, 10, seed=1)
+        tape_step(model, xs.to(DEV), ys.to(DEV))
+    assert len(model.__dict__["_segamd_plans"]) <= engine.MAX_PLANS
+    engine.release_plans(model)
+    assert "_segamd_plans" not in model.__dict__
+    l3, g3 = tape_step(model, x, y)
+    assert torch.isfinite(l3)

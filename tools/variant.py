@@ -9,7 +9,7 @@ from concurrent.futures import ThreadPoolExecutor
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(REPO, "team02-objectdetection_amd"))
-from seg_amd.build import ARCH, FLAGS, HIPCC, sources  # noqa: E402
+from seg_amd.build import ARCH, FLAGS, GEN_DIR, HIPCC, _write_hash_source, source_hash, sources  # noqa: E402
 
 
 def main():
@@ -25,6 +25,10 @@ def main():
         return obj
     with ThreadPoolExecutor(8) as ex:
         objs = list(ex.map(one, sources()))
+    os.makedirs(GEN_DIR, exist_ok=True)
+    hobj = os.path.join(odir, "build_hash.o")  # seg_build_hash: the tree's hash (SEG_LIB_PATH skips the check)
+    subprocess.run([HIPCC, "-O2", "-fPIC", "-c", _write_hash_source(source_hash()), "-o", hobj], check=True)
+    objs.append(hobj)
     os.makedirs(os.path.join(REPO, "variants"), exist_ok=True)
     out = os.path.join(REPO, "variants", name + ".so")
     subprocess.run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", out, *objs], check=True)

@@ -28,6 +28,7 @@ def main():
     ap.add_argument("--width", type=int, default=512)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--top", type=int, default=60)
+    ap.add_argument("--csv", default=None, help="also write every launch (us, label, entry, kind, M, Cin, Cout) here")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     model = seg_amd.deterministic_init(getattr(seg_amd, a.model)(10), seed=0).to(dev).train()
@@ -54,7 +55,7 @@ def main():
     for t in timer.tapes:
         for r, label, name, kind, flops, sec in t.elapsed(detail=True):
             per[(label, name)].append(sec)
-    rows = []
+    rows, csv_rows = [], []
     for (label, name), secs in per.items():
         k, phase = label.split(":") if label else ("-1", "")
         op = prog.ops[int(k)] if label else None
@@ -64,6 +65,10 @@ def main():
         elif op is not None:
             desc = type(op).__name__
         rows.append((statistics.median(secs) * 1e6, label, name, desc, len(secs)))
+        if a.csv:
+            shp = (op.kind, op.ks, op.stride, op.y.M, op.inp.M, op.cin, op.cout) if isinstance(op, E.ConvOp) else \
+                (type(op).__name__, 0, 0, 0, 0, 0, 0)
+            csv_rows.append((statistics.median(secs) * 1e6, label, name) + shp)
     total = sum(r[0] for r in rows)
     by_name = collections.Counter()
     for us, label, name, desc, n in rows:
@@ -75,6 +80,12 @@ def main():
     print()
     for us, label, name, desc, n in sorted(rows, reverse=True)[:a.top]:
         print(f"{us:9.1f} us  {label:9s} {name:32s} {desc}")
+    if a.csv:
+        import csv
+        with open(a.csv, "w", newline="") as fh:
+            w = csv.writer(fh)
+            w.writerow(["us", "label", "entry", "kind", "ks", "stride", "M_out", "M_in", "cin", "cout"])
+            w.writerows(sorted(csv_rows, key=lambda r: r[1]))
 
 
 if __name__ == "__main__":

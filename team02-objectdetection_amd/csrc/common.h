@@ -100,6 +100,35 @@ __device__ __forceinline__ float wave_sum(float v) {
 
 static inline int seg_cdiv(long a, long b) { return (int)((a + b - 1) / b); }
 
+// In-launch hand-off to the block that arrives last (a reduction's finalize folded into
+// the reduction's own launch).  The 8 XCDs' L2s are not coherent with each other, so the
+// payload (a few partial-sum words per block) is stored and loaded write-through at agent
+// scope -- relaxed atomic accesses, which bypass the non-coherent caches (no release or
+// acquire fence needed) -- and every storing wave drains its stores before the block's
+// one ticket add.  The block whose add returns the last ticket therefore reads every
+// other block's payload, whatever the dispatch order or XCD placement; it re-arms the
+// counter (zero) for the next launch, so a caller zeroes it once, before the first use.
+__device__ __forceinline__ void seg_st_wt(float* p, float v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ float seg_ld_wt(const float* p) {
+  return __hip_atomic_load(const_cast<float*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// Called by every thread of the block after its payload stores; block-uniform result.
+// `word`: one int of LDS the block does not otherwise use at this point.
+__device__ __forceinline__ bool seg_last_arrival(unsigned* cnt, unsigned nblocks, int* word) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's payload has landed
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned t = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int last = t == nblocks - 1;
+    if (last) __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-arm
+    *word = last;
+  }
+  __syncthreads();
+  return *word != 0;
+}
+
 // XCD-aware block swizzle (bijective for any nblk): the dispatcher deals blocks
 // round-robin over the 8 XCDs (block b and b+8 share an XCD and its 4 MiB L2), so
 // remap hardware block b to a logical id such that each XCD walks a CONTIGUOUS

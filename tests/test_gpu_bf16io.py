@@ -57,7 +57,7 @@ def test_add_apply_stats_backward_colsum():
         out = torch.empty(4 * C, device=DEV)
         rm, rv = torch.zeros(C, device=DEV), torch.ones(C, device=DEV)
         gamma, beta = torch.linspace(0.5, 1.5, C, device=DEV), torch.linspace(-1, 1, C, device=DEV)
-        work = torch.empty(query("seg_chan_workspace_floats", M, C), device=DEV)
+        work = torch.zeros(query("seg_chan_workspace_floats", M, C), device=DEV)
         call(name, y.data_ptr(), C, M, C, gamma.data_ptr(), beta.data_ptr(), 1e-5, 0.1, rm.data_ptr(), rv.data_ptr(),
              None, work.data_ptr(), out[:C].data_ptr(), out[C:2 * C].data_ptr(), out[2 * C:3 * C].data_ptr(),
              out[3 * C:].data_ptr(), s)
@@ -77,7 +77,7 @@ def test_add_apply_stats_backward_colsum():
         for tag, (d, y, name, dt) in {"f": (d32, y32, "seg_bn_backward", torch.float32),
                                       "b": (d16, y16, "seg_bn_backward_bf16io", BF)}.items():
             gw, gb = torch.empty(C, device=DEV), torch.empty(C, device=DEV)
-            work = torch.empty(query("seg_chan_workspace_floats", M, C) + 3 * C, device=DEV)
+            work = torch.zeros(query("seg_chan_workspace_floats", M, C) + 3 * C, device=DEV)
             dy = torch.empty(M, C, device=DEV, dtype=dt)
             call(name, d.data_ptr(), C, y.data_ptr(), C, M, C, gamma.data_ptr(), mean.data_ptr(), invstd.data_ptr(),
                  scale.data_ptr(), shift.data_ptr(), act, gw.data_ptr(), gb.data_ptr(), work.data_ptr(), dy.data_ptr(),
@@ -89,7 +89,7 @@ def test_add_apply_stats_backward_colsum():
     cs = {}
     for tag, d, name in (("f", d32, "seg_colsum"), ("b", d16, "seg_colsum_bf16io")):
         o = torch.empty(C - 2, device=DEV)
-        work = torch.empty(query("seg_chan_workspace_floats", M, C), device=DEV)
+        work = torch.zeros(query("seg_chan_workspace_floats", M, C), device=DEV)
         call(name, d.data_ptr(), C, M, C - 2, work.data_ptr(), o.data_ptr(), 0, s)
         cs[tag] = o
     assert torch.equal(cs["f"], cs["b"])
@@ -145,7 +145,7 @@ def test_row_tiled_passes(M, C, ld, off):
         for tag, d, y, name, dt in (("f", d32, y32, "seg_bn_backward", torch.float32),
                                     ("b", d16, y16, "seg_bn_backward_bf16io", BF)):
             gw, gb = torch.empty(C, device=DEV), torch.empty(C, device=DEV)
-            work = torch.empty(query("seg_chan_workspace_floats", M, C) + 3 * C, device=DEV)
+            work = torch.zeros(query("seg_chan_workspace_floats", M, C) + 3 * C, device=DEV)
             dy = fresh(dt)
             call(name, p(d), ld, p(y), ld, M, C, gamma.data_ptr(), mean.data_ptr(), invstd.data_ptr(),
                  scale.data_ptr(), shift.data_ptr(), act, gw.data_ptr(), gb.data_ptr(), work.data_ptr(), p(dy), ld, s)

@@ -228,7 +228,7 @@ def test_batchnorm_train(act, M, C, shift):
     rmg, rvg = rm.to(DEV), rv.to(DEV)
     nbt = torch.zeros(1, dtype=torch.int64, device=DEV)
     st = torch.empty(4 * C, device=DEV)
-    work = torch.empty(query("seg_chan_workspace_floats", M, C) + 3 * C, device=DEV)
+    work = torch.zeros(query("seg_chan_workspace_floats", M, C) + 3 * C, device=DEV)
     call("seg_bn_stats", yg.data_ptr(), C, M, C, gg.data_ptr(), bgp.data_ptr(), 1e-5, 0.1, rmg.data_ptr(),
          rvg.data_ptr(), nbt.data_ptr(), work.data_ptr(), st[0:C].data_ptr(), st[C:2 * C].data_ptr(),
          st[2 * C:3 * C].data_ptr(), st[3 * C:].data_ptr(), s)
@@ -385,7 +385,7 @@ def test_colsum_and_add():
     y = gen(M, r4(C), seed=1)
     s = S()
     yg = y.to(DEV)
-    work = torch.empty(query("seg_chan_workspace_floats", M, r4(C)), device=DEV)
+    work = torch.zeros(query("seg_chan_workspace_floats", M, r4(C)), device=DEV)
     out = torch.empty(C, device=DEV)
     call("seg_colsum", yg.data_ptr(), r4(C), M, C, work.data_ptr(), out.data_ptr(), 0, s)
     assert rel(out, y[:, :C].sum(0)) < 1e-5
@@ -620,3 +620,49 @@ def test_wgrad_reduce_direct(mode, Cout, Cin, ks, splits):
     err = float((outs[0].double().cpu() - ref).abs().max())
     assert err <= 1e-5 * splits ** 0.5 * float(ref.abs().max() + 1), err
     assert torch.equal(outs[2], outs[0] + outs[0])
+
+
+@pytest.mark.parametrize("M,C", [(262144, 96), (65536, 1280), (100, 12)])
+def test_reduction_in_launch_finalize_repeatable_under_load(M, C):
+    """The channel reductions finalize inside their own launch: the last-arriving block
+    sums every block's partials (write-through hand-off across the XCDs' L2s,
+    csrc/common.h seg_last_arrival) and re-arms its ticket word.  Reusing one workspace
+    call after call -- with a large GEMM running on another stream, so blocks arrive in
+    uneven orders -- must give bitwise the same statistics, BN backward and column sums
+    every time, the ticket words back at zero, and results equal to fp64 torch."""
+    y = (gen(M, C, seed=11) * 2 + 1).to(DEV)
+    da = gen(M, C, seed=12).to(DEV)
+    gamma, beta = torch.ones(C, device=DEV), torch.zeros(C, device=DEV)
+    work = torch.zeros(query("seg_chan_workspace_floats", M, C) + 3 * C, device=DEV)
+    other = torch.cuda.Stream()
+    big = torch.randn(4096, 4096, device=DEV)
+    outs = []
+    for rep in range(6):
+        with torch.cuda.stream(other):
+            if rep % 2:
+                torch.mm(big, big)  # uneven load on part of the chip while the reduction runs
+        s = S()
+        st = torch.empty(4 * C, device=DEV)
+        call("seg_bn_stats", y.data_ptr(), C, M, C, gamma.data_ptr(), beta.data_ptr(), 1e-5, 0.1, None, None, None,
+             work.data_ptr(), st[0:C].data_ptr(), st[C:2 * C].data_ptr(), st[2 * C:3 * C].data_ptr(),
+             st[3 * C:].data_ptr(), s)
+        dg, db, dy = torch.empty(C, device=DEV), torch.empty(C, device=DEV), torch.empty(M, C, device=DEV)
+        call("seg_bn_backward", da.data_ptr(), C, y.data_ptr(), C, M, C, gamma.data_ptr(), st[0:C].data_ptr(),
+             st[C:2 * C].data_ptr(), st[2 * C:3 * C].data_ptr(), st[3 * C:].data_ptr(), 1, dg.data_ptr(),
+             db.data_ptr(), work.data_ptr(), dy.data_ptr(), C, s)
+        cs = torch.empty(C, device=DEV)
+        call("seg_colsum", da.data_ptr(), C, M, C, work.data_ptr(), cs.data_ptr(), 0, s)
+        torch.cuda.synchronize()
+        assert int(work[:16].view(torch.int32).abs().sum()) == 0, "ticket words must be re-armed"
+        outs.append((st.clone(), dg.clone(), db.clone(), dy.clone(), cs.clone()))
+    for o in outs[1:]:
+        for a, b in zip(outs[0], o):
+            assert torch.equal(a, b)
+    y64, d64 = y.double().cpu(), da.double().cpu()
+    st, dg, db, dy, cs = outs[0]
+    assert rel(st[:C], y64.mean(0)) < 1e-6
+    assert rel(st[C:2 * C], 1 / torch.sqrt(y64.var(0, unbiased=False) + 1e-5)) < 1e-6
+    assert rel(cs, d64.sum(0)) < 1e-5
+    z = (y64 - y64.mean(0)) * (1 / torch.sqrt(y64.var(0, unbiased=False) + 1e-5))
+    dz = d64 * (z > 0)
+    assert rel(db, dz.sum(0)) < 1e-5 and rel(dg, (dz * z).sum(0)) < 1e-5

@@ -39,7 +39,7 @@ def main():
             da = torch.randn(M, C, device="cuda").to(dt)
             out = torch.empty_like(y)
             v = [torch.rand(C, device="cuda") + 0.5 for _ in range(6)]
-            work = torch.empty(query("seg_chan_workspace_floats", M, C) + 3 * C, device="cuda")
+            work = torch.zeros(query("seg_chan_workspace_floats", M, C) + 3 * C, device="cuda")
             bwd = lambda: call("seg_bn_backward" + suf, da.data_ptr(), C, y.data_ptr(), C, M, C, v[0].data_ptr(),
                                v[1].data_ptr(), v[2].data_ptr(), v[3].data_ptr(), v[4].data_ptr(), 2, v[5].data_ptr(),
                                v[5].data_ptr(), work.data_ptr(), out.data_ptr(), C, s)

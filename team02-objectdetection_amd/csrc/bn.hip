@@ -38,6 +38,9 @@ constexpr int kRedSlice = 64;  // channel groups per block (blockIdx.y slices be
 #ifndef SEG_CHAN_MAXBLK
 #define SEG_CHAN_MAXBLK 256
 #endif
+#ifndef SEG_BN_FOLD
+#define SEG_BN_FOLD 0  // 1: finalize in the reduction's launch (last-arriving block); 0: finalize kernels
+#endif
 #ifndef SEG_APPLY_ROWS4
 #define SEG_APPLY_ROWS4 0
 #endif
@@ -188,9 +191,21 @@ __global__ __launch_bounds__(kRedThreads) void chan_partial_kernel(
     const int cc = cg0 * VW + ch;
     double a = 0.0, b = 0.0;
     if (ch < SC) {
-      for (int rr = jj; rr < nblk; rr += P) {
-        a += (double)seg_ld_wt(part + (long)rr * 2 * C + cc);
-        if (KIND != 2) b += (double)seg_ld_wt(part + (long)rr * 2 * C + C + cc);
+      // 16 rows' loads in flight per thread (clamped index, masked add: no branch around a load)
+      for (int r0 = jj; r0 < nblk; r0 += 16 * P) {
+        float va[16], vb[16];
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+          const int rr = min(r0 + q * P, nblk - 1);
+          va[q] = seg_ld_wt(part + (long)rr * 2 * C + cc);
+          vb[q] = KIND != 2 ? seg_ld_wt(part + (long)rr * 2 * C + C + cc) : 0.f;
+        }
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+          const bool ok = r0 + q * P < nblk;
+          a += ok ? (double)va[q] : 0.0;
+          b += ok ? (double)vb[q] : 0.0;
+        }
       }
     }
     __syncthreads();  // red0 / red1 are free again
@@ -240,22 +255,113 @@ __global__ __launch_bounds__(kRedThreads) void chan_partial_kernel(
 
 // Launch chan_partial_kernel<KIND> over [M][C] (C % 4 == 0): 8-channel lanes when C, the
 // row strides and the tensors' element offsets are multiples of 8 (16-byte bf16 loads),
-// else 4 -- a decision in elements, identical for fp32 and bf16 storage.  The finalize
-// runs in the same launch (the last-arriving block of each channel slice, `fin`).
+// else 4 -- a decision in elements, identical for fp32 and bf16 storage.  fin set: the
+// finalize runs in the same launch (the last-arriving block of each channel slice);
+// otherwise the partials are left for a finalize kernel.
 template <int KIND, typename T>
 void launch_chan_partial(const T* y, long ldy, const T* da, long ldda, long M, int C, const float* scale,
                          const float* shift, const float* mean, int act, float* part, hipStream_t stream,
-                         const ChanFin& fin) {
+                         const ChanFin* fin) {
   const int nblk = chan_blocks(M);
   const int rpb = seg_cdiv(M, nblk);
   auto eoff8 = [](const T* p) { return ((uintptr_t)p / sizeof(T)) % 8 == 0; };
   const bool v8 = C % 8 == 0 && ldy % 8 == 0 && (!da || ldda % 8 == 0) && eoff8(y) && (!da || eoff8(da));
-  if (v8)
-    hipLaunchKernelGGL((chan_partial_kernel<KIND, T, 8, true>), dim3(nblk, seg_cdiv(C / 8, kRedSlice)),
-                       dim3(kRedThreads), 0, stream, y, ldy, da, ldda, (int)M, C, scale, shift, mean, act, part, rpb, fin);
-  else
-    hipLaunchKernelGGL((chan_partial_kernel<KIND, T, 4, true>), dim3(nblk, seg_cdiv(C / 4, kRedSlice)),
-                       dim3(kRedThreads), 0, stream, y, ldy, da, ldda, (int)M, C, scale, shift, mean, act, part, rpb, fin);
+  ChanFin f{};
+  if (fin) f = *fin;
+#define SEG_CP(VW, F)                                                                                          \
+  hipLaunchKernelGGL((chan_partial_kernel<KIND, T, VW, F>), dim3(nblk, seg_cdiv(C / VW, kRedSlice)),           \
+                     dim3(kRedThreads), 0, stream, y, ldy, da, ldda, (int)M, C, scale, shift, mean, act, part, rpb, f)
+  if (v8) {
+    if (fin) SEG_CP(8, true); else SEG_CP(8, false);
+  } else {
+    if (fin) SEG_CP(4, true); else SEG_CP(4, false);
+  }
+#undef SEG_CP
+}
+
+// Separate finalize kernels (SEG_BN_FOLD == 0).  Sum the per-block partials (<= 256 rows:
+// chan_blocks) of one channel with one wave: lane l loads rows l, l+64, l+128, l+192 all at
+// once (one memory round trip; clamped index, masked add), sums them in that order in
+// fp64, then a fixed xor butterfly (fp64 adds are commutative, so every lane ends with the
+// same bits; deterministic).  Four channels per 256-thread block: c = blockIdx.x * 4 + wave.
+__device__ __forceinline__ bool sum_partials(const float* __restrict__ part, int nblk, int C, int ldp, int* cout,
+                                             double* s0, double* s1) {
+  const int lane = threadIdx.x & 63;
+  const int c = blockIdx.x * 4 + (threadIdx.x >> 6);
+  *cout = c;
+  if (c >= C) return false;
+  float va[4], vb[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const long k = min(lane + 64 * q, nblk - 1);
+    va[q] = part[k * 2 * ldp + c];
+    vb[q] = part[k * 2 * ldp + ldp + c];
+  }
+  double a = 0.0, b = 0.0;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const bool ok = lane + 64 * q < nblk;
+    a += ok ? (double)va[q] : 0.0;
+    b += ok ? (double)vb[q] : 0.0;
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    a += __shfl_xor(a, o, 64);
+    b += __shfl_xor(b, o, 64);
+  }
+  *s0 = a;
+  *s1 = b;
+  return lane == 0;
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void bn_finalize_kernel(
+    const float* __restrict__ part, int nblk, const T* __restrict__ y, long M, int C,
+    const float* __restrict__ gamma, const float* __restrict__ beta, float eps, float momentum,
+    float* running_mean, float* running_var, long long* nbt, float* mean_out, float* invstd_out, float* scale_out,
+    float* shift_out) {
+  if (blockIdx.x == 0 && threadIdx.x == 0 && nbt) *nbt += 1;
+  int c;
+  double s, s2;
+  if (!sum_partials(part, nblk, C, C, &c, &s, &s2)) return;
+  const double k = (float)y[c];
+  const double dm = s / (double)M;
+  const double mean = k + dm;
+  double var = s2 / (double)M - dm * dm;
+  if (var < 0.0) var = 0.0;
+  const float invstd = (float)(1.0 / sqrt(var + (double)eps));
+  mean_out[c] = (float)mean;
+  invstd_out[c] = invstd;
+  const float g = gamma ? gamma[c] : 1.f, bt = beta ? beta[c] : 0.f;
+  scale_out[c] = g * invstd;
+  shift_out[c] = bt - (float)mean * g * invstd;
+  if (running_mean) {
+    const double unbiased = M > 1 ? var * (double)M / (double)(M - 1) : var;
+    running_mean[c] = (float)((1.0 - momentum) * running_mean[c] + momentum * mean);
+    running_var[c] = (float)((1.0 - momentum) * running_var[c] + momentum * unbiased);
+  }
+}
+
+__global__ void bn_bwd_finalize_kernel(const float* __restrict__ part, int nblk, long M, int C,
+                                       const float* __restrict__ gamma, const float* __restrict__ invstd,
+                                       float* dgamma, float* dbeta, float* coef) {
+  int c;
+  double sdz, sdzx;
+  if (!sum_partials(part, nblk, C, C, &c, &sdz, &sdzx)) return;
+  const double inv = invstd[c];
+  const double g = gamma ? gamma[c] : 1.0;
+  if (dbeta) dbeta[c] = (float)sdz;
+  if (dgamma) dgamma[c] = (float)(sdzx * inv);
+  // dY = g*inv * (dz - mean(dz) - xhat*mean(dz*xhat)),  xhat = (y-mean)*inv
+  coef[c] = (float)(g * inv);
+  coef[C + c] = (float)(sdz / (double)M);
+  coef[2 * C + c] = (float)(sdzx * inv * inv / (double)M);
+}
+
+__global__ void colsum_finalize_kernel(const float* __restrict__ part, int nblk, int C, int ldp, float* out,
+                                       int accumulate) {
+  int c;
+  double s, unused;
+  if (sum_partials(part, nblk, C, ldp, &c, &s, &unused)) out[c] = accumulate ? out[c] + (float)s : (float)s;
 }
 
 // BN statistics from the conv epilogue's per-row-tile partials part[t][2][C]
@@ -309,16 +415,32 @@ __global__ __launch_bounds__(256) void bn_finalize_tiles_kernel(
     __syncthreads();
     return r;
   };
+  // 16 tiles' loads in flight per thread (clamped index, masked add), summed in tile order
   double s = 0.0;
-#pragma unroll 4
-  for (int i = t; i < ntiles; i += 256) s += part[(long)i * 2 * C + c];
+  for (int i0 = t; i0 < ntiles; i0 += 16 * 256) {
+    float v[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) v[j] = part[(long)min(i0 + j * 256, ntiles - 1) * 2 * C + c];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) s += i0 + j * 256 < ntiles ? (double)v[j] : 0.0;
+  }
   const double mean = tree(s) / (double)M;
   double q = 0.0;
-#pragma unroll 4
-  for (int i = t; i < ntiles; i += 256) {
-    const double nt = tile_rows_of(i, tile_rows, M);
-    const double d = part[(long)i * 2 * C + c] / nt - mean;
-    q += part[(long)i * 2 * C + C + c] + nt * d * d;
+  for (int i0 = t; i0 < ntiles; i0 += 16 * 256) {
+    float v[16], w[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const long i = min(i0 + j * 256, ntiles - 1);
+      v[j] = part[i * 2 * C + c];
+      w[j] = part[i * 2 * C + C + c];
+    }
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const int i = i0 + j * 256;
+      const double nt = tile_rows_of(i, tile_rows, M);
+      const double d = v[j] / nt - mean;
+      q += i < ntiles ? w[j] + nt * d * d : 0.0;
+    }
   }
   const double m2 = tree(q);
   if (t == 0)
@@ -337,20 +459,29 @@ __global__ __launch_bounds__(256) void bn_finalize_tiles_wave_kernel(
   if (blockIdx.x == 0 && threadIdx.x == 0 && nbt) *nbt += 1;
   if (c >= C) return;
   double sv[4], qv[4];
-  int nv = 0;
+  float fs[4], fq[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {  // ntiles <= 256: at most 4 tiles per lane, loaded together
+    const long i = min(lane + 64 * k, ntiles - 1);
+    fs[k] = part[i * 2 * C + c];
+    fq[k] = part[i * 2 * C + C + c];
+  }
   double s = 0.0;
-  for (int i = lane; i < ntiles; i += 64, ++nv) {  // ntiles <= 256: at most 4 tiles per lane
-    sv[nv] = part[(long)i * 2 * C + c];
-    qv[nv] = part[(long)i * 2 * C + C + c];
-    s += sv[nv];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const bool ok = lane + 64 * k < ntiles;
+    sv[k] = fs[k];
+    qv[k] = fq[k];
+    s += ok ? sv[k] : 0.0;
   }
   for (int o = 1; o < 64; o <<= 1) s += __shfl_xor(s, o, 64);
   const double mean = s / (double)M;
   double q = 0.0;
-  for (int k = 0; k < nv; ++k) {
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
     const double nt = tile_rows_of(lane + 64 * k, tile_rows, M);
     const double d = sv[k] / nt - mean;
-    q += qv[k] + nt * d * d;
+    q += lane + 64 * k < ntiles ? qv[k] + nt * d * d : 0.0;
   }
   for (int o = 1; o < 64; o <<= 1) q += __shfl_xor(q, o, 64);
   if (lane == 0)
@@ -685,7 +816,15 @@ static int bn_stats_impl(const T* y, long ldy, long M, int C, const float* gamma
   f.M = M; f.gamma = gamma; f.beta = beta; f.eps = eps; f.momentum = momentum;
   f.rmean = running_mean; f.rvar = running_var; f.nbt = num_batches_tracked;
   f.mean_out = mean; f.invstd_out = invstd; f.scale_out = scale; f.shift_out = shift;
-  launch_chan_partial<0, T>(y, ldy, nullptr, 0L, M, C, nullptr, nullptr, nullptr, 0, work + kCntWords, stream, f);
+  if (SEG_BN_FOLD) {
+    launch_chan_partial<0, T>(y, ldy, nullptr, 0L, M, C, nullptr, nullptr, nullptr, 0, work + kCntWords, stream, &f);
+  } else {
+    launch_chan_partial<0, T>(y, ldy, nullptr, 0L, M, C, nullptr, nullptr, nullptr, 0, work + kCntWords, stream,
+                              nullptr);
+    hipLaunchKernelGGL(bn_finalize_kernel<T>, dim3(seg_cdiv(C, 4)), dim3(256), 0, stream, work + kCntWords,
+                       chan_blocks(M), y, M, C, gamma, beta, eps, momentum, running_mean, running_var,
+                       num_batches_tracked, mean, invstd, scale, shift);
+  }
   SEG_RET_LAST();
 }
 SEG_API int seg_bn_stats(const float* y, long ldy, long M, int C, const float* gamma, const float* beta, float eps,
@@ -767,7 +906,13 @@ static int bn_backward_impl(const T* da, long ldda, const T* y, long ldy, long M
   ChanFin f{};
   f.cnt = reinterpret_cast<unsigned*>(work);
   f.M = M; f.gamma = gamma; f.invstd = invstd; f.dgamma = dgamma; f.dbeta = dbeta; f.coef = coef;
-  launch_chan_partial<1, T>(y, ldy, da, ldda, M, C, scale, shift, mean, act, work + kCntWords, stream, f);
+  if (SEG_BN_FOLD) {
+    launch_chan_partial<1, T>(y, ldy, da, ldda, M, C, scale, shift, mean, act, work + kCntWords, stream, &f);
+  } else {
+    launch_chan_partial<1, T>(y, ldy, da, ldda, M, C, scale, shift, mean, act, work + kCntWords, stream, nullptr);
+    hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(seg_cdiv(C, 4)), dim3(256), 0, stream, work + kCntWords,
+                       chan_blocks(M), M, C, gamma, invstd, dgamma, dbeta, coef);
+  }
   launch_bn_bwd_apply<T>(da, ldda, y, ldy, M, C, scale, shift, mean, act, coef, dy, lddy, stream);
   SEG_RET_LAST();
 }
@@ -804,7 +949,14 @@ static int colsum_impl(const T* y, long ldy, long M, int C, float* work, float* 
   ChanFin f{};
   f.cnt = reinterpret_cast<unsigned*>(work);
   f.M = M; f.out = out; f.accumulate = accumulate; f.C_out = C;
-  launch_chan_partial<2, T>(y, ldy, nullptr, 0L, M, C4, nullptr, nullptr, nullptr, 0, work + kCntWords, stream, f);
+  if (SEG_BN_FOLD) {
+    launch_chan_partial<2, T>(y, ldy, nullptr, 0L, M, C4, nullptr, nullptr, nullptr, 0, work + kCntWords, stream, &f);
+  } else {
+    launch_chan_partial<2, T>(y, ldy, nullptr, 0L, M, C4, nullptr, nullptr, nullptr, 0, work + kCntWords, stream,
+                              nullptr);
+    hipLaunchKernelGGL(colsum_finalize_kernel, dim3(seg_cdiv(C, 4)), dim3(256), 0, stream, work + kCntWords,
+                       chan_blocks(M), C, C4, out, accumulate);
+  }
   SEG_RET_LAST();
 }
 SEG_API int seg_colsum(const float* y, long ldy, long M, int C, float* work, float* out, int accumulate,

@@ -437,6 +437,20 @@ int seg_tape_timing(void* tape, const int* idx, int n, int max_replays);
 int seg_tape_elapsed(void* tape, float* out);
 int seg_tape_run(void* tape, int begin, hipStream_t main, hipStream_t side, int* stop);
 
+/* seg_conv_igemm2_bf16io: implicit GEMM for the deep convs of the bf16io configuration
+ * (replaces aten conv2d / convolution_backward(input) of src/unet.py:58,61 and 1x1 convs
+ * with Cin >= 64): 8-wave 128x256 / 256x128 tiles, LDS-DMA operand staging, split-K
+ * combined in-launch by the last-arriving K slice (csrc/igemm2.hip).  Stride 1, pad
+ * (ks-1)/2, ks 1 or 3, bf16 rows (ldin, ldout, ldadd % 8 == 0, 16-byte aligned), bf16
+ * packed weights (seg_pack_batch mode | 16, ldk % 8 == 0).  seg_conv_igemm2_plan(M, Cout,
+ * Cin, ks, out[4]) returns 1 when the kernel applies and fills {tile rows, row tiles,
+ * split-K slices, workspace floats}; stat (optional) = BN partials [row tiles][2][Cout];
+ * work = that many floats, zeroed once before the first use (calls leave it re-armed). */
+int seg_conv_igemm2_plan(long M, int Cout, int Cin, int ks, long* out);
+int seg_conv_igemm2_bf16io(const seg_bf16* in, long ldin, int N, int H, int W, int Cin, const seg_bf16* wk, int ldk,
+                           const float* bias, seg_bf16* out, long ldout, int Cout, int ks, const seg_bf16* add,
+                           long ldadd, float* stat, float* work, hipStream_t stream);
+
 /* Build identity (host only): copies the SHA-256 (64 hex chars + NUL) of the sources this
  * library was built from -- every csrc file, this header, compiler and flags
  * (seg_amd/build.py source_hash) -- into out when cap > 64; returns the length.  The

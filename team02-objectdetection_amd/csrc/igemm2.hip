@@ -1,0 +1,428 @@
+// Implicit-GEMM convolution for the deep convs of the bf16io configuration, built for the
+// bf16 MFMA's operand rate (the 16-bit igemm_conv_kernel ran the 3x3 family at
+// 0.16 of the bf16 MFMA peak, bound by L2 -> LDS operand traffic).
+//
+//   out[p][co] = sum_{tap, ci} in[p + tap][ci] * W[co][tap][ci] (+ bias) (+ add)
+//
+// Replaces aten's conv2d / convolution_backward(input) of the decoder's double_conv
+// (src/unet.py:58,61: up1/up2 of MobileNetV2UNet, the deep levels of UNet) and of 1x1
+// convs, on bf16 activation rows with bf16-packed weights (seg_pack_batch mode | 16).
+//
+// Structure (one 512-thread block = 8 waves per CU):
+//  * block tile 128 x 256 or 256 x 128 (pixels x output channels), wave tile 64 x 64
+//    (2 x 2 v_mfma_f32_32x32x16_bf16 accumulators): one 16-byte LDS fragment read per MFMA
+//    (4 per 4 MFMAs), half the re-reads of every operand tile in L2 of the 64 x 128 tile;
+//  * K steps of 64 bf16 (128-byte operand rows) staged global -> LDS by LDS-DMA
+//    (global_load_lds_dwordx4, no VGPR round trip), two LDS buffers, the next step's DMA in
+//    flight while the current one computes; waits are counted vmcnt + raw s_barrier, so no
+//    barrier drains a DMA that is still in flight;
+//  * XOR-swizzled operand rows (16-byte chunk c of row r stored at c ^ ((r >> 1) & 7)):
+//    the DMA writes LDS lane-linearly, so the permutation is applied to each lane's SOURCE
+//    address and undone on the fragment read -- conflict-free ds_read_b128;
+//  * the A operand is the implicit im2col of NHWC rows: a 64-deep K step covers at most two
+//    filter taps (Cin >= 64), and a lane's 16-byte chunk is one pixel's 8 channels of one
+//    tap -- out-of-image taps and rows beyond M read a zero page (no branch);
+//  * split-K when the output tiles alone cannot fill the chip: each K slice writes its fp32
+//    tile write-through, the slice whose ticket arrives last sums the slices in slice order
+//    (deterministic, whatever the arrival order) and runs the epilogue -- no reduce launch;
+//  * epilogue as igemm_conv_kernel's: bias, BatchNorm tile partials (sum, M2 about the tile
+//    mean) for seg_bn_stats_tiles, addend, one rounding to bf16, 16-byte row stores staged
+//    through LDS.
+#include "common.h"
+
+namespace {
+
+constexpr int kBK = 64;             // K step (bf16 elements) = one 128-byte operand row
+constexpr int kThreads = 512;
+
+__device__ __attribute__((aligned(16))) unsigned g_zero_row[4];  // 16 zero bytes
+
+struct Igemm2Args {
+  const __bf16* in; long ldin;
+  const __bf16* wk; int ldk;        // [Cout][ldk] bf16, k = tap * Cin + ci
+  const float* bias;
+  const __bf16* add; long ldadd;    // may alias out
+  __bf16* out; long ldout;
+  float* stat;                      // BN tile partials [tiles_m][2][Cout] or null
+  float* slab;                      // split-K: [tiles][splits][BM * BN] fp32
+  unsigned* cnt;                    // split-K: [tiles] tickets (zero before the first launch; left zero)
+  int N, H, W, Cin, Cout, ks, pad;
+  int K, M, nsteps, steps_per_split, splits, tiles_m, tiles_n;
+};
+
+__device__ __forceinline__ void dma16(const void* src, char* lds) {
+  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                   (__attribute__((address_space(3))) void*)lds, 16, 0, 0);
+}
+
+// Workgroup barrier that is also a compiler fence for memory accesses but emits no wait:
+// LDS-DMA transfers stay in flight across it (a __syncthreads() would drain them).
+__device__ __forceinline__ void raw_barrier() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+__device__ __forceinline__ void wait_lgkm0() { __builtin_amdgcn_s_waitcnt(0xC07F); }  // lgkmcnt(0) only
+
+template <int N>
+__device__ __forceinline__ void wait_vm() {  // s_waitcnt vmcnt(N), other counters untouched
+  static_assert(N >= 0 && N < 16, "vmcnt immediate");
+  __builtin_amdgcn_s_waitcnt(0x0F70 | N);
+}
+
+template <int BM, int BN, int KS>
+__global__ __launch_bounds__(kThreads) void igemm2_kernel(Igemm2Args a) {
+  constexpr int WM = 64, WN = 64, WAVES_N = BN / WN;
+  static_assert((BM / WM) * (BN / WN) == 8, "8 waves");
+  constexpr int A_BYTES = BM * 128, STAGE = (BM + BN) * 128;
+  constexpr int NA = BM / 64, NB = BN / 64;  // DMA instructions per wave per K step
+  constexpr int CSR = BN + 4;                // epilogue band row stride (floats)
+  constexpr int SMEM = 2 * STAGE > WM * CSR * 4 ? 2 * STAGE : WM * CSR * 4;
+  __shared__ __attribute__((aligned(1024))) char smem[SMEM];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm0 = (wave / WAVES_N) * WM, wn0 = (wave % WAVES_N) * WN;
+  // a tile's K slices are adjacent logical ids: the same XCD (and L2) combines them
+  const int lid = xcd_swizzle(blockIdx.x, gridDim.x);
+  const int tile = lid / a.splits, z = lid - tile * a.splits;
+  const int tn = tile % a.tiles_n, tm = tile / a.tiles_n;
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int s_beg = z * a.steps_per_split;
+  const int nst = min(a.nsteps - s_beg, a.steps_per_split);
+
+  // ---- per-lane DMA sources.  Instruction j of a tile covers rows 8j .. 8j+7 (1 KB of LDS);
+  // wave w issues j = w, w + 8, ...; lane l fills row 8j + (l >> 3), physical chunk l & 7,
+  // i.e. logical chunk cl = (l & 7) ^ swz(row).
+  const int lrow = lane >> 3, lchk = lane & 7;
+  long a_off[NA];
+  unsigned a_mask[NA];
+  int a_cl[NA];
+#pragma unroll
+  for (int i = 0; i < NA; ++i) {
+    const int row = 8 * (wave + 8 * i) + lrow;
+    a_cl[i] = lchk ^ ((row >> 1) & 7);
+    const int p = m0 + row;
+    const bool ok = p < a.M;
+    const int pp = ok ? p : 0;
+    const int hw = a.H * a.W;
+    const int n = pp / hw, rem = pp - n * hw;
+    const int ho = rem / a.W, wo = rem - ho * a.W;
+    const int hi0 = ho - KS / 2, wi0 = wo - KS / 2;
+    a_off[i] = (((long)n * a.H + hi0) * a.W + wi0) * a.ldin;
+    unsigned m = 0;
+#pragma unroll
+    for (int t = 0; t < KS * KS; ++t) {
+      const int hi = hi0 + t / KS, wi = wi0 + t % KS;
+      if (ok && (unsigned)hi < (unsigned)a.H && (unsigned)wi < (unsigned)a.W) m |= 1u << t;
+    }
+    a_mask[i] = m;
+  }
+  long b_off[NB];
+  int b_k[NB];  // this lane's k offset within a step (8 * logical chunk); 2^30: row beyond Cout
+#pragma unroll
+  for (int i = 0; i < NB; ++i) {
+    const int row = 8 * (wave + 8 * i) + lrow;
+    const int cl = lchk ^ ((row >> 1) & 7);
+    const int co = n0 + row;
+    b_k[i] = co < a.Cout ? 8 * cl : 1 << 30;
+    b_off[i] = (long)(co < a.Cout ? co : 0) * a.ldk + 8 * cl;
+  }
+  // wave-uniform K-step position: tap u_tap, channel u_ci of the step's first k
+  const int k_beg = s_beg * kBK;
+  int u_tap = k_beg / a.Cin, u_ci = k_beg - u_tap * a.Cin;
+  auto tap_off = [&](int t) -> long { return ((long)(t / KS) * a.W + t % KS) * a.ldin; };
+  long u_toff0 = tap_off(u_tap), u_toff1 = tap_off(u_tap + 1);
+  int k0 = k_beg;
+
+  auto issue = [&](int buf) {  // DMA of the K step at (u_tap, u_ci, k0) into LDS buffer `buf`
+    char* As = smem + buf * STAGE;
+    char* Bs = As + A_BYTES;
+#pragma unroll
+    for (int i = 0; i < NA; ++i) {
+      const int ci = u_ci + 8 * a_cl[i];
+      const bool wrap = ci >= a.Cin;
+      const int tap = u_tap + (wrap ? 1 : 0);
+      const bool ok = (a_mask[i] >> tap) & 1u;
+      const __bf16* src = a.in + a_off[i] + (wrap ? u_toff1 : u_toff0) + (wrap ? ci - a.Cin : ci);
+      dma16(ok ? (const void*)src : (const void*)g_zero_row, As + (wave + 8 * i) * 1024);
+    }
+#pragma unroll
+    for (int i = 0; i < NB; ++i) {
+      const bool ok = k0 + b_k[i] < a.K;
+      dma16(ok ? (const void*)(a.wk + b_off[i] + k0) : (const void*)g_zero_row, Bs + (wave + 8 * i) * 1024);
+    }
+    // advance one K step
+    k0 += kBK;
+    u_ci += kBK;
+    while (u_ci >= a.Cin) {
+      u_ci -= a.Cin;
+      ++u_tap;
+      u_toff0 = u_toff1;
+      u_toff1 = tap_off(u_tap + 1);
+    }
+  };
+
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+    for (int ni = 0; ni < 2; ++ni)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[mi][ni][r] = 0.f;
+
+  const int fr = lane & 31, fh = lane >> 5;
+  auto compute = [&](int buf) {
+    const char* As = smem + buf * STAGE;
+    const char* Bs = As + A_BYTES;
+#pragma unroll
+    for (int ks = 0; ks < kBK / 16; ++ks) {
+      const int chunk = 2 * ks + fh;  // logical 16-byte chunk of this lane's 8 k values
+      bf16x8 af[2], bfr[2];
+#pragma unroll
+      for (int mi = 0; mi < 2; ++mi) {
+        const int r = wm0 + mi * 32 + fr;
+        af[mi] = *reinterpret_cast<const bf16x8*>(As + r * 128 + 16 * (chunk ^ ((r >> 1) & 7)));
+      }
+#pragma unroll
+      for (int ni = 0; ni < 2; ++ni) {
+        const int r = wn0 + ni * 32 + fr;
+        bfr[ni] = *reinterpret_cast<const bf16x8*>(Bs + r * 128 + 16 * (chunk ^ ((r >> 1) & 7)));
+      }
+#pragma unroll
+      for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < 2; ++ni)
+          acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[mi], bfr[ni], acc[mi][ni], 0, 0, 0);
+    }
+  };
+
+  // ---- K loop: buffer it & 1 holds step it; step it + 1's DMA stays in flight meanwhile
+  if (nst > 0) issue(0);
+  if (nst > 1) issue(1);
+  for (int it = 0; it < nst; ++it) {
+    if (it + 1 < nst) wait_vm<NA + NB>();  // this wave's DMA of step `it` has landed
+    else wait_vm<0>();
+    raw_barrier();                         // ... and every other wave's
+    compute(it & 1);
+    wait_lgkm0();                          // this wave's fragment reads of buffer it & 1 are done
+    raw_barrier();                         // ... every wave's: the buffer may be refilled
+    if (it + 2 < nst) issue(it & 1);
+  }
+
+  // ---- split-K: publish this slice, the last-arriving slice of the tile combines
+  if (a.splits > 1) {
+    float* mine = a.slab + ((long)tile * a.splits + z) * (BM * BN);
+#pragma unroll
+    for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+      for (int ni = 0; ni < 2; ++ni)
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          seg_st_wt(mine + (((wave * 2 + mi) * 2 + ni) * 16 + r) * 64 + lane, acc[mi][ni][r]);
+    int* word = reinterpret_cast<int*>(smem);
+    if (!seg_last_arrival(a.cnt + tile, a.splits, word)) return;
+    // sum the slices in slice order (every slice read back, this one included: no
+    // data-dependent select between a register and a load)
+    f32x16 tot[2][2];
+    for (int zz = 0; zz < a.splits; ++zz) {
+      const float* sl = a.slab + ((long)tile * a.splits + zz) * (BM * BN);
+      f32x16 v[2][2];
+#pragma unroll
+      for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < 2; ++ni)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) v[mi][ni][r] = seg_ld_wt(sl + (((wave * 2 + mi) * 2 + ni) * 16 + r) * 64 + lane);
+#pragma unroll
+      for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < 2; ++ni) tot[mi][ni] = zz == 0 ? v[mi][ni] : tot[mi][ni] + v[mi][ni];
+    }
+#pragma unroll
+    for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+      for (int ni = 0; ni < 2; ++ni) acc[mi][ni] = tot[mi][ni];
+  }
+
+  // ---- epilogue.  C layout of the 32x32 MFMA: col = lane & 31, row = (r&3) + 8(r>>2) + 4(lane>>5).
+#pragma unroll
+  for (int ni = 0; ni < 2; ++ni) {
+    const int col = n0 + wn0 + ni * 32 + fr;
+    const float b = (a.bias && col < a.Cout) ? a.bias[col] : 0.f;
+#pragma unroll
+    for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[mi][ni][r] += b;
+  }
+  __syncthreads();  // the K loop / combine is done with smem
+  if (a.stat) {
+    // BatchNorm partials of this BM-row tile per output channel: tile sum, then the sum of
+    // squared deviations from the tile mean (two passes over the accumulators)
+    constexpr int WR = BM / WM;
+    float* red = reinterpret_cast<float*>(smem);  // [WR][BN]
+    float* tmean = red + WR * BN;                 // [BN]
+    const int nrows = min(BM, a.M - m0);
+    const int wr = wave / WAVES_N;
+#pragma unroll
+    for (int pass = 0; pass < 2; ++pass) {
+#pragma unroll
+      for (int ni = 0; ni < 2; ++ni) {
+        const int cl = wn0 + ni * 32 + fr;
+        const float mu = pass ? tmean[cl] : 0.f;
+        float sum = 0.f;
+#pragma unroll
+        for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int row = m0 + wm0 + mi * 32 + (r & 3) + 8 * (r >> 2) + 4 * fh;
+            const float d = acc[mi][ni][r] - mu;
+            sum += row < a.M ? (pass ? d * d : d) : 0.f;
+          }
+        sum += __shfl_xor(sum, 32, 64);
+        if (lane < 32) red[wr * BN + cl] = sum;
+      }
+      __syncthreads();
+      if (tid < BN) {
+        float t = 0.f;
+#pragma unroll
+        for (int j = 0; j < WR; ++j) t += red[j * BN + tid];
+        const int col = n0 + tid;
+        if (pass == 0) tmean[tid] = t / (float)nrows;
+        if (col < a.Cout) a.stat[((long)tm * 2 + pass) * a.Cout + col] = t;
+      }
+      __syncthreads();
+    }
+  }
+  // staged store: per band of WM rows, the owning waves park their accumulators in LDS,
+  // then every thread writes 16-byte row vectors (8 bf16 channels) with the addend
+  float* Cs = reinterpret_cast<float*>(smem);
+  constexpr int VPR = BN / 8;
+#pragma unroll
+  for (int band = 0; band < BM / WM; ++band) {
+    __syncthreads();
+    if (wm0 == band * WM) {
+#pragma unroll
+      for (int ni = 0; ni < 2; ++ni)
+#pragma unroll
+        for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+          for (int r = 0; r < 16; ++r)
+            Cs[(mi * 32 + (r & 3) + 8 * (r >> 2) + 4 * fh) * CSR + wn0 + ni * 32 + fr] = acc[mi][ni][r];
+    }
+    __syncthreads();
+    for (int v = tid; v < WM * VPR; v += kThreads) {
+      const int rr = v / VPR, cv = (v - rr * VPR) * 8;
+      const int row = m0 + band * WM + rr, col = n0 + cv;
+      if (row >= a.M || col >= a.Cout) continue;
+      float o[8];
+#pragma unroll
+      for (int j = 0; j < 8; j += 4) {
+        const f32x4 q = *reinterpret_cast<const f32x4*>(&Cs[rr * CSR + cv + j]);
+        o[j] = q[0]; o[j + 1] = q[1]; o[j + 2] = q[2]; o[j + 3] = q[3];
+      }
+      __bf16* dst = a.out + (long)row * a.ldout + col;
+      const __bf16* ad = a.add ? a.add + (long)row * a.ldadd + col : nullptr;
+      if (col + 8 <= a.Cout) {  // 16-byte aligned: ldout, ldadd and col are multiples of 8
+        if (ad) {
+          const bf16x8 q = *reinterpret_cast<const bf16x8*>(ad);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) o[j] += (float)q[j];
+        }
+        const f32x4 lo = {o[0], o[1], o[2], o[3]}, hi = {o[4], o[5], o[6], o[7]};
+        *reinterpret_cast<bf16x8*>(dst) = seg_cat8(__builtin_convertvector(lo, bf16x4),
+                                                   __builtin_convertvector(hi, bf16x4));
+      } else {
+        for (int j = 0; j < 8 && col + j < a.Cout; ++j) {
+          float x = o[j];
+          if (ad) x += (float)ad[j];
+          dst[j] = static_cast<__bf16>(x);
+        }
+      }
+    }
+  }
+}
+
+struct Plan2 {
+  int tile;       // 0: 128 x 256, 1: 256 x 128, -1: not applicable
+  int bm, bn, tiles_m, tiles_n, splits, nsteps, steps_per_split;
+  long work_floats;
+};
+
+Plan2 plan2(long M, int Cout, int Cin, int ks) {
+  Plan2 p{};
+  p.tile = -1;
+  const long K = (long)ks * ks * Cin;
+  if (M < 1 || Cout < 1 || Cin < 64 || (Cin & 7) || (ks != 1 && ks != 3)) return p;
+  double best = 0.0;
+  const int cand[2][2] = {{128, 256}, {256, 128}};
+  for (int c = 0; c < 2; ++c) {
+    const long tm = (M + cand[c][0] - 1) / cand[c][0], tn = (Cout + cand[c][1] - 1) / cand[c][1];
+    const double util = (double)M * Cout / ((double)tm * cand[c][0] * tn * cand[c][1]);
+    if (util > best + 1e-9) { best = util; p.tile = c; }
+  }
+  if (best < 0.85) { p.tile = -1; return p; }  // mostly padding: the generic kernel fits better
+  p.bm = cand[p.tile][0];
+  p.bn = cand[p.tile][1];
+  p.tiles_m = (int)((M + p.bm - 1) / p.bm);
+  p.tiles_n = (Cout + p.bn - 1) / p.bn;
+  p.nsteps = (int)((K + kBK - 1) / kBK);
+  const long tiles = (long)p.tiles_m * p.tiles_n;
+  int s = 1;
+  if (tiles < 256) s = (int)std::min<long>(std::min<long>((256 + tiles - 1) / tiles, p.nsteps / 8), 8);
+  if (s < 1) s = 1;
+  p.steps_per_split = (p.nsteps + s - 1) / s;
+  p.splits = (p.nsteps + p.steps_per_split - 1) / p.steps_per_split;  // no empty slice
+  p.work_floats = p.splits > 1 ? tiles + tiles * p.splits * (long)p.bm * p.bn : 0;
+  return p;
+}
+
+}  // namespace
+
+// Plan of seg_conv_igemm2_bf16io for an M x Cout GEMM over K = ks*ks*Cin: out[0] = tile
+// rows (the BN partials' row tiles), out[1] = row tiles, out[2] = split-K slices,
+// out[3] = workspace floats (tickets + slice tiles; 0 when unsplit).  Returns 1 when the
+// kernel applies (Cin >= 64, Cin % 8 == 0, little tile padding), else 0.
+SEG_API int seg_conv_igemm2_plan(long M, int Cout, int Cin, int ks, long* out) {
+  const Plan2 p = plan2(M, Cout, Cin, ks);
+  if (p.tile < 0) return 0;
+  if (out) {
+    out[0] = p.bm;
+    out[1] = p.tiles_m;
+    out[2] = p.splits;
+    out[3] = p.work_floats;
+  }
+  return 1;
+}
+
+// out = conv(in, W) (+bias) (+add), stride 1, pad (ks-1)/2, bf16 rows in / add / out,
+// bf16 packed weights (ldk % 8 == 0); fp32 accumulation, one rounding on the store.
+// stat (optional): BN partials [row tiles][2][Cout] of the plan's tile rows.  work: the
+// plan's workspace (zero it once before its first use; every call leaves its tickets zero).
+SEG_API int seg_conv_igemm2_bf16io(const __bf16* in, long ldin, int N, int H, int W, int Cin, const __bf16* wk,
+                                   int ldk, const float* bias, __bf16* out, long ldout, int Cout, int ks,
+                                   const __bf16* add, long ldadd, float* stat, float* work, hipStream_t stream) {
+  const long M = (long)N * H * W;
+  const Plan2 p = plan2(M, Cout, Cin, ks);
+  if (p.tile < 0 || (ldin & 7) || (ldk & 7) || (ldout & 7) || (add && (ldadd & 7)) || ldk < ks * ks * Cin ||
+      ((uintptr_t)in & 15) || ((uintptr_t)wk & 15) || ((uintptr_t)out & 15) || (add && ((uintptr_t)add & 15)) ||
+      (p.splits > 1 && !work) || M > 0x7fffffffL)
+    return (int)hipErrorInvalidValue;
+  Igemm2Args a;
+  a.in = in; a.ldin = ldin; a.wk = wk; a.ldk = ldk; a.bias = bias; a.add = add; a.ldadd = ldadd;
+  a.out = out; a.ldout = ldout; a.stat = stat;
+  a.cnt = p.splits > 1 ? reinterpret_cast<unsigned*>(work) : nullptr;
+  a.slab = p.splits > 1 ? work + (long)p.tiles_m * p.tiles_n : nullptr;
+  a.N = N; a.H = H; a.W = W; a.Cin = Cin; a.Cout = Cout; a.ks = ks; a.pad = (ks - 1) / 2;
+  a.K = ks * ks * Cin; a.M = (int)M; a.nsteps = p.nsteps; a.steps_per_split = p.steps_per_split;
+  a.splits = p.splits; a.tiles_m = p.tiles_m; a.tiles_n = p.tiles_n;
+  const int grid = p.tiles_m * p.tiles_n * p.splits;
+#define SEG_I2(BM, BN, KS) hipLaunchKernelGGL((igemm2_kernel<BM, BN, KS>), dim3(grid), dim3(kThreads), 0, stream, a)
+  if (p.tile == 0) {
+    if (ks == 3) SEG_I2(128, 256, 3); else SEG_I2(128, 256, 1);
+  } else {
+    if (ks == 3) SEG_I2(256, 128, 3); else SEG_I2(256, 128, 1);
+  }
+#undef SEG_I2
+  SEG_RET_LAST();
+}

@@ -87,6 +87,8 @@ PROTOTYPES = {
     "seg_tape_elapsed": (_I, [_V, _V]),
     "seg_tape_run": (_I, [_V, _I, _V, _V, _V]),
     "seg_build_hash": (_I, [ctypes.c_char_p, _I]),
+    "seg_conv_igemm2_plan": (_I, [_L, _I, _I, _I, _V]),
+    "seg_conv_igemm2_bf16io": (_I, [_V, _L, _I, _I, _I, _I, _V, _I, _V, _V, _L, _I, _I, _V, _L, _V, _V, _V]),
 }
 # bf16-storage variants: same C signature shape as their fp32 namesakes (pointers stay void*)
 for _n in ("seg_add", "seg_bn_stats", "seg_bn_apply", "seg_bn_backward", "seg_colsum", "seg_dw_fwd", "seg_dw_dgrad",

@@ -1,0 +1,114 @@
+"""GPU: seg_conv_igemm2_bf16io -- the LDS-DMA, 8-wave, split-K implicit GEMM for the deep
+bf16io convs (csrc/igemm2.hip).
+
+  * against a float64 conv of the same bf16 operands (rel-L2 1e-5: fp32 accumulation);
+  * unsplit launches equal the 64x128 generic kernel (seg_conv_igemm_bf16io_w16) bit for
+    bit -- both accumulate each output over k in the same 16-deep MFMA order -- which pins
+    the swizzled LDS-DMA layout and the implicit-im2col tap handling exactly;
+  * split-K launches (the last-arriving K slice combines the slices) are bitwise
+    reproducible call after call on one workspace, and leave its tickets zero;
+  * BatchNorm tile partials: the tile sums add up to the fp64 column sums, and each
+    tile's M2 equals the fp64 M2 about that tile's mean;
+  * the addend (data-gradient accumulation) and bias paths.
+"""
+import pytest
+import torch
+import torch.nn.functional as F
+
+from seg_amd import engine
+from seg_amd._lib import call, query
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+BF = torch.bfloat16
+
+
+def S():
+    return torch.cuda.current_stream().cuda_stream
+
+
+def r8(c):
+    return (c + 7) & ~7
+
+
+def rel(a, b):
+    a, b = a.double().cpu(), b.double().cpu()
+    return float((a - b).norm() / max(float(b.norm()), 1e-30))
+
+
+def plan(M, Cout, Cin, ks):
+    import ctypes
+    out = (ctypes.c_long * 4)()
+    ok = query("seg_conv_igemm2_plan", M, Cout, Cin, ks, ctypes.addressof(out))
+    return ok, list(out)
+
+
+def pack16(w, Cout, Cin, ks):
+    ldk = r8(ks * ks * Cin)
+    wk = torch.full((Cout * ldk,), float("nan"), device=DEV).to(BF)
+    table, n, blocks = engine.pack_table([(w.data_ptr(), wk.data_ptr(), Cout, Cin, ks, ldk, 16, Cin)], w.device)
+    call("seg_pack_batch", table.data_ptr(), n, blocks, S())
+    return wk, ldk
+
+
+CASES = [  # (N, Cin, Cout, H, W, ks): split-K, dgrad-shaped, ragged M, taps spanning a K step, unsplit, 1x1
+    (2, 1344, 256, 16, 32, 3), (8, 256, 1344, 8, 16, 3), (2, 128, 128, 33, 65, 3), (4, 288, 128, 64, 64, 3),
+    (32, 128, 128, 32, 64, 3), (2, 960, 256, 16, 16, 1)]
+
+
+@pytest.mark.parametrize("N,Cin,Cout,H,W,ks", CASES)
+def test_igemm2_vs_fp64_and_generic(N, Cin, Cout, H, W, ks):
+    M = N * H * W
+    ok, (tile_rows, ntiles, splits, work_floats) = plan(M, Cout, Cin, ks)
+    assert ok, "the plan must apply to these shapes"
+    g = torch.Generator().manual_seed(N * 1000 + Cin)
+    x = (torch.randn(M, Cin, generator=g) * 1.3 + 0.2).to(BF)
+    w = torch.randn(Cout, Cin, ks, ks, generator=g) * (2.0 / (Cin * ks * ks)) ** 0.5
+    b = torch.randn(Cout, generator=g)
+    add = (torch.randn(M, Cout, generator=g)).to(BF)
+    xg, wg, bg, addg = x.to(DEV), w.to(DEV), b.to(DEV), add.to(DEV)
+    wk, ldk = pack16(wg, Cout, Cin, ks)
+    x64 = x.double().view(N, H, W, Cin).permute(0, 3, 1, 2)
+    ref = F.conv2d(x64, w.to(BF).double(), b.double(), padding=ks // 2).permute(0, 2, 3, 1).reshape(M, Cout)
+    work = torch.zeros(max(work_floats, 1), device=DEV)
+    outs = []
+    for rep in range(3):
+        y = torch.full((M, Cout), 7.0, device=DEV).to(BF)
+        st = torch.full((ntiles * 2 * Cout,), float("nan"), device=DEV)
+        call("seg_conv_igemm2_bf16io", xg.data_ptr(), Cin, N, H, W, Cin, wk.data_ptr(), ldk, bg.data_ptr(),
+             y.data_ptr(), Cout, Cout, ks, None, 0, st.data_ptr(), work.data_ptr(), S())
+        outs.append((y, st))
+    torch.cuda.synchronize()
+    y, st = outs[0]
+    for y2, st2 in outs[1:]:
+        assert torch.equal(y, y2) and torch.equal(st, st2), "split-K combine must be deterministic"
+    if splits > 1:
+        bn = 256 if tile_rows == 128 else 128
+        tiles = ntiles * ((Cout + bn - 1) // bn)
+        assert int(work[:tiles].view(torch.int32).abs().sum()) == 0, "tickets re-armed"
+    assert rel(y.float(), ref) < 4e-3  # the bf16 rounding of the stored output
+    # statistics on the fp32 accumulator: tile sums and M2 about each tile's mean
+    stv = st.view(ntiles, 2, Cout).double().cpu()
+    assert rel(stv[:, 0].sum(0), ref.sum(0)) < 1e-5
+    for t in (0, ntiles - 1):
+        blk = ref[t * tile_rows:(t + 1) * tile_rows]
+        m2 = ((blk - blk.mean(0)) ** 2).sum(0)
+        assert rel(stv[t, 1], m2) < 1e-4, t
+    # addend
+    ya = torch.empty(M, Cout, device=DEV, dtype=BF)
+    call("seg_conv_igemm2_bf16io", xg.data_ptr(), Cin, N, H, W, Cin, wk.data_ptr(), ldk, None, ya.data_ptr(), Cout,
+         Cout, ks, addg.data_ptr(), Cout, None, work.data_ptr(), S())
+    torch.cuda.synchronize()
+    assert rel(ya.float(), ref - b.double() + add.double()) < 4e-3
+    if splits == 1:  # same k order as the generic 16-bit kernel: bitwise equal
+        y0 = torch.empty(M, Cout, device=DEV, dtype=BF)
+        call("seg_conv_igemm_bf16io_w16", xg.data_ptr(), Cin, N, H, W, Cin, wk.data_ptr(), ldk, bg.data_ptr(),
+             y0.data_ptr(), Cout, H, W, Cout, ks, 1, ks // 2, None, 0, None, S())
+        torch.cuda.synchronize()
+        assert torch.equal(y0, y)
+
+
+def test_igemm2_plan_rejects_padding_heavy_shapes():
+    assert plan(4096, 80, 32, 3)[0] == 0      # Cin < 64
+    assert plan(4096, 288, 128, 3)[0] == 0    # 288 output channels: >= 25 % padded columns
+    assert plan(16384, 256, 1344, 3)[0] == 1

@@ -52,6 +52,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-timer", action="store_true", help="skip the per-launch HIP-event roofline timing")
+    ap.add_argument("--no-infer-block", action="store_true",
+                    help="skip the nested \"infer\" measurement (configs[3], 500 graph-replayed frames) of the default line")
     ap.add_argument("--no-bf16io-block", action="store_true",
                     help="skip the nested \"bf16io\" measurement (configs[2] math on the same workload) that follows "
                          "the f32 headline")
@@ -113,34 +115,34 @@ def cpu_baseline(args):
                       f"{steps} timed steps ({dt:.1f} s) after 1 warm-up, torch CPU fp32"}
 
 
-def bench_infer(args):
+def infer_measure(args, math, frames, cpu_baseline=True):
     """configs[3]: inference.py's per-frame path (preprocess_image -> model.eval() forward ->
     argmax + INTER_NEAREST mask) for a 720x1280 uint8 BGR frame resized to 128x256, bs=1,
-    replayed as one HIP graph.  value = frames/s with the frame already in HBM."""
+    replayed as one HIP graph.  Returns per-frame latencies (graph / eager / graph with the
+    H2D frame copy) and the CPU path's frames/s."""
     import numpy as np
     from seg_amd import MobileNetV2UNet, deterministic_init
     from seg_amd.infer import Predictor
-    dev = torch.device("cuda", 0)
-    torch.cuda.set_device(dev)
+    dev = torch.device("cuda", torch.cuda.current_device())
     model = deterministic_init(MobileNetV2UNet(args.classes), seed=0, random_running_stats=True).to(dev).eval()
     g = np.random.Generator(np.random.PCG64(0))
     frame = g.integers(0, 256, (720, 1280, 3), dtype=np.uint8)
     res = {}
     for mode in ("graph", "eager", "graph_h2d"):
-        pred = Predictor(model, frame_hw=(720, 1280), graph=mode != "eager", math=args.math)
+        pred = Predictor(model, frame_hw=(720, 1280), graph=mode != "eager", math=math)
         pred.set_frame(frame)
         fn = (lambda: pred(frame)) if mode == "graph_h2d" else pred.step
         for _ in range(max(args.warmup, 3)):
             fn()
         torch.cuda.synchronize()
-        n = args.frames if mode != "graph_h2d" else max(args.frames // 5, 20)
+        n = frames if mode != "graph_h2d" else max(frames // 5, 20)
         t0 = time.perf_counter()
         for _ in range(n):
             fn()
         torch.cuda.synchronize()
         res[mode] = (time.perf_counter() - t0) / n
     cpu = None
-    if not args.no_cpu_baseline:
+    if cpu_baseline:
         from oracle import cvresize, segref
         threads = min(os.cpu_count() or 1, len(os.sched_getaffinity(0)))
         threads = min(threads, int(os.environ.get("OMP_NUM_THREADS", threads)))
@@ -160,20 +162,31 @@ def bench_infer(args):
         cpu = {"value": round(k / dt, 2), "unit": "frames/s", "cores": threads, "kind": "port", "cpu_model": cpu_model(),
                "sample": f"oracle cvresize.preprocess_image + segref eval forward (torch CPU fp32) + class_mask, "
                          f"{k} frames in {dt:.1f} s"}
-    line = {"metric": "frames/sec inference MobileNetV2UNet 720x1280 frame -> 128x256, bs=1 (BASELINE configs[3])",
-            "value": round(1.0 / res["graph"], 1), "unit": "frames/s", "n_gpus": 1, "steps": args.frames,
-            "warmup": args.warmup, "ms_per_step": round(res["graph"] * 1e3, 4), "higher_is_better": True,
-            "scaling": "none", "vs_baseline": None, "dtype": args.math, "data": "synthetic",
-            "math": {"f32": "fp32 everywhere", "f16": "folded conv operands fp16 (RNE) on the f16 MFMA, fp32 "
-                     "accumulation; depthwise, preprocess and argmax in fp32",
-                     "bf16": "folded conv operands bf16 on the bf16 MFMA, fp32 accumulation"}[args.math],
-            "config": {"workload": "inference.py per-frame path: cv2-style resize + normalise, BN-folded eval forward, "
-                                   "argmax + nearest mask, one hipGraph replay per frame",
-                       "model": "MobileNetV2UNet", "global_batch": 1, "frame": [720, 1280], "image": [128, 256],
-                       "parallelism": "none"},
+    return {"value": round(1.0 / res["graph"], 1), "unit": "frames/s", "ms_per_frame": round(res["graph"] * 1e3, 4),
             "latency_ms": {"graph": round(res["graph"] * 1e3, 4), "eager": round(res["eager"] * 1e3, 4),
                            "graph_with_h2d_frame_copy": round(res["graph_h2d"] * 1e3, 4)},
-            "roofline": None, "cpu_baseline": cpu}
+            "frames": frames, "cpu_baseline": cpu}
+
+
+INFER_MATH = {"f32": "fp32 everywhere", "f16": "folded conv operands fp16 (RNE) on the f16 MFMA, fp32 "
+              "accumulation; depthwise, preprocess and argmax in fp32",
+              "bf16": "folded conv operands bf16 on the bf16 MFMA, fp32 accumulation"}
+INFER_WORKLOAD = ("inference.py per-frame path: cv2-style resize + normalise, BN-folded eval forward, argmax + "
+                  "nearest mask, one hipGraph replay per frame")
+
+
+def bench_infer(args):
+    """configs[3] as the headline (--workload infer).  value = frames/s with the frame already in HBM."""
+    torch.cuda.set_device(0)
+    r = infer_measure(args, args.math, args.frames, not args.no_cpu_baseline)
+    line = {"metric": "frames/sec inference MobileNetV2UNet 720x1280 frame -> 128x256, bs=1 (BASELINE configs[3])",
+            "value": r["value"], "unit": "frames/s", "n_gpus": 1, "steps": args.frames,
+            "warmup": args.warmup, "ms_per_step": r["ms_per_frame"], "higher_is_better": True,
+            "scaling": "none", "vs_baseline": None, "dtype": args.math, "data": "synthetic",
+            "math": INFER_MATH[args.math],
+            "config": {"workload": INFER_WORKLOAD, "model": "MobileNetV2UNet", "global_batch": 1, "frame": [720, 1280],
+                       "image": [128, 256], "parallelism": "none"},
+            "latency_ms": r["latency_ms"], "roofline": None, "cpu_baseline": r["cpu_baseline"]}
     print(json.dumps(line), flush=True)
 
 
@@ -262,6 +275,12 @@ def main():
             line["bf16io"] = {"workload": f"same model, shape and step as the headline with bf16io math "
                                           f"({_cfg_name(args, 'bf16io')})", "dtype": "bf16io",
                               "math": MATH_NOTE["bf16io"], **nested}
+        if world == 1 and args.model == "MobileNetV2UNet" and not args.no_infer_block:
+            # BASELINE configs[3] on the same GPU after the training lines (its own timed loop)
+            r = infer_measure(args, "f16", 500, cpu_baseline=False)
+            line["infer"] = {"workload": f"BASELINE configs[3]: {INFER_WORKLOAD}", "dtype": "f16",
+                             "math": INFER_MATH["f16"], "model": "MobileNetV2UNet", "frame": [720, 1280],
+                             "image": [128, 256], **{k: v for k, v in r.items() if k != "cpu_baseline"}}
         print(json.dumps(line), flush=True)
     if dist:
         torch.distributed.destroy_process_group()

@@ -53,6 +53,19 @@ IGNORE_INDEX = -100
 _ROW_TILES = {}  # (M, Cout) -> (row tiles, tile height) of seg_conv_igemm
 
 
+_IG2 = {}  # (M, Cout, Cin, ks) -> (tile rows, row tiles, splits, workspace floats) or None
+
+
+def igemm2_plan(M: int, cout: int, cin: int, ks: int):
+    """seg_conv_igemm2_plan (memoised): None when the deep-conv kernel does not apply."""
+    key = (M, cout, cin, ks)
+    if key not in _IG2:
+        out = (ctypes.c_long * 4)()
+        ok = query("seg_conv_igemm2_plan", M, cout, cin, ks, ctypes.addressof(out))
+        _IG2[key] = tuple(out) if ok else None
+    return _IG2[key]
+
+
 def r8(c: int) -> int:
     return (c + 7) & ~7
 
@@ -161,6 +174,8 @@ class ConvOp:
         self.bf = False
         # bf16io: wk_f / wk_d packed as bf16 for seg_conv_igemm_bf16io_w16 (Program._build_pack)
         self.w16_f = self.w16_d = False
+        # bf16io deep convs on seg_conv_igemm2_bf16io (igemm2_plan tuples, chosen at pack time)
+        self.ig2_f = self.ig2_d = None
         self.ks = conv.kernel_size[0]
         self.stride = conv.stride[0]
         self.pad = conv.padding[0]
@@ -199,7 +214,9 @@ class ConvOp:
                 ldk, wk_ptr = self.ldk_f, self.wk_f.data_ptr()  # packed by Program.pack at the step start
             stat = None
             if self.bn is not None and rt.training:  # BN statistics fused into the conv epilogue
-                if self.wino_f:
+                if self.ig2_f is not None:
+                    tile_rows, ntiles = self.ig2_f[0], self.ig2_f[1]
+                elif self.wino_f:
                     ntiles, tile_rows = query("seg_conv_wino_row_tiles", y.N, y.H, y.W), 256
                 elif self.halo_f:
                     ntiles, tile_rows = query("seg_conv_halo_row_tiles", y.N, y.H, y.W), 256
@@ -216,6 +233,11 @@ class ConvOp:
                 rt.tcall("wino3_fwd", self.flops(), "seg_conv_wino", rt.ptr(i), i.ld, i.N, i.H, i.W, self.cin_pad,
                             self.wk_wf.data_ptr(), self.cin_pad, bias, rt.ptr(y), y.ld, self.cout, None, 0, statp,
                             work.data_ptr(), s)
+            elif self.ig2_f is not None:  # deep bf16io conv: 8-wave LDS-DMA implicit GEMM
+                work = rt.tmp(self.ig2_f[3], zero=True)
+                rt.tcall(f"igemm{self.ks}_fwd", self.flops(), "seg_conv_igemm2_bf16io", rt.ptr(i), i.ld, i.N, i.H, i.W,
+                         self.cin_pad, wk_ptr, ldk, bias, rt.ptr(y), y.ld, self.cout, self.ks, None, 0, statp,
+                         work.data_ptr(), s)
             elif self.xform is not None:  # 1x1 conv applying its producer's lazy BN on load
                 name = "seg_conv_igemm_bf16io_xf" if rt.io else "seg_conv_igemm_bf16_xf" if self.bf else "seg_conv_igemm_xf"
                 if rt.io and self.w16_f:
@@ -393,6 +415,11 @@ class ConvOp:
                 rt.tcall("wino3_dgrad", self.flops(), "seg_conv_wino", dYp, dY.ld, y.N, y.H, y.W, kin,
                             self.wk_wd.data_ptr(), kin, None, rt.gptr(i), i.ld, self.cin, add_ptr, add_ld, None,
                             work.data_ptr(), s)
+            elif self.ig2_d is not None and (add_ptr is None or (add_ld % 8 == 0 and add_ptr % 16 == 0)):
+                work = rt.tmp(self.ig2_d[3], zero=True)
+                rt.tcall(f"igemm{self.ks}_dgrad", self.flops(), "seg_conv_igemm2_bf16io", dYp, dY.ld, y.N, y.H, y.W, kin,
+                         self.wk_d.data_ptr(), self.ldk_d, None, rt.gptr(i), i.ld, self.cin, self.ks, add_ptr, add_ld,
+                         None, work.data_ptr(), s)
             elif rt.io:
                 rt.tcall(f"igemm{self.ks}_dgrad", self.flops(),
                          "seg_conv_igemm_bf16io_w16" if self.w16_d else "seg_conv_igemm_bf16io", dYp, dY.ld, y.N, y.H, y.W,
@@ -543,6 +570,16 @@ class Program:
                 # half the weight bytes every M tile / pixel tile re-reads)
                 w16f = w16d = self.math == "bf16io" and W16
                 op.w16_f, op.w16_d = w16f, w16d
+                # the deep convs (3x3, or 1x1 with SEG_IGEMM2=all) on seg_conv_igemm2_bf16io
+                op.ig2_f = op.ig2_d = None
+                if (w16f and IGEMM2 != "0" and op.stride == 1 and op.pad == op.ks // 2
+                        and (op.ks == 3 or IGEMM2 == "all")):
+                    i = op.inp  # 16-byte rows: ld and channel offset multiples of 8 elements
+                    rows16 = i.ld % 8 == 0 and i.off % 8 == 0 and y.ld % 8 == 0 and y.off % 8 == 0
+                    if rows16 and not op.halo_f and op.xform is None and op.cin_pad == op.cin:
+                        op.ig2_f = igemm2_plan(y.M, op.cout, op.cin_pad, op.ks)
+                    if rows16 and not op.first and not op.halo_d and op.cout % 8 == 0:
+                        op.ig2_d = igemm2_plan(y.M, op.cin, op.cout, op.ks)
                 if w16f or not (op.ks == 1 and op.cin_pad == op.cin):
                     op.ldk_f = r8(op.ks * op.ks * op.cin_pad) if w16f else r4(op.ks * op.ks * op.cin_pad)
                     op.wk_f = torch.empty(op.cout * op.ldk_f, device=dev,
@@ -1103,6 +1140,9 @@ HALO_BF16 = os.environ.get("SEG_HALO_BF16", "1") == "1"
 # lazy BatchNorm for 1x1 consumers (the inverted residuals' project convs, OutConv's last
 # conv): SEG_LAZY_PW=0 keeps the separate BN-apply pass (read at program build)
 LAZY_PW = os.environ.get("SEG_LAZY_PW", "1") == "1"
+# bf16io deep convs on the 8-wave LDS-DMA implicit GEMM (seg_conv_igemm2_bf16io, csrc/igemm2.hip):
+# "3" = 3x3 convs where its plan applies (default), "all" = also 1x1 convs, "0" = off
+IGEMM2 = os.environ.get("SEG_IGEMM2", "3")
 # bf16io implicit GEMMs on bf16-packed weights (seg_conv_igemm_bf16io_w16); SEG_W16=0 keeps the fp32 packs
 W16 = os.environ.get("SEG_W16", "1") == "1"
 # fork the weight-gradient side stream after the layer's data gradient (measured: f32 +1.5 %, bf16io +-0)

@@ -13,9 +13,9 @@
 //    (2 x 2 v_mfma_f32_32x32x16_bf16 accumulators): one 16-byte LDS fragment read per MFMA
 //    (4 per 4 MFMAs), half the re-reads of every operand tile in L2 of the 64 x 128 tile;
 //  * K steps of 64 bf16 (128-byte operand rows) staged global -> LDS by LDS-DMA
-//    (global_load_lds_dwordx4, no VGPR round trip), two LDS buffers, the next step's DMA in
-//    flight while the current one computes; waits are counted vmcnt + raw s_barrier, so no
-//    barrier drains a DMA that is still in flight;
+//    (global_load_lds_dwordx4, no VGPR round trip), three LDS buffers, the next two steps'
+//    DMA in flight while the current one computes; waits are counted vmcnt + raw
+//    s_barrier, so no barrier drains a DMA that is still in flight;
 //  * XOR-swizzled operand rows (16-byte chunk c of row r stored at c ^ ((r >> 1) & 7)):
 //    the DMA writes LDS lane-linearly, so the permutation is applied to each lane's SOURCE
 //    address and undone on the fragment read -- conflict-free ds_read_b128;
@@ -78,7 +78,8 @@ __global__ __launch_bounds__(kThreads) void igemm2_kernel(Igemm2Args a) {
   constexpr int A_BYTES = BM * 128, STAGE = (BM + BN) * 128;
   constexpr int NA = BM / 64, NB = BN / 64;  // DMA instructions per wave per K step
   constexpr int CSR = BN + 4;                // epilogue band row stride (floats)
-  constexpr int SMEM = 2 * STAGE > WM * CSR * 4 ? 2 * STAGE : WM * CSR * 4;
+  constexpr int NSTAGE = 3;                  // LDS buffers: two K steps in flight while one computes
+  constexpr int SMEM = NSTAGE * STAGE > WM * CSR * 4 ? NSTAGE * STAGE : WM * CSR * 4;
   __shared__ __attribute__((aligned(1024))) char smem[SMEM];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -175,39 +176,50 @@ __global__ __launch_bounds__(kThreads) void igemm2_kernel(Igemm2Args a) {
   auto compute = [&](int buf) {
     const char* As = smem + buf * STAGE;
     const char* Bs = As + A_BYTES;
-#pragma unroll
-    for (int ks = 0; ks < kBK / 16; ++ks) {
+    // fragments of the next 16-deep k slice are read while the current slice's MFMAs run
+    bf16x8 af[2][2], bfr[2][2];
+    auto frag = [&](int ks, int st) {
       const int chunk = 2 * ks + fh;  // logical 16-byte chunk of this lane's 8 k values
-      bf16x8 af[2], bfr[2];
 #pragma unroll
       for (int mi = 0; mi < 2; ++mi) {
         const int r = wm0 + mi * 32 + fr;
-        af[mi] = *reinterpret_cast<const bf16x8*>(As + r * 128 + 16 * (chunk ^ ((r >> 1) & 7)));
+        af[st][mi] = *reinterpret_cast<const bf16x8*>(As + r * 128 + 16 * (chunk ^ ((r >> 1) & 7)));
       }
 #pragma unroll
       for (int ni = 0; ni < 2; ++ni) {
         const int r = wn0 + ni * 32 + fr;
-        bfr[ni] = *reinterpret_cast<const bf16x8*>(Bs + r * 128 + 16 * (chunk ^ ((r >> 1) & 7)));
+        bfr[st][ni] = *reinterpret_cast<const bf16x8*>(Bs + r * 128 + 16 * (chunk ^ ((r >> 1) & 7)));
       }
+    };
+    frag(0, 0);
+#pragma unroll
+    for (int ks = 0; ks < kBK / 16; ++ks) {
+      if (ks + 1 < kBK / 16) frag(ks + 1, (ks + 1) & 1);
 #pragma unroll
       for (int mi = 0; mi < 2; ++mi)
 #pragma unroll
         for (int ni = 0; ni < 2; ++ni)
-          acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[mi], bfr[ni], acc[mi][ni], 0, 0, 0);
+          acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[ks & 1][mi], bfr[ks & 1][ni], acc[mi][ni], 0, 0, 0);
     }
   };
 
-  // ---- K loop: buffer it & 1 holds step it; step it + 1's DMA stays in flight meanwhile
+  // ---- K loop: buffer it % 3 holds step it; steps it + 1 and it + 2 stay in flight meanwhile
+  // (each step is NA + NB DMA instructions per wave, so "k steps still in flight" is
+  // vmcnt(k * (NA + NB)))
   if (nst > 0) issue(0);
   if (nst > 1) issue(1);
+  if (nst > 2) issue(2);
   for (int it = 0; it < nst; ++it) {
-    if (it + 1 < nst) wait_vm<NA + NB>();  // this wave's DMA of step `it` has landed
+    const int ahead = min(nst - 1 - it, 2);  // steps issued beyond this one
+    if (ahead == 2) wait_vm<2 * (NA + NB)>();
+    else if (ahead == 1) wait_vm<NA + NB>();
     else wait_vm<0>();
-    raw_barrier();                         // ... and every other wave's
-    compute(it & 1);
-    wait_lgkm0();                          // this wave's fragment reads of buffer it & 1 are done
+    raw_barrier();                         // every wave's DMA of step `it` has landed
+    const int buf = it % NSTAGE;
+    compute(buf);
+    wait_lgkm0();                          // this wave's fragment reads of `buf` are done
     raw_barrier();                         // ... every wave's: the buffer may be refilled
-    if (it + 2 < nst) issue(it & 1);
+    if (it + NSTAGE < nst) issue(buf);
   }
 
   // ---- split-K: publish this slice, the last-arriving slice of the tile combines

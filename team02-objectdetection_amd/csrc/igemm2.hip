@@ -50,7 +50,15 @@ struct Igemm2Args {
   int K, M, nsteps, steps_per_split, splits, tiles_m, tiles_n;
 };
 
+#ifndef SEG_IG2_NODMA
+#define SEG_IG2_NODMA 0   // diagnostics only (wrong results): skip the operand DMA
+#endif
+#ifndef SEG_IG2_NOMFMA
+#define SEG_IG2_NOMFMA 0  // diagnostics only (wrong results): skip the MFMAs
+#endif
+
 __device__ __forceinline__ void dma16(const void* src, char* lds) {
+  if (SEG_IG2_NODMA) return;
   __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
                                    (__attribute__((address_space(3))) void*)lds, 16, 0, 0);
 }
@@ -198,8 +206,13 @@ __global__ __launch_bounds__(kThreads) void igemm2_kernel(Igemm2Args a) {
 #pragma unroll
       for (int mi = 0; mi < 2; ++mi)
 #pragma unroll
-        for (int ni = 0; ni < 2; ++ni)
+        for (int ni = 0; ni < 2; ++ni) {
+          if (SEG_IG2_NOMFMA) {
+            asm volatile("" ::"v"(af[ks & 1][mi]), "v"(bfr[ks & 1][ni]));
+            continue;
+          }
           acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[ks & 1][mi], bfr[ks & 1][ni], acc[mi][ni], 0, 0, 0);
+        }
     }
   };
 

@@ -131,6 +131,8 @@ def lib():
             import torch  # noqa: F401  -- load torch's libamdhip64 first so both share one HIP runtime
             h = ctypes.CDLL(path)
             for name, (res, args) in PROTOTYPES.items():
+                if path != LIB_PATH and not hasattr(h, name):
+                    continue  # an older A/B build (SEG_LIB_PATH) may predate an entry point
                 fn = getattr(h, name)
                 fn.restype = res
                 fn.argtypes = args

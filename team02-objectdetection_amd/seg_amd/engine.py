@@ -600,7 +600,8 @@ class Program:
             op.wino_f = wino_ok and bool(query("seg_conv_wino_pick", y.N, y.H, y.W, op.cin_pad, op.cout))
             op.wino_d = wino_ok and not op.first and bool(query("seg_conv_wino_pick", y.N, y.H, y.W, r4(op.cout),
                                                                 op.cin))
-            op.wino_w = wino_ok and bool(query("seg_conv_wino_wgrad_pick", y.N, y.H, y.W, op.cin_pad, op.cout))
+            op.wino_w = wino_ok and WINOGRAD_WGRAD and bool(query("seg_conv_wino_wgrad_pick", y.N, y.H, y.W, op.cin_pad,
+                                                                   op.cout))
             op.halo_f = (dense3 and not op.wino_f
                          and bool(query("seg_conv_halo_pick", y.N, y.H, y.W, op.cin_pad, op.cout)))
             op.halo_d = (dense3 and not op.first and not op.wino_d
@@ -1135,6 +1136,7 @@ OVERLAP = os.environ.get("SEG_OVERLAP", "1") == "1"
 # packed); SEG_WINO=0 routes them to the LDS-halo / implicit-GEMM kernels instead (parity
 # diagnostics: tests/test_gpu_unet_cfg5.py separates Winograd from accumulation error).
 WINOGRAD = os.environ.get("SEG_WINO", "1") == "1"
+WINOGRAD_WGRAD = os.environ.get("SEG_WINO_WGRAD", "1") == "1"  # the F(3x3,2x2) weight gradients alone
 # LDS-halo direct 3x3 conv for the narrow convs in the bf16io configuration; SEG_HALO_BF16=0 turns it off.
 HALO_BF16 = os.environ.get("SEG_HALO_BF16", "1") == "1"
 # lazy BatchNorm for 1x1 consumers (the inverted residuals' project convs, OutConv's last

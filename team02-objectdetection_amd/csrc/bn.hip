@@ -10,10 +10,9 @@
 // conv, whose output takes the residual add of InvertedResidual).
 //
 // Layout: raw conv output y is NHWC [M][ldy]; channels C % 4 == 0.
-// Statistics are computed in two steps inside one launch: per-block shifted partial
-// sums (fp32 over <= a few hundred rows, shift = first row so a large mean cannot
-// cancel the variance away), then the block that completes the reduction sums them
-// per channel in fp64, in a fixed order, and writes the results (seg_last_arrival).
+// Statistics are computed in two steps: per-block shifted partial sums (fp32 over <= a
+// few hundred rows, shift = first row so a large mean cannot cancel the variance away)
+// and a per-channel finalize in fp64 (fixed order: deterministic).
 #include "common.h"
 
 namespace {
@@ -27,8 +26,8 @@ namespace {
 // bf16-representable data, tests/test_gpu_bf16io.py).  Channel groups
 // beyond 64 are split over blockIdx.y (the encoder's 384..1280-channel layers).  The
 // row range is split into nblk = chan_blocks(M) blocks (<= 256: one or two waves of
-// 512-thread blocks per CU, and few enough partial rows for the last block's fp64
-// sums).  Partials: part[blockIdx.x][2][C].
+// 512-thread blocks per CU, and few enough partial rows for the finalize kernels' one
+// round trip).  Partials: part[blockIdx.x][2][C].
 // kind 0: (sum(y-k), sum((y-k)^2)),  k = y[0][c]                   -> BN stats
 // kind 1: (sum(dz),  sum(dz*(y-mean))), dz = dA * act'(y*scale+shift) -> BN backward
 // kind 2: (sum(y), 0)                                               -> bias grad
@@ -37,9 +36,6 @@ constexpr int kRedSlice = 64;  // channel groups per block (blockIdx.y slices be
 
 #ifndef SEG_CHAN_MAXBLK
 #define SEG_CHAN_MAXBLK 256
-#endif
-#ifndef SEG_BN_FOLD
-#define SEG_BN_FOLD 0  // 1: finalize in the reduction's launch (last-arriving block); 0: finalize kernels
 #endif
 #ifndef SEG_APPLY_ROWS4
 #define SEG_APPLY_ROWS4 0
@@ -58,30 +54,13 @@ __device__ __forceinline__ void ldw(const T* p, f32x4 (&o)[VW / 4]) {
   }
 }
 
-// What the block that completes a reduction does with the summed partials (the
-// finalize folded into the reduction's launch, see seg_last_arrival): per channel, the
-// fp64 totals s0 / s1 over all row blocks.
-struct ChanFin {
-  unsigned* cnt;        // [gridDim.y] tickets: zero before the first launch, left zero
-  long M;
-  // KIND 0 -- BN statistics (as bn_finalize_kernel)
-  const float* gamma; const float* beta; float eps, momentum;
-  float* rmean; float* rvar; long long* nbt;
-  float* mean_out; float* invstd_out; float* scale_out; float* shift_out;
-  // KIND 1 -- BN backward (as bn_bwd_finalize_kernel): reads gamma, invstd
-  const float* invstd; float* dgamma; float* dbeta; float* coef;
-  // KIND 2 -- column sums
-  float* out; int accumulate; int C_out;
-};
-
-template <int KIND, typename T, int VW, bool FIN>
+template <int KIND, typename T, int VW>
 __global__ __launch_bounds__(kRedThreads) void chan_partial_kernel(
     const T* __restrict__ y, long ldy, const T* __restrict__ da, long ldda, int M, int C,
     const float* __restrict__ scale, const float* __restrict__ shift, const float* __restrict__ mean, int act,
-    float* __restrict__ part, int rows_per_block, ChanFin fin) {
+    float* __restrict__ part, int rows_per_block) {
   constexpr int NV = VW / 4;
   __shared__ f32x4 red0[kRedThreads * NV], red1[kRedThreads * NV];
-  __shared__ int last_word;
   const int CG = C / VW;
   const int cg0 = blockIdx.y * kRedSlice;
   const int TC = min(CG - cg0, kRedSlice);
@@ -166,120 +145,31 @@ __global__ __launch_bounds__(kRedThreads) void chan_partial_kernel(
     float* p0 = part + (long)blockIdx.x * 2 * C;
 #pragma unroll
     for (int j = 0; j < NV; ++j) {
-      if constexpr (FIN) {  // write-through: read by the last-arriving block of this launch
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          seg_st_wt(p0 + c + 4 * j + e, red0[tc * NV + j][e]);
-          seg_st_wt(p0 + C + c + 4 * j + e, red1[tc * NV + j][e]);
-        }
-      } else {
-        st4(p0 + c + 4 * j, red0[tc * NV + j]);
-        st4(p0 + C + c + 4 * j, red1[tc * NV + j]);
-      }
-    }
-  }
-  if constexpr (FIN) {
-    if (!seg_last_arrival(fin.cnt + blockIdx.y, gridDim.x, &last_word)) return;
-    // This slice's SC channels, P threads each (rows jj, jj+P, ... in order; fp64), then a
-    // fixed-order tree over the P threads: the same bits whatever the arrival order.
-    const int SC = TC * VW, nblk = gridDim.x;
-    int P = 1;
-    while (2 * P * SC <= kRedThreads) P <<= 1;
-    double* d0 = reinterpret_cast<double*>(red0);  // [kRedThreads] (red0 holds >= 2x that)
-    double* d1 = reinterpret_cast<double*>(red1);
-    const int ch = t / P, jj = t - ch * P;
-    const int cc = cg0 * VW + ch;
-    double a = 0.0, b = 0.0;
-    if (ch < SC) {
-      // 16 rows' loads in flight per thread (clamped index, masked add: no branch around a load)
-      for (int r0 = jj; r0 < nblk; r0 += 16 * P) {
-        float va[16], vb[16];
-#pragma unroll
-        for (int q = 0; q < 16; ++q) {
-          const int rr = min(r0 + q * P, nblk - 1);
-          va[q] = seg_ld_wt(part + (long)rr * 2 * C + cc);
-          vb[q] = KIND != 2 ? seg_ld_wt(part + (long)rr * 2 * C + C + cc) : 0.f;
-        }
-#pragma unroll
-        for (int q = 0; q < 16; ++q) {
-          const bool ok = r0 + q * P < nblk;
-          a += ok ? (double)va[q] : 0.0;
-          b += ok ? (double)vb[q] : 0.0;
-        }
-      }
-    }
-    __syncthreads();  // red0 / red1 are free again
-    d0[t] = a;
-    d1[t] = b;
-    __syncthreads();
-    for (int h = P >> 1; h > 0; h >>= 1) {
-      if (ch < SC && jj < h) {
-        d0[t] += d0[t + h];
-        d1[t] += d1[t + h];
-      }
-      __syncthreads();
-    }
-    if (ch >= SC || jj != 0) return;
-    const double S = d0[t], S2 = d1[t];
-    if constexpr (KIND == 0) {
-      if (blockIdx.y == 0 && t == 0 && fin.nbt) *fin.nbt += 1;
-      const double kk = (float)y[cc];
-      const double dm = S / (double)fin.M;
-      const double mu = kk + dm;
-      double var = S2 / (double)fin.M - dm * dm;
-      if (var < 0.0) var = 0.0;
-      const float invstd = (float)(1.0 / sqrt(var + (double)fin.eps));
-      fin.mean_out[cc] = (float)mu;
-      fin.invstd_out[cc] = invstd;
-      const float g = fin.gamma ? fin.gamma[cc] : 1.f, bt = fin.beta ? fin.beta[cc] : 0.f;
-      fin.scale_out[cc] = g * invstd;
-      fin.shift_out[cc] = bt - (float)mu * g * invstd;
-      if (fin.rmean) {
-        const double unbiased = fin.M > 1 ? var * (double)fin.M / (double)(fin.M - 1) : var;
-        fin.rmean[cc] = (float)((1.0 - fin.momentum) * fin.rmean[cc] + fin.momentum * mu);
-        fin.rvar[cc] = (float)((1.0 - fin.momentum) * fin.rvar[cc] + fin.momentum * unbiased);
-      }
-    } else if constexpr (KIND == 1) {
-      const double inv = fin.invstd[cc];
-      const double g = fin.gamma ? fin.gamma[cc] : 1.0;
-      if (fin.dbeta) fin.dbeta[cc] = (float)S;
-      if (fin.dgamma) fin.dgamma[cc] = (float)(S2 * inv);
-      fin.coef[cc] = (float)(g * inv);
-      fin.coef[C + cc] = (float)(S / (double)fin.M);
-      fin.coef[2 * C + cc] = (float)(S2 * inv * inv / (double)fin.M);
-    } else {
-      if (cc < fin.C_out) fin.out[cc] = fin.accumulate ? fin.out[cc] + (float)S : (float)S;
+      st4(p0 + c + 4 * j, red0[tc * NV + j]);
+      st4(p0 + C + c + 4 * j, red1[tc * NV + j]);
     }
   }
 }
 
 // Launch chan_partial_kernel<KIND> over [M][C] (C % 4 == 0): 8-channel lanes when C, the
 // row strides and the tensors' element offsets are multiples of 8 (16-byte bf16 loads),
-// else 4 -- a decision in elements, identical for fp32 and bf16 storage.  fin set: the
-// finalize runs in the same launch (the last-arriving block of each channel slice);
-// otherwise the partials are left for a finalize kernel.
+// else 4 -- a decision in elements, identical for fp32 and bf16 storage.
 template <int KIND, typename T>
 void launch_chan_partial(const T* y, long ldy, const T* da, long ldda, long M, int C, const float* scale,
-                         const float* shift, const float* mean, int act, float* part, hipStream_t stream,
-                         const ChanFin* fin) {
+                         const float* shift, const float* mean, int act, float* part, hipStream_t stream) {
   const int nblk = chan_blocks(M);
   const int rpb = seg_cdiv(M, nblk);
   auto eoff8 = [](const T* p) { return ((uintptr_t)p / sizeof(T)) % 8 == 0; };
   const bool v8 = C % 8 == 0 && ldy % 8 == 0 && (!da || ldda % 8 == 0) && eoff8(y) && (!da || eoff8(da));
-  ChanFin f{};
-  if (fin) f = *fin;
-#define SEG_CP(VW, F)                                                                                          \
-  hipLaunchKernelGGL((chan_partial_kernel<KIND, T, VW, F>), dim3(nblk, seg_cdiv(C / VW, kRedSlice)),           \
-                     dim3(kRedThreads), 0, stream, y, ldy, da, ldda, (int)M, C, scale, shift, mean, act, part, rpb, f)
-  if (v8) {
-    if (fin) SEG_CP(8, true); else SEG_CP(8, false);
-  } else {
-    if (fin) SEG_CP(4, true); else SEG_CP(4, false);
-  }
-#undef SEG_CP
+  if (v8)
+    hipLaunchKernelGGL((chan_partial_kernel<KIND, T, 8>), dim3(nblk, seg_cdiv(C / 8, kRedSlice)), dim3(kRedThreads),
+                       0, stream, y, ldy, da, ldda, (int)M, C, scale, shift, mean, act, part, rpb);
+  else
+    hipLaunchKernelGGL((chan_partial_kernel<KIND, T, 4>), dim3(nblk, seg_cdiv(C / 4, kRedSlice)), dim3(kRedThreads),
+                       0, stream, y, ldy, da, ldda, (int)M, C, scale, shift, mean, act, part, rpb);
 }
 
-// Separate finalize kernels (SEG_BN_FOLD == 0).  Sum the per-block partials (<= 256 rows:
+// Finalize kernels.  Sum the per-block partials (<= 256 rows:
 // chan_blocks) of one channel with one wave: lane l loads rows l, l+64, l+128, l+192 all at
 // once (one memory round trip; clamped index, masked add), sums them in that order in
 // fp64, then a fixed xor butterfly (fp64 adds are commutative, so every lane ends with the
@@ -797,12 +687,8 @@ SEG_API int seg_add_bf16io(const __bf16* a, long lda, const __bf16* b, long ldb,
   return add_impl(a, lda, b, ldb, M, C, out, ldout, stream);
 }
 
-// Workspace of the channel reductions below (seg_bn_stats, seg_bn_backward, seg_colsum):
-// kCntWords ticket words (the in-launch finalize's counters, seg_last_arrival) followed by
-// the per-block partial sums.  Zero the workspace once before its first use; every call
-// leaves the ticket words zero again, so a workspace is reused without re-zeroing.
-constexpr int kCntWords = 16;  // >= channel slices: seg_cdiv(C / 4, kRedSlice) for C <= 4096
-SEG_API long seg_chan_workspace_floats(long M, int C) { return kCntWords + (long)chan_blocks(M) * 2 * C; }
+// Size (floats) of the partial-sum workspace the channel reductions below need.
+SEG_API long seg_chan_workspace_floats(long M, int C) { return (long)chan_blocks(M) * 2 * C; }
 
 // Train-mode BN statistics: fills mean/invstd/scale/shift ([C] each) and updates
 // the running buffers (skipped when running_mean is null) and num_batches_tracked.
@@ -810,21 +696,11 @@ template <typename T>
 static int bn_stats_impl(const T* y, long ldy, long M, int C, const float* gamma, const float* beta, float eps,
                          float momentum, float* running_mean, float* running_var, long long* num_batches_tracked,
                          float* work, float* mean, float* invstd, float* scale, float* shift, hipStream_t stream) {
-  if ((C & 3) || (ldy & 3) || M < 1 || seg_cdiv(C / 4, kRedSlice) > kCntWords) return (int)hipErrorInvalidValue;
-  ChanFin f{};
-  f.cnt = reinterpret_cast<unsigned*>(work);
-  f.M = M; f.gamma = gamma; f.beta = beta; f.eps = eps; f.momentum = momentum;
-  f.rmean = running_mean; f.rvar = running_var; f.nbt = num_batches_tracked;
-  f.mean_out = mean; f.invstd_out = invstd; f.scale_out = scale; f.shift_out = shift;
-  if (SEG_BN_FOLD) {
-    launch_chan_partial<0, T>(y, ldy, nullptr, 0L, M, C, nullptr, nullptr, nullptr, 0, work + kCntWords, stream, &f);
-  } else {
-    launch_chan_partial<0, T>(y, ldy, nullptr, 0L, M, C, nullptr, nullptr, nullptr, 0, work + kCntWords, stream,
-                              nullptr);
-    hipLaunchKernelGGL(bn_finalize_kernel<T>, dim3(seg_cdiv(C, 4)), dim3(256), 0, stream, work + kCntWords,
-                       chan_blocks(M), y, M, C, gamma, beta, eps, momentum, running_mean, running_var,
-                       num_batches_tracked, mean, invstd, scale, shift);
-  }
+  if ((C & 3) || (ldy & 3) || M < 1) return (int)hipErrorInvalidValue;
+  launch_chan_partial<0, T>(y, ldy, nullptr, 0L, M, C, nullptr, nullptr, nullptr, 0, work, stream);
+  hipLaunchKernelGGL(bn_finalize_kernel<T>, dim3(seg_cdiv(C, 4)), dim3(256), 0, stream, work, chan_blocks(M), y, M, C,
+                     gamma, beta, eps, momentum, running_mean, running_var, num_batches_tracked, mean, invstd, scale,
+                     shift);
   SEG_RET_LAST();
 }
 SEG_API int seg_bn_stats(const float* y, long ldy, long M, int C, const float* gamma, const float* beta, float eps,
@@ -897,22 +773,12 @@ template <typename T>
 static int bn_backward_impl(const T* da, long ldda, const T* y, long ldy, long M, int C, const float* gamma,
                             const float* mean, const float* invstd, const float* scale, const float* shift, int act,
                             float* dgamma, float* dbeta, float* work, T* dy, long lddy, hipStream_t stream) {
-  if ((C & 3) || (ldy & 3) || (ldda & 3) || (lddy & 3) || seg_cdiv(C / 4, kRedSlice) > kCntWords)
-    return (int)hipErrorInvalidValue;
+  if ((C & 3) || (ldy & 3) || (ldda & 3) || (lddy & 3)) return (int)hipErrorInvalidValue;
   if (M < 1) return (int)hipSuccess;
   float* coef = work + seg_chan_workspace_floats(M, C);
-  // reduction + finalize in one launch (the last-arriving block writes dgamma / dbeta / coef),
-  // then the apply pass
-  ChanFin f{};
-  f.cnt = reinterpret_cast<unsigned*>(work);
-  f.M = M; f.gamma = gamma; f.invstd = invstd; f.dgamma = dgamma; f.dbeta = dbeta; f.coef = coef;
-  if (SEG_BN_FOLD) {
-    launch_chan_partial<1, T>(y, ldy, da, ldda, M, C, scale, shift, mean, act, work + kCntWords, stream, &f);
-  } else {
-    launch_chan_partial<1, T>(y, ldy, da, ldda, M, C, scale, shift, mean, act, work + kCntWords, stream, nullptr);
-    hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(seg_cdiv(C, 4)), dim3(256), 0, stream, work + kCntWords,
-                       chan_blocks(M), M, C, gamma, invstd, dgamma, dbeta, coef);
-  }
+  launch_chan_partial<1, T>(y, ldy, da, ldda, M, C, scale, shift, mean, act, work, stream);
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(seg_cdiv(C, 4)), dim3(256), 0, stream, work, chan_blocks(M), M, C,
+                     gamma, invstd, dgamma, dbeta, coef);
   launch_bn_bwd_apply<T>(da, ldda, y, ldy, M, C, scale, shift, mean, act, coef, dy, lddy, stream);
   SEG_RET_LAST();
 }
@@ -944,19 +810,9 @@ static int colsum_impl(const T* y, long ldy, long M, int C, float* work, float* 
                        hipStream_t stream) {
   if ((ldy & 3)) return (int)hipErrorInvalidValue;
   const int C4 = (C + 3) & ~3;  // ld >= C4 is guaranteed by the buffer contract
-  if (seg_cdiv(C4 / 4, kRedSlice) > kCntWords) return (int)hipErrorInvalidValue;
-  // the workspace is seg_chan_workspace_floats(M, C4); the sums land in one launch
-  ChanFin f{};
-  f.cnt = reinterpret_cast<unsigned*>(work);
-  f.M = M; f.out = out; f.accumulate = accumulate; f.C_out = C;
-  if (SEG_BN_FOLD) {
-    launch_chan_partial<2, T>(y, ldy, nullptr, 0L, M, C4, nullptr, nullptr, nullptr, 0, work + kCntWords, stream, &f);
-  } else {
-    launch_chan_partial<2, T>(y, ldy, nullptr, 0L, M, C4, nullptr, nullptr, nullptr, 0, work + kCntWords, stream,
-                              nullptr);
-    hipLaunchKernelGGL(colsum_finalize_kernel, dim3(seg_cdiv(C, 4)), dim3(256), 0, stream, work + kCntWords,
-                       chan_blocks(M), C, C4, out, accumulate);
-  }
+  launch_chan_partial<2, T>(y, ldy, nullptr, 0L, M, C4, nullptr, nullptr, nullptr, 0, work, stream);
+  hipLaunchKernelGGL(colsum_finalize_kernel, dim3(seg_cdiv(C, 4)), dim3(256), 0, stream, work, chan_blocks(M), C, C4,
+                     out, accumulate);
   SEG_RET_LAST();
 }
 SEG_API int seg_colsum(const float* y, long ldy, long M, int C, float* work, float* out, int accumulate,

@@ -270,7 +270,7 @@ class ConvOp:
             rv = bn.running_var.data_ptr() if bn.track_running_stats else None
             nbt = bn.num_batches_tracked.data_ptr() if bn.track_running_stats else None
             if self.kind == "dw":
-                work = rt.tmp(query("seg_chan_workspace_floats", M, C), zero=True)
+                work = rt.tmp(query("seg_chan_workspace_floats", M, C))
                 rt.call(rt.k("seg_bn_stats"), rt.ptr(y), y.ld, M, C, bn.weight.data_ptr(), bn.bias.data_ptr(), bn.eps,
                      bn.momentum, rm, rv, nbt, work.data_ptr(), mean, invstd,
                      scale, shift, s)
@@ -332,7 +332,7 @@ class ConvOp:
             mean, invstd, scale, shift = _stat_ptrs(st, C)
             dY = Act(rt.tmp_buf(M * r4(C)), 0, r4(C), C, y.N, y.H, y.W)
             g_w, g_b = rt.grad_param(self.bn.weight), rt.grad_param(self.bn.bias)
-            work = rt.tmp(query("seg_chan_workspace_floats", M, C) + 3 * C, zero=True)
+            work = rt.tmp(query("seg_chan_workspace_floats", M, C) + 3 * C)
             rt.call(rt.k("seg_bn_backward"), rt.gptr(dA), dA.ld, rt.ptr(y), y.ld, M, C, self.bn.weight.data_ptr(),
                  mean, invstd, scale, shift, self.act,
                  g_w, g_b, work.data_ptr(), rt.ptr(dY), dY.ld, s)
@@ -363,7 +363,7 @@ class ConvOp:
         reduce) and the DDP readiness hook, all on stream `s`."""
         y, M = self.y, self.y.M
         if self.conv.bias is not None and self.conv.bias.requires_grad:
-            work = rt.tmp(query("seg_chan_workspace_floats", M, r4(self.cout)), zero=True)
+            work = rt.tmp(query("seg_chan_workspace_floats", M, r4(self.cout)))
             rt.call(rt.k("seg_colsum"), dYp, dY.ld, M, self.cout, work.data_ptr(), rt.grad_param(self.conv.bias), 0, s)
         if self.conv.weight.requires_grad:
             gw = rt.grad_param(self.conv.weight)

@@ -623,13 +623,11 @@ def test_wgrad_reduce_direct(mode, Cout, Cin, ks, splits):
 
 
 @pytest.mark.parametrize("M,C", [(262144, 96), (65536, 1280), (100, 12)])
-def test_reduction_in_launch_finalize_repeatable_under_load(M, C):
-    """The channel reductions finalize inside their own launch: the last-arriving block
-    sums every block's partials (write-through hand-off across the XCDs' L2s,
-    csrc/common.h seg_last_arrival) and re-arms its ticket word.  Reusing one workspace
-    call after call -- with a large GEMM running on another stream, so blocks arrive in
-    uneven orders -- must give bitwise the same statistics, BN backward and column sums
-    every time, the ticket words back at zero, and results equal to fp64 torch."""
+def test_reduction_finalize_repeatable_under_load(M, C):
+    """The channel reductions (fixed-order partials + one-round-trip fp64 finalize kernels):
+    reusing one workspace call after call -- with a large GEMM running on another stream,
+    so blocks run in uneven orders -- must give bitwise the same statistics, BN backward
+    and column sums every time, and results equal to fp64 torch."""
     y = (gen(M, C, seed=11) * 2 + 1).to(DEV)
     da = gen(M, C, seed=12).to(DEV)
     gamma, beta = torch.ones(C, device=DEV), torch.zeros(C, device=DEV)
@@ -653,7 +651,6 @@ def test_reduction_in_launch_finalize_repeatable_under_load(M, C):
         cs = torch.empty(C, device=DEV)
         call("seg_colsum", da.data_ptr(), C, M, C, work.data_ptr(), cs.data_ptr(), 0, s)
         torch.cuda.synchronize()
-        assert int(work[:16].view(torch.int32).abs().sum()) == 0, "ticket words must be re-armed"
         outs.append((st.clone(), dg.clone(), db.clone(), dy.clone(), cs.clone()))
     for o in outs[1:]:
         for a, b in zip(outs[0], o):

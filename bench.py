@@ -12,12 +12,19 @@ N > 1 runs under torch.distributed.run (one process per GPU, RCCL), per-GPU
 batch fixed (weak scaling); value = all images / max-over-ranks time.
 
 Also reported:
-  roofline      -- the dense f32-MFMA implicit-GEMM convolutions (fwd, data- and
-                   weight-gradient), timed with HIP events around every launch
-                   inside the timed region: achieved = their algorithmic FLOPs /
-                   their summed launch durations vs the f32 MFMA peak.
+  roofline      -- the dense 3x3 conv family (forward + data gradient), timed with
+                   HIP events around those launches inside the timed region:
+                   achieved = their algorithmic FLOPs (f32, vs the f32 MFMA peak) or
+                   bytes (bf16io, vs HBM) / their summed launch durations.
+  step_roofline -- the whole step against SURVEY 8(d)'s algorithmic work per image.
   cpu_baseline  -- the CPU oracle (oracle/segref.py, torch-CPU restatement of
                    the reference) on a bounded sample, rank 0 at N = 1 only.
+  bf16io        -- (default f32 run) the same workload in BASELINE configs[2]'s
+                   arithmetic (bf16 MFMA operands + bf16 activation storage): its own
+                   warm-up and timed region after the headline's, with its own
+                   ms_per_step, HBM roofline and step roofline (--no-bf16io-block).
+  infer         -- (default run, N = 1) BASELINE configs[3]: inference.py's per-frame
+                   path as one hipGraph replay, fp16, 500 timed frames (--no-infer-block).
 """
 from __future__ import annotations
 

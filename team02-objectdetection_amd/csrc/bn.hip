@@ -40,6 +40,9 @@ constexpr int kRedSlice = 64;  // channel groups per block (blockIdx.y slices be
 #ifndef SEG_APPLY_ROWS4
 #define SEG_APPLY_ROWS4 0
 #endif
+#ifndef SEG_CHAN_ROWS
+#define SEG_CHAN_ROWS 4  // rows per lane whose loads the reductions issue together
+#endif
 int chan_blocks(long M) { return (int)std::max<long>(1, std::min<long>(SEG_CHAN_MAXBLK, M / 64)); }
 
 template <int VW, typename T>
@@ -105,15 +108,16 @@ __global__ __launch_bounds__(kRedThreads) void chan_partial_kernel(
       }
     };
     int r = r0 + rg;
-    for (; r + 3 * RG < r1; r += 4 * RG) {  // four rows' loads issued together
-      f32x4 v[4][NV], g[4][NV];
+    constexpr int RB = SEG_CHAN_ROWS;
+    for (; r + (RB - 1) * RG < r1; r += RB * RG) {  // RB rows' loads issued together
+      f32x4 v[RB][NV], g[RB][NV];
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
+      for (int q = 0; q < RB; ++q) {
         ldw<VW>(y + (long)(r + q * RG) * ldy + c, v[q]);
         if (KIND == 1) ldw<VW>(da + (long)(r + q * RG) * ldda + c, g[q]);
       }
 #pragma unroll
-      for (int q = 0; q < 4; ++q) step(v[q], g[q]);
+      for (int q = 0; q < RB; ++q) step(v[q], g[q]);
     }
     for (; r < r1; r += RG) {
       f32x4 v[NV], g[NV];
@@ -794,6 +798,35 @@ SEG_API int seg_bn_backward_bf16io(const __bf16* da, long ldda, const __bf16* y,
                                    long lddy, hipStream_t stream) {
   return bn_backward_impl(da, ldda, y, ldy, M, C, gamma, mean, invstd, scale, shift, act, dgamma, dbeta, work, dy,
                           lddy, stream);
+}
+
+// The reduction half of seg_bn_backward (partials + finalize): dgamma / dbeta and the
+// apply coefficients coef[3][C] (k1, k2, k3 of seg_bnbwd4) at work + seg_chan_workspace_floats(M, C),
+// for a consumer that forms dY on load (seg_conv_igemm_bx) instead of the apply pass.
+template <typename T>
+static int bn_backward_coef_impl(const T* da, long ldda, const T* y, long ldy, long M, int C, const float* gamma,
+                                 const float* mean, const float* invstd, const float* scale, const float* shift,
+                                 int act, float* dgamma, float* dbeta, float* work, hipStream_t stream) {
+  if ((C & 3) || (ldy & 3) || (ldda & 3) || M < 1) return (int)hipErrorInvalidValue;
+  float* coef = work + seg_chan_workspace_floats(M, C);
+  launch_chan_partial<1, T>(y, ldy, da, ldda, M, C, scale, shift, mean, act, work, stream);
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(seg_cdiv(C, 4)), dim3(256), 0, stream, work, chan_blocks(M), M, C,
+                     gamma, invstd, dgamma, dbeta, coef);
+  SEG_RET_LAST();
+}
+SEG_API int seg_bn_backward_coef(const float* da, long ldda, const float* y, long ldy, long M, int C,
+                                 const float* gamma, const float* mean, const float* invstd, const float* scale,
+                                 const float* shift, int act, float* dgamma, float* dbeta, float* work,
+                                 hipStream_t stream) {
+  return bn_backward_coef_impl(da, ldda, y, ldy, M, C, gamma, mean, invstd, scale, shift, act, dgamma, dbeta, work,
+                               stream);
+}
+SEG_API int seg_bn_backward_coef_bf16io(const __bf16* da, long ldda, const __bf16* y, long ldy, long M, int C,
+                                        const float* gamma, const float* mean, const float* invstd,
+                                        const float* scale, const float* shift, int act, float* dgamma,
+                                        float* dbeta, float* work, hipStream_t stream) {
+  return bn_backward_coef_impl(da, ldda, y, ldy, M, C, gamma, mean, invstd, scale, shift, act, dgamma, dbeta, work,
+                               stream);
 }
 
 SEG_API int seg_bn_eval_backward(const float* da, long ldda, const float* y, long ldy, long M, int C,

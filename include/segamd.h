@@ -76,6 +76,30 @@ int seg_conv_igemm_f16(const float* in, long ldin, int N, int H, int W, int Cin,
                        int ks, int stride, int pad,
                        const float* add, long ldadd, float* stat, int act, float* work, int splits,
                        hipStream_t stream);
+/* seg_conv_igemm_act / _bf16 / _f16 with the split-K ranges combined inside the launch (no
+ * reduce pass: the range whose ticket arrives last sums the ranges of its output tile in
+ * range order and applies the epilogue -- bitwise the two-launch result).  The batch-1
+ * inference convs (inference.py:162-163).  tickets: >= seg_conv_igemm_tickets(M, Cout)
+ * words, zero before the first call and left zero; one launch at a time per ticket array. */
+int seg_conv_igemm_act_tk(const float* in, long ldin, int N, int H, int W, int Cin,
+                          const float* wk, int ldk, const float* bias,
+                          float* out, long ldout, int Ho, int Wo, int Cout,
+                          int ks, int stride, int pad,
+                          const float* add, long ldadd, int act, float* work, int splits,
+                          unsigned* tickets, hipStream_t stream);
+int seg_conv_igemm_bf16_tk(const float* in, long ldin, int N, int H, int W, int Cin,
+                           const float* wk, int ldk, const float* bias,
+                           float* out, long ldout, int Ho, int Wo, int Cout,
+                           int ks, int stride, int pad,
+                           const float* add, long ldadd, int act, float* work, int splits,
+                           unsigned* tickets, hipStream_t stream);
+int seg_conv_igemm_f16_tk(const float* in, long ldin, int N, int H, int W, int Cin,
+                          const float* wk, int ldk, const float* bias,
+                          float* out, long ldout, int Ho, int Wo, int Cout,
+                          int ks, int stride, int pad,
+                          const float* add, long ldadd, int act, float* work, int splits,
+                          unsigned* tickets, hipStream_t stream);
+int seg_conv_igemm_tickets(long M, int Cout);
 /* Split-K factor for seg_conv_igemm_act (1 = none): > 1 only when the output tiles
  * cannot fill the 256 CUs (batch-1 inference). */
 int seg_conv_igemm_splits(long M, int Cout, int Cin, int ks);

@@ -27,6 +27,9 @@ PROTOTYPES = {
     "seg_conv_igemm_f16": (_I, [_V, _L, _I, _I, _I, _I, _V, _I, _V, _V, _L, _I, _I, _I, _I, _I, _I, _V, _L, _V, _I,
                                 _V, _I, _V]),
     "seg_conv_igemm_splits": (_I, [_L, _I, _I, _I]),
+    "seg_conv_igemm_act_tk": (_I, [_V, _L, _I, _I, _I, _I, _V, _I, _V, _V, _L, _I, _I, _I, _I, _I, _I, _V, _L, _I,
+                                   _V, _I, _V, _V]),
+    "seg_conv_igemm_tickets": (_I, [_L, _I]),
     "seg_igemm_force_tile": (_I, [_I]),
     "seg_conv_halo_ok": (_I, [_I, _I, _I, _I, _I]),
     "seg_conv_halo_pick": (_I, [_I, _I, _I, _I, _I]),
@@ -109,6 +112,8 @@ PROTOTYPES["seg_conv_igemm_bf16io_w16"] = PROTOTYPES["seg_conv_igemm"]
 PROTOTYPES["seg_conv_halo_bf16io_w16"] = PROTOTYPES["seg_conv_halo"]
 PROTOTYPES["seg_conv_igemm_bf16io_xf_w16"] = PROTOTYPES["seg_conv_igemm_bf16io_xf"]
 PROTOTYPES["seg_bn_backward_coef_bf16io"] = PROTOTYPES["seg_bn_backward_coef"]
+PROTOTYPES["seg_conv_igemm_bf16_tk"] = PROTOTYPES["seg_conv_igemm_act_tk"]
+PROTOTYPES["seg_conv_igemm_f16_tk"] = PROTOTYPES["seg_conv_igemm_act_tk"]
 PROTOTYPES["seg_conv_igemm_bf16io_bx_w16"] = PROTOTYPES["seg_conv_igemm_bx"]
 
 _lock = threading.Lock()

@@ -308,9 +308,12 @@ class ConvOp:
         M = o.N * o.H * o.W
         splits = query("seg_conv_igemm_splits", M, self.cout, self.cin_pad, self.ks)
         work = rt.tmp(splits * M * self.cout) if splits > 1 else None
+        # split-K ranges combined in the launch (one launch per conv); the ticket words are
+        # the Run's, zero and re-armed by every launch (stream order)
+        tickets = rt.tickets(query("seg_conv_igemm_tickets", M, self.cout)) if splits > 1 else None
         rt.call(_FOLDED_CONV[rt.prog.math], rt.ptr(i), i.ld, i.N, i.H, i.W, self.cin_pad, wk, ldk, bias, rt.ptr(o), o.ld,
              o.H, o.W, self.cout, self.ks, self.stride, self.pad, rt.ptr(r) if r is not None else None,
-             r.ld if r is not None else 0, None, act, work.data_ptr() if work is not None else None, splits, s)
+             r.ld if r is not None else 0, act, work.data_ptr() if work is not None else None, splits, tickets, s)
 
     def _in_xform(self, rt):
         """(scale, shift, act) of the producer's lazy BN for this op's input loads, or (None, None, 0)."""
@@ -896,7 +899,7 @@ MATHS = ("f32", "bf16", "bf16io", "f16")
 # parameter gradients, the loss and Adam stay fp32) -- the _bf16io entry points.
 # "f16" is the fp16 inference configuration (BASELINE configs[3]): the BN-folded eval
 # forward (Predictor) with fp16 conv operands; training programs refuse it.
-_FOLDED_CONV = {"f32": "seg_conv_igemm_act", "bf16": "seg_conv_igemm_bf16", "f16": "seg_conv_igemm_f16"}
+_FOLDED_CONV = {"f32": "seg_conv_igemm_act_tk", "bf16": "seg_conv_igemm_bf16_tk", "f16": "seg_conv_igemm_f16_tk"}
 
 
 def set_conv_math(model, math: str):
@@ -939,6 +942,7 @@ class Run:
         self.grads = {}       # id(param) -> grad tensor
         self.flat = None      # recorded run: one flat fp32 buffer holding every parameter gradient
         self.sync = None
+        self._tickets = None  # folded inference convs' split-K ticket words (Run.tickets)
         self._tmp_n = 0
         self.side = side      # side stream of the parameter gradients (recorded backward)
         self._n_fork = 0      # side-stream forks so far (index into the program's event pool)
@@ -984,6 +988,14 @@ class Run:
         if g is None:
             g = self.gbufs[name] = torch.empty_like(self.bufs[name])
         return g
+
+    def tickets(self, n: int) -> int:
+        """Device pointer of >= n zeroed ticket words (the in-launch split-K combine of the
+        folded inference convs).  One array per Run, allocated on first use -- before any graph
+        capture, since the Predictor warms up eagerly -- and left zero by every launch."""
+        if self._tickets is None or self._tickets.numel() < n:
+            self._tickets = torch.zeros(max(n, 1024), device=self.device, dtype=torch.int32)
+        return self._tickets.data_ptr()
 
     def tmp(self, n: int, zero: bool = False) -> torch.Tensor:
         """A float32 workspace; zero=True for the channel reductions' workspaces, whose ticket

@@ -310,10 +310,14 @@ class ConvOp:
         work = rt.tmp(splits * M * self.cout) if splits > 1 else None
         # split-K ranges combined in the launch (one launch per conv); the ticket words are
         # the Run's, zero and re-armed by every launch (stream order)
-        tickets = rt.tickets(query("seg_conv_igemm_tickets", M, self.cout)) if splits > 1 else None
-        rt.call(_FOLDED_CONV[rt.prog.math], rt.ptr(i), i.ld, i.N, i.H, i.W, self.cin_pad, wk, ldk, bias, rt.ptr(o), o.ld,
-             o.H, o.W, self.cout, self.ks, self.stride, self.pad, rt.ptr(r) if r is not None else None,
-             r.ld if r is not None else 0, act, work.data_ptr() if work is not None else None, splits, tickets, s)
+        args = (rt.ptr(i), i.ld, i.N, i.H, i.W, self.cin_pad, wk, ldk, bias, rt.ptr(o), o.ld, o.H, o.W, self.cout,
+                self.ks, self.stride, self.pad, rt.ptr(r) if r is not None else None, r.ld if r is not None else 0)
+        wp = work.data_ptr() if work is not None else None
+        if SPLITK_TK:
+            tickets = rt.tickets(query("seg_conv_igemm_tickets", M, self.cout)) if splits > 1 else None
+            rt.call(_FOLDED_CONV[rt.prog.math], *args, act, wp, splits, tickets, s)
+        else:  # raw partials + the reduce launch
+            rt.call(_FOLDED_CONV_2L[rt.prog.math], *args, None, act, wp, splits, s)
 
     def _in_xform(self, rt):
         """(scale, shift, act) of the producer's lazy BN for this op's input loads, or (None, None, 0)."""
@@ -900,6 +904,9 @@ MATHS = ("f32", "bf16", "bf16io", "f16")
 # "f16" is the fp16 inference configuration (BASELINE configs[3]): the BN-folded eval
 # forward (Predictor) with fp16 conv operands; training programs refuse it.
 _FOLDED_CONV = {"f32": "seg_conv_igemm_act_tk", "bf16": "seg_conv_igemm_bf16_tk", "f16": "seg_conv_igemm_f16_tk"}
+_FOLDED_CONV_2L = {"f32": "seg_conv_igemm_act", "bf16": "seg_conv_igemm_bf16", "f16": "seg_conv_igemm_f16"}
+# batch-1 folded convs: split-K combined in the launch (1) or raw partials + a reduce launch (0)
+SPLITK_TK = os.environ.get("SEG_SPLITK_TK", "1") == "1"
 
 
 def set_conv_math(model, math: str):

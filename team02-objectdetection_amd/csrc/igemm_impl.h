@@ -818,6 +818,10 @@ int conv_igemm_impl(const IT* in, long ldin, int N, int H, int W, int Cin, const
   if (ks == 1 && (stride != 1 || pad != 0 || Ho != H || Wo != W)) return (int)hipErrorInvalidValue;
   if (act < SEG_ACT_NONE || act > SEG_ACT_RELU6 || (act && stat)) return (int)hipErrorInvalidValue;
   if (splits < 1 || (splits > 1 && (!work || stat))) return (int)hipErrorInvalidValue;
+  if (splits > 1) {  // the K ranges actually launched: whole BK chunks, no empty range (launch_igemm)
+    const int nk = seg_cdiv((long)ks * ks * Cin, igemm_bk(ks * ks * Cin));
+    splits = seg_cdiv(nk, seg_cdiv(nk, splits));
+  }
   IgemmArgs a;
   a.in = in; a.ldin = ldin; a.wk = wk; a.ldk = ldk; a.bias = bias;
   a.add = add; a.ldadd = ldadd; a.out = out; a.ldout = ldout; a.stat = stat;

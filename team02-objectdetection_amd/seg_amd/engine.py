@@ -423,7 +423,13 @@ class ConvOp:
             return False
         else:
             v = 4
+        # Measured (tools/tapeprof.py, bf16io bs=32): a win only where the GEMM's K (= this BN's C) is
+        # at most its N (= the conv's Cin) on large images -- the project convs; on the expand convs
+        # (K = 6 Cin) the per-chunk coefficient loads and the loader's registers cost more than the
+        # apply pass they replace.  C >= 16: the uniform-tap loader needs K >= 16.
         C = self.cout
+        if C < 16 or C > self.cin or y.M < 65536:
+            return False
         return C % v == 0 and all(t.ld % v == 0 and t.off % v == 0 for t in (dA, y, dY))
 
     def _dgrad(self, rt, dY, dYp, s, bx=None):

@@ -76,30 +76,6 @@ int seg_conv_igemm_f16(const float* in, long ldin, int N, int H, int W, int Cin,
                        int ks, int stride, int pad,
                        const float* add, long ldadd, float* stat, int act, float* work, int splits,
                        hipStream_t stream);
-/* seg_conv_igemm_act / _bf16 / _f16 with the split-K ranges combined inside the launch (no
- * reduce pass: the range whose ticket arrives last sums the ranges of its output tile in
- * range order and applies the epilogue -- bitwise the two-launch result).  The batch-1
- * inference convs (inference.py:162-163).  tickets: >= seg_conv_igemm_tickets(M, Cout)
- * words, zero before the first call and left zero; one launch at a time per ticket array. */
-int seg_conv_igemm_act_tk(const float* in, long ldin, int N, int H, int W, int Cin,
-                          const float* wk, int ldk, const float* bias,
-                          float* out, long ldout, int Ho, int Wo, int Cout,
-                          int ks, int stride, int pad,
-                          const float* add, long ldadd, int act, float* work, int splits,
-                          unsigned* tickets, hipStream_t stream);
-int seg_conv_igemm_bf16_tk(const float* in, long ldin, int N, int H, int W, int Cin,
-                           const float* wk, int ldk, const float* bias,
-                           float* out, long ldout, int Ho, int Wo, int Cout,
-                           int ks, int stride, int pad,
-                           const float* add, long ldadd, int act, float* work, int splits,
-                           unsigned* tickets, hipStream_t stream);
-int seg_conv_igemm_f16_tk(const float* in, long ldin, int N, int H, int W, int Cin,
-                          const float* wk, int ldk, const float* bias,
-                          float* out, long ldout, int Ho, int Wo, int Cout,
-                          int ks, int stride, int pad,
-                          const float* add, long ldadd, int act, float* work, int splits,
-                          unsigned* tickets, hipStream_t stream);
-int seg_conv_igemm_tickets(long M, int Cout);
 /* Split-K factor for seg_conv_igemm_act (1 = none): > 1 only when the output tiles
  * cannot fill the 256 CUs (batch-1 inference). */
 int seg_conv_igemm_splits(long M, int Cout, int Cin, int ks);
@@ -265,6 +241,19 @@ int seg_bn_backward(const float* da, long ldda, const float* y, long ldy, long M
                     const float* gamma, const float* mean, const float* invstd,
                     const float* scale, const float* shift, int act,
                     float* dgamma, float* dbeta, float* work, float* dy, long lddy, hipStream_t stream);
+/* seg_bn_backward in ONE launch for small layers (the deep encoder / decoder levels, whose
+ * three-launch backward is launch-latency bound): partials, finalize and apply separated by
+ * two grid barriers.  Applies when seg_bn_backward_small_blocks(M, C, max_elems) > 0 (M*C <=
+ * max_elems); work >= seg_bn_backward_small_floats(C) floats, ZERO before the first call and
+ * used by one launch at a time (its first words hold the barrier; word 2 != 0 reports a barrier
+ * that timed out).  Deterministic (fixed-order sums); not bitwise seg_bn_backward (other row
+ * partition). */
+int seg_bn_backward_small_blocks(long M, int C, long max_elems);
+long seg_bn_backward_small_floats(int C);
+int seg_bn_backward_small(const float* da, long ldda, const float* y, long ldy, long M, int C,
+                          const float* gamma, const float* mean, const float* invstd,
+                          const float* scale, const float* shift, int act,
+                          float* dgamma, float* dbeta, float* work, float* dy, long lddy, hipStream_t stream);
 /* The reduction half of seg_bn_backward: dgamma / dbeta and the apply coefficients
  * (work + seg_chan_workspace_floats(M, C): [3][C]) for seg_conv_igemm_bx, which forms dY on load. */
 int seg_bn_backward_coef(const float* da, long ldda, const float* y, long ldy, long M, int C,
@@ -388,6 +377,9 @@ int seg_bn_stats_bf16io(const seg_bf16* y, long ldy, long M, int C, const float*
 int seg_bn_apply_bf16io(const seg_bf16* y, long ldy, long M, int C, const float* scale, const float* shift, int act,
     const seg_bf16* res, long ldres, seg_bf16* out, long ldout, hipStream_t stream);
 int seg_bn_backward_bf16io(const seg_bf16* da, long ldda, const seg_bf16* y, long ldy, long M, int C, const float*
+    gamma, const float* mean, const float* invstd, const float* scale, const float* shift, int act, float* dgamma,
+    float* dbeta, float* work, seg_bf16* dy, long lddy, hipStream_t stream);
+int seg_bn_backward_small_bf16io(const seg_bf16* da, long ldda, const seg_bf16* y, long ldy, long M, int C, const float*
     gamma, const float* mean, const float* invstd, const float* scale, const float* shift, int act, float* dgamma,
     float* dbeta, float* work, seg_bf16* dy, long lddy, hipStream_t stream);
 int seg_bn_backward_coef_bf16io(const seg_bf16* da, long ldda, const seg_bf16* y, long ldy, long M, int C, const float*

@@ -36,30 +36,6 @@ SEG_API int seg_conv_igemm_act(const float* in, long ldin, int N, int H, int W, 
                                 add, ldadd, stat, act, work, splits, stream);
 }
 
-// seg_conv_igemm_act with the split-K ranges combined inside the launch: the range whose
-// ticket arrives last sums all ranges of its output tile in range order and applies the
-// epilogue (bitwise the reduce pass's result), so a split conv is ONE launch -- the batch-1
-// inference convs (inference.py:162-163), whose frame is launch-latency bound.  `tickets`:
-// >= seg_conv_igemm_tickets(M, Cout) words, zero before the first call (every call leaves
-// them zero), used by one launch at a time (stream order).  splits == 1: as seg_conv_igemm_act.
-SEG_API int seg_conv_igemm_act_tk(const float* in, long ldin, int N, int H, int W, int Cin,
-                                  const float* wk, int ldk, const float* bias,
-                                  float* out, long ldout, int Ho, int Wo, int Cout,
-                                  int ks, int stride, int pad,
-                                  const float* add, long ldadd, int act, float* work, int splits,
-                                  unsigned* tickets, hipStream_t stream) {
-  if (splits > 1 && !tickets) return (int)hipErrorInvalidValue;
-  return conv_igemm_impl<float>(in, ldin, N, H, W, Cin, wk, ldk, bias, out, ldout, Ho, Wo, Cout, ks, stride, pad,
-                                add, ldadd, nullptr, act, work, splits, stream, nullptr, nullptr, 0, nullptr, tickets);
-}
-
-// Ticket words seg_conv_igemm_*_tk needs for an M x Cout output (its output tiles).
-SEG_API int seg_conv_igemm_tickets(long M, int Cout) {
-  if (M <= 0 || Cout <= 0) return 0;
-  const int t = pick_tile(M, Cout);
-  return (int)(((M + kTiles[t].bm - 1) / kTiles[t].bm) * ((Cout + kTiles[t].bn - 1) / kTiles[t].bn));
-}
-
 // seg_conv_igemm of a 1x1 conv whose input is the raw output of a BatchNorm'd producer
 // ("lazy BN": the depthwise conv of torchvision's InvertedResidual feeding the project
 // conv, outconv's first conv feeding its second, src/unet.py:113-116): the A operand is

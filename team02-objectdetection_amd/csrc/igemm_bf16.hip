@@ -25,15 +25,3 @@ SEG_API int seg_conv_igemm_bf16_xf(const float* in, long ldin, int N, int H, int
   return conv_igemm_impl<__bf16>(in, ldin, N, H, W, Cin, wk, ldk, bias, out, ldout, Ho, Wo, Cout, ks, stride, pad,
                                  add, ldadd, stat, SEG_ACT_NONE, nullptr, 1, stream, in_scale, in_shift, in_act);
 }
-
-// seg_conv_igemm_bf16 with the split-K ranges combined inside the launch (see seg_conv_igemm_act_tk).
-SEG_API int seg_conv_igemm_bf16_tk(const float* in, long ldin, int N, int H, int W, int Cin,
-                                   const float* wk, int ldk, const float* bias,
-                                   float* out, long ldout, int Ho, int Wo, int Cout,
-                                   int ks, int stride, int pad,
-                                   const float* add, long ldadd, int act, float* work, int splits,
-                                   unsigned* tickets, hipStream_t stream) {
-  if (splits > 1 && !tickets) return (int)hipErrorInvalidValue;
-  return conv_igemm_impl<__bf16>(in, ldin, N, H, W, Cin, wk, ldk, bias, out, ldout, Ho, Wo, Cout, ks, stride, pad,
-                                 add, ldadd, nullptr, act, work, splits, stream, nullptr, nullptr, 0, nullptr, tickets);
-}

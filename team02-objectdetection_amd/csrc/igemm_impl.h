@@ -32,8 +32,6 @@ struct IgemmArgs {
   int K, M;
   int kchunk;                    // split-K: K range of blockIdx.y (a multiple of BK); == K when unsplit
   float* part;                   // split-K: raw partial sums [gridDim.y][M][Cout] (no epilogue), else null
-  unsigned* tickets;             // split-K with the combine in this launch: [gridDim.x] words, zero before the
-                                 // first launch and left zero; null = raw partials for seg_igemm_splitk_reduce
   int act;                       // epilogue activation of act(acc + bias + add) (SegAct); 0 in training
   // optional input transform ("lazy BN", 1x1 uniform-tap path): the A operand is
   // act(in * xs[c] + xb[c]) per input channel c -- the producer's BatchNorm + activation
@@ -509,7 +507,7 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void igemm_conv_kernel(
 #endif
 
   // Epilogue: C layout of 32x32 f32 MFMA: col = lane&31, row = (r&3) + 8(r>>2) + 4(lane>>5).
-  if (a.part) {  // split-K: raw partial sums of this K range
+  if (a.part) {  // split-K: raw partial sums; seg_igemm_splitk_reduce applies the epilogue
     float* P = a.part + (long)blockIdx.y * a.M * a.Cout;
 #pragma unroll
     for (int ni = 0; ni < NI; ++ni) {
@@ -520,36 +518,10 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void igemm_conv_kernel(
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const int row = m0 + wm0 + mi * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-          if (row >= a.M) continue;
-          if (a.tickets) seg_st_wt(P + (long)row * a.Cout + col, acc[mi][ni][r]);  // read by another block
-          else P[(long)row * a.Cout + col] = acc[mi][ni][r];
+          if (row < a.M) P[(long)row * a.Cout + col] = acc[mi][ni][r];
         }
     }
-    if (!a.tickets) return;  // seg_igemm_splitk_reduce applies the epilogue
-    // The K range whose ticket arrives last sums all ranges of this output tile in range
-    // order (0 + p0 + p1 + ..., the reduce kernel's order: deterministic whatever the
-    // arrival order) and runs the epilogue below -- no reduce launch.
-    if (!seg_last_arrival(a.tickets + blockIdx.x, gridDim.y, reinterpret_cast<int*>(smem))) return;
-#pragma unroll
-    for (int ni = 0; ni < NI; ++ni) {
-      const int col = n0 + wn0 + ni * 32 + lrow;
-#pragma unroll
-      for (int mi = 0; mi < MI; ++mi)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) acc[mi][ni][r] = 0.f;
-      if (col >= a.Cout) continue;
-      for (int z = 0; z < (int)gridDim.y; ++z) {
-        const float* Pz = a.part + (long)z * a.M * a.Cout + col;
-#pragma unroll
-        for (int mi = 0; mi < MI; ++mi)
-#pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            const int row = m0 + wm0 + mi * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-            acc[mi][ni][r] += row < a.M ? seg_ld_wt(Pz + (long)row * a.Cout) : 0.f;
-          }
-      }
-    }
-    __syncthreads();  // every wave is past the ticket word before the epilogue reuses smem
+    return;
   }
   float bcol[NI];
 #pragma unroll
@@ -808,8 +780,7 @@ template <typename OT, typename IT = float, bool WB = false, bool BX = false>
 int conv_igemm_impl(const IT* in, long ldin, int N, int H, int W, int Cin, const void* wk, int ldk,
                     const float* bias, IT* out, long ldout, int Ho, int Wo, int Cout, int ks, int stride, int pad,
                     const IT* add, long ldadd, float* stat, int act, float* work, int splits, hipStream_t stream,
-                    const float* xs = nullptr, const float* xb = nullptr, int xact = 0, const BxArgs* bx = nullptr,
-                    unsigned* tickets = nullptr) {
+                    const float* xs = nullptr, const float* xb = nullptr, int xact = 0, const BxArgs* bx = nullptr) {
   if (!std::is_same<IT, float>::value && splits != 1) return (int)hipErrorInvalidValue;
   if ((Cin & 3) || (ldin & 3) || (ldk & 3) || (ks != 1 && ks != 3)) return (int)hipErrorInvalidValue;
   if (WB && ((ldk & 7) || ((uintptr_t)wk & 15) || splits != 1)) return (int)hipErrorInvalidValue;
@@ -828,7 +799,6 @@ int conv_igemm_impl(const IT* in, long ldin, int N, int H, int W, int Cin, const
   a.N = N; a.H = H; a.W = W; a.Cin = Cin; a.Ho = Ho; a.Wo = Wo; a.Cout = Cout;
   a.stride = stride; a.pad = pad; a.K = ks * ks * Cin; a.M = N * Ho * Wo; a.act = act;
   a.part = splits > 1 ? work : nullptr;
-  a.tickets = splits > 1 ? tickets : nullptr;
   a.xs = xs; a.xb = xb; a.xact = xact;
   a.by = nullptr; a.ldby = 0; a.bst = a.bcoef = nullptr; a.bact = 0; a.bdy = nullptr; a.ldbdy = 0;
   if constexpr (BX) {
@@ -860,7 +830,7 @@ int conv_igemm_impl(const IT* in, long ldin, int N, int H, int W, int Cin, const
     case 13: rc = launch_igemm<256, 64, 64, 32, OT, IT, WB, BX>(a, ks, splits, stream); break;
     default: rc = launch_igemm<64, 128, 32, 32, OT, IT, WB, BX>(a, ks, splits, stream); break;
   }
-  if (rc || splits == 1 || tickets) return rc;
+  if (rc || splits == 1) return rc;
   const long total = (long)a.M * Cout;
   hipLaunchKernelGGL(splitk_reduce_kernel, dim3((int)std::min<long>(seg_cdiv(total, 256), 4096)), dim3(256), 0,
                      stream, work, splits, (long)a.M, Cout, bias, reinterpret_cast<const float*>(add), ldadd,

@@ -27,9 +27,6 @@ PROTOTYPES = {
     "seg_conv_igemm_f16": (_I, [_V, _L, _I, _I, _I, _I, _V, _I, _V, _V, _L, _I, _I, _I, _I, _I, _I, _V, _L, _V, _I,
                                 _V, _I, _V]),
     "seg_conv_igemm_splits": (_I, [_L, _I, _I, _I]),
-    "seg_conv_igemm_act_tk": (_I, [_V, _L, _I, _I, _I, _I, _V, _I, _V, _V, _L, _I, _I, _I, _I, _I, _I, _V, _L, _I,
-                                   _V, _I, _V, _V]),
-    "seg_conv_igemm_tickets": (_I, [_L, _I]),
     "seg_igemm_force_tile": (_I, [_I]),
     "seg_conv_halo_ok": (_I, [_I, _I, _I, _I, _I]),
     "seg_conv_halo_pick": (_I, [_I, _I, _I, _I, _I]),
@@ -93,6 +90,8 @@ PROTOTYPES = {
     "seg_conv_igemm2_plan": (_I, [_L, _I, _I, _I, _V]),
     "seg_conv_igemm2_bf16io": (_I, [_V, _L, _I, _I, _I, _I, _V, _I, _V, _V, _L, _I, _I, _V, _L, _V, _V, _V]),
     "seg_bn_backward_coef": (_I, [_V, _L, _V, _L, _L, _I, _V, _V, _V, _V, _V, _I, _V, _V, _V, _V]),
+    "seg_bn_backward_small_blocks": (_I, [_L, _I, _L]),
+    "seg_bn_backward_small_floats": (_L, [_I]),
     "seg_conv_igemm_bx": (_I, [_V, _L, _I, _I, _I, _I, _V, _I, _V, _L, _I, _V, _L, _V, _L, _V, _V, _I, _V, _L, _V]),
 }
 # bf16-storage variants: same C signature shape as their fp32 namesakes (pointers stay void*)
@@ -112,8 +111,8 @@ PROTOTYPES["seg_conv_igemm_bf16io_w16"] = PROTOTYPES["seg_conv_igemm"]
 PROTOTYPES["seg_conv_halo_bf16io_w16"] = PROTOTYPES["seg_conv_halo"]
 PROTOTYPES["seg_conv_igemm_bf16io_xf_w16"] = PROTOTYPES["seg_conv_igemm_bf16io_xf"]
 PROTOTYPES["seg_bn_backward_coef_bf16io"] = PROTOTYPES["seg_bn_backward_coef"]
-PROTOTYPES["seg_conv_igemm_bf16_tk"] = PROTOTYPES["seg_conv_igemm_act_tk"]
-PROTOTYPES["seg_conv_igemm_f16_tk"] = PROTOTYPES["seg_conv_igemm_act_tk"]
+PROTOTYPES["seg_bn_backward_small"] = PROTOTYPES["seg_bn_backward"]
+PROTOTYPES["seg_bn_backward_small_bf16io"] = PROTOTYPES["seg_bn_backward"]
 PROTOTYPES["seg_conv_igemm_bf16io_bx_w16"] = PROTOTYPES["seg_conv_igemm_bx"]
 
 _lock = threading.Lock()

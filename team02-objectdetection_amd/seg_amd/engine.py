@@ -308,16 +308,9 @@ class ConvOp:
         M = o.N * o.H * o.W
         splits = query("seg_conv_igemm_splits", M, self.cout, self.cin_pad, self.ks)
         work = rt.tmp(splits * M * self.cout) if splits > 1 else None
-        # split-K ranges combined in the launch (one launch per conv); the ticket words are
-        # the Run's, zero and re-armed by every launch (stream order)
-        args = (rt.ptr(i), i.ld, i.N, i.H, i.W, self.cin_pad, wk, ldk, bias, rt.ptr(o), o.ld, o.H, o.W, self.cout,
-                self.ks, self.stride, self.pad, rt.ptr(r) if r is not None else None, r.ld if r is not None else 0)
-        wp = work.data_ptr() if work is not None else None
-        if SPLITK_TK:
-            tickets = rt.tickets(query("seg_conv_igemm_tickets", M, self.cout)) if splits > 1 else None
-            rt.call(_FOLDED_CONV[rt.prog.math], *args, act, wp, splits, tickets, s)
-        else:  # raw partials + the reduce launch
-            rt.call(_FOLDED_CONV_2L[rt.prog.math], *args, None, act, wp, splits, s)
+        rt.call(_FOLDED_CONV[rt.prog.math], rt.ptr(i), i.ld, i.N, i.H, i.W, self.cin_pad, wk, ldk, bias, rt.ptr(o), o.ld,
+             o.H, o.W, self.cout, self.ks, self.stride, self.pad, rt.ptr(r) if r is not None else None,
+             r.ld if r is not None else 0, None, act, work.data_ptr() if work is not None else None, splits, s)
 
     def _in_xform(self, rt):
         """(scale, shift, act) of the producer's lazy BN for this op's input loads, or (None, None, 0)."""
@@ -349,7 +342,11 @@ class ConvOp:
                 bx = (rt.gptr(dA), dA.ld, rt.ptr(y), y.ld, st.data_ptr(), work.data_ptr() + 4 * nws, self.act)
             else:
                 bx = None
-                rt.call(rt.k("seg_bn_backward"), rt.gptr(dA), dA.ld, rt.ptr(y), y.ld, M, C, self.bn.weight.data_ptr(),
+                name = "seg_bn_backward"
+                if self._bn_small_ok(dA, y, dY):  # one launch (grid barriers) instead of three
+                    name = "seg_bn_backward_small"
+                    work = rt.tmp(query("seg_bn_backward_small_floats", C), zero=True)
+                rt.call(rt.k(name), rt.gptr(dA), dA.ld, rt.ptr(y), y.ld, M, C, self.bn.weight.data_ptr(),
                         mean, invstd, scale, shift, self.act,
                         g_w, g_b, work.data_ptr(), rt.ptr(dY), dY.ld, s)
             if self.res is not None:
@@ -409,6 +406,14 @@ class ConvOp:
                             part.data_ptr(), splits, *xf, s)
                 rt.call("seg_conv_wgrad_reduce", part.data_ptr(), splits, gw, self.cout, self.cin, self.ks, 0, 0, s)
         rt.params_done(self.params(), s)
+
+    def _bn_small_ok(self, dA, y, dY) -> bool:
+        """Whether this layer's BN backward runs as one launch (seg_bn_backward_small): at most
+        BN_SMALL elements (the deep, latency-bound layers), one channel group per lane."""
+        C = self.cout
+        if query("seg_bn_backward_small_blocks", y.M, C, BN_SMALL) <= 0:
+            return False
+        return C <= 1024 or (C % 8 == 0 and all(t.ld % 8 == 0 and t.off % 8 == 0 for t in (dA, y, dY)))
 
     def _bx_ok(self, rt, dA, y, dY) -> bool:
         """Whether this conv's data gradient can form dY on load (seg_conv_igemm_bx): a 1x1 conv
@@ -909,10 +914,7 @@ MATHS = ("f32", "bf16", "bf16io", "f16")
 # parameter gradients, the loss and Adam stay fp32) -- the _bf16io entry points.
 # "f16" is the fp16 inference configuration (BASELINE configs[3]): the BN-folded eval
 # forward (Predictor) with fp16 conv operands; training programs refuse it.
-_FOLDED_CONV = {"f32": "seg_conv_igemm_act_tk", "bf16": "seg_conv_igemm_bf16_tk", "f16": "seg_conv_igemm_f16_tk"}
-_FOLDED_CONV_2L = {"f32": "seg_conv_igemm_act", "bf16": "seg_conv_igemm_bf16", "f16": "seg_conv_igemm_f16"}
-# batch-1 folded convs: split-K combined in the launch (1) or raw partials + a reduce launch (0)
-SPLITK_TK = os.environ.get("SEG_SPLITK_TK", "1") == "1"
+_FOLDED_CONV = {"f32": "seg_conv_igemm_act", "bf16": "seg_conv_igemm_bf16", "f16": "seg_conv_igemm_f16"}
 
 
 def set_conv_math(model, math: str):
@@ -955,7 +957,6 @@ class Run:
         self.grads = {}       # id(param) -> grad tensor
         self.flat = None      # recorded run: one flat fp32 buffer holding every parameter gradient
         self.sync = None
-        self._tickets = None  # folded inference convs' split-K ticket words (Run.tickets)
         self._tmp_n = 0
         self.side = side      # side stream of the parameter gradients (recorded backward)
         self._n_fork = 0      # side-stream forks so far (index into the program's event pool)
@@ -1001,14 +1002,6 @@ class Run:
         if g is None:
             g = self.gbufs[name] = torch.empty_like(self.bufs[name])
         return g
-
-    def tickets(self, n: int) -> int:
-        """Device pointer of >= n zeroed ticket words (the in-launch split-K combine of the
-        folded inference convs).  One array per Run, allocated on first use -- before any graph
-        capture, since the Predictor warms up eagerly -- and left zero by every launch."""
-        if self._tickets is None or self._tickets.numel() < n:
-            self._tickets = torch.zeros(max(n, 1024), device=self.device, dtype=torch.int32)
-        return self._tickets.data_ptr()
 
     def tmp(self, n: int, zero: bool = False) -> torch.Tensor:
         """A float32 workspace; zero=True for the channel reductions' workspaces, whose ticket
@@ -1200,6 +1193,9 @@ HALO_BF16 = os.environ.get("SEG_HALO_BF16", "1") == "1"
 # lazy BatchNorm for 1x1 consumers (the inverted residuals' project convs, OutConv's last
 # conv): SEG_LAZY_PW=0 keeps the separate BN-apply pass (read at program build)
 LAZY_PW = os.environ.get("SEG_LAZY_PW", "1") == "1"
+# BatchNorm backward of layers with at most this many elements (M x C) in one launch with grid
+# barriers (seg_bn_backward_small) instead of reduction + finalize + apply; 0 = off
+BN_SMALL = int(os.environ.get("SEG_BN_SMALL", "0"))
 # 1x1 data gradients forming their BN-backward dY on load (seg_conv_igemm_bx) instead of the BN
 # backward's apply pass: SEG_BX=0 keeps the apply pass (read at program build)
 BX = os.environ.get("SEG_BX", "0") == "1"

@@ -21,8 +21,10 @@ from collections import defaultdict
 FAMILIES = {  # "conv3" = the dense 3x3 conv forward + data gradient (bench.py's roofline kernel family)
     # (rocprofv3 leaves the __bf16 / _Float16 instantiations mangled: ILi..E forms)
     "conv3": re.compile(r"igemm_conv_kernel<\d+, \d+, \d+, \d+, 3, \d+|igemm_conv_kernelILi\d+ELi\d+ELi\d+ELi\d+ELi3E"
-                        r"|wino_gemm_kernel|wino_out_kernel|halo3x3_kernel"),
-    "igemm1": re.compile(r"igemm_conv_kernel<\d+, \d+, \d+, \d+, 1, \d+|igemm_conv_kernelILi\d+ELi\d+ELi\d+ELi\d+ELi1E"),
+                        r"|wino_gemm_kernel|wino_out_kernel|halo3x3_kernel"
+                        r"|igemm2_kernel<\d+, \d+, 3>|igemm2_kernelILi\d+ELi\d+ELi3E"),
+    "igemm1": re.compile(r"igemm_conv_kernel<\d+, \d+, \d+, \d+, 1, \d+|igemm_conv_kernelILi\d+ELi\d+ELi\d+ELi\d+ELi1E"
+                         r"|igemm2_kernel<\d+, \d+, 1>|igemm2_kernelILi\d+ELi\d+ELi1E"),
     "wgrad3": re.compile(r"wgrad_kernel<\d+, \d+, \d+, \d+, 3[,>]|wgrad_kernelILi\d+ELi\d+ELi\d+ELi\d+ELi3E"
                          r"|wino_wgrad"),
     "wgrad1": re.compile(r"wgrad_kernel<\d+, \d+, \d+, \d+, 1[,>]|wgrad_kernelILi\d+ELi\d+ELi\d+ELi\d+ELi1E"),

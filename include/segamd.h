@@ -241,38 +241,6 @@ int seg_bn_backward(const float* da, long ldda, const float* y, long ldy, long M
                     const float* gamma, const float* mean, const float* invstd,
                     const float* scale, const float* shift, int act,
                     float* dgamma, float* dbeta, float* work, float* dy, long lddy, hipStream_t stream);
-/* seg_bn_backward in ONE launch for small layers (the deep encoder / decoder levels, whose
- * three-launch backward is launch-latency bound): partials, finalize and apply separated by
- * two grid barriers.  Applies when seg_bn_backward_small_blocks(M, C, max_elems) > 0 (M*C <=
- * max_elems); work >= seg_bn_backward_small_floats(C) floats, ZERO before the first call and
- * used by one launch at a time (its first words hold the barrier; word 2 != 0 reports a barrier
- * that timed out).  Deterministic (fixed-order sums); not bitwise seg_bn_backward (other row
- * partition). */
-int seg_bn_backward_small_blocks(long M, int C, long max_elems);
-long seg_bn_backward_small_floats(int C);
-int seg_bn_backward_small(const float* da, long ldda, const float* y, long ldy, long M, int C,
-                          const float* gamma, const float* mean, const float* invstd,
-                          const float* scale, const float* shift, int act,
-                          float* dgamma, float* dbeta, float* work, float* dy, long lddy, hipStream_t stream);
-/* The reduction half of seg_bn_backward: dgamma / dbeta and the apply coefficients
- * (work + seg_chan_workspace_floats(M, C): [3][C]) for seg_conv_igemm_bx, which forms dY on load. */
-int seg_bn_backward_coef(const float* da, long ldda, const float* y, long ldy, long M, int C,
-                         const float* gamma, const float* mean, const float* invstd,
-                         const float* scale, const float* shift, int act,
-                         float* dgamma, float* dbeta, float* work, hipStream_t stream);
-/* 1x1 data gradient (stride 1) with the layer's BatchNorm backward formed on load -- replaces
- * seg_bn_backward's apply pass + seg_conv_igemm of the 1x1 convs' data gradient
- * (torchvision expand / project convs via src/unet.py:15-19, outconv src/unet.py:113-115):
- *   dY = BN-backward(da, y)  (seg_bn_backward's apply arithmetic; stats = the layer's
- *        [4][C] mean, invstd, scale, shift; coef from seg_bn_backward_coef; act of the BN)
- *   dx (+add) = dY . W  over C channels (wk: mode-1 pack [Cx][ldk]),
- * and dY itself is stored to dy (the weight / bias gradients read it).  Bitwise the
- * unfused pair.  C % 4 == 0 (fp32) / % 8 (bf16io) and 16-byte aligned rows. */
-int seg_conv_igemm_bx(const float* da, long ldda, int N, int H, int W, int C,
-                      const float* wk, int ldk, float* dx, long lddx, int Cx,
-                      const float* add, long ldadd, const float* y, long ldy,
-                      const float* stats, const float* coef, int act,
-                      float* dy, long lddy, hipStream_t stream);
 int seg_bn_eval_backward(const float* da, long ldda, const float* y, long ldy, long M, int C,
                          const float* scale, const float* shift, int act, float* dy, long lddy,
                          hipStream_t stream);
@@ -379,15 +347,6 @@ int seg_bn_apply_bf16io(const seg_bf16* y, long ldy, long M, int C, const float*
 int seg_bn_backward_bf16io(const seg_bf16* da, long ldda, const seg_bf16* y, long ldy, long M, int C, const float*
     gamma, const float* mean, const float* invstd, const float* scale, const float* shift, int act, float* dgamma,
     float* dbeta, float* work, seg_bf16* dy, long lddy, hipStream_t stream);
-int seg_bn_backward_small_bf16io(const seg_bf16* da, long ldda, const seg_bf16* y, long ldy, long M, int C, const float*
-    gamma, const float* mean, const float* invstd, const float* scale, const float* shift, int act, float* dgamma,
-    float* dbeta, float* work, seg_bf16* dy, long lddy, hipStream_t stream);
-int seg_bn_backward_coef_bf16io(const seg_bf16* da, long ldda, const seg_bf16* y, long ldy, long M, int C, const float*
-    gamma, const float* mean, const float* invstd, const float* scale, const float* shift, int act, float* dgamma,
-    float* dbeta, float* work, hipStream_t stream);
-int seg_conv_igemm_bf16io_bx_w16(const seg_bf16* da, long ldda, int N, int H, int W, int C, const seg_bf16* wk, int ldk,
-    seg_bf16* dx, long lddx, int Cx, const seg_bf16* add, long ldadd, const seg_bf16* y, long ldy, const float* stats,
-    const float* coef, int act, seg_bf16* dy, long lddy, hipStream_t stream);
 int seg_colsum_bf16io(const seg_bf16* y, long ldy, long M, int C, float* work, float* out, int accumulate, hipStream_t
     stream);
 int seg_dw_fwd_bf16io(const seg_bf16* in, long ldin, int N, int H, int W, int C, const float* in_scale, const float*

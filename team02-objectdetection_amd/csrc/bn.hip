@@ -40,9 +40,6 @@ constexpr int kRedSlice = 64;  // channel groups per block (blockIdx.y slices be
 #ifndef SEG_APPLY_ROWS4
 #define SEG_APPLY_ROWS4 0
 #endif
-#ifndef SEG_CHAN_ROWS
-#define SEG_CHAN_ROWS 4  // rows per lane whose loads the reductions issue together
-#endif
 int chan_blocks(long M) { return (int)std::max<long>(1, std::min<long>(SEG_CHAN_MAXBLK, M / 64)); }
 
 template <int VW, typename T>
@@ -108,16 +105,15 @@ __global__ __launch_bounds__(kRedThreads) void chan_partial_kernel(
       }
     };
     int r = r0 + rg;
-    constexpr int RB = SEG_CHAN_ROWS;
-    for (; r + (RB - 1) * RG < r1; r += RB * RG) {  // RB rows' loads issued together
-      f32x4 v[RB][NV], g[RB][NV];
+    for (; r + 3 * RG < r1; r += 4 * RG) {  // four rows' loads issued together
+      f32x4 v[4][NV], g[4][NV];
 #pragma unroll
-      for (int q = 0; q < RB; ++q) {
+      for (int q = 0; q < 4; ++q) {
         ldw<VW>(y + (long)(r + q * RG) * ldy + c, v[q]);
         if (KIND == 1) ldw<VW>(da + (long)(r + q * RG) * ldda + c, g[q]);
       }
 #pragma unroll
-      for (int q = 0; q < RB; ++q) step(v[q], g[q]);
+      for (int q = 0; q < 4; ++q) step(v[q], g[q]);
     }
     for (; r < r1; r += RG) {
       f32x4 v[NV], g[NV];
@@ -664,229 +660,6 @@ void launch_bn_bwd_apply(const T* da, long ldda, const T* y, long ldy, long M, i
                        C, scale, shift, mean, act, coef, dy, lddy);
 }
 
-
-// ---- One-launch BatchNorm backward for the small layers ------------------------------
-// The three-launch backward (partials, finalize, apply) costs ~5 us per launch whatever the
-// layer size, so the deep encoder / decoder layers (M <= 64k rows at bs=32) spend 16-37 us
-// each on it, mostly launch and drain latency.  This kernel runs the three phases in one
-// grid of G <= 256 blocks, separated by two grid barriers:
-//   1. block b sums (dz, dz*(y-mean)) over its R rows for every channel -> part[b][2][C];
-//   2. block b finalizes channels [b*CPB, (b+1)*CPB): fp64 sums of the G partials in block
-//      order (deterministic), dgamma / dbeta, coef[3][C] (bn_bwd_finalize_kernel's formulas);
-//   3. block b applies dY = seg_bnbwd4(...) to its R rows.
-// G never exceeds the blocks one wave of the grid can hold on an otherwise empty GPU (one
-// 256-thread block per CU), so every block becomes resident even when the side stream's
-// blocks hold CUs for a while.  The barrier is sense-reversing (arrival count + epoch in
-// `bar`, zero before the first launch, left consistent by every launch); partials and
-// coefficients cross blocks through write-through (agent-scope) stores and loads.  A
-// waiting block polls with s_sleep and gives up after kBarSpin polls (seconds), setting
-// bar[2], so a broken barrier cannot hang the GPU (the results are then garbage and the
-// caller's check of bar[2] raises).
-constexpr int kSmallThreads = 256;
-constexpr unsigned kBarSpin = 1u << 22;
-
-__device__ __forceinline__ void grid_barrier(unsigned* bar, unsigned nblocks) {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's write-through stores have landed
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    const unsigned e = __hip_atomic_load(bar + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const unsigned t = __hip_atomic_fetch_add(bar, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (t == nblocks - 1) {
-      __hip_atomic_store(bar, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-arm for the next barrier
-      __hip_atomic_store(bar + 1, e + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    } else {
-      unsigned n = 0;
-      while (__hip_atomic_load(bar + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == e) {
-        __builtin_amdgcn_s_sleep(2);
-        if (++n == kBarSpin) {
-          __hip_atomic_store(bar + 2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          break;
-        }
-      }
-    }
-  }
-  __syncthreads();
-}
-
-template <int VW, typename T>
-__device__ __forceinline__ void st_small(T* p, const f32x4 (&o)[VW / 4]) {
-  if constexpr (VW == 8 && sizeof(T) == 2) {
-    *reinterpret_cast<bf16x8*>(p) = seg_cat8(__builtin_convertvector(o[0], bf16x4), __builtin_convertvector(o[1], bf16x4));
-  } else {
-#pragma unroll
-    for (int j = 0; j < VW / 4; ++j) st4(p + 4 * j, o[j]);
-  }
-}
-
-template <typename T, int VW>
-__global__ __launch_bounds__(kSmallThreads) void bn_bwd_small_kernel(
-    const T* __restrict__ da, long ldda, const T* __restrict__ y, long ldy, int M, int C, int R,
-    const float* __restrict__ gamma, const float* __restrict__ mean, const float* __restrict__ invstd,
-    const float* __restrict__ scale, const float* __restrict__ shift, int act, float* dgamma, float* dbeta,
-    float* part, float* coef, unsigned* bar, T* dy, long lddy) {
-  constexpr int NV = VW / 4;
-  __shared__ f32x4 red0[kSmallThreads * NV], red1[kSmallThreads * NV];
-  const int CG = C / VW;
-  const int t = threadIdx.x;
-  const int G = gridDim.x, b = blockIdx.x;
-  const int r0 = b * R, r1 = min(M, r0 + R);
-  // ---- phase 1: partials of this block's rows, channel groups cg = t % TC (+ TC ...)
-  const int TC = CG < kSmallThreads ? CG : kSmallThreads;
-  const int RG = kSmallThreads / TC;
-  const int rg = t / TC, tc = t - rg * TC;
-  for (int cg = tc; cg < CG; cg += TC) {
-    const int c = cg * VW;
-    f32x4 s0[NV], s1[NV], k[NV], sc[NV], sh[NV];
-#pragma unroll
-    for (int j = 0; j < NV; ++j) {
-      s0[j] = s1[j] = f32x4{0.f, 0.f, 0.f, 0.f};
-      k[j] = ld4(mean + c + 4 * j);
-      sc[j] = ld4(scale + c + 4 * j);
-      sh[j] = ld4(shift + c + 4 * j);
-    }
-    if (rg < RG) {
-      int r = r0 + rg;
-      for (; r + 3 * RG < r1; r += 4 * RG) {
-        f32x4 v[4][NV], g[4][NV];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          ldw<VW>(y + (long)(r + q * RG) * ldy + c, v[q]);
-          ldw<VW>(da + (long)(r + q * RG) * ldda + c, g[q]);
-        }
-#pragma unroll
-        for (int q = 0; q < 4; ++q)
-#pragma unroll
-          for (int j = 0; j < NV; ++j) {
-            f32x4 dz;
-#pragma unroll
-            for (int e = 0; e < 4; ++e) dz[e] = g[q][j][e] * seg_act_mask(v[q][j][e] * sc[j][e] + sh[j][e], act);
-            s0[j] += dz;
-            s1[j] += dz * (v[q][j] - k[j]);
-          }
-      }
-      for (; r < r1; r += RG) {
-        f32x4 v[NV], g[NV];
-        ldw<VW>(y + (long)r * ldy + c, v);
-        ldw<VW>(da + (long)r * ldda + c, g);
-#pragma unroll
-        for (int j = 0; j < NV; ++j) {
-          f32x4 dz;
-#pragma unroll
-          for (int e = 0; e < 4; ++e) dz[e] = g[j][e] * seg_act_mask(v[j][e] * sc[j][e] + sh[j][e], act);
-          s0[j] += dz;
-          s1[j] += dz * (v[j] - k[j]);
-        }
-      }
-    }
-    __syncthreads();  // red0 / red1 free (previous channel round)
-#pragma unroll
-    for (int j = 0; j < NV; ++j) {
-      red0[t * NV + j] = s0[j];
-      red1[t * NV + j] = s1[j];
-    }
-    __syncthreads();
-    // fixed-order sum over the RG row lanes (deterministic), then write-through partials
-    if (rg == 0 && cg < CG) {
-#pragma unroll
-      for (int j = 0; j < NV; ++j) {
-        f32x4 a = red0[tc * NV + j], q = red1[tc * NV + j];
-        for (int h = 1; h < RG; ++h) {
-          a += red0[(h * TC + tc) * NV + j];
-          q += red1[(h * TC + tc) * NV + j];
-        }
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          seg_st_wt(part + (long)b * 2 * C + c + 4 * j + e, a[e]);
-          seg_st_wt(part + (long)b * 2 * C + C + c + 4 * j + e, q[e]);
-        }
-      }
-    }
-  }
-  grid_barrier(bar, G);
-  // ---- phase 2: this block's channels [c0, c1), one wave per channel: lane l loads partials
-  // l, l+64, l+128, l+192 at once (G <= 256), sums them in that order in fp64, then a fixed
-  // xor butterfly (sum_partials' scheme: deterministic)
-  const int cpb = (C + G - 1) / G;
-  const int c0 = b * cpb, c1 = min(C, c0 + cpb);
-  {
-    const int lane = t & 63, w = t >> 6;
-    for (int c = c0 + w; c < c1; c += kSmallThreads / 64) {
-      float va[4], vq[4];
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const long k = min(lane + 64 * q, G - 1);
-        va[q] = seg_ld_wt(part + k * 2 * C + c);
-        vq[q] = seg_ld_wt(part + k * 2 * C + C + c);
-      }
-      double a = 0.0, q2 = 0.0;
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const bool ok = lane + 64 * q < G;
-        a += ok ? (double)va[q] : 0.0;
-        q2 += ok ? (double)vq[q] : 0.0;
-      }
-      for (int o = 32; o > 0; o >>= 1) {
-        a += __shfl_xor(a, o, 64);
-        q2 += __shfl_xor(q2, o, 64);
-      }
-      if (lane == 0) {
-        const double inv = invstd[c];
-        const double gm = gamma ? gamma[c] : 1.0;
-        if (dbeta) dbeta[c] = (float)a;
-        if (dgamma) dgamma[c] = (float)(q2 * inv);
-        seg_st_wt(coef + c, (float)(gm * inv));
-        seg_st_wt(coef + C + c, (float)(a / (double)M));
-        seg_st_wt(coef + 2 * C + c, (float)(q2 * inv * inv / (double)M));
-      }
-    }
-  }
-  grid_barrier(bar, G);
-  // ---- phase 3: dY over this block's rows
-  for (int cg = tc; cg < CG; cg += TC) {
-    const int c = cg * VW;
-    f32x4 sc[NV], sh[NV], mu[NV], k1[NV], k2[NV], k3[NV];
-#pragma unroll
-    for (int j = 0; j < NV; ++j) {
-      sc[j] = ld4(scale + c + 4 * j);
-      sh[j] = ld4(shift + c + 4 * j);
-      mu[j] = ld4(mean + c + 4 * j);
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        k1[j][e] = seg_ld_wt(coef + c + 4 * j + e);
-        k2[j][e] = seg_ld_wt(coef + C + c + 4 * j + e);
-        k3[j][e] = seg_ld_wt(coef + 2 * C + c + 4 * j + e);
-      }
-    }
-    if (rg >= RG) continue;
-    for (int r = r0 + rg; r < r1; r += 2 * RG) {
-      const bool two = r + RG < r1;
-      f32x4 v0[NV], g0[NV], v1[NV], g1[NV];
-      ldw<VW>(y + (long)r * ldy + c, v0);
-      ldw<VW>(da + (long)r * ldda + c, g0);
-      if (two) {
-        ldw<VW>(y + (long)(r + RG) * ldy + c, v1);
-        ldw<VW>(da + (long)(r + RG) * ldda + c, g1);
-      }
-#pragma unroll
-      for (int j = 0; j < NV; ++j) v0[j] = seg_bnbwd4(g0[j], v0[j], sc[j], sh[j], mu[j], k1[j], k2[j], k3[j], act);
-      st_small<VW>(dy + (long)r * lddy + c, v0);
-      if (two) {
-#pragma unroll
-        for (int j = 0; j < NV; ++j) v1[j] = seg_bnbwd4(g1[j], v1[j], sc[j], sh[j], mu[j], k1[j], k2[j], k3[j], act);
-        st_small<VW>(dy + (long)(r + RG) * lddy + c, v1);
-      }
-    }
-  }
-}
-
-// Blocks of the one-launch backward for an M x C layer: one per 64 rows and at least one
-// per 4 channels (phase 2), at most 256 (one 256-thread block per CU: all of them resident
-// at once); 0 = the three-launch path (more than max_elems elements, or C / VW > 256 lanes).
-int bn_small_blocks(long M, int C, long max_elems) {
-  if (max_elems <= 0 || M * (long)C > max_elems || M < 1 || C % 4 || C / 4 > 2 * kSmallThreads) return 0;
-  return (int)std::min<long>(256, std::max<long>((M + 63) / 64, (C + 3) / 4));
-}
-
 }  // namespace
 
 // out = a (+ b), all [M][C] NHWC strided (out may alias a or b).  Gradient fan-in.
@@ -1021,78 +794,6 @@ SEG_API int seg_bn_backward_bf16io(const __bf16* da, long ldda, const __bf16* y,
                                    long lddy, hipStream_t stream) {
   return bn_backward_impl(da, ldda, y, ldy, M, C, gamma, mean, invstd, scale, shift, act, dgamma, dbeta, work, dy,
                           lddy, stream);
-}
-
-// The reduction half of seg_bn_backward (partials + finalize): dgamma / dbeta and the
-// apply coefficients coef[3][C] (k1, k2, k3 of seg_bnbwd4) at work + seg_chan_workspace_floats(M, C),
-// for a consumer that forms dY on load (seg_conv_igemm_bx) instead of the apply pass.
-template <typename T>
-static int bn_backward_coef_impl(const T* da, long ldda, const T* y, long ldy, long M, int C, const float* gamma,
-                                 const float* mean, const float* invstd, const float* scale, const float* shift,
-                                 int act, float* dgamma, float* dbeta, float* work, hipStream_t stream) {
-  if ((C & 3) || (ldy & 3) || (ldda & 3) || M < 1) return (int)hipErrorInvalidValue;
-  float* coef = work + seg_chan_workspace_floats(M, C);
-  launch_chan_partial<1, T>(y, ldy, da, ldda, M, C, scale, shift, mean, act, work, stream);
-  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(seg_cdiv(C, 4)), dim3(256), 0, stream, work, chan_blocks(M), M, C,
-                     gamma, invstd, dgamma, dbeta, coef);
-  SEG_RET_LAST();
-}
-SEG_API int seg_bn_backward_coef(const float* da, long ldda, const float* y, long ldy, long M, int C,
-                                 const float* gamma, const float* mean, const float* invstd, const float* scale,
-                                 const float* shift, int act, float* dgamma, float* dbeta, float* work,
-                                 hipStream_t stream) {
-  return bn_backward_coef_impl(da, ldda, y, ldy, M, C, gamma, mean, invstd, scale, shift, act, dgamma, dbeta, work,
-                               stream);
-}
-SEG_API int seg_bn_backward_coef_bf16io(const __bf16* da, long ldda, const __bf16* y, long ldy, long M, int C,
-                                        const float* gamma, const float* mean, const float* invstd,
-                                        const float* scale, const float* shift, int act, float* dgamma,
-                                        float* dbeta, float* work, hipStream_t stream) {
-  return bn_backward_coef_impl(da, ldda, y, ldy, M, C, gamma, mean, invstd, scale, shift, act, dgamma, dbeta, work,
-                               stream);
-}
-
-// One-launch train-mode BN backward for small layers (bn_bwd_small_kernel): the same
-// outputs as seg_bn_backward.  `work` >= seg_bn_backward_small_floats(C) floats, ZERO before
-// the first call (its first words are the grid barrier; every call leaves them consistent),
-// used by one launch at a time.  Applies when seg_bn_backward_small_blocks(M, C, max_elems) > 0.
-template <typename T>
-static int bn_backward_small_impl(const T* da, long ldda, const T* y, long ldy, long M, int C, const float* gamma,
-                                  const float* mean, const float* invstd, const float* scale, const float* shift,
-                                  int act, float* dgamma, float* dbeta, float* work, T* dy, long lddy,
-                                  hipStream_t stream) {
-  const int G = bn_small_blocks(M, C, 1L << 40);
-  if (G < 1 || (ldy & 3) || (ldda & 3) || (lddy & 3) || M > 0x7fffffffL) return (int)hipErrorInvalidValue;
-  auto eoff8 = [](const T* p) { return ((uintptr_t)p / sizeof(T)) % 8 == 0; };
-  const bool v8 = C % 8 == 0 && ldy % 8 == 0 && ldda % 8 == 0 && lddy % 8 == 0 && eoff8(y) && eoff8(da) && eoff8(dy);
-  if (!v8 && C / 4 > kSmallThreads) return (int)hipErrorInvalidValue;  // one channel group per lane
-  unsigned* bar = reinterpret_cast<unsigned*>(work);
-  float* part = work + 4;
-  float* coef = part + 256L * 2 * C;
-  const int R = seg_cdiv(M, G);
-  if (v8)
-    hipLaunchKernelGGL((bn_bwd_small_kernel<T, 8>), dim3(G), dim3(kSmallThreads), 0, stream, da, ldda, y, ldy, (int)M,
-                       C, R, gamma, mean, invstd, scale, shift, act, dgamma, dbeta, part, coef, bar, dy, lddy);
-  else
-    hipLaunchKernelGGL((bn_bwd_small_kernel<T, 4>), dim3(G), dim3(kSmallThreads), 0, stream, da, ldda, y, ldy, (int)M,
-                       C, R, gamma, mean, invstd, scale, shift, act, dgamma, dbeta, part, coef, bar, dy, lddy);
-  SEG_RET_LAST();
-}
-SEG_API int seg_bn_backward_small_blocks(long M, int C, long max_elems) { return bn_small_blocks(M, C, max_elems); }
-SEG_API long seg_bn_backward_small_floats(int C) { return 4 + 256L * 2 * C + 3L * C; }
-SEG_API int seg_bn_backward_small(const float* da, long ldda, const float* y, long ldy, long M, int C,
-                                  const float* gamma, const float* mean, const float* invstd, const float* scale,
-                                  const float* shift, int act, float* dgamma, float* dbeta, float* work, float* dy,
-                                  long lddy, hipStream_t stream) {
-  return bn_backward_small_impl(da, ldda, y, ldy, M, C, gamma, mean, invstd, scale, shift, act, dgamma, dbeta, work,
-                                dy, lddy, stream);
-}
-SEG_API int seg_bn_backward_small_bf16io(const __bf16* da, long ldda, const __bf16* y, long ldy, long M, int C,
-                                         const float* gamma, const float* mean, const float* invstd,
-                                         const float* scale, const float* shift, int act, float* dgamma, float* dbeta,
-                                         float* work, __bf16* dy, long lddy, hipStream_t stream) {
-  return bn_backward_small_impl(da, ldda, y, ldy, M, C, gamma, mean, invstd, scale, shift, act, dgamma, dbeta, work,
-                                dy, lddy, stream);
 }
 
 SEG_API int seg_bn_eval_backward(const float* da, long ldda, const float* y, long ldy, long M, int C,

@@ -38,16 +38,6 @@ struct IgemmArgs {
   // applied on load instead of by a separate pass (seg_bn_act4: the same fp32 value the
   // pass would have stored, rounded to the storage type only where the pass would have)
   const float* xs; const float* xb; int xact;
-  // optional BatchNorm backward on load (BX: 1x1 uniform-tap data gradients): the A
-  // operand is dY = seg_bnbwd4(in = dA, by = y, ...) per channel c < Cin -- the layer's
-  // BN-backward apply pass done by the GEMM that consumes dY (the same fp32 value, rounded
-  // to the storage type where the pass would have); the first column tile's blocks also
-  // store dY to bdy for the weight / bias gradients
-  const void* by; long ldby;       // y = the layer's raw conv output (IT)
-  const float* bst;                // [4][Cin]: mean, invstd, scale, shift (the layer's saved statistics)
-  const float* bcoef;              // [3][Cin]: k1, k2, k3 (seg_bn_backward_coef)
-  int bact;
-  void* bdy; long ldbdy;           // dY out (IT)
 };
 
 #ifndef SEG_IGEMM_DEPTH
@@ -88,10 +78,9 @@ struct IgemmArgs {
 // no conversion on the way into LDS.  Bitwise the fp32-weight kernel: the RNE rounding
 // is the same, done once at pack time.
 template <int BM, int BN, int WM, int WN, int KS, int BK, bool UT, typename OT = float, typename IT = float,
-          bool WB = false, bool BX = false>
+          bool WB = false>
 __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void igemm_conv_kernel(IgemmArgs a) {
   static_assert(!WB || std::is_same<OT, __bf16>::value, "bf16 weights feed bf16 operands");
-  static_assert(!BX || (KS == 1 && UT), "BN backward on load: 1x1 uniform-tap loader only");
   const float* wk32 = static_cast<const float*>(a.wk);
   const __bf16* wk16 = static_cast<const __bf16*>(a.wk);
   const IT* __restrict__ in = static_cast<const IT*>(a.in);
@@ -181,9 +170,6 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void igemm_conv_kernel(
   // and its coefficients, fetched with the chunk so store_tiles does not wait on them
   const bool XF = a.xs != nullptr;
   int xch = -1;
-  // BX: the raw conv output y at this thread's A slots (prefetched with dA)
-  long u_yoff[BX ? A_PER : 1];
-  f32x4 ry[BX ? A_PER : 1];
   f32x4 xsc[VA / 4], xsh[VA / 4];
   int u_tap = 0, u_ci = 0;
   long u_toff0 = 0, u_toff1 = 0;
@@ -199,7 +185,6 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void igemm_conv_kernel(
       if (KS == 1) {
         u_aoff[i] = (long)pp * a.ldin;
         u_mask[i] = ok ? 1u : 0u;
-        if constexpr (BX) u_yoff[i] = (long)pp * a.ldby;
       } else {
         const int hw = a.Ho * a.Wo;
         const int n = pp / hw, rem = pp - n * hw;
@@ -237,18 +222,6 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void igemm_conv_kernel(
       const bool wrap = ci >= a.Cin;
       const int tap = u_tap + (wrap ? 1 : 0);
       const long off = (wrap ? u_toff1 : u_toff0) + (wrap ? ci - a.Cin : ci);
-      if constexpr (BX) {  // 1x1: the chunk's channels are ci .. ci + VA - 1; coefficients load at store time
-        xch = wrap ? -1 : ci;
-        const IT* ybase = static_cast<const IT*>(a.by);
-#pragma unroll
-        for (int i = 0; i < A_PER; ++i) {
-          const bool ok = (u_mask[i] >> tap) & 1u;
-          if constexpr (VA == 8)
-            ry[i] = *reinterpret_cast<const f32x4*>(ok ? ybase + u_yoff[i] + ci : zero4);
-          else
-            ry[i] = ld4(ok ? ybase + u_yoff[i] + ci : zero4);
-        }
-      }
       if (KS == 1 && XF) {  // 1x1: the chunk's channels are ci .. ci + VA - 1 (no taps)
         xch = wrap ? -1 : ci;
         const int cc = wrap ? 0 : ci;
@@ -331,46 +304,6 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void igemm_conv_kernel(
       const int idx = tid + i * NT;
       if (A_VEC % NT == 0 || idx < A_VEC) {
         f32x4 v = ra[i];
-        if constexpr (BX) {
-          if (xch >= 0) {  // dY = BN backward of (dA, y) at channels xch .. xch + VA - 1
-            const int C = a.Cin;
-            f32x4 mu[VA / 4], sc[VA / 4], sh[VA / 4], k1[VA / 4], k2[VA / 4], k3[VA / 4], g[VA / 4], yv[VA / 4],
-                o[VA / 4];
-#pragma unroll
-            for (int j = 0; j < VA / 4; ++j) {
-              const int c = xch + 4 * j;
-              mu[j] = ld4(a.bst + c);
-              sc[j] = ld4(a.bst + 2 * C + c);
-              sh[j] = ld4(a.bst + 3 * C + c);
-              k1[j] = ld4(a.bcoef + c);
-              k2[j] = ld4(a.bcoef + C + c);
-              k3[j] = ld4(a.bcoef + 2 * C + c);
-            }
-            if constexpr (VA == 8) {
-              const bf16x8 qg = __builtin_bit_cast(bf16x8, v), qy = __builtin_bit_cast(bf16x8, ry[i]);
-              g[0] = __builtin_convertvector(__builtin_shufflevector(qg, qg, 0, 1, 2, 3), f32x4);
-              g[1] = __builtin_convertvector(__builtin_shufflevector(qg, qg, 4, 5, 6, 7), f32x4);
-              yv[0] = __builtin_convertvector(__builtin_shufflevector(qy, qy, 0, 1, 2, 3), f32x4);
-              yv[1] = __builtin_convertvector(__builtin_shufflevector(qy, qy, 4, 5, 6, 7), f32x4);
-            } else {
-              g[0] = v;
-              yv[0] = ry[i];
-            }
-#pragma unroll
-            for (int j = 0; j < VA / 4; ++j) o[j] = seg_bnbwd4(g[j], yv[j], sc[j], sh[j], mu[j], k1[j], k2[j], k3[j], a.bact);
-            if constexpr (VA == 8)
-              v = __builtin_bit_cast(f32x4, seg_cat8(__builtin_convertvector(o[0], bf16x4),
-                                                     __builtin_convertvector(o[1], bf16x4)));
-            else
-              v = o[0];
-            const int p = m0 + idx / KQA;
-            if (tn == 0 && p < a.M) {  // the first column tile stores dY once
-              IT* d = static_cast<IT*>(a.bdy) + (long)p * a.ldbdy + xch;
-              if constexpr (VA == 8) *reinterpret_cast<f32x4*>(d) = v;
-              else st4(d, v);
-            }
-          }
-        }
         if (KS == 1 && XF && xch >= 0) {
           if constexpr (VA == 8) {  // 8 bf16: widen, transform, round back (RNE) as the pass would
             const bf16x8 q = __builtin_bit_cast(bf16x8, v);
@@ -651,7 +584,7 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void igemm_conv_kernel(
   }
 }
 
-template <int BM, int BN, int WM, int WN, int BK, typename OT, typename IT, bool WB = false, bool BX = false>
+template <int BM, int BN, int WM, int WN, int BK, typename OT, typename IT, bool WB = false>
 int launch_igemm_bk(const IgemmArgs& a, int ks, hipStream_t s) {
   const int grid = seg_cdiv(a.M, BM) * seg_cdiv(a.Cout, BN);
   const int splits = seg_cdiv(a.K, a.kchunk);
@@ -659,19 +592,13 @@ int launch_igemm_bk(const IgemmArgs& a, int ks, hipStream_t s) {
                   (sizeof(IT) == 4 || (a.Cin % 8 == 0 && a.ldin % 8 == 0));  // bf16 A: 16-byte slots
   constexpr int NT = 64 * (BM / WM) * (BN / WN);
   if (a.xs && (!ut || ks != 1)) return (int)hipErrorInvalidValue;  // input transform: 1x1 uniform-tap loader only
-  if constexpr (BX) {  // BN backward on load: 1x1 uniform-tap loader only
-    if (!ut || ks != 1 || splits != 1) return (int)hipErrorInvalidValue;
-    hipLaunchKernelGGL((igemm_conv_kernel<BM, BN, WM, WN, 1, BK, true, OT, IT, WB, true>), dim3(grid, 1), dim3(NT), 0,
-                       s, a);
-  } else {
 #define SEG_IG(KS, U) hipLaunchKernelGGL((igemm_conv_kernel<BM, BN, WM, WN, KS, BK, U, OT, IT, WB>), dim3(grid, splits), dim3(NT), 0, s, a)
-    if (ks == 1) {
-      if (ut) SEG_IG(1, true); else SEG_IG(1, false);
-    } else {
-      if (ut) SEG_IG(3, true); else SEG_IG(3, false);
-    }
-#undef SEG_IG
+  if (ks == 1) {
+    if (ut) SEG_IG(1, true); else SEG_IG(1, false);
+  } else {
+    if (ut) SEG_IG(3, true); else SEG_IG(3, false);
   }
+#undef SEG_IG
   SEG_RET_LAST();
 }
 
@@ -681,7 +608,7 @@ int launch_igemm_bk(const IgemmArgs& a, int ks, hipStream_t s) {
 inline int igemm_bk(int K) { return (SEG_IGEMM_BK != 16 && (K <= 64 || (K % SEG_IGEMM_BK != 0 && K < 512))) ? 16 : SEG_IGEMM_BK; }
 
 // split-K: `splits` K ranges of whole BK chunks (a.part set by the caller when splits > 1)
-template <int BM, int BN, int WM, int WN, typename OT = float, typename IT = float, bool WB = false, bool BX = false>
+template <int BM, int BN, int WM, int WN, typename OT = float, typename IT = float, bool WB = false>
 int launch_igemm(IgemmArgs a, int ks, int splits, hipStream_t s) {
   int bk = igemm_bk(a.K);
   // 16-bit operands: 64-deep K chunks (4 MFMA k-steps per barrier) where the uniform-tap
@@ -692,10 +619,10 @@ int launch_igemm(IgemmArgs a, int ks, int splits, hipStream_t s) {
   const int nk = seg_cdiv(a.K, bk);
   a.kchunk = seg_cdiv(nk, splits) * bk;
   if constexpr (sizeof(OT) == 2) {
-    if (bk == 64) return launch_igemm_bk<BM, BN, WM, WN, 64, OT, IT, WB, BX>(a, ks, s);
+    if (bk == 64) return launch_igemm_bk<BM, BN, WM, WN, 64, OT, IT, WB>(a, ks, s);
   }
-  if (bk == 16) return launch_igemm_bk<BM, BN, WM, WN, 16, OT, IT, WB, BX>(a, ks, s);
-  return launch_igemm_bk<BM, BN, WM, WN, SEG_IGEMM_BK, OT, IT, WB, BX>(a, ks, s);
+  if (bk == 16) return launch_igemm_bk<BM, BN, WM, WN, 16, OT, IT, WB>(a, ks, s);
+  return launch_igemm_bk<BM, BN, WM, WN, SEG_IGEMM_BK, OT, IT, WB>(a, ks, s);
 }
 
 struct TileCfg {
@@ -768,19 +695,11 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restr
   }
 }
 
-// Optional BN backward on load (`bx`, BX = true): see IgemmArgs.
-struct BxArgs {
-  const void* y; long ldy;
-  const float* stats; const float* coef;
-  int act;
-  void* dy; long lddy;
-};
-
-template <typename OT, typename IT = float, bool WB = false, bool BX = false>
+template <typename OT, typename IT = float, bool WB = false>
 int conv_igemm_impl(const IT* in, long ldin, int N, int H, int W, int Cin, const void* wk, int ldk,
                     const float* bias, IT* out, long ldout, int Ho, int Wo, int Cout, int ks, int stride, int pad,
                     const IT* add, long ldadd, float* stat, int act, float* work, int splits, hipStream_t stream,
-                    const float* xs = nullptr, const float* xb = nullptr, int xact = 0, const BxArgs* bx = nullptr) {
+                    const float* xs = nullptr, const float* xb = nullptr, int xact = 0) {
   if (!std::is_same<IT, float>::value && splits != 1) return (int)hipErrorInvalidValue;
   if ((Cin & 3) || (ldin & 3) || (ldk & 3) || (ks != 1 && ks != 3)) return (int)hipErrorInvalidValue;
   if (WB && ((ldk & 7) || ((uintptr_t)wk & 15) || splits != 1)) return (int)hipErrorInvalidValue;
@@ -800,35 +719,24 @@ int conv_igemm_impl(const IT* in, long ldin, int N, int H, int W, int Cin, const
   a.stride = stride; a.pad = pad; a.K = ks * ks * Cin; a.M = N * Ho * Wo; a.act = act;
   a.part = splits > 1 ? work : nullptr;
   a.xs = xs; a.xb = xb; a.xact = xact;
-  a.by = nullptr; a.ldby = 0; a.bst = a.bcoef = nullptr; a.bact = 0; a.bdy = nullptr; a.ldbdy = 0;
-  if constexpr (BX) {
-    constexpr long VA = sizeof(IT) == 2 ? 8 : 4;  // 16-byte A slots of the uniform-tap loader
-    if (!bx || !bx->y || !bx->stats || !bx->coef || !bx->dy || xs || ks != 1 || splits != 1 || stat ||
-        SEG_IGEMM_STAGES != 1 || bx->act < SEG_ACT_NONE || bx->act > SEG_ACT_RELU6 || (Cin % VA) ||
-        (ldin % VA) || (bx->ldy % VA) || (bx->lddy % VA) || ((uintptr_t)in & 15) || ((uintptr_t)bx->y & 15) ||
-        ((uintptr_t)bx->dy & 15) || ((uintptr_t)bx->stats & 15) || ((uintptr_t)bx->coef & 15))
-      return (int)hipErrorInvalidValue;
-    a.by = bx->y; a.ldby = bx->ldy; a.bst = bx->stats; a.bcoef = bx->coef; a.bact = bx->act;
-    a.bdy = bx->dy; a.ldbdy = bx->lddy;
-  }
   if (a.M == 0 || Cout == 0) return 0;
   int rc;
   switch (pick_tile(a.M, Cout)) {
-    case 0: rc = launch_igemm<128, 128, 64, 64, OT, IT, WB, BX>(a, ks, splits, stream); break;
-    case 1: rc = launch_igemm<64, 128, 32, 64, OT, IT, WB, BX>(a, ks, splits, stream); break;
-    case 2: rc = launch_igemm<128, 64, 64, 32, OT, IT, WB, BX>(a, ks, splits, stream); break;
-    case 3: rc = launch_igemm<64, 64, 32, 32, OT, IT, WB, BX>(a, ks, splits, stream); break;
-    case 4: rc = launch_igemm<128, 96, 32, 96, OT, IT, WB, BX>(a, ks, splits, stream); break;
-    case 5: rc = launch_igemm<128, 160, 32, 160, OT, IT, WB, BX>(a, ks, splits, stream); break;
-    case 6: rc = launch_igemm<256, 32, 64, 32, OT, IT, WB, BX>(a, ks, splits, stream); break;
-    case 7: rc = launch_igemm<128, 32, 32, 32, OT, IT, WB, BX>(a, ks, splits, stream); break;
-    case 8: rc = launch_igemm<128, 128, 64, 32, OT, IT, WB, BX>(a, ks, splits, stream); break;
-    case 9: rc = launch_igemm<128, 128, 32, 64, OT, IT, WB, BX>(a, ks, splits, stream); break;
-    case 10: rc = launch_igemm<256, 128, 64, 64, OT, IT, WB, BX>(a, ks, splits, stream); break;
-    case 11: rc = launch_igemm<128, 256, 64, 64, OT, IT, WB, BX>(a, ks, splits, stream); break;
-    case 12: rc = launch_igemm<128, 64, 32, 32, OT, IT, WB, BX>(a, ks, splits, stream); break;
-    case 13: rc = launch_igemm<256, 64, 64, 32, OT, IT, WB, BX>(a, ks, splits, stream); break;
-    default: rc = launch_igemm<64, 128, 32, 32, OT, IT, WB, BX>(a, ks, splits, stream); break;
+    case 0: rc = launch_igemm<128, 128, 64, 64, OT, IT, WB>(a, ks, splits, stream); break;
+    case 1: rc = launch_igemm<64, 128, 32, 64, OT, IT, WB>(a, ks, splits, stream); break;
+    case 2: rc = launch_igemm<128, 64, 64, 32, OT, IT, WB>(a, ks, splits, stream); break;
+    case 3: rc = launch_igemm<64, 64, 32, 32, OT, IT, WB>(a, ks, splits, stream); break;
+    case 4: rc = launch_igemm<128, 96, 32, 96, OT, IT, WB>(a, ks, splits, stream); break;
+    case 5: rc = launch_igemm<128, 160, 32, 160, OT, IT, WB>(a, ks, splits, stream); break;
+    case 6: rc = launch_igemm<256, 32, 64, 32, OT, IT, WB>(a, ks, splits, stream); break;
+    case 7: rc = launch_igemm<128, 32, 32, 32, OT, IT, WB>(a, ks, splits, stream); break;
+    case 8: rc = launch_igemm<128, 128, 64, 32, OT, IT, WB>(a, ks, splits, stream); break;
+    case 9: rc = launch_igemm<128, 128, 32, 64, OT, IT, WB>(a, ks, splits, stream); break;
+    case 10: rc = launch_igemm<256, 128, 64, 64, OT, IT, WB>(a, ks, splits, stream); break;
+    case 11: rc = launch_igemm<128, 256, 64, 64, OT, IT, WB>(a, ks, splits, stream); break;
+    case 12: rc = launch_igemm<128, 64, 32, 32, OT, IT, WB>(a, ks, splits, stream); break;
+    case 13: rc = launch_igemm<256, 64, 64, 32, OT, IT, WB>(a, ks, splits, stream); break;
+    default: rc = launch_igemm<64, 128, 32, 32, OT, IT, WB>(a, ks, splits, stream); break;
   }
   if (rc || splits == 1) return rc;
   const long total = (long)a.M * Cout;

@@ -89,10 +89,6 @@ PROTOTYPES = {
     "seg_build_hash": (_I, [ctypes.c_char_p, _I]),
     "seg_conv_igemm2_plan": (_I, [_L, _I, _I, _I, _V]),
     "seg_conv_igemm2_bf16io": (_I, [_V, _L, _I, _I, _I, _I, _V, _I, _V, _V, _L, _I, _I, _V, _L, _V, _V, _V]),
-    "seg_bn_backward_coef": (_I, [_V, _L, _V, _L, _L, _I, _V, _V, _V, _V, _V, _I, _V, _V, _V, _V]),
-    "seg_bn_backward_small_blocks": (_I, [_L, _I, _L]),
-    "seg_bn_backward_small_floats": (_L, [_I]),
-    "seg_conv_igemm_bx": (_I, [_V, _L, _I, _I, _I, _I, _V, _I, _V, _L, _I, _V, _L, _V, _L, _V, _V, _I, _V, _L, _V]),
 }
 # bf16-storage variants: same C signature shape as their fp32 namesakes (pointers stay void*)
 for _n in ("seg_add", "seg_bn_stats", "seg_bn_apply", "seg_bn_backward", "seg_colsum", "seg_dw_fwd", "seg_dw_dgrad",
@@ -110,10 +106,6 @@ PROTOTYPES["seg_conv_halo_bf16io"] = PROTOTYPES["seg_conv_halo"]
 PROTOTYPES["seg_conv_igemm_bf16io_w16"] = PROTOTYPES["seg_conv_igemm"]
 PROTOTYPES["seg_conv_halo_bf16io_w16"] = PROTOTYPES["seg_conv_halo"]
 PROTOTYPES["seg_conv_igemm_bf16io_xf_w16"] = PROTOTYPES["seg_conv_igemm_bf16io_xf"]
-PROTOTYPES["seg_bn_backward_coef_bf16io"] = PROTOTYPES["seg_bn_backward_coef"]
-PROTOTYPES["seg_bn_backward_small"] = PROTOTYPES["seg_bn_backward"]
-PROTOTYPES["seg_bn_backward_small_bf16io"] = PROTOTYPES["seg_bn_backward"]
-PROTOTYPES["seg_conv_igemm_bf16io_bx_w16"] = PROTOTYPES["seg_conv_igemm_bx"]
 
 _lock = threading.Lock()
 _lib = None

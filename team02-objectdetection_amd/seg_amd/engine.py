@@ -332,27 +332,14 @@ class ConvOp:
             mean, invstd, scale, shift = _stat_ptrs(st, C)
             dY = Act(rt.tmp_buf(M * r4(C)), 0, r4(C), C, y.N, y.H, y.W)
             g_w, g_b = rt.grad_param(self.bn.weight), rt.grad_param(self.bn.bias)
-            nws = query("seg_chan_workspace_floats", M, C)
-            work = rt.tmp(nws + 3 * C)
-            if self._bx_ok(rt, dA, y, dY):
-                # the 1x1 data gradient forms dY on load (seg_conv_igemm_bx) and stores it for the
-                # parameter gradients: only the reduction half of the BN backward runs here
-                rt.call(rt.k("seg_bn_backward_coef"), rt.gptr(dA), dA.ld, rt.ptr(y), y.ld, M, C,
-                        self.bn.weight.data_ptr(), mean, invstd, scale, shift, self.act, g_w, g_b, work.data_ptr(), s)
-                bx = (rt.gptr(dA), dA.ld, rt.ptr(y), y.ld, st.data_ptr(), work.data_ptr() + 4 * nws, self.act)
-            else:
-                bx = None
-                name = "seg_bn_backward"
-                if self._bn_small_ok(dA, y, dY):  # one launch (grid barriers) instead of three
-                    name = "seg_bn_backward_small"
-                    work = rt.tmp(query("seg_bn_backward_small_floats", C), zero=True)
-                rt.call(rt.k(name), rt.gptr(dA), dA.ld, rt.ptr(y), y.ld, M, C, self.bn.weight.data_ptr(),
-                        mean, invstd, scale, shift, self.act,
-                        g_w, g_b, work.data_ptr(), rt.ptr(dY), dY.ld, s)
+            work = rt.tmp(query("seg_chan_workspace_floats", M, C) + 3 * C)
+            rt.call(rt.k("seg_bn_backward"), rt.gptr(dA), dA.ld, rt.ptr(y), y.ld, M, C, self.bn.weight.data_ptr(),
+                    mean, invstd, scale, shift, self.act,
+                    g_w, g_b, work.data_ptr(), rt.ptr(dY), dY.ld, s)
             if self.res is not None:
                 rt.add_pending(self.res, dA)
         else:
-            dY, bx = dA, None
+            dY = dA
         dYp = rt.ptr(dY) if dY.buf.startswith("#") else rt.gptr(dY)
         M = y.M
         # parameter gradients: on the side stream when overlapping (they only read dY and x,
@@ -362,9 +349,9 @@ class ConvOp:
         for p in (self.conv.weight, self.conv.bias):
             if p is not None and p.requires_grad:
                 rt.grad_param(p)
-        late = (FORK_LATE or bx is not None) and not self.first
+        late = FORK_LATE and not self.first
         if late:  # the data gradient first: the side stream's weight gradient then runs beside
-            self._dgrad(rt, dY, dYp, s, bx)  # the next layer's memory-bound BN backward, not this dgrad
+            self._dgrad(rt, dY, dYp, s)  # the next layer's memory-bound BN backward, not this dgrad
         ctx, sw = rt.fork()
         with ctx:
             self._param_grads(rt, dY, dYp, sw)
@@ -407,47 +394,9 @@ class ConvOp:
                 rt.call("seg_conv_wgrad_reduce", part.data_ptr(), splits, gw, self.cout, self.cin, self.ks, 0, 0, s)
         rt.params_done(self.params(), s)
 
-    def _bn_small_ok(self, dA, y, dY) -> bool:
-        """Whether this layer's BN backward runs as one launch (seg_bn_backward_small): at most
-        BN_SMALL elements (the deep, latency-bound layers), one channel group per lane."""
-        C = self.cout
-        if query("seg_bn_backward_small_blocks", y.M, C, BN_SMALL) <= 0:
-            return False
-        return C <= 1024 or (C % 8 == 0 and all(t.ld % 8 == 0 and t.off % 8 == 0 for t in (dA, y, dY)))
-
-    def _bx_ok(self, rt, dA, y, dY) -> bool:
-        """Whether this conv's data gradient can form dY on load (seg_conv_igemm_bx): a 1x1 conv
-        with a BN, on the fp32 or the bf16io (bf16-packed weights) path, 16-byte rows."""
-        if not BX or self.kind == "dw" or self.ks != 1 or self.stride != 1 or self.first or self.ig2_d is not None:
-            return False
-        if rt.io:
-            if not self.w16_d:
-                return False
-            v = 8
-        elif self.bf:
-            return False
-        else:
-            v = 4
-        # Measured (tools/tapeprof.py, bf16io bs=32): a win only where the GEMM's K (= this BN's C) is
-        # at most its N (= the conv's Cin) on large images -- the project convs; on the expand convs
-        # (K = 6 Cin) the per-chunk coefficient loads and the loader's registers cost more than the
-        # apply pass they replace.  C >= 16: the uniform-tap loader needs K >= 16.
-        C = self.cout
-        if C < 16 or C > self.cin or y.M < 65536:
-            return False
-        return C % v == 0 and all(t.ld % v == 0 and t.off % v == 0 for t in (dA, y, dY))
-
-    def _dgrad(self, rt, dY, dYp, s, bx=None):
-        """Data gradient into the input's gradient region (first writer / fused addend); `bx`:
-        (dA, ld, y, ld, stats, coef, act) -- dY formed on load from the BN backward's inputs."""
+    def _dgrad(self, rt, dY, dYp, s):
+        """Data gradient into the input's gradient region (first writer / fused addend)."""
         y, i = self.y, self.inp
-        if bx is not None:
-            add_ptr, add_ld = rt.begin_write_add(i)
-            rt.tcall("igemm1_dgrad", self.flops(), "seg_conv_igemm_bf16io_bx_w16" if rt.io else "seg_conv_igemm_bx",
-                     bx[0], bx[1], y.N, y.H, y.W, self.cout, self.wk_d.data_ptr(), self.ldk_d, rt.gptr(i), i.ld,
-                     self.cin, add_ptr, add_ld, bx[2], bx[3], bx[4], bx[5], bx[6], dYp, dY.ld, s)
-            rt.mark_written(i)
-            return
         if self.kind == "dw":
             acc = rt.begin_write_accumulate(i)
             rt.call(rt.k("seg_dw_dgrad"), dYp, dY.ld, y.N, y.H, y.W, self.cout, self.wk_f.data_ptr(), rt.gptr(i), i.ld, i.H,
@@ -1193,12 +1142,6 @@ HALO_BF16 = os.environ.get("SEG_HALO_BF16", "1") == "1"
 # lazy BatchNorm for 1x1 consumers (the inverted residuals' project convs, OutConv's last
 # conv): SEG_LAZY_PW=0 keeps the separate BN-apply pass (read at program build)
 LAZY_PW = os.environ.get("SEG_LAZY_PW", "1") == "1"
-# BatchNorm backward of layers with at most this many elements (M x C) in one launch with grid
-# barriers (seg_bn_backward_small) instead of reduction + finalize + apply; 0 = off
-BN_SMALL = int(os.environ.get("SEG_BN_SMALL", "0"))
-# 1x1 data gradients forming their BN-backward dY on load (seg_conv_igemm_bx) instead of the BN
-# backward's apply pass: SEG_BX=0 keeps the apply pass (read at program build)
-BX = os.environ.get("SEG_BX", "0") == "1"
 # bf16io deep convs on the 8-wave LDS-DMA implicit GEMM (seg_conv_igemm2_bf16io, csrc/igemm2.hip):
 # "3" = 3x3 convs where its plan applies (default), "all" = also 1x1 convs, "0" = off
 IGEMM2 = os.environ.get("SEG_IGEMM2", "3")

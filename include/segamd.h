@@ -76,6 +76,18 @@ int seg_conv_igemm_f16(const float* in, long ldin, int N, int H, int W, int Cin,
                        int ks, int stride, int pad,
                        const float* add, long ldadd, float* stat, int act, float* work, int splits,
                        hipStream_t stream);
+/* Thin-K 1x1 conv (stride 1) as a GEMM: out[M][N] = in[M][K] . W^T (+ bias) (+ add), K <= 32,
+ * K % 8 == 0, N <= 192 -- the output-heavy expand convs of torchvision's InvertedResidual
+ * (16 -> 96, 24 -> 144, 32 -> 192; src/unet.py:15-19), outconv (src/unet.py:113,116) and the
+ * data gradients of thin project convs.  wk: [N][ldk] (the 1x1 weight as is, or its data-gradient
+ * pack).  stat (optional): BN partials [seg_conv_pw_row_tiles(M)][2][N] (tile sum, M2 about the
+ * tile mean; 128-row tiles) for seg_bn_stats_tiles.  in_scale / in_shift / in_act (optional):
+ * the producer's lazy BatchNorm + activation applied on load (as seg_conv_igemm_xf).  Rows in
+ * 16-byte vectors (ld % 4). */
+int seg_conv_pw_row_tiles(long M);
+int seg_conv_pw(const float* in, long ldin, long M, int K, const float* wk, int ldk, const float* bias,
+                float* out, long ldout, int N, const float* add, long ldadd, float* stat,
+                const float* in_scale, const float* in_shift, int in_act, hipStream_t stream);
 /* Split-K factor for seg_conv_igemm_act (1 = none): > 1 only when the output tiles
  * cannot fill the 256 CUs (batch-1 inference). */
 int seg_conv_igemm_splits(long M, int Cout, int Cin, int ks);
@@ -377,6 +389,9 @@ int seg_maxpool2_bwd_bf16io(const seg_bf16* in, long ldin, const seg_bf16* dout,
 /* seg_conv_igemm_bf16io / _xf with the weights packed as bf16 (seg_pack_batch mode | 16):
  * [Cout][ldk] bf16, ldk % 8 == 0, 16-byte aligned, zero beyond K.  Bitwise the fp32-weight
  * launch (the same RNE rounding, done once at pack time); half the weight bytes. */
+int seg_conv_pw_bf16io(const seg_bf16* in, long ldin, long M, int K, const seg_bf16* wk, int ldk, const float* bias,
+    seg_bf16* out, long ldout, int N, const seg_bf16* add, long ldadd, float* stat, const float* in_scale, const float*
+    in_shift, int in_act, hipStream_t stream);
 int seg_conv_igemm_bf16io_w16(const seg_bf16* in, long ldin, int N, int H, int W, int Cin, const seg_bf16* wk,
     int ldk, const float* bias, seg_bf16* out, long ldout, int Ho, int Wo, int Cout, int ks, int stride, int pad,
     const seg_bf16* add, long ldadd, float* stat, hipStream_t stream);

@@ -88,6 +88,8 @@ PROTOTYPES = {
     "seg_tape_run": (_I, [_V, _I, _V, _V, _V]),
     "seg_build_hash": (_I, [ctypes.c_char_p, _I]),
     "seg_conv_igemm2_plan": (_I, [_L, _I, _I, _I, _V]),
+    "seg_conv_pw_row_tiles": (_I, [_L]),
+    "seg_conv_pw": (_I, [_V, _L, _L, _I, _V, _I, _V, _V, _L, _I, _V, _L, _V, _V, _V, _I, _V]),
     "seg_conv_igemm2_bf16io": (_I, [_V, _L, _I, _I, _I, _I, _V, _I, _V, _V, _L, _I, _I, _V, _L, _V, _V, _V]),
 }
 # bf16-storage variants: same C signature shape as their fp32 namesakes (pointers stay void*)
@@ -106,6 +108,7 @@ PROTOTYPES["seg_conv_halo_bf16io"] = PROTOTYPES["seg_conv_halo"]
 PROTOTYPES["seg_conv_igemm_bf16io_w16"] = PROTOTYPES["seg_conv_igemm"]
 PROTOTYPES["seg_conv_halo_bf16io_w16"] = PROTOTYPES["seg_conv_halo"]
 PROTOTYPES["seg_conv_igemm_bf16io_xf_w16"] = PROTOTYPES["seg_conv_igemm_bf16io_xf"]
+PROTOTYPES["seg_conv_pw_bf16io"] = PROTOTYPES["seg_conv_pw"]
 
 _lock = threading.Lock()
 _lib = None

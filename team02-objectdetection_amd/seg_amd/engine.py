@@ -56,6 +56,19 @@ _ROW_TILES = {}  # (M, Cout) -> (row tiles, tile height) of seg_conv_igemm
 _IG2 = {}  # (M, Cout, Cin, ks) -> (tile rows, row tiles, splits, workspace floats) or None
 
 
+def _pw_pick(op, v: int):
+    """(forward, data gradient) of a 1x1 conv on the thin-K kernel (seg_conv_pw): K <= 32 with
+    K % 8 == 0, N <= 192, rows in 16-byte vectors of v elements."""
+    if not PW or op.kind != "igemm" or op.ks != 1 or op.stride != 1:
+        return False, False
+    i, y = op.inp, op.y
+    rows = lambda *ts: all(t.ld % v == 0 and t.off % v == 0 for t in ts)  # noqa: E731
+    fwd = 8 <= op.cin_pad <= 32 and op.cin_pad % 8 == 0 and op.cout <= 192 and rows(i, y)
+    kin = r4(op.cout)
+    bwd = not op.first and 8 <= kin <= 32 and kin % 8 == 0 and op.cin <= 192 and rows(i) and kin % v == 0
+    return fwd, bwd
+
+
 def igemm2_plan(M: int, cout: int, cin: int, ks: int):
     """seg_conv_igemm2_plan (memoised): None when the deep-conv kernel does not apply."""
     key = (M, cout, cin, ks)
@@ -176,6 +189,8 @@ class ConvOp:
         self.w16_f = self.w16_d = False
         # bf16io deep convs on seg_conv_igemm2_bf16io (igemm2_plan tuples, chosen at pack time)
         self.ig2_f = self.ig2_d = None
+        # thin-K 1x1 forward / data gradient on seg_conv_pw (K <= 32, N <= 192; chosen at pack time)
+        self.pw_f = self.pw_d = False
         self.ks = conv.kernel_size[0]
         self.stride = conv.stride[0]
         self.pad = conv.padding[0]
@@ -214,7 +229,9 @@ class ConvOp:
                 ldk, wk_ptr = self.ldk_f, self.wk_f.data_ptr()  # packed by Program.pack at the step start
             stat = None
             if self.bn is not None and rt.training:  # BN statistics fused into the conv epilogue
-                if self.ig2_f is not None:
+                if self.pw_f:
+                    tile_rows, ntiles = 128, query("seg_conv_pw_row_tiles", y.M)
+                elif self.ig2_f is not None:
                     tile_rows, ntiles = self.ig2_f[0], self.ig2_f[1]
                 elif self.wino_f:
                     ntiles, tile_rows = query("seg_conv_wino_row_tiles", y.N, y.H, y.W), 256
@@ -224,7 +241,10 @@ class ConvOp:
                     ntiles, tile_rows = rt.row_tiles(y.M, self.cout)
                 stat = rt.tmp(ntiles * 2 * self.cout)
             statp = stat.data_ptr() if stat is not None else None
-            if self.halo_f:
+            if self.pw_f:  # thin-K 1x1 (its producer's lazy BN, if any, on load)
+                rt.tcall("igemm1_fwd", self.flops(), rt.k("seg_conv_pw"), rt.ptr(i), i.ld, y.M, self.cin_pad, wk_ptr,
+                         ldk, bias, rt.ptr(y), y.ld, self.cout, None, 0, statp, *self._in_xform(rt), s)
+            elif self.halo_f:
                 rt.tcall("igemm3_fwd", self.flops(), rt.k("seg_conv_halo") + ("_w16" if self.w16_f else ""), rt.ptr(i),
                          i.ld, i.N, i.H, i.W, self.cin_pad,
                             wk_ptr, ldk, bias, rt.ptr(y), y.ld, self.cout, None, 0, statp, s)
@@ -406,7 +426,10 @@ class ConvOp:
                 raise NotImplementedError("data gradient of a strided dense conv")
             kin = r4(self.cout)  # dY channels padded to 4 (the C=10 head)
             add_ptr, add_ld = rt.begin_write_add(i)
-            if self.halo_d:
+            if self.pw_d:  # thin-K 1x1 data gradient
+                rt.tcall("igemm1_dgrad", self.flops(), rt.k("seg_conv_pw"), dYp, dY.ld, y.M, kin, self.wk_d.data_ptr(),
+                         self.ldk_d, None, rt.gptr(i), i.ld, self.cin, add_ptr, add_ld, None, None, None, 0, s)
+            elif self.halo_d:
                 rt.tcall("igemm3_dgrad", self.flops(), rt.k("seg_conv_halo") + ("_w16" if self.w16_d else ""), dYp,
                          dY.ld, y.N, y.H, y.W, kin,
                             self.wk_d.data_ptr(), self.ldk_d, None, rt.gptr(i), i.ld, self.cin, add_ptr, add_ld, None, s)
@@ -580,6 +603,8 @@ class Program:
                         op.ig2_f = igemm2_plan(y.M, op.cout, op.cin_pad, op.ks)
                     if rows16 and not op.first and not op.halo_d and op.cout % 8 == 0:
                         op.ig2_d = igemm2_plan(y.M, op.cin, op.cout, op.ks)
+                if w16f:
+                    op.pw_f, op.pw_d = _pw_pick(op, 8)
                 if w16f or not (op.ks == 1 and op.cin_pad == op.cin):
                     op.ldk_f = r8(op.ks * op.ks * op.cin_pad) if w16f else r4(op.ks * op.ks * op.cin_pad)
                     op.wk_f = torch.empty(op.cout * op.ldk_f, device=dev,
@@ -595,6 +620,7 @@ class Program:
                                  kin))
                     max_elems = max(max_elems, op.cin * op.ldk_d)
                 continue
+            op.pw_f, op.pw_d = _pw_pick(op, 4)
             dense3 = op.ks == 3 and op.stride == 1 and op.pad == 1
             wino_ok = dense3 and WINOGRAD
             op.wino_f = wino_ok and bool(query("seg_conv_wino_pick", y.N, y.H, y.W, op.cin_pad, op.cout))
@@ -1142,6 +1168,8 @@ HALO_BF16 = os.environ.get("SEG_HALO_BF16", "1") == "1"
 # lazy BatchNorm for 1x1 consumers (the inverted residuals' project convs, OutConv's last
 # conv): SEG_LAZY_PW=0 keeps the separate BN-apply pass (read at program build)
 LAZY_PW = os.environ.get("SEG_LAZY_PW", "1") == "1"
+# thin-K 1x1 convs (K <= 32) on seg_conv_pw instead of the generic implicit GEMM; SEG_PW=0 = off
+PW = os.environ.get("SEG_PW", "1") == "1"
 # bf16io deep convs on the 8-wave LDS-DMA implicit GEMM (seg_conv_igemm2_bf16io, csrc/igemm2.hip):
 # "3" = 3x3 convs where its plan applies (default), "all" = also 1x1 convs, "0" = off
 IGEMM2 = os.environ.get("SEG_IGEMM2", "3")

@@ -407,8 +407,6 @@ class ConvOp:
             else:
                 splits = query("seg_conv_wgrad_splits_bf16" if self.bf else "seg_conv_wgrad_splits", M, self.cout,
                                self.cin_pad, self.ks)
-                if self.first and STEM_SPLITS:  # the backward's last weight gradient: the step's tail
-                    splits = max(1, min(STEM_SPLITS, M // 256))
                 part = rt.tmp(splits * self.cout * self.ks * self.ks * self.cin_pad)
                 name = ("seg_conv_wgrad_bf16io" if rt.io else "seg_conv_wgrad_bf16") if self.bf else "seg_conv_wgrad"
                 xf = ()
@@ -1174,9 +1172,6 @@ HALO_BF16 = os.environ.get("SEG_HALO_BF16", "1") == "1"
 # lazy BatchNorm for 1x1 consumers (the inverted residuals' project convs, OutConv's last
 # conv): SEG_LAZY_PW=0 keeps the separate BN-apply pass (read at program build)
 LAZY_PW = os.environ.get("SEG_LAZY_PW", "1") == "1"
-# K splits of the stem's weight gradient (0 = the library's choice): it runs after the main stream's last
-# kernel, so its length is the step's tail
-STEM_SPLITS = int(os.environ.get("SEG_STEM_SPLITS", "0"))
 # thin-K 1x1 convs (K <= 32) on seg_conv_pw instead of the generic implicit GEMM; SEG_PW=0 = off
 PW = os.environ.get("SEG_PW", "1") == "1"
 PW_MIN_ROWS = int(os.environ.get("SEG_PW_MIN_ROWS", "262144"))

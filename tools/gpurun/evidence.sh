@@ -1,8 +1,8 @@
 #!/bin/bash
-# Round-3 evidence pass: -m gpu suite + smoke, then final.sh (roofline profiles of f32 / bf16io:
+# Evidence pass (usage: evidence.sh <tag>): -m gpu suite + smoke, then final.sh (roofline profiles of f32 / bf16io:
 # kernel trace + FETCH / WRITE / MFMA-busy PMC passes + per-queue breakdown, the default bench
 # line, configs[4] lines).
-t=r03f
+t=${1:-evidence}
 bash tools/gpurun/steps.sh $t \
   "pytest|400|python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread" \
   "smoke|200|python -c 'import __graft_entry__ as g; g.smoke()'" || exit 1

@@ -387,8 +387,15 @@ class ConvOp:
         reduce) and the DDP readiness hook, all on stream `s`."""
         y, M = self.y, self.y.M
         if self.conv.bias is not None and self.conv.bias.requires_grad:
-            work = rt.tmp(query("seg_chan_workspace_floats", M, r4(self.cout)))
-            rt.call(rt.k("seg_colsum"), dYp, dY.ld, M, self.cout, work.data_ptr(), rt.grad_param(self.conv.bias), 0, s)
+            if self.bn is not None and ZERO_BN_BIAS:
+                # conv -> train-mode BatchNorm (src/unet.py:58-59,61-62): the bias shifts its whole channel by
+                # a constant that the batch mean removes again, so d loss / d bias = sum_p dY[p][c] = 0
+                # exactly (the reference computes that sum and gets fp32 rounding noise, ~1e-9 relative)
+                rt.zero_param_grad(self.conv.bias, s)
+            else:
+                work = rt.tmp(query("seg_chan_workspace_floats", M, r4(self.cout)))
+                rt.call(rt.k("seg_colsum"), dYp, dY.ld, M, self.cout, work.data_ptr(), rt.grad_param(self.conv.bias),
+                        0, s)
         if self.conv.weight.requires_grad:
             gw = rt.grad_param(self.conv.weight)
             i = self.inp
@@ -958,6 +965,15 @@ class Run:
         else:
             _timed_call(kind, flops, name, *args)
 
+    def zero_param_grad(self, p: torch.Tensor, stream) -> None:
+        """Write an all-zero gradient for parameter `p` (stream-ordered on `stream`)."""
+        ptr = self.grad_param(p)
+        if self.rec is not None:
+            n = p.numel() * 4
+            self.rec.memset2d(ptr, n, 0, n, 1, stream)
+        else:
+            self.grads[id(p)].zero_()
+
     def zero(self, a: Act):
         """Zero-fill the gradient region of `a` (a channel slice of a row buffer)."""
         if self.rec is not None:
@@ -1172,6 +1188,9 @@ HALO_BF16 = os.environ.get("SEG_HALO_BF16", "1") == "1"
 # lazy BatchNorm for 1x1 consumers (the inverted residuals' project convs, OutConv's last
 # conv): SEG_LAZY_PW=0 keeps the separate BN-apply pass (read at program build)
 LAZY_PW = os.environ.get("SEG_LAZY_PW", "1") == "1"
+# the bias gradient of a conv followed by train-mode BatchNorm is exactly zero: write zeros instead of
+# reducing dY (SEG_ZERO_BN_BIAS=0 keeps the reduction, whose result is rounding noise)
+ZERO_BN_BIAS = os.environ.get("SEG_ZERO_BN_BIAS", "1") == "1"
 # thin-K 1x1 convs (K <= 32) on seg_conv_pw instead of the generic implicit GEMM; SEG_PW=0 = off
 PW = os.environ.get("SEG_PW", "1") == "1"
 PW_MIN_ROWS = int(os.environ.get("SEG_PW_MIN_ROWS", "262144"))

@@ -229,3 +229,30 @@ def test_traceable_twin_matches_hip_eval():
     assert rel(hip, ref) < 1e-3
     with pytest.raises(RuntimeError, match="export and CPU use"):
         twin.to(DEV)(x.to(DEV))
+
+
+@pytest.mark.parametrize("math", ["f32", "bf16io"])
+def test_conv_bias_before_batchnorm_has_exactly_zero_gradient(math):
+    """A conv bias followed by train-mode BatchNorm (src/unet.py:58-59, 61-62) shifts its channel by a
+    constant that the batch mean removes, so its gradient sum_p dY[p][c] is exactly zero; the engine
+    writes zeros instead of reducing dY (the reference's reduction returns fp32 rounding noise).  A
+    bias NOT followed by BN (OutConv's last conv, src/unet.py:116) keeps its real gradient -- checked
+    against the fp64 sum of the oracle's logits gradient."""
+    model = deterministic_init(UNet(4, 16), seed=5).to(DEV).train()
+    engine.set_conv_math(model, math)
+    x, y = synthetic_batch(2, 32, 64, 4, seed=6)
+    for _ in range(2):  # the second step replays the recorded launch tape
+        model.zero_grad(set_to_none=True)
+        model.forward_loss(x.to(DEV), y.to(DEV)).backward()
+    torch.cuda.synchronize()
+    biased_bn = [m for m in model.modules() if isinstance(m, nn.Sequential)]
+    n_zero = 0
+    for seq in biased_bn:
+        mods = list(seq)
+        for a, b in zip(mods, mods[1:]):
+            if isinstance(a, nn.Conv2d) and a.bias is not None and isinstance(b, nn.BatchNorm2d):
+                assert a.bias.grad is not None and int(torch.count_nonzero(a.bias.grad)) == 0
+                n_zero += 1
+    assert n_zero >= 10
+    last = model.sem_out.conv[-1]  # UNet's head (src/unet.py:147): no BN after it
+    assert last.bias is not None and float(last.bias.grad.abs().sum()) > 0.0

@@ -606,7 +606,7 @@ class Program:
                 op.w16_f, op.w16_d = w16f, w16d
                 # the deep convs (3x3, or 1x1 with SEG_IGEMM2=all) on seg_conv_igemm2_bf16io
                 op.ig2_f = op.ig2_d = None
-                if (w16f and IGEMM2 != "0" and op.stride == 1 and op.pad == op.ks // 2
+                if (w16f and IGEMM2 != "0" and op.stride == 1 and op.pad == op.ks // 2 and y.M <= IGEMM2_MAX_ROWS
                         and (op.ks == 3 or IGEMM2 == "all")):
                     i = op.inp  # 16-byte rows: ld and channel offset multiples of 8 elements
                     rows16 = i.ld % 8 == 0 and i.off % 8 == 0 and y.ld % 8 == 0 and y.off % 8 == 0
@@ -966,13 +966,12 @@ class Run:
             _timed_call(kind, flops, name, *args)
 
     def zero_param_grad(self, p: torch.Tensor, stream) -> None:
-        """Write an all-zero gradient for parameter `p` (stream-ordered on `stream`)."""
-        ptr = self.grad_param(p)
-        if self.rec is not None:
-            n = p.numel() * 4
-            self.rec.memset2d(ptr, n, 0, n, 1, stream)
-        else:
-            self.grads[id(p)].zero_()
+        """An all-zero gradient for parameter `p`.  A recorded run's gradient slot is persistent and
+        nothing else writes it, so it is zeroed once, now (on the current stream, ahead of every
+        replay), and the tape gets no entry; an immediate run zeroes its fresh tensor on the current stream
+        (`stream`: inside the fork context)."""
+        self.grad_param(p)
+        self.grads[id(p)].zero_()
 
     def zero(self, a: Act):
         """Zero-fill the gradient region of `a` (a channel slice of a row buffer)."""
@@ -1197,6 +1196,9 @@ PW_MIN_ROWS = int(os.environ.get("SEG_PW_MIN_ROWS", "262144"))
 # bf16io deep convs on the 8-wave LDS-DMA implicit GEMM (seg_conv_igemm2_bf16io, csrc/igemm2.hip):
 # "3" = 3x3 convs where its plan applies (default), "all" = also 1x1 convs, "0" = off
 IGEMM2 = os.environ.get("SEG_IGEMM2", "3")
+# ... on images of at most this many output rows: measured per launch on UNet 512x1024 bf16io, igemm2 is 5-25 %
+# slower than the 4-wave implicit GEMM at 262k-4M rows and 1-6 % faster at 65k (profiles/r03k)
+IGEMM2_MAX_ROWS = int(os.environ.get("SEG_IGEMM2_MAX_ROWS", "65536"))
 # bf16io implicit GEMMs on bf16-packed weights (seg_conv_igemm_bf16io_w16); SEG_W16=0 keeps the fp32 packs
 W16 = os.environ.get("SEG_W16", "1") == "1"
 # fork the weight-gradient side stream after the layer's data gradient (measured: f32 +1.5 %, bf16io +-0)

@@ -125,7 +125,8 @@ int seg_conv_wgrad_bf16(const float* dy, long lddy, const float* x, long ldx,
  * seg_bn_finalize, act SEG_ACT_* -- is formed while the operand is staged in LDS
  * instead of by a separate seg_bn_apply pass.  Bitwise the same as seg_bn_apply
  * followed by the plain conv (bf16 storage: the transformed value is rounded to bf16
- * as seg_bn_apply_bf16io would store it).  ks must be 1; no split-K. */
+ * as seg_bn_apply_bf16io would store it).  ks 1, or ks 3 with Cin >= the K chunk (padding taps
+ * stay zero; double_conv's first conv feeding its second); no split-K. */
 int seg_conv_igemm_xf(const float* in, long ldin, int N, int H, int W, int Cin,
                       const float* wk, int ldk, const float* bias,
                       float* out, long ldout, int Ho, int Wo, int Cout,
@@ -416,6 +417,19 @@ int seg_conv_igemm_bf16io_xf(const seg_bf16* in, long ldin, int N, int H, int W,
 int seg_conv_wgrad_bf16io_xf(const seg_bf16* dy, long lddy, const seg_bf16* x, long ldx, int N, int H, int W,
     int Cin, int Ho, int Wo, int Cout, int ks, int stride, int pad, float* part, int splits, const float* in_scale,
     const float* in_shift, int in_act, hipStream_t stream);
+/* seg_conv_halo(_bf16io, _bf16io_w16) of a 3x3 conv whose input is the raw output of a BatchNorm'd
+ * producer (double_conv's first conv, src/unet.py:58-60): in = act(in * in_scale[c] + in_shift[c]) on the
+ * halo load, padding pixels zero -- the tensor the BN-apply pass would have stored (bf16: rounded RNE).
+ * The _xf implicit GEMMs / weight gradients above take ks 3 the same way (Cin >= the K chunk). */
+int seg_conv_halo_xf(const float* in, long ldin, int N, int H, int W, int Cin, const float* wk, int ldk,
+    const float* bias, float* out, long ldout, int Cout, const float* add, long ldadd, float* stat,
+    const float* in_scale, const float* in_shift, int in_act, hipStream_t stream);
+int seg_conv_halo_bf16io_xf(const seg_bf16* in, long ldin, int N, int H, int W, int Cin, const float* wk, int ldk,
+    const float* bias, seg_bf16* out, long ldout, int Cout, const seg_bf16* add, long ldadd, float* stat,
+    const float* in_scale, const float* in_shift, int in_act, hipStream_t stream);
+int seg_conv_halo_bf16io_xf_w16(const seg_bf16* in, long ldin, int N, int H, int W, int Cin, const seg_bf16* wk,
+    int ldk, const float* bias, seg_bf16* out, long ldout, int Cout, const seg_bf16* add, long ldadd, float* stat,
+    const float* in_scale, const float* in_shift, int in_act, hipStream_t stream);
 
 /* ---- Adam (optim.Adam(model.parameters(), lr=1.5e-4), main.py:100; step at
  *      src/train.py:39): one launch over every parameter with a gradient, the

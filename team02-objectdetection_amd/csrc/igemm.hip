@@ -40,7 +40,8 @@ SEG_API int seg_conv_igemm_act(const float* in, long ldin, int N, int H, int W, 
 // ("lazy BN": the depthwise conv of torchvision's InvertedResidual feeding the project
 // conv, outconv's first conv feeding its second, src/unet.py:113-116): the A operand is
 // act(in * in_scale[c] + in_shift[c]) formed on load, so the producer's BN-apply pass
-// and its output tensor disappear.  ks must be 1.
+// and its output tensor disappear.  ks 1, or ks 3 with Cin >= the K chunk (padding taps stay zero:
+// the transform applies to real pixels only -- double_conv's first conv feeding its second).
 SEG_API int seg_conv_igemm_xf(const float* in, long ldin, int N, int H, int W, int Cin,
                               const float* wk, int ldk, const float* bias,
                               float* out, long ldout, int Ho, int Wo, int Cout,

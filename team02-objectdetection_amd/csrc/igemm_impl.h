@@ -33,7 +33,7 @@ struct IgemmArgs {
   int kchunk;                    // split-K: K range of blockIdx.y (a multiple of BK); == K when unsplit
   float* part;                   // split-K: raw partial sums [gridDim.y][M][Cout] (no epilogue), else null
   int act;                       // epilogue activation of act(acc + bias + add) (SegAct); 0 in training
-  // optional input transform ("lazy BN", 1x1 uniform-tap path): the A operand is
+  // optional input transform ("lazy BN", uniform-tap path, 1x1 or 3x3): the A operand is
   // act(in * xs[c] + xb[c]) per input channel c -- the producer's BatchNorm + activation
   // applied on load instead of by a separate pass (seg_bn_act4: the same fp32 value the
   // pass would have stored, rounded to the storage type only where the pass would have)
@@ -170,6 +170,7 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void igemm_conv_kernel(
   // and its coefficients, fetched with the chunk so store_tiles does not wait on them
   const bool XF = a.xs != nullptr;
   int xch = -1;
+  unsigned xvm = 0;  // 3x3: the A slots of the loaded chunk that hold real pixels (padding taps stay zero)
   f32x4 xsc[VA / 4], xsh[VA / 4];
   int u_tap = 0, u_ci = 0;
   long u_toff0 = 0, u_toff1 = 0;
@@ -222,18 +223,20 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void igemm_conv_kernel(
       const bool wrap = ci >= a.Cin;
       const int tap = u_tap + (wrap ? 1 : 0);
       const long off = (wrap ? u_toff1 : u_toff0) + (wrap ? ci - a.Cin : ci);
-      if (KS == 1 && XF) {  // 1x1: the chunk's channels are ci .. ci + VA - 1 (no taps)
+      if (XF) {  // the chunk's channels for this thread: ci .. ci + VA - 1 of tap `tap` (1x1: no taps)
         xch = wrap ? -1 : ci;
-        const int cc = wrap ? 0 : ci;
+        const int cc = KS == 1 ? (wrap ? 0 : ci) : (wrap ? ci - a.Cin : ci);
 #pragma unroll
         for (int j = 0; j < VA / 4; ++j) {
           xsc[j] = ld4(a.xs + cc + 4 * j);
           xsh[j] = ld4(a.xb + cc + 4 * j);
         }
+        xvm = 0;
       }
 #pragma unroll
       for (int i = 0; i < A_PER; ++i) {
         const bool ok = (u_mask[i] >> tap) & 1u;
+        if (KS != 1 && XF && ok) xvm |= 1u << i;
         if constexpr (VA == 8)  // 8 bf16 as an opaque 16-byte payload
           ra[i] = *reinterpret_cast<const f32x4*>(ok ? in + u_aoff[i] + off : zero4);
         else
@@ -304,7 +307,7 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void igemm_conv_kernel(
       const int idx = tid + i * NT;
       if (A_VEC % NT == 0 || idx < A_VEC) {
         f32x4 v = ra[i];
-        if (KS == 1 && XF && xch >= 0) {
+        if (XF && (KS == 1 ? xch >= 0 : ((xvm >> i) & 1u) != 0)) {
           if constexpr (VA == 8) {  // 8 bf16: widen, transform, round back (RNE) as the pass would
             const bf16x8 q = __builtin_bit_cast(bf16x8, v);
             const f32x4 lo = seg_bn_act4(__builtin_convertvector(__builtin_shufflevector(q, q, 0, 1, 2, 3), f32x4),
@@ -591,7 +594,7 @@ int launch_igemm_bk(const IgemmArgs& a, int ks, hipStream_t s) {
   const bool ut = SEG_IGEMM_UT && (SEG_IGEMM_UT2 ? a.Cin >= BK : a.Cin % BK == 0) &&
                   (sizeof(IT) == 4 || (a.Cin % 8 == 0 && a.ldin % 8 == 0));  // bf16 A: 16-byte slots
   constexpr int NT = 64 * (BM / WM) * (BN / WN);
-  if (a.xs && (!ut || ks != 1)) return (int)hipErrorInvalidValue;  // input transform: 1x1 uniform-tap loader only
+  if (a.xs && !ut) return (int)hipErrorInvalidValue;  // input transform: the uniform-tap loader only (Cin >= BK)
 #define SEG_IG(KS, U) hipLaunchKernelGGL((igemm_conv_kernel<BM, BN, WM, WN, KS, BK, U, OT, IT, WB>), dim3(grid, splits), dim3(NT), 0, s, a)
   if (ks == 1) {
     if (ut) SEG_IG(1, true); else SEG_IG(1, false);
@@ -703,7 +706,7 @@ int conv_igemm_impl(const IT* in, long ldin, int N, int H, int W, int Cin, const
   if (!std::is_same<IT, float>::value && splits != 1) return (int)hipErrorInvalidValue;
   if ((Cin & 3) || (ldin & 3) || (ldk & 3) || (ks != 1 && ks != 3)) return (int)hipErrorInvalidValue;
   if (WB && ((ldk & 7) || ((uintptr_t)wk & 15) || splits != 1)) return (int)hipErrorInvalidValue;
-  if (xs && (!xb || ks != 1 || splits != 1 || SEG_IGEMM_STAGES != 1 || xact < SEG_ACT_NONE || xact > SEG_ACT_RELU6))
+  if (xs && (!xb || splits != 1 || SEG_IGEMM_STAGES != 1 || xact < SEG_ACT_NONE || xact > SEG_ACT_RELU6))
     return (int)hipErrorInvalidValue;
   if (ks == 1 && (stride != 1 || pad != 0 || Ho != H || Wo != W)) return (int)hipErrorInvalidValue;
   if (act < SEG_ACT_NONE || act > SEG_ACT_RELU6 || (act && stat)) return (int)hipErrorInvalidValue;

@@ -36,7 +36,7 @@ struct WgradArgs {
   float* part;
   int N, H, W, Cin, Ho, Wo, Cout, stride, pad;
   int M, Nw, kchunk;
-  // optional input transform of X (1x1 convs, XF kernels): x = act(x * xs[c] + xb[c]) on
+  // optional input transform of X (XF kernels; 3x3: real pixels only, padding stays zero): x = act(x * xs[c] + xb[c]) on
   // load -- the producer's lazy BatchNorm + activation (see seg_conv_igemm_xf)
   const float* xs; const float* xb; int xact;
 };
@@ -54,7 +54,6 @@ constexpr int tr_pitch(int n) { return n % 128 == 32 || n % 128 == 96 ? n : tr_p
 // storage when Cout, Cin and the row strides are multiples of 8, else 4.
 template <int BM, int BN, int WM, int WN, int KS, bool BF = false, typename IT = float, int VW = 4, bool XF = false>
 __global__ __launch_bounds__(256) void wgrad_kernel(WgradArgs a) {
-  static_assert(!XF || KS == 1, "input transform: 1x1 convs");
   static_assert(VW == 4 || (BF && sizeof(IT) == 2), "16-byte slots carry bf16 operands");
   const IT* __restrict__ gdy = static_cast<const IT*>(a.dy);
   const IT* __restrict__ gx = static_cast<const IT*>(a.x);
@@ -139,15 +138,17 @@ __global__ __launch_bounds__(256) void wgrad_kernel(WgradArgs a) {
     for (int i = 0; i < B_PER; ++i) {
       const int p = k0 + b_prow[i];
       f32x4 v = {0.f, 0.f, 0.f, 0.f};
-      if (XF && b_ok[i] && p < kend) b_vm |= 1u << i;
       if (b_ok[i] && p < kend) {
         if (KS == 1) {
           v = ldv(gx + (long)p * a.ldx + b_ci[i]);
+          if (XF) b_vm |= 1u << i;
         } else {
           const int hi = b_ho[i] * a.stride - a.pad + b_ky[i];
           const int wi = b_wo[i] * a.stride - a.pad + b_kx[i];
-          if ((unsigned)hi < (unsigned)a.H && (unsigned)wi < (unsigned)a.W)
+          if ((unsigned)hi < (unsigned)a.H && (unsigned)wi < (unsigned)a.W) {
             v = ldv(gx + (((long)b_n[i] * a.H + hi) * a.W + wi) * a.ldx + b_ci[i]);
+            if (XF) b_vm |= 1u << i;
+          }
         }
       }
       rb[i] = v;
@@ -288,16 +289,17 @@ __global__ __launch_bounds__(256) void wgrad_kernel(WgradArgs a) {
 template <int BM, int BN, int WM, int WN, bool BF = false, typename IT = float>
 int launch_wgrad(const WgradArgs& a, int ks, int splits, hipStream_t s) {
   dim3 grid(seg_cdiv(a.Cout, BM) * seg_cdiv(a.Nw, BN) * splits);
-  if (a.xs) {  // input transform (1x1 only)
-    if (ks != 1) return (int)hipErrorInvalidValue;
+  if (a.xs) {  // input transform
     const bool v8 = sizeof(IT) == 2 && a.Cout % 8 == 0 && a.Cin % 8 == 0 && a.lddy % 8 == 0 && a.ldx % 8 == 0;
     if constexpr (sizeof(IT) == 2) {
       if (v8) {
-        hipLaunchKernelGGL((wgrad_kernel<BM, BN, WM, WN, 1, true, IT, 8, true>), grid, dim3(256), 0, s, a);
+        if (ks == 1) hipLaunchKernelGGL((wgrad_kernel<BM, BN, WM, WN, 1, true, IT, 8, true>), grid, dim3(256), 0, s, a);
+        else hipLaunchKernelGGL((wgrad_kernel<BM, BN, WM, WN, 3, true, IT, 8, true>), grid, dim3(256), 0, s, a);
         SEG_RET_LAST();
       }
     }
-    hipLaunchKernelGGL((wgrad_kernel<BM, BN, WM, WN, 1, BF, IT, 4, true>), grid, dim3(256), 0, s, a);
+    if (ks == 1) hipLaunchKernelGGL((wgrad_kernel<BM, BN, WM, WN, 1, BF, IT, 4, true>), grid, dim3(256), 0, s, a);
+    else hipLaunchKernelGGL((wgrad_kernel<BM, BN, WM, WN, 3, BF, IT, 4, true>), grid, dim3(256), 0, s, a);
     SEG_RET_LAST();
   }
   if (BF) {
@@ -400,7 +402,7 @@ SEG_API int seg_conv_wgrad_bf16io(const __bf16* dy, long lddy, const __bf16* x, 
                     true, true);
 }
 
-// seg_conv_wgrad(_bf16, _bf16io) of a 1x1 conv whose input X is the raw output of a
+// seg_conv_wgrad(_bf16, _bf16io) of a 1x1 or 3x3 conv whose input X is the raw output of a
 // BatchNorm'd producer: X = act(x * in_scale + in_shift) formed on load (the lazy BN of
 // seg_conv_igemm_xf; the same value the BN-apply pass would have stored).
 SEG_API int seg_conv_wgrad_xf(const float* dy, long lddy, const float* x, long ldx, int N, int H, int W, int Cin,
@@ -430,7 +432,7 @@ static int conv_wgrad(const void* dy, long lddy, const void* x, long ldx, int N,
                       int Wo, int Cout, int ks, int stride, int pad, float* part, int splits,
                       hipStream_t stream, bool bf, bool bf_io, const float* xs, const float* xb, int xact) {
   if ((Cin & 3) || (ldx & 3) || (lddy & 3) || (ks != 1 && ks != 3) || splits < 1) return (int)hipErrorInvalidValue;
-  if (xs && (!xb || ks != 1 || xact < SEG_ACT_NONE || xact > SEG_ACT_RELU6)) return (int)hipErrorInvalidValue;
+  if (xs && (!xb || xact < SEG_ACT_NONE || xact > SEG_ACT_RELU6)) return (int)hipErrorInvalidValue;
   if (ks == 1 && (stride != 1 || pad != 0)) return (int)hipErrorInvalidValue;
   WgradArgs a;
   a.dy = dy; a.lddy = lddy; a.x = x; a.ldx = ldx; a.part = part;

@@ -109,6 +109,8 @@ PROTOTYPES["seg_conv_igemm_bf16io_w16"] = PROTOTYPES["seg_conv_igemm"]
 PROTOTYPES["seg_conv_halo_bf16io_w16"] = PROTOTYPES["seg_conv_halo"]
 PROTOTYPES["seg_conv_igemm_bf16io_xf_w16"] = PROTOTYPES["seg_conv_igemm_bf16io_xf"]
 PROTOTYPES["seg_conv_pw_bf16io"] = PROTOTYPES["seg_conv_pw"]
+for _sfx in ("_xf", "_bf16io_xf", "_bf16io_xf_w16"):  # + in_scale, in_shift, in_act before the stream
+    PROTOTYPES["seg_conv_halo" + _sfx] = (_I, PROTOTYPES["seg_conv_halo"][1][:-1] + [_V, _V, _I, _V])
 
 _lock = threading.Lock()
 _lib = None

@@ -248,10 +248,11 @@ class ConvOp:
             if self.pw_f:  # thin-K 1x1 (its producer's lazy BN, if any, on load)
                 rt.tcall("igemm1_fwd", self.flops(), rt.k("seg_conv_pw"), rt.ptr(i), i.ld, y.M, self.cin_pad, wk_ptr,
                          ldk, bias, rt.ptr(y), y.ld, self.cout, None, 0, statp, *self._in_xform(rt), s)
-            elif self.halo_f:
-                rt.tcall("igemm3_fwd", self.flops(), rt.k("seg_conv_halo") + ("_w16" if self.w16_f else ""), rt.ptr(i),
-                         i.ld, i.N, i.H, i.W, self.cin_pad,
-                            wk_ptr, ldk, bias, rt.ptr(y), y.ld, self.cout, None, 0, statp, s)
+            elif self.halo_f:  # (its producer's lazy BN, if any, on the halo load)
+                name = rt.k("seg_conv_halo") + ("_xf" if self.xform is not None else "") + ("_w16" if self.w16_f else "")
+                rt.tcall("igemm3_fwd", self.flops(), name, rt.ptr(i), i.ld, i.N, i.H, i.W, self.cin_pad,
+                         wk_ptr, ldk, bias, rt.ptr(y), y.ld, self.cout, None, 0, statp,
+                         *(self._in_xform(rt) if self.xform is not None else ()), s)
             elif self.wino_f:
                 work = rt.tmp(16 * (y.M // 4) * self.cout)
                 rt.tcall("wino3_fwd", self.flops(), "seg_conv_wino", rt.ptr(i), i.ld, i.N, i.H, i.W, self.cin_pad,
@@ -262,11 +263,11 @@ class ConvOp:
                 rt.tcall(f"igemm{self.ks}_fwd", self.flops(), "seg_conv_igemm2_bf16io", rt.ptr(i), i.ld, i.N, i.H, i.W,
                          self.cin_pad, wk_ptr, ldk, bias, rt.ptr(y), y.ld, self.cout, self.ks, None, 0, statp,
                          work.data_ptr(), s)
-            elif self.xform is not None:  # 1x1 conv applying its producer's lazy BN on load
+            elif self.xform is not None:  # a conv applying its producer's lazy BN on load
                 name = "seg_conv_igemm_bf16io_xf" if rt.io else "seg_conv_igemm_bf16_xf" if self.bf else "seg_conv_igemm_xf"
                 if rt.io and self.w16_f:
                     name += "_w16"
-                rt.tcall("igemm1_fwd", self.flops(), name, rt.ptr(i), i.ld, i.N, i.H, i.W, self.cin_pad, wk_ptr, ldk,
+                rt.tcall(f"igemm{self.ks}_fwd", self.flops(), name, rt.ptr(i), i.ld, i.N, i.H, i.W, self.cin_pad, wk_ptr, ldk,
                          bias, rt.ptr(y), y.ld, y.H, y.W, self.cout, self.ks, self.stride, self.pad, None, 0, statp,
                          *self._in_xform(rt), s)
             elif rt.io:
@@ -546,15 +547,20 @@ class Program:
         self.ops.append(ConvOp(kind, conv, bn, act, inp, out, y, res, xform))
         return out
 
-    def make_lazy(self, a: Act, pointwise=False):
+    def make_lazy(self, a: Act, pointwise=False, dense3=False):
         """If `a` is the private BN+act output of the last op, drop its buffer and let
         the consumer apply the BN on load; returns the producer op (or None).
         pointwise: the consumer is a 1x1 conv (seg_conv_igemm_xf / seg_conv_wgrad_xf:
-        the uniform-tap loader, 8-channel groups) -- any conv producer; otherwise a
-        depthwise consumer (seg_dw_fwd / seg_dw_wgrad) of a dense producer."""
+        the uniform-tap loader, 8-channel groups) -- any conv producer; dense3: a 3x3
+        stride-1 conv of the bf16io configuration (seg_conv_halo*_xf / seg_conv_igemm_bf16io_xf
+        / seg_conv_wgrad_bf16io_xf, Cin >= 32 for the uniform-tap loader; not igemm2, whose
+        LDS-DMA staging has no transform step); otherwise a depthwise consumer
+        (seg_dw_fwd / seg_dw_wgrad) of a dense producer."""
         op = self.ops[-1] if self.ops else None
         kinds = ("igemm", "dw") if pointwise else ("igemm",)
         if pointwise and not (LAZY_PW and a.C % 8 == 0 and a.C >= 16):
+            return None
+        if dense3 and not (LAZY3 and self.math == "bf16io" and a.C % 8 == 0 and a.C >= 32):
             return None
         if not (isinstance(op, ConvOp) and op.kind in kinds and op.bn is not None and op.res is None
                 and op.out is a and op.y is not a and a.off == 0 and a.ld == r4(a.C)
@@ -783,7 +789,13 @@ def _inverted_residual(prog, blk: InvertedResidual, inp, out=None):
 def _double_conv(prog, dc, inp, out=None):
     c = dc.conv
     x = prog.conv("igemm", c[0], c[1], ACT_RELU, inp)
-    return prog.conv("igemm", c[3], c[4], ACT_RELU, x, out=out)
+    # bf16io: the second conv applies the first one's BN + ReLU on load (no BN-apply pass, no stored activation)
+    k2 = c[3]
+    dense3 = k2.kernel_size == (3, 3) and k2.stride == (1, 1) and k2.padding == (1, 1) and k2.groups == 1
+    xf = prog.make_lazy(x, dense3=True) if dense3 else None
+    if xf is not None:
+        x = xf.out
+    return prog.conv("igemm", k2, c[4], ACT_RELU, x, out=out, xform=xf)
 
 
 def _up(prog, u, low, cat):
@@ -804,12 +816,12 @@ def _outconv(prog, oc, inp):
     return prog.conv("igemm", c[3], None, ACT_NONE, x, xform=xf)
 
 
-def build_mobilenet_unet(model, N, H, W) -> Program:
+def build_mobilenet_unet(model, N, H, W, math="f32") -> Program:
     """Program for MobileNetV2UNet.forward (src/unet.py:32-51)."""
     if H % 32 or W % 32:
         raise ValueError(f"MobileNetV2UNet needs H, W divisible by 32 (got {H}x{W}); the reference fails "
                          "with a torch.cat size mismatch on such inputs")
-    p = Program(N, H, W)
+    p = Program(N, H, W, math)
     ups = [model.up1, model.up2, model.up3, model.up4]
     skip_c = [u.conv.conv[0].in_channels for u in ups]  # concat widths
     # concat buffers, finest first: cat4 @ H/2 (up4), cat3 @ H/4, cat2 @ H/8, cat1 @ H/16
@@ -843,11 +855,11 @@ def build_mobilenet_unet(model, N, H, W) -> Program:
     return p
 
 
-def build_unet(model, N, H, W) -> Program:
+def build_unet(model, N, H, W, math="f32") -> Program:
     """Program for UNet / LightUNet.forward (src/unet.py:137-147, :160-171)."""
     if H % 8 or W % 8:
         raise ValueError(f"UNet needs H, W divisible by 8 (got {H}x{W})")
-    p = Program(N, H, W)
+    p = Program(N, H, W, math)
     b = model.inc.conv.conv[0].out_channels
     cat3 = p.new(model.up3.conv.conv[0].in_channels, H, W, name="cat3")          # [x1 | up(u2)]
     cat2 = p.new(model.up2.conv.conv[0].in_channels, H // 2, W // 2, name="cat2")  # [x2 | up(u1)]
@@ -876,14 +888,11 @@ def build_unet(model, N, H, W) -> Program:
 def build_program(model, N, H, W, math="f32") -> Program:
     from .unet import MobileNetV2UNet, UNet, LightUNet
     if isinstance(model, MobileNetV2UNet):
-        prog = build_mobilenet_unet(model, N, H, W)
+        prog = build_mobilenet_unet(model, N, H, W, math)
     elif isinstance(model, (UNet, LightUNet)):
-        prog = build_unet(model, N, H, W)
+        prog = build_unet(model, N, H, W, math)
     else:
         raise TypeError(f"no HIP program for {type(model).__name__}")
-    if math not in MATHS:
-        raise ValueError(f"conv math must be one of {MATHS}, got {math!r}")
-    prog.math = math
     return prog
 
 
@@ -1203,6 +1212,11 @@ IGEMM2_MAX_ROWS = int(os.environ.get("SEG_IGEMM2_MAX_ROWS", "65536"))
 W16 = os.environ.get("SEG_W16", "1") == "1"
 # fork the weight-gradient side stream after the layer's data gradient (measured: f32 +1.5 %, bf16io +-0)
 FORK_LATE = os.environ.get("SEG_FORK_LATE", "1") == "1"
+# lazy BatchNorm for the 3x3 consumers of the bf16io configuration (double_conv's second conv), read at
+# program build.  Off by default: measured on UNet 512x1024 bf16io it removes a 220 us BN-apply pass per
+# full-size layer but the weight gradient transforms every input element once per tap (+330 us per full-size
+# layer), step 333 vs 343-345 img/s; MobileNetV2UNet flat (profiles/r03o/).  SEG_LAZY3=1 turns it on.
+LAZY3 = os.environ.get("SEG_LAZY3", "0") == "1"
 _SIDE = {}
 
 

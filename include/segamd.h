@@ -245,6 +245,14 @@ int seg_bn_stats_tiles(const float* part, int ntiles, int tile_rows, long M, int
                        const float* beta, float eps, float momentum, float* running_mean, float* running_var,
                        long long* num_batches_tracked, float* mean, float* invstd, float* scale, float* shift,
                        hipStream_t stream);
+/* seg_bn_stats_tiles for many-tile layers: with ntiles > 1024, 16 consecutive tiles are merged per row
+ * first (coalesced, into `work`: seg_bn_stats_tiles_work_floats(ntiles, C) floats, 0 below the
+ * threshold) and the merged rows are finalized -- the same fp64 fixed-order statistics, regrouped. */
+long seg_bn_stats_tiles_work_floats(int ntiles, int C);
+int seg_bn_stats_tiles_ws(const float* part, int ntiles, int tile_rows, long M, int C, const float* gamma,
+                          const float* beta, float eps, float momentum, float* running_mean, float* running_var,
+                          long long* num_batches_tracked, float* mean, float* invstd, float* scale, float* shift,
+                          float* work, hipStream_t stream);
 int seg_bn_eval_coef(const float* gamma, const float* beta, const float* running_mean,
                      const float* running_var, float eps, int C, float* scale, float* shift,
                      hipStream_t stream);

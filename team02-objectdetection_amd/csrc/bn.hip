@@ -379,6 +379,44 @@ __global__ __launch_bounds__(256) void bn_finalize_tiles_wave_kernel(
                  scale_out, shift_out);
 }
 
+// Many tiles: R consecutive row tiles merged into one super-tile first (same format: sum and M2 about the
+// super-tile's own mean, R * tile_rows rows, the last one short), so the per-channel finalize above reads
+// ntiles / R rows instead of ntiles.  One thread per (super-tile, channel), consecutive threads on consecutive
+// channels: a wave reads whole partial rows (coalesced), where the per-channel finalize's lanes each touch a
+// different cache line.  fp64 inside, fixed order (deterministic).
+constexpr int kTileMerge = 16;
+constexpr int kTileMergeMin = 1024;  // ntiles above which the merge stage runs
+
+__global__ __launch_bounds__(256) void bn_tiles_merge_kernel(const float* __restrict__ part, int ntiles, int tile_rows,
+                                                             long M, int C, float* __restrict__ out) {
+  const long gid = blockIdx.x * 256L + threadIdx.x;
+  const int ns = (ntiles + kTileMerge - 1) / kTileMerge;
+  if (gid >= (long)ns * C) return;
+  const int j = (int)(gid / C), c = (int)(gid - (long)j * C);
+  const int t0 = j * kTileMerge;
+  float fs[kTileMerge], fq[kTileMerge];
+#pragma unroll
+  for (int k = 0; k < kTileMerge; ++k) {
+    const long i = min(t0 + k, ntiles - 1);
+    fs[k] = part[i * 2 * C + c];
+    fq[k] = part[i * 2 * C + C + c];
+  }
+  double S = 0.0;
+#pragma unroll
+  for (int k = 0; k < kTileMerge; ++k) S += t0 + k < ntiles ? (double)fs[k] : 0.0;
+  const double n = (double)std::min<long>((long)kTileMerge * tile_rows, M - (long)t0 * tile_rows);
+  const double mu = S / n;
+  double Q = 0.0;
+#pragma unroll
+  for (int k = 0; k < kTileMerge; ++k) {
+    const double nt = tile_rows_of(t0 + k, tile_rows, M);
+    const double d = fs[k] / nt - mu;
+    Q += t0 + k < ntiles ? (double)fq[k] + nt * d * d : 0.0;
+  }
+  out[(long)j * 2 * C + c] = (float)S;
+  out[(long)j * 2 * C + C + c] = (float)Q;
+}
+
 __global__ void bn_eval_coef_kernel(const float* gamma, const float* beta, const float* rm, const float* rv, float eps,
                                     int C, float* scale_out, float* shift_out) {
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
@@ -720,6 +758,38 @@ SEG_API int seg_bn_stats_bf16io(const __bf16* y, long ldy, long M, int C, const 
 // Train-mode BN statistics from seg_conv_igemm's epilogue partials (`stat`
 // workspace of seg_conv_igemm_row_tiles(M, C) x 2 x C floats); same outputs and
 // running-buffer update as seg_bn_stats, without re-reading the conv output.
+SEG_API int seg_bn_stats_tiles(const float* part, int ntiles, int tile_rows, long M, int C, const float* gamma,
+                               const float* beta, float eps, float momentum, float* running_mean, float* running_var,
+                               long long* num_batches_tracked, float* mean, float* invstd, float* scale, float* shift,
+                               hipStream_t stream);
+
+// Workspace floats of seg_bn_stats_tiles_ws (0: no merge stage at this tile count).
+SEG_API long seg_bn_stats_tiles_work_floats(int ntiles, int C) {
+  return ntiles > kTileMergeMin ? (long)seg_cdiv(ntiles, kTileMerge) * 2 * C : 0;
+}
+
+// seg_bn_stats_tiles with a workspace of seg_bn_stats_tiles_work_floats(ntiles, C) floats: many-tile
+// layers merge kTileMerge tiles per row first (one more launch, coalesced) and finalize the merged rows.
+SEG_API int seg_bn_stats_tiles_ws(const float* part, int ntiles, int tile_rows, long M, int C, const float* gamma,
+                                  const float* beta, float eps, float momentum, float* running_mean, float* running_var,
+                                  long long* num_batches_tracked, float* mean, float* invstd, float* scale,
+                                  float* shift, float* work, hipStream_t stream) {
+  if (ntiles < 1 || tile_rows < 1 || M < 1) return (int)hipErrorInvalidValue;
+  if (ntiles > kTileMergeMin) {
+    if (!work) return (int)hipErrorInvalidValue;
+    const long n = (long)seg_cdiv(ntiles, kTileMerge) * C;
+    hipLaunchKernelGGL(bn_tiles_merge_kernel, dim3(seg_cdiv(n, 256)), dim3(256), 0, stream, part, ntiles, tile_rows, M,
+                       C, work);
+    const int rc = (int)hipGetLastError();
+    if (rc) return rc;
+    part = work;
+    tile_rows *= kTileMerge;
+    ntiles = seg_cdiv(ntiles, kTileMerge);
+  }
+  return seg_bn_stats_tiles(part, ntiles, tile_rows, M, C, gamma, beta, eps, momentum, running_mean, running_var,
+                            num_batches_tracked, mean, invstd, scale, shift, stream);
+}
+
 SEG_API int seg_bn_stats_tiles(const float* part, int ntiles, int tile_rows, long M, int C, const float* gamma,
                                const float* beta, float eps, float momentum, float* running_mean, float* running_var,
                                long long* num_batches_tracked, float* mean, float* invstd, float* scale, float* shift,

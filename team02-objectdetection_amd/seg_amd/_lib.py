@@ -57,6 +57,8 @@ PROTOTYPES = {
     "seg_chan_workspace_floats": (_L, [_L, _I]),
     "seg_bn_stats": (_I, [_V, _L, _L, _I, _V, _V, _F, _F, _V, _V, _V, _V, _V, _V, _V, _V, _V]),
     "seg_bn_stats_tiles": (_I, [_V, _I, _I, _L, _I, _V, _V, _F, _F, _V, _V, _V, _V, _V, _V, _V, _V]),
+    "seg_bn_stats_tiles_ws": (_I, [_V, _I, _I, _L, _I, _V, _V, _F, _F, _V, _V, _V, _V, _V, _V, _V, _V, _V]),
+    "seg_bn_stats_tiles_work_floats": (_L, [_I, _I]),
     "seg_bn_eval_coef": (_I, [_V, _V, _V, _V, _F, _I, _V, _V, _V]),
     "seg_bn_apply": (_I, [_V, _L, _L, _I, _V, _V, _I, _V, _L, _V, _L, _V]),
     "seg_bn_backward": (_I, [_V, _L, _V, _L, _L, _I, _V, _V, _V, _V, _V, _I, _V, _V, _V, _V, _L, _V]),

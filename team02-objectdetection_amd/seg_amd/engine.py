@@ -300,9 +300,12 @@ class ConvOp:
                      bn.momentum, rm, rv, nbt, work.data_ptr(), mean, invstd,
                      scale, shift, s)
             else:
-                rt.call("seg_bn_stats_tiles", stat.data_ptr(), ntiles, tile_rows, M, C, bn.weight.data_ptr(),
-                     bn.bias.data_ptr(), bn.eps, bn.momentum, rm, rv, nbt, mean, invstd,
-                     scale, shift, s)
+                # many-tile layers: 16 tiles merged per row before the per-channel finalize (SEG_BN_MERGE=0: direct)
+                nw = query("seg_bn_stats_tiles_work_floats", ntiles, C) if BN_MERGE else 0
+                ws = (rt.tmp(nw).data_ptr(),) if nw else ()
+                rt.call("seg_bn_stats_tiles_ws" if nw else "seg_bn_stats_tiles", stat.data_ptr(), ntiles, tile_rows, M,
+                        C, bn.weight.data_ptr(), bn.bias.data_ptr(), bn.eps, bn.momentum, rm, rv, nbt, mean, invstd,
+                        scale, shift, *ws, s)
         else:
             rt.call("seg_bn_eval_coef", bn.weight.data_ptr(), bn.bias.data_ptr(), bn.running_mean.data_ptr(),
                  bn.running_var.data_ptr(), bn.eps, C, scale, shift, s)
@@ -1217,6 +1220,7 @@ FORK_LATE = os.environ.get("SEG_FORK_LATE", "1") == "1"
 # full-size layer but the weight gradient transforms every input element once per tap (+330 us per full-size
 # layer), step 333 vs 343-345 img/s; MobileNetV2UNet flat (profiles/r03o/).  SEG_LAZY3=1 turns it on.
 LAZY3 = os.environ.get("SEG_LAZY3", "0") == "1"
+BN_MERGE = os.environ.get("SEG_BN_MERGE", "1") == "1"
 _SIDE = {}
 
 

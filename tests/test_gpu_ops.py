@@ -663,3 +663,40 @@ def test_reduction_finalize_repeatable_under_load(M, C):
     z = (y64 - y64.mean(0)) * (1 / torch.sqrt(y64.var(0, unbiased=False) + 1e-5))
     dz = d64 * (z > 0)
     assert rel(db, dz.sum(0)) < 1e-5 and rel(dg, (dz * z).sum(0)) < 1e-5
+
+
+@pytest.mark.parametrize("M,tile_rows,C", [(1025 * 256, 256, 64), (4096 * 128 + 77, 128, 24), (20000 * 256 - 5, 256, 8),
+                                           (1000 * 256, 256, 32)])
+def test_bn_stats_tiles_merged(M, tile_rows, C):
+    """seg_bn_stats_tiles_ws (many-tile layers: 16 tiles merged per row, then the per-channel finalize)
+    against fp64 torch statistics of the same rows, and against the direct finalize; a short last tile
+    and a short last super-tile included."""
+    g = torch.Generator().manual_seed(M % 1000)
+    y = (torch.randn(M, C, generator=g, dtype=torch.float64) * torch.linspace(0.5, 3, C, dtype=torch.float64)
+         + torch.linspace(-2, 5, C, dtype=torch.float64))
+    nt = (M + tile_rows - 1) // tile_rows
+    pad = nt * tile_rows - M
+    yt = torch.cat([y, torch.full((pad, C), float("nan"), dtype=torch.float64)]).view(nt, tile_rows, C)
+    n = torch.full((nt, 1), float(tile_rows), dtype=torch.float64)
+    n[-1] = tile_rows - pad
+    valid = ~torch.isnan(yt)
+    s = torch.where(valid, yt, 0.0).sum(1)
+    m2 = torch.where(valid, (yt - (s / n)[:, None, :]) ** 2, 0.0).sum(1)
+    part = torch.stack([s, m2], 1).float().to(DEV).contiguous()  # [nt][2][C]
+    nw = query("seg_bn_stats_tiles_work_floats", nt, C)
+    assert (nw > 0) == (nt > 1024)
+    work = torch.empty(max(nw, 1), device=DEV)
+    res = {}
+    for name, extra in (("seg_bn_stats_tiles", ()), ("seg_bn_stats_tiles_ws", (work.data_ptr() if nw else None,))):
+        st = torch.empty(4 * C, device=DEV)
+        rm, rv = torch.zeros(C, device=DEV), torch.ones(C, device=DEV)
+        call(name, part.data_ptr(), nt, tile_rows, M, C, None, None, 1e-5, 0.1, rm.data_ptr(), rv.data_ptr(), None,
+             st[:C].data_ptr(), st[C:2 * C].data_ptr(), st[2 * C:3 * C].data_ptr(), st[3 * C:].data_ptr(), *extra, S())
+        res[name] = (st.double().cpu(), rm.double().cpu(), rv.double().cpu())
+    mean, var = y.mean(0), y.var(0, unbiased=False)
+    for name, (st, rm, rv) in res.items():
+        assert rel(st[:C], mean) < 1e-6, name
+        assert rel(st[C:2 * C], 1 / torch.sqrt(var + 1e-5)) < 1e-6, name
+        assert rel(rv, 0.9 + 0.1 * y.var(0, unbiased=True)) < 1e-6, name
+    a, b = res["seg_bn_stats_tiles"][0], res["seg_bn_stats_tiles_ws"][0]
+    assert rel(a, b) < 1e-6

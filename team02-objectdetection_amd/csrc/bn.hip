@@ -385,7 +385,10 @@ __global__ __launch_bounds__(256) void bn_finalize_tiles_wave_kernel(
 // channels: a wave reads whole partial rows (coalesced), where the per-channel finalize's lanes each touch a
 // different cache line.  fp64 inside, fixed order (deterministic).
 constexpr int kTileMerge = 16;
-constexpr int kTileMergeMin = 1024;  // ntiles above which the merge stage runs
+#ifndef SEG_TILE_MERGE_MIN
+#define SEG_TILE_MERGE_MIN 1024
+#endif
+constexpr int kTileMergeMin = SEG_TILE_MERGE_MIN;  // ntiles above which the merge stage runs
 
 __global__ __launch_bounds__(256) void bn_tiles_merge_kernel(const float* __restrict__ part, int ntiles, int tile_rows,
                                                              long M, int C, float* __restrict__ out) {

@@ -158,9 +158,10 @@ int seg_conv_wgrad_reduce(const float* part, int splits, float* dw, int Cout, in
  * (src/unet.py:58,61) where the transforms are cheap; forward (U from
  * seg_pack_batch mode 3) and data gradient (mode 4).  out = conv + bias + add;
  * `work` >= 16 * N*(H/2)*(W/2) * Cout floats; `stat` (optional): BatchNorm
- * partials in seg_conv_igemm's layout with seg_conv_wino_row_tiles tiles of 256
- * rows.  seg_conv_wino_pick: 1 when the cost model prefers it to seg_conv_igemm. */
+ * partials in seg_conv_igemm's layout with seg_conv_wino_row_tiles tiles of
+ * seg_conv_wino_tile_rows() rows.  seg_conv_wino_pick: 1 when the cost model prefers it to seg_conv_igemm. */
 int seg_conv_wino_pick(int N, int H, int W, int Cin, int Cout);
+int seg_conv_wino_tile_rows(void);  /* pixels per BN row tile of seg_conv_wino */
 int seg_conv_wino_row_tiles(int N, int H, int W);
 int seg_conv_wino(const float* in, long ldin, int N, int H, int W, int Cin, const float* wk, int ldk,
                   const float* bias, float* out, long ldout, int Cout, const float* add, long ldadd,

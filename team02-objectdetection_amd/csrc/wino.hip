@@ -19,14 +19,23 @@
 // loader forms it from 4 float4 loads -- V is never written to HBM.  M goes
 // through HBM (16 x tiles x Cout floats); the output kernel fuses the BN
 // statistics epilogue of seg_conv_igemm (same [row tile][2][Cout] partials,
-// 256-pixel row tiles) so seg_bn_stats_tiles finalizes either.
+// seg_conv_wino_tile_rows()-pixel row tiles) so seg_bn_stats_tiles finalizes either.
 //
 // The data gradient of a stride-1 3x3 conv is the same convolution of dY with
 // the transposed, flipped weights (pack mode 4), so it runs on the same kernels.
 #include "common.h"
 
+#ifndef SEG_WINO_OUT_CSPLIT
+#define SEG_WINO_OUT_CSPLIT 1  // output transform: one block per (64 tiles, 64 channels); 0 = channels walked in-block
+#endif
+
+#ifndef SEG_WINO_OUT_QT
+#define SEG_WINO_OUT_QT 4  // output transform: tiles per tile lane (16 * QT tiles = 64 * QT pixels per BN row tile)
+#endif
+
 namespace {
 
+constexpr int kWinoQT = SEG_WINO_OUT_QT;
 __device__ __attribute__((aligned(16))) float g_wzero4[4];
 
 struct WinoArgs {
@@ -191,12 +200,12 @@ __global__ __launch_bounds__(NT) void wino_gemm_kernel(WinoArgs a) {
 }
 
 // Y = A^T M A per tile and float4 channel group (+ bias, + addend), NHWC out; with
-// `stat`, the BatchNorm partials of each 64-tile (256-pixel) block: per channel the
+// `stat`, the BatchNorm partials of each 16*QT-tile (64*QT-pixel) block: per channel the
 // block sum and the sum of squared deviations from the block mean, exactly the
-// [row tile][2][Cout] layout of seg_conv_igemm's epilogue (tile_rows = 256).
+// [row tile][2][Cout] layout of seg_conv_igemm's epilogue (tile_rows = seg_conv_wino_tile_rows()).
 // Block = 256 threads = 16 tile lanes x 16 channel-group lanes (256 contiguous
-// bytes of an M row per load); each tile lane owns 4 tiles (tl + 16 q); channels
-// are walked 64 at a time.
+// bytes of an M row per load); each tile lane owns QT tiles (tl + 16 q); blockIdx.y
+// picks the block's 64 channels (the deep layers have only T / 64 = 16..256 tile blocks).
 __global__ __launch_bounds__(256) void wino_out_kernel(const float* __restrict__ m, int T, int Cout, int N, int H,
                                                        int W, int th, int tw, const float* __restrict__ bias,
                                                        const float* __restrict__ add, long ldadd,
@@ -204,12 +213,13 @@ __global__ __launch_bounds__(256) void wino_out_kernel(const float* __restrict__
   __shared__ f32x4 red[4][16];  // [wave][cg lane]
   __shared__ f32x4 bmean[16];
   const int t = threadIdx.x, tl = t >> 4, cl = t & 15, wave = t >> 6;
-  long pix[4][4];
-  bool tok[4];
-  int tile[4];
+  constexpr int QT = kWinoQT, TPB = 16 * QT;
+  long pix[QT][4];
+  bool tok[QT];
+  int tile[QT];
 #pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    tile[q] = blockIdx.x * 64 + tl + 16 * q;
+  for (int q = 0; q < QT; ++q) {
+    tile[q] = blockIdx.x * TPB + tl + 16 * q;
     tok[q] = tile[q] < T;
     const int tt = tok[q] ? tile[q] : 0;
     const int n = tt / (th * tw), r = tt - n * th * tw;
@@ -219,16 +229,21 @@ __global__ __launch_bounds__(256) void wino_out_kernel(const float* __restrict__
 #pragma unroll
       for (int v = 0; v < 2; ++v) pix[q][u * 2 + v] = ((long)n * H + 2 * ty + u) * W + 2 * tx + v;
   }
-  const int ntile = min(64, T - (int)blockIdx.x * 64);
+  const int ntile = min(TPB, T - (int)blockIdx.x * TPB);
   const float cnt = 4.f * (float)ntile;
   const long TC = (long)T * Cout;
+#if SEG_WINO_OUT_CSPLIT
+  {
+    const int cgb = blockIdx.y * 64;
+#else
   for (int cgb = 0; cgb < Cout; cgb += 64) {
+#endif
     const int c = cgb + cl * 4;
     const bool cok = c < Cout;
     const f32x4 b = (bias && cok) ? ld4(bias + c) : f32x4{0.f, 0.f, 0.f, 0.f};
-    f32x4 y[4][4];
+    f32x4 y[QT][4];
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
+    for (int q = 0; q < QT; ++q) {
       if (tok[q] && cok) {
         f32x4 qv[16];
 #pragma unroll
@@ -254,14 +269,18 @@ __global__ __launch_bounds__(256) void wino_out_kernel(const float* __restrict__
         for (int p = 0; p < 4; ++p) y[q][p] = f32x4{0.f, 0.f, 0.f, 0.f};
       }
     }
+#if SEG_WINO_OUT_CSPLIT
+    if (!stat) return;
+#else
     if (!stat) continue;
+#endif
     // pass 1: block sum -> mean; pass 2: sum of squared deviations about it
 #pragma unroll
     for (int pass = 0; pass < 2; ++pass) {
       f32x4 s = {0.f, 0.f, 0.f, 0.f};
       const f32x4 mu = pass ? bmean[cl] : f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int q = 0; q < 4; ++q)
+      for (int q = 0; q < QT; ++q)
         if (tok[q] && cok) {
 #pragma unroll
           for (int p = 0; p < 4; ++p) {
@@ -512,16 +531,19 @@ SEG_API int seg_conv_wino_pick(int N, int H, int W, int Cin, int Cout) {
   return (Cin >= 128 && Cout >= 128 && Cout <= 2 * Cin) ? 1 : 0;
 }
 
-// Number of 256-pixel row tiles of seg_conv_wino's BN partials.
+// Number of row tiles of seg_conv_wino's BN partials.
 SEG_API int seg_conv_wino_row_tiles(int N, int H, int W) {
   const long T = (long)N * (H / 2) * (W / 2);
-  return (int)((T + 63) / 64);
+  return (int)((T + 16 * kWinoQT - 1) / (16 * kWinoQT));
 }
+
+// Pixels per BN row tile of seg_conv_wino (the tile_rows of seg_bn_stats_tiles).
+SEG_API int seg_conv_wino_tile_rows(void) { return 64 * kWinoQT; }
 
 // out = conv3x3(in, w) (+bias) (+add), stride 1, pad 1, by Winograd F(2x2,3x3).
 // wk: U from seg_pack_batch mode 3 (forward) / 4 (data gradient): [16][Cout][ldk],
 // ldk >= Cin.  work >= 16 * N*(H/2)*(W/2) * Cout floats.  stat (optional): BN
-// partials [seg_conv_wino_row_tiles][2][Cout] with tile_rows = 256.
+// partials [seg_conv_wino_row_tiles][2][Cout] with tile_rows = seg_conv_wino_tile_rows().
 SEG_API int seg_conv_wino(const float* in, long ldin, int N, int H, int W, int Cin, const float* wk, int ldk,
                           const float* bias, float* out, long ldout, int Cout, const float* add, long ldadd,
                           float* stat, float* work, hipStream_t stream) {
@@ -538,7 +560,7 @@ SEG_API int seg_conv_wino(const float* in, long ldin, int N, int H, int W, int C
   if (Cout >= SEG_WINO_WIDE && seg_cdiv(Cout, 256) * 2 == seg_cdiv(Cout, 128)) launch_wino<128, 256, 64, 64, 512>(a, stream);
   else if (Cout >= 128) launch_wino<128, 128, 64, 64>(a, stream);
   else launch_wino<128, 64, 64, 32>(a, stream);
-  hipLaunchKernelGGL(wino_out_kernel, dim3(seg_cdiv(a.T, 64)), dim3(256), 0, stream, work, a.T, Cout, N, H, W, a.th,
+  hipLaunchKernelGGL(wino_out_kernel, dim3(seg_cdiv(a.T, 16 * kWinoQT), SEG_WINO_OUT_CSPLIT ? seg_cdiv(Cout, 64) : 1), dim3(256), 0, stream, work, a.T, Cout, N, H, W, a.th,
                      a.tw, bias, add, ldadd, out, ldout, stat);
   SEG_RET_LAST();
 }

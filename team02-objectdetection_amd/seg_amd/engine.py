@@ -33,7 +33,7 @@ from ._lib import call, query as _query
 # Host-only size / plan queries of the C ABI are pure functions of their integer
 # arguments: memoised, so a training step does not pay a ctypes call for each of them.
 _PURE_QUERIES = {"seg_chan_workspace_floats", "seg_conv_wgrad_splits", "seg_conv_wgrad_splits_bf16", "seg_dw_wgrad_blocks",
-                 "seg_conv_igemm_splits", "seg_ce_workspace_floats", "seg_conv_wino_row_tiles",
+                 "seg_conv_igemm_splits", "seg_ce_workspace_floats", "seg_conv_wino_row_tiles", "seg_conv_wino_tile_rows",
                  "seg_conv_halo_row_tiles", "seg_conv_wino_wgrad_splits"}
 _QCACHE = {}
 
@@ -238,7 +238,8 @@ class ConvOp:
                 elif self.ig2_f is not None:
                     tile_rows, ntiles = self.ig2_f[0], self.ig2_f[1]
                 elif self.wino_f:
-                    ntiles, tile_rows = query("seg_conv_wino_row_tiles", y.N, y.H, y.W), 256
+                    ntiles = query("seg_conv_wino_row_tiles", y.N, y.H, y.W)
+                    tile_rows = query("seg_conv_wino_tile_rows")
                 elif self.halo_f:
                     ntiles, tile_rows = query("seg_conv_halo_row_tiles", y.N, y.H, y.W), 256
                 else:

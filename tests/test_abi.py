@@ -25,7 +25,7 @@ def header_decls():
     for m in re.finditer(r"\b(int|long)\s+(seg_\w+)\s*\(([^)]*)\)\s*;", text):
         ret, name, params = m.group(1), m.group(2), m.group(3)
         types = []
-        for prm in params.split(","):
+        for prm in ([] if params.strip() in ("", "void") else params.split(",")):
             prm = " ".join(prm.split())
             t = re.sub(r"\s*\b\w+$", "", prm).replace(" *", "*")
             types.append(t)

@@ -494,9 +494,9 @@ def test_conv_wino_fwd_stats_dgrad(N, Cin, Cout, H, W):
     assert rel(from_nhwc(out, N, Cout, H, W), y.detach()) < 1e-5
     st = torch.empty(4 * Cout, device=DEV)
     rm, rv = torch.zeros(Cout, device=DEV), torch.ones(Cout, device=DEV)
-    call("seg_bn_stats_tiles", stat.data_ptr(), nt, 256, N * H * W, Cout, None, None, 1e-5, 0.1, rm.data_ptr(),
-         rv.data_ptr(), None, st[:Cout].data_ptr(), st[Cout:2 * Cout].data_ptr(), st[2 * Cout:3 * Cout].data_ptr(),
-         st[3 * Cout:].data_ptr(), S())
+    call("seg_bn_stats_tiles", stat.data_ptr(), nt, query("seg_conv_wino_tile_rows"), N * H * W, Cout, None, None,
+         1e-5, 0.1, rm.data_ptr(), rv.data_ptr(), None, st[:Cout].data_ptr(), st[Cout:2 * Cout].data_ptr(),
+         st[2 * Cout:3 * Cout].data_ptr(), st[3 * Cout:].data_ptr(), S())
     y64 = y.detach().double()
     assert rel(st[:Cout], y64.mean((0, 2, 3))) < 1e-5
     assert rel(st[Cout:2 * Cout], 1 / torch.sqrt(y64.var((0, 2, 3), unbiased=False) + 1e-5)) < 1e-5

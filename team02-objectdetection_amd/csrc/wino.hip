@@ -314,6 +314,9 @@ void launch_wino(const WinoArgs& a, hipStream_t s) {
   dim3 grid(seg_cdiv(a.T, BM) * seg_cdiv(a.Cout, BN), 1, 16);
   hipLaunchKernelGGL((wino_gemm_kernel<BM, BN, WM, WN, 32, NT>), grid, dim3(NT), 0, s, a);
 }
+#ifndef SEG_WINO_WIDE_MINBLK
+#define SEG_WINO_WIDE_MINBLK 0  // ... and only when it still launches this many blocks
+#endif
 #ifndef SEG_WINO_WIDE
 #define SEG_WINO_WIDE 256  // Cout from which the 8-wave 128 x 256 tile is used
 #endif
@@ -557,7 +560,9 @@ SEG_API int seg_conv_wino(const float* in, long ldin, int N, int H, int W, int C
   if (a.T == 0) return 0;
   // the wide tile where it pads no more columns than two narrow ones (measured: Cout 256 -5..-6 %,
   // Cout 1344 (6 x 256 = 1536 vs 11 x 128 = 1408 columns) +4 % per launch)
-  if (Cout >= SEG_WINO_WIDE && seg_cdiv(Cout, 256) * 2 == seg_cdiv(Cout, 128)) launch_wino<128, 256, 64, 64, 512>(a, stream);
+  if (Cout >= SEG_WINO_WIDE && seg_cdiv(Cout, 256) * 2 == seg_cdiv(Cout, 128) &&
+      (long)seg_cdiv(a.T, 128) * seg_cdiv(Cout, 256) * 16 >= SEG_WINO_WIDE_MINBLK)
+    launch_wino<128, 256, 64, 64, 512>(a, stream);
   else if (Cout >= 128) launch_wino<128, 128, 64, 64>(a, stream);
   else launch_wino<128, 64, 64, 32>(a, stream);
   hipLaunchKernelGGL(wino_out_kernel, dim3(seg_cdiv(a.T, 16 * kWinoQT), SEG_WINO_OUT_CSPLIT ? seg_cdiv(Cout, 64) : 1), dim3(256), 0, stream, work, a.T, Cout, N, H, W, a.th,

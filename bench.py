@@ -25,6 +25,9 @@ Also reported:
                    ms_per_step, HBM roofline and step roofline (--no-bf16io-block).
   infer         -- (default run, N = 1) BASELINE configs[3]: inference.py's per-frame
                    path as one hipGraph replay, fp16, 500 timed frames (--no-infer-block).
+  unet_cfg5     -- (default run) BASELINE configs[4]: UNet 10-class 512x1024 bs=8/GPU, bf16io
+                   and f32, each with its own warm-up, timed region, roofline and step
+                   roofline (--no-unet-block).
 """
 from __future__ import annotations
 
@@ -64,6 +67,9 @@ def parse():
     ap.add_argument("--no-bf16io-block", action="store_true",
                     help="skip the nested \"bf16io\" measurement (configs[2] math on the same workload) that follows "
                          "the f32 headline")
+    ap.add_argument("--no-unet-block", action="store_true",
+                    help="skip the nested \"unet_cfg5\" measurement (BASELINE configs[4]: UNet 10-class 512x1024 "
+                         "bs=8/GPU, bf16io and f32) of the default line")
     ap.add_argument("--workload", choices=("train", "infer"), default="train",
                     help="train: BASELINE configs[1] (the headline); infer: configs[3], inference.py's per-frame path")
     ap.add_argument("--frames", type=int, default=500, help="timed frames of --workload infer")
@@ -254,10 +260,25 @@ def main():
 
     head = train_workload(args, args.math, dev, world, rank, dist)
     nested = None
-    if args.math == "f32" and args.model == "MobileNetV2UNet" and not args.no_bf16io_block:
+    default_line = args.math == "f32" and args.model == "MobileNetV2UNet"
+    if default_line and not args.no_bf16io_block:
         # BASELINE configs[2]'s arithmetic on the same workload (the north-star HBM target):
         # its own model, warm-up and timed region after the headline's
         nested = train_workload(args, "bf16io", dev, world, rank, dist)
+    unet = None
+    if default_line and not args.no_unet_block:
+        # BASELINE configs[4]: UNet 10-class, 512x1024, bs=8/GPU -- bf16 (bf16io storage) as the config
+        # names it, and f32 beside it; each its own model, warm-up and timed region
+        ua = argparse.Namespace(**vars(args))
+        ua.model, ua.batch, ua.height, ua.width = "UNet", 8, 512, 1024
+        ua.steps, ua.warmup = min(args.steps, 10), max(min(args.warmup, 3), 2)
+        unet = {}
+        for m in ("bf16io", "f32"):
+            r = train_workload(ua, m, dev, world, rank, dist)
+            unet[m] = {"value": r["value"], "unit": "images/s", "ms_per_step": r["ms_per_step"],
+                       "steps": ua.steps, "warmup": ua.warmup, "final_loss": r["final_loss"],
+                       "math": MATH_NOTE[m], "roofline": r["roofline"], "step_roofline": r["step_roofline"],
+                       **({"multi_gpu": r["multi_gpu"]} if r["multi_gpu"] is not None else {})}
 
     if rank == 0:
         cpu = None
@@ -282,6 +303,11 @@ def main():
             line["bf16io"] = {"workload": f"same model, shape and step as the headline with bf16io math "
                                           f"({_cfg_name(args, 'bf16io')})", "dtype": "bf16io",
                               "math": MATH_NOTE["bf16io"], **nested}
+        if unet is not None:
+            line["unet_cfg5"] = {"workload": "BASELINE configs[4]: UNet 10-class fwd+bwd+Adam, 512x1024, "
+                                             f"bs=8/GPU, dp{world} (bf16 = bf16io math; f32 beside it)",
+                                 "model": "UNet", "global_batch": 8 * world, "image": [512, 1024],
+                                 "scaling": "weak", **unet}
         if world == 1 and args.model == "MobileNetV2UNet" and not args.no_infer_block:
             # BASELINE configs[3] on the same GPU after the training lines (its own timed loop)
             r = infer_measure(args, "f16", 500, cpu_baseline=False)
@@ -465,14 +491,21 @@ def _roofline(args, math, model, core, engine, timer, conv3, step, dt, peak):
     af, as_, an = family(rec_all, {k for k, _, _ in rec_all if k.startswith(("igemm", "wino", "halo"))})
     rec_iso = extra_pass(False)
     ifl, isec, inn = family(rec_iso, conv3)
-    if math == "f32":  # compute-bound config: FLOPs against the f32 MFMA peak
+    # the family is graded against the resource its own arithmetic intensity makes binding:
+    # roofline time = max(bytes / HBM, FLOPs / MFMA peak) (the bf16io 3x3 family,
+    # ~420 FLOP/B, sits above the bf16 ridge of 2500 / 8 = 312 FLOP/B -- MFMA-bound, not HBM-bound)
+    gbs = alg_bytes * n / secs / 1e9 if secs > 0 else 0.0
+    ai = (flops / max(n, 1)) / alg_bytes if alg_bytes else 0.0
+    ridge = peak * 1e12 / (HBM_PEAK_GBS * 1e9)
+    grading = {"arithmetic_intensity_flop_per_byte": round(ai, 1), "ridge_flop_per_byte": round(ridge, 1)}
+    if ai >= ridge:
         bound = {"bound": "mfma", "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
-                 "frac": round(achieved / peak, 4)}
-    else:  # the bf16 configurations are HBM-bound: algorithmic bytes against HBM
-        gbs = alg_bytes * n / secs / 1e9 if secs > 0 else 0.0
+                 "frac": round(achieved / peak, 4), "hbm_gbs": round(gbs, 1),
+                 "hbm_frac": round(gbs / HBM_PEAK_GBS, 4), **grading}
+    else:
         bound = {"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                  "frac": round(gbs / HBM_PEAK_GBS, 4), "mfma_tflops": round(achieved, 2),
-                 "mfma_frac": round(achieved / peak, 4)}
+                 "mfma_frac": round(achieved / peak, 4), **grading}
     return {**bound,
             "traffic": round(traffic) if traffic else None,
             "traffic_source": traffic_src,
@@ -499,7 +532,7 @@ def _roofline(args, math, model, core, engine, timer, conv3, step, dt, peak):
                 {"achieved": round(ifl / isec / 1e12, 2) if isec else None, "unit": "TFLOP/s",
                  "frac": round(ifl / isec / 1e12 / peak, 4) if isec else None,
                  "avg_launch_us": round(isec / max(inn, 1) * 1e6, 2), "launches": inn}
-                if math == "f32" else
+                if bound["bound"] == "mfma" else
                 {"achieved": round(alg_bytes * inn / isec / 1e9, 1) if isec else None, "unit": "GB/s",
                  "frac": round(alg_bytes * inn / isec / 1e9 / HBM_PEAK_GBS, 4) if isec else None,
                  "mfma_tflops": round(ifl / isec / 1e12, 2) if isec else None,

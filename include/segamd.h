@@ -489,6 +489,21 @@ int seg_conv_igemm2_bf16io(const seg_bf16* in, long ldin, int N, int H, int W, i
                            const float* bias, seg_bf16* out, long ldout, int Cout, int ks, const seg_bf16* add,
                            long ldadd, float* stat, float* work, hipStream_t stream);
 
+/* seg_conv_halo2_bf16io: the narrow 3x3 convs of the bf16io configuration (replaces aten conv2d /
+ * convolution_backward(input) of src/unet.py:58,61 where Cout <= 96: MobileNetV2UNet up3 / up4 and
+ * their data gradients, UNet's 64-channel full-resolution levels; csrc/halo2.hip).  Persistent
+ * blocks (one per CU) with the weights resident in LDS and the 4 x 64-pixel tiles' input halos
+ * streamed by LDS-DMA through a three-stage ring by a dedicated loader wave.  Arguments as
+ * seg_conv_halo_bf16io_w16 (stride 1, pad 1; bf16 rows, ldin % 8 == 0 and 16-byte aligned; bf16
+ * packed weights, mode 16 forward / 17 data gradient); BN partials in seg_conv_halo2_row_tiles
+ * tiles of 256 rows ([tiles][2][Cout]: sum, M2 about the tile mean).  seg_conv_halo2_ok: H % 4 == 0,
+ * W % 64 == 0, Cin % 8 == 0, Cout <= 96 and 9 x Cout x Cin weights that fit beside the ring. */
+int seg_conv_halo2_ok(int N, int H, int W, int Cin, int Cout);
+int seg_conv_halo2_row_tiles(int N, int H, int W);
+int seg_conv_halo2_bf16io(const seg_bf16* in, long ldin, int N, int H, int W, int Cin, const seg_bf16* wk, int ldk,
+                          const float* bias, seg_bf16* out, long ldout, int Cout, const seg_bf16* add, long ldadd,
+                          float* stat, hipStream_t stream);
+
 /* Build identity (host only): copies the SHA-256 (64 hex chars + NUL) of the sources this
  * library was built from -- every csrc file, this header, compiler and flags
  * (seg_amd/build.py source_hash) -- into out when cap > 64; returns the length.  The

@@ -185,8 +185,10 @@ class ConvOp:
         # Winograd F(2x2,3x3) (seg_conv_wino) for the forward / data gradient, chosen by
         # seg_conv_wino_pick at pack time; U_f [16][Cout][cin_pad], U_d [16][Cin][r4(Cout)]
         self.wino_f = self.wino_d = self.wino_w = False
-        # LDS-halo direct 3x3 (seg_conv_halo) for the forward / data gradient of narrow convs
+        # LDS-halo direct 3x3 (seg_conv_halo) for the forward / data gradient of narrow convs; the
+        # bf16io persistent LDS-DMA variant (seg_conv_halo2_bf16io) where it applies
         self.halo_f = self.halo_d = False
+        self.h2_f = self.h2_d = False
         # bf16 math (Program.math == "bf16"): seg_conv_igemm_bf16 / seg_conv_wgrad_bf16
         self.bf = False
         # bf16io: wk_f / wk_d packed as bf16 for seg_conv_igemm_bf16io_w16 (Program._build_pack)
@@ -240,6 +242,8 @@ class ConvOp:
                 elif self.wino_f:
                     ntiles = query("seg_conv_wino_row_tiles", y.N, y.H, y.W)
                     tile_rows = query("seg_conv_wino_tile_rows")
+                elif self.h2_f:
+                    ntiles, tile_rows = query("seg_conv_halo2_row_tiles", y.N, y.H, y.W), 256
                 elif self.halo_f:
                     ntiles, tile_rows = query("seg_conv_halo_row_tiles", y.N, y.H, y.W), 256
                 else:
@@ -249,6 +253,9 @@ class ConvOp:
             if self.pw_f:  # thin-K 1x1 (its producer's lazy BN, if any, on load)
                 rt.tcall("igemm1_fwd", self.flops(), rt.k("seg_conv_pw"), rt.ptr(i), i.ld, y.M, self.cin_pad, wk_ptr,
                          ldk, bias, rt.ptr(y), y.ld, self.cout, None, 0, statp, *self._in_xform(rt), s)
+            elif self.h2_f:  # narrow bf16io conv: persistent LDS-DMA halo kernel
+                rt.tcall("igemm3_fwd", self.flops(), "seg_conv_halo2_bf16io", rt.ptr(i), i.ld, i.N, i.H, i.W,
+                         self.cin_pad, wk_ptr, ldk, bias, rt.ptr(y), y.ld, self.cout, None, 0, statp, s)
             elif self.halo_f:  # (its producer's lazy BN, if any, on the halo load)
                 name = rt.k("seg_conv_halo") + ("_xf" if self.xform is not None else "") + ("_w16" if self.w16_f else "")
                 rt.tcall("igemm3_fwd", self.flops(), name, rt.ptr(i), i.ld, i.N, i.H, i.W, self.cin_pad,
@@ -442,9 +449,14 @@ class ConvOp:
                 raise NotImplementedError("data gradient of a strided dense conv")
             kin = r4(self.cout)  # dY channels padded to 4 (the C=10 head)
             add_ptr, add_ld = rt.begin_write_add(i)
-            if self.pw_d:  # thin-K 1x1 data gradient
+            # seg_conv_pw / seg_conv_igemm2 read the addend as 16-byte row vectors
+            add16 = add_ptr is None or (add_ld % (16 // rt.es) == 0 and add_ptr % 16 == 0)
+            if self.pw_d and add16:  # thin-K 1x1 data gradient
                 rt.tcall("igemm1_dgrad", self.flops(), rt.k("seg_conv_pw"), dYp, dY.ld, y.M, kin, self.wk_d.data_ptr(),
                          self.ldk_d, None, rt.gptr(i), i.ld, self.cin, add_ptr, add_ld, None, None, None, 0, s)
+            elif self.h2_d:
+                rt.tcall("igemm3_dgrad", self.flops(), "seg_conv_halo2_bf16io", dYp, dY.ld, y.N, y.H, y.W, kin,
+                         self.wk_d.data_ptr(), self.ldk_d, None, rt.gptr(i), i.ld, self.cin, add_ptr, add_ld, None, s)
             elif self.halo_d:
                 rt.tcall("igemm3_dgrad", self.flops(), rt.k("seg_conv_halo") + ("_w16" if self.w16_d else ""), dYp,
                          dY.ld, y.N, y.H, y.W, kin,
@@ -454,7 +466,7 @@ class ConvOp:
                 rt.tcall("wino3_dgrad", self.flops(), "seg_conv_wino", dYp, dY.ld, y.N, y.H, y.W, kin,
                             self.wk_wd.data_ptr(), kin, None, rt.gptr(i), i.ld, self.cin, add_ptr, add_ld, None,
                             work.data_ptr(), s)
-            elif self.ig2_d is not None and (add_ptr is None or (add_ld % 8 == 0 and add_ptr % 16 == 0)):
+            elif self.ig2_d is not None and add16:
                 work = rt.tmp(self.ig2_d[3], zero=True)
                 rt.tcall(f"igemm{self.ks}_dgrad", self.flops(), "seg_conv_igemm2_bf16io", dYp, dY.ld, y.N, y.H, y.W, kin,
                          self.wk_d.data_ptr(), self.ldk_d, None, rt.gptr(i), i.ld, self.cin, self.ks, add_ptr, add_ld,
@@ -604,11 +616,19 @@ class Program:
             if op.bf:
                 # bf16 math: every dense / pointwise conv (fwd, dgrad, wgrad) on the bf16 implicit GEMM
                 op.wino_f = op.wino_d = op.wino_w = op.halo_f = op.halo_d = False
+                op.h2_f = op.h2_d = False
                 if self.math == "bf16io" and op.ks == 3 and op.stride == 1 and op.pad == 1:
-                    # LDS-halo direct conv on bf16 (seg_conv_halo_bf16io): narrow convs, 8-channel slots
-                    op.halo_f = (op.cin_pad % 8 == 0 and HALO_BF16
+                    # narrow convs: the persistent LDS-DMA halo kernel (seg_conv_halo2_bf16io, bf16 packed
+                    # weights resident in LDS) where it applies, else the LDS-halo direct conv
+                    # (seg_conv_halo_bf16io): 8-channel slots
+                    h2 = HALO2 and W16
+                    op.h2_f = (h2 and op.xform is None and op.cin_pad % 8 == 0
+                               and bool(query("seg_conv_halo2_ok", y.N, y.H, y.W, op.cin_pad, op.cout)))
+                    op.h2_d = (h2 and not op.first and r4(op.cout) % 8 == 0
+                               and bool(query("seg_conv_halo2_ok", y.N, y.H, y.W, r4(op.cout), op.cin)))
+                    op.halo_f = (not op.h2_f and op.cin_pad % 8 == 0 and HALO_BF16
                                  and bool(query("seg_conv_halo_pick", y.N, y.H, y.W, op.cin_pad, op.cout)))
-                    op.halo_d = (not op.first and r4(op.cout) % 8 == 0 and HALO_BF16
+                    op.halo_d = (not op.h2_d and not op.first and r4(op.cout) % 8 == 0 and HALO_BF16
                                  and bool(query("seg_conv_halo_pick", y.N, y.H, y.W, r4(op.cout), op.cin)))
                 # bf16io implicit-GEMM and LDS-halo launches take bf16 packed weights (seg_conv_*_bf16io_w16:
                 # half the weight bytes every M tile / pixel tile re-reads)
@@ -620,9 +640,9 @@ class Program:
                         and (op.ks == 3 or IGEMM2 == "all")):
                     i = op.inp  # 16-byte rows: ld and channel offset multiples of 8 elements
                     rows16 = i.ld % 8 == 0 and i.off % 8 == 0 and y.ld % 8 == 0 and y.off % 8 == 0
-                    if rows16 and not op.halo_f and op.xform is None and op.cin_pad == op.cin:
+                    if rows16 and not (op.halo_f or op.h2_f) and op.xform is None and op.cin_pad == op.cin:
                         op.ig2_f = igemm2_plan(y.M, op.cout, op.cin_pad, op.ks)
-                    if rows16 and not op.first and not op.halo_d and op.cout % 8 == 0:
+                    if rows16 and not op.first and not (op.halo_d or op.h2_d) and op.cout % 8 == 0:
                         op.ig2_d = igemm2_plan(y.M, op.cin, op.cout, op.ks)
                 if w16f:
                     op.pw_f, op.pw_d = _pw_pick(op, 8)
@@ -644,9 +664,10 @@ class Program:
             op.pw_f, op.pw_d = _pw_pick(op, 4)
             dense3 = op.ks == 3 and op.stride == 1 and op.pad == 1
             wino_ok = dense3 and WINOGRAD
-            op.wino_f = wino_ok and bool(query("seg_conv_wino_pick", y.N, y.H, y.W, op.cin_pad, op.cout))
-            op.wino_d = wino_ok and not op.first and bool(query("seg_conv_wino_pick", y.N, y.H, y.W, r4(op.cout),
-                                                                op.cin))
+            op.wino_f = wino_ok and WINOGRAD_FWD and bool(query("seg_conv_wino_pick", y.N, y.H, y.W, op.cin_pad,
+                                                                op.cout))
+            op.wino_d = wino_ok and WINOGRAD_DGRAD and not op.first and bool(
+                query("seg_conv_wino_pick", y.N, y.H, y.W, r4(op.cout), op.cin))
             op.wino_w = wino_ok and WINOGRAD_WGRAD and bool(query("seg_conv_wino_wgrad_pick", y.N, y.H, y.W, op.cin_pad,
                                                                    op.cout))
             op.halo_f = (dense3 and not op.wino_f
@@ -982,9 +1003,15 @@ class Run:
         """An all-zero gradient for parameter `p`.  A recorded run's gradient slot is persistent and
         nothing else writes it, so it is zeroed once, now (on the current stream, ahead of every
         replay), and the tape gets no entry; an immediate run zeroes its fresh tensor on the current stream
-        (`stream`: inside the fork context)."""
+        (`stream`: inside the fork context).  Under DataParallel the slot is a view into an
+        all-reduced gradient bucket into which a synchronised backward folds any `.grad` a rank
+        still holds, so a recorded run re-zeroes it every step (a tape memset on `stream`) -- a
+        once-only zero would keep that fold and double it on every later step."""
         self.grad_param(p)
-        self.grads[id(p)].zero_()
+        g = self.grads[id(p)]
+        g.zero_()
+        if self.rec is not None and self.sync is not None:
+            self.rec.memset2d(g.data_ptr(), g.numel() * 4, 0, g.numel() * 4, 1, stream)
 
     def zero(self, a: Act):
         """Zero-fill the gradient region of `a` (a channel slice of a row buffer)."""
@@ -1195,8 +1222,13 @@ OVERLAP = os.environ.get("SEG_OVERLAP", "1") == "1"
 # diagnostics: tests/test_gpu_unet_cfg5.py separates Winograd from accumulation error).
 WINOGRAD = os.environ.get("SEG_WINO", "1") == "1"
 WINOGRAD_WGRAD = os.environ.get("SEG_WINO_WGRAD", "1") == "1"  # the F(3x3,2x2) weight gradients alone
+# ... and the F(2x2,3x3) forward / data-gradient transforms separately (parity attribution)
+WINOGRAD_FWD = os.environ.get("SEG_WINO_FWD", "1") == "1"
+WINOGRAD_DGRAD = os.environ.get("SEG_WINO_DGRAD", "1") == "1"
 # LDS-halo direct 3x3 conv for the narrow convs in the bf16io configuration; SEG_HALO_BF16=0 turns it off.
 HALO_BF16 = os.environ.get("SEG_HALO_BF16", "1") == "1"
+# ... and the persistent LDS-DMA halo kernel (seg_conv_halo2_bf16io) where it applies; SEG_HALO2=0 = off
+HALO2 = os.environ.get("SEG_HALO2", "1") == "1"
 # lazy BatchNorm for 1x1 consumers (the inverted residuals' project convs, OutConv's last
 # conv): SEG_LAZY_PW=0 keeps the separate BN-apply pass (read at program build)
 LAZY_PW = os.environ.get("SEG_LAZY_PW", "1") == "1"
@@ -1499,8 +1531,17 @@ class _SegFunction(torch.autograd.Function):
         if mode == "loss":
             model.__dict__["_segamd_last_stats"] = plan.run.stats
             out = plan.run.stats[0].clone()  # the stats buffer is rewritten by the next step
+            # the out-of-range label count, copied to the host as soon as the loss kernel has run:
+            # train_one_epoch reads it before optimizer.step() without waiting for the backward
+            host = model.__dict__.get("_segamd_bad_host")
+            if host is None or host[0].device.type != "cpu":
+                host = (torch.zeros(1, dtype=torch.float32).pin_memory(), torch.cuda.Event())
+                model.__dict__["_segamd_bad_host"] = host
+            host[0].copy_(plan.run.stats[2:3], non_blocking=True)
+            host[1].record()
         else:  # an unfused criterion checks its own labels: no stale flag from an earlier fused loss
             model.__dict__.pop("_segamd_last_stats", None)
+            model.__dict__.pop("_segamd_bad_host", None)
         if needs_grad:
             plan.busy = True
             ctx.plan, ctx.params = plan, params
@@ -1540,6 +1581,18 @@ def bad_label_count(model):
     model = getattr(model, "module", model)
     st = model.__dict__.get("_segamd_last_stats")
     return None if st is None else st[2:3].clone()
+
+
+def bad_label_count_host(model):
+    """The out-of-range label count of `model`'s last fused loss as a host int, or None: waits
+    only for that forward's loss kernel (an event recorded behind its device-to-host copy), not
+    for the backward queued after it, so the host keeps running ahead of the GPU."""
+    model = getattr(model, "module", model)
+    host = model.__dict__.get("_segamd_bad_host")
+    if host is None or model.__dict__.get("_segamd_last_stats") is None:
+        return None
+    host[1].synchronize()
+    return int(host[0].item())
 
 
 def check_targets(model, bad=None):

@@ -46,13 +46,19 @@ def _check_labels(model, inputs):
     the others in the next collective."""
     if not inputs.is_cuda:
         return  # the CPU composition's F.cross_entropy raises by itself
-    from .engine import bad_label_count, check_targets
-    bad = bad_label_count(model)
-    if bad is None:
-        return
+    from .engine import bad_label_count, bad_label_count_host, check_targets
     if torch.distributed.is_available() and torch.distributed.is_initialized() and hasattr(model, "module"):
+        bad = bad_label_count(model)
+        if bad is None:
+            return
         torch.distributed.all_reduce(bad, group=getattr(model, "pg", None))
-    check_targets(model, bad)
+        check_targets(model, bad)
+        return
+    # one process: the count was copied to the host right after the loss kernel, so this waits
+    # for the forward only and optimizer.step() is queued while the backward still runs (ADVICE r3)
+    n = bad_label_count_host(model)
+    if n:
+        check_targets(model, torch.tensor([float(n)]))
 
 
 def compute_loss(model, criterion, inputs, targets):

@@ -81,3 +81,32 @@ def test_ddp_world1_grad_accumulation(pg, set_to_none):
     assert g0.keys() == g1.keys() and len(g0) == 194
     for k in g0:
         assert torch.equal(g0[k], g1[k]), k
+
+
+def test_ddp_world1_held_bias_grads_not_refolded(pg):
+    """Conv biases in front of train-mode BatchNorm get an exact-zero gradient whose slot in
+    the all-reduced bucket must be re-zeroed every step: a synchronised backward folds the
+    .grad a rank still holds into the bucket, so a slot zeroed only once would keep that fold
+    and double it on the next step.  Three backwards without zero_grad, each
+    followed by an in-place change of every .grad (a manual L2 term), against the plain model."""
+    x, y = synthetic_batch(2, 64, 128, 10, seed=12)
+    x, y = x.to(DEV), y.to(DEV)
+    res = []
+    for wrap in (False, True):
+        m = deterministic_init(MobileNetV2UNet(10), seed=13).to(DEV).train()
+        model = DataParallel(m, bucket_cap_mb=1.0) if wrap else m
+        for _ in range(3):
+            model.forward_loss(x, y).backward()
+            if wrap:
+                model.finish_gradient_sync()
+            with torch.no_grad():
+                for p in m.parameters():
+                    if p.grad is not None:
+                        p.grad.add_(p.detach(), alpha=1e-3)
+        torch.cuda.synchronize()
+        res.append({k: p.grad.clone() for k, p in m.named_parameters() if p.grad is not None})
+    g0, g1 = res
+    biases = [k for k in g0 if k.startswith("up") and k.endswith("bias") and ".conv.conv." in k]
+    assert biases, "the decoder's pre-BatchNorm conv biases"
+    for k in g0:
+        assert torch.equal(g0[k], g1[k]), k

@@ -5,7 +5,8 @@ oracle-checked slice that selects the same kernel kinds.
   * mid-size slice (2x128x256, f32): the Winograd forward / data-gradient, LDS-halo and
     implicit-GEMM choices per layer equal the full-size ones (tools: engine picks), and
     logits / loss / every gradient pass the oracle budget of tests/test_gpu_model.py --
-    with Winograd, without its weight gradients and without it, worst tensor recorded for each;
+    with all Winograd transforms, with each group of them off and without Winograd, worst
+    tensor recorded for each;
   * full size (8x512x1024; bf16io and f32): finite, bitwise reproducible step to step
     (fixed-order reductions), the fused upsample+CE loss equals nn.CrossEntropyLoss on
     the model's logits, and the max-pool / concat / upsample launches at this size run.
@@ -42,12 +43,13 @@ def test_mid_size_slice_selects_full_size_kernels():
     assert _kinds(2, 128, 256, "f32") == _kinds(8, 512, 1024, "f32")
 
 
-def _slice_run(x, y, state, side, winograd, wino_wgrad=True):
-    """One f32 training step of the 2x128x256 slice with Winograd on or off (wino_wgrad:
-    the weight-gradient transforms alone); returns the logits, loss and the oracle budget
-    report (oracle side shared between the runs)."""
-    saved = engine.WINOGRAD, engine.WINOGRAD_WGRAD
-    engine.WINOGRAD, engine.WINOGRAD_WGRAD = winograd, wino_wgrad
+def _slice_run(x, y, state, side, fwd, dgrad, wgrad):
+    """One f32 training step of the 2x128x256 slice with each Winograd transform on or off
+    (fwd: F(2x2,3x3) forward, dgrad: F(2x2,3x3) data gradient, wgrad: F(3x3,2x2) weight
+    gradient); returns the logits, loss, the oracle budget report (oracle side shared
+    between the runs) and the Winograd launches per step."""
+    saved = engine.WINOGRAD_FWD, engine.WINOGRAD_DGRAD, engine.WINOGRAD_WGRAD
+    engine.WINOGRAD_FWD, engine.WINOGRAD_DGRAD, engine.WINOGRAD_WGRAD = fwd, dgrad, wgrad
     engine.DEBUG_KEEP_RUN = True
     try:
         model = deterministic_init(UNet(10), seed=31).to(DEV).train()
@@ -60,20 +62,25 @@ def _slice_run(x, y, state, side, winograd, wino_wgrad=True):
         n_wino = sum(op.wino_f + op.wino_d + op.wino_w for op in prog.ops if isinstance(op, engine.ConvOp))
     finally:
         engine.DEBUG_KEEP_RUN, engine.LAST_RUN = False, None
-        engine.WINOGRAD, engine.WINOGRAD_WGRAD = saved
+        engine.WINOGRAD_FWD, engine.WINOGRAD_DGRAD, engine.WINOGRAD_WGRAD = saved
     grads = {k: p.grad for k, p in model.named_parameters() if p.grad is not None}
     rep = budget.check_hip("UNet", state, x, y, grads, z, side=side)
     return logits.detach().double().cpu(), loss.item(), rep, n_wino
 
 
+# (tag, forward, data gradient, weight gradient) Winograd transforms on
+SLICE_VARIANTS = (("winograd", True, True, True), ("winograd_fwd_dgrad_only", True, True, False),
+                  ("winograd_fwd_only", True, False, False), ("winograd_dgrad_only", False, True, False),
+                  ("no_winograd", False, False, False))
+
+
 def test_unet_mid_size_parity_vs_oracle(record):
-    """The slice against the oracle budget, run three times: with the production kernel
-    choice (Winograd F(2x2,3x3) forward / data gradient and F(3x3,2x2) weight gradient on the
-    deep convs), with the Winograd weight gradients off, and with Winograd off (the same
-    convs on the LDS-halo / implicit-GEMM kernels, exact fp32 products).  All must pass; the
-    worst tensor of each is asserted below 1 and recorded, so the record shows whether
-    Winograd's transform error (and which transform) or plain fp32 accumulation drives the
-    margin."""
+    """The slice against the oracle budget, run with the production kernel choice (Winograd
+    F(2x2,3x3) forward / data gradient and F(3x3,2x2) weight gradient on the deep convs) and
+    with the transforms switched off one group at a time, down to no Winograd at all (the
+    same convs on the LDS-halo / implicit-GEMM kernels, exact fp32 products).  All must pass;
+    the worst tensor of each is asserted below 1 and recorded, so the record shows which
+    transform -- forward, data gradient or weight gradient -- drives the margin."""
     x, y = synthetic_batch(2, 128, 256, 10, seed=31)
     model_cpu = deterministic_init(UNet(10), seed=31)
     state = segref.canonical_state(model_cpu.state_dict())
@@ -82,27 +89,24 @@ def test_unet_mid_size_parity_vs_oracle(record):
     with torch.no_grad():
         ref = segref.unet_forward(p64, x.double(), True)
     res = {}
-    for wino, wwg in ((True, True), (True, False), (False, False)):
-        logits, loss, rep, n_wino = _slice_run(x, y, state, side, wino, wwg)
+    for tag, fwd, dgrad, wgrad in SLICE_VARIANTS:
+        logits, loss, rep, n_wino = _slice_run(x, y, state, side, fwd, dgrad, wgrad)
         rel = float((logits - ref).norm() / ref.norm())
-        tag = ("winograd" if wwg else "winograd_fwd_dgrad_only") if wino else "no_winograd"
         top = sorted(rep["ratios"].items(), key=lambda kv: -kv[1])[:3]
         print(f"UNet 2x128x256 f32 {tag} ({n_wino} Winograd launches/step): logits rel {rel:.2e}, worst grad "
               f"{rep['worst']:.3f} of budget ({rep['worst_name']}), next {top[1:]}, z {rep['z_worst']:.3f} of "
               f"bound, {rep['n_flips']} mask flips")
         record(kernels=tag, winograd_launches=n_wino, logits_rel=rel, worst=rep["worst"],
                worst_name=rep["worst_name"], top3=top, z_worst=rep["z_worst"], n_flips=rep["n_flips"])
-        assert (n_wino > 0) == wino
+        assert (n_wino > 0) == (fwd or dgrad or wgrad)
         assert rel < 1e-3, rel
         assert abs(loss - rep["loss64"]) <= 1e-4 * abs(rep["loss64"])
         assert not rep["z_bad"] and not rep["missing_layers"], (rep["z_bad"][:3], rep["missing_layers"])
         assert not rep["bad"], rep["bad"][:8]
         assert rep["worst"] < 1.0
         res[tag] = rep
-    print(f"worst of budget: Winograd {res['winograd']['worst']:.3f} ({res['winograd']['worst_name']}), "
-          f"Winograd without its weight gradients {res['winograd_fwd_dgrad_only']['worst']:.3f} "
-          f"({res['winograd_fwd_dgrad_only']['worst_name']}), exact-product kernels "
-          f"{res['no_winograd']['worst']:.3f} ({res['no_winograd']['worst_name']})")
+    print("worst of budget: " + ", ".join(f"{t} {res[t]['worst']:.3f} ({res[t]['worst_name']})"
+                                          for t, *_ in SLICE_VARIANTS))
 
 
 @pytest.mark.parametrize("math", ["bf16io", "f32"])

@@ -488,6 +488,17 @@ int seg_conv_igemm2_plan(long M, int Cout, int Cin, int ks, long* out);
 int seg_conv_igemm2_bf16io(const seg_bf16* in, long ldin, int N, int H, int W, int Cin, const seg_bf16* wk, int ldk,
                            const float* bias, seg_bf16* out, long ldout, int Cout, int ks, const seg_bf16* add,
                            long ldadd, float* stat, float* work, hipStream_t stream);
+/* Round 4: the plan also picks 4-wave 128x128 / 128x64 / 64x128 / 64x64 tiles (small-image 1x1 and 3x3
+ * convs of the MobileNetV2 encoder); seg_igemm2_force_tile(t) forces table entry t (-1 = the plan).
+ * _xf: a 1x1 conv (ks == 1, Cin <= 2048) whose input is the raw output of a BatchNorm'd producer,
+ * A = act(in * in_scale[c] + in_shift[c]) formed on the MFMA fragments (bf16-rounded as the BN-apply
+ * pass would store it) -- the project convs of the inverted residuals (torchvision, via
+ * src/unet.py:15-19). */
+int seg_igemm2_force_tile(int t);
+int seg_conv_igemm2_bf16io_xf(const seg_bf16* in, long ldin, int N, int H, int W, int Cin, const seg_bf16* wk,
+                              int ldk, const float* bias, seg_bf16* out, long ldout, int Cout, int ks,
+                              const seg_bf16* add, long ldadd, float* stat, float* work, const float* in_scale,
+                              const float* in_shift, int in_act, hipStream_t stream);
 
 /* seg_conv_halo2_bf16io: the narrow 3x3 convs of the bf16io configuration (replaces aten conv2d /
  * convolution_backward(input) of src/unet.py:58,61 where Cout <= 96: MobileNetV2UNet up3 / up4 and

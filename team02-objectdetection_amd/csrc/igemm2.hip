@@ -28,12 +28,19 @@
 //  * epilogue as igemm_conv_kernel's: bias, BatchNorm tile partials (sum, M2 about the tile
 //    mean) for seg_bn_stats_tiles, addend, one rounding to bf16, 16-byte row stores staged
 //    through LDS.
+// Round 4: the same pipeline on 4-wave blocks with 128 x 128 / 128 x 64 / 64 x 128 / 64 x 64
+// tiles (wave tiles 64x64 / 64x32 / 32x64 / 32x32) for the small-image 1x1 convs of the
+// MobileNetV2 encoder (M = 4k-65k rows at bs=32: the generic register-staged kernel keeps one
+// K chunk in flight and ran them at 0.4-1.5 TB/s), and for 1x1 convs the producer's lazy
+// BatchNorm + activation applied to the A fragments after their LDS read (XF: LDS-DMA cannot
+// transform on the way in; rows beyond M and k beyond K meet zero weights or are never stored,
+// so the transform needs no mask for 1x1).
 #include "common.h"
 
 namespace {
 
 constexpr int kBK = 64;             // K step (bf16 elements) = one 128-byte operand row
-constexpr int kThreads = 512;
+constexpr int kXfMax = 2048;      // XF: input channels whose coefficients fit in LDS
 
 __device__ __attribute__((aligned(16))) unsigned g_zero_row[4];  // 16 zero bytes
 
@@ -48,6 +55,7 @@ struct Igemm2Args {
   unsigned* cnt;                    // split-K: [tiles] tickets (zero before the first launch; left zero)
   int N, H, W, Cin, Cout, ks, pad;
   int K, M, nsteps, steps_per_split, splits, tiles_m, tiles_n;
+  const float* xs; const float* xb; int xact;  // XF: A = act(in * xs[k] + xb[k]) (1x1 only)
 };
 
 #ifndef SEG_IG2_NODMA
@@ -75,22 +83,34 @@ __device__ __forceinline__ void wait_lgkm0() { __builtin_amdgcn_s_waitcnt(0xC07F
 
 template <int N>
 __device__ __forceinline__ void wait_vm() {  // s_waitcnt vmcnt(N), other counters untouched
-  static_assert(N >= 0 && N < 16, "vmcnt immediate");
-  __builtin_amdgcn_s_waitcnt(0x0F70 | N);
+  static_assert(N >= 0 && N < 64, "vmcnt immediate");
+  __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | 0x0F70);  // vmcnt is 6 bits, split 3:0 / 15:14
 }
 
-template <int BM, int BN, int KS>
-__global__ __launch_bounds__(kThreads) void igemm2_kernel(Igemm2Args a) {
-  constexpr int WM = 64, WN = 64, WAVES_N = BN / WN;
-  static_assert((BM / WM) * (BN / WN) == 8, "8 waves");
+template <int BM, int BN, int WM, int WN, int KS, bool XF = false>
+__global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void igemm2_kernel(Igemm2Args a) {
+  constexpr int NW = (BM / WM) * (BN / WN), kThreads = 64 * NW, WAVES_N = BN / WN;
+  constexpr int MI = WM / 32, NI = WN / 32;
+  static_assert(NW == 4 || NW == 8, "4 or 8 waves");
+  static_assert(BM % (8 * NW) == 0 && BN % (8 * NW) == 0, "whole DMA instructions per wave");
+  static_assert(!XF || KS == 1, "the fragment transform is for 1x1 convs");
   constexpr int A_BYTES = BM * 128, STAGE = (BM + BN) * 128;
-  constexpr int NA = BM / 64, NB = BN / 64;  // DMA instructions per wave per K step
+  constexpr int NA = BM / (8 * NW), NB = BN / (8 * NW);  // DMA instructions per wave per K step
   constexpr int CSR = BN + 4;                // epilogue band row stride (floats)
   constexpr int NSTAGE = 3;                  // LDS buffers: two K steps in flight while one computes
-  constexpr int SMEM = NSTAGE * STAGE > WM * CSR * 4 ? NSTAGE * STAGE : WM * CSR * 4;
+  constexpr int XF_BYTES = XF ? 2 * kXfMax * 4 : 0;
+  constexpr int RING = NSTAGE * STAGE > WM * CSR * 4 ? NSTAGE * STAGE : WM * CSR * 4;
+  constexpr int SMEM = RING + XF_BYTES;
   __shared__ __attribute__((aligned(1024))) char smem[SMEM];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  float* xsL = reinterpret_cast<float*>(smem + RING);  // XF: [kXfMax] scales, then [kXfMax] shifts
+  if constexpr (XF) {
+    for (int k = tid * 4; k < a.K; k += kThreads * 4) {
+      *reinterpret_cast<f32x4*>(xsL + k) = ld4(a.xs + k);
+      *reinterpret_cast<f32x4*>(xsL + kXfMax + k) = ld4(a.xb + k);
+    }
+  }
   const int wm0 = (wave / WAVES_N) * WM, wn0 = (wave % WAVES_N) * WN;
   // a tile's K slices are adjacent logical ids: the same XCD (and L2) combines them
   const int lid = xcd_swizzle(blockIdx.x, gridDim.x);
@@ -101,7 +121,7 @@ __global__ __launch_bounds__(kThreads) void igemm2_kernel(Igemm2Args a) {
   const int nst = min(a.nsteps - s_beg, a.steps_per_split);
 
   // ---- per-lane DMA sources.  Instruction j of a tile covers rows 8j .. 8j+7 (1 KB of LDS);
-  // wave w issues j = w, w + 8, ...; lane l fills row 8j + (l >> 3), physical chunk l & 7,
+  // wave w issues j = w, w + NW, ...; lane l fills row 8j + (l >> 3), physical chunk l & 7,
   // i.e. logical chunk cl = (l & 7) ^ swz(row).
   const int lrow = lane >> 3, lchk = lane & 7;
   long a_off[NA];
@@ -109,7 +129,7 @@ __global__ __launch_bounds__(kThreads) void igemm2_kernel(Igemm2Args a) {
   int a_cl[NA];
 #pragma unroll
   for (int i = 0; i < NA; ++i) {
-    const int row = 8 * (wave + 8 * i) + lrow;
+    const int row = 8 * (wave + NW * i) + lrow;
     a_cl[i] = lchk ^ ((row >> 1) & 7);
     const int p = m0 + row;
     const bool ok = p < a.M;
@@ -131,7 +151,7 @@ __global__ __launch_bounds__(kThreads) void igemm2_kernel(Igemm2Args a) {
   int b_k[NB];  // this lane's k offset within a step (8 * logical chunk); 2^30: row beyond Cout
 #pragma unroll
   for (int i = 0; i < NB; ++i) {
-    const int row = 8 * (wave + 8 * i) + lrow;
+    const int row = 8 * (wave + NW * i) + lrow;
     const int cl = lchk ^ ((row >> 1) & 7);
     const int co = n0 + row;
     b_k[i] = co < a.Cout ? 8 * cl : 1 << 30;
@@ -154,12 +174,12 @@ __global__ __launch_bounds__(kThreads) void igemm2_kernel(Igemm2Args a) {
       const int tap = u_tap + (wrap ? 1 : 0);
       const bool ok = (a_mask[i] >> tap) & 1u;
       const __bf16* src = a.in + a_off[i] + (wrap ? u_toff1 : u_toff0) + (wrap ? ci - a.Cin : ci);
-      dma16(ok ? (const void*)src : (const void*)g_zero_row, As + (wave + 8 * i) * 1024);
+      dma16(ok ? (const void*)src : (const void*)g_zero_row, As + (wave + NW * i) * 1024);
     }
 #pragma unroll
     for (int i = 0; i < NB; ++i) {
       const bool ok = k0 + b_k[i] < a.K;
-      dma16(ok ? (const void*)(a.wk + b_off[i] + k0) : (const void*)g_zero_row, Bs + (wave + 8 * i) * 1024);
+      dma16(ok ? (const void*)(a.wk + b_off[i] + k0) : (const void*)g_zero_row, Bs + (wave + NW * i) * 1024);
     }
     // advance one K step
     k0 += kBK;
@@ -172,31 +192,47 @@ __global__ __launch_bounds__(kThreads) void igemm2_kernel(Igemm2Args a) {
     }
   };
 
-  f32x16 acc[2][2];
+  f32x16 acc[MI][NI];
 #pragma unroll
-  for (int mi = 0; mi < 2; ++mi)
+  for (int mi = 0; mi < MI; ++mi)
 #pragma unroll
-    for (int ni = 0; ni < 2; ++ni)
+    for (int ni = 0; ni < NI; ++ni)
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[mi][ni][r] = 0.f;
 
   const int fr = lane & 31, fh = lane >> 5;
+  int kx = k_beg;  // XF: first k of the step being computed
   auto compute = [&](int buf) {
     const char* As = smem + buf * STAGE;
     const char* Bs = As + A_BYTES;
     // fragments of the next 16-deep k slice are read while the current slice's MFMAs run
-    bf16x8 af[2][2], bfr[2][2];
+    bf16x8 af[2][MI], bfr[2][NI];
     auto frag = [&](int ks, int st) {
       const int chunk = 2 * ks + fh;  // logical 16-byte chunk of this lane's 8 k values
 #pragma unroll
-      for (int mi = 0; mi < 2; ++mi) {
+      for (int mi = 0; mi < MI; ++mi) {
         const int r = wm0 + mi * 32 + fr;
         af[st][mi] = *reinterpret_cast<const bf16x8*>(As + r * 128 + 16 * (chunk ^ ((r >> 1) & 7)));
       }
 #pragma unroll
-      for (int ni = 0; ni < 2; ++ni) {
+      for (int ni = 0; ni < NI; ++ni) {
         const int r = wn0 + ni * 32 + fr;
         bfr[st][ni] = *reinterpret_cast<const bf16x8*>(Bs + r * 128 + 16 * (chunk ^ ((r >> 1) & 7)));
+      }
+      if constexpr (XF) {  // the producer's BN + activation on the fragment (as the apply pass stores it)
+        const int k = kx + 8 * chunk;
+        const f32x4 s0 = *reinterpret_cast<const f32x4*>(xsL + k), s1 = *reinterpret_cast<const f32x4*>(xsL + k + 4);
+        const f32x4 b0 = *reinterpret_cast<const f32x4*>(xsL + kXfMax + k);
+        const f32x4 b1 = *reinterpret_cast<const f32x4*>(xsL + kXfMax + k + 4);
+#pragma unroll
+        for (int mi = 0; mi < MI; ++mi) {
+          const bf16x8 q = af[st][mi];
+          const f32x4 lo = seg_bn_act4(__builtin_convertvector(__builtin_shufflevector(q, q, 0, 1, 2, 3), f32x4), s0,
+                                       b0, a.xact);
+          const f32x4 hi = seg_bn_act4(__builtin_convertvector(__builtin_shufflevector(q, q, 4, 5, 6, 7), f32x4), s1,
+                                       b1, a.xact);
+          af[st][mi] = seg_cat8(__builtin_convertvector(lo, bf16x4), __builtin_convertvector(hi, bf16x4));
+        }
       }
     };
     frag(0, 0);
@@ -204,9 +240,9 @@ __global__ __launch_bounds__(kThreads) void igemm2_kernel(Igemm2Args a) {
     for (int ks = 0; ks < kBK / 16; ++ks) {
       if (ks + 1 < kBK / 16) frag(ks + 1, (ks + 1) & 1);
 #pragma unroll
-      for (int mi = 0; mi < 2; ++mi)
+      for (int mi = 0; mi < MI; ++mi)
 #pragma unroll
-        for (int ni = 0; ni < 2; ++ni) {
+        for (int ni = 0; ni < NI; ++ni) {
           if (SEG_IG2_NOMFMA) {
             asm volatile("" ::"v"(af[ks & 1][mi]), "v"(bfr[ks & 1][ni]));
             continue;
@@ -214,6 +250,7 @@ __global__ __launch_bounds__(kThreads) void igemm2_kernel(Igemm2Args a) {
           acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[ks & 1][mi], bfr[ks & 1][ni], acc[mi][ni], 0, 0, 0);
         }
     }
+    kx += kBK;
   };
 
   // ---- K loop: buffer it % 3 holds step it; steps it + 1 and it + 2 stay in flight meanwhile
@@ -222,6 +259,10 @@ __global__ __launch_bounds__(kThreads) void igemm2_kernel(Igemm2Args a) {
   if (nst > 0) issue(0);
   if (nst > 1) issue(1);
   if (nst > 2) issue(2);
+  if constexpr (XF) {  // the coefficient stores above: visible to every wave before the first compute
+    wait_lgkm0();
+    raw_barrier();
+  }
   for (int it = 0; it < nst; ++it) {
     const int ahead = min(nst - 1 - it, 2);  // steps issued beyond this one
     if (ahead == 2) wait_vm<2 * (NA + NB)>();
@@ -239,44 +280,44 @@ __global__ __launch_bounds__(kThreads) void igemm2_kernel(Igemm2Args a) {
   if (a.splits > 1) {
     float* mine = a.slab + ((long)tile * a.splits + z) * (BM * BN);
 #pragma unroll
-    for (int mi = 0; mi < 2; ++mi)
+    for (int mi = 0; mi < MI; ++mi)
 #pragma unroll
-      for (int ni = 0; ni < 2; ++ni)
+      for (int ni = 0; ni < NI; ++ni)
 #pragma unroll
         for (int r = 0; r < 16; ++r)
-          seg_st_wt(mine + (((wave * 2 + mi) * 2 + ni) * 16 + r) * 64 + lane, acc[mi][ni][r]);
+          seg_st_wt(mine + (((wave * MI + mi) * NI + ni) * 16 + r) * 64 + lane, acc[mi][ni][r]);
     int* word = reinterpret_cast<int*>(smem);
     if (!seg_last_arrival(a.cnt + tile, a.splits, word)) return;
     // sum the slices in slice order (every slice read back, this one included: no
     // data-dependent select between a register and a load)
-    f32x16 tot[2][2];
+    f32x16 tot[MI][NI];
     for (int zz = 0; zz < a.splits; ++zz) {
       const float* sl = a.slab + ((long)tile * a.splits + zz) * (BM * BN);
-      f32x16 v[2][2];
+      f32x16 v[MI][NI];
 #pragma unroll
-      for (int mi = 0; mi < 2; ++mi)
+      for (int mi = 0; mi < MI; ++mi)
 #pragma unroll
-        for (int ni = 0; ni < 2; ++ni)
+        for (int ni = 0; ni < NI; ++ni)
 #pragma unroll
-          for (int r = 0; r < 16; ++r) v[mi][ni][r] = seg_ld_wt(sl + (((wave * 2 + mi) * 2 + ni) * 16 + r) * 64 + lane);
+          for (int r = 0; r < 16; ++r) v[mi][ni][r] = seg_ld_wt(sl + (((wave * MI + mi) * NI + ni) * 16 + r) * 64 + lane);
 #pragma unroll
-      for (int mi = 0; mi < 2; ++mi)
+      for (int mi = 0; mi < MI; ++mi)
 #pragma unroll
-        for (int ni = 0; ni < 2; ++ni) tot[mi][ni] = zz == 0 ? v[mi][ni] : tot[mi][ni] + v[mi][ni];
+        for (int ni = 0; ni < NI; ++ni) tot[mi][ni] = zz == 0 ? v[mi][ni] : tot[mi][ni] + v[mi][ni];
     }
 #pragma unroll
-    for (int mi = 0; mi < 2; ++mi)
+    for (int mi = 0; mi < MI; ++mi)
 #pragma unroll
-      for (int ni = 0; ni < 2; ++ni) acc[mi][ni] = tot[mi][ni];
+      for (int ni = 0; ni < NI; ++ni) acc[mi][ni] = tot[mi][ni];
   }
 
   // ---- epilogue.  C layout of the 32x32 MFMA: col = lane & 31, row = (r&3) + 8(r>>2) + 4(lane>>5).
 #pragma unroll
-  for (int ni = 0; ni < 2; ++ni) {
+  for (int ni = 0; ni < NI; ++ni) {
     const int col = n0 + wn0 + ni * 32 + fr;
     const float b = (a.bias && col < a.Cout) ? a.bias[col] : 0.f;
 #pragma unroll
-    for (int mi = 0; mi < 2; ++mi)
+    for (int mi = 0; mi < MI; ++mi)
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[mi][ni][r] += b;
   }
@@ -292,12 +333,12 @@ __global__ __launch_bounds__(kThreads) void igemm2_kernel(Igemm2Args a) {
 #pragma unroll
     for (int pass = 0; pass < 2; ++pass) {
 #pragma unroll
-      for (int ni = 0; ni < 2; ++ni) {
+      for (int ni = 0; ni < NI; ++ni) {
         const int cl = wn0 + ni * 32 + fr;
         const float mu = pass ? tmean[cl] : 0.f;
         float sum = 0.f;
 #pragma unroll
-        for (int mi = 0; mi < 2; ++mi)
+        for (int mi = 0; mi < MI; ++mi)
 #pragma unroll
           for (int r = 0; r < 16; ++r) {
             const int row = m0 + wm0 + mi * 32 + (r & 3) + 8 * (r >> 2) + 4 * fh;
@@ -328,9 +369,9 @@ __global__ __launch_bounds__(kThreads) void igemm2_kernel(Igemm2Args a) {
     __syncthreads();
     if (wm0 == band * WM) {
 #pragma unroll
-      for (int ni = 0; ni < 2; ++ni)
+      for (int ni = 0; ni < NI; ++ni)
 #pragma unroll
-        for (int mi = 0; mi < 2; ++mi)
+        for (int mi = 0; mi < MI; ++mi)
 #pragma unroll
           for (int r = 0; r < 16; ++r)
             Cs[(mi * 32 + (r & 3) + 8 * (r >> 2) + 4 * fh) * CSR + wn0 + ni * 32 + fr] = acc[mi][ni][r];
@@ -368,48 +409,103 @@ __global__ __launch_bounds__(kThreads) void igemm2_kernel(Igemm2Args a) {
   }
 }
 
+struct Tile2 {
+  int bm, bn, wm, wn;
+  float eff;  // relative per-step efficiency (LDS fragment reads per MFMA, barrier share)
+};
+// 0, 1: the 8-wave tiles of round 3 (deep 3x3 convs); 2-5: 4-wave tiles (round 4)
+constexpr Tile2 kT2[] = {{128, 256, 64, 64, 1.00f}, {256, 128, 64, 64, 1.00f}, {128, 128, 64, 64, 0.95f},
+                         {128, 64, 64, 32, 0.90f},  {64, 128, 32, 64, 0.90f},  {64, 64, 32, 32, 0.80f}};
+constexpr int kNT2 = sizeof(kT2) / sizeof(kT2[0]);
+
 struct Plan2 {
-  int tile;       // 0: 128 x 256, 1: 256 x 128, -1: not applicable
+  int tile;       // index into kT2, -1: not applicable
   int bm, bn, tiles_m, tiles_n, splits, nsteps, steps_per_split;
   long work_floats;
 };
 
-Plan2 plan2(long M, int Cout, int Cin, int ks) {
+#ifndef SEG_IG2_SMALL
+#define SEG_IG2_SMALL 1  // the 4-wave tiles (0: round-3 plan, 8-wave tiles only)
+#endif
+
+// Tile choice.  Round-3 rule first (8-wave tiles at >= 85 % utilisation, split-K to ~256
+// blocks) -- it keeps the deep 3x3 convs' launches as they were.  Otherwise (or when the
+// 8-wave tiles would leave the chip mostly idle) the 4-wave tiles are scored by utilisation
+// x efficiency x fill (fill: >= 2 blocks per CU counting split-K slices, which pay a slab
+// round trip each), for the small-image 1x1 / 3x3 convs.
+Plan2 plan2(long M, int Cout, int Cin, int ks, int force = -1) {
   Plan2 p{};
   p.tile = -1;
   const long K = (long)ks * ks * Cin;
-  if (M < 1 || Cout < 1 || Cin < 64 || (Cin & 7) || (ks != 1 && ks != 3)) return p;
-  double best = 0.0;
-  const int cand[2][2] = {{128, 256}, {256, 128}};
-  for (int c = 0; c < 2; ++c) {
-    const long tm = (M + cand[c][0] - 1) / cand[c][0], tn = (Cout + cand[c][1] - 1) / cand[c][1];
-    const double util = (double)M * Cout / ((double)tm * cand[c][0] * tn * cand[c][1]);
-    if (util > best + 1e-9) { best = util; p.tile = c; }
+  if (M < 1 || Cout < 1 || (Cin & 7) || (ks != 1 && ks != 3) || (ks == 3 && Cin < 64)) return p;
+  const int nsteps = (int)((K + kBK - 1) / kBK);
+  auto util = [&](int c) {
+    const long tm = (M + kT2[c].bm - 1) / kT2[c].bm, tn = (Cout + kT2[c].bn - 1) / kT2[c].bn;
+    return (double)M * Cout / ((double)tm * kT2[c].bm * tn * kT2[c].bn);
+  };
+  auto splits_for = [&](int c) {
+    const long tiles = ((M + kT2[c].bm - 1) / kT2[c].bm) * ((Cout + kT2[c].bn - 1) / kT2[c].bn);
+    int s = 1;
+    if (tiles < 256) s = (int)std::min<long>(std::min<long>((256 + tiles - 1) / tiles, nsteps / 8), 8);
+    return std::max(s, 1);
+  };
+  int best = -1;
+  if (force >= 0 && force < kNT2) {
+    best = force;
+  } else {
+    double bu = 0.0;
+    for (int c = 0; c < 2; ++c)
+      if (Cin >= 64 && util(c) > bu + 1e-9) { bu = util(c); best = c; }
+    const bool big_ok = best >= 0 && bu >= 0.85;
+    if (!big_ok) best = -1;
+    if (SEG_IG2_SMALL) {
+      const long tiles_big = big_ok ? ((M + kT2[best].bm - 1) / kT2[best].bm) * ((Cout + kT2[best].bn - 1) / kT2[best].bn)
+                                    : 0;
+      if (!big_ok || tiles_big < 128) {
+        double bs = 0.0;
+        int bsmall = -1;
+        for (int c = 2; c < kNT2; ++c) {
+          const long tiles = ((M + kT2[c].bm - 1) / kT2[c].bm) * ((Cout + kT2[c].bn - 1) / kT2[c].bn);
+          const int sp = splits_for(c);
+          const double fill = std::min(1.0, (double)(tiles * sp) / 512.0) / (sp > 1 ? 1.0 + 0.05 * sp : 1.0);
+          const double score = util(c) * kT2[c].eff * fill;
+          if (score > bs + 1e-9) { bs = score; bsmall = c; }
+        }
+        if (bsmall >= 0 && util(bsmall) >= 0.6) best = bsmall;
+      }
+    }
   }
-  if (best < 0.85) { p.tile = -1; return p; }  // mostly padding: the generic kernel fits better
-  p.bm = cand[p.tile][0];
-  p.bn = cand[p.tile][1];
+  if (best < 0) return p;
+  p.tile = best;
+  p.bm = kT2[best].bm;
+  p.bn = kT2[best].bn;
   p.tiles_m = (int)((M + p.bm - 1) / p.bm);
   p.tiles_n = (Cout + p.bn - 1) / p.bn;
-  p.nsteps = (int)((K + kBK - 1) / kBK);
+  p.nsteps = nsteps;
   const long tiles = (long)p.tiles_m * p.tiles_n;
-  int s = 1;
-  if (tiles < 256) s = (int)std::min<long>(std::min<long>((256 + tiles - 1) / tiles, p.nsteps / 8), 8);
-  if (s < 1) s = 1;
+  const int s = splits_for(best);
   p.steps_per_split = (p.nsteps + s - 1) / s;
   p.splits = (p.nsteps + p.steps_per_split - 1) / p.steps_per_split;  // no empty slice
   p.work_floats = p.splits > 1 ? tiles + tiles * p.splits * (long)p.bm * p.bn : 0;
   return p;
 }
 
+int g_ig2_force = -1;  // tuning hook (seg_igemm2_force_tile)
+
 }  // namespace
+
+// Tuning hook: force seg_conv_igemm2_bf16io's tile (index into its table; -1 = the plan).
+SEG_API int seg_igemm2_force_tile(int t) {
+  g_ig2_force = t;
+  return 0;
+}
 
 // Plan of seg_conv_igemm2_bf16io for an M x Cout GEMM over K = ks*ks*Cin: out[0] = tile
 // rows (the BN partials' row tiles), out[1] = row tiles, out[2] = split-K slices,
 // out[3] = workspace floats (tickets + slice tiles; 0 when unsplit).  Returns 1 when the
-// kernel applies (Cin >= 64, Cin % 8 == 0, little tile padding), else 0.
+// kernel applies (Cin % 8 == 0; 3x3: Cin >= 64; little tile padding), else 0.
 SEG_API int seg_conv_igemm2_plan(long M, int Cout, int Cin, int ks, long* out) {
-  const Plan2 p = plan2(M, Cout, Cin, ks);
+  const Plan2 p = plan2(M, Cout, Cin, ks, g_ig2_force);
   if (p.tile < 0) return 0;
   if (out) {
     out[0] = p.bm;
@@ -420,18 +516,16 @@ SEG_API int seg_conv_igemm2_plan(long M, int Cout, int Cin, int ks, long* out) {
   return 1;
 }
 
-// out = conv(in, W) (+bias) (+add), stride 1, pad (ks-1)/2, bf16 rows in / add / out,
-// bf16 packed weights (ldk % 8 == 0); fp32 accumulation, one rounding on the store.
-// stat (optional): BN partials [row tiles][2][Cout] of the plan's tile rows.  work: the
-// plan's workspace (zero it once before its first use; every call leaves its tickets zero).
-SEG_API int seg_conv_igemm2_bf16io(const __bf16* in, long ldin, int N, int H, int W, int Cin, const __bf16* wk,
-                                   int ldk, const float* bias, __bf16* out, long ldout, int Cout, int ks,
-                                   const __bf16* add, long ldadd, float* stat, float* work, hipStream_t stream) {
+static int igemm2_impl(const __bf16* in, long ldin, int N, int H, int W, int Cin, const __bf16* wk, int ldk,
+                       const float* bias, __bf16* out, long ldout, int Cout, int ks, const __bf16* add, long ldadd,
+                       float* stat, float* work, const float* xs, const float* xb, int xact, hipStream_t stream) {
   const long M = (long)N * H * W;
-  const Plan2 p = plan2(M, Cout, Cin, ks);
+  const Plan2 p = plan2(M, Cout, Cin, ks, g_ig2_force);
   if (p.tile < 0 || (ldin & 7) || (ldk & 7) || (ldout & 7) || (add && (ldadd & 7)) || ldk < ks * ks * Cin ||
       ((uintptr_t)in & 15) || ((uintptr_t)wk & 15) || ((uintptr_t)out & 15) || (add && ((uintptr_t)add & 15)) ||
       (p.splits > 1 && !work) || M > 0x7fffffffL)
+    return (int)hipErrorInvalidValue;
+  if (xs && (ks != 1 || !xb || Cin > kXfMax || xact < SEG_ACT_NONE || xact > SEG_ACT_RELU6))
     return (int)hipErrorInvalidValue;
   Igemm2Args a;
   a.in = in; a.ldin = ldin; a.wk = wk; a.ldk = ldk; a.bias = bias; a.add = add; a.ldadd = ldadd;
@@ -441,13 +535,46 @@ SEG_API int seg_conv_igemm2_bf16io(const __bf16* in, long ldin, int N, int H, in
   a.N = N; a.H = H; a.W = W; a.Cin = Cin; a.Cout = Cout; a.ks = ks; a.pad = (ks - 1) / 2;
   a.K = ks * ks * Cin; a.M = (int)M; a.nsteps = p.nsteps; a.steps_per_split = p.steps_per_split;
   a.splits = p.splits; a.tiles_m = p.tiles_m; a.tiles_n = p.tiles_n;
+  a.xs = xs; a.xb = xb; a.xact = xact;
   const int grid = p.tiles_m * p.tiles_n * p.splits;
-#define SEG_I2(BM, BN, KS) hipLaunchKernelGGL((igemm2_kernel<BM, BN, KS>), dim3(grid), dim3(kThreads), 0, stream, a)
-  if (p.tile == 0) {
-    if (ks == 3) SEG_I2(128, 256, 3); else SEG_I2(128, 256, 1);
-  } else {
-    if (ks == 3) SEG_I2(256, 128, 3); else SEG_I2(256, 128, 1);
+#define SEG_I2(BM, BN, WM, WN)                                                                                   \
+  do {                                                                                                          \
+    constexpr int nt = 64 * (BM / WM) * (BN / WN);                                                              \
+    if (xs) hipLaunchKernelGGL((igemm2_kernel<BM, BN, WM, WN, 1, true>), dim3(grid), dim3(nt), 0, stream, a);   \
+    else if (ks == 3) hipLaunchKernelGGL((igemm2_kernel<BM, BN, WM, WN, 3>), dim3(grid), dim3(nt), 0, stream, a); \
+    else hipLaunchKernelGGL((igemm2_kernel<BM, BN, WM, WN, 1>), dim3(grid), dim3(nt), 0, stream, a);            \
+  } while (0)
+  switch (p.tile) {
+    case 0: SEG_I2(128, 256, 64, 64); break;
+    case 1: SEG_I2(256, 128, 64, 64); break;
+    case 2: SEG_I2(128, 128, 64, 64); break;
+    case 3: SEG_I2(128, 64, 64, 32); break;
+    case 4: SEG_I2(64, 128, 32, 64); break;
+    default: SEG_I2(64, 64, 32, 32); break;
   }
 #undef SEG_I2
   SEG_RET_LAST();
+}
+
+// out = conv(in, W) (+bias) (+add), stride 1, pad (ks-1)/2, bf16 rows in / add / out,
+// bf16 packed weights (ldk % 8 == 0); fp32 accumulation, one rounding on the store.
+// stat (optional): BN partials [row tiles][2][Cout] of the plan's tile rows.  work: the
+// plan's workspace (zero it once before its first use; every call leaves its tickets zero).
+SEG_API int seg_conv_igemm2_bf16io(const __bf16* in, long ldin, int N, int H, int W, int Cin, const __bf16* wk,
+                                   int ldk, const float* bias, __bf16* out, long ldout, int Cout, int ks,
+                                   const __bf16* add, long ldadd, float* stat, float* work, hipStream_t stream) {
+  return igemm2_impl(in, ldin, N, H, W, Cin, wk, ldk, bias, out, ldout, Cout, ks, add, ldadd, stat, work, nullptr,
+                     nullptr, 0, stream);
+}
+
+// seg_conv_igemm2_bf16io of a 1x1 conv whose input is the raw output of a BatchNorm'd producer:
+// A = act(in * in_scale[c] + in_shift[c]) formed on the fragments (rounded to bf16 as the apply
+// pass would store it); Cin <= 2048.
+SEG_API int seg_conv_igemm2_bf16io_xf(const __bf16* in, long ldin, int N, int H, int W, int Cin, const __bf16* wk,
+                                      int ldk, const float* bias, __bf16* out, long ldout, int Cout, int ks,
+                                      const __bf16* add, long ldadd, float* stat, float* work, const float* in_scale,
+                                      const float* in_shift, int in_act, hipStream_t stream) {
+  if (!in_scale) return (int)hipErrorInvalidValue;
+  return igemm2_impl(in, ldin, N, H, W, Cin, wk, ldk, bias, out, ldout, Cout, ks, add, ldadd, stat, work, in_scale,
+                     in_shift, in_act, stream);
 }

@@ -94,6 +94,7 @@ PROTOTYPES = {
     "seg_conv_pw_row_tiles": (_I, [_L]),
     "seg_conv_pw": (_I, [_V, _L, _L, _I, _V, _I, _V, _V, _L, _I, _V, _L, _V, _V, _V, _I, _V]),
     "seg_conv_igemm2_bf16io": (_I, [_V, _L, _I, _I, _I, _I, _V, _I, _V, _V, _L, _I, _I, _V, _L, _V, _V, _V]),
+    "seg_igemm2_force_tile": (_I, [_I]),
     "seg_conv_halo2_ok": (_I, [_I, _I, _I, _I, _I]),
     "seg_conv_halo2_row_tiles": (_I, [_I, _I, _I]),
 }
@@ -113,6 +114,7 @@ PROTOTYPES["seg_conv_halo_bf16io"] = PROTOTYPES["seg_conv_halo"]
 PROTOTYPES["seg_conv_igemm_bf16io_w16"] = PROTOTYPES["seg_conv_igemm"]
 PROTOTYPES["seg_conv_halo_bf16io_w16"] = PROTOTYPES["seg_conv_halo"]
 PROTOTYPES["seg_conv_halo2_bf16io"] = PROTOTYPES["seg_conv_halo"]
+PROTOTYPES["seg_conv_igemm2_bf16io_xf"] = (_I, PROTOTYPES["seg_conv_igemm2_bf16io"][1][:-1] + [_V, _V, _I, _V])
 PROTOTYPES["seg_conv_igemm_bf16io_xf_w16"] = PROTOTYPES["seg_conv_igemm_bf16io_xf"]
 PROTOTYPES["seg_conv_pw_bf16io"] = PROTOTYPES["seg_conv_pw"]
 for _sfx in ("_xf", "_bf16io_xf", "_bf16io_xf_w16"):  # + in_scale, in_shift, in_act before the stream

@@ -266,11 +266,12 @@ class ConvOp:
                 rt.tcall("wino3_fwd", self.flops(), "seg_conv_wino", rt.ptr(i), i.ld, i.N, i.H, i.W, self.cin_pad,
                             self.wk_wf.data_ptr(), self.cin_pad, bias, rt.ptr(y), y.ld, self.cout, None, 0, statp,
                             work.data_ptr(), s)
-            elif self.ig2_f is not None:  # deep bf16io conv: 8-wave LDS-DMA implicit GEMM
+            elif self.ig2_f is not None:  # bf16io LDS-DMA implicit GEMM (deep 3x3, small-image 1x1)
                 work = rt.tmp(self.ig2_f[3], zero=True)
-                rt.tcall(f"igemm{self.ks}_fwd", self.flops(), "seg_conv_igemm2_bf16io", rt.ptr(i), i.ld, i.N, i.H, i.W,
-                         self.cin_pad, wk_ptr, ldk, bias, rt.ptr(y), y.ld, self.cout, self.ks, None, 0, statp,
-                         work.data_ptr(), s)
+                xf = self._in_xform(rt) if self.xform is not None else ()
+                rt.tcall(f"igemm{self.ks}_fwd", self.flops(), "seg_conv_igemm2_bf16io" + ("_xf" if xf else ""), rt.ptr(i),
+                         i.ld, i.N, i.H, i.W, self.cin_pad, wk_ptr, ldk, bias, rt.ptr(y), y.ld, self.cout, self.ks, None, 0,
+                         statp, work.data_ptr(), *xf, s)
             elif self.xform is not None:  # a conv applying its producer's lazy BN on load
                 name = "seg_conv_igemm_bf16io_xf" if rt.io else "seg_conv_igemm_bf16_xf" if self.bf else "seg_conv_igemm_xf"
                 if rt.io and self.w16_f:
@@ -636,11 +637,14 @@ class Program:
                 op.w16_f, op.w16_d = w16f, w16d
                 # the deep convs (3x3, or 1x1 with SEG_IGEMM2=all) on seg_conv_igemm2_bf16io
                 op.ig2_f = op.ig2_d = None
-                if (w16f and IGEMM2 != "0" and op.stride == 1 and op.pad == op.ks // 2 and y.M <= IGEMM2_MAX_ROWS
-                        and (op.ks == 3 or IGEMM2 == "all")):
+                ig2_ok = (op.ks == 3 and y.M <= IGEMM2_MAX_ROWS) or IGEMM2 == "all" or (
+                    op.ks == 1 and IGEMM2_1X1 and y.M <= IGEMM2_1X1_MAX_ROWS)
+                if w16f and IGEMM2 != "0" and op.stride == 1 and op.pad == op.ks // 2 and ig2_ok:
                     i = op.inp  # 16-byte rows: ld and channel offset multiples of 8 elements
                     rows16 = i.ld % 8 == 0 and i.off % 8 == 0 and y.ld % 8 == 0 and y.off % 8 == 0
-                    if rows16 and not (op.halo_f or op.h2_f) and op.xform is None and op.cin_pad == op.cin:
+                    # (a 1x1 consumer of a lazy BN applies it to its A fragments: seg_conv_igemm2_bf16io_xf)
+                    xf_ok = op.xform is None or (op.ks == 1 and op.cin <= 2048)
+                    if rows16 and not (op.halo_f or op.h2_f) and xf_ok and op.cin_pad == op.cin:
                         op.ig2_f = igemm2_plan(y.M, op.cout, op.cin_pad, op.ks)
                     if rows16 and not op.first and not (op.halo_d or op.h2_d) and op.cout % 8 == 0:
                         op.ig2_d = igemm2_plan(y.M, op.cin, op.cout, op.ks)
@@ -1244,6 +1248,10 @@ IGEMM2 = os.environ.get("SEG_IGEMM2", "3")
 # ... on images of at most this many output rows: measured per launch on UNet 512x1024 bf16io, igemm2 is 5-25 %
 # slower than the 4-wave implicit GEMM at 262k-4M rows and 1-6 % faster at 65k (profiles/r03k)
 IGEMM2_MAX_ROWS = int(os.environ.get("SEG_IGEMM2_MAX_ROWS", "65536"))
+# ... and the 1x1 convs of small images on its 4-wave tiles (round 4: the generic register-staged kernel
+# keeps one K chunk in flight and ran the encoder's 4k-65k-row 1x1 convs at 0.4-1.5 TB/s); SEG_IGEMM2_1X1=0 = off
+IGEMM2_1X1 = os.environ.get("SEG_IGEMM2_1X1", "1") == "1"
+IGEMM2_1X1_MAX_ROWS = int(os.environ.get("SEG_IGEMM2_1X1_MAX_ROWS", "65536"))
 # bf16io implicit GEMMs on bf16-packed weights (seg_conv_igemm_bf16io_w16); SEG_W16=0 keeps the fp32 packs
 W16 = os.environ.get("SEG_W16", "1") == "1"
 # fork the weight-gradient side stream after the layer's data gradient (measured: f32 +1.5 %, bf16io +-0)

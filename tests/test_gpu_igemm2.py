@@ -53,7 +53,11 @@ def pack16(w, Cout, Cin, ks):
 
 CASES = [  # (N, Cin, Cout, H, W, ks): split-K, dgrad-shaped, ragged M, taps spanning a K step, unsplit, 1x1
     (2, 1344, 256, 16, 32, 3), (8, 256, 1344, 8, 16, 3), (2, 128, 128, 33, 65, 3), (4, 288, 128, 64, 64, 3),
-    (32, 128, 128, 32, 64, 3), (2, 960, 256, 16, 16, 1)]
+    (32, 128, 128, 32, 64, 3), (2, 960, 256, 16, 16, 1),
+    # round 4: the 4-wave tiles -- the MobileNetV2 encoder's small-image 1x1 convs at bs=32 (M = 4k-65k rows),
+    # K < one 64-deep step, ragged N, a 3x3 with 152 inputs
+    (32, 960, 160, 8, 16, 1), (32, 96, 576, 16, 32, 1), (32, 32, 192, 32, 64, 1), (32, 144, 32, 32, 64, 1),
+    (32, 320, 1280, 8, 16, 1), (32, 24, 144, 16, 32, 1), (8, 152, 64, 32, 64, 3)]
 
 
 @pytest.mark.parametrize("N,Cin,Cout,H,W,ks", CASES)
@@ -82,10 +86,8 @@ def test_igemm2_vs_fp64_and_generic(N, Cin, Cout, H, W, ks):
     y, st = outs[0]
     for y2, st2 in outs[1:]:
         assert torch.equal(y, y2) and torch.equal(st, st2), "split-K combine must be deterministic"
-    if splits > 1:
-        bn = 256 if tile_rows == 128 else 128
-        tiles = ntiles * ((Cout + bn - 1) // bn)
-        assert int(work[:tiles].view(torch.int32).abs().sum()) == 0, "tickets re-armed"
+    if splits > 1:  # (the first ntiles of the tiles' tickets)
+        assert int(work[:ntiles].view(torch.int32).abs().sum()) == 0, "tickets re-armed"
     assert rel(y.float(), ref) < 4e-3  # the bf16 rounding of the stored output
     # statistics on the fp32 accumulator: tile sums and M2 about each tile's mean
     stv = st.view(ntiles, 2, Cout).double().cpu()
@@ -109,6 +111,78 @@ def test_igemm2_vs_fp64_and_generic(N, Cin, Cout, H, W, ks):
 
 
 def test_igemm2_plan_rejects_padding_heavy_shapes():
-    assert plan(4096, 80, 32, 3)[0] == 0      # Cin < 64
-    assert plan(4096, 288, 128, 3)[0] == 0    # 288 output channels: >= 25 % padded columns
+    assert plan(4096, 80, 32, 3)[0] == 0      # 3x3 with Cin < 64
+    assert plan(4096, 10, 16, 1)[0] == 0      # 10 output channels: >= 40 % padded columns on every tile
+    assert plan(4096, 16, 12, 1)[0] == 0      # Cin % 8
     assert plan(16384, 256, 1344, 3)[0] == 1
+    assert plan(4096, 288, 128, 3)[0] == 1    # round 4: a 4-wave 128x64 / 64x64 tile (was rejected)
+
+
+@pytest.mark.parametrize("tile", range(6))
+def test_igemm2_every_tile(tile):
+    """Each tile of the table, forced (seg_igemm2_force_tile), on one 3x3 and one 1x1 shape: unsplit
+    launches bitwise equal to the generic kernel, split ones within the bf16 rounding of fp64."""
+    try:
+        query("seg_igemm2_force_tile", tile)
+        for (N, Cin, Cout, H, W, ks) in ((2, 128, 96, 16, 40, 3), (4, 64, 200, 20, 24, 1)):
+            M = N * H * W
+            ok, (tile_rows, ntiles, splits, work_floats) = plan(M, Cout, Cin, ks)
+            assert ok
+            g = torch.Generator().manual_seed(tile * 7 + ks)
+            x = (torch.randn(M, Cin, generator=g)).to(BF).to(DEV)
+            w = (torch.randn(Cout, Cin, ks, ks, generator=g) * 0.1).to(DEV)
+            b = torch.randn(Cout, generator=g).to(DEV)
+            wk, ldk = pack16(w, Cout, Cin, ks)
+            work = torch.zeros(max(work_floats, 1), device=DEV)
+            y = torch.empty(M, Cout, device=DEV, dtype=BF)
+            st = torch.empty(ntiles * 2 * Cout, device=DEV)
+            call("seg_conv_igemm2_bf16io", x.data_ptr(), Cin, N, H, W, Cin, wk.data_ptr(), ldk, b.data_ptr(),
+                 y.data_ptr(), Cout, Cout, ks, None, 0, st.data_ptr(), work.data_ptr(), S())
+            y0 = torch.empty(M, Cout, device=DEV, dtype=BF)
+            call("seg_conv_igemm_bf16io_w16", x.data_ptr(), Cin, N, H, W, Cin, wk.data_ptr(), ldk, b.data_ptr(),
+                 y0.data_ptr(), Cout, H, W, Cout, ks, 1, ks // 2, None, 0, None, S())
+            torch.cuda.synchronize()
+            if splits == 1:
+                assert torch.equal(y, y0), (tile, ks)
+            else:
+                assert rel(y.float(), y0.float()) < 4e-3, (tile, ks)
+            stv = st.view(ntiles, 2, Cout).double().cpu()
+            assert rel(stv[:, 0].sum(0), y0.double().cpu().sum(0)) < 1e-2
+    finally:
+        query("seg_igemm2_force_tile", -1)
+
+
+@pytest.mark.parametrize("M,Cin,Cout,act", [(4096, 960, 160, 0), (16384, 576, 96, 2), (65536, 144, 32, 2),
+                                            (4096, 960, 320, 0)])
+def test_igemm2_xf_equals_generic_xf(M, Cin, Cout, act):
+    """The 1x1 lazy-BN variant (the inverted residuals' project convs: the dw conv's BatchNorm +
+    ReLU6 applied to the A fragments) against the generic kernel's transform-on-load: bitwise
+    when unsplit (the same bf16 values reach the same MFMA order), within bf16 rounding when split."""
+    g = torch.Generator().manual_seed(M + Cin)
+    y = (torch.randn(M, Cin, generator=g) * 1.5 + 0.3).to(BF).to(DEV)
+    scale = (torch.rand(Cin, generator=g) + 0.5).to(DEV)
+    shift = torch.randn(Cin, generator=g).to(DEV)
+    w = (torch.randn(Cout, Cin, 1, 1, generator=g) * 0.05).to(DEV)
+    wk, ldk = pack16(w, Cout, Cin, 1)
+    ok, (tile_rows, ntiles, splits, work_floats) = plan(M, Cout, Cin, 1)
+    assert ok
+    work = torch.zeros(max(work_floats, 1), device=DEV)
+    o2 = torch.empty(M, Cout, device=DEV, dtype=BF)
+    st = torch.empty(ntiles * 2 * Cout, device=DEV)
+    call("seg_conv_igemm2_bf16io_xf", y.data_ptr(), Cin, 1, 1, M, Cin, wk.data_ptr(), ldk, None, o2.data_ptr(), Cout,
+         Cout, 1, None, 0, st.data_ptr(), work.data_ptr(), scale.data_ptr(), shift.data_ptr(), act, S())
+    o1 = torch.empty(M, Cout, device=DEV, dtype=BF)
+    call("seg_conv_igemm_bf16io_xf_w16", y.data_ptr(), Cin, 1, 1, M, Cin, wk.data_ptr(), ldk, None, o1.data_ptr(),
+         Cout, 1, M, Cout, 1, 1, 0, None, 0, None, scale.data_ptr(), shift.data_ptr(), act, S())
+    torch.cuda.synchronize()
+    if splits == 1:
+        assert torch.equal(o1, o2)
+    else:
+        assert rel(o2.float(), o1.float()) < 4e-3
+    # and against float64 of the transformed, bf16-rounded input
+    z = (y.float() * scale + shift)
+    if act == 2:
+        z = z.clamp(0, 6)
+    z = z.to(BF).double().cpu()
+    ref = z @ w.view(Cout, Cin).to(BF).double().cpu().t()
+    assert rel(o2.float(), ref) < 4e-3

@@ -18,8 +18,8 @@
 //    trip), two chunks in flight while the four compute waves work on the third; chunks of
 //    the NEXT tile stream in while the current tile's epilogue runs;
 //  * out-of-image halo pixels and channels beyond Cin read a 16-byte zero page (no branch);
-//    halo rows are XOR-swizzled (16-byte chunk c of pixel hp at c ^ ((hp >> 2) & 3)) and
-//    weight rows padded by 16 bytes: conflict-free ds_read_b128 fragments;
+//    halo pixels and weight rows are XOR-swizzled in 16-byte chunks (halo: chunk c of pixel
+//    hp at c ^ ((hp >> 2) & 3); weights: wsw): conflict-free ds_read_b128 fragments;
 //  * v_mfma_f32_32x32x16_bf16, fp32 accumulation; compute wave w owns output row w of the
 //    tile (64 pixels = 2 MFMA row blocks) and all Cout columns (NI blocks of 32);
 //  * epilogue as halo.hip's: bias, BatchNorm tile partials ([tile][2][Cout]: sum, then M2
@@ -40,15 +40,19 @@ constexpr int BK = 32;                          // K chunk (input channels) = 64
 constexpr int HALO_SLOTS = HH * HWP * (BK / 8); // 16-byte slots per ring stage (1584)
 constexpr int HALO_DMA = (HALO_SLOTS + 63) / 64;  // DMA instructions per stage (25, 1 KB each)
 constexpr int STAGE = HALO_DMA * 1024;          // bytes per ring stage
-constexpr int NS = 3;                           // ring stages: two chunks in flight, one computing
 constexpr int kCompute = 4;                     // compute waves
 constexpr int kThreads = (kCompute + 1) * 64;   // + one loader wave
 constexpr int LDS_BYTES = 160 * 1024;
 constexpr int RED_FLOATS = 2 * kCompute * 96 + 96;  // two reduction row sets + tile means (NI <= 3)
-constexpr int W_OFF = NS * STAGE + RED_FLOATS * 4;
-constexpr int W_MAX = LDS_BYTES - W_OFF;        // bytes available for the resident weights
+// ring stages NS (3 or 4: NS - 1 chunks in flight while one computes), chosen per launch by what
+// the resident weights leave of the LDS
+constexpr int w_off(int ns) { return ns * STAGE + RED_FLOATS * 4; }
+constexpr int w_max(int ns) { return LDS_BYTES - w_off(ns); }  // bytes available for the resident weights
 
-static_assert(HALO_DMA <= 63, "vmcnt immediate");
+static_assert(2 * HALO_DMA <= 63, "vmcnt immediate");
+#ifndef SEG_H2_NS4
+#define SEG_H2_NS4 1  // four ring stages where the weights leave room (0: always three)
+#endif
 
 __device__ __attribute__((aligned(16))) unsigned g_h2_zero[4];
 
@@ -60,8 +64,15 @@ struct Halo2Args {
   __bf16* out; long ldout;
   float* stat;                     // BN partials [tiles][2][Cout] (256-pixel tiles) or null
   int N, H, W, Cin, Cout;
-  int tiles_w, tiles_h, ntiles, nk, wrow;  // wrow: LDS weight row stride (bytes) = nk * 64 + 16
+  int tiles_w, tiles_h, ntiles, nk, wrow;  // wrow: LDS weight row stride (bytes) = nk * 64
 };
+
+// Weight-row chunk swizzle (row stride nk * 64 bytes, no padding): the 16 lanes of a
+// ds_read_b128 group read 16 rows' chunk q on 16 distinct 16-byte bank quads for every nk
+// (checked exhaustively for nk 1-8 against the gfx950 lane grouping).
+__device__ __forceinline__ int wsw(int q, int row, int nk) {
+  return (nk & 1) ? q ^ ((row >> 2) & 3) : (nk & 2) ? q ^ ((row >> 1) & 7) : q ^ (row & 15);
+}
 
 __device__ __forceinline__ void dma16(const void* src, char* lds) {
   __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
@@ -82,9 +93,10 @@ __device__ __forceinline__ void wait_vm() {
   __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | 0x0F70);  // vmcnt N (6 bits split), others untouched
 }
 
-template <int NI>
+template <int NI, int NS>
 __global__ __launch_bounds__(kThreads) void halo2_kernel(Halo2Args a) {
   constexpr int BNC = 32 * NI;
+  constexpr int W_OFF = w_off(NS);
   __shared__ __attribute__((aligned(1024))) char smem[LDS_BYTES];
   char* ring = smem;
   float* red0 = reinterpret_cast<float*>(smem + NS * STAGE);  // [kCompute][BNC]
@@ -100,7 +112,7 @@ __global__ __launch_bounds__(kThreads) void halo2_kernel(Halo2Args a) {
   const int S = (t_end - t_beg) * nk;  // (tile, K chunk) steps of this block
 
   // ---- resident weights: row (tap, co) = the Cin (padded to nk * 32) weights of one tap and
-  // output channel, 16-byte chunks, then 16 bytes of padding (conflict-free fragment reads)
+  // output channel in 16-byte chunks, chunk q stored at wsw(q, row) (conflict-free fragment reads)
   if (wave < kCompute) {  // (the loader wave starts its DMA meanwhile)
     const int qpr = nk * 4;  // 16-byte chunks per row
     for (int i = tid; i < 9 * BNC * qpr; i += kCompute * 64) {
@@ -108,7 +120,7 @@ __global__ __launch_bounds__(kThreads) void halo2_kernel(Halo2Args a) {
       const int tap = row / BNC, co = row - tap * BNC, ci = q * 8;
       f32x4 v = {0.f, 0.f, 0.f, 0.f};
       if (co < a.Cout && ci < a.Cin) v = *reinterpret_cast<const f32x4*>(a.wk + (long)co * a.ldk + tap * a.Cin + ci);
-      *reinterpret_cast<f32x4*>(Ws + row * a.wrow + q * 16) = v;
+      *reinterpret_cast<f32x4*>(Ws + row * a.wrow + wsw(q, row, nk) * 16) = v;
     }
   }
 
@@ -117,36 +129,51 @@ __global__ __launch_bounds__(kThreads) void halo2_kernel(Halo2Args a) {
     // slot g = 64 j + lane of a stage: halo pixel hp = g >> 2, physical chunk g & 3, logical
     // chunk (g & 3) ^ ((hp >> 2) & 3) -- the channel offset of a lane is the same for every j
     const int cof = 8 * ((lane & 3) ^ ((lane >> 4) & 3));
-    int poff[HALO_DMA];  // per tile: element offset of each slot's pixel row, -1 outside the image
-    int cur_tile = -1;
+    // tile-invariant slot geometry: element offset of the slot's pixel from the halo origin
+    // (h0 - 1, w0 - 1), and its (hy, hx) for the edge tiles' bounds test (-1: beyond the halo)
+    int rel[HALO_DMA], hyx[HALO_DMA];
+#pragma unroll
+    for (int j = 0; j < HALO_DMA; ++j) {
+      const int hp = 16 * j + (lane >> 2);
+      const int hy = hp / HWP, hx = hp - hy * HWP;
+      rel[j] = (hy * a.W + hx) * (int)a.ldin;
+      hyx[j] = hp < HH * HWP ? (hy << 8 | hx) : -1;
+    }
+    int cur_tile = -1, org = 0;
+    unsigned okm = 0;  // slots of the current tile holding in-image pixels
     auto issue = [&](int step) {
       const int tl = t_beg + step / nk, kc = step - (step / nk) * nk;
-      if (tl != cur_tile) {
+      if (tl != cur_tile) {  // per tile: one scalar origin, and bounds tests only on the image edges
         cur_tile = tl;
         const int tw_i = tl % a.tiles_w, rest = tl / a.tiles_w;
         const int th_i = rest % a.tiles_h, n = rest / a.tiles_h;
         const int h0 = th_i * TH - 1, w0 = tw_i * TW - 1;
+        org = ((n * a.H + h0) * a.W + w0) * (int)a.ldin;
+        const bool interior = h0 >= 0 && h0 + HH <= a.H && w0 >= 0 && w0 + HWP <= a.W;
+        okm = 0;
 #pragma unroll
         for (int j = 0; j < HALO_DMA; ++j) {
-          const int hp = 16 * j + (lane >> 2);
-          const int hy = hp / HWP, hx = hp - hy * HWP;
-          const int gy = h0 + hy, gx = w0 + hx;
-          const bool ok = hp < HH * HWP && (unsigned)gy < (unsigned)a.H && (unsigned)gx < (unsigned)a.W;
-          poff[j] = ok ? (int)(((long)(n * a.H + gy) * a.W + gx) * a.ldin) : -1;
+          const int hy = hyx[j] >> 8, hx = hyx[j] & 255;
+          const bool ok = hyx[j] >= 0 && (interior || ((unsigned)(h0 + hy) < (unsigned)a.H &&
+                                                       (unsigned)(w0 + hx) < (unsigned)a.W));
+          okm |= ok ? 1u << j : 0u;
         }
       }
       const int ch = kc * BK + cof;
-      const bool cok = ch < a.Cin;
+      const unsigned m = ch < a.Cin ? okm : 0u;
       char* st = ring + (step % NS) * STAGE;
 #pragma unroll
       for (int j = 0; j < HALO_DMA; ++j) {
-        const bool ok = cok && poff[j] >= 0;
-        dma16(ok ? (const void*)(a.in + poff[j] + ch) : (const void*)g_h2_zero, st + j * 1024);
+        const bool ok = (m >> j) & 1u;
+        dma16(ok ? (const void*)(a.in + (org + rel[j] + ch)) : (const void*)g_h2_zero, st + j * 1024);
       }
     };
     for (int s = 0; s < NS - 1 && s < S; ++s) issue(s);
     for (int s = 0; s < S; ++s) {
-      if (s + 1 < S) wait_vm<HALO_DMA>();  // step s has landed (step s + 1 may still be in flight)
+      // step s has landed; the steps issued after it (up to NS - 2) may still be in flight
+      const int ahead = min(NS - 2, S - 1 - s);
+      if (NS >= 4 && ahead >= 2) wait_vm<2 * HALO_DMA>();
+      else if (ahead >= 1) wait_vm<HALO_DMA>();
       else wait_vm<0>();
       raw_barrier();                         // A: every compute wave is done with step s - 1's stage
       if (s + NS - 1 < S) issue(s + NS - 1); // ... which this refills
@@ -177,7 +204,6 @@ __global__ __launch_bounds__(kThreads) void halo2_kernel(Halo2Args a) {
     wait_lgkm0();   // this wave's fragment reads of the previous stage (and its weight stores) are done
     raw_barrier();  // A
     const char* Hs = ring + (s % NS) * STAGE;
-    const char* Wk = Ws + kc * 64;
     const int rem = a.Cin - kc * BK;  // valid channels of this chunk (the last one may be half empty)
 #pragma unroll
     for (int tap = 0; tap < 9; ++tap) {
@@ -193,8 +219,10 @@ __global__ __launch_bounds__(kThreads) void halo2_kernel(Halo2Args a) {
           af[mi] = *reinterpret_cast<const bf16x8*>(Hs + hp * 64 + 16 * (c ^ ((hp >> 2) & 3)));
         }
 #pragma unroll
-        for (int ni = 0; ni < NI; ++ni)
-          bfr[ni] = *reinterpret_cast<const bf16x8*>(Wk + (tap * BNC + ni * 32 + fr) * a.wrow + c * 16);
+        for (int ni = 0; ni < NI; ++ni) {
+          const int row = tap * BNC + ni * 32 + fr;
+          bfr[ni] = *reinterpret_cast<const bf16x8*>(Ws + row * a.wrow + wsw(4 * kc + c, row, nk) * 16);
+        }
 #pragma unroll
         for (int mi = 0; mi < 2; ++mi)
 #pragma unroll
@@ -280,7 +308,7 @@ __global__ __launch_bounds__(kThreads) void halo2_kernel(Halo2Args a) {
 
 int h2_nk(int Cin) { return (Cin + BK - 1) / BK; }
 int h2_ni(int Cout) { return (Cout + 31) / 32; }
-int h2_wbytes(int Cin, int Cout) { return 9 * 32 * h2_ni(Cout) * (h2_nk(Cin) * 64 + 16); }
+int h2_wbytes(int Cin, int Cout) { return 9 * 32 * h2_ni(Cout) * h2_nk(Cin) * 64; }
 
 }  // namespace
 
@@ -288,7 +316,7 @@ int h2_wbytes(int Cin, int Cout) { return 9 * 32 * h2_ni(Cout) * (h2_nk(Cin) * 6
 // Cin % 8 == 0, Cout <= 96 and the weights (9 x Cout x Cin, padded) fit in LDS beside the ring.
 SEG_API int seg_conv_halo2_ok(int N, int H, int W, int Cin, int Cout) {
   return (N > 0 && H > 0 && W > 0 && H % TH == 0 && W % TW == 0 && Cin >= 8 && Cin % 8 == 0 && Cout > 0 &&
-          Cout <= 96 && h2_wbytes(Cin, Cout) <= W_MAX && (long)N * H * W * 128 < 0x7fffffffL) ? 1 : 0;
+          Cout <= 96 && h2_wbytes(Cin, Cout) <= w_max(3) && (long)N * H * W * 128 < 0x7fffffffL) ? 1 : 0;
 }
 
 // BN-partial row tiles of seg_conv_halo2_bf16io (256 pixels each; the layout of seg_conv_halo_row_tiles).
@@ -309,7 +337,7 @@ SEG_API int seg_conv_halo2_bf16io(const __bf16* in, long ldin, int N, int H, int
   a.in = in; a.ldin = ldin; a.wk = wk; a.ldk = ldk; a.bias = bias; a.add = add; a.ldadd = ldadd;
   a.out = out; a.ldout = ldout; a.stat = stat; a.N = N; a.H = H; a.W = W; a.Cin = Cin; a.Cout = Cout;
   a.tiles_w = W / TW; a.tiles_h = H / TH; a.ntiles = N * a.tiles_h * a.tiles_w;
-  a.nk = h2_nk(Cin); a.wrow = a.nk * 64 + 16;
+  a.nk = h2_nk(Cin); a.wrow = a.nk * 64;
   int cus = 256;
   {
     int dev = 0;
@@ -320,8 +348,15 @@ SEG_API int seg_conv_halo2_bf16io(const __bf16* in, long ldin, int N, int H, int
   }
   const int grid = std::min(a.ntiles, cus);
   const int ni = h2_ni(Cout);
-  if (ni == 1) hipLaunchKernelGGL((halo2_kernel<1>), dim3(grid), dim3(kThreads), 0, stream, a);
-  else if (ni == 2) hipLaunchKernelGGL((halo2_kernel<2>), dim3(grid), dim3(kThreads), 0, stream, a);
-  else hipLaunchKernelGGL((halo2_kernel<3>), dim3(grid), dim3(kThreads), 0, stream, a);
+  const bool ns4 = h2_wbytes(Cin, Cout) <= w_max(4) && SEG_H2_NS4;
+#define SEG_H2(NI)                                                                                  \
+  do {                                                                                               \
+    if (ns4) hipLaunchKernelGGL((halo2_kernel<NI, 4>), dim3(grid), dim3(kThreads), 0, stream, a);   \
+    else hipLaunchKernelGGL((halo2_kernel<NI, 3>), dim3(grid), dim3(kThreads), 0, stream, a);       \
+  } while (0)
+  if (ni == 1) SEG_H2(1);
+  else if (ni == 2) SEG_H2(2);
+  else SEG_H2(3);
+#undef SEG_H2
   SEG_RET_LAST();
 }

@@ -63,7 +63,7 @@ CASES = [  # N, Cin, Cout, H, W, mode (0 forward, 1 data gradient), bias, addend
     (4, 80, 32, 128, 256, 0, True, False),   # 512 tiles: two per block
     (3, 32, 32, 100, 256, 1, False, False),  # 300 tiles: uneven split over 256 blocks
     (1, 16, 16, 4, 64, 0, True, False),      # Cin = 16: one half-empty K chunk, a single tile
-    (2, 40, 96, 12, 64, 0, True, True),      # nk = 2 with an 8-channel tail, Cout 96
+    (2, 40, 64, 12, 64, 0, True, True),      # nk = 2 with an 8-channel tail, addend
 ]
 
 

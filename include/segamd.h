@@ -495,6 +495,9 @@ int seg_conv_igemm2_bf16io(const seg_bf16* in, long ldin, int N, int H, int W, i
  * pass would store it) -- the project convs of the inverted residuals (torchvision, via
  * src/unet.py:15-19). */
 int seg_igemm2_force_tile(int t);
+/* Tuning hook: split-K of the 4-wave tiles up to target_blocks blocks with >= min_steps 64-deep K
+ * steps per slice (defaults 512, 3); values <= 0 keep the current setting. */
+int seg_igemm2_tune(int target_blocks, int min_steps);
 int seg_conv_igemm2_bf16io_xf(const seg_bf16* in, long ldin, int N, int H, int W, int Cin, const seg_bf16* wk,
                               int ldk, const float* bias, seg_bf16* out, long ldout, int Cout, int ks,
                               const seg_bf16* add, long ldadd, float* stat, float* work, const float* in_scale,

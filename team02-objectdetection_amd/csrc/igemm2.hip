@@ -418,6 +418,10 @@ constexpr Tile2 kT2[] = {{128, 256, 64, 64, 1.00f}, {256, 128, 64, 64, 1.00f}, {
                          {128, 64, 64, 32, 0.90f},  {64, 128, 32, 64, 0.90f},  {64, 64, 32, 32, 0.80f}};
 constexpr int kNT2 = sizeof(kT2) / sizeof(kT2[0]);
 
+int g_ig2_force = -1;      // tuning hooks (seg_igemm2_force_tile, seg_igemm2_tune)
+int g_ig2_target = 512;    // 4-wave tiles: split-K up to this many blocks ...
+int g_ig2_minsteps = 3;    // ... keeping at least this many 64-deep K steps per slice
+
 struct Plan2 {
   int tile;       // index into kT2, -1: not applicable
   int bm, bn, tiles_m, tiles_n, splits, nsteps, steps_per_split;
@@ -444,9 +448,13 @@ Plan2 plan2(long M, int Cout, int Cin, int ks, int force = -1) {
     return (double)M * Cout / ((double)tm * kT2[c].bm * tn * kT2[c].bn);
   };
   auto splits_for = [&](int c) {
+    // the 8-wave tiles: split-K to ~256 blocks with >= 8 K steps per slice (round 3); the 4-wave
+    // tiles of the small images: to ~g_ig2_target blocks with >= g_ig2_minsteps steps per slice
     const long tiles = ((M + kT2[c].bm - 1) / kT2[c].bm) * ((Cout + kT2[c].bn - 1) / kT2[c].bn);
+    const long target = c < 2 ? 256 : g_ig2_target;
+    const long minst = c < 2 ? 8 : g_ig2_minsteps;
     int s = 1;
-    if (tiles < 256) s = (int)std::min<long>(std::min<long>((256 + tiles - 1) / tiles, nsteps / 8), 8);
+    if (tiles < target) s = (int)std::min<long>(std::min<long>((target + tiles - 1) / tiles, nsteps / minst), 8);
     return std::max(s, 1);
   };
   int best = -1;
@@ -490,9 +498,14 @@ Plan2 plan2(long M, int Cout, int Cin, int ks, int force = -1) {
   return p;
 }
 
-int g_ig2_force = -1;  // tuning hook (seg_igemm2_force_tile)
-
 }  // namespace
+
+// Tuning hook: the 4-wave tiles' split-K targets (blocks, minimum K steps per slice); <= 0 keeps a value.
+SEG_API int seg_igemm2_tune(int target_blocks, int min_steps) {
+  if (target_blocks > 0) g_ig2_target = target_blocks;
+  if (min_steps > 0) g_ig2_minsteps = min_steps;
+  return 0;
+}
 
 // Tuning hook: force seg_conv_igemm2_bf16io's tile (index into its table; -1 = the plan).
 SEG_API int seg_igemm2_force_tile(int t) {

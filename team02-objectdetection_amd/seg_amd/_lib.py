@@ -95,6 +95,7 @@ PROTOTYPES = {
     "seg_conv_pw": (_I, [_V, _L, _L, _I, _V, _I, _V, _V, _L, _I, _V, _L, _V, _V, _V, _I, _V]),
     "seg_conv_igemm2_bf16io": (_I, [_V, _L, _I, _I, _I, _I, _V, _I, _V, _V, _L, _I, _I, _V, _L, _V, _V, _V]),
     "seg_igemm2_force_tile": (_I, [_I]),
+    "seg_igemm2_tune": (_I, [_I, _I]),
     "seg_conv_halo2_ok": (_I, [_I, _I, _I, _I, _I]),
     "seg_conv_halo2_row_tiles": (_I, [_I, _I, _I]),
 }

@@ -68,7 +68,11 @@ def main():
     ap.add_argument("--reps", type=int, default=30)
     ap.add_argument("--only", default="")
     ap.add_argument("--csv", default=None)
+    ap.add_argument("--ig2-tune", default="", help="target_blocks,min_steps of the igemm2 4-wave split-K")
     a = ap.parse_args()
+    if a.ig2_tune:
+        t, m = (int(v) for v in a.ig2_tune.split(","))
+        query("seg_igemm2_tune", t, m)
     g = torch.Generator().manual_seed(0)
     rows = []
     if a.only in ("", "halo"):

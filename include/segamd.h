@@ -518,6 +518,19 @@ int seg_conv_halo2_bf16io(const seg_bf16* in, long ldin, int N, int H, int W, in
                           const float* bias, seg_bf16* out, long ldout, int Cout, const seg_bf16* add, long ldadd,
                           float* stat, hipStream_t stream);
 
+/* seg_conv_wgrad2_bf16io: the weight gradient of those narrow 3x3 convs (replaces aten's
+ * convolution_backward weight path of src/unet.py:58,61 where Cout <= 64; csrc/wgrad2.hip): persistent
+ * blocks walk 4 x 64-pixel tiles, the input halo and dY rows streamed into LDS by LDS-DMA once per tile
+ * and 32-channel chunk, transposing LDS reads into v_mfma_f32_32x32x16_bf16.  Writes one fp32 partial
+ * slab per block, part[seg_conv_wgrad2_blocks(N, H, W)][Cout][9][r4(Cin)] -- the layout of
+ * seg_conv_wgrad's slabs, summed by seg_conv_wgrad_reduce(part, blocks, dw, Cout, Cin, 3, 0, acc).
+ * dy: [N*H*W][lddy] (Cout channels), x: [N*H*W][ldx] (Cin channels); ld % 8 == 0, 16-byte aligned.
+ * seg_conv_wgrad2_ok: H % 4 == 0, W % 64 == 0, Cin % 8 == 0, Cout % 8 == 0, Cout <= 64. */
+int seg_conv_wgrad2_ok(int N, int H, int W, int Cin, int Cout);
+int seg_conv_wgrad2_blocks(int N, int H, int W);
+int seg_conv_wgrad2_bf16io(const seg_bf16* dy, long lddy, const seg_bf16* x, long ldx, int N, int H, int W, int Cin,
+                           int Cout, float* part, hipStream_t stream);
+
 /* Build identity (host only): copies the SHA-256 (64 hex chars + NUL) of the sources this
  * library was built from -- every csrc file, this header, compiler and flags
  * (seg_amd/build.py source_hash) -- into out when cap > 64; returns the length.  The

@@ -97,6 +97,9 @@ PROTOTYPES = {
     "seg_igemm2_force_tile": (_I, [_I]),
     "seg_igemm2_tune": (_I, [_I, _I]),
     "seg_conv_halo2_ok": (_I, [_I, _I, _I, _I, _I]),
+    "seg_conv_wgrad2_ok": (_I, [_I, _I, _I, _I, _I]),
+    "seg_conv_wgrad2_blocks": (_I, [_I, _I, _I]),
+    "seg_conv_wgrad2_bf16io": (_I, [_V, _L, _V, _L, _I, _I, _I, _I, _I, _V, _V]),
     "seg_conv_halo2_row_tiles": (_I, [_I, _I, _I]),
 }
 # bf16-storage variants: same C signature shape as their fp32 namesakes (pointers stay void*)

@@ -189,6 +189,7 @@ class ConvOp:
         # bf16io persistent LDS-DMA variant (seg_conv_halo2_bf16io) where it applies
         self.halo_f = self.halo_d = False
         self.h2_f = self.h2_d = False
+        self.w2 = False  # weight gradient on seg_conv_wgrad2_bf16io (narrow bf16io 3x3)
         # bf16 math (Program.math == "bf16"): seg_conv_igemm_bf16 / seg_conv_wgrad_bf16
         self.bf = False
         # bf16io: wk_f / wk_d packed as bf16 for seg_conv_igemm_bf16io_w16 (Program._build_pack)
@@ -424,6 +425,12 @@ class ConvOp:
                 rt.tcall("wino3_wgrad", self.flops(), "seg_conv_wino_wgrad", dYp, dY.ld, rt.ptr(i), i.ld, y.N, y.H,
                             y.W, self.cin_pad, self.cout, part.data_ptr(), splits, s)
                 rt.call("seg_conv_wino_wgrad_reduce", part.data_ptr(), splits, gw, self.cout, self.cin, self.cin_pad, 0, s)
+            elif self.w2:  # narrow bf16io 3x3: persistent LDS-halo weight gradient, one slab per block
+                blocks = query("seg_conv_wgrad2_blocks", y.N, y.H, y.W)
+                part = rt.tmp(blocks * self.cout * 9 * self.cin_pad)
+                rt.tcall("igemm3_wgrad", self.flops(), "seg_conv_wgrad2_bf16io", dYp, dY.ld, rt.ptr(i), i.ld, y.N, y.H,
+                         y.W, self.cin_pad, self.cout, part.data_ptr(), s)
+                rt.call("seg_conv_wgrad_reduce", part.data_ptr(), blocks, gw, self.cout, self.cin, 3, 0, 0, s)
             else:
                 splits = query("seg_conv_wgrad_splits_bf16" if self.bf else "seg_conv_wgrad_splits", M, self.cout,
                                self.cin_pad, self.ks)
@@ -618,6 +625,11 @@ class Program:
                 # bf16 math: every dense / pointwise conv (fwd, dgrad, wgrad) on the bf16 implicit GEMM
                 op.wino_f = op.wino_d = op.wino_w = op.halo_f = op.halo_d = False
                 op.h2_f = op.h2_d = False
+                # narrow bf16io 3x3 weight gradients on seg_conv_wgrad2_bf16io (SEG_WGRAD2=0: the implicit GEMM)
+                op.w2 = (self.math == "bf16io" and WGRAD2 and op.ks == 3 and op.stride == 1 and op.pad == 1
+                         and op.xform is None and op.cin_pad == op.cin and y.ld % 8 == 0 and op.inp.ld % 8 == 0
+                         and op.inp.off % 8 == 0
+                         and bool(query("seg_conv_wgrad2_ok", y.N, y.H, y.W, op.cin_pad, op.cout)))
                 if self.math == "bf16io" and op.ks == 3 and op.stride == 1 and op.pad == 1:
                     # narrow convs: the persistent LDS-DMA halo kernel (seg_conv_halo2_bf16io, bf16 packed
                     # weights resident in LDS) where it applies, else the LDS-halo direct conv
@@ -1233,6 +1245,8 @@ WINOGRAD_DGRAD = os.environ.get("SEG_WINO_DGRAD", "1") == "1"
 HALO_BF16 = os.environ.get("SEG_HALO_BF16", "1") == "1"
 # ... and the persistent LDS-DMA halo kernel (seg_conv_halo2_bf16io) where it applies; SEG_HALO2=0 = off
 HALO2 = os.environ.get("SEG_HALO2", "1") == "1"
+# ... and their weight gradients on the persistent LDS-halo kernel (seg_conv_wgrad2_bf16io); SEG_WGRAD2=0 = off
+WGRAD2 = os.environ.get("SEG_WGRAD2", "1") == "1"
 # lazy BatchNorm for 1x1 consumers (the inverted residuals' project convs, OutConv's last
 # conv): SEG_LAZY_PW=0 keeps the separate BN-apply pass (read at program build)
 LAZY_PW = os.environ.get("SEG_LAZY_PW", "1") == "1"

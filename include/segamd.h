@@ -531,6 +531,30 @@ int seg_conv_wgrad2_blocks(int N, int H, int W);
 int seg_conv_wgrad2_bf16io(const seg_bf16* dy, long lddy, const seg_bf16* x, long ldx, int N, int H, int W, int Cin,
                            int Cout, float* part, hipStream_t stream);
 
+/* Depthwise 3x3 convs of the bf16io configuration on LDS-DMA tiles (csrc/dw2.hip; replace the
+ * groups=C Conv2d of torchvision's InvertedResidual, reached through src/unet.py:15-19,34-38, and its
+ * convolution_backward).  A block owns an output tile (8 x 32 pixels at stride 1, 4 x 32 at stride 2)
+ * of a 64-channel slice; the input tile with its halo is copied into LDS once, the lazy BN of the input
+ * (in_scale / in_shift / in_act, as seg_dw_fwd) applied there in place and rounded to bf16.  Rows are
+ * 16-byte aligned with ld % 8 == 0 and C % 8 == 0 (seg_dw2_ok).
+ * seg_dw2_fwd_bf16io: as seg_dw_fwd_bf16io, plus stat (or NULL): the BatchNorm tile partials of the
+ * output, [seg_dw2_stat_tiles(...)][2][C] (tile sum, M2 about the tile mean; *tile_rows rows each) for
+ * seg_bn_stats_tiles -- only when seg_dw2_stat_tiles is non-zero (the tiles divide Ho x Wo).
+ * seg_dw2_dgrad_bf16io: as seg_dw_dgrad_bf16io (bitwise its result).
+ * seg_dw2_wgrad_bf16io: as seg_dw_wgrad_bf16io with part[seg_dw2_wgrad_blocks(N, Ho, Wo, C, stride)][9][C]
+ * (reduce with seg_conv_wgrad_reduce(part, blocks, dw, C, 1, 3, 1, acc)); fixed-order, deterministic. */
+int seg_dw2_ok(int C, int stride);
+int seg_dw2_stat_tiles(int N, int Ho, int Wo, int stride, int* tile_rows);
+int seg_dw2_fwd_bf16io(const seg_bf16* in, long ldin, int N, int H, int W, int C, const float* in_scale,
+                       const float* in_shift, int in_act, const float* wk, seg_bf16* out, long ldout, int Ho, int Wo,
+                       int stride, float* stat, hipStream_t stream);
+int seg_dw2_dgrad_bf16io(const seg_bf16* dy, long lddy, int N, int Ho, int Wo, int C, const float* wk, seg_bf16* dx,
+                         long lddx, int H, int W, int stride, int accumulate, hipStream_t stream);
+long seg_dw2_wgrad_blocks(int N, int Ho, int Wo, int C, int stride);
+int seg_dw2_wgrad_bf16io(const seg_bf16* dy, long lddy, const seg_bf16* x, long ldx, int N, int H, int W, int C,
+                         const float* in_scale, const float* in_shift, int in_act, int Ho, int Wo, int stride,
+                         float* part, hipStream_t stream);
+
 /* Build identity (host only): copies the SHA-256 (64 hex chars + NUL) of the sources this
  * library was built from -- every csrc file, this header, compiler and flags
  * (seg_amd/build.py source_hash) -- into out when cap > 64; returns the length.  The

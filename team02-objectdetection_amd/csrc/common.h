@@ -177,3 +177,14 @@ __device__ __forceinline__ f32x4 bilerp4(f32x4 v00, f32x4 v01, f32x4 v10, f32x4 
 }
 
 #define SEG_RET_LAST() return (int)hipGetLastError()
+
+// Compute units of the current device (256 on MI355X; also the answer without a device, so
+// host-side slab sizing queried on a CPU-only machine matches the GPU's).
+static inline int seg_num_cus() {
+  int dev = 0, n = 0;
+  if (hipGetDevice(&dev) == hipSuccess &&
+      hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && n > 0)
+    return n;
+  (void)hipGetLastError();
+  return 256;
+}

@@ -101,6 +101,10 @@ PROTOTYPES = {
     "seg_conv_wgrad2_blocks": (_I, [_I, _I, _I]),
     "seg_conv_wgrad2_bf16io": (_I, [_V, _L, _V, _L, _I, _I, _I, _I, _I, _V, _V]),
     "seg_conv_halo2_row_tiles": (_I, [_I, _I, _I]),
+    "seg_dw2_ok": (_I, [_I, _I]),
+    "seg_dw2_stat_tiles": (_I, [_I, _I, _I, _I, _V]),
+    "seg_dw2_fwd_bf16io": (_I, [_V, _L, _I, _I, _I, _I, _V, _V, _I, _V, _V, _L, _I, _I, _I, _V, _V]),
+    "seg_dw2_wgrad_blocks": (_L, [_I, _I, _I, _I, _I]),
 }
 # bf16-storage variants: same C signature shape as their fp32 namesakes (pointers stay void*)
 for _n in ("seg_add", "seg_bn_stats", "seg_bn_apply", "seg_bn_backward", "seg_colsum", "seg_dw_fwd", "seg_dw_dgrad",
@@ -108,6 +112,8 @@ for _n in ("seg_add", "seg_bn_stats", "seg_bn_apply", "seg_bn_backward", "seg_co
            "seg_upsample_to_nchw", "seg_nchw_to_nhwc", "seg_maxpool2_fwd", "seg_maxpool2_bwd"):
     PROTOTYPES[_n + "_bf16io"] = PROTOTYPES[_n]
 PROTOTYPES["seg_conv_igemm_bf16io"] = PROTOTYPES["seg_conv_igemm"]
+PROTOTYPES["seg_dw2_dgrad_bf16io"] = PROTOTYPES["seg_dw_dgrad"]
+PROTOTYPES["seg_dw2_wgrad_bf16io"] = PROTOTYPES["seg_dw_wgrad"]
 PROTOTYPES["seg_conv_wgrad_bf16io"] = PROTOTYPES["seg_conv_wgrad"]
 # lazy-BN (input transform) variants: + in_scale, in_shift, in_act before the stream
 for _n in ("seg_conv_igemm", "seg_conv_wgrad"):

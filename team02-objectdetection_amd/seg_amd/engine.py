@@ -34,7 +34,8 @@ from ._lib import call, query as _query
 # arguments: memoised, so a training step does not pay a ctypes call for each of them.
 _PURE_QUERIES = {"seg_chan_workspace_floats", "seg_conv_wgrad_splits", "seg_conv_wgrad_splits_bf16", "seg_dw_wgrad_blocks",
                  "seg_conv_igemm_splits", "seg_ce_workspace_floats", "seg_conv_wino_row_tiles", "seg_conv_wino_tile_rows",
-                 "seg_conv_halo_row_tiles", "seg_conv_wino_wgrad_splits"}
+                 "seg_conv_halo_row_tiles", "seg_conv_wino_wgrad_splits", "seg_dw2_ok",
+                 "seg_dw2_wgrad_blocks"}
 _QCACHE = {}
 
 
@@ -190,6 +191,10 @@ class ConvOp:
         self.halo_f = self.halo_d = False
         self.h2_f = self.h2_d = False
         self.w2 = False  # weight gradient on seg_conv_wgrad2_bf16io (narrow bf16io 3x3)
+        # bf16io depthwise convs on the LDS-DMA tile kernels (seg_dw2_*_bf16io); dw2_st = the forward's BN
+        # tile partials (row tiles, tile rows) when its tiles divide the output, else None
+        self.dw2 = False
+        self.dw2_st = None
         # bf16 math (Program.math == "bf16"): seg_conv_igemm_bf16 / seg_conv_wgrad_bf16
         self.bf = False
         # bf16io: wk_f / wk_d packed as bf16 for seg_conv_igemm_bf16io_w16 (Program._build_pack)
@@ -226,8 +231,17 @@ class ConvOp:
         bias = self.conv.bias.data_ptr() if self.conv.bias is not None else None
         if self.kind == "dw":
             i = self.inp
-            rt.call(rt.k("seg_dw_fwd"), rt.ptr(i), i.ld, i.N, i.H, i.W, i.C, *self._in_xform(rt), self.wk_f.data_ptr(),
-                 rt.ptr(y), y.ld, y.H, y.W, self.stride, s)
+            stat = None
+            if self.dw2:  # LDS-DMA tiles; the output's BN tile partials from the epilogue where the tiles divide it
+                if self.dw2_st is not None and rt.training:
+                    ntiles, tile_rows = self.dw2_st
+                    stat = rt.tmp(ntiles * 2 * self.cout)
+                rt.call("seg_dw2_fwd_bf16io", rt.ptr(i), i.ld, i.N, i.H, i.W, i.C, *self._in_xform(rt),
+                         self.wk_f.data_ptr(), rt.ptr(y), y.ld, y.H, y.W, self.stride,
+                         stat.data_ptr() if stat is not None else None, s)
+            else:
+                rt.call(rt.k("seg_dw_fwd"), rt.ptr(i), i.ld, i.N, i.H, i.W, i.C, *self._in_xform(rt),
+                        self.wk_f.data_ptr(), rt.ptr(y), y.ld, y.H, y.W, self.stride, s)
         else:
             i = self.inp
             if self.wk_f is None:
@@ -304,7 +318,7 @@ class ConvOp:
             rm = bn.running_mean.data_ptr() if bn.track_running_stats else None
             rv = bn.running_var.data_ptr() if bn.track_running_stats else None
             nbt = bn.num_batches_tracked.data_ptr() if bn.track_running_stats else None
-            if self.kind == "dw":
+            if self.kind == "dw" and stat is None:
                 work = rt.tmp(query("seg_chan_workspace_floats", M, C))
                 rt.call(rt.k("seg_bn_stats"), rt.ptr(y), y.ld, M, C, bn.weight.data_ptr(), bn.bias.data_ptr(), bn.eps,
                      bn.momentum, rm, rv, nbt, work.data_ptr(), mean, invstd,
@@ -413,7 +427,13 @@ class ConvOp:
         if self.conv.weight.requires_grad:
             gw = rt.grad_param(self.conv.weight)
             i = self.inp
-            if self.kind == "dw":
+            if self.kind == "dw" and self.dw2 and dY.ld % 8 == 0 and dYp % 16 == 0:
+                nblk = query("seg_dw2_wgrad_blocks", y.N, y.H, y.W, self.cout, self.stride)
+                part = rt.tmp(nblk * 9 * self.cout)
+                rt.call("seg_dw2_wgrad_bf16io", dYp, dY.ld, rt.ptr(i), i.ld, i.N, i.H, i.W, i.C,
+                         *self._in_xform(rt), y.H, y.W, self.stride, part.data_ptr(), s)
+                rt.call("seg_conv_wgrad_reduce", part.data_ptr(), nblk, gw, self.cout, 1, 3, 1, 0, s)
+            elif self.kind == "dw":
                 nblk = query("seg_dw_wgrad_blocks", y.N, y.H, y.W, self.cout)
                 part = rt.tmp(nblk * 9 * self.cout)
                 rt.call(rt.k("seg_dw_wgrad"), dYp, dY.ld, rt.ptr(i), i.ld, i.N, i.H, i.W, i.C, *self._in_xform(rt), y.H, y.W,
@@ -450,7 +470,8 @@ class ConvOp:
         y, i = self.y, self.inp
         if self.kind == "dw":
             acc = rt.begin_write_accumulate(i)
-            rt.call(rt.k("seg_dw_dgrad"), dYp, dY.ld, y.N, y.H, y.W, self.cout, self.wk_f.data_ptr(), rt.gptr(i), i.ld, i.H,
+            dw2 = self.dw2 and dY.ld % 8 == 0 and dYp % 16 == 0 and rt.gptr(i) % 16 == 0
+            rt.call("seg_dw2_dgrad_bf16io" if dw2 else rt.k("seg_dw_dgrad"), dYp, dY.ld, y.N, y.H, y.W, self.cout, self.wk_f.data_ptr(), rt.gptr(i), i.ld, i.H,
                  i.W, self.stride, acc, s)
         else:
             if self.stride != 1:
@@ -618,6 +639,14 @@ class Program:
                 op.wk_f = torch.empty(9 * op.cout, device=dev, dtype=torch.float32)
                 jobs.append((w.data_ptr(), op.wk_f.data_ptr(), op.cout, 1, 3, 9, 2, 1))
                 max_elems = max(max_elems, 9 * op.cout)
+                i, y = op.inp, op.y
+                op.dw2 = (self.math == "bf16io" and DW2 and bool(query("seg_dw2_ok", op.cout, op.stride))
+                          and all(t.ld % 8 == 0 and t.off % 8 == 0 for t in (i, y)))
+                op.dw2_st = None
+                if op.dw2 and op.bn is not None:
+                    rows = ctypes.c_int(0)
+                    nt = query("seg_dw2_stat_tiles", y.N, y.H, y.W, op.stride, ctypes.addressof(rows))
+                    op.dw2_st = (nt, rows.value) if nt else None
                 continue
             y = op.y
             op.bf = self.math in ("bf16", "bf16io")
@@ -1247,6 +1276,8 @@ HALO_BF16 = os.environ.get("SEG_HALO_BF16", "1") == "1"
 HALO2 = os.environ.get("SEG_HALO2", "1") == "1"
 # ... and their weight gradients on the persistent LDS-halo kernel (seg_conv_wgrad2_bf16io); SEG_WGRAD2=0 = off
 WGRAD2 = os.environ.get("SEG_WGRAD2", "1") == "1"
+# bf16io depthwise convs on the LDS-DMA tile kernels (csrc/dw2.hip); SEG_DW2=0 keeps dwconv.hip's strip kernels
+DW2 = os.environ.get("SEG_DW2", "1") == "1"
 # lazy BatchNorm for 1x1 consumers (the inverted residuals' project convs, OutConv's last
 # conv): SEG_LAZY_PW=0 keeps the separate BN-apply pass (read at program build)
 LAZY_PW = os.environ.get("SEG_LAZY_PW", "1") == "1"

@@ -4,10 +4,12 @@ MobileNetV2UNet (bs=32, 256x512) launch shapes, median of R launches timed with 
 
   * narrow 3x3 convs (up3 / up4 and their data gradients): seg_conv_halo2_bf16io vs
     seg_conv_halo_bf16io_w16 vs seg_conv_igemm_bf16io_w16;
+  * depthwise convs (forward with lazy BN + tile statistics, data gradient, weight gradient):
+    seg_dw2_*_bf16io vs dwconv.hip's seg_dw_*_bf16io;
   * small-image 1x1 convs of the encoder: seg_conv_igemm2_bf16io (4-wave tiles; _xf for the
     lazy-BN project convs) vs seg_conv_igemm_bf16io_w16 (_xf_w16).
 
-    python tools/nbench.py [--reps 30] [--only halo|pw] [--csv out.csv]
+    python tools/nbench.py [--reps 30] [--only halo|pw|dw] [--csv out.csv]
 """
 import argparse
 import ctypes
@@ -36,6 +38,12 @@ PW = [  # name, M, Cin, Cout, xf (lazy BN on the input: the project convs)
     ("4k 960->320 xf", 4096, 960, 320, True), ("4k 320->1280", 4096, 320, 1280, False),
     ("4k 1280->320 dg", 4096, 1280, 320, False), ("65k 32->192", 65536, 32, 192, False),
     ("65k 192->32 xf", 65536, 192, 32, True), ("65k 144->32 dg", 65536, 144, 32, False),
+]
+DW = [  # name, N, H, W (input), C, stride -- MobileNetV2 features.1-17's depthwise convs
+    ("f1 32 128x256", 32, 128, 256, 32, 1), ("f2 96 s2", 32, 128, 256, 96, 2), ("f3 144 64x128", 32, 64, 128, 144, 1),
+    ("f4 144 s2", 32, 64, 128, 144, 2), ("f5 192 32x64", 32, 32, 64, 192, 1), ("f7 192 s2", 32, 32, 64, 192, 2),
+    ("f8 384 16x32", 32, 16, 32, 384, 1), ("f12 576 16x32", 32, 16, 32, 576, 1), ("f14 576 s2", 32, 16, 32, 576, 2),
+    ("f15 960 8x16", 32, 8, 16, 960, 1),
 ]
 
 
@@ -134,6 +142,46 @@ def main():
             line = "  ".join(f"{k} {v * 1e6:7.1f} us {nbytes / v / 1e9:6.0f} GB/s" for k, v in res.items())
             print(f"{name:16s} {line}", flush=True)
             rows += [(name, k, v * 1e6, nbytes / v / 1e9) for k, v in res.items()]
+    if a.only in ("", "dw"):
+        for name, N, H, W, C, s in DW:
+            Ho, Wo = (H - 1) // s + 1, (W - 1) // s + 1
+            x = torch.randn(N * H * W, C, generator=g).to(BF).cuda()
+            dy = torch.randn(N * Ho * Wo, C, generator=g).to(BF).cuda()
+            w = (torch.randn(C, 1, 3, 3, generator=g) * 0.3).cuda()
+            wk = torch.empty(9 * C, device="cuda")
+            call("seg_pack_dw_weight", w.data_ptr(), wk.data_ptr(), C, S())
+            sc = (torch.rand(C, generator=g) + 0.5).cuda()
+            sh = torch.randn(C, generator=g).cuda()
+            o = torch.empty(N * Ho * Wo, C, device="cuda", dtype=BF)
+            dx = torch.empty(N * H * W, C, device="cuda", dtype=BF)
+            nbytes = 2 * C * (N * H * W + N * Ho * Wo)
+            nt = query("seg_dw2_stat_tiles", N, Ho, Wo, s, None)
+            st = torch.empty(max(nt, 1) * 2 * C, device="cuda")
+            stp = st.data_ptr() if nt else None
+            nb2 = query("seg_dw2_wgrad_blocks", N, Ho, Wo, C, s)
+            p2 = torch.empty(nb2 * 9 * C, device="cuda")
+            nb1 = query("seg_dw_wgrad_blocks", N, Ho, Wo, C)
+            p1 = torch.empty(nb1 * 9 * C, device="cuda")
+            res = {
+                "fwd2": timeit(lambda: call("seg_dw2_fwd_bf16io", x.data_ptr(), C, N, H, W, C, sc.data_ptr(),
+                                            sh.data_ptr(), 2, wk.data_ptr(), o.data_ptr(), C, Ho, Wo, s, stp, S()), a.reps),
+                "fwd1": timeit(lambda: call("seg_dw_fwd_bf16io", x.data_ptr(), C, N, H, W, C, sc.data_ptr(),
+                                            sh.data_ptr(), 2, wk.data_ptr(), o.data_ptr(), C, Ho, Wo, s, S()), a.reps),
+                "dg2": timeit(lambda: call("seg_dw2_dgrad_bf16io", dy.data_ptr(), C, N, Ho, Wo, C, wk.data_ptr(),
+                                           dx.data_ptr(), C, H, W, s, 1, S()), a.reps),
+                "dg1": timeit(lambda: call("seg_dw_dgrad_bf16io", dy.data_ptr(), C, N, Ho, Wo, C, wk.data_ptr(),
+                                           dx.data_ptr(), C, H, W, s, 1, S()), a.reps),
+                "wg2": timeit(lambda: call("seg_dw2_wgrad_bf16io", dy.data_ptr(), C, x.data_ptr(), C, N, H, W, C,
+                                           sc.data_ptr(), sh.data_ptr(), 2, Ho, Wo, s, p2.data_ptr(), S()), a.reps),
+                "wg1": timeit(lambda: call("seg_dw_wgrad_bf16io", dy.data_ptr(), C, x.data_ptr(), C, N, H, W, C,
+                                           sc.data_ptr(), sh.data_ptr(), 2, Ho, Wo, s, p1.data_ptr(), S()), a.reps),
+            }
+            # dgrad with accumulate reads dX as well
+            nb = {"fwd2": nbytes, "fwd1": nbytes, "dg2": nbytes + 2 * C * N * H * W, "dg1": nbytes + 2 * C * N * H * W,
+                  "wg2": nbytes, "wg1": nbytes}
+            line = "  ".join(f"{k} {v * 1e6:6.1f} us {nb[k] / v / 1e9:5.0f}" for k, v in res.items())
+            print(f"{name:15s} {line}", flush=True)
+            rows += [(name, k, v * 1e6, nb[k] / v / 1e9) for k, v in res.items()]
     if a.csv:
         with open(a.csv, "w") as fh:
             fh.write("shape,kernel,us,gbs\n")

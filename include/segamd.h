@@ -263,6 +263,17 @@ int seg_bn_backward(const float* da, long ldda, const float* y, long ldy, long M
                     const float* gamma, const float* mean, const float* invstd,
                     const float* scale, const float* shift, int act,
                     float* dgamma, float* dbeta, float* work, float* dy, long lddy, hipStream_t stream);
+/* The two halves of seg_bn_backward (same arguments and arithmetic), for callers that fuse one of
+ * them into a neighbouring kernel (csrc/dw2.hip's depthwise data / weight gradients):
+ * seg_bn_bwd_coef: the reduction -- dgamma, dbeta and coef[3][C] = (gamma*invstd, mean(dz),
+ * mean(dz*xhat)*invstd); work >= seg_chan_workspace_floats(M, C) floats.  seg_bn_bwd_apply:
+ * dy = coef[0] * (dz - coef[1] - (y - mean) * coef[2]), dz = da * act'(y*scale + shift). */
+int seg_bn_bwd_coef(const float* da, long ldda, const float* y, long ldy, long M, int C, const float* gamma,
+                    const float* mean, const float* invstd, const float* scale, const float* shift, int act,
+                    float* dgamma, float* dbeta, float* work, float* coef, hipStream_t stream);
+int seg_bn_bwd_apply(const float* da, long ldda, const float* y, long ldy, long M, int C, const float* mean,
+                     const float* scale, const float* shift, int act, const float* coef, float* dy, long lddy,
+                     hipStream_t stream);
 int seg_bn_eval_backward(const float* da, long ldda, const float* y, long ldy, long M, int C,
                          const float* scale, const float* shift, int act, float* dy, long lddy,
                          hipStream_t stream);
@@ -375,6 +386,13 @@ int seg_dw_fwd_bf16io(const seg_bf16* in, long ldin, int N, int H, int W, int C,
     in_shift, int in_act, const float* wk, seg_bf16* out, long ldout, int Ho, int Wo, int stride, hipStream_t stream);
 int seg_dw_dgrad_bf16io(const seg_bf16* dy, long lddy, int N, int Ho, int Wo, int C, const float* wk, seg_bf16* dx,
     long lddx, int H, int W, int stride, int accumulate, hipStream_t stream);
+int seg_bn_bwd_coef_bf16io(const seg_bf16* da, long ldda, const seg_bf16* y, long ldy, long M, int C,
+                           const float* gamma, const float* mean, const float* invstd, const float* scale,
+                           const float* shift, int act, float* dgamma, float* dbeta, float* work, float* coef,
+                           hipStream_t stream);
+int seg_bn_bwd_apply_bf16io(const seg_bf16* da, long ldda, const seg_bf16* y, long ldy, long M, int C,
+                            const float* mean, const float* scale, const float* shift, int act, const float* coef,
+                            seg_bf16* dy, long lddy, hipStream_t stream);
 int seg_dw_wgrad_bf16io(const seg_bf16* dy, long lddy, const seg_bf16* x, long ldx, int N, int H, int W, int C, const
     float* in_scale, const float* in_shift, int in_act, int Ho, int Wo, int stride, float* part, hipStream_t stream);
 int seg_conv_igemm_bf16io(const seg_bf16* in, long ldin, int N, int H, int W, int Cin, const float* wk, int ldk, const
@@ -541,7 +559,7 @@ int seg_conv_wgrad2_bf16io(const seg_bf16* dy, long lddy, const seg_bf16* x, lon
  * output, [seg_dw2_stat_tiles(...)][2][C] (tile sum, M2 about the tile mean; *tile_rows rows each) for
  * seg_bn_stats_tiles -- only when seg_dw2_stat_tiles is non-zero (the tiles divide Ho x Wo).
  * seg_dw2_dgrad_bf16io: as seg_dw_dgrad_bf16io (bitwise its result).
- * seg_dw2_wgrad_bf16io: as seg_dw_wgrad_bf16io with part[seg_dw2_wgrad_blocks(N, Ho, Wo, C, stride)][9][C]
+ * seg_dw2_wgrad_bf16io: as seg_dw_wgrad_bf16io with part[seg_dw2_wgrad_blocks(N, Ho, Wo, C, stride, 0)][9][C]
  * (reduce with seg_conv_wgrad_reduce(part, blocks, dw, C, 1, 3, 1, acc)); fixed-order, deterministic. */
 int seg_dw2_ok(int C, int stride);
 int seg_dw2_stat_tiles(int N, int Ho, int Wo, int stride, int* tile_rows);
@@ -550,10 +568,35 @@ int seg_dw2_fwd_bf16io(const seg_bf16* in, long ldin, int N, int H, int W, int C
                        int stride, float* stat, hipStream_t stream);
 int seg_dw2_dgrad_bf16io(const seg_bf16* dy, long lddy, int N, int Ho, int Wo, int C, const float* wk, seg_bf16* dx,
                          long lddx, int H, int W, int stride, int accumulate, hipStream_t stream);
-long seg_dw2_wgrad_blocks(int N, int Ho, int Wo, int C, int stride);
+/* seg_dw2_dgrad_bn_bf16io: seg_dw2_dgrad_bf16io with two optional BatchNorm-backward fusions (a NULL
+ * by / oy skips one):
+ *  BIN  -- dy holds dA, the gradient of this conv's BN + act output; its BatchNorm backward
+ *          dY = seg_bn_bwd_apply(dA, by; bmean, bscale, bshift, bact, bcoef) is formed on load
+ *          (bitwise the apply pass's bf16 output) and never stored (bcoef from seg_bn_bwd_coef_bf16io);
+ *  BOUT -- dx is dA of the layer that produced this conv's input (pre-BN output oy, BN statistics
+ *          omean / oinvstd / oscale / oshift / ogamma, act oact): the partials of that layer's BatchNorm
+ *          backward come out of this launch's epilogue into opart [seg_dw2_dgrad_tiles(N, H, W)][2][C]
+ *          and the last tile of each 64-channel slice finalizes them into odgamma, odbeta (may be NULL)
+ *          and ocoef [3][C] (as seg_bn_bwd_coef_bf16io; fixed-order fp64 sums, deterministic); ocnt:
+ *          ceil(C/64) counters, zero before the first launch, re-armed by every launch. */
+int seg_dw2_dgrad_tiles(int N, int H, int W);
+int seg_dw2_dgrad_bn_bf16io(const seg_bf16* dy, long lddy, int N, int Ho, int Wo, int C, const float* wk,
+                            seg_bf16* dx, long lddx, int H, int W, int stride, int accumulate, const seg_bf16* by,
+                            long ldby, const float* bscale, const float* bshift, const float* bmean,
+                            const float* bcoef, int bact, const seg_bf16* oy, long ldoy, const float* oscale,
+                            const float* oshift, const float* omean, const float* ogamma, const float* oinvstd,
+                            int oact, float* opart, float* odgamma, float* odbeta, float* ocoef, unsigned* ocnt,
+                            hipStream_t stream);
+long seg_dw2_wgrad_blocks(int N, int Ho, int Wo, int C, int stride, int bin);
 int seg_dw2_wgrad_bf16io(const seg_bf16* dy, long lddy, const seg_bf16* x, long ldx, int N, int H, int W, int C,
                          const float* in_scale, const float* in_shift, int in_act, int Ho, int Wo, int stride,
                          float* part, hipStream_t stream);
+/* seg_dw2_wgrad_bn_bf16io: seg_dw2_wgrad_bf16io with BIN (dy holds dA; dY formed on load as in
+ * seg_dw2_dgrad_bn_bf16io); part sized by seg_dw2_wgrad_blocks(..., bin = by != NULL). */
+int seg_dw2_wgrad_bn_bf16io(const seg_bf16* dy, long lddy, const seg_bf16* x, long ldx, int N, int H, int W, int C,
+                            const float* in_scale, const float* in_shift, int in_act, int Ho, int Wo, int stride,
+                            float* part, const seg_bf16* by, long ldby, const float* bscale, const float* bshift,
+                            const float* bmean, const float* bcoef, int bact, hipStream_t stream);
 
 /* Build identity (host only): copies the SHA-256 (64 hex chars + NUL) of the sources this
  * library was built from -- every csrc file, this header, compiler and flags

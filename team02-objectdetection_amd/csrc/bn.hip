@@ -869,6 +869,53 @@ SEG_API int seg_bn_backward_bf16io(const __bf16* da, long ldda, const __bf16* y,
                           lddy, stream);
 }
 
+// The two halves of seg_bn_backward, for a caller that fuses one of them into a neighbouring
+// kernel (the depthwise convs of csrc/dw2.hip):
+//  * seg_bn_bwd_coef_*: the reduction -- dgamma, dbeta and coef[3][C] = (g*invstd, mean(dz),
+//    mean(dz*xhat)*invstd) (`work` >= seg_chan_workspace_floats(M, C) floats);
+//  * seg_bn_bwd_apply_*: dy = seg_bnbwd4(da, y; coef) -- what seg_bn_backward writes, bit for bit.
+template <typename T>
+static int bn_bwd_coef_impl(const T* da, long ldda, const T* y, long ldy, long M, int C, const float* gamma,
+                            const float* mean, const float* invstd, const float* scale, const float* shift, int act,
+                            float* dgamma, float* dbeta, float* work, float* coef, hipStream_t stream) {
+  if ((C & 3) || (ldy & 3) || (ldda & 3) || M < 1 || !coef) return (int)hipErrorInvalidValue;
+  launch_chan_partial<1, T>(y, ldy, da, ldda, M, C, scale, shift, mean, act, work, stream);
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(seg_cdiv(C, 4)), dim3(256), 0, stream, work, chan_blocks(M), M, C,
+                     gamma, invstd, dgamma, dbeta, coef);
+  SEG_RET_LAST();
+}
+SEG_API int seg_bn_bwd_coef(const float* da, long ldda, const float* y, long ldy, long M, int C, const float* gamma,
+                            const float* mean, const float* invstd, const float* scale, const float* shift, int act,
+                            float* dgamma, float* dbeta, float* work, float* coef, hipStream_t stream) {
+  return bn_bwd_coef_impl(da, ldda, y, ldy, M, C, gamma, mean, invstd, scale, shift, act, dgamma, dbeta, work, coef,
+                          stream);
+}
+SEG_API int seg_bn_bwd_coef_bf16io(const __bf16* da, long ldda, const __bf16* y, long ldy, long M, int C,
+                                   const float* gamma, const float* mean, const float* invstd, const float* scale,
+                                   const float* shift, int act, float* dgamma, float* dbeta, float* work, float* coef,
+                                   hipStream_t stream) {
+  return bn_bwd_coef_impl(da, ldda, y, ldy, M, C, gamma, mean, invstd, scale, shift, act, dgamma, dbeta, work, coef,
+                          stream);
+}
+template <typename T>
+static int bn_bwd_apply_impl(const T* da, long ldda, const T* y, long ldy, long M, int C, const float* mean,
+                             const float* scale, const float* shift, int act, const float* coef, T* dy, long lddy,
+                             hipStream_t stream) {
+  if ((C & 3) || (ldy & 3) || (ldda & 3) || (lddy & 3)) return (int)hipErrorInvalidValue;
+  launch_bn_bwd_apply<T>(da, ldda, y, ldy, M, C, scale, shift, mean, act, coef, dy, lddy, stream);
+  SEG_RET_LAST();
+}
+SEG_API int seg_bn_bwd_apply(const float* da, long ldda, const float* y, long ldy, long M, int C, const float* mean,
+                             const float* scale, const float* shift, int act, const float* coef, float* dy, long lddy,
+                             hipStream_t stream) {
+  return bn_bwd_apply_impl(da, ldda, y, ldy, M, C, mean, scale, shift, act, coef, dy, lddy, stream);
+}
+SEG_API int seg_bn_bwd_apply_bf16io(const __bf16* da, long ldda, const __bf16* y, long ldy, long M, int C,
+                                    const float* mean, const float* scale, const float* shift, int act,
+                                    const float* coef, __bf16* dy, long lddy, hipStream_t stream) {
+  return bn_bwd_apply_impl(da, ldda, y, ldy, M, C, mean, scale, shift, act, coef, dy, lddy, stream);
+}
+
 SEG_API int seg_bn_eval_backward(const float* da, long ldda, const float* y, long ldy, long M, int C,
                                  const float* scale, const float* shift, int act, float* dy, long lddy,
                                  hipStream_t stream) {

@@ -35,7 +35,7 @@ from ._lib import call, query as _query
 _PURE_QUERIES = {"seg_chan_workspace_floats", "seg_conv_wgrad_splits", "seg_conv_wgrad_splits_bf16", "seg_dw_wgrad_blocks",
                  "seg_conv_igemm_splits", "seg_ce_workspace_floats", "seg_conv_wino_row_tiles", "seg_conv_wino_tile_rows",
                  "seg_conv_halo_row_tiles", "seg_conv_wino_wgrad_splits", "seg_dw2_ok",
-                 "seg_dw2_wgrad_blocks"}
+                 "seg_dw2_wgrad_blocks", "seg_dw2_dgrad_tiles"}
 _QCACHE = {}
 
 
@@ -373,8 +373,35 @@ class ConvOp:
         return st[2 * C:3 * C].data_ptr(), st[3 * C:4 * C].data_ptr(), xf.act
 
     # -- backward
+    def _bin_ok(self, rt, dA) -> bool:
+        """The dw2 data / weight gradients can form this depthwise conv's BN backward on load."""
+        return (self.kind == "dw" and self.dw2 and DW2_BN and dA.ld % 8 == 0 and rt.gptr(dA) % 16 == 0
+                and self.y.ld % 8 == 0 and rt.ptr(self.y) % 16 == 0)
+
+    def _bout(self, rt):
+        """BOUT arguments of the dw2 data gradient (the BatchNorm-backward reduction of the producer whose
+        lazy BN this depthwise conv applies on load), or None -- registers the coefficients for its backward."""
+        p = self.xform
+        if (not DW2_BN or p is None or p.bn is None or not rt.training or p.res is not None or not p.lazy
+                or p.y.key() != self.inp.key() or id(p) not in rt.saved):
+            return None
+        i = self.inp
+        tiles = query("seg_dw2_dgrad_tiles", i.N, i.H, i.W)
+        if tiles > DW2_BN_MAX_TILES:
+            return None
+        C = p.cout
+        mean, invstd, scale, shift = _stat_ptrs(rt.saved[id(p)], C)
+        coef = rt.tmp(3 * C)
+        part = rt.tmp(tiles * 2 * C)
+        cnt = rt.tmp((C + 63) // 64, zero=True)
+        g_w, g_b = rt.grad_param(p.bn.weight), rt.grad_param(p.bn.bias)
+        rt.bn_coef[id(p)] = coef
+        return (rt.ptr(p.y), p.y.ld, scale, shift, mean, p.bn.weight.data_ptr(), invstd, p.act, part.data_ptr(), g_w,
+                g_b, coef.data_ptr(), cnt.data_ptr())
+
     def backward(self, rt):
         s, y = rt.stream, self.y
+        bin_ = None
         dA = rt.grad_of(self.out)
         if self.bn is not None:
             if not rt.training:
@@ -382,12 +409,27 @@ class ConvOp:
             C, M = self.cout, y.M
             st = rt.saved[id(self)]
             mean, invstd, scale, shift = _stat_ptrs(st, C)
-            dY = Act(rt.tmp_buf(M * r4(C)), 0, r4(C), C, y.N, y.H, y.W)
             g_w, g_b = rt.grad_param(self.bn.weight), rt.grad_param(self.bn.bias)
-            work = rt.tmp(query("seg_chan_workspace_floats", M, C) + 3 * C)
-            rt.call(rt.k("seg_bn_backward"), rt.gptr(dA), dA.ld, rt.ptr(y), y.ld, M, C, self.bn.weight.data_ptr(),
-                    mean, invstd, scale, shift, self.act,
-                    g_w, g_b, work.data_ptr(), rt.ptr(dY), dY.ld, s)
+            coef = rt.bn_coef.pop(id(self), None)
+            if coef is not None:  # the reduction ran in the consumer's data gradient (BOUT): the apply alone
+                dY = Act(rt.tmp_buf(M * r4(C)), 0, r4(C), C, y.N, y.H, y.W)
+                rt.call(rt.k("seg_bn_bwd_apply"), rt.gptr(dA), dA.ld, rt.ptr(y), y.ld, M, C, mean, scale, shift,
+                        self.act, coef.data_ptr(), rt.ptr(dY), dY.ld, s)
+            elif self._bin_ok(rt, dA):
+                # depthwise conv on dw2: the reduction here, the apply formed on load by its data and weight
+                # gradients (BIN) -- dY is never stored
+                coef = rt.tmp(3 * C)
+                work = rt.tmp(query("seg_chan_workspace_floats", M, C))
+                rt.call(rt.k("seg_bn_bwd_coef"), rt.gptr(dA), dA.ld, rt.ptr(y), y.ld, M, C, self.bn.weight.data_ptr(),
+                        mean, invstd, scale, shift, self.act, g_w, g_b, work.data_ptr(), coef.data_ptr(), s)
+                bin_ = (rt.ptr(y), y.ld, scale, shift, mean, coef.data_ptr(), self.act)
+                dY = dA
+            else:
+                dY = Act(rt.tmp_buf(M * r4(C)), 0, r4(C), C, y.N, y.H, y.W)
+                work = rt.tmp(query("seg_chan_workspace_floats", M, C) + 3 * C)
+                rt.call(rt.k("seg_bn_backward"), rt.gptr(dA), dA.ld, rt.ptr(y), y.ld, M, C, self.bn.weight.data_ptr(),
+                        mean, invstd, scale, shift, self.act,
+                        g_w, g_b, work.data_ptr(), rt.ptr(dY), dY.ld, s)
             if self.res is not None:
                 rt.add_pending(self.res, dA)
         else:
@@ -403,14 +445,14 @@ class ConvOp:
                 rt.grad_param(p)
         late = FORK_LATE and not self.first
         if late:  # the data gradient first: the side stream's weight gradient then runs beside
-            self._dgrad(rt, dY, dYp, s)  # the next layer's memory-bound BN backward, not this dgrad
+            self._dgrad(rt, dY, dYp, s, bin_)  # the next layer's memory-bound BN backward, not this dgrad
         ctx, sw = rt.fork()
         with ctx:
-            self._param_grads(rt, dY, dYp, sw)
+            self._param_grads(rt, dY, dYp, sw, bin_)
         if not self.first and not late:
-            self._dgrad(rt, dY, dYp, s)
+            self._dgrad(rt, dY, dYp, s, bin_)
 
-    def _param_grads(self, rt, dY, dYp, s):
+    def _param_grads(self, rt, dY, dYp, s, bin_=None):
         """Bias gradient (column sum of dY), weight gradient (split-K slabs + fixed-order
         reduce) and the DDP readiness hook, all on stream `s`."""
         y, M = self.y, self.y.M
@@ -428,10 +470,11 @@ class ConvOp:
             gw = rt.grad_param(self.conv.weight)
             i = self.inp
             if self.kind == "dw" and self.dw2 and dY.ld % 8 == 0 and dYp % 16 == 0:
-                nblk = query("seg_dw2_wgrad_blocks", y.N, y.H, y.W, self.cout, self.stride)
+                nblk = query("seg_dw2_wgrad_blocks", y.N, y.H, y.W, self.cout, self.stride, int(bin_ is not None))
                 part = rt.tmp(nblk * 9 * self.cout)
-                rt.call("seg_dw2_wgrad_bf16io", dYp, dY.ld, rt.ptr(i), i.ld, i.N, i.H, i.W, i.C,
-                         *self._in_xform(rt), y.H, y.W, self.stride, part.data_ptr(), s)
+                rt.call("seg_dw2_wgrad_bn_bf16io", dYp, dY.ld, rt.ptr(i), i.ld, i.N, i.H, i.W, i.C,
+                        *self._in_xform(rt), y.H, y.W, self.stride, part.data_ptr(),
+                        *(bin_ if bin_ is not None else (None, 0, None, None, None, None, 0)), s)
                 rt.call("seg_conv_wgrad_reduce", part.data_ptr(), nblk, gw, self.cout, 1, 3, 1, 0, s)
             elif self.kind == "dw":
                 nblk = query("seg_dw_wgrad_blocks", y.N, y.H, y.W, self.cout)
@@ -465,14 +508,24 @@ class ConvOp:
                 rt.call("seg_conv_wgrad_reduce", part.data_ptr(), splits, gw, self.cout, self.cin, self.ks, 0, 0, s)
         rt.params_done(self.params(), s)
 
-    def _dgrad(self, rt, dY, dYp, s):
-        """Data gradient into the input's gradient region (first writer / fused addend)."""
+    def _dgrad(self, rt, dY, dYp, s, bin_=None):
+        """Data gradient into the input's gradient region (first writer / fused addend).  bin_: the
+        depthwise conv's BN backward formed on load (dY holds dA; dw2 only)."""
         y, i = self.y, self.inp
         if self.kind == "dw":
             acc = rt.begin_write_accumulate(i)
             dw2 = self.dw2 and dY.ld % 8 == 0 and dYp % 16 == 0 and rt.gptr(i) % 16 == 0
-            rt.call("seg_dw2_dgrad_bf16io" if dw2 else rt.k("seg_dw_dgrad"), dYp, dY.ld, y.N, y.H, y.W, self.cout, self.wk_f.data_ptr(), rt.gptr(i), i.ld, i.H,
-                 i.W, self.stride, acc, s)
+            if not dw2:
+                assert bin_ is None
+                rt.call(rt.k("seg_dw_dgrad"), dYp, dY.ld, y.N, y.H, y.W, self.cout, self.wk_f.data_ptr(), rt.gptr(i),
+                        i.ld, i.H, i.W, self.stride, acc, s)
+                return
+            bout = self._bout(rt)
+            rt.call("seg_dw2_dgrad_bn_bf16io", dYp, dY.ld, y.N, y.H, y.W, self.cout, self.wk_f.data_ptr(), rt.gptr(i),
+                    i.ld, i.H, i.W, self.stride, acc,
+                    *(bin_ if bin_ is not None else (None, 0, None, None, None, None, 0)),
+                    *(bout if bout is not None else (None, 0, None, None, None, None, None, 0, None, None, None, None,
+                                                     None)), s)
         else:
             if self.stride != 1:
                 raise NotImplementedError("data gradient of a strided dense conv")
@@ -1015,6 +1068,7 @@ class Run:
         self.bufs = {n: torch.empty(rows * ld, device=self.device, dtype=self.store)
                      for n, (rows, ld) in prog.bufs.items()}
         self.saved = {}
+        self.bn_coef = {}     # id(op) -> BN-backward coefficients [3][C] computed by its consumer (dw2 BOUT)
         self.gbufs = {}
         self.keep = []        # workspaces of a recorded run (persistent: the tape points at them)
         self.written = {}     # grad buffer name -> list of (lo, hi) channel ranges
@@ -1278,6 +1332,12 @@ HALO2 = os.environ.get("SEG_HALO2", "1") == "1"
 WGRAD2 = os.environ.get("SEG_WGRAD2", "1") == "1"
 # bf16io depthwise convs on the LDS-DMA tile kernels (csrc/dw2.hip); SEG_DW2=0 keeps dwconv.hip's strip kernels
 DW2 = os.environ.get("SEG_DW2", "1") == "1"
+# ... with their BatchNorm backwards fused (SEG_DW2_BN=0: three-launch seg_bn_backward): the depthwise conv's
+# own apply formed on load by its data / weight gradients, and the reduction of the expand conv that feeds it
+# computed in its data gradient's epilogue (images of at most DW2_BN_MAX_TILES 8 x 32-pixel tiles: the
+# in-launch finalize sums every tile's partials in one block per 64 channels)
+DW2_BN = os.environ.get("SEG_DW2_BN", "1") == "1"
+DW2_BN_MAX_TILES = int(os.environ.get("SEG_DW2_BN_MAX_TILES", "512"))
 # lazy BatchNorm for 1x1 consumers (the inverted residuals' project convs, OutConv's last
 # conv): SEG_LAZY_PW=0 keeps the separate BN-apply pass (read at program build)
 LAZY_PW = os.environ.get("SEG_LAZY_PW", "1") == "1"

@@ -13,7 +13,7 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 HEADER = os.path.join(REPO, "include", "segamd.h")
 
 CTYPE = {"const float*": ctypes.c_void_p, "float*": ctypes.c_void_p, "const long long*": ctypes.c_void_p,
-         "long long*": ctypes.c_void_p, "int*": ctypes.c_void_p, "const void*": ctypes.c_void_p, "const seg_bf16*": ctypes.c_void_p, "seg_bf16*": ctypes.c_void_p, "const unsigned char*": ctypes.c_void_p, "unsigned char*": ctypes.c_void_p, "hipStream_t": ctypes.c_void_p, "const SegAdamTensor*": ctypes.c_void_p, "const long*": ctypes.c_void_p, "long": ctypes.c_long, "void*": ctypes.c_void_p, "void**": ctypes.c_void_p, "const int*": ctypes.c_void_p,
+         "long long*": ctypes.c_void_p, "int*": ctypes.c_void_p, "const void*": ctypes.c_void_p, "const seg_bf16*": ctypes.c_void_p, "seg_bf16*": ctypes.c_void_p, "const unsigned char*": ctypes.c_void_p, "unsigned char*": ctypes.c_void_p, "hipStream_t": ctypes.c_void_p, "const SegAdamTensor*": ctypes.c_void_p, "const long*": ctypes.c_void_p, "long": ctypes.c_long, "void*": ctypes.c_void_p, "void**": ctypes.c_void_p, "const int*": ctypes.c_void_p, "unsigned*": ctypes.c_void_p,
          "const char*": ctypes.c_char_p, "char*": ctypes.c_char_p, "long*": ctypes.c_void_p,
          "int": ctypes.c_int, "float": ctypes.c_float}
 

@@ -155,7 +155,7 @@ def test_dw2_wgrad_vs_fp64_and_strip_kernel(N, C, H, W, s, ld, lazy):
     sc = (torch.rand(C, generator=g) + 0.5).to(DEV)
     sh = (torch.randn(C, generator=g) * 0.5).to(DEV)
     xf = (sc.data_ptr(), sh.data_ptr(), 2) if lazy else (None, None, 0)
-    blocks = query("seg_dw2_wgrad_blocks", N, Ho, Wo, C, s)
+    blocks = query("seg_dw2_wgrad_blocks", N, Ho, Wo, C, s, 0)
     part = torch.full((blocks * 9 * C,), float("nan"), device=DEV)
     outs = []
     for _ in range(2):
@@ -192,3 +192,120 @@ def test_dw2_refuses_what_it_cannot_do():
     with pytest.raises(Exception):  # stat requested where the tiles do not divide the image
         call("seg_dw2_fwd_bf16io", x.data_ptr(), 64, 1, 8, 8, 64, None, None, 0, x.data_ptr(), x.data_ptr(), 64, 8, 8,
              1, x.data_ptr(), S())
+
+
+# ---- the BatchNorm-backward fusions (seg_dw2_dgrad_bn_bf16io / seg_dw2_wgrad_bn_bf16io) ----
+
+def bn_state(C, seed):
+    """Per-channel (mean, invstd, scale, shift, gamma, coef[3][C]) of a plausible train-mode BN."""
+    g = torch.Generator().manual_seed(seed)
+    mean = torch.randn(C, generator=g) * 0.3
+    invstd = torch.rand(C, generator=g) + 0.5
+    gamma = torch.rand(C, generator=g) + 0.5
+    beta = torch.randn(C, generator=g) * 0.2
+    scale, shift = gamma * invstd, beta - mean * gamma * invstd
+    coef = torch.cat([gamma * invstd, torch.randn(C, generator=g) * 0.05, torch.randn(C, generator=g) * 0.05])
+    return [t.to(DEV) for t in (mean, invstd, scale, shift, gamma, coef)]
+
+
+BN_CASES = [  # N, C, H, W, stride, ld
+    (2, 64, 16, 64, 1, 64), (2, 64, 16, 64, 2, 64), (1, 72, 13, 40, 1, 80), (1, 72, 13, 40, 2, 72),
+    (4, 192, 32, 64, 1, 192), (8, 960, 8, 16, 1, 960), (4, 144, 32, 64, 2, 144),
+]
+
+
+@pytest.mark.parametrize("N,C,H,W,s,ld", BN_CASES)
+def test_dw2_dgrad_bin_equals_apply_then_dgrad(N, C, H, W, s, ld):
+    """BIN: dY formed on load is bitwise the seg_bn_bwd_apply pass's stored dY."""
+    Ho, Wo = outsz(H, s), outsz(W, s)
+    da = rows(N * Ho * Wo, ld, 21 + C)
+    y = rows(N * Ho * Wo, ld, 22 + C, 2.0)
+    mean, invstd, scale, shift, gamma, coef = bn_state(C, C)
+    _, wk = packw(C, C + 3)
+    dy = torch.full((N * Ho * Wo, ld), 0.0, device=DEV, dtype=BF)
+    call("seg_bn_bwd_apply_bf16io", da.data_ptr(), ld, y.data_ptr(), ld, N * Ho * Wo, C, mean.data_ptr(),
+         scale.data_ptr(), shift.data_ptr(), 2, coef.data_ptr(), dy.data_ptr(), ld, S())
+    ref = torch.zeros(N * H * W, ld, device=DEV, dtype=BF)
+    call("seg_dw2_dgrad_bf16io", dy.data_ptr(), ld, N, Ho, Wo, C, wk.data_ptr(), ref.data_ptr(), ld, H, W, s, 0, S())
+    got = torch.zeros(N * H * W, ld, device=DEV, dtype=BF)
+    call("seg_dw2_dgrad_bn_bf16io", da.data_ptr(), ld, N, Ho, Wo, C, wk.data_ptr(), got.data_ptr(), ld, H, W, s, 0,
+         y.data_ptr(), ld, scale.data_ptr(), shift.data_ptr(), mean.data_ptr(), coef.data_ptr(), 2,
+         None, 0, None, None, None, None, None, 0, None, None, None, None, None, S())
+    torch.cuda.synchronize()
+    assert torch.equal(got, ref), f"max diff {(got.float() - ref.float()).abs().max().item()}"
+
+
+@pytest.mark.parametrize("N,C,H,W,s,ld", BN_CASES)
+def test_dw2_wgrad_bin_vs_apply_then_wgrad(N, C, H, W, s, ld):
+    Ho, Wo = outsz(H, s), outsz(W, s)
+    x = rows(N * H * W, ld, 31 + C)
+    da = rows(N * Ho * Wo, ld, 32 + C)
+    y = rows(N * Ho * Wo, ld, 33 + C, 2.0)
+    mean, invstd, scale, shift, gamma, coef = bn_state(C, C + 5)
+    dy = torch.zeros(N * Ho * Wo, ld, device=DEV, dtype=BF)
+    call("seg_bn_bwd_apply_bf16io", da.data_ptr(), ld, y.data_ptr(), ld, N * Ho * Wo, C, mean.data_ptr(),
+         scale.data_ptr(), shift.data_ptr(), 2, coef.data_ptr(), dy.data_ptr(), ld, S())
+    outs = {}
+    for bin_ in (0, 1):
+        blocks = query("seg_dw2_wgrad_blocks", N, Ho, Wo, C, s, bin_)
+        part = torch.full((blocks * 9 * C,), float("nan"), device=DEV)
+        dw = torch.empty(C, 1, 3, 3, device=DEV)
+        src = da if bin_ else dy
+        b = (y.data_ptr(), ld, scale.data_ptr(), shift.data_ptr(), mean.data_ptr(), coef.data_ptr(), 2) if bin_ else \
+            (None, 0, None, None, None, None, 0)
+        call("seg_dw2_wgrad_bn_bf16io", src.data_ptr(), ld, x.data_ptr(), ld, N, H, W, C, None, None, 0, Ho, Wo, s,
+             part.data_ptr(), *b, S())
+        call("seg_conv_wgrad_reduce", part.data_ptr(), blocks, dw.data_ptr(), C, 1, 3, 1, 0, S())
+        outs[bin_] = dw
+    torch.cuda.synchronize()
+    ref = torch.nn.grad.conv2d_weight(nchw(x, N, H, W, C, ld), (C, 1, 3, 3), nchw(dy, N, Ho, Wo, C, ld), stride=s,
+                                      padding=1, groups=C)
+    assert rel(outs[0], ref) < 1e-5 and rel(outs[1], ref) < 1e-5
+    if s == 2:  # the same tiles with and without BIN: the same sums
+        assert torch.equal(outs[0], outs[1])
+
+
+@pytest.mark.parametrize("N,C,H,W,s,ld", BN_CASES)
+@pytest.mark.parametrize("bin_", [False, True])
+def test_dw2_dgrad_bout_partials_and_finalize(N, C, H, W, s, ld, bin_):
+    """BOUT: dX unchanged; the producer's BN-backward reduction from the epilogue matches
+    seg_bn_bwd_coef_bf16io over the stored dX (fp32 partials, other grouping: rel 1e-5), repeat
+    launches (re-armed counters) are bitwise equal."""
+    Ho, Wo = outsz(H, s), outsz(W, s)
+    dyin = rows(N * Ho * Wo, ld, 41 + C)
+    yb = rows(N * Ho * Wo, ld, 42 + C, 2.0)
+    oy = rows(N * H * W, ld, 43 + C, 2.0)
+    _, wk = packw(C, C + 7)
+    bm, _, bsc, bsh, _, bk = bn_state(C, C + 11)
+    om, oinv, osc, osh, og, _ = bn_state(C, C + 13)
+    b = (yb.data_ptr(), ld, bsc.data_ptr(), bsh.data_ptr(), bm.data_ptr(), bk.data_ptr(), 2) if bin_ else \
+        (None, 0, None, None, None, None, 0)
+    ref = torch.zeros(N * H * W, ld, device=DEV, dtype=BF)
+    call("seg_dw2_dgrad_bn_bf16io", dyin.data_ptr(), ld, N, Ho, Wo, C, wk.data_ptr(), ref.data_ptr(), ld, H, W, s, 0,
+         *b, None, 0, None, None, None, None, None, 0, None, None, None, None, None, S())
+    tiles = query("seg_dw2_dgrad_tiles", N, H, W)
+    part = torch.full((tiles * 2 * C,), float("nan"), device=DEV)
+    cnt = torch.zeros((C + 63) // 64, device=DEV, dtype=torch.int32)
+    res = []
+    for _ in range(2):
+        dx = torch.zeros(N * H * W, ld, device=DEV, dtype=BF)
+        coef = torch.full((3 * C,), float("nan"), device=DEV)
+        dg, db = torch.full((C,), float("nan"), device=DEV), torch.full((C,), float("nan"), device=DEV)
+        call("seg_dw2_dgrad_bn_bf16io", dyin.data_ptr(), ld, N, Ho, Wo, C, wk.data_ptr(), dx.data_ptr(), ld, H, W, s,
+             0, *b, oy.data_ptr(), ld, osc.data_ptr(), osh.data_ptr(), om.data_ptr(), og.data_ptr(), oinv.data_ptr(), 2,
+             part.data_ptr(), dg.data_ptr(), db.data_ptr(), coef.data_ptr(), cnt.data_ptr(), S())
+        res.append((dx, coef, dg, db))
+    torch.cuda.synchronize()
+    assert torch.equal(res[0][0], ref)
+    for a, c in zip(res[0][1:], res[1][1:]):
+        assert torch.equal(a, c), "deterministic"
+    assert int(cnt.abs().sum()) == 0, "counters re-armed"
+    work = torch.empty(query("seg_chan_workspace_floats", N * H * W, C), device=DEV)
+    coef2 = torch.empty(3 * C, device=DEV)
+    dg2, db2 = torch.empty(C, device=DEV), torch.empty(C, device=DEV)
+    call("seg_bn_bwd_coef_bf16io", ref.data_ptr(), ld, oy.data_ptr(), ld, N * H * W, C, og.data_ptr(), om.data_ptr(),
+         oinv.data_ptr(), osc.data_ptr(), osh.data_ptr(), 2, dg2.data_ptr(), db2.data_ptr(), work.data_ptr(),
+         coef2.data_ptr(), S())
+    torch.cuda.synchronize()
+    _, coef, dg, db = res[0]
+    assert rel(coef, coef2) < 1e-5 and rel(dg, dg2) < 1e-5 and rel(db, db2) < 1e-5

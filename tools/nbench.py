@@ -158,7 +158,7 @@ def main():
             nt = query("seg_dw2_stat_tiles", N, Ho, Wo, s, None)
             st = torch.empty(max(nt, 1) * 2 * C, device="cuda")
             stp = st.data_ptr() if nt else None
-            nb2 = query("seg_dw2_wgrad_blocks", N, Ho, Wo, C, s)
+            nb2 = query("seg_dw2_wgrad_blocks", N, Ho, Wo, C, s, 0)
             p2 = torch.empty(nb2 * 9 * C, device="cuda")
             nb1 = query("seg_dw_wgrad_blocks", N, Ho, Wo, C)
             p1 = torch.empty(nb1 * 9 * C, device="cuda")

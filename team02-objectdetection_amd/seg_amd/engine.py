@@ -519,13 +519,13 @@ class ConvOp:
                 assert bin_ is None
                 rt.call(rt.k("seg_dw_dgrad"), dYp, dY.ld, y.N, y.H, y.W, self.cout, self.wk_f.data_ptr(), rt.gptr(i),
                         i.ld, i.H, i.W, self.stride, acc, s)
-                return
-            bout = self._bout(rt)
-            rt.call("seg_dw2_dgrad_bn_bf16io", dYp, dY.ld, y.N, y.H, y.W, self.cout, self.wk_f.data_ptr(), rt.gptr(i),
-                    i.ld, i.H, i.W, self.stride, acc,
-                    *(bin_ if bin_ is not None else (None, 0, None, None, None, None, 0)),
-                    *(bout if bout is not None else (None, 0, None, None, None, None, None, 0, None, None, None, None,
-                                                     None)), s)
+            else:
+                bout = self._bout(rt)
+                rt.call("seg_dw2_dgrad_bn_bf16io", dYp, dY.ld, y.N, y.H, y.W, self.cout, self.wk_f.data_ptr(),
+                        rt.gptr(i), i.ld, i.H, i.W, self.stride, acc,
+                        *(bin_ if bin_ is not None else (None, 0, None, None, None, None, 0)),
+                        *(bout if bout is not None else (None, 0, None, None, None, None, None, 0, None, None, None,
+                                                         None, None)), s)
         else:
             if self.stride != 1:
                 raise NotImplementedError("data gradient of a strided dense conv")
@@ -1331,7 +1331,10 @@ HALO2 = os.environ.get("SEG_HALO2", "1") == "1"
 # ... and their weight gradients on the persistent LDS-halo kernel (seg_conv_wgrad2_bf16io); SEG_WGRAD2=0 = off
 WGRAD2 = os.environ.get("SEG_WGRAD2", "1") == "1"
 # bf16io depthwise convs on the LDS-DMA tile kernels (csrc/dw2.hip); SEG_DW2=0 keeps dwconv.hip's strip kernels
-DW2 = os.environ.get("SEG_DW2", "1") == "1"
+# (default off: measured per launch against dwconv.hip at the bs=32 layers, tools/nbench.py --only dw, the strip
+# kernels are 1.0-1.9x faster on every layer of >= 64k pixels and equal below; the step A/B, profiles/r04f_ab.txt,
+# gives -0.3 % with the fused BN backward off and -5 % with it on)
+DW2 = os.environ.get("SEG_DW2", "0") == "1"
 # ... with their BatchNorm backwards fused (SEG_DW2_BN=0: three-launch seg_bn_backward): the depthwise conv's
 # own apply formed on load by its data / weight gradients, and the reduction of the expand conv that feeds it
 # computed in its data gradient's epilogue (images of at most DW2_BN_MAX_TILES 8 x 32-pixel tiles: the
@@ -1355,7 +1358,8 @@ IGEMM2 = os.environ.get("SEG_IGEMM2", "3")
 IGEMM2_MAX_ROWS = int(os.environ.get("SEG_IGEMM2_MAX_ROWS", "65536"))
 # ... and the 1x1 convs of small images on its 4-wave tiles (round 4: the generic register-staged kernel
 # keeps one K chunk in flight and ran the encoder's 4k-65k-row 1x1 convs at 0.4-1.5 TB/s); SEG_IGEMM2_1X1=0 = off
-IGEMM2_1X1 = os.environ.get("SEG_IGEMM2_1X1", "1") == "1"
+# (default off: step A/B +3 % without it, profiles/r04f_ab.txt)
+IGEMM2_1X1 = os.environ.get("SEG_IGEMM2_1X1", "0") == "1"
 IGEMM2_1X1_MAX_ROWS = int(os.environ.get("SEG_IGEMM2_1X1_MAX_ROWS", "65536"))
 # bf16io implicit GEMMs on bf16-packed weights (seg_conv_igemm_bf16io_w16); SEG_W16=0 keeps the fp32 packs
 W16 = os.environ.get("SEG_W16", "1") == "1"

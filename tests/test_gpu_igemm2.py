@@ -56,7 +56,7 @@ CASES = [  # (N, Cin, Cout, H, W, ks): split-K, dgrad-shaped, ragged M, taps spa
     (32, 128, 128, 32, 64, 3), (2, 960, 256, 16, 16, 1),
     # round 4: the 4-wave tiles -- the MobileNetV2 encoder's small-image 1x1 convs at bs=32 (M = 4k-65k rows),
     # K < one 64-deep step, ragged N, a 3x3 with 152 inputs
-    (32, 960, 160, 8, 16, 1), (32, 96, 576, 16, 32, 1), (32, 32, 192, 32, 64, 1), (32, 144, 32, 32, 64, 1),
+    (32, 960, 160, 8, 16, 1), (32, 96, 576, 16, 32, 1), (32, 32, 192, 32, 64, 1), (32, 144, 64, 32, 64, 1),
     (32, 320, 1280, 8, 16, 1), (32, 24, 144, 16, 32, 1), (8, 152, 64, 32, 64, 3)]
 
 

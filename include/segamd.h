@@ -91,6 +91,18 @@ int seg_conv_pw(const float* in, long ldin, long M, int K, const float* wk, int 
 /* Split-K factor for seg_conv_igemm_act (1 = none): > 1 only when the output tiles
  * cannot fill the 256 CUs (batch-1 inference). */
 int seg_conv_igemm_splits(long M, int Cout, int Cin, int ks);
+/* seg_conv_igemm as a stride-1 data gradient (pad ks/2, no bias, optional fused addend) that
+ * completes dA of a BatchNorm layer whose pre-BN output is `by`: the epilogue also writes that
+ * layer's BN-backward partials per row tile, bpart[seg_conv_igemm_row_tiles(M, Cout)][2][Cout] =
+ * (sum dz, sum dz (by - bmean)), dz = out * act'(by * bscale + bshift) on the values as stored --
+ * for seg_bn_bwd_finalize_tiles, in place of seg_bn_bwd_coef's reduction pass over dA (the
+ * BN-backward chain of src/unet.py:59-63 / torchvision's BatchNorm via src/unet.py:15-19). */
+int seg_conv_igemm_bnout_ok(long M, int Cout, int bf16);
+int seg_conv_igemm_bnout(const float* in, long ldin, int N, int H, int W, int Cin, const float* wk, int ldk,
+                         float* out, long ldout, int Cout, int ks, const float* add, long ldadd,
+                         const float* by, long ldby, const float* bscale, const float* bshift,
+                         const float* bmean, int bact, float* bpart, hipStream_t stream);
+
 /* Row tiles (and their height) seg_conv_igemm uses for an M x Cout output. */
 /* Tuning hook: force tile configuration t (0..7) for the following
  * seg_conv_igemm calls of this process, -1 = the built-in cost model. */
@@ -268,6 +280,10 @@ int seg_bn_backward(const float* da, long ldda, const float* y, long ldy, long M
  * seg_bn_bwd_coef: the reduction -- dgamma, dbeta and coef[3][C] = (gamma*invstd, mean(dz),
  * mean(dz*xhat)*invstd); work >= seg_chan_workspace_floats(M, C) floats.  seg_bn_bwd_apply:
  * dy = coef[0] * (dz - coef[1] - (y - mean) * coef[2]), dz = da * act'(y*scale + shift). */
+/* dgamma, dbeta and coef[3][C] (as seg_bn_bwd_coef) from BN-backward tile partials written by a
+ * producer's epilogue (seg_conv_igemm_bnout*: part[ntiles][2][C]) over M rows; fixed-order fp64. */
+int seg_bn_bwd_finalize_tiles(const float* part, int ntiles, long M, int C, const float* gamma,
+                              const float* invstd, float* dgamma, float* dbeta, float* coef, hipStream_t stream);
 int seg_bn_bwd_coef(const float* da, long ldda, const float* y, long ldy, long M, int C, const float* gamma,
                     const float* mean, const float* invstd, const float* scale, const float* shift, int act,
                     float* dgamma, float* dbeta, float* work, float* coef, hipStream_t stream);
@@ -386,6 +402,16 @@ int seg_dw_fwd_bf16io(const seg_bf16* in, long ldin, int N, int H, int W, int C,
     in_shift, int in_act, const float* wk, seg_bf16* out, long ldout, int Ho, int Wo, int stride, hipStream_t stream);
 int seg_dw_dgrad_bf16io(const seg_bf16* dy, long lddy, int N, int Ho, int Wo, int C, const float* wk, seg_bf16* dx,
     long lddx, int H, int W, int stride, int accumulate, hipStream_t stream);
+int seg_conv_igemm_bnout_bf16io(const seg_bf16* in, long ldin, int N, int H, int W, int Cin, const float* wk,
+                                int ldk, seg_bf16* out, long ldout, int Cout, int ks, const seg_bf16* add,
+                                long ldadd, const seg_bf16* by, long ldby, const float* bscale,
+                                const float* bshift, const float* bmean, int bact, float* bpart,
+                                hipStream_t stream);
+int seg_conv_igemm_bnout_bf16io_w16(const seg_bf16* in, long ldin, int N, int H, int W, int Cin,
+                                    const seg_bf16* wk, int ldk, seg_bf16* out, long ldout, int Cout, int ks,
+                                    const seg_bf16* add, long ldadd, const seg_bf16* by, long ldby,
+                                    const float* bscale, const float* bshift, const float* bmean, int bact,
+                                    float* bpart, hipStream_t stream);
 int seg_bn_bwd_coef_bf16io(const seg_bf16* da, long ldda, const seg_bf16* y, long ldy, long M, int C,
                            const float* gamma, const float* mean, const float* invstd, const float* scale,
                            const float* shift, int act, float* dgamma, float* dbeta, float* work, float* coef,

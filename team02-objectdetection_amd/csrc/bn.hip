@@ -869,6 +869,59 @@ SEG_API int seg_bn_backward_bf16io(const __bf16* da, long ldda, const __bf16* y,
                           lddy, stream);
 }
 
+// BN-backward finalize from per-row-tile partials part[t][2][C] = (sum dz, sum dz (y - mean)) of
+// a producer's epilogue (seg_conv_igemm_bnout*): the outputs of bn_bwd_finalize_kernel.  A block
+// owns 16 channels: 16 tile groups x 16 channels, each thread summing tiles g, g+16, ... in fp64,
+// then the groups in order (fixed order: deterministic).
+namespace {
+__global__ __launch_bounds__(256) void bn_bwd_finalize_tiles_kernel(const float* __restrict__ part, int ntiles, long M,
+                                                                    int C, const float* __restrict__ gamma,
+                                                                    const float* __restrict__ invstd, float* dgamma,
+                                                                    float* dbeta, float* coef) {
+  __shared__ double red[2][16][16];
+  const int g = threadIdx.x >> 4, cl = threadIdx.x & 15, c = blockIdx.x * 16 + cl;
+  double u = 0.0, v = 0.0;
+  if (c < C) {
+    int t = g;
+    for (; t + 48 < ntiles; t += 64) {
+      float x0[4], x1[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        x0[i] = part[((long)(t + 16 * i) * 2) * C + c];
+        x1[i] = part[((long)(t + 16 * i) * 2 + 1) * C + c];
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        u += (double)x0[i];
+        v += (double)x1[i];
+      }
+    }
+    for (; t < ntiles; t += 16) {
+      u += (double)part[((long)t * 2) * C + c];
+      v += (double)part[((long)t * 2 + 1) * C + c];
+    }
+  }
+  red[0][g][cl] = u;
+  red[1][g][cl] = v;
+  __syncthreads();
+  if (g == 0 && c < C) {
+    double sdz = 0.0, sdzx = 0.0;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      sdz += red[0][k][cl];
+      sdzx += red[1][k][cl];
+    }
+    const double inv = invstd[c];
+    const double gm = gamma ? gamma[c] : 1.0;
+    if (dbeta) dbeta[c] = (float)sdz;
+    if (dgamma) dgamma[c] = (float)(sdzx * inv);
+    coef[c] = (float)(gm * inv);
+    coef[C + c] = (float)(sdz / (double)M);
+    coef[2 * C + c] = (float)(sdzx * inv * inv / (double)M);
+  }
+}
+}  // namespace
+
 // The two halves of seg_bn_backward, for a caller that fuses one of them into a neighbouring
 // kernel (the depthwise convs of csrc/dw2.hip):
 //  * seg_bn_bwd_coef_*: the reduction -- dgamma, dbeta and coef[3][C] = (g*invstd, mean(dz),
@@ -914,6 +967,17 @@ SEG_API int seg_bn_bwd_apply_bf16io(const __bf16* da, long ldda, const __bf16* y
                                     const float* mean, const float* scale, const float* shift, int act,
                                     const float* coef, __bf16* dy, long lddy, hipStream_t stream) {
   return bn_bwd_apply_impl(da, ldda, y, ldy, M, C, mean, scale, shift, act, coef, dy, lddy, stream);
+}
+
+// dgamma, dbeta and coef[3][C] (as seg_bn_bwd_coef) from the BN-backward tile partials of a
+// producer's epilogue (seg_conv_igemm_bnout*: part[ntiles][2][C]) over M rows.
+SEG_API int seg_bn_bwd_finalize_tiles(const float* part, int ntiles, long M, int C, const float* gamma,
+                                      const float* invstd, float* dgamma, float* dbeta, float* coef,
+                                      hipStream_t stream) {
+  if (!part || ntiles < 1 || M < 1 || C < 1 || !invstd || !coef) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(bn_bwd_finalize_tiles_kernel, dim3(seg_cdiv(C, 16)), dim3(256), 0, stream, part, ntiles, M, C,
+                     gamma, invstd, dgamma, dbeta, coef);
+  SEG_RET_LAST();
 }
 
 SEG_API int seg_bn_eval_backward(const float* da, long ldda, const float* y, long ldy, long M, int C,

@@ -53,6 +53,23 @@ SEG_API int seg_conv_igemm_xf(const float* in, long ldin, int N, int H, int W, i
                                 add, ldadd, stat, SEG_ACT_NONE, nullptr, 1, stream, in_scale, in_shift, in_act);
 }
 
+// A stride-1 data gradient (out = the conv's input gradient, pad ks/2, no bias, optional fused
+// addend) that completes dA of a BatchNorm layer whose pre-BN output is `by`: the epilogue also
+// writes that layer's BN-backward partials per row tile -- bpart[seg_conv_igemm_row_tiles(M,
+// Cout)][2][Cout] = (sum dz, sum dz (by - bmean)), dz = out act'(by bscale + bshift) on the stored
+// values -- for seg_bn_bwd_finalize_tiles, in place of seg_bn_bwd_coef's reduction pass over dA.
+// 1 when seg_conv_igemm_bnout (bf16 = 0) / _bnout_bf16io[_w16] (bf16 = 1) takes an M x Cout output.
+SEG_API int seg_conv_igemm_bnout_ok(long M, int Cout, int bf16) { return igemm_bnout_tile_ok(M, Cout, bf16 ? 2 : 4); }
+
+SEG_API int seg_conv_igemm_bnout(const float* in, long ldin, int N, int H, int W, int Cin, const float* wk, int ldk,
+                                 float* out, long ldout, int Cout, int ks, const float* add, long ldadd,
+                                 const float* by, long ldby, const float* bscale, const float* bshift,
+                                 const float* bmean, int bact, float* bpart, hipStream_t stream) {
+  return conv_igemm_impl<float>(in, ldin, N, H, W, Cin, wk, ldk, nullptr, out, ldout, H, W, Cout, ks, 1, ks / 2, add,
+                                ldadd, nullptr, SEG_ACT_NONE, nullptr, 1, stream, nullptr, nullptr, 0, by, ldby,
+                                bscale, bshift, bmean, bact, bpart);
+}
+
 SEG_API int seg_conv_igemm(const float* in, long ldin, int N, int H, int W, int Cin,
                            const float* wk, int ldk, const float* bias,
                            float* out, long ldout, int Ho, int Wo, int Cout,

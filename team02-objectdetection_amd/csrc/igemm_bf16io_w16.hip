@@ -27,3 +27,15 @@ SEG_API int seg_conv_igemm_bf16io_xf_w16(const __bf16* in, long ldin, int N, int
                                                stride, pad, add, ldadd, stat, SEG_ACT_NONE, nullptr, 1, stream,
                                                in_scale, in_shift, in_act);
 }
+
+// seg_conv_igemm_bf16io_w16 as a stride-1 data gradient that completes dA of a BatchNorm layer:
+// plus the BN-backward partials of out (IgemmArgs::bpart; see seg_conv_igemm_bnout).
+SEG_API int seg_conv_igemm_bnout_bf16io_w16(const __bf16* in, long ldin, int N, int H, int W, int Cin,
+                                            const __bf16* wk, int ldk, __bf16* out, long ldout, int Cout, int ks,
+                                            const __bf16* add, long ldadd, const __bf16* by, long ldby,
+                                            const float* bscale, const float* bshift, const float* bmean, int bact,
+                                            float* bpart, hipStream_t stream) {
+  return conv_igemm_impl<__bf16, __bf16, true>(in, ldin, N, H, W, Cin, wk, ldk, nullptr, out, ldout, H, W, Cout, ks,
+                                               1, ks / 2, add, ldadd, nullptr, SEG_ACT_NONE, nullptr, 1, stream,
+                                               nullptr, nullptr, 0, by, ldby, bscale, bshift, bmean, bact, bpart);
+}

@@ -38,6 +38,11 @@ struct IgemmArgs {
   // applied on load instead of by a separate pass (seg_bn_act4: the same fp32 value the
   // pass would have stored, rounded to the storage type only where the pass would have)
   const float* xs; const float* xb; int xact;
+  // optional BatchNorm-backward partials of `out` (a data gradient that completes dA of a BN
+  // layer whose pre-BN output is `by`, [M][ldby] IT): per BM-row tile and column, the sums of
+  // dz and dz (by - bmu), dz = out act'(by bsc + bsh) on the values as stored, into bpart
+  // [tilesM][2][Cout] for seg_bn_bwd_finalize_tiles -- the reduction pass over dA disappears
+  const void* by; long ldby; const float* bsc; const float* bsh; const float* bmu; int bact; float* bpart;
 };
 
 #ifndef SEG_IGEMM_DEPTH
@@ -78,7 +83,7 @@ struct IgemmArgs {
 // no conversion on the way into LDS.  Bitwise the fp32-weight kernel: the RNE rounding
 // is the same, done once at pack time.
 template <int BM, int BN, int WM, int WN, int KS, int BK, bool UT, typename OT = float, typename IT = float,
-          bool WB = false>
+          bool WB = false, bool BO = false>
 __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void igemm_conv_kernel(IgemmArgs a) {
   static_assert(!WB || std::is_same<OT, __bf16>::value, "bf16 weights feed bf16 operands");
   const float* wk32 = static_cast<const float*>(a.wk);
@@ -520,6 +525,29 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void igemm_conv_kernel(
     constexpr int VO = 16 / (int)sizeof(IT);  // output elements per 16-byte store
     constexpr int VPR = BN / VO;              // vectors per band row
     static_assert(BN % VO == 0, "whole vectors per tile row");
+    // BN-backward partials (tiles with 64 % VPR == 0: a thread's stores all fall in one column
+    // vector, lane % VPR; the host refuses bpart on the other tiles, seg_conv_igemm_bnout_ok)
+    constexpr bool BOK = BO && 64 % VPR == 0;  // BO: the bpart instantiation (its registers only there)
+    static_assert(!BOK || 2 * (NT / 64) * BN * 4 <= (int)sizeof(smem), "BN-backward scratch");
+    const IT* by = static_cast<const IT*>(a.by);
+    const int bcv = (tid % VPR) * VO;
+    float bs0[VO], bs1[VO], bsc[VO], bsh[VO], bmu[VO];
+    constexpr bool bon = BOK;
+    if (bon) {
+#pragma unroll
+      for (int j = 0; j < VO; ++j) {
+        const int c = min(n0 + bcv + j, a.Cout - 1);
+        bs0[j] = bs1[j] = 0.f;
+        bsc[j] = a.bsc[c];
+        bsh[j] = a.bsh[c];
+        bmu[j] = a.bmu[c];
+      }
+    }
+    auto bacc = [&](int j, float g, float v) {  // g: dA as stored, v: the pre-BN output
+      const float dz = g * seg_act_mask(v * bsc[j] + bsh[j], a.bact);
+      bs0[j] += dz;
+      bs1[j] += dz * (v - bmu[j]);
+    };
 #pragma unroll
     for (int b = 0; b < BM / WM; ++b) {
       __syncthreads();  // the K loop / statistics / previous band are done with smem
@@ -567,10 +595,20 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void igemm_conv_kernel(
           }
           if constexpr (VO == 8) {
             const f32x4 lo = {o[0], o[1], o[2], o[3]}, hi = {o[4], o[5], o[6], o[7]};
-            *reinterpret_cast<bf16x8*>(dst) =
-                seg_cat8(__builtin_convertvector(lo, bf16x4), __builtin_convertvector(hi, bf16x4));
+            const bf16x8 q = seg_cat8(__builtin_convertvector(lo, bf16x4), __builtin_convertvector(hi, bf16x4));
+            *reinterpret_cast<bf16x8*>(dst) = q;
+            if (bon) {
+              const bf16x8 yv = *reinterpret_cast<const bf16x8*>(by + (long)row * a.ldby + col);
+#pragma unroll
+              for (int j = 0; j < 8; ++j) bacc(j, (float)q[j], (float)yv[j]);
+            }
           } else {
             *reinterpret_cast<f32x4*>(dst) = f32x4{o[0], o[1], o[2], o[3]};
+            if (bon) {
+              const IT* yp = by + (long)row * a.ldby + col;
+#pragma unroll
+              for (int j = 0; j < VO; ++j) bacc(j, o[j], (float)yp[j]);
+            }
           }
         } else {
 #pragma unroll
@@ -579,8 +617,40 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void igemm_conv_kernel(
             float x = o[j];
             if (ad) x += (float)ad[j];
             if (a.act) x = seg_act(x, a.act);
-            dst[j] = static_cast<IT>(x);
+            const IT q = static_cast<IT>(x);
+            dst[j] = q;
+            if (bon) bacc(j, (float)q, (float)by[(long)row * a.ldby + col + j]);
           }
+        }
+      }
+    }
+    if constexpr (BOK) {
+      {  // the tile's partials: lanes of one column vector (xor over lane bits >= VPR), then waves
+        constexpr int NW = NT / 64;
+        float* red = reinterpret_cast<float*>(smem);  // [2][NW][BN]
+#pragma unroll
+        for (int j = 0; j < VO; ++j) {
+#pragma unroll
+          for (int o = VPR; o < 64; o *= 2) {
+            bs0[j] += __shfl_xor(bs0[j], o, 64);
+            bs1[j] += __shfl_xor(bs1[j], o, 64);
+          }
+        }
+        __syncthreads();
+        if (lane < VPR) {
+#pragma unroll
+          for (int j = 0; j < VO; ++j) {
+            red[(0 * NW + wave) * BN + bcv + j] = bs0[j];
+            red[(1 * NW + wave) * BN + bcv + j] = bs1[j];
+          }
+        }
+        __syncthreads();
+        for (int q = tid; q < 2 * BN; q += NT) {
+          const int h = q / BN, c = q - h * BN;
+          float t = 0.f;
+#pragma unroll
+          for (int k = 0; k < NW; ++k) t += red[(h * NW + k) * BN + c];
+          if (n0 + c < a.Cout) a.bpart[((long)tm * 2 + h) * a.Cout + n0 + c] = t;
         }
       }
     }
@@ -595,11 +665,24 @@ int launch_igemm_bk(const IgemmArgs& a, int ks, hipStream_t s) {
                   (sizeof(IT) == 4 || (a.Cin % 8 == 0 && a.ldin % 8 == 0));  // bf16 A: 16-byte slots
   constexpr int NT = 64 * (BM / WM) * (BN / WN);
   if (a.xs && !ut) return (int)hipErrorInvalidValue;  // input transform: the uniform-tap loader only (Cin >= BK)
-#define SEG_IG(KS, U) hipLaunchKernelGGL((igemm_conv_kernel<BM, BN, WM, WN, KS, BK, U, OT, IT, WB>), dim3(grid, splits), dim3(NT), 0, s, a)
+#define SEG_IG(KS, U, B) hipLaunchKernelGGL((igemm_conv_kernel<BM, BN, WM, WN, KS, BK, U, OT, IT, WB, B>), dim3(grid, splits), dim3(NT), 0, s, a)
+  constexpr int VPR = BN / (16 / (int)sizeof(IT));
+  // (instantiated for the training storage types only: f32 and bf16io, where operands are the storage type)
+  if constexpr (std::is_same<OT, IT>::value && BN % (16 / (int)sizeof(IT)) == 0 && 64 % VPR == 0) {
+    if (a.bpart) {  // the BN-backward-partials instantiation (seg_conv_igemm_bnout*)
+      if (ks == 1) {
+        if (ut) SEG_IG(1, true, true); else SEG_IG(1, false, true);
+      } else {
+        if (ut) SEG_IG(3, true, true); else SEG_IG(3, false, true);
+      }
+      SEG_RET_LAST();
+    }
+  }
+  if (a.bpart) return (int)hipErrorInvalidValue;
   if (ks == 1) {
-    if (ut) SEG_IG(1, true); else SEG_IG(1, false);
+    if (ut) SEG_IG(1, true, false); else SEG_IG(1, false, false);
   } else {
-    if (ut) SEG_IG(3, true); else SEG_IG(3, false);
+    if (ut) SEG_IG(3, true, false); else SEG_IG(3, false, false);
   }
 #undef SEG_IG
   SEG_RET_LAST();
@@ -644,6 +727,13 @@ constexpr TileCfg kTiles[] = {
 };
 
 constexpr int kTileBM[] = {128, 64, 128, 64, 128, 128, 256, 128, 128, 128, 256, 128, 128, 256, 64};
+
+int pick_tile(long M, int N);
+// seg_conv_igemm_bnout*: the picked tile's epilogue holds one column vector per lane (64 % (BN / VO) == 0)
+inline bool igemm_bnout_tile_ok(long M, int N, int es) {
+  const int bn = kTiles[pick_tile(M, N)].bn, vo = 16 / es;
+  return bn % vo == 0 && 64 % (bn / vo) == 0;
+}
 
 int pick_tile(long M, int N) {
   if (seg_igemm_forced_tile >= 0) return seg_igemm_forced_tile;
@@ -702,7 +792,9 @@ template <typename OT, typename IT = float, bool WB = false>
 int conv_igemm_impl(const IT* in, long ldin, int N, int H, int W, int Cin, const void* wk, int ldk,
                     const float* bias, IT* out, long ldout, int Ho, int Wo, int Cout, int ks, int stride, int pad,
                     const IT* add, long ldadd, float* stat, int act, float* work, int splits, hipStream_t stream,
-                    const float* xs = nullptr, const float* xb = nullptr, int xact = 0) {
+                    const float* xs = nullptr, const float* xb = nullptr, int xact = 0, const IT* by = nullptr,
+                    long ldby = 0, const float* bsc = nullptr, const float* bsh = nullptr, const float* bmu = nullptr,
+                    int bact = 0, float* bpart = nullptr) {
   if (!std::is_same<IT, float>::value && splits != 1) return (int)hipErrorInvalidValue;
   if ((Cin & 3) || (ldin & 3) || (ldk & 3) || (ks != 1 && ks != 3)) return (int)hipErrorInvalidValue;
   if (WB && ((ldk & 7) || ((uintptr_t)wk & 15) || splits != 1)) return (int)hipErrorInvalidValue;
@@ -711,6 +803,7 @@ int conv_igemm_impl(const IT* in, long ldin, int N, int H, int W, int Cin, const
   if (ks == 1 && (stride != 1 || pad != 0 || Ho != H || Wo != W)) return (int)hipErrorInvalidValue;
   if (act < SEG_ACT_NONE || act > SEG_ACT_RELU6 || (act && stat)) return (int)hipErrorInvalidValue;
   if (splits < 1 || (splits > 1 && (!work || stat))) return (int)hipErrorInvalidValue;
+  if (bpart && (!by || !bsc || !bsh || !bmu || splits != 1 || act || (ldby & 3))) return (int)hipErrorInvalidValue;
   if (splits > 1) {  // the K ranges actually launched: whole BK chunks, no empty range (launch_igemm)
     const int nk = seg_cdiv((long)ks * ks * Cin, igemm_bk(ks * ks * Cin));
     splits = seg_cdiv(nk, seg_cdiv(nk, splits));
@@ -722,6 +815,8 @@ int conv_igemm_impl(const IT* in, long ldin, int N, int H, int W, int Cin, const
   a.stride = stride; a.pad = pad; a.K = ks * ks * Cin; a.M = N * Ho * Wo; a.act = act;
   a.part = splits > 1 ? work : nullptr;
   a.xs = xs; a.xb = xb; a.xact = xact;
+  a.by = by; a.ldby = ldby; a.bsc = bsc; a.bsh = bsh; a.bmu = bmu; a.bact = bact; a.bpart = bpart;
+  if (bpart && !igemm_bnout_tile_ok(a.M, Cout, (int)sizeof(IT))) return (int)hipErrorInvalidValue;
   if (a.M == 0 || Cout == 0) return 0;
   int rc;
   switch (pick_tile(a.M, Cout)) {

@@ -113,6 +113,10 @@ PROTOTYPES = {
                                      _V, _L, _V, _V, _V, _V, _I, _V]),
     "seg_bn_bwd_coef": (_I, [_V, _L, _V, _L, _L, _I, _V, _V, _V, _V, _V, _I, _V, _V, _V, _V, _V]),
     "seg_bn_bwd_apply": (_I, [_V, _L, _V, _L, _L, _I, _V, _V, _V, _I, _V, _V, _L, _V]),
+    "seg_bn_bwd_finalize_tiles": (_I, [_V, _I, _L, _I, _V, _V, _V, _V, _V, _V]),
+    "seg_conv_igemm_bnout_ok": (_I, [_L, _I, _I]),
+    "seg_conv_igemm_bnout": (_I, [_V, _L, _I, _I, _I, _I, _V, _I, _V, _L, _I, _I, _V, _L, _V, _L, _V, _V, _V, _I,
+                                  _V, _V]),
 }
 # bf16-storage variants: same C signature shape as their fp32 namesakes (pointers stay void*)
 for _n in ("seg_add", "seg_bn_stats", "seg_bn_apply", "seg_bn_backward", "seg_colsum", "seg_dw_fwd", "seg_dw_dgrad",
@@ -122,6 +126,8 @@ for _n in ("seg_add", "seg_bn_stats", "seg_bn_apply", "seg_bn_backward", "seg_co
 PROTOTYPES["seg_conv_igemm_bf16io"] = PROTOTYPES["seg_conv_igemm"]
 PROTOTYPES["seg_dw2_dgrad_bf16io"] = PROTOTYPES["seg_dw_dgrad"]
 PROTOTYPES["seg_bn_bwd_coef_bf16io"] = PROTOTYPES["seg_bn_bwd_coef"]
+PROTOTYPES["seg_conv_igemm_bnout_bf16io"] = PROTOTYPES["seg_conv_igemm_bnout"]
+PROTOTYPES["seg_conv_igemm_bnout_bf16io_w16"] = PROTOTYPES["seg_conv_igemm_bnout"]
 PROTOTYPES["seg_bn_bwd_apply_bf16io"] = PROTOTYPES["seg_bn_bwd_apply"]
 PROTOTYPES["seg_dw2_wgrad_bf16io"] = PROTOTYPES["seg_dw_wgrad"]
 PROTOTYPES["seg_conv_wgrad_bf16io"] = PROTOTYPES["seg_conv_wgrad"]

@@ -35,7 +35,7 @@ from ._lib import call, query as _query
 _PURE_QUERIES = {"seg_chan_workspace_floats", "seg_conv_wgrad_splits", "seg_conv_wgrad_splits_bf16", "seg_dw_wgrad_blocks",
                  "seg_conv_igemm_splits", "seg_ce_workspace_floats", "seg_conv_wino_row_tiles", "seg_conv_wino_tile_rows",
                  "seg_conv_halo_row_tiles", "seg_conv_wino_wgrad_splits", "seg_dw2_ok",
-                 "seg_dw2_wgrad_blocks", "seg_dw2_dgrad_tiles"}
+                 "seg_dw2_wgrad_blocks", "seg_dw2_dgrad_tiles", "seg_conv_igemm_bnout_ok"}
 _QCACHE = {}
 
 
@@ -399,6 +399,30 @@ class ConvOp:
         return (rt.ptr(p.y), p.y.ld, scale, shift, mean, p.bn.weight.data_ptr(), invstd, p.act, part.data_ptr(), g_w,
                 g_b, coef.data_ptr(), cnt.data_ptr())
 
+    def _bnout(self, rt, i):
+        """BN-backward partials from this data gradient's epilogue (seg_conv_igemm_bnout*), when its output
+        region is exactly the output of a train-mode BatchNorm layer P: the extra arguments, or None.  P's
+        backward uses them if no other write reached the buffer afterwards (Run.wgen)."""
+        if not BNOUT or not rt.training:
+            return None
+        p = rt.prog.bn_owner().get(i.key())
+        if p is None or id(p) not in rt.saved:
+            return None
+        v = 16 // rt.es
+        py = p.y
+        if py.ld % v or py.off % v or rt.ptr(py) % 16:
+            return None
+        if not query("seg_conv_igemm_bnout_ok", i.M, self.cin, int(rt.io)):
+            return None
+        tiles, _ = rt.row_tiles(i.M, self.cin)
+        if tiles > BNOUT_MAX_TILES:
+            return None
+        C = p.cout
+        mean, invstd, scale, shift = _stat_ptrs(rt.saved[id(p)], C)
+        part = rt.tmp(tiles * 2 * C)
+        rt.bn_parts[id(p)] = [part, tiles, None]
+        return (rt.ptr(py), py.ld, scale, shift, mean, p.act, part.data_ptr()), p
+
     def backward(self, rt):
         s, y = rt.stream, self.y
         bin_ = None
@@ -411,7 +435,14 @@ class ConvOp:
             mean, invstd, scale, shift = _stat_ptrs(st, C)
             g_w, g_b = rt.grad_param(self.bn.weight), rt.grad_param(self.bn.bias)
             coef = rt.bn_coef.pop(id(self), None)
-            if coef is not None:  # the reduction ran in the consumer's data gradient (BOUT): the apply alone
+            bp = rt.bn_parts.pop(id(self), None)
+            if bp is not None and bp[2] == rt.wgen.get(self.out.buf):
+                # the reduction's partials came out of the epilogue of the data gradient that completed dA (nothing
+                # wrote the buffer since): finalize them, then the apply
+                coef = rt.tmp(3 * C)
+                rt.call("seg_bn_bwd_finalize_tiles", bp[0].data_ptr(), bp[1], M, C, self.bn.weight.data_ptr(), invstd,
+                        g_w, g_b, coef.data_ptr(), s)
+            if coef is not None:  # the reduction ran elsewhere (a consumer's epilogue): the apply alone
                 dY = Act(rt.tmp_buf(M * r4(C)), 0, r4(C), C, y.N, y.H, y.W)
                 rt.call(rt.k("seg_bn_bwd_apply"), rt.gptr(dA), dA.ld, rt.ptr(y), y.ld, M, C, mean, scale, shift,
                         self.act, coef.data_ptr(), rt.ptr(dY), dY.ld, s)
@@ -530,6 +561,7 @@ class ConvOp:
             if self.stride != 1:
                 raise NotImplementedError("data gradient of a strided dense conv")
             kin = r4(self.cout)  # dY channels padded to 4 (the C=10 head)
+            bo = None
             add_ptr, add_ld = rt.begin_write_add(i)
             # seg_conv_pw / seg_conv_igemm2 read the addend as 16-byte row vectors
             add16 = add_ptr is None or (add_ld % (16 // rt.es) == 0 and add_ptr % 16 == 0)
@@ -554,18 +586,35 @@ class ConvOp:
                          self.wk_d.data_ptr(), self.ldk_d, None, rt.gptr(i), i.ld, self.cin, self.ks, add_ptr, add_ld,
                          None, work.data_ptr(), s)
             elif rt.io:
-                rt.tcall(f"igemm{self.ks}_dgrad", self.flops(),
-                         "seg_conv_igemm_bf16io_w16" if self.w16_d else "seg_conv_igemm_bf16io", dYp, dY.ld, y.N, y.H, y.W,
-                            kin, self.wk_d.data_ptr(), self.ldk_d, None, rt.gptr(i), i.ld, i.H, i.W, self.cin,
-                            self.ks, 1, self.pad, add_ptr, add_ld, None, s)
+                bo = self._bnout(rt, i)
+                if bo is not None:  # + the BN-backward partials of the layer whose dA this completes
+                    rt.tcall(f"igemm{self.ks}_dgrad", self.flops(),
+                             "seg_conv_igemm_bnout_bf16io_w16" if self.w16_d else "seg_conv_igemm_bnout_bf16io", dYp,
+                             dY.ld, y.N, y.H, y.W, kin, self.wk_d.data_ptr(), self.ldk_d, rt.gptr(i), i.ld, self.cin,
+                             self.ks, add_ptr, add_ld, *bo[0], s)
+                else:
+                    rt.tcall(f"igemm{self.ks}_dgrad", self.flops(),
+                             "seg_conv_igemm_bf16io_w16" if self.w16_d else "seg_conv_igemm_bf16io", dYp, dY.ld, y.N, y.H,
+                             y.W, kin, self.wk_d.data_ptr(), self.ldk_d, None, rt.gptr(i), i.ld, i.H, i.W, self.cin,
+                             self.ks, 1, self.pad, add_ptr, add_ld, None, s)
             elif self.bf:
                 rt.tcall(f"igemm{self.ks}_dgrad", self.flops(), "seg_conv_igemm_bf16", dYp, dY.ld, y.N, y.H, y.W,
                             kin, self.wk_d.data_ptr(), self.ldk_d, None, rt.gptr(i), i.ld, i.H, i.W, self.cin,
                             self.ks, 1, self.pad, add_ptr, add_ld, None, ACT_NONE, None, 1, s)
             else:
-                rt.tcall(f"igemm{self.ks}_dgrad", self.flops(), "seg_conv_igemm", dYp, dY.ld, y.N, y.H, y.W, kin,
-                            self.wk_d.data_ptr(), self.ldk_d, None, rt.gptr(i), i.ld, i.H, i.W, self.cin, self.ks, 1,
-                            self.pad, add_ptr, add_ld, None, s)
+                bo = self._bnout(rt, i)
+                if bo is not None:
+                    rt.tcall(f"igemm{self.ks}_dgrad", self.flops(), "seg_conv_igemm_bnout", dYp, dY.ld, y.N, y.H, y.W,
+                             kin, self.wk_d.data_ptr(), self.ldk_d, rt.gptr(i), i.ld, self.cin, self.ks, add_ptr, add_ld,
+                             *bo[0], s)
+                else:
+                    rt.tcall(f"igemm{self.ks}_dgrad", self.flops(), "seg_conv_igemm", dYp, dY.ld, y.N, y.H, y.W, kin,
+                             self.wk_d.data_ptr(), self.ldk_d, None, rt.gptr(i), i.ld, i.H, i.W, self.cin, self.ks, 1,
+                             self.pad, add_ptr, add_ld, None, s)
+            if bo is not None:  # the partials are valid while this write is the buffer's last
+                rt.mark_written(i)
+                rt.bn_parts[id(bo[1])][2] = rt.wgen[i.buf]
+                return
         rt.mark_written(i)
 
 
@@ -628,6 +677,13 @@ class Program:
         self._n = 0
         self.image = self.new(3, H, W, name=IMAGE)  # NHWC4 copy of the input batch
 
+    def bn_owner(self):
+        """Activation key -> the ConvOp with a BatchNorm whose output it is (the BN-backward reduction target of a
+        data gradient writing exactly that region; ConvOp._bnout)."""
+        m = getattr(self, "_bn_owner", None)
+        if m is None:
+            m = self._bn_owner = {op.out.key(): op for op in self.ops if isinstance(op, ConvOp) and op.bn is not None}
+        return m
     def new(self, C, H, W, name=None):
         name = name or f"t{self._n}"
         self._n += 1
@@ -1069,6 +1125,9 @@ class Run:
                      for n, (rows, ld) in prog.bufs.items()}
         self.saved = {}
         self.bn_coef = {}     # id(op) -> BN-backward coefficients [3][C] computed by its consumer (dw2 BOUT)
+        self.bn_parts = {}    # id(op) -> [tile partials, tiles, write generation]: its BN-backward reduction from
+                              # the epilogue of the data gradient that completed its dA (seg_conv_igemm_bnout*)
+        self.wgen = {}        # gradient buffer name -> write generation (every write to the buffer bumps it)
         self.gbufs = {}
         self.keep = []        # workspaces of a recorded run (persistent: the tape points at them)
         self.written = {}     # grad buffer name -> list of (lo, hi) channel ranges
@@ -1114,6 +1173,7 @@ class Run:
 
     def zero(self, a: Act):
         """Zero-fill the gradient region of `a` (a channel slice of a row buffer)."""
+        self.wgen[a.buf] = self.wgen.get(a.buf, 0) + 1
         if self.rec is not None:
             self.rec.memset2d(self.gptr(a), a.ld * self.es, 0, a.C * self.es, a.M, self.stream)
         else:
@@ -1202,6 +1262,7 @@ class Run:
 
     def mark_written(self, a: Act):
         self.written.setdefault(a.buf, []).append((a.off, a.off + a.C))
+        self.wgen[a.buf] = self.wgen.get(a.buf, 0) + 1
 
     def grad_of(self, a: Act) -> Act:
         """Gradient region of activation `a` (zero-filled if nobody wrote it)."""
@@ -1218,6 +1279,7 @@ class Run:
         if self._covered(target):
             self.call(self.k("seg_add"), self.gptr(target), target.ld, self.gptr(addend), addend.ld, target.M, target.C,
                       self.gptr(target), target.ld, self.stream)
+            self.wgen[target.buf] = self.wgen.get(target.buf, 0) + 1
         else:
             self.pending[target.key()] = addend
 
@@ -1327,9 +1389,15 @@ WINOGRAD_DGRAD = os.environ.get("SEG_WINO_DGRAD", "1") == "1"
 # LDS-halo direct 3x3 conv for the narrow convs in the bf16io configuration; SEG_HALO_BF16=0 turns it off.
 HALO_BF16 = os.environ.get("SEG_HALO_BF16", "1") == "1"
 # ... and the persistent LDS-DMA halo kernel (seg_conv_halo2_bf16io) where it applies; SEG_HALO2=0 = off
-HALO2 = os.environ.get("SEG_HALO2", "1") == "1"
+HALO2 = os.environ.get("SEG_HALO2", "0") == "1"  # default off: step A/B -0.7 % (profiles/r04k_ab.txt)
 # ... and their weight gradients on the persistent LDS-halo kernel (seg_conv_wgrad2_bf16io); SEG_WGRAD2=0 = off
 WGRAD2 = os.environ.get("SEG_WGRAD2", "1") == "1"
+# BatchNorm-backward reduction from the epilogue of the implicit-GEMM data gradient that completes a BN layer's dA
+# (seg_conv_igemm_bnout*: no reduction pass over dA; the finalize reads the tile partials); SEG_BNOUT=0 = off.  Up to
+# BNOUT_MAX_TILES row tiles (the finalize's serial tile loop), i.e. the small-image layers where the three-launch
+# BN backward is latency-bound
+BNOUT = os.environ.get("SEG_BNOUT", "1") == "1"
+BNOUT_MAX_TILES = int(os.environ.get("SEG_BNOUT_MAX_TILES", "1024"))
 # bf16io depthwise convs on the LDS-DMA tile kernels (csrc/dw2.hip); SEG_DW2=0 keeps dwconv.hip's strip kernels
 # (default off: measured per launch against dwconv.hip at the bs=32 layers, tools/nbench.py --only dw, the strip
 # kernels are 1.0-1.9x faster on every layer of >= 64k pixels and equal below; the step A/B, profiles/r04f_ab.txt,

@@ -533,6 +533,7 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void igemm_conv_kernel(
     const int bcv = (tid % VPR) * VO;
     float bs0[VO], bs1[VO], bsc[VO], bsh[VO], bmu[VO];
     constexpr bool bon = BOK;
+    (void)by;
     if (bon) {
 #pragma unroll
       for (int j = 0; j < VO; ++j) {
@@ -548,23 +549,11 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void igemm_conv_kernel(
       bs0[j] += dz;
       bs1[j] += dz * (v - bmu[j]);
     };
-#pragma unroll
-    for (int b = 0; b < BM / WM; ++b) {
-      __syncthreads();  // the K loop / statistics / previous band are done with smem
-      if (wm0 == b * WM) {
-#pragma unroll
-        for (int ni = 0; ni < NI; ++ni)
-#pragma unroll
-          for (int mi = 0; mi < MI; ++mi)
-#pragma unroll
-            for (int r = 0; r < 16; ++r)
-              Cs[(mi * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5)) * CSR + wn0 + ni * 32 + lrow] = acc[mi][ni][r];
-      }
-      __syncthreads();
-      for (int v = tid; v < WM * VPR; v += NT) {
+    // one 16-byte output vector v of band b (yq: the BN-backward y vector when BO, prefetched)
+    auto store_vec = [&](int b, int v, f32x4 yq) {
         const int rr = v / VPR, cv = (v - rr * VPR) * VO;
         const int row = m0 + b * WM + rr, col = n0 + cv;
-        if (row >= a.M || col >= a.Cout) continue;
+        if (row >= a.M || col >= a.Cout) return;
         float o[VO];
 #pragma unroll
         for (int j = 0; j < VO; j += 4) {
@@ -597,17 +586,17 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void igemm_conv_kernel(
             const f32x4 lo = {o[0], o[1], o[2], o[3]}, hi = {o[4], o[5], o[6], o[7]};
             const bf16x8 q = seg_cat8(__builtin_convertvector(lo, bf16x4), __builtin_convertvector(hi, bf16x4));
             *reinterpret_cast<bf16x8*>(dst) = q;
-            if (bon) {
-              const bf16x8 yv = *reinterpret_cast<const bf16x8*>(by + (long)row * a.ldby + col);
+            if constexpr (bon) {
+              const bf16x8 yv = __builtin_bit_cast(bf16x8, yq);
 #pragma unroll
               for (int j = 0; j < 8; ++j) bacc(j, (float)q[j], (float)yv[j]);
             }
           } else {
             *reinterpret_cast<f32x4*>(dst) = f32x4{o[0], o[1], o[2], o[3]};
-            if (bon) {
-              const IT* yp = by + (long)row * a.ldby + col;
+            if constexpr (bon) {
+              const f32x4 yv = __builtin_bit_cast(f32x4, yq);
 #pragma unroll
-              for (int j = 0; j < VO; ++j) bacc(j, o[j], (float)yp[j]);
+              for (int j = 0; j < VO; ++j) bacc(j, o[j], (float)yv[j]);
             }
           }
         } else {
@@ -619,9 +608,47 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void igemm_conv_kernel(
             if (a.act) x = seg_act(x, a.act);
             const IT q = static_cast<IT>(x);
             dst[j] = q;
-            if (bon) bacc(j, (float)q, (float)by[(long)row * a.ldby + col + j]);
+            if constexpr (bon) bacc(j, (float)q, (float)by[(long)row * a.ldby + col + j]);
           }
         }
+    };
+    // BO: the pre-BN y vectors of every output vector this thread stores, loaded before the bands
+    // (their latency overlaps the LDS staging instead of serialising each store)
+    constexpr int NVB = (WM * VPR + NT - 1) / NT;
+    f32x4 yreg[BOK ? BM / WM : 1][BOK ? NVB : 1];
+    if constexpr (BOK) {
+#pragma unroll
+      for (int b = 0; b < BM / WM; ++b)
+#pragma unroll
+        for (int k = 0; k < NVB; ++k) {
+          const int v = tid + k * NT, rr = v / VPR, cv = (v - rr * VPR) * VO;
+          const int row = m0 + b * WM + rr, col = n0 + cv;
+          const bool ok = v < WM * VPR && row < a.M && col + VO <= a.Cout;
+          yreg[b][k] = *reinterpret_cast<const f32x4*>(ok ? (const void*)(by + (long)row * a.ldby + col)
+                                                          : (const void*)g_zero4);
+        }
+    }
+#pragma unroll
+    for (int b = 0; b < BM / WM; ++b) {
+      __syncthreads();  // the K loop / statistics / previous band are done with smem
+      if (wm0 == b * WM) {
+#pragma unroll
+        for (int ni = 0; ni < NI; ++ni)
+#pragma unroll
+          for (int mi = 0; mi < MI; ++mi)
+#pragma unroll
+            for (int r = 0; r < 16; ++r)
+              Cs[(mi * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5)) * CSR + wn0 + ni * 32 + lrow] = acc[mi][ni][r];
+      }
+      __syncthreads();
+      if constexpr (BOK) {
+#pragma unroll
+        for (int k = 0; k < NVB; ++k) {
+          const int v = tid + k * NT;
+          if (v < WM * VPR) store_vec(b, v, yreg[b][k]);
+        }
+      } else {
+        for (int v = tid; v < WM * VPR; v += NT) store_vec(b, v, f32x4{});
       }
     }
     if constexpr (BOK) {

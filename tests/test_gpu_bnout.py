@@ -8,7 +8,8 @@ BN-backward chain of src/unet.py:59-63 and torchvision's BatchNorm via src/unet.
     (fp32 partials in another grouping, fp64 finalize: rel 1e-5); f32, bf16io and bf16io with
     bf16 packed weights; 1x1 and 3x3; with a fused addend; ReLU6 / ReLU / no activation mask;
   * the whole MobileNetV2UNet / UNet step with SEG_BNOUT on equals it off within fp32 reduction
-    reordering (f32) and bf16 storage rounding (bf16io).
+    reordering (f32) and bf16 storage rounding (bf16io); the oracle checks of test_gpu_model.py run
+    with it on (the default).
 """
 import ctypes
 
@@ -124,5 +125,10 @@ def test_bnout_step_equals_three_pass(arch, math, tol):
     finally:
         engine.BNOUT = saved
     assert res[True][0] == res[False][0]  # the forward is untouched
-    worst = max(rel(res[True][1][k], res[False][1][k]) for k in res[False][1])
+    # per tensor, relative to max(|g|, 1e-3 * the largest tensor norm): the project BNs' beta gradients are sums
+    # that vanish in exact arithmetic (their dA is a column-centred BN-backward output times a 1x1 weight) and are
+    # rounding noise either way
+    g_max = max(float(g.double().norm()) for g in res[False][1].values())
+    worst = max(float((res[True][1][k].double() - g.double()).norm()) / max(float(g.double().norm()), 1e-3 * g_max)
+                for k, g in res[False][1].items())
     assert worst < tol, worst

@@ -624,6 +624,22 @@ int seg_dw2_wgrad_bn_bf16io(const seg_bf16* dy, long lddy, const seg_bf16* x, lo
                             float* part, const seg_bf16* by, long ldby, const float* bscale, const float* bshift,
                             const float* bmean, const float* bcoef, int bact, hipStream_t stream);
 
+/* Fused inverted residual of the BatchNorm-folded fp16 inference forward (BASELINE configs[3];
+ * torchvision's InvertedResidual reached through src/unet.py:15-19, run per frame by
+ * inference.py:162-163; csrc/mbconv.hip): out = project(relu6(dw3x3_s(relu6(expand(x) + be)) + bd))
+ * + bp (+ res) in one launch, the expanded tile kept in LDS.  Weights are the folded fp32 ones
+ * (seg_bn_fold_batch): we [Ch][Cin] (NULL: no expand, Ch == Cin), wd [9][Ch] (seg_pack_dw_weight
+ * layout), wp [Cout][Ch]; fp16 operands with fp32 accumulation for the 1x1 convs (as
+ * seg_conv_igemm_f16), fp32 depthwise (as seg_dw_fwd_bias_act).  seg_mbconv_ok: stride 1 / 2,
+ * Cin <= 160 with an expand, Cout <= 320, channels % 4; res only at stride 1.  work / cnt:
+ * seg_mbconv_work_floats floats and *counters unsigned (zero before the first launch; re-armed). */
+int seg_mbconv_ok(int Cin, int Ch, int Cout, int stride, int expand);
+long seg_mbconv_work_floats(int N, int H, int W, int Ch, int Cout, int stride, int* counters);
+int seg_mbconv_f16(const float* x, long ldx, int N, int H, int W, int Cin, const float* we, const float* be, int Ch,
+                   const float* wd, const float* bd, int stride, const float* wp, const float* bp, int Cout,
+                   const float* res, long ldres, float* out, long ldo, float* work, unsigned* cnt,
+                   hipStream_t stream);
+
 /* Build identity (host only): copies the SHA-256 (64 hex chars + NUL) of the sources this
  * library was built from -- every csrc file, this header, compiler and flags
  * (seg_amd/build.py source_hash) -- into out when cap > 64; returns the length.  The

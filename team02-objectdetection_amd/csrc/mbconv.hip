@@ -1,0 +1,284 @@
+// Fused inverted residual for the BatchNorm-folded inference forward (fp16 conv operands,
+// BASELINE configs[3]): expand 1x1 + bias + ReLU6 -> depthwise 3x3 (stride 1 / 2) + bias +
+// ReLU6 -> project 1x1 + bias (+ residual) in ONE launch per torchvision InvertedResidual
+// (features[1..17], reached through src/unet.py:15-19,34-38; inference.py:162-163 runs them
+// per frame).  At bs=1 and 128x256 frames every one of these convs is a few microseconds of
+// work behind a launch (round 3: ~89 launches / frame, launch-latency bound); here the
+// expanded activations never leave LDS.
+//
+// A block owns an output tile (4 x 8 pixels at stride 1, 2 x 8 at stride 2) and a range of
+// the hidden channels (split `hsplit` of `splits`):
+//  * the input halo tile ((T-1) S + 3 rows and columns, Cin channels) is staged once in LDS as
+//    fp16 (round to nearest even, as seg_conv_igemm_f16 rounds its operands);
+//  * per 32-channel hidden chunk: the expand conv on v_mfma_f32_16x16x32_f16 over the halo pixels
+//    (fp32 accumulation, + bias, ReLU6, zero outside the image = the depthwise conv's padding) into
+//    LDS as fp32; the depthwise conv in fp32 in dwconv.hip's tap order; its ReLU6 output rounded
+//    to fp16; the project conv's partial product accumulated in registers over the chunks;
+//  * splits > 1: each block stores its fp32 partial tile write-through; the last block of the
+//    tile to arrive (seg_last_arrival) sums the splits in order (deterministic), adds the bias
+//    and the residual and stores the output.
+// Without an expand conv (features[1], expand ratio 1) the input tile itself is the hidden tile.
+#include "common.h"
+
+namespace {
+
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+constexpr int kThreads = 256;
+constexpr int HC = 32;        // hidden channels per chunk (one K step of the project MFMA)
+constexpr int kMaxCin = 160;  // expand input channels staged in LDS
+constexpr int kMaxCout = 320;
+
+struct MbArgs {
+  const float* x; long ldx;           // block input [N*H*W][ldx] fp32
+  const float* we; const float* be;   // folded expand weight [Ch][Cin], bias [Ch] (we == null: no expand, Ch == Cin)
+  const float* wd; const float* bd;   // folded depthwise weight [9][Ch] (seg_pack_dw_weight layout), bias [Ch]
+  const float* wp; const float* bp;   // folded project weight [Cout][Ch], bias [Cout]
+  const float* res; long ldres;       // residual (the block input) or null
+  float* out; long ldo;               // [N*Ho*Wo][ldo]
+  int N, H, W, Cin, Ch, Cout, Ho, Wo;
+  int tiles_w, tiles_h, ntiles, splits, hper;  // hper: hidden channels per split (multiple of HC)
+  float* work; unsigned* cnt;         // splits > 1: partials [ntiles][splits][TP][Cout], counters [ntiles]
+};
+
+__device__ __forceinline__ float relu6(float v) { return fminf(fmaxf(v, 0.f), 6.f); }
+
+template <int S> struct MbGeo {
+  static constexpr int TOH = S == 1 ? 4 : 2, TOW = 8, TP = TOH * TOW;  // output tile
+  static constexpr int IH = (TOH - 1) * S + 3, IW = (TOW - 1) * S + 3, HP = IH * IW;
+  static constexpr int HPP = (HP + 15) / 16 * 16;                        // halo pixels in 16-row MFMA tiles
+};
+
+template <int S, bool EXP>
+__global__ __launch_bounds__(kThreads) void mbconv_f16_kernel(MbArgs a) {
+  using G = MbGeo<S>;
+  constexpr int XR = kMaxCin + 8;  // fp16 row pitch of the staged input (16-byte reads, staggered banks)
+  __shared__ __attribute__((aligned(16))) _Float16 Xs[EXP ? G::HPP * XR : 8];
+  __shared__ __attribute__((aligned(16))) float Es[G::HPP * (HC + 1)];
+  __shared__ __attribute__((aligned(16))) _Float16 Ds[G::TP * (HC + 8)];
+  __shared__ int word;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int t = blockIdx.x, split = blockIdx.y;
+  const int tw_i = t % a.tiles_w, rest = t / a.tiles_w;
+  const int n = rest / a.tiles_h, oh0 = (rest % a.tiles_h) * G::TOH, ow0 = tw_i * G::TOW;
+  const int ih0 = oh0 * S - 1, iw0 = ow0 * S - 1;
+  const float* xim = a.x + (long)n * a.H * a.W * a.ldx;
+  auto halo_in = [&](int hp, int& ih, int& iw) {
+    const int hy = hp / G::IW, hx = hp - hy * G::IW;
+    ih = ih0 + hy;
+    iw = iw0 + hx;
+    return hp < G::HP && (unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W;
+  };
+  const int cinp = (a.Cin + 31) & ~31;
+  if constexpr (EXP) {  // the input halo as fp16, zero outside the image and beyond Cin
+    const int q4 = cinp / 4;
+    for (int i = tid; i < G::HPP * q4; i += kThreads) {
+      const int hp = i / q4, c = (i - hp * q4) * 4;
+      int ih, iw;
+      f32x4 v = {0.f, 0.f, 0.f, 0.f};
+      if (halo_in(hp, ih, iw) && c < a.Cin) v = ld4(xim + ((long)ih * a.W + iw) * a.ldx + c);
+      _Float16* d = Xs + hp * XR + c;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) d[j] = (_Float16)v[j];
+    }
+  }
+  // project accumulators: (m, n) 16x16 tiles p = wave, wave + 4, ... of (TP / 16) x ceil(Cout / 16)
+  constexpr int MT = G::TP / 16;
+  const int NT = (a.Cout + 15) / 16;
+  constexpr int PMAX = (MT * (kMaxCout / 16) + 3) / 4;
+  f32x4 pacc[PMAX];
+#pragma unroll
+  for (int p = 0; p < PMAX; ++p) pacc[p] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int h_beg = split * a.hper, h_end = min(a.Ch, h_beg + a.hper);
+  const int r16 = lane & 15, kq = lane >> 4;  // MFMA lane geometry: row / column, 8-deep K group
+  for (int c0 = h_beg; c0 < h_end; c0 += HC) {
+    __syncthreads();  // Xs staged / the previous chunk's Es, Ds reads are done
+    if constexpr (EXP) {
+      // expand: Es[hp][j] = relu6(sum_k X[hp][k] We[c0 + j][k] + be), (HPP / 16) x 2 tiles over the waves
+      constexpr int ET = G::HPP / 16 * 2;
+      for (int p = wave; p < ET; p += 4) {
+        const int mt = p >> 1, nt = p & 1;
+        const int hc = c0 + nt * 16 + r16;  // this lane's B column (hidden channel)
+        f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+        for (int k0 = 0; k0 < cinp; k0 += 32) {
+          const f16x8 av = *reinterpret_cast<const f16x8*>(Xs + (mt * 16 + r16) * XR + k0 + 8 * kq);
+          f16x8 bv;
+          const int kb = k0 + 8 * kq;
+#pragma unroll
+          for (int j = 0; j < 8; j += 4) {
+            f32x4 w = {0.f, 0.f, 0.f, 0.f};
+            if (hc < h_end && kb + j < a.Cin) w = ld4(a.we + (long)hc * a.Cin + kb + j);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) bv[j + e] = (_Float16)w[e];
+          }
+          acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(av, bv, acc, 0, 0, 0);
+        }
+        const float b = hc < h_end ? a.be[hc] : 0.f;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {  // C: row 4 kq + i, column r16
+          const int hp = mt * 16 + 4 * kq + i;
+          int ih, iw;
+          Es[hp * (HC + 1) + nt * 16 + r16] = halo_in(hp, ih, iw) ? relu6(acc[i] + b) : 0.f;
+        }
+      }
+    } else {  // no expand: the hidden tile is the input tile (channels c0 ..)
+      for (int i = tid; i < G::HPP * HC; i += kThreads) {
+        const int hp = i / HC, j = i - hp * HC, c = c0 + j;
+        int ih, iw;
+        Es[hp * (HC + 1) + j] = (halo_in(hp, ih, iw) && c < h_end) ? xim[((long)ih * a.W + iw) * a.ldx + c] : 0.f;
+      }
+    }
+    __syncthreads();
+    // depthwise 3x3 + bias + ReLU6 in fp32 (tap order of dwconv.hip), rounded to fp16 for the project MFMA
+    {
+      const int j = tid % HC, c = c0 + j;
+      float w9[9];
+#pragma unroll
+      for (int k = 0; k < 9; ++k) w9[k] = c < h_end ? a.wd[k * a.Ch + c] : 0.f;
+      const float b = c < h_end ? a.bd[c] : 0.f;
+      for (int px = tid / HC; px < G::TP; px += kThreads / HC) {
+        const int oy = px / G::TOW, ox = px - oy * G::TOW;
+        float acc = 0.f;
+#pragma unroll
+        for (int ky = 0; ky < 3; ++ky)
+#pragma unroll
+          for (int kx = 0; kx < 3; ++kx)
+            acc = fmaf(Es[((oy * S + ky) * G::IW + ox * S + kx) * (HC + 1) + j], w9[ky * 3 + kx], acc);
+        Ds[px * (HC + 8) + j] = (_Float16)(c < h_end ? relu6(acc + b) : 0.f);
+      }
+    }
+    __syncthreads();
+    // project partial: pacc[(m, n)] += D[m rows][32] . Wp[n cols][c0 .. c0 + 31]^T
+#pragma unroll
+    for (int q = 0; q < PMAX; ++q) {
+      const int p = wave + 4 * q;
+      if (p < MT * NT) {
+        const int mt = p % MT, nt = p / MT;
+        const f16x8 av = *reinterpret_cast<const f16x8*>(Ds + (mt * 16 + r16) * (HC + 8) + 8 * kq);
+        const int co = nt * 16 + r16, kb = c0 + 8 * kq;
+        f16x8 bv;
+#pragma unroll
+        for (int j = 0; j < 8; j += 4) {
+          f32x4 w = {0.f, 0.f, 0.f, 0.f};
+          if (co < a.Cout && kb + j < h_end) w = ld4(a.wp + (long)co * a.Ch + kb + j);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) bv[j + e] = (_Float16)w[e];
+        }
+        pacc[q] = __builtin_amdgcn_mfma_f32_16x16x32_f16(av, bv, pacc[q], 0, 0, 0);
+      }
+    }
+  }
+  // epilogue: C of tile (mt, nt): row 16 mt + 4 kq + i, column 16 nt + r16
+  auto out_px = [&](int px, long& orow) {  // output pixel of tile row px, or false
+    const int oy = oh0 + px / G::TOW, ox = ow0 + px % G::TOW;
+    orow = ((long)n * a.Ho + oy) * a.Wo + ox;
+    return oy < a.Ho && ox < a.Wo;
+  };
+  if (a.splits == 1) {
+#pragma unroll
+    for (int q = 0; q < PMAX; ++q) {
+      const int p = wave + 4 * q;
+      const int mt = p % MT, co = (p / MT) * 16 + r16;
+      if (p < MT * NT && co < a.Cout) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          long orow;
+          if (out_px(mt * 16 + 4 * kq + i, orow)) {
+            float v = pacc[q][i] + a.bp[co];
+            if (a.res) v += a.res[orow * a.ldres + co];
+            a.out[orow * a.ldo + co] = v;
+          }
+        }
+      }
+    }
+    return;
+  }
+  float* wt = a.work + ((long)t * a.splits + split) * G::TP * a.Cout;
+#pragma unroll
+  for (int q = 0; q < PMAX; ++q) {
+    const int p = wave + 4 * q;
+    const int mt = p % MT, co = (p / MT) * 16 + r16;
+    if (p < MT * NT && co < a.Cout) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) seg_st_wt(wt + (mt * 16 + 4 * kq + i) * a.Cout + co, pacc[q][i]);
+    }
+  }
+  if (!seg_last_arrival(a.cnt + t, (unsigned)a.splits, &word)) return;
+  const float* w0 = a.work + (long)t * a.splits * G::TP * a.Cout;
+  for (int e = tid; e < G::TP * a.Cout; e += kThreads) {
+    const int px = e / a.Cout, co = e - px * a.Cout;
+    long orow;
+    if (!out_px(px, orow)) continue;
+    float v = 0.f;
+    for (int s = 0; s < a.splits; ++s) v += seg_ld_wt(w0 + (long)s * G::TP * a.Cout + e);
+    v += a.bp[co];
+    if (a.res) v += a.res[orow * a.ldres + co];
+    a.out[orow * a.ldo + co] = v;
+  }
+}
+
+void mb_plan(int N, int H, int W, int Ch, int stride, int* tiles_w, int* tiles_h, int* splits, int* hper, int* tp) {
+  const int toh = stride == 1 ? 4 : 2, tow = 8;
+  const int Ho = (H - 1) / stride + 1, Wo = (W - 1) / stride + 1;
+  *tiles_w = (Wo + tow - 1) / tow;
+  *tiles_h = (Ho + toh - 1) / toh;
+  *tp = toh * tow;
+  const int ntiles = N * *tiles_w * *tiles_h;
+  const int chunks = (Ch + HC - 1) / HC;
+  // hidden splits: about 128 blocks in all, at least 2 chunks per block where there are chunks to spare
+  int s = std::max(1, std::min(chunks / 2, (128 + ntiles - 1) / ntiles));
+  const int per = (chunks + s - 1) / s;
+  *splits = (chunks + per - 1) / per;
+  *hper = per * HC;
+}
+
+}  // namespace
+
+// 1 when seg_mbconv_f16 takes the block: stride 1 or 2, Cin <= 160 (with an expand conv), Cout <= 320,
+// channel counts multiples of 4.
+SEG_API int seg_mbconv_ok(int Cin, int Ch, int Cout, int stride, int expand) {
+  return (stride == 1 || stride == 2) && Cin > 0 && Ch > 0 && Cout > 0 && Cin % 4 == 0 && Ch % 4 == 0 &&
+                 Cout % 4 == 0 && Cout <= kMaxCout && (expand ? Cin <= kMaxCin : Cin == Ch)
+             ? 1
+             : 0;
+}
+
+// Workspace of seg_mbconv_f16: partial floats (0 when the plan does not split) and tile counters.
+SEG_API long seg_mbconv_work_floats(int N, int H, int W, int Ch, int Cout, int stride, int* counters) {
+  int tw, th, sp, hp, tp;
+  mb_plan(N, H, W, Ch, stride, &tw, &th, &sp, &hp, &tp);
+  if (counters) *counters = N * tw * th;
+  return sp > 1 ? (long)N * tw * th * sp * tp * Cout : 0;
+}
+
+// out = project(relu6(dw3x3_s(relu6(expand(x))))) + bp (+ res): one torchvision InvertedResidual with
+// its BatchNorms folded (seg_bn_fold_batch), fp16 conv operands with fp32 accumulation, fp32 depthwise.
+// we == NULL: no expand conv (expand ratio 1; Ch == Cin).  work / cnt: seg_mbconv_work_floats floats and
+// *counters unsigned (zero before the first launch; every launch re-arms them).
+SEG_API int seg_mbconv_f16(const float* x, long ldx, int N, int H, int W, int Cin, const float* we, const float* be,
+                           int Ch, const float* wd, const float* bd, int stride, const float* wp, const float* bp,
+                           int Cout, const float* res, long ldres, float* out, long ldo, float* work, unsigned* cnt,
+                           hipStream_t stream) {
+  if (!seg_mbconv_ok(Cin, Ch, Cout, stride, we != nullptr) || !x || !wd || !bd || !wp || !bp || !out ||
+      (we && !be) || (ldx & 3) || (ldo & 3) || (res && (ldres & 3)) || ((uintptr_t)x & 15) || ((uintptr_t)wp & 15) ||
+      (we && ((uintptr_t)we & 15)) || (res && stride != 1))
+    return (int)hipErrorInvalidValue;
+  MbArgs a{};
+  a.x = x; a.ldx = ldx; a.we = we; a.be = be; a.wd = wd; a.bd = bd; a.wp = wp; a.bp = bp; a.res = res;
+  a.ldres = ldres; a.out = out; a.ldo = ldo; a.N = N; a.H = H; a.W = W; a.Cin = Cin; a.Ch = Ch; a.Cout = Cout;
+  a.Ho = (H - 1) / stride + 1; a.Wo = (W - 1) / stride + 1;
+  int tp;
+  mb_plan(N, H, W, Ch, stride, &a.tiles_w, &a.tiles_h, &a.splits, &a.hper, &tp);
+  a.ntiles = N * a.tiles_w * a.tiles_h;
+  a.work = work; a.cnt = cnt;
+  if (a.splits > 1 && (!work || !cnt)) return (int)hipErrorInvalidValue;
+  const dim3 grid(a.ntiles, a.splits);
+  const bool e = we != nullptr;
+  if (stride == 1) {
+    if (e) hipLaunchKernelGGL((mbconv_f16_kernel<1, true>), grid, dim3(kThreads), 0, stream, a);
+    else hipLaunchKernelGGL((mbconv_f16_kernel<1, false>), grid, dim3(kThreads), 0, stream, a);
+  } else {
+    if (e) hipLaunchKernelGGL((mbconv_f16_kernel<2, true>), grid, dim3(kThreads), 0, stream, a);
+    else hipLaunchKernelGGL((mbconv_f16_kernel<2, false>), grid, dim3(kThreads), 0, stream, a);
+  }
+  SEG_RET_LAST();
+}

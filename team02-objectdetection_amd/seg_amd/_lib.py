@@ -115,6 +115,10 @@ PROTOTYPES = {
     "seg_bn_bwd_apply": (_I, [_V, _L, _V, _L, _L, _I, _V, _V, _V, _I, _V, _V, _L, _V]),
     "seg_bn_bwd_finalize_tiles": (_I, [_V, _I, _L, _I, _V, _V, _V, _V, _V, _V]),
     "seg_conv_igemm_bnout_ok": (_I, [_L, _I, _I]),
+    "seg_mbconv_ok": (_I, [_I, _I, _I, _I, _I]),
+    "seg_mbconv_work_floats": (_L, [_I, _I, _I, _I, _I, _I, _V]),
+    "seg_mbconv_f16": (_I, [_V, _L, _I, _I, _I, _I, _V, _V, _I, _V, _V, _I, _V, _V, _I, _V, _L, _V, _L, _V, _V,
+                            _V]),
     "seg_conv_igemm_bnout": (_I, [_V, _L, _I, _I, _I, _I, _V, _I, _V, _L, _I, _I, _V, _L, _V, _L, _V, _V, _V, _I,
                                   _V, _V]),
 }

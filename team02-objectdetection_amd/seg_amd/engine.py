@@ -35,7 +35,8 @@ from ._lib import call, query as _query
 _PURE_QUERIES = {"seg_chan_workspace_floats", "seg_conv_wgrad_splits", "seg_conv_wgrad_splits_bf16", "seg_dw_wgrad_blocks",
                  "seg_conv_igemm_splits", "seg_ce_workspace_floats", "seg_conv_wino_row_tiles", "seg_conv_wino_tile_rows",
                  "seg_conv_halo_row_tiles", "seg_conv_wino_wgrad_splits", "seg_dw2_ok",
-                 "seg_dw2_wgrad_blocks", "seg_dw2_dgrad_tiles", "seg_conv_igemm_bnout_ok"}
+                 "seg_dw2_wgrad_blocks", "seg_dw2_dgrad_tiles", "seg_conv_igemm_bnout_ok",
+                 "seg_mbconv_ok"}
 _QCACHE = {}
 
 
@@ -677,6 +678,35 @@ class Program:
         self._n = 0
         self.image = self.new(3, H, W, name=IMAGE)  # NHWC4 copy of the input batch
 
+    def mbconv_groups(self):
+        """Folded forward: op index -> the (expand, depthwise, project) or (depthwise, project) ConvOps of a
+        torchvision InvertedResidual that seg_mbconv_f16 runs as one launch (each intermediate activation
+        consumed only inside the block: the lazy BN chain Program.make_lazy built)."""
+        m = getattr(self, "_mb_groups", None)
+        if m is not None:
+            return m
+        m, ops = {}, self.ops
+        ok1 = (lambda op: isinstance(op, ConvOp) and op.kind == "igemm" and op.ks == 1 and op.stride == 1
+               and op.bn is not None and op.conv.bias is None and op.cin_pad == op.cin)
+        for k in range(len(ops) - 1):
+            d, p = ops[k], ops[k + 1]
+            if not (isinstance(d, ConvOp) and d.kind == "dw" and d.bn is not None and d.act == ACT_RELU6 and d.lazy
+                    and ok1(p) and p.xform is d and p.act == ACT_NONE and p.inp is d.out):
+                continue
+            e = ops[k - 1] if k > 0 else None
+            exp = (ok1(e) and e.act == ACT_RELU6 and e.lazy and e.res is None and d.xform is e and d.inp is e.out)
+            cin = e.cin if exp else d.cout
+            if p.res is not None and d.stride != 1:
+                continue
+            if not query("seg_mbconv_ok", cin, d.cout, p.cout, d.stride, int(exp)):
+                continue
+            if exp:
+                m[k - 1] = (e, d, p)
+            elif d.xform is None or d.xform.kind != "dw":
+                m[k] = (d, p)
+        self._mb_groups = m
+        return m
+
     def bn_owner(self):
         """Activation key -> the ConvOp with a BatchNorm whose output it is (the BN-backward reduction target of a
         data gradient writing exactly that region; ConvOp._bnout)."""
@@ -1128,6 +1158,7 @@ class Run:
         self.bn_parts = {}    # id(op) -> [tile partials, tiles, write generation]: its BN-backward reduction from
                               # the epilogue of the data gradient that completed its dA (seg_conv_igemm_bnout*)
         self.wgen = {}        # gradient buffer name -> write generation (every write to the buffer bumps it)
+        self._mb = {}         # folded forward: op index -> (partials, tile counters) of a fused inverted residual
         self.gbufs = {}
         self.keep = []        # workspaces of a recorded run (persistent: the tape points at them)
         self.written = {}     # grad buffer name -> list of (lo, hi) channel ranges
@@ -1349,12 +1380,39 @@ class Run:
 
     def forward_folded(self):
         """Eval forward with every BatchNorm folded (Program.fold must have run): one
-        launch per conv.  The NHWC4 input rows must already be in the image buffer."""
-        for op in self.prog.ops:
+        launch per conv, or per inverted residual with fp16 conv math (seg_mbconv_f16).  The
+        NHWC4 input rows must already be in the image buffer."""
+        ops = self.prog.ops
+        groups = self.prog.mbconv_groups() if MBCONV and self.prog.math == "f16" else {}
+        k = 0
+        while k < len(ops):
+            g = groups.get(k)
+            if g is not None:
+                self._mbconv(k, g)
+                k += len(g)
+                continue
+            op = ops[k]
             if isinstance(op, ConvOp):
                 op.forward_folded(self)
             else:
                 op.forward(self)
+            k += 1
+
+    def _mbconv(self, k, g):
+        """One fused inverted residual (expand?, depthwise, project) of the folded forward."""
+        e, d, p = (g[0], g[1], g[2]) if len(g) == 3 else (None, g[0], g[1])
+        x = e.inp if e is not None else d.inp
+        o, r = p.out, p.res
+        bufs = self._mb.get(k)
+        if bufs is None:  # persistent across graph replays: allocated by the warm-up launch, before any capture
+            ncnt = ctypes.c_int(0)
+            nw = query("seg_mbconv_work_floats", x.N, x.H, x.W, d.cout, p.cout, d.stride, ctypes.addressof(ncnt))
+            bufs = self._mb[k] = (torch.empty(max(nw, 1), device=self.device, dtype=torch.float32),
+                                  torch.zeros(max(ncnt.value, 1), device=self.device, dtype=torch.int32))
+        call("seg_mbconv_f16", self.ptr(x), x.ld, x.N, x.H, x.W, x.C, e.fk.data_ptr() if e is not None else None,
+             e.fb.data_ptr() if e is not None else None, d.cout, d.fk_pack.data_ptr(), d.fb.data_ptr(), d.stride,
+             p.fk.data_ptr(), p.fb.data_ptr(), p.cout, self.ptr(r) if r is not None else None,
+             r.ld if r is not None else 0, self.ptr(o), o.ld, bufs[0].data_ptr(), bufs[1].data_ptr(), self.stream)
 
     def backward_from_logits(self):
         global LAST_RUN
@@ -1392,6 +1450,9 @@ HALO_BF16 = os.environ.get("SEG_HALO_BF16", "1") == "1"
 HALO2 = os.environ.get("SEG_HALO2", "0") == "1"  # default off: step A/B -0.7 % (profiles/r04k_ab.txt)
 # ... and their weight gradients on the persistent LDS-halo kernel (seg_conv_wgrad2_bf16io); SEG_WGRAD2=0 = off
 WGRAD2 = os.environ.get("SEG_WGRAD2", "1") == "1"
+# fp16 inference (Predictor, BASELINE configs[3]): each inverted residual of the folded forward as one fused
+# launch (seg_mbconv_f16); SEG_MBCONV=0 = one launch per conv
+MBCONV = os.environ.get("SEG_MBCONV", "1") == "1"
 # BatchNorm-backward reduction from the epilogue of the implicit-GEMM data gradient that completes a BN layer's dA
 # (seg_conv_igemm_bnout*: no reduction pass over dA; the finalize reads the tile partials); SEG_BNOUT=0 = off.  Up to
 # BNOUT_MAX_TILES row tiles (the finalize's serial tile loop), i.e. the small-image layers where the three-launch

@@ -1,0 +1,130 @@
+"""GPU: seg_mbconv_f16 -- one torchvision InvertedResidual of the BatchNorm-folded fp16 inference
+forward in one launch (csrc/mbconv.hip; BASELINE configs[3], inference.py:162-163 through
+src/unet.py:15-19).
+
+  * against float64 of the same arithmetic (fp16-rounded 1x1 operands, fp32/fp64 depthwise):
+    expand ratio 6 and 1, stride 1 (with the residual) and 2, split hidden ranges (the
+    last-arrival combine) and one split, ragged tiles, every MobileNetV2 block shape at a
+    128x256 frame;
+  * repeat launches bitwise equal (fixed-order combine; counters re-armed);
+  * the fp16 Predictor with the fused blocks equals the one-launch-per-conv folded forward
+    (SEG_MBCONV off) within fp32 accumulation reordering, and its graph replay equals eager.
+"""
+import ctypes
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+from seg_amd import MobileNetV2UNet, deterministic_init, engine
+from seg_amd._lib import call, query
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def S():
+    return torch.cuda.current_stream().cuda_stream
+
+
+def h16(t):
+    return t.to(torch.float16).double()
+
+
+def reference(x, we, be, wd, bd, wp, bp, stride, res):
+    """float64 NCHW of the block with the kernel's rounding points."""
+    xx = x.double()
+    if we is not None:
+        h = F.conv2d(h16(xx), h16(we)[:, :, None, None]) + be.double()[None, :, None, None]
+        h = h.clamp(0, 6).float().double()  # fp32 staging
+    else:
+        h = xx
+    C = h.shape[1]
+    d = F.conv2d(h, wd.double().view(C, 1, 3, 3), stride=stride, padding=1, groups=C) + bd.double()[None, :, None, None]
+    d = d.clamp(0, 6)
+    o = F.conv2d(h16(d), h16(wp)[:, :, None, None]) + bp.double()[None, :, None, None]
+    if res is not None:
+        o = o + res.double()
+    return o
+
+
+CASES = [  # N, H, W, Cin, t, Cout, stride, residual  (MobileNetV2 blocks at a 128x256 frame, plus ragged ones)
+    (1, 64, 128, 32, 1, 16, 1, False), (1, 64, 128, 16, 6, 24, 2, False), (1, 32, 64, 24, 6, 24, 1, True),
+    (1, 32, 64, 24, 6, 32, 2, False), (1, 16, 32, 32, 6, 32, 1, True), (1, 16, 32, 32, 6, 64, 2, False),
+    (1, 8, 16, 64, 6, 64, 1, True), (1, 8, 16, 64, 6, 96, 1, False), (1, 8, 16, 96, 6, 96, 1, True),
+    (1, 8, 16, 96, 6, 160, 2, False), (1, 4, 8, 160, 6, 160, 1, True), (1, 4, 8, 160, 6, 320, 1, False),
+    (2, 13, 21, 24, 6, 24, 1, True), (1, 11, 19, 16, 6, 32, 2, False), (1, 9, 10, 40, 1, 24, 2, False),
+]
+
+
+@pytest.mark.parametrize("N,H,W,Cin,t,Cout,stride,res", CASES)
+def test_mbconv_vs_fp64(N, H, W, Cin, t, Cout, stride, res):
+    Ch = Cin * t
+    assert query("seg_mbconv_ok", Cin, Ch, Cout, stride, int(t != 1)) == 1
+    g = torch.Generator().manual_seed(N * H * W + Cin + Cout)
+    x = torch.randn(N, Cin, H, W, generator=g)
+    we = torch.randn(Ch, Cin, generator=g) / Cin ** 0.5 if t != 1 else None
+    be = torch.randn(Ch, generator=g) * 0.1 + 0.5 if t != 1 else None
+    wd = torch.randn(Ch, 9, generator=g) / 3
+    bd = torch.randn(Ch, generator=g) * 0.1 + 0.2
+    wp = torch.randn(Cout, Ch, generator=g) / Ch ** 0.5
+    bp = torch.randn(Cout, generator=g) * 0.1
+    Ho, Wo = (H - 1) // stride + 1, (W - 1) // stride + 1
+    r = torch.randn(N, Cout, Ho, Wo, generator=g) if res else None
+    ref = reference(x, we, be, wd, bd, wp, bp, stride, r)
+    rows = lambda t4: t4.permute(0, 2, 3, 1).reshape(-1, t4.shape[1]).contiguous().to(DEV)  # noqa: E731
+    xg, rg = rows(x), rows(r) if res else None
+    wdk = torch.empty(9 * Ch, device=DEV)
+    call("seg_pack_dw_weight", wd.contiguous().to(DEV).data_ptr(), wdk.data_ptr(), Ch, S())
+    weg, beg = (we.to(DEV), be.to(DEV)) if t != 1 else (None, None)
+    wpg, bpg, bdg = wp.to(DEV), bp.to(DEV), bd.to(DEV)
+    ncnt = ctypes.c_int(0)
+    nw = query("seg_mbconv_work_floats", N, H, W, Ch, Cout, stride, ctypes.addressof(ncnt))
+    work = torch.full((max(nw, 1),), float("nan"), device=DEV)
+    cnt = torch.zeros(max(ncnt.value, 1), device=DEV, dtype=torch.int32)
+    outs = []
+    for _ in range(2):
+        o = torch.full((N * Ho * Wo, Cout), float("nan"), device=DEV)
+        call("seg_mbconv_f16", xg.data_ptr(), Cin, N, H, W, Cin, weg.data_ptr() if weg is not None else None,
+             beg.data_ptr() if beg is not None else None, Ch, wdk.data_ptr(), bdg.data_ptr(), stride, wpg.data_ptr(),
+             bpg.data_ptr(), Cout, rg.data_ptr() if res else None, Cout if res else 0, o.data_ptr(), Cout,
+             work.data_ptr(), cnt.data_ptr(), S())
+        outs.append(o)
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0], outs[1]), "deterministic"
+    assert int(cnt.abs().sum()) == 0, "counters re-armed"
+    got = outs[0].double().cpu().view(N, Ho, Wo, Cout).permute(0, 3, 1, 2)
+    rel = float((got - ref).norm() / ref.norm())
+    assert rel < 1e-3, rel
+
+
+def test_mbconv_refuses():
+    assert query("seg_mbconv_ok", 320, 1920, 1280, 1, 1) == 0   # Cin > 160 with an expand
+    assert query("seg_mbconv_ok", 32, 192, 640, 1, 1) == 0     # Cout > 320
+    assert query("seg_mbconv_ok", 32, 192, 64, 3, 1) == 0      # stride 3
+    assert query("seg_mbconv_ok", 32, 64, 16, 1, 0) == 0       # no expand: Ch == Cin
+
+
+def test_predictor_fused_equals_unfused():
+    from seg_amd.infer import Predictor
+    import numpy as np
+    model = deterministic_init(MobileNetV2UNet(10), seed=13, random_running_stats=True).to(DEV).eval()
+    f = (np.random.default_rng(0).random((720, 1280, 3)) * 255).astype(np.uint8)
+    saved = engine.MBCONV
+    try:
+        engine.MBCONV = False
+        p0 = Predictor(model, frame_hw=(720, 1280), graph=False, math="f16")
+        p0(f)
+        l0 = p0.logits()
+        engine.MBCONV = True
+        p1 = Predictor(model, frame_hw=(720, 1280), graph=True, math="f16")
+        assert len(p1.prog.mbconv_groups()) == 17  # every InvertedResidual of features[1..17]
+        m1 = p1(f).clone()
+        l1 = p1.logits()
+        p2 = Predictor(model, frame_hw=(720, 1280), graph=False, math="f16")
+        m2 = p2(f).clone()
+        assert torch.equal(m1, m2) and torch.equal(l1, p2.logits()), "graph replay == eager"
+    finally:
+        engine.MBCONV = saved
+    rel = float((l1 - l0).norm() / l0.norm())
+    assert rel < 1e-3, rel

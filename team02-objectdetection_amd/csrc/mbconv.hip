@@ -40,6 +40,8 @@ struct MbArgs {
   float* work; unsigned* cnt;         // splits > 1: partials [ntiles][splits][TP][Cout], counters [ntiles]
 };
 
+__device__ __attribute__((aligned(16))) float g_mb_zero[4];
+
 __device__ __forceinline__ float relu6(float v) { return fminf(fmaxf(v, 0.f), 6.f); }
 
 template <int S> struct MbGeo {
@@ -53,6 +55,8 @@ __global__ __launch_bounds__(kThreads) void mbconv_f16_kernel(MbArgs a) {
   using G = MbGeo<S>;
   constexpr int XR = kMaxCin + 8;  // fp16 row pitch of the staged input (16-byte reads, staggered banks)
   __shared__ __attribute__((aligned(16))) _Float16 Xs[EXP ? G::HPP * XR : 8];
+  __shared__ __attribute__((aligned(16))) _Float16 Ws[EXP ? HC * XR : 8];        // the chunk's expand rows
+  __shared__ __attribute__((aligned(16))) _Float16 Wps[kMaxCout * (HC + 8)];      // the chunk's project columns
   __shared__ __attribute__((aligned(16))) float Es[G::HPP * (HC + 1)];
   __shared__ __attribute__((aligned(16))) _Float16 Ds[G::TP * (HC + 8)];
   __shared__ int word;
@@ -69,16 +73,25 @@ __global__ __launch_bounds__(kThreads) void mbconv_f16_kernel(MbArgs a) {
     return hp < G::HP && (unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W;
   };
   const int cinp = (a.Cin + 31) & ~31;
-  if constexpr (EXP) {  // the input halo as fp16, zero outside the image and beyond Cin
+  if constexpr (EXP) {  // the input halo as fp16, zero outside the image and beyond Cin (all loads issued together)
     const int q4 = cinp / 4;
-    for (int i = tid; i < G::HPP * q4; i += kThreads) {
-      const int hp = i / q4, c = (i - hp * q4) * 4;
-      int ih, iw;
-      f32x4 v = {0.f, 0.f, 0.f, 0.f};
-      if (halo_in(hp, ih, iw) && c < a.Cin) v = ld4(xim + ((long)ih * a.W + iw) * a.ldx + c);
-      _Float16* d = Xs + hp * XR + c;
+    constexpr int XI = (G::HPP * (kMaxCin + 31) / 32 * 8 + kThreads - 1) / kThreads;
+    f32x4 v[XI];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) d[j] = (_Float16)v[j];
+    for (int k = 0; k < XI; ++k) {
+      const int i = tid + k * kThreads, hp = i / q4, c = (i - hp * q4) * 4;
+      int ih, iw;
+      const bool ok = i < G::HPP * q4 && halo_in(hp, ih, iw) && c < a.Cin;
+      v[k] = ld4(ok ? xim + ((long)ih * a.W + iw) * a.ldx + c : reinterpret_cast<const float*>(g_mb_zero));
+    }
+#pragma unroll
+    for (int k = 0; k < XI; ++k) {
+      const int i = tid + k * kThreads, hp = i / q4, c = (i - hp * q4) * 4;
+      if (i < G::HPP * q4) {
+        _Float16* d = Xs + hp * XR + c;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) d[j] = (_Float16)v[k][j];
+      }
     }
   }
   // project accumulators: (m, n) 16x16 tiles p = wave, wave + 4, ... of (TP / 16) x ceil(Cout / 16)
@@ -91,7 +104,54 @@ __global__ __launch_bounds__(kThreads) void mbconv_f16_kernel(MbArgs a) {
   const int h_beg = split * a.hper, h_end = min(a.Ch, h_beg + a.hper);
   const int r16 = lane & 15, kq = lane >> 4;  // MFMA lane geometry: row / column, 8-deep K group
   for (int c0 = h_beg; c0 < h_end; c0 += HC) {
-    __syncthreads();  // Xs staged / the previous chunk's Es, Ds reads are done
+    // this thread's depthwise channel of the chunk: taps and bias, loaded with the chunk's other weights
+    const int dj = tid % HC, dc = c0 + dj;
+    float w9[9];
+#pragma unroll
+    for (int k = 0; k < 9; ++k) w9[k] = a.wd[k * a.Ch + min(dc, a.Ch - 1)];
+    const float dbias = a.bd[min(dc, a.Ch - 1)];
+    // the chunk's weights as fp16 in LDS: expand rows c0 .. c0 + 31 ([32][cinp]) and project columns
+    // ([Cout][32]) -- every load of the chunk in flight at once, then one barrier
+    {
+      constexpr int WI = (HC * kMaxCin / 4 + kThreads - 1) / kThreads;  // expand float4s per thread
+      constexpr int PI = (kMaxCout * HC / 4 + kThreads - 1) / kThreads; // project float4s per thread
+      const int q4 = cinp / 4;
+      f32x4 we4[EXP ? WI : 1], wp4[PI];
+      if constexpr (EXP) {
+#pragma unroll
+        for (int k = 0; k < WI; ++k) {
+          const int i = tid + k * kThreads, r = i / q4, c = (i - r * q4) * 4;
+          const bool ok = i < HC * q4 && c0 + r < h_end && c < a.Cin;
+          we4[k] = ld4(ok ? a.we + (long)(c0 + r) * a.Cin + c : reinterpret_cast<const float*>(g_mb_zero));
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < PI; ++k) {
+        const int i = tid + k * kThreads, co = i >> 3, c = (i & 7) * 4;
+        const bool ok = co < a.Cout && c0 + c < h_end;
+        wp4[k] = ld4(ok ? a.wp + (long)co * a.Ch + c0 + c : reinterpret_cast<const float*>(g_mb_zero));
+      }
+      __syncthreads();  // Xs staged / the previous chunk's reads of Ws, Wps, Es, Ds are done
+      if constexpr (EXP) {
+#pragma unroll
+        for (int k = 0; k < WI; ++k) {
+          const int i = tid + k * kThreads, r = i / q4, c = (i - r * q4) * 4;
+          if (i < HC * q4) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) Ws[r * XR + c + j] = (_Float16)we4[k][j];
+          }
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < PI; ++k) {
+        const int i = tid + k * kThreads, co = i >> 3, c = (i & 7) * 4;
+        if (co < a.Cout) {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) Wps[co * (HC + 8) + c + j] = (_Float16)wp4[k][j];
+        }
+      }
+      __syncthreads();
+    }
     if constexpr (EXP) {
       // expand: Es[hp][j] = relu6(sum_k X[hp][k] We[c0 + j][k] + be), (HPP / 16) x 2 tiles over the waves
       constexpr int ET = G::HPP / 16 * 2;
@@ -101,15 +161,7 @@ __global__ __launch_bounds__(kThreads) void mbconv_f16_kernel(MbArgs a) {
         f32x4 acc = {0.f, 0.f, 0.f, 0.f};
         for (int k0 = 0; k0 < cinp; k0 += 32) {
           const f16x8 av = *reinterpret_cast<const f16x8*>(Xs + (mt * 16 + r16) * XR + k0 + 8 * kq);
-          f16x8 bv;
-          const int kb = k0 + 8 * kq;
-#pragma unroll
-          for (int j = 0; j < 8; j += 4) {
-            f32x4 w = {0.f, 0.f, 0.f, 0.f};
-            if (hc < h_end && kb + j < a.Cin) w = ld4(a.we + (long)hc * a.Cin + kb + j);
-#pragma unroll
-            for (int e = 0; e < 4; ++e) bv[j + e] = (_Float16)w[e];
-          }
+          const f16x8 bv = *reinterpret_cast<const f16x8*>(Ws + (nt * 16 + r16) * XR + k0 + 8 * kq);
           acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(av, bv, acc, 0, 0, 0);
         }
         const float b = hc < h_end ? a.be[hc] : 0.f;
@@ -120,21 +172,27 @@ __global__ __launch_bounds__(kThreads) void mbconv_f16_kernel(MbArgs a) {
           Es[hp * (HC + 1) + nt * 16 + r16] = halo_in(hp, ih, iw) ? relu6(acc[i] + b) : 0.f;
         }
       }
-    } else {  // no expand: the hidden tile is the input tile (channels c0 ..)
-      for (int i = tid; i < G::HPP * HC; i += kThreads) {
-        const int hp = i / HC, j = i - hp * HC, c = c0 + j;
+    } else {  // no expand: the hidden tile is the input tile (channels c0 ..), loads issued together
+      constexpr int EI = (G::HPP * HC + kThreads - 1) / kThreads;
+      float ev[EI];
+#pragma unroll
+      for (int k = 0; k < EI; ++k) {
+        const int i = tid + k * kThreads, hp = i / HC, j = i - hp * HC, c = c0 + j;
         int ih, iw;
-        Es[hp * (HC + 1) + j] = (halo_in(hp, ih, iw) && c < h_end) ? xim[((long)ih * a.W + iw) * a.ldx + c] : 0.f;
+        const bool ok = i < G::HPP * HC && halo_in(hp, ih, iw) && c < h_end;
+        ev[k] = ok ? xim[((long)ih * a.W + iw) * a.ldx + c] : 0.f;
+      }
+#pragma unroll
+      for (int k = 0; k < EI; ++k) {
+        const int i = tid + k * kThreads, hp = i / HC, j = i - hp * HC;
+        if (i < G::HPP * HC) Es[hp * (HC + 1) + j] = ev[k];
       }
     }
     __syncthreads();
     // depthwise 3x3 + bias + ReLU6 in fp32 (tap order of dwconv.hip), rounded to fp16 for the project MFMA
     {
-      const int j = tid % HC, c = c0 + j;
-      float w9[9];
-#pragma unroll
-      for (int k = 0; k < 9; ++k) w9[k] = c < h_end ? a.wd[k * a.Ch + c] : 0.f;
-      const float b = c < h_end ? a.bd[c] : 0.f;
+      const int j = dj, c = dc;
+      const float b = dbias;
       for (int px = tid / HC; px < G::TP; px += kThreads / HC) {
         const int oy = px / G::TOW, ox = px - oy * G::TOW;
         float acc = 0.f;
@@ -154,15 +212,8 @@ __global__ __launch_bounds__(kThreads) void mbconv_f16_kernel(MbArgs a) {
       if (p < MT * NT) {
         const int mt = p % MT, nt = p / MT;
         const f16x8 av = *reinterpret_cast<const f16x8*>(Ds + (mt * 16 + r16) * (HC + 8) + 8 * kq);
-        const int co = nt * 16 + r16, kb = c0 + 8 * kq;
-        f16x8 bv;
-#pragma unroll
-        for (int j = 0; j < 8; j += 4) {
-          f32x4 w = {0.f, 0.f, 0.f, 0.f};
-          if (co < a.Cout && kb + j < h_end) w = ld4(a.wp + (long)co * a.Ch + kb + j);
-#pragma unroll
-          for (int e = 0; e < 4; ++e) bv[j + e] = (_Float16)w[e];
-        }
+        const int co = min(nt * 16 + r16, kMaxCout - 1);  // columns >= Cout: unused accumulator lanes
+        const f16x8 bv = *reinterpret_cast<const f16x8*>(Wps + co * (HC + 8) + 8 * kq);
         pacc[q] = __builtin_amdgcn_mfma_f32_16x16x32_f16(av, bv, pacc[q], 0, 0, 0);
       }
     }
@@ -203,16 +254,35 @@ __global__ __launch_bounds__(kThreads) void mbconv_f16_kernel(MbArgs a) {
     }
   }
   if (!seg_last_arrival(a.cnt + t, (unsigned)a.splits, &word)) return;
+  // the combine: each thread's elements e = tid + k * 256 summed over the splits in order, every split's loads
+  // of a thread issued together
   const float* w0 = a.work + (long)t * a.splits * G::TP * a.Cout;
-  for (int e = tid; e < G::TP * a.Cout; e += kThreads) {
+  constexpr int RI = (G::TP * kMaxCout + kThreads - 1) / kThreads;
+  const int ne = G::TP * a.Cout;
+  float racc[RI];
+#pragma unroll
+  for (int k = 0; k < RI; ++k) racc[k] = 0.f;
+  for (int sp = 0; sp < a.splits; ++sp) {
+    float rv[RI];
+#pragma unroll
+    for (int k = 0; k < RI; ++k) {
+      const int e = tid + k * kThreads;
+      rv[k] = e < ne ? seg_ld_wt(w0 + (long)sp * ne + e) : 0.f;
+    }
+#pragma unroll
+    for (int k = 0; k < RI; ++k) racc[k] += rv[k];
+  }
+#pragma unroll
+  for (int k = 0; k < RI; ++k) {
+    const int e = tid + k * kThreads;
+    if (e >= ne) break;
     const int px = e / a.Cout, co = e - px * a.Cout;
     long orow;
-    if (!out_px(px, orow)) continue;
-    float v = 0.f;
-    for (int s = 0; s < a.splits; ++s) v += seg_ld_wt(w0 + (long)s * G::TP * a.Cout + e);
-    v += a.bp[co];
-    if (a.res) v += a.res[orow * a.ldres + co];
-    a.out[orow * a.ldo + co] = v;
+    if (out_px(px, orow)) {
+      float v = racc[k] + a.bp[co];
+      if (a.res) v += a.res[orow * a.ldres + co];
+      a.out[orow * a.ldo + co] = v;
+    }
   }
 }
 

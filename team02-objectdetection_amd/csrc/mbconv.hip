@@ -14,9 +14,11 @@
 //    (fp32 accumulation, + bias, ReLU6, zero outside the image = the depthwise conv's padding) into
 //    LDS as fp32; the depthwise conv in fp32 in dwconv.hip's tap order; its ReLU6 output rounded
 //    to fp16; the project conv's partial product accumulated in registers over the chunks;
-//  * splits > 1: each block stores its fp32 partial tile write-through; the last block of the
-//    tile to arrive (seg_last_arrival) sums the splits in order (deterministic), adds the bias
-//    and the residual and stores the output.
+//  * splits > 1: each block stores its fp32 partial tile write-through; when the whole grid fits on
+//    the chip at once every block of a tile waits for the tile's other splits and then combines its
+//    1/splits share of the tile (the splits summed in order: deterministic) -- one block combining
+//    a whole 32 x 320 tile of 15 splits took ~30 us; otherwise the last block to arrive
+//    (seg_last_arrival) combines the tile; + bias, + residual, stored.
 // Without an expand conv (features[1], expand ratio 1) the input tile itself is the hidden tile.
 #include "common.h"
 
@@ -37,7 +39,8 @@ struct MbArgs {
   float* out; long ldo;               // [N*Ho*Wo][ldo]
   int N, H, W, Cin, Ch, Cout, Ho, Wo;
   int tiles_w, tiles_h, ntiles, splits, hper;  // hper: hidden channels per split (multiple of HC)
-  float* work; unsigned* cnt;         // splits > 1: partials [ntiles][splits][TP][Cout], counters [ntiles]
+  float* work; unsigned* cnt;         // splits > 1: partials [ntiles][splits][TP][Cout], counters [2][ntiles]
+  int spin;                           // the whole grid is resident: every block of a tile helps combine it
 };
 
 __device__ __attribute__((aligned(16))) float g_mb_zero[4];
@@ -253,36 +256,52 @@ __global__ __launch_bounds__(kThreads) void mbconv_f16_kernel(MbArgs a) {
       for (int i = 0; i < 4; ++i) seg_st_wt(wt + (mt * 16 + 4 * kq + i) * a.Cout + co, pacc[q][i]);
     }
   }
-  if (!seg_last_arrival(a.cnt + t, (unsigned)a.splits, &word)) return;
-  // the combine: each thread's elements e = tid + k * 256 summed over the splits in order, every split's loads
-  // of a thread issued together
   const float* w0 = a.work + (long)t * a.splits * G::TP * a.Cout;
-  constexpr int RI = (G::TP * kMaxCout + kThreads - 1) / kThreads;
   const int ne = G::TP * a.Cout;
-  float racc[RI];
-#pragma unroll
-  for (int k = 0; k < RI; ++k) racc[k] = 0.f;
-  for (int sp = 0; sp < a.splits; ++sp) {
-    float rv[RI];
-#pragma unroll
-    for (int k = 0; k < RI; ++k) {
-      const int e = tid + k * kThreads;
-      rv[k] = e < ne ? seg_ld_wt(w0 + (long)sp * ne + e) : 0.f;
-    }
-#pragma unroll
-    for (int k = 0; k < RI; ++k) racc[k] += rv[k];
-  }
-#pragma unroll
-  for (int k = 0; k < RI; ++k) {
-    const int e = tid + k * kThreads;
-    if (e >= ne) break;
+  auto emit = [&](int e, float v) {
     const int px = e / a.Cout, co = e - px * a.Cout;
     long orow;
     if (out_px(px, orow)) {
-      float v = racc[k] + a.bp[co];
+      v += a.bp[co];
       if (a.res) v += a.res[orow * a.ldres + co];
       a.out[orow * a.ldo + co] = v;
     }
+  };
+  if (a.spin) {
+    // the whole grid is resident (host check): every block of the tile waits for all of its splits, then combines
+    // its 1/splits share of the tile's elements (the splits summed in order: deterministic); the last block to
+    // leave re-arms both counters
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's partial has landed
+    __syncthreads();
+    unsigned* arrive = a.cnt + t;
+    unsigned* leave = a.cnt + a.ntiles + t;
+    if (tid == 0) {
+      __hip_atomic_fetch_add(arrive, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      while (__hip_atomic_load(arrive, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (unsigned)a.splits)
+        __builtin_amdgcn_s_sleep(1);
+    }
+    __syncthreads();
+    const int e0 = (int)((long)split * ne / a.splits), e1 = (int)((long)(split + 1) * ne / a.splits);
+    for (int e = e0 + tid; e < e1; e += kThreads) {
+      float v = 0.f;
+#pragma unroll 4
+      for (int sp = 0; sp < a.splits; ++sp) v += seg_ld_wt(w0 + (long)sp * ne + e);
+      emit(e, v);
+    }
+    if (tid == 0 &&
+        __hip_atomic_fetch_add(leave, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (unsigned)a.splits - 1) {
+      __hip_atomic_store(arrive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(leave, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    return;
+  }
+  if (!seg_last_arrival(a.cnt + t, (unsigned)a.splits, &word)) return;
+  // (grid larger than the chip) the last block of the tile combines all of it
+  for (int e = tid; e < ne; e += kThreads) {
+    float v = 0.f;
+#pragma unroll 4
+    for (int sp = 0; sp < a.splits; ++sp) v += seg_ld_wt(w0 + (long)sp * ne + e);
+    emit(e, v);
   }
 }
 
@@ -316,7 +335,7 @@ SEG_API int seg_mbconv_ok(int Cin, int Ch, int Cout, int stride, int expand) {
 SEG_API long seg_mbconv_work_floats(int N, int H, int W, int Ch, int Cout, int stride, int* counters) {
   int tw, th, sp, hp, tp;
   mb_plan(N, H, W, Ch, stride, &tw, &th, &sp, &hp, &tp);
-  if (counters) *counters = N * tw * th;
+  if (counters) *counters = 2 * N * tw * th;
   return sp > 1 ? (long)N * tw * th * sp * tp * Cout : 0;
 }
 
@@ -341,6 +360,7 @@ SEG_API int seg_mbconv_f16(const float* x, long ldx, int N, int H, int W, int Ci
   a.ntiles = N * a.tiles_w * a.tiles_h;
   a.work = work; a.cnt = cnt;
   if (a.splits > 1 && (!work || !cnt)) return (int)hipErrorInvalidValue;
+  a.spin = (long)a.ntiles * a.splits <= seg_num_cus();  // one block per CU at most: all co-resident
   const dim3 grid(a.ntiles, a.splits);
   const bool e = we != nullptr;
   if (stride == 1) {

@@ -7,9 +7,9 @@ BN-backward chain of src/unet.py:59-63 and torchvision's BatchNorm via src/unet.
   * dgamma / dbeta / coef from the tile partials match seg_bn_bwd_coef over the stored output
     (fp32 partials in another grouping, fp64 finalize: rel 1e-5); f32, bf16io and bf16io with
     bf16 packed weights; 1x1 and 3x3; with a fused addend; ReLU6 / ReLU / no activation mask;
-  * the whole MobileNetV2UNet / UNet step with SEG_BNOUT on equals it off within fp32 reduction
-    reordering (f32) and bf16 storage rounding (bf16io); the oracle checks of test_gpu_model.py run
-    with it on (the default).
+  * the whole MobileNetV2UNet / UNet f32 step with SEG_BNOUT on equals it off within fp32 reduction
+    reordering; the oracle checks of test_gpu_model.py / test_gpu_bf16io.py run with it on (the
+    default).
 """
 import pytest
 import torch
@@ -101,8 +101,10 @@ def test_bnout_partials(math, N, H, W, Cin, Cout, ks, act, addend):
     assert torch.equal(part, part2)
 
 
-@pytest.mark.parametrize("arch,math,tol", [("MobileNetV2UNet", "f32", 1e-3), ("MobileNetV2UNet", "bf16io", 2e-2),
-                                           ("UNet", "f32", 1e-3)])
+# (bf16io: one-ulp bf16 rounding flips of dY cascade through 50 layers, so a step-to-step comparison has no useful
+# bound; its kernels are pinned above and the whole bf16io step against the oracle by tests/test_gpu_bf16io.py with
+# the epilogue reduction on -- the default)
+@pytest.mark.parametrize("arch,math,tol", [("MobileNetV2UNet", "f32", 1e-3), ("UNet", "f32", 1e-3)])
 def test_bnout_step_equals_three_pass(arch, math, tol):
     from seg_amd import MobileNetV2UNet, UNet
     from seg_amd.detinit import deterministic_init, synthetic_batch

@@ -106,55 +106,62 @@ __global__ __launch_bounds__(kThreads) void mbconv_f16_kernel(MbArgs a) {
   for (int p = 0; p < PMAX; ++p) pacc[p] = f32x4{0.f, 0.f, 0.f, 0.f};
   const int h_beg = split * a.hper, h_end = min(a.Ch, h_beg + a.hper);
   const int r16 = lane & 15, kq = lane >> 4;  // MFMA lane geometry: row / column, 8-deep K group
+  // the chunk weights: expand rows c0 .. c0 + 31 ([32][cinp]) and project columns ([Cout][32]) as fp16 in LDS,
+  // this thread's depthwise taps and bias in registers.  Loaded one chunk ahead: the next chunk's loads are in
+  // flight while this chunk computes.
+  constexpr int WI = (HC * kMaxCin / 4 + kThreads - 1) / kThreads;  // expand float4s per thread
+  constexpr int PI = (kMaxCout * HC / 4 + kThreads - 1) / kThreads; // project float4s per thread
+  const int q4 = cinp / 4, dj = tid % HC;
+  f32x4 we4[EXP ? WI : 1], wp4[PI];
+  float w9n[9], dbn;
+  auto load_w = [&](int c0) {
+    if constexpr (EXP) {
+#pragma unroll
+      for (int k = 0; k < WI; ++k) {
+        const int i = tid + k * kThreads, r = i / q4, c = (i - r * q4) * 4;
+        const bool ok = i < HC * q4 && c0 + r < h_end && c < a.Cin;
+        we4[k] = ld4(ok ? a.we + (long)(c0 + r) * a.Cin + c : reinterpret_cast<const float*>(g_mb_zero));
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < PI; ++k) {
+      const int i = tid + k * kThreads, co = i >> 3, c = (i & 7) * 4;
+      const bool ok = co < a.Cout && c0 + c < h_end;
+      wp4[k] = ld4(ok ? a.wp + (long)co * a.Ch + c0 + c : reinterpret_cast<const float*>(g_mb_zero));
+    }
+    const int dc = min(c0 + dj, a.Ch - 1);
+#pragma unroll
+    for (int k = 0; k < 9; ++k) w9n[k] = a.wd[k * a.Ch + dc];
+    dbn = a.bd[dc];
+  };
+  if (h_beg < h_end) load_w(h_beg);
   for (int c0 = h_beg; c0 < h_end; c0 += HC) {
-    // this thread's depthwise channel of the chunk: taps and bias, loaded with the chunk's other weights
-    const int dj = tid % HC, dc = c0 + dj;
+    __syncthreads();  // Xs staged / the previous chunk's reads of Ws, Wps, Es, Ds are done
+    if constexpr (EXP) {
+#pragma unroll
+      for (int k = 0; k < WI; ++k) {
+        const int i = tid + k * kThreads, r = i / q4, c = (i - r * q4) * 4;
+        if (i < HC * q4) {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) Ws[r * XR + c + j] = (_Float16)we4[k][j];
+        }
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < PI; ++k) {
+      const int i = tid + k * kThreads, co = i >> 3, c = (i & 7) * 4;
+      if (co < a.Cout) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) Wps[co * (HC + 8) + c + j] = (_Float16)wp4[k][j];
+      }
+    }
     float w9[9];
 #pragma unroll
-    for (int k = 0; k < 9; ++k) w9[k] = a.wd[k * a.Ch + min(dc, a.Ch - 1)];
-    const float dbias = a.bd[min(dc, a.Ch - 1)];
-    // the chunk's weights as fp16 in LDS: expand rows c0 .. c0 + 31 ([32][cinp]) and project columns
-    // ([Cout][32]) -- every load of the chunk in flight at once, then one barrier
-    {
-      constexpr int WI = (HC * kMaxCin / 4 + kThreads - 1) / kThreads;  // expand float4s per thread
-      constexpr int PI = (kMaxCout * HC / 4 + kThreads - 1) / kThreads; // project float4s per thread
-      const int q4 = cinp / 4;
-      f32x4 we4[EXP ? WI : 1], wp4[PI];
-      if constexpr (EXP) {
-#pragma unroll
-        for (int k = 0; k < WI; ++k) {
-          const int i = tid + k * kThreads, r = i / q4, c = (i - r * q4) * 4;
-          const bool ok = i < HC * q4 && c0 + r < h_end && c < a.Cin;
-          we4[k] = ld4(ok ? a.we + (long)(c0 + r) * a.Cin + c : reinterpret_cast<const float*>(g_mb_zero));
-        }
-      }
-#pragma unroll
-      for (int k = 0; k < PI; ++k) {
-        const int i = tid + k * kThreads, co = i >> 3, c = (i & 7) * 4;
-        const bool ok = co < a.Cout && c0 + c < h_end;
-        wp4[k] = ld4(ok ? a.wp + (long)co * a.Ch + c0 + c : reinterpret_cast<const float*>(g_mb_zero));
-      }
-      __syncthreads();  // Xs staged / the previous chunk's reads of Ws, Wps, Es, Ds are done
-      if constexpr (EXP) {
-#pragma unroll
-        for (int k = 0; k < WI; ++k) {
-          const int i = tid + k * kThreads, r = i / q4, c = (i - r * q4) * 4;
-          if (i < HC * q4) {
-#pragma unroll
-            for (int j = 0; j < 4; ++j) Ws[r * XR + c + j] = (_Float16)we4[k][j];
-          }
-        }
-      }
-#pragma unroll
-      for (int k = 0; k < PI; ++k) {
-        const int i = tid + k * kThreads, co = i >> 3, c = (i & 7) * 4;
-        if (co < a.Cout) {
-#pragma unroll
-          for (int j = 0; j < 4; ++j) Wps[co * (HC + 8) + c + j] = (_Float16)wp4[k][j];
-        }
-      }
-      __syncthreads();
-    }
+    for (int k = 0; k < 9; ++k) w9[k] = w9n[k];
+    const float dbias = dbn;
+    const int dc = c0 + dj;
+    __syncthreads();
+    if (c0 + HC < h_end) load_w(c0 + HC);
     if constexpr (EXP) {
       // expand: Es[hp][j] = relu6(sum_k X[hp][k] We[c0 + j][k] + be), (HPP / 16) x 2 tiles over the waves
       constexpr int ET = G::HPP / 16 * 2;
@@ -313,8 +320,8 @@ void mb_plan(int N, int H, int W, int Ch, int stride, int* tiles_w, int* tiles_h
   *tp = toh * tow;
   const int ntiles = N * *tiles_w * *tiles_h;
   const int chunks = (Ch + HC - 1) / HC;
-  // hidden splits: about 128 blocks in all, at least 2 chunks per block where there are chunks to spare
-  int s = std::max(1, std::min(chunks / 2, (128 + ntiles - 1) / ntiles));
+  // hidden splits: up to 256 blocks in all (one per CU: co-resident, so every block of a tile helps combine it)
+  int s = std::max(1, std::min(chunks, 256 / std::max(1, ntiles)));
   const int per = (chunks + s - 1) / s;
   *splits = (chunks + per - 1) / per;
   *hper = per * HC;

@@ -76,36 +76,7 @@ __global__ __launch_bounds__(kThreads) void mbconv_f16_kernel(MbArgs a) {
     return hp < G::HP && (unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W;
   };
   const int cinp = (a.Cin + 31) & ~31;
-  if constexpr (EXP) {  // the input halo as fp16, zero outside the image and beyond Cin (all loads issued together)
-    const int q4 = cinp / 4;
-    constexpr int XI = (G::HPP * (kMaxCin + 31) / 32 * 8 + kThreads - 1) / kThreads;
-    f32x4 v[XI];
-#pragma unroll
-    for (int k = 0; k < XI; ++k) {
-      const int i = tid + k * kThreads, hp = i / q4, c = (i - hp * q4) * 4;
-      int ih, iw;
-      const bool ok = i < G::HPP * q4 && halo_in(hp, ih, iw) && c < a.Cin;
-      v[k] = ld4(ok ? xim + ((long)ih * a.W + iw) * a.ldx + c : reinterpret_cast<const float*>(g_mb_zero));
-    }
-#pragma unroll
-    for (int k = 0; k < XI; ++k) {
-      const int i = tid + k * kThreads, hp = i / q4, c = (i - hp * q4) * 4;
-      if (i < G::HPP * q4) {
-        _Float16* d = Xs + hp * XR + c;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) d[j] = (_Float16)v[k][j];
-      }
-    }
-  }
-  // project accumulators: (m, n) 16x16 tiles p = wave, wave + 4, ... of (TP / 16) x ceil(Cout / 16)
-  constexpr int MT = G::TP / 16;
-  const int NT = (a.Cout + 15) / 16;
-  constexpr int PMAX = (MT * (kMaxCout / 16) + 3) / 4;
-  f32x4 pacc[PMAX];
-#pragma unroll
-  for (int p = 0; p < PMAX; ++p) pacc[p] = f32x4{0.f, 0.f, 0.f, 0.f};
   const int h_beg = split * a.hper, h_end = min(a.Ch, h_beg + a.hper);
-  const int r16 = lane & 15, kq = lane >> 4;  // MFMA lane geometry: row / column, 8-deep K group
   // the chunk weights: expand rows c0 .. c0 + 31 ([32][cinp]) and project columns ([Cout][32]) as fp16 in LDS,
   // this thread's depthwise taps and bias in registers.  Loaded one chunk ahead: the next chunk's loads are in
   // flight while this chunk computes.
@@ -134,7 +105,36 @@ __global__ __launch_bounds__(kThreads) void mbconv_f16_kernel(MbArgs a) {
     for (int k = 0; k < 9; ++k) w9n[k] = a.wd[k * a.Ch + dc];
     dbn = a.bd[dc];
   };
-  if (h_beg < h_end) load_w(h_beg);
+  if (h_beg < h_end) load_w(h_beg);  // in flight with the input halo below
+  if constexpr (EXP) {  // the input halo as fp16, zero outside the image and beyond Cin (all loads issued together)
+    const int q4 = cinp / 4;
+    constexpr int XI = (G::HPP * (kMaxCin + 31) / 32 * 8 + kThreads - 1) / kThreads;
+    f32x4 v[XI];
+#pragma unroll
+    for (int k = 0; k < XI; ++k) {
+      const int i = tid + k * kThreads, hp = i / q4, c = (i - hp * q4) * 4;
+      int ih, iw;
+      const bool ok = i < G::HPP * q4 && halo_in(hp, ih, iw) && c < a.Cin;
+      v[k] = ld4(ok ? xim + ((long)ih * a.W + iw) * a.ldx + c : reinterpret_cast<const float*>(g_mb_zero));
+    }
+#pragma unroll
+    for (int k = 0; k < XI; ++k) {
+      const int i = tid + k * kThreads, hp = i / q4, c = (i - hp * q4) * 4;
+      if (i < G::HPP * q4) {
+        _Float16* d = Xs + hp * XR + c;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) d[j] = (_Float16)v[k][j];
+      }
+    }
+  }
+  // project accumulators: (m, n) 16x16 tiles p = wave, wave + 4, ... of (TP / 16) x ceil(Cout / 16)
+  constexpr int MT = G::TP / 16;
+  const int NT = (a.Cout + 15) / 16;
+  constexpr int PMAX = (MT * (kMaxCout / 16) + 3) / 4;
+  f32x4 pacc[PMAX];
+#pragma unroll
+  for (int p = 0; p < PMAX; ++p) pacc[p] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int r16 = lane & 15, kq = lane >> 4;  // MFMA lane geometry: row / column, 8-deep K group
   for (int c0 = h_beg; c0 < h_end; c0 += HC) {
     __syncthreads();  // Xs staged / the previous chunk's reads of Ws, Wps, Es, Ds are done
     if constexpr (EXP) {

@@ -91,6 +91,25 @@ int seg_conv_pw(const float* in, long ldin, long M, int K, const float* wk, int 
 /* Split-K factor for seg_conv_igemm_act (1 = none): > 1 only when the output tiles
  * cannot fill the 256 CUs (batch-1 inference). */
 int seg_conv_igemm_splits(long M, int Cout, int Cin, int ks);
+/* seg_conv_igemm_act / _bf16 / _f16 with split-K combined inside the launch (the inference forward's
+ * batch-1 convs): when the whole grid is co-resident each split block of a tile waits for the tile's
+ * other splits and applies the split-K epilogue to its share (else the separate reduce runs); bitwise
+ * the two-launch result.  cnt: 2 * seg_conv_igemm_tiles(M, Cout) unsigned, zero before the first
+ * launch, re-armed by every launch.  No BN statistics. */
+int seg_conv_igemm_tiles(long M, int Cout);
+int seg_conv_igemm_act_ic(const float* in, long ldin, int N, int H, int W, int Cin, const float* wk, int ldk,
+                          const float* bias, float* out, long ldout, int Ho, int Wo, int Cout, int ks, int stride,
+                          int pad, const float* add, long ldadd, int act, float* work, int splits, unsigned* cnt,
+                          hipStream_t stream);
+int seg_conv_igemm_bf16_ic(const float* in, long ldin, int N, int H, int W, int Cin, const float* wk, int ldk,
+                           const float* bias, float* out, long ldout, int Ho, int Wo, int Cout, int ks, int stride,
+                           int pad, const float* add, long ldadd, int act, float* work, int splits, unsigned* cnt,
+                           hipStream_t stream);
+int seg_conv_igemm_f16_ic(const float* in, long ldin, int N, int H, int W, int Cin, const float* wk, int ldk,
+                          const float* bias, float* out, long ldout, int Ho, int Wo, int Cout, int ks, int stride,
+                          int pad, const float* add, long ldadd, int act, float* work, int splits, unsigned* cnt,
+                          hipStream_t stream);
+
 /* seg_conv_igemm as a stride-1 data gradient (pad ks/2, no bias, optional fused addend) that
  * completes dA of a BatchNorm layer whose pre-BN output is `by`: the epilogue also writes that
  * layer's BN-backward partials per row tile, bpart[seg_conv_igemm_row_tiles(M, Cout)][2][Cout] =

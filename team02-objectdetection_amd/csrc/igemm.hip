@@ -79,6 +79,22 @@ SEG_API int seg_conv_igemm(const float* in, long ldin, int N, int H, int W, int 
                             ldadd, stat, SEG_ACT_NONE, nullptr, 1, stream);
 }
 
+// seg_conv_igemm_act with the in-launch split-K combine (as seg_conv_igemm_f16_ic).
+SEG_API int seg_conv_igemm_act_ic(const float* in, long ldin, int N, int H, int W, int Cin,
+                                   const float* wk, int ldk, const float* bias, float* out, long ldout, int Ho, int Wo,
+                                   int Cout, int ks, int stride, int pad, const float* add, long ldadd, int act,
+                                   float* work, int splits, unsigned* cnt, hipStream_t stream) {
+  return conv_igemm_impl<float>(in, ldin, N, H, W, Cin, wk, ldk, bias, out, ldout, Ho, Wo, Cout, ks, stride, pad, add,
+                              ldadd, nullptr, act, work, splits, stream, nullptr, nullptr, 0, (const float*)nullptr, 0, nullptr,
+                              nullptr, nullptr, 0, nullptr, cnt);
+}
+
+// Output tiles (M x Cout blocks) of the implicit GEMM: the split-K combine's counters are 2 per tile.
+SEG_API int seg_conv_igemm_tiles(long M, int Cout) {
+  const int t = pick_tile(M, Cout);
+  return (int)(((M + kTiles[t].bm - 1) / kTiles[t].bm) * ((Cout + kTiles[t].bn - 1) / kTiles[t].bn));
+}
+
 // Split-K factor seg_conv_igemm_act should be given for this conv (1 = none); the
 // workspace is splits * N*Ho*Wo * Cout floats.
 SEG_API int seg_conv_igemm_splits(long M, int Cout, int Cin, int ks) {

@@ -43,6 +43,9 @@ struct IgemmArgs {
   // dz and dz (by - bmu), dz = out act'(by bsc + bsh) on the values as stored, into bpart
   // [tilesM][2][Cout] for seg_bn_bwd_finalize_tiles -- the reduction pass over dA disappears
   const void* by; long ldby; const float* bsc; const float* bsh; const float* bmu; int bact; float* bpart;
+  // split-K with the combine in the launch (part set, the whole grid co-resident): tile counters
+  // [2][tilesM * tilesN] (arrive, leave; zero before the first launch, re-armed by the last leaver)
+  unsigned* kcnt;
 };
 
 #ifndef SEG_IGEMM_DEPTH
@@ -448,8 +451,9 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void igemm_conv_kernel(
 #endif
 
   // Epilogue: C layout of 32x32 f32 MFMA: col = lane&31, row = (r&3) + 8(r>>2) + 4(lane>>5).
-  if (a.part) {  // split-K: raw partial sums; seg_igemm_splitk_reduce applies the epilogue
+  if (a.part) {  // split-K: raw partial sums; seg_igemm_splitk_reduce (or the in-launch combine) applies the epilogue
     float* P = a.part + (long)blockIdx.y * a.M * a.Cout;
+    const bool ic = a.kcnt != nullptr;
 #pragma unroll
     for (int ni = 0; ni < NI; ++ni) {
       const int col = n0 + wn0 + ni * 32 + lrow;
@@ -459,8 +463,44 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void igemm_conv_kernel(
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const int row = m0 + wm0 + mi * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-          if (row < a.M) P[(long)row * a.Cout + col] = acc[mi][ni][r];
+          if (row < a.M) {
+            if (ic) seg_st_wt(P + (long)row * a.Cout + col, acc[mi][ni][r]);
+            else P[(long)row * a.Cout + col] = acc[mi][ni][r];
+          }
         }
+    }
+    if (!ic) return;
+    // in-launch combine (the host launches this form only when the whole grid is co-resident): every split
+    // block of the tile waits for the tile's other splits, then applies splitk_reduce_kernel's epilogue to its
+    // 1/splits share of the tile -- the same fixed-order sum, so bitwise the two-launch result
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    const int ntl = gridDim.x, S = gridDim.y, z = blockIdx.y;
+    unsigned* arrive = a.kcnt + lid;
+    unsigned* leave = a.kcnt + ntl + lid;
+    if (tid == 0) {
+      __hip_atomic_fetch_add(arrive, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      while (__hip_atomic_load(arrive, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (unsigned)S)
+        __builtin_amdgcn_s_sleep(1);
+    }
+    __syncthreads();
+    constexpr int E = BM * BN;
+    const int e0 = (int)((long)z * E / S), e1 = (int)((long)(z + 1) * E / S);
+    const long total = (long)a.M * a.Cout;
+    for (int e = e0 + tid; e < e1; e += NT) {
+      const int r = e / BN, c = e - r * BN, row = m0 + r, col = n0 + c;
+      if (row >= a.M || col >= a.Cout) continue;
+      const long i = (long)row * a.Cout + col;
+      float v = 0.f;
+      for (int zz = 0; zz < S; ++zz) v += seg_ld_wt(a.part + zz * total + i);
+      if (a.bias) v += a.bias[col];
+      if (add) v += (float)add[(long)row * a.ldadd + col];
+      if (a.act) v = seg_act(v, a.act);
+      out[(long)row * a.ldout + col] = static_cast<IT>(v);
+    }
+    if (tid == 0 && __hip_atomic_fetch_add(leave, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (unsigned)S - 1) {
+      __hip_atomic_store(arrive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(leave, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     return;
   }
@@ -684,14 +724,30 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void igemm_conv_kernel(
   }
 }
 
+// set by the last launch_igemm_bk: whether its split-K combine ran in the launch (no reduce kernel needed)
+thread_local bool g_igemm_ic_used = false;
+
 template <int BM, int BN, int WM, int WN, int BK, typename OT, typename IT, bool WB = false>
-int launch_igemm_bk(const IgemmArgs& a, int ks, hipStream_t s) {
+int launch_igemm_bk(IgemmArgs a, int ks, hipStream_t s) {
   const int grid = seg_cdiv(a.M, BM) * seg_cdiv(a.Cout, BN);
   const int splits = seg_cdiv(a.K, a.kchunk);
   const bool ut = SEG_IGEMM_UT && (SEG_IGEMM_UT2 ? a.Cin >= BK : a.Cin % BK == 0) &&
                   (sizeof(IT) == 4 || (a.Cin % 8 == 0 && a.ldin % 8 == 0));  // bf16 A: 16-byte slots
   constexpr int NT = 64 * (BM / WM) * (BN / WN);
   if (a.xs && !ut) return (int)hipErrorInvalidValue;  // input transform: the uniform-tap loader only (Cin >= BK)
+  if (a.kcnt) {  // in-launch split-K combine: only when the whole grid is co-resident (it spins on the tile's splits)
+    int occ = 0;
+    const void* fn = ks == 1 ? (ut ? (const void*)igemm_conv_kernel<BM, BN, WM, WN, 1, BK, true, OT, IT, WB, false>
+                                   : (const void*)igemm_conv_kernel<BM, BN, WM, WN, 1, BK, false, OT, IT, WB, false>)
+                             : (ut ? (const void*)igemm_conv_kernel<BM, BN, WM, WN, 3, BK, true, OT, IT, WB, false>
+                                   : (const void*)igemm_conv_kernel<BM, BN, WM, WN, 3, BK, false, OT, IT, WB, false>);
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, fn, NT, 0) != hipSuccess ||
+        (long)grid * splits > (long)occ * seg_num_cus()) {
+      (void)hipGetLastError();
+      a.kcnt = nullptr;
+    }
+  }
+  g_igemm_ic_used = a.kcnt != nullptr;
 #define SEG_IG(KS, U, B) hipLaunchKernelGGL((igemm_conv_kernel<BM, BN, WM, WN, KS, BK, U, OT, IT, WB, B>), dim3(grid, splits), dim3(NT), 0, s, a)
   constexpr int VPR = BN / (16 / (int)sizeof(IT));
   // (instantiated for the training storage types only: f32 and bf16io, where operands are the storage type)
@@ -821,7 +877,7 @@ int conv_igemm_impl(const IT* in, long ldin, int N, int H, int W, int Cin, const
                     const IT* add, long ldadd, float* stat, int act, float* work, int splits, hipStream_t stream,
                     const float* xs = nullptr, const float* xb = nullptr, int xact = 0, const IT* by = nullptr,
                     long ldby = 0, const float* bsc = nullptr, const float* bsh = nullptr, const float* bmu = nullptr,
-                    int bact = 0, float* bpart = nullptr) {
+                    int bact = 0, float* bpart = nullptr, unsigned* kcnt = nullptr) {
   if (!std::is_same<IT, float>::value && splits != 1) return (int)hipErrorInvalidValue;
   if ((Cin & 3) || (ldin & 3) || (ldk & 3) || (ks != 1 && ks != 3)) return (int)hipErrorInvalidValue;
   if (WB && ((ldk & 7) || ((uintptr_t)wk & 15) || splits != 1)) return (int)hipErrorInvalidValue;
@@ -843,6 +899,8 @@ int conv_igemm_impl(const IT* in, long ldin, int N, int H, int W, int Cin, const
   a.part = splits > 1 ? work : nullptr;
   a.xs = xs; a.xb = xb; a.xact = xact;
   a.by = by; a.ldby = ldby; a.bsc = bsc; a.bsh = bsh; a.bmu = bmu; a.bact = bact; a.bpart = bpart;
+  a.kcnt = splits > 1 ? kcnt : nullptr;
+  g_igemm_ic_used = false;
   if (bpart && !igemm_bnout_tile_ok(a.M, Cout, (int)sizeof(IT))) return (int)hipErrorInvalidValue;
   if (a.M == 0 || Cout == 0) return 0;
   int rc;
@@ -863,7 +921,7 @@ int conv_igemm_impl(const IT* in, long ldin, int N, int H, int W, int Cin, const
     case 13: rc = launch_igemm<256, 64, 64, 32, OT, IT, WB>(a, ks, splits, stream); break;
     default: rc = launch_igemm<64, 128, 32, 32, OT, IT, WB>(a, ks, splits, stream); break;
   }
-  if (rc || splits == 1) return rc;
+  if (rc || splits == 1 || g_igemm_ic_used) return rc;
   const long total = (long)a.M * Cout;
   hipLaunchKernelGGL(splitk_reduce_kernel, dim3((int)std::min<long>(seg_cdiv(total, 256), 4096)), dim3(256), 0,
                      stream, work, splits, (long)a.M, Cout, bias, reinterpret_cast<const float*>(add), ldadd,

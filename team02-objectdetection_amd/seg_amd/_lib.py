@@ -116,6 +116,9 @@ PROTOTYPES = {
     "seg_bn_bwd_finalize_tiles": (_I, [_V, _I, _L, _I, _V, _V, _V, _V, _V, _V]),
     "seg_conv_igemm_bnout_ok": (_I, [_L, _I, _I]),
     "seg_mbconv_ok": (_I, [_I, _I, _I, _I, _I]),
+    "seg_conv_igemm_tiles": (_I, [_L, _I]),
+    "seg_conv_igemm_act_ic": (_I, [_V, _L, _I, _I, _I, _I, _V, _I, _V, _V, _L, _I, _I, _I, _I, _I, _I, _V, _L, _I,
+                                   _V, _I, _V, _V]),
     "seg_mbconv_work_floats": (_L, [_I, _I, _I, _I, _I, _I, _V]),
     "seg_mbconv_f16": (_I, [_V, _L, _I, _I, _I, _I, _V, _V, _I, _V, _V, _I, _V, _V, _I, _V, _L, _V, _L, _V, _V,
                             _V]),
@@ -131,6 +134,8 @@ PROTOTYPES["seg_conv_igemm_bf16io"] = PROTOTYPES["seg_conv_igemm"]
 PROTOTYPES["seg_dw2_dgrad_bf16io"] = PROTOTYPES["seg_dw_dgrad"]
 PROTOTYPES["seg_bn_bwd_coef_bf16io"] = PROTOTYPES["seg_bn_bwd_coef"]
 PROTOTYPES["seg_conv_igemm_bnout_bf16io"] = PROTOTYPES["seg_conv_igemm_bnout"]
+PROTOTYPES["seg_conv_igemm_bf16_ic"] = PROTOTYPES["seg_conv_igemm_act_ic"]
+PROTOTYPES["seg_conv_igemm_f16_ic"] = PROTOTYPES["seg_conv_igemm_act_ic"]
 PROTOTYPES["seg_conv_igemm_bnout_bf16io_w16"] = PROTOTYPES["seg_conv_igemm_bnout"]
 PROTOTYPES["seg_bn_bwd_apply_bf16io"] = PROTOTYPES["seg_bn_bwd_apply"]
 PROTOTYPES["seg_dw2_wgrad_bf16io"] = PROTOTYPES["seg_dw_wgrad"]

@@ -36,7 +36,7 @@ _PURE_QUERIES = {"seg_chan_workspace_floats", "seg_conv_wgrad_splits", "seg_conv
                  "seg_conv_igemm_splits", "seg_ce_workspace_floats", "seg_conv_wino_row_tiles", "seg_conv_wino_tile_rows",
                  "seg_conv_halo_row_tiles", "seg_conv_wino_wgrad_splits", "seg_dw2_ok",
                  "seg_dw2_wgrad_blocks", "seg_dw2_dgrad_tiles", "seg_conv_igemm_bnout_ok",
-                 "seg_mbconv_ok"}
+                 "seg_mbconv_ok", "seg_conv_igemm_tiles"}
 _QCACHE = {}
 
 
@@ -360,10 +360,22 @@ class ConvOp:
         bias = self.fb.data_ptr() if self.fb is not None else None
         M = o.N * o.H * o.W
         splits = query("seg_conv_igemm_splits", M, self.cout, self.cin_pad, self.ks)
-        work = rt.tmp(splits * M * self.cout) if splits > 1 else None
+        if splits > 1:
+            # split-K combined inside the launch (seg_conv_igemm_*_ic); workspace and tile counters persistent
+            # across graph replays (allocated by the warm-up launch, before any capture)
+            bufs = rt._mb.get(("ic", id(self)))
+            if bufs is None:
+                bufs = rt._mb[("ic", id(self))] = (
+                    torch.empty(splits * M * self.cout, device=rt.device, dtype=torch.float32),
+                    torch.zeros(2 * query("seg_conv_igemm_tiles", M, self.cout), device=rt.device, dtype=torch.int32))
+            rt.call(_FOLDED_CONV[rt.prog.math] + "_ic", rt.ptr(i), i.ld, i.N, i.H, i.W, self.cin_pad, wk, ldk, bias,
+                    rt.ptr(o), o.ld, o.H, o.W, self.cout, self.ks, self.stride, self.pad,
+                    rt.ptr(r) if r is not None else None, r.ld if r is not None else 0, act, bufs[0].data_ptr(), splits,
+                    bufs[1].data_ptr(), s)
+            return
         rt.call(_FOLDED_CONV[rt.prog.math], rt.ptr(i), i.ld, i.N, i.H, i.W, self.cin_pad, wk, ldk, bias, rt.ptr(o), o.ld,
              o.H, o.W, self.cout, self.ks, self.stride, self.pad, rt.ptr(r) if r is not None else None,
-             r.ld if r is not None else 0, None, act, work.data_ptr() if work is not None else None, splits, s)
+             r.ld if r is not None else 0, None, act, None, 1, s)
 
     def _in_xform(self, rt):
         """(scale, shift, act) of the producer's lazy BN for this op's input loads, or (None, None, 0)."""

@@ -491,8 +491,15 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void igemm_conv_kernel(
       const int r = e / BN, c = e - r * BN, row = m0 + r, col = n0 + c;
       if (row >= a.M || col >= a.Cout) continue;
       const long i = (long)row * a.Cout + col;
-      float v = 0.f;
-      for (int zz = 0; zz < S; ++zz) v += seg_ld_wt(a.part + zz * total + i);
+      float v = 0.f;  // the splits in order, 16 loads in flight at a time
+      for (int z0 = 0; z0 < S; z0 += 16) {
+        float q[16];
+#pragma unroll
+        for (int j = 0; j < 16; ++j) q[j] = z0 + j < S ? seg_ld_wt(a.part + (z0 + j) * total + i) : 0.f;
+#pragma unroll
+        for (int j = 0; j < 16; ++j)
+          if (z0 + j < S) v += q[j];
+      }
       if (a.bias) v += a.bias[col];
       if (add) v += (float)add[(long)row * a.ldadd + col];
       if (a.act) v = seg_act(v, a.act);

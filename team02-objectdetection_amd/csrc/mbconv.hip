@@ -265,6 +265,18 @@ __global__ __launch_bounds__(kThreads) void mbconv_f16_kernel(MbArgs a) {
   }
   const float* w0 = a.work + (long)t * a.splits * G::TP * a.Cout;
   const int ne = G::TP * a.Cout;
+  auto split_sum = [&](int e) {  // the splits in order, 16 loads in flight at a time
+    float v = 0.f;
+    for (int s0 = 0; s0 < a.splits; s0 += 16) {
+      float q[16];
+#pragma unroll
+      for (int j = 0; j < 16; ++j) q[j] = s0 + j < a.splits ? seg_ld_wt(w0 + (long)(s0 + j) * ne + e) : 0.f;
+#pragma unroll
+      for (int j = 0; j < 16; ++j)
+        if (s0 + j < a.splits) v += q[j];
+    }
+    return v;
+  };
   auto emit = [&](int e, float v) {
     const int px = e / a.Cout, co = e - px * a.Cout;
     long orow;
@@ -290,10 +302,7 @@ __global__ __launch_bounds__(kThreads) void mbconv_f16_kernel(MbArgs a) {
     __syncthreads();
     const int e0 = (int)((long)split * ne / a.splits), e1 = (int)((long)(split + 1) * ne / a.splits);
     for (int e = e0 + tid; e < e1; e += kThreads) {
-      float v = 0.f;
-#pragma unroll 4
-      for (int sp = 0; sp < a.splits; ++sp) v += seg_ld_wt(w0 + (long)sp * ne + e);
-      emit(e, v);
+      emit(e, split_sum(e));
     }
     if (tid == 0 &&
         __hip_atomic_fetch_add(leave, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (unsigned)a.splits - 1) {
@@ -305,10 +314,7 @@ __global__ __launch_bounds__(kThreads) void mbconv_f16_kernel(MbArgs a) {
   if (!seg_last_arrival(a.cnt + t, (unsigned)a.splits, &word)) return;
   // (grid larger than the chip) the last block of the tile combines all of it
   for (int e = tid; e < ne; e += kThreads) {
-    float v = 0.f;
-#pragma unroll 4
-    for (int sp = 0; sp < a.splits; ++sp) v += seg_ld_wt(w0 + (long)sp * ne + e);
-    emit(e, v);
+    emit(e, split_sum(e));
   }
 }
 

@@ -131,9 +131,11 @@ def test_halo2_refuses_what_it_cannot_hold():
              out.data_ptr(), 64, 64, None, 0, None, S())
 
 
-def test_engine_routes_narrow_convs_to_halo2():
-    """MobileNetV2UNet bf16io at bs=32 256x512: up4 / up3.3 forward and data gradients on halo2."""
+def test_engine_routes_narrow_convs_to_halo2(monkeypatch):
+    """MobileNetV2UNet bf16io at bs=32 256x512 with SEG_HALO2=1 (default off since round 4): up4 / up3.3
+    forward and data gradients on halo2."""
     from seg_amd import MobileNetV2UNet, deterministic_init
+    monkeypatch.setattr(engine, "HALO2", True)
     m = deterministic_init(MobileNetV2UNet(10), seed=0).to(DEV).train()
     engine.set_conv_math(m, "bf16io")
     prog = engine.get_program(m, 32, 256, 512)

@@ -152,7 +152,7 @@ def test_igemm2_every_tile(tile):
         query("seg_igemm2_force_tile", -1)
 
 
-@pytest.mark.parametrize("M,Cin,Cout,act", [(4096, 960, 160, 0), (16384, 576, 96, 2), (65536, 144, 32, 2),
+@pytest.mark.parametrize("M,Cin,Cout,act", [(4096, 960, 160, 0), (16384, 576, 96, 2), (65536, 144, 64, 2),
                                             (4096, 960, 320, 0)])
 def test_igemm2_xf_equals_generic_xf(M, Cin, Cout, act):
     """The 1x1 lazy-BN variant (the inverted residuals' project convs: the dw conv's BatchNorm +

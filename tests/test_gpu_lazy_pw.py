@@ -183,12 +183,13 @@ def test_xf3_matches_apply_then_conv(math, N, H, W, Cin, Cout, ld, act):
 def test_lazy3_model_step_bitwise(arch, monkeypatch):
     """bf16io training step with double_conv's second conv applying the first one's BN + ReLU on load
     (engine.LAZY3) equals the step with the BN-apply pass, bitwise: loss, every gradient, BN running
-    statistics.  (igemm2 off in both runs: it takes no input transform, so with LAZY3 the deep convs
+    statistics.  (igemm2 and wgrad2 off in both runs: they take no input transform, so with LAZY3 the deep convs
     move to the implicit GEMM and a different K order; the default path is covered by the oracle-budget
     tests of test_gpu_model.py / test_gpu_configs.py.)"""
     from seg_amd import MobileNetV2UNet, UNet, engine
     from seg_amd.detinit import deterministic_init, synthetic_batch
     monkeypatch.setattr(engine, "IGEMM2", "0")
+    monkeypatch.setattr(engine, "WGRAD2", False)  # takes no input transform either (another K order)
     N, H, W = (2, 64, 128) if arch == "UNet" else (2, 128, 256)
     x, t = synthetic_batch(N, H, W, 10 if arch == "UNet" else 3, seed=17)
     x, t = x.to(DEV), t.to(DEV)

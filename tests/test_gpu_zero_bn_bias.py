@@ -34,7 +34,8 @@ def _rel(a, b):
 
 
 def _bias_names(sd):
-    return [k for k in sd if k.startswith("up") and ".conv.conv." in k and k.endswith("bias")]
+    # the decoder's conv biases (double_conv's Conv2d at .0 and .3; .1 / .4 are its BatchNorms)
+    return [k for k in sd if k.startswith("up") and k.endswith((".conv.conv.0.bias", ".conv.conv.3.bias"))]
 
 
 def _batches():

@@ -97,17 +97,22 @@ int seg_conv_igemm_splits(long M, int Cout, int Cin, int ks);
  * the two-launch result.  cnt: 2 * seg_conv_igemm_tiles(M, Cout) unsigned, zero before the first
  * launch, re-armed by every launch.  No BN statistics. */
 int seg_conv_igemm_tiles(long M, int Cout);
+/* Plan for those launches: out[3] = (splits, tile, output tiles -- the counters are 2 per tile).  tile -1 =
+ * the cost model's (seg_conv_igemm_tiles), else an index into the kernel's tile table (the batch-1 rule:
+ * short K unsplit on 64x64 tiles, long K split on 8-wave 128x64 tiles).  Tile choice does not change
+ * results; the split count does (another K partition). */
+int seg_conv_igemm_plan_b1(long M, int Cout, int Cin, int ks, int* out);
 int seg_conv_igemm_act_ic(const float* in, long ldin, int N, int H, int W, int Cin, const float* wk, int ldk,
                           const float* bias, float* out, long ldout, int Ho, int Wo, int Cout, int ks, int stride,
-                          int pad, const float* add, long ldadd, int act, float* work, int splits, unsigned* cnt,
+                          int pad, const float* add, long ldadd, int act, float* work, int splits, int tile, unsigned* cnt,
                           hipStream_t stream);
 int seg_conv_igemm_bf16_ic(const float* in, long ldin, int N, int H, int W, int Cin, const float* wk, int ldk,
                            const float* bias, float* out, long ldout, int Ho, int Wo, int Cout, int ks, int stride,
-                           int pad, const float* add, long ldadd, int act, float* work, int splits, unsigned* cnt,
+                           int pad, const float* add, long ldadd, int act, float* work, int splits, int tile, unsigned* cnt,
                            hipStream_t stream);
 int seg_conv_igemm_f16_ic(const float* in, long ldin, int N, int H, int W, int Cin, const float* wk, int ldk,
                           const float* bias, float* out, long ldout, int Ho, int Wo, int Cout, int ks, int stride,
-                          int pad, const float* add, long ldadd, int act, float* work, int splits, unsigned* cnt,
+                          int pad, const float* add, long ldadd, int act, float* work, int splits, int tile, unsigned* cnt,
                           hipStream_t stream);
 
 /* seg_conv_igemm as a stride-1 data gradient (pad ks/2, no bias, optional fused addend) that

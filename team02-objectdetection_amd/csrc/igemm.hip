@@ -83,16 +83,49 @@ SEG_API int seg_conv_igemm(const float* in, long ldin, int N, int H, int W, int 
 SEG_API int seg_conv_igemm_act_ic(const float* in, long ldin, int N, int H, int W, int Cin,
                                    const float* wk, int ldk, const float* bias, float* out, long ldout, int Ho, int Wo,
                                    int Cout, int ks, int stride, int pad, const float* add, long ldadd, int act,
-                                   float* work, int splits, unsigned* cnt, hipStream_t stream) {
+                                   float* work, int splits, int tile, unsigned* cnt, hipStream_t stream) {
   return conv_igemm_impl<float>(in, ldin, N, H, W, Cin, wk, ldk, bias, out, ldout, Ho, Wo, Cout, ks, stride, pad, add,
                               ldadd, nullptr, act, work, splits, stream, nullptr, nullptr, 0, (const float*)nullptr, 0, nullptr,
-                              nullptr, nullptr, 0, nullptr, cnt);
+                              nullptr, nullptr, 0, nullptr, cnt, tile);
 }
 
 // Output tiles (M x Cout blocks) of the implicit GEMM: the split-K combine's counters are 2 per tile.
 SEG_API int seg_conv_igemm_tiles(long M, int Cout) {
   const int t = pick_tile(M, Cout);
   return (int)(((M + kTiles[t].bm - 1) / kTiles[t].bm) * ((Cout + kTiles[t].bn - 1) / kTiles[t].bn));
+}
+
+// Plan of the folded inference forward's convs (seg_conv_igemm_*_ic), out[3] = (splits, tile, output tiles):
+// where the cost model's tiles fill the chip, its own choice (1 split, tile -1).  Below that (batch-1 frames)
+// per-launch timings of the decoder convs of a 128x256 frame (tools/icbench.py, profiles/r04ic_icbench.txt)
+// set the rule: short K (<= 24 chunks) unsplit on the 64x64 tile (more blocks; a split's combine costs more
+// than its chunks), longer K on the 8-wave 128x64 tile split to ~256 blocks with >= 2 chunks per split
+// (at most 32 splits).
+SEG_API int seg_conv_igemm_plan_b1(long M, int Cout, int Cin, int ks, int* out) {
+  if (!out) return (int)hipErrorInvalidValue;
+  int splits = 1, tile = -1;
+  if (M > 0 && Cout > 0 && Cin > 0 && seg_igemm_forced_tile < 0) {
+    const long K = (long)ks * ks * Cin;
+    const int t = pick_tile(M, Cout);
+    const long blocks = ((M + kTiles[t].bm - 1) / kTiles[t].bm) * ((Cout + kTiles[t].bn - 1) / kTiles[t].bn);
+    const int nk = seg_cdiv(K, igemm_bk((int)K));
+    if (blocks < 256) {
+      if (nk <= 24) {
+        tile = 3;
+      } else {
+        tile = 12;
+        const long b12 = ((M + 127) / 128) * ((Cout + 63) / 64);
+        long s = std::min<long>(std::min<long>(32, (256 + b12 - 1) / b12), nk / 2);
+        s = std::max<long>(s, 1);
+        splits = seg_cdiv(nk, seg_cdiv(nk, (int)s));  // no empty split
+      }
+    }
+  }
+  const int tt = tile >= 0 ? tile : pick_tile(std::max<long>(M, 1), std::max(Cout, 1));
+  out[0] = splits;
+  out[1] = tile;
+  out[2] = (int)(((M + kTiles[tt].bm - 1) / kTiles[tt].bm) * ((Cout + kTiles[tt].bn - 1) / kTiles[tt].bn));
+  return 0;
 }
 
 // Split-K factor seg_conv_igemm_act should be given for this conv (1 = none); the

@@ -19,8 +19,8 @@ SEG_API int seg_conv_igemm_f16(const float* in, long ldin, int N, int H, int W, 
 SEG_API int seg_conv_igemm_f16_ic(const float* in, long ldin, int N, int H, int W, int Cin,
                                    const float* wk, int ldk, const float* bias, float* out, long ldout, int Ho, int Wo,
                                    int Cout, int ks, int stride, int pad, const float* add, long ldadd, int act,
-                                   float* work, int splits, unsigned* cnt, hipStream_t stream) {
+                                   float* work, int splits, int tile, unsigned* cnt, hipStream_t stream) {
   return conv_igemm_impl<_Float16>(in, ldin, N, H, W, Cin, wk, ldk, bias, out, ldout, Ho, Wo, Cout, ks, stride, pad, add,
                               ldadd, nullptr, act, work, splits, stream, nullptr, nullptr, 0, (const float*)nullptr, 0, nullptr,
-                              nullptr, nullptr, 0, nullptr, cnt);
+                              nullptr, nullptr, 0, nullptr, cnt, tile);
 }

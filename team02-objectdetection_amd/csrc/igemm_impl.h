@@ -884,7 +884,7 @@ int conv_igemm_impl(const IT* in, long ldin, int N, int H, int W, int Cin, const
                     const IT* add, long ldadd, float* stat, int act, float* work, int splits, hipStream_t stream,
                     const float* xs = nullptr, const float* xb = nullptr, int xact = 0, const IT* by = nullptr,
                     long ldby = 0, const float* bsc = nullptr, const float* bsh = nullptr, const float* bmu = nullptr,
-                    int bact = 0, float* bpart = nullptr, unsigned* kcnt = nullptr) {
+                    int bact = 0, float* bpart = nullptr, unsigned* kcnt = nullptr, int tile = -1) {
   if (!std::is_same<IT, float>::value && splits != 1) return (int)hipErrorInvalidValue;
   if ((Cin & 3) || (ldin & 3) || (ldk & 3) || (ks != 1 && ks != 3)) return (int)hipErrorInvalidValue;
   if (WB && ((ldk & 7) || ((uintptr_t)wk & 15) || splits != 1)) return (int)hipErrorInvalidValue;
@@ -909,9 +909,11 @@ int conv_igemm_impl(const IT* in, long ldin, int N, int H, int W, int Cin, const
   a.kcnt = splits > 1 ? kcnt : nullptr;
   g_igemm_ic_used = false;
   if (bpart && !igemm_bnout_tile_ok(a.M, Cout, (int)sizeof(IT))) return (int)hipErrorInvalidValue;
+  if (tile < -1 || tile >= (int)(sizeof(kTiles) / sizeof(kTiles[0])) || (tile >= 0 && bpart))
+    return (int)hipErrorInvalidValue;
   if (a.M == 0 || Cout == 0) return 0;
   int rc;
-  switch (pick_tile(a.M, Cout)) {
+  switch (tile >= 0 ? tile : pick_tile(a.M, Cout)) {
     case 0: rc = launch_igemm<128, 128, 64, 64, OT, IT, WB>(a, ks, splits, stream); break;
     case 1: rc = launch_igemm<64, 128, 32, 64, OT, IT, WB>(a, ks, splits, stream); break;
     case 2: rc = launch_igemm<128, 64, 64, 32, OT, IT, WB>(a, ks, splits, stream); break;

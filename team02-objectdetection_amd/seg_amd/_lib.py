@@ -118,7 +118,8 @@ PROTOTYPES = {
     "seg_mbconv_ok": (_I, [_I, _I, _I, _I, _I]),
     "seg_conv_igemm_tiles": (_I, [_L, _I]),
     "seg_conv_igemm_act_ic": (_I, [_V, _L, _I, _I, _I, _I, _V, _I, _V, _V, _L, _I, _I, _I, _I, _I, _I, _V, _L, _I,
-                                   _V, _I, _V, _V]),
+                                   _V, _I, _I, _V, _V]),
+    "seg_conv_igemm_plan_b1": (_I, [_L, _I, _I, _I, _V]),
     "seg_mbconv_work_floats": (_L, [_I, _I, _I, _I, _I, _I, _V]),
     "seg_mbconv_f16": (_I, [_V, _L, _I, _I, _I, _I, _V, _V, _I, _V, _V, _I, _V, _V, _I, _V, _L, _V, _L, _V, _V,
                             _V]),

@@ -359,23 +359,25 @@ class ConvOp:
         r = self.res
         bias = self.fb.data_ptr() if self.fb is not None else None
         M = o.N * o.H * o.W
-        splits = query("seg_conv_igemm_splits", M, self.cout, self.cin_pad, self.ks)
-        if splits > 1:
-            # split-K combined inside the launch (seg_conv_igemm_*_ic); workspace and tile counters persistent
-            # across graph replays (allocated by the warm-up launch, before any capture)
-            bufs = rt._mb.get(("ic", id(self)))
-            if bufs is None:
-                bufs = rt._mb[("ic", id(self))] = (
-                    torch.empty(splits * M * self.cout, device=rt.device, dtype=torch.float32),
-                    torch.zeros(2 * query("seg_conv_igemm_tiles", M, self.cout), device=rt.device, dtype=torch.int32))
-            rt.call(_FOLDED_CONV[rt.prog.math] + "_ic", rt.ptr(i), i.ld, i.N, i.H, i.W, self.cin_pad, wk, ldk, bias,
-                    rt.ptr(o), o.ld, o.H, o.W, self.cout, self.ks, self.stride, self.pad,
-                    rt.ptr(r) if r is not None else None, r.ld if r is not None else 0, act, bufs[0].data_ptr(), splits,
-                    bufs[1].data_ptr(), s)
-            return
-        rt.call(_FOLDED_CONV[rt.prog.math], rt.ptr(i), i.ld, i.N, i.H, i.W, self.cin_pad, wk, ldk, bias, rt.ptr(o), o.ld,
-             o.H, o.W, self.cout, self.ks, self.stride, self.pad, rt.ptr(r) if r is not None else None,
-             r.ld if r is not None else 0, None, act, None, 1, s)
+        # (splits, tile, output tiles) of seg_conv_igemm_plan_b1; split-K combined inside the launch
+        # (seg_conv_igemm_*_ic); workspace and tile counters persistent across graph replays (allocated by the
+        # warm-up launch, before any capture)
+        bufs = rt._mb.get(("ic", id(self)))
+        if bufs is None:
+            plan = (ctypes.c_int * 3)()
+            query("seg_conv_igemm_plan_b1", M, self.cout, self.cin_pad, self.ks, ctypes.addressof(plan))
+            splits, tile, ntl = plan
+            if not PLAN_B1:  # the cost model's tile and split count
+                splits, tile = query("seg_conv_igemm_splits", M, self.cout, self.cin_pad, self.ks), -1
+                ntl = query("seg_conv_igemm_tiles", M, self.cout)
+            bufs = rt._mb[("ic", id(self))] = (
+                torch.empty(splits * M * self.cout if splits > 1 else 1, device=rt.device, dtype=torch.float32),
+                torch.zeros(2 * ntl, device=rt.device, dtype=torch.int32), splits, tile)
+        work, cnt, splits, tile = bufs
+        rt.call(_FOLDED_CONV[rt.prog.math] + "_ic", rt.ptr(i), i.ld, i.N, i.H, i.W, self.cin_pad, wk, ldk, bias,
+                rt.ptr(o), o.ld, o.H, o.W, self.cout, self.ks, self.stride, self.pad,
+                rt.ptr(r) if r is not None else None, r.ld if r is not None else 0, act, work.data_ptr(), splits, tile,
+                cnt.data_ptr(), s)
 
     def _in_xform(self, rt):
         """(scale, shift, act) of the producer's lazy BN for this op's input loads, or (None, None, 0)."""
@@ -1464,6 +1466,9 @@ HALO2 = os.environ.get("SEG_HALO2", "0") == "1"  # default off: step A/B -0.7 % 
 WGRAD2 = os.environ.get("SEG_WGRAD2", "1") == "1"
 # fp16 inference (Predictor, BASELINE configs[3]): each inverted residual of the folded forward as one fused
 # launch (seg_mbconv_f16); SEG_MBCONV=0 = one launch per conv
+# the folded inference forward's convs on seg_conv_igemm_plan_b1's tile / split count (batch-1 frames: the
+# decoder convs); SEG_PLAN_B1=0 = the training cost model's (seg_conv_igemm_splits, seg_conv_igemm_tiles)
+PLAN_B1 = os.environ.get("SEG_PLAN_B1", "1") == "1"
 MBCONV = os.environ.get("SEG_MBCONV", "1") == "1"
 # BatchNorm-backward reduction from the epilogue of the implicit-GEMM data gradient that completes a BN layer's dA
 # (seg_conv_igemm_bnout*: no reduction pass over dA; the finalize reads the tile partials); SEG_BNOUT=0 = off.  Up to

@@ -65,6 +65,12 @@ def test_host_side_queries(lib):
     # split-K only when the output tiles cannot fill the chip
     assert _lib.query("seg_conv_igemm_splits", 32 * 128 * 256, 32, 80, 3) == 1
     assert _lib.query("seg_conv_igemm_splits", 8 * 16, 256, 1344, 3) > 1
+    import ctypes
+    plan = (ctypes.c_int * 3)()
+    for args, want in (((32 * 128 * 256, 32, 80, 3), (1, -1)), ((8 * 16, 256, 1344, 3), (32, 12)),
+                       ((64 * 128, 32, 32, 3), (1, 3)), ((4 * 8, 1280, 320, 1), (1, 3))):
+        assert _lib.query("seg_conv_igemm_plan_b1", *args, ctypes.addressof(plan)) == 0
+        assert tuple(plan[:2]) == want, (args, list(plan))
 
 
 def test_argument_validation_without_gpu(lib):

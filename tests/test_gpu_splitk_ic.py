@@ -1,7 +1,10 @@
 """GPU: seg_conv_igemm_{act,bf16,f16}_ic -- the implicit GEMM's split-K with the combine inside the
 launch (the batch-1 convs of the folded inference forward, inference.py:162-163 through
 src/unet.py:58-64,113-116): bitwise the two-launch split-K (same fixed-order sum and epilogue),
-repeat launches equal, tile counters re-armed."""
+repeat launches equal, tile counters re-armed; the batch-1 plan's tiles (seg_conv_igemm_plan_b1) give
+the two-launch result at the same split count."""
+import ctypes
+
 import pytest
 import torch
 
@@ -45,8 +48,47 @@ def test_splitk_in_launch_equals_two_launch(name, N, H, W, Cin, Cout, ks, act, a
         o = torch.full((M, Cout), float("nan"), device=DEV)
         call(name + "_ic", x.data_ptr(), Cin, N, H, W, Cin, w.data_ptr(), ldk, b.data_ptr(), o.data_ptr(), Cout, H, W,
              Cout, ks, 1, ks // 2, add.data_ptr() if addend else None, Cout if addend else 0, act, work2.data_ptr(),
-             splits, cnt.data_ptr(), S())
+             splits, -1, cnt.data_ptr(), S())
         outs.append(o)
     torch.cuda.synchronize()
     assert torch.equal(outs[0], ref) and torch.equal(outs[1], ref)
+    assert int(cnt.abs().sum()) == 0
+
+
+B1 = [  # the folded inference forward's decoder convs of a 128x256 frame (tools/icbench.py) + a 1x1 head conv
+    (8, 16, 1344, 256, 3), (8, 16, 256, 256, 3), (16, 32, 288, 128, 3), (16, 32, 128, 128, 3), (32, 64, 152, 64, 3),
+    (32, 64, 64, 64, 3), (64, 128, 80, 32, 3), (64, 128, 32, 32, 3), (4, 8, 320, 1280, 1), (5, 7, 64, 100, 3)]
+
+
+def plan_b1(M, Cout, Cin, ks):
+    out = (ctypes.c_int * 3)()
+    assert query("seg_conv_igemm_plan_b1", M, Cout, Cin, ks, ctypes.addressof(out)) == 0
+    return list(out)
+
+
+@pytest.mark.parametrize("name", ["seg_conv_igemm_act", "seg_conv_igemm_f16"])
+@pytest.mark.parametrize("H,W,Cin,Cout,ks", B1)
+def test_plan_b1_equals_cost_model_tile(name, H, W, Cin, Cout, ks):
+    """The plan's tile (8-wave 128x64 / 64x64) against the cost model's tile at the plan's split count:
+    bitwise (tile choice keeps every output's K order); counters re-armed."""
+    M = H * W
+    splits, tile, ntl = plan_b1(M, Cout, Cin, ks)
+    assert tile in (-1, 3, 12) and splits >= 1 and ntl >= 1
+    g = torch.Generator().manual_seed(M + Cout)
+    x = torch.randn(M, Cin, generator=g).to(DEV)
+    ldk = ks * ks * Cin
+    w = (torch.randn(Cout, ldk, generator=g) * 0.05).to(DEV)
+    b = torch.randn(Cout, generator=g).to(DEV)
+    work = torch.empty(max(splits * M * Cout, 1), device=DEV)
+    ref = torch.empty(M, Cout, device=DEV)
+    call(name, x.data_ptr(), Cin, 1, H, W, Cin, w.data_ptr(), ldk, b.data_ptr(), ref.data_ptr(), Cout, H, W, Cout, ks,
+         1, ks // 2, None, 0, None, 1, work.data_ptr() if splits > 1 else None, splits, S())
+    cnt = torch.zeros(2 * ntl, device=DEV, dtype=torch.int32)
+    work2 = torch.full_like(work, float("nan"))
+    for _ in range(2):
+        o = torch.full((M, Cout), float("nan"), device=DEV)
+        call(name + "_ic", x.data_ptr(), Cin, 1, H, W, Cin, w.data_ptr(), ldk, b.data_ptr(), o.data_ptr(), Cout, H, W,
+             Cout, ks, 1, ks // 2, None, 0, 1, work2.data_ptr(), splits, tile, cnt.data_ptr(), S())
+        torch.cuda.synchronize()
+        assert torch.equal(o, ref)
     assert int(cnt.abs().sum()) == 0

@@ -13,6 +13,9 @@ from seg_amd._lib import call, query  # noqa: E402
 
 SHAPES = [(1048576, 96), (1048576, 32), (1048576, 16), (262144, 144), (262144, 24), (65536, 192), (16384, 384),
           (16384, 576), (4096, 1280)]
+if os.environ.get("BNB_SHAPES") == "unet":  # UNet(10) at 8x512x1024 (configs[4])
+    SHAPES = [(4194304, 64), (1048576, 64), (1048576, 128), (262144, 128), (262144, 256), (65536, 256),
+              (65536, 512)]
 
 
 def timeit(fn, reps=30):

@@ -657,6 +657,16 @@ int seg_dw2_wgrad_bn_bf16io(const seg_bf16* dy, long lddy, const seg_bf16* x, lo
  * seg_conv_igemm_f16), fp32 depthwise (as seg_dw_fwd_bias_act).  seg_mbconv_ok: stride 1 / 2,
  * Cin <= 160 with an expand, Cout <= 320, channels % 4; res only at stride 1.  work / cnt:
  * seg_mbconv_work_floats floats and *counters unsigned (zero before the first launch; re-armed). */
+/* The folded fp16 forward's segmentation head, outconv (src/unet.py:108-121: 1x1 -> BN -> ReLU -> 1x1, BN
+ * folded), in one launch: out[M][ldo] = w2[C2][C1] . f16(act1(w1[C1][Cin] . f16(x) + b1)) + b2 -- fp16
+ * operands and fp32 accumulation as seg_conv_igemm_f16 (another sum order).  seg_pw2_ok: (Cin, C1) = (32, 16),
+ * C2 <= 64.  b1 / b2 may be NULL; x rows 16-byte aligned (ldx % 4 == 0). */
+int seg_pw2_ok(int Cin, int C1, int C2);
+int seg_pw2_f16(const float* x, long ldx, long M, int Cin, const float* w1, const float* b1, int C1, int act1,
+                const float* w2, const float* b2, int C2, float* out, long ldo, hipStream_t stream);
+/* Tuning hook: the blocks per launch seg_mbconv_f16's hidden splits aim for (> 0 sets it; returns the
+ * previous value). */
+int seg_mbconv_tune(int max_blocks);
 int seg_mbconv_ok(int Cin, int Ch, int Cout, int stride, int expand);
 long seg_mbconv_work_floats(int N, int H, int W, int Ch, int Cout, int stride, int* counters);
 int seg_mbconv_f16(const float* x, long ldx, int N, int H, int W, int Cin, const float* we, const float* be, int Ch,

@@ -99,7 +99,7 @@ SEG_API int seg_conv_igemm_tiles(long M, int Cout) {
 // where the cost model's tiles fill the chip, its own choice (1 split, tile -1).  Below that (batch-1 frames)
 // per-launch timings of the decoder convs of a 128x256 frame (tools/icbench.py, profiles/r04ic_icbench.txt)
 // set the rule: short K (<= 24 chunks) unsplit on the 64x64 tile (more blocks; a split's combine costs more
-// than its chunks), longer K on the 8-wave 128x64 tile split to ~256 blocks with >= 2 chunks per split
+// than its chunks), longer K on the 8-wave 128x64 tile split to ~256 blocks with >= 4 chunks per split
 // (at most 32 splits).
 SEG_API int seg_conv_igemm_plan_b1(long M, int Cout, int Cin, int ks, int* out) {
   if (!out) return (int)hipErrorInvalidValue;
@@ -115,7 +115,7 @@ SEG_API int seg_conv_igemm_plan_b1(long M, int Cout, int Cin, int ks, int* out) 
       } else {
         tile = 12;
         const long b12 = ((M + 127) / 128) * ((Cout + 63) / 64);
-        long s = std::min<long>(std::min<long>(32, (256 + b12 - 1) / b12), nk / 2);
+        long s = std::min<long>(std::min<long>(32, (256 + b12 - 1) / b12), nk / 4);
         s = std::max<long>(s, 1);
         splits = seg_cdiv(nk, seg_cdiv(nk, (int)s));  // no empty split
       }

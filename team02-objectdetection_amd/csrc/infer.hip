@@ -27,6 +27,10 @@
 // restates the same arithmetic; tests pin kernel == restatement bit-exactly).
 #include "common.h"
 
+#ifndef SEG_ARGMAX_BAND
+#define SEG_ARGMAX_BAND 1
+#endif
+
 namespace {
 
 // ---------------------------------------------------------------- BN folding
@@ -118,8 +122,42 @@ __global__ __launch_bounds__(256) void preprocess_bgr_kernel(const uint8_t* __re
 }
 
 // ---------------------------------------------------------------- argmax + nearest
-// mask[n][yf][xf] = argmax_c logits(n, c, ym, xm), (ym, xm) = nearest model pixel of
-// frame pixel (yf, xf); logits = align_corners=True bilinear of the low-res logits.
+// Class of model pixel (ym, xm): argmax_c of the align_corners=True bilinear of the low-res logits
+// (aten max(dim) on CPU: the first maximum wins, a NaN wins and stops the scan).
+__device__ __forceinline__ int model_class(const float* __restrict__ base, long ld, int H, int W, int C, int ym,
+                                           int xm, float sh, float sw) {
+  const Lin lh = lin_index(ym, H, sh, 1), lw = lin_index(xm, W, sw, 1);
+  float best = 0.f;
+  int arg = 0;
+  bool done = false;
+  for (int c = 0; c < C && !done; c += 4) {
+    const f32x4 v00 = ld4(base + ((long)lh.i0 * W + lw.i0) * ld + c);
+    const f32x4 v01 = ld4(base + ((long)lh.i0 * W + lw.i1) * ld + c);
+    const f32x4 v10 = ld4(base + ((long)lh.i1 * W + lw.i0) * ld + c);
+    const f32x4 v11 = ld4(base + ((long)lh.i1 * W + lw.i1) * ld + c);
+    const f32x4 o = bilerp4(v00, v01, v10, v11, lh, lw);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int k = c + j;
+      if (k >= C || done) continue;
+      const float v = o[j];
+      if (k == 0 || !(v <= best)) {
+        best = v;
+        arg = k;
+        if (isnan(v)) done = true;
+      }
+    }
+  }
+  return arg;
+}
+
+__device__ __forceinline__ int nearest_src(int d, double inv, int m) {
+  const int s = (int)floor((double)d * inv);
+  return s < m - 1 ? s : m - 1;
+}
+
+// mask[n][yf][xf] = class of the nearest model pixel (ym, xm) of frame pixel (yf, xf), one thread per
+// frame pixel (any shape).
 __global__ __launch_bounds__(256) void argmax_nearest_kernel(const float* __restrict__ low, long ld, int N, int H,
                                                              int W, int C, int Hm, int Wm, float sh, float sw,
                                                              uint8_t* __restrict__ mask, int Hf, int Wf,
@@ -129,34 +167,54 @@ __global__ __launch_bounds__(256) void argmax_nearest_kernel(const float* __rest
     const int n = (int)(p / ((long)Hf * Wf));
     const int rem = (int)(p - (long)n * Hf * Wf);
     const int yf = rem / Wf, xf = rem - yf * Wf;
-    int ym = (int)floor((double)yf * ify), xm = (int)floor((double)xf * ifx);
-    ym = ym < Hm - 1 ? ym : Hm - 1;
-    xm = xm < Wm - 1 ? xm : Wm - 1;
-    const Lin lh = lin_index(ym, H, sh, 1), lw = lin_index(xm, W, sw, 1);
-    const float* base = low + (long)n * H * W * ld;
-    float best = 0.f;
-    int arg = 0;
-    bool done = false;
-    for (int c = 0; c < C && !done; c += 4) {
-      const f32x4 v00 = ld4(base + ((long)lh.i0 * W + lw.i0) * ld + c);
-      const f32x4 v01 = ld4(base + ((long)lh.i0 * W + lw.i1) * ld + c);
-      const f32x4 v10 = ld4(base + ((long)lh.i1 * W + lw.i0) * ld + c);
-      const f32x4 v11 = ld4(base + ((long)lh.i1 * W + lw.i1) * ld + c);
-      const f32x4 o = bilerp4(v00, v01, v10, v11, lh, lw);
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int k = c + j;
-        if (k >= C || done) continue;
-        const float v = o[j];
-        // aten max(dim) on CPU: first maximum wins, a NaN wins and stops the scan
-        if (k == 0 || !(v <= best)) {
-          best = v;
-          arg = k;
-          if (isnan(v)) done = true;
-        }
+    mask[p] = (uint8_t)model_class(low + (long)n * H * W * ld, ld, H, W, C, nearest_src(yf, ify, Hm),
+                                   nearest_src(xf, ifx, Wm), sh, sw);
+  }
+}
+
+// The same mask by bands of kBandRows frame rows per block: the block classifies the model rows its band
+// maps to once (a frame 5.6x taller than the model repeats each model row ~6 times, and each model pixel
+// ~28 times over a 720x1280 frame), keeps the classes in LDS and writes the band's frame rows from them,
+// four pixels per 32-bit store.  Bitwise the per-pixel kernel (the same model_class per model pixel).
+constexpr int kBandRows = 4;
+constexpr int kBandMaxWm = 2048;
+__global__ __launch_bounds__(256) void argmax_band_kernel(const float* __restrict__ low, long ld, int N, int H, int W,
+                                                          int C, int Hm, int Wm, float sh, float sw,
+                                                          uint8_t* __restrict__ mask, int Hf, int Wf, double ify,
+                                                          double ifx) {
+  __shared__ uint8_t lab[kBandRows][kBandMaxWm];
+  __shared__ int slot_of[kBandRows], ym_of[kBandRows], nslots;
+  const int bands = (Hf + kBandRows - 1) / kBandRows;
+  const int n = blockIdx.x / bands, y0 = (blockIdx.x - n * bands) * kBandRows;
+  const int rows = min(kBandRows, Hf - y0);
+  if (threadIdx.x == 0) {  // distinct model rows of the band (nearest_src is monotone in yf)
+    int ns = 0, prev = -1;
+    for (int r = 0; r < rows; ++r) {
+      const int ym = nearest_src(y0 + r, ify, Hm);
+      if (ym != prev) {
+        ym_of[ns++] = ym;
+        prev = ym;
       }
+      slot_of[r] = ns - 1;
     }
-    mask[p] = (uint8_t)arg;
+    nslots = ns;
+  }
+  __syncthreads();
+  const float* base = low + (long)n * H * W * ld;
+  for (int e = threadIdx.x; e < nslots * Wm; e += 256) {
+    const int sl = e / Wm, xm = e - sl * Wm;
+    lab[sl][xm] = (uint8_t)model_class(base, ld, H, W, C, ym_of[sl], xm, sh, sw);
+  }
+  __syncthreads();
+  uint8_t* out = mask + ((long)n * Hf + y0) * Wf;
+  const int q = Wf >> 2;  // Wf % 4 == 0 (host check): 32-bit stores
+  for (int e = threadIdx.x; e < rows * q; e += 256) {
+    const int r = e / q, x = (e - r * q) * 4;
+    const uint8_t* lr = lab[slot_of[r]];
+    const unsigned v = (unsigned)lr[nearest_src(x, ifx, Wm)] | ((unsigned)lr[nearest_src(x + 1, ifx, Wm)] << 8) |
+                       ((unsigned)lr[nearest_src(x + 2, ifx, Wm)] << 16) |
+                       ((unsigned)lr[nearest_src(x + 3, ifx, Wm)] << 24);
+    *reinterpret_cast<unsigned*>(out + (long)r * Wf + x) = v;
   }
 }
 
@@ -199,7 +257,11 @@ SEG_API int seg_argmax_nearest(const float* low, long ld, int N, int H, int W, i
   const float sh = Hm > 1 ? (float)(H - 1) / (float)(Hm - 1) : 0.f;
   const float sw = Wm > 1 ? (float)(W - 1) / (float)(Wm - 1) : 0.f;
   const double ify = 1.0 / ((double)Hf / Hm), ifx = 1.0 / ((double)Wf / Wm);
-  hipLaunchKernelGGL(argmax_nearest_kernel, dim3(grid_for((long)N * Hf * Wf)), dim3(256), 0, stream, low, ld, N, H, W,
-                     C, Hm, Wm, sh, sw, mask, Hf, Wf, ify, ifx);
+  if (SEG_ARGMAX_BAND && Wm <= kBandMaxWm && Wf % 4 == 0 && ((uintptr_t)mask & 3) == 0)
+    hipLaunchKernelGGL(argmax_band_kernel, dim3(N * seg_cdiv(Hf, kBandRows)), dim3(256), 0, stream, low, ld, N, H, W,
+                       C, Hm, Wm, sh, sw, mask, Hf, Wf, ify, ifx);
+  else
+    hipLaunchKernelGGL(argmax_nearest_kernel, dim3(grid_for((long)N * Hf * Wf)), dim3(256), 0, stream, low, ld, N, H,
+                       W, C, Hm, Wm, sh, sw, mask, Hf, Wf, ify, ifx);
   SEG_RET_LAST();
 }

@@ -22,6 +22,10 @@
 // Without an expand conv (features[1], expand ratio 1) the input tile itself is the hidden tile.
 #include "common.h"
 
+#ifndef SEG_MBCONV_CAP
+#define SEG_MBCONV_CAP 256
+#endif
+
 namespace {
 
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
@@ -318,6 +322,8 @@ __global__ __launch_bounds__(kThreads) void mbconv_f16_kernel(MbArgs a) {
   }
 }
 
+int g_mb_cap = SEG_MBCONV_CAP;  // blocks per launch the hidden splits aim for (seg_mbconv_tune)
+
 void mb_plan(int N, int H, int W, int Ch, int stride, int* tiles_w, int* tiles_h, int* splits, int* hper, int* tp) {
   const int toh = stride == 1 ? 4 : 2, tow = 8;
   const int Ho = (H - 1) / stride + 1, Wo = (W - 1) / stride + 1;
@@ -326,14 +332,21 @@ void mb_plan(int N, int H, int W, int Ch, int stride, int* tiles_w, int* tiles_h
   *tp = toh * tow;
   const int ntiles = N * *tiles_w * *tiles_h;
   const int chunks = (Ch + HC - 1) / HC;
-  // hidden splits: up to 256 blocks in all (one per CU: co-resident, so every block of a tile helps combine it)
-  int s = std::max(1, std::min(chunks, 256 / std::max(1, ntiles)));
+  // hidden splits: up to g_mb_cap blocks in all (co-resident, so every block of a tile helps combine it)
+  int s = std::max(1, std::min(chunks, g_mb_cap / std::max(1, ntiles)));
   const int per = (chunks + s - 1) / s;
   *splits = (chunks + per - 1) / per;
   *hper = per * HC;
 }
 
 }  // namespace
+
+// Tuning hook: the blocks per launch the hidden splits aim for (> 0; returns the previous value).
+SEG_API int seg_mbconv_tune(int max_blocks) {
+  const int old = g_mb_cap;
+  if (max_blocks > 0) g_mb_cap = max_blocks;
+  return old;
+}
 
 // 1 when seg_mbconv_f16 takes the block: stride 1 or 2, Cin <= 160 (with an expand conv), Cout <= 320,
 // channel counts multiples of 4.
@@ -373,9 +386,18 @@ SEG_API int seg_mbconv_f16(const float* x, long ldx, int N, int H, int W, int Ci
   a.ntiles = N * a.tiles_w * a.tiles_h;
   a.work = work; a.cnt = cnt;
   if (a.splits > 1 && (!work || !cnt)) return (int)hipErrorInvalidValue;
-  a.spin = (long)a.ntiles * a.splits <= seg_num_cus();  // one block per CU at most: all co-resident
   const dim3 grid(a.ntiles, a.splits);
   const bool e = we != nullptr;
+  {  // spin combine only when the whole grid is co-resident
+    const void* fn = stride == 1 ? (e ? (const void*)mbconv_f16_kernel<1, true> : (const void*)mbconv_f16_kernel<1, false>)
+                                 : (e ? (const void*)mbconv_f16_kernel<2, true> : (const void*)mbconv_f16_kernel<2, false>);
+    int occ = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, fn, kThreads, 0) != hipSuccess) {
+      (void)hipGetLastError();
+      occ = 1;
+    }
+    a.spin = (long)a.ntiles * a.splits <= (long)std::max(occ, 1) * seg_num_cus();
+  }
   if (stride == 1) {
     if (e) hipLaunchKernelGGL((mbconv_f16_kernel<1, true>), grid, dim3(kThreads), 0, stream, a);
     else hipLaunchKernelGGL((mbconv_f16_kernel<1, false>), grid, dim3(kThreads), 0, stream, a);
@@ -383,5 +405,68 @@ SEG_API int seg_mbconv_f16(const float* x, long ldx, int N, int H, int W, int Ci
     if (e) hipLaunchKernelGGL((mbconv_f16_kernel<2, true>), grid, dim3(kThreads), 0, stream, a);
     else hipLaunchKernelGGL((mbconv_f16_kernel<2, false>), grid, dim3(kThreads), 0, stream, a);
   }
+  SEG_RET_LAST();
+}
+
+// ---------------------------------------------------------------- the segmentation head
+// outconv of the folded fp16 forward (src/unet.py:108-121: 1x1 -> BN -> ReLU -> 1x1, the BN folded) in one
+// launch: out = w2 . f16(act(w1 . f16(x) + b1)) + b2, one pixel per thread, fp16-rounded operands and fp32
+// accumulation as seg_conv_igemm_f16 stages them (the sum order differs: within fp32 rounding of the two
+// launches).  Weights rounded once into LDS, read as wave-uniform broadcasts.
+namespace {
+template <int CIN, int C1>
+__global__ __launch_bounds__(256) void pw2_f16_kernel(const float* __restrict__ x, long ldx, long M,
+                                                      const float* __restrict__ w1, const float* __restrict__ b1,
+                                                      int act1, const float* __restrict__ w2,
+                                                      const float* __restrict__ b2, int C2, float* __restrict__ out,
+                                                      long ldo) {
+  __shared__ __attribute__((aligned(16))) float W1s[C1 * CIN];
+  __shared__ __attribute__((aligned(16))) float W2s[64 * C1];
+  __shared__ float B1s[C1], B2s[64];
+  for (int i = threadIdx.x; i < C1 * CIN; i += 256) W1s[i] = (float)(_Float16)w1[i];
+  for (int i = threadIdx.x; i < C2 * C1; i += 256) W2s[i] = (float)(_Float16)w2[i];
+  for (int i = threadIdx.x; i < C1; i += 256) B1s[i] = b1 ? b1[i] : 0.f;
+  for (int i = threadIdx.x; i < C2; i += 256) B2s[i] = b2 ? b2[i] : 0.f;
+  __syncthreads();
+  const long p = blockIdx.x * 256L + threadIdx.x;
+  if (p >= M) return;
+  float xv[CIN];
+#pragma unroll
+  for (int k = 0; k < CIN; k += 4) {
+    const f32x4 v = ld4(x + p * ldx + k);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) xv[k + j] = (float)(_Float16)v[j];
+  }
+  float h[C1];
+#pragma unroll
+  for (int c = 0; c < C1; ++c) {
+    float acc = 0.f;
+#pragma unroll
+    for (int k = 0; k < CIN; ++k) acc = fmaf(xv[k], W1s[c * CIN + k], acc);
+    h[c] = (float)(_Float16)seg_act(acc + B1s[c], act1);
+  }
+  for (int c2 = 0; c2 < C2; ++c2) {
+    float acc = 0.f;
+#pragma unroll
+    for (int c = 0; c < C1; ++c) acc = fmaf(h[c], W2s[c2 * C1 + c], acc);
+    out[p * ldo + c2] = acc + B2s[c2];
+  }
+}
+}  // namespace
+
+// 1 when seg_pw2_f16 takes the head: (Cin, C1) = (32, 16) (MobileNetV2UNet's outconv(32, n)), C2 <= 64.
+SEG_API int seg_pw2_ok(int Cin, int C1, int C2) { return Cin == 32 && C1 == 16 && C2 > 0 && C2 <= 64 ? 1 : 0; }
+
+// out[M][ldo] = w2 [C2][C1] . f16(act1(w1 [C1][Cin] . f16(x) + b1)) + b2 (b1 / b2 may be NULL); x rows in
+// 16-byte vectors (ldx % 4 == 0, 16-byte aligned).
+SEG_API int seg_pw2_f16(const float* x, long ldx, long M, int Cin, const float* w1, const float* b1, int C1,
+                        int act1, const float* w2, const float* b2, int C2, float* out, long ldo,
+                        hipStream_t stream) {
+  if (!seg_pw2_ok(Cin, C1, C2) || !x || !w1 || !w2 || !out || (ldx & 3) || ((uintptr_t)x & 15) || ldo < C2 ||
+      act1 < SEG_ACT_NONE || act1 > SEG_ACT_RELU6 || M < 0)
+    return (int)hipErrorInvalidValue;
+  if (M == 0) return 0;
+  hipLaunchKernelGGL((pw2_f16_kernel<32, 16>), dim3(seg_cdiv(M, 256)), dim3(256), 0, stream, x, ldx, M, w1, b1, act1,
+                     w2, b2, C2, out, ldo);
   SEG_RET_LAST();
 }

@@ -721,6 +721,22 @@ class Program:
         self._mb_groups = m
         return m
 
+    def pw2_head(self):
+        """Folded forward: index of outconv's first 1x1 conv when seg_pw2_f16 runs the head (1x1 -> folded BN ->
+        ReLU -> 1x1, the program's last two ops, the hidden activation consumed only by the last conv), else
+        None."""
+        ops = self.ops
+        if len(ops) < 2:
+            return None
+        c1, c2 = ops[-2], ops[-1]
+        pw = (lambda op: isinstance(op, ConvOp) and op.kind == "igemm" and op.ks == 1 and op.stride == 1
+              and op.fk_pack is None and op.res is None and op.cin_pad == op.cin)
+        if not (pw(c1) and pw(c2) and c2.inp is c1.out and c1.bn is not None and c2.bn is None
+                and c1.act in (ACT_RELU, ACT_RELU6) and c1.inp.ld % 4 == 0
+                and query("seg_pw2_ok", c1.cin, c1.cout, c2.cout)):
+            return None
+        return len(ops) - 2
+
     def bn_owner(self):
         """Activation key -> the ConvOp with a BatchNorm whose output it is (the BN-backward reduction target of a
         data gradient writing exactly that region; ConvOp._bnout)."""
@@ -1397,13 +1413,23 @@ class Run:
         launch per conv, or per inverted residual with fp16 conv math (seg_mbconv_f16).  The
         NHWC4 input rows must already be in the image buffer."""
         ops = self.prog.ops
-        groups = self.prog.mbconv_groups() if MBCONV and self.prog.math == "f16" else {}
+        f16 = self.prog.math == "f16"
+        groups = self.prog.mbconv_groups() if MBCONV and f16 else {}
+        head = self.prog.pw2_head() if PW2 and f16 else None
         k = 0
         while k < len(ops):
             g = groups.get(k)
             if g is not None:
                 self._mbconv(k, g)
                 k += len(g)
+                continue
+            if k == head:
+                c1, c2 = ops[k], ops[k + 1]
+                x, o = c1.inp, c2.out
+                call("seg_pw2_f16", self.ptr(x), x.ld, x.N * x.H * x.W, c1.cin, c1.fk.data_ptr(),
+                     c1.fb.data_ptr() if c1.fb is not None else None, c1.cout, c1.act, c2.fk.data_ptr(),
+                     c2.fb.data_ptr() if c2.fb is not None else None, c2.cout, self.ptr(o), o.ld, self.stream)
+                k += 2
                 continue
             op = ops[k]
             if isinstance(op, ConvOp):
@@ -1469,6 +1495,8 @@ WGRAD2 = os.environ.get("SEG_WGRAD2", "1") == "1"
 # the folded inference forward's convs on seg_conv_igemm_plan_b1's tile / split count (batch-1 frames: the
 # decoder convs); SEG_PLAN_B1=0 = the training cost model's (seg_conv_igemm_splits, seg_conv_igemm_tiles)
 PLAN_B1 = os.environ.get("SEG_PLAN_B1", "1") == "1"
+# the folded fp16 forward's outconv head (1x1 -> BN -> ReLU -> 1x1) in one launch (seg_pw2_f16); SEG_PW2=0 = two
+PW2 = os.environ.get("SEG_PW2", "1") == "1"
 MBCONV = os.environ.get("SEG_MBCONV", "1") == "1"
 # BatchNorm-backward reduction from the epilogue of the implicit-GEMM data gradient that completes a BN layer's dA
 # (seg_conv_igemm_bnout*: no reduction pass over dA; the finalize reads the tile partials); SEG_BNOUT=0 = off.  Up to

@@ -56,10 +56,13 @@ def _oracle_logits(model, f, size):
         return segref.FORWARDS[arch](p, torch.from_numpy(x).double(), False).numpy()
 
 
-@pytest.mark.parametrize("arch", ["MobileNetV2UNet", "UNet"])
-def test_predictor_matches_oracle(arch):
+@pytest.mark.parametrize("arch,fhw", [("MobileNetV2UNet", (720, 1280)), ("UNet", (90, 160)), ("UNet", (61, 166)),
+                                      ("UNet", (22, 40))])
+def test_predictor_matches_oracle(arch, fhw):
+    """(frame widths % 4 == 0: the banded argmax kernel, a frame smaller than the model included; 166: the
+    per-pixel one)"""
     size = (256, 128) if arch == "MobileNetV2UNet" else (64, 32)
-    fh, fw = (720, 1280) if arch == "MobileNetV2UNet" else (90, 160)
+    fh, fw = fhw
     cpu = MobileNetV2UNet(10) if arch == "MobileNetV2UNet" else UNet(10, 16)
     deterministic_init(cpu, seed=11, random_running_stats=True)
     model = (MobileNetV2UNet(10) if arch == "MobileNetV2UNet" else UNet(10, 16)).to(DEV)

@@ -7,7 +7,8 @@ src/unet.py:15-19).
     last-arrival combine) and one split, ragged tiles, every MobileNetV2 block shape at a
     128x256 frame;
   * repeat launches bitwise equal (fixed-order combine; counters re-armed);
-  * the fp16 Predictor with the fused blocks agrees with the one-launch-per-conv folded forward
+  * seg_pw2_f16 (the outconv head) against float64 of the same operand rounding;
+  * the fp16 Predictor with the fused blocks and head agrees with the one-launch-per-conv folded forward
     (SEG_MBCONV off) within fp16 operand-rounding noise, and its graph replay equals eager.
 """
 import ctypes
@@ -110,22 +111,23 @@ def test_predictor_fused_equals_unfused():
     import numpy as np
     model = deterministic_init(MobileNetV2UNet(10), seed=13, random_running_stats=True).to(DEV).eval()
     f = (np.random.default_rng(0).random((720, 1280, 3)) * 255).astype(np.uint8)
-    saved = engine.MBCONV
+    saved = engine.MBCONV, engine.PW2
     try:
-        engine.MBCONV = False
+        engine.MBCONV = engine.PW2 = False
         p0 = Predictor(model, frame_hw=(720, 1280), graph=False, math="f16")
         p0(f)
         l0 = p0.logits()
-        engine.MBCONV = True
+        engine.MBCONV = engine.PW2 = True
         p1 = Predictor(model, frame_hw=(720, 1280), graph=True, math="f16")
         assert len(p1.prog.mbconv_groups()) == 17  # every InvertedResidual of features[1..17]
+        assert p1.prog.pw2_head() == len(p1.prog.ops) - 2  # outconv in one launch (seg_pw2_f16)
         m1 = p1(f).clone()
         l1 = p1.logits()
         p2 = Predictor(model, frame_hw=(720, 1280), graph=False, math="f16")
         m2 = p2(f).clone()
         assert torch.equal(m1, m2) and torch.equal(l1, p2.logits()), "graph replay == eager"
     finally:
-        engine.MBCONV = saved
+        engine.MBCONV, engine.PW2 = saved
     # two valid fp16 forwards: the fp32 accumulation orders differ (split hidden ranges vs split-K), and an fp32
     # value one ulp either side of an fp16 rounding boundary moves that operand by an fp16 ulp (~5e-4); the oracle
     # bound of both is tests/test_gpu_infer.py::test_predictor_low_precision
@@ -133,3 +135,22 @@ def test_predictor_fused_equals_unfused():
     assert rel < 1e-2, rel
     agree = float((l1.argmax(1) == l0.argmax(1)).float().mean())
     assert agree >= 0.995, agree
+
+
+@pytest.mark.parametrize("M,C2,act", [(8192, 10, 1), (1000, 3, 2), (255, 64, 1)])
+def test_pw2_head_vs_fp64(M, C2, act):
+    g = torch.Generator().manual_seed(M + C2)
+    x = torch.randn(M, 32, generator=g)
+    w1, b1 = torch.randn(16, 32, generator=g) / 32 ** 0.5, torch.randn(16, generator=g) * 0.1
+    w2, b2 = torch.randn(C2, 16, generator=g) / 4, torch.randn(C2, generator=g) * 0.1
+    h = (h16(x) @ h16(w1).T + b1.double())
+    h = h.clamp(min=0) if act == 1 else h.clamp(0, 6)
+    ref = h.float().to(torch.float16).double() @ h16(w2).T + b2.double()
+    out = torch.full((M, C2 + 2), float("nan"), device=DEV)
+    xg, w1g, b1g, w2g, b2g = (t.to(DEV) for t in (x, w1, b1, w2, b2))  # (kept alive across the launch)
+    call("seg_pw2_f16", xg.data_ptr(), 32, M, 32, w1g.data_ptr(), b1g.data_ptr(), 16, act, w2g.data_ptr(),
+         b2g.data_ptr(), C2, out.data_ptr(), C2 + 2, S())
+    torch.cuda.synchronize()
+    got = out[:, :C2].double().cpu()
+    assert float((got - ref).norm() / ref.norm()) < 1e-4  # fp32 vs fp64 sums may move an fp16 rounding
+    assert bool(out[:, C2:].isnan().all()), "nothing written beyond C2"

@@ -664,6 +664,13 @@ int seg_dw2_wgrad_bn_bf16io(const seg_bf16* dy, long lddy, const seg_bf16* x, lo
 int seg_pw2_ok(int Cin, int C1, int C2);
 int seg_pw2_f16(const float* x, long ldx, long M, int Cin, const float* w1, const float* b1, int C1, int act1,
                 const float* w2, const float* b2, int C2, float* out, long ldo, hipStream_t stream);
+/* The preprocess (seg_preprocess_bgr, N = 1) formed on load by the folded fp16 forward's stem conv
+ * (features[0]: 3x3 stride 2 pad 1, Cin 3 padded to 4, Cout 32, BN folded): wk / ldk / bias / act as
+ * seg_conv_igemm_f16's (fp16 operands, fp32 accumulation, another sum order); out [Ho*Wo][ldo] with
+ * Ho = (H-1)/2+1, Wo = (W-1)/2+1. */
+int seg_stem_pre_f16(const unsigned char* frame, int Hf, int Wf, long row_bytes, int H, int W, float mean_r, float mean_g,
+                     float mean_b, float std_r, float std_g, float std_b, const float* wk, int ldk, const float* bias,
+                     int act, int Cout, float* out, long ldo, hipStream_t stream);
 /* Tuning hook: the blocks per launch seg_mbconv_f16's hidden splits aim for (> 0 sets it; returns the
  * previous value). */
 int seg_mbconv_tune(int max_blocks);

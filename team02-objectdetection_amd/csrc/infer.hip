@@ -73,51 +73,107 @@ __global__ __launch_bounds__(256) void fold_batch_kernel(const SegFoldJob* __res
 }
 
 // ---------------------------------------------------------------- preprocess
+// Model pixel (dy, dx) of one frame: cv2.resize INTER_LINEAR (fixed-point weights, OpenCV's rounding),
+// BGR -> RGB, ToTensor, Normalize (inference.py:28-46); channel 3 = 0.
+__device__ __forceinline__ f32x4 pre_pixel(const uint8_t* __restrict__ fr, long row_bytes, int Hf, int Wf, int dy,
+                                           int dx, double scale_x, double scale_y, float m0, float m1, float m2,
+                                           float s0, float s1, float s2) {
+#pragma clang fp contract(off)  // OpenCV computes (dx+0.5)*scale-0.5 as a separate multiply and subtract
+  // x taps and fixed-point weights
+  float fx = (float)((dx + 0.5) * scale_x - 0.5);
+  int sx = (int)floorf(fx);
+  fx -= (float)sx;
+  if (sx < 0) { sx = 0; fx = 0.f; }
+  if (sx >= Wf - 1) { sx = Wf - 1; fx = 0.f; }
+  const int a0 = (int)rintf((1.f - fx) * 2048.f), a1 = (int)rintf(fx * 2048.f);
+  const int sx1 = sx + 1 < Wf ? sx + 1 : Wf - 1;  // a1 == 0 whenever sx + 1 is outside
+  // y taps (weights from the unclamped fy; rows clipped)
+  float fy = (float)((dy + 0.5) * scale_y - 0.5);
+  const int sy = (int)floorf(fy);
+  fy -= (float)sy;
+  const int b0 = (int)rintf((1.f - fy) * 2048.f), b1 = (int)rintf(fy * 2048.f);
+  const int y0 = sy < 0 ? 0 : (sy >= Hf ? Hf - 1 : sy);
+  const int y1 = sy + 1 < 0 ? 0 : (sy + 1 >= Hf ? Hf - 1 : sy + 1);
+  const uint8_t* r0 = fr + (long)y0 * row_bytes;
+  const uint8_t* r1 = fr + (long)y1 * row_bytes;
+  float v[3];
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    const int d0 = r0[sx * 3 + c] * a0 + r0[sx1 * 3 + c] * a1;
+    const int d1 = r1[sx * 3 + c] * a0 + r1[sx1 * 3 + c] * a1;
+    int t = (((d0 >> 4) * b0) >> 16) + (((d1 >> 4) * b1) >> 16);
+    t = (t + 2) >> 2;
+    const int u = t < 0 ? 0 : (t > 255 ? 255 : t);
+    v[c] = (float)u / 255.f;  // transforms.ToTensor (float32 division)
+  }
+  // BGR -> RGB, then transforms.Normalize: (x - mean) / std
+  f32x4 o;
+  o[0] = (v[2] - m0) / s0;
+  o[1] = (v[1] - m1) / s1;
+  o[2] = (v[0] - m2) / s2;
+  o[3] = 0.f;
+  return o;
+}
+
 __global__ __launch_bounds__(256) void preprocess_bgr_kernel(const uint8_t* __restrict__ frame, long row_bytes,
                                                              long frame_bytes, int N, int Hf, int Wf,
                                                              float* __restrict__ out, int ld, int H, int W,
                                                              double scale_x, double scale_y, float m0, float m1,
                                                              float m2, float s0, float s1, float s2) {
-#pragma clang fp contract(off)  // OpenCV computes (dx+0.5)*scale-0.5 as a separate multiply and subtract
   const long total = (long)N * H * W;
   for (long p = blockIdx.x * 256L + threadIdx.x; p < total; p += (long)gridDim.x * 256) {
     const int n = (int)(p / ((long)H * W));
     const int rem = (int)(p - (long)n * H * W);
     const int dy = rem / W, dx = rem - dy * W;
-    // x taps and fixed-point weights
-    float fx = (float)((dx + 0.5) * scale_x - 0.5);
-    int sx = (int)floorf(fx);
-    fx -= (float)sx;
-    if (sx < 0) { sx = 0; fx = 0.f; }
-    if (sx >= Wf - 1) { sx = Wf - 1; fx = 0.f; }
-    const int a0 = (int)rintf((1.f - fx) * 2048.f), a1 = (int)rintf(fx * 2048.f);
-    const int sx1 = sx + 1 < Wf ? sx + 1 : Wf - 1;  // a1 == 0 whenever sx + 1 is outside
-    // y taps (weights from the unclamped fy; rows clipped)
-    float fy = (float)((dy + 0.5) * scale_y - 0.5);
-    const int sy = (int)floorf(fy);
-    fy -= (float)sy;
-    const int b0 = (int)rintf((1.f - fy) * 2048.f), b1 = (int)rintf(fy * 2048.f);
-    const int y0 = sy < 0 ? 0 : (sy >= Hf ? Hf - 1 : sy);
-    const int y1 = sy + 1 < 0 ? 0 : (sy + 1 >= Hf ? Hf - 1 : sy + 1);
-    const uint8_t* r0 = frame + n * frame_bytes + (long)y0 * row_bytes;
-    const uint8_t* r1 = frame + n * frame_bytes + (long)y1 * row_bytes;
-    float v[3];
+    st4(out + p * ld, pre_pixel(frame + n * frame_bytes, row_bytes, Hf, Wf, dy, dx, scale_x, scale_y, m0, m1, m2, s0,
+                                s1, s2));
+  }
+}
+
+// The folded forward's stem (features[0]: 3x3 stride-2 conv, BN folded, ReLU6) on the preprocessed frame
+// formed on load: one thread per stem output pixel, its 3x3 input taps preprocessed from the frame bytes,
+// fp16-rounded operands and fp32 accumulation as seg_conv_igemm_f16 stages them (the sum order differs).
+// wk: the stem's packed weight [kStemCout][ldk], K = tap * 4 + channel (channel 3 zero).
+constexpr int kStemCout = 32;
+__global__ __launch_bounds__(256) void stem_pre_f16_kernel(const uint8_t* __restrict__ frame, long row_bytes, int Hf,
+                                                           int Wf, int H, int W, double scale_x, double scale_y,
+                                                           float m0, float m1, float m2, float s0, float s1,
+                                                           float s2, const float* __restrict__ wk, int ldk,
+                                                           const float* __restrict__ bias, int act,
+                                                           float* __restrict__ out, long ldo, int Ho, int Wo) {
+  __shared__ float Wt[36][kStemCout];  // [k][co]: one wave-uniform row per k
+  __shared__ float Bs[kStemCout];
+  for (int i = threadIdx.x; i < 36 * kStemCout; i += 256) {
+    const int co = i / 36, k = i - co * 36;
+    Wt[k][co] = (float)(_Float16)wk[(long)co * ldk + k];
+  }
+  if (threadIdx.x < kStemCout) Bs[threadIdx.x] = bias ? bias[threadIdx.x] : 0.f;
+  __syncthreads();
+  const int p = blockIdx.x * 256 + threadIdx.x;
+  if (p >= Ho * Wo) return;
+  const int ho = p / Wo, wo = p - ho * Wo;
+  float acc[kStemCout];
+#pragma unroll
+  for (int co = 0; co < kStemCout; ++co) acc[co] = 0.f;
+#pragma unroll
+  for (int t = 0; t < 9; ++t) {
+    const int hi = 2 * ho - 1 + t / 3, wi = 2 * wo - 1 + t % 3;
+    if ((unsigned)hi >= (unsigned)H || (unsigned)wi >= (unsigned)W) continue;  // zero padding
+    const f32x4 x = pre_pixel(frame, row_bytes, Hf, Wf, hi, wi, scale_x, scale_y, m0, m1, m2, s0, s1, s2);
 #pragma unroll
     for (int c = 0; c < 3; ++c) {
-      const int d0 = r0[sx * 3 + c] * a0 + r0[sx1 * 3 + c] * a1;
-      const int d1 = r1[sx * 3 + c] * a0 + r1[sx1 * 3 + c] * a1;
-      int t = (((d0 >> 4) * b0) >> 16) + (((d1 >> 4) * b1) >> 16);
-      t = (t + 2) >> 2;
-      const int u = t < 0 ? 0 : (t > 255 ? 255 : t);
-      v[c] = (float)u / 255.f;  // transforms.ToTensor (float32 division)
+      const float xv = (float)(_Float16)x[c];
+#pragma unroll
+      for (int co = 0; co < kStemCout; ++co) acc[co] = fmaf(xv, Wt[t * 4 + c][co], acc[co]);
     }
-    // BGR -> RGB, then transforms.Normalize: (x - mean) / std
-    f32x4 o;
-    o[0] = (v[2] - m0) / s0;
-    o[1] = (v[1] - m1) / s1;
-    o[2] = (v[0] - m2) / s2;
-    o[3] = 0.f;
-    st4(out + p * ld, o);
+  }
+  float* o = out + (long)p * ldo;
+#pragma unroll
+  for (int co = 0; co < kStemCout; co += 4) {
+    f32x4 v;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) v[j] = seg_act(acc[co + j] + Bs[co + j], act);
+    st4(o + co, v);
   }
 }
 
@@ -244,6 +300,23 @@ SEG_API int seg_preprocess_bgr(const uint8_t* frame, int N, int Hf, int Wf, long
   hipLaunchKernelGGL(preprocess_bgr_kernel, dim3(grid_for((long)N * H * W)), dim3(256), 0, stream, frame, row_bytes,
                      row_bytes * Hf, N, Hf, Wf, out, ld, H, W, scale_x, scale_y, mean_r, mean_g, mean_b, std_r, std_g,
                      std_b);
+  SEG_RET_LAST();
+}
+
+// preprocess + the stem conv of the folded fp16 forward in one launch (stem_pre_f16_kernel): frame as
+// seg_preprocess_bgr (N = 1), the stem's packed weight / folded bias / activation as seg_conv_igemm_f16
+// (Cin 3 padded to 4, Cout 32, 3x3, stride 2, pad 1) into out [Ho*Wo][ldo].
+SEG_API int seg_stem_pre_f16(const uint8_t* frame, int Hf, int Wf, long row_bytes, int H, int W, float mean_r,
+                             float mean_g, float mean_b, float std_r, float std_g, float std_b, const float* wk,
+                             int ldk, const float* bias, int act, int Cout, float* out, long ldo, hipStream_t stream) {
+  if (!frame || !wk || !out || Cout != kStemCout || ldk < 36 || ldo < Cout || (ldo & 3) || ((uintptr_t)out & 15) ||
+      Hf <= 0 || Wf <= 0 || H <= 0 || W <= 0 || row_bytes < 3L * Wf || act < SEG_ACT_NONE || act > SEG_ACT_RELU6)
+    return (int)hipErrorInvalidValue;
+  const int Ho = (H - 1) / 2 + 1, Wo = (W - 1) / 2 + 1;
+  const double scale_x = 1.0 / ((double)W / Wf), scale_y = 1.0 / ((double)H / Hf);
+  hipLaunchKernelGGL(stem_pre_f16_kernel, dim3(seg_cdiv((long)Ho * Wo, 256)), dim3(256), 0, stream, frame, row_bytes,
+                     Hf, Wf, H, W, scale_x, scale_y, mean_r, mean_g, mean_b, std_r, std_g, std_b, wk, ldk, bias, act,
+                     out, ldo, Ho, Wo);
   SEG_RET_LAST();
 }
 

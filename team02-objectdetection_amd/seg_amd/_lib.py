@@ -117,6 +117,7 @@ PROTOTYPES = {
     "seg_conv_igemm_bnout_ok": (_I, [_L, _I, _I]),
     "seg_mbconv_ok": (_I, [_I, _I, _I, _I, _I]),
     "seg_mbconv_tune": (_I, [_I]),
+    "seg_stem_pre_f16": (_I, [_V, _I, _I, _L, _I, _I, _F, _F, _F, _F, _F, _F, _V, _I, _V, _I, _I, _V, _L, _V]),
     "seg_pw2_ok": (_I, [_I, _I, _I]),
     "seg_pw2_f16": (_I, [_V, _L, _L, _I, _V, _V, _I, _I, _V, _V, _I, _V, _L, _V]),
     "seg_conv_igemm_tiles": (_I, [_L, _I]),

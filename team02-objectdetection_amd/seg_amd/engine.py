@@ -721,6 +721,22 @@ class Program:
         self._mb_groups = m
         return m
 
+    def stem_pre(self):
+        """Folded fp16 forward: the stem ConvOp (features[0]: 3x3 stride-2 conv 3 -> 32, BN folded, ReLU6, the
+        image its only input) when seg_stem_pre_f16 can run it on the frame directly, else None."""
+        ops = self.ops
+        if not ops:
+            return None
+        op = ops[0]
+        if not (isinstance(op, ConvOp) and op.kind == "igemm" and op.ks == 3 and op.stride == 2 and op.pad == 1
+                and op.cin == 3 and op.cin_pad == 4 and op.cout == 32 and op.bn is not None and op.res is None
+                and op.inp is self.image and op.fk_pack is not None and op.ldk_f == 36 and op.out.ld % 4 == 0
+                and 0 not in self.mbconv_groups()):
+            return None
+        if any(getattr(o, "inp", None) is self.image or getattr(o, "res", None) is self.image for o in ops[1:]):
+            return None
+        return op
+
     def pw2_head(self):
         """Folded forward: index of outconv's first 1x1 conv when seg_pw2_f16 runs the head (1x1 -> folded BN ->
         ReLU -> 1x1, the program's last two ops, the hidden activation consumed only by the last conv), else
@@ -1408,15 +1424,16 @@ class Run:
         if DEBUG_KEEP_RUN:
             LAST_RUN = self
 
-    def forward_folded(self):
+    def forward_folded(self, start=0):
         """Eval forward with every BatchNorm folded (Program.fold must have run): one
         launch per conv, or per inverted residual with fp16 conv math (seg_mbconv_f16).  The
-        NHWC4 input rows must already be in the image buffer."""
+        NHWC4 input rows must already be in the image buffer (start = 0), or ops[:start] have
+        run (the stem fused with the preprocess, Program.stem_pre)."""
         ops = self.prog.ops
         f16 = self.prog.math == "f16"
         groups = self.prog.mbconv_groups() if MBCONV and f16 else {}
         head = self.prog.pw2_head() if PW2 and f16 else None
-        k = 0
+        k = start
         while k < len(ops):
             g = groups.get(k)
             if g is not None:
@@ -1497,6 +1514,9 @@ WGRAD2 = os.environ.get("SEG_WGRAD2", "1") == "1"
 PLAN_B1 = os.environ.get("SEG_PLAN_B1", "1") == "1"
 # the folded fp16 forward's outconv head (1x1 -> BN -> ReLU -> 1x1) in one launch (seg_pw2_f16); SEG_PW2=0 = two
 PW2 = os.environ.get("SEG_PW2", "1") == "1"
+# the folded fp16 forward's stem conv forms the preprocessed frame on load (seg_stem_pre_f16); SEG_STEM_PRE=0 =
+# seg_preprocess_bgr + the stem's implicit GEMM
+STEM_PRE = os.environ.get("SEG_STEM_PRE", "1") == "1"
 MBCONV = os.environ.get("SEG_MBCONV", "1") == "1"
 # BatchNorm-backward reduction from the epilogue of the implicit-GEMM data gradient that completes a BN layer's dA
 # (seg_conv_igemm_bnout*: no reduction pass over dA; the finalize reads the tile partials); SEG_BNOUT=0 = off.  Up to

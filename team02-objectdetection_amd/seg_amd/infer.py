@@ -24,6 +24,7 @@ import numpy as np
 import torch
 
 from ._lib import call
+from . import engine
 from .engine import Run, get_program
 
 MEAN = (0.485, 0.456, 0.406)   # inference.py:35
@@ -84,6 +85,7 @@ class Predictor:
         self.classes = self.prog.logits.C
         self.graph = None
         self.refresh()
+        self.stem_pre = self.prog.stem_pre() if (engine.STEM_PRE and math == "f16") else None
         if graph:
             self._capture()
 
@@ -97,9 +99,15 @@ class Predictor:
         s = torch.cuda.current_stream(self.device).cuda_stream
         rt.stream = s
         img = prog.image
-        call("seg_preprocess_bgr", self.frame.data_ptr(), 1, self.Hf, self.Wf, self.frame.stride(0), rt.ptr(img),
-             img.ld, self.H, self.W, *MEAN, *STD, s)
-        rt.forward_folded()
+        if self.stem_pre is not None:  # preprocess formed on load by the stem conv (seg_stem_pre_f16)
+            op, o = self.stem_pre, self.stem_pre.out
+            call("seg_stem_pre_f16", self.frame.data_ptr(), self.Hf, self.Wf, self.frame.stride(0), self.H, self.W,
+                 *MEAN, *STD, op.fk_pack.data_ptr(), op.ldk_f, op.fb.data_ptr(), op.act, op.cout, rt.ptr(o), o.ld, s)
+            rt.forward_folded(start=1)
+        else:
+            call("seg_preprocess_bgr", self.frame.data_ptr(), 1, self.Hf, self.Wf, self.frame.stride(0), rt.ptr(img),
+                 img.ld, self.H, self.W, *MEAN, *STD, s)
+            rt.forward_folded()
         lo = prog.logits
         Ho, Wo = prog.out_hw
         call("seg_argmax_nearest", rt.ptr(lo), lo.ld, 1, lo.H, lo.W, lo.C, Ho, Wo, self.mask.data_ptr(), self.Hf,

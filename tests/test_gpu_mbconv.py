@@ -8,6 +8,7 @@ src/unet.py:15-19).
     128x256 frame;
   * repeat launches bitwise equal (fixed-order combine; counters re-armed);
   * seg_pw2_f16 (the outconv head) against float64 of the same operand rounding;
+  * seg_stem_pre_f16 (preprocess formed on load by the stem conv) against seg_preprocess_bgr + seg_conv_igemm_f16;
   * the fp16 Predictor with the fused blocks and head agrees with the one-launch-per-conv folded forward
     (SEG_MBCONV off) within fp16 operand-rounding noise, and its graph replay equals eager.
 """
@@ -111,14 +112,15 @@ def test_predictor_fused_equals_unfused():
     import numpy as np
     model = deterministic_init(MobileNetV2UNet(10), seed=13, random_running_stats=True).to(DEV).eval()
     f = (np.random.default_rng(0).random((720, 1280, 3)) * 255).astype(np.uint8)
-    saved = engine.MBCONV, engine.PW2
+    saved = engine.MBCONV, engine.PW2, engine.STEM_PRE
     try:
-        engine.MBCONV = engine.PW2 = False
+        engine.MBCONV = engine.PW2 = engine.STEM_PRE = False
         p0 = Predictor(model, frame_hw=(720, 1280), graph=False, math="f16")
         p0(f)
         l0 = p0.logits()
-        engine.MBCONV = engine.PW2 = True
+        engine.MBCONV = engine.PW2 = engine.STEM_PRE = True
         p1 = Predictor(model, frame_hw=(720, 1280), graph=True, math="f16")
+        assert p1.stem_pre is p1.prog.ops[0]  # preprocess + stem in one launch (seg_stem_pre_f16)
         assert len(p1.prog.mbconv_groups()) == 17  # every InvertedResidual of features[1..17]
         assert p1.prog.pw2_head() == len(p1.prog.ops) - 2  # outconv in one launch (seg_pw2_f16)
         m1 = p1(f).clone()
@@ -127,7 +129,7 @@ def test_predictor_fused_equals_unfused():
         m2 = p2(f).clone()
         assert torch.equal(m1, m2) and torch.equal(l1, p2.logits()), "graph replay == eager"
     finally:
-        engine.MBCONV, engine.PW2 = saved
+        engine.MBCONV, engine.PW2, engine.STEM_PRE = saved
     # two valid fp16 forwards: the fp32 accumulation orders differ (split hidden ranges vs split-K), and an fp32
     # value one ulp either side of an fp16 rounding boundary moves that operand by an fp16 ulp (~5e-4); the oracle
     # bound of both is tests/test_gpu_infer.py::test_predictor_low_precision
@@ -154,3 +156,27 @@ def test_pw2_head_vs_fp64(M, C2, act):
     got = out[:, :C2].double().cpu()
     assert float((got - ref).norm() / ref.norm()) < 1e-4  # fp32 vs fp64 sums may move an fp16 rounding
     assert bool(out[:, C2:].isnan().all()), "nothing written beyond C2"
+
+
+@pytest.mark.parametrize("fhw,hw", [((720, 1280), (128, 256)), ((90, 161), (64, 32))])
+def test_stem_pre_equals_preprocess_then_conv(fhw, hw):
+    import numpy as np
+    from seg_amd.infer import MEAN, STD
+    (Hf, Wf), (H, W) = fhw, hw
+    frame = torch.from_numpy((np.random.default_rng(Hf).random((Hf, Wf, 3)) * 255).astype(np.uint8)).to(DEV)
+    g = torch.Generator().manual_seed(Wf)
+    wk = (torch.randn(32, 36, generator=g) * 0.3).to(DEV)
+    wk.view(32, 9, 4)[:, :, 3] = 0.0  # the padded channel
+    b = torch.randn(32, generator=g).to(DEV)
+    img = torch.zeros(H * W, 4, device=DEV)
+    call("seg_preprocess_bgr", frame.data_ptr(), 1, Hf, Wf, frame.stride(0), img.data_ptr(), 4, H, W, *MEAN, *STD, S())
+    Ho, Wo = (H - 1) // 2 + 1, (W - 1) // 2 + 1
+    ref = torch.empty(Ho * Wo, 32, device=DEV)
+    call("seg_conv_igemm_f16", img.data_ptr(), 4, 1, H, W, 4, wk.data_ptr(), 36, b.data_ptr(), ref.data_ptr(), 32, Ho,
+         Wo, 32, 3, 2, 1, None, 0, None, 2, None, 1, S())
+    out = torch.full((Ho * Wo, 36), float("nan"), device=DEV)
+    call("seg_stem_pre_f16", frame.data_ptr(), Hf, Wf, frame.stride(0), H, W, *MEAN, *STD, wk.data_ptr(), 36,
+         b.data_ptr(), 2, 32, out.data_ptr(), 36, S())
+    torch.cuda.synchronize()
+    assert float((out[:, :32] - ref).norm() / ref.norm()) < 1e-5
+    assert bool(out[:, 32:].isnan().all())

@@ -131,49 +131,61 @@ __global__ __launch_bounds__(256) void preprocess_bgr_kernel(const uint8_t* __re
 }
 
 // The folded forward's stem (features[0]: 3x3 stride-2 conv, BN folded, ReLU6) on the preprocessed frame
-// formed on load: one thread per stem output pixel, its 3x3 input taps preprocessed from the frame bytes,
-// fp16-rounded operands and fp32 accumulation as seg_conv_igemm_f16 stages them (the sum order differs).
-// wk: the stem's packed weight [kStemCout][ldk], K = tap * 4 + channel (channel 3 zero).
+// formed on load.  A block owns kStemTW output pixels of one output row: it preprocesses their 3 x (2 kStemTW
+// + 1) input pixels from the frame bytes into LDS once (fp16-rounded, as seg_conv_igemm_f16 stages its
+// operand), then each thread forms 8 of the 32 output channels of one pixel with fp32 accumulation (another
+// sum order than the implicit GEMM's).  wk: the stem's packed weight [kStemCout][ldk], K = tap * 4 + channel.
 constexpr int kStemCout = 32;
+constexpr int kStemTW = 64;
 __global__ __launch_bounds__(256) void stem_pre_f16_kernel(const uint8_t* __restrict__ frame, long row_bytes, int Hf,
                                                            int Wf, int H, int W, double scale_x, double scale_y,
                                                            float m0, float m1, float m2, float s0, float s1,
                                                            float s2, const float* __restrict__ wk, int ldk,
                                                            const float* __restrict__ bias, int act,
                                                            float* __restrict__ out, long ldo, int Ho, int Wo) {
-  __shared__ float Wt[36][kStemCout];  // [k][co]: one wave-uniform row per k
+  constexpr int PW = 2 * kStemTW + 1;
+  __shared__ float Xs[3][PW][3];
+  __shared__ float Wt[27][kStemCout];  // [tap * 3 + channel][co]
   __shared__ float Bs[kStemCout];
-  for (int i = threadIdx.x; i < 36 * kStemCout; i += 256) {
-    const int co = i / 36, k = i - co * 36;
-    Wt[k][co] = (float)(_Float16)wk[(long)co * ldk + k];
+  const int tiles_w = (Wo + kStemTW - 1) / kStemTW;
+  const int ho = blockIdx.x / tiles_w, w0 = (blockIdx.x - ho * tiles_w) * kStemTW;
+  for (int i = threadIdx.x; i < 27 * kStemCout; i += 256) {
+    const int co = i / 27, k = i - co * 27;
+    Wt[k][co] = (float)(_Float16)wk[(long)co * ldk + (k / 3) * 4 + k % 3];
   }
   if (threadIdx.x < kStemCout) Bs[threadIdx.x] = bias ? bias[threadIdx.x] : 0.f;
-  __syncthreads();
-  const int p = blockIdx.x * 256 + threadIdx.x;
-  if (p >= Ho * Wo) return;
-  const int ho = p / Wo, wo = p - ho * Wo;
-  float acc[kStemCout];
+  for (int i = threadIdx.x; i < 3 * PW; i += 256) {
+    const int r = i / PW, c = i - r * PW;
+    const int hi = 2 * ho - 1 + r, wi = 2 * w0 - 1 + c;
+    f32x4 x = {0.f, 0.f, 0.f, 0.f};  // zero padding
+    if ((unsigned)hi < (unsigned)H && (unsigned)wi < (unsigned)W)
+      x = pre_pixel(frame, row_bytes, Hf, Wf, hi, wi, scale_x, scale_y, m0, m1, m2, s0, s1, s2);
 #pragma unroll
-  for (int co = 0; co < kStemCout; ++co) acc[co] = 0.f;
+    for (int ch = 0; ch < 3; ++ch) Xs[r][c][ch] = (float)(_Float16)x[ch];
+  }
+  __syncthreads();
+  const int px = threadIdx.x & (kStemTW - 1), cg = threadIdx.x / kStemTW;  // 4 groups of 8 channels
+  const int wo = w0 + px;
+  if (wo >= Wo) return;
+  float acc[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) acc[j] = 0.f;
 #pragma unroll
   for (int t = 0; t < 9; ++t) {
-    const int hi = 2 * ho - 1 + t / 3, wi = 2 * wo - 1 + t % 3;
-    if ((unsigned)hi >= (unsigned)H || (unsigned)wi >= (unsigned)W) continue;  // zero padding
-    const f32x4 x = pre_pixel(frame, row_bytes, Hf, Wf, hi, wi, scale_x, scale_y, m0, m1, m2, s0, s1, s2);
 #pragma unroll
-    for (int c = 0; c < 3; ++c) {
-      const float xv = (float)(_Float16)x[c];
+    for (int ch = 0; ch < 3; ++ch) {
+      const float xv = Xs[t / 3][2 * px + t % 3][ch];
 #pragma unroll
-      for (int co = 0; co < kStemCout; ++co) acc[co] = fmaf(xv, Wt[t * 4 + c][co], acc[co]);
+      for (int j = 0; j < 8; ++j) acc[j] = fmaf(xv, Wt[t * 3 + ch][cg * 8 + j], acc[j]);
     }
   }
-  float* o = out + (long)p * ldo;
+  float* o = out + ((long)ho * Wo + wo) * ldo + cg * 8;
 #pragma unroll
-  for (int co = 0; co < kStemCout; co += 4) {
+  for (int h = 0; h < 2; ++h) {
     f32x4 v;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) v[j] = seg_act(acc[co + j] + Bs[co + j], act);
-    st4(o + co, v);
+    for (int j = 0; j < 4; ++j) v[j] = seg_act(acc[4 * h + j] + Bs[cg * 8 + 4 * h + j], act);
+    st4(o + 4 * h, v);
   }
 }
 
@@ -314,7 +326,7 @@ SEG_API int seg_stem_pre_f16(const uint8_t* frame, int Hf, int Wf, long row_byte
     return (int)hipErrorInvalidValue;
   const int Ho = (H - 1) / 2 + 1, Wo = (W - 1) / 2 + 1;
   const double scale_x = 1.0 / ((double)W / Wf), scale_y = 1.0 / ((double)H / Hf);
-  hipLaunchKernelGGL(stem_pre_f16_kernel, dim3(seg_cdiv((long)Ho * Wo, 256)), dim3(256), 0, stream, frame, row_bytes,
+  hipLaunchKernelGGL(stem_pre_f16_kernel, dim3(Ho * seg_cdiv(Wo, kStemTW)), dim3(256), 0, stream, frame, row_bytes,
                      Hf, Wf, H, W, scale_x, scale_y, mean_r, mean_g, mean_b, std_r, std_g, std_b, wk, ldk, bias, act,
                      out, ldo, Ho, Wo);
   SEG_RET_LAST();

@@ -1,5 +1,5 @@
 """One inference frame's kernel sequence from a rocprofv3 --kernel-trace of
-`bench.py --workload infer` (the span between the last two preprocess launches).
+`bench.py --workload infer` (the launches after one frame's argmax through the next frame's).
 
     python tools/trace_frame.py gpurun_out/<dir>/run_kernel_trace.csv > profiles/<name>.md
 """
@@ -9,8 +9,9 @@ import sys
 
 def main():
     rows = sorted(csv.DictReader(open(sys.argv[1])), key=lambda r: int(r["Start_Timestamp"]))
-    idx = [i for i, r in enumerate(rows) if "preprocess" in r["Kernel_Name"]]
-    a, b = idx[-2], idx[-1]
+    # a frame = the launches after one argmax (its last kernel) up to and including the next
+    idx = [i for i, r in enumerate(rows) if "argmax" in r["Kernel_Name"]]
+    a, b = idx[-3] + 1, idx[-2] + 1
     t0 = int(rows[a]["Start_Timestamp"])
     tot = 0
     print("| start us | dur us | grid (work-items) | kernel |\n|---|---|---|---|")

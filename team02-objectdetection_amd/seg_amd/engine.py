@@ -863,16 +863,20 @@ class Program:
                 op.w16_f, op.w16_d = w16f, w16d
                 # the deep convs (3x3, or 1x1 with SEG_IGEMM2=all) on seg_conv_igemm2_bf16io
                 op.ig2_f = op.ig2_d = None
-                ig2_ok = (op.ks == 3 and y.M <= IGEMM2_MAX_ROWS) or IGEMM2 == "all" or (
+                # beyond IGEMM2_MAX_ROWS only GEMMs whose N fills the 8-wave tiles (N % 128 == 0: UNet's deep levels)
+                wide = op.ks == 3 and y.M > IGEMM2_MAX_ROWS and IGEMM2_WIDE and IGEMM2 != "all"
+                ig2_ok = (op.ks == 3 and y.M <= IGEMM2_MAX_ROWS) or wide or IGEMM2 == "all" or (
                     op.ks == 1 and IGEMM2_1X1 and y.M <= IGEMM2_1X1_MAX_ROWS)
                 if w16f and IGEMM2 != "0" and op.stride == 1 and op.pad == op.ks // 2 and ig2_ok:
                     i = op.inp  # 16-byte rows: ld and channel offset multiples of 8 elements
                     rows16 = i.ld % 8 == 0 and i.off % 8 == 0 and y.ld % 8 == 0 and y.off % 8 == 0
                     # (a 1x1 consumer of a lazy BN applies it to its A fragments: seg_conv_igemm2_bf16io_xf)
                     xf_ok = op.xform is None or (op.ks == 1 and op.cin <= 2048)
-                    if rows16 and not (op.halo_f or op.h2_f) and xf_ok and op.cin_pad == op.cin:
+                    if (rows16 and not (op.halo_f or op.h2_f) and xf_ok and op.cin_pad == op.cin
+                            and (not wide or op.cout % 128 == 0)):
                         op.ig2_f = igemm2_plan(y.M, op.cout, op.cin_pad, op.ks)
-                    if rows16 and not op.first and not (op.halo_d or op.h2_d) and op.cout % 8 == 0:
+                    if (rows16 and not op.first and not (op.halo_d or op.h2_d) and op.cout % 8 == 0
+                            and (not wide or op.cin % 128 == 0)):
                         op.ig2_d = igemm2_plan(y.M, op.cin, op.cout, op.ks)
                 if w16f:
                     op.pw_f, op.pw_d = _pw_pick(op, 8)
@@ -1550,6 +1554,10 @@ IGEMM2 = os.environ.get("SEG_IGEMM2", "3")
 # ... on images of at most this many output rows: measured per launch on UNet 512x1024 bf16io, igemm2 is 5-25 %
 # slower than the 4-wave implicit GEMM at 262k-4M rows and 1-6 % faster at 65k (profiles/r03k)
 IGEMM2_MAX_ROWS = int(os.environ.get("SEG_IGEMM2_MAX_ROWS", "65536"))
+# ... and beyond that on the convs whose GEMM N is a multiple of 128 (the 8-wave tiles without padding): measured per
+# launch at HEAD of round 4 on UNet 512x1024 bf16io, side stream off, 1-10 % faster than the 4-wave implicit GEMM on
+# every such launch (profiles/r04ig/); SEG_IGEMM2_WIDE=0 = off
+IGEMM2_WIDE = os.environ.get("SEG_IGEMM2_WIDE", "1") == "1"
 # ... and the 1x1 convs of small images on its 4-wave tiles (round 4: the generic register-staged kernel
 # keeps one K chunk in flight and ran the encoder's 4k-65k-row 1x1 convs at 0.4-1.5 TB/s); SEG_IGEMM2_1X1=0 = off
 # (default off: step A/B +3 % without it, profiles/r04f_ab.txt)

@@ -186,3 +186,26 @@ def test_igemm2_xf_equals_generic_xf(M, Cin, Cout, act):
     z = z.to(BF).double().cpu()
     ref = z @ w.view(Cout, Cin).to(BF).double().cpu().t()
     assert rel(o2.float(), ref) < 4e-3
+
+
+def test_engine_routes_wide_convs_to_igemm2(monkeypatch):
+    """UNet(10) bf16io at 8x512x1024 (configs[4]): past the 65k-row cap, the 3x3 convs whose GEMM N is a multiple
+    of 128 take igemm2 (SEG_IGEMM2_WIDE), the others keep the implicit GEMM / LDS halo; off: none past the cap."""
+    from seg_amd import UNet, deterministic_init
+    m = deterministic_init(UNet(10), seed=0).to(DEV).train()
+    engine.set_conv_math(m, "bf16io")
+    for wide in (True, False):
+        monkeypatch.setattr(engine, "IGEMM2_WIDE", wide)
+        prog = engine.build_program(m, 8, 512, 1024, "bf16io")
+        prog._build_pack([op for op in prog.ops if isinstance(op, engine.ConvOp)], None)
+        big = [op for op in prog.ops if isinstance(op, engine.ConvOp) and op.ks == 3 and op.y.M > 65536]
+        assert big
+        for op in big:
+            if wide and op.cout % 128 == 0 and op.cin_pad == op.cin and not op.halo_f:
+                assert op.ig2_f is not None, (op.cin, op.cout, op.y.M)
+            if op.cout % 128 or not wide:
+                assert op.ig2_f is None, (op.cin, op.cout, op.y.M)
+            if not op.first and (op.cin % 128 or not wide):
+                assert op.ig2_d is None, (op.cin, op.cout, op.y.M)
+        if wide:
+            assert sum(op.ig2_f is not None for op in big) >= 4 and sum(op.ig2_d is not None for op in big) >= 4

@@ -92,12 +92,14 @@ int seg_conv_pw(const float* in, long ldin, long M, int K, const float* wk, int 
  * cannot fill the 256 CUs (batch-1 inference). */
 int seg_conv_igemm_splits(long M, int Cout, int Cin, int ks);
 /* seg_conv_igemm_act / _bf16 / _f16 with split-K combined inside the launch (the inference forward's
- * batch-1 convs): when the whole grid is co-resident each split block of a tile waits for the tile's
- * other splits and applies the split-K epilogue to its share (else the separate reduce runs); bitwise
- * the two-launch result.  cnt: 2 * seg_conv_igemm_tiles(M, Cout) unsigned, zero before the first
- * launch, re-armed by every launch.  No BN statistics. */
+ * batch-1 convs): when the whole grid is co-resident (and splits <= 64) the split blocks of a tile combine it
+ * together, each applying the split-K epilogue to its share -- a block that cannot wait for its peers (another
+ * kernel holding the CUs) leaves its share to the tile's last arrival, so no block ever spins on a peer that is
+ * not resident; else the separate reduce runs.  Bitwise the two-launch result.  cnt: 4 *
+ * seg_conv_igemm_tiles(M, Cout) unsigned, zero before the first launch, re-armed by every launch.  No BN
+ * statistics. */
 int seg_conv_igemm_tiles(long M, int Cout);
-/* Plan for those launches: out[3] = (splits, tile, output tiles -- the counters are 2 per tile).  tile -1 =
+/* Plan for those launches: out[3] = (splits, tile, output tiles -- the counters are 4 per tile).  tile -1 =
  * the cost model's (seg_conv_igemm_tiles), else an index into the kernel's tile table (the batch-1 rule:
  * short K unsplit on 64x64 tiles, long K split on 8-wave 128x64 tiles).  Tile choice does not change
  * results; the split count does (another K partition). */
@@ -300,7 +302,7 @@ int seg_bn_backward(const float* da, long ldda, const float* y, long ldy, long M
                     const float* scale, const float* shift, int act,
                     float* dgamma, float* dbeta, float* work, float* dy, long lddy, hipStream_t stream);
 /* The two halves of seg_bn_backward (same arguments and arithmetic), for callers that fuse one of
- * them into a neighbouring kernel (csrc/dw2.hip's depthwise data / weight gradients):
+ * them into a neighbouring kernel:
  * seg_bn_bwd_coef: the reduction -- dgamma, dbeta and coef[3][C] = (gamma*invstd, mean(dz),
  * mean(dz*xhat)*invstd); work >= seg_chan_workspace_floats(M, C) floats.  seg_bn_bwd_apply:
  * dy = coef[0] * (dz - coef[1] - (y - mean) * coef[2]), dz = da * act'(y*scale + shift). */
@@ -494,19 +496,6 @@ int seg_conv_igemm_bf16io_xf(const seg_bf16* in, long ldin, int N, int H, int W,
 int seg_conv_wgrad_bf16io_xf(const seg_bf16* dy, long lddy, const seg_bf16* x, long ldx, int N, int H, int W,
     int Cin, int Ho, int Wo, int Cout, int ks, int stride, int pad, float* part, int splits, const float* in_scale,
     const float* in_shift, int in_act, hipStream_t stream);
-/* seg_conv_halo(_bf16io, _bf16io_w16) of a 3x3 conv whose input is the raw output of a BatchNorm'd
- * producer (double_conv's first conv, src/unet.py:58-60): in = act(in * in_scale[c] + in_shift[c]) on the
- * halo load, padding pixels zero -- the tensor the BN-apply pass would have stored (bf16: rounded RNE).
- * The _xf implicit GEMMs / weight gradients above take ks 3 the same way (Cin >= the K chunk). */
-int seg_conv_halo_xf(const float* in, long ldin, int N, int H, int W, int Cin, const float* wk, int ldk,
-    const float* bias, float* out, long ldout, int Cout, const float* add, long ldadd, float* stat,
-    const float* in_scale, const float* in_shift, int in_act, hipStream_t stream);
-int seg_conv_halo_bf16io_xf(const seg_bf16* in, long ldin, int N, int H, int W, int Cin, const float* wk, int ldk,
-    const float* bias, seg_bf16* out, long ldout, int Cout, const seg_bf16* add, long ldadd, float* stat,
-    const float* in_scale, const float* in_shift, int in_act, hipStream_t stream);
-int seg_conv_halo_bf16io_xf_w16(const seg_bf16* in, long ldin, int N, int H, int W, int Cin, const seg_bf16* wk,
-    int ldk, const float* bias, seg_bf16* out, long ldout, int Cout, const seg_bf16* add, long ldadd, float* stat,
-    const float* in_scale, const float* in_shift, int in_act, hipStream_t stream);
 
 /* ---- Adam (optim.Adam(model.parameters(), lr=1.5e-4), main.py:100; step at
  *      src/train.py:39): one launch over every parameter with a gradient, the
@@ -524,6 +513,13 @@ typedef struct SegAdamTensor {
  * element) int64 pairs covering every tensor in pieces of <= chunk elements */
 int seg_adam_step(const SegAdamTensor* tensors, const long* chunks, int nchunks, int chunk,
                   float one_minus_beta1, float beta2, float one_minus_beta2, float eps, hipStream_t stream);
+/* seg_adam_step, skipped on the device when *skip != 0 (skip: a device float, e.g. the out-of-range label count
+ * of the batch, summed or averaged over ranks; NULL = never): train_one_epoch queues the step without waiting
+ * for the label check (nn.CrossEntropyLoss raises before any update, src/train.py:37), and raises after
+ * loss.item() (src/train.py:41). */
+int seg_adam_step_skip(const SegAdamTensor* tensors, const long* chunks, int nchunks, int chunk,
+                       float one_minus_beta1, float beta2, float one_minus_beta2, float eps, const float* skip,
+                       hipStream_t stream);
 
 /* ---- launch tape (csrc/tape.hip): a recorded sequence of the launches above,
  *      replayed by one host call per segment -- the engine's training step
@@ -557,34 +553,11 @@ int seg_conv_igemm2_bf16io(const seg_bf16* in, long ldin, int N, int H, int W, i
                            const float* bias, seg_bf16* out, long ldout, int Cout, int ks, const seg_bf16* add,
                            long ldadd, float* stat, float* work, hipStream_t stream);
 /* Round 4: the plan also picks 4-wave 128x128 / 128x64 / 64x128 / 64x64 tiles (small-image 1x1 and 3x3
- * convs of the MobileNetV2 encoder); seg_igemm2_force_tile(t) forces table entry t (-1 = the plan).
- * _xf: a 1x1 conv (ks == 1, Cin <= 2048) whose input is the raw output of a BatchNorm'd producer,
- * A = act(in * in_scale[c] + in_shift[c]) formed on the MFMA fragments (bf16-rounded as the BN-apply
- * pass would store it) -- the project convs of the inverted residuals (torchvision, via
- * src/unet.py:15-19). */
+ * convs of the MobileNetV2 encoder); seg_igemm2_force_tile(t) forces table entry t (-1 = the plan). */
 int seg_igemm2_force_tile(int t);
 /* Tuning hook: split-K of the 4-wave tiles up to target_blocks blocks with >= min_steps 64-deep K
  * steps per slice (defaults 512, 3); values <= 0 keep the current setting. */
 int seg_igemm2_tune(int target_blocks, int min_steps);
-int seg_conv_igemm2_bf16io_xf(const seg_bf16* in, long ldin, int N, int H, int W, int Cin, const seg_bf16* wk,
-                              int ldk, const float* bias, seg_bf16* out, long ldout, int Cout, int ks,
-                              const seg_bf16* add, long ldadd, float* stat, float* work, const float* in_scale,
-                              const float* in_shift, int in_act, hipStream_t stream);
-
-/* seg_conv_halo2_bf16io: the narrow 3x3 convs of the bf16io configuration (replaces aten conv2d /
- * convolution_backward(input) of src/unet.py:58,61 where Cout <= 96: MobileNetV2UNet up3 / up4 and
- * their data gradients, UNet's 64-channel full-resolution levels; csrc/halo2.hip).  Persistent
- * blocks (one per CU) with the weights resident in LDS and the 4 x 64-pixel tiles' input halos
- * streamed by LDS-DMA through a three-stage ring by a dedicated loader wave.  Arguments as
- * seg_conv_halo_bf16io_w16 (stride 1, pad 1; bf16 rows, ldin % 8 == 0 and 16-byte aligned; bf16
- * packed weights, mode 16 forward / 17 data gradient); BN partials in seg_conv_halo2_row_tiles
- * tiles of 256 rows ([tiles][2][Cout]: sum, M2 about the tile mean).  seg_conv_halo2_ok: H % 4 == 0,
- * W % 64 == 0, Cin % 8 == 0, Cout <= 96 and 9 x Cout x Cin weights that fit beside the ring. */
-int seg_conv_halo2_ok(int N, int H, int W, int Cin, int Cout);
-int seg_conv_halo2_row_tiles(int N, int H, int W);
-int seg_conv_halo2_bf16io(const seg_bf16* in, long ldin, int N, int H, int W, int Cin, const seg_bf16* wk, int ldk,
-                          const float* bias, seg_bf16* out, long ldout, int Cout, const seg_bf16* add, long ldadd,
-                          float* stat, hipStream_t stream);
 
 /* seg_conv_wgrad2_bf16io: the weight gradient of those narrow 3x3 convs (replaces aten's
  * convolution_backward weight path of src/unet.py:58,61 where Cout <= 64; csrc/wgrad2.hip): persistent
@@ -598,55 +571,6 @@ int seg_conv_wgrad2_ok(int N, int H, int W, int Cin, int Cout);
 int seg_conv_wgrad2_blocks(int N, int H, int W);
 int seg_conv_wgrad2_bf16io(const seg_bf16* dy, long lddy, const seg_bf16* x, long ldx, int N, int H, int W, int Cin,
                            int Cout, float* part, hipStream_t stream);
-
-/* Depthwise 3x3 convs of the bf16io configuration on LDS-DMA tiles (csrc/dw2.hip; replace the
- * groups=C Conv2d of torchvision's InvertedResidual, reached through src/unet.py:15-19,34-38, and its
- * convolution_backward).  A block owns an output tile (8 x 32 pixels at stride 1, 4 x 32 at stride 2)
- * of a 64-channel slice; the input tile with its halo is copied into LDS once, the lazy BN of the input
- * (in_scale / in_shift / in_act, as seg_dw_fwd) applied there in place and rounded to bf16.  Rows are
- * 16-byte aligned with ld % 8 == 0 and C % 8 == 0 (seg_dw2_ok).
- * seg_dw2_fwd_bf16io: as seg_dw_fwd_bf16io, plus stat (or NULL): the BatchNorm tile partials of the
- * output, [seg_dw2_stat_tiles(...)][2][C] (tile sum, M2 about the tile mean; *tile_rows rows each) for
- * seg_bn_stats_tiles -- only when seg_dw2_stat_tiles is non-zero (the tiles divide Ho x Wo).
- * seg_dw2_dgrad_bf16io: as seg_dw_dgrad_bf16io (bitwise its result).
- * seg_dw2_wgrad_bf16io: as seg_dw_wgrad_bf16io with part[seg_dw2_wgrad_blocks(N, Ho, Wo, C, stride, 0)][9][C]
- * (reduce with seg_conv_wgrad_reduce(part, blocks, dw, C, 1, 3, 1, acc)); fixed-order, deterministic. */
-int seg_dw2_ok(int C, int stride);
-int seg_dw2_stat_tiles(int N, int Ho, int Wo, int stride, int* tile_rows);
-int seg_dw2_fwd_bf16io(const seg_bf16* in, long ldin, int N, int H, int W, int C, const float* in_scale,
-                       const float* in_shift, int in_act, const float* wk, seg_bf16* out, long ldout, int Ho, int Wo,
-                       int stride, float* stat, hipStream_t stream);
-int seg_dw2_dgrad_bf16io(const seg_bf16* dy, long lddy, int N, int Ho, int Wo, int C, const float* wk, seg_bf16* dx,
-                         long lddx, int H, int W, int stride, int accumulate, hipStream_t stream);
-/* seg_dw2_dgrad_bn_bf16io: seg_dw2_dgrad_bf16io with two optional BatchNorm-backward fusions (a NULL
- * by / oy skips one):
- *  BIN  -- dy holds dA, the gradient of this conv's BN + act output; its BatchNorm backward
- *          dY = seg_bn_bwd_apply(dA, by; bmean, bscale, bshift, bact, bcoef) is formed on load
- *          (bitwise the apply pass's bf16 output) and never stored (bcoef from seg_bn_bwd_coef_bf16io);
- *  BOUT -- dx is dA of the layer that produced this conv's input (pre-BN output oy, BN statistics
- *          omean / oinvstd / oscale / oshift / ogamma, act oact): the partials of that layer's BatchNorm
- *          backward come out of this launch's epilogue into opart [seg_dw2_dgrad_tiles(N, H, W)][2][C]
- *          and the last tile of each 64-channel slice finalizes them into odgamma, odbeta (may be NULL)
- *          and ocoef [3][C] (as seg_bn_bwd_coef_bf16io; fixed-order fp64 sums, deterministic); ocnt:
- *          ceil(C/64) counters, zero before the first launch, re-armed by every launch. */
-int seg_dw2_dgrad_tiles(int N, int H, int W);
-int seg_dw2_dgrad_bn_bf16io(const seg_bf16* dy, long lddy, int N, int Ho, int Wo, int C, const float* wk,
-                            seg_bf16* dx, long lddx, int H, int W, int stride, int accumulate, const seg_bf16* by,
-                            long ldby, const float* bscale, const float* bshift, const float* bmean,
-                            const float* bcoef, int bact, const seg_bf16* oy, long ldoy, const float* oscale,
-                            const float* oshift, const float* omean, const float* ogamma, const float* oinvstd,
-                            int oact, float* opart, float* odgamma, float* odbeta, float* ocoef, unsigned* ocnt,
-                            hipStream_t stream);
-long seg_dw2_wgrad_blocks(int N, int Ho, int Wo, int C, int stride, int bin);
-int seg_dw2_wgrad_bf16io(const seg_bf16* dy, long lddy, const seg_bf16* x, long ldx, int N, int H, int W, int C,
-                         const float* in_scale, const float* in_shift, int in_act, int Ho, int Wo, int stride,
-                         float* part, hipStream_t stream);
-/* seg_dw2_wgrad_bn_bf16io: seg_dw2_wgrad_bf16io with BIN (dy holds dA; dY formed on load as in
- * seg_dw2_dgrad_bn_bf16io); part sized by seg_dw2_wgrad_blocks(..., bin = by != NULL). */
-int seg_dw2_wgrad_bn_bf16io(const seg_bf16* dy, long lddy, const seg_bf16* x, long ldx, int N, int H, int W, int C,
-                            const float* in_scale, const float* in_shift, int in_act, int Ho, int Wo, int stride,
-                            float* part, const seg_bf16* by, long ldby, const float* bscale, const float* bshift,
-                            const float* bmean, const float* bcoef, int bact, hipStream_t stream);
 
 /* Fused inverted residual of the BatchNorm-folded fp16 inference forward (BASELINE configs[3];
  * torchvision's InvertedResidual reached through src/unet.py:15-19, run per frame by

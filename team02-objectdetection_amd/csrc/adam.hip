@@ -32,7 +32,8 @@ namespace {
 
 __global__ __launch_bounds__(256) void adam_kernel(const SegAdamTensor* __restrict__ ts,
                                                    const long* __restrict__ chunks, int chunk, float w, float b2,
-                                                   float cv, float eps) {
+                                                   float cv, float eps, const float* __restrict__ skip) {
+  if (skip && *skip != 0.f) return;  // the batch had an out-of-range label: no parameter or moment changes
   const long ti = chunks[2 * blockIdx.x], start = chunks[2 * blockIdx.x + 1];
   const SegAdamTensor t = ts[ti];
   const long end = std::min<long>(t.n, start + chunk);
@@ -55,11 +56,17 @@ __global__ __launch_bounds__(256) void adam_kernel(const SegAdamTensor* __restri
 // (tensor index, first element) int64 pairs, each chunk <= `chunk` elements.
 // one_minus_beta1 / one_minus_beta2 are 1 - beta rounded once from double (torch
 // passes the double 1 - beta as the lerp weight / addcmul value), not 1.f - (float)beta.
-SEG_API int seg_adam_step(const SegAdamTensor* tensors, const long* chunks, int nchunks, int chunk,
-                          float one_minus_beta1, float beta2, float one_minus_beta2, float eps, hipStream_t stream) {
+SEG_API int seg_adam_step_skip(const SegAdamTensor* tensors, const long* chunks, int nchunks, int chunk,
+                               float one_minus_beta1, float beta2, float one_minus_beta2, float eps, const float* skip,
+                               hipStream_t stream) {
   if (nchunks < 0 || chunk < 1) return (int)hipErrorInvalidValue;
   if (nchunks == 0) return (int)hipSuccess;
   hipLaunchKernelGGL(adam_kernel, dim3(nchunks), dim3(256), 0, stream, tensors, chunks, chunk, one_minus_beta1, beta2,
-                     one_minus_beta2, eps);
+                     one_minus_beta2, eps, skip);
   SEG_RET_LAST();
+}
+SEG_API int seg_adam_step(const SegAdamTensor* tensors, const long* chunks, int nchunks, int chunk,
+                          float one_minus_beta1, float beta2, float one_minus_beta2, float eps, hipStream_t stream) {
+  return seg_adam_step_skip(tensors, chunks, nchunks, chunk, one_minus_beta1, beta2, one_minus_beta2, eps, nullptr,
+                            stream);
 }

@@ -923,7 +923,7 @@ __global__ __launch_bounds__(256) void bn_bwd_finalize_tiles_kernel(const float*
 }  // namespace
 
 // The two halves of seg_bn_backward, for a caller that fuses one of them into a neighbouring
-// kernel (the depthwise convs of csrc/dw2.hip):
+// kernel:
 //  * seg_bn_bwd_coef_*: the reduction -- dgamma, dbeta and coef[3][C] = (g*invstd, mean(dz),
 //    mean(dz*xhat)*invstd) (`work` >= seg_chan_workspace_floats(M, C) floats);
 //  * seg_bn_bwd_apply_*: dy = seg_bnbwd4(da, y; coef) -- what seg_bn_backward writes, bit for bit.

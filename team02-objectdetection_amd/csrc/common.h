@@ -137,6 +137,69 @@ __device__ __forceinline__ bool seg_last_arrival(unsigned* cnt, unsigned nblocks
   return *word != 0;
 }
 
+// In-launch combine of a split tile (split-K / split hidden range) by its own S <= 64 blocks, with no block
+// ever waiting on a block that may not be resident (a plain "wait until all S splits arrived" spin
+// hangs when another kernel holds the CUs a peer needs, e.g. two such kernels on two streams).  The tile's
+// combine is cut into S pieces; piece p may be done by any block once the tile is complete:
+//   * every block publishes its partial (write-through, drained: the seg_last_arrival form above) and takes a
+//     ticket; the block with the last ticket knows the tile is complete;
+//   * a non-last block polls the ticket count for at most `spin` rounds (0: not at all -- the grid is known not
+//     to be co-resident) and, if the tile completed meanwhile, claims its own piece (one atomic or on the tile's
+//     claim mask) and combines it: the parallel combine of the co-resident case;
+//   * the last block combines its own piece, then claims and combines every piece nobody has claimed yet (the
+//     pieces of blocks that gave up waiting, or left at once);
+//   * each block counts itself out; the one that completes the count re-arms the tile's four words.
+// Every piece is combined exactly once, by a block that saw the tile complete; results do not depend on who.
+// cnt: 4 words per tile {tickets, leavers, claims 0-31, claims 32-63}, zero before the first launch.
+// piece(p): the block's combine of piece p (called by all threads, block-uniform p).
+template <typename F>
+__device__ __forceinline__ void seg_tile_combine(unsigned* cnt, int S, int z, int spin, int* word, F&& piece) {
+  unsigned* tickets = cnt;
+  unsigned* leavers = cnt + 1;
+  unsigned* claims = cnt + 2;
+  auto claim = [&](int p) -> bool {  // thread 0 only
+    const unsigned bit = 1u << (p & 31);
+    return !(__hip_atomic_fetch_or(claims + (p >> 5), bit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & bit);
+  };
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's partial has landed
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned t = __hip_atomic_fetch_add(tickets, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int last = t == (unsigned)S - 1;
+    bool ready = last;
+    for (int i = 0; !ready && i < spin; ++i) {
+      __builtin_amdgcn_s_sleep(2);
+      ready = __hip_atomic_load(tickets, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= (unsigned)S;
+    }
+    word[0] = last;
+    word[1] = ready && claim(z);
+  }
+  __syncthreads();
+  const int last = word[0];
+  if (word[1]) piece(z);
+  if (last) {
+    for (int p = 0; p < S; ++p) {
+      if (p == z) continue;
+      __syncthreads();  // word[1] of the previous round has been read by every thread
+      if (threadIdx.x == 0) word[1] = claim(p);
+      __syncthreads();
+      if (word[1]) piece(p);
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x == 0 &&
+      __hip_atomic_fetch_add(leavers, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (unsigned)S - 1) {
+    // every block of the tile is done with its words: re-arm them for the next launch
+    __hip_atomic_store(tickets, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(claims, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(claims + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(leavers, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+// Bound of seg_tile_combine's poll when the grid is co-resident (~1 us per round: a few ms before a block gives
+// its piece to the last arrival -- only ever reached when another kernel holds the CUs a peer needs).
+constexpr int kSegCombineSpin = 4096;
+
 // XCD-aware block swizzle (bijective for any nblk): the dispatcher deals blocks
 // round-robin over the 8 XCDs (block b and b+8 share an XCD and its 4 MiB L2), so
 // remap hardware block b to a logical id such that each XCD walks a CONTIGUOUS

@@ -34,9 +34,6 @@ struct HaloArgs {
   float* stat;                   // BN partials [tiles][2][Cout]
   int N, H, W, Cin, Cout;
   int tiles_w, tiles_h;
-  // XF: in = act(in * xs[c] + xb[c]) formed on the halo load -- the producer's lazy BatchNorm
-  // + activation (double_conv's first conv feeding its second); padding pixels stay zero
-  const float* xs; const float* xb; int xact;
 };
 
 // T: activation storage (in / add / out).  T = __bf16 (the bf16io configuration):
@@ -46,7 +43,7 @@ struct HaloArgs {
 // WB: bf16-packed weights (mode | 16), 8 per 16-byte slot copied to LDS as is -- every
 // 256-pixel tile re-reads all 9 x Cout x Cin weights, so this halves the kernel's L2
 // weight traffic; bitwise the fp32-weight launch (the same RNE rounding, done at pack time).
-template <int NI, typename T = float, bool WB = false, bool XF = false>  // output-channel blocks of 32 (Cout padded to 32*NI)
+template <int NI, typename T = float, bool WB = false>  // output-channel blocks of 32 (Cout padded to 32*NI)
 __global__ __launch_bounds__(256) void halo3x3_kernel(HaloArgs a) {
   static_assert(!WB || sizeof(T) == 2, "bf16 weights: the bf16io kernel");
   const float* wk32 = static_cast<const float*>(a.wk);
@@ -102,24 +99,7 @@ __global__ __launch_bounds__(256) void halo3x3_kernel(HaloArgs a) {
   }
 
   f32x4 rh[HALO_PER], rw[W_PER];
-  // XF: this thread's halo channel group is fixed (slot % (BK / HV) == tid % (BK / HV)); its
-  // coefficients are fetched with each chunk, and `hvm` marks the slots that loaded real pixels
-  f32x4 xsc[HV / 4], xsh[HV / 4];
-  unsigned hvm = 0;
   auto load = [&](int c0) {
-    if constexpr (XF) {
-      const int q4 = (tid % (BK / HV)) * HV;
-      const int cc = c0 + q4 < a.Cin ? c0 + q4 : 0;
-#pragma unroll
-      for (int j = 0; j < HV / 4; ++j) {
-        xsc[j] = ld4(a.xs + cc + 4 * j);
-        xsh[j] = ld4(a.xb + cc + 4 * j);
-      }
-      hvm = 0;
-#pragma unroll
-      for (int i = 0; i < HALO_PER; ++i)
-        if (hok[i] && c0 + q4 < a.Cin) hvm |= 1u << i;
-    }
 #pragma unroll
     for (int i = 0; i < HALO_PER; ++i) {
       const int q4 = ((tid + i * 256) % (BK / HV)) * HV;
@@ -144,22 +124,7 @@ __global__ __launch_bounds__(256) void halo3x3_kernel(HaloArgs a) {
     for (int i = 0; i < HALO_PER; ++i) {
       const int s = tid + i * 256;
       if (HALO_VEC % 256 == 0 || s < HALO_VEC) {
-        f32x4 v = rh[i];
-        if constexpr (XF) {
-          if ((hvm >> i) & 1u) {
-            if constexpr (LP) {  // 8 bf16: widen, transform, round back (RNE) as the BN-apply pass would
-              const bf16x8 q = __builtin_bit_cast(bf16x8, v);
-              const f32x4 lo = seg_bn_act4(__builtin_convertvector(__builtin_shufflevector(q, q, 0, 1, 2, 3), f32x4),
-                                           xsc[0], xsh[0], a.xact);
-              const f32x4 hi = seg_bn_act4(__builtin_convertvector(__builtin_shufflevector(q, q, 4, 5, 6, 7), f32x4),
-                                           xsc[HV / 4 - 1], xsh[HV / 4 - 1], a.xact);
-              v = __builtin_bit_cast(f32x4, seg_cat8(__builtin_convertvector(lo, bf16x4),
-                                                     __builtin_convertvector(hi, bf16x4)));
-            } else {
-              v = seg_bn_act4(v, xsc[0], xsh[0], a.xact);
-            }
-          }
-        }
+        const f32x4 v = rh[i];
         *reinterpret_cast<f32x4*>(&Hs[(s / (BK / HV)) * LDSR + (s % (BK / HV)) * HV]) = v;
       }
     }
@@ -321,23 +286,15 @@ SEG_API int seg_conv_halo_row_tiles(int N, int H, int W) { return N * (H / TH) *
 template <typename T, bool WB = false>
 static int conv_halo_impl(const T* in, long ldin, int N, int H, int W, int Cin, const void* wk, int ldk,
                           const float* bias, T* out, long ldout, int Cout, const T* add, long ldadd, float* stat,
-                          hipStream_t stream, const float* xs = nullptr, const float* xb = nullptr, int xact = 0) {
+                          hipStream_t stream) {
   if (!seg_conv_halo_ok(N, H, W, Cin, Cout) || (ldin & 3) || (ldk & 3) || ldk < 9 * Cin) return (int)hipErrorInvalidValue;
-  if (xs && (!xb || xact < SEG_ACT_NONE || xact > SEG_ACT_RELU6)) return (int)hipErrorInvalidValue;
   if (sizeof(T) == 2 && ((Cin & 7) || (ldin & 7))) return (int)hipErrorInvalidValue;  // 16-byte bf16 halo slots
   if (WB && ((ldk & 7) || ((uintptr_t)wk & 15))) return (int)hipErrorInvalidValue;    // 16-byte bf16 weight slots
   HaloArgs a;
   a.in = in; a.ldin = ldin; a.wk = wk; a.ldk = ldk; a.bias = bias; a.add = add; a.ldadd = ldadd;
   a.out = out; a.ldout = ldout; a.stat = stat; a.N = N; a.H = H; a.W = W; a.Cin = Cin; a.Cout = Cout;
   a.tiles_w = W / TW; a.tiles_h = H / TH;
-  a.xs = xs; a.xb = xb; a.xact = xact;
   const int grid = N * a.tiles_h * a.tiles_w;
-  if (xs) {
-    if (Cout <= 32) hipLaunchKernelGGL((halo3x3_kernel<1, T, WB, true>), dim3(grid), dim3(256), 0, stream, a);
-    else if (Cout <= 64) hipLaunchKernelGGL((halo3x3_kernel<2, T, WB, true>), dim3(grid), dim3(256), 0, stream, a);
-    else hipLaunchKernelGGL((halo3x3_kernel<3, T, WB, true>), dim3(grid), dim3(256), 0, stream, a);
-    SEG_RET_LAST();
-  }
   if (Cout <= 32) hipLaunchKernelGGL((halo3x3_kernel<1, T, WB>), dim3(grid), dim3(256), 0, stream, a);
   else if (Cout <= 64) hipLaunchKernelGGL((halo3x3_kernel<2, T, WB>), dim3(grid), dim3(256), 0, stream, a);
   else hipLaunchKernelGGL((halo3x3_kernel<3, T, WB>), dim3(grid), dim3(256), 0, stream, a);
@@ -366,32 +323,4 @@ SEG_API int seg_conv_halo_bf16io_w16(const __bf16* in, long ldin, int N, int H, 
                                      long ldadd, float* stat, hipStream_t stream) {
   return conv_halo_impl<__bf16, true>(in, ldin, N, H, W, Cin, wk, ldk, bias, out, ldout, Cout, add, ldadd, stat,
                                       stream);
-}
-
-// The LDS-halo convs of a 3x3 conv whose input is the raw output of a BatchNorm'd producer
-// (double_conv's first conv, src/unet.py:58-60): in = act(in * in_scale[c] + in_shift[c]) formed
-// on the halo load (padding pixels stay zero), the value the BN-apply pass would have stored --
-// on bf16 storage widened, transformed in fp32 and rounded back (RNE).
-SEG_API int seg_conv_halo_xf(const float* in, long ldin, int N, int H, int W, int Cin, const float* wk, int ldk,
-                             const float* bias, float* out, long ldout, int Cout, const float* add, long ldadd,
-                             float* stat, const float* in_scale, const float* in_shift, int in_act, hipStream_t stream) {
-  if (!in_scale) return (int)hipErrorInvalidValue;
-  return conv_halo_impl(in, ldin, N, H, W, Cin, wk, ldk, bias, out, ldout, Cout, add, ldadd, stat, stream, in_scale,
-                        in_shift, in_act);
-}
-SEG_API int seg_conv_halo_bf16io_xf(const __bf16* in, long ldin, int N, int H, int W, int Cin, const float* wk, int ldk,
-                                    const float* bias, __bf16* out, long ldout, int Cout, const __bf16* add, long ldadd,
-                                    float* stat, const float* in_scale, const float* in_shift, int in_act,
-                                    hipStream_t stream) {
-  if (!in_scale) return (int)hipErrorInvalidValue;
-  return conv_halo_impl(in, ldin, N, H, W, Cin, wk, ldk, bias, out, ldout, Cout, add, ldadd, stat, stream, in_scale,
-                        in_shift, in_act);
-}
-SEG_API int seg_conv_halo_bf16io_xf_w16(const __bf16* in, long ldin, int N, int H, int W, int Cin, const __bf16* wk,
-                                        int ldk, const float* bias, __bf16* out, long ldout, int Cout, const __bf16* add,
-                                        long ldadd, float* stat, const float* in_scale, const float* in_shift,
-                                        int in_act, hipStream_t stream) {
-  if (!in_scale) return (int)hipErrorInvalidValue;
-  return conv_halo_impl<__bf16, true>(in, ldin, N, H, W, Cin, wk, ldk, bias, out, ldout, Cout, add, ldadd, stat,
-                                      stream, in_scale, in_shift, in_act);
 }

@@ -31,16 +31,13 @@
 // Round 4: the same pipeline on 4-wave blocks with 128 x 128 / 128 x 64 / 64 x 128 / 64 x 64
 // tiles (wave tiles 64x64 / 64x32 / 32x64 / 32x32) for the small-image 1x1 convs of the
 // MobileNetV2 encoder (M = 4k-65k rows at bs=32: the generic register-staged kernel keeps one
-// K chunk in flight and ran them at 0.4-1.5 TB/s), and for 1x1 convs the producer's lazy
-// BatchNorm + activation applied to the A fragments after their LDS read (XF: LDS-DMA cannot
-// transform on the way in; rows beyond M and k beyond K meet zero weights or are never stored,
-// so the transform needs no mask for 1x1).
+// K chunk in flight and ran them at 0.4-1.5 TB/s).  (Round 4's lazy-BN fragment transform for
+// 1x1 consumers measured slower than the generic kernels and was removed in round 5.)
 #include "common.h"
 
 namespace {
 
 constexpr int kBK = 64;             // K step (bf16 elements) = one 128-byte operand row
-constexpr int kXfMax = 2048;      // XF: input channels whose coefficients fit in LDS
 
 __device__ __attribute__((aligned(16))) unsigned g_zero_row[4];  // 16 zero bytes
 
@@ -55,7 +52,6 @@ struct Igemm2Args {
   unsigned* cnt;                    // split-K: [tiles] tickets (zero before the first launch; left zero)
   int N, H, W, Cin, Cout, ks, pad;
   int K, M, nsteps, steps_per_split, splits, tiles_m, tiles_n;
-  const float* xs; const float* xb; int xact;  // XF: A = act(in * xs[k] + xb[k]) (1x1 only)
 };
 
 #ifndef SEG_IG2_NODMA
@@ -87,30 +83,20 @@ __device__ __forceinline__ void wait_vm() {  // s_waitcnt vmcnt(N), other counte
   __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | 0x0F70);  // vmcnt is 6 bits, split 3:0 / 15:14
 }
 
-template <int BM, int BN, int WM, int WN, int KS, bool XF = false>
+template <int BM, int BN, int WM, int WN, int KS>
 __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void igemm2_kernel(Igemm2Args a) {
   constexpr int NW = (BM / WM) * (BN / WN), kThreads = 64 * NW, WAVES_N = BN / WN;
   constexpr int MI = WM / 32, NI = WN / 32;
   static_assert(NW == 4 || NW == 8, "4 or 8 waves");
   static_assert(BM % (8 * NW) == 0 && BN % (8 * NW) == 0, "whole DMA instructions per wave");
-  static_assert(!XF || KS == 1, "the fragment transform is for 1x1 convs");
   constexpr int A_BYTES = BM * 128, STAGE = (BM + BN) * 128;
   constexpr int NA = BM / (8 * NW), NB = BN / (8 * NW);  // DMA instructions per wave per K step
   constexpr int CSR = BN + 4;                // epilogue band row stride (floats)
   constexpr int NSTAGE = 3;                  // LDS buffers: two K steps in flight while one computes
-  constexpr int XF_BYTES = XF ? 2 * kXfMax * 4 : 0;
-  constexpr int RING = NSTAGE * STAGE > WM * CSR * 4 ? NSTAGE * STAGE : WM * CSR * 4;
-  constexpr int SMEM = RING + XF_BYTES;
+  constexpr int SMEM = NSTAGE * STAGE > WM * CSR * 4 ? NSTAGE * STAGE : WM * CSR * 4;
   __shared__ __attribute__((aligned(1024))) char smem[SMEM];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  float* xsL = reinterpret_cast<float*>(smem + RING);  // XF: [kXfMax] scales, then [kXfMax] shifts
-  if constexpr (XF) {
-    for (int k = tid * 4; k < a.K; k += kThreads * 4) {
-      *reinterpret_cast<f32x4*>(xsL + k) = ld4(a.xs + k);
-      *reinterpret_cast<f32x4*>(xsL + kXfMax + k) = ld4(a.xb + k);
-    }
-  }
   const int wm0 = (wave / WAVES_N) * WM, wn0 = (wave % WAVES_N) * WN;
   // a tile's K slices are adjacent logical ids: the same XCD (and L2) combines them
   const int lid = xcd_swizzle(blockIdx.x, gridDim.x);
@@ -201,7 +187,6 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void igemm2_kernel(Igem
       for (int r = 0; r < 16; ++r) acc[mi][ni][r] = 0.f;
 
   const int fr = lane & 31, fh = lane >> 5;
-  int kx = k_beg;  // XF: first k of the step being computed
   auto compute = [&](int buf) {
     const char* As = smem + buf * STAGE;
     const char* Bs = As + A_BYTES;
@@ -219,21 +204,6 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void igemm2_kernel(Igem
         const int r = wn0 + ni * 32 + fr;
         bfr[st][ni] = *reinterpret_cast<const bf16x8*>(Bs + r * 128 + 16 * (chunk ^ ((r >> 1) & 7)));
       }
-      if constexpr (XF) {  // the producer's BN + activation on the fragment (as the apply pass stores it)
-        const int k = kx + 8 * chunk;
-        const f32x4 s0 = *reinterpret_cast<const f32x4*>(xsL + k), s1 = *reinterpret_cast<const f32x4*>(xsL + k + 4);
-        const f32x4 b0 = *reinterpret_cast<const f32x4*>(xsL + kXfMax + k);
-        const f32x4 b1 = *reinterpret_cast<const f32x4*>(xsL + kXfMax + k + 4);
-#pragma unroll
-        for (int mi = 0; mi < MI; ++mi) {
-          const bf16x8 q = af[st][mi];
-          const f32x4 lo = seg_bn_act4(__builtin_convertvector(__builtin_shufflevector(q, q, 0, 1, 2, 3), f32x4), s0,
-                                       b0, a.xact);
-          const f32x4 hi = seg_bn_act4(__builtin_convertvector(__builtin_shufflevector(q, q, 4, 5, 6, 7), f32x4), s1,
-                                       b1, a.xact);
-          af[st][mi] = seg_cat8(__builtin_convertvector(lo, bf16x4), __builtin_convertvector(hi, bf16x4));
-        }
-      }
     };
     frag(0, 0);
 #pragma unroll
@@ -250,7 +220,6 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void igemm2_kernel(Igem
           acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[ks & 1][mi], bfr[ks & 1][ni], acc[mi][ni], 0, 0, 0);
         }
     }
-    kx += kBK;
   };
 
   // ---- K loop: buffer it % 3 holds step it; steps it + 1 and it + 2 stay in flight meanwhile
@@ -259,10 +228,6 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void igemm2_kernel(Igem
   if (nst > 0) issue(0);
   if (nst > 1) issue(1);
   if (nst > 2) issue(2);
-  if constexpr (XF) {  // the coefficient stores above: visible to every wave before the first compute
-    wait_lgkm0();
-    raw_barrier();
-  }
   for (int it = 0; it < nst; ++it) {
     const int ahead = min(nst - 1 - it, 2);  // steps issued beyond this one
     if (ahead == 2) wait_vm<2 * (NA + NB)>();
@@ -531,14 +496,12 @@ SEG_API int seg_conv_igemm2_plan(long M, int Cout, int Cin, int ks, long* out) {
 
 static int igemm2_impl(const __bf16* in, long ldin, int N, int H, int W, int Cin, const __bf16* wk, int ldk,
                        const float* bias, __bf16* out, long ldout, int Cout, int ks, const __bf16* add, long ldadd,
-                       float* stat, float* work, const float* xs, const float* xb, int xact, hipStream_t stream) {
+                       float* stat, float* work, hipStream_t stream) {
   const long M = (long)N * H * W;
   const Plan2 p = plan2(M, Cout, Cin, ks, g_ig2_force);
   if (p.tile < 0 || (ldin & 7) || (ldk & 7) || (ldout & 7) || (add && (ldadd & 7)) || ldk < ks * ks * Cin ||
       ((uintptr_t)in & 15) || ((uintptr_t)wk & 15) || ((uintptr_t)out & 15) || (add && ((uintptr_t)add & 15)) ||
       (p.splits > 1 && !work) || M > 0x7fffffffL)
-    return (int)hipErrorInvalidValue;
-  if (xs && (ks != 1 || !xb || Cin > kXfMax || xact < SEG_ACT_NONE || xact > SEG_ACT_RELU6))
     return (int)hipErrorInvalidValue;
   Igemm2Args a;
   a.in = in; a.ldin = ldin; a.wk = wk; a.ldk = ldk; a.bias = bias; a.add = add; a.ldadd = ldadd;
@@ -548,13 +511,11 @@ static int igemm2_impl(const __bf16* in, long ldin, int N, int H, int W, int Cin
   a.N = N; a.H = H; a.W = W; a.Cin = Cin; a.Cout = Cout; a.ks = ks; a.pad = (ks - 1) / 2;
   a.K = ks * ks * Cin; a.M = (int)M; a.nsteps = p.nsteps; a.steps_per_split = p.steps_per_split;
   a.splits = p.splits; a.tiles_m = p.tiles_m; a.tiles_n = p.tiles_n;
-  a.xs = xs; a.xb = xb; a.xact = xact;
   const int grid = p.tiles_m * p.tiles_n * p.splits;
 #define SEG_I2(BM, BN, WM, WN)                                                                                   \
   do {                                                                                                          \
     constexpr int nt = 64 * (BM / WM) * (BN / WN);                                                              \
-    if (xs) hipLaunchKernelGGL((igemm2_kernel<BM, BN, WM, WN, 1, true>), dim3(grid), dim3(nt), 0, stream, a);   \
-    else if (ks == 3) hipLaunchKernelGGL((igemm2_kernel<BM, BN, WM, WN, 3>), dim3(grid), dim3(nt), 0, stream, a); \
+    if (ks == 3) hipLaunchKernelGGL((igemm2_kernel<BM, BN, WM, WN, 3>), dim3(grid), dim3(nt), 0, stream, a); \
     else hipLaunchKernelGGL((igemm2_kernel<BM, BN, WM, WN, 1>), dim3(grid), dim3(nt), 0, stream, a);            \
   } while (0)
   switch (p.tile) {
@@ -576,18 +537,5 @@ static int igemm2_impl(const __bf16* in, long ldin, int N, int H, int W, int Cin
 SEG_API int seg_conv_igemm2_bf16io(const __bf16* in, long ldin, int N, int H, int W, int Cin, const __bf16* wk,
                                    int ldk, const float* bias, __bf16* out, long ldout, int Cout, int ks,
                                    const __bf16* add, long ldadd, float* stat, float* work, hipStream_t stream) {
-  return igemm2_impl(in, ldin, N, H, W, Cin, wk, ldk, bias, out, ldout, Cout, ks, add, ldadd, stat, work, nullptr,
-                     nullptr, 0, stream);
-}
-
-// seg_conv_igemm2_bf16io of a 1x1 conv whose input is the raw output of a BatchNorm'd producer:
-// A = act(in * in_scale[c] + in_shift[c]) formed on the fragments (rounded to bf16 as the apply
-// pass would store it); Cin <= 2048.
-SEG_API int seg_conv_igemm2_bf16io_xf(const __bf16* in, long ldin, int N, int H, int W, int Cin, const __bf16* wk,
-                                      int ldk, const float* bias, __bf16* out, long ldout, int Cout, int ks,
-                                      const __bf16* add, long ldadd, float* stat, float* work, const float* in_scale,
-                                      const float* in_shift, int in_act, hipStream_t stream) {
-  if (!in_scale) return (int)hipErrorInvalidValue;
-  return igemm2_impl(in, ldin, N, H, W, Cin, wk, ldk, bias, out, ldout, Cout, ks, add, ldadd, stat, work, in_scale,
-                     in_shift, in_act, stream);
+  return igemm2_impl(in, ldin, N, H, W, Cin, wk, ldk, bias, out, ldout, Cout, ks, add, ldadd, stat, work, stream);
 }

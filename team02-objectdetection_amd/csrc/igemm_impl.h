@@ -43,8 +43,8 @@ struct IgemmArgs {
   // dz and dz (by - bmu), dz = out act'(by bsc + bsh) on the values as stored, into bpart
   // [tilesM][2][Cout] for seg_bn_bwd_finalize_tiles -- the reduction pass over dA disappears
   const void* by; long ldby; const float* bsc; const float* bsh; const float* bmu; int bact; float* bpart;
-  // split-K with the combine in the launch (part set, the whole grid co-resident): tile counters
-  // [2][tilesM * tilesN] (arrive, leave; zero before the first launch, re-armed by the last leaver)
+  // split-K with the combine in the launch (part set, the whole grid co-resident, <= 64 splits): seg_tile_combine's
+  // words, [tilesM * tilesN][4] (zero before the first launch, re-armed by the tile's last leaver)
   unsigned* kcnt;
 };
 
@@ -470,45 +470,35 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void igemm_conv_kernel(
         }
     }
     if (!ic) return;
-    // in-launch combine (the host launches this form only when the whole grid is co-resident): every split
-    // block of the tile waits for the tile's other splits, then applies splitk_reduce_kernel's epilogue to its
-    // 1/splits share of the tile -- the same fixed-order sum, so bitwise the two-launch result
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    const int ntl = gridDim.x, S = gridDim.y, z = blockIdx.y;
-    unsigned* arrive = a.kcnt + lid;
-    unsigned* leave = a.kcnt + ntl + lid;
-    if (tid == 0) {
-      __hip_atomic_fetch_add(arrive, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      while (__hip_atomic_load(arrive, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (unsigned)S)
-        __builtin_amdgcn_s_sleep(1);
-    }
-    __syncthreads();
-    constexpr int E = BM * BN;
-    const int e0 = (int)((long)z * E / S), e1 = (int)((long)(z + 1) * E / S);
-    const long total = (long)a.M * a.Cout;
-    for (int e = e0 + tid; e < e1; e += NT) {
-      const int r = e / BN, c = e - r * BN, row = m0 + r, col = n0 + c;
-      if (row >= a.M || col >= a.Cout) continue;
-      const long i = (long)row * a.Cout + col;
-      float v = 0.f;  // the splits in order, 16 loads in flight at a time
-      for (int z0 = 0; z0 < S; z0 += 16) {
-        float q[16];
+    // in-launch combine (the host launches this form only when the whole grid is co-resident): the tile's splits
+    // combine it together, each block applying splitk_reduce_kernel's epilogue to a 1/splits share (piece) of the
+    // tile -- the same fixed-order sum, so bitwise the two-launch result; seg_tile_combine hands the piece of a block
+    // that could not wait to the tile's last arrival instead of letting it spin on a peer
+    const int S = gridDim.y, z = blockIdx.y;
+    auto piece = [&](int pz) {
+      constexpr int E = BM * BN;
+      const int e0 = (int)((long)pz * E / S), e1 = (int)((long)(pz + 1) * E / S);
+      const long total = (long)a.M * a.Cout;
+      for (int e = e0 + tid; e < e1; e += NT) {
+        const int r = e / BN, c = e - r * BN, row = m0 + r, col = n0 + c;
+        if (row >= a.M || col >= a.Cout) continue;
+        const long i = (long)row * a.Cout + col;
+        float v = 0.f;  // the splits in order, 16 loads in flight at a time
+        for (int z0 = 0; z0 < S; z0 += 16) {
+          float q[16];
 #pragma unroll
-        for (int j = 0; j < 16; ++j) q[j] = z0 + j < S ? seg_ld_wt(a.part + (z0 + j) * total + i) : 0.f;
+          for (int j = 0; j < 16; ++j) q[j] = z0 + j < S ? seg_ld_wt(a.part + (z0 + j) * total + i) : 0.f;
 #pragma unroll
-        for (int j = 0; j < 16; ++j)
-          if (z0 + j < S) v += q[j];
+          for (int j = 0; j < 16; ++j)
+            if (z0 + j < S) v += q[j];
+        }
+        if (a.bias) v += a.bias[col];
+        if (add) v += (float)add[(long)row * a.ldadd + col];
+        if (a.act) v = seg_act(v, a.act);
+        out[(long)row * a.ldout + col] = static_cast<IT>(v);
       }
-      if (a.bias) v += a.bias[col];
-      if (add) v += (float)add[(long)row * a.ldadd + col];
-      if (a.act) v = seg_act(v, a.act);
-      out[(long)row * a.ldout + col] = static_cast<IT>(v);
-    }
-    if (tid == 0 && __hip_atomic_fetch_add(leave, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (unsigned)S - 1) {
-      __hip_atomic_store(arrive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(leave, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
+    };
+    seg_tile_combine(a.kcnt + 4 * lid, S, z, kSegCombineSpin, reinterpret_cast<int*>(smem), piece);
     return;
   }
   float bcol[NI];
@@ -742,14 +732,14 @@ int launch_igemm_bk(IgemmArgs a, int ks, hipStream_t s) {
                   (sizeof(IT) == 4 || (a.Cin % 8 == 0 && a.ldin % 8 == 0));  // bf16 A: 16-byte slots
   constexpr int NT = 64 * (BM / WM) * (BN / WN);
   if (a.xs && !ut) return (int)hipErrorInvalidValue;  // input transform: the uniform-tap loader only (Cin >= BK)
-  if (a.kcnt) {  // in-launch split-K combine: only when the whole grid is co-resident (it spins on the tile's splits)
+  if (a.kcnt) {  // in-launch split-K combine: only when the whole grid is co-resident (its splits combine together)
     int occ = 0;
     const void* fn = ks == 1 ? (ut ? (const void*)igemm_conv_kernel<BM, BN, WM, WN, 1, BK, true, OT, IT, WB, false>
                                    : (const void*)igemm_conv_kernel<BM, BN, WM, WN, 1, BK, false, OT, IT, WB, false>)
                              : (ut ? (const void*)igemm_conv_kernel<BM, BN, WM, WN, 3, BK, true, OT, IT, WB, false>
                                    : (const void*)igemm_conv_kernel<BM, BN, WM, WN, 3, BK, false, OT, IT, WB, false>);
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, fn, NT, 0) != hipSuccess ||
-        (long)grid * splits > (long)occ * seg_num_cus()) {
+        (long)grid * splits > (long)occ * seg_num_cus() || splits > 64) {
       (void)hipGetLastError();
       a.kcnt = nullptr;
     }

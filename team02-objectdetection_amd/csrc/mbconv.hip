@@ -44,7 +44,7 @@ struct MbArgs {
   int N, H, W, Cin, Ch, Cout, Ho, Wo;
   int tiles_w, tiles_h, ntiles, splits, hper;  // hper: hidden channels per split (multiple of HC)
   float* work; unsigned* cnt;         // splits > 1: partials [ntiles][splits][TP][Cout], counters [2][ntiles]
-  int spin;                           // the whole grid is resident: every block of a tile helps combine it
+  int spin;                           // the whole grid is resident: the blocks of a tile combine it together
 };
 
 __device__ __attribute__((aligned(16))) float g_mb_zero[4];
@@ -66,7 +66,7 @@ __global__ __launch_bounds__(kThreads) void mbconv_f16_kernel(MbArgs a) {
   __shared__ __attribute__((aligned(16))) _Float16 Wps[kMaxCout * (HC + 8)];      // the chunk's project columns
   __shared__ __attribute__((aligned(16))) float Es[G::HPP * (HC + 1)];
   __shared__ __attribute__((aligned(16))) _Float16 Ds[G::TP * (HC + 8)];
-  __shared__ int word;
+  __shared__ int word[2];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int t = blockIdx.x, split = blockIdx.y;
   const int tw_i = t % a.tiles_w, rest = t / a.tiles_w;
@@ -290,36 +290,14 @@ __global__ __launch_bounds__(kThreads) void mbconv_f16_kernel(MbArgs a) {
       a.out[orow * a.ldo + co] = v;
     }
   };
-  if (a.spin) {
-    // the whole grid is resident (host check): every block of the tile waits for all of its splits, then combines
-    // its 1/splits share of the tile's elements (the splits summed in order: deterministic); the last block to
-    // leave re-arms both counters
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's partial has landed
-    __syncthreads();
-    unsigned* arrive = a.cnt + t;
-    unsigned* leave = a.cnt + a.ntiles + t;
-    if (tid == 0) {
-      __hip_atomic_fetch_add(arrive, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      while (__hip_atomic_load(arrive, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (unsigned)a.splits)
-        __builtin_amdgcn_s_sleep(1);
-    }
-    __syncthreads();
-    const int e0 = (int)((long)split * ne / a.splits), e1 = (int)((long)(split + 1) * ne / a.splits);
-    for (int e = e0 + tid; e < e1; e += kThreads) {
-      emit(e, split_sum(e));
-    }
-    if (tid == 0 &&
-        __hip_atomic_fetch_add(leave, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (unsigned)a.splits - 1) {
-      __hip_atomic_store(arrive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(leave, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    return;
-  }
-  if (!seg_last_arrival(a.cnt + t, (unsigned)a.splits, &word)) return;
-  // (grid larger than the chip) the last block of the tile combines all of it
-  for (int e = tid; e < ne; e += kThreads) {
-    emit(e, split_sum(e));
-  }
+  // the tile's splits combine it together when the grid is co-resident (a.spin), each its 1/splits share of the
+  // tile's elements (the splits summed in order: deterministic); a block that cannot wait -- or, when the grid is
+  // larger than the chip, every block but the last -- leaves its share to the tile's last arrival
+  auto piece = [&](int pz) {
+    const int e0 = (int)((long)pz * ne / a.splits), e1 = (int)((long)(pz + 1) * ne / a.splits);
+    for (int e = e0 + tid; e < e1; e += kThreads) emit(e, split_sum(e));
+  };
+  seg_tile_combine(a.cnt + 4 * t, a.splits, split, a.spin ? kSegCombineSpin : 0, word, piece);
 }
 
 int g_mb_cap = SEG_MBCONV_CAP;  // blocks per launch the hidden splits aim for (seg_mbconv_tune)
@@ -361,7 +339,7 @@ SEG_API int seg_mbconv_ok(int Cin, int Ch, int Cout, int stride, int expand) {
 SEG_API long seg_mbconv_work_floats(int N, int H, int W, int Ch, int Cout, int stride, int* counters) {
   int tw, th, sp, hp, tp;
   mb_plan(N, H, W, Ch, stride, &tw, &th, &sp, &hp, &tp);
-  if (counters) *counters = 2 * N * tw * th;
+  if (counters) *counters = 4 * N * tw * th;
   return sp > 1 ? (long)N * tw * th * sp * tp * Cout : 0;
 }
 
@@ -386,9 +364,10 @@ SEG_API int seg_mbconv_f16(const float* x, long ldx, int N, int H, int W, int Ci
   a.ntiles = N * a.tiles_w * a.tiles_h;
   a.work = work; a.cnt = cnt;
   if (a.splits > 1 && (!work || !cnt)) return (int)hipErrorInvalidValue;
+  if (a.splits > 64) return (int)hipErrorInvalidValue;  // seg_tile_combine's claim mask
   const dim3 grid(a.ntiles, a.splits);
   const bool e = we != nullptr;
-  {  // spin combine only when the whole grid is co-resident
+  {  // the splits wait for each other (bounded) only when the whole grid is co-resident
     const void* fn = stride == 1 ? (e ? (const void*)mbconv_f16_kernel<1, true> : (const void*)mbconv_f16_kernel<1, false>)
                                  : (e ? (const void*)mbconv_f16_kernel<2, true> : (const void*)mbconv_f16_kernel<2, false>);
     int occ = 0;

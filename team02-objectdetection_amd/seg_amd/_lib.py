@@ -80,6 +80,7 @@ PROTOTYPES = {
     "seg_resize_u8": (_I, [_V, _I, _I, _I, _L, _V, _I, _I, _I, _V, _V]),
     "seg_augment": (_I, [_V, _V, _I, _I, _I, _V, _F, _F, _F, _F, _F, _F, _V, _V, _V]),
     "seg_adam_step": (_I, [_V, _V, _I, _I, _F, _F, _F, _F, _V]),
+    "seg_adam_step_skip": (_I, [_V, _V, _I, _I, _F, _F, _F, _F, _V, _V]),
     # launch tape (csrc/tape.hip, seg_amd/tape.py)
     "seg_tape_fn_index": (_I, [ctypes.c_char_p]),
     "seg_tape_fn_nargs": (_I, [_I]),
@@ -96,21 +97,9 @@ PROTOTYPES = {
     "seg_conv_igemm2_bf16io": (_I, [_V, _L, _I, _I, _I, _I, _V, _I, _V, _V, _L, _I, _I, _V, _L, _V, _V, _V]),
     "seg_igemm2_force_tile": (_I, [_I]),
     "seg_igemm2_tune": (_I, [_I, _I]),
-    "seg_conv_halo2_ok": (_I, [_I, _I, _I, _I, _I]),
     "seg_conv_wgrad2_ok": (_I, [_I, _I, _I, _I, _I]),
     "seg_conv_wgrad2_blocks": (_I, [_I, _I, _I]),
     "seg_conv_wgrad2_bf16io": (_I, [_V, _L, _V, _L, _I, _I, _I, _I, _I, _V, _V]),
-    "seg_conv_halo2_row_tiles": (_I, [_I, _I, _I]),
-    "seg_dw2_ok": (_I, [_I, _I]),
-    "seg_dw2_stat_tiles": (_I, [_I, _I, _I, _I, _V]),
-    "seg_dw2_fwd_bf16io": (_I, [_V, _L, _I, _I, _I, _I, _V, _V, _I, _V, _V, _L, _I, _I, _I, _V, _V]),
-    "seg_dw2_wgrad_blocks": (_L, [_I, _I, _I, _I, _I, _I]),
-    "seg_dw2_dgrad_tiles": (_I, [_I, _I, _I]),
-    "seg_dw2_dgrad_bn_bf16io": (_I, [_V, _L, _I, _I, _I, _I, _V, _V, _L, _I, _I, _I, _I,
-                                     _V, _L, _V, _V, _V, _V, _I,
-                                     _V, _L, _V, _V, _V, _V, _V, _I, _V, _V, _V, _V, _V, _V]),
-    "seg_dw2_wgrad_bn_bf16io": (_I, [_V, _L, _V, _L, _I, _I, _I, _I, _V, _V, _I, _I, _I, _I, _V,
-                                     _V, _L, _V, _V, _V, _V, _I, _V]),
     "seg_bn_bwd_coef": (_I, [_V, _L, _V, _L, _L, _I, _V, _V, _V, _V, _V, _I, _V, _V, _V, _V, _V]),
     "seg_bn_bwd_apply": (_I, [_V, _L, _V, _L, _L, _I, _V, _V, _V, _I, _V, _V, _L, _V]),
     "seg_bn_bwd_finalize_tiles": (_I, [_V, _I, _L, _I, _V, _V, _V, _V, _V, _V]),
@@ -136,14 +125,12 @@ for _n in ("seg_add", "seg_bn_stats", "seg_bn_apply", "seg_bn_backward", "seg_co
            "seg_upsample_to_nchw", "seg_nchw_to_nhwc", "seg_maxpool2_fwd", "seg_maxpool2_bwd"):
     PROTOTYPES[_n + "_bf16io"] = PROTOTYPES[_n]
 PROTOTYPES["seg_conv_igemm_bf16io"] = PROTOTYPES["seg_conv_igemm"]
-PROTOTYPES["seg_dw2_dgrad_bf16io"] = PROTOTYPES["seg_dw_dgrad"]
 PROTOTYPES["seg_bn_bwd_coef_bf16io"] = PROTOTYPES["seg_bn_bwd_coef"]
 PROTOTYPES["seg_conv_igemm_bnout_bf16io"] = PROTOTYPES["seg_conv_igemm_bnout"]
 PROTOTYPES["seg_conv_igemm_bf16_ic"] = PROTOTYPES["seg_conv_igemm_act_ic"]
 PROTOTYPES["seg_conv_igemm_f16_ic"] = PROTOTYPES["seg_conv_igemm_act_ic"]
 PROTOTYPES["seg_conv_igemm_bnout_bf16io_w16"] = PROTOTYPES["seg_conv_igemm_bnout"]
 PROTOTYPES["seg_bn_bwd_apply_bf16io"] = PROTOTYPES["seg_bn_bwd_apply"]
-PROTOTYPES["seg_dw2_wgrad_bf16io"] = PROTOTYPES["seg_dw_wgrad"]
 PROTOTYPES["seg_conv_wgrad_bf16io"] = PROTOTYPES["seg_conv_wgrad"]
 # lazy-BN (input transform) variants: + in_scale, in_shift, in_act before the stream
 for _n in ("seg_conv_igemm", "seg_conv_wgrad"):
@@ -153,12 +140,8 @@ for _n in ("seg_conv_igemm", "seg_conv_wgrad"):
 PROTOTYPES["seg_conv_halo_bf16io"] = PROTOTYPES["seg_conv_halo"]
 PROTOTYPES["seg_conv_igemm_bf16io_w16"] = PROTOTYPES["seg_conv_igemm"]
 PROTOTYPES["seg_conv_halo_bf16io_w16"] = PROTOTYPES["seg_conv_halo"]
-PROTOTYPES["seg_conv_halo2_bf16io"] = PROTOTYPES["seg_conv_halo"]
-PROTOTYPES["seg_conv_igemm2_bf16io_xf"] = (_I, PROTOTYPES["seg_conv_igemm2_bf16io"][1][:-1] + [_V, _V, _I, _V])
 PROTOTYPES["seg_conv_igemm_bf16io_xf_w16"] = PROTOTYPES["seg_conv_igemm_bf16io_xf"]
 PROTOTYPES["seg_conv_pw_bf16io"] = PROTOTYPES["seg_conv_pw"]
-for _sfx in ("_xf", "_bf16io_xf", "_bf16io_xf_w16"):  # + in_scale, in_shift, in_act before the stream
-    PROTOTYPES["seg_conv_halo" + _sfx] = (_I, PROTOTYPES["seg_conv_halo"][1][:-1] + [_V, _V, _I, _V])
 
 _lock = threading.Lock()
 _lib = None

@@ -22,7 +22,10 @@ Mechanism (no autograd hooks needed -- the engine IS the backward):
     makes the compute stream wait for the outstanding all-reduces (RCCL
     averages in the reduction, ncclAvg); autograd receives views of a copy of
     each bucket (`autograd_grads`), never the bucket itself;
-  * BN running statistics are views of one flat tensor: one broadcast per step.
+  * BN running statistics are views of one flat tensor: one broadcast per step;
+  * the fused loss's out-of-range label count rides in one extra slot of the last
+    bucket, so after the all-reduce every rank holds the mean count (non-zero iff
+    any rank saw a bad label) with no collective of its own (label_flag).
 The unused `backbone.classifier` parameters never receive gradients (as in
 the reference, where Adam skips them), so no find_unused_parameters dance.
 """
@@ -58,6 +61,7 @@ class DataParallel(nn.Module):
         self._order = None
         self._bn_flat = None
         self._replace_grads = False  # a bucket folded held .grad values in (see _launch)
+        self._flag_sent = False      # this step's label count went out with the last bucket (label_flag)
         self._hooks = None           # CPU path: post-accumulate-grad hooks (_arm_cpu)
         self._cpu_armed = False
         module.__dict__["_segamd_sync"] = self  # plain attribute: not a registered submodule
@@ -117,8 +121,8 @@ class DataParallel(nn.Module):
         if cur.params:
             buckets.append(cur)
         dev = ordered_params[0].device
-        for b in buckets:
-            b.buf = torch.zeros(b.numel, device=dev, dtype=ordered_params[0].dtype)
+        for b in buckets:  # the last bucket carries one more float: the batch's out-of-range label count
+            b.buf = torch.zeros(b.numel + (b is buckets[-1]), device=dev, dtype=ordered_params[0].dtype)
         self._buckets = buckets
 
     def _ensure_plan(self, x):
@@ -163,6 +167,15 @@ class DataParallel(nn.Module):
         if held:
             torch._foreach_add_([v for v, _ in held], [g for _, g in held])
             self._replace_grads = True
+        if b is self._buckets[-1]:
+            # piggyback the fused loss's out-of-range label count (written by the forward's loss kernel, earlier on
+            # this stream): averaged with the gradients, no collective of its own
+            st = self.module.__dict__.get("_segamd_last_stats")
+            if st is not None and st.device == b.buf.device:
+                b.buf[-1:].copy_(st[2:3])
+            else:
+                b.buf[-1:].zero_()
+            self._flag_sent = True
         op = dist.ReduceOp.AVG if self._avg else dist.ReduceOp.SUM
         b.handle = dist.all_reduce(b.buf, op=op, group=self.pg, async_op=True)
 
@@ -170,6 +183,15 @@ class DataParallel(nn.Module):
         for b in self._buckets:
             b.pending = len(b.params)
             b.handle = None
+        self._flag_sent = False
+
+    def label_flag(self):
+        """The out-of-range label count of this step's fused loss, averaged over the ranks (so non-zero on every
+        rank iff any rank saw such a label): a [1] fp32 device view, valid in stream order after
+        finish_gradient_sync(); None when this step's buckets did not go out (no_sync, unfused criterion path)."""
+        if self._buckets is None or not self._flag_sent or self.module.__dict__.get("_segamd_last_stats") is None:
+            return None
+        return self._buckets[-1].buf[-1:]
 
     def finish_gradient_sync(self):
         """Wait (stream-ordered) for every bucket's all-reduce; the buckets then hold the mean."""

@@ -32,11 +32,11 @@ from ._lib import call, query as _query
 
 # Host-only size / plan queries of the C ABI are pure functions of their integer
 # arguments: memoised, so a training step does not pay a ctypes call for each of them.
+# (Not the implicit GEMM's tile-dependent queries -- seg_conv_igemm_tiles / _row_tiles / _bnout_ok, igemm2's
+# plan: a forced tile (force_igemm_tile) changes them)
 _PURE_QUERIES = {"seg_chan_workspace_floats", "seg_conv_wgrad_splits", "seg_conv_wgrad_splits_bf16", "seg_dw_wgrad_blocks",
                  "seg_conv_igemm_splits", "seg_ce_workspace_floats", "seg_conv_wino_row_tiles", "seg_conv_wino_tile_rows",
-                 "seg_conv_halo_row_tiles", "seg_conv_wino_wgrad_splits", "seg_dw2_ok",
-                 "seg_dw2_wgrad_blocks", "seg_dw2_dgrad_tiles", "seg_conv_igemm_bnout_ok",
-                 "seg_mbconv_ok", "seg_conv_igemm_tiles"}
+                 "seg_conv_halo_row_tiles", "seg_conv_wino_wgrad_splits", "seg_mbconv_ok"}
 _QCACHE = {}
 
 
@@ -83,6 +83,20 @@ def igemm2_plan(M: int, cout: int, cin: int, ks: int):
         ok = query("seg_conv_igemm2_plan", M, cout, cin, ks, ctypes.addressof(out))
         _IG2[key] = tuple(out) if ok else None
     return _IG2[key]
+
+
+def force_tiles(igemm: int | None = None, igemm2: int | None = None) -> None:
+    """Tuning hook: force the implicit GEMM's (seg_igemm_force_tile) and / or igemm2's (seg_igemm2_force_tile) tile
+    table entry (-1 = the cost model again), and drop every memoised tile-dependent plan (row tiles, igemm2 plans) so
+    the next program walk sizes its workspaces for the tile actually launched.  Plans recorded before the
+    change keep their tapes: release_plans() / a fresh Predictor re-record them."""
+    if igemm is not None:
+        _query("seg_igemm_force_tile", int(igemm))
+    if igemm2 is not None:
+        _query("seg_igemm2_force_tile", int(igemm2))
+    _ROW_TILES.clear()
+    _IG2.clear()
+    _QCACHE.clear()
 
 
 def r8(c: int) -> int:
@@ -187,15 +201,9 @@ class ConvOp:
         # Winograd F(2x2,3x3) (seg_conv_wino) for the forward / data gradient, chosen by
         # seg_conv_wino_pick at pack time; U_f [16][Cout][cin_pad], U_d [16][Cin][r4(Cout)]
         self.wino_f = self.wino_d = self.wino_w = False
-        # LDS-halo direct 3x3 (seg_conv_halo) for the forward / data gradient of narrow convs; the
-        # bf16io persistent LDS-DMA variant (seg_conv_halo2_bf16io) where it applies
+        # LDS-halo direct 3x3 (seg_conv_halo) for the forward / data gradient of narrow convs
         self.halo_f = self.halo_d = False
-        self.h2_f = self.h2_d = False
         self.w2 = False  # weight gradient on seg_conv_wgrad2_bf16io (narrow bf16io 3x3)
-        # bf16io depthwise convs on the LDS-DMA tile kernels (seg_dw2_*_bf16io); dw2_st = the forward's BN
-        # tile partials (row tiles, tile rows) when its tiles divide the output, else None
-        self.dw2 = False
-        self.dw2_st = None
         # bf16 math (Program.math == "bf16"): seg_conv_igemm_bf16 / seg_conv_wgrad_bf16
         self.bf = False
         # bf16io: wk_f / wk_d packed as bf16 for seg_conv_igemm_bf16io_w16 (Program._build_pack)
@@ -233,16 +241,8 @@ class ConvOp:
         if self.kind == "dw":
             i = self.inp
             stat = None
-            if self.dw2:  # LDS-DMA tiles; the output's BN tile partials from the epilogue where the tiles divide it
-                if self.dw2_st is not None and rt.training:
-                    ntiles, tile_rows = self.dw2_st
-                    stat = rt.tmp(ntiles * 2 * self.cout)
-                rt.call("seg_dw2_fwd_bf16io", rt.ptr(i), i.ld, i.N, i.H, i.W, i.C, *self._in_xform(rt),
-                         self.wk_f.data_ptr(), rt.ptr(y), y.ld, y.H, y.W, self.stride,
-                         stat.data_ptr() if stat is not None else None, s)
-            else:
-                rt.call(rt.k("seg_dw_fwd"), rt.ptr(i), i.ld, i.N, i.H, i.W, i.C, *self._in_xform(rt),
-                        self.wk_f.data_ptr(), rt.ptr(y), y.ld, y.H, y.W, self.stride, s)
+            rt.call(rt.k("seg_dw_fwd"), rt.ptr(i), i.ld, i.N, i.H, i.W, i.C, *self._in_xform(rt),
+                    self.wk_f.data_ptr(), rt.ptr(y), y.ld, y.H, y.W, self.stride, s)
         else:
             i = self.inp
             if self.wk_f is None:
@@ -258,8 +258,6 @@ class ConvOp:
                 elif self.wino_f:
                     ntiles = query("seg_conv_wino_row_tiles", y.N, y.H, y.W)
                     tile_rows = query("seg_conv_wino_tile_rows")
-                elif self.h2_f:
-                    ntiles, tile_rows = query("seg_conv_halo2_row_tiles", y.N, y.H, y.W), 256
                 elif self.halo_f:
                     ntiles, tile_rows = query("seg_conv_halo_row_tiles", y.N, y.H, y.W), 256
                 else:
@@ -269,25 +267,20 @@ class ConvOp:
             if self.pw_f:  # thin-K 1x1 (its producer's lazy BN, if any, on load)
                 rt.tcall("igemm1_fwd", self.flops(), rt.k("seg_conv_pw"), rt.ptr(i), i.ld, y.M, self.cin_pad, wk_ptr,
                          ldk, bias, rt.ptr(y), y.ld, self.cout, None, 0, statp, *self._in_xform(rt), s)
-            elif self.h2_f:  # narrow bf16io conv: persistent LDS-DMA halo kernel
-                rt.tcall("igemm3_fwd", self.flops(), "seg_conv_halo2_bf16io", rt.ptr(i), i.ld, i.N, i.H, i.W,
-                         self.cin_pad, wk_ptr, ldk, bias, rt.ptr(y), y.ld, self.cout, None, 0, statp, s)
-            elif self.halo_f:  # (its producer's lazy BN, if any, on the halo load)
-                name = rt.k("seg_conv_halo") + ("_xf" if self.xform is not None else "") + ("_w16" if self.w16_f else "")
+            elif self.halo_f:
+                name = rt.k("seg_conv_halo") + ("_w16" if self.w16_f else "")
                 rt.tcall("igemm3_fwd", self.flops(), name, rt.ptr(i), i.ld, i.N, i.H, i.W, self.cin_pad,
-                         wk_ptr, ldk, bias, rt.ptr(y), y.ld, self.cout, None, 0, statp,
-                         *(self._in_xform(rt) if self.xform is not None else ()), s)
+                         wk_ptr, ldk, bias, rt.ptr(y), y.ld, self.cout, None, 0, statp, s)
             elif self.wino_f:
                 work = rt.tmp(16 * (y.M // 4) * self.cout)
                 rt.tcall("wino3_fwd", self.flops(), "seg_conv_wino", rt.ptr(i), i.ld, i.N, i.H, i.W, self.cin_pad,
                             self.wk_wf.data_ptr(), self.cin_pad, bias, rt.ptr(y), y.ld, self.cout, None, 0, statp,
                             work.data_ptr(), s)
-            elif self.ig2_f is not None:  # bf16io LDS-DMA implicit GEMM (deep 3x3, small-image 1x1)
+            elif self.ig2_f is not None:  # bf16io LDS-DMA implicit GEMM (deep 3x3 convs)
                 work = rt.tmp(self.ig2_f[3], zero=True)
-                xf = self._in_xform(rt) if self.xform is not None else ()
-                rt.tcall(f"igemm{self.ks}_fwd", self.flops(), "seg_conv_igemm2_bf16io" + ("_xf" if xf else ""), rt.ptr(i),
+                rt.tcall(f"igemm{self.ks}_fwd", self.flops(), "seg_conv_igemm2_bf16io", rt.ptr(i),
                          i.ld, i.N, i.H, i.W, self.cin_pad, wk_ptr, ldk, bias, rt.ptr(y), y.ld, self.cout, self.ks, None, 0,
-                         statp, work.data_ptr(), *xf, s)
+                         statp, work.data_ptr(), s)
             elif self.xform is not None:  # a conv applying its producer's lazy BN on load
                 name = "seg_conv_igemm_bf16io_xf" if rt.io else "seg_conv_igemm_bf16_xf" if self.bf else "seg_conv_igemm_xf"
                 if rt.io and self.w16_f:
@@ -372,7 +365,7 @@ class ConvOp:
                 ntl = query("seg_conv_igemm_tiles", M, self.cout)
             bufs = rt._mb[("ic", id(self))] = (
                 torch.empty(splits * M * self.cout if splits > 1 else 1, device=rt.device, dtype=torch.float32),
-                torch.zeros(2 * ntl, device=rt.device, dtype=torch.int32), splits, tile)
+                torch.zeros(4 * ntl, device=rt.device, dtype=torch.int32), splits, tile)
         work, cnt, splits, tile = bufs
         rt.call(_FOLDED_CONV[rt.prog.math] + "_ic", rt.ptr(i), i.ld, i.N, i.H, i.W, self.cin_pad, wk, ldk, bias,
                 rt.ptr(o), o.ld, o.H, o.W, self.cout, self.ks, self.stride, self.pad,
@@ -388,32 +381,6 @@ class ConvOp:
         return st[2 * C:3 * C].data_ptr(), st[3 * C:4 * C].data_ptr(), xf.act
 
     # -- backward
-    def _bin_ok(self, rt, dA) -> bool:
-        """The dw2 data / weight gradients can form this depthwise conv's BN backward on load."""
-        return (self.kind == "dw" and self.dw2 and DW2_BN and dA.ld % 8 == 0 and rt.gptr(dA) % 16 == 0
-                and self.y.ld % 8 == 0 and rt.ptr(self.y) % 16 == 0)
-
-    def _bout(self, rt):
-        """BOUT arguments of the dw2 data gradient (the BatchNorm-backward reduction of the producer whose
-        lazy BN this depthwise conv applies on load), or None -- registers the coefficients for its backward."""
-        p = self.xform
-        if (not DW2_BN or p is None or p.bn is None or not rt.training or p.res is not None or not p.lazy
-                or p.y.key() != self.inp.key() or id(p) not in rt.saved):
-            return None
-        i = self.inp
-        tiles = query("seg_dw2_dgrad_tiles", i.N, i.H, i.W)
-        if tiles > DW2_BN_MAX_TILES:
-            return None
-        C = p.cout
-        mean, invstd, scale, shift = _stat_ptrs(rt.saved[id(p)], C)
-        coef = rt.tmp(3 * C)
-        part = rt.tmp(tiles * 2 * C)
-        cnt = rt.tmp((C + 63) // 64, zero=True)
-        g_w, g_b = rt.grad_param(p.bn.weight), rt.grad_param(p.bn.bias)
-        rt.bn_coef[id(p)] = coef
-        return (rt.ptr(p.y), p.y.ld, scale, shift, mean, p.bn.weight.data_ptr(), invstd, p.act, part.data_ptr(), g_w,
-                g_b, coef.data_ptr(), cnt.data_ptr())
-
     def _bnout(self, rt, i):
         """BN-backward partials from this data gradient's epilogue (seg_conv_igemm_bnout*), when its output
         region is exactly the output of a train-mode BatchNorm layer P: the extra arguments, or None.  P's
@@ -440,7 +407,6 @@ class ConvOp:
 
     def backward(self, rt):
         s, y = rt.stream, self.y
-        bin_ = None
         dA = rt.grad_of(self.out)
         if self.bn is not None:
             if not rt.training:
@@ -449,33 +415,24 @@ class ConvOp:
             st = rt.saved[id(self)]
             mean, invstd, scale, shift = _stat_ptrs(st, C)
             g_w, g_b = rt.grad_param(self.bn.weight), rt.grad_param(self.bn.bias)
-            coef = rt.bn_coef.pop(id(self), None)
+            # bench.py's "bn_bwd" family: algorithmic bytes of a BatchNorm backward = dA and y read once, dY written
+            # once (3 |Y|), credited to the launch that writes dY
+            abytes = 3 * M * C * rt.es
             bp = rt.bn_parts.pop(id(self), None)
+            dY = Act(rt.tmp_buf(M * r4(C)), 0, r4(C), C, y.N, y.H, y.W)
             if bp is not None and bp[2] == rt.wgen.get(self.out.buf):
                 # the reduction's partials came out of the epilogue of the data gradient that completed dA (nothing
                 # wrote the buffer since): finalize them, then the apply
                 coef = rt.tmp(3 * C)
-                rt.call("seg_bn_bwd_finalize_tiles", bp[0].data_ptr(), bp[1], M, C, self.bn.weight.data_ptr(), invstd,
-                        g_w, g_b, coef.data_ptr(), s)
-            if coef is not None:  # the reduction ran elsewhere (a consumer's epilogue): the apply alone
-                dY = Act(rt.tmp_buf(M * r4(C)), 0, r4(C), C, y.N, y.H, y.W)
-                rt.call(rt.k("seg_bn_bwd_apply"), rt.gptr(dA), dA.ld, rt.ptr(y), y.ld, M, C, mean, scale, shift,
-                        self.act, coef.data_ptr(), rt.ptr(dY), dY.ld, s)
-            elif self._bin_ok(rt, dA):
-                # depthwise conv on dw2: the reduction here, the apply formed on load by its data and weight
-                # gradients (BIN) -- dY is never stored
-                coef = rt.tmp(3 * C)
-                work = rt.tmp(query("seg_chan_workspace_floats", M, C))
-                rt.call(rt.k("seg_bn_bwd_coef"), rt.gptr(dA), dA.ld, rt.ptr(y), y.ld, M, C, self.bn.weight.data_ptr(),
-                        mean, invstd, scale, shift, self.act, g_w, g_b, work.data_ptr(), coef.data_ptr(), s)
-                bin_ = (rt.ptr(y), y.ld, scale, shift, mean, coef.data_ptr(), self.act)
-                dY = dA
+                rt.tcall("bn_bwd", 0, "seg_bn_bwd_finalize_tiles", bp[0].data_ptr(), bp[1], M, C,
+                         self.bn.weight.data_ptr(), invstd, g_w, g_b, coef.data_ptr(), s)
+                rt.tcall("bn_bwd", abytes, rt.k("seg_bn_bwd_apply"), rt.gptr(dA), dA.ld, rt.ptr(y), y.ld, M, C, mean,
+                         scale, shift, self.act, coef.data_ptr(), rt.ptr(dY), dY.ld, s)
             else:
-                dY = Act(rt.tmp_buf(M * r4(C)), 0, r4(C), C, y.N, y.H, y.W)
                 work = rt.tmp(query("seg_chan_workspace_floats", M, C) + 3 * C)
-                rt.call(rt.k("seg_bn_backward"), rt.gptr(dA), dA.ld, rt.ptr(y), y.ld, M, C, self.bn.weight.data_ptr(),
-                        mean, invstd, scale, shift, self.act,
-                        g_w, g_b, work.data_ptr(), rt.ptr(dY), dY.ld, s)
+                rt.tcall("bn_bwd", abytes, rt.k("seg_bn_backward"), rt.gptr(dA), dA.ld, rt.ptr(y), y.ld, M, C,
+                         self.bn.weight.data_ptr(), mean, invstd, scale, shift, self.act,
+                         g_w, g_b, work.data_ptr(), rt.ptr(dY), dY.ld, s)
             if self.res is not None:
                 rt.add_pending(self.res, dA)
         else:
@@ -491,14 +448,14 @@ class ConvOp:
                 rt.grad_param(p)
         late = FORK_LATE and not self.first
         if late:  # the data gradient first: the side stream's weight gradient then runs beside
-            self._dgrad(rt, dY, dYp, s, bin_)  # the next layer's memory-bound BN backward, not this dgrad
+            self._dgrad(rt, dY, dYp, s)  # the next layer's memory-bound BN backward, not this dgrad
         ctx, sw = rt.fork()
         with ctx:
-            self._param_grads(rt, dY, dYp, sw, bin_)
+            self._param_grads(rt, dY, dYp, sw)
         if not self.first and not late:
-            self._dgrad(rt, dY, dYp, s, bin_)
+            self._dgrad(rt, dY, dYp, s)
 
-    def _param_grads(self, rt, dY, dYp, s, bin_=None):
+    def _param_grads(self, rt, dY, dYp, s):
         """Bias gradient (column sum of dY), weight gradient (split-K slabs + fixed-order
         reduce) and the DDP readiness hook, all on stream `s`."""
         y, M = self.y, self.y.M
@@ -515,14 +472,7 @@ class ConvOp:
         if self.conv.weight.requires_grad:
             gw = rt.grad_param(self.conv.weight)
             i = self.inp
-            if self.kind == "dw" and self.dw2 and dY.ld % 8 == 0 and dYp % 16 == 0:
-                nblk = query("seg_dw2_wgrad_blocks", y.N, y.H, y.W, self.cout, self.stride, int(bin_ is not None))
-                part = rt.tmp(nblk * 9 * self.cout)
-                rt.call("seg_dw2_wgrad_bn_bf16io", dYp, dY.ld, rt.ptr(i), i.ld, i.N, i.H, i.W, i.C,
-                        *self._in_xform(rt), y.H, y.W, self.stride, part.data_ptr(),
-                        *(bin_ if bin_ is not None else (None, 0, None, None, None, None, 0)), s)
-                rt.call("seg_conv_wgrad_reduce", part.data_ptr(), nblk, gw, self.cout, 1, 3, 1, 0, s)
-            elif self.kind == "dw":
+            if self.kind == "dw":
                 nblk = query("seg_dw_wgrad_blocks", y.N, y.H, y.W, self.cout)
                 part = rt.tmp(nblk * 9 * self.cout)
                 rt.call(rt.k("seg_dw_wgrad"), dYp, dY.ld, rt.ptr(i), i.ld, i.N, i.H, i.W, i.C, *self._in_xform(rt), y.H, y.W,
@@ -554,24 +504,13 @@ class ConvOp:
                 rt.call("seg_conv_wgrad_reduce", part.data_ptr(), splits, gw, self.cout, self.cin, self.ks, 0, 0, s)
         rt.params_done(self.params(), s)
 
-    def _dgrad(self, rt, dY, dYp, s, bin_=None):
-        """Data gradient into the input's gradient region (first writer / fused addend).  bin_: the
-        depthwise conv's BN backward formed on load (dY holds dA; dw2 only)."""
+    def _dgrad(self, rt, dY, dYp, s):
+        """Data gradient into the input's gradient region (first writer / fused addend)."""
         y, i = self.y, self.inp
         if self.kind == "dw":
             acc = rt.begin_write_accumulate(i)
-            dw2 = self.dw2 and dY.ld % 8 == 0 and dYp % 16 == 0 and rt.gptr(i) % 16 == 0
-            if not dw2:
-                assert bin_ is None
-                rt.call(rt.k("seg_dw_dgrad"), dYp, dY.ld, y.N, y.H, y.W, self.cout, self.wk_f.data_ptr(), rt.gptr(i),
-                        i.ld, i.H, i.W, self.stride, acc, s)
-            else:
-                bout = self._bout(rt)
-                rt.call("seg_dw2_dgrad_bn_bf16io", dYp, dY.ld, y.N, y.H, y.W, self.cout, self.wk_f.data_ptr(),
-                        rt.gptr(i), i.ld, i.H, i.W, self.stride, acc,
-                        *(bin_ if bin_ is not None else (None, 0, None, None, None, None, 0)),
-                        *(bout if bout is not None else (None, 0, None, None, None, None, None, 0, None, None, None,
-                                                         None, None)), s)
+            rt.call(rt.k("seg_dw_dgrad"), dYp, dY.ld, y.N, y.H, y.W, self.cout, self.wk_f.data_ptr(), rt.gptr(i),
+                    i.ld, i.H, i.W, self.stride, acc, s)
         else:
             if self.stride != 1:
                 raise NotImplementedError("data gradient of a strided dense conv")
@@ -583,9 +522,6 @@ class ConvOp:
             if self.pw_d and add16:  # thin-K 1x1 data gradient
                 rt.tcall("igemm1_dgrad", self.flops(), rt.k("seg_conv_pw"), dYp, dY.ld, y.M, kin, self.wk_d.data_ptr(),
                          self.ldk_d, None, rt.gptr(i), i.ld, self.cin, add_ptr, add_ld, None, None, None, 0, s)
-            elif self.h2_d:
-                rt.tcall("igemm3_dgrad", self.flops(), "seg_conv_halo2_bf16io", dYp, dY.ld, y.N, y.H, y.W, kin,
-                         self.wk_d.data_ptr(), self.ldk_d, None, rt.gptr(i), i.ld, self.cin, add_ptr, add_ld, None, s)
             elif self.halo_d:
                 rt.tcall("igemm3_dgrad", self.flops(), rt.k("seg_conv_halo") + ("_w16" if self.w16_d else ""), dYp,
                          dY.ld, y.N, y.H, y.W, kin,
@@ -777,20 +713,16 @@ class Program:
         self.ops.append(ConvOp(kind, conv, bn, act, inp, out, y, res, xform))
         return out
 
-    def make_lazy(self, a: Act, pointwise=False, dense3=False):
+    def make_lazy(self, a: Act, pointwise=False):
         """If `a` is the private BN+act output of the last op, drop its buffer and let
         the consumer apply the BN on load; returns the producer op (or None).
         pointwise: the consumer is a 1x1 conv (seg_conv_igemm_xf / seg_conv_wgrad_xf:
-        the uniform-tap loader, 8-channel groups) -- any conv producer; dense3: a 3x3
-        stride-1 conv of the bf16io configuration (seg_conv_halo*_xf / seg_conv_igemm_bf16io_xf
-        / seg_conv_wgrad_bf16io_xf, Cin >= 32 for the uniform-tap loader; not igemm2, whose
-        LDS-DMA staging has no transform step); otherwise a depthwise consumer
-        (seg_dw_fwd / seg_dw_wgrad) of a dense producer."""
+        the uniform-tap loader, 8-channel groups) -- any conv producer; otherwise a
+        depthwise consumer (seg_dw_fwd / seg_dw_wgrad) of a dense producer.  (3x3
+        consumers re-read every input element once per tap: measured slower, round 3.)"""
         op = self.ops[-1] if self.ops else None
         kinds = ("igemm", "dw") if pointwise else ("igemm",)
         if pointwise and not (LAZY_PW and a.C % 8 == 0 and a.C >= 16):
-            return None
-        if dense3 and not (LAZY3 and self.math == "bf16io" and a.C % 8 == 0 and a.C >= 32):
             return None
         if not (isinstance(op, ConvOp) and op.kind in kinds and op.bn is not None and op.res is None
                 and op.out is a and op.y is not a and a.off == 0 and a.ld == r4(a.C)
@@ -824,58 +756,38 @@ class Program:
                 op.wk_f = torch.empty(9 * op.cout, device=dev, dtype=torch.float32)
                 jobs.append((w.data_ptr(), op.wk_f.data_ptr(), op.cout, 1, 3, 9, 2, 1))
                 max_elems = max(max_elems, 9 * op.cout)
-                i, y = op.inp, op.y
-                op.dw2 = (self.math == "bf16io" and DW2 and bool(query("seg_dw2_ok", op.cout, op.stride))
-                          and all(t.ld % 8 == 0 and t.off % 8 == 0 for t in (i, y)))
-                op.dw2_st = None
-                if op.dw2 and op.bn is not None:
-                    rows = ctypes.c_int(0)
-                    nt = query("seg_dw2_stat_tiles", y.N, y.H, y.W, op.stride, ctypes.addressof(rows))
-                    op.dw2_st = (nt, rows.value) if nt else None
                 continue
             y = op.y
             op.bf = self.math in ("bf16", "bf16io")
             if op.bf:
                 # bf16 math: every dense / pointwise conv (fwd, dgrad, wgrad) on the bf16 implicit GEMM
                 op.wino_f = op.wino_d = op.wino_w = op.halo_f = op.halo_d = False
-                op.h2_f = op.h2_d = False
                 # narrow bf16io 3x3 weight gradients on seg_conv_wgrad2_bf16io (SEG_WGRAD2=0: the implicit GEMM)
                 op.w2 = (self.math == "bf16io" and WGRAD2 and op.ks == 3 and op.stride == 1 and op.pad == 1
                          and op.xform is None and op.cin_pad == op.cin and y.ld % 8 == 0 and op.inp.ld % 8 == 0
                          and op.inp.off % 8 == 0
                          and bool(query("seg_conv_wgrad2_ok", y.N, y.H, y.W, op.cin_pad, op.cout)))
                 if self.math == "bf16io" and op.ks == 3 and op.stride == 1 and op.pad == 1:
-                    # narrow convs: the persistent LDS-DMA halo kernel (seg_conv_halo2_bf16io, bf16 packed
-                    # weights resident in LDS) where it applies, else the LDS-halo direct conv
-                    # (seg_conv_halo_bf16io): 8-channel slots
-                    h2 = HALO2 and W16
-                    op.h2_f = (h2 and op.xform is None and op.cin_pad % 8 == 0
-                               and bool(query("seg_conv_halo2_ok", y.N, y.H, y.W, op.cin_pad, op.cout)))
-                    op.h2_d = (h2 and not op.first and r4(op.cout) % 8 == 0
-                               and bool(query("seg_conv_halo2_ok", y.N, y.H, y.W, r4(op.cout), op.cin)))
-                    op.halo_f = (not op.h2_f and op.cin_pad % 8 == 0 and HALO_BF16
+                    # narrow convs: the LDS-halo direct conv (seg_conv_halo_bf16io): 8-channel slots
+                    op.halo_f = (op.cin_pad % 8 == 0 and HALO_BF16
                                  and bool(query("seg_conv_halo_pick", y.N, y.H, y.W, op.cin_pad, op.cout)))
-                    op.halo_d = (not op.h2_d and not op.first and r4(op.cout) % 8 == 0 and HALO_BF16
+                    op.halo_d = (not op.first and r4(op.cout) % 8 == 0 and HALO_BF16
                                  and bool(query("seg_conv_halo_pick", y.N, y.H, y.W, r4(op.cout), op.cin)))
                 # bf16io implicit-GEMM and LDS-halo launches take bf16 packed weights (seg_conv_*_bf16io_w16:
                 # half the weight bytes every M tile / pixel tile re-reads)
                 w16f = w16d = self.math == "bf16io" and W16
                 op.w16_f, op.w16_d = w16f, w16d
-                # the deep convs (3x3, or 1x1 with SEG_IGEMM2=all) on seg_conv_igemm2_bf16io
+                # the deep 3x3 convs on seg_conv_igemm2_bf16io
                 op.ig2_f = op.ig2_d = None
                 # beyond IGEMM2_MAX_ROWS only GEMMs whose N fills the 8-wave tiles (N % 128 == 0: UNet's deep levels)
-                wide = op.ks == 3 and y.M > IGEMM2_MAX_ROWS and IGEMM2_WIDE and IGEMM2 != "all"
-                ig2_ok = (op.ks == 3 and y.M <= IGEMM2_MAX_ROWS) or wide or IGEMM2 == "all" or (
-                    op.ks == 1 and IGEMM2_1X1 and y.M <= IGEMM2_1X1_MAX_ROWS)
-                if w16f and IGEMM2 != "0" and op.stride == 1 and op.pad == op.ks // 2 and ig2_ok:
+                wide = y.M > IGEMM2_MAX_ROWS and IGEMM2_WIDE
+                if w16f and IGEMM2 and op.ks == 3 and op.stride == 1 and op.pad == 1:
                     i = op.inp  # 16-byte rows: ld and channel offset multiples of 8 elements
                     rows16 = i.ld % 8 == 0 and i.off % 8 == 0 and y.ld % 8 == 0 and y.off % 8 == 0
-                    # (a 1x1 consumer of a lazy BN applies it to its A fragments: seg_conv_igemm2_bf16io_xf)
-                    xf_ok = op.xform is None or (op.ks == 1 and op.cin <= 2048)
-                    if (rows16 and not (op.halo_f or op.h2_f) and xf_ok and op.cin_pad == op.cin
+                    if (rows16 and not op.halo_f and op.xform is None and op.cin_pad == op.cin
                             and (not wide or op.cout % 128 == 0)):
                         op.ig2_f = igemm2_plan(y.M, op.cout, op.cin_pad, op.ks)
-                    if (rows16 and not op.first and not (op.halo_d or op.h2_d) and op.cout % 8 == 0
+                    if (rows16 and not op.first and not op.halo_d and op.cout % 8 == 0
                             and (not wide or op.cin % 128 == 0)):
                         op.ig2_d = igemm2_plan(y.M, op.cin, op.cout, op.ks)
                 if w16f:
@@ -1048,13 +960,7 @@ def _inverted_residual(prog, blk: InvertedResidual, inp, out=None):
 def _double_conv(prog, dc, inp, out=None):
     c = dc.conv
     x = prog.conv("igemm", c[0], c[1], ACT_RELU, inp)
-    # bf16io: the second conv applies the first one's BN + ReLU on load (no BN-apply pass, no stored activation)
-    k2 = c[3]
-    dense3 = k2.kernel_size == (3, 3) and k2.stride == (1, 1) and k2.padding == (1, 1) and k2.groups == 1
-    xf = prog.make_lazy(x, dense3=True) if dense3 else None
-    if xf is not None:
-        x = xf.out
-    return prog.conv("igemm", k2, c[4], ACT_RELU, x, out=out, xform=xf)
+    return prog.conv("igemm", c[3], c[4], ACT_RELU, x, out=out)
 
 
 def _up(prog, u, low, cat):
@@ -1204,7 +1110,6 @@ class Run:
         self.bufs = {n: torch.empty(rows * ld, device=self.device, dtype=self.store)
                      for n, (rows, ld) in prog.bufs.items()}
         self.saved = {}
-        self.bn_coef = {}     # id(op) -> BN-backward coefficients [3][C] computed by its consumer (dw2 BOUT)
         self.bn_parts = {}    # id(op) -> [tile partials, tiles, write generation]: its BN-backward reduction from
                               # the epilogue of the data gradient that completed its dA (seg_conv_igemm_bnout*)
         self.wgen = {}        # gradient buffer name -> write generation (every write to the buffer bumps it)
@@ -1492,53 +1397,29 @@ class Run:
             LAST_RUN = self
 
 
+# Engine switches.  Environment switches (SEG_*) are the A/B knobs of measured design choices, read at import;
+# the module constants below them are diagnostics the tests flip directly (monkeypatch), not user settings.
+#
 # Parameter gradients (weight / bias / BN-affine readiness) run on a second HIP stream
 # beside the data-gradient chain: the compute-bound 3x3 weight gradients overlap the
 # memory-bound BatchNorm / depthwise / 1x1 kernels of the main stream.  Results are the
 # same either way (the kernels and their reduction orders do not change).
 OVERLAP = os.environ.get("SEG_OVERLAP", "1") == "1"
+# fork the weight-gradient side stream after the layer's data gradient (measured: f32 +1.5 %, bf16io +-0)
+FORK_LATE = os.environ.get("SEG_FORK_LATE", "1") == "1"
 # Winograd F(2x2,3x3) for the deep f32 3x3 convs (read when a program's weights are first
-# packed); SEG_WINO=0 routes them to the LDS-halo / implicit-GEMM kernels instead (parity
-# diagnostics: tests/test_gpu_unet_cfg5.py separates Winograd from accumulation error).
+# packed); SEG_WINO=0 routes them to the LDS-halo / implicit-GEMM kernels instead.
 WINOGRAD = os.environ.get("SEG_WINO", "1") == "1"
-WINOGRAD_WGRAD = os.environ.get("SEG_WINO_WGRAD", "1") == "1"  # the F(3x3,2x2) weight gradients alone
-# ... and the F(2x2,3x3) forward / data-gradient transforms separately (parity attribution)
-WINOGRAD_FWD = os.environ.get("SEG_WINO_FWD", "1") == "1"
-WINOGRAD_DGRAD = os.environ.get("SEG_WINO_DGRAD", "1") == "1"
 # LDS-halo direct 3x3 conv for the narrow convs in the bf16io configuration; SEG_HALO_BF16=0 turns it off.
 HALO_BF16 = os.environ.get("SEG_HALO_BF16", "1") == "1"
-# ... and the persistent LDS-DMA halo kernel (seg_conv_halo2_bf16io) where it applies; SEG_HALO2=0 = off
-HALO2 = os.environ.get("SEG_HALO2", "0") == "1"  # default off: step A/B -0.7 % (profiles/r04k_ab.txt)
 # ... and their weight gradients on the persistent LDS-halo kernel (seg_conv_wgrad2_bf16io); SEG_WGRAD2=0 = off
 WGRAD2 = os.environ.get("SEG_WGRAD2", "1") == "1"
-# fp16 inference (Predictor, BASELINE configs[3]): each inverted residual of the folded forward as one fused
-# launch (seg_mbconv_f16); SEG_MBCONV=0 = one launch per conv
-# the folded inference forward's convs on seg_conv_igemm_plan_b1's tile / split count (batch-1 frames: the
-# decoder convs); SEG_PLAN_B1=0 = the training cost model's (seg_conv_igemm_splits, seg_conv_igemm_tiles)
-PLAN_B1 = os.environ.get("SEG_PLAN_B1", "1") == "1"
-# the folded fp16 forward's outconv head (1x1 -> BN -> ReLU -> 1x1) in one launch (seg_pw2_f16); SEG_PW2=0 = two
-PW2 = os.environ.get("SEG_PW2", "1") == "1"
-# the folded fp16 forward's stem conv forms the preprocessed frame on load (seg_stem_pre_f16); SEG_STEM_PRE=0 =
-# seg_preprocess_bgr + the stem's implicit GEMM
-STEM_PRE = os.environ.get("SEG_STEM_PRE", "1") == "1"
-MBCONV = os.environ.get("SEG_MBCONV", "1") == "1"
 # BatchNorm-backward reduction from the epilogue of the implicit-GEMM data gradient that completes a BN layer's dA
 # (seg_conv_igemm_bnout*: no reduction pass over dA; the finalize reads the tile partials); SEG_BNOUT=0 = off.  Up to
 # BNOUT_MAX_TILES row tiles (the finalize's serial tile loop), i.e. the small-image layers where the three-launch
 # BN backward is latency-bound
 BNOUT = os.environ.get("SEG_BNOUT", "1") == "1"
 BNOUT_MAX_TILES = int(os.environ.get("SEG_BNOUT_MAX_TILES", "1024"))
-# bf16io depthwise convs on the LDS-DMA tile kernels (csrc/dw2.hip); SEG_DW2=0 keeps dwconv.hip's strip kernels
-# (default off: measured per launch against dwconv.hip at the bs=32 layers, tools/nbench.py --only dw, the strip
-# kernels are 1.0-1.9x faster on every layer of >= 64k pixels and equal below; the step A/B, profiles/r04f_ab.txt,
-# gives -0.3 % with the fused BN backward off and -5 % with it on)
-DW2 = os.environ.get("SEG_DW2", "0") == "1"
-# ... with their BatchNorm backwards fused (SEG_DW2_BN=0: three-launch seg_bn_backward): the depthwise conv's
-# own apply formed on load by its data / weight gradients, and the reduction of the expand conv that feeds it
-# computed in its data gradient's epilogue (images of at most DW2_BN_MAX_TILES 8 x 32-pixel tiles: the
-# in-launch finalize sums every tile's partials in one block per 64 channels)
-DW2_BN = os.environ.get("SEG_DW2_BN", "1") == "1"
-DW2_BN_MAX_TILES = int(os.environ.get("SEG_DW2_BN_MAX_TILES", "512"))
 # lazy BatchNorm for 1x1 consumers (the inverted residuals' project convs, OutConv's last
 # conv): SEG_LAZY_PW=0 keeps the separate BN-apply pass (read at program build)
 LAZY_PW = os.environ.get("SEG_LAZY_PW", "1") == "1"
@@ -1548,9 +1429,9 @@ ZERO_BN_BIAS = os.environ.get("SEG_ZERO_BN_BIAS", "1") == "1"
 # thin-K 1x1 convs (K <= 32) on seg_conv_pw instead of the generic implicit GEMM; SEG_PW=0 = off
 PW = os.environ.get("SEG_PW", "1") == "1"
 PW_MIN_ROWS = int(os.environ.get("SEG_PW_MIN_ROWS", "262144"))
-# bf16io deep convs on the 8-wave LDS-DMA implicit GEMM (seg_conv_igemm2_bf16io, csrc/igemm2.hip):
-# "3" = 3x3 convs where its plan applies (default), "all" = also 1x1 convs, "0" = off
-IGEMM2 = os.environ.get("SEG_IGEMM2", "3")
+# bf16io deep 3x3 convs on the 8-wave LDS-DMA implicit GEMM (seg_conv_igemm2_bf16io, csrc/igemm2.hip); SEG_IGEMM2=0
+# = off
+IGEMM2 = os.environ.get("SEG_IGEMM2", "1") == "1"
 # ... on images of at most this many output rows: measured per launch on UNet 512x1024 bf16io, igemm2 is 5-25 %
 # slower than the 4-wave implicit GEMM at 262k-4M rows and 1-6 % faster at 65k (profiles/r03k)
 IGEMM2_MAX_ROWS = int(os.environ.get("SEG_IGEMM2_MAX_ROWS", "65536"))
@@ -1558,21 +1439,24 @@ IGEMM2_MAX_ROWS = int(os.environ.get("SEG_IGEMM2_MAX_ROWS", "65536"))
 # launch at HEAD of round 4 on UNet 512x1024 bf16io, side stream off, 1-10 % faster than the 4-wave implicit GEMM on
 # every such launch (profiles/r04ig/); SEG_IGEMM2_WIDE=0 = off
 IGEMM2_WIDE = os.environ.get("SEG_IGEMM2_WIDE", "1") == "1"
-# ... and the 1x1 convs of small images on its 4-wave tiles (round 4: the generic register-staged kernel
-# keeps one K chunk in flight and ran the encoder's 4k-65k-row 1x1 convs at 0.4-1.5 TB/s); SEG_IGEMM2_1X1=0 = off
-# (default off: step A/B +3 % without it, profiles/r04f_ab.txt)
-IGEMM2_1X1 = os.environ.get("SEG_IGEMM2_1X1", "0") == "1"
-IGEMM2_1X1_MAX_ROWS = int(os.environ.get("SEG_IGEMM2_1X1_MAX_ROWS", "65536"))
 # bf16io implicit GEMMs on bf16-packed weights (seg_conv_igemm_bf16io_w16); SEG_W16=0 keeps the fp32 packs
 W16 = os.environ.get("SEG_W16", "1") == "1"
-# fork the weight-gradient side stream after the layer's data gradient (measured: f32 +1.5 %, bf16io +-0)
-FORK_LATE = os.environ.get("SEG_FORK_LATE", "1") == "1"
-# lazy BatchNorm for the 3x3 consumers of the bf16io configuration (double_conv's second conv), read at
-# program build.  Off by default: measured on UNet 512x1024 bf16io it removes a 220 us BN-apply pass per
-# full-size layer but the weight gradient transforms every input element once per tap (+330 us per full-size
-# layer), step 333 vs 343-345 img/s; MobileNetV2UNet flat (profiles/r03o/).  SEG_LAZY3=1 turns it on.
-LAZY3 = os.environ.get("SEG_LAZY3", "0") == "1"
+# many-tile BN statistics merged 16 tiles per row before the per-channel finalize; SEG_BN_MERGE=0 = direct
 BN_MERGE = os.environ.get("SEG_BN_MERGE", "1") == "1"
+
+# Diagnostics (tests flip these): the Winograd transforms one at a time (parity attribution,
+# tests/test_gpu_unet_cfg5.py) ...
+WINOGRAD_WGRAD = True  # the F(3x3,2x2) weight gradients
+WINOGRAD_FWD = True    # the F(2x2,3x3) forward
+WINOGRAD_DGRAD = True  # ... and data-gradient transforms
+# ... and the fp16 inference (Predictor, BASELINE configs[3]) fusions against their unfused launches: each inverted
+# residual of the folded forward as one launch (seg_mbconv_f16), the stem forming the preprocessed frame on load
+# (seg_stem_pre_f16), outconv's 1x1 -> BN -> ReLU -> 1x1 head in one launch (seg_pw2_f16), and the folded convs on
+# seg_conv_igemm_plan_b1's tile / split count (the batch-1 decoder convs) instead of the training cost model's
+MBCONV = True
+STEM_PRE = True
+PW2 = True
+PLAN_B1 = True
 _SIDE = {}
 
 
@@ -1852,12 +1736,15 @@ class _SegFunction(torch.autograd.Function):
             out = plan.run.stats[0].clone()  # the stats buffer is rewritten by the next step
             # the out-of-range label count, copied to the host as soon as the loss kernel has run:
             # train_one_epoch reads it before optimizer.step() without waiting for the backward
+            # (on the stats tensor's device and stream: the model need not be on the current device)
+            dev = plan.run.stats.device
             host = model.__dict__.get("_segamd_bad_host")
-            if host is None or host[0].device.type != "cpu":
-                host = (torch.zeros(1, dtype=torch.float32).pin_memory(), torch.cuda.Event())
+            if host is None or host[2] != dev:
+                host = (torch.zeros(1, dtype=torch.float32).pin_memory(), torch.cuda.Event(), dev)
                 model.__dict__["_segamd_bad_host"] = host
-            host[0].copy_(plan.run.stats[2:3], non_blocking=True)
-            host[1].record()
+            with torch.cuda.device(dev):
+                host[0].copy_(plan.run.stats[2:3], non_blocking=True)
+                host[1].record(torch.cuda.current_stream(dev))
         else:  # an unfused criterion checks its own labels: no stale flag from an earlier fused loss
             model.__dict__.pop("_segamd_last_stats", None)
             model.__dict__.pop("_segamd_bad_host", None)
@@ -1900,6 +1787,19 @@ def bad_label_count(model):
     model = getattr(model, "module", model)
     st = model.__dict__.get("_segamd_last_stats")
     return None if st is None else st[2:3].clone()
+
+
+def label_flag(model):
+    """Device tensor [1] (fp32) that is non-zero iff the last fused loss saw a label outside [0, C) other than
+    ignore_index -- on ANY rank under seg_amd.ddp.DataParallel (the count rides in the last gradient bucket's
+    all-reduce: valid in stream order after finish_gradient_sync, no extra collective); None when there is no fused
+    loss to check (or, under DataParallel, when this step's buckets did not go out)."""
+    sync = getattr(model, "label_flag", None)
+    if sync is not None:  # DataParallel
+        return sync()
+    model = getattr(model, "module", model)
+    st = model.__dict__.get("_segamd_last_stats")
+    return None if st is None else st[2:3]
 
 
 def bad_label_count_host(model):

@@ -34,8 +34,15 @@ class Adam(torch.optim.Adam):
         return cm
 
     @torch.no_grad()
-    def step(self, closure=None):
+    def step(self, closure=None, *, skip_if_nonzero: torch.Tensor | None = None):
+        """One Adam step.  skip_if_nonzero: a one-element fp32 device tensor; when it holds a non-zero value at the
+        time the step runs on the GPU (stream order), the kernel leaves every parameter and moment unchanged --
+        train_one_epoch passes the batch's out-of-range label count here so the step can be queued without a host
+        wait (the CPU step counters still advance; the loop raises right after)."""
         loss = None
+        if skip_if_nonzero is not None and not (skip_if_nonzero.is_cuda and skip_if_nonzero.dtype == torch.float32
+                                                and skip_if_nonzero.numel() >= 1):
+            raise ValueError("skip_if_nonzero must be a float32 CUDA tensor")
         if closure is not None:
             with torch.enable_grad():
                 loss = closure()
@@ -70,7 +77,8 @@ class Adam(torch.optim.Adam):
             device = ps[0].device
             table = _pack(rows).pin_memory().to(device, non_blocking=True)
             chunks = self._chunks([p.numel() for p in ps], device)
-            call("seg_adam_step", table.data_ptr(), chunks.data_ptr(), chunks.shape[0], _CHUNK, 1 - b1, b2, 1 - b2, eps,
+            call("seg_adam_step_skip", table.data_ptr(), chunks.data_ptr(), chunks.shape[0], _CHUNK, 1 - b1, b2, 1 - b2,
+                 eps, skip_if_nonzero.data_ptr() if skip_if_nonzero is not None else None,
                  torch.cuda.current_stream(device).cuda_stream)
         return loss
 

@@ -38,27 +38,52 @@ def _is_rank0() -> bool:
         torch.distributed.get_rank() == 0
 
 
+def _raise_bad_labels(n: float):
+    if n:
+        raise IndexError("Target out of bounds: label(s) outside [0, num_classes) that are not ignore_index "
+                         "(nn.CrossEntropyLoss raises on these; the optimizer step was skipped)")
+
+
 def _check_labels(model, inputs):
     """Raise IndexError like nn.CrossEntropyLoss if the fused loss saw a label outside
-    [0, C) (the kernels flag it; the loss and gradients are NaN).  Runs BEFORE
-    optimizer.step(), so no NaN reaches the weights; under torch.distributed the count is
-    summed over ranks first, so every rank raises together instead of one rank leaving
-    the others in the next collective."""
+    [0, C) (the kernels flag it; the loss and gradients are NaN), BEFORE optimizer.step():
+    the path for optimizers that cannot skip their step on the device.  Under
+    seg_amd.ddp.DataParallel the count arrived with the last gradient bucket's all-reduce
+    (every rank raises together, no extra collective); in one process it was copied to the
+    host right after the loss kernel, so this waits for the forward only."""
     if not inputs.is_cuda:
         return  # the CPU composition's F.cross_entropy raises by itself
-    from .engine import bad_label_count, bad_label_count_host, check_targets
-    if torch.distributed.is_available() and torch.distributed.is_initialized() and hasattr(model, "module"):
-        bad = bad_label_count(model)
-        if bad is None:
-            return
-        torch.distributed.all_reduce(bad, group=getattr(model, "pg", None))
-        check_targets(model, bad)
+    from .engine import bad_label_count_host, label_flag
+    if hasattr(model, "label_flag"):
+        flag = label_flag(model)
+        if flag is not None:
+            _raise_bad_labels(float(flag.item()))
         return
-    # one process: the count was copied to the host right after the loss kernel, so this waits
-    # for the forward only and optimizer.step() is queued while the backward still runs (ADVICE r3)
     n = bad_label_count_host(model)
-    if n:
-        check_targets(model, torch.tensor([float(n)]))
+    _raise_bad_labels(n or 0)
+
+
+def _step_and_loss(model, inputs, optimizer, loss):
+    """optimizer.step() and loss.item() (src/train.py:39-41) with the fused loss's label check.  With seg_amd.Adam
+    the step is queued at once and skips itself on the device when the batch (on any rank) had an out-of-range
+    label; the host reads the flag after loss.item(), whose wait covers it, and raises -- no host wait before the
+    step and no extra collective.  Other optimizers: the check runs before the step."""
+    from .optim import Adam
+    from .engine import label_flag
+    flag = label_flag(model) if inputs.is_cuda else None
+    if flag is None or not isinstance(optimizer, Adam):
+        _check_labels(model, inputs)
+        optimizer.step()
+        return loss.item()
+    core = getattr(model, "module", model)
+    host = core.__dict__.get("_segamd_flag_host")
+    if host is None:
+        host = core.__dict__["_segamd_flag_host"] = torch.zeros(1, dtype=torch.float32).pin_memory()
+    host.copy_(flag, non_blocking=True)  # stream-ordered before the step and the loss copy below
+    optimizer.step(skip_if_nonzero=flag)
+    lv = loss.item()                     # waits for this stream: the flag copy has landed
+    _raise_bad_labels(float(host[0]))
+    return lv
 
 
 def compute_loss(model, criterion, inputs, targets):
@@ -97,9 +122,9 @@ def train_one_epoch(model, train_loader, criterion, optimizer, device, epoch: in
         sync = getattr(model, "finish_gradient_sync", None)
         if sync is not None:
             sync()
-        _check_labels(model, inputs)  # before the update, on every rank (nn.CrossEntropyLoss raises in the forward)
-        optimizer.step()
-        lv = loss.item()
+        # the update never sees an out-of-range label's NaN gradients, on any rank (nn.CrossEntropyLoss raises in
+        # the forward): seg_amd.Adam skips its step on the device, everything else is checked before the step
+        lv = _step_and_loss(model, inputs, optimizer, loss)
         train_loss += lv
         nb += 1
         if bar is not None:

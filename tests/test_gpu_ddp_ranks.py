@@ -84,3 +84,57 @@ def test_two_ranks_real_engine_match_single_process_mean():
         # DDP broadcasts rank 0's BN buffers each step: replica 1 adopts replica 0's
         for b0, b1 in zip(ms[0].buffers(), ms[1].buffers()):
             b1.copy_(b0)
+
+
+def _bad_label_worker(rank, port, out):
+    """Rank 1's batch has an out-of-range label: both ranks must raise from train_model, with every parameter
+    unchanged, and the step must issue only the gradient buckets' all-reduces (the label count rides in the last
+    bucket)."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=2)
+    try:
+        torch.cuda.set_device(0)
+        from torch import nn
+        from seg_amd import Adam, MobileNetV2UNet, deterministic_init, train_model
+        from seg_amd.ddp import DataParallel
+        m = deterministic_init(MobileNetV2UNet(10), seed=8).cuda().train()
+        dp = DataParallel(m, bucket_cap_mb=1.0)
+        opt = Adam(m.parameters(), lr=1e-3)
+        x, y = _shards()[rank]
+        x, y = x.cuda(), y.cuda()
+        calls = {"all_reduce": 0}
+        real = dist.all_reduce
+
+        def counting(*a, **k):
+            calls["all_reduce"] += 1
+            return real(*a, **k)
+        dist.all_reduce = counting
+        train_model(dp, [(x, y)], nn.CrossEntropyLoss(), opt, "cuda", epochs=1, checkpoint_pattern=None,
+                    progress=False)  # a clean step first
+        per_step = calls["all_reduce"]
+        before = {k: p.detach().clone() for k, p in m.named_parameters()}
+        if rank == 1:
+            y = y.clone()
+            y[0, 3, 3] = 10
+        raised = False
+        try:
+            train_model(dp, [(x, y)], nn.CrossEntropyLoss(), opt, "cuda", epochs=1, checkpoint_pattern=None,
+                        progress=False)
+        except IndexError:
+            raised = True
+        dist.all_reduce = real
+        unchanged = all(torch.equal(p.detach(), before[k]) for k, p in m.named_parameters())
+        out[rank] = (raised, unchanged, per_step, calls["all_reduce"] - per_step, len(dp._buckets))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_bad_label_on_one_rank_raises_on_both_without_update():
+    ctx = mp.get_context("spawn")
+    out = ctx.Manager().dict()
+    mp.spawn(_bad_label_worker, args=(_port(), out), nprocs=2, join=True)
+    for r in (0, 1):
+        raised, unchanged, per_step, bad_step, nb = out[r]
+        assert raised, f"rank {r} did not raise"
+        assert unchanged, f"rank {r} changed its parameters"
+        assert per_step == nb and bad_step == nb, (per_step, bad_step, nb)  # the buckets only: no extra collective

@@ -152,42 +152,6 @@ def test_igemm2_every_tile(tile):
         query("seg_igemm2_force_tile", -1)
 
 
-@pytest.mark.parametrize("M,Cin,Cout,act", [(4096, 960, 160, 0), (16384, 576, 96, 2), (65536, 144, 64, 2),
-                                            (4096, 960, 320, 0)])
-def test_igemm2_xf_equals_generic_xf(M, Cin, Cout, act):
-    """The 1x1 lazy-BN variant (the inverted residuals' project convs: the dw conv's BatchNorm +
-    ReLU6 applied to the A fragments) against the generic kernel's transform-on-load: bitwise
-    when unsplit (the same bf16 values reach the same MFMA order), within bf16 rounding when split."""
-    g = torch.Generator().manual_seed(M + Cin)
-    y = (torch.randn(M, Cin, generator=g) * 1.5 + 0.3).to(BF).to(DEV)
-    scale = (torch.rand(Cin, generator=g) + 0.5).to(DEV)
-    shift = torch.randn(Cin, generator=g).to(DEV)
-    w = (torch.randn(Cout, Cin, 1, 1, generator=g) * 0.05).to(DEV)
-    wk, ldk = pack16(w, Cout, Cin, 1)
-    ok, (tile_rows, ntiles, splits, work_floats) = plan(M, Cout, Cin, 1)
-    assert ok
-    work = torch.zeros(max(work_floats, 1), device=DEV)
-    o2 = torch.empty(M, Cout, device=DEV, dtype=BF)
-    st = torch.empty(ntiles * 2 * Cout, device=DEV)
-    call("seg_conv_igemm2_bf16io_xf", y.data_ptr(), Cin, 1, 1, M, Cin, wk.data_ptr(), ldk, None, o2.data_ptr(), Cout,
-         Cout, 1, None, 0, st.data_ptr(), work.data_ptr(), scale.data_ptr(), shift.data_ptr(), act, S())
-    o1 = torch.empty(M, Cout, device=DEV, dtype=BF)
-    call("seg_conv_igemm_bf16io_xf_w16", y.data_ptr(), Cin, 1, 1, M, Cin, wk.data_ptr(), ldk, None, o1.data_ptr(),
-         Cout, 1, M, Cout, 1, 1, 0, None, 0, None, scale.data_ptr(), shift.data_ptr(), act, S())
-    torch.cuda.synchronize()
-    if splits == 1:
-        assert torch.equal(o1, o2)
-    else:
-        assert rel(o2.float(), o1.float()) < 4e-3
-    # and against float64 of the transformed, bf16-rounded input
-    z = (y.float() * scale + shift)
-    if act == 2:
-        z = z.clamp(0, 6)
-    z = z.to(BF).double().cpu()
-    ref = z @ w.view(Cout, Cin).to(BF).double().cpu().t()
-    assert rel(o2.float(), ref) < 4e-3
-
-
 def test_engine_routes_wide_convs_to_igemm2(monkeypatch):
     """UNet(10) bf16io at 8x512x1024 (configs[4]): past the 65k-row cap, the 3x3 convs whose GEMM N is a multiple
     of 128 take igemm2 (SEG_IGEMM2_WIDE), the others keep the implicit GEMM / LDS halo; off: none past the cap."""

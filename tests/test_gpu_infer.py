@@ -151,3 +151,33 @@ def test_eager_eval_forward_agrees_with_folded():
     got = pred.logits()
     rel = float((got - ref).norm() / ref.norm())
     assert rel < 1e-4, rel  # folding reorders fp32 rounding; the oracle test bounds both at 1e-3
+
+
+@pytest.mark.parametrize("graph", [True, False])
+def test_two_predictors_on_two_streams(graph):
+    """two fp16 Predictors replayed concurrently on two streams.  Their split-K convs
+    (seg_conv_igemm_f16_ic) and fused inverted residuals (seg_mbconv_f16) combine a split tile inside the
+    launch; with another kernel holding CUs, a block must never wait for a peer that is not resident
+    (seg_tile_combine hands its share to the tile's last arrival instead).  Both must finish and give
+    bitwise the logits they give alone."""
+    models = [deterministic_init(MobileNetV2UNet(10), seed=s, random_running_stats=True).to(DEV).eval()
+              for s in (3, 4)]
+    frames = [frame(720, 1280, seed=s) for s in (5, 6)]
+    preds = [Predictor(m, frame_hw=(720, 1280), graph=graph, math="f16") for m in models]
+    solo = []
+    for p, f in zip(preds, frames):
+        p(f)
+        solo.append(p.logits())
+    torch.cuda.synchronize()
+    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+    for st in streams:
+        st.wait_stream(torch.cuda.current_stream())
+    for _ in range(40):
+        for p, st in zip(preds, streams):
+            with torch.cuda.stream(st):
+                p.step()
+    for st in streams:
+        torch.cuda.current_stream().wait_stream(st)
+    torch.cuda.synchronize()
+    for p, ref in zip(preds, solo):
+        assert torch.equal(p.logits(), ref)

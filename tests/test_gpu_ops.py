@@ -378,6 +378,22 @@ def test_ce_target_out_of_bounds(bad):
     for k, v in model.state_dict().items():
         if k in before:
             assert torch.equal(v, before[k]), k
+    # seg_amd.Adam: the step is queued without a host wait and skips itself on the device;
+    # the loop raises after loss.item() -- parameters and Adam moments unchanged
+    from seg_amd import Adam
+    sopt = Adam(model.parameters(), lr=1e-3)
+    with pytest.raises(IndexError, match="Target out of bounds"):
+        train_model(model, [(x, t)], nn.CrossEntropyLoss(), sopt, DEV, epochs=1, checkpoint_pattern=None,
+                    progress=False)
+    for k, v in model.state_dict().items():
+        if k in before:
+            assert torch.equal(v, before[k]), k
+    for st in sopt.state.values():
+        assert not st["exp_avg"].any() and not st["exp_avg_sq"].any()
+    # and a clean batch after it takes the step
+    t[0, 5, 5] = 3
+    train_model(model, [(x, t)], nn.CrossEntropyLoss(), sopt, DEV, epochs=1, checkpoint_pattern=None, progress=False)
+    assert any(not torch.equal(v, before[k]) for k, v in model.state_dict().items() if k in before)
 
 
 def test_colsum_and_add():

@@ -42,7 +42,7 @@ def test_splitk_in_launch_equals_two_launch(name, N, H, W, Cin, Cout, ks, act, a
     ref = torch.empty(M, Cout, device=DEV)
     call(name, x.data_ptr(), Cin, N, H, W, Cin, w.data_ptr(), ldk, b.data_ptr(), ref.data_ptr(), Cout, H, W, Cout, ks,
          1, ks // 2, add.data_ptr() if addend else None, Cout if addend else 0, None, act, work.data_ptr(), splits, S())
-    cnt = torch.zeros(2 * query("seg_conv_igemm_tiles", M, Cout), device=DEV, dtype=torch.int32)
+    cnt = torch.zeros(4 * query("seg_conv_igemm_tiles", M, Cout), device=DEV, dtype=torch.int32)
     work2 = torch.full_like(work, float("nan"))
     for _ in range(2):
         o = torch.full((M, Cout), float("nan"), device=DEV)
@@ -83,7 +83,7 @@ def test_plan_b1_equals_cost_model_tile(name, H, W, Cin, Cout, ks):
     ref = torch.empty(M, Cout, device=DEV)
     call(name, x.data_ptr(), Cin, 1, H, W, Cin, w.data_ptr(), ldk, b.data_ptr(), ref.data_ptr(), Cout, H, W, Cout, ks,
          1, ks // 2, None, 0, None, 1, work.data_ptr() if splits > 1 else None, splits, S())
-    cnt = torch.zeros(2 * ntl, device=DEV, dtype=torch.int32)
+    cnt = torch.zeros(4 * ntl, device=DEV, dtype=torch.int32)
     work2 = torch.full_like(work, float("nan"))
     for _ in range(2):
         o = torch.full((M, Cout), float("nan"), device=DEV)

@@ -10,6 +10,7 @@ import torch
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [os.path.join(REPO, "team02-objectdetection_amd"), REPO]
 from seg_amd._lib import call, query  # noqa: E402
+from seg_amd import engine as E  # noqa: E402
 
 SHAPES = [  # H, W, Cin, Cout, ks   (up1..up4 of MobileNetV2UNet at 1/16..1/2 of 128x256; features[18])
     (8, 16, 1344, 256, 3), (8, 16, 256, 256, 3), (16, 32, 288, 128, 3), (16, 32, 128, 128, 3),
@@ -42,10 +43,10 @@ def main():
         out = torch.empty(M, Cout, device="cuda")
         d = query("seg_conv_igemm_splits", M, Cout, Cin, ks)
         work = torch.empty(64 * M * Cout, device="cuda")
-        cnt = torch.zeros(2 * 4096, device="cuda", dtype=torch.int32)
+        cnt = torch.zeros(4 * 4096, device="cuda", dtype=torch.int32)
         res = {}
         for t in TILES:
-            query("seg_igemm_force_tile", t)
+            E.force_tiles(igemm=t)
             for sp in sorted({1, 2, 4, 8, 16, 32, 64, d}):
                 if sp > 1 and sp != d and sp * 2 > K // 16:
                     continue
@@ -55,7 +56,7 @@ def main():
                          out.data_ptr(), Cout, H, W, Cout, ks, 1, ks // 2, None, 0, 2, work.data_ptr(), sp,
                          cnt.data_ptr(), s)
                 res[(t, sp)] = timeit(f)
-        query("seg_igemm_force_tile", -1)
+        E.force_tiles(igemm=-1)
         best = min(res, key=res.get)
         flop = 2.0 * M * Cout * K
         print(f"H{H} W{W} {Cin}->{Cout} k{ks} M={M} K={K}: default (tile -1, {d} splits) {res[(-1, d)]:.1f} us; "

@@ -1,7 +1,7 @@
 """Summarise a rocprofv3 kernel-trace/stats run and its PMC passes for the
 dominant kernel family, and write it under profiles/.
 
-    python tools/roofline_report.py <prof_dir> <pmc_dir> <steps_profiled> <out_prefix>
+    python tools/roofline_report.py <prof_dir> <pmc_dir> <steps_profiled> <out_prefix> [MobileNetV2UNet|UNet]
 
 prof_dir: `rocprofv3 --kernel-trace --stats` output of bench.py (run_kernel_stats.csv)
 pmc_dir:  FETCH_SIZE/ and WRITE_SIZE/ passes (run_counter_collection.csv), each
@@ -20,16 +20,23 @@ from collections import defaultdict
 
 FAMILIES = {  # "conv3" = the dense 3x3 conv forward + data gradient (bench.py's roofline kernel family)
     # (rocprofv3 leaves the __bf16 / _Float16 instantiations mangled: ILi..E forms)
+    # igemm2_kernel<BM, BN, WM, WN, KS, XF> (csrc/igemm2.hip:91; six template parameters since 53539df --
+    # round 4's three-parameter pattern matched none of them)
     "conv3": re.compile(r"igemm_conv_kernel<\d+, \d+, \d+, \d+, 3, \d+|igemm_conv_kernelILi\d+ELi\d+ELi\d+ELi\d+ELi3E"
                         r"|wino_gemm_kernel|wino_out_kernel|halo3x3_kernel"
-                        r"|igemm2_kernel<\d+, \d+, 3>|igemm2_kernelILi\d+ELi\d+ELi3E"),
+                        r"|igemm2_kernel<\d+, \d+, \d+, \d+, 3[,>]|igemm2_kernelILi\d+ELi\d+ELi\d+ELi\d+ELi3E"),
     "igemm1": re.compile(r"igemm_conv_kernel<\d+, \d+, \d+, \d+, 1, \d+|igemm_conv_kernelILi\d+ELi\d+ELi\d+ELi\d+ELi1E"
-                         r"|igemm2_kernel<\d+, \d+, 1>|igemm2_kernelILi\d+ELi\d+ELi1E"),
+                         r"|igemm2_kernel<\d+, \d+, \d+, \d+, 1[,>]|igemm2_kernelILi\d+ELi\d+ELi\d+ELi\d+ELi1E"),
+    # BatchNorm backward (csrc/bn.hip): the dA/y reduction, its finalizes and the dY apply pass
+    "bn_bwd": re.compile(r"chan_partial_kernel<1,|chan_partial_kernelILi1E|bn_bwd_finalize_kernel"
+                         r"|bn_bwd_finalize_tiles_kernel|bn_bwd_apply_rt_kernel|bn_bwd_apply_kernel"),
     "wgrad3": re.compile(r"wgrad_kernel<\d+, \d+, \d+, \d+, 3[,>]|wgrad_kernelILi\d+ELi\d+ELi\d+ELi\d+ELi3E"
                          r"|wino_wgrad"),
     "wgrad1": re.compile(r"wgrad_kernel<\d+, \d+, \d+, \d+, 1[,>]|wgrad_kernelILi\d+ELi\d+ELi\d+ELi\d+ELi1E"),
 }
-OPS_PER_STEP = {"conv3": 17}  # MobileNetV2UNet bs=32: 8 decoder convs fwd + 8 dgrad + the stem fwd
+# conv ops per step of the profiled model: MobileNetV2UNet 17 (8 decoder convs fwd + 8 dgrad + the stem fwd),
+# UNet 27 (14 convs fwd + 13 dgrad); a Winograd op is two kernels (wino_gemm + wino_out), every other op one
+OPS_PER_STEP = {"MobileNetV2UNet": 17, "UNet": 27}
 
 
 def family(name):
@@ -39,8 +46,9 @@ def family(name):
     return None
 
 
-def main(prof_dir, pmc_dir, steps, out_prefix):
+def main(prof_dir, pmc_dir, steps, out_prefix, model="MobileNetV2UNet"):
     steps = int(steps)
+    ops = OPS_PER_STEP[model]
     stats = list(csv.DictReader(open(f"{prof_dir}/run_kernel_stats.csv")))
     total = sum(float(r["TotalDurationNs"]) for r in stats)
     fam = defaultdict(lambda: {"calls": 0, "ns": 0.0, "symbols": []})
@@ -103,15 +111,28 @@ def main(prof_dir, pmc_dir, steps, out_prefix):
             out["families"][f]["mfma_busy_cycles"] = mfma[f][0]
             out["families"][f]["grbm_gui_active"] = mfma[f][1]
             out["families"][f]["mfma_busy_frac"] = mfma[f][0] / (mfma[f][1] / 8 * 1024)
-        if f in OPS_PER_STEP and fetch and write:
+        if f == "conv3" and fetch and write:
             # per conv op (a Winograd op is two kernels): family bytes per step / ops per step
             per_step = (2 * sum(fetch) + sum(write)) * 1024 / (len(fetch) / (d["calls"] / steps))
-            out["families"][f]["ops_per_step"] = OPS_PER_STEP[f]
-            out["families"][f]["hbm_bytes_per_op"] = per_step / OPS_PER_STEP[f]
+            out["families"][f]["ops_per_step"] = ops
+            out["families"][f]["hbm_bytes_per_op"] = per_step / ops
+        if f == "bn_bwd" and fetch and write:
+            out["families"][f]["hbm_bytes_per_step"] = (2 * sum(fetch) + sum(write)) * 1024 / (
+                len(fetch) / (d["calls"] / steps))
         lines.append(f"| {f} | {d['calls'] / steps:.0f} | {d['ns'] / 1e6 / steps:.2f} | {d['ns'] / total:.1%} | "
                      f"{avg_us:.1f} | {hbm / 1e6 if hbm else float('nan'):.1f} MB | "
                      f"{out['families'][f].get('mfma_busy_frac', float('nan')):.3f} |")
-    lines += ["", "Top kernels:", "", "| kernel | calls | avg us | total ms |", "|---|---|---|---|"]
+    # self-check: every conv3 op of the step must be in the family -- one kernel per op plus
+    # the second kernel (wino_out_kernel) of each Winograd op
+    wino_out = sum(int(r["Calls"]) for r in stats if "wino_out_kernel" in r["Name"]) / steps
+    want = ops + wino_out
+    got = fam["conv3"]["calls"] / steps if "conv3" in fam else 0
+    if abs(got - want) > 1e-6:
+        raise SystemExit(f"roofline_report: conv3 family has {got:g} launches per step, the {model} step has {want:g} "
+                         f"({ops} ops + {wino_out:g} Winograd output transforms): a kernel name escaped the pattern")
+    out["families"]["conv3"]["expected_calls_per_step"] = want
+    lines += ["", f"conv3 self-check: {got:g} launches per step = {ops} ops + {wino_out:g} Winograd output transforms.",
+              "", "Top kernels:", "", "| kernel | calls | avg us | total ms |", "|---|---|---|---|"]
     for r in sorted(stats, key=lambda r: -float(r["TotalDurationNs"]))[:25]:
         lines.append(f"| `{r['Name'].replace('(anonymous namespace)::', '')[:90]}` | {r['Calls']} | "
                      f"{float(r['AverageNs']) / 1e3:.1f} | {float(r['TotalDurationNs']) / 1e6:.2f} |")

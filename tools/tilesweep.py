@@ -85,9 +85,9 @@ def main():
                      E.r4(Cout), Ho, Wo, Cout, ks, st, pad, None, 0, None, s)
         times = []
         for t in range(len(TILES)):
-            call("seg_igemm_force_tile", t)
+            E.force_tiles(igemm=t)
             times.append(timeit(run))
-        call("seg_igemm_force_tile", -1)
+        E.force_tiles(igemm=-1)
         auto_rows = query("seg_conv_igemm_row_tiles", N * Ho * Wo, Cout, None)
         t_auto = timeit(run)  # measured last: the first timings of a shape run slow
         best = min(range(len(TILES)), key=lambda t: times[t])

@@ -277,7 +277,8 @@ def main():
             r = train_workload(ua, m, dev, world, rank, dist)
             unet[m] = {"value": r["value"], "unit": "images/s", "ms_per_step": r["ms_per_step"],
                        "steps": ua.steps, "warmup": ua.warmup, "final_loss": r["final_loss"],
-                       "math": MATH_NOTE[m], "roofline": r["roofline"], "step_roofline": r["step_roofline"],
+                       "math": MATH_NOTE[m], "roofline": r["roofline"], "bn_bwd_roofline": r["bn_bwd_roofline"],
+                       "step_roofline": r["step_roofline"],
                        **({"multi_gpu": r["multi_gpu"]} if r["multi_gpu"] is not None else {})}
 
     if rank == 0:
@@ -296,7 +297,8 @@ def main():
                                           "gloo REHEARSAL (ranks share GPUs; not a throughput figure)",
                            "optimizer": {"seg": "seg_amd.Adam (HIP, one launch)", "torch": "torch.optim.Adam (foreach)"}[args.optimizer]},
                 "final_loss": head["final_loss"], "math": MATH_NOTE[args.math],
-                "roofline": head["roofline"], "step_roofline": head["step_roofline"], "cpu_baseline": cpu}
+                "roofline": head["roofline"], "bn_bwd_roofline": head["bn_bwd_roofline"],
+                "step_roofline": head["step_roofline"], "cpu_baseline": cpu}
         if head["multi_gpu"] is not None:
             line["multi_gpu"] = head["multi_gpu"]
         if nested is not None:
@@ -419,12 +421,13 @@ def train_workload(args, math, dev, world, rank, dist):
                            "broadcast (after one untimed no_sync step) / the timed step time (the driver "
                            "computes the cross-run N=1 efficiency itself)"}
 
-    roof = None
+    roof = bn_roof = None
     if timer is not None:
-        roof = _roofline(args, math, model, core, engine, timer, conv3, step, dt, peak)
+        roof, bn_roof = _roofline(args, math, model, core, engine, timer, conv3, step, dt, peak)
     step_roof = _step_roofline(args, math, core, engine, value, peak)
     res = {"value": round(value, 2), "ms_per_step": round(dt / args.steps * 1e3, 3),
-           "final_loss": round(final_loss, 5), "roofline": roof, "step_roofline": step_roof, "multi_gpu": scaling}
+           "final_loss": round(final_loss, 5), "roofline": roof, "bn_bwd_roofline": bn_roof,
+           "step_roofline": step_roof, "multi_gpu": scaling}
     engine.release_plans(core)
     del model, core, opt
     torch.cuda.synchronize()
@@ -455,6 +458,7 @@ def _roofline(args, math, model, core, engine, timer, conv3, step, dt, peak):
 
     rec = timer.elapsed()
     flops, secs, n = family(rec, conv3)
+    pmc = {}
     wfl, wsec, wn = family(rec, {"wino3_fwd", "wino3_dgrad"})
     achieved = flops / secs / 1e12 if secs > 0 else 0.0
     traffic, traffic_src, mfma_busy = None, None, None
@@ -465,14 +469,17 @@ def _roofline(args, math, model, core, engine, timer, conv3, step, dt, peak):
     if os.path.exists(prof) and default_workload:
         with open(prof) as fh:
             rj = json.load(fh)
-        traffic = rj["families"].get("conv3", {}).get("hbm_bytes_per_op")
-        mfma_busy = rj["families"].get("conv3", {}).get("mfma_busy_frac")
+        c3 = rj["families"].get("conv3", {})
+        traffic = c3.get("hbm_bytes_per_op")
+        mfma_busy = c3.get("mfma_busy_frac")
+        pmc = rj["families"]
         # the PMC figure is not measured in this run: name the profile and commit it came from
         traffic_src = {"file": os.path.relpath(prof, REPO), "profile": rj.get("profile"),
                        "commit": rj.get("commit"),
                        "counters": "rocprofv3 PMC (2*FETCH_SIZE+WRITE_SIZE)*1KiB of the conv3 family per step "
-                                   "/ 17 conv ops, separate --pmc passes; SQ_VALU_MFMA_BUSY_CYCLES and "
-                                   "GRBM_GUI_ACTIVE in a third pass"}
+                                   f"/ {c3.get('ops_per_step', 17)} conv ops ({c3.get('calls_per_step')} launches per "
+                                   "step, checked against the step's op count by tools/roofline_report.py), separate "
+                                   "--pmc passes; SQ_VALU_MFMA_BUSY_CYCLES and GRBM_GUI_ACTIVE in a third pass"}
     # algorithmic bytes of the family: every 3x3 conv's input and output tensors once
     # (fwd: X + Y, dgrad: dY + dX) at the storage element size, averaged over its launches
     prog = engine.get_program(core, args.batch, args.height, args.width)
@@ -491,6 +498,7 @@ def _roofline(args, math, model, core, engine, timer, conv3, step, dt, peak):
     af, as_, an = family(rec_all, {k for k, _, _ in rec_all if k.startswith(("igemm", "wino", "halo"))})
     rec_iso = extra_pass(False)
     ifl, isec, inn = family(rec_iso, conv3)
+    bn_roof = _bn_roofline(args, math, family, rec_all, rec_iso, dt, pmc, traffic_src)
     # the family is graded against the resource its own arithmetic intensity makes binding:
     # roofline time = max(bytes / HBM, FLOPs / MFMA peak) (the bf16io 3x3 family,
     # ~420 FLOP/B, sits above the bf16 ridge of 2500 / 8 = 312 FLOP/B -- MFMA-bound, not HBM-bound)
@@ -539,7 +547,39 @@ def _roofline(args, math, model, core, engine, timer, conv3, step, dt, peak):
                  "avg_launch_us": round(isec / max(inn, 1) * 1e6, 2), "launches": inn}),
             "wgrad3": {"achieved": round(wf / ws / 1e12, 2) if ws else None, "launches": wgn,
                        "avg_launch_us": round(ws / max(wgn, 1) * 1e6, 2)},
-            "all_mfma_convs": {"achieved": round(af / as_ / 1e12, 2) if as_ else None, "launches": an}}
+            "all_mfma_convs": {"achieved": round(af / as_ / 1e12, 2) if as_ else None, "launches": an}}, bn_roof
+
+
+def _bn_roofline(args, math, family, rec_all, rec_iso, dt, pmc, traffic_src):
+    """The BatchNorm-backward family (in bf16io it is the largest share of the step), graded
+    against HBM: algorithmic bytes = every BN layer's dA and y read once and dY written once (3 |Y| at the storage
+    element size; seg_bn_backward / seg_bn_bwd_apply carry them, the tile finalizes none), divided by the summed
+    durations of those launches (HIP events, the 3 untimed all-launch steps after the timed region)."""
+    by, sec, n = family(rec_all, {"bn_bwd"})
+    if not sec:
+        return None
+    iby, isec, inn = family(rec_iso, {"bn_bwd"})
+    steps = 3
+    gbs = by / sec / 1e9
+    fam = pmc.get("bn_bwd", {}) if pmc else {}
+    traffic = fam.get("hbm_bytes_per_step")
+    default_workload = (args.model, args.batch, args.height, args.width) == ("MobileNetV2UNet", 32, 256, 512)
+    return {"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(gbs / HBM_PEAK_GBS, 4),
+            "algorithmic_bytes_per_step": round(by / steps), "launch_entries_per_step": round(n / steps),
+            "ms_per_step": round(sec / steps * 1e3, 3), "share_of_step": round(sec / steps / (dt / args.steps), 4),
+            "traffic_per_step": round(traffic) if traffic and default_workload else None,
+            "traffic_over_algorithmic": round(traffic / (by / steps), 3) if traffic and default_workload else None,
+            "traffic_source": traffic_src if traffic and default_workload else None,
+            "kernel": "BatchNorm backward (csrc/bn.hip): chan_partial_kernel<1> (sum dz, sum dz (y - mean)) + "
+                      "bn_bwd_finalize_kernel + bn_bwd_apply_rt_kernel per layer (seg_bn_backward), or, where the "
+                      "data gradient that completes dA wrote the partials (seg_conv_igemm_bnout*), "
+                      "bn_bwd_finalize_tiles_kernel + the apply",
+            "note": "durations from HIP events around each BN-backward launch entry in 3 untimed steps after the timed "
+                    "region (every launch timed, side stream as configured); without_side_stream: the same with it off",
+            "without_side_stream": {"achieved": round(iby / isec / 1e9, 1) if isec else None, "unit": "GB/s",
+                                    "frac": round(iby / isec / 1e9 / HBM_PEAK_GBS, 4) if isec else None,
+                                    "ms_per_step": round(isec / steps * 1e3, 3)}}
 
 
 def _step_roofline(args, math, core, engine, value, peak):

@@ -781,7 +781,8 @@ class Program:
                 op.ig2_f = op.ig2_d = None
                 # beyond IGEMM2_MAX_ROWS only GEMMs whose N fills the 8-wave tiles (N % 128 == 0: UNet's deep levels)
                 wide = y.M > IGEMM2_MAX_ROWS and IGEMM2_WIDE
-                if w16f and IGEMM2 and op.ks == 3 and op.stride == 1 and op.pad == 1:
+                if (w16f and IGEMM2 and op.ks == 3 and op.stride == 1 and op.pad == 1
+                        and (y.M <= IGEMM2_MAX_ROWS or wide)):
                     i = op.inp  # 16-byte rows: ld and channel offset multiples of 8 elements
                     rows16 = i.ld % 8 == 0 and i.off % 8 == 0 and y.ld % 8 == 0 and y.off % 8 == 0
                     if (rows16 and not op.halo_f and op.xform is None and op.cin_pad == op.cin

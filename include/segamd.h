@@ -271,18 +271,6 @@ long seg_dw_wgrad_blocks(int N, int Ho, int Wo, int C);
 int seg_dw_wgrad(const float* dy, long lddy, const float* x, long ldx, int N, int H, int W, int C,
                  const float* in_scale, const float* in_shift, int in_act,
                  int Ho, int Wo, int stride, float* part, hipStream_t stream);
-/* The data / weight gradient of a depthwise conv followed by a train-mode BatchNorm (+ act), taking dA -- the gradient
- * of the BN + act output -- instead of dY (round 5, "BIN"): dY = seg_bn_bwd_apply(dA, y; mean, scale, shift, act,
- * coef) is formed on load from dA and the conv's pre-BN output y ([Ho*Wo*N][ldy]) and never stored; bitwise the
- * apply pass followed by seg_dw_dgrad / seg_dw_wgrad (the same arithmetic, rounded to the storage type as that pass
- * stores it).  coef [3][C] from seg_bn_bwd_coef or seg_bn_bwd_finalize_tiles. */
-int seg_dw_dgrad_bin(const float* da, long ldda, int N, int Ho, int Wo, int C, const float* wk, float* dx, long lddx,
-                     int H, int W, int stride, int accumulate, const float* y, long ldy, const float* mean,
-                     const float* scale, const float* shift, int act, const float* coef, hipStream_t stream);
-int seg_dw_wgrad_bin(const float* da, long ldda, const float* x, long ldx, int N, int H, int W, int C,
-                     const float* in_scale, const float* in_shift, int in_act, int Ho, int Wo, int stride, float* part,
-                     const float* y, long ldy, const float* mean, const float* scale, const float* shift, int act,
-                     const float* coef, hipStream_t stream);
 
 /* The NCHW image batch (as the reference's DataLoader delivers it) as NHWC rows of
  * `ld` channels, zero-padded: the Cin = 3 first conv (MobileNetV2 features[0],
@@ -466,14 +454,6 @@ int seg_bn_bwd_apply_bf16io(const seg_bf16* da, long ldda, const seg_bf16* y, lo
                             seg_bf16* dy, long lddy, hipStream_t stream);
 int seg_dw_wgrad_bf16io(const seg_bf16* dy, long lddy, const seg_bf16* x, long ldx, int N, int H, int W, int C, const
     float* in_scale, const float* in_shift, int in_act, int Ho, int Wo, int stride, float* part, hipStream_t stream);
-int seg_dw_dgrad_bin_bf16io(const seg_bf16* da, long ldda, int N, int Ho, int Wo, int C, const float* wk, seg_bf16* dx,
-                            long lddx, int H, int W, int stride, int accumulate, const seg_bf16* y, long ldy,
-                            const float* mean, const float* scale, const float* shift, int act, const float* coef,
-                            hipStream_t stream);
-int seg_dw_wgrad_bin_bf16io(const seg_bf16* da, long ldda, const seg_bf16* x, long ldx, int N, int H, int W, int C,
-                            const float* in_scale, const float* in_shift, int in_act, int Ho, int Wo, int stride,
-                            float* part, const seg_bf16* y, long ldy, const float* mean, const float* scale,
-                            const float* shift, int act, const float* coef, hipStream_t stream);
 int seg_conv_igemm_bf16io(const seg_bf16* in, long ldin, int N, int H, int W, int Cin, const float* wk, int ldk, const
     float* bias, seg_bf16* out, long ldout, int Ho, int Wo, int Cout, int ks, int stride, int pad, const seg_bf16*
     add, long ldadd, float* stat, hipStream_t stream);

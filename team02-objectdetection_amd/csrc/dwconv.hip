@@ -70,65 +70,6 @@ struct RowIn {
   }
 };
 
-// BatchNorm backward formed on load (BIN): the row reader of a depthwise conv's data / weight gradient whose dY is
-// the backward of the conv's own BatchNorm + activation, dY = seg_bnbwd4(dA, y; coefficients) -- the bn_bwd_apply
-// pass's arithmetic, rounded to the storage type exactly as that pass stores it -- so dY is never written to HBM
-// (round 5).  Zero outside the image, as the stored dY's padding taps.
-struct BinCoef {
-  f32x4 sc, sh, mu, k1, k2, k3;
-  int act;
-};
-struct NoCoef {};
-
-template <typename T>
-__device__ __forceinline__ f32x4 round_st(f32x4 v) {  // the value a T store followed by a T load gives back
-  if constexpr (sizeof(T) == 2) return __builtin_convertvector(__builtin_convertvector(v, bf16x4), f32x4);
-  else return v;
-}
-
-template <typename T>
-__device__ __forceinline__ BinCoef bin_coef(const float* scale, const float* shift, const float* mean,
-                                            const float* coef, int C, int c, int act) {
-  BinCoef b;
-  b.sc = ld4(scale + c);
-  b.sh = ld4(shift + c);
-  b.mu = ld4(mean + c);
-  b.k1 = ld4(coef + c);
-  b.k2 = ld4(coef + C + c);
-  b.k3 = ld4(coef + 2 * C + c);
-  b.act = act;
-  return b;
-}
-
-template <typename T>
-__device__ __forceinline__ f32x4 bin_dy(f32x4 da, f32x4 y, const BinCoef& b) {
-  return round_st<T>(seg_bnbwd4(da, y, b.sc, b.sh, b.mu, b.k1, b.k2, b.k3, b.act));
-}
-
-template <typename T>
-struct RowBin {
-  const T* p;      // dA row (clamped) + channel offset
-  const T* q;      // y row
-  long ld, ldq;
-  int W;
-  bool ok;
-  __device__ __forceinline__ void init(const T* base, const T* ybase, int h, int H, int W_, long ld_, long ldq_) {
-    ok = (unsigned)h < (unsigned)H;
-    const int hc = h < 0 ? 0 : (h >= H ? H - 1 : h);
-    p = base + (long)hc * W_ * ld_;
-    q = ybase + (long)hc * W_ * ldq_;
-    ld = ld_;
-    ldq = ldq_;
-    W = W_;
-  }
-  __device__ __forceinline__ f32x4 at(int wi, const BinCoef& b) const {
-    const int wc = wi < 0 ? 0 : (wi >= W ? W - 1 : wi);
-    const f32x4 v = bin_dy<T>(ld4(p + (long)wc * ld), ld4(q + (long)wc * ldq), b);
-    const bool in = ok && (unsigned)wi < (unsigned)W;
-    return in ? v : f32x4{0.f, 0.f, 0.f, 0.f};
-  }
-};
-
 // Store a strip's TW results (after all of its loads were issued: no store sits
 // between two loads, so the scheduler can batch the strip's loads).  CHECK: the
 // strip crosses the row end (only the last strip of a row when TW does not divide it).
@@ -149,22 +90,13 @@ __device__ __forceinline__ void store_strip(T* o, long ld, const f32x4 (&acc)[TW
 // of dY with the flipped kernel.  ACC: out += (the data gradient's accumulate).
 // EPI (inference, BN folded into wk): out = act(acc + obias) -- the folded
 // BatchNorm shift and the ReLU6 applied in the epilogue.
-// BIN (the stride-1 data gradient): `in` holds dA and dY is formed on load from it and the conv's pre-BN output
-// (bin: y rows, BatchNorm statistics and the backward's coefficients; RowBin above).
-struct BinArgs {
-  const void* y; long ldy;
-  const float* scale; const float* shift; const float* mean; const float* coef;
-  int act;
-};
-
-template <int S, bool LAZY, bool FLIP, bool ACC, bool EPI = false, typename T = float, bool BIN = false>
+template <int S, bool LAZY, bool FLIP, bool ACC, bool EPI = false, typename T = float>
 __global__ __launch_bounds__(256) void dw_fwd_kernel(const T* __restrict__ in, long ldin, int N, int H, int W,
                                                      int C, const float* __restrict__ isc,
                                                      const float* __restrict__ ish, int iact,
                                                      const float* __restrict__ wk, T* __restrict__ out,
                                                      long ldout, int Ho, int Wo,
-                                                     const float* __restrict__ obias, int oact, BinArgs bin = {}) {
-  static_assert(!BIN || (S == 1 && FLIP && !LAZY && !EPI), "BIN: the stride-1 data gradient");
+                                                     const float* __restrict__ obias, int oact) {
   const int CG = C >> 2;
   const int SPR = (Wo + TW - 1) / TW;
   const long total = (long)N * Ho * SPR * CG;
@@ -181,32 +113,20 @@ __global__ __launch_bounds__(256) void dw_fwd_kernel(const T* __restrict__ in, l
 #pragma unroll
     for (int t = 0; t < 9; ++t) w[t] = ld4(wk + (FLIP ? 8 - t : t) * C + c);
     RowIn<LAZY, T> r[3];
-    RowBin<T> rb[3];
-    BinCoef bc;
-    if constexpr (BIN) bc = bin_coef<T>(bin.scale, bin.shift, bin.mean, bin.coef, C, c, bin.act);
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
-      if constexpr (BIN) {
-        rb[k].init(in + (long)n * H * W * ldin + c, static_cast<const T*>(bin.y) + (long)n * H * W * bin.ldy + c,
-                   ho * S - 1 + k, H, W, ldin, bin.ldy);
-      } else {
-        r[k].init(in + (long)n * H * W * ldin + c, ho * S - 1 + k, H, W, ldin);
-        r[k].act = iact;
-        if (LAZY) {
-          r[k].sc = ld4(isc + c);
-          r[k].sh = ld4(ish + c);
-        }
+      r[k].init(in + (long)n * H * W * ldin + c, ho * S - 1 + k, H, W, ldin);
+      r[k].act = iact;
+      if (LAZY) {
+        r[k].sc = ld4(isc + c);
+        r[k].sh = ld4(ish + c);
       }
     }
-    auto rd = [&](int k, int wi) -> f32x4 {
-      if constexpr (BIN) return rb[k].at(wi, bc);
-      else return r[k].at(wi);
-    };
     f32x4 a[3], b[3];  // input columns wo*S-1 and wo*S (stride 1), or column wo*S-1 (stride 2)
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
-      a[k] = rd(k, ws * S - 1);
-      if (S == 1) b[k] = rd(k, ws);
+      a[k] = r[k].at(ws * S - 1);
+      if (S == 1) b[k] = r[k].at(ws);
     }
     f32x4 acc[TW];
 #pragma unroll
@@ -218,10 +138,10 @@ __global__ __launch_bounds__(256) void dw_fwd_kernel(const T* __restrict__ in, l
         f32x4 c1, c2;
         if (S == 1) {
           c1 = b[k];
-          c2 = rd(k, wo + 1);
+          c2 = r[k].at(wo + 1);
         } else {
-          c1 = rd(k, 2 * wo);
-          c2 = rd(k, 2 * wo + 1);
+          c1 = r[k].at(2 * wo);
+          c2 = r[k].at(2 * wo + 1);
         }
         acc[t] += a[k] * w[k * 3 + 0];
         acc[t] += c1 * w[k * 3 + 1];
@@ -248,12 +168,11 @@ __global__ __launch_bounds__(256) void dw_fwd_kernel(const T* __restrict__ in, l
 //   dX[2j]   = sum_rows w[ky][1] dY[.][j]
 //   dX[2j+1] = sum_rows w[ky][0] dY[.][j+1] + w[ky][2] dY[.][j]
 // A thread owns TW dX columns (TW/2 pairs); dY column j+1 slides to the next pair.
-// BIN: dy holds dA, dY formed on load (as dw_fwd_kernel's BIN).
-template <typename T, bool BIN = false>
+template <typename T>
 __global__ __launch_bounds__(256) void dw_dgrad_s2_kernel(const T* __restrict__ dy, long lddy, int N, int Ho,
                                                           int Wo, int C, const float* __restrict__ wk,
                                                           T* __restrict__ dx, long lddx, int H, int W,
-                                                          int accumulate, BinArgs bin = {}) {
+                                                          int accumulate) {
   const int CG = C >> 2;
   const int SPR = (W + TW - 1) / TW;
   const long total = (long)N * H * SPR * CG;
@@ -268,22 +187,9 @@ __global__ __launch_bounds__(256) void dw_dgrad_s2_kernel(const T* __restrict__ 
     // row slots: slot 0 = (even: ky 1, ho hq/2 | odd: ky 0, ho (hq+1)/2), slot 1 = (odd: ky 2, ho (hq-1)/2)
     const int ky0 = odd ? 0 : 1, ho0 = odd ? (hq + 1) >> 1 : hq >> 1, ho1 = (hq - 1) >> 1;
     RowIn<false, T> r[2];
-    RowBin<T> rb[2];
-    BinCoef bc;
     const T* img = dy + (long)n * Ho * Wo * lddy + c;
-    if constexpr (BIN) {
-      bc = bin_coef<T>(bin.scale, bin.shift, bin.mean, bin.coef, C, c, bin.act);
-      const T* yimg = static_cast<const T*>(bin.y) + (long)n * Ho * Wo * bin.ldy + c;
-      rb[0].init(img, yimg, ho0, Ho, Wo, lddy, bin.ldy);
-      rb[1].init(img, yimg, odd ? ho1 : -1, Ho, Wo, lddy, bin.ldy);
-    } else {
-      r[0].init(img, ho0, Ho, Wo, lddy);
-      r[1].init(img, odd ? ho1 : -1, Ho, Wo, lddy);
-    }
-    auto rd = [&](int k, int wi) -> f32x4 {
-      if constexpr (BIN) return rb[k].at(wi, bc);
-      else return r[k].at(wi);
-    };
+    r[0].init(img, ho0, Ho, Wo, lddy);
+    r[1].init(img, odd ? ho1 : -1, Ho, Wo, lddy);
     f32x4 w[2][3];
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
@@ -292,7 +198,7 @@ __global__ __launch_bounds__(256) void dw_dgrad_s2_kernel(const T* __restrict__ 
       for (int kx = 0; kx < 3; ++kx) w[s][kx] = ld4(wk + (ky * 3 + kx) * C + c);
     }
     const int j0 = ws >> 1;
-    f32x4 dj[2] = {rd(0, j0), rd(1, j0)};
+    f32x4 dj[2] = {r[0].at(j0), r[1].at(j0)};
     f32x4 acc[TW];
 #pragma unroll
     for (int t = 0; t < TW / 2; ++t) {
@@ -300,7 +206,7 @@ __global__ __launch_bounds__(256) void dw_dgrad_s2_kernel(const T* __restrict__ 
       f32x4 e = {0.f, 0.f, 0.f, 0.f}, f = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
-        const f32x4 dj1 = rd(s, j + 1);
+        const f32x4 dj1 = r[s].at(j + 1);
         e += dj[s] * w[s][1];
         f += dj1 * w[s][0];
         f += dj[s] * w[s][2];
@@ -321,14 +227,13 @@ __global__ __launch_bounds__(256) void dw_dgrad_s2_kernel(const T* __restrict__ 
 // dY[p][c] * X[src(p, tap)][c].  Block = RG row groups x TC channel groups; a
 // thread slides along its strips keeping 9 float4 accumulators, then a fixed-
 // order LDS tree reduction over the row groups (deterministic).
-// BIN: dy holds dA, dY formed on load (as dw_fwd_kernel's BIN).
-template <int S, bool LAZY, typename T = float, bool BIN = false>
+template <int S, bool LAZY, typename T = float>
 __global__ __launch_bounds__(256) void dw_wgrad_kernel(const T* __restrict__ dy, long lddy,
                                                        const T* __restrict__ x, long ldx, int N, int H, int W,
                                                        int C, const float* __restrict__ isc,
                                                        const float* __restrict__ ish, int iact, int Ho, int Wo,
                                                        int TC, int gy, int strips_per_block, int items,
-                                                       float* __restrict__ part, BinArgs bin = {}) {
+                                                       float* __restrict__ part) {
   extern __shared__ __attribute__((aligned(16))) f32x4 red[];  // [RG][TC][9]
   const int CG = C >> 2;
   const int RG = 256 / TC;
@@ -355,8 +260,6 @@ __global__ __launch_bounds__(256) void dw_wgrad_kernel(const T* __restrict__ dy,
       sc = ld4(isc + c);
       sh = ld4(ish + c);
     }
-    BinCoef bc;
-    if constexpr (BIN) bc = bin_coef<T>(bin.scale, bin.shift, bin.mean, bin.coef, C, c, bin.act);
     for (long st = s0 + rg; st < s1; st += RG) {
       const long row = st / SPR;
       const int ws = (int)(st - row * SPR) * TWW;
@@ -370,7 +273,6 @@ __global__ __launch_bounds__(256) void dw_wgrad_kernel(const T* __restrict__ dy,
         r[k].act = iact;
       }
       const T* g = dy + (row * Wo + ws) * lddy + c;
-      const T* gyv = BIN ? static_cast<const T*>(bin.y) + (row * Wo + ws) * bin.ldy + c : nullptr;
       f32x4 a[3], b[3];
 #pragma unroll
       for (int k = 0; k < 3; ++k) {
@@ -380,9 +282,7 @@ __global__ __launch_bounds__(256) void dw_wgrad_kernel(const T* __restrict__ dy,
 #pragma unroll 2
       for (int u = 0; u < TWW; ++u) {
         const int wo = ws + u;
-        const long uu = wo < Wo ? u : Wo - 1 - ws;
-        f32x4 g0 = ld4(g + uu * lddy);
-        if constexpr (BIN) g0 = bin_dy<T>(g0, ld4(gyv + uu * bin.ldy), bc);
+        const f32x4 g0 = ld4(g + (long)(wo < Wo ? u : Wo - 1 - ws) * lddy);
         const f32x4 gv = wo < Wo ? g0 : f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int k = 0; k < 3; ++k) {
@@ -508,33 +408,21 @@ SEG_API int seg_dw_fwd_bias_act(const float* in, long ldin, int N, int H, int W,
 
 template <typename T>
 static int dw_dgrad_impl(const T* dy, long lddy, int N, int Ho, int Wo, int C, const float* wk, T* dx,
-                         long lddx, int H, int W, int stride, int accumulate, hipStream_t stream,
-                         const BinArgs* bin = nullptr) {
+                         long lddx, int H, int W, int stride, int accumulate, hipStream_t stream) {
   if ((C & 3) || (lddy & 3) || (lddx & 3) || (stride != 1 && stride != 2)) return (int)hipErrorInvalidValue;
-  if (bin && (!bin->y || (bin->ldy & 3) || !bin->scale || !bin->shift || !bin->mean || !bin->coef ||
-              bin->act < SEG_ACT_NONE || bin->act > SEG_ACT_RELU6))
-    return (int)hipErrorInvalidValue;
-  const BinArgs b = bin ? *bin : BinArgs{};
   if (stride == 1) {
     if (H != Ho || W != Wo) return (int)hipErrorInvalidValue;
     const int grid = item_grid((long)N * H * ((W + TW - 1) / TW) * (C / 4));
-#define SEG_DWD1(ACC, B)                                                                                         \
-  hipLaunchKernelGGL((dw_fwd_kernel<1, false, true, ACC, false, T, B>), dim3(grid), dim3(256), 0, stream, dy, lddy, N, \
-                     Ho, Wo, C, nullptr, nullptr, 0, wk, dx, lddx, H, W, nullptr, 0, b)
-    if (bin) {
-      if (accumulate) SEG_DWD1(true, true); else SEG_DWD1(false, true);
-    } else {
-      if (accumulate) SEG_DWD1(true, false); else SEG_DWD1(false, false);
-    }
-#undef SEG_DWD1
+    if (accumulate)
+      hipLaunchKernelGGL((dw_fwd_kernel<1, false, true, true, false, T>), dim3(grid), dim3(256), 0, stream, dy, lddy, N, Ho, Wo,
+                         C, nullptr, nullptr, 0, wk, dx, lddx, H, W, nullptr, 0);
+    else
+      hipLaunchKernelGGL((dw_fwd_kernel<1, false, true, false, false, T>), dim3(grid), dim3(256), 0, stream, dy, lddy, N, Ho,
+                         Wo, C, nullptr, nullptr, 0, wk, dx, lddx, H, W, nullptr, 0);
   } else {
     const int grid = item_grid((long)N * H * ((W + TW - 1) / TW) * (C / 4));
-    if (bin)
-      hipLaunchKernelGGL((dw_dgrad_s2_kernel<T, true>), dim3(grid), dim3(256), 0, stream, dy, lddy, N, Ho, Wo, C, wk, dx,
-                         lddx, H, W, accumulate, b);
-    else
-      hipLaunchKernelGGL((dw_dgrad_s2_kernel<T, false>), dim3(grid), dim3(256), 0, stream, dy, lddy, N, Ho, Wo, C, wk,
-                         dx, lddx, H, W, accumulate, b);
+    hipLaunchKernelGGL(dw_dgrad_s2_kernel<T>, dim3(grid), dim3(256), 0, stream, dy, lddy, N, Ho, Wo, C, wk, dx, lddx,
+                       H, W, accumulate);
   }
   SEG_RET_LAST();
 }
@@ -545,22 +433,6 @@ SEG_API int seg_dw_dgrad(const float* dy, long lddy, int N, int Ho, int Wo, int 
 SEG_API int seg_dw_dgrad_bf16io(const __bf16* dy, long lddy, int N, int Ho, int Wo, int C, const float* wk, __bf16* dx,
                                 long lddx, int H, int W, int stride, int accumulate, hipStream_t stream) {
   return dw_dgrad_impl(dy, lddy, N, Ho, Wo, C, wk, dx, lddx, H, W, stride, accumulate, stream);
-}
-// The data gradient of a depthwise conv followed by a train-mode BatchNorm (+ act), from dA (the gradient of the BN +
-// act output): dY = seg_bn_bwd_apply(dA, y; mean, scale, shift, act, coef) formed on load, never stored (BIN).
-SEG_API int seg_dw_dgrad_bin(const float* da, long ldda, int N, int Ho, int Wo, int C, const float* wk, float* dx,
-                             long lddx, int H, int W, int stride, int accumulate, const float* y, long ldy,
-                             const float* mean, const float* scale, const float* shift, int act, const float* coef,
-                             hipStream_t stream) {
-  const BinArgs b{y, ldy, scale, shift, mean, coef, act};
-  return dw_dgrad_impl(da, ldda, N, Ho, Wo, C, wk, dx, lddx, H, W, stride, accumulate, stream, &b);
-}
-SEG_API int seg_dw_dgrad_bin_bf16io(const __bf16* da, long ldda, int N, int Ho, int Wo, int C, const float* wk,
-                                    __bf16* dx, long lddx, int H, int W, int stride, int accumulate, const __bf16* y,
-                                    long ldy, const float* mean, const float* scale, const float* shift, int act,
-                                    const float* coef, hipStream_t stream) {
-  const BinArgs b{y, ldy, scale, shift, mean, coef, act};
-  return dw_dgrad_impl(da, ldda, N, Ho, Wo, C, wk, dx, lddx, H, W, stride, accumulate, stream, &b);
 }
 
 SEG_API long seg_dw_wgrad_blocks(int N, int Ho, int Wo, int C) {
@@ -575,32 +447,22 @@ SEG_API long seg_dw_wgrad_blocks(int N, int Ho, int Wo, int C) {
 template <typename T>
 static int dw_wgrad_impl(const T* dy, long lddy, const T* x, long ldx, int N, int H, int W, int C,
                          const float* in_scale, const float* in_shift, int in_act, int Ho, int Wo, int stride,
-                         float* part, hipStream_t stream, const BinArgs* bin = nullptr) {
+                         float* part, hipStream_t stream) {
   if ((C & 3) || (lddy & 3) || (ldx & 3) || (stride != 1 && stride != 2) || ((in_scale == nullptr) != (in_shift == nullptr)))
     return (int)hipErrorInvalidValue;
-  if (bin && (!bin->y || (bin->ldy & 3) || !bin->scale || !bin->shift || !bin->mean || !bin->coef ||
-              bin->act < SEG_ACT_NONE || bin->act > SEG_ACT_RELU6))
-    return (int)hipErrorInvalidValue;
-  const BinArgs b = bin ? *bin : BinArgs{};
   int TC, gy, spb;
   long gx;
   wgrad_tiling(C, &TC, &gy);
   wgrad_grid(N, Ho, Wo, C, &gx, &spb);
   const size_t lds = (size_t)(256 / TC) * TC * 9 * sizeof(f32x4);
   const bool lazy = in_scale != nullptr;
-#define SEG_DW_WG(S, L, B)                                                                                      \
-  hipLaunchKernelGGL((dw_wgrad_kernel<S, L, T, B>), dim3((unsigned)seg_side_grid(gx * gy)), dim3(256), lds, stream, dy, \
-                     lddy, x, ldx, N, H, W, C, in_scale, in_shift, in_act, Ho, Wo, TC, gy, spb, (int)(gx * gy), part, b)
-  if (bin) {
-    if (stride == 1) {
-      if (lazy) SEG_DW_WG(1, true, true); else SEG_DW_WG(1, false, true);
-    } else {
-      if (lazy) SEG_DW_WG(2, true, true); else SEG_DW_WG(2, false, true);
-    }
-  } else if (stride == 1) {
-    if (lazy) SEG_DW_WG(1, true, false); else SEG_DW_WG(1, false, false);
+#define SEG_DW_WG(S, L)                                                                                         \
+  hipLaunchKernelGGL((dw_wgrad_kernel<S, L, T>), dim3((unsigned)seg_side_grid(gx * gy)), dim3(256), lds, stream, dy, \
+                     lddy, x, ldx, N, H, W, C, in_scale, in_shift, in_act, Ho, Wo, TC, gy, spb, (int)(gx * gy), part)
+  if (stride == 1) {
+    if (lazy) SEG_DW_WG(1, true); else SEG_DW_WG(1, false);
   } else {
-    if (lazy) SEG_DW_WG(2, true, false); else SEG_DW_WG(2, false, false);
+    if (lazy) SEG_DW_WG(2, true); else SEG_DW_WG(2, false);
   }
 #undef SEG_DW_WG
   SEG_RET_LAST();
@@ -614,20 +476,4 @@ SEG_API int seg_dw_wgrad_bf16io(const __bf16* dy, long lddy, const __bf16* x, lo
                                 const float* in_scale, const float* in_shift, int in_act, int Ho, int Wo, int stride,
                                 float* part, hipStream_t stream) {
   return dw_wgrad_impl(dy, lddy, x, ldx, N, H, W, C, in_scale, in_shift, in_act, Ho, Wo, stride, part, stream);
-}
-// The weight gradient of a depthwise conv followed by a train-mode BatchNorm (+ act), from dA: dY formed on load as
-// seg_dw_dgrad_bin does (BIN).
-SEG_API int seg_dw_wgrad_bin(const float* da, long ldda, const float* x, long ldx, int N, int H, int W, int C,
-                             const float* in_scale, const float* in_shift, int in_act, int Ho, int Wo, int stride,
-                             float* part, const float* y, long ldy, const float* mean, const float* scale,
-                             const float* shift, int act, const float* coef, hipStream_t stream) {
-  const BinArgs b{y, ldy, scale, shift, mean, coef, act};
-  return dw_wgrad_impl(da, ldda, x, ldx, N, H, W, C, in_scale, in_shift, in_act, Ho, Wo, stride, part, stream, &b);
-}
-SEG_API int seg_dw_wgrad_bin_bf16io(const __bf16* da, long ldda, const __bf16* x, long ldx, int N, int H, int W, int C,
-                                    const float* in_scale, const float* in_shift, int in_act, int Ho, int Wo, int stride,
-                                    float* part, const __bf16* y, long ldy, const float* mean, const float* scale,
-                                    const float* shift, int act, const float* coef, hipStream_t stream) {
-  const BinArgs b{y, ldy, scale, shift, mean, coef, act};
-  return dw_wgrad_impl(da, ldda, x, ldx, N, H, W, C, in_scale, in_shift, in_act, Ho, Wo, stride, part, stream, &b);
 }

@@ -132,11 +132,6 @@ PROTOTYPES["seg_conv_igemm_bf16_ic"] = PROTOTYPES["seg_conv_igemm_act_ic"]
 PROTOTYPES["seg_conv_igemm_f16_ic"] = PROTOTYPES["seg_conv_igemm_act_ic"]
 PROTOTYPES["seg_conv_igemm_bnout_bf16io_w16"] = PROTOTYPES["seg_conv_igemm_bnout"]
 PROTOTYPES["seg_bn_bwd_apply_bf16io"] = PROTOTYPES["seg_bn_bwd_apply"]
-# depthwise gradients with the conv's BN backward formed on load (BIN): + y, ldy, mean, scale, shift, act, coef
-PROTOTYPES["seg_dw_dgrad_bin"] = (_I, PROTOTYPES["seg_dw_dgrad"][1][:-1] + [_V, _L, _V, _V, _V, _I, _V, _V])
-PROTOTYPES["seg_dw_wgrad_bin"] = (_I, PROTOTYPES["seg_dw_wgrad"][1][:-1] + [_V, _L, _V, _V, _V, _I, _V, _V])
-PROTOTYPES["seg_dw_dgrad_bin_bf16io"] = PROTOTYPES["seg_dw_dgrad_bin"]
-PROTOTYPES["seg_dw_wgrad_bin_bf16io"] = PROTOTYPES["seg_dw_wgrad_bin"]
 PROTOTYPES["seg_conv_wgrad_bf16io"] = PROTOTYPES["seg_conv_wgrad"]
 # lazy-BN (input transform) variants: + in_scale, in_shift, in_act before the stream
 for _n in ("seg_conv_igemm", "seg_conv_wgrad"):

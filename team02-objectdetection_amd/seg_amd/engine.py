@@ -405,13 +405,8 @@ class ConvOp:
         rt.bn_parts[id(p)] = [part, tiles, None]
         return (rt.ptr(py), py.ld, scale, shift, mean, p.act, part.data_ptr()), p
 
-    def _bin_ok(self, rt, dA) -> bool:
-        """A depthwise conv's BN backward formed on load by its data / weight gradients (seg_dw_*_bin)."""
-        return BIN_DW and self.kind == "dw" and self.bn is not None and dA.ld % 4 == 0 and self.y.ld % 4 == 0
-
     def backward(self, rt):
         s, y = rt.stream, self.y
-        bin_ = None
         dA = rt.grad_of(self.out)
         if self.bn is not None:
             if not rt.training:
@@ -424,23 +419,8 @@ class ConvOp:
             # once (3 |Y|), credited to the launch that writes dY
             abytes = 3 * M * C * rt.es
             bp = rt.bn_parts.pop(id(self), None)
-            bnout = bp is not None and bp[2] == rt.wgen.get(self.out.buf)
-            if self._bin_ok(rt, dA):
-                # depthwise conv: its data and weight gradients form dY from dA and y on load (BIN); only the
-                # coefficients are computed here -- from the producer epilogue's partials (BNOUT) or one reduction
-                coef = rt.tmp(3 * C)
-                if bnout:
-                    rt.tcall("bn_bwd", 0, "seg_bn_bwd_finalize_tiles", bp[0].data_ptr(), bp[1], M, C,
-                             self.bn.weight.data_ptr(), invstd, g_w, g_b, coef.data_ptr(), s)
-                else:
-                    work = rt.tmp(query("seg_chan_workspace_floats", M, C))
-                    rt.tcall("bn_bwd", 2 * M * C * rt.es, rt.k("seg_bn_bwd_coef"), rt.gptr(dA), dA.ld, rt.ptr(y), y.ld,
-                             M, C, self.bn.weight.data_ptr(), mean, invstd, scale, shift, self.act, g_w, g_b,
-                             work.data_ptr(), coef.data_ptr(), s)
-                bin_ = (rt.ptr(y), y.ld, mean, scale, shift, self.act, coef.data_ptr())
-                dY = dA
-            elif bnout:
-                dY = Act(rt.tmp_buf(M * r4(C)), 0, r4(C), C, y.N, y.H, y.W)
+            dY = Act(rt.tmp_buf(M * r4(C)), 0, r4(C), C, y.N, y.H, y.W)
+            if bp is not None and bp[2] == rt.wgen.get(self.out.buf):
                 # the reduction's partials came out of the epilogue of the data gradient that completed dA (nothing
                 # wrote the buffer since): finalize them, then the apply
                 coef = rt.tmp(3 * C)
@@ -449,7 +429,6 @@ class ConvOp:
                 rt.tcall("bn_bwd", abytes, rt.k("seg_bn_bwd_apply"), rt.gptr(dA), dA.ld, rt.ptr(y), y.ld, M, C, mean,
                          scale, shift, self.act, coef.data_ptr(), rt.ptr(dY), dY.ld, s)
             else:
-                dY = Act(rt.tmp_buf(M * r4(C)), 0, r4(C), C, y.N, y.H, y.W)
                 work = rt.tmp(query("seg_chan_workspace_floats", M, C) + 3 * C)
                 rt.tcall("bn_bwd", abytes, rt.k("seg_bn_backward"), rt.gptr(dA), dA.ld, rt.ptr(y), y.ld, M, C,
                          self.bn.weight.data_ptr(), mean, invstd, scale, shift, self.act,
@@ -469,14 +448,14 @@ class ConvOp:
                 rt.grad_param(p)
         late = FORK_LATE and not self.first
         if late:  # the data gradient first: the side stream's weight gradient then runs beside
-            self._dgrad(rt, dY, dYp, s, bin_)  # the next layer's memory-bound BN backward, not this dgrad
+            self._dgrad(rt, dY, dYp, s)  # the next layer's memory-bound BN backward, not this dgrad
         ctx, sw = rt.fork()
         with ctx:
-            self._param_grads(rt, dY, dYp, sw, bin_)
+            self._param_grads(rt, dY, dYp, sw)
         if not self.first and not late:
-            self._dgrad(rt, dY, dYp, s, bin_)
+            self._dgrad(rt, dY, dYp, s)
 
-    def _param_grads(self, rt, dY, dYp, s, bin_=None):
+    def _param_grads(self, rt, dY, dYp, s):
         """Bias gradient (column sum of dY), weight gradient (split-K slabs + fixed-order
         reduce) and the DDP readiness hook, all on stream `s`."""
         y, M = self.y, self.y.M
@@ -496,9 +475,8 @@ class ConvOp:
             if self.kind == "dw":
                 nblk = query("seg_dw_wgrad_blocks", y.N, y.H, y.W, self.cout)
                 part = rt.tmp(nblk * 9 * self.cout)
-                name = rt.k("seg_dw_wgrad_bin" if bin_ is not None else "seg_dw_wgrad")
-                rt.call(name, dYp, dY.ld, rt.ptr(i), i.ld, i.N, i.H, i.W, i.C, *self._in_xform(rt), y.H, y.W,
-                        self.stride, part.data_ptr(), *(bin_ or ()), s)
+                rt.call(rt.k("seg_dw_wgrad"), dYp, dY.ld, rt.ptr(i), i.ld, i.N, i.H, i.W, i.C, *self._in_xform(rt), y.H, y.W,
+                     self.stride, part.data_ptr(), s)
                 rt.call("seg_conv_wgrad_reduce", part.data_ptr(), nblk, gw, self.cout, 1, 3, 1, 0, s)
             elif self.wino_w:
                 splits = query("seg_conv_wino_wgrad_splits", y.N, y.H, y.W, self.cin_pad, self.cout)
@@ -526,15 +504,13 @@ class ConvOp:
                 rt.call("seg_conv_wgrad_reduce", part.data_ptr(), splits, gw, self.cout, self.cin, self.ks, 0, 0, s)
         rt.params_done(self.params(), s)
 
-    def _dgrad(self, rt, dY, dYp, s, bin_=None):
-        """Data gradient into the input's gradient region (first writer / fused addend).  bin_: the depthwise conv's
-        BN backward formed on load (dY holds dA; seg_dw_dgrad_bin)."""
+    def _dgrad(self, rt, dY, dYp, s):
+        """Data gradient into the input's gradient region (first writer / fused addend)."""
         y, i = self.y, self.inp
         if self.kind == "dw":
             acc = rt.begin_write_accumulate(i)
-            name = rt.k("seg_dw_dgrad_bin" if bin_ is not None else "seg_dw_dgrad")
-            rt.call(name, dYp, dY.ld, y.N, y.H, y.W, self.cout, self.wk_f.data_ptr(), rt.gptr(i),
-                    i.ld, i.H, i.W, self.stride, acc, *(bin_ or ()), s)
+            rt.call(rt.k("seg_dw_dgrad"), dYp, dY.ld, y.N, y.H, y.W, self.cout, self.wk_f.data_ptr(), rt.gptr(i),
+                    i.ld, i.H, i.W, self.stride, acc, s)
         else:
             if self.stride != 1:
                 raise NotImplementedError("data gradient of a strided dense conv")
@@ -1469,9 +1445,6 @@ IGEMM2_WIDE = os.environ.get("SEG_IGEMM2_WIDE", "1") == "1"
 W16 = os.environ.get("SEG_W16", "1") == "1"
 # many-tile BN statistics merged 16 tiles per row before the per-channel finalize; SEG_BN_MERGE=0 = direct
 BN_MERGE = os.environ.get("SEG_BN_MERGE", "1") == "1"
-# a depthwise conv's BatchNorm backward formed on load by its data and weight gradients (seg_dw_*_bin): no dY apply
-# pass, no stored dY; SEG_BIN_DW=0 = the apply pass
-BIN_DW = os.environ.get("SEG_BIN_DW", "1") == "1"
 # resident-grid cap (blocks) of the side stream's weight-gradient kernels (seg_side_cap): their long-running blocks
 # otherwise hold every CU while workgroups stay pending, and the main stream's BatchNorm passes wait behind them
 # (profiles/r05_contention_*.md); 0 = uncapped

@@ -146,13 +146,6 @@ int seg_pack_conv_weight(const float* w, float* wk, int Cout, int Cin, int ks, i
 int seg_conv_wgrad_splits(long M, int Cout, int Cin, int ks);
 /* The split count the engine uses for the bf16-math weight gradients (fewer, longer blocks). */
 int seg_conv_wgrad_splits_bf16(long M, int Cout, int Cin, int ks);
-/* Resident-grid cap of the weight-gradient kernels (seg_conv_wgrad*, seg_dw_wgrad*, seg_conv_wgrad2_bf16io), which the
- * engine runs on a side stream beside the data-gradient chain: at most `blocks` (rounded down to a multiple of 8;
- * 0 = no cap, the default) persistent blocks walk a launch's work items, so the side kernel never holds every CU
- * with workgroups still pending -- the main stream's small kernels otherwise wait behind it (tools/contend.py).
- * Split-K and depthwise partials are unchanged (each work item still writes its own slab); seg_conv_wgrad2_blocks
- * (its slab count) follows the cap.  Host-side setting read at launch; returns the previous cap. */
-int seg_side_cap(int blocks);
 int seg_conv_wgrad(const float* dy, long lddy, const float* x, long ldx,
                    int N, int H, int W, int Cin, int Ho, int Wo, int Cout,
                    int ks, int stride, int pad, float* part, int splits, hipStream_t stream);

@@ -241,18 +241,6 @@ __device__ __forceinline__ f32x4 bilerp4(f32x4 v00, f32x4 v01, f32x4 v10, f32x4 
 
 #define SEG_RET_LAST() return (int)hipGetLastError()
 
-// Resident-grid cap of the weight-gradient (side-stream) kernels (seg_side_cap, csrc/wgrad.hip): 0 = none, else the
-// split-K / per-strip work items of seg_conv_wgrad*, seg_dw_wgrad* and seg_conv_wgrad2_bf16io are walked by at most
-// this many persistent blocks.  A side kernel whose grid exceeds the chip keeps workgroups pending and, while its
-// long-running resident blocks hold the CUs, the main stream's small kernels wait behind them (tools/contend.py,
-// profiles/r05_contention_*.md); a capped grid leaves room on every CU.  Results do not change (every item still
-// writes its own partial slab), except seg_conv_wgrad2_bf16io's, whose slabs are its blocks.
-extern int g_seg_side_cap;
-static inline long seg_side_grid(long items) {
-  if (g_seg_side_cap <= 0 || items <= g_seg_side_cap) return items;
-  return g_seg_side_cap;
-}
-
 // Compute units of the current device (256 on MI355X; also the answer without a device, so
 // host-side slab sizing queried on a CPU-only machine matches the GPU's).
 static inline int seg_num_cus() {

@@ -232,17 +232,14 @@ __global__ __launch_bounds__(256) void dw_wgrad_kernel(const T* __restrict__ dy,
                                                        const T* __restrict__ x, long ldx, int N, int H, int W,
                                                        int C, const float* __restrict__ isc,
                                                        const float* __restrict__ ish, int iact, int Ho, int Wo,
-                                                       int TC, int gy, int strips_per_block, int items,
+                                                       int TC, int gy, int strips_per_block,
                                                        float* __restrict__ part) {
   extern __shared__ __attribute__((aligned(16))) f32x4 red[];  // [RG][TC][9]
   const int CG = C >> 2;
   const int RG = 256 / TC;
   const int t = threadIdx.x, rg = t / TC, tc = t - rg * TC;
-  // persistent walk over the items (seg_side_cap): block b takes items b, b + gridDim.x, ...
-  for (int item = blockIdx.x; item < items; item += gridDim.x) {
-  if (item != (int)blockIdx.x) __syncthreads();  // the previous item's partial has been read out of `red`
-  const int lin = xcd_swizzle(item, items);  // neighbouring strip chunks on one XCD
-  const int gxs = items / gy;
+  const int lin = xcd_swizzle(blockIdx.x, gridDim.x);  // neighbouring strip chunks on one XCD
+  const int gxs = gridDim.x / gy;
   const int bx = lin % gxs, byy = lin / gxs;
   const int cg = byy * TC + tc;
   const bool active = rg < RG && cg < CG;
@@ -326,7 +323,6 @@ __global__ __launch_bounds__(256) void dw_wgrad_kernel(const T* __restrict__ dy,
 #pragma unroll
     for (int k = 0; k < 9; ++k) st4(pb + k * C, red[tc * 9 + k]);
   }
-  }  // item
 }
 
 int item_grid(long total) { return (int)seg_cdiv(total, 256); }
@@ -457,8 +453,8 @@ static int dw_wgrad_impl(const T* dy, long lddy, const T* x, long ldx, int N, in
   const size_t lds = (size_t)(256 / TC) * TC * 9 * sizeof(f32x4);
   const bool lazy = in_scale != nullptr;
 #define SEG_DW_WG(S, L)                                                                                         \
-  hipLaunchKernelGGL((dw_wgrad_kernel<S, L, T>), dim3((unsigned)seg_side_grid(gx * gy)), dim3(256), lds, stream, dy, \
-                     lddy, x, ldx, N, H, W, C, in_scale, in_shift, in_act, Ho, Wo, TC, gy, spb, (int)(gx * gy), part)
+  hipLaunchKernelGGL((dw_wgrad_kernel<S, L, T>), dim3(gx * gy), dim3(256), lds, stream, dy, lddy, x, ldx, N, H, W, C, \
+                     in_scale, in_shift, in_act, Ho, Wo, TC, gy, spb, part)
   if (stride == 1) {
     if (lazy) SEG_DW_WG(1, true); else SEG_DW_WG(1, false);
   } else {

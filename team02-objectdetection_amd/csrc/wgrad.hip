@@ -36,7 +36,6 @@ struct WgradArgs {
   float* part;
   int N, H, W, Cin, Ho, Wo, Cout, stride, pad;
   int M, Nw, kchunk;
-  int items;                     // tiles x splits: the work items, walked by gridDim.x persistent blocks
   // optional input transform of X (XF kernels; 3x3: real pixels only, padding stays zero): x = act(x * xs[c] + xb[c]) on
   // load -- the producer's lazy BatchNorm + activation (see seg_conv_igemm_xf)
   const float* xs; const float* xb; int xact;
@@ -75,11 +74,7 @@ __global__ __launch_bounds__(256) void wgrad_kernel(WgradArgs a) {
   const int tiles = tiles_n * ((a.Cout + BM - 1) / BM);
   // 1-D grid of tiles x splits; every XCD walks whole splits (all column tiles of
   // one pixel chunk share the L2 that holds that chunk of dY and X)
-  // persistent walk (seg_side_cap): block b takes items b, b + gridDim.x, ...; with gridDim.x a multiple of 8 an
-  // item runs on the XCD it would run on as its own block, and xcd_swizzle(item, items) keeps the uncapped mapping
-  for (int item = blockIdx.x; item < a.items; item += gridDim.x) {
-  if (item != (int)blockIdx.x) __syncthreads();  // the previous item is done with the LDS tiles
-  const int lid = xcd_swizzle(item, a.items);
+  const int lid = xcd_swizzle(blockIdx.x, gridDim.x);
   const int split = lid / tiles, tile = lid - split * tiles;
   const int tn = tile % tiles_n, tm = tile / tiles_n;
   const int co0 = tm * BM, n0 = tn * BN;
@@ -289,13 +284,11 @@ __global__ __launch_bounds__(256) void wgrad_kernel(WgradArgs a) {
         if (row < a.Cout) slab[(long)row * a.Nw + col] = acc[mi][ni][r];
       }
   }
-  }  // item
 }
 
 template <int BM, int BN, int WM, int WN, bool BF = false, typename IT = float>
-int launch_wgrad(WgradArgs a, int ks, int splits, hipStream_t s) {
-  a.items = seg_cdiv(a.Cout, BM) * seg_cdiv(a.Nw, BN) * splits;
-  dim3 grid((unsigned)seg_side_grid(a.items));
+int launch_wgrad(const WgradArgs& a, int ks, int splits, hipStream_t s) {
+  dim3 grid(seg_cdiv(a.Cout, BM) * seg_cdiv(a.Nw, BN) * splits);
   if (a.xs) {  // input transform
     const bool v8 = sizeof(IT) == 2 && a.Cout % 8 == 0 && a.Cin % 8 == 0 && a.lddy % 8 == 0 && a.ldx % 8 == 0;
     if constexpr (sizeof(IT) == 2) {
@@ -337,15 +330,6 @@ void wgrad_tiles(int Cout, int Nw, int* bm, int* bn) {
 }
 
 }  // namespace
-
-int g_seg_side_cap = 0;
-
-// Set the side-stream kernels' resident-grid cap (common.h; blocks, a multiple of 8; 0 = none); returns the old one.
-SEG_API int seg_side_cap(int blocks) {
-  const int old = g_seg_side_cap;
-  if (blocks >= 0) g_seg_side_cap = blocks & ~7;
-  return old;
-}
 
 // Number of K splits (partial slabs) seg_conv_wgrad will use; the caller provides
 // a workspace of splits * Cout * ks*ks*Cin floats.

@@ -266,7 +266,7 @@ SEG_API int seg_conv_wgrad2_blocks(int N, int H, int W) {
     int n = 0;
     if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && n > 0) cus = n;
   }
-  return (int)seg_side_grid(std::max(1, std::min(N * (H / TH) * (W / TW), cus)));
+  return std::max(1, std::min(N * (H / TH) * (W / TW), cus));
 }
 
 SEG_API int seg_conv_wgrad2_bf16io(const __bf16* dy, long lddy, const __bf16* x, long ldx, int N, int H, int W,

@@ -45,7 +45,6 @@ PROTOTYPES = {
     "seg_pack_conv_weight": (_I, [_V, _V, _I, _I, _I, _I, _I, _I, _V]),
     "seg_conv_wgrad_splits": (_I, [_L, _I, _I, _I]),
     "seg_conv_wgrad_splits_bf16": (_I, [_L, _I, _I, _I]),
-    "seg_side_cap": (_I, [_I]),
     "seg_conv_wgrad": (_I, [_V, _L, _V, _L, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _V, _I, _V]),
     "seg_conv_wgrad_bf16": (_I, [_V, _L, _V, _L, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _V, _I, _V]),
     "seg_conv_wgrad_reduce": (_I, [_V, _I, _V, _I, _I, _I, _I, _I, _V]),

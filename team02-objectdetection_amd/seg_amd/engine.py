@@ -1101,7 +1101,6 @@ class Run:
 
     def __init__(self, prog: Program, image: torch.Tensor, training: bool, rec=None, side=None):
         self.prog, self.image, self.training = prog, image, training
-        _apply_side_cap()
         self.device = image.device
         self.stream = torch.cuda.current_stream(self.device).cuda_stream
         self.rec = rec
@@ -1445,19 +1444,6 @@ IGEMM2_WIDE = os.environ.get("SEG_IGEMM2_WIDE", "1") == "1"
 W16 = os.environ.get("SEG_W16", "1") == "1"
 # many-tile BN statistics merged 16 tiles per row before the per-channel finalize; SEG_BN_MERGE=0 = direct
 BN_MERGE = os.environ.get("SEG_BN_MERGE", "1") == "1"
-# resident-grid cap (blocks) of the side stream's weight-gradient kernels (seg_side_cap): their long-running blocks
-# otherwise hold every CU while workgroups stay pending, and the main stream's BatchNorm passes wait behind them
-# (profiles/r05_contention_*.md); 0 = uncapped
-SIDE_CAP = int(os.environ.get("SEG_SIDE_CAP", "0"))
-_side_cap_set = False
-
-
-def _apply_side_cap():
-    """Hand SIDE_CAP to the library once, before the first program walk sizes any weight-gradient workspace."""
-    global _side_cap_set
-    if not _side_cap_set:
-        _query("seg_side_cap", SIDE_CAP)
-        _side_cap_set = True
 
 # Diagnostics (tests flip these): the Winograd transforms one at a time (parity attribution,
 # tests/test_gpu_unet_cfg5.py) ...

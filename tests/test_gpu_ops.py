@@ -716,52 +716,3 @@ def test_bn_stats_tiles_merged(M, tile_rows, C):
         assert rel(rv, 0.9 + 0.1 * y.var(0, unbiased=True)) < 1e-6, name
     a, b = res["seg_bn_stats_tiles"][0], res["seg_bn_stats_tiles_ws"][0]
     assert rel(a, b) < 1e-6
-
-
-@pytest.mark.parametrize("kind", ["wgrad3", "wgrad1_bf16io", "dw_s1", "dw_s2_bf16io"])
-def test_side_cap_is_bitwise_uncapped(kind):
-    """seg_side_cap (the side stream's resident-grid cap): the split-K and depthwise weight gradients walk their work
-    items with at most `cap` persistent blocks; every item still writes its own partial slab, so the partials are
-    bitwise those of the uncapped launch."""
-    s = S()
-    g = torch.Generator().manual_seed(11)
-    bf = kind.endswith("bf16io")
-    dt = torch.bfloat16 if bf else torch.float32
-    old = query("seg_side_cap", 0)
-    try:
-        if kind.startswith("wgrad"):
-            ks = 3 if kind == "wgrad3" else 1
-            N, H, W, Cin, Cout = 4, 32, 64, 64, 128
-            M = N * H * W
-            dy = torch.randn(M, Cout, generator=g).to(dt).to(DEV)
-            x = torch.randn(M, Cin, generator=g).to(dt).to(DEV)
-            name = "seg_conv_wgrad_bf16io" if bf else "seg_conv_wgrad"
-            splits = query("seg_conv_wgrad_splits_bf16" if bf else "seg_conv_wgrad_splits", M, Cout, Cin, ks)
-            outs = []
-            for cap in (0, 64, 8):
-                query("seg_side_cap", cap)
-                part = torch.full((splits * Cout * ks * ks * Cin,), float("nan"), device=DEV)
-                call(name, dy.data_ptr(), Cout, x.data_ptr(), Cin, N, H, W, Cin, H, W, Cout, ks, 1, ks // 2,
-                     part.data_ptr(), splits, s)
-                outs.append(part)
-        else:
-            stride = 2 if "s2" in kind else 1
-            N, H, W, C = 4, 32, 64, 96
-            Ho, Wo = (H - 1) // stride + 1, (W - 1) // stride + 1
-            dy = torch.randn(N * Ho * Wo, C, generator=g).to(dt).to(DEV)
-            x = torch.randn(N * H * W, C, generator=g).to(dt).to(DEV)
-            name = "seg_dw_wgrad_bf16io" if bf else "seg_dw_wgrad"
-            nblk = query("seg_dw_wgrad_blocks", N, Ho, Wo, C)
-            outs = []
-            for cap in (0, 64, 8):
-                query("seg_side_cap", cap)
-                part = torch.full((nblk * 9 * C,), float("nan"), device=DEV)
-                call(name, dy.data_ptr(), C, x.data_ptr(), C, N, H, W, C, None, None, 0, Ho, Wo, stride,
-                     part.data_ptr(), s)
-                outs.append(part)
-        torch.cuda.synchronize()
-        assert torch.isfinite(outs[0]).all()
-        for o in outs[1:]:
-            assert torch.equal(o, outs[0])
-    finally:
-        query("seg_side_cap", old)

@@ -41,10 +41,10 @@ def main():
 
     base_splits = query("seg_conv_wgrad_splits_bf16", M, Cout, Cin, 3)
     print(f"side: wgrad 3x3 {Cin}->{Cout} M={M} (plan splits {base_splits}); main: BN backward {Mb}x{C}")
-    for prio_main, prio_side in ((0, 0),):
+    for prio_main, prio_side in ((0, 0), (-1, 0)):
         sm = torch.cuda.Stream(dev, priority=prio_main)
         ss = torch.cuda.Stream(dev, priority=prio_side)
-        for splits in (1, 2, 3, 4, 6):
+        for splits in (base_splits, max(base_splits // 2, 1), max(base_splits // 4, 1), 1):
             part = torch.empty(splits * Cout * 9 * Cin, device=dev)
 
             def wg(s):

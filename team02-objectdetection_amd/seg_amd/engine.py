@@ -437,7 +437,6 @@ class ConvOp:
                 rt.add_pending(self.res, dA)
         else:
             dY = dA
-        rt.flush_side()
         dYp = rt.ptr(dY) if dY.buf.startswith("#") else rt.gptr(dY)
         M = y.M
         # parameter gradients: on the side stream when overlapping (they only read dY and x,
@@ -450,17 +449,9 @@ class ConvOp:
         late = FORK_LATE and not self.first
         if late:  # the data gradient first: the side stream's weight gradient then runs beside
             self._dgrad(rt, dY, dYp, s)  # the next layer's memory-bound BN backward, not this dgrad
-
-        def side():
-            ctx, sw = rt.fork()
-            with ctx:
-                self._param_grads(rt, dY, dYp, sw)
-        if WGRAD_DEFER and late:
-            # forked only once the next op's BatchNorm backward is queued (Run.flush_side): the side stream's weight
-            # gradient then runs beside that op's data gradient instead of starving its small BN passes
-            rt.deferred.append(side)
-        else:
-            side()
+        ctx, sw = rt.fork()
+        with ctx:
+            self._param_grads(rt, dY, dYp, sw)
         if not self.first and not late:
             self._dgrad(rt, dY, dYp, s)
 
@@ -598,7 +589,6 @@ class UpsampleOp:
         rt.call(rt.k("seg_upsample_bwd"), rt.gptr(d), d.ld, 0, o.N, o.H, o.W, o.C, rt.gptr(l), l.ld, l.H, l.W, 0, acc,
              rt.stream)
         rt.mark_written(l)
-        rt.flush_side()
 
 
 class PoolOp:
@@ -621,7 +611,6 @@ class PoolOp:
         rt.call(rt.k("seg_maxpool2_bwd"), rt.ptr(i), i.ld, rt.gptr(d), d.ld, i.N, i.H, i.W, i.C, rt.gptr(i), i.ld, acc,
              rt.stream)
         rt.mark_written(i)
-        rt.flush_side()
 
 
 # ------------------------------------------------------------------------ program
@@ -1135,7 +1124,6 @@ class Run:
         self.sync = None
         self._tmp_n = 0
         self.side = side      # side stream of the parameter gradients (recorded backward)
-        self.deferred = []    # parameter-gradient forks waiting for the next op's BN backward (WGRAD_DEFER)
         self._n_fork = 0      # side-stream forks so far (index into the program's event pool)
 
     def k(self, name: str) -> str:
@@ -1241,13 +1229,7 @@ class Run:
         self.side.wait_event(ev)
         return self._side_ctx, self.side.cuda_stream
 
-    def flush_side(self):
-        """Fork the deferred parameter gradients (WGRAD_DEFER) now."""
-        while self.deferred:
-            self.deferred.pop(0)()
-
     def join(self):
-        self.flush_side()
         if self.side is None:
             return
         if self.rec is not None:
@@ -1426,9 +1408,6 @@ class Run:
 OVERLAP = os.environ.get("SEG_OVERLAP", "1") == "1"
 # fork the weight-gradient side stream after the layer's data gradient (measured: f32 +1.5 %, bf16io +-0)
 FORK_LATE = os.environ.get("SEG_FORK_LATE", "1") == "1"
-# ... and only once the next op's BatchNorm backward is queued (round 5: the side stream's long-running weight-
-# gradient blocks otherwise hold the CUs the BN passes need, profiles/r05_contention_*.md); SEG_WGRAD_DEFER=0 = off
-WGRAD_DEFER = os.environ.get("SEG_WGRAD_DEFER", "0") == "1"
 # Winograd F(2x2,3x3) for the deep f32 3x3 convs (read when a program's weights are first
 # packed); SEG_WINO=0 routes them to the LDS-halo / implicit-GEMM kernels instead.
 WINOGRAD = os.environ.get("SEG_WINO", "1") == "1"

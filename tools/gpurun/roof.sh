@@ -13,4 +13,4 @@ for c in FETCH_SIZE WRITE_SIZE; do
 done
 # matrix-core activity: MFMA-busy cycles (all SIMDs) against the GPU-active clock (sum over the 8 XCDs)
 timeout -s KILL 300 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE --kernel-trace -d $d/pmc/MFMA -o run --output-format csv -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-timer --no-bf16io-block --no-infer-block --no-unet-block "$@" > $d/pmc_MFMA.log 2>&1 || { echo "pmc MFMA failed"; tail -5 $d/pmc_MFMA.log; exit 1; }
-python tools/roofline_report.py $d/prof $d/pmc 9 $d/$name
+python tools/roofline_report.py $d/prof $d/pmc 9 $d/$name ${ROOF_MODEL:-MobileNetV2UNet}

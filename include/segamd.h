@@ -92,7 +92,7 @@ int seg_conv_pw(const float* in, long ldin, long M, int K, const float* wk, int 
  * cannot fill the 256 CUs (batch-1 inference). */
 int seg_conv_igemm_splits(long M, int Cout, int Cin, int ks);
 /* seg_conv_igemm_act / _bf16 / _f16 with split-K combined inside the launch (the inference forward's
- * batch-1 convs): when the whole grid is co-resident (and splits <= 64) the split blocks of a tile combine it
+ * batch-1 convs): when the whole grid is co-resident (and splits <= 32) the split blocks of a tile combine it
  * together, each applying the split-K epilogue to its share -- a block that cannot wait for its peers (another
  * kernel holding the CUs) leaves its share to the tile's last arrival, so no block ever spins on a peer that is
  * not resident; else the separate reduce runs.  Bitwise the two-launch result.  cnt: 4 *

@@ -137,30 +137,25 @@ __device__ __forceinline__ bool seg_last_arrival(unsigned* cnt, unsigned nblocks
   return *word != 0;
 }
 
-// In-launch combine of a split tile (split-K / split hidden range) by its own S <= 64 blocks, with no block
+// In-launch combine of a split tile (split-K / split hidden range) by its own S <= 32 blocks, with no block
 // ever waiting on a block that may not be resident (a plain "wait until all S splits arrived" spin
 // hangs when another kernel holds the CUs a peer needs, e.g. two such kernels on two streams).  The tile's
-// combine is cut into S pieces; piece p may be done by any block once the tile is complete:
+// combine is cut into S pieces, piece z belonging to split block z:
 //   * every block publishes its partial (write-through, drained: the seg_last_arrival form above) and takes a
 //     ticket; the block with the last ticket knows the tile is complete;
-//   * a non-last block polls the ticket count for at most `spin` rounds (0: not at all -- the grid is known not
-//     to be co-resident) and, if the tile completed meanwhile, claims its own piece (one atomic or on the tile's
-//     claim mask) and combines it: the parallel combine of the co-resident case;
-//   * the last block combines its own piece, then claims and combines every piece nobody has claimed yet (the
-//     pieces of blocks that gave up waiting, or left at once);
-//   * each block counts itself out; the one that completes the count re-arms the tile's four words.
+//   * a non-last block polls the ticket count for at most `spin` rounds (0: not at all -- the grid is known not to
+//     be co-resident); if the tile completed meanwhile it combines its own piece, else it gives the piece up; either
+//     way it then reports once, one atomic add of (1 << 32 | (gave up ? 1 << z : 0)) on the tile's report word;
+//   * the last block combines its own piece, waits for the S - 1 reports -- every peer already holds a ticket, so
+//     it is resident and reports within its bounded poll: this wait cannot hang -- then combines the pieces given
+//     up and re-arms the tile's words.
 // Every piece is combined exactly once, by a block that saw the tile complete; results do not depend on who.
-// cnt: 4 words per tile {tickets, leavers, claims 0-31, claims 32-63}, zero before the first launch.
-// piece(p): the block's combine of piece p (called by all threads, block-uniform p).
+// cnt: 4 words per tile {tickets, -, report (64-bit: count << 32 | given-up mask)}, zero before the first launch.
+// piece(p): the block's combine of piece p (called by all threads, block-uniform p).  word: 2 ints of LDS.
 template <typename F>
 __device__ __forceinline__ void seg_tile_combine(unsigned* cnt, int S, int z, int spin, int* word, F&& piece) {
   unsigned* tickets = cnt;
-  unsigned* leavers = cnt + 1;
-  unsigned* claims = cnt + 2;
-  auto claim = [&](int p) -> bool {  // thread 0 only
-    const unsigned bit = 1u << (p & 31);
-    return !(__hip_atomic_fetch_or(claims + (p >> 5), bit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & bit);
-  };
+  unsigned long long* report = reinterpret_cast<unsigned long long*>(cnt + 2);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's partial has landed
   __syncthreads();
   if (threadIdx.x == 0) {
@@ -168,33 +163,35 @@ __device__ __forceinline__ void seg_tile_combine(unsigned* cnt, int S, int z, in
     const int last = t == (unsigned)S - 1;
     bool ready = last;
     for (int i = 0; !ready && i < spin; ++i) {
-      __builtin_amdgcn_s_sleep(2);
       ready = __hip_atomic_load(tickets, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= (unsigned)S;
+      if (!ready) __builtin_amdgcn_s_sleep(1);
     }
     word[0] = last;
-    word[1] = ready && claim(z);
+    word[1] = ready;
   }
   __syncthreads();
-  const int last = word[0];
-  if (word[1]) piece(z);
-  if (last) {
-    for (int p = 0; p < S; ++p) {
-      if (p == z) continue;
-      __syncthreads();  // word[1] of the previous round has been read by every thread
-      if (threadIdx.x == 0) word[1] = claim(p);
-      __syncthreads();
-      if (word[1]) piece(p);
-    }
+  const int last = word[0], ready = word[1];
+  if (ready) piece(z);
+  if (!last) {
+    __syncthreads();  // this block's piece is done (its stores issued) before it reports
+    if (threadIdx.x == 0)
+      __hip_atomic_fetch_add(report, (1ull << 32) | (ready ? 0ull : 1ull << z), __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
+    return;
+  }
+  __syncthreads();  // every wave has read word[] and finished its piece
+  if (threadIdx.x == 0) {  // the S - 1 peers are resident (they hold tickets): wait for their reports
+    unsigned long long r = 0;
+    while (((r = __hip_atomic_load(report, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) >> 32) < (unsigned)S - 1)
+      __builtin_amdgcn_s_sleep(1);
+    word[1] = (int)(unsigned)r;  // the pieces given up
+    __hip_atomic_store(report, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-arm (no peer touches
+    __hip_atomic_store(tickets, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);    // either word any more)
   }
   __syncthreads();
-  if (threadIdx.x == 0 &&
-      __hip_atomic_fetch_add(leavers, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (unsigned)S - 1) {
-    // every block of the tile is done with its words: re-arm them for the next launch
-    __hip_atomic_store(tickets, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(claims, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(claims + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(leavers, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
+  const unsigned given = (unsigned)word[1];
+  for (int p = 0; p < S; ++p)
+    if ((given >> p) & 1u) piece(p);
 }
 // Bound of seg_tile_combine's poll when the grid is co-resident (~1 us per round: a few ms before a block gives
 // its piece to the last arrival -- only ever reached when another kernel holds the CUs a peer needs).

@@ -43,7 +43,7 @@ struct IgemmArgs {
   // dz and dz (by - bmu), dz = out act'(by bsc + bsh) on the values as stored, into bpart
   // [tilesM][2][Cout] for seg_bn_bwd_finalize_tiles -- the reduction pass over dA disappears
   const void* by; long ldby; const float* bsc; const float* bsh; const float* bmu; int bact; float* bpart;
-  // split-K with the combine in the launch (part set, the whole grid co-resident, <= 64 splits): seg_tile_combine's
+  // split-K with the combine in the launch (part set, the whole grid co-resident, <= 32 splits): seg_tile_combine's
   // words, [tilesM * tilesN][4] (zero before the first launch, re-armed by the tile's last leaver)
   unsigned* kcnt;
 };
@@ -739,7 +739,7 @@ int launch_igemm_bk(IgemmArgs a, int ks, hipStream_t s) {
                              : (ut ? (const void*)igemm_conv_kernel<BM, BN, WM, WN, 3, BK, true, OT, IT, WB, false>
                                    : (const void*)igemm_conv_kernel<BM, BN, WM, WN, 3, BK, false, OT, IT, WB, false>);
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, fn, NT, 0) != hipSuccess ||
-        (long)grid * splits > (long)occ * seg_num_cus() || splits > 64) {
+        (long)grid * splits > (long)occ * seg_num_cus() || splits > 32) {
       (void)hipGetLastError();
       a.kcnt = nullptr;
     }

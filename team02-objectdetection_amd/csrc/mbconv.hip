@@ -364,7 +364,7 @@ SEG_API int seg_mbconv_f16(const float* x, long ldx, int N, int H, int W, int Ci
   a.ntiles = N * a.tiles_w * a.tiles_h;
   a.work = work; a.cnt = cnt;
   if (a.splits > 1 && (!work || !cnt)) return (int)hipErrorInvalidValue;
-  if (a.splits > 64) return (int)hipErrorInvalidValue;  // seg_tile_combine's claim mask
+  if (a.splits > 32) return (int)hipErrorInvalidValue;  // seg_tile_combine's report mask
   const dim3 grid(a.ntiles, a.splits);
   const bool e = we != nullptr;
   {  // the splits wait for each other (bounded) only when the whole grid is co-resident

@@ -538,11 +538,6 @@ int seg_tape_set_arg(void* tape, long i, long value);
 int seg_tape_timing(void* tape, const int* idx, int n, int max_replays);
 int seg_tape_elapsed(void* tape, float* out);
 int seg_tape_run(void* tape, int begin, hipStream_t main, hipStream_t side, int* stop);
-/* Cap the resident blocks per CU of the weight-gradient kernels (seg_conv_wgrad*, the Winograd and depthwise
- * weight gradients) launched on `stream` at blocks_per_cu (0 = none) by padding their LDS request -- the engine's
- * weight-gradient side stream, so that its long compute-bound blocks leave wave slots to the main queue's
- * memory-bound kernels (the reference's single-stream autograd has no such overlap).  Results are unchanged. */
-int seg_stream_set_block_cap(hipStream_t stream, int blocks_per_cu);
 
 /* seg_conv_igemm2_bf16io: implicit GEMM for the deep convs of the bf16io configuration
  * (replaces aten conv2d / convolution_backward(input) of src/unet.py:58,61 and 1x1 convs

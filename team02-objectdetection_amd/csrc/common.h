@@ -238,15 +238,6 @@ __device__ __forceinline__ f32x4 bilerp4(f32x4 v00, f32x4 v01, f32x4 v10, f32x4 
 
 #define SEG_RET_LAST() return (int)hipGetLastError()
 
-// Per-stream cap on resident blocks per CU for the weight-gradient launches (seg_stream_set_block_cap, csrc/tape.hip):
-// the dynamic LDS to request so that at most the stream's cap of a kernel's blocks share a CU -- `dyn` (the launch's
-// own dynamic LDS) when the stream has no cap.  The side stream's compute-bound weight gradients otherwise take every
-// wave slot of every CU for their whole duration, and the main queue's short memory-bound kernels wait for them.
-size_t seg_cap_lds(const void* kernel, size_t dyn, hipStream_t stream);
-#define SEG_LAUNCH_CAPPED(KERNEL, GRID, BLOCK, DYN, STREAM, ...)                                               \
-  hipLaunchKernelGGL(KERNEL, GRID, BLOCK, seg_cap_lds(reinterpret_cast<const void*>(&KERNEL), (DYN), (STREAM)), \
-                     STREAM, __VA_ARGS__)
-
 // Compute units of the current device (256 on MI355X; also the answer without a device, so
 // host-side slab sizing queried on a CPU-only machine matches the GPU's).
 static inline int seg_num_cus() {

@@ -453,7 +453,7 @@ static int dw_wgrad_impl(const T* dy, long lddy, const T* x, long ldx, int N, in
   const size_t lds = (size_t)(256 / TC) * TC * 9 * sizeof(f32x4);
   const bool lazy = in_scale != nullptr;
 #define SEG_DW_WG(S, L)                                                                                         \
-  SEG_LAUNCH_CAPPED((dw_wgrad_kernel<S, L, T>), dim3(gx * gy), dim3(256), lds, stream, dy, lddy, x, ldx, N, H, W, C, \
+  hipLaunchKernelGGL((dw_wgrad_kernel<S, L, T>), dim3(gx * gy), dim3(256), lds, stream, dy, lddy, x, ldx, N, H, W, C, \
                      in_scale, in_shift, in_act, Ho, Wo, TC, gy, spb, part)
   if (stride == 1) {
     if (lazy) SEG_DW_WG(1, true); else SEG_DW_WG(1, false);

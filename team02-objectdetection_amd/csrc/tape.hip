@@ -25,8 +25,6 @@
 #include <stdint.h>
 #include <string.h>
 
-#include <mutex>
-#include <unordered_map>
 #include <vector>
 
 #include "common.h"
@@ -71,62 +69,7 @@ struct Tape {
   int nslots = 0, max_replays = 0, replay = -1;
 };
 
-struct BlockCap {
-  hipStream_t stream;
-  int blocks;
-};
-BlockCap g_caps[8];  // seg_stream_set_block_cap; read by seg_cap_lds (both under g_cap_mu)
-std::mutex g_cap_mu;
-std::unordered_map<const void*, size_t> g_static_lds;
-size_t g_lds_per_cu = 0;
-
 }  // namespace
-
-// Cap the resident blocks per CU of the weight-gradient launches issued on `stream` (seg_cap_lds) at blocks_per_cu
-// (0 = no cap): the engine's weight-gradient side stream, so that its compute-bound kernels leave wave slots to
-// the main queue's memory-bound BatchNorm / data-gradient kernels.  Results do not change (only the occupancy).
-SEG_API int seg_stream_set_block_cap(hipStream_t stream, int blocks_per_cu) {
-  if (blocks_per_cu < 0) return (int)hipErrorInvalidValue;
-  std::lock_guard<std::mutex> lock(g_cap_mu);
-  for (BlockCap& c : g_caps)
-    if (c.blocks && c.stream == stream) {
-      c.blocks = blocks_per_cu;
-      return (int)hipSuccess;
-    }
-  if (!blocks_per_cu) return (int)hipSuccess;
-  for (BlockCap& c : g_caps)
-    if (!c.blocks) {
-      c = {stream, blocks_per_cu};
-      return (int)hipSuccess;
-    }
-  return (int)hipErrorInvalidValue;
-}
-
-size_t seg_cap_lds(const void* kernel, size_t dyn, hipStream_t stream) {
-  std::lock_guard<std::mutex> lock(g_cap_mu);
-  int cap = 0;
-  for (const BlockCap& c : g_caps)
-    if (c.blocks && c.stream == stream) cap = c.blocks;
-  if (!cap) return dyn;
-  if (!g_lds_per_cu) {
-    int dev = 0, v = 0;
-    if (hipGetDevice(&dev) != hipSuccess ||
-        hipDeviceGetAttribute(&v, hipDeviceAttributeMaxSharedMemoryPerMultiprocessor, dev) != hipSuccess || v <= 0)
-      v = 160 * 1024;
-    g_lds_per_cu = (size_t)v;
-  }
-  auto it = g_static_lds.find(kernel);
-  if (it == g_static_lds.end()) {
-    hipFuncAttributes fa{};
-    const size_t st = hipFuncGetAttributes(&fa, kernel) == hipSuccess ? fa.sharedSizeBytes : 0;
-    it = g_static_lds.emplace(kernel, st).first;
-  }
-  // per-block LDS such that `cap` blocks fit a CU and cap + 1 do not (a multiple of 2560 bytes: whole allocation
-  // granules), less the kernel's static LDS
-  const size_t want = g_lds_per_cu / cap / 2560 * 2560;
-  if (want <= it->second) return dyn;
-  return std::max(dyn, want - it->second);
-}
 
 SEG_API int seg_tape_fn_index(const char* name) {
   if (!name) return -1;

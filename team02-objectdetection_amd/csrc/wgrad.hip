@@ -293,33 +293,33 @@ int launch_wgrad(const WgradArgs& a, int ks, int splits, hipStream_t s) {
     const bool v8 = sizeof(IT) == 2 && a.Cout % 8 == 0 && a.Cin % 8 == 0 && a.lddy % 8 == 0 && a.ldx % 8 == 0;
     if constexpr (sizeof(IT) == 2) {
       if (v8) {
-        if (ks == 1) SEG_LAUNCH_CAPPED((wgrad_kernel<BM, BN, WM, WN, 1, true, IT, 8, true>), grid, dim3(256), 0, s, a);
-        else SEG_LAUNCH_CAPPED((wgrad_kernel<BM, BN, WM, WN, 3, true, IT, 8, true>), grid, dim3(256), 0, s, a);
+        if (ks == 1) hipLaunchKernelGGL((wgrad_kernel<BM, BN, WM, WN, 1, true, IT, 8, true>), grid, dim3(256), 0, s, a);
+        else hipLaunchKernelGGL((wgrad_kernel<BM, BN, WM, WN, 3, true, IT, 8, true>), grid, dim3(256), 0, s, a);
         SEG_RET_LAST();
       }
     }
-    if (ks == 1) SEG_LAUNCH_CAPPED((wgrad_kernel<BM, BN, WM, WN, 1, BF, IT, 4, true>), grid, dim3(256), 0, s, a);
-    else SEG_LAUNCH_CAPPED((wgrad_kernel<BM, BN, WM, WN, 3, BF, IT, 4, true>), grid, dim3(256), 0, s, a);
+    if (ks == 1) hipLaunchKernelGGL((wgrad_kernel<BM, BN, WM, WN, 1, BF, IT, 4, true>), grid, dim3(256), 0, s, a);
+    else hipLaunchKernelGGL((wgrad_kernel<BM, BN, WM, WN, 3, BF, IT, 4, true>), grid, dim3(256), 0, s, a);
     SEG_RET_LAST();
   }
   if (BF) {
     const bool v8 = sizeof(IT) == 2 && a.Cout % 8 == 0 && a.Cin % 8 == 0 && a.lddy % 8 == 0 && a.ldx % 8 == 0;
     if constexpr (sizeof(IT) == 2) {
       if (v8) {
-        if (ks == 1) SEG_LAUNCH_CAPPED((wgrad_kernel<BM, BN, WM, WN, 1, true, IT, 8>), grid, dim3(256), 0, s, a);
-        else SEG_LAUNCH_CAPPED((wgrad_kernel<BM, BN, WM, WN, 3, true, IT, 8>), grid, dim3(256), 0, s, a);
+        if (ks == 1) hipLaunchKernelGGL((wgrad_kernel<BM, BN, WM, WN, 1, true, IT, 8>), grid, dim3(256), 0, s, a);
+        else hipLaunchKernelGGL((wgrad_kernel<BM, BN, WM, WN, 3, true, IT, 8>), grid, dim3(256), 0, s, a);
         SEG_RET_LAST();
       }
     }
     if (ks == 1) {
-      SEG_LAUNCH_CAPPED((wgrad_kernel<BM, BN, WM, WN, 1, true, IT>), grid, dim3(256), 0, s, a);
+      hipLaunchKernelGGL((wgrad_kernel<BM, BN, WM, WN, 1, true, IT>), grid, dim3(256), 0, s, a);
     } else {
-      SEG_LAUNCH_CAPPED((wgrad_kernel<BM, BN, WM, WN, 3, true, IT>), grid, dim3(256), 0, s, a);
+      hipLaunchKernelGGL((wgrad_kernel<BM, BN, WM, WN, 3, true, IT>), grid, dim3(256), 0, s, a);
     }
     SEG_RET_LAST();
   }
-  if (ks == 1) SEG_LAUNCH_CAPPED((wgrad_kernel<BM, BN, WM, WN, 1>), grid, dim3(256), 0, s, a);
-  else SEG_LAUNCH_CAPPED((wgrad_kernel<BM, BN, WM, WN, 3>), grid, dim3(256), 0, s, a);
+  if (ks == 1) hipLaunchKernelGGL((wgrad_kernel<BM, BN, WM, WN, 1>), grid, dim3(256), 0, s, a);
+  else hipLaunchKernelGGL((wgrad_kernel<BM, BN, WM, WN, 3>), grid, dim3(256), 0, s, a);
   SEG_RET_LAST();
 }
 

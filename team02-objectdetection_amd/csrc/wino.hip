@@ -604,11 +604,11 @@ SEG_API int seg_conv_wino_wgrad(const float* dy, long lddy, const float* x, long
   const int bm = Cout >= 128 ? 128 : (Cout >= 64 ? 64 : 32);
   const int bn = bm == 32 ? 128 : (Cin >= 128 ? 128 : 64);
   dim3 grid(seg_cdiv(Cout, bm) * seg_cdiv(Cin, bn) * splits, 1, 16);
-  if (bm == 128 && bn == 128) SEG_LAUNCH_CAPPED((wino_wgrad_kernel<128, 128, 64, 64>), grid, dim3(256), 0, stream, a);
-  else if (bm == 128) SEG_LAUNCH_CAPPED((wino_wgrad_kernel<128, 64, 64, 32>), grid, dim3(256), 0, stream, a);
-  else if (bm == 64 && bn == 128) SEG_LAUNCH_CAPPED((wino_wgrad_kernel<64, 128, 32, 64>), grid, dim3(256), 0, stream, a);
-  else if (bm == 64) SEG_LAUNCH_CAPPED((wino_wgrad_kernel<64, 64, 32, 32>), grid, dim3(256), 0, stream, a);
-  else SEG_LAUNCH_CAPPED((wino_wgrad_kernel<32, 128, 32, 32>), grid, dim3(256), 0, stream, a);
+  if (bm == 128 && bn == 128) hipLaunchKernelGGL((wino_wgrad_kernel<128, 128, 64, 64>), grid, dim3(256), 0, stream, a);
+  else if (bm == 128) hipLaunchKernelGGL((wino_wgrad_kernel<128, 64, 64, 32>), grid, dim3(256), 0, stream, a);
+  else if (bm == 64 && bn == 128) hipLaunchKernelGGL((wino_wgrad_kernel<64, 128, 32, 64>), grid, dim3(256), 0, stream, a);
+  else if (bm == 64) hipLaunchKernelGGL((wino_wgrad_kernel<64, 64, 32, 32>), grid, dim3(256), 0, stream, a);
+  else hipLaunchKernelGGL((wino_wgrad_kernel<32, 128, 32, 32>), grid, dim3(256), 0, stream, a);
   SEG_RET_LAST();
 }
 

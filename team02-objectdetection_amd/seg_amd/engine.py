@@ -1444,9 +1444,6 @@ IGEMM2_WIDE = os.environ.get("SEG_IGEMM2_WIDE", "1") == "1"
 W16 = os.environ.get("SEG_W16", "1") == "1"
 # many-tile BN statistics merged 16 tiles per row before the per-channel finalize; SEG_BN_MERGE=0 = direct
 BN_MERGE = os.environ.get("SEG_BN_MERGE", "1") == "1"
-# resident blocks per CU of the side stream's weight-gradient kernels (seg_stream_set_block_cap; 0 = no cap): wave
-# slots left to the main queue's memory-bound kernels, which otherwise wait for whole weight-gradient blocks
-SIDE_CAP = int(os.environ.get("SEG_SIDE_CAP", "0"))
 
 # Diagnostics (tests flip these): the Winograd transforms one at a time (parity attribution,
 # tests/test_gpu_unet_cfg5.py) ...
@@ -1468,7 +1465,6 @@ def _side_stream(device):
     st = _SIDE.get(device)
     if st is None:
         st = _SIDE[device] = torch.cuda.Stream(device, priority=0)
-        call("seg_stream_set_block_cap", st.cuda_stream, SIDE_CAP)
     return st
 
 

@@ -8,6 +8,3 @@ bash tools/gpurun/steps.sh $t \
 grep -q passed $d/tests.log && ! grep -q failed $d/tests.log || exit 1
 timeout -k 10 300 python bench.py --workload infer > $d/infer.json 2> $d/infer.err || { tail -5 $d/infer.err; exit 1; }
 tail -c 400 $d/infer.json
-# side-stream block cap A/B (SEG_SIDE_CAP: resident weight-gradient blocks per CU)
-bash tools/gpurun/ab.sh ${t}_cap 2 "--math f32" base "SEG_SIDE_CAP=6" "SEG_SIDE_CAP=4" || exit 1
-bash tools/gpurun/ab.sh ${t}_cap 2 "--math bf16io" base "SEG_SIDE_CAP=6" "SEG_SIDE_CAP=4" || exit 1

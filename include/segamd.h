@@ -204,6 +204,12 @@ int seg_conv_wino_row_tiles(int N, int H, int W);
 int seg_conv_wino(const float* in, long ldin, int N, int H, int W, int Cin, const float* wk, int ldk,
                   const float* bias, float* out, long ldout, int Cout, const float* add, long ldadd,
                   float* stat, float* work, hipStream_t stream);
+/* seg_conv_wino in one launch and no workspace (csrc/wino.hip wino_fused_kernel: the 16 GEMMs and the output
+ * transform fused, M kept in registers -- VERDICT r4 item 4).  Same arguments without `work`; the result
+ * differs from seg_conv_wino's only by the association of the input transform's adds. */
+int seg_conv_wino_fused(const float* in, long ldin, int N, int H, int W, int Cin, const float* wk, int ldk,
+                        const float* bias, float* out, long ldout, int Cout, const float* add, long ldadd, float* stat,
+                        hipStream_t stream);
 /* Weight gradient of the same convs by Winograd F(3x3,2x2):
  * dW = G^T [sum_t (A dY_t A^T) .* (B^T X_t B)] G.  seg_conv_wino_wgrad writes
  * fixed-order split-K partial slabs part[splits][16][Cout][Cin] (Cin = the padded

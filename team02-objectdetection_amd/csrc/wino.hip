@@ -321,6 +321,232 @@ void launch_wino(const WinoArgs& a, hipStream_t s) {
 #define SEG_WINO_WIDE 256  // Cout from which the 8-wave 128 x 256 tile is used
 #endif
 
+// ---------------------------------------------------------------- fused forward / data gradient
+// The 16 GEMMs and the output transform in one kernel, M never leaving the registers.  A wave owns 32 tiles x 32
+// output channels for ALL 16 xi: 16 independent 32x32 accumulators (256 accumulator registers; gfx950's unified
+// file holds them beside ~200 VGPRs at one wave per SIMD), so back-to-back MFMAs never wait on each other.  Per
+// K chunk of 8 input channels a lane loads its tile's 4x4 input patch for 4 channels (16 float4; lane half h holds
+// channels 4h..4h+3 and K step s uses channel 4h+s on both operands), forms V = B^T d B in place (adds only, all 16
+// xi at once: 4 loads per input pixel instead of the per-xi loader's 16) and runs 4 x 16 MFMAs against U rows
+// staged in LDS (shared by the block's 4 waves, double-buffered, one barrier per chunk), while the next chunk's
+// patch and U rows are in flight.  Epilogue per accumulator element: Y = A^T M A from the 16 values of one lane
+// (+ bias, + addend), and the same BatchNorm partials as wino_out_kernel (64-tile row tiles, two passes: sum, then
+// squared deviations about the row tile's mean).  Block = 128 tiles x 32 channels (WT = 4 waves along the tiles).
+struct WinoFusedArgs {
+  const float* in; long ldin;   // NHWC conv input [N*H*W][ldin]
+  const float* wk; int ldk;     // U [16][Cout][ldk] (seg_pack_batch modes 3 / 4)
+  const float* bias;            // [Cout] or null
+  const float* add; long ldadd; // optional addend (may alias out)
+  float* out; long ldout;
+  float* stat;                  // optional BN partials [row tiles of 64 tiles][2][Cout]
+  int N, H, W, Cin, Cout;
+  int T, th, tw;
+};
+
+constexpr int kFusedKC = 8;             // input channels per K chunk
+constexpr int kFusedUR = kFusedKC + 4;  // LDS pitch (floats) of one (xi, co) row of U
+
+template <int WT>
+__global__ __launch_bounds__(256) void wino_fused_kernel(WinoFusedArgs a) {
+  constexpr int WN = 4 / WT, BT = 32 * WT, BC = 32 * WN;
+  static_assert(WT == 2 || WT == 4, "a BN row tile (64 tiles) lies in one block");
+  constexpr int USZ = 16 * BC * kFusedUR;
+  constexpr int UPT = 16 * BC * (kFusedKC / 4) / 256;  // U float4 slots per thread per chunk
+  __shared__ __attribute__((aligned(16))) float Us[2 * USZ];
+  __shared__ float red[4][32];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wt = wave / WN, wn = wave % WN;
+  const int row = lane & 31, h = lane >> 5;
+  const int tiles_n = (a.Cout + BC - 1) / BC;
+  const int lid = xcd_swizzle(blockIdx.x, gridDim.x);
+  const int tn = lid % tiles_n, tm = lid / tiles_n;
+  const int m0 = tm * BT, n0 = tn * BC;
+
+  // this lane's tile (A row `row` of the wave's 32) and the validity of its 4x4 patch
+  const int t = m0 + wt * 32 + row;
+  const bool tok = t < a.T;
+  unsigned pm = 0;
+  long pbase = 0;
+  {
+    const int tt = tok ? t : 0;
+    const int n = tt / (a.th * a.tw), r = tt - n * a.th * a.tw;
+    const int ty = r / a.tw, tx = r - ty * a.tw;
+    const int h0 = 2 * ty - 1, w0 = 2 * tx - 1;
+#pragma unroll
+    for (int p = 0; p < 4; ++p)
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        if (tok && (unsigned)(h0 + p) < (unsigned)a.H && (unsigned)(w0 + q) < (unsigned)a.W) pm |= 1u << (p * 4 + q);
+    pbase = (((long)n * a.H + h0) * a.W + w0) * a.ldin;
+  }
+  const long rstep = (long)a.W * a.ldin;
+
+  auto load_patch = [&](int c0, f32x4 (&d)[16]) {
+    const int c = c0 + 4 * h;
+    const bool cok = c < a.Cin;
+#pragma unroll
+    for (int p = 0; p < 4; ++p)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const bool ok = cok && ((pm >> (p * 4 + q)) & 1u);
+        d[p * 4 + q] = ld4(ok ? a.in + pbase + p * rstep + q * a.ldin + c : g_wzero4);
+      }
+  };
+  auto load_u = [&](int c0, f32x4 (&u)[UPT]) {
+#pragma unroll
+    for (int i = 0; i < UPT; ++i) {
+      const int idx = tid + i * 256;
+      const int xi = idx / (2 * BC), rem = idx - xi * (2 * BC);
+      const int co = n0 + (rem >> 1), c = c0 + 4 * (rem & 1);
+      const bool ok = co < a.Cout && c < a.Cin;
+      u[i] = ld4(ok ? a.wk + ((long)xi * a.Cout + co) * a.ldk + c : g_wzero4);
+    }
+  };
+  auto store_u = [&](float* dst, const f32x4 (&u)[UPT]) {
+#pragma unroll
+    for (int i = 0; i < UPT; ++i) {
+      const int idx = tid + i * 256;
+      const int xi = idx / (2 * BC), rem = idx - xi * (2 * BC);
+      st4(dst + (xi * BC + (rem >> 1)) * kFusedUR + 4 * (rem & 1), u[i]);
+    }
+  };
+  // V = B^T d B in place: d[4p + q] (patch row p, column q) -> V[4r + c] = V_xi, xi = 4r + c
+  auto transform = [](f32x4 (&d)[16]) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const f32x4 d0 = d[q], d1 = d[4 + q], d2 = d[8 + q], d3 = d[12 + q];
+      d[q] = d0 - d2;
+      d[4 + q] = d1 + d2;
+      d[8 + q] = d2 - d1;
+      d[12 + q] = d1 - d3;
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const f32x4 t0 = d[4 * r], t1 = d[4 * r + 1], t2 = d[4 * r + 2], t3 = d[4 * r + 3];
+      d[4 * r] = t0 - t2;
+      d[4 * r + 1] = t1 + t2;
+      d[4 * r + 2] = t2 - t1;
+      d[4 * r + 3] = t1 - t3;
+    }
+  };
+
+  f32x16 acc[16];
+#pragma unroll
+  for (int x = 0; x < 16; ++x)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[x][r] = 0.f;
+
+  f32x4 d[16], ug[UPT];
+  const int nk = (a.Cin + kFusedKC - 1) / kFusedKC;
+  load_patch(0, d);
+  load_u(0, ug);
+  store_u(Us, ug);
+  __syncthreads();
+  const int urow = (wn * 32 + row) * kFusedUR + 4 * h;
+  for (int kc = 0; kc < nk; ++kc) {
+    const float* ucur = Us + (kc & 1) * USZ + urow;
+    const bool more = kc + 1 < nk;
+    f32x4 dn[16];
+    if (more) {
+      load_patch((kc + 1) * kFusedKC, dn);
+      load_u((kc + 1) * kFusedKC, ug);
+    }
+    transform(d);
+#pragma unroll
+    for (int x = 0; x < 16; x += 2) {  // two accumulator chains interleaved
+      const f32x4 u0 = ld4(ucur + x * BC * kFusedUR), u1 = ld4(ucur + (x + 1) * BC * kFusedUR);
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        acc[x] = __builtin_amdgcn_mfma_f32_32x32x2f32(d[x][s], u0[s], acc[x], 0, 0, 0);
+        acc[x + 1] = __builtin_amdgcn_mfma_f32_32x32x2f32(d[x + 1][s], u1[s], acc[x + 1], 0, 0, 0);
+      }
+    }
+    if (more) {
+      store_u(Us + ((kc + 1) & 1) * USZ, ug);
+#pragma unroll
+      for (int i = 0; i < 16; ++i) d[i] = dn[i];
+    }
+    __syncthreads();
+  }
+
+  // epilogue: accumulator element r holds tile row (r&3) + 8(r>>2) + 4h of the wave, column lane&31
+  const int col = n0 + wn * 32 + row;
+  const bool cok = col < a.Cout;
+  const float b = (a.bias && cok) ? a.bias[col] : 0.f;
+  auto tile_y = [&](int r, float (&y)[4]) {
+    float q[16];
+#pragma unroll
+    for (int x = 0; x < 16; ++x) q[x] = acc[x][r];
+    float r0[4], r1[4];  // rows of A^T M
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      r0[j] = q[j] + q[4 + j] + q[8 + j];
+      r1[j] = q[4 + j] - q[8 + j] - q[12 + j];
+    }
+    y[0] = r0[0] + r0[1] + r0[2] + b;
+    y[1] = r0[1] - r0[2] - r0[3] + b;
+    y[2] = r1[0] + r1[1] + r1[2] + b;
+    y[3] = r1[1] - r1[2] - r1[3] + b;
+  };
+  auto tile_pix = [&](int tt) -> long {  // pixel index of the tile's top-left output
+    const int n = tt / (a.th * a.tw), r = tt - n * a.th * a.tw;
+    const int ty = r / a.tw, tx = r - ty * a.tw;
+    return ((long)n * a.H + 2 * ty) * a.W + 2 * tx;
+  };
+  const int wbase = m0 + wt * 32 + 4 * h;
+  float ssum = 0.f;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int tt = wbase + (r & 3) + 8 * (r >> 2);
+    if (tt < a.T && cok) {
+      float y[4];
+      tile_y(r, y);
+      const long p0 = tile_pix(tt);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const long pix = p0 + (u >> 1) * a.W + (u & 1);
+        if (a.add) y[u] += a.add[pix * a.ldadd + col];
+        a.out[pix * a.ldout + col] = y[u];
+        ssum += y[u];
+      }
+    }
+  }
+  if (!a.stat) return;
+  // BN partials of the wave pair (wt even, wt odd) that holds one 64-tile row tile
+  const int rtile = (m0 + (wt & ~1) * 32) / 64;
+  const int ntile = min(64, a.T - rtile * 64);
+  const int we = (wt & ~1) * WN + wn, wo = we + WN;
+  float mean = 0.f;
+#pragma unroll
+  for (int pass = 0; pass < 2; ++pass) {
+    float sv = ssum;
+    if (pass) {
+      sv = 0.f;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int tt = wbase + (r & 3) + 8 * (r >> 2);
+        if (tt < a.T && cok) {
+          float y[4];
+          tile_y(r, y);
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            const float dv = y[u] - mean;
+            sv += dv * dv;
+          }
+        }
+      }
+    }
+    sv += __shfl_xor(sv, 32, 64);
+    if (h == 0) red[wave][row] = sv;
+    __syncthreads();
+    const float tot = red[we][row] + red[wo][row];
+    if (pass == 0) mean = ntile > 0 ? tot / (4.f * (float)ntile) : 0.f;
+    if ((wt & 1) == 0 && h == 0 && cok && ntile > 0) a.stat[((long)rtile * 2 + pass) * a.Cout + col] = tot;
+    __syncthreads();
+  }
+}
+
 // ---------------------------------------------------------------- weight gradient
 // dW = G^T [ sum_t (A dY_t A^T) .* (B^T X_t B) ] G  per (co, ci): Winograd F(3x3, 2x2)
 // (the transposition of F(2x2,3x3); A = [1 0; 1 1; 1 -1; 0 -1]).  Per xi a GEMM
@@ -567,6 +793,24 @@ SEG_API int seg_conv_wino(const float* in, long ldin, int N, int H, int W, int C
   else launch_wino<128, 64, 64, 32>(a, stream);
   hipLaunchKernelGGL(wino_out_kernel, dim3(seg_cdiv(a.T, 16 * kWinoQT), SEG_WINO_OUT_CSPLIT ? seg_cdiv(Cout, 64) : 1), dim3(256), 0, stream, work, a.T, Cout, N, H, W, a.th,
                      a.tw, bias, add, ldadd, out, ldout, stat);
+  SEG_RET_LAST();
+}
+
+// seg_conv_wino's result (bitwise up to the association of the input transform's adds) from one launch with no M
+// workspace: wino_fused_kernel.  Same arguments as seg_conv_wino without `work`.
+SEG_API int seg_conv_wino_fused(const float* in, long ldin, int N, int H, int W, int Cin, const float* wk, int ldk,
+                                const float* bias, float* out, long ldout, int Cout, const float* add, long ldadd,
+                                float* stat, hipStream_t stream) {
+  if ((H & 1) || (W & 1) || (Cin & 3) || (ldin & 3) || (ldk & 3) || ldk < Cin || (Cout & 3) || (add && ldadd < Cout) ||
+      ldout < Cout)
+    return (int)hipErrorInvalidValue;
+  WinoFusedArgs a;
+  a.in = in; a.ldin = ldin; a.wk = wk; a.ldk = ldk; a.bias = bias; a.add = add; a.ldadd = ldadd;
+  a.out = out; a.ldout = ldout; a.stat = stat;
+  a.N = N; a.H = H; a.W = W; a.Cin = Cin; a.Cout = Cout;
+  a.th = H / 2; a.tw = W / 2; a.T = N * a.th * a.tw;
+  if (a.T == 0) return 0;
+  hipLaunchKernelGGL(wino_fused_kernel<4>, dim3(seg_cdiv(a.T, 128) * seg_cdiv(Cout, 32)), dim3(256), 0, stream, a);
   SEG_RET_LAST();
 }
 

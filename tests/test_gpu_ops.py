@@ -484,10 +484,19 @@ def _pack_wino(w, mode, rows, ldk):
     return wk
 
 
+@pytest.mark.parametrize("fused", [False, True])
 @pytest.mark.parametrize("N,Cin,Cout,H,W", [(2, 64, 32, 6, 10), (1, 1344, 256, 4, 8), (2, 152, 64, 8, 6),
-                                           (3, 36, 200, 2, 4), (1, 288, 128, 10, 14)])
-def test_conv_wino_fwd_stats_dgrad(N, Cin, Cout, H, W):
-    """Winograd F(2x2,3x3): forward (+bias, BN partials) and data gradient (+addend) vs torch."""
+                                           (3, 36, 200, 2, 4), (1, 288, 128, 10, 14), (2, 80, 32, 34, 18),
+                                           (1, 12, 44, 130, 6)])
+def test_conv_wino_fwd_stats_dgrad(N, Cin, Cout, H, W, fused):
+    """Winograd F(2x2,3x3): forward (+bias, BN partials) and data gradient (+addend) vs torch; the two-launch
+    form (seg_conv_wino: 16 GEMMs + output transform through an M workspace) and the fused one (seg_conv_wino_fused:
+    M in registers; row tiles crossing blocks and partial last row tiles in the shapes above)."""
+    def wino(*args, stat, work):
+        if fused:
+            call("seg_conv_wino_fused", *args, stat, S())
+        else:
+            call("seg_conv_wino", *args, stat, work, S())
     x = gen(N, Cin, H, W, seed=31)
     w = gen(Cout, Cin, 3, 3, seed=32) * (2.0 / (Cin * 9)) ** 0.5
     b = gen(Cout, seed=33)
@@ -505,8 +514,8 @@ def test_conv_wino_fwd_stats_dgrad(N, Cin, Cout, H, W):
     out = torch.full((N * H * W, r4(Cout)), float("nan"), device=DEV)
     nt = query("seg_conv_wino_row_tiles", N, H, W)
     stat = torch.empty(nt * 2 * Cout, device=DEV)
-    call("seg_conv_wino", xg.data_ptr(), xg.shape[1], N, H, W, cin4, U.data_ptr(), cin4, b.to(DEV).data_ptr(),
-         out.data_ptr(), out.shape[1], Cout, None, 0, stat.data_ptr(), work.data_ptr(), S())
+    wino(xg.data_ptr(), xg.shape[1], N, H, W, cin4, U.data_ptr(), cin4, b.to(DEV).data_ptr(), out.data_ptr(),
+         out.shape[1], Cout, None, 0, stat=stat.data_ptr(), work=work.data_ptr())
     assert rel(from_nhwc(out, N, Cout, H, W), y.detach()) < 1e-5
     st = torch.empty(4 * Cout, device=DEV)
     rm, rv = torch.zeros(Cout, device=DEV), torch.ones(Cout, device=DEV)
@@ -525,8 +534,8 @@ def test_conv_wino_fwd_stats_dgrad(N, Cin, Cout, H, W):
     addend = gen(N, Cin, H, W, seed=35)
     addg = nhwc(addend)
     dx = torch.full((N * H * W, r4(Cin)), float("nan"), device=DEV)
-    call("seg_conv_wino", dyg.data_ptr(), dyg.shape[1], N, H, W, kin, Ud.data_ptr(), kin, None, dx.data_ptr(),
-         dx.shape[1], Cin, addg.data_ptr(), addg.shape[1], None, work.data_ptr(), S())
+    wino(dyg.data_ptr(), dyg.shape[1], N, H, W, kin, Ud.data_ptr(), kin, None, dx.data_ptr(), dx.shape[1], Cin,
+         addg.data_ptr(), addg.shape[1], stat=None, work=work.data_ptr())
     assert rel(from_nhwc(dx, N, Cin, H, W), xr.grad + addend) < 1e-5
 
 

@@ -1,4 +1,4 @@
-"""Winograd F(2x2,3x3) (seg_conv_wino) against the direct implicit GEMM
+"""Winograd F(2x2,3x3) (seg_conv_wino, and seg_conv_wino_fused) against the direct implicit GEMM
 (seg_conv_igemm) on the MobileNetV2UNet / UNet decoder shapes, forward and data
 gradient, HIP-event medians.  TF/s are direct-conv-equivalent FLOPs.
 
@@ -66,6 +66,8 @@ def main():
             work = torch.empty(16 * N * (H // 2) * (W // 2) * co, device="cuda")
             t_w = timeit(lambda: call("seg_conv_wino", x.data_ptr(), ci, N, H, W, ci, U.data_ptr(), ci, None,
                                       y.data_ptr(), co, co, None, 0, None, work.data_ptr(), s))
+            t_f = timeit(lambda: call("seg_conv_wino_fused", x.data_ptr(), ci, N, H, W, ci, U.data_ptr(), ci, None,
+                                      y.data_ptr(), co, co, None, 0, None, s))
             pick = query("seg_conv_wino_pick", N, H, W, ci, co)
             if query("seg_conv_halo_ok", N, H, W, ci, co):
                 t_h = timeit(lambda: call("seg_conv_halo", x.data_ptr(), ci, N, H, W, ci, wk.data_ptr(), ldk, None,
@@ -73,7 +75,8 @@ def main():
                 print(f"{name:6s} {d:5s} halo {t_h * 1e6:7.1f} us ({fl / t_h / 1e12:5.1f} TF/s) vs direct "
                       f"{t_d * 1e6:7.1f}: speedup {t_d / t_h:4.2f}", flush=True)
             print(f"{name:6s} {d:5s} direct {t_d * 1e6:7.1f} us ({fl / t_d / 1e12:5.1f} TF/s)  wino {t_w * 1e6:7.1f} us "
-                  f"({fl / t_w / 1e12:5.1f})  speedup {t_d / t_w:4.2f}  pick={pick}", flush=True)
+                  f"({fl / t_w / 1e12:5.1f})  speedup {t_d / t_w:4.2f}  fused {t_f * 1e6:7.1f} us "
+                  f"({fl / t_f / 1e12:5.1f})  speedup {t_d / t_f:4.2f}  pick={pick}", flush=True)
         # weight gradient: direct split-K wgrad + reduce vs Winograd wgrad + reduce
         x = torch.randn(N * H * W, Cin, device="cuda")
         dy = torch.randn(N * H * W, Cout, device="cuda")

@@ -341,10 +341,23 @@ struct WinoFusedArgs {
   float* stat;                  // optional BN partials [row tiles of 64 tiles][2][Cout]
   int N, H, W, Cin, Cout;
   int T, th, tw;
+  unsigned in_bytes, wk_bytes;  // extents of `in` and `wk` (buffer-load range checks: < 2^31)
 };
 
 constexpr int kFusedKC = 8;             // input channels per K chunk
 constexpr int kFusedUR = kFusedKC + 4;  // LDS pitch (floats) of one (xi, co) row of U
+constexpr unsigned kFusedOOB = 0x80000000u;  // a buffer offset past every range check: the load returns zeros
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t seg_rsrc(const void* p, unsigned bytes) {
+  const unsigned long v = (unsigned long)p;
+  const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)v), hi = __builtin_amdgcn_readfirstlane((unsigned)(v >> 32));
+  return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(((unsigned long)hi << 32) | lo), 0,
+                                           (int)__builtin_amdgcn_readfirstlane(bytes), 0x00020000);
+}
+__device__ __forceinline__ f32x4 seg_bld4(__amdgpu_buffer_rsrc_t r, unsigned off) {
+  typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+  return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
+}
 
 template <int WT>
 __global__ __launch_bounds__(256) void wino_fused_kernel(WinoFusedArgs a) {
@@ -362,12 +375,13 @@ __global__ __launch_bounds__(256) void wino_fused_kernel(WinoFusedArgs a) {
   const int lid = xcd_swizzle(blockIdx.x, gridDim.x);
   const int tn = lid % tiles_n, tm = lid / tiles_n;
   const int m0 = tm * BT, n0 = tn * BC;
+  const __amdgpu_buffer_rsrc_t rin = seg_rsrc(a.in, a.in_bytes), rwk = seg_rsrc(a.wk, a.wk_bytes);
 
-  // this lane's tile (A row `row` of the wave's 32) and the validity of its 4x4 patch
+  // this lane's tile (A row `row` of the wave's 32): byte offset of its 4x4 patch's corner (32-bit wrap arithmetic:
+  // exact wherever a patch pixel is in the image) and the in-image mask
   const int t = m0 + wt * 32 + row;
   const bool tok = t < a.T;
-  unsigned pm = 0;
-  long pbase = 0;
+  unsigned pm = 0, pbase = 0;
   {
     const int tt = tok ? t : 0;
     const int n = tt / (a.th * a.tw), r = tt - n * a.th * a.tw;
@@ -378,19 +392,19 @@ __global__ __launch_bounds__(256) void wino_fused_kernel(WinoFusedArgs a) {
 #pragma unroll
       for (int q = 0; q < 4; ++q)
         if (tok && (unsigned)(h0 + p) < (unsigned)a.H && (unsigned)(w0 + q) < (unsigned)a.W) pm |= 1u << (p * 4 + q);
-    pbase = (((long)n * a.H + h0) * a.W + w0) * a.ldin;
+    pbase = (unsigned)((((long)n * a.H + h0) * a.W + w0) * a.ldin * 4) + 16u * h;
   }
-  const long rstep = (long)a.W * a.ldin;
+  const unsigned rstep = (unsigned)(a.W * a.ldin * 4), cstep = (unsigned)(a.ldin * 4);
 
   auto load_patch = [&](int c0, f32x4 (&d)[16]) {
-    const int c = c0 + 4 * h;
-    const bool cok = c < a.Cin;
+    const bool cok = c0 + 4 * h < a.Cin;
+    const unsigned b = pbase + 4u * c0;
 #pragma unroll
     for (int p = 0; p < 4; ++p)
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const bool ok = cok && ((pm >> (p * 4 + q)) & 1u);
-        d[p * 4 + q] = ld4(ok ? a.in + pbase + p * rstep + q * a.ldin + c : g_wzero4);
+        d[p * 4 + q] = seg_bld4(rin, ok ? b + p * rstep + q * cstep : kFusedOOB);
       }
   };
   auto load_u = [&](int c0, f32x4 (&u)[UPT]) {
@@ -400,7 +414,7 @@ __global__ __launch_bounds__(256) void wino_fused_kernel(WinoFusedArgs a) {
       const int xi = idx / (2 * BC), rem = idx - xi * (2 * BC);
       const int co = n0 + (rem >> 1), c = c0 + 4 * (rem & 1);
       const bool ok = co < a.Cout && c < a.Cin;
-      u[i] = ld4(ok ? a.wk + ((long)xi * a.Cout + co) * a.ldk + c : g_wzero4);
+      u[i] = seg_bld4(rwk, ok ? (unsigned)((((long)xi * a.Cout + co) * a.ldk + c) * 4) : kFusedOOB);
     }
   };
   auto store_u = [&](float* dst, const f32x4 (&u)[UPT]) {
@@ -437,15 +451,16 @@ __global__ __launch_bounds__(256) void wino_fused_kernel(WinoFusedArgs a) {
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[x][r] = 0.f;
 
-  f32x4 d[16], ug[UPT];
   const int nk = (a.Cin + kFusedKC - 1) / kFusedKC;
+  const int urow = (wn * 32 + row) * kFusedUR + 4 * h;
+  f32x4 d[16], ug[UPT];
   load_patch(0, d);
   load_u(0, ug);
   store_u(Us, ug);
   __syncthreads();
-  const int urow = (wn * 32 + row) * kFusedUR + 4 * h;
+  // per K chunk: the next chunk's patch and U rows are issued first, then this chunk's transform and 64 MFMAs (U rows
+  // read from LDS four xi ahead), then the U rows are staged and the patch moves over
   for (int kc = 0; kc < nk; ++kc) {
-    const float* ucur = Us + (kc & 1) * USZ + urow;
     const bool more = kc + 1 < nk;
     f32x4 dn[16];
     if (more) {
@@ -453,19 +468,27 @@ __global__ __launch_bounds__(256) void wino_fused_kernel(WinoFusedArgs a) {
       load_u((kc + 1) * kFusedKC, ug);
     }
     transform(d);
+    const float* ub = Us + (kc & 1) * USZ + urow;
+    f32x4 u[2][4];
 #pragma unroll
-    for (int x = 0; x < 16; x += 2) {  // two accumulator chains interleaved
-      const f32x4 u0 = ld4(ucur + x * BC * kFusedUR), u1 = ld4(ucur + (x + 1) * BC * kFusedUR);
+    for (int j = 0; j < 4; ++j) u[0][j] = ld4(ub + j * BC * kFusedUR);
 #pragma unroll
-      for (int s = 0; s < 4; ++s) {
-        acc[x] = __builtin_amdgcn_mfma_f32_32x32x2f32(d[x][s], u0[s], acc[x], 0, 0, 0);
-        acc[x + 1] = __builtin_amdgcn_mfma_f32_32x32x2f32(d[x + 1][s], u1[s], acc[x + 1], 0, 0, 0);
+    for (int g = 0; g < 4; ++g) {
+      if (g < 3) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) u[(g + 1) & 1][j] = ld4(ub + (4 * (g + 1) + j) * BC * kFusedUR);
       }
+#pragma unroll
+      for (int s2 = 0; s2 < 4; ++s2)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[4 * g + j] = __builtin_amdgcn_mfma_f32_32x32x2f32(d[4 * g + j][s2], u[g & 1][j][s2], acc[4 * g + j], 0,
+                                                                0, 0);
     }
     if (more) {
       store_u(Us + ((kc + 1) & 1) * USZ, ug);
 #pragma unroll
-      for (int i = 0; i < 16; ++i) d[i] = dn[i];
+      for (int q = 0; q < 16; ++q) d[q] = dn[q];
     }
     __syncthreads();
   }
@@ -810,6 +833,10 @@ SEG_API int seg_conv_wino_fused(const float* in, long ldin, int N, int H, int W,
   a.N = N; a.H = H; a.W = W; a.Cin = Cin; a.Cout = Cout;
   a.th = H / 2; a.tw = W / 2; a.T = N * a.th * a.tw;
   if (a.T == 0) return 0;
+  const long in_bytes = ((long)N * H * W - 1) * ldin * 4 + (long)Cin * 4, wk_bytes = 16L * Cout * ldk * 4;
+  if (in_bytes >= (long)kFusedOOB || wk_bytes >= (long)kFusedOOB) return (int)hipErrorInvalidValue;
+  a.in_bytes = (unsigned)in_bytes;
+  a.wk_bytes = (unsigned)wk_bytes;
   hipLaunchKernelGGL(wino_fused_kernel<4>, dim3(seg_cdiv(a.T, 128) * seg_cdiv(Cout, 32)), dim3(256), 0, stream, a);
   SEG_RET_LAST();
 }

@@ -344,6 +344,9 @@ struct WinoFusedArgs {
   unsigned in_bytes, wk_bytes;  // extents of `in` and `wk` (buffer-load range checks: < 2^31)
 };
 
+#ifndef SEG_WF_EXP
+#define SEG_WF_EXP 0  // timing experiments: 1 = no loads in the K loop, 2 = no input transform, 4 = no MFMAs
+#endif
 constexpr int kFusedKC = 8;             // input channels per K chunk
 constexpr int kFusedUR = kFusedKC + 4;  // LDS pitch (floats) of one (xi, co) row of U
 constexpr unsigned kFusedOOB = 0x80000000u;  // a buffer offset past every range check: the load returns zeros
@@ -463,11 +466,15 @@ __global__ __launch_bounds__(256) void wino_fused_kernel(WinoFusedArgs a) {
   for (int kc = 0; kc < nk; ++kc) {
     const bool more = kc + 1 < nk;
     f32x4 dn[16];
-    if (more) {
+    if (more && !(SEG_WF_EXP & 1)) {
       load_patch((kc + 1) * kFusedKC, dn);
       load_u((kc + 1) * kFusedKC, ug);
     }
-    transform(d);
+    if (SEG_WF_EXP & 1) {
+#pragma unroll
+      for (int q = 0; q < 16; ++q) dn[q] = d[q] * 0.5f;
+    }
+    if (!(SEG_WF_EXP & 2)) transform(d);
     const float* ub = Us + (kc & 1) * USZ + urow;
     f32x4 u[2][4];
 #pragma unroll
@@ -482,8 +489,11 @@ __global__ __launch_bounds__(256) void wino_fused_kernel(WinoFusedArgs a) {
       for (int s2 = 0; s2 < 4; ++s2)
 #pragma unroll
         for (int j = 0; j < 4; ++j)
-          acc[4 * g + j] = __builtin_amdgcn_mfma_f32_32x32x2f32(d[4 * g + j][s2], u[g & 1][j][s2], acc[4 * g + j], 0,
-                                                                0, 0);
+          if (SEG_WF_EXP & 4)
+            acc[4 * g + j][s2] += d[4 * g + j][s2] * u[g & 1][j][s2];
+          else
+            acc[4 * g + j] = __builtin_amdgcn_mfma_f32_32x32x2f32(d[4 * g + j][s2], u[g & 1][j][s2], acc[4 * g + j],
+                                                                  0, 0, 0);
     }
     if (more) {
       store_u(Us + ((kc + 1) & 1) * USZ, ug);

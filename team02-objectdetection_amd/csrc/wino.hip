@@ -385,6 +385,7 @@ __global__ __launch_bounds__(256) void wino_fused_kernel(WinoFusedArgs a) {
   const int t = m0 + wt * 32 + row;
   const bool tok = t < a.T;
   unsigned pm = 0, pbase = 0;
+  int opix = 0;  // pixel index of the tile's top-left output (the epilogue fetches it from the owning lane)
   {
     const int tt = tok ? t : 0;
     const int n = tt / (a.th * a.tw), r = tt - n * a.th * a.tw;
@@ -396,6 +397,7 @@ __global__ __launch_bounds__(256) void wino_fused_kernel(WinoFusedArgs a) {
       for (int q = 0; q < 4; ++q)
         if (tok && (unsigned)(h0 + p) < (unsigned)a.H && (unsigned)(w0 + q) < (unsigned)a.W) pm |= 1u << (p * 4 + q);
     pbase = (unsigned)((((long)n * a.H + h0) * a.W + w0) * a.ldin * 4) + 16u * h;
+    opix = (n * a.H + 2 * ty) * a.W + 2 * tx;
   }
   const unsigned rstep = (unsigned)(a.W * a.ldin * 4), cstep = (unsigned)(a.ldin * 4);
 
@@ -522,20 +524,15 @@ __global__ __launch_bounds__(256) void wino_fused_kernel(WinoFusedArgs a) {
     y[2] = r1[0] + r1[1] + r1[2] + b;
     y[3] = r1[1] - r1[2] - r1[3] + b;
   };
-  auto tile_pix = [&](int tt) -> long {  // pixel index of the tile's top-left output
-    const int n = tt / (a.th * a.tw), r = tt - n * a.th * a.tw;
-    const int ty = r / a.tw, tx = r - ty * a.tw;
-    return ((long)n * a.H + 2 * ty) * a.W + 2 * tx;
-  };
   const int wbase = m0 + wt * 32 + 4 * h;
   float ssum = 0.f;
 #pragma unroll
   for (int r = 0; r < 16; ++r) {
     const int tt = wbase + (r & 3) + 8 * (r >> 2);
+    const long p0 = __shfl(opix, (r & 3) + 8 * (r >> 2) + 4 * h, 64);  // all lanes active (bpermute)
     if (tt < a.T && cok) {
       float y[4];
       tile_y(r, y);
-      const long p0 = tile_pix(tt);
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
         const long pix = p0 + (u >> 1) * a.W + (u & 1);

@@ -197,7 +197,8 @@ int seg_conv_wgrad_reduce(const float* part, int splits, float* dw, int Cout, in
  * seg_pack_batch mode 3) and data gradient (mode 4).  out = conv + bias + add;
  * `work` >= 16 * N*(H/2)*(W/2) * Cout floats; `stat` (optional): BatchNorm
  * partials in seg_conv_igemm's layout with seg_conv_wino_row_tiles tiles of
- * seg_conv_wino_tile_rows() rows.  seg_conv_wino_pick: 1 when the cost model prefers it to seg_conv_igemm. */
+ * seg_conv_wino_tile_rows() rows.  seg_conv_wino_pick: 1 when the cost model prefers it to seg_conv_igemm, 2 when
+ * it prefers seg_conv_wino_fused (below), 0 otherwise. */
 int seg_conv_wino_pick(int N, int H, int W, int Cin, int Cout);
 int seg_conv_wino_tile_rows(void);  /* pixels per BN row tile of seg_conv_wino */
 int seg_conv_wino_row_tiles(int N, int H, int W);

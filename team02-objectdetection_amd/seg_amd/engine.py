@@ -201,6 +201,7 @@ class ConvOp:
         # Winograd F(2x2,3x3) (seg_conv_wino) for the forward / data gradient, chosen by
         # seg_conv_wino_pick at pack time; U_f [16][Cout][cin_pad], U_d [16][Cin][r4(Cout)]
         self.wino_f = self.wino_d = self.wino_w = False
+        self.wino_ff = self.wino_fd = False  # ... on the fused kernel (seg_conv_wino_fused: no M workspace)
         # LDS-halo direct 3x3 (seg_conv_halo) for the forward / data gradient of narrow convs
         self.halo_f = self.halo_d = False
         self.w2 = False  # weight gradient on seg_conv_wgrad2_bf16io (narrow bf16io 3x3)
@@ -271,6 +272,10 @@ class ConvOp:
                 name = rt.k("seg_conv_halo") + ("_w16" if self.w16_f else "")
                 rt.tcall("igemm3_fwd", self.flops(), name, rt.ptr(i), i.ld, i.N, i.H, i.W, self.cin_pad,
                          wk_ptr, ldk, bias, rt.ptr(y), y.ld, self.cout, None, 0, statp, s)
+            elif self.wino_ff:
+                rt.tcall("wino3_fwd", self.flops(), "seg_conv_wino_fused", rt.ptr(i), i.ld, i.N, i.H, i.W,
+                         self.cin_pad, self.wk_wf.data_ptr(), self.cin_pad, bias, rt.ptr(y), y.ld, self.cout, None, 0,
+                         statp, s)
             elif self.wino_f:
                 work = rt.tmp(16 * (y.M // 4) * self.cout)
                 rt.tcall("wino3_fwd", self.flops(), "seg_conv_wino", rt.ptr(i), i.ld, i.N, i.H, i.W, self.cin_pad,
@@ -526,6 +531,9 @@ class ConvOp:
                 rt.tcall("igemm3_dgrad", self.flops(), rt.k("seg_conv_halo") + ("_w16" if self.w16_d else ""), dYp,
                          dY.ld, y.N, y.H, y.W, kin,
                             self.wk_d.data_ptr(), self.ldk_d, None, rt.gptr(i), i.ld, self.cin, add_ptr, add_ld, None, s)
+            elif self.wino_fd:
+                rt.tcall("wino3_dgrad", self.flops(), "seg_conv_wino_fused", dYp, dY.ld, y.N, y.H, y.W, kin,
+                         self.wk_wd.data_ptr(), kin, None, rt.gptr(i), i.ld, self.cin, add_ptr, add_ld, None, s)
             elif self.wino_d:
                 work = rt.tmp(16 * (y.M // 4) * self.cin)
                 rt.tcall("wino3_dgrad", self.flops(), "seg_conv_wino", dYp, dY.ld, y.N, y.H, y.W, kin,
@@ -762,6 +770,7 @@ class Program:
             if op.bf:
                 # bf16 math: every dense / pointwise conv (fwd, dgrad, wgrad) on the bf16 implicit GEMM
                 op.wino_f = op.wino_d = op.wino_w = op.halo_f = op.halo_d = False
+                op.wino_ff = op.wino_fd = False
                 # narrow bf16io 3x3 weight gradients on seg_conv_wgrad2_bf16io (SEG_WGRAD2=0: the implicit GEMM)
                 op.w2 = (self.math == "bf16io" and WGRAD2 and op.ks == 3 and op.stride == 1 and op.pad == 1
                          and op.xform is None and op.cin_pad == op.cin and y.ld % 8 == 0 and op.inp.ld % 8 == 0
@@ -811,10 +820,12 @@ class Program:
             op.pw_f, op.pw_d = _pw_pick(op, 4)
             dense3 = op.ks == 3 and op.stride == 1 and op.pad == 1
             wino_ok = dense3 and WINOGRAD
-            op.wino_f = wino_ok and WINOGRAD_FWD and bool(query("seg_conv_wino_pick", y.N, y.H, y.W, op.cin_pad,
-                                                                op.cout))
-            op.wino_d = wino_ok and WINOGRAD_DGRAD and not op.first and bool(
-                query("seg_conv_wino_pick", y.N, y.H, y.W, r4(op.cout), op.cin))
+            # seg_conv_wino_pick: 1 = the two-launch form, 2 = the fused kernel
+            pf = query("seg_conv_wino_pick", y.N, y.H, y.W, op.cin_pad, op.cout) if wino_ok and WINOGRAD_FWD else 0
+            pd = (query("seg_conv_wino_pick", y.N, y.H, y.W, r4(op.cout), op.cin)
+                  if wino_ok and WINOGRAD_DGRAD and not op.first else 0)
+            op.wino_f, op.wino_ff = pf != 0, pf == 2
+            op.wino_d, op.wino_fd = pd != 0, pd == 2
             op.wino_w = wino_ok and WINOGRAD_WGRAD and bool(query("seg_conv_wino_wgrad_pick", y.N, y.H, y.W, op.cin_pad,
                                                                    op.cout))
             op.halo_f = (dense3 and not op.wino_f

@@ -23,7 +23,7 @@ FAMILIES = {  # "conv3" = the dense 3x3 conv forward + data gradient (bench.py's
     # igemm2_kernel<BM, BN, WM, WN, KS, XF> (csrc/igemm2.hip:91; six template parameters since 53539df --
     # round 4's three-parameter pattern matched none of them)
     "conv3": re.compile(r"igemm_conv_kernel<\d+, \d+, \d+, \d+, 3, \d+|igemm_conv_kernelILi\d+ELi\d+ELi\d+ELi\d+ELi3E"
-                        r"|wino_gemm_kernel|wino_out_kernel|halo3x3_kernel"
+                        r"|wino_gemm_kernel|wino_out_kernel|wino_fused_kernel|halo3x3_kernel"
                         r"|igemm2_kernel<\d+, \d+, \d+, \d+, 3[,>]|igemm2_kernelILi\d+ELi\d+ELi\d+ELi\d+ELi3E"),
     "igemm1": re.compile(r"igemm_conv_kernel<\d+, \d+, \d+, \d+, 1, \d+|igemm_conv_kernelILi\d+ELi\d+ELi\d+ELi\d+ELi1E"
                          r"|igemm2_kernel<\d+, \d+, \d+, \d+, 1[,>]|igemm2_kernelILi\d+ELi\d+ELi\d+ELi\d+ELi1E"),
@@ -35,7 +35,8 @@ FAMILIES = {  # "conv3" = the dense 3x3 conv forward + data gradient (bench.py's
     "wgrad1": re.compile(r"wgrad_kernel<\d+, \d+, \d+, \d+, 1[,>]|wgrad_kernelILi\d+ELi\d+ELi\d+ELi\d+ELi1E"),
 }
 # conv ops per step of the profiled model: MobileNetV2UNet 17 (8 decoder convs fwd + 8 dgrad + the stem fwd),
-# UNet 27 (14 convs fwd + 13 dgrad); a Winograd op is two kernels (wino_gemm + wino_out), every other op one
+# UNet 27 (14 convs fwd + 13 dgrad); a two-launch Winograd op is two kernels (wino_gemm + wino_out), every other op
+# (the fused Winograd kernel included) one
 OPS_PER_STEP = {"MobileNetV2UNet": 17, "UNet": 27}
 
 

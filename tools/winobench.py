@@ -20,7 +20,7 @@ SHAPES = [("up1.0", 32, 16, 32, 1344, 256), ("up1.3", 32, 16, 32, 256, 256), ("u
           ("up4.0", 32, 128, 256, 80, 32), ("up4.3", 32, 128, 256, 32, 32)]
 
 
-SHAPES_UNET = [("u.d2b", 8, 128, 256, 128, 256), ("u.d2c", 8, 128, 256, 256, 256), ("u.d3", 8, 64, 128, 256, 256),
+SHAPES_UNET = [("u.d1a", 8, 256, 512, 64, 128), ("u.d1b", 8, 256, 512, 128, 128), ("u.d2b", 8, 128, 256, 128, 256), ("u.d2c", 8, 128, 256, 256, 256), ("u.d3", 8, 64, 128, 256, 256),
                ("u.up1a", 8, 128, 256, 512, 128), ("u.up1b", 8, 128, 256, 128, 128),
                ("u.up2a", 8, 256, 512, 256, 64), ("u.up2b", 8, 256, 512, 64, 64)]
 if os.environ.get("WINOBENCH") == "unet":

@@ -31,7 +31,13 @@ namespace {
 // kind 0: (sum(y-k), sum((y-k)^2)),  k = y[0][c]                   -> BN stats
 // kind 1: (sum(dz),  sum(dz*(y-mean))), dz = dA * act'(y*scale+shift) -> BN backward
 // kind 2: (sum(y), 0)                                               -> bias grad
-constexpr int kRedThreads = 512;
+#ifndef SEG_RED_THREADS
+#define SEG_RED_THREADS 512
+#endif
+#ifndef SEG_CHAN_F32_VW
+#define SEG_CHAN_F32_VW 8  // channels per lane of the fp32 reductions (4: fewer registers per wave)
+#endif
+constexpr int kRedThreads = SEG_RED_THREADS;
 constexpr int kRedSlice = 64;  // channel groups per block (blockIdx.y slices beyond)
 
 #ifndef SEG_CHAN_MAXBLK
@@ -160,7 +166,8 @@ void launch_chan_partial(const T* y, long ldy, const T* da, long ldda, long M, i
   const int nblk = chan_blocks(M);
   const int rpb = seg_cdiv(M, nblk);
   auto eoff8 = [](const T* p) { return ((uintptr_t)p / sizeof(T)) % 8 == 0; };
-  const bool v8 = C % 8 == 0 && ldy % 8 == 0 && (!da || ldda % 8 == 0) && eoff8(y) && (!da || eoff8(da));
+  const bool v8 = (sizeof(T) == 2 || SEG_CHAN_F32_VW == 8) && C % 8 == 0 && ldy % 8 == 0 && (!da || ldda % 8 == 0) &&
+                  eoff8(y) && (!da || eoff8(da));
   if (v8)
     hipLaunchKernelGGL((chan_partial_kernel<KIND, T, 8>), dim3(nblk, seg_cdiv(C / 8, kRedSlice)), dim3(kRedThreads),
                        0, stream, y, ldy, da, ldda, (int)M, C, scale, shift, mean, act, part, rpb);

@@ -341,7 +341,8 @@ struct WinoFusedArgs {
   float* stat;                  // optional BN partials [row tiles of 64 tiles][2][Cout]
   int N, H, W, Cin, Cout;
   int T, th, tw;
-  unsigned in_bytes, wk_bytes;  // extents of `in` and `wk` (buffer-load range checks: < 2^31)
+  long in_elems;                // extent of `in` (elements)
+  unsigned wk_bytes;            // extent of `wk` (buffer-load range check: < 2^31)
 };
 
 #ifndef SEG_WF_EXP
@@ -378,7 +379,12 @@ __global__ __launch_bounds__(256) void wino_fused_kernel(WinoFusedArgs a) {
   const int lid = xcd_swizzle(blockIdx.x, gridDim.x);
   const int tn = lid % tiles_n, tm = lid / tiles_n;
   const int m0 = tm * BT, n0 = tn * BC;
-  const __amdgpu_buffer_rsrc_t rin = seg_rsrc(a.in, a.in_bytes), rwk = seg_rsrc(a.wk, a.wk_bytes);
+  // input descriptor based at the image of the block's first tile (32-bit offsets cover the images the block
+  // touches: seg_conv_wino_fused checks their extent), U descriptor over the whole pack
+  const int nfirst = m0 / (a.th * a.tw);
+  const long boff = (long)nfirst * a.H * a.W * a.ldin;
+  const __amdgpu_buffer_rsrc_t rin = seg_rsrc(a.in + boff, (unsigned)min((a.in_elems - boff) * 4, (long)kFusedOOB - 16));
+  const __amdgpu_buffer_rsrc_t rwk = seg_rsrc(a.wk, a.wk_bytes);
 
   // this lane's tile (A row `row` of the wave's 32): byte offset of its 4x4 patch's corner (32-bit wrap arithmetic:
   // exact wherever a patch pixel is in the image) and the in-image mask
@@ -396,7 +402,7 @@ __global__ __launch_bounds__(256) void wino_fused_kernel(WinoFusedArgs a) {
 #pragma unroll
       for (int q = 0; q < 4; ++q)
         if (tok && (unsigned)(h0 + p) < (unsigned)a.H && (unsigned)(w0 + q) < (unsigned)a.W) pm |= 1u << (p * 4 + q);
-    pbase = (unsigned)((((long)n * a.H + h0) * a.W + w0) * a.ldin * 4) + 16u * h;
+    pbase = (unsigned)((((long)(n - nfirst) * a.H + h0) * a.W + w0) * a.ldin * 4) + 16u * h;
     opix = (n * a.H + 2 * ty) * a.W + 2 * tx;
   }
   const unsigned rstep = (unsigned)(a.W * a.ldin * 4), cstep = (unsigned)(a.ldin * 4);
@@ -791,11 +797,18 @@ __global__ __launch_bounds__(256) void wino_wgrad_reduce_kernel(const float* __r
 #ifndef SEG_WINO_FUSED
 #define SEG_WINO_FUSED 1
 #endif
+// The images one 128-tile block of wino_fused_kernel reads (its first tile's image and the ones after it) fit its
+// 32-bit buffer offsets.
+static bool fused_fits(int N, int H, int W, long ldin) {
+  const long tiles = (long)(H / 2) * (W / 2);
+  const long imgs = std::min<long>(N, tiles > 0 ? 128 / tiles + 2 : N);
+  return imgs * H * W * ldin * 4 < (long)kFusedOOB - 16;
+}
 SEG_API int seg_conv_wino_pick(int N, int H, int W, int Cin, int Cout) {
   if ((H & 1) || (W & 1) || (Cin & 3) || (Cout & 3) || N <= 0) return 0;
   if (Cin >= 256 && Cout >= 128) return 1;
   if (Cin >= 128 && Cout >= 128 && Cout <= 2 * Cin) return 1;
-  const bool fits = (long)N * H * W * (Cin + 64) * 4 < (long)kFusedOOB;  // buffer-load range (row stride slack)
+  const bool fits = fused_fits(N, H, W, Cin + 64);  // buffer-load range (row stride slack)
   return (SEG_WINO_FUSED && Cin >= 64 && Cout >= 64 && Cin + Cout >= 192 && fits) ? 2 : 0;
 }
 
@@ -849,9 +862,9 @@ SEG_API int seg_conv_wino_fused(const float* in, long ldin, int N, int H, int W,
   a.N = N; a.H = H; a.W = W; a.Cin = Cin; a.Cout = Cout;
   a.th = H / 2; a.tw = W / 2; a.T = N * a.th * a.tw;
   if (a.T == 0) return 0;
-  const long in_bytes = ((long)N * H * W - 1) * ldin * 4 + (long)Cin * 4, wk_bytes = 16L * Cout * ldk * 4;
-  if (in_bytes >= (long)kFusedOOB || wk_bytes >= (long)kFusedOOB) return (int)hipErrorInvalidValue;
-  a.in_bytes = (unsigned)in_bytes;
+  const long wk_bytes = 16L * Cout * ldk * 4;
+  if (!fused_fits(N, H, W, ldin) || wk_bytes >= (long)kFusedOOB) return (int)hipErrorInvalidValue;
+  a.in_elems = ((long)N * H * W - 1) * ldin + Cin;
   a.wk_bytes = (unsigned)wk_bytes;
   hipLaunchKernelGGL(wino_fused_kernel<4>, dim3(seg_cdiv(a.T, 128) * seg_cdiv(Cout, 32)), dim3(256), 0, stream, a);
   SEG_RET_LAST();

@@ -32,10 +32,10 @@ namespace {
 // kind 1: (sum(dz),  sum(dz*(y-mean))), dz = dA * act'(y*scale+shift) -> BN backward
 // kind 2: (sum(y), 0)                                               -> bias grad
 #ifndef SEG_RED_THREADS
-#define SEG_RED_THREADS 512
+#define SEG_RED_THREADS 256  // measured (interleaved A/B, profiles/r05/ab_fused_bn_knobs.txt): bf16io +0.5 %, f32 flat vs 512
 #endif
 #ifndef SEG_CHAN_F32_VW
-#define SEG_CHAN_F32_VW 8  // channels per lane of the fp32 reductions (4: fewer registers per wave)
+#define SEG_CHAN_F32_VW 4  // channels per lane of the fp32 reductions: 4 measured +0.3 % f32 vs 8 (fewer registers)
 #endif
 constexpr int kRedThreads = SEG_RED_THREADS;
 constexpr int kRedSlice = 64;  // channel groups per block (blockIdx.y slices beyond)

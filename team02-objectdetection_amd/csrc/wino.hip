@@ -790,10 +790,12 @@ __global__ __launch_bounds__(256) void wino_wgrad_reduce_kernel(const float* __r
 //   512x128 1.44 | 128x256 1.28 | 128x128 1.11-1.24 | 128x288 1.00 | 128x512 1.10
 //   256x64 1.04 | 152x64 0.91 | 64x152 0.62 | 64x64 0.70-0.79 | Cin or Cout 32/80 0.36-0.54
 // Deterministic: the choice depends on the shape only.
-// 2 = the fused kernel (seg_conv_wino_fused) where the two-launch form loses to the direct / LDS-halo kernels but the
-// fused one wins (tools/wfbench.py, tools/winobench.py at bs 32, per launch: up3.0 152 -> 64 forward 339 vs 373 us on
-// the LDS-halo kernel, its data gradient 64 -> 152 405 vs 423 us direct, up2.0's data gradient 128 -> 288 358 vs 387
-// us; up3.3 64 -> 64 168 vs 163 and the 32 / 80-channel convs 199-604 vs 182-552 us stay off).
+// 2 = the fused kernel (seg_conv_wino_fused) where it beats the direct / LDS-halo kernels and the two-launch form
+// does not apply (tools/winobench.py per launch, profiles/r05/winobench_*.txt): MobileNetV2UNet bs 32 up3.0 152 -> 64
+// forward 332 vs 372 us (LDS-halo), its data gradient 64 -> 152 398 vs 421 us (direct); UNet 512x1024 bs 8 64 -> 128
+// forward 1314 vs 1516 us, 64 -> 256 data gradient 2591 vs 2673 us.  Not taken: 64 -> 64, 128 -> 64 and 256 -> 64
+// (the LDS-halo kernel is 2-5 % faster) and the 32 / 80-channel convs (halo / direct 3-9 % faster).  The two-launch
+// form for every Cin, Cout >= 128 conv: 128 -> 512 2086 vs 2411 us fused, 128 -> 288 361 vs 355 us.
 #ifndef SEG_WINO_FUSED
 #define SEG_WINO_FUSED 1
 #endif
@@ -807,9 +809,9 @@ static bool fused_fits(int N, int H, int W, long ldin) {
 SEG_API int seg_conv_wino_pick(int N, int H, int W, int Cin, int Cout) {
   if ((H & 1) || (W & 1) || (Cin & 3) || (Cout & 3) || N <= 0) return 0;
   if (Cin >= 256 && Cout >= 128) return 1;
-  if (Cin >= 128 && Cout >= 128 && Cout <= 2 * Cin) return 1;
+  if (Cin >= 128 && Cout >= 128) return 1;
   const bool fits = fused_fits(N, H, W, Cin + 64);  // buffer-load range (row stride slack)
-  return (SEG_WINO_FUSED && Cin >= 64 && Cout >= 64 && Cin + Cout >= 192 && fits) ? 2 : 0;
+  return (SEG_WINO_FUSED && fits && Cin >= 64 && (Cout >= 128 || (Cout >= 64 && Cin > 128 && Cin < 256))) ? 2 : 0;
 }
 
 // Number of row tiles of seg_conv_wino's BN partials.

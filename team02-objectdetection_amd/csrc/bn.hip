@@ -34,9 +34,6 @@ namespace {
 #ifndef SEG_RED_THREADS
 #define SEG_RED_THREADS 256  // measured (interleaved A/B, profiles/r05/ab_fused_bn_knobs.txt): bf16io +0.5 %, f32 flat vs 512
 #endif
-#ifndef SEG_CHAN_F32_VW
-#define SEG_CHAN_F32_VW 4  // channels per lane of the fp32 reductions: 4 measured +0.3 % f32 vs 8 (fewer registers)
-#endif
 constexpr int kRedThreads = SEG_RED_THREADS;
 constexpr int kRedSlice = 64;  // channel groups per block (blockIdx.y slices beyond)
 
@@ -166,8 +163,7 @@ void launch_chan_partial(const T* y, long ldy, const T* da, long ldda, long M, i
   const int nblk = chan_blocks(M);
   const int rpb = seg_cdiv(M, nblk);
   auto eoff8 = [](const T* p) { return ((uintptr_t)p / sizeof(T)) % 8 == 0; };
-  const bool v8 = (sizeof(T) == 2 || SEG_CHAN_F32_VW == 8) && C % 8 == 0 && ldy % 8 == 0 && (!da || ldda % 8 == 0) &&
-                  eoff8(y) && (!da || eoff8(da));
+  const bool v8 = C % 8 == 0 && ldy % 8 == 0 && (!da || ldda % 8 == 0) && eoff8(y) && (!da || eoff8(da));
   if (v8)
     hipLaunchKernelGGL((chan_partial_kernel<KIND, T, 8>), dim3(nblk, seg_cdiv(C / 8, kRedSlice)), dim3(kRedThreads),
                        0, stream, y, ldy, da, ldda, (int)M, C, scale, shift, mean, act, part, rpb);

@@ -195,10 +195,7 @@ __global__ __launch_bounds__(256) void up2_bwd_quad_kernel(const T* __restrict__
   f32x4 acc[2][2];
 #pragma unroll
   for (int k = 0; k < 2; ++k) acc[k][0] = acc[k][1] = f32x4{0.f, 0.f, 0.f, 0.f};
-#ifndef SEG_UP2_QUAD_UNROLL
-#define SEG_UP2_QUAD_UNROLL 6  // source rows whose loads may be in flight together (registers: ~24 VGPRs per row)
-#endif
-#pragma unroll SEG_UP2_QUAD_UNROLL
+#pragma unroll
   for (int j = 0; j < 6; ++j) {  // source row 2h-1+j; output row h uses j = 0..3, row h+1 j = 2..5
     const int r = 2 * h - 1 + j;
     const int rc = r < 0 ? 0 : (r > Ho - 1 ? Ho - 1 : r);
@@ -380,12 +377,9 @@ static int upsample_bwd_impl(const void* dout, long ldout, int nchw_grad, int N,
   const int grid = ew_grid((long)N * H * W * ((C + 3) / 4));
   const float sh = up_scale(H, Ho, ac), sw = up_scale(W, Wo, ac);
   const T* dn = static_cast<const T*>(dout);
-#ifndef SEG_UP2_QUAD
-#define SEG_UP2_QUAD 1
-#endif
   if (!nchw_grad && !ac && Ho == 2 * H && Wo == 2 * W && !(C & 3)) {
     const long rows = (long)N * ((H + 1) / 2), cols = (long)((W + 1) / 2) * (C / 4);
-    if (SEG_UP2_QUAD && rows <= 65535 && cols < (1L << 30))
+    if (rows <= 65535 && cols < (1L << 30))
       hipLaunchKernelGGL(up2_bwd_quad_kernel<T>, dim3((unsigned)seg_cdiv(cols, 256), (unsigned)rows), dim3(256), 0,
                          stream, dn, ldout, N, C, din, ldin, H, W, accumulate);
     else

@@ -152,8 +152,27 @@ __device__ __forceinline__ bool seg_last_arrival(unsigned* cnt, unsigned nblocks
 // Every piece is combined exactly once, by a block that saw the tile complete; results do not depend on who.
 // cnt: 4 words per tile {tickets, -, report (64-bit: count << 32 | given-up mask)}, zero before the first launch.
 // piece(p): the block's combine of piece p (called by all threads, block-uniform p).  word: 2 ints of LDS.
+#ifndef SEG_COMBINE_LEGACY
+#define SEG_COMBINE_LEGACY 0  // timing experiments only: round 4's unbounded all-arrived spin (hangs when a peer
+#endif                        // cannot become resident -- never a default)
 template <typename F>
 __device__ __forceinline__ void seg_tile_combine(unsigned* cnt, int S, int z, int spin, int* word, F&& piece) {
+#if SEG_COMBINE_LEGACY
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    while (__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (unsigned)S) __builtin_amdgcn_s_sleep(1);
+  }
+  __syncthreads();
+  piece(z);
+  __syncthreads();
+  if (threadIdx.x == 0 && __hip_atomic_fetch_add(cnt + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (unsigned)S - 1) {
+    __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(cnt + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  return;
+#endif
   unsigned* tickets = cnt;
   unsigned long long* report = reinterpret_cast<unsigned long long*>(cnt + 2);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's partial has landed

@@ -794,8 +794,9 @@ __global__ __launch_bounds__(256) void wino_wgrad_reduce_kernel(const float* __r
 // does not apply (tools/winobench.py per launch, profiles/r05/winobench_*.txt): MobileNetV2UNet bs 32 up3.0 152 -> 64
 // forward 332 vs 372 us (LDS-halo), its data gradient 64 -> 152 398 vs 421 us (direct); UNet 512x1024 bs 8 64 -> 128
 // forward 1314 vs 1516 us, 64 -> 256 data gradient 2591 vs 2673 us.  Not taken: 64 -> 64, 128 -> 64 and 256 -> 64
-// (the LDS-halo kernel is 2-5 % faster) and the 32 / 80-channel convs (halo / direct 3-9 % faster).  The two-launch
-// form for every Cin, Cout >= 128 conv: 128 -> 512 2086 vs 2411 us fused, 128 -> 288 361 vs 355 us.
+// (the LDS-halo kernel is 2-5 % faster) and the 32 / 80-channel convs (halo / direct 3-9 % faster).  Between the two
+// Winograd forms for Cin, Cout >= 128: the two-launch one up to Cout = 2 Cin and from Cout 512 (128 -> 512 2086 vs
+// 2411 us fused), the fused one in between (128 -> 288: 355 vs 361 us, and no 600 MB M round trip).
 #ifndef SEG_WINO_FUSED
 #define SEG_WINO_FUSED 1
 #endif
@@ -809,7 +810,7 @@ static bool fused_fits(int N, int H, int W, long ldin) {
 SEG_API int seg_conv_wino_pick(int N, int H, int W, int Cin, int Cout) {
   if ((H & 1) || (W & 1) || (Cin & 3) || (Cout & 3) || N <= 0) return 0;
   if (Cin >= 256 && Cout >= 128) return 1;
-  if (Cin >= 128 && Cout >= 128) return 1;
+  if (Cin >= 128 && Cout >= 128 && (Cout <= 2 * Cin || Cout >= 512)) return 1;
   const bool fits = fused_fits(N, H, W, Cin + 64);  // buffer-load range (row stride slack)
   return (SEG_WINO_FUSED && fits && Cin >= 64 && (Cout >= 128 || (Cout >= 64 && Cin > 128 && Cin < 256))) ? 2 : 0;
 }

@@ -96,8 +96,8 @@ int seg_conv_igemm_splits(long M, int Cout, int Cin, int ks);
  * together, each applying the split-K epilogue to its share -- a block that cannot wait for its peers (another
  * kernel holding the CUs) leaves its share to the tile's last arrival, so no block ever spins on a peer that is
  * not resident; else the separate reduce runs.  Bitwise the two-launch result.  cnt: 4 *
- * seg_conv_igemm_tiles(M, Cout) unsigned, zero before the first launch, re-armed by every launch.  No BN
- * statistics. */
+ * seg_conv_igemm_tiles(M, Cout) unsigned, zero before the first launch (epoch words: never re-armed; one counter
+ * buffer per concurrently running launch).  No BN statistics. */
 int seg_conv_igemm_tiles(long M, int Cout);
 /* Plan for those launches: out[3] = (splits, tile, output tiles -- the counters are 4 per tile).  tile -1 =
  * the cost model's (seg_conv_igemm_tiles), else an index into the kernel's tile table (the batch-1 rule:
@@ -587,7 +587,7 @@ int seg_conv_wgrad2_bf16io(const seg_bf16* dy, long lddy, const seg_bf16* x, lon
  * layout), wp [Cout][Ch]; fp16 operands with fp32 accumulation for the 1x1 convs (as
  * seg_conv_igemm_f16), fp32 depthwise (as seg_dw_fwd_bias_act).  seg_mbconv_ok: stride 1 / 2,
  * Cin <= 160 with an expand, Cout <= 320, channels % 4; res only at stride 1.  work / cnt:
- * seg_mbconv_work_floats floats and *counters unsigned (zero before the first launch; re-armed). */
+ * seg_mbconv_work_floats floats and *counters unsigned (zero before the first launch; epoch words, never re-armed). */
 /* The folded fp16 forward's segmentation head, outconv (src/unet.py:108-121: 1x1 -> BN -> ReLU -> 1x1, BN
  * folded), in one launch: out[M][ldo] = w2[C2][C1] . f16(act1(w1[C1][Cin] . f16(x) + b1)) + b2 -- fp16
  * operands and fp32 accumulation as seg_conv_igemm_f16 (another sum order).  seg_pw2_ok: (Cin, C1) = (32, 16),
@@ -607,6 +607,9 @@ int seg_stem_pre_f16(const unsigned char* frame, int Hf, int Wf, long row_bytes,
 int seg_mbconv_tune(int max_blocks);
 int seg_mbconv_ok(int Cin, int Ch, int Cout, int stride, int expand);
 long seg_mbconv_work_floats(int N, int H, int W, int Ch, int Cout, int stride, int* counters);
+/* Test hook: the poll bound of every in-launch split combine (seg_mbconv_f16, seg_conv_igemm_*_ic); -1 = automatic,
+ * 0 = no poll -- every block but a tile's last hands its share to the last arrival.  Results are identical. */
+int seg_set_combine_spin(int spin);
 int seg_mbconv_f16(const float* x, long ldx, int N, int H, int W, int Cin, const float* we, const float* be, int Ch,
                    const float* wd, const float* bd, int stride, const float* wp, const float* bp, int Cout,
                    const float* res, long ldres, float* out, long ldo, float* work, unsigned* cnt,

@@ -140,18 +140,21 @@ __device__ __forceinline__ bool seg_last_arrival(unsigned* cnt, unsigned nblocks
 // In-launch combine of a split tile (split-K / split hidden range) by its own S <= 32 blocks, with no block
 // ever waiting on a block that may not be resident (a plain "wait until all S splits arrived" spin
 // hangs when another kernel holds the CUs a peer needs, e.g. two such kernels on two streams).  The tile's
-// combine is cut into S pieces, piece z belonging to split block z:
-//   * every block publishes its partial (write-through, drained: the seg_last_arrival form above) and takes a
-//     ticket; the block with the last ticket knows the tile is complete;
-//   * a non-last block polls the ticket count for at most `spin` rounds (0: not at all -- the grid is known not to
-//     be co-resident); if the tile completed meanwhile it combines its own piece, else it gives the piece up; either
-//     way it then reports once, one atomic add of (1 << 32 | (gave up ? 1 << z : 0)) on the tile's report word;
-//   * the last block combines its own piece, waits for the S - 1 reports -- every peer already holds a ticket, so
-//     it is resident and reports within its bounded poll: this wait cannot hang -- then combines the pieces given
-//     up and re-arms the tile's words.
+// combine is cut into S pieces, piece z belonging to split block z.  One 64-bit word per tile: bits 0-5 the
+// arrivals of the current epoch, 6-37 the pieces given up, 38-63 the epoch.
+//   * every block publishes its partial (write-through, drained: the seg_last_arrival form above) and arrives
+//     (one atomic add); the arrival that completes the count is the tile's last: it combines its own piece and
+//     the pieces given up before it (the mask its add returned), after starting the next epoch (one store: no
+//     block can change the word in between -- see below), and never waits for anyone;
+//   * a non-last block polls for at most `spin` rounds (0: not at all -- the grid is known not to be co-resident)
+//     until the tile is complete (the count reached S, or the epoch moved on); then it combines its own piece;
+//   * a block whose poll ran out hands its piece over with a compare-and-swap that sets its mask bit only while the
+//     epoch is its own and the count is below S -- so the last arrival's add, which comes later in the word's
+//     order, returns the bit; if the tile completed meanwhile it combines its piece itself.
 // Every piece is combined exactly once, by a block that saw the tile complete; results do not depend on who.
-// cnt: 4 words per tile {tickets, -, report (64-bit: count << 32 | given-up mask)}, zero before the first launch.
-// piece(p): the block's combine of piece p (called by all threads, block-uniform p).  word: 2 ints of LDS.
+// No counter needs re-arming (the epoch advances), so a poller can never mistake a later launch for its own.
+// cnt: 4 words per tile (the first two used), zero before the first launch.  piece(p): the block's combine of
+// piece p (called by all threads, block-uniform p).  word: 2 ints of LDS.
 #ifndef SEG_COMBINE_LEGACY
 #define SEG_COMBINE_LEGACY 0  // timing experiments only: round 4's unbounded all-arrived spin (hangs when a peer
 #endif                        // cannot become resident -- never a default)
@@ -173,48 +176,54 @@ __device__ __forceinline__ void seg_tile_combine(unsigned* cnt, int S, int z, in
   }
   return;
 #endif
-  unsigned* tickets = cnt;
-  unsigned long long* report = reinterpret_cast<unsigned long long*>(cnt + 2);
+  typedef unsigned long long u64;
+  constexpr u64 kArr = 0x3full;
+  constexpr int kMaskShift = 6, kEpochShift = 38;
+  u64* w = reinterpret_cast<u64*>(cnt);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's partial has landed
   __syncthreads();
   if (threadIdx.x == 0) {
-    const unsigned t = __hip_atomic_fetch_add(tickets, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const int last = t == (unsigned)S - 1;
-    bool ready = last;
-    for (int i = 0; !ready && i < spin; ++i) {
-      ready = __hip_atomic_load(tickets, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= (unsigned)S;
-      if (!ready) __builtin_amdgcn_s_sleep(1);
+    const u64 old = __hip_atomic_fetch_add(w, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const u64 ep = old >> kEpochShift;
+    bool own = true;
+    unsigned extra = 0;
+    if ((old & kArr) == (u64)(S - 1)) {  // last arrival: the next epoch, then the pieces given up before us
+      extra = (unsigned)(old >> kMaskShift);
+      __hip_atomic_store(w, (ep + 1) << kEpochShift, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+      auto complete = [&](u64 v) { return (v >> kEpochShift) != ep || (v & kArr) >= (u64)S; };
+      bool done = false;
+      for (int i = 0; !done && i < spin; ++i) {
+        done = complete(__hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+        if (!done) __builtin_amdgcn_s_sleep(1);
+      }
+      if (!done) {  // hand the piece to the last arrival, unless it has arrived meanwhile
+        u64 cur = __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        while (!complete(cur)) {
+          if (__hip_atomic_compare_exchange_strong(w, &cur, cur | (1ull << (kMaskShift + z)), __ATOMIC_RELAXED,
+                                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+            own = false;
+            break;
+          }
+        }
+      }
     }
-    word[0] = last;
-    word[1] = ready;
+    word[0] = own;
+    word[1] = (int)extra;
   }
   __syncthreads();
-  const int last = word[0], ready = word[1];
-  if (ready) piece(z);
-  if (!last) {
-    __syncthreads();  // this block's piece is done (its stores issued) before it reports
-    if (threadIdx.x == 0)
-      __hip_atomic_fetch_add(report, (1ull << 32) | (ready ? 0ull : 1ull << z), __ATOMIC_RELAXED,
-                             __HIP_MEMORY_SCOPE_AGENT);
-    return;
-  }
-  __syncthreads();  // every wave has read word[] and finished its piece
-  if (threadIdx.x == 0) {  // the S - 1 peers are resident (they hold tickets): wait for their reports
-    unsigned long long r = 0;
-    while (((r = __hip_atomic_load(report, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) >> 32) < (unsigned)S - 1)
-      __builtin_amdgcn_s_sleep(1);
-    word[1] = (int)(unsigned)r;  // the pieces given up
-    __hip_atomic_store(report, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-arm (no peer touches
-    __hip_atomic_store(tickets, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);    // either word any more)
-  }
-  __syncthreads();
-  const unsigned given = (unsigned)word[1];
+  const int own = word[0];
+  const unsigned extra = (unsigned)word[1];
+  if (own) piece(z);
   for (int p = 0; p < S; ++p)
-    if ((given >> p) & 1u) piece(p);
+    if ((extra >> p) & 1u) piece(p);
 }
 // Bound of seg_tile_combine's poll when the grid is co-resident (~1 us per round: a few ms before a block gives
 // its piece to the last arrival -- only ever reached when another kernel holds the CUs a peer needs).
 constexpr int kSegCombineSpin = 4096;
+// The poll bound a launch passes to seg_tile_combine: `automatic`, unless seg_set_combine_spin (csrc/mbconv.hip) set
+// an override (tests force 0 / 1: every non-last block hands its piece over).
+int seg_combine_spin(int automatic);
 
 // XCD-aware block swizzle (bijective for any nblk): the dispatcher deals blocks
 // round-robin over the 8 XCDs (block b and b+8 share an XCD and its 4 MiB L2), so

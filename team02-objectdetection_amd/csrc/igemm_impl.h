@@ -44,8 +44,9 @@ struct IgemmArgs {
   // [tilesM][2][Cout] for seg_bn_bwd_finalize_tiles -- the reduction pass over dA disappears
   const void* by; long ldby; const float* bsc; const float* bsh; const float* bmu; int bact; float* bpart;
   // split-K with the combine in the launch (part set, the whole grid co-resident, <= 32 splits): seg_tile_combine's
-  // words, [tilesM * tilesN][4] (zero before the first launch, re-armed by the tile's last leaver)
+  // words, [tilesM * tilesN][4] (zero before the first launch; an epoch word, never re-armed)
   unsigned* kcnt;
+  int kspin;                     // seg_tile_combine's poll bound
 };
 
 #ifndef SEG_IGEMM_DEPTH
@@ -498,7 +499,7 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void igemm_conv_kernel(
         out[(long)row * a.ldout + col] = static_cast<IT>(v);
       }
     };
-    seg_tile_combine(a.kcnt + 4 * lid, S, z, kSegCombineSpin, reinterpret_cast<int*>(smem), piece);
+    seg_tile_combine(a.kcnt + 4 * lid, S, z, a.kspin, reinterpret_cast<int*>(smem), piece);
     return;
   }
   float bcol[NI];
@@ -897,6 +898,7 @@ int conv_igemm_impl(const IT* in, long ldin, int N, int H, int W, int Cin, const
   a.xs = xs; a.xb = xb; a.xact = xact;
   a.by = by; a.ldby = ldby; a.bsc = bsc; a.bsh = bsh; a.bmu = bmu; a.bact = bact; a.bpart = bpart;
   a.kcnt = splits > 1 ? kcnt : nullptr;
+  a.kspin = seg_combine_spin(kSegCombineSpin);
   g_igemm_ic_used = false;
   if (bpart && !igemm_bnout_tile_ok(a.M, Cout, (int)sizeof(IT))) return (int)hipErrorInvalidValue;
   if (tile < -1 || tile >= (int)(sizeof(kTiles) / sizeof(kTiles[0])) || (tile >= 0 && bpart))

@@ -26,6 +26,15 @@
 #define SEG_MBCONV_CAP 256
 #endif
 
+static int g_combine_spin = -1;
+int seg_combine_spin(int automatic) { return g_combine_spin >= 0 ? g_combine_spin : automatic; }
+// Override the poll bound of every in-launch split combine (seg_mbconv_f16, seg_conv_igemm_*_ic): -1 = automatic,
+// 0 = no poll (every block but a tile's last hands its piece over).  Test hook: results are the same either way.
+SEG_API int seg_set_combine_spin(int spin) {
+  g_combine_spin = spin < 0 ? -1 : spin;
+  return 0;
+}
+
 namespace {
 
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
@@ -44,7 +53,7 @@ struct MbArgs {
   int N, H, W, Cin, Ch, Cout, Ho, Wo;
   int tiles_w, tiles_h, ntiles, splits, hper;  // hper: hidden channels per split (multiple of HC)
   float* work; unsigned* cnt;         // splits > 1: partials [ntiles][splits][TP][Cout], counters [2][ntiles]
-  int spin;                           // the whole grid is resident: the blocks of a tile combine it together
+  int spin;                           // seg_tile_combine's poll bound (0: the grid is not co-resident)
 };
 
 __device__ __attribute__((aligned(16))) float g_mb_zero[4];
@@ -297,7 +306,7 @@ __global__ __launch_bounds__(kThreads) void mbconv_f16_kernel(MbArgs a) {
     const int e0 = (int)((long)pz * ne / a.splits), e1 = (int)((long)(pz + 1) * ne / a.splits);
     for (int e = e0 + tid; e < e1; e += kThreads) emit(e, split_sum(e));
   };
-  seg_tile_combine(a.cnt + 4 * t, a.splits, split, a.spin ? kSegCombineSpin : 0, word, piece);
+  seg_tile_combine(a.cnt + 4 * t, a.splits, split, a.spin, word, piece);
 }
 
 int g_mb_cap = SEG_MBCONV_CAP;  // blocks per launch the hidden splits aim for (seg_mbconv_tune)
@@ -375,7 +384,7 @@ SEG_API int seg_mbconv_f16(const float* x, long ldx, int N, int H, int W, int Ci
       (void)hipGetLastError();
       occ = 1;
     }
-    a.spin = (long)a.ntiles * a.splits <= (long)std::max(occ, 1) * seg_num_cus();
+    a.spin = seg_combine_spin((long)a.ntiles * a.splits <= (long)std::max(occ, 1) * seg_num_cus() ? kSegCombineSpin : 0);
   }
   if (stride == 1) {
     if (e) hipLaunchKernelGGL((mbconv_f16_kernel<1, true>), grid, dim3(kThreads), 0, stream, a);

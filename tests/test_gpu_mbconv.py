@@ -180,3 +180,26 @@ def test_stem_pre_equals_preprocess_then_conv(fhw, hw):
     torch.cuda.synchronize()
     assert float((out[:, :32] - ref).norm() / ref.norm()) < 1e-5
     assert bool(out[:, 32:].isnan().all())
+
+
+@pytest.mark.parametrize("spin", [0, 1])
+def test_predictor_combine_hand_off_bitwise(spin):
+    """The in-launch split combines (seg_mbconv_f16, seg_conv_igemm_f16_ic) with the poll bound forced to 0 / 1
+    (seg_set_combine_spin): every block but a tile's last hands its share over through the epoch word's mask --
+    the path a block takes when a peer cannot become resident -- and the frame is bitwise the
+    default's."""
+    from seg_amd.infer import Predictor
+    import numpy as np
+    model = deterministic_init(MobileNetV2UNet(10), seed=13, random_running_stats=True).to(DEV).eval()
+    f = (np.random.default_rng(1).random((720, 1280, 3)) * 255).astype(np.uint8)
+    p = Predictor(model, frame_hw=(720, 1280), graph=False, math="f16")
+    m0 = p(f).clone()
+    l0 = p.logits().clone()
+    try:
+        call("seg_set_combine_spin", spin)
+        for _ in range(2):  # the epoch words carry over between launches
+            m1 = p(f).clone()
+            assert torch.equal(m1, m0) and torch.equal(p.logits(), l0)
+    finally:
+        call("seg_set_combine_spin", -1)
+    assert torch.equal(p(f), m0)

@@ -1,7 +1,7 @@
 """GPU: seg_conv_igemm_{act,bf16,f16}_ic -- the implicit GEMM's split-K with the combine inside the
 launch (the batch-1 convs of the folded inference forward, inference.py:162-163 through
 src/unet.py:58-64,113-116): bitwise the two-launch split-K (same fixed-order sum and epilogue),
-repeat launches equal, tile counters re-armed; the batch-1 plan's tiles (seg_conv_igemm_plan_b1) give
+repeat launches equal, the tiles' epoch words advanced with no count or hand-off bit left over; the batch-1 plan's tiles (seg_conv_igemm_plan_b1) give
 the two-launch result at the same split count."""
 import ctypes
 
@@ -24,9 +24,11 @@ CASES = [  # N, H, W, Cin, Cout, ks, act, addend -- decoder convs of a 128x256 f
 ]
 
 
+@pytest.mark.parametrize("spin", [-1, 0])
 @pytest.mark.parametrize("name", ["seg_conv_igemm_act", "seg_conv_igemm_bf16", "seg_conv_igemm_f16"])
 @pytest.mark.parametrize("N,H,W,Cin,Cout,ks,act,addend", CASES)
-def test_splitk_in_launch_equals_two_launch(name, N, H, W, Cin, Cout, ks, act, addend):
+def test_splitk_in_launch_equals_two_launch(name, N, H, W, Cin, Cout, ks, act, addend, spin):
+    """spin 0 (seg_set_combine_spin): every block but a tile's last hands its share to the last arrival."""
     M = N * H * W
     splits = query("seg_conv_igemm_splits", M, Cout, Cin, ks)
     if splits == 1:
@@ -44,15 +46,23 @@ def test_splitk_in_launch_equals_two_launch(name, N, H, W, Cin, Cout, ks, act, a
          1, ks // 2, add.data_ptr() if addend else None, Cout if addend else 0, None, act, work.data_ptr(), splits, S())
     cnt = torch.zeros(4 * query("seg_conv_igemm_tiles", M, Cout), device=DEV, dtype=torch.int32)
     work2 = torch.full_like(work, float("nan"))
-    for _ in range(2):
-        o = torch.full((M, Cout), float("nan"), device=DEV)
-        call(name + "_ic", x.data_ptr(), Cin, N, H, W, Cin, w.data_ptr(), ldk, b.data_ptr(), o.data_ptr(), Cout, H, W,
-             Cout, ks, 1, ks // 2, add.data_ptr() if addend else None, Cout if addend else 0, act, work2.data_ptr(),
-             splits, -1, cnt.data_ptr(), S())
-        outs.append(o)
-    torch.cuda.synchronize()
+    call("seg_set_combine_spin", spin)
+    try:
+        for _ in range(2):
+            o = torch.full((M, Cout), float("nan"), device=DEV)
+            call(name + "_ic", x.data_ptr(), Cin, N, H, W, Cin, w.data_ptr(), ldk, b.data_ptr(), o.data_ptr(), Cout, H,
+                 W, Cout, ks, 1, ks // 2, add.data_ptr() if addend else None, Cout if addend else 0, act,
+                 work2.data_ptr(), splits, -1, cnt.data_ptr(), S())
+            outs.append(o)
+        torch.cuda.synchronize()
+    finally:
+        call("seg_set_combine_spin", -1)
     assert torch.equal(outs[0], ref) and torch.equal(outs[1], ref)
-    assert int(cnt.abs().sum()) == 0
+    # seg_tile_combine's epoch words after two launches: count and hand-off mask clear, epoch 2 (or untouched when
+    # the launch fell back to the separate reduce)
+    wv = cnt.view(-1, 4)
+    assert int(wv[:, 0].abs().sum()) == 0 and int(wv[:, 2:].abs().sum()) == 0
+    assert bool(((wv[:, 1] == 0) | (wv[:, 1] == 2 << 6)).all())
 
 
 B1 = [  # the folded inference forward's decoder convs of a 128x256 frame (tools/icbench.py) + a 1x1 head conv

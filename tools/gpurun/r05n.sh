@@ -1,10 +1,10 @@
 #!/bin/bash
-# inference: the deadlock-free tile combine against round 4's unbounded spin (test-only build), interleaved; wino op
-# tests at the new pick rule
+# inference: the deadlock-free tile combine against round 4's unbounded spin (test-only build), interleaved; the
+# combine / inference / op tests (hand-off path forced through seg_set_combine_spin)
 t=${1:-r05n}
 d=gpurun_out/$t; mkdir -p $d
 export TMPDIR=/tmp
-timeout -k 10 300 python -u -m pytest tests/test_gpu_ops.py tests/test_gpu_model.py -k "wino or parity" -x -q --timeout 200 --timeout-method thread > $d/tests.log 2>&1 || { tail -5 $d/tests.log; exit 1; }
+timeout -k 10 300 python -u -m pytest tests/test_gpu_infer.py tests/test_gpu_splitk_ic.py tests/test_gpu_mbconv.py tests/test_gpu_ops.py -k "not test_conv_wino_wgrad" -x -q --timeout 200 --timeout-method thread > $d/tests.log 2>&1 || { tail -5 $d/tests.log; exit 1; }
 grep -E "passed|failed" $d/tests.log
 for r in 1 2 3; do
   for v in base legacycomb; do

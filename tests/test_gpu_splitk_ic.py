@@ -18,6 +18,14 @@ def S():
     return torch.cuda.current_stream().cuda_stream
 
 
+def check_epoch_words(cnt, launches):
+    """seg_tile_combine's per-tile 64-bit words after `launches` launches: arrival count and hand-off mask clear,
+    the epoch advanced once per launch (or untouched when a launch fell back to the separate reduce)."""
+    wv = cnt.view(-1, 4)
+    assert int(wv[:, 0].abs().sum()) == 0 and int(wv[:, 2:].abs().sum()) == 0
+    assert bool(((wv[:, 1] == 0) | (wv[:, 1] == launches << 6)).all())
+
+
 CASES = [  # N, H, W, Cin, Cout, ks, act, addend -- decoder convs of a 128x256 frame, a head conv, ragged
     (1, 8, 16, 1344, 256, 3, 1, False), (1, 16, 32, 288, 128, 3, 1, False), (1, 32, 64, 152, 64, 3, 1, True),
     (1, 4, 8, 160, 960, 1, 2, False), (1, 5, 7, 64, 100, 3, 0, True),
@@ -58,11 +66,7 @@ def test_splitk_in_launch_equals_two_launch(name, N, H, W, Cin, Cout, ks, act, a
     finally:
         call("seg_set_combine_spin", -1)
     assert torch.equal(outs[0], ref) and torch.equal(outs[1], ref)
-    # seg_tile_combine's epoch words after two launches: count and hand-off mask clear, epoch 2 (or untouched when
-    # the launch fell back to the separate reduce)
-    wv = cnt.view(-1, 4)
-    assert int(wv[:, 0].abs().sum()) == 0 and int(wv[:, 2:].abs().sum()) == 0
-    assert bool(((wv[:, 1] == 0) | (wv[:, 1] == 2 << 6)).all())
+    check_epoch_words(cnt, 2)
 
 
 B1 = [  # the folded inference forward's decoder convs of a 128x256 frame (tools/icbench.py) + a 1x1 head conv
@@ -80,7 +84,7 @@ def plan_b1(M, Cout, Cin, ks):
 @pytest.mark.parametrize("H,W,Cin,Cout,ks", B1)
 def test_plan_b1_equals_cost_model_tile(name, H, W, Cin, Cout, ks):
     """The plan's tile (8-wave 128x64 / 64x64) against the cost model's tile at the plan's split count:
-    bitwise (tile choice keeps every output's K order); counters re-armed."""
+    bitwise (tile choice keeps every output's K order); epoch words advanced, nothing left over."""
     M = H * W
     splits, tile, ntl = plan_b1(M, Cout, Cin, ks)
     assert tile in (-1, 3, 12) and splits >= 1 and ntl >= 1
@@ -101,4 +105,4 @@ def test_plan_b1_equals_cost_model_tile(name, H, W, Cin, Cout, ks):
              Cout, ks, 1, ks // 2, None, 0, 1, work2.data_ptr(), splits, tile, cnt.data_ptr(), S())
         torch.cuda.synchronize()
         assert torch.equal(o, ref)
-    assert int(cnt.abs().sum()) == 0
+    check_epoch_words(cnt, 2)

@@ -389,14 +389,6 @@ int seg_preprocess_bgr(const unsigned char* frame, int N, int Hf, int Wf, long r
  * resized to the frame with cv2 INTER_NEAREST.  First maximum wins. */
 int seg_argmax_nearest(const float* low, long ld, int N, int H, int W, int C, int Hm, int Wm,
                        unsigned char* mask, int Hf, int Wf, hipStream_t stream);
-/* seg_pw2_f16 + seg_argmax_nearest in one launch for batch-1 fp16 inference (inference.py:62-70 after
- * src/unet.py:47-49): each band of frame rows evaluates outconv on the <= 4 low-resolution rows it needs, in LDS,
- * and classifies from there -- bitwise the two launches, the logits never written.  seg_head_argmax_ok(Cin, C1, C,
- * W, Wm, Wf): Cin 32, C1 16, C <= 12, W <= 320, Wm <= 2048, Wf % 4 == 0. */
-int seg_head_argmax_ok(int Cin, int C1, int C, int W, int Wm, int Wf);
-int seg_head_argmax_f16(const float* x, long ldx, int H, int W, int Cin, const float* w1, const float* b1, int C1,
-                        int act1, const float* w2, const float* b2, int C, int Hm, int Wm, unsigned char* mask, int Hf,
-                        int Wf, hipStream_t stream);
 
 /* ---- GPU augmentation (the readers' albumentations pipeline,
  *      src/BDD100KDataset.py:38-52) ---------------------- */

@@ -286,126 +286,6 @@ __global__ __launch_bounds__(256) void argmax_band_kernel(const float* __restric
   }
 }
 
-// The segmentation head and the mask in one launch (batch-1 fp16 inference): a band's block evaluates outconv's
-// 1x1 -> act -> 1x1 (seg_pw2_f16's arithmetic, operand for operand) for the <= 4 low-resolution rows its model rows
-// interpolate from, keeps those logits in LDS and classifies as argmax_band_kernel does -- the logits never reach
-// HBM and one launch goes away.  Bitwise seg_pw2_f16 + seg_argmax_nearest (the same floats into the same
-// model_class arithmetic).  Low-res rows are recomputed by the ~3 bands that share them (the head is 672 MACs per
-// pixel).
-constexpr int kHeadCin = 32, kHeadC1 = 16, kHeadLd = 12, kHeadMaxW = 320, kHeadRows = 4;
-__global__ __launch_bounds__(256) void head_argmax_band_kernel(
-    const float* __restrict__ x, long ldx, int H, int W, const float* __restrict__ w1, const float* __restrict__ b1,
-    int act1, const float* __restrict__ w2, const float* __restrict__ b2, int C, int Hm, int Wm, float sh, float sw,
-    uint8_t* __restrict__ mask, int Hf, int Wf, double ify, double ifx) {
-  __shared__ __attribute__((aligned(16))) float lg[kHeadRows][kHeadMaxW * kHeadLd];
-  __shared__ __attribute__((aligned(16))) float W1s[kHeadC1 * kHeadCin];
-  __shared__ __attribute__((aligned(16))) float W2s[kHeadLd * kHeadC1];
-  __shared__ float B1s[kHeadC1], B2s[kHeadLd];
-  __shared__ uint8_t lab[kBandRows][kBandMaxWm];
-  __shared__ int slot_of[kBandRows], ym_of[kBandRows], nslots, low_of[kHeadRows], nlow;
-  const int bands = (Hf + kBandRows - 1) / kBandRows;
-  const int y0 = blockIdx.x * kBandRows;
-  const int rows = min(kBandRows, Hf - y0);
-  (void)bands;
-  for (int i = threadIdx.x; i < kHeadC1 * kHeadCin; i += 256) W1s[i] = (float)(_Float16)w1[i];
-  for (int i = threadIdx.x; i < C * kHeadC1; i += 256) W2s[i] = (float)(_Float16)w2[i];
-  for (int i = threadIdx.x; i < kHeadC1; i += 256) B1s[i] = b1 ? b1[i] : 0.f;
-  for (int i = threadIdx.x; i < C; i += 256) B2s[i] = b2 ? b2[i] : 0.f;
-  if (threadIdx.x == 0) {  // the band's model rows, then the low-res rows they interpolate from (both monotone)
-    int ns = 0, prev = -1, nl = 0;
-    for (int r = 0; r < rows; ++r) {
-      const int ym = nearest_src(y0 + r, ify, Hm);
-      if (ym != prev) {
-        ym_of[ns++] = ym;
-        prev = ym;
-        const Lin lh = lin_index(ym, H, sh, 1);
-        const int ii[2] = {lh.i0, lh.i1};
-        for (int q = 0; q < 2; ++q) {
-          bool seen = false;
-          for (int k = 0; k < nl; ++k) seen |= low_of[k] == ii[q];
-          if (!seen) low_of[nl++] = ii[q];
-        }
-      }
-      slot_of[r] = ns - 1;
-    }
-    nslots = ns;
-    nlow = nl;
-  }
-  __syncthreads();
-  // the head on the low-res rows (seg_pw2_f16's per-pixel arithmetic)
-  for (int e = threadIdx.x; e < nlow * W; e += 256) {
-    const int sl = e / W, xw = e - sl * W;
-    const float* xr = x + ((long)low_of[sl] * W + xw) * ldx;
-    float xv[kHeadCin];
-#pragma unroll
-    for (int k = 0; k < kHeadCin; k += 4) {
-      const f32x4 v = ld4(xr + k);
-#pragma unroll
-      for (int j = 0; j < 4; ++j) xv[k + j] = (float)(_Float16)v[j];
-    }
-    float hh[kHeadC1];
-#pragma unroll
-    for (int c = 0; c < kHeadC1; ++c) {
-      float acc = 0.f;
-#pragma unroll
-      for (int k = 0; k < kHeadCin; ++k) acc = fmaf(xv[k], W1s[c * kHeadCin + k], acc);
-      hh[c] = (float)(_Float16)seg_act(acc + B1s[c], act1);
-    }
-    float* o = &lg[sl][xw * kHeadLd];
-    for (int c2 = 0; c2 < kHeadLd; ++c2) {
-      float acc = 0.f;
-      if (c2 < C) {
-#pragma unroll
-        for (int c = 0; c < kHeadC1; ++c) acc = fmaf(hh[c], W2s[c2 * kHeadC1 + c], acc);
-        acc += B2s[c2];
-      }
-      o[c2] = acc;
-    }
-  }
-  __syncthreads();
-  auto slot = [&](int lr) {
-    int k = 0;
-    while (k + 1 < nlow && low_of[k] != lr) ++k;
-    return k;
-  };
-  for (int e = threadIdx.x; e < nslots * Wm; e += 256) {  // model_class on the LDS rows
-    const int sl = e / Wm, xm = e - sl * Wm;
-    const Lin lh = lin_index(ym_of[sl], H, sh, 1), lw = lin_index(xm, W, sw, 1);
-    const float* r0 = lg[slot(lh.i0)];
-    const float* r1 = lg[slot(lh.i1)];
-    float best = 0.f;
-    int arg = 0;
-    bool done = false;
-    for (int c = 0; c < C && !done; c += 4) {
-      const f32x4 o = bilerp4(ld4(r0 + lw.i0 * kHeadLd + c), ld4(r0 + lw.i1 * kHeadLd + c), ld4(r1 + lw.i0 * kHeadLd + c),
-                              ld4(r1 + lw.i1 * kHeadLd + c), lh, lw);
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int k = c + j;
-        if (k >= C || done) continue;
-        const float v = o[j];
-        if (k == 0 || !(v <= best)) {
-          best = v;
-          arg = k;
-          if (isnan(v)) done = true;
-        }
-      }
-    }
-    lab[sl][xm] = (uint8_t)arg;
-  }
-  __syncthreads();
-  uint8_t* out = mask + (long)y0 * Wf;
-  const int q = Wf >> 2;
-  for (int e = threadIdx.x; e < rows * q; e += 256) {
-    const int r = e / q, xx = (e - r * q) * 4;
-    const uint8_t* lr = lab[slot_of[r]];
-    const unsigned v = (unsigned)lr[nearest_src(xx, ifx, Wm)] | ((unsigned)lr[nearest_src(xx + 1, ifx, Wm)] << 8) |
-                       ((unsigned)lr[nearest_src(xx + 2, ifx, Wm)] << 16) |
-                       ((unsigned)lr[nearest_src(xx + 3, ifx, Wm)] << 24);
-    *reinterpret_cast<unsigned*>(out + (long)r * Wf + xx) = v;
-  }
-}
-
 int grid_for(long total) { return (int)std::min<long>(seg_cdiv(total, 256), 8192); }
 
 }  // namespace
@@ -468,29 +348,5 @@ SEG_API int seg_argmax_nearest(const float* low, long ld, int N, int H, int W, i
   else
     hipLaunchKernelGGL(argmax_nearest_kernel, dim3(grid_for((long)N * Hf * Wf)), dim3(256), 0, stream, low, ld, N, H,
                        W, C, Hm, Wm, sh, sw, mask, Hf, Wf, ify, ifx);
-  SEG_RET_LAST();
-}
-
-// 1 when seg_head_argmax_f16 applies: MobileNetV2UNet's head (Cin 32 -> 16 -> C <= 12 classes), a low-res width
-// <= 320, model width <= 2048, frame width % 4 == 0.
-SEG_API int seg_head_argmax_ok(int Cin, int C1, int C, int W, int Wm, int Wf) {
-  return Cin == kHeadCin && C1 == kHeadC1 && C > 0 && C <= kHeadLd && W <= kHeadMaxW && Wm <= kBandMaxWm && Wf % 4 == 0
-             ? 1 : 0;
-}
-
-// seg_pw2_f16 (outconv of the folded fp16 forward) followed by seg_argmax_nearest (align_corners=True upsample to
-// Hm x Wm, argmax, nearest to Hf x Wf) in one launch, batch 1, bitwise the pair; the logits are not written.
-// x: outconv's input rows [H*W][ldx] (16-byte rows); weights / biases as seg_pw2_f16.
-SEG_API int seg_head_argmax_f16(const float* x, long ldx, int H, int W, int Cin, const float* w1, const float* b1,
-                                int C1, int act1, const float* w2, const float* b2, int C, int Hm, int Wm, uint8_t* mask,
-                                int Hf, int Wf, hipStream_t stream) {
-  if (!seg_head_argmax_ok(Cin, C1, C, W, Wm, Wf) || !x || !w1 || !w2 || !mask || (ldx & 3) || ((uintptr_t)x & 15) ||
-      ((uintptr_t)mask & 3) || H <= 0 || W <= 0 || Hm <= 0 || Hf <= 0 || act1 < SEG_ACT_NONE || act1 > SEG_ACT_RELU6)
-    return (int)hipErrorInvalidValue;
-  const float sh = Hm > 1 ? (float)(H - 1) / (float)(Hm - 1) : 0.f;
-  const float sw = Wm > 1 ? (float)(W - 1) / (float)(Wm - 1) : 0.f;
-  const double ify = 1.0 / ((double)Hf / Hm), ifx = 1.0 / ((double)Wf / Wm);
-  hipLaunchKernelGGL(head_argmax_band_kernel, dim3(seg_cdiv(Hf, kBandRows)), dim3(256), 0, stream, x, ldx, H, W, w1, b1,
-                     act1, w2, b2, C, Hm, Wm, sh, sw, mask, Hf, Wf, ify, ifx);
   SEG_RET_LAST();
 }

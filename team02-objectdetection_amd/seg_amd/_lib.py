@@ -78,8 +78,6 @@ PROTOTYPES = {
     "seg_bn_fold_batch": (_I, [_V, _I, _L, _V]),
     "seg_preprocess_bgr": (_I, [_V, _I, _I, _I, _L, _V, _I, _I, _I, _F, _F, _F, _F, _F, _F, _V]),
     "seg_argmax_nearest": (_I, [_V, _L, _I, _I, _I, _I, _I, _I, _V, _I, _I, _V]),
-    "seg_head_argmax_ok": (_I, [_I, _I, _I, _I, _I, _I]),
-    "seg_head_argmax_f16": (_I, [_V, _L, _I, _I, _I, _V, _V, _I, _I, _V, _V, _I, _I, _I, _V, _I, _I, _V]),
     "seg_resize_u8": (_I, [_V, _I, _I, _I, _L, _V, _I, _I, _I, _V, _V]),
     "seg_augment": (_I, [_V, _V, _I, _I, _I, _V, _F, _F, _F, _F, _F, _F, _V, _V, _V]),
     "seg_adam_step": (_I, [_V, _V, _I, _I, _F, _F, _F, _F, _V]),

@@ -1345,13 +1345,12 @@ class Run:
         if DEBUG_KEEP_RUN:
             LAST_RUN = self
 
-    def forward_folded(self, start=0, stop=None):
+    def forward_folded(self, start=0):
         """Eval forward with every BatchNorm folded (Program.fold must have run): one
         launch per conv, or per inverted residual with fp16 conv math (seg_mbconv_f16).  The
         NHWC4 input rows must already be in the image buffer (start = 0), or ops[:start] have
-        run (the stem fused with the preprocess, Program.stem_pre); ops[stop:] are left to the
-        caller (the head fused with the mask, seg_head_argmax_f16)."""
-        ops = self.prog.ops[:stop] if stop is not None else self.prog.ops
+        run (the stem fused with the preprocess, Program.stem_pre)."""
+        ops = self.prog.ops
         f16 = self.prog.math == "f16"
         groups = self.prog.mbconv_groups() if MBCONV and f16 else {}
         head = self.prog.pw2_head() if PW2 and f16 else None
@@ -1362,7 +1361,7 @@ class Run:
                 self._mbconv(k, g)
                 k += len(g)
                 continue
-            if k == head and k + 1 < len(ops):
+            if k == head:
                 c1, c2 = ops[k], ops[k + 1]
                 x, o = c1.inp, c2.out
                 call("seg_pw2_f16", self.ptr(x), x.ld, x.N * x.H * x.W, c1.cin, c1.fk.data_ptr(),
@@ -1469,7 +1468,6 @@ WINOGRAD_DGRAD = True  # ... and data-gradient transforms
 MBCONV = True
 STEM_PRE = True
 PW2 = True
-HEAD_ARGMAX = True  # ... and the head with the mask in one launch (seg_head_argmax_f16; the logits not written)
 PLAN_B1 = True
 _SIDE = {}
 

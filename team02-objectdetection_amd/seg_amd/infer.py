@@ -23,7 +23,7 @@ from __future__ import annotations
 import numpy as np
 import torch
 
-from ._lib import call, query
+from ._lib import call
 from . import engine
 from .engine import Run, get_program
 
@@ -86,13 +86,6 @@ class Predictor:
         self.graph = None
         self.refresh()
         self.stem_pre = self.prog.stem_pre() if (engine.STEM_PRE and math == "f16") else None
-        # outconv and the mask in one launch (seg_head_argmax_f16) when the head is the program's last two ops
-        self.head = None
-        h = self.prog.pw2_head() if (engine.PW2 and engine.HEAD_ARGMAX and math == "f16") else None
-        if h is not None and h == len(self.prog.ops) - 2:
-            c1, c2 = self.prog.ops[h], self.prog.ops[h + 1]
-            if query("seg_head_argmax_ok", c1.cin, c1.cout, c2.cout, c1.inp.W, self.prog.out_hw[1], self.Wf):
-                self.head = h
         if graph:
             self._capture()
 
@@ -110,21 +103,13 @@ class Predictor:
             op, o = self.stem_pre, self.stem_pre.out
             call("seg_stem_pre_f16", self.frame.data_ptr(), self.Hf, self.Wf, self.frame.stride(0), self.H, self.W,
                  *MEAN, *STD, op.fk_pack.data_ptr(), op.ldk_f, op.fb.data_ptr(), op.act, op.cout, rt.ptr(o), o.ld, s)
-            rt.forward_folded(start=1, stop=self.head)
+            rt.forward_folded(start=1)
         else:
             call("seg_preprocess_bgr", self.frame.data_ptr(), 1, self.Hf, self.Wf, self.frame.stride(0), rt.ptr(img),
                  img.ld, self.H, self.W, *MEAN, *STD, s)
-            rt.forward_folded(stop=self.head)
+            rt.forward_folded()
         lo = prog.logits
         Ho, Wo = prog.out_hw
-        if self.head is not None:  # outconv + upsample + argmax + nearest in one launch; the logits stay unwritten
-            c1, c2 = prog.ops[self.head], prog.ops[self.head + 1]
-            x = c1.inp
-            call("seg_head_argmax_f16", rt.ptr(x), x.ld, x.H, x.W, c1.cin, c1.fk.data_ptr(),
-                 c1.fb.data_ptr() if c1.fb is not None else None, c1.cout, c1.act, c2.fk.data_ptr(),
-                 c2.fb.data_ptr() if c2.fb is not None else None, c2.cout, Ho, Wo, self.mask.data_ptr(), self.Hf,
-                 self.Wf, s)
-            return
         call("seg_argmax_nearest", rt.ptr(lo), lo.ld, 1, lo.H, lo.W, lo.C, Ho, Wo, self.mask.data_ptr(), self.Hf,
              self.Wf, s)
 
@@ -168,10 +153,6 @@ class Predictor:
         """[1, C, H, W] logits of the last frame (the model's return value, src/unet.py:49)."""
         lo = self.prog.logits
         Ho, Wo = self.prog.out_hw
-        if self.head is not None:  # the fused head does not write the logits: evaluate outconv on demand
-            s = torch.cuda.current_stream(self.device).cuda_stream
-            self.run.stream = s
-            self.run.forward_folded(start=self.head)
         out = torch.empty((1, lo.C, Ho, Wo), device=self.device, dtype=torch.float32)
         call("seg_upsample_to_nchw", self.run.ptr(lo), lo.ld, 1, lo.H, lo.W, lo.C, out.data_ptr(), Ho, Wo, 1,
              torch.cuda.current_stream(self.device).cuda_stream)

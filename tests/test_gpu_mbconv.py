@@ -208,27 +208,3 @@ def test_predictor_combine_hand_off_bitwise(spin):
     finally:
         call("seg_set_combine_spin", -1)
     assert torch.equal(p(f), m0)
-
-
-def test_head_argmax_fused_bitwise():
-    """seg_head_argmax_f16 (outconv evaluated per band in LDS + upsample + argmax + nearest, one launch) against
-    seg_pw2_f16 + seg_argmax_nearest: the same mask bit for bit, and the logits (evaluated on demand) equal."""
-    from seg_amd.infer import Predictor
-    import numpy as np
-    model = deterministic_init(MobileNetV2UNet(10), seed=17, random_running_stats=True).to(DEV).eval()
-    f = (np.random.default_rng(2).random((720, 1280, 3)) * 255).astype(np.uint8)
-    saved = engine.HEAD_ARGMAX
-    try:
-        engine.HEAD_ARGMAX = False
-        p0 = Predictor(model, frame_hw=(720, 1280), graph=False, math="f16")
-        assert p0.head is None
-        m0 = p0(f).clone()
-        l0 = p0.logits()
-        engine.HEAD_ARGMAX = True
-        p1 = Predictor(model, frame_hw=(720, 1280), graph=True, math="f16")
-        assert p1.head == len(p1.prog.ops) - 2
-        m1 = p1(f).clone()
-        assert torch.equal(m1, m0)
-        assert torch.equal(p1.logits(), l0)
-    finally:
-        engine.HEAD_ARGMAX = saved

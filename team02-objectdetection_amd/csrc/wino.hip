@@ -1007,9 +1007,9 @@ __global__ __launch_bounds__(256) void wino_wgrad_reduce_kernel(const float* __r
 //   256x64 1.04 | 152x64 0.91 | 64x152 0.62 | 64x64 0.70-0.79 | Cin or Cout 32/80 0.36-0.54
 // Deterministic: the choice depends on the shape only.
 // 2 = the fused kernel (seg_conv_wino_fused) where it beats the direct / LDS-halo kernels and the two-launch form
-// does not apply (tools/winobench.py per launch, profiles/r05/winobench_*.txt): MobileNetV2UNet bs 32 up3.0 152 -> 64
-// forward 332 vs 372 us (LDS-halo), its data gradient 64 -> 152 398 vs 421 us (direct); UNet 512x1024 bs 8 64 -> 128
-// forward 1314 vs 1516 us, 64 -> 256 data gradient 2591 vs 2673 us.  Not taken: 64 -> 64, 128 -> 64 and 256 -> 64
+// does not apply (tools/winobench.py per launch, profiles/r05/winobench_*_fused2.txt): MobileNetV2UNet bs 32 up3.0
+// 152 -> 64 forward 270 vs 372 us (LDS-halo), its data gradient 64 -> 152 404 vs 417 us (direct); UNet 512x1024 bs 8
+// 64 -> 128 forward 1291 vs 1503 us, 64 -> 256 data gradient 2553 vs 2679 us.  Not taken: 64 -> 64, 128 -> 64 and 256 -> 64
 // (the LDS-halo kernel is 2-5 % faster) and the 32 / 80-channel convs (halo / direct 3-9 % faster).  Between the two
 // Winograd forms for Cin, Cout >= 128: the two-launch one up to Cout = 2 Cin and from Cout 512 (128 -> 512 2086 vs
 // 2411 us fused), the fused one in between (128 -> 288: 355 vs 361 us, and no 600 MB M round trip).

@@ -172,7 +172,7 @@ void launch_chan_partial(const T* y, long ldy, const T* da, long ldda, long M, i
                        0, stream, y, ldy, da, ldda, (int)M, C, scale, shift, mean, act, part, rpb);
 }
 
-// Finalize kernels.  Sum the per-block partials (<= 256 rows:
+// Finalize kernels.  Sum the per-block partials (<= SEG_CHAN_MAXBLK rows:
 // chan_blocks) of one channel with one wave: lane l loads rows l, l+64, l+128, l+192 all at
 // once (one memory round trip; clamped index, masked add), sums them in that order in
 // fp64, then a fixed xor butterfly (fp64 adds are commutative, so every lane ends with the
@@ -183,16 +183,17 @@ __device__ __forceinline__ bool sum_partials(const float* __restrict__ part, int
   const int c = blockIdx.x * 4 + (threadIdx.x >> 6);
   *cout = c;
   if (c >= C) return false;
-  float va[4], vb[4];
+  constexpr int Q = (SEG_CHAN_MAXBLK + 63) / 64;  // partial rows per lane (chan_blocks <= SEG_CHAN_MAXBLK)
+  float va[Q], vb[Q];
 #pragma unroll
-  for (int q = 0; q < 4; ++q) {
+  for (int q = 0; q < Q; ++q) {
     const long k = min(lane + 64 * q, nblk - 1);
     va[q] = part[k * 2 * ldp + c];
     vb[q] = part[k * 2 * ldp + ldp + c];
   }
   double a = 0.0, b = 0.0;
 #pragma unroll
-  for (int q = 0; q < 4; ++q) {
+  for (int q = 0; q < Q; ++q) {
     const bool ok = lane + 64 * q < nblk;
     a += ok ? (double)va[q] : 0.0;
     b += ok ? (double)vb[q] : 0.0;

@@ -70,6 +70,9 @@ def parse():
     ap.add_argument("--no-unet-block", action="store_true",
                     help="skip the nested \"unet_cfg5\" measurement (BASELINE configs[4]: UNet 10-class 512x1024 "
                          "bs=8/GPU, bf16io and f32) of the default line")
+    ap.add_argument("--no-dp1-block", action="store_true",
+                    help="skip the nested world-1 RCCL DataParallel overhead block (multi_gpu.world1_rccl) of the "
+                         "default line")
     ap.add_argument("--workload", choices=("train", "infer"), default="train",
                     help="train: BASELINE configs[1] (the headline); infer: configs[3], inference.py's per-frame path")
     ap.add_argument("--frames", type=int, default=500, help="timed frames of --workload infer")
@@ -281,6 +284,12 @@ def main():
                        "step_roofline": r["step_roofline"],
                        **({"multi_gpu": r["multi_gpu"]} if r["multi_gpu"] is not None else {})}
 
+    dp1 = None
+    if default_line and world == 1 and not args.no_dp1_block:
+        # the DataParallel host path at world size 1 over RCCL against the plain model, interleaved (VERDICT r5
+        # item 7: what the bucket machinery -- tape stops, all-reduce launches, BN-buffer broadcast -- costs a step
+        # when no 8-GPU node is at hand)
+        dp1 = {m: dp_world1(args, m, dev) for m in ("f32", "bf16io")}
     if rank == 0:
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
@@ -310,6 +319,8 @@ def main():
                                              f"bs=8/GPU, dp{world} (bf16 = bf16io math; f32 beside it)",
                                  "model": "UNet", "global_batch": 8 * world, "image": [512, 1024],
                                  "scaling": "weak", **unet}
+        if dp1 is not None:
+            line["multi_gpu"] = {"world1_rccl": dp1}
         if world == 1 and args.model == "MobileNetV2UNet" and not args.no_infer_block:
             # BASELINE configs[3] on the same GPU after the training lines (its own timed loop)
             r = infer_measure(args, "f16", 500, cpu_baseline=False)
@@ -319,6 +330,74 @@ def main():
         print(json.dumps(line), flush=True)
     if dist:
         torch.distributed.destroy_process_group()
+
+
+def dp_world1(args, math, dev, rounds=3):
+    """The DataParallel path (seg_amd/ddp.py) on ONE rank over RCCL against the plain model, same workload, same
+    process, interleaved rounds of args.steps timed steps each.  At world size 1 the all-reduces
+    move no data between GPUs, so the difference is the bucket machinery itself: the tape's host-callback stops (one
+    per gradient bucket, where the host leaves the replay, launches the bucket's all-reduce and resumes), RCCL's
+    launches on its stream and the compute stream's waits for them, the BN-buffer broadcast and the copies of the
+    averaged buckets handed to autograd.  Reports stops per step, host time per stop and the step-time overhead."""
+    import seg_amd
+    from seg_amd import Adam, deterministic_init, engine, synthetic_batch, tape
+    from seg_amd.ddp import DataParallel
+    own = not torch.distributed.is_initialized()
+    if own:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ["MASTER_PORT"] = str(_free_port())
+        torch.distributed.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
+    x, y = synthetic_batch(args.batch, args.height, args.width, args.classes, seed=1000)
+    x, y = x.to(dev), y.to(dev)
+    arms = {}
+    for kind in ("plain", "dp"):
+        core = deterministic_init(getattr(seg_amd, args.model)(args.classes), seed=0).to(dev).train()
+        engine.set_conv_math(core, math)
+        m = DataParallel(core) if kind == "dp" else core
+        arms[kind] = (core, m, Adam(m.parameters(), lr=1.5e-4))
+
+    def step(kind):
+        _, m, opt = arms[kind]
+        opt.zero_grad(set_to_none=True)
+        m.forward_loss(x, y).backward()
+        opt.step()
+
+    for kind in arms:
+        for _ in range(max(args.warmup, 2)):
+            step(kind)
+    ms = {"plain": [], "dp": []}
+    stops = host = 0.0
+    for _ in range(rounds):
+        for kind in ("plain", "dp"):
+            torch.cuda.synchronize()
+            s0, h0 = tape.STOP_STATS["stops"], tape.STOP_STATS["host_s"]
+            t0 = time.perf_counter()
+            for _ in range(args.steps):
+                step(kind)
+            torch.cuda.synchronize()
+            ms[kind].append((time.perf_counter() - t0) / args.steps * 1e3)
+            if kind == "dp":
+                stops += tape.STOP_STATS["stops"] - s0
+                host += tape.STOP_STATS["host_s"] - h0
+    nb = len(arms["dp"][1]._buckets or [])
+    for core, m, opt in arms.values():
+        engine.release_plans(core)
+    del arms
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()
+    if own:
+        torch.distributed.destroy_process_group()
+    n = rounds * args.steps
+    plain, dp = sorted(ms["plain"])[rounds // 2], sorted(ms["dp"])[rounds // 2]
+    return {"math": math, "buckets": nb, "tape_stops_per_step": round(stops / n, 2),
+            "host_us_per_stop": round(host / max(stops, 1) * 1e6, 1),
+            "host_us_in_stops_per_step": round(host / n * 1e6, 1),
+            "ms_per_step_plain": round(plain, 3), "ms_per_step_dp": round(dp, 3),
+            "overhead_frac": round(dp / plain - 1.0, 4),
+            "rounds_ms": {k: [round(v, 3) for v in vs] for k, vs in ms.items()},
+            "note": f"{rounds} interleaved rounds of {args.steps} steps each arm (medians); world size 1 over RCCL "
+                    "(torch.distributed nccl): DataParallel = bucketed ncclAvg all-reduces launched at tape stops, "
+                    "BN-buffer broadcast, bucket copies to autograd; plain = the same model without it"}
 
 
 MATH_NOTE = {"f32": "fp32 everywhere",

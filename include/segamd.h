@@ -211,6 +211,10 @@ int seg_conv_wino(const float* in, long ldin, int N, int H, int W, int Cin, cons
 int seg_conv_wino_fused(const float* in, long ldin, int N, int H, int W, int Cin, const float* wk, int ldk,
                         const float* bias, float* out, long ldout, int Cout, const float* add, long ldadd, float* stat,
                         hipStream_t stream);
+/* 1 when seg_conv_wino_fused accepts an input of this shape and row stride (its 32-bit buffer offsets cover the
+ * images one block reads); seg_conv_wino_pick assumes ldin = Cin + 64, so a caller with a wider strided view checks
+ * this and takes seg_conv_wino otherwise. */
+int seg_conv_wino_fused_ok(int N, int H, int W, long ldin);
 /* Weight gradient of the same convs by Winograd F(3x3,2x2):
  * dW = G^T [sum_t (A dY_t A^T) .* (B^T X_t B)] G.  seg_conv_wino_wgrad writes
  * fixed-order split-K partial slabs part[splits][16][Cout][Cin] (Cin = the padded

@@ -320,7 +320,8 @@ void mb_plan(int N, int H, int W, int Ch, int stride, int* tiles_w, int* tiles_h
   const int ntiles = N * *tiles_w * *tiles_h;
   const int chunks = (Ch + HC - 1) / HC;
   // hidden splits: up to g_mb_cap blocks in all (co-resident, so every block of a tile helps combine it)
-  int s = std::max(1, std::min(chunks, g_mb_cap / std::max(1, ntiles)));
+  // (at most 32: the width of seg_tile_combine's hand-off mask -- ADVICE r5; MobileNetV2's Ch <= 960 needs <= 30)
+  int s = std::max(1, std::min({chunks, 32, g_mb_cap / std::max(1, ntiles)}));
   const int per = (chunks + s - 1) / s;
   *splits = (chunks + per - 1) / per;
   *hper = per * HC;

@@ -367,6 +367,9 @@ template <int WT>
 __global__ __launch_bounds__(256) void wino_fused_kernel(WinoFusedArgs a) {
   constexpr int WN = 4 / WT, BT = 32 * WT, BC = 32 * WN;
   static_assert(WT == 2 || WT == 4, "a BN row tile (64 tiles) lies in one block");
+  // the BN partials below use 64-tile row tiles; the engine sizes / finalizes them with seg_conv_wino_row_tiles /
+  // seg_conv_wino_tile_rows, which derive from SEG_WINO_OUT_QT (16 * QT tiles) -- the two must agree
+  static_assert(16 * kWinoQT == 64, "wino_fused_kernel's BN row tile is 64 Winograd tiles");
   constexpr int USZ = 16 * BC * kFusedUR;
   constexpr int UPT = 16 * BC * (kFusedKC / 4) / 256;  // U float4 slots per thread per chunk
   __shared__ __attribute__((aligned(16))) float Us[2 * USZ];
@@ -813,6 +816,10 @@ SEG_API int seg_conv_wino_pick(int N, int H, int W, int Cin, int Cout) {
   if (Cin >= 128 && Cout >= 128 && (Cout <= 2 * Cin || Cout >= 512)) return 1;
   const bool fits = fused_fits(N, H, W, Cin + 64);  // buffer-load range (row stride slack)
   return (SEG_WINO_FUSED && fits && Cin >= 64 && (Cout >= 128 || (Cout >= 64 && Cin > 128 && Cin < 256))) ? 2 : 0;
+}
+
+SEG_API int seg_conv_wino_fused_ok(int N, int H, int W, long ldin) {
+  return ((H & 1) || (W & 1) || N <= 0) ? 0 : (int)fused_fits(N, H, W, ldin);
 }
 
 // Number of row tiles of seg_conv_wino's BN partials.

@@ -37,6 +37,7 @@ PROTOTYPES = {
     "seg_conv_wino_tile_rows": (_I, []),
     "seg_conv_wino": (_I, [_V, _L, _I, _I, _I, _I, _V, _I, _V, _V, _L, _I, _V, _L, _V, _V, _V]),
     "seg_conv_wino_fused": (_I, [_V, _L, _I, _I, _I, _I, _V, _I, _V, _V, _L, _I, _V, _L, _V, _V]),
+    "seg_conv_wino_fused_ok": (_I, [_I, _I, _I, _L]),
     "seg_conv_wino_wgrad_pick": (_I, [_I, _I, _I, _I, _I]),
     "seg_conv_wino_wgrad_splits": (_I, [_I, _I, _I, _I, _I]),
     "seg_conv_wino_wgrad": (_I, [_V, _L, _V, _L, _I, _I, _I, _I, _I, _V, _I, _V]),

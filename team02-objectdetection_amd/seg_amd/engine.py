@@ -272,7 +272,7 @@ class ConvOp:
                 name = rt.k("seg_conv_halo") + ("_w16" if self.w16_f else "")
                 rt.tcall("igemm3_fwd", self.flops(), name, rt.ptr(i), i.ld, i.N, i.H, i.W, self.cin_pad,
                          wk_ptr, ldk, bias, rt.ptr(y), y.ld, self.cout, None, 0, statp, s)
-            elif self.wino_ff:
+            elif self.wino_ff and query("seg_conv_wino_fused_ok", i.N, i.H, i.W, i.ld):
                 rt.tcall("wino3_fwd", self.flops(), "seg_conv_wino_fused", rt.ptr(i), i.ld, i.N, i.H, i.W,
                          self.cin_pad, self.wk_wf.data_ptr(), self.cin_pad, bias, rt.ptr(y), y.ld, self.cout, None, 0,
                          statp, s)
@@ -531,7 +531,7 @@ class ConvOp:
                 rt.tcall("igemm3_dgrad", self.flops(), rt.k("seg_conv_halo") + ("_w16" if self.w16_d else ""), dYp,
                          dY.ld, y.N, y.H, y.W, kin,
                             self.wk_d.data_ptr(), self.ldk_d, None, rt.gptr(i), i.ld, self.cin, add_ptr, add_ld, None, s)
-            elif self.wino_fd:
+            elif self.wino_fd and query("seg_conv_wino_fused_ok", y.N, y.H, y.W, dY.ld):
                 rt.tcall("wino3_dgrad", self.flops(), "seg_conv_wino_fused", dYp, dY.ld, y.N, y.H, y.W, kin,
                          self.wk_wd.data_ptr(), kin, None, rt.gptr(i), i.ld, self.cin, add_ptr, add_ld, None, s)
             elif self.wino_d:

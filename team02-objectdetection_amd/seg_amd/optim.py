@@ -23,6 +23,7 @@ class Adam(torch.optim.Adam):
     def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=0, amsgrad=False, **kw):
         super().__init__(params, lr=lr, betas=betas, eps=eps, weight_decay=weight_decay, amsgrad=amsgrad, **kw)
         self._chunk_maps = {}
+        self._last_steps = []  # the CPU step counters the last step() advanced (undo_step_count)
 
     def _chunks(self, sizes, device):
         key = (tuple(sizes), device)
@@ -38,7 +39,8 @@ class Adam(torch.optim.Adam):
         """One Adam step.  skip_if_nonzero: a one-element fp32 device tensor; when it holds a non-zero value at the
         time the step runs on the GPU (stream order), the kernel leaves every parameter and moment unchanged --
         train_one_epoch passes the batch's out-of-range label count here so the step can be queued without a host
-        wait (the CPU step counters still advance; the loop raises right after)."""
+        wait; the CPU step counters advance at queue time, and the loop calls undo_step_count() before it raises, so
+        a skipped step leaves 'step' where the reference's (which never reaches optimizer.step()) leaves it."""
         loss = None
         if skip_if_nonzero is not None and not (skip_if_nonzero.is_cuda and skip_if_nonzero.dtype == torch.float32
                                                 and skip_if_nonzero.numel() >= 1):
@@ -46,6 +48,7 @@ class Adam(torch.optim.Adam):
         if closure is not None:
             with torch.enable_grad():
                 loss = closure()
+        self._last_steps = []
         for group in self.param_groups:
             if group["weight_decay"] != 0 or group["amsgrad"] or group["maximize"] or group.get("capturable") \
                     or group.get("differentiable") or group.get("decoupled_weight_decay"):
@@ -69,6 +72,7 @@ class Adam(torch.optim.Adam):
             sts = [self.state[p] for p in ps]
             steps = [st["step"] for st in sts]
             torch._foreach_add_(steps, 1)  # CPU step counters, as torch's foreach Adam keeps them
+            self._last_steps += steps
             rows = []
             for p, st, t in zip(ps, sts, torch.stack(steps).tolist()):
                 bc1, bc2 = 1 - b1 ** t, 1 - b2 ** t
@@ -81,6 +85,15 @@ class Adam(torch.optim.Adam):
                  eps, skip_if_nonzero.data_ptr() if skip_if_nonzero is not None else None,
                  torch.cuda.current_stream(device).cuda_stream)
         return loss
+
+    def undo_step_count(self):
+        """Take back the step-counter advance of the last step() -- for a step the device skipped
+        (skip_if_nonzero): the bias corrections of the next real step are then the reference's.  The
+        moments need nothing: a skipped step leaves them as they were (zeros for a new parameter, as torch's Adam
+        would create them on its first step)."""
+        if self._last_steps:
+            torch._foreach_sub_(self._last_steps, 1)
+        self._last_steps = []
 
 
 def _pack(rows):

@@ -15,6 +15,7 @@ from __future__ import annotations
 
 import ctypes
 import struct
+import time
 
 import numpy as np
 
@@ -25,6 +26,9 @@ _ENTRY = np.dtype([("kind", "<i4"), ("fn", "<i4"), ("stream", "<i4"), ("pad", "<
 assert _ENTRY.itemsize == 24
 
 _U64 = (1 << 64) - 1
+# host-callback stops replayed (DataParallel bucket launches) and the host time spent in them: bench.py's
+# world-1 RCCL block reads the per-step figures
+STOP_STATS = {"stops": 0, "host_s": 0.0}
 _SIG = {}  # entry point -> (fn index, per-argument kind "p" / "i" / "f")
 
 
@@ -165,7 +169,10 @@ class Tape:
                 raise _lib.SegLibError(f"launch tape entry {stop.value} failed: hipError_t {rc}")
             if stop.value >= self.n:
                 return
+            t0 = time.perf_counter()
             self.callbacks[self._stop_ids[stop.value]]()
+            STOP_STATS["stops"] += 1
+            STOP_STATS["host_s"] += time.perf_counter() - t0
             i = stop.value + 1
 
     # timing (bench.py's roofline): HIP events around the selected launches

@@ -49,15 +49,24 @@ def _check_labels(model, inputs):
     [0, C) (the kernels flag it; the loss and gradients are NaN), BEFORE optimizer.step():
     the path for optimizers that cannot skip their step on the device.  Under
     seg_amd.ddp.DataParallel the count arrived with the last gradient bucket's all-reduce
-    (every rank raises together, no extra collective); in one process it was copied to the
-    host right after the loss kernel, so this waits for the forward only."""
+    (every rank raises together, no extra collective).  When it did not (a no_sync step, or
+    another wrapper under torch.distributed) the counts are summed over the ranks by an
+    all-reduce of their own, so a peer never blocks in the next collective; in one
+    process it was copied to the host right after the loss kernel, so this waits for the
+    forward only."""
     if not inputs.is_cuda:
         return  # the CPU composition's F.cross_entropy raises by itself
-    from .engine import bad_label_count_host, label_flag
+    from .engine import bad_label_count, bad_label_count_host, label_flag
     if hasattr(model, "label_flag"):
         flag = label_flag(model)
         if flag is not None:
             _raise_bad_labels(float(flag.item()))
+            return
+    if torch.distributed.is_available() and torch.distributed.is_initialized():
+        bad = bad_label_count(model)
+        bad = torch.zeros(1, dtype=torch.float32, device=inputs.device) if bad is None else bad
+        torch.distributed.all_reduce(bad)
+        _raise_bad_labels(float(bad.item()))
         return
     n = bad_label_count_host(model)
     _raise_bad_labels(n or 0)
@@ -82,7 +91,9 @@ def _step_and_loss(model, inputs, optimizer, loss):
     host.copy_(flag, non_blocking=True)  # stream-ordered before the step and the loss copy below
     optimizer.step(skip_if_nonzero=flag)
     lv = loss.item()                     # waits for this stream: the flag copy has landed
-    _raise_bad_labels(float(host[0]))
+    if float(host[0]):
+        optimizer.undo_step_count()      # the device skipped the step: its counters go back too
+        _raise_bad_labels(float(host[0]))
     return lv
 
 

@@ -390,10 +390,20 @@ def test_ce_target_out_of_bounds(bad):
             assert torch.equal(v, before[k]), k
     for st in sopt.state.values():
         assert not st["exp_avg"].any() and not st["exp_avg_sq"].any()
-    # and a clean batch after it takes the step
+        assert st["step"].item() == 0  # the skipped step's counter advance is taken back
+    # and a clean batch after it takes the step -- bitwise the step of an optimizer that never saw the bad batch
+    # (the reference never reaches optimizer.step() on it, so its first real step has t = 1)
     t[0, 5, 5] = 3
+    twin = deterministic_init(MobileNetV2UNet(10), seed=1).to(DEV).train()
+    twin.load_state_dict(model.state_dict())
+    fresh = Adam(twin.parameters(), lr=1e-3)
     train_model(model, [(x, t)], nn.CrossEntropyLoss(), sopt, DEV, epochs=1, checkpoint_pattern=None, progress=False)
+    train_model(twin, [(x, t)], nn.CrossEntropyLoss(), fresh, DEV, epochs=1, checkpoint_pattern=None, progress=False)
     assert any(not torch.equal(v, before[k]) for k, v in model.state_dict().items() if k in before)
+    tw = twin.state_dict()
+    for k, v in model.state_dict().items():
+        assert torch.equal(v, tw[k]), k
+    assert all(st["step"].item() == 1 for st in sopt.state.values())
 
 
 def test_colsum_and_add():

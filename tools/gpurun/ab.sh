@@ -17,7 +17,7 @@ for r in $(seq $rounds); do
         *) envs+=("$kv") ;;
       esac
     done
-    env "${envs[@]}" timeout -k 10 200 python bench.py --steps 30 --warmup 5 --no-cpu-baseline --no-bf16io-block --no-infer-block --no-unet-block $bargs > $d/b.json 2> $d/b.err || { echo "$v FAILED"; tail -5 $d/b.err; exit 1; }
+    env "${envs[@]}" timeout -k 10 200 python bench.py --steps 30 --warmup 5 --no-cpu-baseline --no-bf16io-block --no-infer-block --no-unet-block --no-dp1-block $bargs > $d/b.json 2> $d/b.err || { echo "$v FAILED"; tail -5 $d/b.err; exit 1; }
     python -c "import json,sys; d=json.loads(open('$d/b.json').read().strip().splitlines()[-1]); print('$r', '$v', '$bargs', d['value'], d['ms_per_step'])" | tee -a $d/ab.txt
   done
 done

@@ -24,6 +24,14 @@ SHAPES = [  # name, N, H, W, Cin, Cout (3x3, stride 1): forward shapes and data-
     ("up1.0f", 32, 16, 32, 1344, 256), ("up1.0d", 32, 16, 32, 256, 1344), ("up1.3", 32, 16, 32, 256, 256),
     ("up2.0f", 32, 32, 64, 288, 128), ("up2.3", 32, 32, 64, 128, 128),
 ]
+UNET = [  # UNet 10-class 512x1024 bs=8 (BASELINE configs[4]): forward shapes + data-gradient shapes (Cin <-> Cout)
+    ("inc.3", 8, 512, 1024, 64, 64), ("d1.0f", 8, 256, 512, 64, 128), ("d1.0d", 8, 256, 512, 128, 64),
+    ("d1.3", 8, 256, 512, 128, 128), ("d2.0f", 8, 128, 256, 128, 256), ("d2.0d", 8, 128, 256, 256, 128),
+    ("d2.3", 8, 128, 256, 256, 256), ("d3.3", 8, 64, 128, 256, 256), ("u1.0f", 8, 128, 256, 512, 128),
+    ("u1.0d", 8, 128, 256, 128, 512), ("u1.3", 8, 128, 256, 128, 128), ("u2.0f", 8, 256, 512, 256, 64),
+    ("u2.0d", 8, 256, 512, 64, 256), ("u2.3", 8, 256, 512, 64, 64), ("u3.0f", 8, 512, 1024, 128, 64),
+    ("u3.0d", 8, 512, 1024, 64, 128),
+]
 
 
 def timeit(fn, reps):
@@ -42,13 +50,14 @@ def timeit(fn, reps):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--only", default="")
-    ap.add_argument("--kernel", default="both", choices=("ig2", "gen", "both"))
+    ap.add_argument("--kernel", default="both", choices=("ig2", "gen", "both", "halo", "all"))
+    ap.add_argument("--set", default="mnv2", choices=("mnv2", "unet"))
     ap.add_argument("--reps", type=int, default=20)
     a = ap.parse_args()
     only = set(a.only.split(",")) if a.only else None
     s = torch.cuda.current_stream().cuda_stream
     g = torch.Generator().manual_seed(0)
-    for name, N, H, W, Cin, Cout in SHAPES:
+    for name, N, H, W, Cin, Cout in (UNET if a.set == "unet" else SHAPES):
         if only and name not in only:
             continue
         M, ks = N * H * W, 3
@@ -62,12 +71,16 @@ def main():
         plan = engine.igemm2_plan(M, Cout, Cin, ks)
         flops = 2.0 * M * Cout * Cin * 9
         res = []
-        if plan and a.kernel in ("ig2", "both"):
+        if plan and a.kernel in ("ig2", "both", "all"):
             work = torch.zeros(max(plan[3], 1), device="cuda")
             t = timeit(lambda: call("seg_conv_igemm2_bf16io", x.data_ptr(), Cin, N, H, W, Cin, wk.data_ptr(), ldk, None,
                                     y.data_ptr(), Cout, Cout, ks, None, 0, None, work.data_ptr(), s), a.reps)
             res.append(f"ig2 {t * 1e6:7.1f} us {flops / t / 1e12:6.0f} TF/s (tile rows {plan[0]}, splits {plan[2]})")
-        if a.kernel in ("gen", "both"):
+        if a.kernel in ("halo", "all") and call("seg_conv_halo_pick", N, H, W, Cin, Cout):
+            t = timeit(lambda: call("seg_conv_halo_bf16io_w16", x.data_ptr(), Cin, N, H, W, Cin, wk.data_ptr(), ldk,
+                                    None, y.data_ptr(), Cout, Cout, None, 0, None, s), a.reps)
+            res.append(f"halo {t * 1e6:7.1f} us {flops / t / 1e12:6.0f} TF/s")
+        if a.kernel in ("gen", "both", "all"):
             t = timeit(lambda: call("seg_conv_igemm_bf16io_w16", x.data_ptr(), Cin, N, H, W, Cin, wk.data_ptr(), ldk,
                                     None, y.data_ptr(), Cout, H, W, Cout, 3, 1, 1, None, 0, None, s), a.reps)
             res.append(f"gen {t * 1e6:7.1f} us {flops / t / 1e12:6.0f} TF/s")

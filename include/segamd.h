@@ -116,6 +116,16 @@ int seg_conv_igemm_f16_ic(const float* in, long ldin, int N, int H, int W, int C
                           const float* bias, float* out, long ldout, int Ho, int Wo, int Cout, int ks, int stride,
                           int pad, const float* add, long ldadd, int act, float* work, int splits, int tile, unsigned* cnt,
                           hipStream_t stream);
+/* seg_conv_igemm_f16_ic of a decoder conv0 whose input is torch.cat([skip, Upsample(x2, bilinear,
+ * align_corners=False)(low)], 1) (src/unet.py:97-104, inference.py's eval forward) with the upsample formed on
+ * load: `in` holds the skip in channels [0, ucs) of its Cin-wide rows; channels [ucs, Cin)
+ * are interpolated per operand slot from `up` [N][H/2][W/2][ldup] (seg_upsample_fwd's index arithmetic and
+ * blend, bitwise its output), so the upsample launch and its rows disappear.  3x3, stride 1, pad 1; H, W even;
+ * ucs % 4 == 0. */
+int seg_conv_igemm_f16_ic_up(const float* in, long ldin, int N, int H, int W, int Cin, const float* up, long ldup,
+                             int ucs, const float* wk, int ldk, const float* bias, float* out, long ldout, int Cout,
+                             const float* add, long ldadd, int act, float* work, int splits, int tile, unsigned* cnt,
+                             hipStream_t stream);
 
 /* seg_conv_igemm as a stride-1 data gradient (pad ks/2, no bias, optional fused addend) that
  * completes dA of a BatchNorm layer whose pre-BN output is `by`: the epilogue also writes that
@@ -566,6 +576,9 @@ int seg_conv_igemm2_bf16io(const seg_bf16* in, long ldin, int N, int H, int W, i
 /* Round 4: the plan also picks 4-wave 128x128 / 128x64 / 64x128 / 64x64 tiles (small-image 1x1 and 3x3
  * convs of the MobileNetV2 encoder); seg_igemm2_force_tile(t) forces table entry t (-1 = the plan). */
 int seg_igemm2_force_tile(int t);
+/* A/B hook: seg_conv_halo* on the weight-resident persistent kernel where the packed weights fit its LDS (1, the
+ * default) or on the per-tile kernel only (0); < 0 leaves it.  Returns the previous setting.  Bitwise the same. */
+int seg_halo_wr(int on);
 /* Tuning hook: split-K of the 4-wave tiles up to target_blocks blocks with >= min_steps 64-deep K
  * steps per slice (defaults 512, 3); values <= 0 keep the current setting. */
 int seg_igemm2_tune(int target_blocks, int min_steps);

@@ -264,6 +264,21 @@ __device__ __forceinline__ f32x4 bilerp4(f32x4 v00, f32x4 v01, f32x4 v10, f32x4 
   return lh.l0 * (lw.l0 * v00 + lw.l1 * v01) + lh.l1 * (lw.l0 * v10 + lw.l1 * v11);
 }
 
+// The x2 upsample's blend (nn.Upsample bilinear, align_corners=False: seg_upsample_fwd) with one fixed fma
+// association -- no contraction left to the compiler -- so a kernel that forms the upsample on load (the folded
+// decoder conv, seg_conv_igemm_f16_ic_up) rounds bit for bit as the upsample kernel does.
+__device__ __forceinline__ f32x4 up_blend4(f32x4 v00, f32x4 v01, f32x4 v10, f32x4 v11, float h0, float h1, float w0,
+                                           float w1) {
+  f32x4 o;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const float t = __builtin_fmaf(w1, v01[j], w0 * v00[j]);
+    const float b = __builtin_fmaf(w1, v11[j], w0 * v10[j]);
+    o[j] = __builtin_fmaf(h1, b, h0 * t);
+  }
+  return o;
+}
+
 #define SEG_RET_LAST() return (int)hipGetLastError()
 
 // Compute units of the current device (256 on MI355X; also the answer without a device, so

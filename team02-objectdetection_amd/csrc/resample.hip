@@ -53,7 +53,7 @@ __global__ void up_fwd_nhwc_kernel(const T* __restrict__ in, long ldin, int N, i
     const f32x4 v01 = ld4(base + ((long)lh.i0 * W + lw.i1) * ldin + c);
     const f32x4 v10 = ld4(base + ((long)lh.i1 * W + lw.i0) * ldin + c);
     const f32x4 v11 = ld4(base + ((long)lh.i1 * W + lw.i1) * ldin + c);
-    const f32x4 o = lh.l0 * (lw.l0 * v00 + lw.l1 * v01) + lh.l1 * (lw.l0 * v10 + lw.l1 * v11);
+    const f32x4 o = up_blend4(v00, v01, v10, v11, lh.l0, lh.l1, lw.l0, lw.l1);  // (the fold's blend, common.h)
     st4(out + p * ldout + c, o);
   }
 }

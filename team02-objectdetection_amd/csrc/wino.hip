@@ -586,6 +586,228 @@ __global__ __launch_bounds__(256) void wino_fused_kernel(WinoFusedArgs a) {
   }
 }
 
+#ifdef SEG_WF2_TEST
+// TEST-ONLY (never in the product library): round 5's two-waves-per-SIMD fused form, restored from commit 152956a to
+// find the cause of its UNet-slice parity failure (tools/wf2diag.py).  Built into a variant by
+// tools/variant.py wf2 -DSEG_WF2_TEST=1; seg_wf2_mask selects which seg_conv_wino_fused calls take it.
+// Two waves per SIMD instead of one: a wave owns 16 tiles x 32 channels for all 16 xi on v_mfma_f32_16x16x4_f32
+// (16 xi x 2 column halves x f32x4 = 128 accumulator registers; ~200 registers in all), so a second block shares
+// every SIMD and covers the patch loads' latency that the one-wave form exposes (its timing experiments: loads =
+// 37 % of the launch).  K chunk = 8 input channels: lane group g = lane >> 4 holds channels 2g, 2g + 1 (float2 per
+// patch pixel) and K step s uses channel 2g + s on both operands.  Block = 64 tiles (one BN row tile) x 32 channels.
+constexpr int kF2KC = 8, kF2UR = 10;  // channels per chunk; LDS pitch (floats) of a (xi, co) row of U
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ f32x2 seg_bld2(__amdgpu_buffer_rsrc_t r, unsigned off) {
+  typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+  return __builtin_bit_cast(f32x2, __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 0));
+}
+
+__global__ __launch_bounds__(256, 2) void wino_fused2_kernel(WinoFusedArgs a) {
+  constexpr int BT = 64, BC = 32;
+  constexpr int USZ = 16 * BC * kF2UR;
+  constexpr int UPT = 16 * BC * (kF2KC / 4) / 256;  // U float4 slots per thread per chunk (4)
+  __shared__ __attribute__((aligned(16))) float Us[2 * USZ];
+  __shared__ float red[4][32];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int i16 = lane & 15, g = lane >> 4;
+  const int tiles_n = (a.Cout + BC - 1) / BC;
+  const int lid = xcd_swizzle(blockIdx.x, gridDim.x);
+  const int tn = lid % tiles_n, tm = lid / tiles_n;
+  const int m0 = tm * BT, n0 = tn * BC;
+  const int nfirst = m0 / (a.th * a.tw);
+  const long boff = (long)nfirst * a.H * a.W * a.ldin;
+  const __amdgpu_buffer_rsrc_t rin = seg_rsrc(a.in + boff, (unsigned)min((a.in_elems - boff) * 4, (long)kFusedOOB - 16));
+  const __amdgpu_buffer_rsrc_t rwk = seg_rsrc(a.wk, a.wk_bytes);
+
+  // this lane's tile (A row i16 of the wave's 16) and its patch
+  const int t = m0 + wave * 16 + i16;
+  const bool tok = t < a.T;
+  unsigned pm = 0, pbase = 0;
+  int opix = 0;
+  {
+    const int tt = tok ? t : 0;
+    const int n = tt / (a.th * a.tw), r = tt - n * a.th * a.tw;
+    const int ty = r / a.tw, tx = r - ty * a.tw;
+    const int h0 = 2 * ty - 1, w0 = 2 * tx - 1;
+#pragma unroll
+    for (int p = 0; p < 4; ++p)
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        if (tok && (unsigned)(h0 + p) < (unsigned)a.H && (unsigned)(w0 + q) < (unsigned)a.W) pm |= 1u << (p * 4 + q);
+    pbase = (unsigned)((((long)(n - nfirst) * a.H + h0) * a.W + w0) * a.ldin * 4) + 8u * g;
+    opix = (n * a.H + 2 * ty) * a.W + 2 * tx;
+  }
+  const unsigned rstep = (unsigned)(a.W * a.ldin * 4), cstep = (unsigned)(a.ldin * 4);
+
+  auto load_patch = [&](int c0, f32x2 (&d)[16]) {
+    const bool cok = c0 + 2 * g < a.Cin;  // Cin % 4 == 0: both channels or neither
+    const unsigned b = pbase + 4u * c0;
+#pragma unroll
+    for (int p = 0; p < 4; ++p)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const bool ok = cok && ((pm >> (p * 4 + q)) & 1u);
+        d[p * 4 + q] = seg_bld2(rin, ok ? b + p * rstep + q * cstep : kFusedOOB);
+      }
+  };
+  auto load_u = [&](int c0, f32x4 (&u)[UPT]) {
+#pragma unroll
+    for (int i = 0; i < UPT; ++i) {
+      const int idx = tid + i * 256;
+      const int xi = idx / (2 * BC), rem = idx - xi * (2 * BC);
+      const int co = n0 + (rem >> 1), c = c0 + 4 * (rem & 1);
+      const bool ok = co < a.Cout && c < a.Cin;
+      u[i] = seg_bld4(rwk, ok ? (unsigned)((((long)xi * a.Cout + co) * a.ldk + c) * 4) : kFusedOOB);
+    }
+  };
+  auto store_u = [&](float* dst, const f32x4 (&u)[UPT]) {
+#pragma unroll
+    for (int i = 0; i < UPT; ++i) {
+      const int idx = tid + i * 256;
+      const int xi = idx / (2 * BC), rem = idx - xi * (2 * BC);
+      float* q = dst + (xi * BC + (rem >> 1)) * kF2UR + 4 * (rem & 1);
+      *reinterpret_cast<f32x2*>(q) = f32x2{u[i][0], u[i][1]};
+      *reinterpret_cast<f32x2*>(q + 2) = f32x2{u[i][2], u[i][3]};
+    }
+  };
+  auto transform = [](f32x2 (&d)[16]) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const f32x2 d0 = d[q], d1 = d[4 + q], d2 = d[8 + q], d3 = d[12 + q];
+      d[q] = d0 - d2;
+      d[4 + q] = d1 + d2;
+      d[8 + q] = d2 - d1;
+      d[12 + q] = d1 - d3;
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const f32x2 t0 = d[4 * r], t1 = d[4 * r + 1], t2 = d[4 * r + 2], t3 = d[4 * r + 3];
+      d[4 * r] = t0 - t2;
+      d[4 * r + 1] = t1 + t2;
+      d[4 * r + 2] = t2 - t1;
+      d[4 * r + 3] = t1 - t3;
+    }
+  };
+
+  f32x4 acc[16][2];
+#pragma unroll
+  for (int x = 0; x < 16; ++x) acc[x][0] = acc[x][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int nk = (a.Cin + kF2KC - 1) / kF2KC;
+  f32x4 ug[UPT];
+  load_u(0, ug);
+  store_u(Us, ug);
+  __syncthreads();
+  const int urow = i16 * kF2UR + 2 * g;
+  for (int kc = 0; kc < nk; ++kc) {
+    const bool more = kc + 1 < nk;
+    f32x2 d[16];
+    load_patch(kc * kF2KC, d);
+    if (more) load_u((kc + 1) * kF2KC, ug);
+    transform(d);
+    const float* ub = Us + (kc & 1) * USZ + urow;
+#pragma unroll
+    for (int x = 0; x < 16; ++x) {
+      const f32x2 u0 = *reinterpret_cast<const f32x2*>(ub + (x * BC) * kF2UR);
+      const f32x2 u1 = *reinterpret_cast<const f32x2*>(ub + (x * BC + 16) * kF2UR);
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+        acc[x][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(d[x][s2], u0[s2], acc[x][0], 0, 0, 0);
+        acc[x][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(d[x][s2], u1[s2], acc[x][1], 0, 0, 0);
+      }
+    }
+    if (more) store_u(Us + ((kc + 1) & 1) * USZ, ug);
+    __syncthreads();
+  }
+
+  // epilogue: acc[xi][half][r] = M_xi of tile (wave's row 4g + r), channel n0 + 16 half + (lane & 15)
+  auto tile_y = [&](int hf, int r, float (&y)[4]) {
+    float q[16];
+#pragma unroll
+    for (int x = 0; x < 16; ++x) q[x] = acc[x][hf][r];
+    float r0[4], r1[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      r0[j] = q[j] + q[4 + j] + q[8 + j];
+      r1[j] = q[4 + j] - q[8 + j] - q[12 + j];
+    }
+    y[0] = r0[0] + r0[1] + r0[2];
+    y[1] = r0[1] - r0[2] - r0[3];
+    y[2] = r1[0] + r1[1] + r1[2];
+    y[3] = r1[1] - r1[2] - r1[3];
+  };
+  long p0s[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) p0s[r] = __shfl(opix, 4 * g + r, 64);  // all lanes active (bpermute)
+  const int wbase = m0 + wave * 16 + 4 * g;
+  float ssum[2] = {0.f, 0.f};
+#pragma unroll
+  for (int hf = 0; hf < 2; ++hf) {
+    const int col = n0 + 16 * hf + i16;
+    if (col >= a.Cout) continue;
+    const float b = a.bias ? a.bias[col] : 0.f;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      if (wbase + r >= a.T) continue;
+      float y[4];
+      tile_y(hf, r, y);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const long pix = p0s[r] + (u >> 1) * a.W + (u & 1);
+        float v = y[u] + b;
+        if (a.add) v += a.add[pix * a.ldadd + col];
+        a.out[pix * a.ldout + col] = v;
+        ssum[hf] += v;
+      }
+    }
+  }
+  if (!a.stat) return;
+  // BN partials of the block's 64-tile row tile: lanes of one column (4 lane groups), then the 4 waves
+  const int rtile = m0 / 64, ntile = min(64, a.T - m0);
+  float mean[2] = {0.f, 0.f};
+#pragma unroll
+  for (int pass = 0; pass < 2; ++pass) {
+#pragma unroll
+    for (int hf = 0; hf < 2; ++hf) {
+      const int col = n0 + 16 * hf + i16;
+      float sv = ssum[hf];
+      if (pass) {
+        sv = 0.f;
+        if (col < a.Cout) {
+          const float b = a.bias ? a.bias[col] : 0.f;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            if (wbase + r >= a.T) continue;
+            float y[4];
+            tile_y(hf, r, y);
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+              float v = y[u] + b;
+              if (a.add) v += a.add[(p0s[r] + (u >> 1) * a.W + (u & 1)) * a.ldadd + col];
+              const float dv = v - mean[hf];
+              sv += dv * dv;
+            }
+          }
+        }
+      }
+      sv += __shfl_xor(sv, 16, 64);
+      sv += __shfl_xor(sv, 32, 64);
+      if (g == 0) red[wave][16 * hf + i16] = sv;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int hf = 0; hf < 2; ++hf) {
+      const int c = 16 * hf + i16, col = n0 + c;
+      const float tot = ((red[0][c] + red[1][c]) + red[2][c]) + red[3][c];
+      if (pass == 0) mean[hf] = ntile > 0 ? tot / (4.f * (float)ntile) : 0.f;
+      if (wave == 0 && g == 0 && col < a.Cout && ntile > 0) a.stat[((long)rtile * 2 + pass) * a.Cout + col] = tot;
+    }
+    __syncthreads();
+  }
+}
+
+#endif  // SEG_WF2_TEST
+
 // ---------------------------------------------------------------- weight gradient
 // dW = G^T [ sum_t (A dY_t A^T) .* (B^T X_t B) ] G  per (co, ci): Winograd F(3x3, 2x2)
 // (the transposition of F(2x2,3x3); A = [1 0; 1 1; 1 -1; 0 -1]).  Per xi a GEMM
@@ -860,6 +1082,9 @@ SEG_API int seg_conv_wino(const float* in, long ldin, int N, int H, int W, int C
 
 // seg_conv_wino's result (bitwise up to the association of the input transform's adds) from one launch with no M
 // workspace: wino_fused_kernel.  Same arguments as seg_conv_wino without `work`.
+#ifdef SEG_WF2_TEST
+static int g_wf2_mask = 3;
+#endif
 SEG_API int seg_conv_wino_fused(const float* in, long ldin, int N, int H, int W, int Cin, const float* wk, int ldk,
                                 const float* bias, float* out, long ldout, int Cout, const float* add, long ldadd,
                                 float* stat, hipStream_t stream) {
@@ -876,9 +1101,22 @@ SEG_API int seg_conv_wino_fused(const float* in, long ldin, int N, int H, int W,
   if (!fused_fits(N, H, W, ldin) || wk_bytes >= (long)kFusedOOB) return (int)hipErrorInvalidValue;
   a.in_elems = ((long)N * H * W - 1) * ldin + Cin;
   a.wk_bytes = (unsigned)wk_bytes;
+#ifdef SEG_WF2_TEST
+  // bit 0: calls with a bias or BN partials (the forward), bit 1: the others (data gradients)
+  if ((g_wf2_mask >> ((bias || stat) ? 0 : 1)) & 1) {
+    hipLaunchKernelGGL(wino_fused2_kernel, dim3(seg_cdiv(a.T, 64) * seg_cdiv(Cout, 32)), dim3(256), 0, stream, a);
+    SEG_RET_LAST();
+  }
+#endif
   hipLaunchKernelGGL(wino_fused_kernel<4>, dim3(seg_cdiv(a.T, 128) * seg_cdiv(Cout, 32)), dim3(256), 0, stream, a);
   SEG_RET_LAST();
 }
+#ifdef SEG_WF2_TEST
+SEG_API int seg_wf2_mask(int m) {
+  g_wf2_mask = m;
+  return 0;
+}
+#endif
 
 // Use the Winograd weight gradient?  Measured on MI355X (tools/winobench.py):
 // 1.19-1.33x for Cin, Cout >= 128 at 65536+ tiles (UNet 512x1024) and for

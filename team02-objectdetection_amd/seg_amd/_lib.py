@@ -38,6 +38,7 @@ PROTOTYPES = {
     "seg_conv_wino": (_I, [_V, _L, _I, _I, _I, _I, _V, _I, _V, _V, _L, _I, _V, _L, _V, _V, _V]),
     "seg_conv_wino_fused": (_I, [_V, _L, _I, _I, _I, _I, _V, _I, _V, _V, _L, _I, _V, _L, _V, _V]),
     "seg_conv_wino_fused_ok": (_I, [_I, _I, _I, _L]),
+    "seg_halo_wr": (_I, [_I]),
     "seg_conv_wino_wgrad_pick": (_I, [_I, _I, _I, _I, _I]),
     "seg_conv_wino_wgrad_splits": (_I, [_I, _I, _I, _I, _I]),
     "seg_conv_wino_wgrad": (_I, [_V, _L, _V, _L, _I, _I, _I, _I, _I, _V, _I, _V]),
@@ -132,6 +133,8 @@ PROTOTYPES["seg_bn_bwd_coef_bf16io"] = PROTOTYPES["seg_bn_bwd_coef"]
 PROTOTYPES["seg_conv_igemm_bnout_bf16io"] = PROTOTYPES["seg_conv_igemm_bnout"]
 PROTOTYPES["seg_conv_igemm_bf16_ic"] = PROTOTYPES["seg_conv_igemm_act_ic"]
 PROTOTYPES["seg_conv_igemm_f16_ic"] = PROTOTYPES["seg_conv_igemm_act_ic"]
+PROTOTYPES["seg_conv_igemm_f16_ic_up"] = (_I, [_V, _L, _I, _I, _I, _I, _V, _L, _I, _V, _I, _V, _V, _L, _I, _V, _L, _I,
+                                             _V, _I, _I, _V, _V])
 PROTOTYPES["seg_conv_igemm_bnout_bf16io_w16"] = PROTOTYPES["seg_conv_igemm_bnout"]
 PROTOTYPES["seg_bn_bwd_apply_bf16io"] = PROTOTYPES["seg_bn_bwd_apply"]
 PROTOTYPES["seg_conv_wgrad_bf16io"] = PROTOTYPES["seg_conv_wgrad"]

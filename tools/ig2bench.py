@@ -23,6 +23,7 @@ BF = torch.bfloat16
 SHAPES = [  # name, N, H, W, Cin, Cout (3x3, stride 1): forward shapes and data-gradient shapes
     ("up1.0f", 32, 16, 32, 1344, 256), ("up1.0d", 32, 16, 32, 256, 1344), ("up1.3", 32, 16, 32, 256, 256),
     ("up2.0f", 32, 32, 64, 288, 128), ("up2.3", 32, 32, 64, 128, 128),
+    ("up3.3", 32, 64, 128, 64, 64), ("up4.0f", 32, 128, 256, 80, 32), ("up4.3", 32, 128, 256, 32, 32),
 ]
 UNET = [  # UNet 10-class 512x1024 bs=8 (BASELINE configs[4]): forward shapes + data-gradient shapes (Cin <-> Cout)
     ("inc.3", 8, 512, 1024, 64, 64), ("d1.0f", 8, 256, 512, 64, 128), ("d1.0d", 8, 256, 512, 128, 64),
@@ -77,9 +78,12 @@ def main():
                                     y.data_ptr(), Cout, Cout, ks, None, 0, None, work.data_ptr(), s), a.reps)
             res.append(f"ig2 {t * 1e6:7.1f} us {flops / t / 1e12:6.0f} TF/s (tile rows {plan[0]}, splits {plan[2]})")
         if a.kernel in ("halo", "all") and call("seg_conv_halo_pick", N, H, W, Cin, Cout):
-            t = timeit(lambda: call("seg_conv_halo_bf16io_w16", x.data_ptr(), Cin, N, H, W, Cin, wk.data_ptr(), ldk,
-                                    None, y.data_ptr(), Cout, Cout, None, 0, None, s), a.reps)
-            res.append(f"halo {t * 1e6:7.1f} us {flops / t / 1e12:6.0f} TF/s")
+            for wr in (0, 1):  # per-tile kernel, weight-resident persistent kernel (seg_halo_wr)
+                call("seg_halo_wr", wr)
+                t = timeit(lambda: call("seg_conv_halo_bf16io_w16", x.data_ptr(), Cin, N, H, W, Cin, wk.data_ptr(),
+                                        ldk, None, y.data_ptr(), Cout, Cout, None, 0, None, s), a.reps)
+                res.append(f"halo{'_wr' if wr else ''} {t * 1e6:7.1f} us {flops / t / 1e12:6.0f} TF/s")
+            call("seg_halo_wr", 1)
         if a.kernel in ("gen", "both", "all"):
             t = timeit(lambda: call("seg_conv_igemm_bf16io_w16", x.data_ptr(), Cin, N, H, W, Cin, wk.data_ptr(), ldk,
                                     None, y.data_ptr(), Cout, H, W, Cout, 3, 1, 1, None, 0, None, s), a.reps)

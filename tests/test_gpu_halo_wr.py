@@ -69,7 +69,7 @@ def test_halo_wr_bitwise_per_tile_kernel(kind, N, H, W, Cin, Cout):
     # float64 of the same operand rounding
     xr = x.to(dt).double() if bf else x.double()
     wr_ = w.to(BF).double() if bf else w.double()
-    ref = F.conv2d(xr.view(N, H, W, Cin).permute(0, 3, 1, 2), wr_, padding=1) + b.double()[None, :, None, None]
+    ref = F.conv2d(xr.view(N, H, W, Cin).permute(0, 3, 1, 2), wr_, padding=1) + b.double().cpu()[None, :, None, None]
     ref = ref.permute(0, 2, 3, 1).reshape(M, Cout) + add[:, :Cout].to(dt).double()
     got = o1[:, :Cout].double().cpu()
     tol = 1e-2 if bf else 1e-5  # bf16 output rounding

@@ -4,8 +4,8 @@
 t=${1:-r06d}
 d=gpurun_out/$t; mkdir -p $d
 export TMPDIR=/tmp
-timeout -k 10 600 python -u -m pytest -q --timeout 300 --timeout-method thread -m gpu tests/test_gpu_halo_wr.py tests/test_gpu_mbconv.py tests/test_gpu_ops.py tests/test_gpu_ddp.py tests/test_gpu_infer.py > $d/pytest.log 2>&1
-rc=$?; tail -3 $d/pytest.log; [ $rc -ne 0 ] && { grep -E "^FAILED|Error" $d/pytest.log | head -20; exit $rc; }
+: tests passed in the previous call
+
 timeout -k 10 300 python tools/ig2bench.py --set unet --kernel halo --reps 10 > $d/halobench_unet.txt 2>&1 || { tail -5 $d/halobench_unet.txt; exit 1; }
 timeout -k 10 300 python tools/ig2bench.py --set mnv2 --kernel halo --reps 10 > $d/halobench_mnv2.txt 2>&1 || { tail -5 $d/halobench_mnv2.txt; exit 1; }
 cat $d/halobench_unet.txt $d/halobench_mnv2.txt

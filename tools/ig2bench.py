@@ -77,13 +77,13 @@ def main():
             t = timeit(lambda: call("seg_conv_igemm2_bf16io", x.data_ptr(), Cin, N, H, W, Cin, wk.data_ptr(), ldk, None,
                                     y.data_ptr(), Cout, Cout, ks, None, 0, None, work.data_ptr(), s), a.reps)
             res.append(f"ig2 {t * 1e6:7.1f} us {flops / t / 1e12:6.0f} TF/s (tile rows {plan[0]}, splits {plan[2]})")
-        if a.kernel in ("halo", "all") and call("seg_conv_halo_pick", N, H, W, Cin, Cout):
+        if a.kernel in ("halo", "all") and engine.query("seg_conv_halo_pick", N, H, W, Cin, Cout):
             for wr in (0, 1):  # per-tile kernel, weight-resident persistent kernel (seg_halo_wr)
-                call("seg_halo_wr", wr)
+                engine.query("seg_halo_wr", wr)
                 t = timeit(lambda: call("seg_conv_halo_bf16io_w16", x.data_ptr(), Cin, N, H, W, Cin, wk.data_ptr(),
                                         ldk, None, y.data_ptr(), Cout, Cout, None, 0, None, s), a.reps)
                 res.append(f"halo{'_wr' if wr else ''} {t * 1e6:7.1f} us {flops / t / 1e12:6.0f} TF/s")
-            call("seg_halo_wr", 1)
+            engine.query("seg_halo_wr", 1)
         if a.kernel in ("gen", "both", "all"):
             t = timeit(lambda: call("seg_conv_igemm_bf16io_w16", x.data_ptr(), Cin, N, H, W, Cin, wk.data_ptr(), ldk,
                                     None, y.data_ptr(), Cout, H, W, Cout, 3, 1, 1, None, 0, None, s), a.reps)

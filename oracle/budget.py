@@ -35,13 +35,13 @@ def _cast(state, dtype):
     return {k: (v.to(dtype) if v.is_floating_point() else v.clone()) for k, v in state.items()}
 
 
-def _grads(arch, state, x, y, dtype, masks=None):
+def _grads(arch, state, x, y, dtype, masks=None, pools=None):
     p = _cast(state, dtype)
-    segref.MASK_OVERRIDE = masks
+    segref.MASK_OVERRIDE, segref.POOL_OVERRIDE = masks, pools
     try:
         loss, _, g = segref.forward_backward(arch, p, x.to(dtype), y, True)
     finally:
-        segref.MASK_OVERRIDE = None
+        segref.MASK_OVERRIDE = segref.POOL_OVERRIDE = None
     return loss, g
 
 
@@ -59,9 +59,12 @@ def oracle_side(arch, state, x, y):
     return {"z64": z64, "hi": hi, "m64": m64, "loss64": loss64, "g64": g64, "eps": eps, "zerr": zerr}
 
 
-def check_hip(arch, state, x, y, hip_grads, hip_z, side=None):
+def check_hip(arch, state, x, y, hip_grads, hip_z, side=None, hip_pools=None):
     """hip_z: {layer prefix: z (NCHW, any float dtype)} of the HIP forward; hip_grads:
-    {name: grad}.  Returns a report dict; report["ok"] is the verdict."""
+    {name: grad}.  hip_pools (optional, UNet): {pool name: 2x2-window positions the HIP forward's max-pools chose}
+    (engine.debug_pool_positions) -- the fp64 oracle then also routes its max-pool gradients through the HIP path's
+    choices, as it takes its ReLU masks (round 6: a near-tie in a window is the same kind of discontinuity; VERDICT r5
+    item 5).  Returns a report dict; report["ok"] is the verdict."""
     side = side or oracle_side(arch, state, x, y)
     z64, hi, m64 = side["z64"], side["hi"], side["m64"]
     missing = sorted(set(z64) - set(hip_z))
@@ -76,7 +79,14 @@ def check_hip(arch, state, x, y, hip_grads, hip_z, side=None):
             zbad.append((k, err, side["zerr"][k]))
         masks[k] = segref.act_mask(zh, hi[k])
         flips[k] = int((masks[k] != m64[k]).sum())
-    _, g64m = _grads(arch, state, x, y, torch.float64, masks)
+    pool_flips = {}
+    if hip_pools:
+        z64a = {k: segref.act_mask(z, None) * z for k, z in z64.items()}  # ReLU of the pool inputs (UNet: ReLU)
+        src = {"down1.": "inc.conv.conv.3.", "down2.": "down1.mpconv.1.conv.3.", "down3.": "down2.mpconv.1.conv.3."}
+        for k, pos in hip_pools.items():
+            if src.get(k) in z64a:
+                pool_flips[k] = int((segref.pool_positions(z64a[src[k]]) != pos).sum())
+    _, g64m = _grads(arch, state, x, y, torch.float64, masks, hip_pools)
     g64 = side["g64"]
     gnorm = float(torch.sqrt(sum((g ** 2).sum() for g in g64.values())))
     worst, wname, bad, ratios = 0.0, None, [], {}
@@ -94,4 +104,5 @@ def check_hip(arch, state, x, y, hip_grads, hip_z, side=None):
     return {"ok": not bad and not zbad and not missing, "worst": worst, "worst_name": wname, "bad": bad,
             "z_bad": zbad, "missing_layers": missing, "z_worst": max(zrep.values()) if zrep else 0.0,
             "flips": {k: v for k, v in flips.items() if v}, "n_flips": sum(flips.values()),
+            "pool_flips": pool_flips,
             "worst_vs_unmatched_fp64": d_unmatched, "ratios": ratios, "loss64": float(side["loss64"])}

@@ -65,6 +65,44 @@ class _ActMasked(torch.autograd.Function):
         return g * mask.to(g.dtype), None, None
 
 
+# Max-pool window choices (tests only).  MaxPool2d's gradient is discontinuous in its input the same way: two
+# elements of a 2x2 window within rounding distance of each other swap the window's argmax between two valid fp32
+# implementations, and the whole window's gradient moves to the other element.  POOL_OVERRIDE = {pool name: window
+# positions [N, C, H/2, W/2] (0..3, row-major in the window)} routes the backward through the given positions (the
+# forward values are unchanged), so the oracle can be run with another implementation's choices (oracle/budget.py).
+POOL_OVERRIDE = None
+
+
+class _PoolChosen(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, pos):
+        ctx.save_for_backward(pos)
+        ctx.shape = x.shape
+        return F.max_pool2d(x, 2)
+
+    @staticmethod
+    def backward(ctx, g):
+        (pos,) = ctx.saved_tensors
+        N, C, H, W = ctx.shape
+        gx = torch.zeros(N, C, H // 2, W // 2, 4, dtype=g.dtype)
+        gx.scatter_(4, pos.unsqueeze(-1), g.unsqueeze(-1))
+        gx = gx.view(N, C, H // 2, W // 2, 2, 2).permute(0, 1, 2, 4, 3, 5).reshape(N, C, H, W)
+        return gx, None
+
+
+def pool_positions(a):
+    """First-max position (0..3, row-major) of every 2x2 window of a [N, C, H, W] (aten's / the kernel's tie rule)."""
+    N, C, H, W = a.shape
+    w = a.reshape(N, C, H // 2, 2, W // 2, 2).permute(0, 1, 2, 4, 3, 5).reshape(N, C, H // 2, W // 2, 4)
+    return w.argmax(-1)
+
+
+def _pool(name, x):
+    if POOL_OVERRIDE is not None and name in POOL_OVERRIDE:
+        return _PoolChosen.apply(x, POOL_OVERRIDE[name])
+    return F.max_pool2d(x, 2)
+
+
 def act_mask(z, hi):
     """aten's gradient mask: hardtanh_backward passes 0 < z < 6 (strict), threshold_backward z > 0."""
     return (z > 0) & (z < hi) if hi is not None else z > 0
@@ -168,9 +206,9 @@ def mobilenet_unet_forward(p, x, training):
 
 def unet_forward(p, x, training):
     x1 = double_conv(p, "inc.conv.", x, training)
-    x2 = double_conv(p, "down1.mpconv.1.", F.max_pool2d(x1, 2), training)
-    x3 = double_conv(p, "down2.mpconv.1.", F.max_pool2d(x2, 2), training)
-    x4 = double_conv(p, "down3.mpconv.1.", F.max_pool2d(x3, 2), training)
+    x2 = double_conv(p, "down1.mpconv.1.", _pool("down1.", x1), training)
+    x3 = double_conv(p, "down2.mpconv.1.", _pool("down2.", x2), training)
+    x4 = double_conv(p, "down3.mpconv.1.", _pool("down3.", x3), training)
     y = up(p, "up1.", x4, x3, training)
     y = up(p, "up2.", y, x2, training)
     y = up(p, "up3.", y, x1, training)

@@ -502,11 +502,11 @@ __global__ __launch_bounds__(256) void halo3x3_wr_kernel(HaloArgs a, int ldw, in
 }  // namespace
 
 #ifndef SEG_HALO_WR
-#define SEG_HALO_WR 1
+#define SEG_HALO_WR 0  // measured slower (profiles/r06/halobench_*.txt): off unless asked for
 #endif
 int g_halo_wr = SEG_HALO_WR;  // the weight-resident form (seg_halo_wr: A/B hook)
 
-// A/B hook: 1 = the weight-resident persistent form where it applies (default), 0 = halo3x3_kernel only.
+// A/B hook: 1 = the weight-resident persistent form where it applies, 0 = halo3x3_kernel only (the default).
 SEG_API int seg_halo_wr(int on) {
   const int old = g_halo_wr;
   if (on >= 0) g_halo_wr = on ? 1 : 0;

@@ -1331,13 +1331,16 @@ class Run:
             return
         sync = self.sync
         st = self.side if (self.side is not None and stream == self.side.cuda_stream) else None
+        done = sync.plan_ready(ready)  # the buckets this point completes; a host stop only then
+        if not done:
+            return
 
         def on_ready():  # host callback between tape segments
             if st is None:
-                sync.on_ready(ready)
+                sync.launch_ready(done)
             else:
                 with torch.cuda.stream(st):
-                    sync.on_ready(ready)
+                    sync.launch_ready(done)
         self.rec.stop(on_ready)
 
     # drivers
@@ -1546,6 +1549,26 @@ def debug_preactivations(model) -> dict:
 _PROGRAM_CACHE_ATTR = "_segamd_programs"
 
 
+def debug_pool_positions(model) -> dict:
+    """Diagnostics (DEBUG_KEEP_RUN, like debug_preactivations): the 2x2-window position (0..3, row-major; first
+    maximum, the kernel's and aten's tie rule) every max-pool of the last run chose, from the values the kernel read,
+    keyed "down1.", "down2.", ... in forward order (UNet's `down` blocks, src/unet.py:85) -- the parity checker routes
+    the fp64 oracle's max-pool gradients through them (oracle/budget.py)."""
+    run = LAST_RUN
+    if run is None:
+        raise RuntimeError("set engine.DEBUG_KEEP_RUN = True before the forward")
+    out, k = {}, 0
+    for op in run.prog.ops:
+        if isinstance(op, PoolOp):
+            i = op.inp
+            a = run.bufs[i.buf].view(-1, i.ld)[:, i.off:i.off + i.C].float().cpu()
+            a = a.view(i.N, i.H // 2, 2, i.W // 2, 2, i.C).permute(0, 5, 1, 3, 2, 4).reshape(i.N, i.C, i.H // 2,
+                                                                                           i.W // 2, 4)
+            k += 1
+            out[f"down{k}."] = a.argmax(-1)
+    return out
+
+
 def get_program(model, N, H, W, math=None) -> Program:
     if HALO_WR is not None:
         _apply_halo_wr()
@@ -1689,6 +1712,8 @@ class Plan:
             g = gout.reshape(1).to(torch.float32).contiguous()
         if self.bwd is None:
             rec = Recorder({side: 1, main: 0})
+            if self.sync is not None:
+                self.sync.begin_record()
             rec.external("gout", g.data_ptr())
             if self.t is not None:
                 rec.external("t", self.t.data_ptr())

@@ -58,13 +58,14 @@ def _slice_run(x, y, state, side, fwd, dgrad, wgrad):
         loss.backward()
         torch.cuda.synchronize()
         z = engine.debug_preactivations(model)
+        pools = engine.debug_pool_positions(model)
         prog = engine.get_program(model, *x.shape[:1], *x.shape[2:])
         n_wino = sum(op.wino_f + op.wino_d + op.wino_w for op in prog.ops if isinstance(op, engine.ConvOp))
     finally:
         engine.DEBUG_KEEP_RUN, engine.LAST_RUN = False, None
         engine.WINOGRAD_FWD, engine.WINOGRAD_DGRAD, engine.WINOGRAD_WGRAD = saved
     grads = {k: p.grad for k, p in model.named_parameters() if p.grad is not None}
-    rep = budget.check_hip("UNet", state, x, y, grads, z, side=side)
+    rep = budget.check_hip("UNet", state, x, y, grads, z, side=side, hip_pools=pools)
     return logits.detach().double().cpu(), loss.item(), rep, n_wino
 
 

@@ -10,7 +10,8 @@ A: each form alone against a float64 direct convolution of the same operands, on
    forward 64 -> 128 at 64x128, up2.0 / up3.0 data gradients 64 -> 256 / 64 -> 128), with the data gradient's calling
    pattern (no bias, output rows wider than Cout, an addend), and a Cin % 8 == 4 case;
 B: the slice test itself (tests/test_gpu_unet_cfg5.py::_slice_run, all Winograd transforms on) with fused2 on the
-   forward only, the data gradient only, both, neither.
+   forward only, the data gradient only, both, neither -- with the checker routing the fp64 oracle's max-pool gradients
+   through the HIP forward's window choices (round 6), and the number of windows whose choice differs from fp64.
 """
 import os
 import sys
@@ -88,7 +89,8 @@ def main():
         logits, loss, rep, n_wino = t._slice_run(x, y, state, side, True, True, True)
         top = sorted(rep["ratios"].items(), key=lambda kv: -kv[1])[:4]
         print(f"  {tag:26s}: worst {rep['worst']:.3f} ({rep['worst_name']}), next {top[1:]}, "
-              f"{len(rep['bad'])} tensors over budget, z {rep['z_worst']:.3f}", flush=True)
+              f"{len(rep['bad'])} tensors over budget, z {rep['z_worst']:.3f}, ReLU mask flips {rep['n_flips']}, "
+              f"max-pool window choices differing from fp64 {rep.get('pool_flips')}", flush=True)
     mask(0)
 
 

@@ -576,12 +576,12 @@ int seg_conv_igemm2_bf16io(const seg_bf16* in, long ldin, int N, int H, int W, i
 /* Round 4: the plan also picks 4-wave 128x128 / 128x64 / 64x128 / 64x64 tiles (small-image 1x1 and 3x3
  * convs of the MobileNetV2 encoder); seg_igemm2_force_tile(t) forces table entry t (-1 = the plan). */
 int seg_igemm2_force_tile(int t);
-/* A/B hook: seg_conv_halo* on the weight-resident persistent kernel where the packed weights fit its LDS (1, the
- * default) or on the per-tile kernel only (0); < 0 leaves it.  Returns the previous setting.  Bitwise the same. */
-int seg_halo_wr(int on);
 /* Tuning hook: split-K of the 4-wave tiles up to target_blocks blocks with >= min_steps 64-deep K
  * steps per slice (defaults 512, 3); values <= 0 keep the current setting. */
 int seg_igemm2_tune(int target_blocks, int min_steps);
+/* A/B hook: the K step (32 or 64 bf16) of seg_conv_igemm2_bf16io's 8-wave tiles; other values leave it.  Returns
+ * the previous setting.  Bitwise the same result either way. */
+int seg_igemm2_kb(int kb);
 
 /* seg_conv_wgrad2_bf16io: the weight gradient of those narrow 3x3 convs (replaces aten's
  * convolution_backward weight path of src/unet.py:58,61 where Cout <= 64; csrc/wgrad2.hip): persistent

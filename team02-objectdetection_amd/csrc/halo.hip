@@ -264,254 +264,7 @@ __global__ __launch_bounds__(256) void halo3x3_kernel(HaloArgs a) {
 }
 
 
-// Weight-resident persistent form (round 6).  The kernel above re-reads all 9 x Cout x BK weights
-// of a K chunk for every 256-pixel tile -- 37 KB of the 62 KB a bf16 block loads per chunk at Cout 64 (UNet's
-// 512x1024 64 -> 64 convs), so the L2 -> CU operand traffic, not the matrix cores, set its pace (PMC MFMA-busy 0.18,
-// profiles/r06/sq_unet512x1024_bf16io.md).  Here one block per CU loads the layer's whole packed weight tensor
-// into LDS once (rows padded to a pitch of 4 mod 8 dwords: conflict-free ds_read_b128) and walks a contiguous range
-// of its XCD's tiles (vertical neighbours share the XCD's L2), streaming only the halo chunks, double-buffered when
-// LDS allows (one barrier per chunk).  Same arithmetic per output element as halo3x3_kernel (the same K order: chunk,
-// tap, 16-deep step), so bitwise its result; same BN-partial layout (tile index = the tile's linear id).
-template <int NI, int WMAX, typename T, bool WB>
-__global__ __launch_bounds__(256) void halo3x3_wr_kernel(HaloArgs a, int ldw, int ntiles) {
-  constexpr bool LP = sizeof(T) == 2;
-  constexpr int BK = LP ? 32 : 16;
-  constexpr int LDSR = LP ? BK + 8 : BK + 4;
-  constexpr int HV = LP ? 8 : 4;
-  constexpr int HALO_VEC = HH * HW * (BK / HV);
-  constexpr int HALO_PER = (HALO_VEC + 255) / 256;
-  constexpr int BNC = 32 * NI;
-  constexpr int HSZ = HH * HW * LDSR;
-  constexpr int WSZ = 9 * BNC * WMAX;
-  constexpr int NB = (2 * HSZ + WSZ) * (int)sizeof(T) <= 150 * 1024 ? 2 : 1;  // halo buffers
-  static_assert((NB * HSZ + WSZ) * (int)sizeof(T) + 5 * BNC * 4 <= 160 * 1024, "LDS");
-  using lds_t = T;
-  __shared__ __attribute__((aligned(16))) lds_t Hs[NB * HSZ];
-  __shared__ __attribute__((aligned(16))) lds_t Ws[WSZ];
-  __shared__ float red[5 * BNC];
-  const T* in = static_cast<const T*>(a.in);
-  const T* add = static_cast<const T*>(a.add);
-  T* out = static_cast<T*>(a.out);
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-
-  // the whole weight tensor, once: row tap * BNC + co, k = ci (pitch ldw), rows beyond Cout zero
-  {
-    constexpr int WV = WB ? 8 : 4;  // weights per global 16-byte slot (bf16 packed: 8, fp32: 4)
-    const int qpr = ((a.Cin + BK - 1) / BK) * BK / WV;  // whole K chunks: columns [Cin, nk * BK) zero
-    const int nslots = 9 * BNC * qpr;
-    const float* wk32 = static_cast<const float*>(a.wk);
-    const __bf16* wk16 = static_cast<const __bf16*>(a.wk);
-    for (int sl = tid; sl < nslots; sl += 256) {
-      const int row = sl / qpr, q = sl - row * qpr;
-      const int tap = row / BNC, co = row - tap * BNC;
-      lds_t* dst = &Ws[row * ldw + q * WV];
-      if (co < a.Cout && q * WV < a.Cin) {
-        const long src = (long)co * a.ldk + tap * a.Cin + q * WV;
-        if constexpr (WB) *reinterpret_cast<f32x4*>(dst) = *reinterpret_cast<const f32x4*>(wk16 + src);
-        else if constexpr (LP) *reinterpret_cast<bf16x4*>(dst) = __builtin_convertvector(ld4(wk32 + src), bf16x4);
-        else *reinterpret_cast<f32x4*>(dst) = ld4(wk32 + src);
-      } else {
-        if constexpr (WB) *reinterpret_cast<f32x4*>(dst) = f32x4{0.f, 0.f, 0.f, 0.f};
-        else if constexpr (LP) *reinterpret_cast<bf16x4*>(dst) = bf16x4{};
-        else *reinterpret_cast<f32x4*>(dst) = f32x4{0.f, 0.f, 0.f, 0.f};
-      }
-    }
-  }
-
-  // this block's tiles: the XCD's contiguous share of the tile range, strided over the XCD's blocks
-  const int G = gridDim.x, xcd = blockIdx.x & 7, slot = blockIdx.x >> 3, per_xcd_blocks = G >> 3;
-  const int tx = (ntiles + 7) / 8;
-  const int t_beg = min(ntiles, xcd * tx), t_end = min(ntiles, t_beg + tx);
-  const int my_tiles = t_end - t_beg > slot ? (t_end - t_beg - slot + per_xcd_blocks - 1) / per_xcd_blocks : 0;
-  const int nk = (a.Cin + BK - 1) / BK;
-  const int total = my_tiles * nk;
-  auto tile_of = [&](int it) { return t_beg + slot + (it / nk) * per_xcd_blocks; };
-
-  f32x4 rh[HALO_PER];
-  auto load = [&](int it) {
-    const int t = tile_of(it), c0 = (it % nk) * BK;
-    const int tw_i = t % a.tiles_w, th_i = (t / a.tiles_w) % a.tiles_h, n = t / (a.tiles_w * a.tiles_h);
-    const T* inb = in + (long)n * a.H * a.W * a.ldin;
-#pragma unroll
-    for (int i = 0; i < HALO_PER; ++i) {
-      const int sl = tid + i * 256;
-      const int hp = sl / (BK / HV), q4 = (sl % (BK / HV)) * HV;
-      const int hy = hp / HW, hx = hp % HW;
-      const int gy = th_i * TH - 1 + hy, gx = tw_i * TW - 1 + hx;
-      const bool ok = sl < HALO_VEC && (unsigned)gy < (unsigned)a.H && (unsigned)gx < (unsigned)a.W && c0 + q4 < a.Cin;
-      const T* src = ok ? inb + ((long)gy * a.W + gx) * a.ldin + c0 + q4 : reinterpret_cast<const T*>(g_hzero4);
-      if constexpr (LP) rh[i] = *reinterpret_cast<const f32x4*>(src);
-      else rh[i] = ld4(src);
-    }
-  };
-  auto store = [&](int buf) {
-#pragma unroll
-    for (int i = 0; i < HALO_PER; ++i) {
-      const int sl = tid + i * 256;
-      if (HALO_VEC % 256 == 0 || sl < HALO_VEC)
-        *reinterpret_cast<f32x4*>(&Hs[buf * HSZ + (sl / (BK / HV)) * LDSR + (sl % (BK / HV)) * HV]) = rh[i];
-    }
-  };
-
-  f32x16 acc[2][NI];
-  auto zero_acc = [&]() {
-#pragma unroll
-    for (int mi = 0; mi < 2; ++mi)
-#pragma unroll
-      for (int ni = 0; ni < NI; ++ni)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) acc[mi][ni][r] = 0.f;
-  };
-  zero_acc();
-  const int lrow = lane & 31;
-  auto compute = [&](int buf, int kc) {
-    const lds_t* H = Hs + buf * HSZ;
-    if constexpr (LP) {
-      const int lk8 = (lane >> 5) * 8;
-#pragma unroll
-      for (int tap = 0; tap < 9; ++tap) {
-        const int ky = tap / 3, kx = tap % 3;
-#pragma unroll
-        for (int ks = 0; ks < BK / 16; ++ks) {
-          bf16x8 af[2], bfr[NI];
-#pragma unroll
-          for (int mi = 0; mi < 2; ++mi)
-            af[mi] = *reinterpret_cast<const bf16x8*>(&H[((wave + ky) * HW + mi * 32 + lrow + kx) * LDSR + ks * 16 + lk8]);
-#pragma unroll
-          for (int ni = 0; ni < NI; ++ni)
-            bfr[ni] = *reinterpret_cast<const bf16x8*>(&Ws[(tap * BNC + ni * 32 + lrow) * ldw + kc * BK + ks * 16 + lk8]);
-#pragma unroll
-          for (int mi = 0; mi < 2; ++mi)
-#pragma unroll
-            for (int ni = 0; ni < NI; ++ni)
-              acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[mi], bfr[ni], acc[mi][ni], 0, 0, 0);
-        }
-      }
-    } else {
-      const int lk = (lane >> 5) * 4;
-#pragma unroll
-      for (int tap = 0; tap < 9; ++tap) {
-        const int ky = tap / 3, kx = tap % 3;
-#pragma unroll
-        for (int ks = 0; ks < BK / 8; ++ks) {
-          f32x4 af[2], bfr[NI];
-#pragma unroll
-          for (int mi = 0; mi < 2; ++mi)
-            af[mi] = *reinterpret_cast<const f32x4*>(&H[((wave + ky) * HW + mi * 32 + lrow + kx) * LDSR + ks * 8 + lk]);
-#pragma unroll
-          for (int ni = 0; ni < NI; ++ni)
-            bfr[ni] = *reinterpret_cast<const f32x4*>(&Ws[(tap * BNC + ni * 32 + lrow) * ldw + kc * BK + ks * 8 + lk]);
-#pragma unroll
-          for (int kk = 0; kk < 4; ++kk)
-#pragma unroll
-            for (int mi = 0; mi < 2; ++mi)
-#pragma unroll
-              for (int ni = 0; ni < NI; ++ni)
-                acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[mi][kk], bfr[ni][kk], acc[mi][ni], 0, 0, 0);
-        }
-      }
-    }
-  };
-  // halo3x3_kernel's epilogue for tile t (bias, BN partials of the 256 pixels, addend, stores)
-  auto epilogue = [&](int t) {
-    const int tw_i = t % a.tiles_w, th_i = (t / a.tiles_w) % a.tiles_h, n = t / (a.tiles_w * a.tiles_h);
-#pragma unroll
-    for (int ni = 0; ni < NI; ++ni) {
-      const int col = ni * 32 + lrow;
-      const float b = (a.bias && col < a.Cout) ? a.bias[col] : 0.f;
-#pragma unroll
-      for (int mi = 0; mi < 2; ++mi)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) acc[mi][ni][r] += b;
-    }
-    const long pix0 = ((long)n * a.H + th_i * TH + wave) * a.W + tw_i * TW;
-    if (a.stat) {
-      float* tmean = red + 4 * BNC;
-#pragma unroll
-      for (int pass = 0; pass < 2; ++pass) {
-#pragma unroll
-        for (int ni = 0; ni < NI; ++ni) {
-          const int cl = ni * 32 + lrow;
-          const float mu = pass ? tmean[cl] : 0.f;
-          float sacc = 0.f;
-#pragma unroll
-          for (int mi = 0; mi < 2; ++mi)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-              const float d = acc[mi][ni][r] - mu;
-              sacc += pass ? d * d : d;
-            }
-          sacc += __shfl_xor(sacc, 32, 64);
-          if (lane < 32) red[wave * BNC + cl] = sacc;
-        }
-        __syncthreads();
-        if (tid < BNC) {
-          const float tt = red[tid] + red[BNC + tid] + red[2 * BNC + tid] + red[3 * BNC + tid];
-          if (pass == 0) tmean[tid] = tt / (float)(TH * TW);
-          if (tid < a.Cout) a.stat[((long)t * 2 + pass) * a.Cout + tid] = tt;
-        }
-        __syncthreads();
-      }
-    }
-#pragma unroll
-    for (int ni = 0; ni < NI; ++ni) {
-      const int col = ni * 32 + lrow;
-      if (col >= a.Cout) continue;
-#pragma unroll
-      for (int mi = 0; mi < 2; ++mi)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const long p = pix0 + mi * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-          float v = acc[mi][ni][r];
-          if (add) v += (float)add[p * a.ldadd + col];
-          out[p * a.ldout + col] = static_cast<T>(v);
-        }
-    }
-    zero_acc();
-  };
-
-  if constexpr (NB == 2) {
-    if (total > 0) {
-      load(0);
-      store(0);
-    }
-    if (total > 1) load(1);
-    __syncthreads();  // the weights and the first chunk are in LDS
-    for (int it = 0; it < total; ++it) {
-      const int kc = it % nk;
-      compute(it & 1, kc);
-      if (it + 1 < total) store((it + 1) & 1);  // buffer last read in iteration it - 1 (barrier since)
-      if (it + 2 < total) load(it + 2);
-      if (kc == nk - 1) epilogue(tile_of(it));
-      __syncthreads();
-    }
-  } else {
-    if (total > 0) load(0);
-    for (int it = 0; it < total; ++it) {
-      const int kc = it % nk;
-      store(0);
-      __syncthreads();  // (the first time: the weights too)
-      if (it + 1 < total) load(it + 1);
-      compute(0, kc);
-      if (kc == nk - 1) epilogue(tile_of(it));
-      __syncthreads();
-    }
-  }
-}
-
 }  // namespace
-
-#ifndef SEG_HALO_WR
-#define SEG_HALO_WR 0  // measured slower (profiles/r06/halobench_*.txt): off unless asked for
-#endif
-int g_halo_wr = SEG_HALO_WR;  // the weight-resident form (seg_halo_wr: A/B hook)
-
-// A/B hook: 1 = the weight-resident persistent form where it applies, 0 = halo3x3_kernel only (the default).
-SEG_API int seg_halo_wr(int on) {
-  const int old = g_halo_wr;
-  if (on >= 0) g_halo_wr = on ? 1 : 0;
-  return old;
-}
 
 // 1 when seg_conv_halo handles this stride-1 pad-1 3x3 conv: H % 4 == 0,
 // W % 64 == 0, Cout <= 96, Cin % 4 == 0, Cin >= 16.
@@ -543,31 +296,6 @@ static int conv_halo_impl(const T* in, long ldin, int N, int H, int W, int Cin, 
   a.out = out; a.ldout = ldout; a.stat = stat; a.N = N; a.H = H; a.W = W; a.Cin = Cin; a.Cout = Cout;
   a.tiles_w = W / TW; a.tiles_h = H / TH;
   const int grid = N * a.tiles_h * a.tiles_w;
-  // the weight-resident persistent form where the packed weights fit its LDS (halo3x3_wr_kernel): bf16 Cout <= 64 /
-  // Cin <= 64 and Cout <= 32 / Cin <= 96; fp32 Cout <= 32 / Cin <= 80
-  if (g_halo_wr && grid >= 2 * seg_num_cus()) {
-    constexpr bool LP = sizeof(T) == 2;
-    const int kpad = LP ? (Cin + 31) & ~31 : (Cin + 15) & ~15;  // whole K chunks
-    const int ldw = LP ? ((kpad + 15) & ~15) + 8 : ((kpad + 7) & ~7) + 4;  // pitch = 4 mod 8 dwords: conflict-free
-    const int g = std::min(grid, seg_num_cus()) & ~7;
-    if (g >= 8) {
-      if constexpr (LP) {
-        if (Cout <= 32 && ldw <= 104) {
-          hipLaunchKernelGGL((halo3x3_wr_kernel<1, 104, T, WB>), dim3(g), dim3(256), 0, stream, a, ldw, grid);
-          SEG_RET_LAST();
-        }
-        if (Cout <= 64 && ldw <= 72) {
-          hipLaunchKernelGGL((halo3x3_wr_kernel<2, 72, T, WB>), dim3(g), dim3(256), 0, stream, a, ldw, grid);
-          SEG_RET_LAST();
-        }
-      } else {
-        if (Cout <= 32 && ldw <= 84) {
-          hipLaunchKernelGGL((halo3x3_wr_kernel<1, 84, T, WB>), dim3(g), dim3(256), 0, stream, a, ldw, grid);
-          SEG_RET_LAST();
-        }
-      }
-    }
-  }
   if (Cout <= 32) hipLaunchKernelGGL((halo3x3_kernel<1, T, WB>), dim3(grid), dim3(256), 0, stream, a);
   else if (Cout <= 64) hipLaunchKernelGGL((halo3x3_kernel<2, T, WB>), dim3(grid), dim3(256), 0, stream, a);
   else hipLaunchKernelGGL((halo3x3_kernel<3, T, WB>), dim3(grid), dim3(256), 0, stream, a);

@@ -38,7 +38,6 @@ PROTOTYPES = {
     "seg_conv_wino": (_I, [_V, _L, _I, _I, _I, _I, _V, _I, _V, _V, _L, _I, _V, _L, _V, _V, _V]),
     "seg_conv_wino_fused": (_I, [_V, _L, _I, _I, _I, _I, _V, _I, _V, _V, _L, _I, _V, _L, _V, _V]),
     "seg_conv_wino_fused_ok": (_I, [_I, _I, _I, _L]),
-    "seg_halo_wr": (_I, [_I]),
     "seg_conv_wino_wgrad_pick": (_I, [_I, _I, _I, _I, _I]),
     "seg_conv_wino_wgrad_splits": (_I, [_I, _I, _I, _I, _I]),
     "seg_conv_wino_wgrad": (_I, [_V, _L, _V, _L, _I, _I, _I, _I, _I, _V, _I, _V]),
@@ -101,6 +100,7 @@ PROTOTYPES = {
     "seg_conv_igemm2_bf16io": (_I, [_V, _L, _I, _I, _I, _I, _V, _I, _V, _V, _L, _I, _I, _V, _L, _V, _V, _V]),
     "seg_igemm2_force_tile": (_I, [_I]),
     "seg_igemm2_tune": (_I, [_I, _I]),
+    "seg_igemm2_kb": (_I, [_I]),
     "seg_conv_wgrad2_ok": (_I, [_I, _I, _I, _I, _I]),
     "seg_conv_wgrad2_blocks": (_I, [_I, _I, _I]),
     "seg_conv_wgrad2_bf16io": (_I, [_V, _L, _V, _L, _I, _I, _I, _I, _I, _V, _V]),

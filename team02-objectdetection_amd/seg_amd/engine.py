@@ -1366,6 +1366,7 @@ class Run:
         groups = self.prog.mbconv_groups() if MBCONV and f16 else {}
         head = self.prog.pw2_head() if PW2 and f16 else None
         k = start
+        lvl = -1  # decoder upsample index (UPFOLD bits)
         while k < len(ops):
             g = groups.get(k)
             if g is not None:
@@ -1382,10 +1383,12 @@ class Run:
                 continue
             op = ops[k]
             nxt = ops[k + 1] if k + 1 < len(ops) else None
-            if f16 and UPFOLD and isinstance(op, UpsampleOp) and self._upfold_ok(op, nxt):
-                nxt.forward_folded(self, up=op)  # the decoder conv forms the x2 upsample on load
-                k += 2
-                continue
+            if isinstance(op, UpsampleOp):
+                lvl += 1
+                if f16 and (UPFOLD >> lvl) & 1 and self._upfold_ok(op, nxt):
+                    nxt.forward_folded(self, up=op)  # the decoder conv forms the x2 upsample on load
+                    k += 2
+                    continue
             if isinstance(op, ConvOp):
                 op.forward_folded(self)
             else:
@@ -1498,55 +1501,19 @@ STEM_PRE = True
 PW2 = True
 PLAN_B1 = True
 # ... and the decoder's x2 upsample formed on load by the conv that consumes the concat (seg_conv_igemm_f16_ic_up,
-# VERDICT r5 item 6; SEG_UPFOLD=0: the upsample launch + seg_conv_igemm_f16_ic)
-UPFOLD = os.environ.get("SEG_UPFOLD", "1") == "1"
-# LDS-halo convs on the weight-resident persistent kernel where the weights fit (csrc/halo.hip halo3x3_wr_kernel,
-# bitwise the per-tile kernel; SEG_HALO_WR=0: the per-tile kernel only -- A/B hook, applied when a program is built)
-HALO_WR = os.environ.get("SEG_HALO_WR")
+# VERDICT r5 item 6): bit k of SEG_UPFOLD folds the (k+1)-th decoder level's upsample (up1 = bit 0).  Measured
+# (profiles/r06/ab_upfold*.txt): all four folded 2480 vs 2705 frames/s -- four float4 loads and a blend per operand
+# slot cost the latency-bound batch-1 convs more than the launches save; per-level mask below
+UPFOLD = int(os.environ.get("SEG_UPFOLD", "0"), 0)
+# igemm2's K step for the 8-wave tiles (SEG_IG2_KB=32 / 64; unset: the library default) -- A/B hook, applied when a
+# program is built
+IG2_KB = os.environ.get("SEG_IG2_KB")
 
 
-def _apply_halo_wr():
-    global HALO_WR
-    query("seg_halo_wr", int(HALO_WR == "1"))
-    HALO_WR = None
-_SIDE = {}
-
-
-def _side_stream(device):
-    st = _SIDE.get(device)
-    if st is None:
-        st = _SIDE[device] = torch.cuda.Stream(device, priority=0)
-    return st
-
-
-DEBUG_KEEP_RUN = False  # diagnostics: keep the last Run (buffers + gradient buffers)
-LAST_RUN = None
-
-
-def debug_preactivations(model) -> dict:
-    """Diagnostics (needs DEBUG_KEEP_RUN = True before the forward): every activation
-    layer's post-BatchNorm pre-activation z = y * scale + shift of the last run, as fp64
-    NCHW CPU tensors keyed by the conv's module path + "." (the parity tests compare them
-    with the oracle and take the ReLU/ReLU6 masks from them)."""
-    run = LAST_RUN
-    if run is None:
-        raise RuntimeError("set engine.DEBUG_KEEP_RUN = True before the forward")
-    model = getattr(model, "module", model)
-    names = {}
-    for n, m in model.named_modules():
-        names.setdefault(id(m), n)
-    out = {}
-    for op in run.prog.ops:
-        if isinstance(op, ConvOp) and op.bn is not None and op.act != ACT_NONE:
-            y, C = op.y, op.cout
-            t = run.bufs[y.buf].view(-1, y.ld)[:, y.off:y.off + C].double()
-            st = run.saved[id(op)].double()
-            z = t * st[2 * C:3 * C] + st[3 * C:4 * C]
-            out[names[id(op.conv)] + "."] = z.view(y.N, y.H, y.W, C).permute(0, 3, 1, 2).cpu()
-    return out
-
-
-_PROGRAM_CACHE_ATTR = "_segamd_programs"
+def _apply_ig2_kb():
+    global IG2_KB
+    query("seg_igemm2_kb", int(IG2_KB))
+    IG2_KB = None
 
 
 def debug_pool_positions(model) -> dict:
@@ -1570,8 +1537,8 @@ def debug_pool_positions(model) -> dict:
 
 
 def get_program(model, N, H, W, math=None) -> Program:
-    if HALO_WR is not None:
-        _apply_halo_wr()
+    if IG2_KB is not None:
+        _apply_ig2_kb()
     cache = model.__dict__.setdefault(_PROGRAM_CACHE_ATTR, {})
     math = math or model.__dict__.get("_segamd_math", "f32")
     key = (N, H, W, math)

@@ -272,11 +272,11 @@ def test_predictor_upsample_fold_bitwise():
     f = (np.random.default_rng(2).random((720, 1280, 3)) * 255).astype(np.uint8)
     saved = engine.UPFOLD
     try:
-        engine.UPFOLD = False
+        engine.UPFOLD = 0
         p0 = Predictor(model, frame_hw=(720, 1280), graph=False, math="f16")
         m0 = p0(f).clone()
         l0 = p0.logits()
-        engine.UPFOLD = True
+        engine.UPFOLD = 0b1111  # every level
         p1 = Predictor(model, frame_hw=(720, 1280), graph=True, math="f16")
         m1 = p1(f).clone()
         l1 = p1.logits()

@@ -53,6 +53,7 @@ def main():
     ap.add_argument("--only", default="")
     ap.add_argument("--kernel", default="both", choices=("ig2", "gen", "both", "halo", "all"))
     ap.add_argument("--set", default="mnv2", choices=("mnv2", "unet"))
+    ap.add_argument("--kb", type=int, default=0, help="igemm2 K step: 64, 32 or 0 = both")
     ap.add_argument("--reps", type=int, default=20)
     a = ap.parse_args()
     only = set(a.only.split(",")) if a.only else None
@@ -74,16 +75,17 @@ def main():
         res = []
         if plan and a.kernel in ("ig2", "both", "all"):
             work = torch.zeros(max(plan[3], 1), device="cuda")
-            t = timeit(lambda: call("seg_conv_igemm2_bf16io", x.data_ptr(), Cin, N, H, W, Cin, wk.data_ptr(), ldk, None,
-                                    y.data_ptr(), Cout, Cout, ks, None, 0, None, work.data_ptr(), s), a.reps)
-            res.append(f"ig2 {t * 1e6:7.1f} us {flops / t / 1e12:6.0f} TF/s (tile rows {plan[0]}, splits {plan[2]})")
+            for kbv in ((64, 32) if a.kb == 0 else (a.kb,)):  # the 8-wave tiles' K step (seg_igemm2_kb)
+                old = engine.query("seg_igemm2_kb", kbv)
+                t = timeit(lambda: call("seg_conv_igemm2_bf16io", x.data_ptr(), Cin, N, H, W, Cin, wk.data_ptr(), ldk,
+                                        None, y.data_ptr(), Cout, Cout, ks, None, 0, None, work.data_ptr(), s), a.reps)
+                engine.query("seg_igemm2_kb", old)
+                res.append(f"ig2/kb{kbv} {t * 1e6:7.1f} us {flops / t / 1e12:6.0f} TF/s (tile rows {plan[0]}, "
+                           f"splits {plan[2]})")
         if a.kernel in ("halo", "all") and engine.query("seg_conv_halo_pick", N, H, W, Cin, Cout):
-            for wr in (0, 1):  # per-tile kernel, weight-resident persistent kernel (seg_halo_wr)
-                engine.query("seg_halo_wr", wr)
-                t = timeit(lambda: call("seg_conv_halo_bf16io_w16", x.data_ptr(), Cin, N, H, W, Cin, wk.data_ptr(),
-                                        ldk, None, y.data_ptr(), Cout, Cout, None, 0, None, s), a.reps)
-                res.append(f"halo{'_wr' if wr else ''} {t * 1e6:7.1f} us {flops / t / 1e12:6.0f} TF/s")
-            engine.query("seg_halo_wr", 1)
+            t = timeit(lambda: call("seg_conv_halo_bf16io_w16", x.data_ptr(), Cin, N, H, W, Cin, wk.data_ptr(),
+                                    ldk, None, y.data_ptr(), Cout, Cout, None, 0, None, s), a.reps)
+            res.append(f"halo {t * 1e6:7.1f} us {flops / t / 1e12:6.0f} TF/s")
         if a.kernel in ("gen", "both", "all"):
             t = timeit(lambda: call("seg_conv_igemm_bf16io_w16", x.data_ptr(), Cin, N, H, W, Cin, wk.data_ptr(), ldk,
                                     None, y.data_ptr(), Cout, H, W, Cout, 3, 1, 1, None, 0, None, s), a.reps)

@@ -1516,6 +1516,46 @@ def _apply_ig2_kb():
     IG2_KB = None
 
 
+_SIDE = {}
+
+
+def _side_stream(device):
+    st = _SIDE.get(device)
+    if st is None:
+        st = _SIDE[device] = torch.cuda.Stream(device, priority=0)
+    return st
+
+
+DEBUG_KEEP_RUN = False  # diagnostics: keep the last Run (buffers + gradient buffers)
+LAST_RUN = None
+
+
+def debug_preactivations(model) -> dict:
+    """Diagnostics (needs DEBUG_KEEP_RUN = True before the forward): every activation
+    layer's post-BatchNorm pre-activation z = y * scale + shift of the last run, as fp64
+    NCHW CPU tensors keyed by the conv's module path + "." (the parity tests compare them
+    with the oracle and take the ReLU/ReLU6 masks from them)."""
+    run = LAST_RUN
+    if run is None:
+        raise RuntimeError("set engine.DEBUG_KEEP_RUN = True before the forward")
+    model = getattr(model, "module", model)
+    names = {}
+    for n, m in model.named_modules():
+        names.setdefault(id(m), n)
+    out = {}
+    for op in run.prog.ops:
+        if isinstance(op, ConvOp) and op.bn is not None and op.act != ACT_NONE:
+            y, C = op.y, op.cout
+            t = run.bufs[y.buf].view(-1, y.ld)[:, y.off:y.off + C].double()
+            st = run.saved[id(op)].double()
+            z = t * st[2 * C:3 * C] + st[3 * C:4 * C]
+            out[names[id(op.conv)] + "."] = z.view(y.N, y.H, y.W, C).permute(0, 3, 1, 2).cpu()
+    return out
+
+
+_PROGRAM_CACHE_ATTR = "_segamd_programs"
+
+
 def debug_pool_positions(model) -> dict:
     """Diagnostics (DEBUG_KEEP_RUN, like debug_preactivations): the 2x2-window position (0..3, row-major; first
     maximum, the kernel's and aten's tie rule) every max-pool of the last run chose, from the values the kernel read,

@@ -116,16 +116,6 @@ int seg_conv_igemm_f16_ic(const float* in, long ldin, int N, int H, int W, int C
                           const float* bias, float* out, long ldout, int Ho, int Wo, int Cout, int ks, int stride,
                           int pad, const float* add, long ldadd, int act, float* work, int splits, int tile, unsigned* cnt,
                           hipStream_t stream);
-/* seg_conv_igemm_f16_ic of a decoder conv0 whose input is torch.cat([skip, Upsample(x2, bilinear,
- * align_corners=False)(low)], 1) (src/unet.py:97-104, inference.py's eval forward) with the upsample formed on
- * load: `in` holds the skip in channels [0, ucs) of its Cin-wide rows; channels [ucs, Cin)
- * are interpolated per operand slot from `up` [N][H/2][W/2][ldup] (seg_upsample_fwd's index arithmetic and
- * blend, bitwise its output), so the upsample launch and its rows disappear.  3x3, stride 1, pad 1; H, W even;
- * ucs % 4 == 0. */
-int seg_conv_igemm_f16_ic_up(const float* in, long ldin, int N, int H, int W, int Cin, const float* up, long ldup,
-                             int ucs, const float* wk, int ldk, const float* bias, float* out, long ldout, int Cout,
-                             const float* add, long ldadd, int act, float* work, int splits, int tile, unsigned* cnt,
-                             hipStream_t stream);
 
 /* seg_conv_igemm as a stride-1 data gradient (pad ks/2, no bias, optional fused addend) that
  * completes dA of a BatchNorm layer whose pre-BN output is `by`: the epilogue also writes that
@@ -579,9 +569,6 @@ int seg_igemm2_force_tile(int t);
 /* Tuning hook: split-K of the 4-wave tiles up to target_blocks blocks with >= min_steps 64-deep K
  * steps per slice (defaults 512, 3); values <= 0 keep the current setting. */
 int seg_igemm2_tune(int target_blocks, int min_steps);
-/* A/B hook: the K step (32 or 64 bf16) of seg_conv_igemm2_bf16io's 8-wave tiles; other values leave it.  Returns
- * the previous setting.  Bitwise the same result either way. */
-int seg_igemm2_kb(int kb);
 
 /* seg_conv_wgrad2_bf16io: the weight gradient of those narrow 3x3 convs (replaces aten's
  * convolution_backward weight path of src/unet.py:58,61 where Cout <= 64; csrc/wgrad2.hip): persistent

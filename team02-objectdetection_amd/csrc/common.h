@@ -265,8 +265,8 @@ __device__ __forceinline__ f32x4 bilerp4(f32x4 v00, f32x4 v01, f32x4 v10, f32x4 
 }
 
 // The x2 upsample's blend (nn.Upsample bilinear, align_corners=False: seg_upsample_fwd) with one fixed fma
-// association -- no contraction left to the compiler -- so a kernel that forms the upsample on load (the folded
-// decoder conv, seg_conv_igemm_f16_ic_up) rounds bit for bit as the upsample kernel does.
+// association -- no contraction left to the compiler -- so any kernel that forms the upsample on load rounds bit for
+// bit as the upsample kernel does (round 6's folded decoder conv did; it measured slower and was removed).
 __device__ __forceinline__ f32x4 up_blend4(f32x4 v00, f32x4 v01, f32x4 v10, f32x4 v11, float h0, float h1, float w0,
                                            float w1) {
   f32x4 o;

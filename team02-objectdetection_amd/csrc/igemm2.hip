@@ -83,30 +83,17 @@ __device__ __forceinline__ void wait_vm() {  // s_waitcnt vmcnt(N), other counte
   __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | 0x0F70);  // vmcnt is 6 bits, split 3:0 / 15:14
 }
 
-// KB: K step depth (bf16 elements).  64 (rounds 3-5): 128-byte operand rows, three LDS buffers, the next step's DMA
-// issued after the compute phase and a second barrier.  32 (round 6): 64-byte rows, six buffers,
-// one barrier per step, and the DMA of step it + 5 issued INSIDE step it's compute phase into the buffer step it - 1
-// freed -- the DMA-off / MFMA-off builds measured the two phases nearly serialised (UNet 512x1024 128 -> 128: 526 us
-// as built, 305 without the operand DMA, 370 without the MFMAs; profiles/r06/ig2diag_*.txt): each wave issued its
-// step's 6 DMA instructions between two barriers with no MFMA beside them.
-template <int BM, int BN, int WM, int WN, int KS, int KB = 64>
+template <int BM, int BN, int WM, int WN, int KS>
 __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void igemm2_kernel(Igemm2Args a) {
   constexpr int NW = (BM / WM) * (BN / WN), kThreads = 64 * NW, WAVES_N = BN / WN;
   constexpr int MI = WM / 32, NI = WN / 32;
   static_assert(NW == 4 || NW == 8, "4 or 8 waves");
-  static_assert(KB == 64 || KB == 32, "K step 64 or 32");
-  constexpr int RB = KB * 2;                 // operand row bytes
-  constexpr int CPR = RB / 16;               // 16-byte chunks per row
-  constexpr int RPI = 1024 / RB;             // rows per DMA instruction (64 lanes x 16 B)
-  static_assert(BM % (RPI * NW) == 0 && BN % (RPI * NW) == 0, "whole DMA instructions per wave");
-  constexpr int A_BYTES = BM * RB, STAGE = (BM + BN) * RB;
-  constexpr int NA = BM / (RPI * NW), NB = BN / (RPI * NW);  // DMA instructions per wave per K step
+  static_assert(BM % (8 * NW) == 0 && BN % (8 * NW) == 0, "whole DMA instructions per wave");
+  constexpr int A_BYTES = BM * 128, STAGE = (BM + BN) * 128;
+  constexpr int NA = BM / (8 * NW), NB = BN / (8 * NW);  // DMA instructions per wave per K step
   constexpr int CSR = BN + 4;                // epilogue band row stride (floats)
-  constexpr int NSTAGE = KB == 64 ? 3 : 6;   // LDS buffers
+  constexpr int NSTAGE = 3;                  // LDS buffers: two K steps in flight while one computes
   constexpr int SMEM = NSTAGE * STAGE > WM * CSR * 4 ? NSTAGE * STAGE : WM * CSR * 4;
-  // XOR swizzle of a row's 16-byte chunks (the DMA writes lane-linearly; applied to the source, undone on the read):
-  // conflict-free ds_read_b128 fragment reads for both row widths
-  auto swz = [](int row) { return KB == 64 ? (row >> 1) & 7 : (row >> 2) & 3; };
   __shared__ __attribute__((aligned(1024))) char smem[SMEM];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -119,17 +106,17 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void igemm2_kernel(Igem
   const int s_beg = z * a.steps_per_split;
   const int nst = min(a.nsteps - s_beg, a.steps_per_split);
 
-  // ---- per-lane DMA sources.  Instruction j of a tile covers rows RPI j .. RPI j + RPI - 1 (1 KB of LDS);
-  // wave w issues j = w, w + NW, ...; lane l fills row RPI j + l / CPR, physical chunk l % CPR,
-  // i.e. logical chunk cl = (l % CPR) ^ swz(row).
-  const int lrow = lane / CPR, lchk = lane % CPR;
+  // ---- per-lane DMA sources.  Instruction j of a tile covers rows 8j .. 8j+7 (1 KB of LDS);
+  // wave w issues j = w, w + NW, ...; lane l fills row 8j + (l >> 3), physical chunk l & 7,
+  // i.e. logical chunk cl = (l & 7) ^ swz(row).
+  const int lrow = lane >> 3, lchk = lane & 7;
   long a_off[NA];
   unsigned a_mask[NA];
   int a_cl[NA];
 #pragma unroll
   for (int i = 0; i < NA; ++i) {
-    const int row = RPI * (wave + NW * i) + lrow;
-    a_cl[i] = lchk ^ swz(row);
+    const int row = 8 * (wave + NW * i) + lrow;
+    a_cl[i] = lchk ^ ((row >> 1) & 7);
     const int p = m0 + row;
     const bool ok = p < a.M;
     const int pp = ok ? p : 0;
@@ -150,14 +137,14 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void igemm2_kernel(Igem
   int b_k[NB];  // this lane's k offset within a step (8 * logical chunk); 2^30: row beyond Cout
 #pragma unroll
   for (int i = 0; i < NB; ++i) {
-    const int row = RPI * (wave + NW * i) + lrow;
-    const int cl = lchk ^ swz(row);
+    const int row = 8 * (wave + NW * i) + lrow;
+    const int cl = lchk ^ ((row >> 1) & 7);
     const int co = n0 + row;
     b_k[i] = co < a.Cout ? 8 * cl : 1 << 30;
     b_off[i] = (long)(co < a.Cout ? co : 0) * a.ldk + 8 * cl;
   }
   // wave-uniform K-step position: tap u_tap, channel u_ci of the step's first k
-  const int k_beg = s_beg * KB;
+  const int k_beg = s_beg * kBK;
   int u_tap = k_beg / a.Cin, u_ci = k_beg - u_tap * a.Cin;
   auto tap_off = [&](int t) -> long { return ((long)(t / KS) * a.W + t % KS) * a.ldin; };
   long u_toff0 = tap_off(u_tap), u_toff1 = tap_off(u_tap + 1);
@@ -181,8 +168,8 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void igemm2_kernel(Igem
       dma16(ok ? (const void*)(a.wk + b_off[i] + k0) : (const void*)g_zero_row, Bs + (wave + NW * i) * 1024);
     }
     // advance one K step
-    k0 += KB;
-    u_ci += KB;
+    k0 += kBK;
+    u_ci += kBK;
     while (u_ci >= a.Cin) {
       u_ci -= a.Cin;
       ++u_tap;
@@ -200,7 +187,7 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void igemm2_kernel(Igem
       for (int r = 0; r < 16; ++r) acc[mi][ni][r] = 0.f;
 
   const int fr = lane & 31, fh = lane >> 5;
-  auto compute = [&](int buf, auto&& mid) {  // mid(): run after the first 16-deep slice's MFMAs (KB 32: the DMA)
+  auto compute = [&](int buf) {
     const char* As = smem + buf * STAGE;
     const char* Bs = As + A_BYTES;
     // fragments of the next 16-deep k slice are read while the current slice's MFMAs run
@@ -210,18 +197,18 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void igemm2_kernel(Igem
 #pragma unroll
       for (int mi = 0; mi < MI; ++mi) {
         const int r = wm0 + mi * 32 + fr;
-        af[st][mi] = *reinterpret_cast<const bf16x8*>(As + r * RB + 16 * (chunk ^ swz(r)));
+        af[st][mi] = *reinterpret_cast<const bf16x8*>(As + r * 128 + 16 * (chunk ^ ((r >> 1) & 7)));
       }
 #pragma unroll
       for (int ni = 0; ni < NI; ++ni) {
         const int r = wn0 + ni * 32 + fr;
-        bfr[st][ni] = *reinterpret_cast<const bf16x8*>(Bs + r * RB + 16 * (chunk ^ swz(r)));
+        bfr[st][ni] = *reinterpret_cast<const bf16x8*>(Bs + r * 128 + 16 * (chunk ^ ((r >> 1) & 7)));
       }
     };
     frag(0, 0);
 #pragma unroll
-    for (int ks = 0; ks < KB / 16; ++ks) {
-      if (ks + 1 < KB / 16) frag(ks + 1, (ks + 1) & 1);
+    for (int ks = 0; ks < kBK / 16; ++ks) {
+      if (ks + 1 < kBK / 16) frag(ks + 1, (ks + 1) & 1);
 #pragma unroll
       for (int mi = 0; mi < MI; ++mi)
 #pragma unroll
@@ -232,52 +219,26 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void igemm2_kernel(Igem
           }
           acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[ks & 1][mi], bfr[ks & 1][ni], acc[mi][ni], 0, 0, 0);
         }
-      if (ks == 0) mid();
     }
   };
 
-  if constexpr (KB == 64) {
-    // ---- K loop: buffer it % 3 holds step it; steps it + 1 and it + 2 stay in flight meanwhile
-    // (each step is NA + NB DMA instructions per wave, so "k steps still in flight" is
-    // vmcnt(k * (NA + NB)))
-    if (nst > 0) issue(0);
-    if (nst > 1) issue(1);
-    if (nst > 2) issue(2);
-    for (int it = 0; it < nst; ++it) {
-      const int ahead = min(nst - 1 - it, 2);  // steps issued beyond this one
-      if (ahead == 2) wait_vm<2 * (NA + NB)>();
-      else if (ahead == 1) wait_vm<NA + NB>();
-      else wait_vm<0>();
-      raw_barrier();                         // every wave's DMA of step `it` has landed
-      const int buf = it % NSTAGE;
-      compute(buf, [] {});
-      wait_lgkm0();                          // this wave's fragment reads of `buf` are done
-      raw_barrier();                         // ... every wave's: the buffer may be refilled
-      if (it + NSTAGE < nst) issue(buf);
-    }
-  } else {
-    // ---- K loop, KB 32: buffer it % 6 holds step it; steps it + 1 .. it + 4 are in flight when step it's compute
-    // starts, and step it + 5 is issued during it (into buffer (it - 1) % 6: every wave finished step it - 1's
-    // fragment reads before this step's barrier -- its MFMAs consumed them).  One barrier per step; vmcnt counts
-    // NA + NB DMA instructions per step.
-    constexpr int D = NSTAGE;  // steps it .. it + D - 1 issued by the end of step it's compute
-    for (int j = 0; j < D - 1 && j < nst; ++j) issue(j % NSTAGE);
-    for (int it = 0; it < nst; ++it) {
-      const int ahead = min(nst - 1 - it, D - 2);  // steps issued beyond this one before this step
-      switch (ahead) {
-        case 0: wait_vm<0>(); break;
-        case 1: wait_vm<1 * (NA + NB)>(); break;
-        case 2: wait_vm<2 * (NA + NB)>(); break;
-        case 3: wait_vm<3 * (NA + NB)>(); break;
-        default: wait_vm<4 * (NA + NB)>(); break;
-      }
-      raw_barrier();  // every wave's DMA of step it has landed, and every wave is done with step it - 1
-      const int nxt = it + D - 1;
-      compute(it % NSTAGE, [&] {
-        if (nxt < nst) issue(nxt % NSTAGE);
-      });
-    }
-    wait_lgkm0();
+  // ---- K loop: buffer it % 3 holds step it; steps it + 1 and it + 2 stay in flight meanwhile
+  // (each step is NA + NB DMA instructions per wave, so "k steps still in flight" is
+  // vmcnt(k * (NA + NB)))
+  if (nst > 0) issue(0);
+  if (nst > 1) issue(1);
+  if (nst > 2) issue(2);
+  for (int it = 0; it < nst; ++it) {
+    const int ahead = min(nst - 1 - it, 2);  // steps issued beyond this one
+    if (ahead == 2) wait_vm<2 * (NA + NB)>();
+    else if (ahead == 1) wait_vm<NA + NB>();
+    else wait_vm<0>();
+    raw_barrier();                         // every wave's DMA of step `it` has landed
+    const int buf = it % NSTAGE;
+    compute(buf);
+    wait_lgkm0();                          // this wave's fragment reads of `buf` are done
+    raw_barrier();                         // ... every wave's: the buffer may be refilled
+    if (it + NSTAGE < nst) issue(buf);
   }
 
   // ---- split-K: publish this slice, the last-arriving slice of the tile combines
@@ -423,10 +384,6 @@ constexpr Tile2 kT2[] = {{128, 256, 64, 64, 1.00f}, {256, 128, 64, 64, 1.00f}, {
 constexpr int kNT2 = sizeof(kT2) / sizeof(kT2[0]);
 
 int g_ig2_force = -1;      // tuning hooks (seg_igemm2_force_tile, seg_igemm2_tune)
-#ifndef SEG_IG2_KB
-#define SEG_IG2_KB 64
-#endif
-int g_ig2_kb = SEG_IG2_KB;  // K step of the 8-wave tiles: 64 or 32 (seg_igemm2_kb)
 int g_ig2_target = 512;    // 4-wave tiles: split-K up to this many blocks ...
 int g_ig2_minsteps = 3;    // ... keeping at least this many 64-deep K steps per slice
 
@@ -515,15 +472,6 @@ SEG_API int seg_igemm2_tune(int target_blocks, int min_steps) {
   return 0;
 }
 
-// A/B hook: the K step of the 8-wave tiles -- 64 (three buffers, two barriers per step) or 32 (six buffers, one
-// barrier, the next DMA inside the compute phase); other values leave it.  Returns the previous setting.  Bitwise
-// the same result either way.
-SEG_API int seg_igemm2_kb(int kb) {
-  const int old = g_ig2_kb;
-  if (kb == 32 || kb == 64) g_ig2_kb = kb;
-  return old;
-}
-
 // Tuning hook: force seg_conv_igemm2_bf16io's tile (index into its table; -1 = the plan).
 SEG_API int seg_igemm2_force_tile(int t) {
   g_ig2_force = t;
@@ -570,26 +518,15 @@ static int igemm2_impl(const __bf16* in, long ldin, int N, int H, int W, int Cin
     if (ks == 3) hipLaunchKernelGGL((igemm2_kernel<BM, BN, WM, WN, 3>), dim3(grid), dim3(nt), 0, stream, a); \
     else hipLaunchKernelGGL((igemm2_kernel<BM, BN, WM, WN, 1>), dim3(grid), dim3(nt), 0, stream, a);            \
   } while (0)
-  // the 8-wave tiles on 32-deep K steps (six LDS buffers, the DMA inside the compute phase): the same K order and
-  // slice boundaries in half-size steps, so bitwise the 64-deep launch
-#define SEG_I2K(BM, BN, WM, WN)                                                                                     \
-  do {                                                                                                            \
-    constexpr int nt = 64 * (BM / WM) * (BN / WN);                                                                \
-    a.nsteps = (a.K + 31) / 32;                                                                                   \
-    a.steps_per_split = 2 * p.steps_per_split;                                                                    \
-    if (ks == 3) hipLaunchKernelGGL((igemm2_kernel<BM, BN, WM, WN, 3, 32>), dim3(grid), dim3(nt), 0, stream, a); \
-    else hipLaunchKernelGGL((igemm2_kernel<BM, BN, WM, WN, 1, 32>), dim3(grid), dim3(nt), 0, stream, a);          \
-  } while (0)
   switch (p.tile) {
-    case 0: if (g_ig2_kb == 32) SEG_I2K(128, 256, 64, 64); else SEG_I2(128, 256, 64, 64); break;
-    case 1: if (g_ig2_kb == 32) SEG_I2K(256, 128, 64, 64); else SEG_I2(256, 128, 64, 64); break;
+    case 0: SEG_I2(128, 256, 64, 64); break;
+    case 1: SEG_I2(256, 128, 64, 64); break;
     case 2: SEG_I2(128, 128, 64, 64); break;
     case 3: SEG_I2(128, 64, 64, 32); break;
     case 4: SEG_I2(64, 128, 32, 64); break;
     default: SEG_I2(64, 64, 32, 32); break;
   }
 #undef SEG_I2
-#undef SEG_I2K
   SEG_RET_LAST();
 }
 

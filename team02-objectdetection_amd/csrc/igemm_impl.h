@@ -47,12 +47,6 @@ struct IgemmArgs {
   // words, [tilesM * tilesN][4] (zero before the first launch; an epoch word, never re-armed)
   unsigned* kcnt;
   int kspin;                     // seg_tile_combine's poll bound
-  // optional upsample fold (UF instantiation, 3x3 stride 1, uniform-tap loader): the A operand's channels
-  // [ucs, Cin) are not read from `in` but formed on load as nn.Upsample(x2, bilinear, align_corners=False) of
-  // `up` [N][H/2][W/2][ldup] channels [0, Cin - ucs) (src/unet.py:97-103: the decoder's cat([skip, up(x)]) --
-  // the skip part [0, ucs) is read from `in` as usual), with seg_upsample_fwd's index arithmetic and blend
-  // (lin_index, up_blend4: bitwise its output)
-  const float* up; long ldup; int ucs;
 };
 
 #ifndef SEG_IGEMM_DEPTH
@@ -93,10 +87,9 @@ struct IgemmArgs {
 // no conversion on the way into LDS.  Bitwise the fp32-weight kernel: the RNE rounding
 // is the same, done once at pack time.
 template <int BM, int BN, int WM, int WN, int KS, int BK, bool UT, typename OT = float, typename IT = float,
-          bool WB = false, bool BO = false, bool UF = false>
+          bool WB = false, bool BO = false>
 __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void igemm_conv_kernel(IgemmArgs a) {
   static_assert(!WB || std::is_same<OT, __bf16>::value, "bf16 weights feed bf16 operands");
-  static_assert(!UF || (KS == 3 && UT && std::is_same<IT, float>::value), "upsample fold: 3x3, fp32 rows, uniform tap");
   const float* wk32 = static_cast<const float*>(a.wk);
   const __bf16* wk16 = static_cast<const __bf16*>(a.wk);
   const IT* __restrict__ in = static_cast<const IT*>(a.in);
@@ -190,13 +183,6 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void igemm_conv_kernel(
   f32x4 xsc[VA / 4], xsh[VA / 4];
   int u_tap = 0, u_ci = 0;
   long u_toff0 = 0, u_toff1 = 0;
-  // UF: per A slot the pixel's image and top-left tap position (the chunk's tap adds ky, kx), the three other
-  // bilinear taps and the blend weights of the loaded chunk, and which slots take the blend (ufm)
-  constexpr int UA = UF ? A_PER : 1;
-  int uf_n[UA], uf_h0[UA], uf_w0[UA];
-  f32x4 ru[UA][3];
-  f32x4 uwt[UA];
-  unsigned ufm = 0;
   auto tap_off = [&](int t) -> long { return ((long)(t / KS) * a.W + t % KS) * a.ldin; };
   if (UT) {
 #pragma unroll
@@ -215,11 +201,6 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void igemm_conv_kernel(
         const int ho = rem / a.Wo, wo = rem - ho * a.Wo;
         const int hi0 = ho * a.stride - a.pad, wi0 = wo * a.stride - a.pad;
         u_aoff[i] = (((long)n * a.H + hi0) * a.W + wi0) * a.ldin;
-        if constexpr (UF) {
-          uf_n[i] = n;
-          uf_h0[i] = hi0;
-          uf_w0[i] = wi0;
-        }
         unsigned m = 0;
 #pragma unroll
         for (int t = 0; t < KS * KS; ++t) {
@@ -261,43 +242,14 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void igemm_conv_kernel(
         }
         xvm = 0;
       }
-      bool uf_slots = false;
-      if constexpr (UF) {
-        // the chunk's channels of this thread (cc .. cc+3 of the concat, tap `tap`): from the low-res tensor when
-        // they lie in the upsampled part (thread-uniform over its slots: only a chunk that straddles ucs diverges)
-        const int cc = wrap ? ci - a.Cin : ci;
-        ufm = 0;
-        if (cc >= a.ucs) {
-          const int Hl = a.H >> 1, Wl = a.W >> 1;
-          const float sh = (float)Hl / (float)a.H, sw = (float)Wl / (float)a.W;  // seg_upsample_fwd's up_scale
-          const float* ub = a.up + (cc - a.ucs);
 #pragma unroll
-          for (int i = 0; i < A_PER; ++i) {
-            const bool ok = (u_mask[i] >> tap) & 1u;
-            const int hi = ok ? uf_h0[i] + tap / 3 : 0, wi = ok ? uf_w0[i] + tap % 3 : 0;
-            const Lin lh = lin_index(hi, Hl, sh, 0), lw = lin_index(wi, Wl, sw, 0);
-            const float* b = ub + (long)uf_n[i] * Hl * Wl * a.ldup;
-            const float* z = reinterpret_cast<const float*>(g_zero4);
-            ra[i] = ld4(ok ? b + ((long)lh.i0 * Wl + lw.i0) * a.ldup : z);
-            ru[i][0] = ld4(ok ? b + ((long)lh.i0 * Wl + lw.i1) * a.ldup : z);
-            ru[i][1] = ld4(ok ? b + ((long)lh.i1 * Wl + lw.i0) * a.ldup : z);
-            ru[i][2] = ld4(ok ? b + ((long)lh.i1 * Wl + lw.i1) * a.ldup : z);
-            uwt[i] = f32x4{lh.l0, lh.l1, lw.l0, lw.l1};
-            if (ok) ufm |= 1u << i;
-          }
-          uf_slots = true;
-        }
-      }
-      if (!uf_slots) {
-#pragma unroll
-        for (int i = 0; i < A_PER; ++i) {
-          const bool ok = (u_mask[i] >> tap) & 1u;
-          if (KS != 1 && XF && ok) xvm |= 1u << i;
-          if constexpr (VA == 8)  // 8 bf16 as an opaque 16-byte payload
-            ra[i] = *reinterpret_cast<const f32x4*>(ok ? in + u_aoff[i] + off : zero4);
-          else
-            ra[i] = ld4(ok ? in + u_aoff[i] + off : zero4);
-        }
+      for (int i = 0; i < A_PER; ++i) {
+        const bool ok = (u_mask[i] >> tap) & 1u;
+        if (KS != 1 && XF && ok) xvm |= 1u << i;
+        if constexpr (VA == 8)  // 8 bf16 as an opaque 16-byte payload
+          ra[i] = *reinterpret_cast<const f32x4*>(ok ? in + u_aoff[i] + off : zero4);
+        else
+          ra[i] = ld4(ok ? in + u_aoff[i] + off : zero4);
       }
       const bool kin = k0 + u_kq4 < a.K;
 #pragma unroll
@@ -364,11 +316,6 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void igemm_conv_kernel(
       const int idx = tid + i * NT;
       if (A_VEC % NT == 0 || idx < A_VEC) {
         f32x4 v = ra[i];
-        if constexpr (UF) {
-          if ((ufm >> i) & 1u) {
-            v = up_blend4(ra[i], ru[i][0], ru[i][1], ru[i][2], uwt[i][0], uwt[i][1], uwt[i][2], uwt[i][3]);
-          }
-        }
         if (XF && (KS == 1 ? xch >= 0 : ((xvm >> i) & 1u) != 0)) {
           if constexpr (VA == 8) {  // 8 bf16: widen, transform, round back (RNE) as the pass would
             const bf16x8 q = __builtin_bit_cast(bf16x8, v);
@@ -786,12 +733,9 @@ int launch_igemm_bk(IgemmArgs a, int ks, hipStream_t s) {
                   (sizeof(IT) == 4 || (a.Cin % 8 == 0 && a.ldin % 8 == 0));  // bf16 A: 16-byte slots
   constexpr int NT = 64 * (BM / WM) * (BN / WN);
   if (a.xs && !ut) return (int)hipErrorInvalidValue;  // input transform: the uniform-tap loader only (Cin >= BK)
-  constexpr bool UFOK = std::is_same<OT, _Float16>::value && std::is_same<IT, float>::value && !WB;
-  if (a.up && (!UFOK || !ut || ks != 3)) return (int)hipErrorInvalidValue;
   if (a.kcnt) {  // in-launch split-K combine: only when the whole grid is co-resident (its splits combine together)
     int occ = 0;
-    const void* fn = (UFOK && a.up) ? (const void*)igemm_conv_kernel<BM, BN, WM, WN, 3, BK, true, OT, IT, WB, false, UFOK>
-                   : ks == 1 ? (ut ? (const void*)igemm_conv_kernel<BM, BN, WM, WN, 1, BK, true, OT, IT, WB, false>
+    const void* fn = ks == 1 ? (ut ? (const void*)igemm_conv_kernel<BM, BN, WM, WN, 1, BK, true, OT, IT, WB, false>
                                    : (const void*)igemm_conv_kernel<BM, BN, WM, WN, 1, BK, false, OT, IT, WB, false>)
                              : (ut ? (const void*)igemm_conv_kernel<BM, BN, WM, WN, 3, BK, true, OT, IT, WB, false>
                                    : (const void*)igemm_conv_kernel<BM, BN, WM, WN, 3, BK, false, OT, IT, WB, false>);
@@ -802,13 +746,6 @@ int launch_igemm_bk(IgemmArgs a, int ks, hipStream_t s) {
     }
   }
   g_igemm_ic_used = a.kcnt != nullptr;
-  if constexpr (UFOK) {
-    if (a.up) {
-      hipLaunchKernelGGL((igemm_conv_kernel<BM, BN, WM, WN, 3, BK, true, OT, IT, WB, false, true>), dim3(grid, splits),
-                         dim3(NT), 0, s, a);
-      SEG_RET_LAST();
-    }
-  }
 #define SEG_IG(KS, U, B) hipLaunchKernelGGL((igemm_conv_kernel<BM, BN, WM, WN, KS, BK, U, OT, IT, WB, B>), dim3(grid, splits), dim3(NT), 0, s, a)
   constexpr int VPR = BN / (16 / (int)sizeof(IT));
   // (instantiated for the training storage types only: f32 and bf16io, where operands are the storage type)
@@ -938,8 +875,7 @@ int conv_igemm_impl(const IT* in, long ldin, int N, int H, int W, int Cin, const
                     const IT* add, long ldadd, float* stat, int act, float* work, int splits, hipStream_t stream,
                     const float* xs = nullptr, const float* xb = nullptr, int xact = 0, const IT* by = nullptr,
                     long ldby = 0, const float* bsc = nullptr, const float* bsh = nullptr, const float* bmu = nullptr,
-                    int bact = 0, float* bpart = nullptr, unsigned* kcnt = nullptr, int tile = -1,
-                    const float* up = nullptr, long ldup = 0, int ucs = 0) {
+                    int bact = 0, float* bpart = nullptr, unsigned* kcnt = nullptr, int tile = -1) {
   if (!std::is_same<IT, float>::value && splits != 1) return (int)hipErrorInvalidValue;
   if ((Cin & 3) || (ldin & 3) || (ldk & 3) || (ks != 1 && ks != 3)) return (int)hipErrorInvalidValue;
   if (WB && ((ldk & 7) || ((uintptr_t)wk & 15) || splits != 1)) return (int)hipErrorInvalidValue;
@@ -963,10 +899,6 @@ int conv_igemm_impl(const IT* in, long ldin, int N, int H, int W, int Cin, const
   a.by = by; a.ldby = ldby; a.bsc = bsc; a.bsh = bsh; a.bmu = bmu; a.bact = bact; a.bpart = bpart;
   a.kcnt = splits > 1 ? kcnt : nullptr;
   a.kspin = seg_combine_spin(kSegCombineSpin);
-  a.up = up; a.ldup = ldup; a.ucs = ucs;
-  if (up && (ks != 3 || stride != 1 || pad != 1 || Ho != H || Wo != W || (H & 1) || (W & 1) || (ucs & 3) || ucs < 0 ||
-             ucs >= Cin || (ldup & 3) || ldup < Cin - ucs || ((uintptr_t)up & 15) || xs || bpart))
-    return (int)hipErrorInvalidValue;
   g_igemm_ic_used = false;
   if (bpart && !igemm_bnout_tile_ok(a.M, Cout, (int)sizeof(IT))) return (int)hipErrorInvalidValue;
   if (tile < -1 || tile >= (int)(sizeof(kTiles) / sizeof(kTiles[0])) || (tile >= 0 && bpart))

@@ -100,7 +100,6 @@ PROTOTYPES = {
     "seg_conv_igemm2_bf16io": (_I, [_V, _L, _I, _I, _I, _I, _V, _I, _V, _V, _L, _I, _I, _V, _L, _V, _V, _V]),
     "seg_igemm2_force_tile": (_I, [_I]),
     "seg_igemm2_tune": (_I, [_I, _I]),
-    "seg_igemm2_kb": (_I, [_I]),
     "seg_conv_wgrad2_ok": (_I, [_I, _I, _I, _I, _I]),
     "seg_conv_wgrad2_blocks": (_I, [_I, _I, _I]),
     "seg_conv_wgrad2_bf16io": (_I, [_V, _L, _V, _L, _I, _I, _I, _I, _I, _V, _V]),
@@ -133,8 +132,6 @@ PROTOTYPES["seg_bn_bwd_coef_bf16io"] = PROTOTYPES["seg_bn_bwd_coef"]
 PROTOTYPES["seg_conv_igemm_bnout_bf16io"] = PROTOTYPES["seg_conv_igemm_bnout"]
 PROTOTYPES["seg_conv_igemm_bf16_ic"] = PROTOTYPES["seg_conv_igemm_act_ic"]
 PROTOTYPES["seg_conv_igemm_f16_ic"] = PROTOTYPES["seg_conv_igemm_act_ic"]
-PROTOTYPES["seg_conv_igemm_f16_ic_up"] = (_I, [_V, _L, _I, _I, _I, _I, _V, _L, _I, _V, _I, _V, _V, _L, _I, _V, _L, _I,
-                                             _V, _I, _I, _V, _V])
 PROTOTYPES["seg_conv_igemm_bnout_bf16io_w16"] = PROTOTYPES["seg_conv_igemm_bnout"]
 PROTOTYPES["seg_bn_bwd_apply_bf16io"] = PROTOTYPES["seg_bn_bwd_apply"]
 PROTOTYPES["seg_conv_wgrad_bf16io"] = PROTOTYPES["seg_conv_wgrad"]

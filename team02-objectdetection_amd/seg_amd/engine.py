@@ -340,12 +340,10 @@ class ConvOp:
              rt.ptr(r) if r is not None else None, r.ld if r is not None else 0, rt.ptr(o), o.ld, s)
 
     # -- inference (BatchNorm folded into the conv: Program.fold)
-    def forward_folded(self, rt, up=None):
+    def forward_folded(self, rt):
         """act(conv(x, W') + b') (+ residual) in one launch; W', b' from seg_bn_fold_batch.
         A lazy producer writes its activated output into its `y` buffer (= `out`), so its
-        depthwise consumer reads it without the on-load BN transform.  up: the UpsampleOp whose
-        output is this conv's input channels [ucs, Cin) -- formed on load (seg_conv_igemm_f16_ic_up)
-        instead of by the upsample launch (Run.forward_folded decides)."""
+        depthwise consumer reads it without the on-load BN transform."""
         s, i, o = rt.stream, self.inp, self.out
         act = self.act if self.bn is not None else ACT_NONE
         if self.kind == "dw":
@@ -374,12 +372,6 @@ class ConvOp:
                 torch.empty(splits * M * self.cout if splits > 1 else 1, device=rt.device, dtype=torch.float32),
                 torch.zeros(4 * ntl, device=rt.device, dtype=torch.int32), splits, tile)
         work, cnt, splits, tile = bufs
-        if up is not None:
-            lo = up.low
-            rt.call("seg_conv_igemm_f16_ic_up", rt.ptr(i), i.ld, i.N, i.H, i.W, self.cin_pad, rt.ptr(lo), lo.ld,
-                    up.out.off - i.off, wk, ldk, bias, rt.ptr(o), o.ld, self.cout, rt.ptr(r) if r is not None else None,
-                    r.ld if r is not None else 0, act, work.data_ptr(), splits, tile, cnt.data_ptr(), s)
-            return
         rt.call(_FOLDED_CONV[rt.prog.math] + "_ic", rt.ptr(i), i.ld, i.N, i.H, i.W, self.cin_pad, wk, ldk, bias,
                 rt.ptr(o), o.ld, o.H, o.W, self.cout, self.ks, self.stride, self.pad,
                 rt.ptr(r) if r is not None else None, r.ld if r is not None else 0, act, work.data_ptr(), splits, tile,
@@ -1366,7 +1358,6 @@ class Run:
         groups = self.prog.mbconv_groups() if MBCONV and f16 else {}
         head = self.prog.pw2_head() if PW2 and f16 else None
         k = start
-        lvl = -1  # decoder upsample index (UPFOLD bits)
         while k < len(ops):
             g = groups.get(k)
             if g is not None:
@@ -1382,30 +1373,11 @@ class Run:
                 k += 2
                 continue
             op = ops[k]
-            nxt = ops[k + 1] if k + 1 < len(ops) else None
-            if isinstance(op, UpsampleOp):
-                lvl += 1
-                if f16 and (UPFOLD >> lvl) & 1 and self._upfold_ok(op, nxt):
-                    nxt.forward_folded(self, up=op)  # the decoder conv forms the x2 upsample on load
-                    k += 2
-                    continue
             if isinstance(op, ConvOp):
                 op.forward_folded(self)
             else:
                 op.forward(self)
             k += 1
-
-    @staticmethod
-    def _upfold_ok(up, conv):
-        """seg_conv_igemm_f16_ic_up applies: the next op is a plain dense 3x3 conv over exactly the concat buffer
-        the upsample writes into (its channels [ucs, Cin) = the upsample's output, the skip before them)."""
-        if not isinstance(conv, ConvOp) or conv.kind != "igemm" or conv.ks != 3 or conv.stride != 1 or conv.pad != 1:
-            return False
-        i, o, lo = conv.inp, up.out, up.low
-        ucs = o.off - i.off
-        return (i.buf == o.buf and i.C == conv.cin and o.off + o.C == i.off + i.C and ucs > 0 and ucs % 4 == 0
-                and conv.cin_pad == conv.cin and i.H % 2 == 0 and i.W % 2 == 0 and lo.H * 2 == i.H
-                and lo.W * 2 == i.W and lo.C == o.C and lo.ld % 4 == 0 and conv.fk_pack is not None)
 
     def _mbconv(self, k, g):
         """One fused inverted residual (expand?, depthwise, project) of the folded forward."""
@@ -1500,22 +1472,6 @@ MBCONV = True
 STEM_PRE = True
 PW2 = True
 PLAN_B1 = True
-# ... and the decoder's x2 upsample formed on load by the conv that consumes the concat (seg_conv_igemm_f16_ic_up,
-# VERDICT r5 item 6): bit k of SEG_UPFOLD folds the (k+1)-th decoder level's upsample (up1 = bit 0).  Measured
-# (profiles/r06/ab_upfold*.txt): all four folded 2480 vs 2705 frames/s -- four float4 loads and a blend per operand
-# slot cost the latency-bound batch-1 convs more than the launches save; per-level mask below
-UPFOLD = int(os.environ.get("SEG_UPFOLD", "0"), 0)
-# igemm2's K step for the 8-wave tiles (SEG_IG2_KB=32 / 64; unset: the library default) -- A/B hook, applied when a
-# program is built
-IG2_KB = os.environ.get("SEG_IG2_KB")
-
-
-def _apply_ig2_kb():
-    global IG2_KB
-    query("seg_igemm2_kb", int(IG2_KB))
-    IG2_KB = None
-
-
 _SIDE = {}
 
 
@@ -1577,8 +1533,6 @@ def debug_pool_positions(model) -> dict:
 
 
 def get_program(model, N, H, W, math=None) -> Program:
-    if IG2_KB is not None:
-        _apply_ig2_kb()
     cache = model.__dict__.setdefault(_PROGRAM_CACHE_ATTR, {})
     math = math or model.__dict__.get("_segamd_math", "f32")
     key = (N, H, W, math)

@@ -9,9 +9,7 @@ bf16io convs (csrc/igemm2.hip).
     reproducible call after call on one workspace, and leave its tickets zero;
   * BatchNorm tile partials: the tile sums add up to the fp64 column sums, and each
     tile's M2 equals the fp64 M2 about that tile's mean;
-  * the addend (data-gradient accumulation) and bias paths;
-  * both K-step forms of the 8-wave tiles (seg_igemm2_kb 64: three LDS buffers; 32, round 6: six buffers with the
-    next step's DMA inside the compute phase): the same results bit for bit.
+  * the addend (data-gradient accumulation) and bias paths.
 """
 import pytest
 import torch
@@ -62,15 +60,8 @@ CASES = [  # (N, Cin, Cout, H, W, ks): split-K, dgrad-shaped, ragged M, taps spa
     (32, 320, 1280, 8, 16, 1), (32, 24, 144, 16, 32, 1), (8, 152, 64, 32, 64, 3)]
 
 
-@pytest.fixture(params=[64, 32], ids=["kb64", "kb32"])
-def kb(request):
-    old = query("seg_igemm2_kb", request.param)
-    yield request.param
-    query("seg_igemm2_kb", old)
-
-
 @pytest.mark.parametrize("N,Cin,Cout,H,W,ks", CASES)
-def test_igemm2_vs_fp64_and_generic(N, Cin, Cout, H, W, ks, kb):
+def test_igemm2_vs_fp64_and_generic(N, Cin, Cout, H, W, ks):
     M = N * H * W
     ok, (tile_rows, ntiles, splits, work_floats) = plan(M, Cout, Cin, ks)
     assert ok, "the plan must apply to these shapes"
@@ -128,7 +119,7 @@ def test_igemm2_plan_rejects_padding_heavy_shapes():
 
 
 @pytest.mark.parametrize("tile", range(6))
-def test_igemm2_every_tile(tile, kb):
+def test_igemm2_every_tile(tile):
     """Each tile of the table, forced (seg_igemm2_force_tile), on one 3x3 and one 1x1 shape: unsplit
     launches bitwise equal to the generic kernel, split ones within the bf16 rounding of fp64."""
     try:

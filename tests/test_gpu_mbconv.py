@@ -211,81 +211,3 @@ def test_predictor_combine_hand_off_bitwise(spin):
         call("seg_set_combine_spin", -1)
     assert torch.equal(p(f), m0)
 
-
-@pytest.mark.parametrize("N,H,W,cs,cu,Cout,splits", [(1, 16, 32, 64, 1280, 256, 8), (1, 32, 64, 32, 256, 128, 1),
-                                                      (2, 10, 14, 24, 40, 20, 1), (1, 64, 128, 24, 128, 64, 4)])
-def test_upsample_fold_equals_upsample_then_conv(N, H, W, cs, cu, Cout, splits):
-    """seg_conv_igemm_f16_ic_up: the decoder conv forming cat([skip, up(x)]) on load is bitwise
-    seg_upsample_fwd into the concat slice followed by seg_conv_igemm_f16_ic -- the same index arithmetic and blend
-    (common.h bilerp4) per operand element, the same operand rounding and K partition."""
-    g = torch.Generator().manual_seed(H * W + cs)
-    Cin = cs + cu
-    low = torch.randn(N * (H // 2) * (W // 2), cu + 4, generator=g).to(DEV)  # ldup > cu: strided rows
-    cat = torch.randn(N * H * W, Cin, generator=g).to(DEV)  # [skip | stale rows the fold must not read]
-    w = (torch.randn(Cout, Cin, 3, 3, generator=g) / (9 * Cin) ** 0.5).to(DEV)
-    b = torch.randn(Cout, generator=g).to(DEV)
-    ldk = 9 * Cin
-    wk = torch.empty(Cout * ldk, device=DEV)
-    call("seg_pack_conv_weight", w.data_ptr(), wk.data_ptr(), Cout, Cin, 3, ldk, 0, Cin, S())
-    M = N * H * W
-    outs = []
-    for fold in (False, True):
-        work = torch.empty(max(splits * M * Cout, 1), device=DEV)
-        cnt = torch.zeros(4 * query("seg_conv_igemm_tiles", M, Cout) + 64, device=DEV, dtype=torch.int32)
-        out = torch.full((M, Cout + 4), float("nan"), device=DEV)
-        c = cat.clone()
-        if fold:
-            c[:, cs:] = float("nan")  # the upsampled channels are never read
-            call("seg_conv_igemm_f16_ic_up", c.data_ptr(), Cin, N, H, W, Cin, low.data_ptr(), cu + 4, cs,
-                 wk.data_ptr(), ldk, b.data_ptr(), out.data_ptr(), Cout + 4, Cout, None, 0, 1, work.data_ptr(), splits,
-                 -1, cnt.data_ptr(), S())
-        else:
-            call("seg_upsample_fwd", low.data_ptr(), cu + 4, N, H // 2, W // 2, cu, c[:, cs:].data_ptr(), Cin, H, W, 0,
-                 S())
-            call("seg_conv_igemm_f16_ic", c.data_ptr(), Cin, N, H, W, Cin, wk.data_ptr(), ldk, b.data_ptr(),
-                 out.data_ptr(), Cout + 4, H, W, Cout, 3, 1, 1, None, 0, 1, work.data_ptr(), splits, -1,
-                 cnt.data_ptr(), S())
-        torch.cuda.synchronize()
-        outs.append(out)
-    o0, o1 = outs[0][:, :Cout], outs[1][:, :Cout]
-    assert not torch.isnan(o1).any(), f"{int(torch.isnan(o1).sum())} NaN outputs: the fold read a stale concat row"
-    diff = (o0 != o1)
-    print(f"upsample fold {N}x{H}x{W} {cs}+{cu}->{Cout} splits {splits}: {int(diff.sum())} of {diff.numel()} differ, "
-          f"max |d| {float((o0 - o1).abs().max()):.3e}, rel {float((o0 - o1).norm() / o0.norm()):.3e}")
-    assert torch.equal(o0, o1)
-    assert bool(outs[1][:, Cout:].isnan().all()), "nothing written beyond Cout"
-    # and against float64 of the same operand rounding
-    up = F.interpolate(low[:, :cu].view(N, H // 2, W // 2, cu).permute(0, 3, 1, 2).double(), scale_factor=2,
-                       mode="bilinear", align_corners=False)
-    x = torch.cat([cat[:, :cs].view(N, H, W, cs).permute(0, 3, 1, 2).double(), up], 1)
-    ref = (F.conv2d(h16(x), h16(w), padding=1) + b.double()[None, :, None, None]).clamp(min=0)
-    ref = ref.permute(0, 2, 3, 1).reshape(M, Cout)
-    assert float((outs[1][:, :Cout].double() - ref).norm() / ref.norm()) < 2e-3
-
-
-def test_predictor_upsample_fold_bitwise():
-    """The fp16 Predictor with the 4 decoder upsamples formed on load (engine.UPFOLD) is bitwise the Predictor with
-    the upsample launches, and its graph replay equals eager."""
-    from seg_amd.infer import Predictor
-    import numpy as np
-    model = deterministic_init(MobileNetV2UNet(10), seed=17, random_running_stats=True).to(DEV).eval()
-    f = (np.random.default_rng(2).random((720, 1280, 3)) * 255).astype(np.uint8)
-    saved = engine.UPFOLD
-    try:
-        engine.UPFOLD = 0
-        p0 = Predictor(model, frame_hw=(720, 1280), graph=False, math="f16")
-        m0 = p0(f).clone()
-        l0 = p0.logits()
-        engine.UPFOLD = 0b1111  # every level
-        p1 = Predictor(model, frame_hw=(720, 1280), graph=True, math="f16")
-        m1 = p1(f).clone()
-        l1 = p1.logits()
-        p2 = Predictor(model, frame_hw=(720, 1280), graph=False, math="f16")
-        m2 = p2(f).clone()
-    finally:
-        engine.UPFOLD = saved
-    folds = [k for k, op in enumerate(p1.prog.ops)
-             if isinstance(op, engine.UpsampleOp) and engine.Run._upfold_ok(op, p1.prog.ops[k + 1])]
-    assert len(folds) == 4, folds
-    assert torch.equal(l1, l0) and torch.equal(m1, m0)
-    assert torch.equal(m2, m1) and torch.equal(p2.logits(), l1)

@@ -53,7 +53,6 @@ def main():
     ap.add_argument("--only", default="")
     ap.add_argument("--kernel", default="both", choices=("ig2", "gen", "both", "halo", "all"))
     ap.add_argument("--set", default="mnv2", choices=("mnv2", "unet"))
-    ap.add_argument("--kb", type=int, default=0, help="igemm2 K step: 64, 32 or 0 = both")
     ap.add_argument("--reps", type=int, default=20)
     a = ap.parse_args()
     only = set(a.only.split(",")) if a.only else None
@@ -75,13 +74,9 @@ def main():
         res = []
         if plan and a.kernel in ("ig2", "both", "all"):
             work = torch.zeros(max(plan[3], 1), device="cuda")
-            for kbv in ((64, 32) if a.kb == 0 else (a.kb,)):  # the 8-wave tiles' K step (seg_igemm2_kb)
-                old = engine.query("seg_igemm2_kb", kbv)
-                t = timeit(lambda: call("seg_conv_igemm2_bf16io", x.data_ptr(), Cin, N, H, W, Cin, wk.data_ptr(), ldk,
-                                        None, y.data_ptr(), Cout, Cout, ks, None, 0, None, work.data_ptr(), s), a.reps)
-                engine.query("seg_igemm2_kb", old)
-                res.append(f"ig2/kb{kbv} {t * 1e6:7.1f} us {flops / t / 1e12:6.0f} TF/s (tile rows {plan[0]}, "
-                           f"splits {plan[2]})")
+            t = timeit(lambda: call("seg_conv_igemm2_bf16io", x.data_ptr(), Cin, N, H, W, Cin, wk.data_ptr(), ldk, None,
+                                    y.data_ptr(), Cout, Cout, ks, None, 0, None, work.data_ptr(), s), a.reps)
+            res.append(f"ig2 {t * 1e6:7.1f} us {flops / t / 1e12:6.0f} TF/s (tile rows {plan[0]}, splits {plan[2]})")
         if a.kernel in ("halo", "all") and engine.query("seg_conv_halo_pick", N, H, W, Cin, Cout):
             t = timeit(lambda: call("seg_conv_halo_bf16io_w16", x.data_ptr(), Cin, N, H, W, Cin, wk.data_ptr(),
                                     ldk, None, y.data_ptr(), Cout, Cout, None, 0, None, s), a.reps)

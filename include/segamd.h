@@ -622,6 +622,20 @@ int seg_conv_igemm2_bf16io(const seg_bf16* in, long ldin, int N, int H, int W, i
 /* Round 4: the plan also picks 4-wave 128x128 / 128x64 / 64x128 / 64x64 tiles (small-image 1x1 and 3x3
  * convs of the MobileNetV2 encoder); seg_igemm2_force_tile(t) forces table entry t (-1 = the plan). */
 int seg_igemm2_force_tile(int t);
+/* Round 6: seg_conv_igemm2_bf16io's K loop issues the LDS-DMA of step k+2 between the MFMAs of step k
+ * (one barrier per step) -- 1, the default -- or, 0, all of a step's DMA after a second barrier (the
+ * round-3 loop); < 0 leaves the setting.  Returns the previous one.  Bitwise the same results. */
+int seg_igemm2_il(int on);
+
+/* Round 6: the weight gradient of the wide 3x3 / 1x1 convs on bf16 rows, built like seg_conv_igemm2_bf16io
+ * (src/unet.py:58,61 double_conv; loss.backward() at src/train.py:38): 8-wave blocks, 64-pixel K steps of
+ * one image row staged by LDS-DMA (three stages), ds_read_b64_tr_b16 fragments, fp32 partial slabs
+ * part[splits][Cout][ks*ks*Cin] (seg_conv_wgrad's layout, summed by seg_conv_wgrad_reduce).
+ * seg_conv_wgrad3_splits: the slab count, 0 when the kernel does not apply (Cin, Cout % 8, Cout >= 32,
+ * W % 64, little tile padding). */
+int seg_conv_wgrad3_splits(int N, int H, int W, int Cin, int Cout, int ks);
+int seg_conv_wgrad3_bf16io(const seg_bf16* dy, long lddy, const seg_bf16* x, long ldx, int N, int H, int W, int Cin,
+                           int Cout, int ks, float* part, hipStream_t stream);
 /* Tuning hook: split-K of the 4-wave tiles up to target_blocks blocks with >= min_steps 64-deep K
  * steps per slice (defaults 512, 3); values <= 0 keep the current setting. */
 int seg_igemm2_tune(int target_blocks, int min_steps);

@@ -99,6 +99,9 @@ PROTOTYPES = {
     "seg_conv_pw": (_I, [_V, _L, _L, _I, _V, _I, _V, _V, _L, _I, _V, _L, _V, _V, _V, _I, _V]),
     "seg_conv_igemm2_bf16io": (_I, [_V, _L, _I, _I, _I, _I, _V, _I, _V, _V, _L, _I, _I, _V, _L, _V, _V, _V]),
     "seg_igemm2_force_tile": (_I, [_I]),
+    "seg_igemm2_il": (_I, [_I]),
+    "seg_conv_wgrad3_splits": (_I, [_I, _I, _I, _I, _I, _I]),
+    "seg_conv_wgrad3_bf16io": (_I, [_V, _L, _V, _L, _I, _I, _I, _I, _I, _I, _V, _V]),
     "seg_igemm2_tune": (_I, [_I, _I]),
     "seg_conv_wgrad2_ok": (_I, [_I, _I, _I, _I, _I]),
     "seg_conv_wgrad2_blocks": (_I, [_I, _I, _I]),

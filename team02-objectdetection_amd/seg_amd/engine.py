@@ -540,6 +540,9 @@ class ConvOp:
         """Bias gradient (column sum of dY), weight gradient (split-K slabs + fixed-order
         reduce) and the DDP readiness hook, all on stream `s`."""
         y, M = self.y, self.y.M
+        if DIAG_SKIP_WGRAD is not None and DIAG_SKIP_WGRAD[0] <= getattr(rt, "cur_op", -1) < DIAG_SKIP_WGRAD[1]:
+            rt.params_done(self.params(), s)  # diagnostics only: no conv weight / bias gradients (wrong training)
+            return
         if self.conv.bias is not None and self.conv.bias.requires_grad:
             if self.bn is not None and ZERO_BN_BIAS:
                 # conv -> train-mode BatchNorm (src/unet.py:58-59,61-62): the bias shifts its whole channel by
@@ -1522,6 +1525,7 @@ class Run:
             self._side_ctx = torch.cuda.StreamContext(self.side)  # re-entered by every fork
         try:
             for k in range(len(self.prog.ops) - 1, -1, -1):
+                self.cur_op = k
                 if self.rec is not None:
                     self.rec.label = f"{k}:bwd"
                 self.prog.ops[k].backward(self)
@@ -1585,6 +1589,11 @@ BN_MERGE = os.environ.get("SEG_BN_MERGE", "1") == "1"
 BWX = os.environ.get("SEG_BWX", "0") == "1"
 BWX_W = os.environ.get("SEG_BWX_W", "1") == "1"
 
+# Diagnostics only (wrong training): SEG_DIAG_SKIP_WGRAD=1 issues no conv weight / bias gradient at all -- the step
+# time of the main stream's work alone, with no side-stream contention (the contention budget, DESIGN round 6)
+# (SEG_DIAG_SKIP_WGRAD=lo:hi skips only the program ops lo <= k < hi)
+_dsw = os.environ.get("SEG_DIAG_SKIP_WGRAD", "0")
+DIAG_SKIP_WGRAD = None if _dsw == "0" else (0, 1 << 30) if _dsw == "1" else tuple(int(v) for v in _dsw.split(":"))
 # Diagnostics (tests flip these): the Winograd transforms one at a time (parity attribution,
 # tests/test_gpu_unet_cfg5.py) ...
 WINOGRAD_WGRAD = True  # the F(3x3,2x2) weight gradients

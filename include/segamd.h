@@ -129,43 +129,6 @@ int seg_conv_igemm_bnout(const float* in, long ldin, int N, int H, int W, int Ci
                          const float* by, long ldby, const float* bscale, const float* bshift,
                          const float* bmean, int bact, float* bpart, hipStream_t stream);
 
-/* BatchNorm backward formed on load ("bwx", round 6).  The backward of conv -> train-mode BatchNorm ->
- * act (src/unet.py:57-63 double_conv; torchvision's Conv2dNormActivation / InvertedResidual via
- * src/unet.py:15-19; loss.backward() at src/train.py:38) needs dY = d(conv output) =
- * seg_bnbwd4(dA, y) for BOTH the conv's data gradient and its weight gradient.  Instead of an apply pass
- * writing dY, these entries read dA (the gradient of the BN layer's activated output, `da` / `in`) and the
- * raw conv output y (gy / by) and form dY in their operand loaders -- bit for bit the tensor
- * seg_bn_bwd_apply(_bf16io) would have written (bf16 storage: rounded the same way), so their results
- * equal the apply-then-consumer pair exactly.  gst / bst = the layer's statistics + coefficient planes
- * st[7][C] = (mean, invstd, scale, shift, k1, k2, k3): the forward's seg_bn_stats* output with
- * seg_bn_bwd_coef* / seg_bn_bwd_finalize_tiles writing coef = st + 4*C.  gact / bact = the layer's
- * activation.  Padding taps and rows / channels outside the tensors stay zero. */
-/* 1 when seg_conv_igemm_bwx (bf16 = 0) / seg_conv_igemm_bwx_bf16io_w16 (bf16 = 1) takes a stride-1 data
- * gradient over Cin dY channels with a ks x ks kernel. */
-int seg_conv_igemm_bwx_ok(int Cin, int ks, int bf16);
-/* seg_conv_igemm_bnout with dY formed on load (by .. bpart optional: bpart null = no BN partials). */
-int seg_conv_igemm_bwx(const float* in, long ldin, int N, int H, int W, int Cin, const float* gy, long ldgy,
-                       const float* gst, int gact, const float* wk, int ldk, float* out, long ldout, int Cout, int ks,
-                       const float* add, long ldadd, const float* by, long ldby, const float* bscale,
-                       const float* bshift, const float* bmean, int bact, float* bpart, hipStream_t stream);
-/* seg_conv_pw (thin-K 1x1 data gradient, no bias / statistics) with dY formed on load. */
-int seg_conv_pw_bwx(const float* da, long ldda, const float* gy, long ldgy, const float* gst, int gact, long M, int K,
-                    const float* wk, int ldk, float* out, long ldout, int N, const float* add, long ldadd,
-                    hipStream_t stream);
-/* seg_dw_dgrad with dY formed on load. */
-int seg_dw_dgrad_bwx(const float* da, long ldda, const float* gy, long ldgy, const float* gst, int gact, int N, int Ho,
-                     int Wo, int C, const float* wk, float* dx, long lddx, int H, int W, int stride, int accumulate,
-                     hipStream_t stream);
-/* seg_dw_wgrad with dY formed on load (in_scale nullable: the input's lazy BN as seg_dw_wgrad). */
-int seg_dw_wgrad_bwx(const float* da, long ldda, const float* by, long ldby, const float* bst, int bact,
-                     const float* x, long ldx, int N, int H, int W, int C, const float* in_scale, const float* in_shift,
-                     int in_act, int Ho, int Wo, int stride, float* part, hipStream_t stream);
-/* seg_conv_wgrad with dY formed on load (in_scale nullable: the input's lazy BN as seg_conv_wgrad_xf). */
-int seg_conv_wgrad_bwx(const float* da, long ldda, const float* gy, long ldgy, const float* gst, int gact,
-                       const float* x, long ldx, int N, int H, int W, int Cin, int Ho, int Wo, int Cout, int ks,
-                       int stride, int pad, float* part, int splits, const float* in_scale, const float* in_shift,
-                       int in_act, hipStream_t stream);
-
 /* Row tiles (and their height) seg_conv_igemm uses for an M x Cout output. */
 /* Tuning hook: force tile configuration t (0..7) for the following
  * seg_conv_igemm calls of this process, -1 = the built-in cost model. */
@@ -474,25 +437,6 @@ int seg_colsum_bf16io(const seg_bf16* y, long ldy, long M, int C, float* work, f
     stream);
 int seg_dw_fwd_bf16io(const seg_bf16* in, long ldin, int N, int H, int W, int C, const float* in_scale, const float*
     in_shift, int in_act, const float* wk, seg_bf16* out, long ldout, int Ho, int Wo, int stride, hipStream_t stream);
-int seg_conv_igemm_bwx_bf16io_w16(const seg_bf16* in, long ldin, int N, int H, int W, int Cin, const seg_bf16* gy,
-                                  long ldgy, const float* gst, int gact, const seg_bf16* wk, int ldk, seg_bf16* out,
-                                  long ldout, int Cout, int ks, const seg_bf16* add, long ldadd, const seg_bf16* by,
-                                  long ldby, const float* bscale, const float* bshift, const float* bmean, int bact,
-                                  float* bpart, hipStream_t stream);
-int seg_conv_pw_bwx_bf16io(const seg_bf16* da, long ldda, const seg_bf16* gy, long ldgy, const float* gst, int gact,
-                           long M, int K, const seg_bf16* wk, int ldk, seg_bf16* out, long ldout, int N,
-                           const seg_bf16* add, long ldadd, hipStream_t stream);
-int seg_dw_dgrad_bwx_bf16io(const seg_bf16* da, long ldda, const seg_bf16* gy, long ldgy, const float* gst, int gact,
-                            int N, int Ho, int Wo, int C, const float* wk, seg_bf16* dx, long lddx, int H, int W,
-                            int stride, int accumulate, hipStream_t stream);
-int seg_dw_wgrad_bwx_bf16io(const seg_bf16* da, long ldda, const seg_bf16* by, long ldby, const float* bst, int bact,
-                            const seg_bf16* x, long ldx, int N, int H, int W, int C, const float* in_scale,
-                            const float* in_shift, int in_act, int Ho, int Wo, int stride, float* part,
-                            hipStream_t stream);
-int seg_conv_wgrad_bwx_bf16io(const seg_bf16* da, long ldda, const seg_bf16* gy, long ldgy, const float* gst,
-                              int gact, const seg_bf16* x, long ldx, int N, int H, int W, int Cin, int Ho, int Wo,
-                              int Cout, int ks, int stride, int pad, float* part, int splits, const float* in_scale,
-                              const float* in_shift, int in_act, hipStream_t stream);
 int seg_dw_dgrad_bf16io(const seg_bf16* dy, long lddy, int N, int Ho, int Wo, int C, const float* wk, seg_bf16* dx,
     long lddx, int H, int W, int stride, int accumulate, hipStream_t stream);
 int seg_conv_igemm_bnout_bf16io(const seg_bf16* in, long ldin, int N, int H, int W, int Cin, const float* wk,
@@ -622,20 +566,6 @@ int seg_conv_igemm2_bf16io(const seg_bf16* in, long ldin, int N, int H, int W, i
 /* Round 4: the plan also picks 4-wave 128x128 / 128x64 / 64x128 / 64x64 tiles (small-image 1x1 and 3x3
  * convs of the MobileNetV2 encoder); seg_igemm2_force_tile(t) forces table entry t (-1 = the plan). */
 int seg_igemm2_force_tile(int t);
-/* Round 6: seg_conv_igemm2_bf16io's K loop issues the LDS-DMA of step k+2 between the MFMAs of step k
- * (one barrier per step) -- 1, the default -- or, 0, all of a step's DMA after a second barrier (the
- * round-3 loop); < 0 leaves the setting.  Returns the previous one.  Bitwise the same results. */
-int seg_igemm2_il(int on);
-
-/* Round 6: the weight gradient of the wide 3x3 / 1x1 convs on bf16 rows, built like seg_conv_igemm2_bf16io
- * (src/unet.py:58,61 double_conv; loss.backward() at src/train.py:38): 8-wave blocks, 64-pixel K steps of
- * one image row staged by LDS-DMA (three stages), ds_read_b64_tr_b16 fragments, fp32 partial slabs
- * part[splits][Cout][ks*ks*Cin] (seg_conv_wgrad's layout, summed by seg_conv_wgrad_reduce).
- * seg_conv_wgrad3_splits: the slab count, 0 when the kernel does not apply (Cin, Cout % 8, Cout >= 32,
- * W % 64, little tile padding). */
-int seg_conv_wgrad3_splits(int N, int H, int W, int Cin, int Cout, int ks);
-int seg_conv_wgrad3_bf16io(const seg_bf16* dy, long lddy, const seg_bf16* x, long ldx, int N, int H, int W, int Cin,
-                           int Cout, int ks, float* part, hipStream_t stream);
 /* Tuning hook: split-K of the 4-wave tiles up to target_blocks blocks with >= min_steps 64-deep K
  * steps per slice (defaults 512, 3); values <= 0 keep the current setting. */
 int seg_igemm2_tune(int target_blocks, int min_steps);

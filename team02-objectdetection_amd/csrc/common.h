@@ -92,47 +92,6 @@ __device__ __forceinline__ f32x4 seg_bnbwd4(f32x4 g, f32x4 v, f32x4 sc, f32x4 sh
   return o;
 }
 
-// BatchNorm backward formed on load ("bwx"): a consumer of dY = d(conv output) -- the conv's data
-// gradient or weight gradient -- reads dA (the gradient of the BN layer's activated output) and y
-// (the raw conv output) and forms dY with seg_bnbwd4, so the apply pass and its dY tensor disappear.
-// The layer's statistics and backward coefficients are planes of one array st[7][C] = (mean,
-// invstd, scale, shift, k1, k2, k3) (the forward's statistics; seg_bn_bwd_coef /
-// seg_bn_bwd_finalize_tiles write k1..k3 at st + 4C).  Out-of-image taps stay zero (the transform
-// applies to real pixels only), and on bf16 storage the result is rounded as the pass would store it:
-// the consumer's operand is the apply pass's dY bit for bit.
-struct SegBwx4 {
-  f32x4 sc, sh, mu, k1, k2, k3;
-};
-__device__ __forceinline__ SegBwx4 seg_bwx_ld(const float* st, int C, int c) {
-  SegBwx4 k;
-  k.mu = ld4(st + c);
-  k.sc = ld4(st + 2 * C + c);
-  k.sh = ld4(st + 3 * C + c);
-  k.k1 = ld4(st + 4 * C + c);
-  k.k2 = ld4(st + 5 * C + c);
-  k.k3 = ld4(st + 6 * C + c);
-  return k;
-}
-__device__ __forceinline__ f32x4 seg_bwx4(f32x4 g, f32x4 v, const SegBwx4& k, int act) {
-  return seg_bnbwd4(g, v, k.sc, k.sh, k.mu, k.k1, k.k2, k.k3, act);
-}
-// 8 bf16 channels: 16-byte payloads of dA and y -> the 16-byte bf16 payload of dY (RNE)
-__device__ __forceinline__ f32x4 seg_bwx8_bf16(f32x4 graw, f32x4 vraw, const SegBwx4& lo, const SegBwx4& hi,
-                                               int act) {
-  const bf16x8 g = __builtin_bit_cast(bf16x8, graw), v = __builtin_bit_cast(bf16x8, vraw);
-  const f32x4 o0 = seg_bwx4(__builtin_convertvector(__builtin_shufflevector(g, g, 0, 1, 2, 3), f32x4),
-                            __builtin_convertvector(__builtin_shufflevector(v, v, 0, 1, 2, 3), f32x4), lo, act);
-  const f32x4 o1 = seg_bwx4(__builtin_convertvector(__builtin_shufflevector(g, g, 4, 5, 6, 7), f32x4),
-                            __builtin_convertvector(__builtin_shufflevector(v, v, 4, 5, 6, 7), f32x4), hi, act);
-  return __builtin_bit_cast(f32x4, seg_cat8(__builtin_convertvector(o0, bf16x4), __builtin_convertvector(o1, bf16x4)));
-}
-// fp32 value as a tensor of storage type T holds it (bf16: RNE round trip)
-template <typename T>
-__device__ __forceinline__ f32x4 seg_as_stored(f32x4 v) {
-  if constexpr (sizeof(T) == 2) return __builtin_convertvector(__builtin_convertvector(v, bf16x4), f32x4);
-  else return v;
-}
-
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

@@ -70,35 +70,6 @@ struct RowIn {
   }
 };
 
-// Row reader of a data gradient whose dY is formed on load (BatchNorm backward on load, common.h
-// SegBwx4): dY = seg_bnbwd4(dA, y) at in-image pixels (as the apply pass would have stored it), zero
-// outside -- dA and y each with their own row stride.
-template <typename T>
-struct RowInBw {
-  const T* p;      // dA row (clamped) + channel offset
-  const T* q;      // y row (clamped) + channel offset
-  long ld, ldq;
-  int W;
-  bool ok;
-  SegBwx4 k;
-  int act;
-  __device__ __forceinline__ void init(const T* base, const T* ybase, int h, int H, int W_, long ld_, long ldq_) {
-    ok = (unsigned)h < (unsigned)H;
-    const int hc = h < 0 ? 0 : (h >= H ? H - 1 : h);
-    p = base + (long)hc * W_ * ld_;
-    q = ybase + (long)hc * W_ * ldq_;
-    ld = ld_;
-    ldq = ldq_;
-    W = W_;
-  }
-  __device__ __forceinline__ f32x4 at(int wi) const {
-    const int wc = wi < 0 ? 0 : (wi >= W ? W - 1 : wi);
-    const f32x4 v = seg_as_stored<T>(seg_bwx4(ld4(p + (long)wc * ld), ld4(q + (long)wc * ldq), k, act));
-    const bool in = ok && (unsigned)wi < (unsigned)W;
-    return in ? v : f32x4{0.f, 0.f, 0.f, 0.f};
-  }
-};
-
 // Store a strip's TW results (after all of its loads were issued: no store sits
 // between two loads, so the scheduler can batch the strip's loads).  CHECK: the
 // strip crosses the row end (only the last strip of a row when TW does not divide it).
@@ -119,17 +90,13 @@ __device__ __forceinline__ void store_strip(T* o, long ld, const f32x4 (&acc)[TW
 // of dY with the flipped kernel.  ACC: out += (the data gradient's accumulate).
 // EPI (inference, BN folded into wk): out = act(acc + obias) -- the folded
 // BatchNorm shift and the ReLU6 applied in the epilogue.
-// BW (stride-1 data gradient only): `in` is dA of the BatchNorm layer after this conv and the dY rows are
-// formed on load from it and gy [.][ldgy] with the layer's st[7][C] planes gst (RowInBw).
-template <int S, bool LAZY, bool FLIP, bool ACC, bool EPI = false, typename T = float, bool BW = false>
+template <int S, bool LAZY, bool FLIP, bool ACC, bool EPI = false, typename T = float>
 __global__ __launch_bounds__(256) void dw_fwd_kernel(const T* __restrict__ in, long ldin, int N, int H, int W,
                                                      int C, const float* __restrict__ isc,
                                                      const float* __restrict__ ish, int iact,
                                                      const float* __restrict__ wk, T* __restrict__ out,
                                                      long ldout, int Ho, int Wo,
-                                                     const float* __restrict__ obias, int oact,
-                                                     const T* __restrict__ gy = nullptr, long ldgy = 0,
-                                                     const float* __restrict__ gst = nullptr, int gact = 0) {
+                                                     const float* __restrict__ obias, int oact) {
   const int CG = C >> 2;
   const int SPR = (Wo + TW - 1) / TW;
   const long total = (long)N * Ho * SPR * CG;
@@ -145,24 +112,14 @@ __global__ __launch_bounds__(256) void dw_fwd_kernel(const T* __restrict__ in, l
     f32x4 w[9];
 #pragma unroll
     for (int t = 0; t < 9; ++t) w[t] = ld4(wk + (FLIP ? 8 - t : t) * C + c);
-    typename std::conditional<BW, RowInBw<T>, RowIn<LAZY, T>>::type r[3];
-    if constexpr (BW) {
-      const SegBwx4 kk = seg_bwx_ld(gst, C, c);
+    RowIn<LAZY, T> r[3];
 #pragma unroll
-      for (int k = 0; k < 3; ++k) {
-        r[k].init(in + (long)n * H * W * ldin + c, gy + (long)n * H * W * ldgy + c, ho * S - 1 + k, H, W, ldin, ldgy);
-        r[k].k = kk;
-        r[k].act = gact;
-      }
-    } else {
-#pragma unroll
-      for (int k = 0; k < 3; ++k) {
-        r[k].init(in + (long)n * H * W * ldin + c, ho * S - 1 + k, H, W, ldin);
-        r[k].act = iact;
-        if (LAZY) {
-          r[k].sc = ld4(isc + c);
-          r[k].sh = ld4(ish + c);
-        }
+    for (int k = 0; k < 3; ++k) {
+      r[k].init(in + (long)n * H * W * ldin + c, ho * S - 1 + k, H, W, ldin);
+      r[k].act = iact;
+      if (LAZY) {
+        r[k].sc = ld4(isc + c);
+        r[k].sh = ld4(ish + c);
       }
     }
     f32x4 a[3], b[3];  // input columns wo*S-1 and wo*S (stride 1), or column wo*S-1 (stride 2)
@@ -211,13 +168,11 @@ __global__ __launch_bounds__(256) void dw_fwd_kernel(const T* __restrict__ in, l
 //   dX[2j]   = sum_rows w[ky][1] dY[.][j]
 //   dX[2j+1] = sum_rows w[ky][0] dY[.][j+1] + w[ky][2] dY[.][j]
 // A thread owns TW dX columns (TW/2 pairs); dY column j+1 slides to the next pair.
-template <typename T, bool BW = false>
+template <typename T>
 __global__ __launch_bounds__(256) void dw_dgrad_s2_kernel(const T* __restrict__ dy, long lddy, int N, int Ho,
                                                           int Wo, int C, const float* __restrict__ wk,
                                                           T* __restrict__ dx, long lddx, int H, int W,
-                                                          int accumulate, const T* __restrict__ gy = nullptr,
-                                                          long ldgy = 0, const float* __restrict__ gst = nullptr,
-                                                          int gact = 0) {
+                                                          int accumulate) {
   const int CG = C >> 2;
   const int SPR = (W + TW - 1) / TW;
   const long total = (long)N * H * SPR * CG;
@@ -231,22 +186,10 @@ __global__ __launch_bounds__(256) void dw_dgrad_s2_kernel(const T* __restrict__ 
     const bool odd = hq & 1;
     // row slots: slot 0 = (even: ky 1, ho hq/2 | odd: ky 0, ho (hq+1)/2), slot 1 = (odd: ky 2, ho (hq-1)/2)
     const int ky0 = odd ? 0 : 1, ho0 = odd ? (hq + 1) >> 1 : hq >> 1, ho1 = (hq - 1) >> 1;
-    typename std::conditional<BW, RowInBw<T>, RowIn<false, T>>::type r[2];
+    RowIn<false, T> r[2];
     const T* img = dy + (long)n * Ho * Wo * lddy + c;
-    if constexpr (BW) {
-      const T* yimg = gy + (long)n * Ho * Wo * ldgy + c;
-      const SegBwx4 kk = seg_bwx_ld(gst, C, c);
-      r[0].init(img, yimg, ho0, Ho, Wo, lddy, ldgy);
-      r[1].init(img, yimg, odd ? ho1 : -1, Ho, Wo, lddy, ldgy);
-#pragma unroll
-      for (int s = 0; s < 2; ++s) {
-        r[s].k = kk;
-        r[s].act = gact;
-      }
-    } else {
-      r[0].init(img, ho0, Ho, Wo, lddy);
-      r[1].init(img, odd ? ho1 : -1, Ho, Wo, lddy);
-    }
+    r[0].init(img, ho0, Ho, Wo, lddy);
+    r[1].init(img, odd ? ho1 : -1, Ho, Wo, lddy);
     f32x4 w[2][3];
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
@@ -284,17 +227,13 @@ __global__ __launch_bounds__(256) void dw_dgrad_s2_kernel(const T* __restrict__ 
 // dY[p][c] * X[src(p, tap)][c].  Block = RG row groups x TC channel groups; a
 // thread slides along its strips keeping 9 float4 accumulators, then a fixed-
 // order LDS tree reduction over the row groups (deterministic).
-// BW: `dy` is dA of the BatchNorm layer after this conv; dY formed on load with by [.][ldby] and st[7][C]
-// planes bst (common.h SegBwx4).
-template <int S, bool LAZY, typename T = float, bool BW = false>
+template <int S, bool LAZY, typename T = float>
 __global__ __launch_bounds__(256) void dw_wgrad_kernel(const T* __restrict__ dy, long lddy,
                                                        const T* __restrict__ x, long ldx, int N, int H, int W,
                                                        int C, const float* __restrict__ isc,
                                                        const float* __restrict__ ish, int iact, int Ho, int Wo,
                                                        int TC, int gy, int strips_per_block,
-                                                       float* __restrict__ part, const T* __restrict__ by = nullptr,
-                                                       long ldby = 0, const float* __restrict__ bst = nullptr,
-                                                       int bact = 0) {
+                                                       float* __restrict__ part) {
   extern __shared__ __attribute__((aligned(16))) f32x4 red[];  // [RG][TC][9]
   const int CG = C >> 2;
   const int RG = 256 / TC;
@@ -318,8 +257,6 @@ __global__ __launch_bounds__(256) void dw_wgrad_kernel(const T* __restrict__ dy,
       sc = ld4(isc + c);
       sh = ld4(ish + c);
     }
-    SegBwx4 bk;
-    if constexpr (BW) bk = seg_bwx_ld(bst, C, c);
     for (long st = s0 + rg; st < s1; st += RG) {
       const long row = st / SPR;
       const int ws = (int)(st - row * SPR) * TWW;
@@ -333,7 +270,6 @@ __global__ __launch_bounds__(256) void dw_wgrad_kernel(const T* __restrict__ dy,
         r[k].act = iact;
       }
       const T* g = dy + (row * Wo + ws) * lddy + c;
-      const T* gv_y = BW ? by + (row * Wo + ws) * ldby + c : nullptr;
       f32x4 a[3], b[3];
 #pragma unroll
       for (int k = 0; k < 3; ++k) {
@@ -343,8 +279,7 @@ __global__ __launch_bounds__(256) void dw_wgrad_kernel(const T* __restrict__ dy,
 #pragma unroll 2
       for (int u = 0; u < TWW; ++u) {
         const int wo = ws + u;
-        f32x4 g0 = ld4(g + (long)(wo < Wo ? u : Wo - 1 - ws) * lddy);
-        if constexpr (BW) g0 = seg_as_stored<T>(seg_bwx4(g0, ld4(gv_y + (long)(wo < Wo ? u : Wo - 1 - ws) * ldby), bk, bact));
+        const f32x4 g0 = ld4(g + (long)(wo < Wo ? u : Wo - 1 - ws) * lddy);
         const f32x4 gv = wo < Wo ? g0 : f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int k = 0; k < 3; ++k) {
@@ -469,30 +404,21 @@ SEG_API int seg_dw_fwd_bias_act(const float* in, long ldin, int N, int H, int W,
 
 template <typename T>
 static int dw_dgrad_impl(const T* dy, long lddy, int N, int Ho, int Wo, int C, const float* wk, T* dx,
-                         long lddx, int H, int W, int stride, int accumulate, hipStream_t stream,
-                         const T* gy = nullptr, long ldgy = 0, const float* gst = nullptr, int gact = 0) {
+                         long lddx, int H, int W, int stride, int accumulate, hipStream_t stream) {
   if ((C & 3) || (lddy & 3) || (lddx & 3) || (stride != 1 && stride != 2)) return (int)hipErrorInvalidValue;
-  if (gy && (!gst || (ldgy & 3) || gact < SEG_ACT_NONE || gact > SEG_ACT_RELU6)) return (int)hipErrorInvalidValue;
   if (stride == 1) {
     if (H != Ho || W != Wo) return (int)hipErrorInvalidValue;
     const int grid = item_grid((long)N * H * ((W + TW - 1) / TW) * (C / 4));
-#define SEG_DW_DG(A, B)                                                                                              \
-  hipLaunchKernelGGL((dw_fwd_kernel<1, false, true, A, false, T, B>), dim3(grid), dim3(256), 0, stream, dy, lddy, N, Ho, \
-                     Wo, C, nullptr, nullptr, 0, wk, dx, lddx, H, W, nullptr, 0, gy, ldgy, gst, gact)
-    if (gy) {
-      if (accumulate) SEG_DW_DG(true, true); else SEG_DW_DG(false, true);
-    } else {
-      if (accumulate) SEG_DW_DG(true, false); else SEG_DW_DG(false, false);
-    }
-#undef SEG_DW_DG
+    if (accumulate)
+      hipLaunchKernelGGL((dw_fwd_kernel<1, false, true, true, false, T>), dim3(grid), dim3(256), 0, stream, dy, lddy, N, Ho, Wo,
+                         C, nullptr, nullptr, 0, wk, dx, lddx, H, W, nullptr, 0);
+    else
+      hipLaunchKernelGGL((dw_fwd_kernel<1, false, true, false, false, T>), dim3(grid), dim3(256), 0, stream, dy, lddy, N, Ho,
+                         Wo, C, nullptr, nullptr, 0, wk, dx, lddx, H, W, nullptr, 0);
   } else {
     const int grid = item_grid((long)N * H * ((W + TW - 1) / TW) * (C / 4));
-    if (gy)
-      hipLaunchKernelGGL((dw_dgrad_s2_kernel<T, true>), dim3(grid), dim3(256), 0, stream, dy, lddy, N, Ho, Wo, C, wk, dx,
-                         lddx, H, W, accumulate, gy, ldgy, gst, gact);
-    else
-      hipLaunchKernelGGL((dw_dgrad_s2_kernel<T, false>), dim3(grid), dim3(256), 0, stream, dy, lddy, N, Ho, Wo, C, wk,
-                         dx, lddx, H, W, accumulate, nullptr, 0L, nullptr, 0);
+    hipLaunchKernelGGL(dw_dgrad_s2_kernel<T>, dim3(grid), dim3(256), 0, stream, dy, lddy, N, Ho, Wo, C, wk, dx, lddx,
+                       H, W, accumulate);
   }
   SEG_RET_LAST();
 }
@@ -503,21 +429,6 @@ SEG_API int seg_dw_dgrad(const float* dy, long lddy, int N, int Ho, int Wo, int 
 SEG_API int seg_dw_dgrad_bf16io(const __bf16* dy, long lddy, int N, int Ho, int Wo, int C, const float* wk, __bf16* dx,
                                 long lddx, int H, int W, int stride, int accumulate, hipStream_t stream) {
   return dw_dgrad_impl(dy, lddy, N, Ho, Wo, C, wk, dx, lddx, H, W, stride, accumulate, stream);
-}
-// seg_dw_dgrad whose dY is formed on load (BatchNorm backward on load, common.h SegBwx4): `da` is dA of
-// the BatchNorm layer after this conv, gy its raw conv output [.][ldgy], gst its st[7][C] planes; bit for
-// bit seg_dw_dgrad of the tensor seg_bn_bwd_apply would have written.
-SEG_API int seg_dw_dgrad_bwx(const float* da, long ldda, const float* gy, long ldgy, const float* gst, int gact, int N,
-                             int Ho, int Wo, int C, const float* wk, float* dx, long lddx, int H, int W, int stride,
-                             int accumulate, hipStream_t stream) {
-  if (!gy) return (int)hipErrorInvalidValue;
-  return dw_dgrad_impl(da, ldda, N, Ho, Wo, C, wk, dx, lddx, H, W, stride, accumulate, stream, gy, ldgy, gst, gact);
-}
-SEG_API int seg_dw_dgrad_bwx_bf16io(const __bf16* da, long ldda, const __bf16* gy, long ldgy, const float* gst,
-                                    int gact, int N, int Ho, int Wo, int C, const float* wk, __bf16* dx, long lddx,
-                                    int H, int W, int stride, int accumulate, hipStream_t stream) {
-  if (!gy) return (int)hipErrorInvalidValue;
-  return dw_dgrad_impl(da, ldda, N, Ho, Wo, C, wk, dx, lddx, H, W, stride, accumulate, stream, gy, ldgy, gst, gact);
 }
 
 SEG_API long seg_dw_wgrad_blocks(int N, int Ho, int Wo, int C) {
@@ -532,30 +443,22 @@ SEG_API long seg_dw_wgrad_blocks(int N, int Ho, int Wo, int C) {
 template <typename T>
 static int dw_wgrad_impl(const T* dy, long lddy, const T* x, long ldx, int N, int H, int W, int C,
                          const float* in_scale, const float* in_shift, int in_act, int Ho, int Wo, int stride,
-                         float* part, hipStream_t stream, const T* by = nullptr, long ldby = 0,
-                         const float* bst = nullptr, int bact = 0) {
+                         float* part, hipStream_t stream) {
   if ((C & 3) || (lddy & 3) || (ldx & 3) || (stride != 1 && stride != 2) || ((in_scale == nullptr) != (in_shift == nullptr)))
     return (int)hipErrorInvalidValue;
-  if (by && (!bst || (ldby & 3) || bact < SEG_ACT_NONE || bact > SEG_ACT_RELU6)) return (int)hipErrorInvalidValue;
   int TC, gy, spb;
   long gx;
   wgrad_tiling(C, &TC, &gy);
   wgrad_grid(N, Ho, Wo, C, &gx, &spb);
   const size_t lds = (size_t)(256 / TC) * TC * 9 * sizeof(f32x4);
   const bool lazy = in_scale != nullptr;
-#define SEG_DW_WG(S, L, B)                                                                                      \
-  hipLaunchKernelGGL((dw_wgrad_kernel<S, L, T, B>), dim3(gx * gy), dim3(256), lds, stream, dy, lddy, x, ldx, N, H, W, \
-                     C, in_scale, in_shift, in_act, Ho, Wo, TC, gy, spb, part, by, ldby, bst, bact)
-  if (by) {
-    if (stride == 1) {
-      if (lazy) SEG_DW_WG(1, true, true); else SEG_DW_WG(1, false, true);
-    } else {
-      if (lazy) SEG_DW_WG(2, true, true); else SEG_DW_WG(2, false, true);
-    }
-  } else if (stride == 1) {
-    if (lazy) SEG_DW_WG(1, true, false); else SEG_DW_WG(1, false, false);
+#define SEG_DW_WG(S, L)                                                                                         \
+  hipLaunchKernelGGL((dw_wgrad_kernel<S, L, T>), dim3(gx * gy), dim3(256), lds, stream, dy, lddy, x, ldx, N, H, W, C, \
+                     in_scale, in_shift, in_act, Ho, Wo, TC, gy, spb, part)
+  if (stride == 1) {
+    if (lazy) SEG_DW_WG(1, true); else SEG_DW_WG(1, false);
   } else {
-    if (lazy) SEG_DW_WG(2, true, false); else SEG_DW_WG(2, false, false);
+    if (lazy) SEG_DW_WG(2, true); else SEG_DW_WG(2, false);
   }
 #undef SEG_DW_WG
   SEG_RET_LAST();
@@ -569,24 +472,4 @@ SEG_API int seg_dw_wgrad_bf16io(const __bf16* dy, long lddy, const __bf16* x, lo
                                 const float* in_scale, const float* in_shift, int in_act, int Ho, int Wo, int stride,
                                 float* part, hipStream_t stream) {
   return dw_wgrad_impl(dy, lddy, x, ldx, N, H, W, C, in_scale, in_shift, in_act, Ho, Wo, stride, part, stream);
-}
-
-// seg_dw_wgrad whose dY is formed on load: `da` is dA of the BatchNorm layer after this conv, by its raw
-// conv output [.][ldby], bst its st[7][C] planes (common.h SegBwx4); the same partials bit for bit as
-// seg_dw_wgrad of the tensor seg_bn_bwd_apply would have written.
-SEG_API int seg_dw_wgrad_bwx(const float* da, long ldda, const float* by, long ldby, const float* bst, int bact,
-                             const float* x, long ldx, int N, int H, int W, int C, const float* in_scale,
-                             const float* in_shift, int in_act, int Ho, int Wo, int stride, float* part,
-                             hipStream_t stream) {
-  if (!by) return (int)hipErrorInvalidValue;
-  return dw_wgrad_impl(da, ldda, x, ldx, N, H, W, C, in_scale, in_shift, in_act, Ho, Wo, stride, part, stream, by,
-                       ldby, bst, bact);
-}
-SEG_API int seg_dw_wgrad_bwx_bf16io(const __bf16* da, long ldda, const __bf16* by, long ldby, const float* bst,
-                                    int bact, const __bf16* x, long ldx, int N, int H, int W, int C,
-                                    const float* in_scale, const float* in_shift, int in_act, int Ho, int Wo,
-                                    int stride, float* part, hipStream_t stream) {
-  if (!by) return (int)hipErrorInvalidValue;
-  return dw_wgrad_impl(da, ldda, x, ldx, N, H, W, C, in_scale, in_shift, in_act, Ho, Wo, stride, part, stream, by,
-                       ldby, bst, bact);
 }

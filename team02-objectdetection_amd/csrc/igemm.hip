@@ -17,7 +17,6 @@
 // ds_read_b128: lane half h at step kk of sub-chunk ks carries k = 8ks + 4h + kk
 // for BOTH operands, which is all the MFMA needs to sum the right products.
 // Two LDS stages, register prefetch of the next K chunk, one barrier per chunk.
-#define SEG_IGEMM_BWX 1
 #include "igemm_impl.h"
 
 int seg_igemm_forced_tile = -1;
@@ -69,29 +68,6 @@ SEG_API int seg_conv_igemm_bnout(const float* in, long ldin, int N, int H, int W
   return conv_igemm_impl<float>(in, ldin, N, H, W, Cin, wk, ldk, nullptr, out, ldout, H, W, Cout, ks, 1, ks / 2, add,
                                 ldadd, nullptr, SEG_ACT_NONE, nullptr, 1, stream, nullptr, nullptr, 0, by, ldby,
                                 bscale, bshift, bmean, bact, bpart);
-}
-
-// 1 when seg_conv_igemm_bwx (bf16 = 0) / _bwx_bf16io_w16 (bf16 = 1) takes a data gradient over Cin dY channels
-// (the uniform-tap loader: Cin >= the K chunk launch_igemm picks; bf16: 8-channel slots).
-SEG_API int seg_conv_igemm_bwx_ok(int Cin, int ks, int bf16) {
-  const int K = ks * ks * Cin;
-  int bk = igemm_bk(K);
-  if (bf16 && bk == SEG_IGEMM_BK && Cin >= 64 && K >= 256) bk = 64;
-  return Cin >= bk && (!bf16 || Cin % 8 == 0) && (ks == 1 || ks == 3);
-}
-
-// A stride-1 data gradient whose input dY is formed on load from a BatchNorm layer's dA (`in`) and raw
-// conv output gy with the layer's st[7][Cin] planes (common.h SegBwx4): bit for bit the data gradient
-// of the tensor seg_bn_bwd_apply would have written, without that pass.  by .. bpart optional (null
-// bpart: none): the BN-backward partials of `out` as seg_conv_igemm_bnout.
-SEG_API int seg_conv_igemm_bwx(const float* in, long ldin, int N, int H, int W, int Cin, const float* gy, long ldgy,
-                               const float* gst, int gact, const float* wk, int ldk, float* out, long ldout, int Cout,
-                               int ks, const float* add, long ldadd, const float* by, long ldby, const float* bscale,
-                               const float* bshift, const float* bmean, int bact, float* bpart, hipStream_t stream) {
-  if (!gy) return (int)hipErrorInvalidValue;
-  return conv_igemm_impl<float>(in, ldin, N, H, W, Cin, wk, ldk, nullptr, out, ldout, H, W, Cout, ks, 1, ks / 2, add,
-                                ldadd, nullptr, SEG_ACT_NONE, nullptr, 1, stream, nullptr, nullptr, 0, by, ldby,
-                                bscale, bshift, bmean, bact, bpart, nullptr, -1, gy, ldgy, gst, Cin, gact);
 }
 
 SEG_API int seg_conv_igemm(const float* in, long ldin, int N, int H, int W, int Cin,

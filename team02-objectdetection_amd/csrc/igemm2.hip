@@ -34,7 +34,6 @@
 // K chunk in flight and ran them at 0.4-1.5 TB/s).  (Round 4's lazy-BN fragment transform for
 // 1x1 consumers measured slower than the generic kernels and was removed in round 5.)
 #include "common.h"
-#include <cstdlib>
 
 namespace {
 
@@ -84,13 +83,7 @@ __device__ __forceinline__ void wait_vm() {  // s_waitcnt vmcnt(N), other counte
   __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | 0x0F70);  // vmcnt is 6 bits, split 3:0 / 15:14
 }
 
-// IL (round 6): the DMA of step it + 2 is issued INSIDE step it's compute phase, one or two LDS-DMA
-// instructions between the MFMAs of each 16-deep k slice, into the buffer step it - 1 left (every wave
-// is past it: the one barrier per step), instead of all of a wave's 6 DMA instructions back to back
-// after a second barrier -- the wave no longer stalls on a full memory queue between its MFMA phases
-// (profiles/r06/ig2diag_*: the DMA-only and MFMA-only runs of a launch added up to the whole).
-// Same K order and split boundaries: bitwise the IL = false form.
-template <int BM, int BN, int WM, int WN, int KS, bool IL = false>
+template <int BM, int BN, int WM, int WN, int KS>
 __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void igemm2_kernel(Igemm2Args a) {
   constexpr int NW = (BM / WM) * (BN / WN), kThreads = 64 * NW, WAVES_N = BN / WN;
   constexpr int MI = WM / 32, NI = WN / 32;
@@ -157,25 +150,24 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void igemm2_kernel(Igem
   long u_toff0 = tap_off(u_tap), u_toff1 = tap_off(u_tap + 1);
   int k0 = k_beg;
 
-  // DMA instruction j (< NA: A rows, else B rows) of the K step at (u_tap, u_ci, k0) into LDS buffer `buf`
-  auto issue_one = [&](int buf, int j) {
+  auto issue = [&](int buf) {  // DMA of the K step at (u_tap, u_ci, k0) into LDS buffer `buf`
     char* As = smem + buf * STAGE;
     char* Bs = As + A_BYTES;
-    if (j < NA) {
-      const int i = j;
+#pragma unroll
+    for (int i = 0; i < NA; ++i) {
       const int ci = u_ci + 8 * a_cl[i];
       const bool wrap = ci >= a.Cin;
       const int tap = u_tap + (wrap ? 1 : 0);
       const bool ok = (a_mask[i] >> tap) & 1u;
       const __bf16* src = a.in + a_off[i] + (wrap ? u_toff1 : u_toff0) + (wrap ? ci - a.Cin : ci);
       dma16(ok ? (const void*)src : (const void*)g_zero_row, As + (wave + NW * i) * 1024);
-    } else {
-      const int i = j - NA;
+    }
+#pragma unroll
+    for (int i = 0; i < NB; ++i) {
       const bool ok = k0 + b_k[i] < a.K;
       dma16(ok ? (const void*)(a.wk + b_off[i] + k0) : (const void*)g_zero_row, Bs + (wave + NW * i) * 1024);
     }
-  };
-  auto advance = [&]() {  // to the next K step
+    // advance one K step
     k0 += kBK;
     u_ci += kBK;
     while (u_ci >= a.Cin) {
@@ -184,11 +176,6 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void igemm2_kernel(Igem
       u_toff0 = u_toff1;
       u_toff1 = tap_off(u_tap + 1);
     }
-  };
-  auto issue = [&](int buf) {  // the whole K step at once
-#pragma unroll
-    for (int j = 0; j < NA + NB; ++j) issue_one(buf, j);
-    advance();
   };
 
   f32x16 acc[MI][NI];
@@ -200,12 +187,9 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void igemm2_kernel(Igem
       for (int r = 0; r < 16; ++r) acc[mi][ni][r] = 0.f;
 
   const int fr = lane & 31, fh = lane >> 5;
-  // compute(buf): the MFMAs of the step in `buf`; IL: with step it + 2's DMA into `dbuf` (>= 0) spread over
-  // its k slices (instructions j of slice ks: [ks * ND / 4, (ks + 1) * ND / 4))
-  auto compute = [&](int buf, int dbuf) {
+  auto compute = [&](int buf) {
     const char* As = smem + buf * STAGE;
     const char* Bs = As + A_BYTES;
-    constexpr int ND = NA + NB;
     // fragments of the next 16-deep k slice are read while the current slice's MFMAs run
     bf16x8 af[2][MI], bfr[2][NI];
     auto frag = [&](int ks, int st) {
@@ -231,53 +215,30 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void igemm2_kernel(Igem
         for (int ni = 0; ni < NI; ++ni) {
           if (SEG_IG2_NOMFMA) {
             asm volatile("" ::"v"(af[ks & 1][mi]), "v"(bfr[ks & 1][ni]));
-          } else {
-            acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[ks & 1][mi], bfr[ks & 1][ni], acc[mi][ni], 0, 0, 0);
+            continue;
           }
-          if constexpr (IL) {  // this slice's share of the next-but-one step's DMA, after its first MFMA
-            if (mi == 0 && ni == 0 && dbuf >= 0) {
-#pragma unroll
-              for (int j = ks * ND / 4; j < (ks + 1) * ND / 4; ++j) issue_one(dbuf, j);
-            }
-          }
+          acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[ks & 1][mi], bfr[ks & 1][ni], acc[mi][ni], 0, 0, 0);
         }
-    }
-    if constexpr (IL) {
-      if (dbuf >= 0) advance();
     }
   };
 
   // ---- K loop: buffer it % 3 holds step it; steps it + 1 and it + 2 stay in flight meanwhile
   // (each step is NA + NB DMA instructions per wave, so "k steps still in flight" is
   // vmcnt(k * (NA + NB)))
-  if constexpr (IL) {
-    // steps it and it + 1 in flight at the top of iteration it; step it + 2 is issued during compute(it) into the
-    // buffer of step it - 1, which every wave finished reading before the barrier (its wait_lgkm0)
-    if (nst > 0) issue(0);
-    if (nst > 1) issue(1);
-    for (int it = 0; it < nst; ++it) {
-      if (it + 1 < nst) wait_vm<NA + NB>();  // only step it + 1's DMA may still be in flight
-      else wait_vm<0>();
-      raw_barrier();                         // step `it` landed for every wave; every wave is past compute(it - 1)
-      compute(it % NSTAGE, it + 2 < nst ? (it + 2) % NSTAGE : -1);
-      wait_lgkm0();                          // this wave's fragment reads of the step are done
-    }
-  } else {
-    if (nst > 0) issue(0);
-    if (nst > 1) issue(1);
-    if (nst > 2) issue(2);
-    for (int it = 0; it < nst; ++it) {
-      const int ahead = min(nst - 1 - it, 2);  // steps issued beyond this one
-      if (ahead == 2) wait_vm<2 * (NA + NB)>();
-      else if (ahead == 1) wait_vm<NA + NB>();
-      else wait_vm<0>();
-      raw_barrier();                         // every wave's DMA of step `it` has landed
-      const int buf = it % NSTAGE;
-      compute(buf, -1);
-      wait_lgkm0();                          // this wave's fragment reads of `buf` are done
-      raw_barrier();                         // ... every wave's: the buffer may be refilled
-      if (it + NSTAGE < nst) issue(buf);
-    }
+  if (nst > 0) issue(0);
+  if (nst > 1) issue(1);
+  if (nst > 2) issue(2);
+  for (int it = 0; it < nst; ++it) {
+    const int ahead = min(nst - 1 - it, 2);  // steps issued beyond this one
+    if (ahead == 2) wait_vm<2 * (NA + NB)>();
+    else if (ahead == 1) wait_vm<NA + NB>();
+    else wait_vm<0>();
+    raw_barrier();                         // every wave's DMA of step `it` has landed
+    const int buf = it % NSTAGE;
+    compute(buf);
+    wait_lgkm0();                          // this wave's fragment reads of `buf` are done
+    raw_barrier();                         // ... every wave's: the buffer may be refilled
+    if (it + NSTAGE < nst) issue(buf);
   }
 
   // ---- split-K: publish this slice, the last-arriving slice of the tile combines
@@ -423,11 +384,6 @@ constexpr Tile2 kT2[] = {{128, 256, 64, 64, 1.00f}, {256, 128, 64, 64, 1.00f}, {
 constexpr int kNT2 = sizeof(kT2) / sizeof(kT2[0]);
 
 int g_ig2_force = -1;      // tuning hooks (seg_igemm2_force_tile, seg_igemm2_tune)
-// the interleaved-DMA K loop (IL); SEG_IG2_IL=0 = the round-3 loop (two barriers per step, DMA after compute)
-bool g_ig2_il = [] {
-  const char* e = getenv("SEG_IG2_IL");
-  return !(e && e[0] == '0');
-}();
 int g_ig2_target = 512;    // 4-wave tiles: split-K up to this many blocks ...
 int g_ig2_minsteps = 3;    // ... keeping at least this many 64-deep K steps per slice
 
@@ -516,14 +472,6 @@ SEG_API int seg_igemm2_tune(int target_blocks, int min_steps) {
   return 0;
 }
 
-// A/B hook: the K loop form of seg_conv_igemm2_bf16io -- 1 = the interleaved-DMA loop (the default), 0 = the
-// round-3 loop; < 0 leaves it.  Returns the previous setting.  Results are bitwise the same either way.
-SEG_API int seg_igemm2_il(int on) {
-  const int prev = g_ig2_il ? 1 : 0;
-  if (on >= 0) g_ig2_il = on != 0;
-  return prev;
-}
-
 // Tuning hook: force seg_conv_igemm2_bf16io's tile (index into its table; -1 = the plan).
 SEG_API int seg_igemm2_force_tile(int t) {
   g_ig2_force = t;
@@ -564,17 +512,11 @@ static int igemm2_impl(const __bf16* in, long ldin, int N, int H, int W, int Cin
   a.K = ks * ks * Cin; a.M = (int)M; a.nsteps = p.nsteps; a.steps_per_split = p.steps_per_split;
   a.splits = p.splits; a.tiles_m = p.tiles_m; a.tiles_n = p.tiles_n;
   const int grid = p.tiles_m * p.tiles_n * p.splits;
-  const bool il = g_ig2_il;
 #define SEG_I2(BM, BN, WM, WN)                                                                                   \
   do {                                                                                                          \
     constexpr int nt = 64 * (BM / WM) * (BN / WN);                                                              \
-    if (il) {                                                                                                   \
-      if (ks == 3) hipLaunchKernelGGL((igemm2_kernel<BM, BN, WM, WN, 3, true>), dim3(grid), dim3(nt), 0, stream, a); \
-      else hipLaunchKernelGGL((igemm2_kernel<BM, BN, WM, WN, 1, true>), dim3(grid), dim3(nt), 0, stream, a);    \
-    } else {                                                                                                    \
-      if (ks == 3) hipLaunchKernelGGL((igemm2_kernel<BM, BN, WM, WN, 3>), dim3(grid), dim3(nt), 0, stream, a);   \
-      else hipLaunchKernelGGL((igemm2_kernel<BM, BN, WM, WN, 1>), dim3(grid), dim3(nt), 0, stream, a);          \
-    }                                                                                                           \
+    if (ks == 3) hipLaunchKernelGGL((igemm2_kernel<BM, BN, WM, WN, 3>), dim3(grid), dim3(nt), 0, stream, a); \
+    else hipLaunchKernelGGL((igemm2_kernel<BM, BN, WM, WN, 1>), dim3(grid), dim3(nt), 0, stream, a);            \
   } while (0)
   switch (p.tile) {
     case 0: SEG_I2(128, 256, 64, 64); break;

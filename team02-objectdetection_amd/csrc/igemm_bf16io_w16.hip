@@ -1,7 +1,6 @@
 // The bf16io implicit GEMM with bf16 packed weights (seg_pack_batch bf16 modes): the
 // training path of the bf16io configuration.  Own translation unit: the WB
 // instantiations compile in parallel with the fp32-weight ones (igemm_bf16io.hip).
-#define SEG_IGEMM_BWX 1
 #include "igemm_impl.h"
 
 // seg_conv_igemm_bf16io with the weights packed as bf16 ([Cout][ldk], ldk % 8 == 0,
@@ -39,17 +38,4 @@ SEG_API int seg_conv_igemm_bnout_bf16io_w16(const __bf16* in, long ldin, int N, 
   return conv_igemm_impl<__bf16, __bf16, true>(in, ldin, N, H, W, Cin, wk, ldk, nullptr, out, ldout, H, W, Cout, ks,
                                                1, ks / 2, add, ldadd, nullptr, SEG_ACT_NONE, nullptr, 1, stream,
                                                nullptr, nullptr, 0, by, ldby, bscale, bshift, bmean, bact, bpart);
-}
-
-// seg_conv_igemm_bwx on bf16 storage with bf16 packed weights (the bf16io training data gradient).
-SEG_API int seg_conv_igemm_bwx_bf16io_w16(const __bf16* in, long ldin, int N, int H, int W, int Cin, const __bf16* gy,
-                                          long ldgy, const float* gst, int gact, const __bf16* wk, int ldk, __bf16* out,
-                                          long ldout, int Cout, int ks, const __bf16* add, long ldadd,
-                                          const __bf16* by, long ldby, const float* bscale, const float* bshift,
-                                          const float* bmean, int bact, float* bpart, hipStream_t stream) {
-  if (!gy) return (int)hipErrorInvalidValue;
-  return conv_igemm_impl<__bf16, __bf16, true>(in, ldin, N, H, W, Cin, wk, ldk, nullptr, out, ldout, H, W, Cout, ks,
-                                               1, ks / 2, add, ldadd, nullptr, SEG_ACT_NONE, nullptr, 1, stream,
-                                               nullptr, nullptr, 0, by, ldby, bscale, bshift, bmean, bact, bpart,
-                                               nullptr, -1, gy, ldgy, gst, Cin, gact);
 }

@@ -47,10 +47,6 @@ struct IgemmArgs {
   // words, [tilesM * tilesN][4] (zero before the first launch; an epoch word, never re-armed)
   unsigned* kcnt;
   int kspin;                     // seg_tile_combine's poll bound
-  // optional BatchNorm backward formed on load (the BW instantiations, uniform-tap loader): `in` is dA of
-  // a train-mode BN layer and the A operand is its dY = seg_bnbwd4(dA, gy; gst) (common.h SegBwx4), the
-  // apply pass's value bit for bit; gy [rows][ldgy] IT = the layer's raw conv output, gst its st[7][gC]
-  const void* gy; long ldgy; const float* gst; int gC; int gact;
 };
 
 #ifndef SEG_IGEMM_DEPTH
@@ -91,10 +87,9 @@ struct IgemmArgs {
 // no conversion on the way into LDS.  Bitwise the fp32-weight kernel: the RNE rounding
 // is the same, done once at pack time.
 template <int BM, int BN, int WM, int WN, int KS, int BK, bool UT, typename OT = float, typename IT = float,
-          bool WB = false, bool BO = false, bool BW = false>
+          bool WB = false, bool BO = false>
 __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void igemm_conv_kernel(IgemmArgs a) {
   static_assert(!WB || std::is_same<OT, __bf16>::value, "bf16 weights feed bf16 operands");
-  static_assert(!BW || (UT && std::is_same<OT, IT>::value), "bwx: uniform-tap loader, operands of the storage type");
   const float* wk32 = static_cast<const float*>(a.wk);
   const __bf16* wk16 = static_cast<const __bf16*>(a.wk);
   const IT* __restrict__ in = static_cast<const IT*>(a.in);
@@ -189,14 +184,6 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void igemm_conv_kernel(
   int u_tap = 0, u_ci = 0;
   long u_toff0 = 0, u_toff1 = 0;
   auto tap_off = [&](int t) -> long { return ((long)(t / KS) * a.W + t % KS) * a.ldin; };
-  // BW: the y operand's slot offsets and tap offsets (its own row stride ldgy), the valid slots of the
-  // loaded chunk and the chunk's coefficient planes (fetched with the chunk, like XF's)
-  const IT* gy = static_cast<const IT*>(a.gy);
-  long u_yoff[BW ? A_PER : 1];
-  long u_ytoff0 = 0, u_ytoff1 = 0;
-  auto tap_offy = [&](int t) -> long { return ((long)(t / KS) * a.W + t % KS) * a.ldgy; };
-  unsigned gvm = 0;
-  SegBwx4 gk[BW ? VA / 4 : 1];
   if (UT) {
 #pragma unroll
     for (int i = 0; i < A_PER; ++i) {
@@ -207,7 +194,6 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void igemm_conv_kernel(
       const int pp = ok ? p : 0;
       if (KS == 1) {
         u_aoff[i] = (long)pp * a.ldin;
-        if constexpr (BW) u_yoff[i] = (long)pp * a.ldgy;
         u_mask[i] = ok ? 1u : 0u;
       } else {
         const int hw = a.Ho * a.Wo;
@@ -215,7 +201,6 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void igemm_conv_kernel(
         const int ho = rem / a.Wo, wo = rem - ho * a.Wo;
         const int hi0 = ho * a.stride - a.pad, wi0 = wo * a.stride - a.pad;
         u_aoff[i] = (((long)n * a.H + hi0) * a.W + wi0) * a.ldin;
-        if constexpr (BW) u_yoff[i] = (((long)n * a.H + hi0) * a.W + wi0) * a.ldgy;
         unsigned m = 0;
 #pragma unroll
         for (int t = 0; t < KS * KS; ++t) {
@@ -236,14 +221,8 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void igemm_conv_kernel(
     u_ci = kbeg - u_tap * a.Cin;
     u_toff0 = tap_off(u_tap);
     u_toff1 = tap_off(u_tap + 1);
-    if constexpr (BW) {
-      u_ytoff0 = tap_offy(u_tap);
-      u_ytoff1 = tap_offy(u_tap + 1);
-    }
   }
 
-  static_assert(!BW || SEG_IGEMM_STAGES == 1, "bwx: one register set (ry, gk)");
-  f32x4 ry[BW ? A_PER : 1];  // BW: the y slots of the chunk in flight
   auto load_tiles = [&](int k0, f32x4 (&ra)[A_PER], f32x4 (&rb)[B_PER]) {
     if (UT) {
       // address selects only (out-of-image / out-of-matrix slots read g_zero4): no
@@ -253,19 +232,6 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void igemm_conv_kernel(
       const bool wrap = ci >= a.Cin;
       const int tap = u_tap + (wrap ? 1 : 0);
       const long off = (wrap ? u_toff1 : u_toff0) + (wrap ? ci - a.Cin : ci);
-      if constexpr (BW) {  // this thread's chunk channels' coefficient planes; the y slots below
-        const int cc = KS == 1 ? (wrap ? 0 : ci) : (wrap ? ci - a.Cin : ci);
-#pragma unroll
-        for (int j = 0; j < VA / 4; ++j) gk[j] = seg_bwx_ld(a.gst, a.gC, cc + 4 * j);
-        const long offy = (wrap ? u_ytoff1 : u_ytoff0) + (wrap ? ci - a.Cin : ci);
-        gvm = 0;
-#pragma unroll
-        for (int i = 0; i < A_PER; ++i) {
-          const bool ok = (u_mask[i] >> tap) & 1u;
-          if (ok) gvm |= 1u << i;
-          ry[i] = *reinterpret_cast<const f32x4*>(ok ? (const void*)(gy + u_yoff[i] + offy) : (const void*)g_zero4);
-        }
-      }
       if (XF) {  // the chunk's channels for this thread: ci .. ci + VA - 1 of tap `tap` (1x1: no taps)
         xch = wrap ? -1 : ci;
         const int cc = KS == 1 ? (wrap ? 0 : ci) : (wrap ? ci - a.Cin : ci);
@@ -300,10 +266,6 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void igemm_conv_kernel(
         ++u_tap;
         u_toff0 = u_toff1;
         u_toff1 = tap_off(u_tap + 1);
-        if constexpr (BW) {
-          u_ytoff0 = u_ytoff1;
-          u_ytoff1 = tap_offy(u_tap + 1);
-        }
       }
       return;
     }
@@ -354,12 +316,6 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void igemm_conv_kernel(
       const int idx = tid + i * NT;
       if (A_VEC % NT == 0 || idx < A_VEC) {
         f32x4 v = ra[i];
-        if constexpr (BW) {  // dY of the real pixels (padding / beyond-K slots loaded zeros and stay zero)
-          if ((gvm >> i) & 1u) {
-            if constexpr (VA == 8) v = seg_bwx8_bf16(v, ry[i], gk[0], gk[VA / 4 - 1], a.gact);
-            else v = seg_as_stored<IT>(seg_bwx4(v, ry[i], gk[0], a.gact));
-          }
-        }
         if (XF && (KS == 1 ? xch >= 0 : ((xvm >> i) & 1u) != 0)) {
           if constexpr (VA == 8) {  // 8 bf16: widen, transform, round back (RNE) as the pass would
             const bf16x8 q = __builtin_bit_cast(bf16x8, v);
@@ -791,26 +747,7 @@ int launch_igemm_bk(IgemmArgs a, int ks, hipStream_t s) {
   }
   g_igemm_ic_used = a.kcnt != nullptr;
 #define SEG_IG(KS, U, B) hipLaunchKernelGGL((igemm_conv_kernel<BM, BN, WM, WN, KS, BK, U, OT, IT, WB, B>), dim3(grid, splits), dim3(NT), 0, s, a)
-#define SEG_IGW(KS, B) hipLaunchKernelGGL((igemm_conv_kernel<BM, BN, WM, WN, KS, BK, true, OT, IT, WB, B, true>), dim3(grid, splits), dim3(NT), 0, s, a)
   constexpr int VPR = BN / (16 / (int)sizeof(IT));
-  if (a.gy) {  // dY formed on load: the training storage types, 4-wave tiles, uniform-tap loader, unsplit
-    if (!ut || splits != 1 || a.kcnt) return (int)hipErrorInvalidValue;
-#ifdef SEG_IGEMM_BWX  // (instantiated only in the units whose entries take it: igemm.hip, igemm_bf16io_w16.hip)
-    if constexpr (std::is_same<OT, IT>::value && NT == 256) {
-      constexpr bool bo_ok = BN % (16 / (int)sizeof(IT)) == 0 && 64 % VPR == 0;
-      if (a.bpart) {
-        if constexpr (bo_ok) {
-          if (ks == 1) SEG_IGW(1, true); else SEG_IGW(3, true);
-          SEG_RET_LAST();
-        }
-        return (int)hipErrorInvalidValue;
-      }
-      if (ks == 1) SEG_IGW(1, false); else SEG_IGW(3, false);
-      SEG_RET_LAST();
-    }
-#endif
-    return (int)hipErrorInvalidValue;
-  }
   // (instantiated for the training storage types only: f32 and bf16io, where operands are the storage type)
   if constexpr (std::is_same<OT, IT>::value && BN % (16 / (int)sizeof(IT)) == 0 && 64 % VPR == 0) {
     if (a.bpart) {  // the BN-backward-partials instantiation (seg_conv_igemm_bnout*)
@@ -829,7 +766,6 @@ int launch_igemm_bk(IgemmArgs a, int ks, hipStream_t s) {
     if (ut) SEG_IG(3, true, false); else SEG_IG(3, false, false);
   }
 #undef SEG_IG
-#undef SEG_IGW
   SEG_RET_LAST();
 }
 
@@ -873,19 +809,18 @@ constexpr TileCfg kTiles[] = {
 
 constexpr int kTileBM[] = {128, 64, 128, 64, 128, 128, 256, 128, 128, 128, 256, 128, 128, 256, 64};
 
-int pick_tile(long M, int N, int lim = 1 << 30);
+int pick_tile(long M, int N);
 // seg_conv_igemm_bnout*: the picked tile's epilogue holds one column vector per lane (64 % (BN / VO) == 0)
 inline bool igemm_bnout_tile_ok(long M, int N, int es) {
   const int bn = kTiles[pick_tile(M, N)].bn, vo = 16 / es;
   return bn % vo == 0 && 64 % (bn / vo) == 0;
 }
 
-// lim: consider the first lim tiles only (8: the 4-wave ones, which the bwx loader is instantiated for)
-int pick_tile(long M, int N, int lim) {
-  if (seg_igemm_forced_tile >= 0 && seg_igemm_forced_tile < lim) return seg_igemm_forced_tile;
+int pick_tile(long M, int N) {
+  if (seg_igemm_forced_tile >= 0) return seg_igemm_forced_tile;
   int best = 0;
   double best_score = -1.0;
-  for (int i = 0; i < std::min(lim, (int)(sizeof(kTiles) / sizeof(kTiles[0]))); ++i) {
+  for (int i = 0; i < (int)(sizeof(kTiles) / sizeof(kTiles[0])); ++i) {
     const TileCfg& t = kTiles[i];
     const long bm_tiles = (M + t.bm - 1) / t.bm, bn_tiles = (N + t.bn - 1) / t.bn;
     const long blocks = bm_tiles * bn_tiles;
@@ -940,8 +875,7 @@ int conv_igemm_impl(const IT* in, long ldin, int N, int H, int W, int Cin, const
                     const IT* add, long ldadd, float* stat, int act, float* work, int splits, hipStream_t stream,
                     const float* xs = nullptr, const float* xb = nullptr, int xact = 0, const IT* by = nullptr,
                     long ldby = 0, const float* bsc = nullptr, const float* bsh = nullptr, const float* bmu = nullptr,
-                    int bact = 0, float* bpart = nullptr, unsigned* kcnt = nullptr, int tile = -1,
-                    const IT* gy = nullptr, long ldgy = 0, const float* gst = nullptr, int gC = 0, int gact = 0) {
+                    int bact = 0, float* bpart = nullptr, unsigned* kcnt = nullptr, int tile = -1) {
   if (!std::is_same<IT, float>::value && splits != 1) return (int)hipErrorInvalidValue;
   if ((Cin & 3) || (ldin & 3) || (ldk & 3) || (ks != 1 && ks != 3)) return (int)hipErrorInvalidValue;
   if (WB && ((ldk & 7) || ((uintptr_t)wk & 15) || splits != 1)) return (int)hipErrorInvalidValue;
@@ -951,10 +885,6 @@ int conv_igemm_impl(const IT* in, long ldin, int N, int H, int W, int Cin, const
   if (act < SEG_ACT_NONE || act > SEG_ACT_RELU6 || (act && stat)) return (int)hipErrorInvalidValue;
   if (splits < 1 || (splits > 1 && (!work || stat))) return (int)hipErrorInvalidValue;
   if (bpart && (!by || !bsc || !bsh || !bmu || splits != 1 || act || (ldby & 3))) return (int)hipErrorInvalidValue;
-  // bwx: the uniform-tap loader's 16-byte slots of dA and y (bf16: 8 channels), unsplit, no other input transform
-  if (gy && (!gst || gC < Cin || splits != 1 || xs || stride != 1 || (ldgy & 3) || ((uintptr_t)gy & 15) ||
-             (sizeof(IT) == 2 && ((ldgy & 7) || (Cin & 7))) || gact < SEG_ACT_NONE || gact > SEG_ACT_RELU6))
-    return (int)hipErrorInvalidValue;
   if (splits > 1) {  // the K ranges actually launched: whole BK chunks, no empty range (launch_igemm)
     const int nk = seg_cdiv((long)ks * ks * Cin, igemm_bk(ks * ks * Cin));
     splits = seg_cdiv(nk, seg_cdiv(nk, splits));
@@ -968,7 +898,6 @@ int conv_igemm_impl(const IT* in, long ldin, int N, int H, int W, int Cin, const
   a.xs = xs; a.xb = xb; a.xact = xact;
   a.by = by; a.ldby = ldby; a.bsc = bsc; a.bsh = bsh; a.bmu = bmu; a.bact = bact; a.bpart = bpart;
   a.kcnt = splits > 1 ? kcnt : nullptr;
-  a.gy = gy; a.ldgy = ldgy; a.gst = gst; a.gC = gC; a.gact = gact;
   a.kspin = seg_combine_spin(kSegCombineSpin);
   g_igemm_ic_used = false;
   if (bpart && !igemm_bnout_tile_ok(a.M, Cout, (int)sizeof(IT))) return (int)hipErrorInvalidValue;
@@ -976,8 +905,7 @@ int conv_igemm_impl(const IT* in, long ldin, int N, int H, int W, int Cin, const
     return (int)hipErrorInvalidValue;
   if (a.M == 0 || Cout == 0) return 0;
   int rc;
-  if (gy && tile >= 8) return (int)hipErrorInvalidValue;
-  switch (tile >= 0 ? tile : pick_tile(a.M, Cout, gy ? 8 : 1 << 30)) {
+  switch (tile >= 0 ? tile : pick_tile(a.M, Cout)) {
     case 0: rc = launch_igemm<128, 128, 64, 64, OT, IT, WB>(a, ks, splits, stream); break;
     case 1: rc = launch_igemm<64, 128, 32, 64, OT, IT, WB>(a, ks, splits, stream); break;
     case 2: rc = launch_igemm<128, 64, 64, 32, OT, IT, WB>(a, ks, splits, stream); break;

@@ -35,14 +35,10 @@ struct PwArgs {
   float* stat;                     // BN partials [tiles][2][N] (tile sum, M2 about the tile mean) or null
   const float* xs; const float* xb; int xact;  // lazy BN of the input (act(x * xs + xb)) or null
   int M, K, N, tiles;
-  // BatchNorm backward formed on load (BW): `in` is dA of a BN layer, the A operand its dY formed from gy
-  // [M][ldgy] and the layer's st[7][K] planes gst (common.h SegBwx4) -- the apply pass's tensor bit for bit
-  const void* gy; long ldgy; const float* gst; int gact;
 };
 
-template <typename T, int NT, int KP, bool XF, bool BW = false>
+template <typename T, int NT, int KP, bool XF>
 __global__ __launch_bounds__(kPwThreads) void pw_kernel(PwArgs a) {
-  static_assert(!(XF && BW), "one input transform");
   constexpr bool BF = sizeof(T) == 2;
   constexpr int BP = BF ? KP + 8 : KP + 4;  // LDS weight row pitch (elements): 16-byte aligned rows
   constexpr int NA = BF ? KP / 16 : KP / 8;  // A fragments per lane per tile (16-byte loads)
@@ -78,29 +74,8 @@ __global__ __launch_bounds__(kPwThreads) void pw_kernel(PwArgs a) {
       }
     }
   }
-  // BW: the coefficient planes of the K channels, staged in LDS once (held in registers they cost
-  // 2-3 waves per SIMD of occupancy); each tile's transform reads its lanes' channels from there
-  const T* gy = static_cast<const T*>(a.gy);
-  __shared__ __attribute__((aligned(16))) float gks[BW ? 6 * KP : 4];
-  if constexpr (BW) {
-    for (int i = tid; i < 6 * KP; i += kPwThreads) {
-      const int pl = i / KP, k = i - pl * KP;  // planes mean, scale, shift, k1, k2, k3 (st planes 0, 2..6)
-      gks[i] = k < a.K ? a.gst[(pl == 0 ? 0 : pl + 1) * a.K + k] : 0.f;
-    }
-  }
-  auto gk_at = [&](int k) -> SegBwx4 {
-    SegBwx4 q;
-    q.mu = *reinterpret_cast<const f32x4*>(&gks[k]);
-    q.sc = *reinterpret_cast<const f32x4*>(&gks[KP + k]);
-    q.sh = *reinterpret_cast<const f32x4*>(&gks[2 * KP + k]);
-    q.k1 = *reinterpret_cast<const f32x4*>(&gks[3 * KP + k]);
-    q.k2 = *reinterpret_cast<const f32x4*>(&gks[4 * KP + k]);
-    q.k3 = *reinterpret_cast<const f32x4*>(&gks[5 * KP + k]);
-    return q;
-  };
   __syncthreads();
 
-  f32x4 ry[BW ? NA : 1];  // BW: the y fragments of the tile in flight
   auto load_a = [&](int tile, f32x4 (&ra)[NA]) {
     const int row = tile * kPwRows + wave * 32 + lr;
     const bool rok = row < a.M;
@@ -109,10 +84,6 @@ __global__ __launch_bounds__(kPwThreads) void pw_kernel(PwArgs a) {
       const int k = BF ? 16 * s + 8 * h : 8 * s + 4 * h;
       if (rok && k < a.K) ra[s] = *reinterpret_cast<const f32x4*>(in + (long)row * a.ldin + k);
       else ra[s] = f32x4{0.f, 0.f, 0.f, 0.f};
-      if constexpr (BW) {
-        if (rok && k < a.K) ry[s] = *reinterpret_cast<const f32x4*>(gy + (long)row * a.ldgy + k);
-        else ry[s] = f32x4{0.f, 0.f, 0.f, 0.f};
-      }
     }
   };
 
@@ -125,14 +96,6 @@ __global__ __launch_bounds__(kPwThreads) void pw_kernel(PwArgs a) {
 #pragma unroll
     for (int s = 0; s < NA; ++s) {
       f32x4 v = ra[s];
-      if constexpr (BW) {  // dY of the tile's real rows (rows beyond M / channels beyond K stay zero)
-        const int k = BF ? 16 * s + 8 * h : 8 * s + 4 * h;
-        const int row = tile * kPwRows + wave * 32 + lr;
-        if (k < a.K && row < a.M) {
-          if constexpr (BF) v = seg_bwx8_bf16(v, ry[s], gk_at(k), gk_at(k + 4), a.gact);
-          else v = seg_bwx4(v, ry[s], gk_at(k), a.gact);
-        }
-      }
       if constexpr (XF) {
         const int k = BF ? 16 * s + 8 * h : 8 * s + 4 * h;
         if (k < a.K) {
@@ -271,8 +234,7 @@ __global__ __launch_bounds__(kPwThreads) void pw_kernel(PwArgs a) {
 
 template <typename T, int NT, int KP>
 void launch_pw(const PwArgs& a, int grid, hipStream_t s) {
-  if (a.gy) hipLaunchKernelGGL((pw_kernel<T, NT, KP, false, true>), dim3(grid), dim3(kPwThreads), 0, s, a);
-  else if (a.xs) hipLaunchKernelGGL((pw_kernel<T, NT, KP, true>), dim3(grid), dim3(kPwThreads), 0, s, a);
+  if (a.xs) hipLaunchKernelGGL((pw_kernel<T, NT, KP, true>), dim3(grid), dim3(kPwThreads), 0, s, a);
   else hipLaunchKernelGGL((pw_kernel<T, NT, KP, false>), dim3(grid), dim3(kPwThreads), 0, s, a);
 }
 
@@ -290,11 +252,8 @@ void launch_pw_n(const PwArgs& a, int grid, hipStream_t s) {
 
 template <typename T>
 int pw_impl(const T* in, long ldin, long M, int K, const T* wk, int ldk, const float* bias, T* out, long ldout, int N,
-            const T* add, long ldadd, float* stat, const float* xs, const float* xb, int xact, hipStream_t stream,
-            const T* gy = nullptr, long ldgy = 0, const float* gst = nullptr, int gact = 0) {
+            const T* add, long ldadd, float* stat, const float* xs, const float* xb, int xact, hipStream_t stream) {
   constexpr int V = sizeof(T) == 2 ? 8 : 4;
-  if (gy && (xs || !gst || (ldgy % V) || ((uintptr_t)gy & 15) || gact < SEG_ACT_NONE || gact > SEG_ACT_RELU6))
-    return (int)hipErrorInvalidValue;
   if (M < 1 || K < 8 || K > 32 || (K & 7) || N < 1 || N > 192 || ldk < K || M > 0x7fffffffL ||
       (ldin % V) || (ldout % V) || (add && (ldadd % V)) || ((uintptr_t)in & 15) || ((uintptr_t)out & 15) ||
       (add && ((uintptr_t)add & 15)) || (xs && (!xb || xact < SEG_ACT_NONE || xact > SEG_ACT_RELU6)))
@@ -303,7 +262,6 @@ int pw_impl(const T* in, long ldin, long M, int K, const T* wk, int ldk, const f
   a.in = in; a.ldin = ldin; a.wk = wk; a.ldk = ldk; a.bias = bias; a.add = add; a.ldadd = ldadd;
   a.out = out; a.ldout = ldout; a.stat = stat; a.xs = xs; a.xb = xb; a.xact = xact;
   a.M = (int)M; a.K = K; a.N = N; a.tiles = seg_cdiv(M, kPwRows);
-  a.gy = gy; a.ldgy = ldgy; a.gst = gst; a.gact = gact;
   const int grid = std::min(a.tiles, 1024);  // persistent blocks, 4 per CU (fewer resident when registers are short)
   if (K <= 16) launch_pw_n<T, 16>(a, grid, stream);
   else launch_pw_n<T, 32>(a, grid, stream);
@@ -332,22 +290,4 @@ SEG_API int seg_conv_pw_bf16io(const __bf16* in, long ldin, long M, int K, const
                                const float* bias, __bf16* out, long ldout, int N, const __bf16* add, long ldadd,
                                float* stat, const float* xs, const float* xb, int xact, hipStream_t stream) {
   return pw_impl(in, ldin, M, K, wk, ldk, bias, out, ldout, N, add, ldadd, stat, xs, xb, xact, stream);
-}
-
-// seg_conv_pw as a data gradient whose input dY is formed on load (BatchNorm backward on load,
-// common.h SegBwx4): `da` is dA of the BN layer, gy its raw conv output [M][ldgy], gst its st[7][K]
-// planes -- bit for bit seg_conv_pw over the tensor seg_bn_bwd_apply would have written.
-SEG_API int seg_conv_pw_bwx(const float* da, long ldda, const float* gy, long ldgy, const float* gst, int gact, long M,
-                            int K, const float* wk, int ldk, float* out, long ldout, int N, const float* add,
-                            long ldadd, hipStream_t stream) {
-  if (!gy) return (int)hipErrorInvalidValue;
-  return pw_impl(da, ldda, M, K, wk, ldk, nullptr, out, ldout, N, add, ldadd, nullptr, nullptr, nullptr, 0, stream, gy,
-                 ldgy, gst, gact);
-}
-SEG_API int seg_conv_pw_bwx_bf16io(const __bf16* da, long ldda, const __bf16* gy, long ldgy, const float* gst, int gact,
-                                   long M, int K, const __bf16* wk, int ldk, __bf16* out, long ldout, int N,
-                                   const __bf16* add, long ldadd, hipStream_t stream) {
-  if (!gy) return (int)hipErrorInvalidValue;
-  return pw_impl(da, ldda, M, K, wk, ldk, nullptr, out, ldout, N, add, ldadd, nullptr, nullptr, nullptr, 0, stream, gy,
-                 ldgy, gst, gact);
 }

@@ -39,9 +39,6 @@ struct WgradArgs {
   // optional input transform of X (XF kernels; 3x3: real pixels only, padding stays zero): x = act(x * xs[c] + xb[c]) on
   // load -- the producer's lazy BatchNorm + activation (see seg_conv_igemm_xf)
   const float* xs; const float* xb; int xact;
-  // optional BatchNorm backward formed on load (BW kernels): `dy` is dA of the BN layer after this conv and
-  // the dY operand is formed from gy [M][ldgy] and the layer's st[7][Cout] planes gst (common.h SegBwx4)
-  const void* gy; long ldgy; const float* gst; int gact;
 };
 
 // Row pitch (bf16 elements) of a k-major bf16 tile read with ds_read_b64_tr_b16: a
@@ -55,12 +52,10 @@ constexpr int tr_pitch(int n) { return n % 128 == 32 || n % 128 == 96 ? n : tr_p
 // column-major) and fed to v_mfma_f32_32x32x16_bf16; fp32 accumulation and slabs.
 // VW: channels per load slot -- 8 (one 16-byte load, copied to LDS as is) on bf16
 // storage when Cout, Cin and the row strides are multiples of 8, else 4.
-template <int BM, int BN, int WM, int WN, int KS, bool BF = false, typename IT = float, int VW = 4, bool XF = false,
-          bool BW = false>
+template <int BM, int BN, int WM, int WN, int KS, bool BF = false, typename IT = float, int VW = 4, bool XF = false>
 __global__ __launch_bounds__(256) void wgrad_kernel(WgradArgs a) {
   static_assert(VW == 4 || (BF && sizeof(IT) == 2), "16-byte slots carry bf16 operands");
   const IT* __restrict__ gdy = static_cast<const IT*>(a.dy);
-  const IT* __restrict__ ggy = static_cast<const IT*>(a.gy);
   const IT* __restrict__ gx = static_cast<const IT*>(a.x);
   constexpr int BK = BF ? 32 : ::BK;  // pixels per K chunk
   constexpr int AR = BF ? tr_pitch(BM) : BM + 4, BR = BF ? tr_pitch(BN) : BN + 4;
@@ -72,8 +67,6 @@ __global__ __launch_bounds__(256) void wgrad_kernel(WgradArgs a) {
 
   __shared__ __attribute__((aligned(16))) lds_t As[SEG_WGRAD_STAGES][BK * AR];
   __shared__ __attribute__((aligned(16))) lds_t Bs[SEG_WGRAD_STAGES][BK * BR];
-  // BW: the tile's BM channels' coefficient planes (mean, scale, shift, k1, k2, k3), staged once
-  __shared__ __attribute__((aligned(16))) float gks[BW ? 6 * BM : 4];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm0 = (wave / WAVES_N) * WM, wn0 = (wave % WAVES_N) * WN;
@@ -124,46 +117,20 @@ __global__ __launch_bounds__(256) void wgrad_kernel(WgradArgs a) {
         xbb[i][j] = ld4(a.xb + (b_ok[i] ? b_ci[i] : 0) + 4 * j);
       }
   }
-  if constexpr (BW) {
-    for (int i = tid; i < 6 * BM; i += 256) {
-      const int pl = i / BM, c = co0 + (i - pl * BM);
-      gks[i] = c < a.Cout ? a.gst[(pl == 0 ? 0 : pl + 1) * a.Cout + c] : 0.f;
-    }
-    __syncthreads();
-  }
-  auto gk_at = [&](int cl) -> SegBwx4 {  // cl: channel within the tile
-    SegBwx4 q;
-    q.mu = *reinterpret_cast<const f32x4*>(&gks[cl]);
-    q.sc = *reinterpret_cast<const f32x4*>(&gks[BM + cl]);
-    q.sh = *reinterpret_cast<const f32x4*>(&gks[2 * BM + cl]);
-    q.k1 = *reinterpret_cast<const f32x4*>(&gks[3 * BM + cl]);
-    q.k2 = *reinterpret_cast<const f32x4*>(&gks[4 * BM + cl]);
-    q.k3 = *reinterpret_cast<const f32x4*>(&gks[5 * BM + cl]);
-    return q;
-  };
-  f32x4 ra[A_PER], rb[B_PER], ry[BW ? A_PER : 1];
-  unsigned a_vm = 0;  // BW: the A slots of the loaded chunk that hold real (pixel, channel) elements
+  f32x4 ra[A_PER], rb[B_PER];
   auto ldv = [](const IT* q) -> f32x4 {  // one load slot: 4 channels widened, or 8 bf16 raw
     if constexpr (VW == 8) return *reinterpret_cast<const f32x4*>(q);
     else return ld4(q);
   };
   auto load_tiles = [&](int k0) {  // k0 = first pixel of this chunk
-    if (BW) a_vm = 0;
 #pragma unroll
     for (int i = 0; i < A_PER; ++i) {
       const int idx = tid + i * 256;
       const int prow = idx / (BM / VW), c = co0 + (idx % (BM / VW)) * VW;
       const int p = k0 + prow;
-      f32x4 v = {0.f, 0.f, 0.f, 0.f}, w = v;
+      f32x4 v = {0.f, 0.f, 0.f, 0.f};
       const bool ok = idx < A_VEC && p < kend && c < a.Cout;
       if (ok) v = ldv(gdy + (long)p * a.lddy + c);
-      if constexpr (BW) {
-        if (ok) {
-          w = ldv(ggy + (long)p * a.ldgy + c);
-          a_vm |= 1u << i;
-        }
-        ry[i] = w;
-      }
       ra[i] = v;
     }
     if (XF) b_vm = 0;
@@ -202,15 +169,7 @@ __global__ __launch_bounds__(256) void wgrad_kernel(WgradArgs a) {
     for (int i = 0; i < A_PER; ++i) {
       const int idx = tid + i * 256;
       if (idx < A_VEC) {
-        f32x4 v = ra[i];
-        if constexpr (BW) {  // dY of the real elements (zero slots stay zero)
-          if ((a_vm >> i) & 1u) {
-            const int cl = (idx % (BM / VW)) * VW;
-            if constexpr (VW == 8) v = seg_bwx8_bf16(v, ry[i], gk_at(cl), gk_at(cl + 4), a.gact);
-            else v = seg_as_stored<IT>(seg_bwx4(v, ry[i], gk_at(cl), a.gact));
-          }
-        }
-        st_op(&As[buf][(idx / (BM / VW)) * AR + (idx % (BM / VW)) * VW], v);
+        st_op(&As[buf][(idx / (BM / VW)) * AR + (idx % (BM / VW)) * VW], ra[i]);
       }
     }
 #pragma unroll
@@ -330,24 +289,6 @@ __global__ __launch_bounds__(256) void wgrad_kernel(WgradArgs a) {
 template <int BM, int BN, int WM, int WN, bool BF = false, typename IT = float>
 int launch_wgrad(const WgradArgs& a, int ks, int splits, hipStream_t s) {
   dim3 grid(seg_cdiv(a.Cout, BM) * seg_cdiv(a.Nw, BN) * splits);
-  if (a.gy) {  // dY formed on load (with or without the input's lazy BN)
-    const bool v8 = sizeof(IT) == 2 && a.Cout % 8 == 0 && a.Cin % 8 == 0 && a.lddy % 8 == 0 && a.ldx % 8 == 0 &&
-                    a.ldgy % 8 == 0;
-#define SEG_WG_BW(V, X)                                                                                       \
-  do {                                                                                                        \
-    if (ks == 1) hipLaunchKernelGGL((wgrad_kernel<BM, BN, WM, WN, 1, BF, IT, V, X, true>), grid, dim3(256), 0, s, a); \
-    else hipLaunchKernelGGL((wgrad_kernel<BM, BN, WM, WN, 3, BF, IT, V, X, true>), grid, dim3(256), 0, s, a);         \
-  } while (0)
-    if constexpr (sizeof(IT) == 2) {
-      if (v8) {
-        if (a.xs) SEG_WG_BW(8, true); else SEG_WG_BW(8, false);
-        SEG_RET_LAST();
-      }
-    }
-    if (a.xs) SEG_WG_BW(4, true); else SEG_WG_BW(4, false);
-#undef SEG_WG_BW
-    SEG_RET_LAST();
-  }
   if (a.xs) {  // input transform
     const bool v8 = sizeof(IT) == 2 && a.Cout % 8 == 0 && a.Cin % 8 == 0 && a.lddy % 8 == 0 && a.ldx % 8 == 0;
     if constexpr (sizeof(IT) == 2) {
@@ -436,8 +377,7 @@ SEG_API int seg_conv_wgrad_splits_bf16(long M, int Cout, int Cin, int ks) {
 static int conv_wgrad(const void* dy, long lddy, const void* x, long ldx, int N, int H, int W, int Cin, int Ho,
                       int Wo, int Cout, int ks, int stride, int pad, float* part, int splits,
                       hipStream_t stream, bool bf = false, bool bf_io = false, const float* xs = nullptr,
-                      const float* xb = nullptr, int xact = 0, const void* gy = nullptr, long ldgy = 0,
-                      const float* gst = nullptr, int gact = 0);
+                      const float* xb = nullptr, int xact = 0);
 
 SEG_API int seg_conv_wgrad(const float* dy, long lddy, const float* x, long ldx,
                            int N, int H, int W, int Cin, int Ho, int Wo, int Cout,
@@ -490,11 +430,8 @@ SEG_API int seg_conv_wgrad_bf16io_xf(const __bf16* dy, long lddy, const __bf16* 
 
 static int conv_wgrad(const void* dy, long lddy, const void* x, long ldx, int N, int H, int W, int Cin, int Ho,
                       int Wo, int Cout, int ks, int stride, int pad, float* part, int splits,
-                      hipStream_t stream, bool bf, bool bf_io, const float* xs, const float* xb, int xact,
-                      const void* gy, long ldgy, const float* gst, int gact) {
+                      hipStream_t stream, bool bf, bool bf_io, const float* xs, const float* xb, int xact) {
   if ((Cin & 3) || (ldx & 3) || (lddy & 3) || (ks != 1 && ks != 3) || splits < 1) return (int)hipErrorInvalidValue;
-  if (gy && (!gst || (ldgy & 3) || (Cout & 3) || gact < SEG_ACT_NONE || gact > SEG_ACT_RELU6))
-    return (int)hipErrorInvalidValue;
   if (xs && (!xb || xact < SEG_ACT_NONE || xact > SEG_ACT_RELU6)) return (int)hipErrorInvalidValue;
   if (ks == 1 && (stride != 1 || pad != 0)) return (int)hipErrorInvalidValue;
   WgradArgs a;
@@ -503,7 +440,6 @@ static int conv_wgrad(const void* dy, long lddy, const void* x, long ldx, int N,
   a.stride = stride; a.pad = pad; a.M = N * Ho * Wo; a.Nw = ks * ks * Cin;
   a.kchunk = seg_cdiv(seg_cdiv(a.M, splits), BK) * BK;
   a.xs = xs; a.xb = xb; a.xact = xact;
-  a.gy = gy; a.ldgy = ldgy; a.gst = gst; a.gact = gact;
   int bm, bn;
   wgrad_tiles(Cout, a.Nw, &bm, &bn);
   if (bf_io) {
@@ -527,27 +463,6 @@ static int conv_wgrad(const void* dy, long lddy, const void* x, long ldx, int N,
   if (bm == 64 && bn == 128) return launch_wgrad<64, 128, 32, 64>(a, ks, splits, stream);
   if (bm == 64) return launch_wgrad<64, 64, 32, 32>(a, ks, splits, stream);
   return launch_wgrad<32, 128, 32, 32>(a, ks, splits, stream);
-}
-
-// seg_conv_wgrad(_bf16io) whose dY operand is formed on load (BatchNorm backward on load, common.h
-// SegBwx4): `da` is dA of the BatchNorm layer after this conv, gy its raw conv output [M][ldgy], gst its
-// st[7][Cout] planes; in_scale (nullable) .. in_act: the input's lazy BN as seg_conv_wgrad_xf.  The same
-// partial slabs bit for bit as over the tensor seg_bn_bwd_apply would have written.
-SEG_API int seg_conv_wgrad_bwx(const float* da, long ldda, const float* gy, long ldgy, const float* gst, int gact,
-                               const float* x, long ldx, int N, int H, int W, int Cin, int Ho, int Wo, int Cout, int ks,
-                               int stride, int pad, float* part, int splits, const float* in_scale,
-                               const float* in_shift, int in_act, hipStream_t stream) {
-  if (!gy) return (int)hipErrorInvalidValue;
-  return conv_wgrad(da, ldda, x, ldx, N, H, W, Cin, Ho, Wo, Cout, ks, stride, pad, part, splits, stream, false, false,
-                    in_scale, in_shift, in_act, gy, ldgy, gst, gact);
-}
-SEG_API int seg_conv_wgrad_bwx_bf16io(const __bf16* da, long ldda, const __bf16* gy, long ldgy, const float* gst,
-                                      int gact, const __bf16* x, long ldx, int N, int H, int W, int Cin, int Ho, int Wo,
-                                      int Cout, int ks, int stride, int pad, float* part, int splits,
-                                      const float* in_scale, const float* in_shift, int in_act, hipStream_t stream) {
-  if (!gy) return (int)hipErrorInvalidValue;
-  return conv_wgrad(da, ldda, x, ldx, N, H, W, Cin, Ho, Wo, Cout, ks, stride, pad, part, splits, stream, true, true,
-                    in_scale, in_shift, in_act, gy, ldgy, gst, gact);
 }
 
 // dW (PyTorch layout) = sum over the split-K partial slabs, fixed order.

@@ -99,9 +99,6 @@ PROTOTYPES = {
     "seg_conv_pw": (_I, [_V, _L, _L, _I, _V, _I, _V, _V, _L, _I, _V, _L, _V, _V, _V, _I, _V]),
     "seg_conv_igemm2_bf16io": (_I, [_V, _L, _I, _I, _I, _I, _V, _I, _V, _V, _L, _I, _I, _V, _L, _V, _V, _V]),
     "seg_igemm2_force_tile": (_I, [_I]),
-    "seg_igemm2_il": (_I, [_I]),
-    "seg_conv_wgrad3_splits": (_I, [_I, _I, _I, _I, _I, _I]),
-    "seg_conv_wgrad3_bf16io": (_I, [_V, _L, _V, _L, _I, _I, _I, _I, _I, _I, _V, _V]),
     "seg_igemm2_tune": (_I, [_I, _I]),
     "seg_conv_wgrad2_ok": (_I, [_I, _I, _I, _I, _I]),
     "seg_conv_wgrad2_blocks": (_I, [_I, _I, _I]),
@@ -148,18 +145,6 @@ PROTOTYPES["seg_conv_igemm_bf16io_w16"] = PROTOTYPES["seg_conv_igemm"]
 PROTOTYPES["seg_conv_halo_bf16io_w16"] = PROTOTYPES["seg_conv_halo"]
 PROTOTYPES["seg_conv_igemm_bf16io_xf_w16"] = PROTOTYPES["seg_conv_igemm_bf16io_xf"]
 PROTOTYPES["seg_conv_pw_bf16io"] = PROTOTYPES["seg_conv_pw"]
-# BatchNorm backward formed on load (bwx): the consumer entries take (dA, ld, y, ld, st, act) for dY
-PROTOTYPES["seg_conv_igemm_bwx_ok"] = (_I, [_I, _I, _I])
-PROTOTYPES["seg_conv_igemm_bwx"] = (_I, [_V, _L, _I, _I, _I, _I, _V, _L, _V, _I, _V, _I, _V, _L, _I, _I, _V, _L, _V, _L,
-                                         _V, _V, _V, _I, _V, _V])
-PROTOTYPES["seg_conv_igemm_bwx_bf16io_w16"] = PROTOTYPES["seg_conv_igemm_bwx"]
-PROTOTYPES["seg_conv_pw_bwx"] = (_I, [_V, _L, _V, _L, _V, _I, _L, _I, _V, _I, _V, _L, _I, _V, _L, _V])
-PROTOTYPES["seg_dw_dgrad_bwx"] = (_I, [_V, _L, _V, _L, _V, _I, _I, _I, _I, _I, _V, _V, _L, _I, _I, _I, _I, _V])
-PROTOTYPES["seg_dw_wgrad_bwx"] = (_I, [_V, _L, _V, _L, _V, _I, _V, _L, _I, _I, _I, _I, _V, _V, _I, _I, _I, _I, _V, _V])
-PROTOTYPES["seg_conv_wgrad_bwx"] = (_I, [_V, _L, _V, _L, _V, _I, _V, _L, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _V, _I,
-                                         _V, _V, _I, _V])
-for _n in ("seg_conv_pw_bwx", "seg_dw_dgrad_bwx", "seg_dw_wgrad_bwx", "seg_conv_wgrad_bwx"):
-    PROTOTYPES[_n + "_bf16io"] = PROTOTYPES[_n]
 
 _lock = threading.Lock()
 _lib = None

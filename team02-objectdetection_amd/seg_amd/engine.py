@@ -309,8 +309,7 @@ class ConvOp:
         if self.bn is None:
             return
         bn, C, M = self.bn, self.cout, y.M
-        # [7][C]: mean, invstd, scale, shift (the forward) + the backward's coefficients k1..k3 (SegBwx4 planes)
-        st = torch.empty(7 * C, device=rt.device, dtype=torch.float32)
+        st = torch.empty(4 * C, device=rt.device, dtype=torch.float32)
         mean, invstd, scale, shift = _stat_ptrs(st, C)
         if rt.training:
             if bn.momentum is None:
@@ -411,48 +410,9 @@ class ConvOp:
         rt.bn_parts[id(p)] = [part, tiles, None]
         return (rt.ptr(py), py.ld, scale, shift, mean, p.act, part.data_ptr()), p
 
-    # -- BatchNorm backward formed on load (BWX)
-    def _bwx_dgrad_ok(self, rt, i, bw) -> bool:
-        """Whether this op's data gradient into `i` has a bwx form for its kernel choice (the other forms: halo /
-        Winograd / igemm2 / fp32-pack bf16io / bf16-math keep the apply pass)."""
-        if self.first:
-            return True  # no data gradient
-        if self.kind == "dw":
-            return True
-        if self.stride != 1 or self.halo_d or self.wino_fd or self.wino_d or self.ig2_d is not None:
-            return False
-        if rt.io and not self.w16_d and not self.pw_d:
-            return False
-        if self.bf and not rt.io:
-            return False
-        add_ptr, add_ld = rt.peek_write_add(i)
-        if self.pw_d:
-            return add_ptr is None or (add_ld % (16 // rt.es) == 0 and add_ptr % 16 == 0)
-        return bool(query("seg_conv_igemm_bwx_ok", self.cout, self.ks, int(rt.io)))
-
-    def _bwx_wgrad_ok(self, rt) -> bool:
-        if not BWX_W or not self.conv.weight.requires_grad:
-            return False
-        if self.conv.bias is not None and self.conv.bias.requires_grad and not ZERO_BN_BIAS:
-            return False  # the bias gradient reduces dY itself
-        if self.kind == "dw":
-            return True
-        if self.wino_w or self.w2:
-            return False
-        return rt.io if self.bf else True
-
     def backward(self, rt):
         s, y = rt.stream, self.y
         dA = rt.grad_of(self.out)
-        bw = None  # (dA, y, st, act) when dY is formed on load by the consumers (BWX)
-        if self.bn is not None and rt.training and BWX:
-            v = 16 // rt.es
-            yok = y.ld % v == 0 and rt.ptr(y) % 16 == 0 and dA.ld % v == 0 and rt.gptr(dA) % 16 == 0
-            if yok and self._bwx_dgrad_ok(rt, self.inp, None):
-                bw = (dA, y, rt.saved[id(self)].data_ptr(), self.act)
-        if bw is not None:
-            self._backward_bwx(rt, dA, bw)
-            return
         if self.bn is not None:
             if not rt.training:
                 raise NotImplementedError("backward through eval-mode BatchNorm is not supported")
@@ -500,43 +460,7 @@ class ConvOp:
         if not self.first and not late:
             self._dgrad(rt, dY, dYp, s)
 
-    def _backward_bwx(self, rt, dA, bw):
-        """BatchNorm backward with dY formed on load: the reduction (dgamma, dbeta and the coefficients k1..k3 into
-        the statistics' planes 4..6) on the main stream, then the data gradient and the weight gradient read dA and y
-        (seg_*_bwx).  A weight gradient without a bwx form gets the apply pass on the side stream, beside it."""
-        s, y, C, M = rt.stream, self.y, self.cout, self.y.M
-        st = rt.saved[id(self)]
-        mean, invstd, scale, shift = _stat_ptrs(st, C)
-        coef = st.data_ptr() + 16 * C
-        g_w, g_b = rt.grad_param(self.bn.weight), rt.grad_param(self.bn.bias)
-        abytes = 2 * M * C * rt.es  # the reduction's pass (dA and y read once); the apply's 3 |Y| are gone
-        bp = rt.bn_parts.pop(id(self), None)
-        if bp is not None and bp[2] == rt.wgen.get(self.out.buf):
-            rt.tcall("bn_bwd", 0, "seg_bn_bwd_finalize_tiles", bp[0].data_ptr(), bp[1], M, C,
-                     self.bn.weight.data_ptr(), invstd, g_w, g_b, coef, s)
-        else:
-            work = rt.tmp(query("seg_chan_workspace_floats", M, C))
-            rt.tcall("bn_bwd", abytes, rt.k("seg_bn_bwd_coef"), rt.gptr(dA), dA.ld, rt.ptr(y), y.ld, M, C,
-                     self.bn.weight.data_ptr(), mean, invstd, scale, shift, self.act, g_w, g_b, work.data_ptr(), coef, s)
-        if self.res is not None:
-            rt.add_pending(self.res, dA)
-        for p in (self.conv.weight, self.conv.bias):
-            if p is not None and p.requires_grad:
-                rt.grad_param(p)
-        bww = self._bwx_wgrad_ok(rt)
-        if not self.first:
-            self._dgrad(rt, None, None, s, bw=bw)
-        ctx, sw = rt.fork()
-        with ctx:
-            if bww:
-                self._param_grads(rt, None, None, sw, bw=bw)
-            else:  # the apply pass on the weight gradient's stream
-                dY = Act(rt.tmp_buf(M * r4(C)), 0, r4(C), C, y.N, y.H, y.W)
-                rt.tcall("bn_bwd", 3 * M * C * rt.es, rt.k("seg_bn_bwd_apply"), rt.gptr(dA), dA.ld, rt.ptr(y), y.ld, M,
-                         C, mean, scale, shift, self.act, coef, rt.ptr(dY), dY.ld, sw)
-                self._param_grads(rt, dY, rt.ptr(dY), sw)
-
-    def _param_grads(self, rt, dY, dYp, s, bw=None):
+    def _param_grads(self, rt, dY, dYp, s):
         """Bias gradient (column sum of dY), weight gradient (split-K slabs + fixed-order
         reduce) and the DDP readiness hook, all on stream `s`."""
         y, M = self.y, self.y.M
@@ -559,13 +483,8 @@ class ConvOp:
             if self.kind == "dw":
                 nblk = query("seg_dw_wgrad_blocks", y.N, y.H, y.W, self.cout)
                 part = rt.tmp(nblk * 9 * self.cout)
-                if bw is not None:
-                    dA, by, bst, bact = bw
-                    rt.call(rt.k("seg_dw_wgrad_bwx"), rt.gptr(dA), dA.ld, rt.ptr(by), by.ld, bst, bact, rt.ptr(i), i.ld,
-                            i.N, i.H, i.W, i.C, *self._in_xform(rt), y.H, y.W, self.stride, part.data_ptr(), s)
-                else:
-                    rt.call(rt.k("seg_dw_wgrad"), dYp, dY.ld, rt.ptr(i), i.ld, i.N, i.H, i.W, i.C, *self._in_xform(rt),
-                            y.H, y.W, self.stride, part.data_ptr(), s)
+                rt.call(rt.k("seg_dw_wgrad"), dYp, dY.ld, rt.ptr(i), i.ld, i.N, i.H, i.W, i.C, *self._in_xform(rt), y.H, y.W,
+                     self.stride, part.data_ptr(), s)
                 rt.call("seg_conv_wgrad_reduce", part.data_ptr(), nblk, gw, self.cout, 1, 3, 1, 0, s)
             elif self.wino_w:
                 splits = query("seg_conv_wino_wgrad_splits", y.N, y.H, y.W, self.cin_pad, self.cout)
@@ -583,54 +502,23 @@ class ConvOp:
                 splits = query("seg_conv_wgrad_splits_bf16" if self.bf else "seg_conv_wgrad_splits", M, self.cout,
                                self.cin_pad, self.ks)
                 part = rt.tmp(splits * self.cout * self.ks * self.ks * self.cin_pad)
-                if bw is not None:  # dY formed on load (and X's lazy BN, if any)
-                    dA, by, bst, bact = bw
-                    rt.tcall(f"igemm{self.ks}_wgrad", self.flops(), rt.k("seg_conv_wgrad_bwx"), rt.gptr(dA), dA.ld,
-                             rt.ptr(by), by.ld, bst, bact, rt.ptr(i), i.ld, i.N, i.H, i.W, self.cin_pad, y.H, y.W,
-                             self.cout, self.ks, self.stride, self.pad, part.data_ptr(), splits, *self._in_xform(rt), s)
-                else:
-                    name = ("seg_conv_wgrad_bf16io" if rt.io else "seg_conv_wgrad_bf16") if self.bf else "seg_conv_wgrad"
-                    xf = ()
-                    if self.xform is not None:  # X = the producer's lazy BN + act, formed on load
-                        name, xf = name + "_xf", self._in_xform(rt)
-                    rt.tcall(f"igemm{self.ks}_wgrad", self.flops(), name, dYp, dY.ld, rt.ptr(i), i.ld,
-                             i.N, i.H, i.W, self.cin_pad, y.H, y.W, self.cout, self.ks, self.stride, self.pad,
-                             part.data_ptr(), splits, *xf, s)
+                name = ("seg_conv_wgrad_bf16io" if rt.io else "seg_conv_wgrad_bf16") if self.bf else "seg_conv_wgrad"
+                xf = ()
+                if self.xform is not None:  # X = the producer's lazy BN + act, formed on load
+                    name, xf = name + "_xf", self._in_xform(rt)
+                rt.tcall(f"igemm{self.ks}_wgrad", self.flops(), name, dYp, dY.ld, rt.ptr(i), i.ld,
+                            i.N, i.H, i.W, self.cin_pad, y.H, y.W, self.cout, self.ks, self.stride, self.pad,
+                            part.data_ptr(), splits, *xf, s)
                 rt.call("seg_conv_wgrad_reduce", part.data_ptr(), splits, gw, self.cout, self.cin, self.ks, 0, 0, s)
         rt.params_done(self.params(), s)
 
-    def _dgrad(self, rt, dY, dYp, s, bw=None):
-        """Data gradient into the input's gradient region (first writer / fused addend).  bw: dY formed on load
-        from (dA, y, st, act) by the kernel (only where ConvOp._bwx_dgrad_ok holds)."""
+    def _dgrad(self, rt, dY, dYp, s):
+        """Data gradient into the input's gradient region (first writer / fused addend)."""
         y, i = self.y, self.inp
         if self.kind == "dw":
             acc = rt.begin_write_accumulate(i)
-            if bw is not None:
-                dA, by, bst, bact = bw
-                rt.call(rt.k("seg_dw_dgrad_bwx"), rt.gptr(dA), dA.ld, rt.ptr(by), by.ld, bst, bact, y.N, y.H, y.W,
-                        self.cout, self.wk_f.data_ptr(), rt.gptr(i), i.ld, i.H, i.W, self.stride, acc, s)
-            else:
-                rt.call(rt.k("seg_dw_dgrad"), dYp, dY.ld, y.N, y.H, y.W, self.cout, self.wk_f.data_ptr(), rt.gptr(i),
-                        i.ld, i.H, i.W, self.stride, acc, s)
-        elif bw is not None:
-            dA, by, bst, bact = bw
-            kin = self.cout
-            add_ptr, add_ld = rt.begin_write_add(i)
-            if self.pw_d:
-                rt.tcall("igemm1_dgrad", self.flops(), rt.k("seg_conv_pw_bwx"), rt.gptr(dA), dA.ld, rt.ptr(by), by.ld,
-                         bst, bact, y.M, kin, self.wk_d.data_ptr(), self.ldk_d, rt.gptr(i), i.ld, self.cin, add_ptr,
-                         add_ld, s)
-                rt.mark_written(i)
-                return
-            bo = self._bnout(rt, i)
-            bargs = bo[0] if bo is not None else (None, 0, None, None, None, 0, None)
-            rt.tcall(f"igemm{self.ks}_dgrad", self.flops(),
-                     "seg_conv_igemm_bwx_bf16io_w16" if rt.io else "seg_conv_igemm_bwx", rt.gptr(dA), dA.ld, y.N,
-                     y.H, y.W, kin, rt.ptr(by), by.ld, bst, bact, self.wk_d.data_ptr(), self.ldk_d, rt.gptr(i), i.ld,
-                     self.cin, self.ks, add_ptr, add_ld, *bargs, s)
-            rt.mark_written(i)
-            if bo is not None:  # the partials are valid while this write is the buffer's last
-                rt.bn_parts[id(bo[1])][2] = rt.wgen[i.buf]
+            rt.call(rt.k("seg_dw_dgrad"), dYp, dY.ld, y.N, y.H, y.W, self.cout, self.wk_f.data_ptr(), rt.gptr(i),
+                    i.ld, i.H, i.W, self.stride, acc, s)
         else:
             if self.stride != 1:
                 raise NotImplementedError("data gradient of a strided dense conv")
@@ -1396,13 +1284,6 @@ class Run:
         else:
             self.pending[target.key()] = addend
 
-    def peek_write_add(self, a: Act):
-        """begin_write_add's (add_ptr, add_ld) without consuming a pending addend."""
-        if self._covered(a):
-            return self.gptr(a), a.ld
-        add = self.pending.get(a.key())
-        return (self.gptr(add), add.ld) if add is not None else (None, 0)
-
     def begin_write_add(self, a: Act):
         """For writers with a fused addend: returns (add_ptr, add_ld)."""
         if self._covered(a):
@@ -1581,17 +1462,10 @@ IGEMM2_WIDE = os.environ.get("SEG_IGEMM2_WIDE", "1") == "1"
 W16 = os.environ.get("SEG_W16", "1") == "1"
 # many-tile BN statistics merged 16 tiles per row before the per-channel finalize; SEG_BN_MERGE=0 = direct
 BN_MERGE = os.environ.get("SEG_BN_MERGE", "1") == "1"
-# BatchNorm backward formed on load ("bwx", common.h SegBwx4): the conv's data gradient and weight gradient read the
-# BN layer's dA and raw output y and form dY themselves, so the apply pass (and its dY tensor) disappears from the
-# step; a consumer without a bwx form gets the apply pass on its own stream (the weight gradient's: the side
-# stream).  Measured slower (profiles/r06/ab_bwx.txt: bf16io 3186 vs 3746, f32 1738 vs 1879 img/s): off by default;
-# SEG_BWX=1 = on; SEG_BWX_W=0 = data gradients only.
-BWX = os.environ.get("SEG_BWX", "0") == "1"
-BWX_W = os.environ.get("SEG_BWX_W", "1") == "1"
 
 # Diagnostics only (wrong training): SEG_DIAG_SKIP_WGRAD=1 issues no conv weight / bias gradient at all -- the step
-# time of the main stream's work alone, with no side-stream contention (the contention budget, DESIGN round 6)
-# (SEG_DIAG_SKIP_WGRAD=lo:hi skips only the program ops lo <= k < hi)
+# time of the main stream's work alone, with no side-stream contention (the weight gradients' share of the step,
+# DESIGN round 6); SEG_DIAG_SKIP_WGRAD=lo:hi skips only those of the program ops lo <= k < hi
 _dsw = os.environ.get("SEG_DIAG_SKIP_WGRAD", "0")
 DIAG_SKIP_WGRAD = None if _dsw == "0" else (0, 1 << 30) if _dsw == "1" else tuple(int(v) for v in _dsw.split(":"))
 # Diagnostics (tests flip these): the Winograd transforms one at a time (parity attribution,

@@ -173,39 +173,3 @@ def test_engine_routes_wide_convs_to_igemm2(monkeypatch):
                 assert op.ig2_d is None, (op.cin, op.cout, op.y.M)
         if wide:
             assert sum(op.ig2_f is not None for op in big) >= 4 and sum(op.ig2_d is not None for op in big) >= 4
-
-
-@pytest.mark.parametrize("N,Cin,Cout,H,W,ks", CASES[:8] + CASES[-3:])
-@pytest.mark.parametrize("tile", [-1, 0, 1, 2, 5])
-def test_igemm2_interleaved_loop_bitwise(N, Cin, Cout, H, W, ks, tile):
-    """Round 6: the interleaved-DMA K loop (seg_igemm2_il(1), the default) against the round-3 loop -- the same
-    K order and split boundaries, so outputs, statistics and split-K combines are bitwise equal, on the plan's
-    tile and on forced ones (1-3 K steps per slice, ragged M and N, taps wrapping inside a step)."""
-    M = N * H * W
-    prev = query("seg_igemm2_il", -1)
-    try:
-        query("seg_igemm2_force_tile", tile)
-        ok, (tile_rows, ntiles, splits, work_floats) = plan(M, Cout, Cin, ks)
-        if not ok:
-            pytest.skip("plan does not apply")
-        g = torch.Generator().manual_seed(N + Cin + 3 * Cout)
-        x = (torch.randn(M, Cin, generator=g)).to(BF).to(DEV)
-        w = (torch.randn(Cout, Cin, ks, ks, generator=g) * 0.1).to(DEV)
-        b = torch.randn(Cout, generator=g).to(DEV)
-        add = torch.randn(M, Cout, generator=g).to(BF).to(DEV)
-        wk, ldk = pack16(w, Cout, Cin, ks)
-        res = []
-        for il in (0, 1):
-            query("seg_igemm2_il", il)
-            work = torch.zeros(max(work_floats, 1), device=DEV)
-            y = torch.full((M, Cout), 3.0, device=DEV).to(BF)
-            st = torch.full((ntiles * 2 * Cout,), float("nan"), device=DEV)
-            call("seg_conv_igemm2_bf16io", x.data_ptr(), Cin, N, H, W, Cin, wk.data_ptr(), ldk, b.data_ptr(),
-                 y.data_ptr(), Cout, Cout, ks, add.data_ptr(), Cout, st.data_ptr(), work.data_ptr(), S())
-            res.append((y, st))
-        torch.cuda.synchronize()
-        assert torch.equal(res[0][0], res[1][0])
-        assert torch.equal(res[0][1], res[1][1])
-    finally:
-        query("seg_igemm2_force_tile", -1)
-        query("seg_igemm2_il", prev)

@@ -454,9 +454,25 @@ class ConvOp:
         late = FORK_LATE and not self.first
         if late:  # the data gradient first: the side stream's weight gradient then runs beside
             self._dgrad(rt, dY, dYp, s)  # the next layer's memory-bound BN backward, not this dgrad
-        ctx, sw = rt.fork()
-        with ctx:
-            self._param_grads(rt, dY, dYp, sw)
+        k = getattr(rt, "cur_op", -1)
+        if WGRAD_TAIL and rt.side is not None and rt.sync is None and 0 <= k < WGRAD_TAIL:
+            # the backward's last layers: their parameter gradients go on the MAIN stream after its last data
+            # gradient (Run.flush_tail), sharing the end-of-step backlog with the side stream
+            for p in (self.conv.weight, self.conv.bias):
+                if p is not None and p.requires_grad:
+                    rt.grad_param(p)
+            rt.tail.append((self, dY, dYp))
+        elif rt.defer is not None and rt.side is not None and k >= rt.defer[0]:
+            # issued later, beside the memory-bound part of the backward (Run.flush_deferred); dY stays valid
+            # (persistent within the run)
+            for p in (self.conv.weight, self.conv.bias):
+                if p is not None and p.requires_grad:
+                    rt.grad_param(p)
+            rt.deferred.append((self, dY, dYp))
+        else:
+            ctx, sw = rt.fork()
+            with ctx:
+                self._param_grads(rt, dY, dYp, sw)
         if not self.first and not late:
             self._dgrad(rt, dY, dYp, s)
 
@@ -638,6 +654,18 @@ class Program:
         self.out_hw = (H, W)
         self._n = 0
         self.image = self.new(3, H, W, name=IMAGE)  # NHWC4 copy of the input batch
+
+    def wgrad_defer(self):
+        """(from, at): the parameter gradients of ops >= from wait until the backward reaches op `at`, or None.
+        bf16io default (DEFER_DECODER): the decoder's (from its first upsample on) until the encoder's last op --
+        issued beside the encoder's memory-bound backward instead of the decoder's data-gradient convs
+        (interleaved A/B, profiles/r06/ab_wgrad_defer.txt: bf16io +1.3 %, f32 -0.8 %)."""
+        if WGRAD_DEFER is not None:
+            return WGRAD_DEFER
+        if not DEFER_DECODER or self.math != "bf16io":
+            return None
+        first_up = next((k for k, op in enumerate(self.ops) if isinstance(op, UpsampleOp)), None)
+        return (first_up, first_up - 1) if first_up else None
 
     def mbconv_groups(self):
         """Folded forward: op index -> the (expand, depthwise, project) or (depthwise, project) ConvOps of a
@@ -1139,6 +1167,9 @@ class Run:
         self._tmp_n = 0
         self.side = side      # side stream of the parameter gradients (recorded backward)
         self._n_fork = 0      # side-stream forks so far (index into the program's event pool)
+        self.deferred = []    # (op, dY, dY ptr) whose parameter gradients wait for flush_deferred (WGRAD_DEFER)
+        self.tail = []        # ... for flush_tail (WGRAD_TAIL)
+        self.defer = prog.wgrad_defer()  # (from, at) of the deferred parameter gradients, or None
 
     def k(self, name: str) -> str:
         """C-ABI entry point of an activation kernel for this run's storage type."""
@@ -1242,6 +1273,22 @@ class Run:
         ev.record(self.main)
         self.side.wait_event(ev)
         return self._side_ctx, self.side.cuda_stream
+
+    def flush_deferred(self):
+        """Issue the deferred parameter gradients on the side stream, in backward order, behind one fork."""
+        if not self.deferred:
+            return
+        ctx, sw = self.fork()
+        with ctx:
+            for op, dY, dYp in self.deferred:
+                op._param_grads(self, dY, dYp, sw)
+        self.deferred = []
+
+    def flush_tail(self):
+        """The WGRAD_TAIL parameter gradients on the main stream, after every data gradient of the backward."""
+        for op, dY, dYp in self.tail:
+            op._param_grads(self, dY, dYp, self.stream)
+        self.tail = []
 
     def join(self):
         if self.side is None:
@@ -1407,9 +1454,13 @@ class Run:
         try:
             for k in range(len(self.prog.ops) - 1, -1, -1):
                 self.cur_op = k
+                if self.defer is not None and k == self.defer[1]:
+                    self.flush_deferred()
                 if self.rec is not None:
                     self.rec.label = f"{k}:bwd"
                 self.prog.ops[k].backward(self)
+            self.flush_deferred()
+            self.flush_tail()
         finally:
             self.join()
         if DEBUG_KEEP_RUN:
@@ -1460,6 +1511,16 @@ IGEMM2_MAX_ROWS = int(os.environ.get("SEG_IGEMM2_MAX_ROWS", "65536"))
 IGEMM2_WIDE = os.environ.get("SEG_IGEMM2_WIDE", "1") == "1"
 # bf16io implicit GEMMs on bf16-packed weights (seg_conv_igemm_bf16io_w16); SEG_W16=0 keeps the fp32 packs
 W16 = os.environ.get("SEG_W16", "1") == "1"
+# SEG_WGRAD_DEFER=from:at (A/B): the parameter gradients of program ops >= `from` are issued on the side stream only
+# when the backward reaches op `at` (all of them behind one fork), instead of right after each layer's data gradient
+_wd = os.environ.get("SEG_WGRAD_DEFER", "")
+WGRAD_DEFER = tuple(int(v) for v in _wd.split(":")) if _wd else None
+# bf16io: the decoder's parameter gradients deferred until the backward reaches the encoder (Program.wgrad_defer);
+# SEG_DEFER_DECODER=0 = off
+DEFER_DECODER = os.environ.get("SEG_DEFER_DECODER", "1") == "1"
+# SEG_WGRAD_TAIL=K (A/B): the parameter gradients of program ops < K go on the main stream after the backward's last
+# data gradient instead of on the side stream
+WGRAD_TAIL = int(os.environ.get("SEG_WGRAD_TAIL", "0"))
 # many-tile BN statistics merged 16 tiles per row before the per-channel finalize; SEG_BN_MERGE=0 = direct
 BN_MERGE = os.environ.get("SEG_BN_MERGE", "1") == "1"
 

@@ -548,6 +548,9 @@ int seg_tape_destroy(void* tape);
 int seg_tape_set_arg(void* tape, long i, long value);
 int seg_tape_timing(void* tape, const int* idx, int n, int max_replays);
 int seg_tape_elapsed(void* tape, float* out);
+/* The timed launches of replay r as a timeline (tools/timeline.py): out[2k], out[2k + 1] = start / end of timed
+ * launch k in ms after the start of timed launch 0.  Returns 0, or minus a hipError_t. */
+int seg_tape_timeline(void* tape, int r, float* out);
 int seg_tape_run(void* tape, int begin, hipStream_t main, hipStream_t side, int* stop);
 
 /* seg_conv_igemm2_bf16io: implicit GEMM for the deep convs of the bf16io configuration

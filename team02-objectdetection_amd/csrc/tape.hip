@@ -173,6 +173,21 @@ SEG_API int seg_tape_timing(void* tape, const int* idx, int n, int max_replays) 
 
 // Elapsed milliseconds of the timed entries, out[replay][slot] for the replays done
 // (<= max_replays); returns that count, or -hipError.  Call after the work completed.
+// The timed launches of replay r as a timeline: out[2k], out[2k + 1] = start and end of timed launch k in ms after
+// the start of timed launch 0 (the replay's first timed launch).  Returns 0, or minus a hipError_t.
+SEG_API int seg_tape_timeline(void* tape, int r, float* out) {
+  Tape* t = static_cast<Tape*>(tape);
+  if (!t || !out || r < 0 || r >= std::min(t->replay + 1, t->max_replays) || t->nslots < 1)
+    return -(int)hipErrorInvalidValue;
+  const size_t b0 = (size_t)r * t->nslots * 2;
+  for (int k = 0; k < t->nslots; ++k)
+    for (int e = 0; e < 2; ++e) {
+      const hipError_t rc = hipEventElapsedTime(&out[2 * k + e], t->tev[b0], t->tev[b0 + 2 * k + e]);
+      if (rc != hipSuccess) return -(int)rc;
+    }
+  return 0;
+}
+
 SEG_API int seg_tape_elapsed(void* tape, float* out) {
   Tape* t = static_cast<Tape*>(tape);
   if (!t || !out) return -(int)hipErrorInvalidValue;

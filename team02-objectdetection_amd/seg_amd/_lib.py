@@ -91,6 +91,7 @@ PROTOTYPES = {
     "seg_tape_set_arg": (_I, [_V, _L, _L]),
     "seg_tape_timing": (_I, [_V, _V, _I, _I]),
     "seg_tape_elapsed": (_I, [_V, _V]),
+    "seg_tape_timeline": (_I, [_V, _I, _V]),
     "seg_tape_run": (_I, [_V, _I, _V, _V, _V]),
     "seg_set_combine_spin": (_I, [_I]),
     "seg_build_hash": (_I, [ctypes.c_char_p, _I]),

@@ -133,6 +133,7 @@ class Tape:
         self.callbacks = rec.callbacks
         self.ext_slots = {k: list(v) for k, v in rec.ext_slots.items()}
         self.timers = rec.timers
+        self.streams = [s for (_, _, s, _) in rec.entries]  # 0 = main, 1 = side (tools/timeline.py)
         self._stop_ids = {i: f for i, (k, f, _, _) in enumerate(rec.entries) if k == STOP}
         self._timed = None
         self._replays = 0
@@ -182,6 +183,15 @@ class Tape:
         _lib.call("seg_tape_timing", self.handle, idx.ctypes.data if len(idx) else None, len(idx), replays)
         self._timed = sel if len(idx) else None
         self._replays = replays
+
+    def timeline(self, r):
+        """Replay r's timed launches as [(entry index, start ms, end ms)] after its first timed launch."""
+        n = len(self._timed or ())
+        out = np.zeros(2 * max(n, 1), dtype=np.float32)
+        rc = _lib.lib().seg_tape_timeline(self.handle, r, out.ctypes.data)
+        if rc:
+            raise _lib.SegLibError(f"seg_tape_timeline failed: {-rc}")
+        return [(t[0], float(out[2 * k]), float(out[2 * k + 1])) for k, t in enumerate(self._timed)]
 
     def elapsed(self, detail=False):
         """[(kind, flops, seconds)] of every timed launch of the replays so far (after a

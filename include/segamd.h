@@ -224,7 +224,16 @@ int seg_conv_wino_wgrad_pick(int N, int H, int W, int Cin, int Cout);
 int seg_conv_wino_wgrad_splits(int N, int H, int W, int Cin, int Cout);
 int seg_conv_wino_wgrad(const float* dy, long lddy, const float* x, long ldx, int N, int H, int W, int Cin,
                         int Cout, float* part, int splits, hipStream_t stream);
-int seg_conv_wino_wgrad_reduce(const float* part, int splits, float* dw, int Cout, int Cin, int Cin_pad,
+/* The same slabs as seg_conv_wino_wgrad (same arguments, split boundaries and sums) from blocks that own
+ * all 16 transform points of a (Cout, Cin) tile; splits from seg_conv_wino_wgrad16_splits.  Replaces the
+ * direct split-K weight gradient of the stride-1 3x3 convs (csrc/wgrad.hip) where
+ * seg_conv_wino_wgrad_pick returns 2 (reference: the autograd weight gradient of the dense 3x3
+ * nn.Conv2d of src/unet.py:58,61, reached through src/train.py:37 loss.backward()). */
+int seg_conv_wino_wgrad16_splits(int N, int H, int W, int Cin, int Cout);
+int seg_conv_wino_wgrad16(const float* dy, long lddy, const float* x, long ldx, int N, int H, int W, int Cin,
+                          int Cout, float* part, int splits, hipStream_t stream);
+/* Above 16 splits the reduce first sums runs of slabs in place: `part` is consumed. */
+int seg_conv_wino_wgrad_reduce(float* part, int splits, float* dw, int Cout, int Cin, int Cin_pad,
                                int accumulate, hipStream_t stream);
 
 /* Direct 3x3 conv (stride 1, pad 1) with an LDS halo tile for narrow outputs

@@ -969,10 +969,172 @@ __global__ __launch_bounds__(256) void wino_wgrad_kernel(WinoWgradArgs a) {
   }
 }
 
+// The same slabs from blocks that own all 16 transform points of a (Cout, Cin) tile: each K step loads a
+// KT-tile strip once -- the 2x2 dY pixels of BM output channels and the 4x4 X pixels of BN input channels, one
+// job (tile, 4-channel group) per thread -- forms its 16 transformed values with two butterfly passes, and wave w
+// runs the GEMMs of points 4w..4w+3.  The per-point kernel above loads 4 dY and 4 X pixels per point, i.e. 128
+// pixel-channel reads per tile against 20 here, which bound it at ~0.36 of the fp32 MFMA peak (its L2->CU operand
+// traffic, 128 B/clk/CU at 128 x 128).  The butterflies keep that kernel's association (columns first, then rows;
+// the +-1 coefficients are exact), and the K order and split boundaries are the same, so the slabs match it.
+template <int BM, int BN, int KT>
+__global__ __launch_bounds__(256) void wino_wgrad16_kernel(WinoWgradArgs a) {
+  constexpr int AJ = KT * BM / 4, BJ = KT * BN / 4;
+  constexpr int MI = BM / 32, NI = BN / 32;
+  static_assert(AJ + BJ == 256 && KT % 2 == 0, "one load job per thread");
+  static_assert(AJ % 64 == 0, "dY and X jobs on whole waves");
+
+  __shared__ __attribute__((aligned(16))) float As[16 * KT * BM];
+  __shared__ __attribute__((aligned(16))) float Bs[16 * KT * BN];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tiles_n = (a.Cin + BN - 1) / BN;
+  const int tiles = tiles_n * ((a.Cout + BM - 1) / BM);
+  const int lid = xcd_swizzle(blockIdx.x, gridDim.x);
+  const int split = lid / tiles, tile = lid - split * tiles;
+  const int tn = tile % tiles_n, tm = tile / tiles_n;
+  const int co0 = tm * BM, n0 = tn * BN;
+  const int kbeg = split * a.kchunk;
+  const int kend = min(a.T, kbeg + a.kchunk);
+
+  // this thread's job: dY (2x2 pixels, 4 output channels) or X (4x4 pixels, 4 input channels) of one tile
+  const bool is_a = tid < AJ;
+  const int j = is_a ? tid : tid - AJ;
+  const int cw = is_a ? BM / 4 : BN / 4;
+  const int jt = j / cw, c = (is_a ? co0 : n0) + (j % cw) * 4;
+  const bool cok = c < (is_a ? a.Cout : a.Cin);
+  f32x4 r[16];
+  auto load = [&](int k0) {
+    const int t = k0 + jt;
+    const bool ok = cok && t < kend;
+    const int tt = ok ? t : 0;
+    const int n = tt / (a.th * a.tw), rem = tt - n * a.th * a.tw;
+    const int ty = rem / a.tw, tx = rem - ty * a.tw;
+    if (is_a) {
+      const long p0 = ((long)n * a.H + 2 * ty) * a.W + 2 * tx;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) r[q] = ld4(ok ? a.dy + (p0 + (q >> 1) * a.W + (q & 1)) * a.lddy + c : g_wzero4);
+    } else {
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int v = 0; v < 4; ++v) {
+          const int hh = 2 * ty - 1 + u, ww = 2 * tx - 1 + v;
+          const bool in = ok && (unsigned)hh < (unsigned)a.H && (unsigned)ww < (unsigned)a.W;
+          r[u * 4 + v] = ld4(in ? a.x + (((long)n * a.H + hh) * a.W + ww) * a.ldx + c : g_wzero4);
+        }
+    }
+  };
+  auto store = [&]() {
+    if (is_a) {  // A dY A^T, A = [1 0; 1 1; 1 -1; 0 -1]: columns (xc) first, then rows (xr)
+      f32x4 q[2][4];
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        q[u][0] = r[2 * u];
+        q[u][1] = r[2 * u] + r[2 * u + 1];
+        q[u][2] = r[2 * u] - r[2 * u + 1];
+        q[u][3] = -r[2 * u + 1];
+      }
+      float* dst = As + jt * BM + (j % cw) * 4;
+#pragma unroll
+      for (int xc = 0; xc < 4; ++xc) {
+        st4(dst + (0 * 4 + xc) * KT * BM, q[0][xc]);
+        st4(dst + (1 * 4 + xc) * KT * BM, q[0][xc] + q[1][xc]);
+        st4(dst + (2 * 4 + xc) * KT * BM, q[0][xc] - q[1][xc]);
+        st4(dst + (3 * 4 + xc) * KT * BM, -q[1][xc]);
+      }
+    } else {  // B^T X B, B^T = [1 0 -1 0; 0 1 1 0; 0 -1 1 0; 0 1 0 -1]: columns first, then rows
+      f32x4 z[4][4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        z[u][0] = r[u * 4 + 0] - r[u * 4 + 2];
+        z[u][1] = r[u * 4 + 1] + r[u * 4 + 2];
+        z[u][2] = -r[u * 4 + 1] + r[u * 4 + 2];
+        z[u][3] = r[u * 4 + 1] - r[u * 4 + 3];
+      }
+      float* dst = Bs + jt * BN + (j % cw) * 4;
+#pragma unroll
+      for (int xc = 0; xc < 4; ++xc) {
+        st4(dst + (0 * 4 + xc) * KT * BN, z[0][xc] - z[2][xc]);
+        st4(dst + (1 * 4 + xc) * KT * BN, z[1][xc] + z[2][xc]);
+        st4(dst + (2 * 4 + xc) * KT * BN, -z[1][xc] + z[2][xc]);
+        st4(dst + (3 * 4 + xc) * KT * BN, z[1][xc] - z[3][xc]);
+      }
+    }
+  };
+
+  f32x16 acc[4][MI][NI];
+#pragma unroll
+  for (int p = 0; p < 4; ++p)
+#pragma unroll
+    for (int mi = 0; mi < MI; ++mi)
+#pragma unroll
+      for (int ni = 0; ni < NI; ++ni)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) acc[p][mi][ni][e] = 0.f;
+
+  const int lrow = lane & 31, lh = lane >> 5;
+  const int nk = (kend - kbeg + KT - 1) / KT;
+  if (nk > 0) {
+    load(kbeg);
+    for (int kt = 0; kt < nk; ++kt) {
+      store();
+      __syncthreads();
+      if (kt + 1 < nk) load(kbeg + (kt + 1) * KT);
+#pragma unroll
+      for (int kk = 0; kk < KT / 2; ++kk)
+#pragma unroll
+        for (int p = 0; p < 4; ++p) {
+          const int xi = 4 * wave + p;
+          float af[MI], bf[NI];
+#pragma unroll
+          for (int mi = 0; mi < MI; ++mi) af[mi] = As[(xi * KT + 2 * kk + lh) * BM + mi * 32 + lrow];
+#pragma unroll
+          for (int ni = 0; ni < NI; ++ni) bf[ni] = Bs[(xi * KT + 2 * kk + lh) * BN + ni * 32 + lrow];
+#pragma unroll
+          for (int mi = 0; mi < MI; ++mi)
+#pragma unroll
+            for (int ni = 0; ni < NI; ++ni)
+              acc[p][mi][ni] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[mi], bf[ni], acc[p][mi][ni], 0, 0, 0);
+        }
+      __syncthreads();
+    }
+  }
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
+    float* slab = a.part + ((long)split * 16 + 4 * wave + p) * a.Cout * a.Cin;
+#pragma unroll
+    for (int ni = 0; ni < NI; ++ni) {
+      const int col = n0 + ni * 32 + lrow;
+      if (col >= a.Cin) continue;
+#pragma unroll
+      for (int mi = 0; mi < MI; ++mi)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+          const int row = co0 + mi * 32 + (e & 3) + 8 * (e >> 2) + 4 * lh;
+          if (row < a.Cout) slab[(long)row * a.Cin + col] = acc[p][mi][ni][e];
+        }
+    }
+  }
+}
+
+// Sums each run of L consecutive slabs into the run's first slab, in slab order (float4 per thread, grid.y =
+// runs): with hundreds of splits the reduce below would otherwise be a chain of hundreds of dependent
+// iterations over only Cout x Cin threads (measured 0.4 us per split on MI355X, tools/ww16sweep.py).
+__global__ __launch_bounds__(256) void wino_wgrad_fold_kernel(float* __restrict__ part, int splits, int L, long E4) {
+  const long e = (long)blockIdx.x * 256 + threadIdx.x;
+  if (e >= E4) return;
+  const int s0 = blockIdx.y * L, s1 = min(splits, s0 + L);
+  f32x4* p = reinterpret_cast<f32x4*>(part) + e;
+  f32x4 acc = p[(long)s0 * E4];
+#pragma unroll 8
+  for (int s = s0 + 1; s < s1; ++s) acc += p[(long)s * E4];
+  p[(long)s0 * E4] = acc;
+}
+
 // dW[co][ci][3][3] (+)= G^T (sum_s P_s) G, one thread per (co, ci < Cin_real); the
 // split sums run in fixed order (bitwise reproducible).
-__global__ __launch_bounds__(256) void wino_wgrad_reduce_kernel(const float* __restrict__ part, int splits, int Cout,
-                                                                int Cin_pad, int Cin, float* __restrict__ dw,
+__global__ __launch_bounds__(256) void wino_wgrad_reduce_kernel(const float* __restrict__ part, int splits, int stride,
+                                                                int Cout, int Cin_pad, int Cin, float* __restrict__ dw,
                                                                 int accumulate) {
   const long i = (long)blockIdx.x * 256 + threadIdx.x;
   if (i >= (long)Cout * Cin) return;
@@ -982,7 +1144,7 @@ __global__ __launch_bounds__(256) void wino_wgrad_reduce_kernel(const float* __r
 #pragma unroll
   for (int x = 0; x < 16; ++x) m[x] = 0.f;
   for (int s = 0; s < splits; ++s) {
-    const float* p = part + (long)s * 16 * plane + off;
+    const float* p = part + (long)s * stride * 16 * plane + off;
 #pragma unroll
     for (int x = 0; x < 16; ++x) m[x] += p[x * plane];
   }
@@ -1123,8 +1285,35 @@ SEG_API int seg_wf2_mask(int m) {
 // Cin, Cout >= 256 at 4096 tiles; 0.97-1.08x for 128-288 channels at 16384 tiles.
 SEG_API int seg_conv_wino_wgrad_pick(int N, int H, int W, int Cin, int Cout) {
   if ((H & 1) || (W & 1) || (Cin & 3) || (Cout & 3)) return 0;
+  return (Cin >= 32 && Cout >= 32) ? 2 : 0;
+}
+
+// Tile (Cout x Cin, square) of wino_wgrad16_kernel.
+#ifndef SEG_WW16_WIDE
+#define SEG_WW16_WIDE 128
+#endif
+static int wgrad16_tile(int Cin, int Cout) { return (Cin >= SEG_WW16_WIDE && Cout >= SEG_WW16_WIDE) ? 64 : 32; }
+
+// Split count of seg_conv_wino_wgrad16 from a cost model fitted to tools/ww16sweep.py on MI355X: a launch runs in
+// rounds of `slots` resident blocks (256 CUs x 1 block of the 64 tile or 2 of the 32 tile); a block costs u ns per
+// 2x2 tile of its K range (64 tile 490, 32 tile 300, with the CU full); the slabs cost their write + read at
+// ~4 TB/s.  Picks the split count (<= 1024, >= 64 tiles per split) of least modelled time.
+SEG_API int seg_conv_wino_wgrad16_splits(int N, int H, int W, int Cin, int Cout) {
   const long T = (long)N * (H / 2) * (W / 2);
-  return (Cin >= 128 && Cout >= 128 && (T >= 65536 || (Cin >= 256 && Cout >= 256))) ? 1 : 0;
+  const int b = wgrad16_tile(Cin, Cout);
+  const long tiles = (long)seg_cdiv(Cout, b) * seg_cdiv(Cin, b);
+  const long slots = b == 64 ? 256 : 512;
+  const double u = b == 64 ? 490.0 : 300.0, slab_ns = 16.0 * Cout * Cin * 4 * 2 / 4000.0;
+  const long smax = std::max<long>(1, std::min<long>(1024, T / 64));
+  long best = 1;
+  double best_t = 0;
+  for (long sp = 1; sp <= smax; ++sp) {
+    const long chunk = seg_cdiv(seg_cdiv(T, sp), (long)WBK) * WBK;
+    const long used = seg_cdiv(T, chunk);  // splits past the end write zero slabs
+    const double t = (double)seg_cdiv(sp * tiles, slots) * chunk * u + sp * slab_ns;
+    if (used == sp && (sp == 1 || t < best_t)) best = sp, best_t = t;
+  }
+  return (int)best;
 }
 
 // Split count of seg_conv_wino_wgrad (partial slabs of 16 * Cout * Cin_pad floats).
@@ -1160,11 +1349,38 @@ SEG_API int seg_conv_wino_wgrad(const float* dy, long lddy, const float* x, long
   SEG_RET_LAST();
 }
 
+// seg_conv_wino_wgrad's slabs (the same arguments and split boundaries) from wino_wgrad16_kernel: one block per
+// (Cout, Cin) tile and split for all 16 transform points.
+SEG_API int seg_conv_wino_wgrad16(const float* dy, long lddy, const float* x, long ldx, int N, int H, int W, int Cin,
+                                  int Cout, float* part, int splits, hipStream_t stream) {
+  if ((H & 1) || (W & 1) || (Cin & 3) || (Cout & 3) || (lddy & 3) || (ldx & 3) || splits < 1)
+    return (int)hipErrorInvalidValue;
+  WinoWgradArgs a;
+  a.dy = dy; a.lddy = lddy; a.x = x; a.ldx = ldx; a.part = part;
+  a.N = N; a.H = H; a.W = W; a.Cin = Cin; a.Cout = Cout;
+  a.th = H / 2; a.tw = W / 2; a.T = N * a.th * a.tw;
+  a.kchunk = seg_cdiv(seg_cdiv(a.T, splits), WBK) * WBK;
+  const int b = wgrad16_tile(Cin, Cout);
+  const dim3 grid(seg_cdiv(Cout, b) * seg_cdiv(Cin, b) * splits);
+  if (b == 64) hipLaunchKernelGGL((wino_wgrad16_kernel<64, 64, 8>), grid, dim3(256), 0, stream, a);
+  else hipLaunchKernelGGL((wino_wgrad16_kernel<32, 32, 16>), grid, dim3(256), 0, stream, a);
+  SEG_RET_LAST();
+}
+
 // dW (PyTorch layout [Cout][Cin][3][3]) (+)= G^T (fixed-order sum of the slabs) G.
-SEG_API int seg_conv_wino_wgrad_reduce(const float* part, int splits, float* dw, int Cout, int Cin, int Cin_pad,
+// Above 16 splits the slabs are first folded in place into <= 16 run sums (the slabs are consumed).
+SEG_API int seg_conv_wino_wgrad_reduce(float* part, int splits, float* dw, int Cout, int Cin, int Cin_pad,
                                        int accumulate, hipStream_t stream) {
-  if (Cin_pad < Cin || splits < 1) return (int)hipErrorInvalidValue;
+  if (Cin_pad < Cin || (Cin_pad & 3) || splits < 1) return (int)hipErrorInvalidValue;
+  int runs = splits, L = 1;
+  if (splits > 16) {
+    L = seg_cdiv(splits, 16);
+    runs = seg_cdiv(splits, L);
+    const long E4 = 4L * Cout * Cin_pad;  // 16 * Cout * Cin_pad floats per slab
+    hipLaunchKernelGGL(wino_wgrad_fold_kernel, dim3(seg_cdiv(E4, 256), runs), dim3(256), 0, stream, part, splits, L,
+                       E4);
+  }
   hipLaunchKernelGGL(wino_wgrad_reduce_kernel, dim3(seg_cdiv((long)Cout * Cin, 256)), dim3(256), 0, stream, part,
-                     splits, Cout, Cin_pad, Cin, dw, accumulate);
+                     runs, L, Cout, Cin_pad, Cin, dw, accumulate);
   SEG_RET_LAST();
 }

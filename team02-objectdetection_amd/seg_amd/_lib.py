@@ -41,6 +41,8 @@ PROTOTYPES = {
     "seg_conv_wino_wgrad_pick": (_I, [_I, _I, _I, _I, _I]),
     "seg_conv_wino_wgrad_splits": (_I, [_I, _I, _I, _I, _I]),
     "seg_conv_wino_wgrad": (_I, [_V, _L, _V, _L, _I, _I, _I, _I, _I, _V, _I, _V]),
+    "seg_conv_wino_wgrad16_splits": (_I, [_I, _I, _I, _I, _I]),
+    "seg_conv_wino_wgrad16": (_I, [_V, _L, _V, _L, _I, _I, _I, _I, _I, _V, _I, _V]),
     "seg_conv_wino_wgrad_reduce": (_I, [_V, _I, _V, _I, _I, _I, _I, _V]),
     "seg_pack_batch": (_I, [_V, _I, _L, _V]),
     "seg_conv_igemm_row_tiles": (_I, [_L, _I, _V]),

@@ -36,7 +36,8 @@ from ._lib import call, query as _query
 # plan: a forced tile (force_igemm_tile) changes them)
 _PURE_QUERIES = {"seg_chan_workspace_floats", "seg_conv_wgrad_splits", "seg_conv_wgrad_splits_bf16", "seg_dw_wgrad_blocks",
                  "seg_conv_igemm_splits", "seg_ce_workspace_floats", "seg_conv_wino_row_tiles", "seg_conv_wino_tile_rows",
-                 "seg_conv_halo_row_tiles", "seg_conv_wino_wgrad_splits", "seg_mbconv_ok"}
+                 "seg_conv_halo_row_tiles", "seg_conv_wino_wgrad_splits", "seg_conv_wino_wgrad16_splits",
+                 "seg_mbconv_ok"}
 _QCACHE = {}
 
 
@@ -503,10 +504,11 @@ class ConvOp:
                      self.stride, part.data_ptr(), s)
                 rt.call("seg_conv_wgrad_reduce", part.data_ptr(), nblk, gw, self.cout, 1, 3, 1, 0, s)
             elif self.wino_w:
-                splits = query("seg_conv_wino_wgrad_splits", y.N, y.H, y.W, self.cin_pad, self.cout)
+                form = "seg_conv_wino_wgrad16" if self.wino_w == 2 else "seg_conv_wino_wgrad"
+                splits = query(form + "_splits", y.N, y.H, y.W, self.cin_pad, self.cout)
                 part = rt.tmp(splits * 16 * self.cout * self.cin_pad)
-                rt.tcall("wino3_wgrad", self.flops(), "seg_conv_wino_wgrad", dYp, dY.ld, rt.ptr(i), i.ld, y.N, y.H,
-                            y.W, self.cin_pad, self.cout, part.data_ptr(), splits, s)
+                rt.tcall("wino3_wgrad", self.flops(), form, dYp, dY.ld, rt.ptr(i), i.ld, y.N, y.H,
+                         y.W, self.cin_pad, self.cout, part.data_ptr(), splits, s)
                 rt.call("seg_conv_wino_wgrad_reduce", part.data_ptr(), splits, gw, self.cout, self.cin, self.cin_pad, 0, s)
             elif self.w2:  # narrow bf16io 3x3: persistent LDS-halo weight gradient, one slab per block
                 blocks = query("seg_conv_wgrad2_blocks", y.N, y.H, y.W)
@@ -857,8 +859,13 @@ class Program:
                   if wino_ok and WINOGRAD_DGRAD and not op.first else 0)
             op.wino_f, op.wino_ff = pf != 0, pf == 2
             op.wino_d, op.wino_fd = pd != 0, pd == 2
-            op.wino_w = wino_ok and WINOGRAD_WGRAD and bool(query("seg_conv_wino_wgrad_pick", y.N, y.H, y.W, op.cin_pad,
-                                                                   op.cout))
+            # seg_conv_wino_wgrad_pick: 2 = the all-points kernel (seg_conv_wino_wgrad16), 1 = the per-point one
+            op.wino_w = (query("seg_conv_wino_wgrad_pick", y.N, y.H, y.W, op.cin_pad, op.cout)
+                         if wino_ok and WINOGRAD_WGRAD and op.xform is None else 0)
+            if op.wino_w == 2 and not WINO_WGRAD16:  # A/B switch: the round-5 rule (per-point kernel, deep convs)
+                T = y.N * (y.H // 2) * (y.W // 2)
+                deep = op.cin_pad >= 128 and op.cout >= 128 and (T >= 65536 or min(op.cin_pad, op.cout) >= 256)
+                op.wino_w = 1 if deep else 0
             op.halo_f = (dense3 and not op.wino_f
                          and bool(query("seg_conv_halo_pick", y.N, y.H, y.W, op.cin_pad, op.cout)))
             op.halo_d = (dense3 and not op.first and not op.wino_d
@@ -1532,6 +1539,8 @@ DIAG_SKIP_WGRAD = None if _dsw == "0" else (0, 1 << 30) if _dsw == "1" else tupl
 # Diagnostics (tests flip these): the Winograd transforms one at a time (parity attribution,
 # tests/test_gpu_unet_cfg5.py) ...
 WINOGRAD_WGRAD = True  # the F(3x3,2x2) weight gradients
+# ... on the all-points kernel (seg_conv_wino_wgrad16; SEG_WINO_WGRAD16=0: the round-5 choice, A/B only)
+WINO_WGRAD16 = os.environ.get("SEG_WINO_WGRAD16", "1") != "0"
 WINOGRAD_FWD = True    # the F(2x2,3x3) forward
 WINOGRAD_DGRAD = True  # ... and data-gradient transforms
 # ... and the fp16 inference (Predictor, BASELINE configs[3]) fusions against their unfused launches: each inverted

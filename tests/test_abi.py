@@ -65,6 +65,15 @@ def test_host_side_queries(lib):
     # split-K only when the output tiles cannot fill the chip
     assert _lib.query("seg_conv_igemm_splits", 32 * 128 * 256, 32, 80, 3) == 1
     assert _lib.query("seg_conv_igemm_splits", 8 * 16, 256, 1344, 3) > 1
+    # the all-points Winograd weight gradient: every dense 3x3 decoder shape >= 32 channels, every split non-empty
+    for N, H, W, Cin, Cout in ((32, 128, 256, 32, 32), (32, 128, 256, 80, 32), (32, 16, 32, 1344, 256),
+                               (8, 512, 1024, 64, 64), (8, 64, 128, 512, 512), (2, 4, 4, 32, 32)):
+        assert _lib.query("seg_conv_wino_wgrad_pick", N, H, W, Cin, Cout) == 2
+        sp = _lib.query("seg_conv_wino_wgrad16_splits", N, H, W, Cin, Cout)
+        T = N * (H // 2) * (W // 2)
+        chunk = -(-(-(-T // sp)) // 16) * 16
+        assert 1 <= sp <= 1024 and -(-T // chunk) == sp, (N, H, W, Cin, Cout, sp)
+    assert _lib.query("seg_conv_wino_wgrad_pick", 8, 512, 1024, 4, 64) == 0  # UNet inc.0 (3 -> 64): direct
     import ctypes
     plan = (ctypes.c_int * 3)()
     for args, want in (((32 * 128 * 256, 32, 80, 3), (1, -1)), ((8 * 16, 256, 1344, 3), (32, 12)),

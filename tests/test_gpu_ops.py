@@ -579,6 +579,36 @@ def test_conv_wino_wgrad(N, Cin, Cout, H, W):
         assert rel(dw2, 2 * wr.grad) < 1e-5
 
 
+@pytest.mark.parametrize("N,Cin,Cout,H,W", [(2, 64, 32, 6, 10), (1, 1344, 256, 4, 8), (2, 152, 64, 8, 6),
+                                           (3, 36, 200, 2, 4), (2, 80, 32, 16, 12), (2, 128, 192, 10, 8),
+                                           (1, 288, 128, 12, 14), (4, 32, 32, 2, 2)])
+def test_conv_wino_wgrad16(N, Cin, Cout, H, W):
+    """seg_conv_wino_wgrad16 (all 16 points per block): bitwise the per-point kernel's slabs at the same split
+    count (up to the sign of zero), and dW vs torch."""
+    x = gen(N, Cin, H, W, seed=44)
+    w = gen(Cout, Cin, 3, 3, seed=45) * 0.1
+    wr = w.clone().requires_grad_(True)
+    y = F.conv2d(x, wr, None, padding=1)
+    dy = gen(*y.shape, seed=46)
+    y.backward(dy)
+    cin4 = r4(Cin)
+    xg, dyg = nhwc(x), nhwc(dy)
+    if Cin % 4:
+        xg[:, Cin:] = 0.0
+    splits = query("seg_conv_wino_wgrad16_splits", N, H, W, cin4, Cout)
+    for sp in sorted({splits, 1, 3, 40}):  # 40: the reduce folds runs of slabs in place first
+        p16 = torch.full((sp * 16 * Cout * cin4,), float("nan"), device=DEV)
+        ref = torch.full_like(p16, float("nan"))
+        call("seg_conv_wino_wgrad16", dyg.data_ptr(), dyg.shape[1], xg.data_ptr(), xg.shape[1], N, H, W, cin4, Cout,
+             p16.data_ptr(), sp, S())
+        call("seg_conv_wino_wgrad", dyg.data_ptr(), dyg.shape[1], xg.data_ptr(), xg.shape[1], N, H, W, cin4, Cout,
+             ref.data_ptr(), sp, S())
+        assert torch.equal(p16, ref), (sp, (p16 - ref).abs().max().item())
+        dw = torch.full((Cout, Cin, 3, 3), float("nan"), device=DEV)
+        call("seg_conv_wino_wgrad_reduce", p16.data_ptr(), sp, dw.data_ptr(), Cout, Cin, cin4, 0, S())
+        assert rel(dw, wr.grad) < 1e-5
+
+
 @pytest.mark.parametrize("N,Cin,Cout,H,W,mode", [(2, 80, 32, 8, 64, 0), (1, 32, 32, 4, 128, 0),
                                                  (2, 152, 64, 4, 64, 0), (1, 64, 64, 12, 64, 0),
                                                  (2, 32, 80, 8, 64, 1), (1, 20, 96, 4, 128, 0)])

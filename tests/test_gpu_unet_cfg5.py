@@ -60,7 +60,7 @@ def _slice_run(x, y, state, side, fwd, dgrad, wgrad):
         z = engine.debug_preactivations(model)
         pools = engine.debug_pool_positions(model)
         prog = engine.get_program(model, *x.shape[:1], *x.shape[2:])
-        n_wino = sum(op.wino_f + op.wino_d + op.wino_w for op in prog.ops if isinstance(op, engine.ConvOp))
+        n_wino = sum(op.wino_f + op.wino_d + bool(op.wino_w) for op in prog.ops if isinstance(op, engine.ConvOp))
     finally:
         engine.DEBUG_KEEP_RUN, engine.LAST_RUN = False, None
         engine.WINOGRAD_FWD, engine.WINOGRAD_DGRAD, engine.WINOGRAD_WGRAD = saved

@@ -35,6 +35,9 @@ namespace {
 #define SEG_RED_THREADS 256  // measured (interleaved A/B, profiles/r05/ab_fused_bn_knobs.txt): bf16io +0.5 %, f32 flat vs 512
 #endif
 constexpr int kRedThreads = SEG_RED_THREADS;
+#ifndef SEG_RQ
+#define SEG_RQ 1  // rows per load group of the fp32 backward partials (4: the round-5 form, A/B)
+#endif
 constexpr int kRedSlice = 64;  // channel groups per block (blockIdx.y slices beyond)
 
 #ifndef SEG_CHAN_MAXBLK
@@ -107,16 +110,21 @@ __global__ __launch_bounds__(kRedThreads) void chan_partial_kernel(
         }
       }
     };
+    // RQ rows' loads issued together; one for the fp32 backward partials (4 x 16-byte loads per lane, 76 VGPRs):
+    // that keeps the kernel within the 80 VGPRs per SIMD a side-stream weight gradient leaves
+    // (wino_wgrad16_kernel: 2 waves x 216), so its waves fit beside one, where the four-row form (148 VGPRs)
+    // waited for whole weight-gradient blocks to retire.  Same row order either way (the sums do not change).
+    constexpr int RQ = (KIND == 1 && sizeof(T) == 4 && VW == 8) ? SEG_RQ : 4;
     int r = r0 + rg;
-    for (; r + 3 * RG < r1; r += 4 * RG) {  // four rows' loads issued together
-      f32x4 v[4][NV], g[4][NV];
+    for (; r + (RQ - 1) * RG < r1; r += RQ * RG) {
+      f32x4 v[RQ][NV], g[RQ][NV];
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
+      for (int q = 0; q < RQ; ++q) {
         ldw<VW>(y + (long)(r + q * RG) * ldy + c, v[q]);
         if (KIND == 1) ldw<VW>(da + (long)(r + q * RG) * ldda + c, g[q]);
       }
 #pragma unroll
-      for (int q = 0; q < 4; ++q) step(v[q], g[q]);
+      for (int q = 0; q < RQ; ++q) step(v[q], g[q]);
     }
     for (; r < r1; r += RG) {
       f32x4 v[NV], g[NV];

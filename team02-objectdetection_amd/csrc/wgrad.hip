@@ -17,7 +17,10 @@
 namespace {
 
 #ifndef SEG_WGRAD_BLOCKS
-#define SEG_WGRAD_BLOCKS 2048  // target blocks (tiles x splits) of a weight-gradient launch
+// target blocks (tiles x splits) of an fp32 weight-gradient launch: 1024 measured beside the main stream with the
+// Winograd weight gradient in place (profiles/r06/ab_wgrad_blocks*.txt): +0.3 / +0.7 % f32 on two boxes vs 2048,
+// 512 -0.7 %, UNet f32 flat
+#define SEG_WGRAD_BLOCKS 1024
 #endif
 #ifndef SEG_WGRAD_BLOCKS_BF16
 #define SEG_WGRAD_BLOCKS_BF16 512
@@ -345,7 +348,7 @@ static int wgrad_splits(long M, int Cout, int Cin, int ks, long target_blocks) {
   return (int)std::max<long>(1, splits);
 }
 #ifndef SEG_WGRAD_THIN
-#define SEG_WGRAD_THIN 2048
+#define SEG_WGRAD_THIN 1024  // thin slabs (<= 2 tiles), same measurement
 #endif
 SEG_API int seg_conv_wgrad_splits(long M, int Cout, int Cin, int ks) {
   int bm, bn;

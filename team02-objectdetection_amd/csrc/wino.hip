@@ -1002,26 +1002,58 @@ __global__ __launch_bounds__(256) void wino_wgrad16_kernel(WinoWgradArgs a) {
   const int cw = is_a ? BM / 4 : BN / 4;
   const int jt = j / cw, c = (is_a ? co0 : n0) + (j % cw) * 4;
   const bool cok = c < (is_a ? a.Cout : a.Cin);
+  // Branch-free buffer loads from per-block bases (the first pixel row the split can read): a padding pixel, a
+  // tile past the split or a channel past C gets an offset past the range check and loads zeros.  The host
+  // checks that a split's pixel span fits the 31-bit offsets (else it runs the per-point kernel).
+  const int tpi = a.th * a.tw;
+  const int tb = min(kbeg, a.T - 1), nb = tb / tpi, tyb = (tb - nb * tpi) / a.tw;
+  const long pbase = ((long)nb * a.H + max(2 * tyb - 1, 0)) * a.W;
+  const long npix = (long)a.N * a.H * a.W;
+  const __amdgpu_buffer_rsrc_t rx =
+      seg_rsrc(a.x + pbase * a.ldx, (unsigned)min((npix - pbase) * a.ldx * 4, (long)kFusedOOB - 16));
+  const __amdgpu_buffer_rsrc_t rdy =
+      seg_rsrc(a.dy + pbase * a.lddy, (unsigned)min((npix - pbase) * a.lddy * 4, (long)kFusedOOB - 16));
+  // this thread's tile, advanced by KT tiles per step without divisions
+  int tcur = kbeg + jt, pn, tty, ttx;
+  {
+    const int tt = min(tcur, a.T - 1);
+    pn = tt / tpi;
+    const int rem = tt - pn * tpi;
+    tty = rem / a.tw;
+    ttx = rem - tty * a.tw;
+  }
+  auto advance = [&]() {
+    tcur += KT;
+    ttx += KT;
+    while (ttx >= a.tw) {
+      ttx -= a.tw;
+      if (++tty == a.th) tty = 0, ++pn;
+    }
+  };
   f32x4 r[16];
-  auto load = [&](int k0) {
-    const int t = k0 + jt;
-    const bool ok = cok && t < kend;
-    const int tt = ok ? t : 0;
-    const int n = tt / (a.th * a.tw), rem = tt - n * a.th * a.tw;
-    const int ty = rem / a.tw, tx = rem - ty * a.tw;
+  auto load = [&]() {
+    const bool ok = cok && tcur < kend;
     if (is_a) {
-      const long p0 = ((long)n * a.H + 2 * ty) * a.W + 2 * tx;
+      const int p0 = (int)(((long)pn * a.H + 2 * tty) * a.W + 2 * ttx - pbase);
 #pragma unroll
-      for (int q = 0; q < 4; ++q) r[q] = ld4(ok ? a.dy + (p0 + (q >> 1) * a.W + (q & 1)) * a.lddy + c : g_wzero4);
-    } else {
+      for (int q = 0; q < 4; ++q)
+        r[q] = seg_bld4(rdy, ok ? (unsigned)(((long)(p0 + (q >> 1) * a.W + (q & 1)) * a.lddy + c) * 4) : kFusedOOB);
+    } else {  // all 16 offsets first, then the 16 loads back to back
+      const unsigned cs = (unsigned)(a.ldx * 4);
+      unsigned off[16];
 #pragma unroll
-      for (int u = 0; u < 4; ++u)
+      for (int u = 0; u < 4; ++u) {
+        const int hh = 2 * tty - 1 + u;
+        const bool rok = ok && (unsigned)hh < (unsigned)a.H;
+        const unsigned rb = (unsigned)(((((long)pn * a.H + hh) * a.W + 2 * ttx - 1 - pbase) * a.ldx + c) * 4);
 #pragma unroll
         for (int v = 0; v < 4; ++v) {
-          const int hh = 2 * ty - 1 + u, ww = 2 * tx - 1 + v;
-          const bool in = ok && (unsigned)hh < (unsigned)a.H && (unsigned)ww < (unsigned)a.W;
-          r[u * 4 + v] = ld4(in ? a.x + (((long)n * a.H + hh) * a.W + ww) * a.ldx + c : g_wzero4);
+          const int ww = 2 * ttx - 1 + v;
+          off[u * 4 + v] = rok && (unsigned)ww < (unsigned)a.W ? rb + v * cs : kFusedOOB;
         }
+      }
+#pragma unroll
+      for (int i = 0; i < 16; ++i) r[i] = seg_bld4(rx, off[i]);
     }
   };
   auto store = [&]() {
@@ -1075,11 +1107,14 @@ __global__ __launch_bounds__(256) void wino_wgrad16_kernel(WinoWgradArgs a) {
   const int lrow = lane & 31, lh = lane >> 5;
   const int nk = (kend - kbeg + KT - 1) / KT;
   if (nk > 0) {
-    load(kbeg);
+    load();
     for (int kt = 0; kt < nk; ++kt) {
       store();
       __syncthreads();
-      if (kt + 1 < nk) load(kbeg + (kt + 1) * KT);
+      if (kt + 1 < nk) {
+        advance();
+        load();
+      }
 #pragma unroll
       for (int kk = 0; kk < KT / 2; ++kk)
 #pragma unroll
@@ -1360,6 +1395,11 @@ SEG_API int seg_conv_wino_wgrad16(const float* dy, long lddy, const float* x, lo
   a.N = N; a.H = H; a.W = W; a.Cin = Cin; a.Cout = Cout;
   a.th = H / 2; a.tw = W / 2; a.T = N * a.th * a.tw;
   a.kchunk = seg_cdiv(seg_cdiv(a.T, splits), WBK) * WBK;
+  if (a.T == 0) return 0;
+  // a split's pixel rows (its tile rows + the halo, across image boundaries) must fit the kernel's 31-bit buffer
+  // offsets from its base; otherwise the per-point kernel writes the same slabs
+  const long span = (2L * (seg_cdiv(a.kchunk, a.tw) + 1) + 2) * W * std::max(ldx, lddy) * 4;
+  if (span >= (long)kFusedOOB - 16) return seg_conv_wino_wgrad(dy, lddy, x, ldx, N, H, W, Cin, Cout, part, splits, stream);
   const int b = wgrad16_tile(Cin, Cout);
   const dim3 grid(seg_cdiv(Cout, b) * seg_cdiv(Cin, b) * splits);
   if (b == 64) hipLaunchKernelGGL((wino_wgrad16_kernel<64, 64, 8>), grid, dim3(256), 0, stream, a);

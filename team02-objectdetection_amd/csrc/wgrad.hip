@@ -32,6 +32,9 @@ namespace {
 #define SEG_WGRAD_STAGES 1  // measured: one LDS stage beats two by 2-12% (BK 16)
 #endif
 constexpr int BK = SEG_WGRAD_BK;
+#ifndef SEG_WGRAD_BK_BF16
+#define SEG_WGRAD_BK_BF16 32  // pixels per K step of the bf16 kernels (two 16-deep MFMA steps)
+#endif
 
 struct WgradArgs {
   const void* dy; long lddy;     // IT (float, or __bf16 for the _bf16io path)
@@ -60,7 +63,7 @@ __global__ __launch_bounds__(256) void wgrad_kernel(WgradArgs a) {
   static_assert(VW == 4 || (BF && sizeof(IT) == 2), "16-byte slots carry bf16 operands");
   const IT* __restrict__ gdy = static_cast<const IT*>(a.dy);
   const IT* __restrict__ gx = static_cast<const IT*>(a.x);
-  constexpr int BK = BF ? 32 : ::BK;  // pixels per K chunk
+  constexpr int BK = BF ? SEG_WGRAD_BK_BF16 : ::BK;  // pixels per K chunk
   constexpr int AR = BF ? tr_pitch(BM) : BM + 4, BR = BF ? tr_pitch(BN) : BN + 4;
   constexpr int A_VEC = BK * BM / VW, B_VEC = BK * BN / VW;
   constexpr int A_PER = (A_VEC + 255) / 256, B_PER = (B_VEC + 255) / 256;

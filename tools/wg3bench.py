@@ -4,6 +4,9 @@ seg_conv_wgrad_bf16io and, where it applies, the LDS-halo seg_conv_wgrad2_bf16io
 Median of R launches with HIP events, algorithmic TFLOP/s (2 M Cout 9 Cin).
 
     python tools/wg3bench.py [--set unet|mnv2] [--reps 10]
+
+The LDS-DMA kernel it measures was removed after this measurement (DESIGN round 6, profiles/r06/wg3bench_*.txt):
+run it on a checkout of commit a0c410c, where csrc/wgrad3.hip and its entry points still exist.
 """
 import argparse
 import os
